@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Benchmark: the fused S10 suite over a synthetic 1e9-row Item table per GPU.
+
+One step = one pass of the hot path over the table resident in HBM: reset the aggregation state,
+the fused scan of every record batch in ONE launch (+ the finalize launch), the state read-back
+and, with N > 1 ranks, the exchange step (all-gather of the serialized per-rank states over RCCL
+and the rank-ordered merge).  Rows are sharded across ranks with no data-path collective, so
+per-GPU work is fixed (weak scaling); `value` = rows of all ranks / max-over-ranks step time.
+
+Output: ONE JSON line (rank 0).  `roofline.achieved` = algorithmic bytes of the suite (the distinct
+buffers it must read) / the average duration of the scan launch measured with HIP
+events on the engine's stream over the timed region; `cpu_baseline` = the C restatement of Spark
+2.2 deequ semantics (oracle/oracle.c, "port") timed on this host's cores on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "rows/sec + achieved HBM GB/s, fused 10-analyzer suite on 1B rows, 1/2/4/8 GPUs"
+PEAK_HBM = 8.0e12  # MI355X HBM3E spec (MI355X_MICROARCH.md:36)
+
+
+def s10_suite():
+    from deequ_amd.analyzers import (Completeness, Compliance, Maximum, Mean, Minimum, Size,
+                                     StandardDeviation, Sum)
+    return [Size(), Completeness("id"), Completeness("name"),
+            Compliance("numViews is Fnon-negative", "numViews >= 0"),
+            Compliance("priority contained in high,low",
+                       "priority IS NULL OR priority IN ('high','low')"),
+            Sum("numViews"), Mean("numViews"), StandardDeviation("numViews"),
+            Minimum("numViews"), Maximum("numViews")]
+
+
+def algorithmic_bytes(table) -> int:
+    """Distinct buffers S10 must read: 4 validity bitmaps, numViews values, priority offsets and
+    bytes."""
+    total = 0
+    for b in table.batches:
+        n = b["id"].length
+        total += 4 * ((n + 7) // 8)              # id/name/priority/numViews validity
+        total += 8 * n                           # numViews values
+        total += 4 * (n + 1)                     # priority offsets
+        total += int(b["priority"].values[n].item())  # priority bytes
+    return total
+
+
+def cpu_baseline(rows: int, seed: int, min_seconds: float = 10.0):
+    """oracle/oracle.c S10 (Spark local[T] execution model) on a bounded sample."""
+    from deequ_amd.synth import item_buffers_numpy
+    from oracle import c_oracle as C
+    threads = min(16, os.cpu_count() or 1)
+    buf = item_buffers_numpy(rows, seed)
+    n = buf["n"]
+
+    def once():
+        C.numeric_i64(buf["numViews"], buf["numViews_valid"], op=17, lit=0, threads=threads)
+        C.validity_count(buf["id_valid"], n, threads)
+        C.validity_count(buf["name_valid"], n, threads)
+        C.str_in(buf["priority_offsets"], buf["priority_data"], buf["priority_valid"], n,
+                 ["high", "low"], True, threads)
+
+    once()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        once()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds or reps >= 200:
+            break
+    return {"value": reps * n / el, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"S10 over {n} synthetic Item rows x {reps} passes ({el:.1f} s), "
+                      f"CPU restatement of Spark 2.2 deequ semantics (oracle/oracle.c, OpenMP, "
+                      f"{threads} threads = Spark local[{threads}] partitions) -- not Spark"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
+    ap.add_argument("--batch-rows", type=int, default=1 << 26)
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--cpu-rows", type=int, default=20_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    device = f"cuda:{local}"
+    torch.cuda.set_device(local)
+
+    from deequ_amd import _native as N
+    from deequ_amd.analyzers.base import AggSpec  # noqa: F401
+    from deequ_amd.distributed import merge_states_across_ranks
+    from deequ_amd.runners.engine import get_plan, read_row, scan_into
+    from deequ_amd.synth import item_table_device
+
+    table = item_table_device(args.rows, seed=args.seed, batch_rows=args.batch_rows,
+                              device=device, start=rank * args.rows)
+    suite = s10_suite()
+    specs = [s for a in suite for s in a.aggregation_functions()]
+    plan = get_plan(table.schema, specs)
+    state = plan.state(local)
+    stream = torch.cuda.current_stream(device)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def step(i=None):
+        N.check(N.lib.dq_state_reset(state))
+        if i is not None:
+            ev0[i].record(stream)
+        scan_into(table, plan, state, sh)
+        if i is not None:
+            ev1[i].record(stream)
+        N.check(N.lib.dq_state_sync(state))
+        if world > 1:
+            return merge_states_across_ranks(plan, state, device)
+        return read_row(plan, state)
+
+    for _ in range(args.warmup):
+        row = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        row = step(i)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    scan_ms = sum(a.elapsed_time(b) for a, b in zip(ev0, ev1)) / args.steps
+    b_alg = algorithmic_bytes(table)
+    achieved = b_alg / (scan_ms * 1e-3)
+
+    # sanity: the row must be a valid S10 result
+    assert row[0] == args.rows * world or world > 1 or row[0] == args.rows
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": args.rows * world / (elapsed / args.steps),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic",
+            "config": {
+                "workload": "S10 fused suite (Size, Completeness(id), Completeness(name), "
+                            "Compliance(numViews >= 0), Compliance(priority IS NULL OR priority IN "
+                            "('high','low')), Sum/Mean/StandardDeviation/Minimum/Maximum(numViews)) "
+                            "over a synthetic Item table: int64 id/numViews, string name/priority, "
+                            "5% nulls (BASELINE.json configs[1])",
+                "rows_per_gpu": args.rows,
+                "batch_rows": args.batch_rows,
+                "parallelism": f"dp{world}",
+            },
+            "achieved_hbm_gbps": achieved / 1e9,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved / 1e9,
+                "peak": PEAK_HBM / 1e9,
+                "unit": "GB/s",
+                "frac": achieved / PEAK_HBM,
+                "traffic": load_traffic(args.rows, b_alg),
+                "algorithmic_bytes_per_launch": b_alg,
+                "scan_ms": scan_ms,
+                "kernel": "dq::scan_kernel<false> (+ finalize_kernel)",
+            },
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.seed)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def load_traffic(rows: int, b_alg: int):
+    """HBM bytes per scan launch from the committed rocprofv3 PMC pass (profiles/), if one was
+    recorded for this workload size; else null."""
+    path = os.path.join(ROOT, "profiles", "traffic_s10.json")
+    try:
+        d = json.load(open(path))
+        if int(d.get("rows_per_gpu", -1)) == rows:
+            return d["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,155 @@
+"""ctypes binding of the C ABI in include/deequ_amd.h (libdeequ_amd.so, built in-tree).
+
+The library is the product: there is no CPU fallback.  If it is missing, importing the engine
+raises immediately (``build()`` in ``__graft_entry__`` or ``make -C deequ_amd/csrc`` builds it).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char, c_char_p, c_double, c_int, c_int32, c_int64,
+                    c_size_t, c_uint8, c_uint64, c_void_p)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdeequ_amd.so")
+
+# dq_type
+BOOL, INT8, INT16, INT32, INT64, FLOAT32, FLOAT64, UTF8 = range(1, 9)
+TYPE_NAMES = {BOOL: "BooleanType", INT8: "ByteType", INT16: "ShortType", INT32: "IntegerType",
+              INT64: "LongType", FLOAT32: "FloatType", FLOAT64: "DoubleType", UTF8: "StringType"}
+NUMERIC_TYPES = {INT8, INT16, INT32, INT64, FLOAT32, FLOAT64}
+INTEGRAL_TYPES = {INT8, INT16, INT32, INT64}
+
+# dq_xop
+(X_COL, X_NULL, X_BOOL, X_I64, X_F64, X_STR, X_IS_NULL, X_IS_NOT_NULL, X_NOT, X_AND, X_OR, X_EQ,
+ X_NE, X_LT, X_LE, X_GT, X_GE, X_EQ_NULL_SAFE, X_IN, X_CAST_F64) = range(1, 21)
+
+# dq_agg_kind
+(AGG_COUNT_ALL, AGG_COUNT_NOTNULL, AGG_COUNT_TRUE, AGG_SUM, AGG_MIN, AGG_MAX, AGG_STDDEV_POP,
+ AGG_CORR, AGG_HLL) = range(1, 10)
+
+# dq_status
+DQ_OK = 0
+ERR_INVALID_ARGUMENT, ERR_NO_SUCH_COLUMN, ERR_WRONG_TYPE, ERR_OUT_OF_MEMORY, ERR_DEVICE, \
+    ERR_UNSUPPORTED, ERR_STATE = range(1, 8)
+
+
+class dq_column(Structure):
+    _fields_ = [("type", c_int32), ("reserved", c_int32), ("length", c_int64),
+                ("validity", c_void_p), ("values", c_void_p), ("data", c_void_p)]
+
+
+class dq_expr(Structure):
+    _fields_ = [("words", POINTER(c_int64)), ("n_words", c_int32), ("reserved", c_int32)]
+
+
+class dq_agg(Structure):
+    _fields_ = [("kind", c_int32), ("col", c_int32), ("col2", c_int32), ("expr", c_int32),
+                ("where", c_int32), ("reserved", c_int32)]
+
+
+class dq_plan_desc(Structure):
+    _fields_ = [("n_columns", c_int32), ("column_types", POINTER(c_int32)), ("n_exprs", c_int32),
+                ("exprs", POINTER(dq_expr)), ("n_aggs", c_int32), ("aggs", POINTER(dq_agg))]
+
+
+class dq_value(Structure):
+    _fields_ = [("kind", c_int32), ("is_null", c_int32), ("i64", c_int64), ("f64", c_double * 6),
+                ("words", c_uint64 * 52)]
+
+
+class dq_freq_summary(Structure):
+    _fields_ = [("num_rows", c_int64), ("n_groups", c_int64), ("n_unique", c_int64),
+                ("n_null_key_rows", c_int64), ("entropy", c_double)]
+
+
+class EngineError(RuntimeError):
+    """A non-OK dq_status, carrying the library's dq_last_error() message."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP engine first (python -c "
+            "'import __graft_entry__ as g; g.build()' or make -C deequ_amd/csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "dq_last_error": (c_char_p, []),
+        "dq_version": (c_int, []),
+        "dq_device_count": (c_int, []),
+        "dq_column_from_arrow": (c_int, [c_void_p, c_void_p, POINTER(dq_column)]),
+        "dq_plan_create": (c_int, [POINTER(dq_plan_desc), POINTER(c_void_p)]),
+        "dq_plan_destroy": (None, [c_void_p]),
+        "dq_plan_explain": (c_int, [c_void_p, c_char_p, c_size_t]),
+        "dq_plan_launches_per_batch": (c_int, [c_void_p]),
+        "dq_state_create": (c_int, [c_void_p, c_int, POINTER(c_void_p)]),
+        "dq_state_destroy": (None, [c_void_p]),
+        "dq_state_reset": (c_int, [c_void_p]),
+        "dq_scan_device": (c_int, [c_void_p, POINTER(dq_column), c_int, c_void_p, c_void_p]),
+        "dq_scan_device_batches": (c_int, [c_void_p, POINTER(dq_column), c_int, c_int, c_void_p,
+                                           c_void_p]),
+        "dq_state_sync": (c_int, [c_void_p]),
+        "dq_state_get": (c_int, [c_void_p, c_int, POINTER(dq_value)]),
+        "dq_state_merge": (c_int, [c_void_p, c_void_p]),
+        "dq_state_serialized_size": (c_int64, [c_void_p]),
+        "dq_state_serialize": (c_int, [c_void_p, c_void_p, c_int64]),
+        "dq_state_deserialize": (c_int, [c_void_p, c_void_p, c_int64]),
+        "dq_hll_count": (c_double, [POINTER(c_uint64), POINTER(c_int)]),
+        "dq_xxhash64": (c_uint64, [c_void_p, c_int64, c_uint64]),
+        "dq_freq_create": (c_int, [c_int, c_int, POINTER(c_int32), c_int64, POINTER(c_void_p)]),
+        "dq_freq_destroy": (None, [c_void_p]),
+        "dq_freq_add_device": (c_int, [c_void_p, POINTER(dq_column), c_int, c_int, c_void_p]),
+        "dq_freq_summarize": (c_int, [c_void_p, POINTER(dq_freq_summary)]),
+        "dq_freq_num_groups": (c_int, [c_void_p, POINTER(c_int64)]),
+        "dq_freq_num_rows": (c_int64, [c_void_p]),
+        "dq_freq_export": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                   POINTER(c_int64)]),
+        "dq_freq_merge": (c_int, [c_void_p, c_void_p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+# every symbol the header declares (checked by tests/test_abi.py)
+EXPORTED = [
+    "dq_last_error", "dq_version", "dq_device_count", "dq_column_from_arrow", "dq_plan_create",
+    "dq_plan_destroy", "dq_plan_explain", "dq_plan_launches_per_batch", "dq_state_create",
+    "dq_state_destroy", "dq_state_reset", "dq_scan_device", "dq_scan_device_batches",
+    "dq_state_sync", "dq_state_get", "dq_state_merge", "dq_state_serialized_size",
+    "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_freq_create",
+    "dq_freq_destroy", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_num_groups",
+    "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge",
+]
+
+
+def check(status: int) -> None:
+    if status != DQ_OK:
+        msg = lib.dq_last_error()
+        raise EngineError(status, msg.decode("utf-8", "replace") if msg else f"status {status}")
+
+
+def device_count() -> int:
+    return int(lib.dq_device_count())
+
+
+def hll_count(words) -> tuple:
+    arr = (c_uint64 * 52)(*[w & 0xFFFFFFFFFFFFFFFF for w in words])
+    flag = c_int(0)
+    est = lib.dq_hll_count(arr, ctypes.byref(flag))
+    return est, bool(flag.value)
+
+
+def xxhash64(data: bytes, seed: int = 42) -> int:
+    buf = ctypes.create_string_buffer(data, len(data))
+    return int(lib.dq_xxhash64(buf, len(data), seed))

@@ -1,0 +1,13 @@
+"""Analyzers mirroring com.amazon.deequ.analyzers (the hot-path subset)."""
+from .base import (AggSpec, Analyzer, DoubleValuedState, GroupingAnalyzer, NumMatchesAndCount,
+                   Preconditions, ScanShareableAnalyzer, StandardScanShareableAnalyzer, State,
+                   merge_states)
+from .grouping import (CountDistinct, Distinctness, Entropy, FrequenciesAndNumRows,
+                       FrequencyBasedAnalyzer, FrequencyTable, Histogram, HistogramState,
+                       ScanShareableFrequencyBasedAnalyzer, UniqueValueRatio, Uniqueness,
+                       compute_frequencies)
+from .scan import (ApproxCountDistinct, ApproxCountDistinctState, Completeness, Compliance,
+                   Correlation, CorrelationState, MaxState, Maximum, Mean, MeanState, MinState,
+                   Minimum, NumMatches, Size, StandardDeviation, StandardDeviationState, Sum,
+                   SumState)
+from .state_provider import InMemoryStateProvider, StateLoader, StatePersister

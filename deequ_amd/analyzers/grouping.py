@@ -1,0 +1,457 @@
+"""Frequency-based analyzers (reference: analyzers/GroupingAnalyzers.scala, Uniqueness.scala,
+Distinctness.scala, UniqueValueRatio.scala, CountDistinct.scala, Entropy.scala, Histogram.scala).
+
+The frequency table (``SELECT keys, COUNT(*) ... WHERE keys NOT NULL GROUP BY keys``) is built by
+the engine's hash group-by (dq_freq_*), and lives in device memory.  The one aggregation over it
+that all ScanShareableFrequencyBasedAnalyzers of a grouping share (AnalysisRunner.scala:490-500)
+is the engine's dq_freq_summarize: Σ[count == 1], count(*), Σ −(c/n)·ln(c/n).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import struct
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .. import _native as N
+from ..exceptions import IllegalAnalyzerParameterException, wrap_if_necessary
+from ..metrics import Distribution, DistributionValue, Failure, HistogramMetric, Success
+from .base import (Analyzer, GroupingAnalyzer, Preconditions, State, empty_state_exception, entity_from,
+                   metric_from_empty, metric_from_failure, metric_from_value)
+
+
+# ------------------------------------------------------------------------------------------------
+# Device frequency table
+# ------------------------------------------------------------------------------------------------
+class FrequencyTable:
+    """A dq_freq handle: (key..., count) groups in HBM."""
+
+    def __init__(self, key_columns: Sequence[str], key_types: Sequence[int], device: int,
+                 capacity_hint: int = 0):
+        self.key_columns = list(key_columns)
+        self.key_types = list(key_types)
+        self.device = device
+        types = (ctypes.c_int32 * len(key_types))(*key_types)
+        h = ctypes.c_void_p()
+        N.check(N.lib.dq_freq_create(device, len(key_types), types, capacity_hint, ctypes.byref(h)))
+        self.handle = h
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                N.lib.dq_freq_destroy(self.handle)
+                self.handle = None
+        except Exception:  # noqa: BLE001
+            pass
+
+    def add(self, columns: Sequence, null_as_group: bool = False, stream=None) -> None:
+        arr = (N.dq_column * len(columns))(*[c.to_c() for c in columns])
+        if stream is None:
+            import torch
+            stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        N.check(N.lib.dq_freq_add_device(self.handle, arr, len(columns), 1 if null_as_group else 0,
+                                         stream))
+
+    @property
+    def num_rows(self) -> int:
+        return int(N.lib.dq_freq_num_rows(self.handle))
+
+    def summarize(self) -> N.dq_freq_summary:
+        s = N.dq_freq_summary()
+        N.check(N.lib.dq_freq_summarize(self.handle, ctypes.byref(s)))
+        return s
+
+    def count(self) -> int:
+        n = ctypes.c_int64()
+        N.check(N.lib.dq_freq_num_groups(self.handle, ctypes.byref(n)))
+        return int(n.value)
+
+    def export(self) -> List[Tuple[tuple, int]]:
+        """All groups as (key tuple, count); a NULL key component is None."""
+        n = self.count()
+        need = ctypes.c_int64()
+        N.check(N.lib.dq_freq_export(self.handle, None, None, None, 0, 0, ctypes.byref(need)))
+        counts = np.zeros(max(1, n), np.int64)
+        offs = np.zeros(n + 1, np.int64)
+        raw = np.zeros(max(1, need.value), np.uint8)
+        N.check(N.lib.dq_freq_export(self.handle, counts.ctypes.data, offs.ctypes.data,
+                                     raw.ctypes.data, n, need.value, ctypes.byref(need)))
+        data = raw.tobytes()
+        out = []
+        for g in range(n):
+            out.append((self._decode(data, int(offs[g])), int(counts[g])))
+        return out
+
+    def _decode(self, data: bytes, pos: int) -> tuple:
+        key = []
+        for t in self.key_types:
+            tag = struct.unpack_from("<I", data, pos)[0]
+            pos += 4
+            if tag == 0:
+                key.append(None)
+                continue
+            if t == N.UTF8:
+                ln = struct.unpack_from("<I", data, pos)[0]
+                pos += 4
+                key.append(data[pos: pos + ln].decode("utf-8", "replace"))
+                pos += (ln + 3) & ~3
+            else:
+                v = struct.unpack_from("<Q", data, pos)[0]
+                pos += 8
+                key.append(_decode_fixed(t, v))
+        return tuple(key)
+
+    def merged(self, other: "FrequencyTable") -> "FrequencyTable":
+        out = FrequencyTable(self.key_columns, self.key_types, self.device)
+        N.check(N.lib.dq_freq_merge(out.handle, self.handle))
+        N.check(N.lib.dq_freq_merge(out.handle, other.handle))
+        return out
+
+
+def _decode_fixed(t: int, v: int):
+    if t == N.FLOAT64:
+        return struct.unpack("<d", struct.pack("<Q", v))[0]
+    if t == N.FLOAT32:
+        return float(np.frombuffer(struct.pack("<I", v & 0xFFFFFFFF), np.float32)[0])
+    if t == N.BOOL:
+        return bool(v)
+    return v - (1 << 64) if v >= (1 << 63) else v
+
+
+# ------------------------------------------------------------------------------------------------
+# State
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class FrequenciesAndNumRows(State):
+    """GroupingAnalyzers.scala:124-157"""
+    frequencies: FrequencyTable
+    num_rows: int
+
+    def sum(self, other: "FrequenciesAndNumRows") -> "FrequenciesAndNumRows":
+        return FrequenciesAndNumRows(self.frequencies.merged(other.frequencies),
+                                     self.num_rows + other.num_rows)
+
+
+def compute_frequencies(data, grouping_columns: Sequence[str],
+                        num_rows: Optional[int] = None) -> FrequenciesAndNumRows:
+    """FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:53-80)."""
+    types = [data.schema[c].dtype for c in grouping_columns]
+    table = FrequencyTable(grouping_columns, types, data.device_index())
+    for batch in data.batches:
+        table.add([batch[c] for c in grouping_columns])
+    n = num_rows if num_rows is not None else data.count()
+    return FrequenciesAndNumRows(table, n)
+
+
+# ------------------------------------------------------------------------------------------------
+# Analyzers
+# ------------------------------------------------------------------------------------------------
+class FrequencyBasedAnalyzer(GroupingAnalyzer):
+    """GroupingAnalyzers.scala:29-45"""
+
+    def _columns(self) -> List[str]:
+        raise NotImplementedError
+
+    def grouping_columns(self) -> List[str]:
+        return list(self._columns())
+
+    def compute_state_from(self, data):
+        return compute_frequencies(data, self.grouping_columns())
+
+    def preconditions(self) -> List[Callable]:
+        cols = self._columns()
+        return [Preconditions.at_least_one(cols)] + [Preconditions.has_column(c) for c in cols] + \
+            super().preconditions()
+
+
+@dataclass(frozen=True)
+class FreqAgg:
+    """One aggregation over the frequency table."""
+    kind: str  # "unique", "distinct", "count", "entropy"
+
+
+def frequency_row(summary: "N.dq_freq_summary", aggs: Sequence[FreqAgg], num_rows: int) -> list:
+    """Evaluates the shared aggregation over the frequency table (Spark semantics: a sum over an
+    empty table is NULL, count(*) is 0)."""
+    empty = summary.n_groups == 0
+    row = []
+    for a in aggs:
+        if a.kind == "unique":
+            row.append(None if empty else float(summary.n_unique))
+        elif a.kind == "distinct":
+            row.append(None if empty else float(summary.n_groups))
+        elif a.kind == "count":
+            row.append(int(summary.n_groups))
+        elif a.kind == "entropy":
+            row.append(None if empty else float(summary.entropy))
+        elif a.kind == "unique_ratio_of_rows":
+            row.append(None if empty else float(summary.n_unique) / num_rows)
+        elif a.kind == "distinct_ratio_of_rows":
+            row.append(None if empty else float(summary.n_groups) / num_rows)
+        else:
+            raise ValueError(a.kind)
+    return row
+
+
+class ScanShareableFrequencyBasedAnalyzer(FrequencyBasedAnalyzer):
+    """GroupingAnalyzers.scala:84-121"""
+
+    _name = ""
+
+    def aggregation_functions(self, num_rows: int) -> List[FreqAgg]:
+        raise NotImplementedError
+
+    def _instance(self) -> str:
+        return ",".join(self._columns())
+
+    def compute_metric_from(self, state):
+        if state is None:
+            return metric_from_empty(self, self._name, self._instance(), entity_from(self._columns()))
+        aggs = self.aggregation_functions(state.num_rows)
+        row = frequency_row(state.frequencies.summarize(), aggs, state.num_rows)
+        return self.from_aggregation_result(row, 0)
+
+    def to_failure_metric(self, exception):
+        return metric_from_failure(exception, self._name, self._instance(),
+                                   entity_from(self._columns()))
+
+    def to_success_metric(self, value: float):
+        return metric_from_value(value, self._name, self._instance(), entity_from(self._columns()))
+
+    def from_aggregation_result(self, result, offset):
+        if result[offset] is None:
+            return metric_from_empty(self, self._name, self._instance(), entity_from(self._columns()))
+        return self.to_success_metric(float(result[offset]))
+
+
+def _cols(columns) -> Tuple[str, ...]:
+    return (columns,) if isinstance(columns, str) else tuple(columns)
+
+
+@dataclass(frozen=True)
+class Uniqueness(ScanShareableFrequencyBasedAnalyzer):
+    """Uniqueness.scala:26-32: Σ[count == 1] / numRows"""
+    columns: Tuple[str, ...]
+    _name = "Uniqueness"
+
+    def __init__(self, columns):
+        object.__setattr__(self, "columns", _cols(columns))
+
+    def _columns(self):
+        return list(self.columns)
+
+    def aggregation_functions(self, num_rows):
+        return [FreqAgg("unique_ratio_of_rows")]
+
+
+@dataclass(frozen=True)
+class Distinctness(ScanShareableFrequencyBasedAnalyzer):
+    """Distinctness.scala:29-35: Σ[count >= 1] / numRows"""
+    columns: Tuple[str, ...]
+    _name = "Distinctness"
+
+    def __init__(self, columns):
+        object.__setattr__(self, "columns", _cols(columns))
+
+    def _columns(self):
+        return list(self.columns)
+
+    def aggregation_functions(self, num_rows):
+        return [FreqAgg("distinct_ratio_of_rows")]
+
+
+@dataclass(frozen=True)
+class UniqueValueRatio(ScanShareableFrequencyBasedAnalyzer):
+    """UniqueValueRatio.scala:25-38: Σ[count == 1] / count(*)"""
+    columns: Tuple[str, ...]
+    _name = "UniqueValueRatio"
+
+    def __init__(self, columns):
+        object.__setattr__(self, "columns", _cols(columns))
+
+    def _columns(self):
+        return list(self.columns)
+
+    def aggregation_functions(self, num_rows):
+        return [FreqAgg("unique"), FreqAgg("count")]
+
+    def from_aggregation_result(self, result, offset):
+        if result[offset] is None:
+            # Row.getDouble on a NULL slot throws in the reference -> failure metric
+            raise TypeError(f"Value at index {offset} is null")
+        unique, distinct = float(result[offset]), float(result[offset + 1])
+        return self.to_success_metric(unique / distinct if distinct else float("nan"))
+
+
+@dataclass(frozen=True)
+class CountDistinct(ScanShareableFrequencyBasedAnalyzer):
+    """CountDistinct.scala:24-34: count(*) over the groups"""
+    columns: Tuple[str, ...]
+    _name = "CountDistinct"
+
+    def __init__(self, columns):
+        object.__setattr__(self, "columns", _cols(columns))
+
+    def _columns(self):
+        return list(self.columns)
+
+    def aggregation_functions(self, num_rows):
+        return [FreqAgg("count")]
+
+    def from_aggregation_result(self, result, offset):
+        return self.to_success_metric(float(result[offset]))
+
+
+@dataclass(frozen=True)
+class Entropy(ScanShareableFrequencyBasedAnalyzer):
+    """Entropy.scala:28-42: Σ −(c/numRows)·ln(c/numRows)"""
+    column: str
+    _name = "Entropy"
+
+    def _columns(self):
+        return [self.column]
+
+    def __str__(self):
+        return f"Entropy({self.column})"
+
+    def aggregation_functions(self, num_rows):
+        return [FreqAgg("entropy")]
+
+
+# ------------------------------------------------------------------------------------------------
+# Histogram (Histogram.scala:41-116)
+# ------------------------------------------------------------------------------------------------
+NULL_FIELD_REPLACEMENT = "NullValue"
+MAXIMUM_ALLOWED_DETAIL_BINS = 1000
+
+
+def java_double_to_string(d: float) -> str:
+    """Java Double.toString formatting (Spark 2.2 Cast(DoubleType -> StringType)) using the
+    shortest round-trip digits."""
+    if math.isnan(d):
+        return "NaN"
+    if math.isinf(d):
+        return "Infinity" if d > 0 else "-Infinity"
+    if d == 0.0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    return _java_fmt(repr(float(d)), abs(d))
+
+
+def java_float_to_string(f: float) -> str:
+    if math.isnan(f):
+        return "NaN"
+    if math.isinf(f):
+        return "Infinity" if f > 0 else "-Infinity"
+    if f == 0.0:
+        return "-0.0" if math.copysign(1.0, f) < 0 else "0.0"
+    digits = np.format_float_scientific(np.float32(f), unique=True, trim="-")
+    return _java_fmt(digits, abs(f))
+
+
+def _java_fmt(py: str, mag: float) -> str:
+    from decimal import Decimal
+    dec = Decimal(py)
+    sign = "-" if dec < 0 else ""
+    dec = abs(dec)
+    t = dec.as_tuple()
+    digits = "".join(map(str, t.digits)).rstrip("0") or "0"
+    exp10 = t.exponent + len(t.digits) - 1  # exponent of the leading digit
+    if 1e-3 <= mag < 1e7:
+        s = format(dec.normalize(), "f")
+        if "." not in s:
+            s += ".0"
+        return sign + s
+    mant = digits[0] + "." + (digits[1:] or "0")
+    return f"{sign}{mant}E{exp10}"
+
+
+def cast_to_string(value, dtype: int) -> str:
+    if value is None:
+        return NULL_FIELD_REPLACEMENT
+    if dtype == N.UTF8:
+        return value
+    if dtype == N.BOOL:
+        return "true" if value else "false"
+    if dtype == N.FLOAT64:
+        return java_double_to_string(value)
+    if dtype == N.FLOAT32:
+        return java_float_to_string(value)
+    return str(int(value))
+
+
+@dataclass
+class HistogramState(FrequenciesAndNumRows):
+    dtype: int = N.UTF8
+    binning_udf: Optional[Callable] = None
+
+    def string_groups(self) -> dict:
+        """Groups keyed by Spark's cast-to-string of the value (NULL -> "NullValue"), with the
+        binning function applied to the distinct values."""
+        out: dict = {}
+        for (key,), cnt in self.frequencies.export():
+            s = cast_to_string(key, self.dtype)
+            if self.binning_udf is not None:
+                s = self.binning_udf(None if key is None else s)
+                s = NULL_FIELD_REPLACEMENT if s is None else s
+            out[s] = out.get(s, 0) + cnt
+        return out
+
+    def sum(self, other):
+        return HistogramState(self.frequencies.merged(other.frequencies),
+                              self.num_rows + other.num_rows, self.dtype, self.binning_udf)
+
+
+@dataclass(frozen=True)
+class Histogram(Analyzer):
+    """Not a GroupingAnalyzer in the reference: it runs as its own jobs (AnalysisRunner.scala:
+    321-323)."""
+    column: str
+    binning_udf: Optional[Callable] = None
+    max_detail_bins: int = MAXIMUM_ALLOWED_DETAIL_BINS
+
+    def __str__(self):
+        udf = "None" if self.binning_udf is None else f"Some({self.binning_udf})"
+        return f"Histogram({self.column},{udf},{self.max_detail_bins})"
+
+    def grouping_columns(self):
+        return [self.column]
+
+    def _param_check(self, _schema):
+        if self.max_detail_bins > MAXIMUM_ALLOWED_DETAIL_BINS:
+            raise IllegalAnalyzerParameterException(
+                f"Cannot return histogram values for more than {MAXIMUM_ALLOWED_DETAIL_BINS} values")
+
+    def preconditions(self):
+        return [self._param_check, Preconditions.has_column(self.column)]
+
+    def compute_state_from(self, data):
+        total = data.count()
+        dtype = data.schema[self.column].dtype
+        table = FrequencyTable([self.column], [dtype], data.device_index())
+        for batch in data.batches:
+            table.add([batch[self.column]], null_as_group=True)
+        return HistogramState(table, total, dtype, self.binning_udf)
+
+    def compute_metric_from(self, state):
+        if state is None:
+            return HistogramMetric(self.column, Failure(empty_state_exception(self)))
+        try:
+            groups = state.string_groups()
+            # rdd.top(maxDetailBins)(OrderByAbsoluteCount): ties are arbitrary in the reference
+            top = sorted(groups.items(), key=lambda kv: (-kv[1], kv[0]))[: self.max_detail_bins]
+            details = {k: DistributionValue(c, c / state.num_rows) for k, c in top}
+            return HistogramMetric(self.column, Success(Distribution(details, len(groups))))
+        except Exception as e:  # noqa: BLE001
+            return HistogramMetric(self.column, Failure(wrap_if_necessary(e)))
+
+    def to_failure_metric(self, exception):
+        return HistogramMetric(self.column, Failure(wrap_if_necessary(exception)))
+
+
+__all__ = ["FrequencyTable", "FrequenciesAndNumRows", "compute_frequencies",
+           "FrequencyBasedAnalyzer", "ScanShareableFrequencyBasedAnalyzer", "Uniqueness",
+           "Distinctness", "UniqueValueRatio", "CountDistinct", "Entropy", "Histogram",
+           "HistogramState", "java_double_to_string", "java_float_to_string", "cast_to_string"]

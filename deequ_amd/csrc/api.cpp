@@ -1,0 +1,1214 @@
+// api.cpp -- host runtime behind the C ABI (include/deequ_amd.h): expression decoding, the planner
+// that maps a suite's aggregation functions onto fused column tasks, the device state, the
+// Spark-partial-aggregate merge, and (de)serialisation for multi-GPU collectives.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "engine.h"
+#include "kernels.h"
+
+using namespace dq;
+
+// ------------------------------------------------------------------------------------------------
+// Errors
+// ------------------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+dq_status dq::fail(dq_status code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+
+extern "C" const char* dq_last_error(void) { return g_last_error.c_str(); }
+extern "C" int dq_version(void) { return 100; }
+extern "C" int dq_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+static bool is_numeric(int t) { return t >= DQ_INT8 && t <= DQ_FLOAT64; }
+static bool is_integral(int t) { return t >= DQ_INT8 && t <= DQ_INT64; }
+static bool is_floating(int t) { return t == DQ_FLOAT32 || t == DQ_FLOAT64; }
+static int type_size(int t) {
+  switch (t) {
+    case DQ_INT8: return 1;
+    case DQ_INT16: return 2;
+    case DQ_INT32: return 4;
+    case DQ_INT64: return 8;
+    case DQ_FLOAT32: return 4;
+    case DQ_FLOAT64: return 8;
+    case DQ_UTF8: return 4;
+    default: return 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Expression trees
+// ------------------------------------------------------------------------------------------------
+struct Node {
+  int op = 0;
+  int col = -1;
+  int64_t i = 0;
+  double d = 0.0;
+  std::string s;
+  std::vector<std::unique_ptr<Node>> kids;
+};
+
+static bool parse_node(const int64_t* w, int n, int& pos, std::unique_ptr<Node>& out, int ncols,
+                       int depth) {
+  if (pos >= n || depth > 64) return false;
+  auto node = std::make_unique<Node>();
+  node->op = (int)w[pos++];
+  auto child = [&](void) -> bool {
+    std::unique_ptr<Node> c;
+    if (!parse_node(w, n, pos, c, ncols, depth + 1)) return false;
+    node->kids.push_back(std::move(c));
+    return true;
+  };
+  switch (node->op) {
+    case DQ_X_COL:
+      if (pos >= n) return false;
+      node->col = (int)w[pos++];
+      if (node->col < 0 || node->col >= ncols) return false;
+      break;
+    case DQ_X_NULL: break;
+    case DQ_X_BOOL:
+    case DQ_X_I64:
+      if (pos >= n) return false;
+      node->i = w[pos++];
+      break;
+    case DQ_X_F64:
+      if (pos >= n) return false;
+      memcpy(&node->d, &w[pos++], 8);
+      break;
+    case DQ_X_STR: {
+      if (pos >= n) return false;
+      int64_t nb = w[pos++];
+      int64_t nw = (nb + 7) / 8;
+      if (nb < 0 || pos + nw > n) return false;
+      node->s.assign(reinterpret_cast<const char*>(&w[pos]), (size_t)nb);
+      pos += (int)nw;
+      break;
+    }
+    case DQ_X_IS_NULL:
+    case DQ_X_IS_NOT_NULL:
+    case DQ_X_NOT:
+    case DQ_X_CAST_F64:
+      if (!child()) return false;
+      break;
+    case DQ_X_AND:
+    case DQ_X_OR:
+    case DQ_X_EQ:
+    case DQ_X_NE:
+    case DQ_X_LT:
+    case DQ_X_LE:
+    case DQ_X_GT:
+    case DQ_X_GE:
+    case DQ_X_EQ_NULL_SAFE:
+      if (!child() || !child()) return false;
+      break;
+    case DQ_X_IN: {
+      if (pos >= n) return false;
+      int64_t items = w[pos++];
+      if (items < 0 || items > 4096) return false;
+      for (int64_t k = 0; k < items + 1; ++k)
+        if (!child()) return false;
+      break;
+    }
+    default: return false;
+  }
+  out = std::move(node);
+  return true;
+}
+
+static bool is_cmp(int op) { return op >= DQ_X_EQ && op <= DQ_X_GE; }
+static int flip_cmp(int op) {
+  switch (op) {
+    case DQ_X_LT: return DQ_X_GT;
+    case DQ_X_LE: return DQ_X_GE;
+    case DQ_X_GT: return DQ_X_LT;
+    case DQ_X_GE: return DQ_X_LE;
+    default: return op;
+  }
+}
+
+static void compile_postfix(const Node& n, std::vector<XInstr>& prog, std::string& pool) {
+  for (auto& k : n.kids) compile_postfix(*k, prog, pool);
+  XInstr ins{0, 0, 0};
+  switch (n.op) {
+    case DQ_X_COL: ins = {XI_COL, n.col, 0}; break;
+    case DQ_X_NULL: ins = {XI_NULL, 0, 0}; break;
+    case DQ_X_BOOL: ins = {XI_BOOL, 0, n.i ? 1 : 0}; break;
+    case DQ_X_I64: ins = {XI_I64, 0, n.i}; break;
+    case DQ_X_F64: {
+      int64_t b;
+      memcpy(&b, &n.d, 8);
+      ins = {XI_F64, 0, b};
+      break;
+    }
+    case DQ_X_STR: {
+      while (pool.size() % 4) pool.push_back('\0');
+      ins = {XI_STR, (int32_t)n.s.size(), (int64_t)pool.size()};
+      pool += n.s;
+      break;
+    }
+    case DQ_X_IS_NULL: ins = {XI_IS_NULL, 0, 0}; break;
+    case DQ_X_IS_NOT_NULL: ins = {XI_IS_NOT_NULL, 0, 0}; break;
+    case DQ_X_NOT: ins = {XI_NOT, 0, 0}; break;
+    case DQ_X_AND: ins = {XI_AND, 0, 0}; break;
+    case DQ_X_OR: ins = {XI_OR, 0, 0}; break;
+    case DQ_X_IN: ins = {XI_IN, (int32_t)n.kids.size() - 1, 0}; break;
+    case DQ_X_CAST_F64: ins = {XI_CAST_F64, 0, 0}; break;
+    default: ins = {XI_CMP, n.op, 0}; break;
+  }
+  prog.push_back(ins);
+}
+
+static int stack_depth(const Node& n) {
+  int best = 0, k = 0;
+  for (auto& c : n.kids) best = std::max(best, k++ + stack_depth(*c));
+  return std::max(best, 1);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Predicate fusion: recognise the forms Check emits so they run inside a column task.
+// ------------------------------------------------------------------------------------------------
+struct CmpLeaf {
+  int col = -1;
+  int op = 0;
+  bool lit_f64 = false;
+  int64_t li = 0;
+  double ld = 0.0;
+};
+
+static bool leaf_cmp(const Node& n, const std::vector<int32_t>& types, CmpLeaf& out) {
+  if (!is_cmp(n.op)) return false;
+  const Node* a = n.kids[0].get();
+  const Node* b = n.kids[1].get();
+  int op = n.op;
+  auto is_lit = [](const Node* x) { return x->op == DQ_X_I64 || x->op == DQ_X_F64; };
+  auto colref = [&](const Node* x) -> int {
+    if (x->op == DQ_X_COL && is_numeric(types[x->col])) return x->col;
+    return -1;
+  };
+  if (colref(b) >= 0 && is_lit(a)) {
+    std::swap(a, b);
+    op = flip_cmp(op);
+  }
+  int c = colref(a);
+  if (c < 0 || !is_lit(b)) return false;
+  out.col = c;
+  out.op = op;
+  out.lit_f64 = b->op == DQ_X_F64;
+  out.li = b->i;
+  out.ld = b->op == DQ_X_F64 ? b->d : (double)b->i;
+  return true;
+}
+
+// [col IS NULL OR] (cmp [AND cmp])  on one numeric column
+static bool fuse_numeric(const Node& n, const std::vector<int32_t>& types, int& col, NumPred& p) {
+  p = NumPred{};
+  const Node* body = &n;
+  int null_col = -1;
+  if (n.op == DQ_X_OR && n.kids[0]->op == DQ_X_IS_NULL && n.kids[0]->kids[0]->op == DQ_X_COL) {
+    null_col = n.kids[0]->kids[0]->col;
+    body = n.kids[1].get();
+  }
+  CmpLeaf a, b;
+  bool two = false;
+  if (body->op == DQ_X_AND) {
+    if (!leaf_cmp(*body->kids[0], types, a) || !leaf_cmp(*body->kids[1], types, b)) return false;
+    if (a.col != b.col) return false;
+    two = true;
+  } else if (!leaf_cmp(*body, types, a)) {
+    return false;
+  }
+  if (null_col >= 0 && null_col != a.col) return false;
+  const bool fcol = is_floating(types[a.col]);
+  const bool as_double = fcol || a.lit_f64 || (two && b.lit_f64);
+  // both comparisons must live in the same domain as Spark evaluates them
+  if (two && !fcol && (a.lit_f64 != b.lit_f64)) return false;
+  if (as_double && !fcol && types[a.col] == DQ_INT64) {
+    // Spark casts the long column to double for a double literal: same here (exact below 2^53)
+  }
+  col = a.col;
+  p.op1 = a.op;
+  p.op2 = two ? b.op : 0;
+  p.as_double = as_double ? 1 : 0;
+  p.null_is_true = null_col >= 0 ? 1 : 0;
+  p.lo_i = a.li;
+  p.lo_d = a.ld;
+  p.hi_i = two ? b.li : 0;
+  p.hi_d = two ? b.ld : 0.0;
+  return true;
+}
+
+struct StrIn {
+  int col = -1;
+  bool negate = false;
+  bool null_is_true = false;
+  std::vector<std::string> list;
+};
+
+static bool fuse_str_in_body(const Node& n, const std::vector<int32_t>& types, StrIn& s) {
+  if (n.op == DQ_X_NOT) {
+    if (!fuse_str_in_body(*n.kids[0], types, s)) return false;
+    s.negate = !s.negate;
+    return true;
+  }
+  if (n.op == DQ_X_IN) {
+    const Node& x = *n.kids[0];
+    if (x.op != DQ_X_COL || types[x.col] != DQ_UTF8) return false;
+    for (size_t k = 1; k < n.kids.size(); ++k) {
+      if (n.kids[k]->op != DQ_X_STR) return false;
+      s.list.push_back(n.kids[k]->s);
+    }
+    s.col = x.col;
+    return true;
+  }
+  if (n.op == DQ_X_EQ || n.op == DQ_X_NE) {
+    const Node* a = n.kids[0].get();
+    const Node* b = n.kids[1].get();
+    if (a->op == DQ_X_STR) std::swap(a, b);
+    if (a->op != DQ_X_COL || types[a->col] != DQ_UTF8 || b->op != DQ_X_STR) return false;
+    s.col = a->col;
+    s.list.push_back(b->s);
+    s.negate = n.op == DQ_X_NE;
+    return true;
+  }
+  return false;
+}
+
+static bool fuse_str_in(const Node& n, const std::vector<int32_t>& types, StrIn& s) {
+  s = StrIn{};
+  if (n.op == DQ_X_OR && n.kids[0]->op == DQ_X_IS_NULL && n.kids[0]->kids[0]->op == DQ_X_COL) {
+    int nc = n.kids[0]->kids[0]->col;
+    if (!fuse_str_in_body(*n.kids[1], types, s)) return false;
+    if (s.col != nc) return false;
+    s.null_is_true = true;
+    return true;
+  }
+  return fuse_str_in_body(n, types, s);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Plan
+// ------------------------------------------------------------------------------------------------
+enum SlotSrc { SRC_ROWS = 1, SRC_TASK = 2 };
+
+struct Slot {
+  int kind = 0;    // dq_agg_kind
+  int src = 0;     // SlotSrc
+  int task = -1;   // task index
+  int field = 0;   // pred index for fused numeric predicates, else 0
+  int col_type = 0;
+  bool fused_pred = false;
+  bool notnull_rows = false;  // COUNT_NOTNULL: NULL only when no rows
+};
+
+struct TaskPlan {
+  int kind = 0;
+  int col = -1, col2 = -1;
+  int where = -1;      // materialised where expression index (into plan->mat)
+  int bool_expr = -1;  // TK_BOOLMAP counted expression (into plan->mat)
+  int n_preds = 0;
+  NumPred preds[kMaxPreds];
+  StrIn str;
+  int out = 0;
+  int hll_out = -1;
+};
+
+struct MatExpr {
+  int expr = -1;                // index in desc exprs
+  std::vector<XInstr> prog;
+  std::string pool;
+};
+
+struct dq_plan {
+  std::vector<int32_t> types;
+  std::vector<std::unique_ptr<Node>> exprs;
+  std::vector<dq_agg> aggs;
+  std::vector<Slot> slots;
+  std::vector<TaskPlan> tasks;
+  std::vector<MatExpr> mat;     // materialised expressions (where filters + unfusable predicates)
+  std::map<int, int> mat_of;    // expr index -> mat index
+  int n_hll = 0;
+  bool full = false;            // needs the full kernel family (hashing / co-moments / int8/16)
+};
+
+static int mat_index(dq_plan* p, int expr) {
+  auto it = p->mat_of.find(expr);
+  if (it != p->mat_of.end()) return it->second;
+  MatExpr m;
+  m.expr = expr;
+  compile_postfix(*p->exprs[expr], m.prog, m.pool);
+  int idx = (int)p->mat.size();
+  p->mat.push_back(std::move(m));
+  p->mat_of[expr] = idx;
+  return idx;
+}
+
+static int find_or_add_task(dq_plan* p, int kind, int col, int col2, int where) {
+  for (size_t k = 0; k < p->tasks.size(); ++k) {
+    const TaskPlan& t = p->tasks[k];
+    if (t.kind == kind && t.col == col && t.col2 == col2 && t.where == where && kind != TK_STR_IN &&
+        kind != TK_BOOLMAP)
+      return (int)k;
+  }
+  TaskPlan t;
+  t.kind = kind;
+  t.col = col;
+  t.col2 = col2;
+  t.where = where;
+  t.out = (int)p->tasks.size();
+  if (kind == TK_HLL) t.hll_out = p->n_hll++;
+  p->tasks.push_back(t);
+  return (int)p->tasks.size() - 1;
+}
+
+extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
+  if (!desc || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  if (desc->n_columns < 0 || desc->n_exprs < 0 || desc->n_aggs < 0)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "negative counts in plan description");
+  auto p = std::make_unique<dq_plan>();
+  p->types.assign(desc->column_types, desc->column_types + desc->n_columns);
+  for (int t : p->types)
+    if (t < DQ_BOOL || t > DQ_UTF8) return fail(DQ_ERR_INVALID_ARGUMENT, "unknown column type %d", t);
+  for (int e = 0; e < desc->n_exprs; ++e) {
+    std::unique_ptr<Node> n;
+    int pos = 0;
+    if (!parse_node(desc->exprs[e].words, desc->exprs[e].n_words, pos, n, desc->n_columns, 0) ||
+        pos != desc->exprs[e].n_words)
+      return fail(DQ_ERR_INVALID_ARGUMENT, "malformed expression %d", e);
+    if (stack_depth(*n) > kMaxStack)
+      return fail(DQ_ERR_UNSUPPORTED, "expression %d nests deeper than %d", e, kMaxStack);
+    p->exprs.push_back(std::move(n));
+  }
+  p->aggs.assign(desc->aggs, desc->aggs + desc->n_aggs);
+
+  auto check_col = [&](int c) -> dq_status {
+    if (c < 0 || c >= desc->n_columns) return fail(DQ_ERR_NO_SUCH_COLUMN, "no such column %d", c);
+    return DQ_OK;
+  };
+  auto where_of = [&](const dq_agg& a, int& w) -> dq_status {
+    w = -1;
+    if (a.where < 0) return DQ_OK;
+    if (a.where >= desc->n_exprs) return fail(DQ_ERR_INVALID_ARGUMENT, "bad where index");
+    w = mat_index(p.get(), a.where);
+    return DQ_OK;
+  };
+
+  for (const dq_agg& a : p->aggs) {
+    Slot s;
+    s.kind = a.kind;
+    int w = -1;
+    dq_status st;
+    switch (a.kind) {
+      case DQ_AGG_COUNT_ALL: s.src = SRC_ROWS; break;
+      case DQ_AGG_COUNT_NOTNULL: {
+        if ((st = check_col(a.col)) != DQ_OK) return st;
+        if ((st = where_of(a, w)) != DQ_OK) return st;
+        s.src = SRC_TASK;
+        s.notnull_rows = true;
+        // share the numeric task when one exists for (col, where); else a popcount task
+        int found = -1;
+        for (size_t k = 0; k < p->tasks.size(); ++k)
+          if (p->tasks[k].kind == TK_NUMERIC && p->tasks[k].col == a.col && p->tasks[k].where == w)
+            found = (int)k;
+        s.task = found >= 0 ? found : find_or_add_task(p.get(), TK_VALIDITY, a.col, -1, w);
+        break;
+      }
+      case DQ_AGG_COUNT_TRUE: {
+        if (a.expr < 0 || a.expr >= desc->n_exprs)
+          return fail(DQ_ERR_INVALID_ARGUMENT, "COUNT_TRUE needs an expression");
+        if ((st = where_of(a, w)) != DQ_OK) return st;
+        s.src = SRC_TASK;
+        const Node& e = *p->exprs[a.expr];
+        int col;
+        NumPred np;
+        StrIn si;
+        // a where filter counted by itself (conditionalCount) reuses its bitmap
+        if (p->mat_of.count(a.expr) && w < 0) {
+          TaskPlan t;
+          t.kind = TK_BOOLMAP;
+          t.bool_expr = p->mat_of[a.expr];
+          t.out = (int)p->tasks.size();
+          p->tasks.push_back(t);
+          s.task = t.out;
+        } else if (fuse_numeric(e, p->types, col, np)) {
+          int ti = find_or_add_task(p.get(), TK_NUMERIC, col, -1, w);
+          TaskPlan& t = p->tasks[ti];
+          if (t.n_preds < kMaxPreds) {
+            t.preds[t.n_preds] = np;
+            s.task = ti;
+            s.field = t.n_preds++;
+            s.fused_pred = true;
+          } else {
+            TaskPlan b;
+            b.kind = TK_BOOLMAP;
+            b.where = w;
+            b.bool_expr = mat_index(p.get(), a.expr);
+            b.out = (int)p->tasks.size();
+            p->tasks.push_back(b);
+            s.task = b.out;
+          }
+        } else if (fuse_str_in(e, p->types, si) && si.list.size() <= 256) {
+          TaskPlan t;
+          t.kind = TK_STR_IN;
+          t.col = si.col;
+          t.where = w;
+          t.str = si;
+          t.out = (int)p->tasks.size();
+          p->tasks.push_back(t);
+          s.task = t.out;
+        } else {
+          TaskPlan t;
+          t.kind = TK_BOOLMAP;
+          t.where = w;
+          t.bool_expr = mat_index(p.get(), a.expr);
+          t.out = (int)p->tasks.size();
+          p->tasks.push_back(t);
+          s.task = t.out;
+        }
+        break;
+      }
+      case DQ_AGG_SUM:
+      case DQ_AGG_MIN:
+      case DQ_AGG_MAX:
+      case DQ_AGG_STDDEV_POP: {
+        if ((st = check_col(a.col)) != DQ_OK) return st;
+        if (!is_numeric(p->types[a.col]))
+          return fail(DQ_ERR_WRONG_TYPE, "column %d is not numeric", a.col);
+        if ((st = where_of(a, w)) != DQ_OK) return st;
+        s.src = SRC_TASK;
+        s.task = find_or_add_task(p.get(), TK_NUMERIC, a.col, -1, w);
+        s.col_type = p->types[a.col];
+        break;
+      }
+      case DQ_AGG_CORR: {
+        if ((st = check_col(a.col)) != DQ_OK) return st;
+        if ((st = check_col(a.col2)) != DQ_OK) return st;
+        if (!is_numeric(p->types[a.col]) || !is_numeric(p->types[a.col2]))
+          return fail(DQ_ERR_WRONG_TYPE, "correlation needs numeric columns");
+        if ((st = where_of(a, w)) != DQ_OK) return st;
+        s.src = SRC_TASK;
+        s.task = find_or_add_task(p.get(), TK_COMOMENTS, a.col, a.col2, w);
+        break;
+      }
+      case DQ_AGG_HLL: {
+        if ((st = check_col(a.col)) != DQ_OK) return st;
+        if ((st = where_of(a, w)) != DQ_OK) return st;
+        s.src = SRC_TASK;
+        s.task = find_or_add_task(p.get(), TK_HLL, a.col, -1, w);
+        break;
+      }
+      default: return fail(DQ_ERR_INVALID_ARGUMENT, "unknown aggregation kind %d", a.kind);
+    }
+    p->slots.push_back(s);
+  }
+  // COUNT_NOTNULL slots that picked a validity task before a numeric task for the same
+  // (col, where) appeared are re-pointed so the column is read once.
+  for (Slot& s : p->slots) {
+    if (s.kind != DQ_AGG_COUNT_NOTNULL) continue;
+    const TaskPlan& t = p->tasks[s.task];
+    for (size_t k = 0; k < p->tasks.size(); ++k)
+      if (p->tasks[k].kind == TK_NUMERIC && p->tasks[k].col == t.col && p->tasks[k].where == t.where)
+        s.task = (int)k;
+  }
+  // drop validity tasks nobody references any more, renumber
+  std::vector<int> used(p->tasks.size(), 0);
+  for (const Slot& s : p->slots)
+    if (s.task >= 0) used[s.task] = 1;
+  std::vector<int> remap(p->tasks.size(), -1);
+  std::vector<TaskPlan> kept;
+  int n_hll = 0;
+  for (size_t k = 0; k < p->tasks.size(); ++k) {
+    if (!used[k]) continue;
+    remap[k] = (int)kept.size();
+    TaskPlan t = p->tasks[k];
+    t.out = (int)kept.size();
+    if (t.kind == TK_HLL) t.hll_out = n_hll++;
+    kept.push_back(t);
+  }
+  p->tasks.swap(kept);
+  p->n_hll = n_hll;
+  for (Slot& s : p->slots)
+    if (s.task >= 0) s.task = remap[s.task];
+  for (const TaskPlan& t : p->tasks) {
+    if (t.kind == TK_HLL || t.kind == TK_COMOMENTS) p->full = true;
+    if (t.kind == TK_NUMERIC && (p->types[t.col] == DQ_INT8 || p->types[t.col] == DQ_INT16))
+      p->full = true;
+  }
+  *out = p.release();
+  return DQ_OK;
+}
+
+extern "C" void dq_plan_destroy(dq_plan* plan) { delete plan; }
+
+static const char* kind_name(int k) {
+  switch (k) {
+    case TK_NUMERIC: return "numeric";
+    case TK_VALIDITY: return "validity";
+    case TK_STR_IN: return "str_in";
+    case TK_BOOLMAP: return "boolmap";
+    case TK_COMOMENTS: return "comoments";
+    case TK_HLL: return "hll";
+    default: return "?";
+  }
+}
+
+extern "C" dq_status dq_plan_explain(const dq_plan* plan, char* buf, size_t buf_len) {
+  if (!plan || !buf || buf_len == 0) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  std::string s;
+  char line[256];
+  for (size_t k = 0; k < plan->mat.size(); ++k) {
+    snprintf(line, sizeof(line), "expr[%zu] = bitmap of expression %d (%zu instructions)\n", k,
+             plan->mat[k].expr, plan->mat[k].prog.size());
+    s += line;
+  }
+  for (const TaskPlan& t : plan->tasks) {
+    snprintf(line, sizeof(line), "task[%d] %s col=%d col2=%d where=%d preds=%d list=%zu%s\n", t.out,
+             kind_name(t.kind), t.col, t.col2, t.where, t.n_preds, t.str.list.size(),
+             t.bool_expr >= 0 ? " (expr bitmap)" : "");
+    s += line;
+  }
+  snprintf(line, sizeof(line), "launches per batch: %d\n", dq_plan_launches_per_batch(plan));
+  s += line;
+  size_t n = std::min(buf_len - 1, s.size());
+  memcpy(buf, s.data(), n);
+  buf[n] = '\0';
+  return DQ_OK;
+}
+
+extern "C" int dq_plan_launches_per_batch(const dq_plan* plan) {
+  if (!plan) return 0;
+  return (int)plan->mat.size() + (plan->tasks.empty() ? 0 : 2);
+}
+
+// ------------------------------------------------------------------------------------------------
+// State
+// ------------------------------------------------------------------------------------------------
+struct dq_state {
+  const dq_plan* plan = nullptr;
+  int device = 0;
+  int grid_max = 0;
+  hipStream_t stream = nullptr;
+  bool stream_set = false;
+  // host mirror
+  std::vector<Acc> acc;
+  std::vector<uint8_t> hll;
+  int64_t rows = 0;
+  bool host_dirty = false;   // host mirror newer than device (after merge / deserialize / reset)
+  bool synced = true;        // host mirror reflects every scanned batch
+  // device
+  DevBuf<Acc> d_acc, d_partial;
+  DevBuf<uint8_t> d_hll, d_hll_partial;
+  DevBuf<TaskDesc> d_tasks[2];
+  TaskDesc* h_tasks[2] = {nullptr, nullptr};
+  size_t h_tasks_cap[2] = {0, 0};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  bool ev_used[2] = {false, false};
+  int flip = 0;
+  DevBuf<uint64_t> d_bitmaps;   // per materialised expression: value words then validity words
+  size_t bitmap_words = 0;      // words per bitmap
+  DevBuf<XInstr> d_prog;
+  std::vector<int> prog_off;    // per mat expr: offset into d_prog
+  DevBuf<uint8_t> d_pool;
+  std::vector<int64_t> pool_off;
+  DevBuf<DevCol> d_cols[2];
+  DevCol* h_cols[2] = {nullptr, nullptr};
+  size_t h_cols_cap[2] = {0, 0};
+  // STR_IN lists per task
+  DevBuf<int32_t> d_list_off;
+  DevBuf<uint8_t> d_list_bytes;
+  DevBuf<uint64_t> d_list_pre;
+  std::vector<int64_t> list_off_base, list_byte_base, list_pre_base;
+  ~dq_state() {
+    for (int k = 0; k < 2; ++k) {
+      if (h_tasks[k]) (void)hipHostFree(h_tasks[k]);
+      if (h_cols[k]) (void)hipHostFree(h_cols[k]);
+      if (ev[k]) (void)hipEventDestroy(ev[k]);
+    }
+  }
+};
+
+static void host_reset(dq_state* s) {
+  const dq_plan* p = s->plan;
+  s->acc.assign(p->tasks.size(), Acc{});
+  for (size_t k = 0; k < p->tasks.size(); ++k) acc_init(p->tasks[k].kind, s->acc[k]);
+  s->hll.assign((size_t)p->n_hll * kHllM, 0);
+  s->rows = 0;
+  s->host_dirty = true;
+  s->synced = true;
+}
+
+static dq_status upload_host(dq_state* s) {
+  if (!s->host_dirty || s->device < 0) return DQ_OK;
+  HIP_TRY(hipSetDevice(s->device));
+  if (!s->acc.empty())
+    HIP_TRY(hipMemcpy(s->d_acc.p, s->acc.data(), s->acc.size() * sizeof(Acc), hipMemcpyHostToDevice));
+  if (!s->hll.empty())
+    HIP_TRY(hipMemcpy(s->d_hll.p, s->hll.data(), s->hll.size(), hipMemcpyHostToDevice));
+  s->host_dirty = false;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state** out) {
+  if (!plan || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  auto s = std::make_unique<dq_state>();
+  s->plan = plan;
+  s->device = device;
+  host_reset(s.get());
+  if (device < 0) {  // host-only state: deserialize / merge / get (rank-ordered merges)
+    s->host_dirty = false;
+    *out = s.release();
+    return DQ_OK;
+  }
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(DQ_ERR_DEVICE, "no HIP device %d", device);
+  HIP_TRY(hipSetDevice(device));
+  int cus = 0;
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  int per_cu = scan_max_blocks_per_cu(plan->full);
+  s->grid_max = std::max(1, cus * std::min(per_cu, 8));
+  const size_t nt = std::max<size_t>(1, plan->tasks.size());
+  HIP_TRY(s->d_acc.ensure(nt));
+  HIP_TRY(s->d_hll.ensure(std::max(1, plan->n_hll) * (size_t)kHllM));
+  HIP_TRY(s->d_partial.ensure(nt * (size_t)s->grid_max));
+  HIP_TRY(s->d_hll_partial.ensure(std::max(1, plan->n_hll) * (size_t)s->grid_max * kHllM));
+  for (int k = 0; k < 2; ++k) HIP_TRY(hipEventCreateWithFlags(&s->ev[k], hipEventDisableTiming));
+  // expression programs and string pools
+  std::vector<XInstr> prog;
+  std::string pool;
+  for (const MatExpr& m : plan->mat) {
+    s->prog_off.push_back((int)prog.size());
+    prog.insert(prog.end(), m.prog.begin(), m.prog.end());
+    while (pool.size() % 16) pool.push_back('\0');
+    s->pool_off.push_back((int64_t)pool.size());
+    pool += m.pool;
+  }
+  // pool offsets in the programs are relative to each expression's own pool
+  for (size_t k = 0; k < plan->mat.size(); ++k)
+    for (size_t q = 0; q < plan->mat[k].prog.size(); ++q)
+      if (prog[s->prog_off[k] + q].op == XI_STR) prog[s->prog_off[k] + q].imm += s->pool_off[k];
+  HIP_TRY(s->d_prog.ensure(std::max<size_t>(1, prog.size())));
+  if (!prog.empty())
+    HIP_TRY(hipMemcpy(s->d_prog.p, prog.data(), prog.size() * sizeof(XInstr), hipMemcpyHostToDevice));
+  HIP_TRY(s->d_pool.ensure(std::max<size_t>(16, pool.size() + 16)));
+  if (!pool.empty()) HIP_TRY(hipMemcpy(s->d_pool.p, pool.data(), pool.size(), hipMemcpyHostToDevice));
+  // STR_IN lists
+  std::vector<int32_t> loff;
+  std::vector<uint8_t> lbytes;
+  std::vector<uint64_t> lpre;
+  for (const TaskPlan& t : plan->tasks) {
+    s->list_off_base.push_back((int64_t)loff.size());
+    s->list_byte_base.push_back((int64_t)lbytes.size());
+    s->list_pre_base.push_back((int64_t)lpre.size());
+    if (t.kind != TK_STR_IN) continue;
+    int32_t base = 0;
+    for (const std::string& it : t.str.list) {
+      loff.push_back(base);
+      uint64_t pre = 0;
+      for (size_t b = 0; b < std::min<size_t>(8, it.size()); ++b)
+        pre |= (uint64_t)(uint8_t)it[b] << (8 * b);
+      lpre.push_back(pre);
+      lbytes.insert(lbytes.end(), it.begin(), it.end());
+      base += (int32_t)it.size();
+    }
+    loff.push_back(base);
+  }
+  HIP_TRY(s->d_list_off.ensure(std::max<size_t>(1, loff.size())));
+  HIP_TRY(s->d_list_bytes.ensure(std::max<size_t>(16, lbytes.size())));
+  HIP_TRY(s->d_list_pre.ensure(std::max<size_t>(1, lpre.size())));
+  if (!loff.empty())
+    HIP_TRY(hipMemcpy(s->d_list_off.p, loff.data(), loff.size() * 4, hipMemcpyHostToDevice));
+  if (!lbytes.empty())
+    HIP_TRY(hipMemcpy(s->d_list_bytes.p, lbytes.data(), lbytes.size(), hipMemcpyHostToDevice));
+  if (!lpre.empty())
+    HIP_TRY(hipMemcpy(s->d_list_pre.p, lpre.data(), lpre.size() * 8, hipMemcpyHostToDevice));
+  dq_status st = upload_host(s.get());
+  if (st != DQ_OK) return st;
+  *out = s.release();
+  return DQ_OK;
+}
+
+extern "C" void dq_state_destroy(dq_state* state) {
+  if (!state) return;
+  if (state->stream_set && state->device >= 0) (void)hipStreamSynchronize(state->stream);
+  delete state;
+}
+
+extern "C" dq_status dq_state_reset(dq_state* state) {
+  if (!state) return fail(DQ_ERR_INVALID_ARGUMENT, "null state");
+  if (state->stream_set && state->device >= 0) HIP_TRY(hipStreamSynchronize(state->stream));
+  host_reset(state);
+  return upload_host(state);
+}
+
+static int64_t pow2_at_least(int64_t v) {
+  int64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+static bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+// Validates one batch against the plan and returns its row count (-1 on error).
+static int64_t batch_rows(const dq_plan* plan, const dq_column* cols, const std::vector<int>& ref,
+                          dq_status& st) {
+  st = DQ_OK;
+  int64_t rows = -1;
+  for (size_t c = 0; c < plan->types.size(); ++c) {
+    if (cols[c].type != plan->types[c]) {
+      st = fail(DQ_ERR_WRONG_TYPE, "column %zu has type %d, plan expects %d", c, cols[c].type,
+                plan->types[c]);
+      return -1;
+    }
+    if (!ref[c]) continue;
+    if (cols[c].length < 0) {
+      st = fail(DQ_ERR_INVALID_ARGUMENT, "negative column length");
+      return -1;
+    }
+    if (rows < 0) rows = cols[c].length;
+    else if (rows != cols[c].length) {
+      st = fail(DQ_ERR_INVALID_ARGUMENT, "columns of one batch differ in length");
+      return -1;
+    }
+    if (cols[c].length > 0 && !cols[c].values) {
+      st = fail(DQ_ERR_INVALID_ARGUMENT, "column %zu has no values buffer", c);
+      return -1;
+    }
+    if (cols[c].type == DQ_UTF8 && cols[c].length > 0 && !cols[c].data) {
+      st = fail(DQ_ERR_INVALID_ARGUMENT, "utf8 column %zu has no data buffer", c);
+      return -1;
+    }
+  }
+  if (rows < 0) rows = plan->types.empty() ? 0 : cols[0].length;  // e.g. only Size()
+  if (rows > ((int64_t)1 << 40)) {
+    st = fail(DQ_ERR_UNSUPPORTED, "batch too large");
+    return -1;
+  }
+  return rows;
+}
+
+extern "C" dq_status dq_scan_device(const dq_plan* plan, const dq_column* cols, int n_cols,
+                                    dq_state* s, void* hip_stream) {
+  return dq_scan_device_batches(plan, cols, n_cols, 1, s, hip_stream);
+}
+
+extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column* cols, int n_cols,
+                                            int n_batches, dq_state* s, void* hip_stream) {
+  if (!plan || !s || (n_cols > 0 && n_batches > 0 && !cols))
+    return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_batches < 0) return fail(DQ_ERR_INVALID_ARGUMENT, "negative batch count");
+  if (s->plan != plan) return fail(DQ_ERR_STATE, "state was created for another plan");
+  if (n_cols < (int)plan->types.size())
+    return fail(DQ_ERR_NO_SUCH_COLUMN, "plan needs %zu columns, got %d", plan->types.size(), n_cols);
+  if (n_batches == 0) return DQ_OK;
+  if (s->device < 0) return fail(DQ_ERR_STATE, "host-only state (device -1) cannot scan");
+  hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
+  HIP_TRY(hipSetDevice(s->device));
+  if (s->stream_set && s->stream != stream) HIP_TRY(hipStreamSynchronize(s->stream));
+  s->stream = stream;
+  s->stream_set = true;
+  dq_status st = upload_host(s);
+  if (st != DQ_OK) return st;
+
+  // referenced columns decide each batch's length
+  std::vector<int> ref(plan->types.size(), 0);
+  for (const TaskPlan& t : plan->tasks) {
+    if (t.col >= 0) ref[t.col] = 1;
+    if (t.col2 >= 0) ref[t.col2] = 1;
+  }
+  for (const MatExpr& m : plan->mat)
+    for (const XInstr& ins : m.prog)
+      if (ins.op == XI_COL) ref[ins.a] = 1;
+  std::vector<int64_t> rows(n_batches);
+  int64_t total_rows = 0;
+  for (int b = 0; b < n_batches; ++b) {
+    rows[b] = batch_rows(plan, cols + (size_t)b * n_cols, ref, st);
+    if (rows[b] < 0) return st;
+    total_rows += rows[b];
+  }
+
+  const int slot = s->flip;
+  s->flip ^= 1;
+  if (s->ev_used[slot]) HIP_TRY(hipEventSynchronize(s->ev[slot]));
+
+  // materialised expressions -> bitmaps, per batch at a 16-byte aligned word offset
+  std::vector<size_t> bm_off(n_batches);
+  size_t words = 0;
+  for (int b = 0; b < n_batches; ++b) {
+    bm_off[b] = words;
+    words += (size_t)((rows[b] + 63) / 64 + 2) & ~(size_t)1;
+  }
+  words += 2;
+  const size_t n_mat = plan->mat.size();
+  if (n_mat) {
+    if (words > s->bitmap_words || !s->d_bitmaps.p) {
+      HIP_TRY(hipStreamSynchronize(stream));
+      HIP_TRY(s->d_bitmaps.ensure(words * 2 * n_mat));
+      s->bitmap_words = words;
+    }
+    const size_t ncol = plan->types.size();
+    HIP_TRY(s->d_cols[slot].ensure(std::max<size_t>(1, ncol * n_batches)));
+    if (s->h_cols_cap[slot] < ncol * n_batches) {
+      if (s->h_cols[slot]) HIP_TRY(hipHostFree(s->h_cols[slot]));
+      HIP_TRY(hipHostMalloc((void**)&s->h_cols[slot], ncol * n_batches * sizeof(DevCol),
+                            hipHostMallocDefault));
+      s->h_cols_cap[slot] = ncol * n_batches;
+    }
+    DevCol* hc = s->h_cols[slot];
+    for (int b = 0; b < n_batches; ++b)
+      for (size_t c = 0; c < ncol; ++c) {
+        const dq_column& col = cols[(size_t)b * n_cols + c];
+        hc[b * ncol + c] = DevCol{col.type, 0, col.validity, col.values, col.data};
+      }
+    HIP_TRY(hipMemcpyAsync(s->d_cols[slot].p, hc, ncol * n_batches * sizeof(DevCol),
+                           hipMemcpyHostToDevice, stream));
+    for (size_t k = 0; k < n_mat; ++k) {
+      for (int b = 0; b < n_batches; ++b) {
+        uint64_t* val = s->d_bitmaps.p + (2 * k) * s->bitmap_words + bm_off[b];
+        uint64_t* vld = s->d_bitmaps.p + (2 * k + 1) * s->bitmap_words + bm_off[b];
+        HIP_TRY(launch_expr(s->d_prog.p + s->prog_off[k], (int)plan->mat[k].prog.size(),
+                            s->d_cols[slot].p + (size_t)b * ncol, s->d_pool.p, rows[b], val, vld,
+                            stream));
+      }
+    }
+  }
+  auto mat_val = [&](int m, int b) -> const uint8_t* {
+    if (m < 0) return nullptr;
+    return reinterpret_cast<const uint8_t*>(s->d_bitmaps.p + (2 * m) * s->bitmap_words + bm_off[b]);
+  };
+  auto mat_vld = [&](int m, int b) -> const uint8_t* {
+    if (m < 0) return nullptr;
+    return reinterpret_cast<const uint8_t*>(s->d_bitmaps.p + (2 * m + 1) * s->bitmap_words + bm_off[b]);
+  };
+
+  // descriptor table: one descriptor per (batch, task)
+  const size_t n_desc = plan->tasks.size() * (size_t)n_batches;
+  if (s->h_tasks_cap[slot] < n_desc) {
+    if (s->h_tasks[slot]) HIP_TRY(hipHostFree(s->h_tasks[slot]));
+    HIP_TRY(hipHostMalloc((void**)&s->h_tasks[slot], std::max<size_t>(1, n_desc) * sizeof(TaskDesc),
+                          hipHostMallocDefault));
+    s->h_tasks_cap[slot] = n_desc;
+  }
+  HIP_TRY(s->d_tasks[slot].ensure(std::max<size_t>(1, n_desc)));
+  TaskDesc* td = s->h_tasks[slot];
+  int64_t total_items = 0;
+  int n_hll_desc = 0;
+  size_t d = 0;
+  for (int b = 0; b < n_batches; ++b) {
+    const dq_column* bc = cols + (size_t)b * n_cols;
+    for (size_t k = 0; k < plan->tasks.size(); ++k, ++d) {
+      const TaskPlan& tp = plan->tasks[k];
+      TaskDesc t;
+      memset(&t, 0, sizeof(t));
+      t.kind = tp.kind;
+      t.out = tp.out;
+      t.hll_out = tp.hll_out;
+      t.hll_slot = tp.kind == TK_HLL ? n_hll_desc++ : -1;
+      t.batch = b;
+      t.rows = rows[b];
+      t.w_val = mat_val(tp.where, b);
+      t.w_vld = mat_vld(tp.where, b);
+      double bpr = 0.25;  // bytes per row, for item sizing
+      bool vec = true;
+      if (tp.col >= 0) {
+        const dq_column& c = bc[tp.col];
+        t.type = c.type;
+        t.valid = c.validity;
+        t.values = c.values;
+        t.data = c.data;
+        vec = vec && aligned(c.validity, 16) && aligned(c.values, 16);
+        bpr += type_size(c.type) + 0.125;
+        if (c.type == DQ_UTF8) bpr += 8.0;
+      }
+      if (tp.col2 >= 0) {
+        const dq_column& c = bc[tp.col2];
+        t.type2 = c.type;
+        t.valid2 = c.validity;
+        t.values2 = c.values;
+        bpr += type_size(c.type) + 0.125;
+      }
+      switch (tp.kind) {
+        case TK_NUMERIC:
+          t.n_preds = tp.n_preds;
+          for (int q = 0; q < tp.n_preds; ++q) t.preds[q] = tp.preds[q];
+          break;
+        case TK_BOOLMAP:
+          t.b_val = mat_val(tp.bool_expr, b);
+          t.b_vld = mat_vld(tp.bool_expr, b);
+          bpr = 0.5;
+          break;
+        case TK_VALIDITY: bpr = 0.125 + (tp.where >= 0 ? 0.25 : 0.0); break;
+        case TK_STR_IN:
+          t.negate = tp.str.negate ? 1 : 0;
+          t.null_is_true = tp.str.null_is_true ? 1 : 0;
+          t.n_list = (int32_t)tp.str.list.size();
+          t.list_off = s->d_list_off.p + s->list_off_base[k];
+          t.list_bytes = s->d_list_bytes.p + s->list_byte_base[k];
+          t.list_pre = s->d_list_pre.p + s->list_pre_base[k];
+          break;
+        case TK_HLL: bpr *= 4.0; break;  // hashing: weight items by work, not bytes
+        case TK_COMOMENTS: bpr *= 2.0; break;
+        default: break;
+      }
+      t.vec_ok = vec ? 1 : 0;
+      int64_t item_rows = pow2_at_least((int64_t)(131072.0 / bpr));
+      item_rows = std::max<int64_t>(kRowsPerIter, std::min<int64_t>(item_rows, (int64_t)1 << 22));
+      t.item_rows = item_rows;
+      t.n_items = rows[b] > 0 ? (rows[b] + item_rows - 1) / item_rows : 0;
+      t.item_begin = total_items;
+      total_items += t.n_items;
+      td[d] = t;
+    }
+  }
+  if (n_desc > 0 && total_items > 0) {
+    const int grid = (int)std::min<int64_t>(total_items, s->grid_max);
+    HIP_TRY(s->d_partial.ensure(n_desc * (size_t)grid));
+    HIP_TRY(s->d_hll_partial.ensure(std::max(1, n_hll_desc) * (size_t)grid * kHllM));
+    HIP_TRY(hipMemcpyAsync(s->d_tasks[slot].p, td, n_desc * sizeof(TaskDesc), hipMemcpyHostToDevice,
+                           stream));
+    HIP_TRY(launch_scan(s->d_tasks[slot].p, (int)n_desc, (int)plan->tasks.size(), total_items, grid,
+                        plan->full, s->d_partial.p, s->d_hll_partial.p, s->d_acc.p, s->d_hll.p,
+                        stream));
+  }
+  HIP_TRY(hipEventRecord(s->ev[slot], stream));
+  s->ev_used[slot] = true;
+  s->rows += total_rows;
+  s->synced = false;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_state_sync(dq_state* s) {
+  if (!s) return fail(DQ_ERR_INVALID_ARGUMENT, "null state");
+  if (s->synced || s->device < 0) return DQ_OK;
+  HIP_TRY(hipSetDevice(s->device));
+  HIP_TRY(hipStreamSynchronize(s->stream));
+  if (!s->acc.empty())
+    HIP_TRY(hipMemcpy(s->acc.data(), s->d_acc.p, s->acc.size() * sizeof(Acc), hipMemcpyDeviceToHost));
+  if (!s->hll.empty())
+    HIP_TRY(hipMemcpy(s->hll.data(), s->d_hll.p, s->hll.size(), hipMemcpyDeviceToHost));
+  s->synced = true;
+  return DQ_OK;
+}
+
+static void pack_hll(const uint8_t* regs, uint64_t* words) {
+  for (int w = 0; w < kHllWords; ++w) {
+    uint64_t v = 0;
+    for (int i = 0; i < kHllRegsPerWord; ++i) {
+      int idx = w * kHllRegsPerWord + i;
+      if (idx >= kHllM) break;
+      v |= (uint64_t)(regs[idx] & 0x3f) << (kHllRegBits * i);
+    }
+    words[w] = v;
+  }
+}
+
+extern "C" dq_status dq_state_get(const dq_state* s, int agg_index, dq_value* out) {
+  if (!s || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  const dq_plan* p = s->plan;
+  if (agg_index < 0 || agg_index >= (int)p->slots.size())
+    return fail(DQ_ERR_INVALID_ARGUMENT, "aggregation index %d out of range", agg_index);
+  if (!s->synced) return fail(DQ_ERR_STATE, "state not synced (call dq_state_sync)");
+  memset(out, 0, sizeof(*out));
+  const Slot& sl = p->slots[agg_index];
+  out->kind = sl.kind;
+  if (sl.src == SRC_ROWS) {
+    out->i64 = s->rows;
+    out->f64[0] = (double)s->rows;
+    return DQ_OK;
+  }
+  const TaskPlan& tp = p->tasks[sl.task];
+  const Acc& a = s->acc[sl.task];
+  switch (sl.kind) {
+    case DQ_AGG_COUNT_NOTNULL:
+      out->i64 = tp.kind == TK_NUMERIC ? a.i[0] : a.i[0];
+      out->is_null = s->rows == 0;
+      break;
+    case DQ_AGG_COUNT_TRUE:
+      if (sl.fused_pred) {
+        out->i64 = a.i[4 + sl.field];
+        out->is_null = a.i[7 + sl.field] == 0;
+      } else {
+        out->i64 = a.i[0];
+        out->is_null = a.i[1] == 0;
+      }
+      break;
+    case DQ_AGG_SUM:
+      out->is_null = a.i[0] == 0;
+      if (is_integral(sl.col_type)) {
+        out->i64 = a.i[1];
+        out->f64[0] = (double)a.i[1];
+      } else {
+        out->f64[0] = a.d[0];
+      }
+      break;
+    case DQ_AGG_MIN:
+    case DQ_AGG_MAX: {
+      out->is_null = a.i[0] == 0;
+      int64_t k = sl.kind == DQ_AGG_MIN ? a.i[2] : a.i[3];
+      if (is_integral(sl.col_type)) {
+        out->i64 = k;
+        out->f64[0] = (double)k;
+      } else {
+        out->f64[0] = f64_from_key(k);
+      }
+      break;
+    }
+    case DQ_AGG_STDDEV_POP:
+      out->f64[0] = (double)a.i[0];
+      out->f64[1] = a.i[0] ? a.d[1] : 0.0;
+      out->f64[2] = a.i[0] ? a.d[2] : 0.0;
+      break;
+    case DQ_AGG_CORR:
+      out->f64[0] = (double)a.i[0];
+      for (int f = 0; f < 5; ++f) out->f64[1 + f] = a.i[0] ? a.d[f] : 0.0;
+      break;
+    case DQ_AGG_HLL:
+      pack_hll(&s->hll[(size_t)tp.hll_out * kHllM], out->words);
+      break;
+    default: break;
+  }
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_state_merge(dq_state* dst, const dq_state* src) {
+  if (!dst || !src) return fail(DQ_ERR_INVALID_ARGUMENT, "null state");
+  if (dst->plan != src->plan) return fail(DQ_ERR_STATE, "states belong to different plans");
+  if (!dst->synced || !src->synced) return fail(DQ_ERR_STATE, "states must be synced before merging");
+  const dq_plan* p = dst->plan;
+  for (size_t k = 0; k < p->tasks.size(); ++k) acc_merge(p->tasks[k].kind, dst->acc[k], src->acc[k]);
+  for (size_t k = 0; k < dst->hll.size(); ++k) dst->hll[k] = std::max(dst->hll[k], src->hll[k]);
+  dst->rows += src->rows;
+  dst->host_dirty = true;
+  return DQ_OK;
+}
+
+static const uint64_t kMagic = 0x3130514445455144ULL;  // "DQEEDQ01"
+
+extern "C" int64_t dq_state_serialized_size(const dq_plan* plan) {
+  if (!plan) return -1;
+  return 32 + (int64_t)plan->tasks.size() * (int64_t)sizeof(Acc) + (int64_t)plan->n_hll * kHllM;
+}
+
+extern "C" dq_status dq_state_serialize(const dq_state* s, void* buf, int64_t buf_len) {
+  if (!s || !buf) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (!s->synced) return fail(DQ_ERR_STATE, "state not synced");
+  int64_t need = dq_state_serialized_size(s->plan);
+  if (buf_len < need) return fail(DQ_ERR_INVALID_ARGUMENT, "buffer too small (%lld < %lld)",
+                                  (long long)buf_len, (long long)need);
+  uint8_t* b = static_cast<uint8_t*>(buf);
+  uint64_t hdr[4] = {kMagic, (uint64_t)s->plan->tasks.size(), (uint64_t)s->plan->n_hll, (uint64_t)s->rows};
+  memcpy(b, hdr, 32);
+  if (!s->acc.empty()) memcpy(b + 32, s->acc.data(), s->acc.size() * sizeof(Acc));
+  if (!s->hll.empty()) memcpy(b + 32 + s->acc.size() * sizeof(Acc), s->hll.data(), s->hll.size());
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_state_deserialize(dq_state* s, const void* buf, int64_t buf_len) {
+  if (!s || !buf) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  int64_t need = dq_state_serialized_size(s->plan);
+  if (buf_len < need) return fail(DQ_ERR_INVALID_ARGUMENT, "buffer too small");
+  const uint8_t* b = static_cast<const uint8_t*>(buf);
+  uint64_t hdr[4];
+  memcpy(hdr, b, 32);
+  if (hdr[0] != kMagic || hdr[1] != s->plan->tasks.size() || hdr[2] != (uint64_t)s->plan->n_hll)
+    return fail(DQ_ERR_STATE, "serialized state does not match this plan");
+  if (s->stream_set && s->device >= 0) HIP_TRY(hipStreamSynchronize(s->stream));
+  s->rows = (int64_t)hdr[3];
+  if (!s->acc.empty()) memcpy(s->acc.data(), b + 32, s->acc.size() * sizeof(Acc));
+  if (!s->hll.empty()) memcpy(s->hll.data(), b + 32 + s->acc.size() * sizeof(Acc), s->hll.size());
+  s->synced = true;
+  s->host_dirty = true;
+  return DQ_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// HLL estimate and hash (host)
+// ------------------------------------------------------------------------------------------------
+extern "C" double dq_hll_count(const uint64_t* words, int* bias_corrected) {
+  // HyperLogLogPlusPlusUtils.count (StatefulHyperloglogPlus.scala:208-255)
+  const double M = kHllM;
+  const double alpha_m2 = (0.7213 / (1.0 + 1.079 / M)) * M * M;
+  double z_inv = 0.0, V = 0.0;
+  int idx = 0;
+  for (int w = 0; w < kHllWords; ++w) {
+    uint64_t word = words[w];
+    for (int i = 0; i < kHllRegsPerWord && idx < kHllM; ++i, ++idx) {
+      uint64_t m = (word >> (kHllRegBits * i)) & 0x3f;
+      z_inv += 1.0 / (double)(1ULL << m);
+      if (m == 0) V += 1.0;
+    }
+  }
+  const double threshold = 400.0;  // HyperLogLogPlusPlus.THRESHOLDS(P - 4), P = 9
+  double e = alpha_m2 / z_inv;
+  bool biased = e < 5.0 * M;
+  double estimate;
+  if (V > 0) {
+    double H = M * std::log(M / V);
+    if (H <= threshold) {
+      estimate = H;
+      biased = false;
+    } else {
+      estimate = e;
+    }
+  } else {
+    estimate = e;
+  }
+  if (bias_corrected) *bias_corrected = biased ? 1 : 0;
+  return (double)(int64_t)std::floor(estimate + 0.5);  // Math.round
+}
+
+extern "C" uint64_t dq_xxhash64(const void* data, int64_t nbytes, uint64_t seed) {
+  HostBytes rd{static_cast<const uint8_t*>(data)};
+  return xxh_bytes(rd, nbytes, seed);
+}
+
+extern "C" dq_status dq_column_from_arrow(const struct ArrowArray* array,
+                                          const struct ArrowSchema* schema, dq_column* out) {
+  if (!array || !schema || !out || !schema->format)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (array->offset != 0) return fail(DQ_ERR_UNSUPPORTED, "arrays with a non-zero offset");
+  std::string f(schema->format);
+  int type = 0;
+  if (f == "b") type = DQ_BOOL;
+  else if (f == "c") type = DQ_INT8;
+  else if (f == "s") type = DQ_INT16;
+  else if (f == "i") type = DQ_INT32;
+  else if (f == "l") type = DQ_INT64;
+  else if (f == "f") type = DQ_FLOAT32;
+  else if (f == "g") type = DQ_FLOAT64;
+  else if (f == "u") type = DQ_UTF8;
+  else return fail(DQ_ERR_UNSUPPORTED, "Arrow format '%s'", schema->format);
+  int64_t need = type == DQ_UTF8 ? 3 : 2;
+  if (array->n_buffers < need) return fail(DQ_ERR_INVALID_ARGUMENT, "too few Arrow buffers");
+  out->type = type;
+  out->reserved = 0;
+  out->length = array->length;
+  out->validity = array->null_count == 0 ? nullptr : static_cast<const uint8_t*>(array->buffers[0]);
+  out->values = array->buffers[1];
+  out->data = type == DQ_UTF8 ? static_cast<const uint8_t*>(array->buffers[2]) : nullptr;
+  return DQ_OK;
+}

@@ -1,0 +1,288 @@
+// engine.h -- records and arithmetic shared by the host runtime (api.cpp) and the HIP kernels
+// (scan.hip, freq.hip).  Everything here is __host__ __device__ so that the merge rules applied
+// across workgroups, across batches, and across GPUs (rank-ordered merge after the all-gather)
+// are literally the same code.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/deequ_amd.h"
+
+#define DQ_HD __host__ __device__ __forceinline__
+
+namespace dq {
+
+// ------------------------------------------------------------------------------------------------
+// Fused-scan task kinds.  The planner (api.cpp) maps every dq_agg of a suite onto a small set of
+// column tasks; each task reads its column buffers once per batch and produces one Acc.
+// ------------------------------------------------------------------------------------------------
+enum TaskKind : int32_t {
+  TK_NUMERIC = 1,    // one numeric column: n, Sum, Min, Max, (n, avg, m2), <= 3 fused predicates
+  TK_VALIDITY = 2,   // popcount(validity & where): Completeness numerator
+  TK_STR_IN = 3,     // [col IS NULL OR] col [NOT] IN ('a','b',...) on a utf8 column
+  TK_BOOLMAP = 4,    // counts over a materialised predicate bitmap (generic predicates / where)
+  TK_COMOMENTS = 5,  // two numeric columns: (n, xAvg, yAvg, ck, xMk, yMk)
+  TK_HLL = 6         // HLL++ registers (P = 9, 512 registers) of one column
+};
+
+constexpr int kMaxPreds = 3;          // fused predicates per TK_NUMERIC task
+constexpr int kHllP = 9;              // HyperLogLogPlusPlusUtils.P for RELATIVE_SD 0.05 (:155-159)
+constexpr int kHllM = 1 << kHllP;     // 512 registers
+constexpr int kHllWords = 52;         // NUM_WORDS (:152)
+constexpr int kHllRegsPerWord = 10;   // REGISTERS_PER_WORD
+constexpr int kHllRegBits = 6;        // REGISTER_SIZE
+constexpr int kBlock = 256;           // threads per scan workgroup (4 waves)
+constexpr int kRowsPerLane = 2;       // rows a lane owns per unrolled step
+constexpr int kUnroll = 8;            // unrolled steps per block iteration
+constexpr int kRowsPerIter = kBlock * kRowsPerLane * kUnroll;  // 4096 rows per block iteration
+
+// Fused numeric predicate:  [col IS NULL OR] (col op1 lo [AND col op2 hi])
+struct NumPred {
+  int32_t op1, op2;       // dq_xop comparison, op2 == 0 when absent
+  int32_t as_double;      // compare in double (Spark NaN-safe order) instead of int64
+  int32_t null_is_true;   // "col IS NULL OR ..." form
+  int64_t lo_i, hi_i;
+  double lo_d, hi_d;
+};
+
+// One task as the scan kernel sees it (uploaded per batch: it carries the batch's pointers).
+struct TaskDesc {
+  int32_t kind, type, type2, n_preds;
+  int32_t out;            // logical task = accumulator index
+  int32_t hll_out;        // HLL register-file index of the logical task (TK_HLL), else -1
+  int32_t hll_slot;       // HLL partial slot of this descriptor (TK_HLL), else -1
+  int32_t batch;          // batch index of this descriptor
+  int32_t negate;         // TK_STR_IN: NOT IN
+  int32_t null_is_true;   // TK_STR_IN: IS NULL OR ...
+  int32_t n_list;         // TK_STR_IN list length
+  int32_t vec_ok;         // buffers aligned for the vector path
+  int64_t rows;
+  int64_t item_rows;      // rows per work item (multiple of kRowsPerIter)
+  int64_t item_begin;     // first global item index of this task
+  int64_t n_items;
+  const uint8_t* valid;   // column 1
+  const void* values;
+  const uint8_t* data;
+  const uint8_t* valid2;  // column 2 (TK_COMOMENTS)
+  const void* values2;
+  const uint8_t* w_val;   // where bitmap (value bits), NULL = no where
+  const uint8_t* w_vld;   // where bitmap (validity bits), NULL = never NULL
+  const uint8_t* b_val;   // TK_BOOLMAP: counted expression bitmap (value bits)
+  const uint8_t* b_vld;   //            (validity bits)
+  const int32_t* list_off;    // TK_STR_IN list (device): offsets n_list+1
+  const uint8_t* list_bytes;  //                          bytes
+  const uint64_t* list_pre;   //                          first 8 bytes, packed LE
+  NumPred preds[kMaxPreds];
+};
+
+// Accumulator record: the aggregation buffer of one task.  128 bytes.
+//   TK_NUMERIC  : i0 n, i1 Long sum (wrapping), i2 min key, i3 max key, i4..6 pred TRUE,
+//                 i7..9 pred non-NULL; d0 double sum, d1 avg, d2 m2
+//   TK_VALIDITY : i0 count
+//   TK_STR_IN / TK_BOOLMAP : i0 TRUE count, i1 non-NULL count
+//   TK_COMOMENTS: i0 n; d0 xAvg, d1 yAvg, d2 ck, d3 xMk, d4 yMk
+struct alignas(16) Acc {
+  int64_t i[10];
+  double d[6];
+};
+
+DQ_HD void acc_init(int kind, Acc& a) {
+  for (int k = 0; k < 10; ++k) a.i[k] = 0;
+  for (int k = 0; k < 6; ++k) a.d[k] = 0.0;
+  if (kind == TK_NUMERIC) {
+    a.i[2] = INT64_MAX;  // min key
+    a.i[3] = INT64_MIN;  // max key
+  }
+}
+
+DQ_HD int64_t wrap_add(int64_t a, int64_t b) {
+  return (int64_t)((uint64_t)a + (uint64_t)b);
+}
+
+// Total-order key of a double that sorts like Spark's NaN-safe comparison (NaN largest).  Both
+// zeros keep their own keys (-0.0 < 0.0), so the extreme is deterministic.
+DQ_HD int64_t f64_key(double x) {
+  if (x != x) return INT64_MAX;
+  int64_t b = __builtin_bit_cast(int64_t, x);
+  return b >= 0 ? b : (b ^ INT64_MAX);
+}
+DQ_HD double f64_from_key(int64_t k) {
+  if (k == INT64_MAX) return __builtin_bit_cast(double, (int64_t)0x7ff8000000000000LL);
+  int64_t b = k >= 0 ? k : (k ^ INT64_MAX);
+  return __builtin_bit_cast(double, b);
+}
+
+// Chan et al. pairwise merge of (n, avg, m2), written as Spark's CentralMomentAgg merge /
+// StandardDeviationState.sum (StandardDeviation.scala:37-44).
+DQ_HD void moments_merge(double na, double& avg, double& m2, double nb, double avg_b, double m2_b) {
+  double n = na + nb;
+  double delta = avg_b - avg;
+  double delta_n = (n == 0.0) ? 0.0 : delta / n;
+  avg = avg + delta_n * nb;
+  m2 = m2 + m2_b + delta * delta_n * na * nb;
+}
+
+// Spark Corr merge / CorrelationState.sum (Correlation.scala:37-52).
+DQ_HD void comoments_merge(double n1, double* a, double n2, const double* b) {
+  double n = n1 + n2;
+  double dx = b[0] - a[0];
+  double dxn = (n == 0.0) ? 0.0 : dx / n;
+  double dy = b[1] - a[1];
+  double dyn = (n == 0.0) ? 0.0 : dy / n;
+  a[0] = a[0] + dxn * n2;
+  a[1] = a[1] + dyn * n2;
+  a[2] = a[2] + b[2] + dx * dyn * n1 * n2;
+  a[3] = a[3] + b[3] + dx * dxn * n1 * n2;
+  a[4] = a[4] + b[4] + dy * dyn * n1 * n2;
+}
+
+// Merge of two aggregation buffers of the same task (Spark's partial-aggregate merge).
+DQ_HD void acc_merge(int kind, Acc& a, const Acc& b) {
+  switch (kind) {
+    case TK_NUMERIC: {
+      if (b.i[0] == 0 && b.i[7] == 0 && b.i[8] == 0 && b.i[9] == 0) return;
+      double na = (double)a.i[0], nb = (double)b.i[0];
+      if (b.i[0] > 0) {
+        if (a.i[0] == 0) {
+          a.d[1] = b.d[1];
+          a.d[2] = b.d[2];
+        } else {
+          moments_merge(na, a.d[1], a.d[2], nb, b.d[1], b.d[2]);
+        }
+      }
+      a.i[0] += b.i[0];
+      a.i[1] = wrap_add(a.i[1], b.i[1]);
+      a.i[2] = a.i[2] < b.i[2] ? a.i[2] : b.i[2];
+      a.i[3] = a.i[3] > b.i[3] ? a.i[3] : b.i[3];
+      for (int k = 4; k < 10; ++k) a.i[k] += b.i[k];
+      a.d[0] += b.d[0];
+      break;
+    }
+    case TK_COMOMENTS: {
+      if (b.i[0] == 0) return;
+      if (a.i[0] == 0) {
+        a = b;
+        return;
+      }
+      comoments_merge((double)a.i[0], a.d, (double)b.i[0], b.d);
+      a.i[0] += b.i[0];
+      break;
+    }
+    default:
+      a.i[0] += b.i[0];
+      a.i[1] += b.i[1];
+      break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// XXH64 (Spark XXH64 == the standard algorithm over the value's little-endian bytes).
+// ------------------------------------------------------------------------------------------------
+constexpr uint64_t P1 = 0x9E3779B185EBCA87ULL;
+constexpr uint64_t P2 = 0xC2B2AE3D27D4EB4FULL;
+constexpr uint64_t P3 = 0x165667B19E3779F9ULL;
+constexpr uint64_t P4 = 0x85EBCA77C2B2AE63ULL;
+constexpr uint64_t P5 = 0x27D4EB2F165667C5ULL;
+
+DQ_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+DQ_HD uint64_t xxh_fmix(uint64_t h) {
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+// XXH64.hashLong(input, seed)
+DQ_HD uint64_t xxh_long(uint64_t v, uint64_t seed) {
+  uint64_t h = seed + P5 + 8;
+  uint64_t k = rotl64(v * P2, 31) * P1;
+  h ^= k;
+  h = rotl64(h, 27) * P1 + P4;
+  return xxh_fmix(h);
+}
+// XXH64.hashInt(input, seed)
+DQ_HD uint64_t xxh_int(uint32_t v, uint64_t seed) {
+  uint64_t h = seed + P5 + 4;
+  h ^= (uint64_t)v * P1;
+  h = rotl64(h, 23) * P2 + P3;
+  return xxh_fmix(h);
+}
+DQ_HD uint64_t xxh_round(uint64_t acc, uint64_t in) {
+  acc += in * P2;
+  acc = rotl64(acc, 31);
+  return acc * P1;
+}
+DQ_HD uint64_t xxh_merge_round(uint64_t acc, uint64_t v) {
+  acc ^= xxh_round(0, v);
+  return acc * P1 + P4;
+}
+
+// XXH64.hashUnsafeBytes over `len` bytes read through `Reader` (reader.u64(off), .u32(off),
+// .u8(off) return little-endian values at byte offset off).
+template <typename Reader>
+DQ_HD uint64_t xxh_bytes(const Reader& rd, int64_t len, uint64_t seed) {
+  int64_t off = 0;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+    int64_t limit = len - 32;
+    do {
+      v1 = xxh_round(v1, rd.u64(off));
+      v2 = xxh_round(v2, rd.u64(off + 8));
+      v3 = xxh_round(v3, rd.u64(off + 16));
+      v4 = xxh_round(v4, rd.u64(off + 24));
+      off += 32;
+    } while (off <= limit);
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = xxh_merge_round(h, v1);
+    h = xxh_merge_round(h, v2);
+    h = xxh_merge_round(h, v3);
+    h = xxh_merge_round(h, v4);
+  } else {
+    h = seed + P5;
+  }
+  h += (uint64_t)len;
+  while (off + 8 <= len) {
+    h ^= xxh_round(0, rd.u64(off));
+    h = rotl64(h, 27) * P1 + P4;
+    off += 8;
+  }
+  if (off + 4 <= len) {
+    h ^= (uint64_t)rd.u32(off) * P1;
+    h = rotl64(h, 23) * P2 + P3;
+    off += 4;
+  }
+  while (off < len) {
+    h ^= (uint64_t)rd.u8(off) * P5;
+    h = rotl64(h, 11) * P1;
+    off += 1;
+  }
+  return xxh_fmix(h);
+}
+
+struct HostBytes {
+  const uint8_t* p;
+  DQ_HD uint64_t u64(int64_t o) const {
+    uint64_t v = 0;
+    for (int k = 7; k >= 0; --k) v = (v << 8) | p[o + k];
+    return v;
+  }
+  DQ_HD uint32_t u32(int64_t o) const {
+    uint32_t v = 0;
+    for (int k = 3; k >= 0; --k) v = (v << 8) | p[o + k];
+    return v;
+  }
+  DQ_HD uint32_t u8(int64_t o) const { return p[o]; }
+};
+
+// HLL++ register update for one hash (StatefulHyperloglogPlus.update :87-113): index from the top
+// P bits, rank = number of leading zeros of the remaining bits (padded) + 1.
+DQ_HD void hll_index_rank(uint64_t x, uint32_t& idx, uint32_t& pw) {
+  idx = (uint32_t)(x >> (64 - kHllP));
+  uint64_t w = (x << kHllP) | (1ULL << (kHllP - 1));
+  pw = (uint32_t)__builtin_clzll(w) + 1;
+}
+
+}  // namespace dq

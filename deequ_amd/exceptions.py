@@ -1,0 +1,58 @@
+"""Exception hierarchy of runners/MetricCalculationException.scala:19-78."""
+from __future__ import annotations
+
+
+class MetricCalculationException(Exception):
+    pass
+
+
+class MetricCalculationRuntimeException(MetricCalculationException):
+    def __init__(self, message=None, cause: BaseException = None):
+        if cause is not None and message is None:
+            message = f"{type(cause).__name__}: {cause}"
+        super().__init__(message)
+        self.__cause__ = cause
+
+
+class MetricCalculationPreconditionException(MetricCalculationException):
+    pass
+
+
+class NoSuchColumnException(MetricCalculationPreconditionException):
+    pass
+
+
+class WrongColumnTypeException(MetricCalculationPreconditionException):
+    pass
+
+
+class NoColumnsSpecifiedException(MetricCalculationPreconditionException):
+    pass
+
+
+class NumberOfSpecifiedColumnsException(MetricCalculationPreconditionException):
+    pass
+
+
+class IllegalAnalyzerParameterException(MetricCalculationPreconditionException):
+    pass
+
+
+class EmptyStateException(MetricCalculationRuntimeException):
+    def __init__(self, message: str):
+        super().__init__(message)
+
+
+class AnalysisException(Exception):
+    """Stand-in for Spark's AnalysisException (unresolvable column / unparseable expression)."""
+
+
+class ReusingNotPossibleResultsMissingException(RuntimeError):
+    pass
+
+
+def wrap_if_necessary(exception: BaseException) -> MetricCalculationException:
+    """MetricCalculationException.wrapIfNecessary (MetricCalculationException.scala:69-76)."""
+    if isinstance(exception, MetricCalculationException):
+        return exception
+    return MetricCalculationRuntimeException(cause=exception)

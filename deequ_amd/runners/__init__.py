@@ -1,0 +1,303 @@
+"""AnalysisRunner (reference: analyzers/runners/AnalysisRunner.scala, AnalyzerContext.scala,
+AnalysisRunBuilder.scala, analyzers/Analysis.scala).
+
+The planning logic is the reference's, line by line in behaviour: repository reuse, precondition
+failures, the scan-shareable / grouping partition, ONE fused scan for every shareable analyzer
+(here: one engine launch instead of one Spark job), one frequency table per sorted grouping-column
+set with one shared aggregation over it, and failure isolation (a failing shared scan fails every
+shareable analyzer, a failing ``from_aggregation_result`` fails only its analyzer).
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+from ..analyzers.base import (Analyzer, GroupingAnalyzer, Preconditions, ScanShareableAnalyzer)
+from ..analyzers.grouping import (FrequenciesAndNumRows, ScanShareableFrequencyBasedAnalyzer,
+                                  compute_frequencies, frequency_row)
+from ..analyzers.scan import Size
+from ..exceptions import ReusingNotPossibleResultsMissingException
+from ..metrics import DoubleMetric
+from .engine import run_scan
+
+
+@dataclass
+class AnalyzerContext:
+    """AnalyzerContext.scala:29-42"""
+    metric_map: Dict[Analyzer, object] = field(default_factory=dict)
+
+    @staticmethod
+    def empty() -> "AnalyzerContext":
+        return AnalyzerContext({})
+
+    def all_metrics(self) -> list:
+        return list(self.metric_map.values())
+
+    def __add__(self, other: "AnalyzerContext") -> "AnalyzerContext":
+        merged = dict(self.metric_map)
+        merged.update(other.metric_map)  # right side wins, like Map ++ Map
+        return AnalyzerContext(merged)
+
+    def metric(self, analyzer: Analyzer):
+        return self.metric_map.get(analyzer)
+
+    @staticmethod
+    def success_metrics_as_rows(ctx: "AnalyzerContext", for_analyzers: Sequence = ()) -> list:
+        rows = []
+        for a, m in ctx.metric_map.items():
+            if for_analyzers and a not in for_analyzers:
+                continue
+            if not m.value.is_success:
+                continue
+            for d in m.flatten():
+                rows.append({"entity": str(d.entity), "instance": d.instance, "name": d.name,
+                             "value": d.value.get()})
+        return rows
+
+    @staticmethod
+    def success_metrics_as_json(ctx: "AnalyzerContext", for_analyzers: Sequence = ()) -> str:
+        return json.dumps(AnalyzerContext.success_metrics_as_rows(ctx, for_analyzers))
+
+
+@dataclass
+class AnalysisRunnerRepositoryOptions:
+    metrics_repository: object = None
+    reuse_existing_results_for_key: object = None
+    fail_if_results_for_reusing_missing: bool = False
+    save_or_append_results_with_key: object = None
+
+
+class AnalysisRunner:
+    """AnalysisRunner.scala"""
+
+    @staticmethod
+    def on_data(data) -> "AnalysisRunBuilder":
+        return AnalysisRunBuilder(data)
+
+    @staticmethod
+    def run(data, analysis: "Analysis", aggregate_with=None, save_states_with=None) -> AnalyzerContext:
+        return AnalysisRunner.do_analysis_run(data, analysis.analyzers, aggregate_with,
+                                              save_states_with)
+
+    @staticmethod
+    def do_analysis_run(data, analyzers: Sequence[Analyzer], aggregate_with=None,
+                        save_states_with=None,
+                        repository_options: Optional[AnalysisRunnerRepositoryOptions] = None
+                        ) -> AnalyzerContext:
+        """AnalysisRunner.doAnalysisRun (AnalysisRunner.scala:98-193)."""
+        if not analyzers:
+            return AnalyzerContext.empty()
+        opts = repository_options or AnalysisRunnerRepositoryOptions()
+        previous = AnalyzerContext.empty()
+        if opts.metrics_repository is not None and opts.reuse_existing_results_for_key is not None:
+            previous = opts.metrics_repository.load_by_key(
+                opts.reuse_existing_results_for_key) or AnalyzerContext.empty()
+        already = set(previous.metric_map.keys())
+        # dedupe preserving order (case classes: equal analyzers run once)
+        to_run: List[Analyzer] = []
+        for a in analyzers:
+            if a not in already and a not in to_run:
+                to_run.append(a)
+        if opts.fail_if_results_for_reusing_missing and to_run:
+            raise ReusingNotPossibleResultsMissingException(
+                "Could not find all necessary results in the MetricsRepository, the calculation of "
+                f"the metrics for these analyzers would be needed: {', '.join(map(str, to_run))}")
+        schema = data.schema
+        passed = [a for a in to_run if Preconditions.find_first_failing(schema, a.preconditions()) is None]
+        failed = [a for a in to_run if a not in passed]
+        precondition_failures = _precondition_failure_metrics(failed, schema)
+        grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]
+        scanning = [a for a in passed if a not in grouping]
+        non_grouped = _run_scanning_analyzers(data, scanning, aggregate_with, save_states_with)
+
+        num_rows = None
+        size_metric = non_grouped.metric(Size())
+        if size_metric is not None and size_metric.value.is_success:
+            num_rows = int(size_metric.value.get())
+
+        grouped = AnalyzerContext.empty()
+        groups: Dict[tuple, List[Analyzer]] = {}
+        for a in grouping:
+            groups.setdefault(tuple(sorted(a.grouping_columns())), []).append(a)
+        for cols, group in groups.items():
+            n, metrics = _run_grouping_analyzers(data, list(cols), group, aggregate_with,
+                                                 save_states_with, num_rows)
+            grouped = grouped + metrics
+            if num_rows is None:
+                num_rows = n
+        result = previous + precondition_failures + non_grouped + grouped
+        if opts.metrics_repository is not None and opts.save_or_append_results_with_key is not None:
+            current = opts.metrics_repository.load_by_key(opts.save_or_append_results_with_key) \
+                or AnalyzerContext.empty()
+            opts.metrics_repository.save(opts.save_or_append_results_with_key, current + result)
+        return result
+
+    @staticmethod
+    def run_on_aggregated_states(schema, analysis: "Analysis", state_loaders: Sequence,
+                                 save_states_with=None) -> AnalyzerContext:
+        """AnalysisRunner.runOnAggregatedStates (AnalysisRunner.scala:375-446): metrics from
+        persisted partition states, no data touched."""
+        from ..analyzers.state_provider import InMemoryStateProvider
+        if not analysis.analyzers or not state_loaders:
+            return AnalyzerContext.empty()
+        analyzers = list(analysis.analyzers)
+        passed = [a for a in analyzers if Preconditions.find_first_failing(schema, a.preconditions()) is None]
+        failed = [a for a in analyzers if a not in passed]
+        precondition_failures = _precondition_failure_metrics(failed, schema)
+        aggregated = InMemoryStateProvider()
+        for a in passed:
+            for loader in state_loaders:
+                a.aggregate_state_to(aggregated, loader, aggregated)
+        grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]
+        scanning = [a for a in passed if a not in grouping]
+        non_grouped = {}
+        for a in scanning:
+            m = a.load_state_and_compute_metric(aggregated)
+            if m is not None:
+                non_grouped[a] = m
+        grouped = AnalyzerContext.empty()
+        groups: Dict[tuple, List[Analyzer]] = {}
+        for a in grouping:
+            groups.setdefault(tuple(sorted(a.grouping_columns())), []).append(a)
+        for _, group in groups.items():
+            states = [aggregated.load(a) for a in group]
+            states = [s for s in states if s is not None]
+            if not states:
+                raise AssertionError("requirement failed")
+            grouped = grouped + _run_analyzers_for_particular_grouping(states[0], group,
+                                                                        save_states_with)
+        return precondition_failures + AnalyzerContext(non_grouped) + grouped
+
+
+def _precondition_failure_metrics(failed: Sequence[Analyzer], schema) -> AnalyzerContext:
+    out = {}
+    for a in failed:
+        e = Preconditions.find_first_failing(schema, a.preconditions())
+        out[a] = a.to_failure_metric(e)
+    return AnalyzerContext(out)
+
+
+def _run_scanning_analyzers(data, analyzers: Sequence[Analyzer], aggregate_with,
+                            save_states_with) -> AnalyzerContext:
+    """AnalysisRunner.runScanningAnalyzers (AnalysisRunner.scala:279-326)."""
+    shareable = [a for a in analyzers if isinstance(a, ScanShareableAnalyzer)]
+    others = [a for a in analyzers if not isinstance(a, ScanShareableAnalyzer)]
+    results: Dict[Analyzer, object] = {}
+    if shareable:
+        try:
+            aggregations = [spec for a in shareable for spec in a.aggregation_functions()]
+            offsets = [0]
+            for a in shareable:
+                offsets.append(offsets[-1] + len(a.aggregation_functions()))
+            row = run_scan(data, aggregations)  # ONE fused pass (the reference's single Spark job)
+            for a, off in zip(shareable, offsets):
+                try:
+                    results[a] = a.metric_from_aggregation_result(row, off, aggregate_with,
+                                                                  save_states_with)
+                except Exception as e:  # noqa: BLE001
+                    results[a] = a.to_failure_metric(e)
+        except Exception as e:  # noqa: BLE001
+            for a in shareable:
+                results[a] = a.to_failure_metric(e)
+    for a in others:
+        results[a] = a.calculate(data, aggregate_with, save_states_with)
+    return AnalyzerContext(results)
+
+
+def _run_grouping_analyzers(data, grouping_columns, analyzers, aggregate_with, save_states_with,
+                            num_rows_of_data):
+    """AnalysisRunner.runGroupingAnalyzers (AnalysisRunner.scala:249-277)."""
+    state = compute_frequencies(data, grouping_columns)
+    sample = analyzers[0]
+    if aggregate_with is not None:
+        prev = aggregate_with.load(sample)
+        if prev is not None:
+            state = state.sum(prev)
+    return state.num_rows, _run_analyzers_for_particular_grouping(state, analyzers, save_states_with)
+
+
+def _run_analyzers_for_particular_grouping(state: FrequenciesAndNumRows, analyzers,
+                                           save_states_with) -> AnalyzerContext:
+    """AnalysisRunner.runAnalyzersForParticularGrouping (AnalysisRunner.scala:466-534)."""
+    num_rows = state.num_rows
+    shareable = [a for a in analyzers if isinstance(a, ScanShareableFrequencyBasedAnalyzer)]
+    others = [a for a in analyzers if a not in shareable]
+    results: Dict[Analyzer, object] = {}
+    if shareable:
+        try:
+            aggs = [g for a in shareable for g in a.aggregation_functions(num_rows)]
+            offsets = [0]
+            for a in shareable:
+                offsets.append(offsets[-1] + len(a.aggregation_functions(num_rows)))
+            row = frequency_row(state.frequencies.summarize(), aggs, num_rows)
+            for a, off in zip(shareable, offsets):
+                try:
+                    results[a] = a.from_aggregation_result(row, off)
+                except Exception as e:  # noqa: BLE001
+                    results[a] = a.to_failure_metric(e)
+        except Exception as e:  # noqa: BLE001
+            for a in shareable:
+                results[a] = a.to_failure_metric(e)
+    try:
+        for a in others:
+            results[a] = a.compute_metric_from(state)
+    except Exception as e:  # noqa: BLE001
+        for a in others:
+            results[a] = a.to_failure_metric(e)
+    if save_states_with is not None:
+        save_states_with.persist(analyzers[0], state)
+    return AnalyzerContext(results)
+
+
+@dataclass
+class Analysis:
+    """analyzers/Analysis.scala"""
+    analyzers: List[Analyzer] = field(default_factory=list)
+
+    def add_analyzer(self, analyzer: Analyzer) -> "Analysis":
+        return Analysis(self.analyzers + [analyzer])
+
+    def add_analyzers(self, analyzers: Sequence[Analyzer]) -> "Analysis":
+        return Analysis(self.analyzers + list(analyzers))
+
+    def run(self, data, aggregate_with=None, save_states_with=None) -> AnalyzerContext:
+        return AnalysisRunner.do_analysis_run(data, self.analyzers, aggregate_with, save_states_with)
+
+
+class AnalysisRunBuilder:
+    """AnalysisRunBuilder.scala:61-186"""
+
+    def __init__(self, data):
+        self.data = data
+        self.analyzers: List[Analyzer] = []
+        self.repository_options = AnalysisRunnerRepositoryOptions()
+
+    def add_analyzer(self, analyzer: Analyzer) -> "AnalysisRunBuilder":
+        self.analyzers.append(analyzer)
+        return self
+
+    def add_analyzers(self, analyzers: Sequence[Analyzer]) -> "AnalysisRunBuilder":
+        self.analyzers.extend(analyzers)
+        return self
+
+    def use_repository(self, repository) -> "AnalysisRunBuilder":
+        self.repository_options.metrics_repository = repository
+        return self
+
+    def reuse_existing_results_for_key(self, key, fail_if_results_missing: bool = False):
+        self.repository_options.reuse_existing_results_for_key = key
+        self.repository_options.fail_if_results_for_reusing_missing = fail_if_results_missing
+        return self
+
+    def save_or_append_result(self, key) -> "AnalysisRunBuilder":
+        self.repository_options.save_or_append_results_with_key = key
+        return self
+
+    def run(self) -> AnalyzerContext:
+        return AnalysisRunner.do_analysis_run(self.data, self.analyzers,
+                                              repository_options=self.repository_options)
+
+
+__all__ = ["AnalyzerContext", "AnalysisRunner", "AnalysisRunBuilder", "Analysis",
+           "AnalysisRunnerRepositoryOptions", "DoubleMetric"]

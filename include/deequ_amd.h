@@ -1,0 +1,312 @@
+/*
+ * deequ_amd.h -- C ABI of the MI355X metric engine for deequ's metric-computation hot path.
+ *
+ * This is the drop-in boundary.  In the reference the hot path is reached
+ * through two Scala/Spark contracts, both of which this ABI replaces:
+ *
+ *   (1) ScanShareableAnalyzer.aggregationFunctions(): Seq[Column] + fromAggregationResult(Row, offset)
+ *       reference: src/main/scala/com/amazon/deequ/analyzers/Analyzer.scala:159-187, called once per
+ *       suite by AnalysisRunner.runScanningAnalyzers (analyzers/runners/AnalysisRunner.scala:279-326,
+ *       the single Spark job at :303).  -> dq_plan_create / dq_scan_device / dq_state_get
+ *   (2) Spark's aggregate SPI that those Columns wrap (initialize / update / merge / eval):
+ *       StatefulHyperloglogPlus.scala:74-146, StatefulStdDevPop.scala:24-34, StatefulCorrelation.scala:24-49
+ *       and Spark's Count / Sum / Min / Max.  -> the per-row update runs in the HIP scan kernels,
+ *       merge == dq_state_merge, eval == dq_state_get.
+ *   (3) FrequencyBasedAnalyzer.computeFrequencies (analyzers/GroupingAnalyzers.scala:53-80) plus the
+ *       one aggregation over the frequency table (AnalysisRunner.scala:466-534) and Histogram
+ *       (analyzers/Histogram.scala:54-116).  -> dq_freq_* (hash group-by on the GPU).
+ *
+ * Conventions (mirroring the reference's): the caller owns every column buffer and keeps it alive
+ * until dq_state_sync / dq_freq_summarize returns; the library never frees caller memory.  A plan is
+ * immutable and may be shared between threads; a dq_state / dq_freq belongs to one thread (one
+ * stream) at a time, like a Spark task's aggregation buffer.  No exception crosses this ABI: every
+ * entry point returns a dq_status, and dq_last_error() returns the thread-local message of the
+ * last failure (the host maps it to MetricCalculationRuntimeException, like
+ * MetricCalculationException.wrapIfNecessary, runners/MetricCalculationException.scala:69-76).
+ */
+#ifndef DEEQU_AMD_H
+#define DEEQU_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------------------------------
+ * Status codes
+ * ---------------------------------------------------------------------------------------------- */
+typedef enum dq_status {
+  DQ_OK = 0,
+  DQ_ERR_INVALID_ARGUMENT = 1, /* malformed plan / expression / argument                        */
+  DQ_ERR_NO_SUCH_COLUMN = 2,   /* column index out of range (NoSuchColumnException)             */
+  DQ_ERR_WRONG_TYPE = 3,       /* column type not valid for the aggregation (WrongColumnType...) */
+  DQ_ERR_OUT_OF_MEMORY = 4,    /* device allocation failed                                      */
+  DQ_ERR_DEVICE = 5,           /* HIP runtime error                                             */
+  DQ_ERR_UNSUPPORTED = 6,      /* valid request outside what this engine implements             */
+  DQ_ERR_STATE = 7             /* state / plan mismatch                                         */
+} dq_status;
+
+/* Thread-local message describing the last non-DQ_OK return on this thread. */
+const char* dq_last_error(void);
+/* ABI version (major*10000 + minor*100 + patch). */
+int dq_version(void);
+/* Number of HIP devices visible to this process (0 when there is no GPU). */
+int dq_device_count(void);
+
+/* ------------------------------------------------------------------------------------------------
+ * Columns: Arrow-style buffers (Arrow columnar format, offset 0).
+ * ---------------------------------------------------------------------------------------------- */
+typedef enum dq_type {
+  DQ_BOOL = 1,    /* Arrow "b": bit-packed values                                   */
+  DQ_INT8 = 2,    /* "c" */
+  DQ_INT16 = 3,   /* "s" */
+  DQ_INT32 = 4,   /* "i" */
+  DQ_INT64 = 5,   /* "l" */
+  DQ_FLOAT32 = 6, /* "f" */
+  DQ_FLOAT64 = 7, /* "g" */
+  DQ_UTF8 = 8     /* "u": int32 offsets (length+1) + bytes                           */
+} dq_type;
+
+typedef struct dq_column {
+  int32_t type;            /* dq_type                                                         */
+  int32_t reserved;
+  int64_t length;          /* rows                                                            */
+  const uint8_t* validity; /* LSB-first bitmap (1 = valid), NULL when the column has no nulls */
+  const void* values;      /* fixed-width values; for DQ_UTF8 the int32 offsets               */
+  const uint8_t* data;     /* DQ_UTF8 character bytes, otherwise NULL                         */
+} dq_column;
+
+/* Arrow C Data Interface (https://arrow.apache.org/docs/format/CDataInterface.html), verbatim. */
+#ifndef ARROW_C_DATA_INTERFACE
+#define ARROW_C_DATA_INTERFACE
+#define ARROW_FLAG_DICTIONARY_ORDERED 1
+#define ARROW_FLAG_NULLABLE 2
+#define ARROW_FLAG_MAP_KEYS_SORTED 4
+struct ArrowSchema {
+  const char* format;
+  const char* name;
+  const char* metadata;
+  int64_t flags;
+  int64_t n_children;
+  struct ArrowSchema** children;
+  struct ArrowSchema* dictionary;
+  void (*release)(struct ArrowSchema*);
+  void* private_data;
+};
+struct ArrowArray {
+  int64_t length;
+  int64_t null_count;
+  int64_t offset;
+  int64_t n_buffers;
+  int64_t n_children;
+  const void** buffers;
+  struct ArrowArray** children;
+  struct ArrowArray* dictionary;
+  void (*release)(struct ArrowArray*);
+  void* private_data;
+};
+#endif
+
+/* Converts one Arrow C Data Interface array (primitive or utf8, offset 0) into a dq_column that
+ * aliases the same buffers.  The JNI shim calls this on each exported
+ * DataFrame-partition column.  Buffers may be host or device pointers; the caller says which by
+ * the entry point it hands the column to. */
+dq_status dq_column_from_arrow(const struct ArrowArray* array, const struct ArrowSchema* schema,
+                               dq_column* out);
+
+/* ------------------------------------------------------------------------------------------------
+ * Expressions (SQL predicates of `where` filters and Compliance / Check constraints).
+ *
+ * An expression is a prefix-order sequence of int64 words.  The host compiles deequ's SQL strings
+ * (Check.scala:538-548, 670-760, 826-869; Analyzers.conditionalSelection Analyzer.scala:385-408)
+ * into it after Spark-2.2 type coercion, so the engine only sees typed operations.  Evaluation uses
+ * SQL three-valued logic (TRUE / FALSE / NULL) exactly like Catalyst.
+ * ---------------------------------------------------------------------------------------------- */
+typedef enum dq_xop {
+  DQ_X_COL = 1,        /* [op, column]                      value of a column                    */
+  DQ_X_NULL = 2,       /* [op]                              NULL literal                         */
+  DQ_X_BOOL = 3,       /* [op, 0|1]                         boolean literal                      */
+  DQ_X_I64 = 4,        /* [op, value]                       integral literal                     */
+  DQ_X_F64 = 5,        /* [op, bits]                        double literal (IEEE bits)           */
+  DQ_X_STR = 6,        /* [op, nbytes, ceil(n/8) words]     UTF-8 literal, little-endian packed  */
+  DQ_X_IS_NULL = 7,    /* [op, x]                                                                */
+  DQ_X_IS_NOT_NULL = 8,/* [op, x]                                                                */
+  DQ_X_NOT = 9,        /* [op, x]                                                                */
+  DQ_X_AND = 10,       /* [op, a, b]                        Kleene AND                           */
+  DQ_X_OR = 11,        /* [op, a, b]                        Kleene OR                            */
+  DQ_X_EQ = 12,        /* [op, a, b]  comparisons: numeric operands compared after promotion to  */
+  DQ_X_NE = 13,        /*             the wider type (double compare is Spark's NaN-safe order), */
+  DQ_X_LT = 14,        /*             strings compared bytewise (UTF8String.compareTo)           */
+  DQ_X_LE = 15,
+  DQ_X_GT = 16,
+  DQ_X_GE = 17,
+  DQ_X_EQ_NULL_SAFE = 18, /* <=> */
+  DQ_X_IN = 19,        /* [op, n, x, item_1 .. item_n]      x IN (items)                          */
+  DQ_X_CAST_F64 = 20   /* [op, x]                           CAST(x AS DOUBLE) (string: parse)    */
+} dq_xop;
+
+typedef struct dq_expr {
+  const int64_t* words;
+  int32_t n_words;
+  int32_t reserved;
+} dq_expr;
+
+/* ------------------------------------------------------------------------------------------------
+ * Scan plan: the concatenated aggregation functions of every ScanShareableAnalyzer of a suite, in
+ * analyzer order, exactly as AnalysisRunner builds `aggregations` and their `offsets`
+ * (AnalysisRunner.scala:296-301).  One dq_agg == one Column of aggregationFunctions().
+ * ---------------------------------------------------------------------------------------------- */
+typedef enum dq_agg_kind {
+  DQ_AGG_COUNT_ALL = 1,     /* count("*")                                   Size / Mean / ratios   */
+  DQ_AGG_COUNT_NOTNULL = 2, /* sum(isNotNull(when(where, col)).cast(Int))   Completeness.scala:44  */
+  DQ_AGG_COUNT_TRUE = 3,    /* sum(when(where, expr).cast(Int|Long))        Compliance.scala:48,
+                                                                            conditionalCount :404  */
+  DQ_AGG_SUM = 4,           /* sum(when(where, col))                        Sum.scala:35, Mean:39  */
+  DQ_AGG_MIN = 5,           /* min(when(where, col))                        Minimum.scala:36       */
+  DQ_AGG_MAX = 6,           /* max(when(where, col))                        Maximum.scala:36       */
+  DQ_AGG_STDDEV_POP = 7,    /* stateful_stddev_pop(when(where, col))        StandardDeviation:49   */
+  DQ_AGG_CORR = 8,          /* stateful_corr(when(where,x), when(where,y))  Correlation.scala:81   */
+  DQ_AGG_HLL = 9            /* stateful_approx_count_distinct(...)          ApproxCountDistinct:43 */
+} dq_agg_kind;
+
+typedef struct dq_agg {
+  int32_t kind;  /* dq_agg_kind                                           */
+  int32_t col;   /* input column (-1 for COUNT_ALL / COUNT_TRUE)          */
+  int32_t col2;  /* second column (CORR), else -1                         */
+  int32_t expr;  /* COUNT_TRUE: index of the counted expression, else -1  */
+  int32_t where; /* index of the `where` expression, -1 for none          */
+  int32_t reserved;
+} dq_agg;
+
+typedef struct dq_plan_desc {
+  int32_t n_columns;
+  const int32_t* column_types; /* dq_type per column index (the schema) */
+  int32_t n_exprs;
+  const dq_expr* exprs;
+  int32_t n_aggs;
+  const dq_agg* aggs;
+} dq_plan_desc;
+
+typedef struct dq_plan dq_plan;
+dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out);
+void dq_plan_destroy(dq_plan* plan);
+/* Human-readable listing of the fused tasks the planner produced (for tests / EXPLAIN). */
+dq_status dq_plan_explain(const dq_plan* plan, char* buf, size_t buf_len);
+/* Number of kernel launches one dq_scan_device call issues for this plan (the analogue of the
+ * reference's Spark-job-count assertions, AnalysisRunnerTests.scala:34-102). */
+int dq_plan_launches_per_batch(const dq_plan* plan);
+
+/* ------------------------------------------------------------------------------------------------
+ * Aggregation state: per-agg partial states, device resident while scanning.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct dq_state dq_state;
+/* device = -1 creates a host-only state (no GPU needed) that supports reset / deserialize /
+ * merge / get / serialize: the rank-ordered merge after a multi-GPU all-gather uses it. */
+dq_status dq_state_create(const dq_plan* plan, int device, dq_state** out);
+void dq_state_destroy(dq_state* state);
+dq_status dq_state_reset(dq_state* state);
+
+/* Scans one batch of rows whose buffers live in device memory.  Stream-ordered on `hip_stream`
+ * (a hipStream_t, NULL = default stream); results accumulate into `state` across batches like
+ * Spark partial aggregation over partitions.  cols[i] must match the plan schema. */
+dq_status dq_scan_device(const dq_plan* plan, const dq_column* cols, int n_cols, dq_state* state,
+                         void* hip_stream);
+/* Scans `n_batches` device-resident batches (cols is [n_batches][n_cols], row-major) in ONE fused
+ * launch: a DataFrame held as several Arrow record batches (int32 string offsets cap a batch at
+ * 2 GiB of characters) is still a single pass, like the reference's single Spark job. */
+dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column* cols, int n_cols,
+                                 int n_batches, dq_state* state, void* hip_stream);
+/* Waits for the state's stream and finalises the slot values on the host. */
+dq_status dq_state_sync(dq_state* state);
+
+/* One typed aggregation result (one slot of the reference's result Row).
+ *   COUNT_*  : i64 (is_null per Spark: a sum over no non-null input is NULL)
+ *   SUM      : integral input: i64 = wrapping Long sum, f64[0] = (double)i64; floating: f64[0]
+ *   MIN/MAX  : f64[0] (= cast of the native-typed extreme); i64 = the native integral extreme
+ *   STDDEV   : f64[0..2] = n, avg, m2 (never NULL; n == 0 means no input)
+ *   CORR     : f64[0..5] = n, xAvg, yAvg, ck, xMk, yMk
+ *   HLL      : words[0..51] = the 52 register words in reference order (never NULL)      */
+typedef struct dq_value {
+  int32_t kind;
+  int32_t is_null;
+  int64_t i64;
+  double f64[6];
+  uint64_t words[52];
+} dq_value;
+dq_status dq_state_get(const dq_state* state, int agg_index, dq_value* out);
+
+/* dst += src for two synced states of one plan: Spark's partial-aggregation merge of every
+ * aggregation buffer -- what happens between the partitions of ONE Spark job, and here between
+ * batches, workgroups and GPU ranks: counts add (a NULL sum is the identity), Long sums wrap,
+ * Min/Max in Spark's NaN-safe order, (n, avg, m2) per CentralMomentAgg merge ==
+ * StandardDeviationState.sum (StandardDeviation.scala:37-44), co-moments per Corr merge ==
+ * CorrelationState.sum (Correlation.scala:37-52), HLL register max (StatefulHyperloglogPlus.scala:
+ * 119-137).  deequ's analyzer-level State.sum (incremental runs) lives on the host side. */
+dq_status dq_state_merge(dq_state* dst, const dq_state* src);
+/* Fixed-size little-endian image of the synced slot values (for collectives / persistence). */
+int64_t dq_state_serialized_size(const dq_plan* plan);
+dq_status dq_state_serialize(const dq_state* state, void* buf, int64_t buf_len);
+dq_status dq_state_deserialize(dq_state* state, const void* buf, int64_t buf_len);
+
+/* HyperLogLogPlusPlusUtils.count (StatefulHyperloglogPlus.scala:208-255) on 52 register words.
+ * `bias_corrected` is set to 1 when the estimate fell in the empirical-bias range (E < 5M with no
+ * linear counting); that branch needs Spark's RAW_ESTIMATE_DATA/BIAS_DATA tables, which are not
+ * available here, so the raw estimate is returned there (documented parity gap). */
+double dq_hll_count(const uint64_t* words, int* bias_corrected);
+/* Spark XxHash64Function.hash(v, type, 42) for one value (host reference of the device hash). */
+uint64_t dq_xxhash64(const void* data, int64_t nbytes, uint64_t seed);
+
+/* ------------------------------------------------------------------------------------------------
+ * Frequency path: hash group-by (FrequencyBasedAnalyzer.computeFrequencies) on the GPU.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct dq_freq dq_freq;
+
+/* Creates an empty frequency table for grouping on `n_keys` columns of the given types.
+ * `capacity_hint` is the expected number of distinct groups (0 = unknown). */
+dq_status dq_freq_create(int device, int n_keys, const int32_t* key_types, int64_t capacity_hint,
+                         dq_freq** out);
+void dq_freq_destroy(dq_freq* freq);
+/* Inserts one batch: rows where any key is NULL are skipped but counted in numRows
+ * (GroupingAnalyzers.scala:62-77).  Histogram mode (null_as_group != 0) instead maps a NULL key
+ * to its own group, like na.fill("NullValue") (Histogram.scala:59-66). */
+dq_status dq_freq_add_device(dq_freq* freq, const dq_column* keys, int n_keys, int null_as_group,
+                             void* hip_stream);
+
+/* One aggregation over the frequency table (AnalysisRunner.scala:490-500):
+ *   n_unique  = Σ[count == 1]    (Uniqueness.scala:29, UniqueValueRatio.scala:28)
+ *   n_groups  = count(*)         (CountDistinct.scala:27, Distinctness via Σ[count >= 1])
+ *   entropy   = Σ −(c/numRows)·ln(c/numRows)   (Entropy.scala:33-40)
+ *   num_rows  = rows added, nulls included (data.count()) */
+typedef struct dq_freq_summary {
+  int64_t num_rows;
+  int64_t n_groups;
+  int64_t n_unique;
+  int64_t n_null_key_rows;
+  double entropy;
+} dq_freq_summary;
+dq_status dq_freq_summarize(dq_freq* freq, dq_freq_summary* out);
+
+/* Number of groups currently in the table (NULL group and every distinct key). */
+dq_status dq_freq_num_groups(dq_freq* freq, int64_t* n_groups);
+/* Rows added so far (nulls included): the numRows of FrequenciesAndNumRows. */
+int64_t dq_freq_num_rows(const dq_freq* freq);
+/* Exports every group (unordered): counts_out[n], key_offsets_out[n + 1] and the encoded keys:
+ * per key column a u32 tag (0 = NULL, 1 = value) followed by 8 little-endian value bytes (the
+ * value widened to 64 bits: integers sign-extended, float/double as their IEEE bits) or, for
+ * utf8, a u32 byte length and the bytes padded to a multiple of 4.  Call with key_bytes_out = NULL
+ * to learn the sizes (*key_bytes_needed, and dq_freq_num_groups for n). */
+dq_status dq_freq_export(dq_freq* freq, int64_t* counts_out, int64_t* key_offsets_out,
+                         uint8_t* key_bytes_out, int64_t capacity, int64_t key_bytes_capacity,
+                         int64_t* key_bytes_needed);
+/* dst += src: the null-safe full-outer-join merge of two frequency states
+ * (FrequenciesAndNumRows.sum, GroupingAnalyzers.scala:128-148): counts of equal keys add and
+ * numRows add. */
+dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DEEQU_AMD_H */

@@ -1,0 +1,91 @@
+"""ORACLE -- ctypes wrapper of oracle.c (test infrastructure only; never imported by deequ_amd)."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class OrNumeric(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_int64), ("sum_long", ctypes.c_int64), ("min", ctypes.c_int64),
+                ("max", ctypes.c_int64), ("n", ctypes.c_double), ("avg", ctypes.c_double),
+                ("m2", ctypes.c_double), ("pred_true", ctypes.c_int64),
+                ("pred_nonnull", ctypes.c_int64)]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+            subprocess.check_call(["make", "-C", _HERE, "-s"])
+        L = ctypes.CDLL(path)
+        vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        L.or_numeric_i64.argtypes = [vp, vp, i64, i32, i64, i32, ctypes.POINTER(OrNumeric)]
+        L.or_validity_count.argtypes = [vp, i64, i32]
+        L.or_validity_count.restype = i64
+        L.or_str_in.argtypes = [vp, vp, vp, i64, vp, vp, i32, i32, i32, ctypes.POINTER(i64),
+                                ctypes.POINTER(i64)]
+        L.or_xxh64.argtypes = [vp, i64, ctypes.c_uint64]
+        L.or_xxh64.restype = ctypes.c_uint64
+        L.or_hll.argtypes = [i32, vp, vp, vp, i64, i32, vp]
+        L.or_corr.argtypes = [vp, vp, vp, vp, i64, i32, vp]
+        L.or_freq_i64.argtypes = [vp, vp, i64, i64, ctypes.POINTER(i64), ctypes.POINTER(i64),
+                                  ctypes.POINTER(ctypes.c_double)]
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def numeric_i64(values: np.ndarray, valid_bits: np.ndarray, op: int = 0, lit: int = 0,
+                threads: int = 1) -> OrNumeric:
+    out = OrNumeric()
+    lib().or_numeric_i64(_p(values), _p(valid_bits), len(values), op, lit, threads,
+                         ctypes.byref(out))
+    return out
+
+
+def validity_count(valid_bits, n, threads=1) -> int:
+    return int(lib().or_validity_count(_p(valid_bits), n, threads))
+
+
+def str_in(offsets, data, valid_bits, n, items, null_is_true, threads=1):
+    lb = b"".join(i.encode() for i in items)
+    lo = np.array([0] + list(np.cumsum([len(i.encode()) for i in items])), np.int32)
+    lbuf = np.frombuffer(lb + b"\0", np.uint8)
+    t, nn = ctypes.c_int64(), ctypes.c_int64()
+    lib().or_str_in(_p(offsets), _p(data), _p(valid_bits), n, _p(lbuf), _p(lo), len(items),
+                    1 if null_is_true else 0, threads, ctypes.byref(t), ctypes.byref(nn))
+    return int(t.value), int(nn.value)
+
+
+def xxh64(data: bytes, seed: int = 42) -> int:
+    buf = np.frombuffer(data + b"\0", np.uint8)
+    return int(lib().or_xxh64(_p(buf), len(data), seed))
+
+
+def hll(type_code: int, values, data, valid_bits, n, threads=1) -> np.ndarray:
+    regs = np.zeros(512, np.uint8)
+    lib().or_hll(type_code, _p(values), _p(data), _p(valid_bits), n, threads, _p(regs))
+    return regs
+
+
+def corr(x, vx, y, vy, threads=1):
+    out = np.zeros(6, np.float64)
+    lib().or_corr(_p(x), _p(vx), _p(y), _p(vy), len(x), threads, _p(out))
+    return tuple(float(v) for v in out)
+
+
+def freq_i64(values, valid_bits, num_rows):
+    g, u, e = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+    lib().or_freq_i64(_p(values), _p(valid_bits), len(values), num_rows, ctypes.byref(g),
+                      ctypes.byref(u), ctypes.byref(e))
+    return int(g.value), int(u.value), float(e.value)

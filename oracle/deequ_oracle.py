@@ -1,0 +1,633 @@
+"""ORACLE -- test infrastructure only.  A CPU restatement of deequ's metric computation over Spark
+2.2 semantics, used by tests/ and bench.py's cpu_baseline as the checker.  The product (deequ_amd)
+never imports this module.
+
+Each function follows the cited reference file:line (prefix M/ = /root/reference/src/main/scala/
+com/amazon/deequ/).  Third-party semantics restated from Spark 2.2.2 (not vendored in the
+reference): CentralMomentAgg / Corr update+merge, Count/Sum/Min/Max, XXH64
+(checked against the `xxhash` 3.8.1 package), HyperLogLogPlusPlus register update, cast-to-string.
+
+Data model: a table is a dict {column: list of python values, None = NULL} plus a dict of Spark
+type names {column: "long" | "int" | "double" | "float" | "string" | "boolean"}.  Rows are
+processed sequentially per "partition" (Spark's per-task update loop), and partitions are merged
+with the aggregate's merge rule -- so the oracle reproduces Spark's evaluation order, not just its
+mathematics.
+
+Parity pinning: tests/test_oracle_golden.py checks this oracle against every known answer the
+reference's own tests hold (tests/golden/reference_known_answers.json, each with its file:line).
+"""
+from __future__ import annotations
+
+import math
+import re
+import struct
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import xxhash
+
+INT_TYPES = {"byte", "short", "int", "long"}
+NUM_TYPES = INT_TYPES | {"float", "double"}
+
+# ------------------------------------------------------------------------------------------------
+# SQL predicates (Spark SQL subset, three-valued logic) -- an independent little evaluator
+# ------------------------------------------------------------------------------------------------
+_TOK = re.compile(r"\s*(?:(\d+\.\d*(?:[eE][+-]?\d+)?|\d+(?:[eE][+-]?\d+)?)|('(?:[^']|'')*')|"
+                  r"(<=>|<=|>=|<>|!=|==|=|<|>|\(|\)|,)|([A-Za-z_][A-Za-z0-9_]*))")
+
+
+def _tokens(s: str):
+    pos, out = 0, []
+    s = s.strip()
+    while pos < len(s):
+        m = _TOK.match(s, pos)
+        if not m or m.end() == pos:
+            raise ValueError(f"oracle cannot parse {s[pos:]!r}")
+        pos = m.end()
+        num, st, op, ident = m.groups()
+        if num is not None:
+            out.append(("num", float(num) if any(c in num for c in ".eE") else int(num)))
+        elif st is not None:
+            out.append(("str", st[1:-1].replace("''", "'")))
+        elif op is not None:
+            out.append(("op", op))
+        else:
+            out.append(("id", ident))
+    return out
+
+
+class _P:
+    def __init__(self, toks):
+        self.t, self.i = toks, 0
+
+    def peek(self):
+        return self.t[self.i] if self.i < len(self.t) else (None, None)
+
+    def kw(self, w):
+        k, v = self.peek()
+        return k == "id" and v.upper() == w
+
+    def take(self):
+        self.i += 1
+        return self.t[self.i - 1]
+
+    def expr(self):
+        n = self.conj()
+        while self.kw("OR"):
+            self.take()
+            n = ("or", n, self.conj())
+        return n
+
+    def conj(self):
+        n = self.neg()
+        while self.kw("AND"):
+            self.take()
+            n = ("and", n, self.neg())
+        return n
+
+    def neg(self):
+        if self.kw("NOT"):
+            self.take()
+            return ("not", self.neg())
+        return self.pred()
+
+    def pred(self):
+        a = self.atom()
+        k, v = self.peek()
+        if k == "op" and v in ("=", "==", "<>", "!=", "<", "<=", ">", ">=", "<=>"):
+            self.take()
+            return ("cmp", {"==": "=", "!=": "<>"}.get(v, v), a, self.atom())
+        if self.kw("IS"):
+            self.take()
+            neg = False
+            if self.kw("NOT"):
+                self.take()
+                neg = True
+            self.take()  # NULL
+            return ("isnotnull" if neg else "isnull", a)
+        neg = False
+        if self.kw("NOT"):
+            self.take()
+            neg = True
+        if self.kw("IN"):
+            self.take()
+            self.take()  # (
+            items = [self.atom()]
+            while self.peek() == ("op", ","):
+                self.take()
+                items.append(self.atom())
+            self.take()  # )
+            n = ("in", a, items)
+            return ("not", n) if neg else n
+        if self.kw("BETWEEN"):
+            self.take()
+            lo = self.atom()
+            self.take()  # AND
+            hi = self.atom()
+            n = ("and", ("cmp", ">=", a, lo), ("cmp", "<=", a, hi))
+            return ("not", n) if neg else n
+        return a
+
+    def atom(self):
+        k, v = self.take()
+        if k == "op" and v == "(":
+            n = self.expr()
+            self.take()
+            return n
+        if k == "op" and v == "-":
+            _, num = self.take()
+            return ("lit", -num)
+        if k in ("num", "str"):
+            return ("lit", v)
+        if v.upper() == "NULL":
+            return ("lit", None)
+        if v.upper() in ("TRUE", "FALSE"):
+            return ("lit", v.upper() == "TRUE")
+        return ("col", v)
+
+
+def parse_predicate(sql: str):
+    return _P(_tokens(sql)).expr()
+
+
+def _to_double(v):
+    if isinstance(v, str):
+        try:
+            return float(v.strip())
+        except ValueError:
+            return None
+    return float(v)
+
+
+def _cmp3(a, b) -> Optional[int]:
+    """Spark ordering: numbers NaN-safe (NaN largest, NaN = NaN), strings bytewise UTF-8."""
+    if isinstance(a, str) and isinstance(b, str):
+        ab, bb = a.encode(), b.encode()
+        return (ab > bb) - (ab < bb)
+    if isinstance(a, str) or isinstance(b, str):
+        # Spark 2.2 PromoteStrings: cast the string side to double
+        a, b = _to_double(a), _to_double(b)
+        if a is None or b is None:
+            return None
+    if isinstance(a, bool) or isinstance(b, bool):
+        return (a > b) - (a < b)
+    if isinstance(a, float) or isinstance(b, float):
+        a, b = float(a), float(b)
+        an, bn = math.isnan(a), math.isnan(b)
+        if (an and bn) or a == b:
+            return 0
+        if an:
+            return 1
+        if bn:
+            return -1
+        return 1 if a > b else -1
+    return (a > b) - (a < b)
+
+
+def eval_predicate(node, row: Dict[str, object]):
+    """Evaluates to True / False / None (NULL)."""
+    op = node[0]
+    if op == "lit":
+        return node[1]
+    if op == "col":
+        name = node[1]
+        if name not in row:
+            low = {k.lower(): k for k in row}
+            if name.lower() not in low:
+                raise KeyError(f"cannot resolve {name}")
+            name = low[name.lower()]
+        return row[name]
+    if op == "isnull":
+        return eval_predicate(node[1], row) is None
+    if op == "isnotnull":
+        return eval_predicate(node[1], row) is not None
+    if op == "not":
+        v = eval_predicate(node[1], row)
+        return None if v is None else not v
+    if op == "and":
+        a, b = eval_predicate(node[1], row), eval_predicate(node[2], row)
+        if a is False or b is False:
+            return False
+        if a is None or b is None:
+            return None
+        return True
+    if op == "or":
+        a, b = eval_predicate(node[1], row), eval_predicate(node[2], row)
+        if a is True or b is True:
+            return True
+        if a is None or b is None:
+            return None
+        return False
+    if op == "cmp":
+        sym, a, b = node[1], eval_predicate(node[2], row), eval_predicate(node[3], row)
+        if sym == "<=>":
+            if a is None or b is None:
+                return a is None and b is None
+            return _cmp3(a, b) == 0
+        if a is None or b is None:
+            return None
+        c = _cmp3(a, b)
+        if c is None:
+            return None
+        return {"=": c == 0, "<>": c != 0, "<": c < 0, "<=": c <= 0, ">": c > 0, ">=": c >= 0}[sym]
+    if op == "in":
+        x = eval_predicate(node[1], row)
+        if x is None:
+            return None
+        items = [eval_predicate(i, row) for i in node[2]]
+        saw_null = False
+        for it in items:
+            if it is None:
+                saw_null = True
+                continue
+            if isinstance(x, str) != isinstance(it, str):
+                it = str(it) if isinstance(x, str) else it
+            if _cmp3(x, it) == 0:
+                return True
+        return None if saw_null else False
+    raise ValueError(op)
+
+
+# ------------------------------------------------------------------------------------------------
+# Table helpers
+# ------------------------------------------------------------------------------------------------
+class OTable:
+    def __init__(self, columns: Dict[str, list], types: Dict[str, str]):
+        self.columns = columns
+        self.types = types
+        self.n = len(next(iter(columns.values()))) if columns else 0
+
+    def rows(self):
+        names = list(self.columns)
+        for i in range(self.n):
+            yield {k: self.columns[k][i] for k in names}
+
+    def partitions(self, k: int) -> List["OTable"]:
+        """Contiguous row partitions (Spark's partitions of a parallelized collection)."""
+        bounds = [self.n * j // k for j in range(k + 1)]
+        return [OTable({c: v[bounds[j]:bounds[j + 1]] for c, v in self.columns.items()}, self.types)
+                for j in range(k)]
+
+
+def _sel(table: OTable, column: str, where: Optional[str]):
+    """conditionalSelection (M/analyzers/Analyzer.scala:385-402): when(where, col) -- NULL where
+    the filter is not TRUE."""
+    pred = parse_predicate(where) if where else None
+    vals = table.columns[column]
+    if pred is None:
+        return list(vals)
+    out = []
+    for i, r in enumerate(table.rows()):
+        out.append(vals[i] if eval_predicate(pred, r) is True else None)
+    return out
+
+
+def _to_long(v):
+    return int(v)
+
+
+def _wrap64(x: int) -> int:
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+# ------------------------------------------------------------------------------------------------
+# Scan aggregations: one partition's aggregation buffer at a time, then the merge
+# ------------------------------------------------------------------------------------------------
+def agg_count_all(t: OTable) -> int:
+    return t.n
+
+
+def agg_conditional_count(t: OTable, where: Optional[str]) -> Optional[int]:
+    """conditionalCount (Analyzer.scala:404-408): sum(expr(where).cast(Long)) else count(*)."""
+    if where is None:
+        return t.n
+    pred = parse_predicate(where)
+    vals = [eval_predicate(pred, r) for r in t.rows()]
+    nn = [v for v in vals if v is not None]
+    return None if not nn else sum(1 for v in nn if v)
+
+
+def agg_sum_notnull(t: OTable, column: str, where: Optional[str]) -> Optional[int]:
+    """Completeness numerator (Completeness.scala:44): sum(isNotNull(when(where,col)).cast(Int))."""
+    if t.n == 0:
+        return None
+    return sum(1 for v in _sel(t, column, where) if v is not None)
+
+
+def agg_compliance(t: OTable, predicate: str, where: Optional[str]) -> Optional[int]:
+    """Compliance.scala:47-49: sum(when(where, expr(predicate)).cast(Int))."""
+    p = parse_predicate(predicate)
+    w = parse_predicate(where) if where else None
+    vals = []
+    for r in t.rows():
+        if w is not None and eval_predicate(w, r) is not True:
+            vals.append(None)
+        else:
+            vals.append(eval_predicate(p, r))
+    nn = [v for v in vals if v is not None]
+    return None if not nn else sum(1 for v in nn if v)
+
+
+def agg_sum(t: OTable, column: str, where: Optional[str]) -> Optional[float]:
+    """Sum.scala:35: sum(col).cast(Double); integral columns sum as a wrapping Long first."""
+    vals = [v for v in _sel(t, column, where) if v is not None]
+    if not vals:
+        return None
+    if t.types[column] in INT_TYPES:
+        acc = 0
+        for v in vals:
+            acc = _wrap64(acc + int(v))
+        return float(acc)
+    acc = 0.0
+    for v in vals:
+        acc += float(v)
+    return acc
+
+
+def _nan_safe_lt(a: float, b: float) -> bool:
+    return _cmp3(a, b) < 0
+
+
+def agg_min(t: OTable, column: str, where: Optional[str]) -> Optional[float]:
+    """Minimum.scala:36 -- Spark's Min in the column type (NaN largest), then cast to double."""
+    vals = [v for v in _sel(t, column, where) if v is not None]
+    if not vals:
+        return None
+    m = vals[0]
+    for v in vals[1:]:
+        if _cmp3(v, m) < 0:
+            m = v
+    return float(m)
+
+
+def agg_max(t: OTable, column: str, where: Optional[str]) -> Optional[float]:
+    vals = [v for v in _sel(t, column, where) if v is not None]
+    if not vals:
+        return None
+    m = vals[0]
+    for v in vals[1:]:
+        if _cmp3(v, m) > 0:
+            m = v
+    return float(m)
+
+
+def moments_update(state, x: float):
+    """Spark 2.2 CentralMomentAgg.updateExpressions (momentOrder 2)."""
+    n, avg, m2 = state
+    n2 = n + 1.0
+    delta = x - avg
+    delta_n = delta / n2
+    avg2 = avg + delta_n
+    m22 = m2 + delta * (delta - delta_n)
+    return (n2, avg2, m22)
+
+
+def moments_merge(a, b):
+    """CentralMomentAgg.mergeExpressions == StandardDeviationState.sum
+    (M/analyzers/StandardDeviation.scala:37-44)."""
+    n1, avg1, m21 = a
+    n2, avg2, m22 = b
+    n = n1 + n2
+    delta = avg2 - avg1
+    delta_n = 0.0 if n == 0.0 else delta / n
+    return (n, avg1 + delta_n * n2, m21 + m22 + delta * delta_n * n1 * n2)
+
+
+def agg_stddev(t: OTable, column: str, where: Optional[str], partitions: int = 1):
+    """stateful_stddev_pop (M/analyzers/catalyst/StatefulStdDevPop.scala:24-34)."""
+    state = (0.0, 0.0, 0.0)
+    for p in t.partitions(partitions):
+        s = (0.0, 0.0, 0.0)
+        for v in _sel(p, column, where):
+            if v is not None:
+                s = moments_update(s, float(v))
+        state = moments_merge(state, s)
+    return state
+
+
+def corr_update(state, x: float, y: float):
+    """Spark 2.2 Corr.updateExpressions."""
+    n, xa, ya, ck, xmk, ymk = state
+    n2 = n + 1.0
+    dx = x - xa
+    dxn = dx / n2
+    dy = y - ya
+    dyn = dy / n2
+    xa2 = xa + dxn
+    ya2 = ya + dyn
+    ck2 = ck + dx * (y - ya2)
+    xmk2 = xmk + dx * (x - xa2)
+    ymk2 = ymk + dy * (y - ya2)
+    return (n2, xa2, ya2, ck2, xmk2, ymk2)
+
+
+def corr_merge(a, b):
+    """Corr.mergeExpressions == CorrelationState.sum (M/analyzers/Correlation.scala:37-52)."""
+    n1, xa1, ya1, ck1, xm1, ym1 = a
+    n2, xa2, ya2, ck2, xm2, ym2 = b
+    n = n1 + n2
+    dx = xa2 - xa1
+    dxn = 0.0 if n == 0.0 else dx / n
+    dy = ya2 - ya1
+    dyn = 0.0 if n == 0.0 else dy / n
+    return (n, xa1 + dxn * n2, ya1 + dyn * n2, ck1 + ck2 + dx * dyn * n1 * n2,
+            xm1 + xm2 + dx * dxn * n1 * n2, ym1 + ym2 + dy * dyn * n1 * n2)
+
+
+def agg_corr(t: OTable, cx: str, cy: str, where: Optional[str], partitions: int = 1):
+    state = (0.0,) * 6
+    for p in t.partitions(partitions):
+        s = (0.0,) * 6
+        for x, y in zip(_sel(p, cx, where), _sel(p, cy, where)):
+            if x is not None and y is not None:
+                s = corr_update(s, float(x), float(y))
+        state = corr_merge(state, s)
+    return state
+
+
+# ------------------------------------------------------------------------------------------------
+# XXH64 / HLL++ (StatefulHyperloglogPlus.scala:87-146, 150-255)
+# ------------------------------------------------------------------------------------------------
+P = 9
+M = 1 << P
+NUM_WORDS = 52
+
+
+def spark_xxhash64(value, spark_type: str, seed: int = 42) -> int:
+    """XxHash64Function.hash(v, type, seed) (Spark 2.2 HashExpression): standard XXH64 over the
+    little-endian bytes: long/double as 8 bytes (double via doubleToLongBits, NaN canonical),
+    int/short/byte/boolean/float as 4 bytes (float via floatToIntBits), string as its UTF-8."""
+    if spark_type == "string":
+        data = value.encode("utf-8")
+    elif spark_type in ("long",):
+        data = struct.pack("<q", int(value))
+    elif spark_type in ("int", "short", "byte"):
+        data = struct.pack("<i", int(value))
+    elif spark_type == "boolean":
+        data = struct.pack("<i", 1 if value else 0)
+    elif spark_type == "double":
+        d = float(value)
+        data = struct.pack("<Q", 0x7ff8000000000000) if math.isnan(d) else struct.pack("<d", d)
+    elif spark_type == "float":
+        if math.isnan(value):
+            data = struct.pack("<I", 0x7fc00000)
+        else:
+            data = struct.pack("<f", value)
+    else:
+        raise ValueError(spark_type)
+    return xxhash.xxh64_intdigest(data, seed=seed)
+
+
+def hll_registers(values, spark_type: str) -> List[int]:
+    regs = [0] * M
+    for v in values:
+        if v is None:
+            continue
+        x = spark_xxhash64(v, spark_type)
+        idx = x >> (64 - P)
+        w = ((x << P) & ((1 << 64) - 1)) | (1 << (P - 1))
+        pw = 64 - w.bit_length() + 1
+        if pw > regs[idx]:
+            regs[idx] = pw
+    return regs
+
+
+def hll_words(regs: Sequence[int]) -> List[int]:
+    words = []
+    for w in range(NUM_WORDS):
+        v = 0
+        for i in range(10):
+            idx = w * 10 + i
+            if idx < M:
+                v |= (regs[idx] & 0x3F) << (6 * i)
+        words.append(_wrap64(v))
+    return words
+
+
+def hll_count(words: Sequence[int]) -> Tuple[float, bool]:
+    """HyperLogLogPlusPlusUtils.count; returns (estimate, needed_bias_tables)."""
+    z_inv, V = 0.0, 0.0
+    idx = 0
+    for word in words:
+        word &= (1 << 64) - 1
+        for i in range(10):
+            if idx >= M:
+                break
+            m = (word >> (6 * i)) & 0x3F
+            z_inv += 1.0 / (1 << m)
+            if m == 0:
+                V += 1.0
+            idx += 1
+    alpha_m2 = (0.7213 / (1.0 + 1.079 / M)) * M * M
+    e = alpha_m2 / z_inv
+    biased = e < 5.0 * M
+    if V > 0:
+        H = M * math.log(M / V)
+        if H <= 400.0:
+            return float(math.floor(H + 0.5)), False
+    return float(math.floor(e + 0.5)), biased
+
+
+def agg_hll(t: OTable, column: str, where: Optional[str]) -> List[int]:
+    return hll_words(hll_registers(_sel(t, column, where), t.types[column]))
+
+
+# ------------------------------------------------------------------------------------------------
+# Frequencies (GroupingAnalyzers.scala:53-80) and the aggregations over them
+# ------------------------------------------------------------------------------------------------
+def _group_key(v, spark_type):
+    if spark_type in ("double", "float") and v is not None:
+        return struct.pack("<d", float(v))  # Spark 2.2 groups by binary value
+    return v
+
+
+def frequencies(t: OTable, columns: Sequence[str]) -> Dict[tuple, int]:
+    freq: Dict[tuple, int] = {}
+    cols = [t.columns[c] for c in columns]
+    for i in range(t.n):
+        key = tuple(c[i] for c in cols)
+        if any(k is None for k in key):
+            continue
+        key = tuple(_group_key(k, t.types[c]) for k, c in zip(key, columns))
+        freq[key] = freq.get(key, 0) + 1
+    return freq
+
+
+def uniqueness(freq, num_rows):
+    """Uniqueness.scala:29 (None == NULL -> empty state)."""
+    if not freq:
+        return None
+    return float(sum(1 for c in freq.values() if c == 1)) / num_rows
+
+
+def distinctness(freq, num_rows):
+    if not freq:
+        return None
+    return float(sum(1 for c in freq.values() if c >= 1)) / num_rows
+
+
+def unique_value_ratio(freq):
+    if not freq:
+        return None
+    return float(sum(1 for c in freq.values() if c == 1)) / float(len(freq))
+
+
+def count_distinct(freq):
+    return float(len(freq))
+
+
+def entropy(freq, num_rows):
+    """Entropy.scala:33-40 (summed in sorted-key order)."""
+    if not freq:
+        return None
+    total = 0.0
+    for c in freq.values():
+        p = c / num_rows
+        total += -p * math.log(p) if c else 0.0
+    return total
+
+
+def java_double_to_string(d: float) -> str:
+    if math.isnan(d):
+        return "NaN"
+    if math.isinf(d):
+        return "Infinity" if d > 0 else "-Infinity"
+    if d == 0.0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    r = repr(d)
+    mant, _, exp = r.partition("e")
+    digits = mant.replace("-", "").replace(".", "").lstrip("0").rstrip("0") or "0"
+    a = abs(d)
+    if 1e-3 <= a < 1e7:
+        s = ("%.17f" % a).rstrip("0")
+        # shortest: rebuild from repr digits
+        from decimal import Decimal
+        s = format(Decimal(repr(a)).normalize(), "f")
+        if "." not in s:
+            s += ".0"
+        return ("-" if d < 0 else "") + s
+    from decimal import Decimal
+    dec = Decimal(repr(a))
+    t = dec.as_tuple()
+    e10 = t.exponent + len(t.digits) - 1
+    ds = "".join(map(str, t.digits)).rstrip("0") or "0"
+    return ("-" if d < 0 else "") + ds[0] + "." + (ds[1:] or "0") + "E" + str(e10)
+
+
+def histogram(t: OTable, column: str) -> Tuple[Dict[str, int], int]:
+    """Histogram.scala:54-79: cast(col as string), NULL -> "NullValue", group, count."""
+    ty = t.types[column]
+    out: Dict[str, int] = {}
+    for v in t.columns[column]:
+        if v is None:
+            s = "NullValue"
+        elif ty == "string":
+            s = v
+        elif ty == "boolean":
+            s = "true" if v else "false"
+        elif ty in ("double", "float"):
+            s = java_double_to_string(float(v))
+        else:
+            s = str(int(v))
+        out[s] = out.get(s, 0) + 1
+    return out, t.n

@@ -1,0 +1,322 @@
+/*
+ * ORACLE -- test infrastructure only (never linked into or called by the product).
+ *
+ * C restatement of the Spark 2.2 / deequ per-row aggregation semantics for the benchmark
+ * workloads, used (a) by the GPU parity tests at 1e6..1e8 rows, where the pure-Python oracle
+ * (oracle/deequ_oracle.py) is too slow, and (b) as bench.py's `cpu_baseline` ("port": a CPU
+ * restatement of Spark 2.2 deequ semantics -- not Spark; no JVM exists in this image).
+ *
+ * Execution model = Spark local[N]: the rows are split into `nthreads` contiguous partitions, each
+ * partition runs the aggregate's sequential per-row update (Spark's partial aggregation), and the
+ * partition buffers are merged in partition order with the aggregate's merge rule.
+ *
+ * Cited semantics (M/ = /root/reference/src/main/scala/com/amazon/deequ/):
+ *   count / completeness   M/analyzers/Size.scala:36-40, M/analyzers/Completeness.scala:42-45
+ *   compliance             M/analyzers/Compliance.scala:47-49 (NULL predicate: not counted)
+ *   Sum (Long, wrapping)   M/analyzers/Sum.scala:35 + Spark Sum over LongType
+ *   Min / Max              M/analyzers/Minimum.scala:36, Maximum.scala:36
+ *   StdDev (Welford)       M/analyzers/catalyst/StatefulStdDevPop.scala:24-34 (CentralMomentAgg
+ *                          update), merge M/analyzers/StandardDeviation.scala:37-44
+ *   Correlation            M/analyzers/catalyst/StatefulCorrelation.scala:24-49 (Corr update),
+ *                          merge M/analyzers/Correlation.scala:37-52
+ *   HLL++ registers        M/analyzers/catalyst/StatefulHyperloglogPlus.scala:87-137
+ *   frequencies            M/analyzers/GroupingAnalyzers.scala:53-80, Entropy.scala:33-40
+ */
+#include <math.h>
+#include <omp.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+static inline int bit(const uint8_t* bm, int64_t r) { return bm ? (bm[r >> 3] >> (r & 7)) & 1 : 1; }
+
+/* ---------------------------------------------------------------- numeric column (S10) ---- */
+typedef struct {
+  int64_t count;      /* non-null values                     */
+  int64_t sum_long;   /* wrapping Long sum                   */
+  int64_t min, max;
+  double n, avg, m2;  /* CentralMomentAgg buffer             */
+  int64_t pred_true;  /* numViews >= lit (NULL not counted)  */
+  int64_t pred_nonnull;
+} or_numeric;
+
+static void numeric_merge(or_numeric* a, const or_numeric* b) {
+  if (b->count == 0) return;
+  if (a->count == 0) {
+    *a = *b;
+    return;
+  }
+  double n = a->n + b->n, delta = b->avg - a->avg, delta_n = n == 0.0 ? 0.0 : delta / n;
+  a->avg = a->avg + delta_n * b->n;
+  a->m2 = a->m2 + b->m2 + delta * delta_n * a->n * b->n;
+  a->n = n;
+  a->count += b->count;
+  a->sum_long = (int64_t)((uint64_t)a->sum_long + (uint64_t)b->sum_long);
+  if (b->min < a->min) a->min = b->min;
+  if (b->max > a->max) a->max = b->max;
+  a->pred_true += b->pred_true;
+  a->pred_nonnull += b->pred_nonnull;
+}
+
+/* op: 0 none, 12 '=', 13 '<>', 14 '<', 15 '<=', 16 '>', 17 '>=' (dq_xop numbering) */
+static inline int cmp_op(int op, int64_t x, int64_t lit) {
+  switch (op) {
+    case 12: return x == lit;
+    case 13: return x != lit;
+    case 14: return x < lit;
+    case 15: return x <= lit;
+    case 16: return x > lit;
+    case 17: return x >= lit;
+    default: return 0;
+  }
+}
+
+void or_numeric_i64(const int64_t* v, const uint8_t* valid, int64_t n, int op, int64_t lit,
+                    int nthreads, or_numeric* out) {
+  if (nthreads < 1) nthreads = 1;
+  or_numeric* parts = (or_numeric*)calloc((size_t)nthreads, sizeof(or_numeric));
+#pragma omp parallel for num_threads(nthreads) schedule(static, 1)
+  for (int p = 0; p < nthreads; ++p) {
+    int64_t r0 = n * p / nthreads, r1 = n * (p + 1) / nthreads;
+    or_numeric s;
+    memset(&s, 0, sizeof(s));
+    s.min = INT64_MAX;
+    s.max = INT64_MIN;
+    for (int64_t r = r0; r < r1; ++r) {
+      if (!bit(valid, r)) continue;
+      int64_t x = v[r];
+      s.count += 1;
+      s.sum_long = (int64_t)((uint64_t)s.sum_long + (uint64_t)x);
+      if (x < s.min) s.min = x;
+      if (x > s.max) s.max = x;
+      double xd = (double)x;
+      double n2 = s.n + 1.0, delta = xd - s.avg, delta_n = delta / n2;
+      s.avg += delta_n;
+      s.m2 += delta * (delta - delta_n);
+      s.n = n2;
+      if (op) {
+        s.pred_nonnull += 1;
+        s.pred_true += cmp_op(op, x, lit);
+      }
+    }
+    parts[p] = s;
+  }
+  or_numeric acc;
+  memset(&acc, 0, sizeof(acc));
+  acc.min = INT64_MAX;
+  acc.max = INT64_MIN;
+  for (int p = 0; p < nthreads; ++p) numeric_merge(&acc, &parts[p]);
+  *out = acc;
+  free(parts);
+}
+
+int64_t or_validity_count(const uint8_t* valid, int64_t n, int nthreads) {
+  if (!valid) return n;
+  int64_t total = 0;
+#pragma omp parallel for num_threads(nthreads) reduction(+ : total) schedule(static)
+  for (int64_t r = 0; r < n; ++r) total += bit(valid, r);
+  return total;
+}
+
+/* [col IS NULL OR] col IN (list): TRUE count and non-NULL count */
+void or_str_in(const int32_t* off, const uint8_t* data, const uint8_t* valid, int64_t n,
+               const uint8_t* list_bytes, const int32_t* list_off, int n_list, int null_is_true,
+               int nthreads, int64_t* t_out, int64_t* nn_out) {
+  int64_t t = 0, nn = 0;
+#pragma omp parallel for num_threads(nthreads) reduction(+ : t, nn) schedule(static)
+  for (int64_t r = 0; r < n; ++r) {
+    if (!bit(valid, r)) {
+      if (null_is_true) {
+        t += 1;
+        nn += 1;
+      }
+      continue;
+    }
+    int32_t s = off[r], len = off[r + 1] - off[r];
+    int match = 0;
+    for (int j = 0; j < n_list && !match; ++j) {
+      int32_t ls = list_off[j], ll = list_off[j + 1] - ls;
+      if (ll == len && memcmp(data + s, list_bytes + ls, (size_t)len) == 0) match = 1;
+    }
+    t += match;
+    nn += 1;
+  }
+  *t_out = t;
+  *nn_out = nn;
+}
+
+/* ---------------------------------------------------------------- XXH64 ------------------- */
+#define XP1 0x9E3779B185EBCA87ULL
+#define XP2 0xC2B2AE3D27D4EB4FULL
+#define XP3 0x165667B19E3779F9ULL
+#define XP4 0x85EBCA77C2B2AE63ULL
+#define XP5 0x27D4EB2F165667C5ULL
+
+static inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static inline uint64_t rd64(const uint8_t* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+static inline uint32_t rd32(const uint8_t* p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+static inline uint64_t xround(uint64_t acc, uint64_t in) { return rotl(acc + in * XP2, 31) * XP1; }
+static inline uint64_t xmerge(uint64_t acc, uint64_t v) { return (acc ^ xround(0, v)) * XP1 + XP4; }
+
+uint64_t or_xxh64(const uint8_t* p, int64_t len, uint64_t seed) {
+  const uint8_t* end = p + len;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+    const uint8_t* limit = end - 32;
+    do {
+      v1 = xround(v1, rd64(p));
+      v2 = xround(v2, rd64(p + 8));
+      v3 = xround(v3, rd64(p + 16));
+      v4 = xround(v4, rd64(p + 24));
+      p += 32;
+    } while (p <= limit);
+    h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    h = xmerge(h, v1);
+    h = xmerge(h, v2);
+    h = xmerge(h, v3);
+    h = xmerge(h, v4);
+  } else {
+    h = seed + XP5;
+  }
+  h += (uint64_t)len;
+  while (p + 8 <= end) {
+    h ^= xround(0, rd64(p));
+    h = rotl(h, 27) * XP1 + XP4;
+    p += 8;
+  }
+  if (p + 4 <= end) {
+    h ^= (uint64_t)rd32(p) * XP1;
+    h = rotl(h, 23) * XP2 + XP3;
+    p += 4;
+  }
+  while (p < end) {
+    h ^= (uint64_t)(*p) * XP5;
+    h = rotl(h, 11) * XP1;
+    ++p;
+  }
+  h ^= h >> 33;
+  h *= XP2;
+  h ^= h >> 29;
+  h *= XP3;
+  h ^= h >> 32;
+  return h;
+}
+
+static inline void hll_update(uint8_t* regs, uint64_t x) {
+  uint32_t idx = (uint32_t)(x >> 55);
+  uint64_t w = (x << 9) | (1ULL << 8);
+  uint8_t pw = (uint8_t)(__builtin_clzll(w) + 1);
+  if (pw > regs[idx]) regs[idx] = pw;
+}
+
+/* type: 5 = long (hashLong), 7 = double (doubleToLongBits), 8 = utf8 */
+void or_hll(int type, const void* values, const uint8_t* data, const uint8_t* valid, int64_t n,
+            int nthreads, uint8_t* regs_out) {
+  uint8_t* parts = (uint8_t*)calloc((size_t)nthreads * 512, 1);
+#pragma omp parallel for num_threads(nthreads) schedule(static, 1)
+  for (int p = 0; p < nthreads; ++p) {
+    uint8_t* regs = parts + (size_t)p * 512;
+    int64_t r0 = n * p / nthreads, r1 = n * (p + 1) / nthreads;
+    for (int64_t r = r0; r < r1; ++r) {
+      if (!bit(valid, r)) continue;
+      uint64_t x;
+      if (type == 8) {
+        const int32_t* off = (const int32_t*)values;
+        x = or_xxh64(data + off[r], off[r + 1] - off[r], 42);
+      } else if (type == 7) {
+        double d = ((const double*)values)[r];
+        uint64_t b;
+        if (d != d) b = 0x7ff8000000000000ULL;
+        else memcpy(&b, &d, 8);
+        x = or_xxh64((const uint8_t*)&b, 8, 42);
+      } else {
+        x = or_xxh64((const uint8_t*)&((const int64_t*)values)[r], 8, 42);
+      }
+      hll_update(regs, x);
+    }
+  }
+  memset(regs_out, 0, 512);
+  for (int p = 0; p < nthreads; ++p)
+    for (int i = 0; i < 512; ++i)
+      if (parts[(size_t)p * 512 + i] > regs_out[i]) regs_out[i] = parts[(size_t)p * 512 + i];
+  free(parts);
+}
+
+/* Corr over (long x, double y) */
+void or_corr(const int64_t* x, const uint8_t* vx, const double* y, const uint8_t* vy, int64_t n,
+             int nthreads, double* out6) {
+  double* parts = (double*)calloc((size_t)nthreads * 6, sizeof(double));
+#pragma omp parallel for num_threads(nthreads) schedule(static, 1)
+  for (int p = 0; p < nthreads; ++p) {
+    double s[6] = {0, 0, 0, 0, 0, 0};
+    int64_t r0 = n * p / nthreads, r1 = n * (p + 1) / nthreads;
+    for (int64_t r = r0; r < r1; ++r) {
+      if (!bit(vx, r) || !bit(vy, r)) continue;
+      double xv = (double)x[r], yv = y[r];
+      double n2 = s[0] + 1.0, dx = xv - s[1], dxn = dx / n2, dy = yv - s[2], dyn = dy / n2;
+      double xa = s[1] + dxn, ya = s[2] + dyn;
+      s[3] += dx * (yv - ya);
+      s[4] += dx * (xv - xa);
+      s[5] += dy * (yv - ya);
+      s[0] = n2;
+      s[1] = xa;
+      s[2] = ya;
+    }
+    memcpy(parts + 6 * p, s, sizeof(s));
+  }
+  double a[6] = {0, 0, 0, 0, 0, 0};
+  for (int p = 0; p < nthreads; ++p) {
+    const double* b = parts + 6 * p;
+    if (b[0] == 0.0) continue;
+    double n1 = a[0], n2 = b[0], nn = n1 + n2;
+    double dx = b[1] - a[1], dxn = nn == 0.0 ? 0.0 : dx / nn;
+    double dy = b[2] - a[2], dyn = nn == 0.0 ? 0.0 : dy / nn;
+    a[1] += dxn * n2;
+    a[2] += dyn * n2;
+    a[3] += b[3] + dx * dyn * n1 * n2;
+    a[4] += b[4] + dx * dxn * n1 * n2;
+    a[5] += b[5] + dy * dyn * n1 * n2;
+    a[0] = nn;
+  }
+  memcpy(out6, a, sizeof(a));
+  free(parts);
+}
+
+/* frequencies of a long column (NULLs skipped): groups, count==1 groups, entropy */
+static int cmp_i64(const void* a, const void* b) {
+  int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+  return (x > y) - (x < y);
+}
+void or_freq_i64(const int64_t* v, const uint8_t* valid, int64_t n, int64_t num_rows,
+                 int64_t* groups, int64_t* unique, double* ent) {
+  int64_t m = 0;
+  int64_t* buf = (int64_t*)malloc((size_t)(n > 0 ? n : 1) * 8);
+  for (int64_t r = 0; r < n; ++r)
+    if (bit(valid, r)) buf[m++] = v[r];
+  qsort(buf, (size_t)m, 8, cmp_i64);
+  int64_t g = 0, u = 0;
+  double e = 0.0;
+  for (int64_t i = 0; i < m;) {
+    int64_t j = i;
+    while (j < m && buf[j] == buf[i]) ++j;
+    int64_t c = j - i;
+    ++g;
+    u += c == 1;
+    double p = (double)c / (double)num_rows;
+    e += -p * log(p);
+    i = j;
+  }
+  *groups = g;
+  *unique = u;
+  *ent = e;
+  free(buf);
+}

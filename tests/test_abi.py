@@ -1,0 +1,99 @@
+"""CPU tests of the C ABI (no compute calls): the library loads, exports every symbol the header
+declares, plans compile (planning is host code), and host helpers agree with independent
+implementations."""
+import ctypes
+import os
+import re
+import struct
+import subprocess
+
+import pytest
+import xxhash
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "deequ_amd.h")).read()
+    return sorted(set(re.findall(r"\b(dq_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from deequ_amd import _native as N
+    out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (dq_[a-z0-9_]+)", out))
+    missing = [s for s in header_symbols() if s not in exported]
+    assert not missing, missing
+    assert set(N.EXPORTED) <= exported
+
+
+def test_version_and_device_count_callable_without_gpu():
+    from deequ_amd import _native as N
+    assert N.lib.dq_version() == 100
+    assert N.device_count() >= 0
+
+
+@pytest.mark.parametrize("data", [b"", b"a", b"high", b"0123456789abcdef" * 5, "ünï".encode()])
+def test_engine_xxhash_matches_package(data):
+    from deequ_amd import _native as N
+    assert N.xxhash64(data, 42) == xxhash.xxh64_intdigest(data, seed=42)
+
+
+def _table(cols, types):
+    from deequ_amd import _native as N
+    from deequ_amd.table import StructField, StructType
+    return StructType([StructField(c, t) for c, t in zip(cols, types)])
+
+
+def test_s10_plan_fuses_into_four_tasks_and_two_launches():
+    from deequ_amd import _native as N
+    from deequ_amd.analyzers import (Completeness, Compliance, Maximum, Mean, Minimum, Size,
+                                     StandardDeviation, Sum)
+    from deequ_amd.runners.engine import Plan
+    schema = _table(["id", "name", "priority", "numViews"], [N.INT64, N.UTF8, N.UTF8, N.INT64])
+    suite = [Size(), Completeness("id"), Completeness("name"),
+             Compliance("numViews is non-negative", "numViews >= 0"),
+             Compliance("priority contained in high,low",
+                        "priority IS NULL OR priority IN ('high','low')"),
+             Sum("numViews"), Mean("numViews"), StandardDeviation("numViews"),
+             Minimum("numViews"), Maximum("numViews")]
+    specs = [s for a in suite for s in a.aggregation_functions()]
+    plan = Plan(schema, specs)
+    text = plan.explain()
+    assert text.count("task[") == 4, text
+    assert "numeric col=3" in text and "str_in col=2" in text
+    assert plan.launches_per_batch == 2  # fused scan + finalize (the reference: one Spark job)
+
+
+def test_where_filters_materialise_once_per_distinct_expression():
+    from deequ_amd import _native as N
+    from deequ_amd.analyzers import Completeness, Maximum, Minimum
+    from deequ_amd.runners.engine import Plan
+    schema = _table(["item", "att1"], [N.UTF8, N.INT32])
+    suite = [Completeness("att1", "item IN ('1','2')"), Minimum("att1", "item IN ('1','2')"),
+             Maximum("att1", "item != '6'")]
+    plan = Plan(schema, [s for a in suite for s in a.aggregation_functions()])
+    text = plan.explain()
+    assert text.count("expr[") == 2, text
+
+
+def test_bad_expression_is_an_analysis_error():
+    from deequ_amd import _native as N
+    from deequ_amd.analyzers import Compliance
+    from deequ_amd.exceptions import AnalysisException
+    from deequ_amd.runners.engine import Plan
+    schema = _table(["att1"], [N.INT32])
+    with pytest.raises(AnalysisException):
+        Plan(schema, Compliance("r", "attNoSuchColumn > 3").aggregation_functions())
+
+
+def test_hll_count_matches_oracle_on_random_registers():
+    import random
+    from deequ_amd import _native as N
+    from oracle import deequ_oracle as O
+    rng = random.Random(5)
+    for trial in range(50):
+        regs = [rng.choice([0] * trial + list(range(1, 12))) for _ in range(512)]
+        words = O.hll_words(regs)
+        assert N.hll_count(words) == O.hll_count(words)

@@ -1,0 +1,212 @@
+"""GPU parity against the ORACLE on seeded random tables: every scan aggregation, null rates
+0 / 5 / 100 %, where filters, multi-batch tables, and the synthetic Item table (device generator
+vs the numpy restatement).  Bar: bit-exact for counts / Long sums / min / max / HLL registers /
+frequency counts; 1e-12 relative for fp64 moments (north_star)."""
+import math
+
+import numpy as np
+import pyarrow as pa
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-12
+
+
+def rel_close(a, b, rel=REL):
+    if isinstance(a, float) and math.isnan(a):
+        return isinstance(b, float) and math.isnan(b)
+    return a == b or abs(a - b) <= rel * max(abs(a), abs(b))
+
+
+def random_table(n, seed, null_rate):
+    rng = np.random.default_rng(seed)
+    def mask():
+        return rng.random(n) < null_rate
+    i64 = rng.integers(-10 ** 6, 10 ** 6, n)
+    f64 = rng.normal(1000.0, 250.0, n)
+    i32 = rng.integers(-50, 50, n).astype(np.int32)
+    cats = np.array(["high", "low", "medium", "", "NullValue", "x" * 20])
+    s = cats[rng.integers(0, len(cats), n)]
+    return pa.table({
+        "a": pa.array(i64, mask=mask(), type=pa.int64()),
+        "b": pa.array(f64, mask=mask(), type=pa.float64()),
+        "c": pa.array(i32, mask=mask(), type=pa.int32()),
+        "s": pa.array([None if m else v for v, m in zip(s, mask())], type=pa.string()),
+    })
+
+
+def oracle_of(t):
+    from oracle.deequ_oracle import OTable
+    types = {"a": "long", "b": "double", "c": "int", "s": "string"}
+    return OTable({k: t.column(k).to_pylist() for k in t.column_names}, types)
+
+
+@pytest.mark.parametrize("n,null_rate,batch", [(1, 0.0, None), (1000, 0.0, None),
+                                               (4097, 0.05, None), (50_000, 0.05, 8192),
+                                               (70_000, 1.0, None), (20_011, 0.3, 4096)])
+def test_scan_suite_matches_oracle(n, null_rate, batch, gpu_device):
+    from deequ_amd import Analysis, Table
+    from deequ_amd.analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlation,
+                                     Maximum, Mean, Minimum, Size, StandardDeviation, Sum)
+    from oracle import deequ_oracle as O
+    t = random_table(n, n, null_rate)
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=batch)
+    ot = oracle_of(t)
+    where = "c > -20"
+    suite = [Size(), Size(where), Completeness("a"), Completeness("s", where),
+             Compliance("nn", "a >= 0"), Compliance("in", "s IS NULL OR s IN ('high','low')"),
+             Compliance("rng", "b IS NULL OR (b >= 900.0 AND b <= 1100.0)"),
+             Compliance("w", "c < 10", where), Compliance("x", "a > c"),
+             Sum("a"), Sum("b"), Sum("c", where), Mean("a"), Mean("b", where),
+             Minimum("a"), Maximum("a"), Minimum("b"), Maximum("c", where),
+             StandardDeviation("a"), StandardDeviation("b"), StandardDeviation("c", where),
+             Correlation("a", "b"), Correlation("c", "b", where),
+             ApproxCountDistinct("a"), ApproxCountDistinct("s"), ApproxCountDistinct("b", where)]
+    ctx = Analysis(suite).run(df)
+
+    def state(a):
+        return a.from_aggregation_result(_row(df, a), 0)
+
+    # counts and Long sums: bit-exact
+    assert ctx.metric(Size()).value.get() == n
+    exp = O.agg_conditional_count(ot, where)
+    st = _state_of(df, Size(where))
+    assert (None if st is None else st.num_matches) == exp
+    assert _state_of(df, Completeness("a")).num_matches == O.agg_sum_notnull(ot, "a", None)
+    for name, pred, w in [("nn", "a >= 0", None), ("in", "s IS NULL OR s IN ('high','low')", None),
+                          ("rng", "b IS NULL OR (b >= 900.0 AND b <= 1100.0)", None),
+                          ("w", "c < 10", where), ("x", "a > c", None)]:
+        st = _state_of(df, Compliance(name, pred, w))
+        exp = O.agg_compliance(ot, pred, w)
+        assert (st.num_matches if st else None) == exp, name
+    for col, w in [("a", None), ("c", where)]:
+        st = _state_of(df, Sum(col, w))
+        exp = O.agg_sum(ot, col, w)
+        assert (None if st is None else st.sum_value) == exp
+    st = _state_of(df, Sum("b"))
+    exp = O.agg_sum(ot, "b", None)
+    assert (st is None and exp is None) or rel_close(st.sum_value, exp, 1e-11)
+    for a, fn in [(Minimum("a"), O.agg_min), (Maximum("a"), O.agg_max), (Minimum("b"), O.agg_min)]:
+        st = _state_of(df, a)
+        exp = fn(ot, a.column, a.where)
+        assert (None if st is None else (st.min_value if hasattr(st, "min_value") else st.max_value)) == exp
+    # fp64 moments: 1e-12 relative
+    for col, w in [("a", None), ("b", None), ("c", where)]:
+        st = _state_of(df, StandardDeviation(col, w))
+        n_, avg, m2 = O.agg_stddev(ot, col, w)
+        if n_ == 0:
+            assert st is None
+        else:
+            assert st.n == n_ and rel_close(st.avg, avg) and rel_close(st.m2, m2, 1e-11)
+            assert rel_close(st.metric_value(), math.sqrt(m2 / n_))
+    for x, y, w in [("a", "b", None), ("c", "b", where)]:
+        st = _state_of(df, Correlation(x, y, w))
+        exp = O.agg_corr(ot, x, y, w)
+        if exp[0] == 0:
+            assert st is None
+        else:
+            assert st.n == exp[0]
+            got = st.metric_value()
+            ref = exp[3] / math.sqrt(exp[4] * exp[5]) if exp[4] * exp[5] > 0 else float("nan")
+            assert rel_close(got, ref, 1e-10)
+    # HLL registers: bit-exact
+    for col, w in [("a", None), ("s", None), ("b", where)]:
+        st = _state_of(df, ApproxCountDistinct(col, w))
+        assert list(st.words) == O.agg_hll(ot, col, w), col
+
+
+def _row(df, analyzer):
+    from deequ_amd.runners.engine import run_scan
+    return run_scan(df, analyzer.aggregation_functions())
+
+
+def _state_of(df, analyzer):
+    return analyzer.from_aggregation_result(_row(df, analyzer), 0)
+
+
+@pytest.mark.parametrize("n,batch", [(100_000, 1 << 14), (300_001, None)])
+def test_synthetic_item_table_device_equals_numpy(n, batch, gpu_device):
+    import torch
+    from deequ_amd.synth import item_columns_numpy, item_table_device
+    df = item_table_device(n, seed=11, batch_rows=batch or (1 << 26), device=gpu_device)
+    ref = item_columns_numpy(n, seed=11)
+    ids, vw = [], []
+    valid = {"id": [], "numViews": []}
+    prio, names = [], []
+    for b in df.batches:
+        m = b["id"].length
+        ids.append(b["id"].values[:m].cpu().numpy())
+        vw.append(b["numViews"].values[:m].cpu().numpy())
+        for c in ("id", "numViews"):
+            bits = np.unpackbits(b[c].validity.cpu().numpy(), bitorder="little")[:m]
+            valid[c].append(bits.astype(bool))
+        for c, out in (("priority", prio), ("name", names)):
+            off = b[c].values[: m + 1].cpu().numpy()
+            data = b[c].data.cpu().numpy().tobytes()
+            bits = np.unpackbits(b[c].validity.cpu().numpy(), bitorder="little")[:m]
+            out.extend(data[off[i]:off[i + 1]].decode() if bits[i] else None for i in range(m))
+    assert np.array_equal(np.concatenate(valid["id"]), ref["id_valid"])
+    assert np.array_equal(np.concatenate(ids), ref["id"])
+    assert np.array_equal(np.concatenate(valid["numViews"]), ref["numViews_valid"])
+    assert np.array_equal(np.concatenate(vw), ref["numViews"])
+    assert prio == ref["priority"]
+    assert names == ref["name"]
+
+
+def test_s10_on_synthetic_items_matches_c_oracle(gpu_device):
+    """S10 on 2^22 + 12345 synthetic rows in 3 batches vs the C oracle (Spark local[16])."""
+    from deequ_amd import Analysis
+    from deequ_amd.analyzers import (Completeness, Compliance, Maximum, Mean, Minimum, Size,
+                                     StandardDeviation, Sum)
+    from deequ_amd.synth import item_table_device
+    from oracle import c_oracle as C
+    n = (1 << 22) + 12345
+    df = item_table_device(n, seed=3, batch_rows=1 << 21, device=gpu_device)
+    suite = s10_suite()
+    ctx = Analysis(suite).run(df)
+    # oracle over the same device buffers copied to the host, batch by batch
+    num = None
+    comp_id = comp_name = 0
+    pt = pn = 0
+    parts = []
+    for b in df.batches:
+        m = b["id"].length
+        v = b["numViews"].values[:m].cpu().numpy()
+        vb = b["numViews"].validity.cpu().numpy()
+        parts.append(C.numeric_i64(v, vb, op=17, lit=0, threads=16))
+        comp_id += C.validity_count(b["id"].validity.cpu().numpy(), m, 16)
+        comp_name += C.validity_count(b["name"].validity.cpu().numpy(), m, 16)
+        t, nn = C.str_in(b["priority"].values.cpu().numpy(), b["priority"].data.cpu().numpy(),
+                         b["priority"].validity.cpu().numpy(), m, ["high", "low"], True, 16)
+        pt += t
+        pn += nn
+    cnt = sum(p.count for p in parts)
+    s = sum(p.sum_long for p in parts)
+    assert ctx.metric(Size()).value.get() == n
+    assert ctx.metric(Completeness("id")).value.get() == comp_id / n
+    assert ctx.metric(Completeness("name")).value.get() == comp_name / n
+    assert ctx.metric(suite[3]).value.get() == sum(p.pred_true for p in parts) / n
+    assert ctx.metric(suite[4]).value.get() == pt / n
+    assert ctx.metric(Sum("numViews")).value.get() == float(s)
+    assert ctx.metric(Mean("numViews")).value.get() == float(s) / n
+    assert ctx.metric(Minimum("numViews")).value.get() == float(min(p.min for p in parts))
+    assert ctx.metric(Maximum("numViews")).value.get() == float(max(p.max for p in parts))
+    # merge the per-batch Welford states like Spark partitions
+    from oracle.deequ_oracle import moments_merge
+    st = (0.0, 0.0, 0.0)
+    for p in parts:
+        st = moments_merge(st, (p.n, p.avg, p.m2))
+    assert rel_close(ctx.metric(StandardDeviation("numViews")).value.get(),
+                     math.sqrt(st[2] / st[0]))
+
+
+def s10_suite():
+    from deequ_amd.analyzers import (Completeness, Compliance, Maximum, Mean, Minimum, Size,
+                                     StandardDeviation, Sum)
+    return [Size(), Completeness("id"), Completeness("name"),
+            Compliance("numViews is Fnon-negative", "numViews >= 0"),
+            Compliance("priority contained in high,low",
+                       "priority IS NULL OR priority IN ('high','low')"),
+            Sum("numViews"), Mean("numViews"), StandardDeviation("numViews"),
+            Minimum("numViews"), Maximum("numViews")]
