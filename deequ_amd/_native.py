@@ -76,6 +76,10 @@ def _load() -> ctypes.CDLL:
         raise ImportError(
             f"{LIB_PATH} is missing: build the HIP engine first (python -c "
             "'import __graft_entry__ as g; g.build()' or make -C deequ_amd/csrc)")
+    # One HIP runtime per process: torch's wheel bundles libamdhip64 (soname libamdhip64.so.7).
+    # Loading torch first lets our DT_NEEDED libamdhip64.so.7 bind to that same copy; loading
+    # /opt/rocm's first would leave two HSA runtimes in the process and the second finds no device.
+    import torch  # noqa: F401
     lib = ctypes.CDLL(LIB_PATH)
     sig = {
         "dq_last_error": (c_char_p, []),

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -353,6 +354,26 @@ struct dq_plan {
   bool full = false;            // needs the full kernel family (hashing / co-moments / int8/16)
 };
 
+// Scan kernel instantiation that runs a task (kernels.h BodyClass).
+static int body_class(const dq_plan* p, const TaskPlan& t) {
+  switch (t.kind) {
+    case TK_NUMERIC:
+      switch (p->types[t.col]) {
+        case DQ_INT8: return BC_NUM_I8;
+        case DQ_INT16: return BC_NUM_I16;
+        case DQ_INT32: return BC_NUM_I32;
+        case DQ_INT64: return BC_NUM_I64;
+        case DQ_FLOAT32: return BC_NUM_F32;
+        default: return BC_NUM_F64;
+      }
+    case TK_VALIDITY:
+    case TK_BOOLMAP: return BC_BITS;
+    case TK_STR_IN: return BC_STR_IN;
+    case TK_COMOMENTS: return BC_CORR;
+    default: return BC_HLL;
+  }
+}
+
 static int mat_index(dq_plan* p, int expr) {
   auto it = p->mat_of.find(expr);
   if (it != p->mat_of.end()) return it->second;
@@ -552,11 +573,12 @@ extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
   p->n_hll = n_hll;
   for (Slot& s : p->slots)
     if (s.task >= 0) s.task = remap[s.task];
-  for (const TaskPlan& t : p->tasks) {
+  for (const TaskPlan& t : p->tasks)
     if (t.kind == TK_HLL || t.kind == TK_COMOMENTS) p->full = true;
-    if (t.kind == TK_NUMERIC && (p->types[t.col] == DQ_INT8 || p->types[t.col] == DQ_INT16))
-      p->full = true;
-  }
+  // each workgroup keeps every HLL task's 512 registers in LDS (2 KiB per task)
+  if (p->n_hll > 32)
+    return fail(DQ_ERR_UNSUPPORTED, "%d ApproxCountDistinct aggregations in one plan (max 32)",
+                p->n_hll);
   *out = p.release();
   return DQ_OK;
 }
@@ -600,7 +622,14 @@ extern "C" dq_status dq_plan_explain(const dq_plan* plan, char* buf, size_t buf_
 
 extern "C" int dq_plan_launches_per_batch(const dq_plan* plan) {
   if (!plan) return 0;
-  return (int)plan->mat.size() + (plan->tasks.empty() ? 0 : 2);
+  int classes = 0;
+  for (int c = 0; c < kBodyClasses; ++c) {
+    bool used = false;
+    for (const TaskPlan& t : plan->tasks) used = used || body_class(plan, t) == c;
+    classes += used ? 1 : 0;
+  }
+  // expression bitmaps + one scan launch per body class + the two finalize launches
+  return (int)plan->mat.size() + classes + (plan->tasks.empty() ? 0 : 2);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -609,7 +638,7 @@ extern "C" int dq_plan_launches_per_batch(const dq_plan* plan) {
 struct dq_state {
   const dq_plan* plan = nullptr;
   int device = 0;
-  int grid_max = 0;
+  int grid[kBodyClasses] = {};   // persistent grid of each scan kernel instantiation
   hipStream_t stream = nullptr;
   bool stream_set = false;
   // host mirror
@@ -619,8 +648,10 @@ struct dq_state {
   bool host_dirty = false;   // host mirror newer than device (after merge / deserialize / reset)
   bool synced = true;        // host mirror reflects every scanned batch
   // device
-  DevBuf<Acc> d_acc, d_partial;
-  DevBuf<uint8_t> d_hll, d_hll_partial;
+  DevBuf<Acc> d_acc, d_partial, d_partial2;
+  DevBuf<uint8_t> d_hll;
+  DevBuf<uint32_t> d_hll_stage;  // per-launch HLL registers (u32), kept zero between launches
+  DevBuf<uint32_t> d_queue;      // work-item counter of the scan kernel, kept zero between launches
   DevBuf<TaskDesc> d_tasks[2];
   TaskDesc* h_tasks[2] = {nullptr, nullptr};
   size_t h_tasks_cap[2] = {0, 0};
@@ -636,11 +667,11 @@ struct dq_state {
   DevBuf<DevCol> d_cols[2];
   DevCol* h_cols[2] = {nullptr, nullptr};
   size_t h_cols_cap[2] = {0, 0};
-  // STR_IN lists per task
-  DevBuf<int32_t> d_list_off;
-  DevBuf<uint8_t> d_list_bytes;
+  // STR_IN lists per task (entries sorted by length, see TaskDesc)
+  DevBuf<int32_t> d_list_i32;    // per task: start[kListLenSlots + 2], len[n], boff[n]
   DevBuf<uint64_t> d_list_pre;
-  std::vector<int64_t> list_off_base, list_byte_base, list_pre_base;
+  DevBuf<uint8_t> d_list_bytes;
+  std::vector<int64_t> list_i32_base, list_pre_base, list_byte_base;
   ~dq_state() {
     for (int k = 0; k < 2; ++k) {
       if (h_tasks[k]) (void)hipHostFree(h_tasks[k]);
@@ -667,6 +698,8 @@ static dq_status upload_host(dq_state* s) {
     HIP_TRY(hipMemcpy(s->d_acc.p, s->acc.data(), s->acc.size() * sizeof(Acc), hipMemcpyHostToDevice));
   if (!s->hll.empty())
     HIP_TRY(hipMemcpy(s->d_hll.p, s->hll.data(), s->hll.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(s->d_queue.p, 0, kBodyClasses * sizeof(uint32_t)));
+  HIP_TRY(hipMemset(s->d_hll_stage.p, 0, s->d_hll_stage.n * sizeof(uint32_t)));
   s->host_dirty = false;
   return DQ_OK;
 }
@@ -689,13 +722,18 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
   HIP_TRY(hipSetDevice(device));
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  int per_cu = scan_max_blocks_per_cu(plan->full);
-  s->grid_max = std::max(1, cus * std::min(per_cu, 8));
+  for (int c = 0; c < kBodyClasses; ++c) s->grid[c] = 0;
+  for (const TaskPlan& t : plan->tasks) {
+    const int c = body_class(plan, t);
+    if (!s->grid[c]) s->grid[c] = std::max(1, cus * std::min(scan_max_blocks_per_cu(c, plan->n_hll), 8));
+  }
   const size_t nt = std::max<size_t>(1, plan->tasks.size());
   HIP_TRY(s->d_acc.ensure(nt));
   HIP_TRY(s->d_hll.ensure(std::max(1, plan->n_hll) * (size_t)kHllM));
-  HIP_TRY(s->d_partial.ensure(nt * (size_t)s->grid_max));
-  HIP_TRY(s->d_hll_partial.ensure(std::max(1, plan->n_hll) * (size_t)s->grid_max * kHllM));
+  HIP_TRY(s->d_hll_stage.ensure(std::max(1, plan->n_hll) * (size_t)kHllM));
+  HIP_TRY(s->d_queue.ensure(kBodyClasses));
+  HIP_TRY(s->d_partial.ensure(1024));
+  HIP_TRY(s->d_partial2.ensure(nt * (size_t)kFinParts));
   for (int k = 0; k < 2; ++k) HIP_TRY(hipEventCreateWithFlags(&s->ev[k], hipEventDisableTiming));
   // expression programs and string pools
   std::vector<XInstr> prog;
@@ -716,36 +754,47 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
     HIP_TRY(hipMemcpy(s->d_prog.p, prog.data(), prog.size() * sizeof(XInstr), hipMemcpyHostToDevice));
   HIP_TRY(s->d_pool.ensure(std::max<size_t>(16, pool.size() + 16)));
   if (!pool.empty()) HIP_TRY(hipMemcpy(s->d_pool.p, pool.data(), pool.size(), hipMemcpyHostToDevice));
-  // STR_IN lists
-  std::vector<int32_t> loff;
-  std::vector<uint8_t> lbytes;
+  // STR_IN lists: entries sorted by byte length and bucketed (TaskDesc::list_start)
+  std::vector<int32_t> li32;
   std::vector<uint64_t> lpre;
+  std::vector<uint8_t> lbytes;
   for (const TaskPlan& t : plan->tasks) {
-    s->list_off_base.push_back((int64_t)loff.size());
-    s->list_byte_base.push_back((int64_t)lbytes.size());
+    s->list_i32_base.push_back((int64_t)li32.size());
     s->list_pre_base.push_back((int64_t)lpre.size());
+    s->list_byte_base.push_back((int64_t)lbytes.size());
     if (t.kind != TK_STR_IN) continue;
-    int32_t base = 0;
-    for (const std::string& it : t.str.list) {
-      loff.push_back(base);
+    std::vector<std::string> items = t.str.list;
+    std::stable_sort(items.begin(), items.end(),
+                     [](const std::string& a, const std::string& b) { return a.size() < b.size(); });
+    // start[L] = number of entries whose bucket (length, or kListLenSlots when > 64) is < L, so
+    // bucket L holds entries [start[L], start[L + 1])
+    std::vector<int32_t> start(kListLenSlots + 2, 0);
+    for (int L = 0; L < kListLenSlots + 2; ++L)
+      for (const std::string& it : items)
+        start[L] += ((it.size() <= 64 ? (int)it.size() : kListLenSlots) < L) ? 1 : 0;
+    li32.insert(li32.end(), start.begin(), start.end());
+    std::vector<int32_t> lens, boffs;
+    for (const std::string& it : items) {
+      lens.push_back((int32_t)it.size());
+      boffs.push_back((int32_t)(lbytes.size() - s->list_byte_base.back()));
       uint64_t pre = 0;
       for (size_t b = 0; b < std::min<size_t>(8, it.size()); ++b)
         pre |= (uint64_t)(uint8_t)it[b] << (8 * b);
       lpre.push_back(pre);
       lbytes.insert(lbytes.end(), it.begin(), it.end());
-      base += (int32_t)it.size();
     }
-    loff.push_back(base);
+    li32.insert(li32.end(), lens.begin(), lens.end());
+    li32.insert(li32.end(), boffs.begin(), boffs.end());
   }
-  HIP_TRY(s->d_list_off.ensure(std::max<size_t>(1, loff.size())));
-  HIP_TRY(s->d_list_bytes.ensure(std::max<size_t>(16, lbytes.size())));
+  lbytes.resize(lbytes.size() + 16, 0);  // unaligned 8-byte reads past an entry's end stay inside
+  HIP_TRY(s->d_list_i32.ensure(std::max<size_t>(1, li32.size())));
   HIP_TRY(s->d_list_pre.ensure(std::max<size_t>(1, lpre.size())));
-  if (!loff.empty())
-    HIP_TRY(hipMemcpy(s->d_list_off.p, loff.data(), loff.size() * 4, hipMemcpyHostToDevice));
-  if (!lbytes.empty())
-    HIP_TRY(hipMemcpy(s->d_list_bytes.p, lbytes.data(), lbytes.size(), hipMemcpyHostToDevice));
+  HIP_TRY(s->d_list_bytes.ensure(lbytes.size()));
+  if (!li32.empty())
+    HIP_TRY(hipMemcpy(s->d_list_i32.p, li32.data(), li32.size() * 4, hipMemcpyHostToDevice));
   if (!lpre.empty())
     HIP_TRY(hipMemcpy(s->d_list_pre.p, lpre.data(), lpre.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_list_bytes.p, lbytes.data(), lbytes.size(), hipMemcpyHostToDevice));
   dq_status st = upload_host(s.get());
   if (st != DQ_OK) return st;
   *out = s.release();
@@ -772,6 +821,8 @@ static int64_t pow2_at_least(int64_t v) {
 }
 
 static bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+
+
 
 // Validates one batch against the plan and returns its row count (-1 on error).
 static int64_t batch_rows(const dq_plan* plan, const dq_column* cols, const std::vector<int>& ref,
@@ -916,24 +967,30 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
   HIP_TRY(s->d_tasks[slot].ensure(std::max<size_t>(1, n_desc)));
   TaskDesc* td = s->h_tasks[slot];
   int64_t total_items = 0;
-  int n_hll_desc = 0;
   size_t d = 0;
-  for (int b = 0; b < n_batches; ++b) {
-    const dq_column* bc = cols + (size_t)b * n_cols;
-    for (size_t k = 0; k < plan->tasks.size(); ++k, ++d) {
-      const TaskPlan& tp = plan->tasks[k];
+  // class-major, then task-major: the items of one body class form one launch, and the items of
+  // one logical task one contiguous range (finalize relies on it)
+  std::vector<ScanLaunch> launches;
+  std::vector<size_t> order;
+  for (int c = 0; c < kBodyClasses; ++c)
+    for (size_t k = 0; k < plan->tasks.size(); ++k)
+      if (body_class(plan, plan->tasks[k]) == c) order.push_back(k);
+  for (size_t k : order) {
+    const TaskPlan& tp = plan->tasks[k];
+    for (int b = 0; b < n_batches; ++b, ++d) {
+      const dq_column* bc = cols + (size_t)b * n_cols;
       TaskDesc t;
       memset(&t, 0, sizeof(t));
       t.kind = tp.kind;
       t.out = tp.out;
       t.hll_out = tp.hll_out;
-      t.hll_slot = tp.kind == TK_HLL ? n_hll_desc++ : -1;
       t.batch = b;
       t.rows = rows[b];
       t.w_val = mat_val(tp.where, b);
       t.w_vld = mat_vld(tp.where, b);
-      double bpr = 0.25;  // bytes per row, for item sizing
-      bool vec = true;
+      // item sizing: ~128 KiB of the task's buffers per item (a few bodies weighted by work)
+      double bpr = 0.0;
+      bool vec = aligned(t.w_val, 16) && aligned(t.w_vld, 16);
       if (tp.col >= 0) {
         const dq_column& c = bc[tp.col];
         t.type = c.type;
@@ -959,40 +1016,60 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
         case TK_BOOLMAP:
           t.b_val = mat_val(tp.bool_expr, b);
           t.b_vld = mat_vld(tp.bool_expr, b);
-          bpr = 0.5;
+          vec = vec && aligned(t.b_val, 16) && aligned(t.b_vld, 16);
+          bpr = 0.25;
           break;
-        case TK_VALIDITY: bpr = 0.125 + (tp.where >= 0 ? 0.25 : 0.0); break;
-        case TK_STR_IN:
+        case TK_VALIDITY: bpr = 0.125; break;
+        case TK_STR_IN: {
           t.negate = tp.str.negate ? 1 : 0;
           t.null_is_true = tp.str.null_is_true ? 1 : 0;
           t.n_list = (int32_t)tp.str.list.size();
-          t.list_off = s->d_list_off.p + s->list_off_base[k];
-          t.list_bytes = s->d_list_bytes.p + s->list_byte_base[k];
+          const int32_t* base = s->d_list_i32.p + s->list_i32_base[k];
+          t.list_start = base;
+          t.list_len = base + kListLenSlots + 2;
+          t.list_boff = base + kListLenSlots + 2 + t.n_list;
           t.list_pre = s->d_list_pre.p + s->list_pre_base[k];
+          t.list_bytes = s->d_list_bytes.p + s->list_byte_base[k];
           break;
+        }
         case TK_HLL: bpr *= 4.0; break;  // hashing: weight items by work, not bytes
         case TK_COMOMENTS: bpr *= 2.0; break;
         default: break;
       }
+      if (tp.where >= 0) bpr += 0.25;
       t.vec_ok = vec ? 1 : 0;
-      int64_t item_rows = pow2_at_least((int64_t)(131072.0 / bpr));
-      item_rows = std::max<int64_t>(kRowsPerIter, std::min<int64_t>(item_rows, (int64_t)1 << 22));
+      int64_t item_rows = pow2_at_least((int64_t)(131072.0 / std::max(bpr, 1e-3)));
+      item_rows = std::max<int64_t>(kItemAlign, std::min<int64_t>(item_rows, (int64_t)1 << 22));
       t.item_rows = item_rows;
       t.n_items = rows[b] > 0 ? (rows[b] + item_rows - 1) / item_rows : 0;
       t.item_begin = total_items;
       total_items += t.n_items;
       td[d] = t;
     }
+    const int c = body_class(plan, tp);
+    if (launches.empty() || launches.back().body != c)
+      launches.push_back(ScanLaunch{c, s->grid[c], (uint32_t)td[d - n_batches].item_begin, 0});
+    launches.back().item_hi = (uint32_t)total_items;
+  }
+  if (total_items >= ((int64_t)1 << 31))
+    return fail(DQ_ERR_UNSUPPORTED, "scan of %lld work items exceeds one launch",
+                (long long)total_items);
+  if (getenv("DQ_DEBUG")) {
+    for (const ScanLaunch& L : launches)
+      fprintf(stderr, "[dq] launch body=%d grid=%d items=[%u,%u)\n", L.body, L.grid, L.item_lo,
+              L.item_hi);
+    for (size_t q = 0; q < n_desc; ++q)
+      fprintf(stderr, "[dq] desc %zu kind=%d out=%d rows=%lld item_rows=%lld items=[%lld,+%lld) vec=%d\n",
+              q, td[q].kind, td[q].out, (long long)td[q].rows, (long long)td[q].item_rows,
+              (long long)td[q].item_begin, (long long)td[q].n_items, td[q].vec_ok);
   }
   if (n_desc > 0 && total_items > 0) {
-    const int grid = (int)std::min<int64_t>(total_items, s->grid_max);
-    HIP_TRY(s->d_partial.ensure(n_desc * (size_t)grid));
-    HIP_TRY(s->d_hll_partial.ensure(std::max(1, n_hll_desc) * (size_t)grid * kHllM));
+    HIP_TRY(s->d_partial.ensure((size_t)total_items));
     HIP_TRY(hipMemcpyAsync(s->d_tasks[slot].p, td, n_desc * sizeof(TaskDesc), hipMemcpyHostToDevice,
                            stream));
-    HIP_TRY(launch_scan(s->d_tasks[slot].p, (int)n_desc, (int)plan->tasks.size(), total_items, grid,
-                        plan->full, s->d_partial.p, s->d_hll_partial.p, s->d_acc.p, s->d_hll.p,
-                        stream));
+    HIP_TRY(launch_scan(s->d_tasks[slot].p, (int)n_desc, (int)plan->tasks.size(), launches.data(),
+                        (int)launches.size(), plan->n_hll, s->d_queue.p, s->d_partial.p,
+                        s->d_partial2.p, s->d_hll_stage.p, s->d_acc.p, s->d_hll.p, stream));
   }
   HIP_TRY(hipEventRecord(s->ev[slot], stream));
   s->ev_used[slot] = true;

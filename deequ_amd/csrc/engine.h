@@ -33,9 +33,10 @@ constexpr int kHllWords = 52;         // NUM_WORDS (:152)
 constexpr int kHllRegsPerWord = 10;   // REGISTERS_PER_WORD
 constexpr int kHllRegBits = 6;        // REGISTER_SIZE
 constexpr int kBlock = 256;           // threads per scan workgroup (4 waves)
-constexpr int kRowsPerLane = 2;       // rows a lane owns per unrolled step
-constexpr int kUnroll = 8;            // unrolled steps per block iteration
-constexpr int kRowsPerIter = kBlock * kRowsPerLane * kUnroll;  // 4096 rows per block iteration
+constexpr int kWaveRows = 1024;       // rows per wave iteration of a streaming body (16 per lane)
+constexpr int kItemAlign = 1024;      // work items are whole wave iterations (rows % 1024 == 0)
+constexpr int kFinParts = 32;         // first-stage finalize workgroups per logical task
+constexpr int kListLenSlots = 65;     // STR_IN lists bucketed by length 0..64, then "longer"
 
 // Fused numeric predicate:  [col IS NULL OR] (col op1 lo [AND col op2 hi])
 struct NumPred {
@@ -46,20 +47,20 @@ struct NumPred {
   double lo_d, hi_d;
 };
 
-// One task as the scan kernel sees it (uploaded per batch: it carries the batch's pointers).
+// One (task, batch) descriptor as the scan kernel sees it: it carries the batch's pointers and the
+// range of global work items [item_begin, item_begin + n_items) that cover the batch's rows.
 struct TaskDesc {
   int32_t kind, type, type2, n_preds;
   int32_t out;            // logical task = accumulator index
   int32_t hll_out;        // HLL register-file index of the logical task (TK_HLL), else -1
-  int32_t hll_slot;       // HLL partial slot of this descriptor (TK_HLL), else -1
   int32_t batch;          // batch index of this descriptor
   int32_t negate;         // TK_STR_IN: NOT IN
   int32_t null_is_true;   // TK_STR_IN: IS NULL OR ...
   int32_t n_list;         // TK_STR_IN list length
   int32_t vec_ok;         // buffers aligned for the vector path
   int64_t rows;
-  int64_t item_rows;      // rows per work item (multiple of kRowsPerIter)
-  int64_t item_begin;     // first global item index of this task
+  int64_t item_rows;      // rows per work item (multiple of kItemAlign)
+  int64_t item_begin;     // first global item index of this descriptor
   int64_t n_items;
   const uint8_t* valid;   // column 1
   const void* values;
@@ -70,9 +71,13 @@ struct TaskDesc {
   const uint8_t* w_vld;   // where bitmap (validity bits), NULL = never NULL
   const uint8_t* b_val;   // TK_BOOLMAP: counted expression bitmap (value bits)
   const uint8_t* b_vld;   //            (validity bits)
-  const int32_t* list_off;    // TK_STR_IN list (device): offsets n_list+1
-  const uint8_t* list_bytes;  //                          bytes
-  const uint64_t* list_pre;   //                          first 8 bytes, packed LE
+  // TK_STR_IN list (device), entries sorted by byte length: entries of length L <= 64 are
+  // [list_start[L], list_start[L + 1]), longer ones [list_start[65], list_start[66]).
+  const int32_t* list_start;
+  const int32_t* list_len;
+  const int32_t* list_boff;   // byte offset of each entry in list_bytes (padded by 8 bytes)
+  const uint64_t* list_pre;   // first min(len, 8) bytes of each entry, little-endian
+  const uint8_t* list_bytes;
   NumPred preds[kMaxPreds];
 };
 

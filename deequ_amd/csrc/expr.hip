@@ -1,0 +1,293 @@
+// expr.hip -- the generic predicate interpreter: materialises a `where` filter or a Compliance
+// predicate that the planner could not fuse into a column task as two Arrow boolean bitmaps (value
+// bits, validity bits), with Spark SQL three-valued logic (Analyzers.conditionalSelection,
+// Analyzer.scala:385-408; Compliance.scala:37-53).
+#include <hip/hip_runtime.h>
+
+#include "device_util.h"
+#include "kernels.h"
+
+namespace dq {
+
+// ------------------------------------------------------------------------------------------------
+// Generic predicate evaluation (the slow path for expressions that the planner cannot fuse):
+// a postfix program over typed values with Kleene logic; one lane per row, results ballot-packed
+// into Arrow boolean bitmaps (value bits, validity bits).
+// ------------------------------------------------------------------------------------------------
+struct V {
+  int32_t tag;  // 0 NULL, 1 BOOL, 2 I64, 3 F64, 4 STR
+  int32_t len;
+  int64_t i;
+  double d;
+  const uint8_t* p;
+};
+
+DQ_DEV int cmp_str(const uint8_t* a, int32_t la, const uint8_t* b, int32_t lb) {
+  DevBytes ra{a}, rb{b};
+  int32_t n = la < lb ? la : lb;
+  for (int32_t k = 0; k < n; ++k) {
+    int32_t d = (int32_t)ra.u8(k) - (int32_t)rb.u8(k);
+    if (d) return d < 0 ? -1 : 1;
+  }
+  return la == lb ? 0 : (la < lb ? -1 : 1);
+}
+
+// three-way compare of two non-NULL values; returns 2 when incomparable
+DQ_DEV int cmp_vals(const V& a, const V& b) {
+  if (a.tag == 4 && b.tag == 4) return cmp_str(a.p, a.len, b.p, b.len);
+  if (a.tag == 4 || b.tag == 4) return 2;
+  if (a.tag == 3 || b.tag == 3) {
+    double x = a.tag == 3 ? a.d : (double)a.i, y = b.tag == 3 ? b.d : (double)b.i;
+    return cmp3_f64(x, y);
+  }
+  return cmp3_i64(a.i, b.i);
+}
+
+// Java Double.parseDouble subset (what Spark 2.2's Cast(StringType -> DoubleType) calls): trims
+// ASCII whitespace/control chars, sign, digits, '.', exponent, optional [dDfF] suffix, NaN,
+// Infinity.  Correctly rounded when the decimal significand < 2^53 and |exp10| <= 22; otherwise the
+// nearest of two roundings (documented).  Returns false when the string is not a number -> NULL.
+DQ_DEV bool parse_f64(const uint8_t* s, int32_t len, double& out) {
+  DevBytes rd{s};
+  int32_t b = 0, e = len;
+  while (b < e && rd.u8(b) <= 32) ++b;
+  while (e > b && rd.u8(e - 1) <= 32) --e;
+  if (b >= e) return false;
+  bool neg = false;
+  uint32_t c = rd.u8(b);
+  if (c == '+' || c == '-') {
+    neg = c == '-';
+    ++b;
+  }
+  if (e - b == 3 && rd.u8(b) == 'N' && rd.u8(b + 1) == 'a' && rd.u8(b + 2) == 'N') {
+    out = __builtin_nan("");
+    return true;
+  }
+  if (e - b == 8) {
+    const char* inf = "Infinity";
+    bool ok = true;
+    for (int k = 0; k < 8; ++k) ok &= rd.u8(b + k) == (uint32_t)inf[k];
+    if (ok) {
+      out = neg ? -__builtin_inf() : __builtin_inf();
+      return true;
+    }
+  }
+  if (e > b) {
+    uint32_t last = rd.u8(e - 1);
+    if (last == 'd' || last == 'D' || last == 'f' || last == 'F') --e;
+  }
+  uint64_t mant = 0;
+  int digits = 0, exp10 = 0;
+  bool any = false, dot = false, overflow_digits = false;
+  int32_t k = b;
+  for (; k < e; ++k) {
+    c = rd.u8(k);
+    if (c >= '0' && c <= '9') {
+      any = true;
+      if (mant < 100000000000000000ULL) {
+        mant = mant * 10 + (c - '0');
+        if (mant) ++digits;
+        if (dot) --exp10;
+      } else {
+        overflow_digits = true;
+        if (!dot) ++exp10;
+      }
+    } else if (c == '.' && !dot) {
+      dot = true;
+    } else {
+      break;
+    }
+  }
+  if (!any) return false;
+  if (k < e) {
+    c = rd.u8(k);
+    if (c != 'e' && c != 'E') return false;
+    ++k;
+    bool eneg = false;
+    if (k < e && (rd.u8(k) == '+' || rd.u8(k) == '-')) {
+      eneg = rd.u8(k) == '-';
+      ++k;
+    }
+    if (k >= e) return false;
+    int ev = 0;
+    for (; k < e; ++k) {
+      c = rd.u8(k);
+      if (c < '0' || c > '9') return false;
+      if (ev < 100000) ev = ev * 10 + (c - '0');
+    }
+    exp10 += eneg ? -ev : ev;
+  }
+  (void)overflow_digits;
+  (void)digits;
+  double v = (double)mant;
+  const double p10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                          1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  if (exp10 >= 0) {
+    while (exp10 > 22) {
+      v *= 1e22;
+      exp10 -= 22;
+    }
+    v *= p10[exp10];
+  } else {
+    while (exp10 < -22) {
+      v /= 1e22;
+      exp10 += 22;
+    }
+    v /= p10[-exp10];
+  }
+  out = neg ? -v : v;
+  return true;
+}
+
+__global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__ prog, int n_instr,
+                                                      const DevCol* __restrict__ cols,
+                                                      const uint8_t* __restrict__ pool, int64_t rows,
+                                                      uint64_t* __restrict__ out_val,
+                                                      uint64_t* __restrict__ out_vld) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
+  const int64_t n_words = (rows + 63) >> 6;
+  for (int64_t w = wave; w < n_words; w += n_waves) {
+    const int64_t r = w * 64 + lane;
+    V st[kMaxStack];
+    int sp = 0;
+    bool in_range = r < rows;
+    if (in_range) {
+      for (int pc = 0; pc < n_instr; ++pc) {
+        const XInstr ins = prog[pc];
+        switch (ins.op) {
+          case XI_COL: {
+            const DevCol& c = cols[ins.a];
+            V v{};
+            if (!bit1(c.valid, r)) {
+              v.tag = 0;
+            } else if (c.type == DQ_UTF8) {
+              const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
+              v.tag = 4;
+              v.p = c.data + off[r];
+              v.len = off[r + 1] - off[r];
+            } else if (c.type == DQ_BOOL) {
+              v.tag = 1;
+              v.i = bit1(reinterpret_cast<const uint8_t*>(c.values), r);
+            } else if (is_float_type(c.type)) {
+              v.tag = 3;
+              v.d = load_f64(c.type, c.values, r);
+            } else {
+              v.tag = 2;
+              v.i = load_i64(c.type, c.values, r);
+            }
+            st[sp++] = v;
+            break;
+          }
+          case XI_NULL: st[sp++] = V{0, 0, 0, 0.0, nullptr}; break;
+          case XI_BOOL: st[sp++] = V{1, 0, ins.imm, 0.0, nullptr}; break;
+          case XI_I64: st[sp++] = V{2, 0, ins.imm, 0.0, nullptr}; break;
+          case XI_F64: st[sp++] = V{3, 0, 0, __builtin_bit_cast(double, ins.imm), nullptr}; break;
+          case XI_STR: st[sp++] = V{4, ins.a, 0, 0.0, pool + ins.imm}; break;
+          case XI_IS_NULL: st[sp - 1] = V{1, 0, st[sp - 1].tag == 0 ? 1 : 0, 0.0, nullptr}; break;
+          case XI_IS_NOT_NULL: st[sp - 1] = V{1, 0, st[sp - 1].tag != 0 ? 1 : 0, 0.0, nullptr}; break;
+          case XI_NOT:
+            if (st[sp - 1].tag != 0) st[sp - 1].i = st[sp - 1].i ? 0 : 1;
+            break;
+          case XI_AND: {
+            V b = st[--sp];
+            V a = st[sp - 1];
+            // Kleene: FALSE dominates, then NULL
+            bool af = a.tag != 0 && !a.i, bf = b.tag != 0 && !b.i;
+            if (af || bf) st[sp - 1] = V{1, 0, 0, 0.0, nullptr};
+            else if (a.tag == 0 || b.tag == 0) st[sp - 1] = V{0, 0, 0, 0.0, nullptr};
+            else st[sp - 1] = V{1, 0, 1, 0.0, nullptr};
+            break;
+          }
+          case XI_OR: {
+            V b = st[--sp];
+            V a = st[sp - 1];
+            bool at = a.tag != 0 && a.i, bt = b.tag != 0 && b.i;
+            if (at || bt) st[sp - 1] = V{1, 0, 1, 0.0, nullptr};
+            else if (a.tag == 0 || b.tag == 0) st[sp - 1] = V{0, 0, 0, 0.0, nullptr};
+            else st[sp - 1] = V{1, 0, 0, 0.0, nullptr};
+            break;
+          }
+          case XI_CMP: {
+            V b = st[--sp];
+            V a = st[sp - 1];
+            if (ins.a == DQ_X_EQ_NULL_SAFE) {
+              int eq;
+              if (a.tag == 0 || b.tag == 0) eq = (a.tag == 0 && b.tag == 0);
+              else eq = cmp_vals(a, b) == 0;
+              st[sp - 1] = V{1, 0, eq, 0.0, nullptr};
+            } else if (a.tag == 0 || b.tag == 0) {
+              st[sp - 1] = V{0, 0, 0, 0.0, nullptr};
+            } else {
+              int c = cmp_vals(a, b);
+              if (c == 2) st[sp - 1] = V{0, 0, 0, 0.0, nullptr};
+              else st[sp - 1] = V{1, 0, (op_mask(ins.a) >> (c + 1)) & 1, 0.0, nullptr};
+            }
+            break;
+          }
+          case XI_IN: {
+            const int n = ins.a;
+            const int base = sp - n - 1;
+            V x = st[base];
+            V res{0, 0, 0, 0.0, nullptr};
+            if (x.tag != 0) {
+              bool found = false, saw_null = false;
+              for (int q = 0; q < n; ++q) {
+                const V& it = st[base + 1 + q];
+                if (it.tag == 0) {
+                  saw_null = true;
+                } else if (cmp_vals(x, it) == 0) {
+                  found = true;
+                }
+              }
+              if (found) res = V{1, 0, 1, 0.0, nullptr};
+              else if (!saw_null) res = V{1, 0, 0, 0.0, nullptr};
+            }
+            sp = base;
+            st[sp++] = res;
+            break;
+          }
+          case XI_CAST_F64: {
+            V& a = st[sp - 1];
+            if (a.tag == 2 || a.tag == 1) {
+              a.d = (double)a.i;
+              a.tag = 3;
+            } else if (a.tag == 4) {
+              double d;
+              if (parse_f64(a.p, a.len, d)) a = V{3, 0, 0, d, nullptr};
+              else a = V{0, 0, 0, 0.0, nullptr};
+            }
+            break;
+          }
+          default: break;
+        }
+      }
+    }
+    const V& res = st[0];
+    const bool valid = in_range && sp == 1 && res.tag != 0;
+    const bool truth = valid && res.i != 0;
+    const uint64_t bv = __ballot(truth);
+    const uint64_t bn = __ballot(valid);
+    if (lane == 0) {
+      out_val[w] = bv;
+      out_vld[w] = bn;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host-side launchers
+// ------------------------------------------------------------------------------------------------
+hipError_t launch_expr(const XInstr* prog, int n_instr, const DevCol* cols, const uint8_t* pool,
+                       int64_t rows, uint64_t* out_val, uint64_t* out_vld, hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  int64_t words = (rows + 63) / 64;
+  int64_t blocks = (words + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(expr_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, prog, n_instr,
+                     cols, pool, rows, out_val, out_vld);
+  return hipGetLastError();
+}
+
+}  // namespace dq

@@ -89,10 +89,38 @@ constexpr int kMaxStack = 16;
 
 hipError_t launch_expr(const XInstr* prog, int n_instr, const DevCol* cols, const uint8_t* pool,
                        int64_t rows, uint64_t* out_val, uint64_t* out_vld, hipStream_t stream);
-// tasks: n_tasks descriptors (one per logical task and batch); n_logical accumulators.
-hipError_t launch_scan(const TaskDesc* tasks, int n_tasks, int n_logical, int64_t total_items,
-                       int grid, bool full, Acc* partial, uint8_t* hll_partial, Acc* acc,
-                       uint8_t* hll_acc, hipStream_t stream);
-int scan_max_blocks_per_cu(bool full);
+// Body classes of the scan: one kernel instantiation each (scan.hip).
+enum BodyClass : int32_t {
+  BC_NUM_I8 = 0,
+  BC_NUM_I16,
+  BC_NUM_I32,
+  BC_NUM_I64,
+  BC_NUM_F32,
+  BC_NUM_F64,
+  BC_BITS,     // TK_VALIDITY, TK_BOOLMAP
+  BC_STR_IN,
+  BC_CORR,
+  BC_HLL,
+  kBodyClasses
+};
+
+// One scan launch: the items [item_lo, item_hi) of every task of body class `body`.
+struct ScanLaunch {
+  int32_t body;
+  int32_t grid;
+  uint32_t item_lo, item_hi;
+};
+
+// Fused scan over n_desc (task, batch) descriptors numbered class-major then task-major (each
+// logical task owns one contiguous range of work items), one launch per entry of `launches`, then
+// the two finalize launches that fold the item partials into acc[n_tasks] / hll_acc.
+// queues[kBodyClasses] must be 0 on entry (finalize re-arms them), `partial` holds one record per
+// item, `partial2` n_tasks * kFinParts, `hll_stage` n_hll * kHllM zeroed u32 registers (finalize
+// clears them again).
+hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const ScanLaunch* launches,
+                       int n_launches, int n_hll, uint32_t* queues, Acc* partial, Acc* partial2,
+                       uint32_t* hll_stage, Acc* acc, uint8_t* hll_acc, hipStream_t stream);
+size_t scan_lds_bytes(int body, int n_hll);
+int scan_max_blocks_per_cu(int body, int n_hll);
 
 }  // namespace dq

@@ -32,7 +32,7 @@ NUM_TYPES = INT_TYPES | {"float", "double"}
 # SQL predicates (Spark SQL subset, three-valued logic) -- an independent little evaluator
 # ------------------------------------------------------------------------------------------------
 _TOK = re.compile(r"\s*(?:(\d+\.\d*(?:[eE][+-]?\d+)?|\d+(?:[eE][+-]?\d+)?)|('(?:[^']|'')*')|"
-                  r"(<=>|<=|>=|<>|!=|==|=|<|>|\(|\)|,)|([A-Za-z_][A-Za-z0-9_]*))")
+                  r"(<=>|<=|>=|<>|!=|==|=|<|>|\(|\)|,|-)|([A-Za-z_][A-Za-z0-9_]*))")
 
 
 def _tokens(s: str):

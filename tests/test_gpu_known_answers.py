@@ -92,7 +92,7 @@ def test_analysis_runs_each_analyzer_once_and_shares_the_scan(gpu_device):
                         StandardDeviation("att1"), Minimum("att1"), Maximum("att1")]).run(df)
     finally:
         R.run_scan = real
-    assert calls == [11]  # ONE fused scan for all seven analyzers
+    assert calls == [10]  # ONE fused scan for all seven analyzers (1+2+2+2+1+1+1 slots)
     assert ctx.metric(Mean("att1")).value.get() == 3.5
 
 
