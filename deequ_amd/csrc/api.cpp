@@ -1030,6 +1030,12 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
           t.list_boff = base + kListLenSlots + 2 + t.n_list;
           t.list_pre = s->d_list_pre.p + s->list_pre_base[k];
           t.list_bytes = s->d_list_bytes.p + s->list_byte_base[k];
+          t.list_small = t.n_list <= 8 ? 1 : 0;
+          t.list_lenmask = 0;
+          for (const std::string& it : tp.str.list) {
+            if (it.size() > 8) t.list_small = 0;
+            else t.list_lenmask |= 1ULL << it.size();
+          }
           break;
         }
         case TK_HLL: bpr *= 4.0; break;  // hashing: weight items by work, not bytes

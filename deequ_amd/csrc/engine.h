@@ -58,6 +58,9 @@ struct TaskDesc {
   int32_t null_is_true;   // TK_STR_IN: IS NULL OR ...
   int32_t n_list;         // TK_STR_IN list length
   int32_t vec_ok;         // buffers aligned for the vector path
+  int32_t list_small;     // TK_STR_IN: <= 8 entries, each <= 8 bytes (scalar compare path)
+  int32_t pad0;
+  uint64_t list_lenmask;  // TK_STR_IN small lists: bit L set when an entry has length L
   int64_t rows;
   int64_t item_rows;      // rows per work item (multiple of kItemAlign)
   int64_t item_begin;     // first global item index of this descriptor

@@ -259,6 +259,26 @@ DQ_DEV void bits_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
   int64_t r0 = r_begin;
   if (t.vec_ok) {
     const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
+    // 4 KiB of each bitmap per wave and step: four 1 KiB wave-instructions in flight per bitmap
+    for (; r0 + 32768 <= r_end; r0 += 32768) {
+      uint4 a[4], b[4], x[4], y[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t byte = (r0 >> 3) + 1024 * k + 16 * l;
+        a[k] = A ? *reinterpret_cast<const uint4*>(A + byte) : ones;
+        b[k] = B ? *reinterpret_cast<const uint4*>(B + byte) : ones;
+        x[k] = WV ? *reinterpret_cast<const uint4*>(WV + byte) : ones;
+        y[k] = WD ? *reinterpret_cast<const uint4*>(WD + byte) : ones;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t m0 = b[k].x & x[k].x & y[k].x, m1 = b[k].y & x[k].y & y[k].y,
+                       m2 = b[k].z & x[k].z & y[k].z, m3 = b[k].w & x[k].w & y[k].w;
+        c0 += __popc(a[k].x & m0) + __popc(a[k].y & m1) + __popc(a[k].z & m2) +
+              __popc(a[k].w & m3);
+        c1 += __popc(m0) + __popc(m1) + __popc(m2) + __popc(m3);
+      }
+    }
     for (; r0 + 8192 <= r_end; r0 += 8192) {  // 1 KiB of each bitmap per wave-instruction
       const int64_t byte = (r0 >> 3) + 16 * l;
       const uint4 a = A ? *reinterpret_cast<const uint4*>(A + byte) : ones;
@@ -310,57 +330,138 @@ DQ_DEV uint32_t str_in_match(const TaskDesc& t, const uint8_t* data, int32_t s, 
   return 0u;
 }
 
-// Lane l owns rows r0 + 4l .. r0 + 4l + 3 of a 256-row step: one 16-byte offsets load per lane
-// (the fifth offset comes from the next lane), then one unaligned 8-byte load per candidate
-// string; the wave's string loads all fall into the same ~1 KiB of character data.
+// Small lists (<= 8 entries of <= 8 bytes, the isContainedIn form): membership is a compare of the
+// string's length and masked 8-byte prefix against entries loaded once per item into scalar
+// registers; strings whose length no entry has are never loaded.
+struct SmallList {
+  int32_t n;
+  int32_t len[8];
+  uint64_t pre[8], mask[8];
+  DQ_DEV void load(const TaskDesc& t) {
+    n = t.n_list;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      len[k] = k < n ? t.list_len[k] : -1;
+      pre[k] = k < n ? t.list_pre[k] : 0;
+      mask[k] = len[k] >= 8 ? ~0ULL : ((1ULL << (8 * (len[k] < 0 ? 0 : len[k]))) - 1);
+    }
+  }
+  // v = 8 bytes starting at the string (bytes past its end are ignored through the mask)
+  DQ_DEV uint32_t match(uint64_t v, int32_t l) const {
+    uint32_t hit = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k >= n) break;
+      hit |= (len[k] == l && ((v ^ pre[k]) & mask[k]) == 0) ? 1u : 0u;
+    }
+    return hit;
+  }
+};
+
+// Rows of one lane: o[0..4] offsets of 4 consecutive rows, vb / wt their validity / where bits.
+DQ_DEV void str_in_rows(const TaskDesc& t, const int32_t (&o)[5], uint32_t vb, uint32_t wt,
+                        int32_t dlen, int64_t& ct, int64_t& cn) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!((wt >> j) & 1u)) continue;
+    if ((vb >> j) & 1u) {
+      ct += str_in_match(t, t.data, o[j], o[j + 1] - o[j], dlen) ^ (uint32_t)t.negate;
+      cn += 1;
+    } else if (t.null_is_true) {
+      ct += 1;
+      cn += 1;
+    }
+  }
+}
+
+// Lane l owns rows r0 + 256g + 4l .. + 3 (g < 4) of a 1024-row step: one 16-byte offsets load per
+// lane and group (the fifth offset comes from the next lane), then -- small lists -- one unaligned
+// 8-byte load per candidate string, all 16 in flight together; the wave's string loads of a
+// group fall into the same ~1 KiB of character data, so the bytes leave HBM once.
 DQ_DEV void str_in_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& acc) {
   const int l = lane_id();
   const int32_t* off = reinterpret_cast<const int32_t*>(t.values);
   const int32_t dlen = off[t.rows];
   int64_t ct = 0, cn = 0;
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += 256) {
-    const int64_t rb = r0 + 4 * l;
-    int32_t o[5];
-    uint32_t vb, wt;
-    if (t.vec_ok && r0 + 256 <= r_end) {
-      const int4 q = *reinterpret_cast<const int4*>(off + rb);
-      const int32_t last = off[r0 + 256];
-      const int32_t nxt = __shfl_down(q.x, 1);
-      o[0] = q.x;
-      o[1] = q.y;
-      o[2] = q.z;
-      o[3] = q.w;
-      o[4] = l == 63 ? last : nxt;
-      const int64_t wi = (r0 >> 5) + (l >> 3);
-      const int sh = (l & 7) * 4;
-      vb = t.valid ? (reinterpret_cast<const uint32_t*>(t.valid)[wi] >> sh) & 0xfu : 0xfu;
-      wt = t.w_val ? ((reinterpret_cast<const uint32_t*>(t.w_val)[wi] &
-                       reinterpret_cast<const uint32_t*>(t.w_vld)[wi]) >> sh) & 0xfu
-                   : 0xfu;
-    } else {
-      vb = wt = 0;
+  int64_t r0 = r_begin;
+  if (t.vec_ok) {
+    for (; r0 + kWaveRows <= r_end; r0 += kWaveRows) {
+      int4 q[4];
+      int32_t last[4];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) o[j] = (rb + j <= r_end) ? off[rb + j] : 0;
+      for (int g = 0; g < 4; ++g) {
+        q[g] = *reinterpret_cast<const int4*>(off + r0 + 256 * g + 4 * l);
+        last[g] = off[r0 + 256 * g + 256];
+      }
+      uint32_t vb = 0xffffu, wt = 0xffffu;
+      if (t.valid) {
+        ChunkBits c;
+        c.load(t.valid, r0);
+        vb = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t r = rb + j;
-        if (r < r_end) {
-          vb |= bit1(t.valid, r) << j;
-          wt |= (t.w_val ? (bit1(t.w_val, r) & bit1(t.w_vld, r)) : 1u) << j;
+        for (int g = 0; g < 4; ++g) vb |= c.get(256 * g + 4 * l, 4) << (4 * g);
+      }
+      if (t.w_val) {
+        ChunkBits wa, wb;
+        wa.load(t.w_val, r0);
+        wb.load(t.w_vld, r0);
+        wt = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int o = 256 * g + 4 * l;
+          wt |= (wa.get(o, 4) & wb.get(o, 4)) << (4 * g);
         }
       }
-    }
+      int32_t o[4][5];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!((wt >> j) & 1u)) continue;
-      if ((vb >> j) & 1u) {
-        ct += str_in_match(t, t.data, o[j], o[j + 1] - o[j], dlen) ^ (uint32_t)t.negate;
-        cn += 1;
-      } else if (t.null_is_true) {
-        ct += 1;
-        cn += 1;
+      for (int g = 0; g < 4; ++g) {
+        const int32_t nxt = __shfl_down(q[g].x, 1);
+        o[g][0] = q[g].x;
+        o[g][1] = q[g].y;
+        o[g][2] = q[g].z;
+        o[g][3] = q[g].w;
+        o[g][4] = l == 63 ? last[g] : nxt;
+      }
+      // small list and every string of the step has 8 readable bytes: one unconditional
+      // unaligned 8-byte load per row, all 16 in flight, and no per-row branches
+      if (t.list_small && (int64_t)last[3] + 8 <= (int64_t)dlen) {
+        SmallList sl;
+        sl.load(t);
+        uint64_t v[16];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) __builtin_memcpy(&v[4 * g + j], t.data + o[g][j], 8);
+        uint32_t hits = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            hits |= sl.match(v[4 * g + j], o[g][j + 1] - o[g][j]) << (4 * g + j);
+        const uint32_t sel = vb & wt, nulls = t.null_is_true ? (wt & ~vb & 0xffffu) : 0u;
+        ct += __popc((t.negate ? ~hits : hits) & sel) + __popc(nulls);
+        cn += __popc(sel) + __popc(nulls);
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) str_in_rows(t, o[g], vb >> (4 * g), wt >> (4 * g), dlen, ct, cn);
       }
     }
+  }
+  for (; r0 < r_end; r0 += 256) {  // tail (and unaligned buffers): 4 rows per lane, bounds-checked
+    const int64_t rb = r0 + 4 * l;
+    int32_t o[5];
+    uint32_t vb = 0, wt = 0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) o[j] = (rb + j <= r_end) ? off[rb + j] : 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t r = rb + j;
+      if (r < r_end) {
+        vb |= bit1(t.valid, r) << j;
+        wt |= (t.w_val ? (bit1(t.w_val, r) & bit1(t.w_vld, r)) : 1u) << j;
+      }
+    }
+    str_in_rows(t, o, vb, wt, dlen, ct, cn);
   }
   acc.i[0] = ct;
   acc.i[1] = cn;
