@@ -32,7 +32,7 @@ def s10_suite():
     from deequ_amd.analyzers import (Completeness, Compliance, Maximum, Mean, Minimum, Size,
                                      StandardDeviation, Sum)
     return [Size(), Completeness("id"), Completeness("name"),
-            Compliance("numViews is Fnon-negative", "numViews >= 0"),
+            Compliance("numViews is non-negative", "numViews >= 0"),
             Compliance("priority contained in high,low",
                        "priority IS NULL OR priority IN ('high','low')"),
             Sum("numViews"), Mean("numViews"), StandardDeviation("numViews"),

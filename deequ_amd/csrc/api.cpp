@@ -622,14 +622,17 @@ extern "C" dq_status dq_plan_explain(const dq_plan* plan, char* buf, size_t buf_
 
 extern "C" int dq_plan_launches_per_batch(const dq_plan* plan) {
   if (!plan) return 0;
-  int classes = 0;
+  int classes = 0, hll = 0;
   for (int c = 0; c < kBodyClasses; ++c) {
     bool used = false;
     for (const TaskPlan& t : plan->tasks) used = used || body_class(plan, t) == c;
-    classes += used ? 1 : 0;
+    if (c == BC_HLL) hll = used ? 1 : 0;
+    else classes += used ? 1 : 0;
   }
-  // expression bitmaps + one scan launch per body class + the two finalize launches
-  return (int)plan->mat.size() + classes + (plan->tasks.empty() ? 0 : 2);
+  // two or more non-HLL body classes share one mixed launch (dq_scan_device_batches)
+  if (classes >= 2 && !getenv("DQ_NO_MIXED")) classes = 1;
+  // expression bitmaps + the scan launches + the two finalize launches
+  return (int)plan->mat.size() + classes + hll + (plan->tasks.empty() ? 0 : 2);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -638,7 +641,7 @@ extern "C" int dq_plan_launches_per_batch(const dq_plan* plan) {
 struct dq_state {
   const dq_plan* plan = nullptr;
   int device = 0;
-  int grid[kBodyClasses] = {};   // persistent grid of each scan kernel instantiation
+  int grid[kQueues] = {};        // persistent grid of each scan kernel (+ the mixed kernel)
   hipStream_t stream = nullptr;
   bool stream_set = false;
   // host mirror
@@ -651,7 +654,9 @@ struct dq_state {
   DevBuf<Acc> d_acc, d_partial, d_partial2;
   DevBuf<uint8_t> d_hll;
   DevBuf<uint32_t> d_hll_stage;  // per-launch HLL registers (u32), kept zero between launches
-  DevBuf<uint32_t> d_queue;      // work-item counter of the scan kernel, kept zero between launches
+  DevBuf<uint32_t> d_queue;      // work-item counters of the scan kernels, kept zero between launches
+  DevBuf<uint32_t> d_order[2];   // mixed launch: queue position -> item (per descriptor slot)
+  std::vector<uint32_t> order_sig[2];  // per-class item ranges d_order[slot] was built for
   DevBuf<TaskDesc> d_tasks[2];
   TaskDesc* h_tasks[2] = {nullptr, nullptr};
   size_t h_tasks_cap[2] = {0, 0};
@@ -698,7 +703,7 @@ static dq_status upload_host(dq_state* s) {
     HIP_TRY(hipMemcpy(s->d_acc.p, s->acc.data(), s->acc.size() * sizeof(Acc), hipMemcpyHostToDevice));
   if (!s->hll.empty())
     HIP_TRY(hipMemcpy(s->d_hll.p, s->hll.data(), s->hll.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(s->d_queue.p, 0, kBodyClasses * sizeof(uint32_t)));
+  HIP_TRY(hipMemset(s->d_queue.p, 0, kQueues * sizeof(uint32_t)));
   HIP_TRY(hipMemset(s->d_hll_stage.p, 0, s->d_hll_stage.n * sizeof(uint32_t)));
   s->host_dirty = false;
   return DQ_OK;
@@ -722,16 +727,17 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
   HIP_TRY(hipSetDevice(device));
   int cus = 0;
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  for (int c = 0; c < kBodyClasses; ++c) s->grid[c] = 0;
+  for (int c = 0; c < kQueues; ++c) s->grid[c] = 0;
   for (const TaskPlan& t : plan->tasks) {
     const int c = body_class(plan, t);
     if (!s->grid[c]) s->grid[c] = std::max(1, cus * std::min(scan_max_blocks_per_cu(c, plan->n_hll), 8));
   }
+  s->grid[kBodyMixed] = std::max(1, cus * std::min(scan_max_blocks_per_cu(kBodyMixed, 0), 8));
   const size_t nt = std::max<size_t>(1, plan->tasks.size());
   HIP_TRY(s->d_acc.ensure(nt));
   HIP_TRY(s->d_hll.ensure(std::max(1, plan->n_hll) * (size_t)kHllM));
   HIP_TRY(s->d_hll_stage.ensure(std::max(1, plan->n_hll) * (size_t)kHllM));
-  HIP_TRY(s->d_queue.ensure(kBodyClasses));
+  HIP_TRY(s->d_queue.ensure(kQueues));
   HIP_TRY(s->d_partial.ensure(1024));
   HIP_TRY(s->d_partial2.ensure(nt * (size_t)kFinParts));
   for (int k = 0; k < 2; ++k) HIP_TRY(hipEventCreateWithFlags(&s->ev[k], hipEventDisableTiming));
@@ -982,6 +988,7 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
       TaskDesc t;
       memset(&t, 0, sizeof(t));
       t.kind = tp.kind;
+      t.body = body_class(plan, tp);
       t.out = tp.out;
       t.hll_out = tp.hll_out;
       t.batch = b;
@@ -1032,9 +1039,19 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
           t.list_bytes = s->d_list_bytes.p + s->list_byte_base[k];
           t.list_small = t.n_list <= 8 ? 1 : 0;
           t.list_lenmask = 0;
-          for (const std::string& it : tp.str.list) {
-            if (it.size() > 8) t.list_small = 0;
-            else t.list_lenmask |= 1ULL << it.size();
+          for (int e = 0; e < 8; ++e) t.list_key[e] = 0xFEULL << 56;  // no row key has top byte 0xFE
+          for (size_t e = 0; e < tp.str.list.size(); ++e) {
+            const std::string& it = tp.str.list[e];
+            if (it.size() > 7) {
+              t.list_small = 0;
+              continue;
+            }
+            t.list_lenmask |= 1ULL << it.size();
+            if (e < 8) {
+              uint64_t key = (uint64_t)it.size() << 56;
+              for (size_t q = 0; q < it.size(); ++q) key |= (uint64_t)(uint8_t)it[q] << (8 * q);
+              t.list_key[e] = key;
+            }
           }
           break;
         }
@@ -1054,12 +1071,54 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
     }
     const int c = body_class(plan, tp);
     if (launches.empty() || launches.back().body != c)
-      launches.push_back(ScanLaunch{c, s->grid[c], (uint32_t)td[d - n_batches].item_begin, 0});
+      launches.push_back(ScanLaunch{c, s->grid[c], (uint32_t)td[d - n_batches].item_begin, 0, nullptr});
     launches.back().item_hi = (uint32_t)total_items;
   }
   if (total_items >= ((int64_t)1 << 31))
     return fail(DQ_ERR_UNSUPPORTED, "scan of %lld work items exceeds one launch",
                 (long long)total_items);
+  // Two or more non-HLL classes: one mixed launch over their items, interleaved in proportion to
+  // each class's item count (item j of a class with n items sorts at (j + 1/2) / n), so string
+  // gathers and streaming bodies run side by side.  HLL keeps its own launch (LDS registers).
+  {
+    std::vector<ScanLaunch> plain, hll;
+    for (const ScanLaunch& L : launches) (L.body == BC_HLL ? hll : plain).push_back(L);
+    if (plain.size() >= 2 && !getenv("DQ_NO_MIXED")) {
+      std::vector<uint32_t> sig;
+      for (const ScanLaunch& L : plain) {
+        sig.push_back(L.item_lo);
+        sig.push_back(L.item_hi);
+      }
+      const uint32_t n_order = plain.back().item_hi;  // non-HLL classes precede BC_HLL
+      if (plain.front().item_lo != 0) return fail(DQ_ERR_STATE, "unexpected item layout");
+      if (s->order_sig[slot] != sig) {
+        std::vector<uint32_t> order;
+        order.reserve(n_order);
+        std::vector<uint32_t> next(plain.size(), 0);
+        for (uint32_t q = 0; q < n_order; ++q) {
+          int best = -1;
+          double best_key = 0.0;
+          for (size_t c = 0; c < plain.size(); ++c) {
+            const uint32_t n = plain[c].item_hi - plain[c].item_lo;
+            if (next[c] >= n) continue;
+            const double key = (next[c] + 0.5) / (double)n;
+            if (best < 0 || key < best_key) {
+              best = (int)c;
+              best_key = key;
+            }
+          }
+          order.push_back(plain[best].item_lo + next[best]++);
+        }
+        HIP_TRY(s->d_order[slot].ensure(std::max<size_t>(1, order.size())));
+        HIP_TRY(hipMemcpy(s->d_order[slot].p, order.data(), order.size() * sizeof(uint32_t),
+                          hipMemcpyHostToDevice));
+        s->order_sig[slot] = sig;
+      }
+      launches.clear();
+      launches.push_back(ScanLaunch{kBodyMixed, s->grid[kBodyMixed], 0, n_order, s->d_order[slot].p});
+      for (const ScanLaunch& L : hll) launches.push_back(L);
+    }
+  }
   if (getenv("DQ_DEBUG")) {
     for (const ScanLaunch& L : launches)
       fprintf(stderr, "[dq] launch body=%d grid=%d items=[%u,%u)\n", L.body, L.grid, L.item_lo,

@@ -58,9 +58,12 @@ struct TaskDesc {
   int32_t null_is_true;   // TK_STR_IN: IS NULL OR ...
   int32_t n_list;         // TK_STR_IN list length
   int32_t vec_ok;         // buffers aligned for the vector path
-  int32_t list_small;     // TK_STR_IN: <= 8 entries, each <= 8 bytes (scalar compare path)
-  int32_t pad0;
+  int32_t list_small;     // TK_STR_IN: <= 8 entries, each <= 7 bytes (packed-key compare path)
+  int32_t body;           // scan body class (kernels.h BodyClass)
   uint64_t list_lenmask;  // TK_STR_IN small lists: bit L set when an entry has length L
+  // TK_STR_IN small lists: entry k as (bytes, zero-padded) | length << 56; unused = 0xFE << 56
+  // (a row of 8+ bytes keys to ~0, so it matches neither an entry nor an unused slot)
+  uint64_t list_key[8];
   int64_t rows;
   int64_t item_rows;      // rows per work item (multiple of kItemAlign)
   int64_t item_begin;     // first global item index of this descriptor

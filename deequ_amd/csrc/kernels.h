@@ -103,18 +103,23 @@ enum BodyClass : int32_t {
   BC_HLL,
   kBodyClasses
 };
+// A launch of the mixed kernel: every non-HLL body class in one grid, items taken in an
+// interleaved order so latency-bound bodies (string gathers) overlap bandwidth-bound ones.
+constexpr int kBodyMixed = kBodyClasses;
+constexpr int kQueues = kBodyClasses + 1;  // one work counter per launch kind
 
 // One scan launch: the items [item_lo, item_hi) of every task of body class `body`.
 struct ScanLaunch {
-  int32_t body;
+  int32_t body;            // BodyClass, or kBodyMixed
   int32_t grid;
-  uint32_t item_lo, item_hi;
+  uint32_t item_lo, item_hi;  // kBodyMixed: item_lo = 0, item_hi = entries of `order`
+  const uint32_t* order;   // kBodyMixed: queue position -> global item index
 };
 
 // Fused scan over n_desc (task, batch) descriptors numbered class-major then task-major (each
 // logical task owns one contiguous range of work items), one launch per entry of `launches`, then
 // the two finalize launches that fold the item partials into acc[n_tasks] / hll_acc.
-// queues[kBodyClasses] must be 0 on entry (finalize re-arms them), `partial` holds one record per
+// queues[kQueues] must be 0 on entry (finalize re-arms them), `partial` holds one record per
 // item, `partial2` n_tasks * kFinParts, `hll_stage` n_hll * kHllM zeroed u32 registers (finalize
 // clears them again).
 hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const ScanLaunch* launches,

@@ -63,8 +63,9 @@ def test_s10_plan_fuses_into_four_tasks_and_two_launches():
     text = plan.explain()
     assert text.count("task[") == 4, text
     assert "numeric col=3" in text and "str_in col=2" in text
-    # one scan launch per body class (validity, numeric int64, string IN) + two finalize launches
-    assert plan.launches_per_batch == 5
+    # ONE mixed scan launch for the three body classes (validity, numeric int64, string IN) + the
+    # two finalize launches
+    assert plan.launches_per_batch == 3
 
 
 def test_where_filters_materialise_once_per_distinct_expression():

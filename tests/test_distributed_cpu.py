@@ -1,0 +1,133 @@
+"""world_size-2 `gloo` test of the multi-GPU exchange step on the CPU.
+
+Each rank holds the aggregation buffer of its contiguous row shard -- built here from the shard's
+values exactly as the scan kernels would leave it (n, wrapping Long sum, min/max keys, Welford
+(avg, m2), the predicate counters) -- and then runs the product's exchange step
+(`merge_states_across_ranks`: all-gather of the serialized states + rank-ordered merge through
+dq_state_merge).  The merged row must equal the single-pass oracle over the whole column: counts,
+wrapping sums and extremes bit-exact, (avg, m2) within the 1e-12 relative tolerance of
+StandardDeviation (Spark's Chan merge, StandardDeviation.scala:37-44).  No GPU is touched: the
+states are host-only (dq_state_create(device = -1)).
+"""
+import os
+import socket
+import struct
+
+import numpy as np
+import pytest
+
+MAGIC = 0x3130514445455144  # "DQEEDQ01", the engine's serialized-state header (api.cpp)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _suite():
+    from deequ_amd.analyzers import (Compliance, Maximum, Mean, Minimum, Size, StandardDeviation,
+                                     Sum)
+    return [Size(), Sum("x"), Mean("x"), StandardDeviation("x"), Minimum("x"), Maximum("x"),
+            Compliance("x non-negative", "x >= 0")]
+
+
+def _schema():
+    from deequ_amd import _native as N
+    from deequ_amd.table import StructField, StructType
+    return StructType([StructField("x", N.INT64)])
+
+
+def _column(n, seed):
+    rng = np.random.default_rng(seed)
+    x = rng.integers(-(2 ** 40), 2 ** 40, size=n, dtype=np.int64)
+    x[:5] = np.iinfo(np.int64).max  # forces the Long sum to wrap
+    valid = rng.random(n) > 0.05
+    return x, valid
+
+
+def _wrapping_sum(xs):
+    return int(np.sum(xs.astype(np.uint64), dtype=np.uint64).astype(np.int64))
+
+
+def _shard_image(plan, x, valid):
+    """The serialized state a rank's scan would produce for its shard (one TK_NUMERIC task)."""
+    text = plan.explain()
+    assert text.count("task[") == 1 and "numeric" in text, text
+    xs = x[valid]
+    n = int(xs.size)
+    i = [0] * 10
+    d = [0.0] * 6
+    i[0] = n
+    i[1] = _wrapping_sum(xs) if n else 0
+    i[2] = int(xs.min()) if n else int(np.iinfo(np.int64).max)
+    i[3] = int(xs.max()) if n else int(np.iinfo(np.int64).min)
+    i[4] = int(np.sum(xs >= 0))  # predicate TRUE
+    i[7] = n                     # predicate non-NULL
+    avg = m2 = 0.0
+    for k, v in enumerate(xs.astype(np.float64).tolist(), 1):  # CentralMomentAgg update per row
+        delta = v - avg
+        avg += delta / k
+        m2 += delta * (v - avg)
+    d[0] = float(np.sum(xs.astype(np.float64)))
+    d[1], d[2] = avg, m2
+    hdr = struct.pack("<4Q", MAGIC, 1, 0, int(x.size))
+    return hdr + struct.pack("<10q6d", *i, *d)
+
+
+def _worker(rank, world, port, n, seed, out_q):
+    import ctypes
+
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from deequ_amd import _native as N
+        from deequ_amd.distributed import merge_states_across_ranks, shard_bounds
+        from deequ_amd.runners.engine import get_plan
+        suite = _suite()
+        plan = get_plan(_schema(), [s for a in suite for s in a.aggregation_functions()])
+        x, valid = _column(n, seed)
+        lo, hi = shard_bounds(n, rank, world, align=64)
+        img = _shard_image(plan, x[lo:hi], valid[lo:hi])
+        st = ctypes.c_void_p()
+        N.check(N.lib.dq_state_create(plan.handle, -1, ctypes.byref(st)))
+        buf = ctypes.create_string_buffer(img, len(img))
+        N.check(N.lib.dq_state_deserialize(st, buf, len(img)))
+        row = merge_states_across_ranks(plan, st)
+        N.lib.dq_state_destroy(st)
+        out_q.put((rank, row))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [1000, 4099])
+def test_gloo_world2_merge_matches_single_pass(n):
+    import torch.multiprocessing as mp
+    world, seed = 2, 11
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rows = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert rows[0] == rows[1]  # every rank merges in rank order: identical rows
+
+    x, valid = _column(n, seed)
+    xs = x[valid]
+    size, s, mean_sum, mean_cnt, sd, mn, mx, c_true, c_cnt = rows[0]
+    assert size == n and mean_cnt == n
+    wrapped = _wrapping_sum(xs)
+    assert s == float(wrapped) and mean_sum == float(wrapped)
+    assert mn == float(xs.min()) and mx == float(xs.max())
+    assert c_true == int(np.sum(xs >= 0)) and c_cnt == n
+    f = xs.astype(np.float64)
+    m2 = float(np.sum((f - f.mean()) ** 2))
+    assert sd[0] == xs.size
+    assert sd[1] == pytest.approx(f.mean(), rel=1e-12)
+    assert sd[2] == pytest.approx(m2, rel=1e-12)
