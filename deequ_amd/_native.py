@@ -113,6 +113,15 @@ def _load() -> ctypes.CDLL:
         "dq_freq_export": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                    POINTER(c_int64)]),
         "dq_freq_merge": (c_int, [c_void_p, c_void_p]),
+        "dq_loader_create": (c_int, [c_int, POINTER(c_void_p)]),
+        "dq_loader_destroy": (None, [c_void_p]),
+        "dq_loader_stage": (c_int, [c_void_p, POINTER(dq_column), c_int, POINTER(dq_column),
+                                    c_void_p]),
+        "dq_loader_release": (c_int, [c_void_p, c_void_p]),
+        "dq_scan_host": (c_int, [c_void_p, c_void_p, POINTER(dq_column), c_int, c_void_p,
+                                 c_void_p]),
+        "dq_freq_add_host": (c_int, [c_void_p, c_void_p, POINTER(dq_column), c_int, c_int,
+                                     c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)
@@ -133,7 +142,9 @@ EXPORTED = [
     "dq_state_sync", "dq_state_get", "dq_state_merge", "dq_state_serialized_size",
     "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_freq_create",
     "dq_freq_destroy", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_num_groups",
-    "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge",
+    "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge", "dq_loader_create",
+    "dq_loader_destroy", "dq_loader_stage", "dq_loader_release", "dq_scan_host",
+    "dq_freq_add_host",
 ]
 
 

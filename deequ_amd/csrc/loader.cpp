@@ -1,0 +1,188 @@
+// loader.cpp -- columnar handoff: host-resident Arrow batches (what a Spark partition exports
+// through the Arrow C Data Interface) staged into HBM for the device entry points.
+//
+// Two device staging slots alternate.  Batch k's buffers are copied H2D on the loader's own copy
+// stream while batch k-1 is scanned on the caller's stream; a slot is refilled only after the
+// work that read it (recorded by dq_loader_release) has finished, and the scan of a slot waits
+// for its copy.  So PCIe transfer and the HBM-bound scan overlap, and the caller's stream sees the
+// usual stream order.  The reference's equivalent is Spark feeding UnsafeRows of a partition into
+// the aggregation iterator (AnalysisRunner.scala:303); ownership stays with the caller exactly as
+// there (the loader never frees or retains the host buffers after dq_loader_stage returns).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "engine.h"
+#include "kernels.h"
+
+using namespace dq;
+
+namespace {
+
+struct Slot {
+  DevBuf<uint8_t> buf;
+  hipEvent_t copied = nullptr;
+  hipEvent_t consumed = nullptr;
+  bool used = false;
+};
+
+size_t fixed_width(int t) {
+  switch (t) {
+    case DQ_INT8: return 1;
+    case DQ_INT16: return 2;
+    case DQ_INT32: case DQ_FLOAT32: return 4;
+    case DQ_INT64: case DQ_FLOAT64: return 8;
+    default: return 0;
+  }
+}
+
+size_t round_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+}  // namespace
+
+struct dq_loader {
+  int device = 0;
+  hipStream_t copy = nullptr;
+  Slot slot[2];
+  int next = 0;
+  int staged = -1;
+  ~dq_loader() {
+    for (Slot& s : slot) {
+      if (s.copied) (void)hipEventDestroy(s.copied);
+      if (s.consumed) (void)hipEventDestroy(s.consumed);
+    }
+    if (copy) (void)hipStreamDestroy(copy);
+  }
+};
+
+extern "C" dq_status dq_loader_create(int device, dq_loader** out) {
+  if (!out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  if (device < 0) return fail(DQ_ERR_INVALID_ARGUMENT, "loader needs a device");
+  auto l = new dq_loader();
+  l->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&l->copy, hipStreamNonBlocking);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+    e = hipEventCreateWithFlags(&l->slot[k].copied, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&l->slot[k].consumed, hipEventDisableTiming);
+  }
+  if (e != hipSuccess) {
+    delete l;
+    return fail(DQ_ERR_DEVICE, "HIP error %s creating the loader", hipGetErrorString(e));
+  }
+  *out = l;
+  return DQ_OK;
+}
+
+extern "C" void dq_loader_destroy(dq_loader* l) {
+  if (!l) return;
+  (void)hipSetDevice(l->device);
+  for (Slot& s : l->slot)
+    if (s.used) (void)hipEventSynchronize(s.consumed);
+  (void)hipStreamSynchronize(l->copy);
+  delete l;
+}
+
+extern "C" dq_status dq_loader_stage(dq_loader* l, const dq_column* host_cols, int n_cols,
+                                     dq_column* dev_cols, void* hip_stream) {
+  if (!l || (n_cols > 0 && (!host_cols || !dev_cols)) || n_cols < 0)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (l->staged >= 0) return fail(DQ_ERR_STATE, "previous staged batch was not released");
+  hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
+  HIP_TRY(hipSetDevice(l->device));
+  // layout of the slot: per column validity | values | data, each 256-byte aligned
+  std::vector<size_t> nv(n_cols), nval(n_cols), ndat(n_cols);
+  size_t total = 0;
+  for (int c = 0; c < n_cols; ++c) {
+    const dq_column& h = host_cols[c];
+    if (h.length < 0) return fail(DQ_ERR_INVALID_ARGUMENT, "column %d: negative length", c);
+    const size_t n = (size_t)h.length;
+    nv[c] = h.validity ? (n + 7) / 8 : 0;
+    if (h.type == DQ_UTF8) {
+      nval[c] = h.values ? 4 * (n + 1) : 0;
+      const int32_t* off = static_cast<const int32_t*>(h.values);
+      const int32_t end = off ? off[n] : 0;
+      if (end < 0) return fail(DQ_ERR_INVALID_ARGUMENT, "column %d: negative string offset", c);
+      ndat[c] = h.data ? (size_t)end : 0;
+    } else if (h.type == DQ_BOOL) {
+      nval[c] = h.values ? (n + 7) / 8 : 0;
+      ndat[c] = 0;
+    } else {
+      const size_t w = fixed_width(h.type);
+      if (!w) return fail(DQ_ERR_WRONG_TYPE, "column %d: unknown type %d", c, h.type);
+      nval[c] = h.values ? w * n : 0;
+      ndat[c] = 0;
+    }
+    total += round_up(nv[c]) + round_up(nval[c]) + round_up(ndat[c]);
+  }
+  const int k = l->next;
+  l->next ^= 1;
+  Slot& s = l->slot[k];
+  if (s.used) {
+    if (s.buf.n < total) HIP_TRY(hipEventSynchronize(s.consumed));  // about to free it
+    else HIP_TRY(hipStreamWaitEvent(l->copy, s.consumed, 0));
+  }
+  if (s.buf.n < total) HIP_TRY(s.buf.ensure(total + total / 8));
+  uint8_t* p = s.buf.p;
+  for (int c = 0; c < n_cols; ++c) {
+    const dq_column& h = host_cols[c];
+    dq_column d = h;
+    auto put = [&](const void* src, size_t bytes, const void** dst_field) -> hipError_t {
+      if (!bytes) return hipSuccess;
+      hipError_t e = hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, l->copy);
+      *dst_field = p;
+      p += round_up(bytes);
+      return e;
+    };
+    const void* vp = nullptr;
+    const void* dp = nullptr;
+    const void* valp = nullptr;
+    HIP_TRY(put(h.validity, nv[c], &vp));
+    HIP_TRY(put(h.values, nval[c], &valp));
+    HIP_TRY(put(h.data, ndat[c], &dp));
+    d.validity = static_cast<const uint8_t*>(h.validity ? vp : nullptr);
+    d.values = h.values ? valp : nullptr;
+    d.data = static_cast<const uint8_t*>(h.data ? dp : nullptr);
+    if (h.type == DQ_UTF8 && h.data && ndat[c] == 0) d.data = s.buf.p;  // empty strings only
+    if (h.values && nval[c] == 0) d.values = s.buf.p;                   // zero-row column
+    dev_cols[c] = d;
+  }
+  HIP_TRY(hipEventRecord(s.copied, l->copy));
+  HIP_TRY(hipStreamWaitEvent(stream, s.copied, 0));
+  l->staged = k;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_loader_release(dq_loader* l, void* hip_stream) {
+  if (!l) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (l->staged < 0) return fail(DQ_ERR_STATE, "no staged batch");
+  HIP_TRY(hipSetDevice(l->device));
+  Slot& s = l->slot[l->staged];
+  HIP_TRY(hipEventRecord(s.consumed, reinterpret_cast<hipStream_t>(hip_stream)));
+  s.used = true;
+  l->staged = -1;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_scan_host(dq_loader* l, const dq_plan* plan, const dq_column* host_cols,
+                                  int n_cols, dq_state* state, void* hip_stream) {
+  std::vector<dq_column> dev(std::max(0, n_cols));
+  dq_status st = dq_loader_stage(l, host_cols, n_cols, dev.data(), hip_stream);
+  if (st != DQ_OK) return st;
+  st = dq_scan_device(plan, dev.data(), n_cols, state, hip_stream);
+  dq_status rs = dq_loader_release(l, hip_stream);
+  return st != DQ_OK ? st : rs;
+}
+
+extern "C" dq_status dq_freq_add_host(dq_loader* l, dq_freq* freq, const dq_column* host_keys,
+                                      int n_keys, int null_as_group, void* hip_stream) {
+  std::vector<dq_column> dev(std::max(0, n_keys));
+  dq_status st = dq_loader_stage(l, host_keys, n_keys, dev.data(), hip_stream);
+  if (st != DQ_OK) return st;
+  st = dq_freq_add_device(freq, dev.data(), n_keys, null_as_group, hip_stream);
+  dq_status rs = dq_loader_release(l, hip_stream);
+  return st != DQ_OK ? st : rs;
+}

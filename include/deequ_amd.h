@@ -305,6 +305,33 @@ dq_status dq_freq_export(dq_freq* freq, int64_t* counts_out, int64_t* key_offset
  * numRows add. */
 dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src);
 
+/* ------------------------------------------------------------------------------------------------
+ * Columnar handoff: host-resident Arrow batches -> HBM (the JNI shim's entry).
+ *
+ * In the reference a Spark partition's rows stream through the aggregation iterator of the one
+ * `data.agg(...)` job (AnalysisRunner.scala:303) and of the grouping job
+ * (GroupingAnalyzers.scala:62-77).  Here a partition arrives as host Arrow buffers
+ * (dq_column_from_arrow), is copied into one of two device staging slots on the loader's copy
+ * stream, and is scanned on the caller's stream; the copy of batch k+1 overlaps the scan of
+ * batch k.  The caller keeps the host buffers valid until the call returns (the loader retains
+ * nothing of them afterwards).  One loader per thread / stream, like a dq_state.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct dq_loader dq_loader;
+dq_status dq_loader_create(int device, dq_loader** out);
+void dq_loader_destroy(dq_loader* loader);
+/* Stages one host batch: enqueues its H2D copies and makes `hip_stream` wait for them; writes the
+ * device-pointer columns to dev_cols[n_cols].  Every staged batch must be released (below) after
+ * the work that reads dev_cols has been enqueued on `hip_stream`. */
+dq_status dq_loader_stage(dq_loader* loader, const dq_column* host_cols, int n_cols,
+                          dq_column* dev_cols, void* hip_stream);
+dq_status dq_loader_release(dq_loader* loader, void* hip_stream);
+/* stage + dq_scan_device + release. */
+dq_status dq_scan_host(dq_loader* loader, const dq_plan* plan, const dq_column* host_cols,
+                       int n_cols, dq_state* state, void* hip_stream);
+/* stage + dq_freq_add_device + release. */
+dq_status dq_freq_add_host(dq_loader* loader, dq_freq* freq, const dq_column* host_keys, int n_keys,
+                           int null_as_group, void* hip_stream);
+
 #ifdef __cplusplus
 }
 #endif
