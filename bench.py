@@ -73,7 +73,7 @@ def cpu_baseline(rows: int, seed: int, min_seconds: float = 10.0):
         once()
         reps += 1
         el = time.perf_counter() - t0
-        if el >= min_seconds or reps >= 200:
+        if el >= min_seconds or reps >= 5000:
             break
     return {"value": reps * n / el, "unit": "rows/s", "cores": threads, "kind": "port",
             "sample": f"S10 over {n} synthetic Item rows x {reps} passes ({el:.1f} s), "

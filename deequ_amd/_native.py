@@ -122,6 +122,10 @@ def _load() -> ctypes.CDLL:
                                  c_void_p]),
         "dq_freq_add_host": (c_int, [c_void_p, c_void_p, POINTER(dq_column), c_int, c_int,
                                      c_void_p]),
+        "dq_freq_partition_sizes": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+        "dq_freq_partition": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+        "dq_freq_add_records_device": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                               c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)
@@ -144,8 +148,10 @@ EXPORTED = [
     "dq_freq_destroy", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_num_groups",
     "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge", "dq_loader_create",
     "dq_loader_destroy", "dq_loader_stage", "dq_loader_release", "dq_scan_host",
-    "dq_freq_add_host",
+    "dq_freq_add_host", "dq_freq_partition_sizes", "dq_freq_partition",
+    "dq_freq_add_records_device",
 ]
+FREQ_RECORD_BYTES = 24  # sizeof(dq_freq_record)
 
 
 def check(status: int) -> None:

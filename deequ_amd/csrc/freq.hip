@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(256) freq_insert_kernel(FreqDev f, int64_t row
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * chunk;
   const int64_t r1 = min(r0 + chunk, rows);
-  unsigned long long nulls = 0, null_group = 0;
+  unsigned long long nulls = 0, null_group = 0, sentinel = 0;
   for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
     uint64_t key;
     bool is_null;
@@ -301,6 +301,10 @@ __global__ void __launch_bounds__(256) freq_insert_kernel(FreqDev f, int64_t row
     }
     if (is_null) {  // exact mode NULL group (histogram)
       ++null_group;
+      continue;
+    }
+    if (f.exact && key == kEmpty) {  // the key equal to the empty marker lives outside the tables
+      ++sentinel;
       continue;
     }
     bool done = false;
@@ -332,6 +336,7 @@ __global__ void __launch_bounds__(256) freq_insert_kernel(FreqDev f, int64_t row
   }
   if (nulls) atomicAdd(&f.counters[C_NULL_ROWS], nulls);
   if (null_group) atomicAdd(&f.counters[C_NULL_GROUP], null_group);
+  if (sentinel) atomicAdd(&f.counters[C_SENTINEL], sentinel);
 }
 
 DQ_DEV int64_t find_slot(const FreqDev& f, uint64_t key) {
@@ -446,6 +451,156 @@ __global__ void __launch_bounds__(256) freq_compact_kernel(const uint64_t* keys,
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Hash repartition (multi-GPU frequency path): the reference's groupBy runs a
+// partial HashAggregate per partition, a hash-partitioned Exchange and a final aggregate
+// (GroupingAnalyzers.scala:70).  Here each rank's table IS the partial aggregate; its groups are cut
+// into one segment per owner rank (owner from the HIGH bits of the slot hash, so the owner's own
+// table, which indexes by the low bits, stays uniformly loaded), exchanged by RCCL all-to-all, and
+// re-inserted with their counts on the owner.
+// Wire format per segment: fixed records {key, count, enc_off} (enc_off = byte offset of the group's
+// encoded key inside the segment's var bytes; unused in exact mode) + var bytes (8-aligned).
+// ------------------------------------------------------------------------------------------------
+struct FreqRecord {
+  uint64_t key;
+  uint64_t count;
+  uint64_t enc_off;
+};
+
+constexpr int kMaxParts = 64;
+
+DQ_DEV uint32_t owner_of(uint64_t key, int exact, uint32_t parts) {
+  uint64_t h = exact ? mix64(key) : key;
+  return (uint32_t)(((h >> 40) * (uint64_t)parts) >> 24);
+}
+
+DQ_DEV uint64_t enc_record_size(const uint8_t* enc, const int32_t* types, int n_keys) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(enc);
+  uint64_t size = 0;
+  for (int q = 0; q < n_keys; ++q) {
+    uint32_t tag = w[size / 4];
+    size += 4;
+    if (!tag) continue;
+    if (types[q] == DQ_UTF8) size += 4 + ((w[size / 4] + 3) & ~3u);
+    else size += 8;
+  }
+  return size;
+}
+
+struct PartArgs {
+  int32_t types[kMaxKeys];
+  int32_t n_keys;
+  int32_t exact;
+  uint32_t parts;
+  uint32_t pad;
+};
+
+// pass 1: records and var bytes per owner
+__global__ void __launch_bounds__(256) freq_part_count_kernel(const uint64_t* keys, const uint64_t* reps,
+                                                              const uint8_t* arena, uint64_t cap,
+                                                              PartArgs a,
+                                                              unsigned long long* n_rec,
+                                                              unsigned long long* n_var) {
+  __shared__ unsigned long long lr[kMaxParts], lv[kMaxParts];
+  for (int i = threadIdx.x; i < kMaxParts; i += blockDim.x) lr[i] = lv[i] = 0;
+  __syncthreads();
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t k = keys[s];
+    if (k == kEmpty) continue;
+    uint32_t o = owner_of(k, a.exact, a.parts);
+    atomicAdd(&lr[o], 1ULL);
+    if (!a.exact) atomicAdd(&lv[o], (enc_record_size(arena + reps[s], a.types, a.n_keys) + 7) & ~7ULL);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < a.parts; i += blockDim.x) {
+    if (lr[i]) atomicAdd(&n_rec[i], lr[i]);
+    if (lv[i]) atomicAdd(&n_var[i], lv[i]);
+  }
+}
+
+// pass 2: scatter into the owner segments (rec_base / var_base = exclusive prefix sums of pass 1)
+__global__ void __launch_bounds__(256) freq_part_scatter_kernel(
+    const uint64_t* keys, const uint64_t* counts, const uint64_t* reps, const uint8_t* arena,
+    uint64_t cap, PartArgs a, const unsigned long long* rec_base, const unsigned long long* var_base,
+    unsigned long long* rec_cur, unsigned long long* var_cur, FreqRecord* out_rec, uint8_t* out_var) {
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t k = keys[s];
+    if (k == kEmpty) continue;
+    uint32_t o = owner_of(k, a.exact, a.parts);
+    unsigned long long i = atomicAdd(&rec_cur[o], 1ULL);
+    FreqRecord r{k, counts[s], 0};
+    if (!a.exact) {
+      const uint8_t* enc = arena + reps[s];
+      uint64_t size = enc_record_size(enc, a.types, a.n_keys);
+      unsigned long long off = atomicAdd(&var_cur[o], (size + 7) & ~7ULL);
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(enc);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(out_var + var_base[o] + off);
+      for (uint64_t q = 0; q < size / 4; ++q) dst[q] = src[q];
+      r.enc_off = off;
+    }
+    out_rec[rec_base[o] + i] = r;
+  }
+}
+
+struct SrcSegs {
+  int64_t rec_start[kMaxParts + 1];  // records of source j: [rec_start[j], rec_start[j+1])
+  int64_t var_base[kMaxParts];       // byte offset of source j's var segment
+  int32_t n_src;
+};
+
+DQ_DEV const uint8_t* record_enc(const FreqRecord& r, int64_t i, const uint8_t* var,
+                                 const SrcSegs& segs) {
+  int j = 0;
+  while (j + 1 < segs.n_src && i >= segs.rec_start[j + 1]) ++j;
+  return var + segs.var_base[j] + r.enc_off;
+}
+
+// Re-inserts received groups with their counts (the final aggregate after the Exchange).
+__global__ void __launch_bounds__(256) freq_insert_records_kernel(FreqDev f, const FreqRecord* rec,
+                                                                  const uint8_t* var, SrcSegs segs,
+                                                                  PartArgs a) {
+  const int64_t n = segs.rec_start[segs.n_src];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    FreqRecord r = rec[i];
+    if (f.exact) {
+      insert_global(f, r.key, r.count, RowSrc{0});
+    } else {
+      const uint8_t* enc = record_enc(r, i, var, segs);
+      insert_global(f, r.key, r.count, ArenaSrc{enc, enc_record_size(enc, a.types, a.n_keys)});
+    }
+  }
+}
+
+// Hashed mode: every received group must carry the same encoded key as the group it landed in, so
+// a 64-bit hash collision between groups of different ranks is detected, never merged.
+__global__ void __launch_bounds__(256) freq_verify_records_kernel(FreqDev f, const FreqRecord* rec,
+                                                                  const uint8_t* var, SrcSegs segs,
+                                                                  PartArgs a) {
+  const int64_t n = segs.rec_start[segs.n_src];
+  unsigned long long bad = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    FreqRecord r = rec[i];
+    const uint32_t* enc = reinterpret_cast<const uint32_t*>(record_enc(r, i, var, segs));
+    int64_t slot = find_slot(f, r.key);
+    if (slot < 0 || f.reps[slot] == ~0ULL) {
+      ++bad;
+      continue;
+    }
+    const uint32_t* have = reinterpret_cast<const uint32_t*>(f.arena + f.reps[slot]);
+    uint64_t size = enc_record_size(reinterpret_cast<const uint8_t*>(enc), a.types, a.n_keys);
+    for (uint64_t q = 0; q < size / 4; ++q)
+      if (have[q] != enc[q]) {
+        ++bad;
+        break;
+      }
+  }
+  if (bad) atomicAdd(&f.counters[C_COLLISIONS], bad);
+}
+
 __global__ void fill_u64(uint64_t* p, uint64_t n, uint64_t v) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x)
@@ -497,6 +652,8 @@ static FreqDev dev_view(dq_freq* f) {
   d.n_keys = f->n_keys;
   d.exact = f->exact ? 1 : 0;
   d.null_as_group = f->mode_null_as_group > 0 ? 1 : 0;
+  // key types are needed by every kernel that sizes an encoded key (rehash / merge re-inserts)
+  for (int k = 0; k < f->n_keys; ++k) d.cols[k].type = f->types[k];
   return d;
 }
 
@@ -555,6 +712,11 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
   for (int t : f->types)
     if (t < DQ_BOOL || t > DQ_UTF8) return fail(DQ_ERR_INVALID_ARGUMENT, "bad key type %d", t);
   f->exact = n_keys == 1 && f->types[0] != DQ_UTF8;
+  if (n_keys > 1)
+    for (int t : f->types)
+      if (t != DQ_UTF8)
+        return fail(DQ_ERR_UNSUPPORTED,
+                    "grouping on several columns is implemented for string columns only");
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(f->counters.ensure(C_N));
   HIP_TRY(hipMemset(f->counters.p, 0, C_N * 8));
@@ -841,3 +1003,175 @@ extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src) {
 }
 
 extern "C" int64_t dq_freq_num_rows(const dq_freq* f) { return f ? f->num_rows : -1; }
+
+// ------------------------------------------------------------------------------------------------
+// Hash repartition for the multi-GPU frequency path (see the kernels above)
+// ------------------------------------------------------------------------------------------------
+static PartArgs part_args(const dq_freq* f, int n_parts) {
+  PartArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int k = 0; k < f->n_keys; ++k) a.types[k] = f->types[k];
+  a.n_keys = f->n_keys;
+  a.exact = f->exact ? 1 : 0;
+  a.parts = (uint32_t)n_parts;
+  return a;
+}
+
+// Per-owner record counts and var bytes (device counting pass).
+static dq_status part_sizes(dq_freq* f, int n_parts, std::vector<unsigned long long>& rec,
+                            std::vector<unsigned long long>& var) {
+  DevBuf<unsigned long long> cnt;
+  HIP_TRY(cnt.ensure(2 * kMaxParts));
+  HIP_TRY(hipMemsetAsync(cnt.p, 0, 2 * kMaxParts * 8, f->stream));
+  hipLaunchKernelGGL(freq_part_count_kernel, dim3(grid_for(f->cap)), dim3(256), 0, f->stream,
+                     f->keys.p, f->exact ? nullptr : f->reps.p, f->arena.p, f->cap,
+                     part_args(f, n_parts), cnt.p, cnt.p + kMaxParts);
+  HIP_TRY(hipGetLastError());
+  std::vector<unsigned long long> h(2 * kMaxParts);
+  HIP_TRY(hipStreamSynchronize(f->stream));
+  HIP_TRY(hipMemcpy(h.data(), cnt.p, h.size() * 8, hipMemcpyDeviceToHost));
+  rec.assign(h.begin(), h.begin() + n_parts);
+  var.assign(h.begin() + kMaxParts, h.begin() + kMaxParts + n_parts);
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_freq_partition_sizes(dq_freq* f, int n_parts, int64_t* rec_counts,
+                                             int64_t* var_bytes, int64_t* special) {
+  if (!f || !rec_counts || !var_bytes || !special)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_parts < 1 || n_parts > kMaxParts)
+    return fail(DQ_ERR_UNSUPPORTED, "n_parts must be in [1, %d]", kMaxParts);
+  HIP_TRY(hipSetDevice(f->device));
+  dq_status st = pull_counters(f);
+  if (st != DQ_OK) return st;
+  std::vector<unsigned long long> rec, var;
+  st = part_sizes(f, n_parts, rec, var);
+  if (st != DQ_OK) return st;
+  for (int i = 0; i < n_parts; ++i) {
+    rec_counts[i] = (int64_t)rec[i];
+    var_bytes[i] = (int64_t)var[i];
+  }
+  special[0] = (int64_t)f->h_counters[C_SENTINEL];
+  special[1] = (int64_t)f->h_counters[C_NULL_GROUP];
+  special[2] = (int64_t)f->h_counters[C_NULL_ROWS];
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_freq_partition(dq_freq* f, int n_parts, dq_freq_record* records,
+                                       uint8_t* var, void* hip_stream) {
+  if (!f) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_parts < 1 || n_parts > kMaxParts)
+    return fail(DQ_ERR_UNSUPPORTED, "n_parts must be in [1, %d]", kMaxParts);
+  HIP_TRY(hipSetDevice(f->device));
+  HIP_TRY(hipStreamSynchronize(f->stream));
+  f->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  std::vector<unsigned long long> rec, var_n;
+  dq_status st = part_sizes(f, n_parts, rec, var_n);
+  if (st != DQ_OK) return st;
+  unsigned long long total_rec = 0, total_var = 0;
+  std::vector<unsigned long long> base(4 * kMaxParts, 0);  // rec_base, var_base, rec_cur, var_cur
+  for (int i = 0; i < n_parts; ++i) {
+    base[i] = total_rec;
+    base[kMaxParts + i] = total_var;
+    total_rec += rec[i];
+    total_var += var_n[i];
+  }
+  if (total_rec == 0) return DQ_OK;
+  if (!records || (total_var && !var)) return fail(DQ_ERR_INVALID_ARGUMENT, "null output buffer");
+  DevBuf<unsigned long long> dbase;
+  HIP_TRY(dbase.ensure(base.size()));
+  HIP_TRY(hipMemcpyAsync(dbase.p, base.data(), base.size() * 8, hipMemcpyHostToDevice, f->stream));
+  hipLaunchKernelGGL(freq_part_scatter_kernel, dim3(grid_for(f->cap)), dim3(256), 0, f->stream,
+                     f->keys.p, f->counts.p, f->exact ? nullptr : f->reps.p, f->arena.p, f->cap,
+                     part_args(f, n_parts), dbase.p, dbase.p + kMaxParts, dbase.p + 2 * kMaxParts,
+                     dbase.p + 3 * kMaxParts, reinterpret_cast<FreqRecord*>(records), var);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(f->stream));  // dbase is freed on return
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record* records,
+                                                const uint8_t* var, int n_src,
+                                                const int64_t* src_records,
+                                                const int64_t* src_var_bytes, int64_t num_rows,
+                                                const int64_t* special, int null_as_group,
+                                                void* hip_stream) {
+  if (!f || !src_records || !src_var_bytes || !special)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_src < 1 || n_src > kMaxParts)
+    return fail(DQ_ERR_UNSUPPORTED, "n_src must be in [1, %d]", kMaxParts);
+  int mode = null_as_group ? 1 : 0;
+  if (f->mode_null_as_group >= 0 && f->mode_null_as_group != mode)
+    return fail(DQ_ERR_STATE, "null_as_group must be the same for every batch");
+  f->mode_null_as_group = mode;
+  HIP_TRY(hipSetDevice(f->device));
+  HIP_TRY(hipStreamSynchronize(f->stream));
+  f->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  SrcSegs segs;
+  memset(&segs, 0, sizeof(segs));
+  segs.n_src = n_src;
+  int64_t total_rec = 0, total_var = 0;
+  for (int j = 0; j < n_src; ++j) {
+    if (src_records[j] < 0 || src_var_bytes[j] < 0 || (src_var_bytes[j] & 7))
+      return fail(DQ_ERR_INVALID_ARGUMENT, "bad segment sizes for source %d", j);
+    segs.rec_start[j] = total_rec;
+    segs.var_base[j] = total_var;
+    total_rec += src_records[j];
+    total_var += src_var_bytes[j];
+  }
+  segs.rec_start[n_src] = total_rec;
+  if (total_rec && !records) return fail(DQ_ERR_INVALID_ARGUMENT, "null records");
+  if (!f->exact && total_var && !var) return fail(DQ_ERR_INVALID_ARGUMENT, "null var bytes");
+  dq_status st = pull_counters(f);
+  if (st != DQ_OK) return st;
+  uint64_t need = 2 * (f->h_counters[C_OCCUPIED] + (uint64_t)total_rec) + 2;
+  if (need > f->cap) {
+    uint64_t cap = f->cap;
+    while (cap < need) cap <<= 1;
+    st = rehash(f, cap);
+    if (st != DQ_OK) return st;
+  }
+  if (!f->exact) {
+    uint64_t want = f->arena_used + (uint64_t)total_var + 64;
+    if (want > f->arena.n) {
+      DevBuf<uint8_t> bigger;
+      HIP_TRY(bigger.ensure(std::max<uint64_t>(want, f->arena.n * 2)));
+      if (f->arena_used)
+        HIP_TRY(hipMemcpyAsync(bigger.p, f->arena.p, f->arena_used, hipMemcpyDeviceToDevice, f->stream));
+      HIP_TRY(hipStreamSynchronize(f->stream));
+      f->arena.swap(bigger);
+    }
+  }
+  FreqDev d = dev_view(f);
+  for (int k = 0; k < f->n_keys; ++k) d.cols[k].type = f->types[k];
+  const PartArgs a = part_args(f, n_src);
+  const auto* rec = reinterpret_cast<const FreqRecord*>(records);
+  if (total_rec) {
+    unsigned grid = grid_for((uint64_t)total_rec);
+    hipLaunchKernelGGL(freq_insert_records_kernel, dim3(grid), dim3(256), 0, f->stream, d, rec, var,
+                       segs, a);
+    HIP_TRY(hipGetLastError());
+    if (!f->exact) {
+      hipLaunchKernelGGL(freq_verify_records_kernel, dim3(grid), dim3(256), 0, f->stream, d, rec,
+                         var, segs, a);
+      HIP_TRY(hipGetLastError());
+    }
+  }
+  st = pull_counters(f);
+  if (st != DQ_OK) return st;
+  unsigned long long c[C_N];
+  for (int k = 0; k < C_N; ++k) c[k] = f->h_counters[k];
+  c[C_SENTINEL] += (unsigned long long)special[0];
+  c[C_NULL_GROUP] += (unsigned long long)special[1];
+  c[C_NULL_ROWS] += (unsigned long long)special[2];
+  HIP_TRY(hipMemcpy(f->counters.p, c, sizeof(c), hipMemcpyHostToDevice));
+  f->num_rows += num_rows;
+  st = pull_counters(f);
+  if (st != DQ_OK) return st;
+  if (f->h_counters[C_ARENA_OVF]) return fail(DQ_ERR_OUT_OF_MEMORY, "frequency table arena overflow");
+  if (f->h_counters[C_COLLISIONS])
+    return fail(DQ_ERR_UNSUPPORTED,
+                "64-bit key-hash collision between distinct groups detected (%llu groups)",
+                (unsigned long long)f->h_counters[C_COLLISIONS]);
+  return DQ_OK;
+}

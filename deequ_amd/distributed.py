@@ -79,3 +79,137 @@ def run_scan_distributed(table_shard, specs):
     N.check(N.lib.dq_state_reset(state))
     scan_into(table_shard, plan, state)
     return merge_states_across_ranks(plan, state, table_shard.device)
+
+
+# ------------------------------------------------------------------------------------------------
+# Frequency path: hash repartition by owner rank, then a local count
+# ------------------------------------------------------------------------------------------------
+def freq_partition(table, n_parts: int, stream=None):
+    """Cuts a rank's partial frequency table into `n_parts` owner segments on the device.
+
+    Returns (records, var, rec_counts, var_bytes, special): `records` / `var` are uint8 device
+    tensors holding the segments back to back (24-byte dq_freq_record each; 8-aligned encoded keys),
+    `rec_counts` / `var_bytes` the per-owner sizes, `special` the groups kept outside the slot table
+    (dq_freq_partition_sizes)."""
+    import torch
+    rc = np.zeros(n_parts, np.int64)
+    vb = np.zeros(n_parts, np.int64)
+    sp = np.zeros(3, np.int64)
+    N.check(N.lib.dq_freq_partition_sizes(table.handle, n_parts, rc.ctypes.data, vb.ctypes.data,
+                                          sp.ctypes.data))
+    dev = f"cuda:{table.device}"
+    rec = torch.empty(int(rc.sum()) * N.FREQ_RECORD_BYTES, dtype=torch.uint8, device=dev)
+    var = torch.empty(int(vb.sum()), dtype=torch.uint8, device=dev)
+    if stream is None:
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    N.check(N.lib.dq_freq_partition(table.handle, n_parts, rec.data_ptr() if rec.numel() else None,
+                                    var.data_ptr() if var.numel() else None, stream))
+    return rec, var, rc, vb, sp
+
+
+def exchange_segments(rec, var, rec_counts, var_bytes):
+    """All-to-all of owner segments (segment j of every rank goes to rank j): one all-to-all of the
+    sizes, then one of the fixed records and one of the encoded keys.  Over RCCL each peer pair has
+    its own xGMI link, so the exchange runs on all 7 links at once.  Returns the received
+    (records, var, src_rec_counts, src_var_bytes), sources in rank order."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    dev = rec.device
+    sizes = torch.from_numpy(np.stack([rec_counts, var_bytes], 1).reshape(-1).copy()).to(dev)
+    got = torch.empty_like(sizes)
+    dist.all_to_all_single(got, sizes)
+    got = got.cpu().numpy().reshape(world, 2)
+    src_rc, src_vb = got[:, 0].copy(), got[:, 1].copy()
+    rb = N.FREQ_RECORD_BYTES
+    recv_rec = torch.empty(int(src_rc.sum()) * rb, dtype=torch.uint8, device=dev)
+    dist.all_to_all_single(recv_rec, rec, output_split_sizes=(src_rc * rb).tolist(),
+                           input_split_sizes=(np.asarray(rec_counts) * rb).tolist())
+    recv_var = torch.empty(int(src_vb.sum()), dtype=torch.uint8, device=dev)
+    if int(np.sum(var_bytes)) or int(src_vb.sum()):
+        dist.all_to_all_single(recv_var, var, output_split_sizes=src_vb.tolist(),
+                               input_split_sizes=np.asarray(var_bytes).tolist())
+    return recv_rec, recv_var, src_rc, src_vb
+
+
+def freq_add_records(table, rec, var, src_rc, src_vb, num_rows: int, special,
+                     null_as_group: bool = False, stream=None) -> None:
+    import torch
+    n_src = len(src_rc)
+    rc = np.ascontiguousarray(src_rc, np.int64)
+    vb = np.ascontiguousarray(src_vb, np.int64)
+    sp = np.ascontiguousarray(special, np.int64)
+    if stream is None:
+        stream = ctypes.c_void_p(torch.cuda.current_stream(f"cuda:{table.device}").cuda_stream)
+    N.check(N.lib.dq_freq_add_records_device(
+        table.handle, rec.data_ptr() if rec.numel() else None,
+        var.data_ptr() if var.numel() else None, n_src, rc.ctypes.data, vb.ctypes.data,
+        int(num_rows), sp.ctypes.data, 1 if null_as_group else 0, stream))
+
+
+def freq_repartition(local, null_as_group: bool = False):
+    """The Exchange + final aggregate of the distributed groupBy: every rank partitions its partial
+    table by owner, the segments meet in one all-to-all, and each rank counts the groups it owns.
+    Afterwards every group lives on exactly one rank; every rank's numRows is the global row count
+    (data.count(), GroupingAnalyzers.scala:74-77); the outside-table groups live on rank 0."""
+    import torch
+    import torch.distributed as dist
+    from .analyzers.grouping import FrequencyTable
+    world, rank = dist.get_world_size(), dist.get_rank()
+    rec, var, rc, vb, sp = freq_partition(local, world)
+    recv_rec, recv_var, src_rc, src_vb = exchange_segments(rec, var, rc, vb)
+    tot = torch.tensor([local.num_rows, *sp.tolist()], dtype=torch.int64, device=rec.device)
+    dist.all_reduce(tot)
+    tot = tot.cpu().numpy()
+    owned = FrequencyTable(local.key_columns, local.key_types, local.device,
+                           capacity_hint=int(src_rc.sum()))
+    special = tot[1:] if rank == 0 else np.zeros(3, np.int64)
+    freq_add_records(owned, recv_rec, recv_var, src_rc, src_vb, int(tot[0]), special, null_as_group)
+    return owned
+
+
+class DistributedFrequencies:
+    """The frequency table of a distributed groupBy: each rank holds the groups it owns.  The one
+    aggregation over the table (AnalysisRunner.scala:490-500) is a local summary plus an int64 sum
+    all-reduce and a rank-ordered fp64 sum of the entropy partials (deterministic)."""
+
+    def __init__(self, owned):
+        self.owned = owned
+        self.key_columns = owned.key_columns
+        self.key_types = owned.key_types
+
+    @property
+    def num_rows(self) -> int:
+        return self.owned.num_rows
+
+    def summarize(self):
+        import torch
+        import torch.distributed as dist
+        s = self.owned.summarize()
+        dev = "cpu" if dist.get_backend() == "gloo" else f"cuda:{self.owned.device}"
+        ints = torch.tensor([s.n_groups, s.n_unique, s.n_null_key_rows], dtype=torch.int64,
+                            device=dev)
+        dist.all_reduce(ints)
+        ent = torch.tensor([s.entropy], dtype=torch.float64, device=dev)
+        parts = torch.empty(dist.get_world_size(), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(parts, ent)
+        out = N.dq_freq_summary()
+        out.num_rows = s.num_rows
+        out.n_groups, out.n_unique, out.n_null_key_rows = (int(v) for v in ints.cpu().tolist())
+        total = 0.0
+        for v in parts.cpu().tolist():  # rank order
+            total += v
+        out.entropy = total
+        return out
+
+    def count(self) -> int:
+        return int(self.summarize().n_groups)
+
+
+def compute_frequencies_distributed(data_shard, grouping_columns):
+    """FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:53-80) over a row-sharded
+    table: local partial aggregate on each rank's shard, then freq_repartition."""
+    from .analyzers.grouping import FrequenciesAndNumRows, compute_frequencies
+    local = compute_frequencies(data_shard, grouping_columns).frequencies
+    owned = freq_repartition(local)
+    return FrequenciesAndNumRows(DistributedFrequencies(owned), owned.num_rows)

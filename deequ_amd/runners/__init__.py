@@ -207,8 +207,14 @@ def _run_scanning_analyzers(data, analyzers: Sequence[Analyzer], aggregate_with,
 
 def _run_grouping_analyzers(data, grouping_columns, analyzers, aggregate_with, save_states_with,
                             num_rows_of_data):
-    """AnalysisRunner.runGroupingAnalyzers (AnalysisRunner.scala:249-277)."""
-    state = compute_frequencies(data, grouping_columns)
+    """AnalysisRunner.runGroupingAnalyzers (AnalysisRunner.scala:249-277).  The reference's
+    groupBy is lazy, so a failure of the grouping surfaces inside the one aggregation over the
+    frequencies, whose try fails every analyzer of the grouping (:490-505); the engine's eager
+    group-by error is mapped the same way."""
+    try:
+        state = compute_frequencies(data, grouping_columns)
+    except Exception as e:  # noqa: BLE001
+        return None, AnalyzerContext({a: a.to_failure_metric(e) for a in analyzers})
     sample = analyzers[0]
     if aggregate_with is not None:
         prev = aggregate_with.load(sample)

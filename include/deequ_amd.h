@@ -306,6 +306,40 @@ dq_status dq_freq_export(dq_freq* freq, int64_t* counts_out, int64_t* key_offset
 dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src);
 
 /* ------------------------------------------------------------------------------------------------
+ * Multi-GPU frequency path: hash repartition.
+ *
+ * Replaces the hash-partitioned Exchange between Spark's partial and final HashAggregate of the
+ * groupBy in computeFrequencies (GroupingAnalyzers.scala:67-72).  Each rank's table is the partial
+ * aggregate of its row shard.  dq_freq_partition cuts its groups into n_parts owner segments
+ * (owner = a hash of the group key, so every group has exactly one owner); the caller exchanges
+ * the segments with an all-to-all (RCCL over xGMI) and each owner re-inserts what it received with
+ * dq_freq_add_records_device, which adds counts of equal keys exactly like FrequenciesAndNumRows.sum
+ * (GroupingAnalyzers.scala:128-148).  Records are device memory; var holds the encoded keys of
+ * hashed-mode tables (string / multi-column / NULL-group keys), 8-byte aligned per group.
+ * ---------------------------------------------------------------------------------------------- */
+typedef struct dq_freq_record {
+  uint64_t key;     /* exact mode: the widened key value; hashed mode: the 64-bit group hash      */
+  uint64_t count;   /* rows in the group                                                          */
+  uint64_t enc_off; /* hashed mode: byte offset of the encoded key within the segment's var bytes */
+} dq_freq_record;
+/* Per owner: rec_counts[n_parts] records and var_bytes[n_parts] bytes.  special[3] = the groups
+ * kept outside the slot table, which the caller routes to ONE owner: {count of the key equal to
+ * INT64_MIN in exact mode, count of the NULL group (Histogram), rows skipped for a NULL key}. */
+dq_status dq_freq_partition_sizes(dq_freq* freq, int n_parts, int64_t* rec_counts,
+                                  int64_t* var_bytes, int64_t* special);
+/* Writes the owner segments back to back (segment j at the exclusive prefix sums of the sizes
+ * above) into device buffers records[Σ rec_counts] and var[Σ var_bytes]. */
+dq_status dq_freq_partition(dq_freq* freq, int n_parts, dq_freq_record* records, uint8_t* var,
+                            void* hip_stream);
+/* Inserts n_src received segments laid back to back (src_records[j] records, src_var_bytes[j]
+ * var bytes each), adds num_rows to the table's numRows and special[3] to its outside-table groups.
+ * A 64-bit hash collision between distinct groups is detected (DQ_ERR_UNSUPPORTED), never merged. */
+dq_status dq_freq_add_records_device(dq_freq* freq, const dq_freq_record* records,
+                                     const uint8_t* var, int n_src, const int64_t* src_records,
+                                     const int64_t* src_var_bytes, int64_t num_rows,
+                                     const int64_t* special, int null_as_group, void* hip_stream);
+
+/* ------------------------------------------------------------------------------------------------
  * Columnar handoff: host-resident Arrow batches -> HBM (the JNI shim's entry).
  *
  * In the reference a Spark partition's rows stream through the aggregation iterator of the one

@@ -131,3 +131,57 @@ def test_gloo_world2_merge_matches_single_pass(n):
     assert sd[0] == xs.size
     assert sd[1] == pytest.approx(f.mean(), rel=1e-12)
     assert sd[2] == pytest.approx(m2, rel=1e-12)
+
+
+def _exchange_worker(rank, world, port, out_q):
+    """Each rank sends owner segment j (records tagged (src, dst, i), var bytes tagged too) to rank
+    j through the product's exchange step (deequ_amd.distributed.exchange_segments)."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from deequ_amd.distributed import exchange_segments
+        rc = np.array([(rank + 2 * j) % 4 for j in range(world)], np.int64)   # ragged, some empty
+        vb = np.array([8 * ((rank * 3 + j) % 3) for j in range(world)], np.int64)
+        recs, var = [], []
+        for j in range(world):
+            for i in range(int(rc[j])):
+                recs.append(np.array([rank, j, i], np.uint64))
+            var.append(np.full(int(vb[j]), 16 * rank + j, np.uint8))
+        rec_t = torch.from_numpy(np.concatenate(recs).view(np.uint8).copy() if recs
+                                 else np.zeros(0, np.uint8))
+        var_t = torch.from_numpy(np.concatenate(var))
+        got_rec, got_var, src_rc, src_vb = exchange_segments(rec_t, var_t, rc, vb)
+        out_q.put((rank, got_rec.numpy().view(np.uint64).reshape(-1, 3).tolist(),
+                   got_var.numpy().tolist(), src_rc.tolist(), src_vb.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world3_frequency_segment_exchange():
+    """The all-to-all of the multi-GPU frequency path routes owner segment j of
+    every rank to rank j, sources in rank order, with ragged and empty segments."""
+    import torch.multiprocessing as mp
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (rec, var, rc, vb) for r, rec, var, rc, vb in (q.get(timeout=180) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for dst in range(world):
+        rec, var, rc, vb = res[dst]
+        exp_rec, exp_var = [], []
+        for src in range(world):
+            n = (src + 2 * dst) % 4
+            exp_rec += [[src, dst, i] for i in range(n)]
+            exp_var += [16 * src + dst] * (8 * ((src * 3 + dst) % 3))
+            assert rc[src] == n
+        assert rec == exp_rec
+        assert var == exp_var
