@@ -192,7 +192,7 @@ def main():
                 "traffic": load_traffic(args.rows, b_alg),
                 "algorithmic_bytes_per_launch": b_alg,
                 "scan_ms": scan_ms,
-                "kernel": "dq::scan_kernel<false> (+ finalize_kernel)",
+                "kernel": "dq::scan_mixed_kernel (+ finalize1/finalize2)",
             },
         }
         if not args.no_cpu_baseline:
