@@ -629,7 +629,12 @@ extern "C" int dq_plan_launches_per_batch(const dq_plan* plan) {
     if (c == BC_HLL) hll = used ? 1 : 0;
     else classes += used ? 1 : 0;
   }
-  // two or more non-HLL body classes share one mixed launch (dq_scan_device_batches)
+  // two or more body classes share one mixed launch (dq_scan_device_batches); HLL joins it when
+  // its LDS registers fit (kMixedHllMax)
+  if (hll && plan->n_hll <= kMixedHllMax && classes >= 1) {
+    classes += 1;
+    hll = 0;
+  }
   if (classes >= 2 && !getenv("DQ_NO_MIXED")) classes = 1;
   // expression bitmaps + the scan launches + the two finalize launches
   return (int)plan->mat.size() + classes + hll + (plan->tasks.empty() ? 0 : 2);
@@ -642,6 +647,7 @@ struct dq_state {
   const dq_plan* plan = nullptr;
   int device = 0;
   int grid[kQueues] = {};        // persistent grid of each scan kernel (+ the mixed kernel)
+  int mix_hll = 0;               // HLL tasks carried by the mixed launch (0: HLL launches alone)
   hipStream_t stream = nullptr;
   bool stream_set = false;
   // host mirror
@@ -732,7 +738,10 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
     const int c = body_class(plan, t);
     if (!s->grid[c]) s->grid[c] = std::max(1, cus * std::min(scan_max_blocks_per_cu(c, plan->n_hll), 8));
   }
-  s->grid[kBodyMixed] = std::max(1, cus * std::min(scan_max_blocks_per_cu(kBodyMixed, 0), 8));
+  // the mixed launch also carries the HLL items when their LDS registers fit beside it
+  s->mix_hll = plan->n_hll <= kMixedHllMax ? plan->n_hll : 0;
+  s->grid[kBodyMixed] =
+      std::max(1, cus * std::min(scan_max_blocks_per_cu(kBodyMixed, s->mix_hll), 8));
   const size_t nt = std::max<size_t>(1, plan->tasks.size());
   HIP_TRY(s->d_acc.ensure(nt));
   HIP_TRY(s->d_hll.ensure(std::max(1, plan->n_hll) * (size_t)kHllM));
@@ -1077,19 +1086,21 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
   if (total_items >= ((int64_t)1 << 31))
     return fail(DQ_ERR_UNSUPPORTED, "scan of %lld work items exceeds one launch",
                 (long long)total_items);
-  // Two or more non-HLL classes: one mixed launch over their items, interleaved in proportion to
+  // Two or more body classes: one mixed launch over their items, interleaved in proportion to
   // each class's item count (item j of a class with n items sorts at (j + 1/2) / n), so string
-  // gathers and streaming bodies run side by side.  HLL keeps its own launch (LDS registers).
+  // gathers, XXH64 hashing and streaming bodies run side by side.  HLL joins the mixed launch when
+  // its LDS registers fit (s->mix_hll), else it keeps its own launch.
   {
     std::vector<ScanLaunch> plain, hll;
-    for (const ScanLaunch& L : launches) (L.body == BC_HLL ? hll : plain).push_back(L);
+    for (const ScanLaunch& L : launches)
+      (L.body == BC_HLL && !s->mix_hll ? hll : plain).push_back(L);
     if (plain.size() >= 2 && !getenv("DQ_NO_MIXED")) {
       std::vector<uint32_t> sig;
       for (const ScanLaunch& L : plain) {
         sig.push_back(L.item_lo);
         sig.push_back(L.item_hi);
       }
-      const uint32_t n_order = plain.back().item_hi;  // non-HLL classes precede BC_HLL
+      const uint32_t n_order = plain.back().item_hi;  // classes are numbered in item order
       if (plain.front().item_lo != 0) return fail(DQ_ERR_STATE, "unexpected item layout");
       if (s->order_sig[slot] != sig) {
         std::vector<uint32_t> order;
@@ -1115,7 +1126,10 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
         s->order_sig[slot] = sig;
       }
       launches.clear();
-      launches.push_back(ScanLaunch{kBodyMixed, s->grid[kBodyMixed], 0, n_order, s->d_order[slot].p});
+      bool has_hll = false;
+      for (const ScanLaunch& L : plain) has_hll = has_hll || L.body == BC_HLL;
+      launches.push_back(ScanLaunch{kBodyMixed, s->grid[kBodyMixed], 0, n_order,
+                                    s->d_order[slot].p, has_hll ? s->mix_hll : 0});
       for (const ScanLaunch& L : hll) launches.push_back(L);
     }
   }

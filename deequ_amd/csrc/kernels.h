@@ -114,7 +114,14 @@ struct ScanLaunch {
   int32_t grid;
   uint32_t item_lo, item_hi;  // kBodyMixed: item_lo = 0, item_hi = entries of `order`
   const uint32_t* order;   // kBodyMixed: queue position -> global item index
+  int32_t lds_hll = 0;     // kBodyMixed: HLL tasks whose registers the launch keeps in LDS
 };
+
+// Most HLL tasks whose LDS registers (2 KiB each) ride in the mixed launch.  0 = HLL always keeps
+// its own launch: measured on MI355X (profiles/r1e, configs[3] at 1.25e9 rows), HLL inside the
+// mixed grid took 11.19 ms vs 6.67 + 3.78 ms as two launches -- the XXH64 body is bound by
+// quarter-rate 64-bit multiplies and needs the occupancy the mixed kernel's 3 waves/SIMD denies.
+constexpr int kMixedHllMax = 0;
 
 // Fused scan over n_desc (task, batch) descriptors numbered class-major then task-major (each
 // logical task owns one contiguous range of work items), one launch per entry of `launches`, then

@@ -546,9 +546,53 @@ DQ_DEV void corr_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
 // TK_HLL: the workgroup's 512 registers of each HLL task live in LDS (one u32 per register);
 // atomicMax only when the rank can raise the register.  Flushed once per workgroup at the end.
 // ------------------------------------------------------------------------------------------------
+DQ_DEV uint32_t bits32(const uint8_t* bm, int64_t word) {
+  return bm ? reinterpret_cast<const uint32_t*>(bm)[word] : ~0u;
+}
+
+DQ_DEV void hll_update(uint32_t* regs, uint64_t h) {
+  uint32_t idx, pw;
+  hll_index_rank(h, idx, pw);
+  if (pw > regs[idx]) atomicMax(&regs[idx], pw);
+}
+
+// 8-byte keys (Long, Double), 1024 rows per wave: eight 16-byte loads per lane in flight (each
+// wave-instruction one contiguous 1 KiB), lane l owns rows r0 + 128k + 2l and +1; their validity /
+// where bits come from one dword per bitmap and k (L1-resident, the wave's 128-byte slice).
+DQ_DEV void hll_chunk8(const TaskDesc& t, int64_t r0, bool dbl, uint32_t* regs) {
+  const int l = lane_id();
+  const uint64_t* v = reinterpret_cast<const uint64_t*>(t.values);
+  uint4 q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) q[k] = *reinterpret_cast<const uint4*>(v + r0 + 128 * k + 2 * l);
+  const int64_t w0 = (r0 >> 5) + (l >> 4);
+  const uint32_t sh = (uint32_t)(2 * l) & 31u;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t w = w0 + 4 * k;
+    uint32_t s = bits32(t.valid, w);
+    if (t.w_val) s &= bits32(t.w_val, w) & bits32(t.w_vld, w);
+    s = (s >> sh) & 3u;
+    uint64_t x0 = (uint64_t)q[k].x | ((uint64_t)q[k].y << 32);
+    uint64_t x1 = (uint64_t)q[k].z | ((uint64_t)q[k].w << 32);
+    if (dbl) {  // doubleToLongBits: every NaN hashes as the canonical one
+      if (__builtin_bit_cast(double, x0) != __builtin_bit_cast(double, x0)) x0 = 0x7ff8000000000000ULL;
+      if (__builtin_bit_cast(double, x1) != __builtin_bit_cast(double, x1)) x1 = 0x7ff8000000000000ULL;
+    }
+    const uint64_t h0 = xxh_long(x0, 42), h1 = xxh_long(x1, 42);
+    if (s & 1u) hll_update(regs, h0);
+    if (s & 2u) hll_update(regs, h1);
+  }
+}
+
 DQ_DEV void hll_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint32_t* regs) {
   const int l = lane_id();
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += 256) {
+  int64_t r_fast = r_begin;
+  if (t.vec_ok && (t.type == DQ_INT64 || t.type == DQ_FLOAT64)) {
+    const bool dbl = t.type == DQ_FLOAT64;
+    for (; r_fast + 1024 <= r_end; r_fast += 1024) hll_chunk8(t, r_fast, dbl, regs);
+  }
+  for (int64_t r0 = r_fast; r0 < r_end; r0 += 256) {
 #pragma unroll 2
     for (int k = 0; k < 4; ++k) {
       const int64_t r = r0 + 64 * k + l;
@@ -556,10 +600,7 @@ DQ_DEV void hll_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint32_t
       uint32_t s = bit1(t.valid, r);
       if (t.w_val) s &= bit1(t.w_val, r) & bit1(t.w_vld, r);
       if (!s) continue;
-      const uint64_t x = hash_row(t.type, t.values, t.data, r);
-      uint32_t idx, pw;
-      hll_index_rank(x, idx, pw);
-      if (pw > regs[idx]) atomicMax(&regs[idx], pw);
+      hll_update(regs, hash_row(t.type, t.values, t.data, r));
     }
   }
 }
@@ -641,7 +682,14 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const TaskDesc* __restrict
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 3)))
 scan_mixed_kernel(const TaskDesc* __restrict__ tasks, int n_desc, uint32_t n_order,
                   const uint32_t* __restrict__ order, uint32_t* __restrict__ queue,
-                  Acc* __restrict__ partial) {
+                  Acc* __restrict__ partial, uint32_t* __restrict__ hll_stage, int n_hll) {
+  // HLL items (compute-bound XXH64) interleave with the streaming bodies; their registers live in
+  // this workgroup's LDS as in scan_kernel<BC_HLL> and are flushed once at the end
+  extern __shared__ uint32_t mix_lds[];
+  if (n_hll) {
+    for (int i = threadIdx.x; i < n_hll * kHllM; i += kBlock) mix_lds[i] = 0;
+    __syncthreads();
+  }
   const int l = lane_id();
   for (uint32_t guard = 0; guard <= n_order; ++guard) {
     uint32_t q = 0;
@@ -670,10 +718,18 @@ scan_mixed_kernel(const TaskDesc* __restrict__ tasks, int n_desc, uint32_t n_ord
       case BC_BITS: bits_item(t, r_begin, r_end, a); break;
       case BC_STR_IN: str_in_item(t, r_begin, r_end, a); break;
       case BC_CORR: corr_item(t, r_begin, r_end, a); break;
+      case BC_HLL: hll_item(t, r_begin, r_end, mix_lds + t.hll_out * kHllM); continue;
       default: break;
     }
     wave_reduce(t.kind, a);
     if (l == 0) partial[item] = a;
+  }
+  if (n_hll) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < n_hll * kHllM; i += kBlock) {
+      const uint32_t v = mix_lds[i];
+      if (v) atomicMax(&hll_stage[i], v);
+    }
   }
 }
 
@@ -780,8 +836,10 @@ hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const Sca
     const ScanLaunch& L = launches[k];
     if (L.item_hi <= L.item_lo) continue;
     if (L.body == kBodyMixed) {
-      hipLaunchKernelGGL(scan_mixed_kernel, dim3(L.grid), dim3(kBlock), 0, stream, tasks, n_desc,
-                         L.item_hi, L.order, queues + kBodyMixed, partial);
+      const int mix_hll = L.lds_hll;
+      hipLaunchKernelGGL(scan_mixed_kernel, dim3(L.grid), dim3(kBlock),
+                         (size_t)mix_hll * kHllM * 4, stream, tasks, n_desc, L.item_hi, L.order,
+                         queues + kBodyMixed, partial, hll_stage, mix_hll);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       continue;
@@ -825,7 +883,8 @@ int scan_max_blocks_per_cu(int body, int n_hll) {
     case BC_HLL: return occupancy_of<BC_HLL>(n_hll);
     case kBodyMixed: {
       int n = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_mixed_kernel, kBlock, 0) != hipSuccess)
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_mixed_kernel, kBlock,
+                                                       (size_t)n_hll * kHllM * 4) != hipSuccess)
         n = 2;
       return n > 0 ? n : 1;
     }

@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Single-GPU measurements of BASELINE.json configs[2] and configs[3] (the default bench.py line is
+configs[1], S10).  Not part of the driver's bench contract; the JSON lines land in profiles/.
+
+  c3: Uniqueness + Distinctness + Entropy + Histogram-style grouping on the high-cardinality int64
+      `id` (exact-mode hash group-by, ~N groups) and the 3-value string `priority` (hashed mode,
+      LDS-resident groups).  One step = both group-bys over the table resident in HBM + the one
+      aggregation over each frequency table (dq_freq_summarize).
+      B_alg = key bytes read once: id validity + values (8.125 B/row);
+      priority validity + offsets + bytes.  Hash-table traffic excluded.
+  c4: ApproxCountDistinct(id) (HLL++, P = 9) + Correlation(id, score) on an Item table with an
+      fp64 `score` column.  One step = the fused scan (HLL launch + co-moment launch + finalize).
+      B_alg = id validity + values + score validity + values = 16.25 B/row.
+
+Usage: python tools/bench_workloads.py c3|c4 [--rows N] [--steps K] [--warmup W]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PEAK = 8.0e12
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("workload", choices=["c3", "c4"])
+    ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch-rows", type=int, default=1 << 26)
+    args = ap.parse_args()
+    import torch
+    dev = "cuda:0"
+    from deequ_amd.synth import item_table_device
+    rows = args.rows or (1_000_000_000 if args.workload == "c3" else 1_250_000_000)
+    table = item_table_device(rows, seed=9, batch_rows=args.batch_rows, device=dev,
+                              extra=args.workload == "c4")
+    stream = torch.cuda.current_stream(dev)
+    e0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    e1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    nb = lambda n: (n + 7) // 8  # noqa: E731
+
+    if args.workload == "c3":
+        from deequ_amd import _native as N
+        from deequ_amd.analyzers.grouping import FrequencyTable
+
+        def step():
+            out = {}
+            for col, ty in (("id", N.INT64), ("priority", N.UTF8)):
+                ft = FrequencyTable([col], [ty], 0, capacity_hint=rows if col == "id" else 0)
+                for b in table.batches:
+                    ft.add([b[col]])
+                s = ft.summarize()
+                out[col] = (s.n_groups, s.n_unique, s.entropy)
+                del ft
+            return out
+        b_alg = 0
+        for b in table.batches:
+            m = b["id"].length
+            b_alg += nb(m) + 8 * m + nb(m) + 4 * (m + 1) + int(b["priority"].values[m].item())
+        kernel = "dq::freq_insert_kernel (+ freq_verify_kernel for priority, freq_summary_kernel)"
+        desc = ("Uniqueness/Distinctness/Entropy grouping on int64 id (~N groups, exact mode) and "
+                "string priority (3 groups, hashed mode) over a synthetic Item table, 5% nulls "
+                "(BASELINE.json configs[2], 1 GPU)")
+        metric_unit = "rows/s"
+    else:
+        from deequ_amd import _native as N
+        from deequ_amd.analyzers import ApproxCountDistinct, Correlation
+        from deequ_amd.runners.engine import get_plan, read_row, scan_into
+        suite = [ApproxCountDistinct("id"), Correlation("id", "score")]
+        specs = [s for a in suite for s in a.aggregation_functions()]
+        plan = get_plan(table.schema, specs)
+        state = plan.state(0)
+        sh = ctypes.c_void_p(stream.cuda_stream)
+
+        def step():
+            N.check(N.lib.dq_state_reset(state))
+            scan_into(table, plan, state, sh)
+            N.check(N.lib.dq_state_sync(state))
+            return read_row(plan, state)
+        b_alg = 0
+        for b in table.batches:
+            m = b["id"].length
+            b_alg += 2 * nb(m) + 16 * m
+        kernel = "dq::scan_kernel<HLL> + dq::scan_mixed_kernel (co-moments) + finalize"
+        desc = ("ApproxCountDistinct(id) + Correlation(id, score) over a synthetic Item table "
+                "with fp64 score, 5% nulls (BASELINE.json configs[3], per-GPU shard of 1e10 "
+                "rows over 8 GPUs = 1.25e9 rows, 1 GPU)")
+        metric_unit = "rows/s"
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        e0[i].record(stream)
+        res = step()
+        e1[i].record(stream)
+    torch.cuda.synchronize(dev)
+    el = (time.perf_counter() - t0) / args.steps
+    dev_ms = sum(a.elapsed_time(b) for a, b in zip(e0, e1)) / args.steps
+    achieved = b_alg / (dev_ms * 1e-3)
+    print(json.dumps({
+        "workload": args.workload, "desc": desc, "rows": rows, "unit": metric_unit,
+        "value": rows / el, "ms_per_step": el * 1e3, "device_ms_per_step": dev_ms,
+        "steps": args.steps, "warmup": args.warmup,
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK / 1e9,
+                     "unit": "GB/s", "frac": achieved / PEAK, "algorithmic_bytes": b_alg,
+                     "kernel": kernel},
+        "result": repr(res)[:300],
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

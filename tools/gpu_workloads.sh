@@ -1,0 +1,14 @@
+#!/bin/bash
+# configs[2] / configs[3] single-GPU measurements + rocprofv3 kernel stats (tools/bench_workloads.py)
+set -o pipefail
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+O=gpurun_out
+T=${TAG:-r1c}
+mkdir -p $O
+timeout -k 10 120 python -u tools/bench_workloads.py c3 --rows 1000000 --steps 2 > $O/wl_c3_small_$T.json 2>&1 &&
+timeout -k 10 120 python -u tools/bench_workloads.py c4 --rows 1000000 --steps 2 > $O/wl_c4_small_$T.json 2>&1 &&
+timeout -k 10 300 python -u tools/bench_workloads.py c4 > $O/wl_c4_$T.json 2>&1 &&
+timeout -k 10 400 python -u tools/bench_workloads.py c3 --steps 3 > $O/wl_c3_$T.json 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c4_$T -o run -- python3 tools/bench_workloads.py c4 --steps 3 > $O/prof_c4_$T.log 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_$T -o run -- python3 tools/bench_workloads.py c3 --steps 2 > $O/prof_c3_$T.log 2>&1
