@@ -9,5 +9,7 @@ from .metrics import (Distribution, DistributionValue, DoubleMetric, Entity, Fai
                       HistogramMetric, KeyedDoubleMetric, Success)
 from .runners import Analysis, AnalysisRunner, AnalyzerContext  # noqa: F401
 from .table import Table  # noqa: F401
+from .checks import Check, CheckLevel, CheckResult, CheckStatus, ConstraintStatus  # noqa: F401
+from .verification import VerificationResult, VerificationSuite  # noqa: F401
 
 __version__ = "0.1.0"
