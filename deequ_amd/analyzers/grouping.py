@@ -55,6 +55,13 @@ class FrequencyTable:
         N.check(N.lib.dq_freq_add_device(self.handle, arr, len(columns), 1 if null_as_group else 0,
                                          stream))
 
+    def reset(self, stream=None) -> None:
+        """Empties the table, keeping its device capacity (dq_freq_reset)."""
+        if stream is None:
+            import torch
+            stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        N.check(N.lib.dq_freq_reset(self.handle, stream))
+
     @property
     def num_rows(self) -> int:
         return int(N.lib.dq_freq_num_rows(self.handle))

@@ -247,18 +247,28 @@ DQ_DEV void write_arena(const FreqDev& f, uint64_t slot, const ArenaSrc& s) {
   f.reps[slot] = off;
 }
 
+// Sum over the wave, added to a table counter by lane 0: the counters are single addresses, so
+// one atomic per row (every new group, every NULL row) would serialize the whole launch on them.
+// Every lane of the wave must call it (the kernels call it after their row loops).
+DQ_DEV void wave_count(unsigned long long* counter, unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (__lane_id() == 0 && v) atomicAdd(counter, v);
+}
+
+// Returns 1 when the call created the group (the caller counts C_OCCUPIED with wave_count).
 template <typename Src>
-DQ_DEV void insert_global(const FreqDev& f, uint64_t key, uint64_t cnt, const Src& src) {
+DQ_DEV uint32_t insert_global(const FreqDev& f, uint64_t key, uint64_t cnt, const Src& src) {
   if (f.exact && key == kEmpty) {
     atomicAdd(&f.counters[C_SENTINEL], (unsigned long long)cnt);
-    return;
+    return 0;
   }
   uint64_t slot = (f.exact ? mix64(key) : key) & f.mask;
   for (uint64_t probe = 0; probe <= f.mask; ++probe) {
     uint64_t k = __hip_atomic_load(&f.keys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (k == key) {
       atomicAdd(reinterpret_cast<unsigned long long*>(&f.counts[slot]), (unsigned long long)cnt);
-      return;
+      return 0;
     }
     if (k == kEmpty) {
       unsigned long long prev =
@@ -266,18 +276,18 @@ DQ_DEV void insert_global(const FreqDev& f, uint64_t key, uint64_t cnt, const Sr
                     (unsigned long long)key);
       if (prev == kEmpty) {
         atomicAdd(reinterpret_cast<unsigned long long*>(&f.counts[slot]), (unsigned long long)cnt);
-        atomicAdd(&f.counters[C_OCCUPIED], 1ULL);
         if (!f.exact) write_arena(f, slot, src);
-        return;
+        return 1;
       }
       if (prev == key) {
         atomicAdd(reinterpret_cast<unsigned long long*>(&f.counts[slot]), (unsigned long long)cnt);
-        return;
+        return 0;
       }
     }
     slot = (slot + 1) & f.mask;
   }
   atomicAdd(&f.counters[C_ARENA_OVF], 1ULL);  // table full: the host sized it, cannot happen
+  return 0;
 }
 
 __global__ void __launch_bounds__(256) freq_insert_kernel(FreqDev f, int64_t rows, int64_t chunk) {
@@ -291,7 +301,7 @@ __global__ void __launch_bounds__(256) freq_insert_kernel(FreqDev f, int64_t row
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * chunk;
   const int64_t r1 = min(r0 + chunk, rows);
-  unsigned long long nulls = 0, null_group = 0, sentinel = 0;
+  unsigned long long nulls = 0, null_group = 0, sentinel = 0, created = 0;
   for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
     uint64_t key;
     bool is_null;
@@ -328,15 +338,16 @@ __global__ void __launch_bounds__(256) freq_insert_kernel(FreqDev f, int64_t row
       }
       ls = (ls + 1) & (kLdsSlots - 1);
     }
-    if (!done) insert_global(f, key, 1, RowSrc{r});
+    if (!done) created += insert_global(f, key, 1, RowSrc{r});
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kLdsSlots; i += blockDim.x) {
-    if (lkeys[i] != kEmpty) insert_global(f, lkeys[i], lcnt[i], RowSrc{lrep[i]});
+    if (lkeys[i] != kEmpty) created += insert_global(f, lkeys[i], lcnt[i], RowSrc{lrep[i]});
   }
-  if (nulls) atomicAdd(&f.counters[C_NULL_ROWS], nulls);
-  if (null_group) atomicAdd(&f.counters[C_NULL_GROUP], null_group);
-  if (sentinel) atomicAdd(&f.counters[C_SENTINEL], sentinel);
+  wave_count(&f.counters[C_OCCUPIED], created);
+  wave_count(&f.counters[C_NULL_ROWS], nulls);
+  wave_count(&f.counters[C_NULL_GROUP], null_group);
+  wave_count(&f.counters[C_SENTINEL], sentinel);
 }
 
 DQ_DEV int64_t find_slot(const FreqDev& f, uint64_t key) {
@@ -368,13 +379,14 @@ __global__ void __launch_bounds__(256) freq_merge_kernel(FreqDev dst, const uint
                                                          const uint64_t* counts, const uint64_t* reps,
                                                          const uint8_t* arena, uint64_t cap,
                                                          int n_keys) {
+  unsigned long long created = 0;
   for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
        s += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t k = keys[s];
     if (k == kEmpty) continue;
     uint64_t c = counts[s];
     if (dst.exact) {
-      insert_global(dst, k, c, RowSrc{0});
+      created += insert_global(dst, k, c, RowSrc{0});
     } else {
       const uint8_t* enc = arena + reps[s];
       // size of the encoded record
@@ -392,9 +404,10 @@ __global__ void __launch_bounds__(256) freq_merge_kernel(FreqDev dst, const uint
           size += 8;
         }
       }
-      insert_global(dst, k, c, ArenaSrc{enc, size});
+      created += insert_global(dst, k, c, ArenaSrc{enc, size});
     }
   }
+  wave_count(&dst.counters[C_OCCUPIED], created);
 }
 
 // Σ[count == 1], count(*), Σ −(c/n)·ln(c/n): per-block partials in a fixed slot order.
@@ -562,16 +575,19 @@ __global__ void __launch_bounds__(256) freq_insert_records_kernel(FreqDev f, con
                                                                   const uint8_t* var, SrcSegs segs,
                                                                   PartArgs a) {
   const int64_t n = segs.rec_start[segs.n_src];
+  unsigned long long created = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     FreqRecord r = rec[i];
     if (f.exact) {
-      insert_global(f, r.key, r.count, RowSrc{0});
+      created += insert_global(f, r.key, r.count, RowSrc{0});
     } else {
       const uint8_t* enc = record_enc(r, i, var, segs);
-      insert_global(f, r.key, r.count, ArenaSrc{enc, enc_record_size(enc, a.types, a.n_keys)});
+      created += insert_global(f, r.key, r.count,
+                               ArenaSrc{enc, enc_record_size(enc, a.types, a.n_keys)});
     }
   }
+  wave_count(&f.counters[C_OCCUPIED], created);
 }
 
 // Hashed mode: every received group must carry the same encoded key as the group it landed in, so
@@ -727,6 +743,25 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
   dq_status st = rehash(f.get(), cap);
   if (st != DQ_OK) return st;
   *out = f.release();
+  return DQ_OK;
+}
+
+// Empties the table but keeps its capacity (slot arrays and arena), like a Spark task reusing its
+// aggregation buffer: repeated group-bys of the same shape pay no device allocation.
+extern "C" dq_status dq_freq_reset(dq_freq* f, void* hip_stream) {
+  if (!f) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  HIP_TRY(hipSetDevice(f->device));
+  f->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  hipLaunchKernelGGL(fill_u64, dim3(grid_for(f->cap)), dim3(256), 0, f->stream, f->keys.p, f->cap,
+                     kEmpty);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemsetAsync(f->counts.p, 0, f->cap * 8, f->stream));
+  HIP_TRY(hipMemsetAsync(f->counters.p, 0, C_N * 8, f->stream));
+  HIP_TRY(hipMemsetAsync(f->arena_cursor.p, 0, 8, f->stream));
+  for (int k = 0; k < C_N; ++k) f->h_counters[k] = 0;
+  f->arena_used = 0;
+  f->num_rows = 0;
+  f->mode_null_as_group = -1;
   return DQ_OK;
 }
 

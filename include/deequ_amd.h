@@ -268,6 +268,10 @@ typedef struct dq_freq dq_freq;
 dq_status dq_freq_create(int device, int n_keys, const int32_t* key_types, int64_t capacity_hint,
                          dq_freq** out);
 void dq_freq_destroy(dq_freq* freq);
+/* Empties the table (groups, counters, numRows) and keeps its device capacity, stream-ordered on
+ * `hip_stream`.  Replaces re-creating the per-task aggregation buffer of the grouping job
+ * (GroupingAnalyzers.scala:70, a fresh HashAggregate buffer per task). */
+dq_status dq_freq_reset(dq_freq* freq, void* hip_stream);
 /* Inserts one batch: rows where any key is NULL are skipped but counted in numRows
  * (GroupingAnalyzers.scala:62-77).  Histogram mode (null_as_group != 0) instead maps a NULL key
  * to its own group, like na.fill("NullValue") (Histogram.scala:59-66). */

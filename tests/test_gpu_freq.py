@@ -163,3 +163,22 @@ def test_repartition_histogram_null_group(col, gpu_device):
             assert key not in got
             got[key] = cnt
     assert got == exp
+
+
+@pytest.mark.parametrize("cols", [("id",), ("s",)])
+def test_reset_table_equals_fresh_table(cols, gpu_device):
+    """dq_freq_reset keeps capacity but no groups, counters or numRows."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    t1, t2 = _table(20_000, seed=91), _table(7_000, seed=92)
+    d1, d2 = Table.from_arrow(t1, device=gpu_device), Table.from_arrow(t2, device=gpu_device)
+    types = [d1.schema[c].dtype for c in cols]
+    ft = FrequencyTable(list(cols), types, 0, capacity_hint=20_000)
+    for b in d1.batches:
+        ft.add([b[c] for c in cols])
+    ft.reset()
+    for b in d2.batches:
+        ft.add([b[c] for c in cols])
+    assert ft.num_rows == 7_000
+    assert dict(ft.export()) == O.frequencies(_otable(t2), list(cols))

@@ -49,15 +49,19 @@ def main():
         from deequ_amd import _native as N
         from deequ_amd.analyzers.grouping import FrequencyTable
 
+        # one table per grouping, created once with its capacity and reset every step (the
+        # aggregation buffer is reused; the step still clears it, inserts every row, summarizes)
+        tables = {"id": FrequencyTable(["id"], [N.INT64], 0, capacity_hint=rows),
+                  "priority": FrequencyTable(["priority"], [N.UTF8], 0)}
+
         def step():
             out = {}
-            for col, ty in (("id", N.INT64), ("priority", N.UTF8)):
-                ft = FrequencyTable([col], [ty], 0, capacity_hint=rows if col == "id" else 0)
+            for col, ft in tables.items():
+                ft.reset()
                 for b in table.batches:
                     ft.add([b[col]])
                 s = ft.summarize()
                 out[col] = (s.n_groups, s.n_unique, s.entropy)
-                del ft
             return out
         b_alg = 0
         for b in table.batches:
