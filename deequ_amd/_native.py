@@ -11,7 +11,8 @@ from ctypes import (POINTER, Structure, c_char, c_char_p, c_double, c_int, c_int
                     c_size_t, c_uint8, c_uint64, c_void_p)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdeequ_amd.so")
+# DQ_LIB_PATH: diagnostic A/B builds only (tools/); the product loads the in-tree library
+LIB_PATH = os.environ.get("DQ_LIB_PATH") or os.path.join(_HERE, "libdeequ_amd.so")
 
 # dq_type
 BOOL, INT8, INT16, INT32, INT64, FLOAT32, FLOAT64, UTF8 = range(1, 9)

@@ -25,6 +25,23 @@
 
 namespace dq {
 
+// Once-read streaming loads: 16 bytes per lane, non-temporal by default (DQ_NT_LOADS=0 builds the
+// default-policy variant for A/B measurement).  Every buffer the scan streams is read exactly once.
+#ifndef DQ_NT_LOADS
+#define DQ_NT_LOADS 1
+#endif
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) v4u* gptr;  // global: global_load, not flat_load
+#if DQ_NT_LOADS
+  const v4u v = __builtin_nontemporal_load((gptr)p);
+#else
+  const v4u v = *(gptr)p;
+#endif
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+
 // ------------------------------------------------------------------------------------------------
 // Reductions
 // ------------------------------------------------------------------------------------------------
@@ -172,7 +189,7 @@ DQ_DEV void num_chunk_fast(NumLane& L, const TaskDesc& t, int64_t r0) {
   const T* v = reinterpret_cast<const T*>(t.values) + r0;
   uint4 raw[U];
 #pragma unroll
-  for (int k = 0; k < U; ++k) raw[k] = *reinterpret_cast<const uint4*>(v + (k * 64 + l) * VPL);
+  for (int k = 0; k < U; ++k) raw[k] = ld16(v + (k * 64 + l) * VPL);
   uint32_t vb = 0xffffu, wt = 0xffffu;
   if (t.valid) {
     ChunkBits c;
@@ -266,10 +283,10 @@ DQ_DEV void bits_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int64_t byte = (r0 >> 3) + 1024 * k + 16 * l;
-        a[k] = A ? *reinterpret_cast<const uint4*>(A + byte) : ones;
-        b[k] = B ? *reinterpret_cast<const uint4*>(B + byte) : ones;
-        x[k] = WV ? *reinterpret_cast<const uint4*>(WV + byte) : ones;
-        y[k] = WD ? *reinterpret_cast<const uint4*>(WD + byte) : ones;
+        a[k] = A ? ld16(A + byte) : ones;
+        b[k] = B ? ld16(B + byte) : ones;
+        x[k] = WV ? ld16(WV + byte) : ones;
+        y[k] = WD ? ld16(WD + byte) : ones;
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -282,10 +299,10 @@ DQ_DEV void bits_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
     }
     for (; r0 + 8192 <= r_end; r0 += 8192) {  // 1 KiB of each bitmap per wave-instruction
       const int64_t byte = (r0 >> 3) + 16 * l;
-      const uint4 a = A ? *reinterpret_cast<const uint4*>(A + byte) : ones;
-      const uint4 b = B ? *reinterpret_cast<const uint4*>(B + byte) : ones;
-      const uint4 x = WV ? *reinterpret_cast<const uint4*>(WV + byte) : ones;
-      const uint4 y = WD ? *reinterpret_cast<const uint4*>(WD + byte) : ones;
+      const uint4 a = A ? ld16(A + byte) : ones;
+      const uint4 b = B ? ld16(B + byte) : ones;
+      const uint4 x = WV ? ld16(WV + byte) : ones;
+      const uint4 y = WD ? ld16(WD + byte) : ones;
       const uint32_t m0 = b.x & x.x & y.x, m1 = b.y & x.y & y.y, m2 = b.z & x.z & y.z,
                      m3 = b.w & x.w & y.w;
       c0 += __popc(a.x & m0) + __popc(a.y & m1) + __popc(a.z & m2) + __popc(a.w & m3);
@@ -384,7 +401,10 @@ struct StrStep {
   DQ_DEV void load(const TaskDesc& t, const int32_t* off, int64_t r0, int l) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      q[g] = *reinterpret_cast<const int4*>(off + r0 + 256 * g + 4 * l);
+      {
+        const uint4 u = ld16(off + r0 + 256 * g + 4 * l);
+        q[g] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
+      }
       last[g] = off[r0 + 256 * g + 256];
     }
     if (t.valid) c.load(t.valid, r0);
@@ -564,7 +584,7 @@ DQ_DEV void hll_chunk8(const TaskDesc& t, int64_t r0, bool dbl, uint32_t* regs) 
   const uint64_t* v = reinterpret_cast<const uint64_t*>(t.values);
   uint4 q[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) q[k] = *reinterpret_cast<const uint4*>(v + r0 + 128 * k + 2 * l);
+  for (int k = 0; k < 8; ++k) q[k] = ld16(v + r0 + 128 * k + 2 * l);
   const int64_t w0 = (r0 >> 5) + (l >> 4);
   const uint32_t sh = (uint32_t)(2 * l) & 31u;
 #pragma unroll
