@@ -40,6 +40,18 @@ __device__ __forceinline__ uint4 ld16(const void* p) {
 #endif
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// Scalar loads through the global address space (global_load_*, not flat_load_*: flat loads also
+// count against lgkmcnt, so every LDS / scalar wait would wait for them too).
+__device__ __forceinline__ uint32_t ldg32(const void* p) {
+  return *(const __attribute__((address_space(1))) uint32_t*)p;
+}
+__device__ __forceinline__ int32_t ldg_i32(const int32_t* p) {
+  return *(const __attribute__((address_space(1))) int32_t*)p;
+}
+__device__ __forceinline__ uint64_t ldg64_unaligned(const void* p) {
+  typedef uint64_t __attribute__((aligned(1))) u64u;
+  return *(const __attribute__((address_space(1))) u64u*)p;
+}
 
 
 // ------------------------------------------------------------------------------------------------
@@ -63,7 +75,7 @@ DQ_DEV void wave_reduce(int kind, Acc& a) {
 struct ChunkBits {
   uint32_t w;
   DQ_DEV void load(const uint8_t* bm, int64_t r0) {
-    w = reinterpret_cast<const uint32_t*>(bm)[(r0 >> 5) + (lane_id() & 31)];
+    w = ldg32(reinterpret_cast<const uint32_t*>(bm) + (r0 >> 5) + (lane_id() & 31));
   }
   DQ_DEV uint32_t get(int o, int n) const {
     return (lane_read(w, o >> 5) >> (o & 31)) & ((1u << n) - 1u);
@@ -405,7 +417,7 @@ struct StrStep {
         const uint4 u = ld16(off + r0 + 256 * g + 4 * l);
         q[g] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
       }
-      last[g] = off[r0 + 256 * g + 256];
+      last[g] = ldg_i32(off + r0 + 256 * g + 256);
     }
     if (t.valid) c.load(t.valid, r0);
   }
@@ -460,7 +472,7 @@ DQ_DEV void str_in_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& 
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) __builtin_memcpy(&v[4 * g + j], t.data + o[g][j], 8);
+          for (int j = 0; j < 4; ++j) v[4 * g + j] = ldg64_unaligned(t.data + o[g][j]);
         __builtin_amdgcn_sched_barrier(0);
         if (more) cur.load(t, off, r0 + kWaveRows, l);
         __builtin_amdgcn_sched_barrier(0);
@@ -567,7 +579,7 @@ DQ_DEV void corr_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
 // atomicMax only when the rank can raise the register.  Flushed once per workgroup at the end.
 // ------------------------------------------------------------------------------------------------
 DQ_DEV uint32_t bits32(const uint8_t* bm, int64_t word) {
-  return bm ? reinterpret_cast<const uint32_t*>(bm)[word] : ~0u;
+  return bm ? ldg32(reinterpret_cast<const uint32_t*>(bm) + word) : ~0u;
 }
 
 DQ_DEV void hll_update(uint32_t* regs, uint64_t h) {
