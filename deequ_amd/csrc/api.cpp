@@ -1022,6 +1022,7 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
         t.type2 = c.type;
         t.valid2 = c.validity;
         t.values2 = c.values;
+        vec = vec && aligned(c.validity, 16) && aligned(c.values, 16);
         bpr += type_size(c.type) + 0.125;
       }
       switch (tp.kind) {

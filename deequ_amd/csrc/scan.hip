@@ -52,6 +52,10 @@ __device__ __forceinline__ uint64_t ldg64_unaligned(const void* p) {
   typedef uint64_t __attribute__((aligned(1))) u64u;
   return *(const __attribute__((address_space(1))) u64u*)p;
 }
+// 32 rows of a validity / where bitmap (all ones when the bitmap is absent)
+__device__ __forceinline__ uint32_t bits32(const uint8_t* bm, int64_t word) {
+  return bm ? ldg32(reinterpret_cast<const uint32_t*>(bm) + word) : ~0u;
+}
 
 
 // ------------------------------------------------------------------------------------------------
@@ -516,11 +520,85 @@ DQ_DEV void str_in_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& 
 // TK_COMOMENTS (Correlation): rows where x and y are both non-NULL (and where is TRUE).
 // Lane l owns rows r0 + 128k + 2l + {0, 1} (k < 4) of a 512-row step.
 // ------------------------------------------------------------------------------------------------
+// Vector path for two 8-byte columns (Long / Double), 1024 rows per wave: sixteen 16-byte loads
+// per lane in flight (each wave-instruction one contiguous 1 KiB); lane l owns rows
+// r0 + 128k + 2l + {0, 1} (k < 8).  The lane's 16 selected rows form one block: two-pass
+// (mean, co-moments), then one Chan merge -- 2 divisions per 16 rows instead of per 8.
+DQ_DEV double as_f64(uint64_t bits, bool is_long) {
+  return is_long ? (double)(int64_t)bits : __builtin_bit_cast(double, bits);
+}
+
+DQ_DEV void corr_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int64_t& n, double* c) {
+  const int l = lane_id();
+  const uint64_t* X = reinterpret_cast<const uint64_t*>(t.values) + r0 + 2 * l;
+  const uint64_t* Y = reinterpret_cast<const uint64_t*>(t.values2) + r0 + 2 * l;
+  uint4 qx[8], qy[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    qx[k] = ld16(X + 128 * k);
+    qy[k] = ld16(Y + 128 * k);
+  }
+  const int64_t w0 = (r0 >> 5) + (l >> 4);
+  const uint32_t sh = (uint32_t)(2 * l) & 31u;
+  uint32_t sel = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t w = w0 + 4 * k;
+    uint32_t s = bits32(t.valid, w) & bits32(t.valid2, w);
+    if (t.w_val) s &= bits32(t.w_val, w) & bits32(t.w_vld, w);
+    sel |= ((s >> sh) & 3u) << (2 * k);
+  }
+  const int nb = __popc(sel);
+  if (!nb) return;
+  double xs[16], ys[16];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    xs[2 * k] = as_f64((uint64_t)qx[k].x | ((uint64_t)qx[k].y << 32), xl);
+    xs[2 * k + 1] = as_f64((uint64_t)qx[k].z | ((uint64_t)qx[k].w << 32), xl);
+    ys[2 * k] = as_f64((uint64_t)qy[k].x | ((uint64_t)qy[k].y << 32), yl);
+    ys[2 * k + 1] = as_f64((uint64_t)qy[k].z | ((uint64_t)qy[k].w << 32), yl);
+  }
+  double sx = 0, sy = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if ((sel >> i) & 1u) {
+      sx += xs[i];
+      sy += ys[i];
+    }
+  }
+  double b[5];
+  b[0] = sx / nb;
+  b[1] = sy / nb;
+  b[2] = b[3] = b[4] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if ((sel >> i) & 1u) {
+      const double dx = xs[i] - b[0], dy = ys[i] - b[1];
+      b[2] += dx * dy;
+      b[3] += dx * dx;
+      b[4] += dy * dy;
+    }
+  }
+  if (n == 0) {
+    for (int f = 0; f < 5; ++f) c[f] = b[f];
+  } else {
+    comoments_merge((double)n, c, (double)nb, b);
+  }
+  n += nb;
+}
+
 DQ_DEV void corr_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& acc) {
   const int l = lane_id();
   int64_t n = 0;
   double c[5] = {0, 0, 0, 0, 0};  // xAvg, yAvg, ck, xMk, yMk
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += 512) {
+  int64_t r_fast = r_begin;
+  const bool x8 = t.type == DQ_INT64 || t.type == DQ_FLOAT64;
+  const bool y8 = t.type2 == DQ_INT64 || t.type2 == DQ_FLOAT64;
+  if (t.vec_ok && x8 && y8) {
+    const bool xl = t.type == DQ_INT64, yl = t.type2 == DQ_INT64;
+    for (; r_fast + 1024 <= r_end; r_fast += 1024) corr_chunk8(t, r_fast, xl, yl, n, c);
+  }
+  for (int64_t r0 = r_fast; r0 < r_end; r0 += 512) {
     double xs[8], ys[8];
     uint32_t sel = 0;
 #pragma unroll
@@ -578,10 +656,6 @@ DQ_DEV void corr_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
 // TK_HLL: the workgroup's 512 registers of each HLL task live in LDS (one u32 per register);
 // atomicMax only when the rank can raise the register.  Flushed once per workgroup at the end.
 // ------------------------------------------------------------------------------------------------
-DQ_DEV uint32_t bits32(const uint8_t* bm, int64_t word) {
-  return bm ? ldg32(reinterpret_cast<const uint32_t*>(bm) + word) : ~0u;
-}
-
 DQ_DEV void hll_update(uint32_t* regs, uint64_t h) {
   uint32_t idx, pw;
   hll_index_rank(h, idx, pw);

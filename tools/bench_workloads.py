@@ -91,7 +91,7 @@ def main():
         for b in table.batches:
             m = b["id"].length
             b_alg += 2 * nb(m) + 16 * m
-        kernel = "dq::scan_kernel<HLL> + dq::scan_mixed_kernel (co-moments) + finalize"
+        kernel = "dq::scan_kernel<BC_CORR> (co-moments) + dq::scan_kernel<BC_HLL> + finalize"
         desc = ("ApproxCountDistinct(id) + Correlation(id, score) over a synthetic Item table "
                 "with fp64 score, 5% nulls (BASELINE.json configs[3], per-GPU shard of 1e10 "
                 "rows over 8 GPUs = 1.25e9 rows, 1 GPU)")
