@@ -1065,13 +1065,14 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
           }
           break;
         }
-        case TK_HLL: bpr *= 4.0; break;  // hashing: weight items by work, not bytes
-        case TK_COMOMENTS: bpr *= 2.0; break;
+        // (items of HLL / co-moment tasks were once sized by work -- 4x / 2x the bytes -- but
+        // then the single dequeue word, ~88 dequeues/us, became the bound: items are sized by
+        // bytes only)
         default: break;
       }
       if (tp.where >= 0) bpr += 0.25;
       t.vec_ok = vec ? 1 : 0;
-      int64_t item_rows = pow2_at_least((int64_t)(131072.0 / std::max(bpr, 1e-3)));
+      int64_t item_rows = pow2_at_least((int64_t)(kItemBytes / std::max(bpr, 1e-3)));
       item_rows = std::max<int64_t>(kItemAlign, std::min<int64_t>(item_rows, (int64_t)1 << 22));
       t.item_rows = item_rows;
       t.n_items = rows[b] > 0 ? (rows[b] + item_rows - 1) / item_rows : 0;

@@ -34,6 +34,12 @@ constexpr int kHllRegsPerWord = 10;   // REGISTERS_PER_WORD
 constexpr int kHllRegBits = 6;        // REGISTER_SIZE
 constexpr int kBlock = 256;           // threads per scan workgroup (4 waves)
 constexpr int kWaveRows = 1024;       // rows per wave iteration of a streaming body (16 per lane)
+// Work-item size target in buffer bytes: big enough that the one dequeue word (~88 dequeues/us)
+// is never the bound, small enough that the persistent grid's tail stays short.
+#ifndef DQ_ITEM_BYTES
+#define DQ_ITEM_BYTES 262144
+#endif
+constexpr double kItemBytes = DQ_ITEM_BYTES;
 constexpr int kItemAlign = 1024;      // work items are whole wave iterations (rows % 1024 == 0)
 constexpr int kFinParts = 32;         // first-stage finalize workgroups per logical task
 constexpr int kListLenSlots = 65;     // STR_IN lists bucketed by length 0..64, then "longer"
