@@ -118,9 +118,10 @@ struct ScanLaunch {
 };
 
 // Most HLL tasks whose LDS registers (2 KiB each) ride in the mixed launch.  0 = HLL always keeps
-// its own launch: measured on MI355X (profiles/r1e, configs[3] at 1.25e9 rows), HLL inside the
-// mixed grid took 11.19 ms vs 6.67 + 3.78 ms as two launches -- the XXH64 body is bound by
-// quarter-rate 64-bit multiplies and needs the occupancy the mixed kernel's 3 waves/SIMD denies.
+// its own launch: measured on MI355X at configs[3] (1.25e9 rows), HLL inside the mixed grid took
+// 6.18 ms per step vs 5.74 ms as its own launch (and 11.19 vs 10.45 ms with the earlier 128 KiB
+// work-sized items) -- the XXH64 body is bound by quarter-rate 64-bit multiplies and needs the
+// occupancy the mixed kernel's 3 waves/SIMD denies.
 constexpr int kMixedHllMax = 0;
 
 // Fused scan over n_desc (task, batch) descriptors numbered class-major then task-major (each
