@@ -4,10 +4,10 @@
 // partials in a fixed order and fold them into the running state (Spark's final-mode merge).
 //
 // Work decomposition.  The host cuts every (task, batch) descriptor into work items of
-// `item_rows` rows (~128 KiB of the task's buffers, a multiple of 1024 rows) and numbers the items
+// `item_rows` rows (~256 KiB of the task's buffers, a multiple of 1024 rows) and numbers the items
 // task-major, so each logical task owns one contiguous range of global item indices.  The grid is
 // persistent (a few workgroups per CU); every WAVE pulls items from one global counter (one
-// returning atomic per ~128 KiB), streams the item's rows and writes the item's partial
+// returning atomic per ~256 KiB), streams the item's rows and writes the item's partial
 // aggregation buffer (Acc) to partial[item].  Because a partial depends only on its item, never
 // on which wave ran it, the result is bit-identical from run to run although the schedule is
 // dynamic, and HBM-bound bodies of different cost (bitmap popcounts, Welford moments, string
