@@ -850,7 +850,7 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
 extern "C" dq_status dq_freq_summarize(dq_freq* f, dq_freq_summary* out) {
   if (!f || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   HIP_TRY(hipSetDevice(f->device));
-  const unsigned G = grid_for(f->cap, 1024);
+  const unsigned G = grid_for(f->cap, 8192);  // >= 32 blocks per CU: enough loads in flight
   DevBuf<int64_t> pi;
   DevBuf<double> pd;
   HIP_TRY(pi.ensure(2 * G));
