@@ -13,7 +13,8 @@ from dataclasses import dataclass, fields
 from typing import Callable, List, Optional, Sequence
 
 from .. import _native as N
-from ..exceptions import (EmptyStateException, NoColumnsSpecifiedException,
+from ..exceptions import (EmptyStateException, MetricCalculationException,
+                          NoColumnsSpecifiedException,
                           NoSuchColumnException, NumberOfSpecifiedColumnsException,
                           WrongColumnTypeException, wrap_if_necessary)
 from ..metrics import DoubleMetric, Entity, Failure, Success
@@ -267,8 +268,11 @@ class StandardScanShareableAnalyzer(ScanShareableAnalyzer):
 
     def compute_metric_from(self, state) -> DoubleMetric:
         if state is not None:
-            return metric_from_value(state.metric_value(), self._name, self._instance(),
-                                     self._entity)
+            try:
+                value = state.metric_value()
+            except MetricCalculationException as e:
+                return self.to_failure_metric(e)
+            return metric_from_value(value, self._name, self._instance(), self._entity)
         return metric_from_empty(self, self._name, self._instance(), self._entity)
 
     def to_failure_metric(self, exception) -> DoubleMetric:

@@ -11,6 +11,7 @@ from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
 from .. import _native as N
+from ..exceptions import HllBiasTablesUnavailableException
 from ..metrics import Entity
 from .base import (AggSpec, DoubleValuedState, NumMatchesAndCount, Preconditions,
                    StandardScanShareableAnalyzer, conditional_count, count_all, if_no_nulls_in)
@@ -411,8 +412,19 @@ class ApproxCountDistinctState(DoubleValuedState):
         return ApproxCountDistinctState(hll_merge_words(self.words, other.words))
 
     def metric_value(self) -> float:
-        est, _ = N.hll_count(self.words)
+        """HyperLogLogPlusPlusUtils.count (StatefulHyperloglogPlus.scala:208-255).  Where the
+        reference would subtract its empirical bias (E < 5M, no linear counting) the tables are
+        missing here, so the metric is a Failure rather than a silently different number."""
+        est, needs_bias = N.hll_count(self.words)
+        if needs_bias:
+            raise HllBiasTablesUnavailableException(
+                f"ApproxCountDistinct raw estimate {est:.0f} lies in the HLL++ bias-correction range "
+                f"(< {5 * _M}); Spark's BIAS_DATA tables are not available to this engine")
         return est
+
+    def raw_estimate(self) -> float:
+        """The estimate without the bias correction (equal to deequ's outside that range)."""
+        return N.hll_count(self.words)[0]
 
 
 @dataclass(frozen=True)

@@ -1316,7 +1316,10 @@ extern "C" double dq_hll_count(const uint64_t* words, int* bias_corrected) {
     uint64_t word = words[w];
     for (int i = 0; i < kHllRegsPerWord && idx < kHllM; ++i, ++idx) {
       uint64_t m = (word >> (kHllRegBits * i)) & 0x3f;
-      z_inv += 1.0 / (double)(1ULL << m);
+      // `1.0 / (1 << Midx)` (:220): `1` is a Scala Int and Midx a Long, so the JVM shifts a 32-bit
+      // int by Midx & 31 (JLS 15.19): register 31 adds 1/Int.MinValue = -2^-31 and a register
+      // m >= 32 adds 2^-(m-32).  Restated literally -- the estimate must equal deequ's.
+      z_inv += 1.0 / (double)(int32_t)(1u << (m & 31));
       if (m == 0) V += 1.0;
     }
   }
@@ -1336,7 +1339,14 @@ extern "C" double dq_hll_count(const uint64_t* words, int* bias_corrected) {
     estimate = e;
   }
   if (bias_corrected) *bias_corrected = biased ? 1 : 0;
-  return (double)(int64_t)std::floor(estimate + 0.5);  // Math.round
+  // JDK 8 Math.round(double): (long) floor(a + 0.5) except for the largest double below 0.5; the
+  // (long) cast saturates and maps NaN to 0 (JLS 5.1.3).  A register >= 31 can make zInverse
+  // tiny or negative, so the saturating cases are reachable.
+  if (estimate != estimate || estimate == 0x1.fffffffffffffp-2) return 0.0;
+  const double f = std::floor(estimate + 0.5);
+  if (f >= 9223372036854775808.0) return (double)INT64_MAX;
+  if (f <= -9223372036854775808.0) return (double)INT64_MIN;
+  return (double)(int64_t)f;
 }
 
 extern "C" uint64_t dq_xxhash64(const void* data, int64_t nbytes, uint64_t seed) {

@@ -43,6 +43,13 @@ class EmptyStateException(MetricCalculationRuntimeException):
         super().__init__(message)
 
 
+class HllBiasTablesUnavailableException(MetricCalculationRuntimeException):
+    """ApproxCountDistinct's estimate fell in HLL++'s empirical-bias range (raw estimate E < 5M and
+    no linear counting): the reference subtracts estimateBias(E) from Spark's RAW_ESTIMATE_DATA /
+    BIAS_DATA tables (StatefulHyperloglogPlus.scala:235-237, 257-295), which are not available to
+    this engine.  Raised instead of returning a value that would differ from deequ's."""
+
+
 class AnalysisException(Exception):
     """Stand-in for Spark's AnalysisException (unresolvable column / unparseable expression)."""
 

@@ -504,6 +504,14 @@ def hll_words(regs: Sequence[int]) -> List[int]:
     return words
 
 
+def _jvm_int_one_shl(m: int) -> int:
+    """Scala `1 << Midx` with `1: Int` and `Midx: Long` (StatefulHyperloglogPlus.scala:220): the
+    JVM shifts the 32-bit int by Midx & 31 (JLS 15.19) and the result wraps to a signed int, so
+    1 << 31 == Int.MinValue and 1 << 32 == 1."""
+    v = (1 << (m & 31)) & 0xFFFFFFFF
+    return v - (1 << 32) if v >= (1 << 31) else v
+
+
 def hll_count(words: Sequence[int]) -> Tuple[float, bool]:
     """HyperLogLogPlusPlusUtils.count; returns (estimate, needed_bias_tables)."""
     z_inv, V = 0.0, 0.0
@@ -514,7 +522,7 @@ def hll_count(words: Sequence[int]) -> Tuple[float, bool]:
             if idx >= M:
                 break
             m = (word >> (6 * i)) & 0x3F
-            z_inv += 1.0 / (1 << m)
+            z_inv += 1.0 / _jvm_int_one_shl(m)
             if m == 0:
                 V += 1.0
             idx += 1
@@ -524,8 +532,23 @@ def hll_count(words: Sequence[int]) -> Tuple[float, bool]:
     if V > 0:
         H = M * math.log(M / V)
         if H <= 400.0:
-            return float(math.floor(H + 0.5)), False
-    return float(math.floor(e + 0.5)), biased
+            return java_math_round(H), False
+    return java_math_round(e), biased
+
+
+def java_math_round(a: float) -> float:
+    """JDK 8 Math.round(double) as a double: (long) floor(a + 0.5), except 0.49999999999999994
+    rounds to 0; the (long) cast saturates and maps NaN to 0 (JLS 5.1.3)."""
+    if a != a:
+        return 0.0
+    if a == 0.49999999999999994:
+        return 0.0
+    f = a + 0.5
+    if f >= 2.0 ** 63:
+        return float(2 ** 63 - 1)
+    if f <= -(2.0 ** 63):
+        return float(-(2 ** 63))
+    return float(math.floor(f))
 
 
 def agg_hll(t: OTable, column: str, where: Optional[str]) -> List[int]:

@@ -76,10 +76,72 @@ def histogram_expected(ot, col):
     return {"num_rows": n, "bins": len(h), "counts": {k: v for k, v in sorted(h.items())}}
 
 
+# int64 values whose XXH64 (seed 42) has HLL++ rank 31..39 (found by
+# tools/find_high_rank_longs.c; cross-checked against the xxhash package in test_golden_vectors).
+HIGH_RANK_LONGS = [(555506679, 31, 13), (1608524621, 32, 27), (283986680, 33, 480),
+                   (3880637358, 34, 342), (7613979340, 35, 178), (19364577309, 36, 321),
+                   (56728968515, 37, 240), (379893492375, 38, 473), (483058871146, 39, 15)]
+
+
+def hll_high_register_sets():
+    """Register files with registers 29..56: the range where count()'s `1 << Midx` (a Scala Int
+    shifted by a Long, StatefulHyperloglogPlus.scala:220) departs from 2^Midx.  Backgrounds look
+    like a 1e9..1e10-distinct sketch (registers ~ 18..26) plus small / empty ones."""
+    import random
+    from oracle import deequ_oracle as O
+    rng = random.Random(2031)
+    sets = []
+
+    def bg(center):
+        return [max(1, min(30, center + int(rng.expovariate(1.0)) - int(rng.expovariate(1.0))))
+                for _ in range(O.M)]
+    for hi in range(29, 57):                      # one high register on a realistic background
+        regs = bg(21)
+        regs[rng.randrange(O.M)] = hi
+        sets.append(regs)
+    for k in (2, 9, 40):                          # several registers >= 31
+        regs = bg(23)
+        for _ in range(k):
+            regs[rng.randrange(O.M)] = rng.randrange(31, 57)
+        sets.append(regs)
+    regs = [0] * O.M                              # linear-counting path with a 31 and a 40
+    regs[3], regs[77] = 31, 40
+    sets.append(regs)
+    sets.append([31] * O.M)                       # zInverse < 0: negative estimate
+    sets.append([32] * O.M)                       # 1 << 32 == 1 on an Int: estimate of M*M*alpha
+    sets.append([31] * 256 + [1] * 256)           # zInverse == 128 - 2^-23
+    return sets
+
+
+def hll_high_register_vectors():
+    from oracle import deequ_oracle as O
+    out = []
+    for regs in hll_high_register_sets():
+        words = O.hll_words(regs)
+        est, corrected = O.hll_count(words)
+        out.append({"words": [int(w) for w in words], "estimate": est, "bias_corrected": corrected,
+                    "max_register": max(regs)})
+    return out
+
+
+def high_rank_column_expected():
+    """A 4099-row long column: 4090 values 0..4089 plus the 9 HIGH_RANK_LONGS."""
+    from oracle import deequ_oracle as O
+    values = list(range(4090)) + [v for v, _, _ in HIGH_RANK_LONGS]
+    regs = O.hll_registers(values, "long")
+    words = O.hll_words(regs)
+    est, corrected = O.hll_count(words)
+    return {"values_note": "range(4090) + HIGH_RANK_LONGS values", "words": [int(w) for w in words],
+            "estimate": est, "bias_corrected": corrected,
+            "high_rank_longs": [list(x) for x in HIGH_RANK_LONGS]}
+
+
 def main():
     from oracle import deequ_oracle as O
     out = {"generator": "tests/golden/make_golden.py (oracle/deequ_oracle.py)",
            "xxh64_seed42": {}, "cases": {}}
+    out["hll_high_registers"] = hll_high_register_vectors()
+    out["hll_high_rank_column"] = high_rank_column_expected()
     for ty, vals in XXH_INPUTS.items():
         out["xxh64_seed42"][ty] = [[v, O.spark_xxhash64(v, ty)] for v in vals]
     for name, n, seed, null_rate, batch in CASES:

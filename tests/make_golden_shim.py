@@ -10,3 +10,5 @@ oracle_table = _m.oracle_table
 scan_expected = _m.scan_expected
 freq_expected = _m.freq_expected
 histogram_expected = _m.histogram_expected
+hll_high_register_sets = _m.hll_high_register_sets
+high_rank_column_expected = _m.high_rank_column_expected

@@ -99,3 +99,21 @@ def test_hll_count_matches_oracle_on_random_registers():
         regs = [rng.choice([0] * trial + list(range(1, 12))) for _ in range(512)]
         words = O.hll_words(regs)
         assert N.hll_count(words) == O.hll_count(words)
+
+
+def test_approx_count_distinct_in_bias_range_is_a_failure_not_a_wrong_number():
+    """~1000 distinct values: E < 5M and no linear counting, where the reference subtracts Spark's
+    empirical bias (StatefulHyperloglogPlus.scala:235-237); those tables are absent, so the metric
+    must fail loudly (HllBiasTablesUnavailableException) instead of returning the raw estimate."""
+    from deequ_amd.analyzers import ApproxCountDistinct
+    from deequ_amd.analyzers.scan import ApproxCountDistinctState
+    from deequ_amd.exceptions import HllBiasTablesUnavailableException
+    from oracle import deequ_oracle as O
+    words = tuple(O.hll_words(O.hll_registers(list(range(1000)), "long")))
+    assert O.hll_count(words)[1]
+    m = ApproxCountDistinct("c").compute_metric_from(ApproxCountDistinctState(words))
+    assert m.value.is_failure
+    assert isinstance(m.value.exception, HllBiasTablesUnavailableException)
+    small = tuple(O.hll_words(O.hll_registers(list(range(50)), "long")))
+    assert ApproxCountDistinct("c").compute_metric_from(ApproxCountDistinctState(small)).value.get() \
+        == O.hll_count(small)[0]
