@@ -92,6 +92,21 @@ class FrequencyTable:
             out.append((self._decode(data, int(offs[g])), int(counts[g])))
         return out
 
+    def topk(self, k: int) -> List[Tuple[tuple, int]]:
+        """The k largest groups by count, descending (dq_freq_topk: only these keys leave the
+        device; rdd.top(maxDetailBins) in Histogram.scala:78, ties in any order)."""
+        n, need = ctypes.c_int64(), ctypes.c_int64()
+        N.check(N.lib.dq_freq_topk(self.handle, k, None, None, None, 0, ctypes.byref(n),
+                                   ctypes.byref(need)))
+        counts = np.zeros(max(1, n.value), np.int64)
+        offs = np.zeros(n.value + 1, np.int64)
+        raw = np.zeros(max(1, need.value), np.uint8)
+        N.check(N.lib.dq_freq_topk(self.handle, k, counts.ctypes.data, offs.ctypes.data,
+                                   raw.ctypes.data, need.value, ctypes.byref(n),
+                                   ctypes.byref(need)))
+        data = raw.tobytes()
+        return [(self._decode(data, int(offs[g])), int(counts[g])) for g in range(n.value)]
+
     def _decode(self, data: bytes, pos: int) -> tuple:
         key = []
         for t in self.key_types:
@@ -389,20 +404,35 @@ def cast_to_string(value, dtype: int) -> str:
     return str(int(value))
 
 
+def _python_dtype(value, column_dtype: int) -> int:
+    """Type of a binning UDF's result, for its cast to string."""
+    if value is None or isinstance(value, str):
+        return N.UTF8
+    if isinstance(value, bool):
+        return N.BOOL
+    if isinstance(value, float):
+        return N.FLOAT64
+    if isinstance(value, int):
+        return N.INT64
+    return column_dtype
+
+
 @dataclass
 class HistogramState(FrequenciesAndNumRows):
     dtype: int = N.UTF8
     binning_udf: Optional[Callable] = None
 
     def string_groups(self) -> dict:
-        """Groups keyed by Spark's cast-to-string of the value (NULL -> "NullValue"), with the
-        binning function applied to the distinct values."""
+        """Every group keyed by Spark's cast-to-string of the (binned) value, NULL -> "NullValue"
+        (Histogram.scala:59-66).  The binning function is host code (a Spark UDF in the
+        reference), so it runs on the distinct values after the device group-by."""
         out: dict = {}
         for (key,), cnt in self.frequencies.export():
-            s = cast_to_string(key, self.dtype)
             if self.binning_udf is not None:
-                s = self.binning_udf(None if key is None else s)
-                s = NULL_FIELD_REPLACEMENT if s is None else s
+                key = self.binning_udf(key)
+                s = cast_to_string(key, _python_dtype(key, self.dtype))
+            else:
+                s = cast_to_string(key, self.dtype)
             out[s] = out.get(s, 0) + cnt
         return out
 
@@ -446,11 +476,18 @@ class Histogram(Analyzer):
         if state is None:
             return HistogramMetric(self.column, Failure(empty_state_exception(self)))
         try:
-            groups = state.string_groups()
-            # rdd.top(maxDetailBins)(OrderByAbsoluteCount): ties are arbitrary in the reference
-            top = sorted(groups.items(), key=lambda kv: (-kv[1], kv[0]))[: self.max_detail_bins]
+            if state.binning_udf is None:
+                # device top-N: only max_detail_bins groups reach the host (Histogram.scala:78-79)
+                top = [(cast_to_string(key, state.dtype), c)
+                       for (key,), c in state.frequencies.topk(self.max_detail_bins)]
+                bins = state.frequencies.count()
+            else:
+                groups = state.string_groups()
+                # rdd.top(maxDetailBins)(OrderByAbsoluteCount): ties are arbitrary in the reference
+                top = sorted(groups.items(), key=lambda kv: (-kv[1], kv[0]))[: self.max_detail_bins]
+                bins = len(groups)
             details = {k: DistributionValue(c, c / state.num_rows) for k, c in top}
-            return HistogramMetric(self.column, Success(Distribution(details, len(groups))))
+            return HistogramMetric(self.column, Success(Distribution(details, bins)))
         except Exception as e:  # noqa: BLE001
             return HistogramMetric(self.column, Failure(wrap_if_necessary(e)))
 

@@ -1,16 +1,35 @@
-// freq.hip -- hash group-by for the frequency analyzers (FrequencyBasedAnalyzer.computeFrequencies,
-// GroupingAnalyzers.scala:53-80, and Histogram.scala:54-69) plus the one aggregation over the
-// frequency table that every ScanShareableFrequencyBasedAnalyzer shares (AnalysisRunner.scala:
-// 490-500): Σ[count == 1], count(*), Σ −(c/n)·ln(c/n).
+// freq.hip -- the hash group-by of the frequency analyzers (FrequencyBasedAnalyzer.
+// computeFrequencies, GroupingAnalyzers.scala:53-80; Histogram.scala:54-69) and the one
+// aggregation over the frequency table that every ScanShareableFrequencyBasedAnalyzer shares
+// (AnalysisRunner.scala:490-500): Σ[count == 1], count(*), Σ −(c/n)·ln(c/n); plus Histogram's
+// top-N (Histogram.scala:78-79).
 //
-// Table: open addressing (linear probing) in HBM, structure of arrays keys[] / counts[] (/ reps[]).
-//   * exact mode  -- one fixed-width key column: the key is the value itself widened to 64 bits;
-//   * hashed mode -- string keys, several key columns, or NULL-as-a-group (Histogram): the key is a
-//     64-bit hash of the composite key; the first row of every group writes its encoded key into a
-//     device arena (reps[] = arena offset) and a verification pass compares every row against its
-//     group's encoded key, so a hash collision is detected instead of silently merging groups.
-// Each workgroup first aggregates into a 2048-entry LDS table, so low-cardinality keys (priority:
-// 3 groups) cost LDS atomics, not HBM atomics; keys that do not fit go straight to the HBM table.
+// A radix-partitioned group-by, so that every pass streams HBM and every count happens in LDS
+// (random HBM atomics into a billion-slot table ran at 1.4 % of HBM peak in round 1):
+//
+//   phase A (per added batch; freq_phaseA): one 1024-thread workgroup per chunk of 8192 rows
+//     (4096 in hashed mode).  Each row's key is hashed (freq_codec.h); the first 1024 rows of the
+//     chunk go through a 2048-slot LDS table that collapses repeated keys (bypassed for the rest
+//     of the chunk when fewer than 1/16 of them repeated, i.e. high-cardinality keys), and every
+//     resulting record is counting-sorted in LDS by the top 9 bits of its hash (512 buckets) and
+//     written out as ONE contiguous chunk region plus a 513-entry u16 bucket histogram.
+//   phase B (finalize; freq_phaseB): the chunk histograms are transposed and scanned per bucket;
+//     a bucket's records are cut into units of ~kTile/2 records (whole chunk segments), and each
+//     unit is counting-sorted by the next s hash bits (s chosen so that a final partition holds a
+//     few thousand groups) into a contiguous output plus its sub-bucket histogram.
+//   phase C (finalize; freq_phaseC): one workgroup per partition (bucket, sub-bucket) gathers its
+//     pieces of every unit of the bucket and counts them in an LDS hash table (8192 slots exact,
+//     4608 hashed), then emits the partition's Σ[c==1], #groups and entropy partial, optionally
+//     its top-4 groups (Histogram) or every group (export, merge, repartition).  A partition whose
+//     groups do not fit is recounted in 2, 4, ... passes over disjoint hash subsets.
+//
+// Exact mode (one fixed-width key) carries 8-byte records (h << 8 | count digit) whose hash is a
+// bijection of the value; hashed mode (strings, several keys, Histogram on strings) carries
+// 16-byte records {h, rep << 8 | count digit} where rep points at the group's encoded key in a
+// device arena, and groups that meet on one hash are compared byte for byte (freq_codec.h), so a
+// 64-bit collision never merges groups.  Counts of equal keys are SUMMED in every pass, which is
+// also what FrequenciesAndNumRows.sum (GroupingAnalyzers.scala:128-148) needs: merging two tables
+// appends one's chunks to the other's.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,487 +39,936 @@
 #include <vector>
 
 #include "engine.h"
+#include "freq_codec.h"
 #include "kernels.h"
 
 namespace dq {
 
 #define DQ_DEV __device__ __forceinline__
 
-constexpr uint64_t kEmpty = 0x8000000000000000ULL;
-constexpr int kLdsSlots = 2048;
-constexpr int kLdsProbes = 8;
-constexpr int kMaxKeys = 8;
+constexpr int kBucketBits = 9;
+constexpr int kBuckets = 1 << kBucketBits;
+constexpr int kHistRow = kBuckets + 1;  // u16 exclusive bucket prefix of a chunk + its total
+constexpr int kThreads = 1024;
+constexpr int kMaxSubBits = 9;
+constexpr int kFilterShift = 32;        // hash bits that split an overflowing partition
+constexpr int kCand = 4;                // top groups kept per partition for Histogram
+constexpr int kMaxParts = 64;
+constexpr uint64_t kEmptyKey = ~0ULL;
+constexpr uint64_t kNotReady = ~0ULL;
 
-enum Counter { C_OCCUPIED = 0, C_NULL_ROWS, C_NULL_GROUP, C_SENTINEL, C_COLLISIONS, C_ARENA_OVF, C_N };
+enum Counter { C_NULL_ROWS = 0, C_NULL_GROUP, C_COLLISIONS, C_N };
 
-struct KeyCol {
-  int32_t type;
-  int32_t pad;
-  const uint8_t* valid;
-  const void* values;
-  const uint8_t* data;
+template <bool HASHED>
+struct FM;
+template <>
+struct FM<false> {
+  static constexpr int kTile = 8192;    // rows (and at most records) per phase-A chunk
+  static constexpr int kRB = 8;         // bytes per record
+  static constexpr int kDedupe = 2048;  // phase-A LDS table slots
+  static constexpr int kTableC = 8192;  // phase-C LDS table slots
+  static constexpr int kTarget = 4000;  // groups per final partition the sizing aims at
 };
-
-struct FreqDev {
-  uint64_t* keys;
-  uint64_t* counts;
-  uint64_t* reps;
-  uint64_t mask;
-  uint8_t* arena;
-  uint64_t* arena_cursor;
-  uint64_t arena_cap;
-  unsigned long long* counters;
-  int32_t n_keys;
-  int32_t exact;
-  int32_t null_as_group;
-  int32_t pad;
-  KeyCol cols[kMaxKeys];
+template <>
+struct FM<true> {
+  static constexpr int kTile = 4096;
+  static constexpr int kRB = 16;
+  static constexpr int kDedupe = 1024;
+  static constexpr int kTableC = 4608;
+  static constexpr int kTarget = 2500;
 };
-
-DQ_DEV uint32_t fbit(const uint8_t* bm, int64_t r) { return bm ? ((bm[r >> 3] >> (r & 7)) & 1u) : 1u; }
-
-DQ_HD uint64_t mix64(uint64_t z) {
-  z ^= z >> 33;
-  z *= 0xff51afd7ed558ccdULL;
-  z ^= z >> 33;
-  z *= 0xc4ceb9fe1a85ec53ULL;
-  z ^= z >> 33;
-  return z;
+template <bool HASHED>
+constexpr int unit_half() {
+  return FM<HASHED>::kTile / 2;
+}
+template <bool HASHED>
+constexpr int unit_max() {  // a unit: whole chunk segments starting inside one half-tile window
+  return unit_half<HASHED>() + FM<HASHED>::kTile;
 }
 
-DQ_DEV uint64_t widen(int type, const void* v, int64_t r) {
-  switch (type) {
-    case DQ_INT8: return (uint64_t)(int64_t) reinterpret_cast<const int8_t*>(v)[r];
-    case DQ_INT16: return (uint64_t)(int64_t) reinterpret_cast<const int16_t*>(v)[r];
-    case DQ_INT32: return (uint64_t)(int64_t) reinterpret_cast<const int32_t*>(v)[r];
-    case DQ_INT64: return (uint64_t) reinterpret_cast<const int64_t*>(v)[r];
-    case DQ_FLOAT32: return (uint64_t)__builtin_bit_cast(uint32_t, reinterpret_cast<const float*>(v)[r]);
-    case DQ_FLOAT64: return __builtin_bit_cast(uint64_t, reinterpret_cast<const double*>(v)[r]);
-    case DQ_BOOL: return fbit(reinterpret_cast<const uint8_t*>(v), r);
-    default: return 0;
-  }
-}
-
-struct FBytes {  // aligned-dword reader (see DevBytes in scan.hip)
-  const uint8_t* p;
-  DQ_DEV uint32_t u32(int64_t o) const {
-    uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-    uint32_t sh = (uint32_t)(a & 3) * 8;
-    uint32_t w0 = w[0];
-    if (sh == 0) return w0;
-    return (w0 >> sh) | (w[1] << (32 - sh));
-  }
-  DQ_DEV uint64_t u64(int64_t o) const { return (uint64_t)u32(o) | ((uint64_t)u32(o + 4) << 32); }
-  DQ_DEV uint32_t u8(int64_t o) const {
-    uintptr_t a = reinterpret_cast<uintptr_t>(p + o);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-    return (w[0] >> ((a & 3) * 8)) & 0xffu;
-  }
-};
-
-// Row key: hash (hashed mode) or widened value (exact mode).  Returns false when the row is
-// skipped (a NULL key outside histogram mode); sets is_null for an exact-mode NULL group row.
-DQ_DEV bool row_key(const FreqDev& f, int64_t r, uint64_t& key, bool& is_null) {
-  is_null = false;
-  if (f.exact) {
-    const KeyCol& c = f.cols[0];
-    if (!fbit(c.valid, r)) {
-      is_null = true;
-      return f.null_as_group != 0;
-    }
-    key = widen(c.type, c.values, r);
-    return true;
-  }
-  uint64_t h = 0x243F6A8885A308D3ULL;
-  for (int k = 0; k < f.n_keys; ++k) {
-    const KeyCol& c = f.cols[k];
-    uint64_t ch;
-    if (!fbit(c.valid, r)) {
-      if (!f.null_as_group) return false;
-      ch = 0x6e756c6c6e756c6cULL + k;
-    } else if (c.type == DQ_UTF8) {
-      const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
-      int32_t s = off[r], e = off[r + 1];
-      FBytes rd{c.data + s};
-      ch = xxh_bytes(rd, (int64_t)(e - s), 17 + k);
-    } else {
-      ch = xxh_long(widen(c.type, c.values, r), 17 + k);
-    }
-    h = rotl64(h ^ ch, 27) * P1 + P4;
-  }
-  h = mix64(h);
-  if (h == kEmpty) h ^= 1;
-  key = h;
-  return true;
-}
-
-// encoded key: per column u32 tag (0 NULL, 1 value) then 8 value bytes, or u32 length + bytes
-// padded to 4
-DQ_DEV uint64_t encoded_size(const FreqDev& f, int64_t r) {
-  uint64_t n = 0;
-  for (int k = 0; k < f.n_keys; ++k) {
-    const KeyCol& c = f.cols[k];
-    n += 4;
-    if (!fbit(c.valid, r)) continue;
-    if (c.type == DQ_UTF8) {
-      const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
-      n += 4 + (((uint64_t)(off[r + 1] - off[r]) + 3) & ~3ULL);
-    } else {
-      n += 8;
-    }
-  }
-  return n;
-}
-
-DQ_DEV void encode_row(const FreqDev& f, int64_t r, uint8_t* dst) {
-  uint32_t* w = reinterpret_cast<uint32_t*>(dst);
-  for (int k = 0; k < f.n_keys; ++k) {
-    const KeyCol& c = f.cols[k];
-    if (!fbit(c.valid, r)) {
-      *w++ = 0;
-      continue;
-    }
-    *w++ = 1;
-    if (c.type == DQ_UTF8) {
-      const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
-      int32_t s = off[r], e = off[r + 1], len = e - s;
-      *w++ = (uint32_t)len;
-      FBytes rd{c.data + s};
-      for (int32_t q = 0; q < len; q += 4) {
-        uint32_t v = 0;
-        for (int b = 0; b < 4 && q + b < len; ++b) v |= rd.u8(q + b) << (8 * b);
-        *w++ = v;
-      }
-    } else {
-      uint64_t v = widen(c.type, c.values, r);
-      *w++ = (uint32_t)v;
-      *w++ = (uint32_t)(v >> 32);
-    }
-  }
-}
-
-DQ_DEV bool row_matches(const FreqDev& f, int64_t r, const uint8_t* enc) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(enc);
-  for (int k = 0; k < f.n_keys; ++k) {
-    const KeyCol& c = f.cols[k];
-    uint32_t tag = *w++;
-    bool valid = fbit(c.valid, r) != 0;
-    if (!valid) {
-      if (tag != 0) return false;
-      continue;
-    }
-    if (tag != 1) return false;
-    if (c.type == DQ_UTF8) {
-      const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
-      int32_t s = off[r], e = off[r + 1], len = e - s;
-      if (*w++ != (uint32_t)len) return false;
-      FBytes rd{c.data + s};
-      for (int32_t q = 0; q < len; q += 4) {
-        uint32_t v = 0;
-        for (int b = 0; b < 4 && q + b < len; ++b) v |= rd.u8(q + b) << (8 * b);
-        uint32_t mask = len - q >= 4 ? 0xffffffffu : ((1u << (8 * (len - q))) - 1u);
-        if ((*w++ & mask) != v) return false;
-      }
-    } else {
-      uint64_t v = widen(c.type, c.values, r);
-      uint64_t s = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-      w += 2;
-      if (s != v) return false;
-    }
-  }
-  return true;
-}
-
-// Source of a group's encoded key when a new group is created in the HBM table.
-struct RowSrc {
-  int64_t row;
-};
-struct ArenaSrc {
-  const uint8_t* enc;
-  uint64_t size;
-};
-
-DQ_DEV void write_arena(const FreqDev& f, uint64_t slot, const RowSrc& s) {
-  uint64_t size = encoded_size(f, s.row);
-  unsigned long long off = atomicAdd(reinterpret_cast<unsigned long long*>(f.arena_cursor),
-                                     (unsigned long long)size);
-  if (off + size > f.arena_cap) {
-    atomicAdd(&f.counters[C_ARENA_OVF], 1ULL);
-    f.reps[slot] = ~0ULL;
-    return;
-  }
-  encode_row(f, s.row, f.arena + off);
-  f.reps[slot] = off;
-}
-DQ_DEV void write_arena(const FreqDev& f, uint64_t slot, const ArenaSrc& s) {
-  unsigned long long off = atomicAdd(reinterpret_cast<unsigned long long*>(f.arena_cursor),
-                                     (unsigned long long)s.size);
-  if (off + s.size > f.arena_cap) {
-    atomicAdd(&f.counters[C_ARENA_OVF], 1ULL);
-    f.reps[slot] = ~0ULL;
-    return;
-  }
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(s.enc);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(f.arena + off);
-  for (uint64_t q = 0; q < s.size / 4; ++q) dst[q] = src[q];
-  f.reps[slot] = off;
-}
-
-// Sum over the wave, added to a table counter by lane 0: the counters are single addresses, so
-// one atomic per row (every new group, every NULL row) would serialize the whole launch on them.
-// Every lane of the wave must call it (the kernels call it after their row loops).
-DQ_DEV void wave_count(unsigned long long* counter, unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  if (__lane_id() == 0 && v) atomicAdd(counter, v);
-}
-
-// Returns 1 when the call created the group (the caller counts C_OCCUPIED with wave_count).
-template <typename Src>
-DQ_DEV uint32_t insert_global(const FreqDev& f, uint64_t key, uint64_t cnt, const Src& src) {
-  if (f.exact && key == kEmpty) {
-    atomicAdd(&f.counters[C_SENTINEL], (unsigned long long)cnt);
-    return 0;
-  }
-  uint64_t slot = (f.exact ? mix64(key) : key) & f.mask;
-  for (uint64_t probe = 0; probe <= f.mask; ++probe) {
-    uint64_t k = __hip_atomic_load(&f.keys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k == key) {
-      atomicAdd(reinterpret_cast<unsigned long long*>(&f.counts[slot]), (unsigned long long)cnt);
-      return 0;
-    }
-    if (k == kEmpty) {
-      unsigned long long prev =
-          atomicCAS(reinterpret_cast<unsigned long long*>(&f.keys[slot]), (unsigned long long)kEmpty,
-                    (unsigned long long)key);
-      if (prev == kEmpty) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(&f.counts[slot]), (unsigned long long)cnt);
-        if (!f.exact) write_arena(f, slot, src);
-        return 1;
-      }
-      if (prev == key) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(&f.counts[slot]), (unsigned long long)cnt);
-        return 0;
-      }
-    }
-    slot = (slot + 1) & f.mask;
-  }
-  atomicAdd(&f.counters[C_ARENA_OVF], 1ULL);  // table full: the host sized it, cannot happen
-  return 0;
-}
-
-__global__ void __launch_bounds__(256) freq_insert_kernel(FreqDev f, int64_t rows, int64_t chunk) {
-  __shared__ unsigned long long lkeys[kLdsSlots];
-  __shared__ unsigned int lcnt[kLdsSlots];
-  __shared__ long long lrep[kLdsSlots];
-  for (int i = threadIdx.x; i < kLdsSlots; i += blockDim.x) {
-    lkeys[i] = kEmpty;
-    lcnt[i] = 0;
-  }
-  __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * chunk;
-  const int64_t r1 = min(r0 + chunk, rows);
-  unsigned long long nulls = 0, null_group = 0, sentinel = 0, created = 0;
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) {
-    uint64_t key;
-    bool is_null;
-    if (!row_key(f, r, key, is_null)) {
-      ++nulls;
-      continue;
-    }
-    if (is_null) {  // exact mode NULL group (histogram)
-      ++null_group;
-      continue;
-    }
-    if (f.exact && key == kEmpty) {  // the key equal to the empty marker lives outside the tables
-      ++sentinel;
-      continue;
-    }
-    bool done = false;
-    uint32_t ls = (uint32_t)mix64(key) & (kLdsSlots - 1);
-    for (int p = 0; p < kLdsProbes && !done; ++p) {
-      unsigned long long k = lkeys[ls];
-      if (k == key) {
-        atomicAdd(&lcnt[ls], 1u);
-        done = true;
-      } else if (k == kEmpty) {
-        unsigned long long prev = atomicCAS(&lkeys[ls], (unsigned long long)kEmpty,
-                                            (unsigned long long)key);
-        if (prev == kEmpty) {
-          lrep[ls] = r;
-          atomicAdd(&lcnt[ls], 1u);
-          done = true;
-        } else if (prev == key) {
-          atomicAdd(&lcnt[ls], 1u);
-          done = true;
-        }
-      }
-      ls = (ls + 1) & (kLdsSlots - 1);
-    }
-    if (!done) created += insert_global(f, key, 1, RowSrc{r});
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kLdsSlots; i += blockDim.x) {
-    if (lkeys[i] != kEmpty) created += insert_global(f, lkeys[i], lcnt[i], RowSrc{lrep[i]});
-  }
-  wave_count(&f.counters[C_OCCUPIED], created);
-  wave_count(&f.counters[C_NULL_ROWS], nulls);
-  wave_count(&f.counters[C_NULL_GROUP], null_group);
-  wave_count(&f.counters[C_SENTINEL], sentinel);
-}
-
-DQ_DEV int64_t find_slot(const FreqDev& f, uint64_t key) {
-  uint64_t slot = key & f.mask;
-  for (uint64_t probe = 0; probe <= f.mask; ++probe) {
-    uint64_t k = f.keys[slot];
-    if (k == key) return (int64_t)slot;
-    if (k == kEmpty) return -1;
-    slot = (slot + 1) & f.mask;
-  }
-  return -1;
-}
-
-__global__ void __launch_bounds__(256) freq_verify_kernel(FreqDev f, int64_t rows) {
-  unsigned long long bad = 0;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
-       r += (int64_t)gridDim.x * blockDim.x) {
-    uint64_t key;
-    bool is_null;
-    if (!row_key(f, r, key, is_null)) continue;
-    int64_t slot = find_slot(f, key);
-    if (slot < 0 || f.reps[slot] == ~0ULL || !row_matches(f, r, f.arena + f.reps[slot])) ++bad;
-  }
-  if (bad) atomicAdd(&f.counters[C_COLLISIONS], bad);
-}
-
-// Re-inserts the groups of another table (merge / rehash).
-__global__ void __launch_bounds__(256) freq_merge_kernel(FreqDev dst, const uint64_t* keys,
-                                                         const uint64_t* counts, const uint64_t* reps,
-                                                         const uint8_t* arena, uint64_t cap,
-                                                         int n_keys) {
-  unsigned long long created = 0;
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t k = keys[s];
-    if (k == kEmpty) continue;
-    uint64_t c = counts[s];
-    if (dst.exact) {
-      created += insert_global(dst, k, c, RowSrc{0});
-    } else {
-      const uint8_t* enc = arena + reps[s];
-      // size of the encoded record
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(enc);
-      uint64_t size = 0;
-      for (int q = 0; q < n_keys; ++q) {
-        uint32_t tag = w[size / 4];
-        size += 4;
-        if (!tag) continue;
-        const KeyCol& col = dst.cols[q];
-        if (col.type == DQ_UTF8) {
-          uint32_t len = w[size / 4];
-          size += 4 + ((len + 3) & ~3u);
-        } else {
-          size += 8;
-        }
-      }
-      created += insert_global(dst, k, c, ArenaSrc{enc, size});
-    }
-  }
-  wave_count(&dst.counters[C_OCCUPIED], created);
-}
-
-// Σ[count == 1], count(*), Σ −(c/n)·ln(c/n): per-block partials in a fixed slot order.
-__global__ void __launch_bounds__(256) freq_summary_kernel(const uint64_t* keys,
-                                                           const uint64_t* counts, uint64_t cap,
-                                                           double num_rows, int64_t* out_i,
-                                                           double* out_d) {
-  __shared__ int64_t sg[256], su[256];
-  __shared__ double se[256];
-  const uint64_t per = (cap + gridDim.x - 1) / gridDim.x;
-  const uint64_t s0 = (uint64_t)blockIdx.x * per, s1 = min(s0 + per, cap);
-  int64_t g = 0, u = 0;
-  double e = 0.0;
-  for (uint64_t s = s0 + threadIdx.x; s < s1; s += blockDim.x) {
-    if (keys[s] == kEmpty) continue;
-    uint64_t c = counts[s];
-    ++g;
-    u += c == 1;
-    double p = (double)c / num_rows;
-    e += -p * log(p);
-  }
-  sg[threadIdx.x] = g;
-  su[threadIdx.x] = u;
-  se[threadIdx.x] = e;
-  __syncthreads();
-  for (int st = 128; st > 0; st >>= 1) {
-    if ((int)threadIdx.x < st) {
-      sg[threadIdx.x] += sg[threadIdx.x + st];
-      su[threadIdx.x] += su[threadIdx.x + st];
-      se[threadIdx.x] += se[threadIdx.x + st];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    out_i[2 * blockIdx.x] = sg[0];
-    out_i[2 * blockIdx.x + 1] = su[0];
-    out_d[blockIdx.x] = se[0];
-  }
-}
-
-__global__ void __launch_bounds__(256) freq_compact_kernel(const uint64_t* keys,
-                                                           const uint64_t* counts,
-                                                           const uint64_t* reps, uint64_t cap,
-                                                           unsigned long long* cursor,
-                                                           uint64_t* out_keys, uint64_t* out_counts,
-                                                           uint64_t* out_reps) {
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    if (keys[s] == kEmpty) continue;
-    unsigned long long i = atomicAdd(cursor, 1ULL);
-    out_keys[i] = keys[s];
-    out_counts[i] = counts[s];
-    if (reps) out_reps[i] = reps[s];
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Hash repartition (multi-GPU frequency path): the reference's groupBy runs a
-// partial HashAggregate per partition, a hash-partitioned Exchange and a final aggregate
-// (GroupingAnalyzers.scala:70).  Here each rank's table IS the partial aggregate; its groups are cut
-// into one segment per owner rank (owner from the HIGH bits of the slot hash, so the owner's own
-// table, which indexes by the low bits, stays uniformly loaded), exchanged by RCCL all-to-all, and
-// re-inserted with their counts on the owner.
-// Wire format per segment: fixed records {key, count, enc_off} (enc_off = byte offset of the group's
-// encoded key inside the segment's var bytes; unused in exact mode) + var bytes (8-aligned).
-// ------------------------------------------------------------------------------------------------
-struct FreqRecord {
+struct RecIn {  // == dq_freq_record
   uint64_t key;
   uint64_t count;
   uint64_t enc_off;
 };
 
-constexpr int kMaxParts = 64;
+struct Group {  // one materialised group
+  uint64_t h;
+  uint64_t count;
+  uint64_t rep;  // hashed: arena offset of the encoded key
+};
 
-DQ_DEV uint32_t owner_of(uint64_t key, int exact, uint32_t parts) {
-  uint64_t h = exact ? mix64(key) : key;
-  return (uint32_t)(((h >> 40) * (uint64_t)parts) >> 24);
+struct FEntry {  // phase-C work item of a recount: partition p, hash subset v of 2^f
+  uint32_t p, f, v, pad;
+};
+
+struct SrcSegs {
+  int64_t rec_start[kMaxParts + 1];
+  int64_t var_base[kMaxParts];
+  int32_t n_src;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Device helpers
+// ------------------------------------------------------------------------------------------------
+DQ_DEV uint64_t lds_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+DQ_DEV void lds_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-DQ_DEV uint64_t enc_record_size(const uint8_t* enc, const int32_t* types, int n_keys) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(enc);
-  uint64_t size = 0;
-  for (int q = 0; q < n_keys; ++q) {
-    uint32_t tag = w[size / 4];
-    size += 4;
-    if (!tag) continue;
-    if (types[q] == DQ_UTF8) size += 4 + ((w[size / 4] + 3) & ~3u);
-    else size += 8;
+// Exclusive scan of one u32 per thread over the workgroup; returns the thread's prefix and sets
+// `total`.  Every thread of the block must call it.
+DQ_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+  const int lane = __lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
   }
-  return size;
+  if (lane == 63) s_wave[wave] = x;
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t w = lane < nw ? s_wave[lane] : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(w, o);
+      if (lane >= o) w += y;
+    }
+    if (lane < nw) s_wave[lane] = w;
+  }
+  __syncthreads();
+  const uint32_t base = wave ? s_wave[wave - 1] : 0u;
+  total = s_wave[nw - 1];
+  __syncthreads();
+  return base + x - v;
 }
 
-struct PartArgs {
+template <typename T>
+DQ_DEV T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Fixed-order block sums (every thread calls; the result is valid in every thread).
+DQ_DEV uint64_t block_sum_u64(uint64_t v, uint64_t* s) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (__lane_id() == 0) s[wave] = v;
+  __syncthreads();
+  uint64_t t = 0;
+  for (int w = 0; w < nw; ++w) t += s[w];
+  __syncthreads();
+  return t;
+}
+DQ_DEV double block_sum_f64(double v, double* s) {
+  v = wave_sum(v);
+  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (__lane_id() == 0) s[wave] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int w = 0; w < nw; ++w) t += s[w];
+  __syncthreads();
+  return t;
+}
+
+// Sum over the wave, added to a table counter by lane 0 (counters are single addresses).
+DQ_DEV void wave_count(unsigned long long* counter, unsigned long long v) {
+  v = wave_sum(v);
+  if (__lane_id() == 0 && v) atomicAdd(counter, v);
+}
+
+// last index j in [0, n) with pos[j] <= x (pos non-decreasing, pos[0] = 0 <= x)
+DQ_DEV uint32_t seg_of(const uint32_t* pos, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;  // answer in [lo, hi)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pos[mid] <= x) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+DQ_DEV int64_t seg_var_base(const SrcSegs& s, int64_t i) {
+  int j = 0;
+  while (j + 1 < s.n_src && i >= s.rec_start[j + 1]) ++j;
+  return s.var_base[j];
+}
+
+template <typename F>
+DQ_DEV void for_digits(uint64_t c, F&& f) {
+  for (uint32_t e = 0; c; c >>= 2, ++e)
+    if (c & 3) f((e << 2) | (uint32_t)(c & 3));
+}
+
+DQ_DEV uint32_t bucket_of(uint64_t h) { return (uint32_t)(h >> (64 - kBucketBits)); }
+// sub-bucket (the s hash bits below the bucket bits); x = h or the exact record >> 8 (both hold
+// hash bits 54..0 in place)
+DQ_DEV uint32_t sub_of(uint64_t x, int s) {
+  return s ? (uint32_t)((x >> (64 - kBucketBits - s)) & ((1u << s) - 1u)) : 0u;
+}
+DQ_DEV uint64_t xrec_h(uint64_t rec, uint32_t b) {
+  return ((uint64_t)b << 55) | ((rec >> 8) & ((1ULL << 55) - 1));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase A: rows (or received records) -> bucket-sorted chunk regions
+// ------------------------------------------------------------------------------------------------
+struct AArgs {
+  KeySet ks;
+  int32_t types[kMaxKeys];
+  int32_t n_keys;
+  int32_t pad;
+  int64_t n_items;
+  int64_t tile_items;
+  const RecIn* rin;
+  uint64_t var_arena_base;
+  SrcSegs segs;
+  uint8_t* recs;
+  uint16_t* hist;
+  uint8_t* arena;
+  unsigned long long* arena_cursor;
+  unsigned long long* counters;
+};
+
+template <bool HASHED, bool FROM_REC>
+__global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
+  using M = FM<HASHED>;
+  constexpr int T = M::kTile, D = M::kDedupe, W = M::kRB / 8;
+  constexpr int ROUNDS = FROM_REC ? 1 : T / kThreads;
+  __shared__ uint32_t bh[kBuckets], bcur[kBuckets];
+  __shared__ uint64_t dkey[D], dcnt[D];
+  __shared__ uint64_t drep[HASHED ? D : 1];
+  __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ uint64_t s_red[kThreads / 64];
+  __shared__ uint32_t s_hits, s_bypass;
+  __shared__ unsigned long long s_arena_base, s_arena_cur;
+  __shared__ uint64_t sortbuf[T * W];
+
+  const int tid = threadIdx.x;
+  const int64_t chunk = blockIdx.x;
+  const int64_t i0 = chunk * a.tile_items;
+  const int64_t i1 = min(i0 + a.tile_items, a.n_items);
+  for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
+  for (int i = tid; i < D; i += kThreads) {
+    dkey[i] = kEmptyKey;
+    dcnt[i] = 0;
+    if (HASHED) drep[i] = kNotReady;
+  }
+  if (tid == 0) {
+    s_hits = 0;
+    s_bypass = 0;
+    s_arena_cur = 0;
+  }
+  __syncthreads();
+
+  uint64_t rh[ROUNDS], rcnt[ROUNDS], rrep[ROUNDS];
+  bool raw[ROUNDS];
+  unsigned long long nulls = 0, nullg = 0;
+#pragma unroll
+  for (int j = 0; j < ROUNDS; ++j) {
+    raw[j] = false;
+    rh[j] = rcnt[j] = rrep[j] = 0;
+    const int64_t i = i0 + (int64_t)j * kThreads + tid;
+    if (i < i1) {
+      uint64_t h = 0, c = 1, rep = 0;
+      bool keyed = true;
+      if constexpr (FROM_REC) {
+        const RecIn r = a.rin[i];
+        c = r.count;
+        h = HASHED ? r.key : fmix_bij(r.key);
+        if (HASHED) rep = a.var_arena_base + (uint64_t)seg_var_base(a.segs, i) + r.enc_off;
+        keyed = c != 0;
+      } else {
+        const int kind = row_kind(a.ks, i, !HASHED);
+        if (kind == ROW_SKIP) {
+          ++nulls;
+          keyed = false;
+        } else if (kind == ROW_NULL_GROUP) {
+          ++nullg;
+          keyed = false;
+        } else {
+          h = HASHED ? row_hash_hashed(a.ks, i) : row_hash_exact(a.ks, i);
+          rep = (uint64_t)(i - i0);
+        }
+      }
+      if (keyed) {
+        bool done = false;
+        if (!s_bypass && h != kEmptyKey) {
+          uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
+          for (int pr = 0; pr < 4 && !done; ++pr) {
+            uint64_t k = lds_load(&dkey[slot]);
+            bool claimed = false;
+            if (k == kEmptyKey) {
+              const uint64_t prev = atomicCAS((unsigned long long*)&dkey[slot], kEmptyKey, h);
+              if (prev == kEmptyKey) claimed = true;
+              else k = prev;
+            }
+            if (claimed) {
+              if (HASHED) lds_store(&drep[slot], rep);
+              atomicAdd((unsigned long long*)&dcnt[slot], c);
+              done = true;
+            } else if (k == h) {
+              bool same = true;
+              if constexpr (HASHED) {
+                const uint64_t r2 = lds_load(&drep[slot]);
+                if (r2 == kNotReady) break;  // being claimed right now: keep the row raw
+                if (r2 != rep) {
+                  if constexpr (FROM_REC)
+                    same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
+                                     reinterpret_cast<const uint32_t*>(a.arena + rep), a.types,
+                                     a.n_keys);
+                  else
+                    same = rows_equal(a.ks, i0 + (int64_t)r2, i0 + (int64_t)rep);
+                }
+              }
+              if (same) {
+                atomicAdd((unsigned long long*)&dcnt[slot], c);
+                if (j == 0) atomicAdd(&s_hits, 1u);
+                done = true;
+              }
+            }
+            slot = (slot + 1) & (D - 1);
+          }
+        }
+        if (!done) {
+          raw[j] = true;
+          rh[j] = h;
+          rcnt[j] = c;
+          rrep[j] = rep;
+          const uint32_t b = bucket_of(h);
+          for_digits(c, [&](uint32_t) { atomicAdd(&bh[b], 1u); });
+        }
+      }
+    }
+    if (!FROM_REC && ROUNDS > 1 && j == 0) {
+      __syncthreads();
+      // fewer than 1/16 of the first kThreads rows repeated a key: high cardinality, so the
+      // LDS table would only cost probes for the rest of the chunk
+      if (tid == 0) s_bypass = s_hits * 16u < (uint32_t)kThreads ? 1u : 0u;
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+
+  // records of the collapsed groups count into the bucket histogram
+  for (int sl = tid; sl < D; sl += kThreads) {
+    const uint64_t k = dkey[sl];
+    if (k == kEmptyKey) continue;
+    const uint32_t b = bucket_of(k);
+    for_digits(dcnt[sl], [&](uint32_t) { atomicAdd(&bh[b], 1u); });
+  }
+  __syncthreads();
+  uint32_t total;
+  const uint32_t mine = tid < kBuckets ? bh[tid] : 0u;
+  const uint32_t ex = block_excl_scan(mine, s_wave, total);
+  uint16_t* hrow = a.hist + chunk * kHistRow;
+  if (tid < kBuckets) {
+    bcur[tid] = ex;
+    hrow[tid] = (uint16_t)ex;
+  }
+  if (tid == 0) hrow[kBuckets] = (uint16_t)total;
+
+  // hashed rows: one arena allocation per chunk for the encoded keys of its records
+  if constexpr (HASHED && !FROM_REC) {
+    uint64_t need = 0;
+#pragma unroll
+    for (int j = 0; j < ROUNDS; ++j)
+      if (raw[j]) need += row_enc_size(a.ks, i0 + (int64_t)rrep[j]);
+    for (int sl = tid; sl < D; sl += kThreads)
+      if (dkey[sl] != kEmptyKey) need += row_enc_size(a.ks, i0 + (int64_t)drep[sl]);
+    const uint64_t all = block_sum_u64(need, s_red);
+    if (tid == 0) s_arena_base = all ? atomicAdd(a.arena_cursor, (unsigned long long)all) : 0ULL;
+  }
+  __syncthreads();
+
+  auto put = [&](uint64_t h, uint32_t code, uint64_t rep) {
+    const uint32_t pos = atomicAdd(&bcur[bucket_of(h)], 1u);
+    if constexpr (HASHED) {
+      sortbuf[2 * pos] = h;
+      sortbuf[2 * pos + 1] = (rep << 8) | code;
+    } else {
+      sortbuf[pos] = (h << 8) | code;
+    }
+  };
+  auto arena_rep = [&](int64_t row) -> uint64_t {  // hashed rows: copy the key into the arena
+    const uint32_t sz = row_enc_size(a.ks, row);
+    const uint64_t off = s_arena_base + atomicAdd(&s_arena_cur, (unsigned long long)sz);
+    row_encode(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
+    return off;
+  };
+#pragma unroll
+  for (int j = 0; j < ROUNDS; ++j) {
+    if (!raw[j]) continue;
+    uint64_t rep = rrep[j];
+    if constexpr (HASHED && !FROM_REC) rep = arena_rep(i0 + (int64_t)rrep[j]);
+    const uint64_t h = rh[j];
+    for_digits(rcnt[j], [&](uint32_t code) { put(h, code, rep); });
+  }
+  for (int sl = tid; sl < D; sl += kThreads) {
+    const uint64_t k = dkey[sl];
+    if (k == kEmptyKey) continue;
+    uint64_t rep = HASHED ? drep[sl] : 0;
+    if constexpr (HASHED && !FROM_REC) rep = arena_rep(i0 + (int64_t)drep[sl]);
+    for_digits(dcnt[sl], [&](uint32_t code) { put(k, code, rep); });
+  }
+  __syncthreads();
+  uint64_t* out = reinterpret_cast<uint64_t*>(a.recs) + chunk * (int64_t)T * W;
+  for (uint32_t q = tid; q < total * W; q += kThreads) out[q] = sortbuf[q];
+  if (!FROM_REC) {
+    wave_count(&a.counters[C_NULL_ROWS], nulls);
+    wave_count(&a.counters[C_NULL_GROUP], nullg);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Finalize: transpose the chunk histograms, scan them per bucket
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) freq_hist_transpose(const uint16_t* hist, int64_t n,
+                                                           uint16_t* lenT, uint16_t* offT) {
+  __shared__ uint16_t tile[64][kHistRow + 1];
+  const int64_t c0 = (int64_t)blockIdx.x * 64;
+  for (int idx = threadIdx.x; idx < 64 * kHistRow; idx += 256) {
+    const int cc = idx / kHistRow, b = idx % kHistRow;
+    tile[cc][b] = c0 + cc < n ? hist[(c0 + cc) * kHistRow + b] : 0;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < kBuckets * 64; idx += 256) {
+    const int b = idx / 64, cc = idx % 64;
+    if (c0 + cc < n) {
+      lenT[(int64_t)b * n + c0 + cc] = (uint16_t)(tile[cc][b + 1] - tile[cc][b]);
+      offT[(int64_t)b * n + c0 + cc] = tile[cc][b];
+    }
+  }
+}
+
+// prefT[b][0..n] = exclusive prefix of lenT[b][*] (prefT[b][n] = bucket total)
+__global__ void __launch_bounds__(kThreads) freq_bucket_scan(const uint16_t* lenT, int64_t n,
+                                                             uint32_t* prefT,
+                                                             unsigned long long* totals) {
+  __shared__ uint32_t s_wave[kThreads / 64];
+  const int b = blockIdx.x;
+  const uint16_t* len = lenT + (int64_t)b * n;
+  uint32_t* pre = prefT + (int64_t)b * (n + 1);
+  uint32_t carry = 0;
+  constexpr int PER = 8;
+  for (int64_t base = 0; base < n; base += (int64_t)kThreads * PER) {
+    uint32_t v[PER], sum = 0;
+    const int64_t my = base + (int64_t)threadIdx.x * PER;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      v[k] = my + k < n ? len[my + k] : 0u;
+      sum += v[k];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(sum, s_wave, tot) + carry;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (my + k < n) pre[my + k] = ex;
+      ex += v[k];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) {
+    pre[n] = carry;
+    totals[b] = carry;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase B: a bucket's unit -> sorted by the next s hash bits
+// ------------------------------------------------------------------------------------------------
+struct BArgs {
+  const uint8_t* recs;
+  const uint16_t* lenT;
+  const uint16_t* offT;
+  const uint32_t* prefT;
+  int64_t n_chunks;
+  const uint32_t* unit_start;
+  const unsigned long long* bucket_base;
+  int32_t s;
+  int32_t hstride;
+  uint8_t* recsB;
+  uint16_t* histB;
+  unsigned long long* unit_out;
+};
+
+DQ_DEV int64_t lower_bound_u32(const uint32_t* a, int64_t lo, int64_t hi, uint64_t x) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((uint64_t)a[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <bool HASHED>
+__global__ void __launch_bounds__(kThreads) freq_phaseB(BArgs a) {
+  using M = FM<HASHED>;
+  constexpr int W = M::kRB / 8, H = unit_half<HASHED>(), UM = unit_max<HASHED>();
+  constexpr int KB = (UM + kThreads - 1) / kThreads;
+  __shared__ uint32_t sw_pos[kThreads];
+  __shared__ uint32_t sw_c[kThreads];
+  __shared__ uint16_t sw_off[kThreads];
+  __shared__ uint32_t sh[kBuckets + 1];
+  __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ int64_t s_c0, s_c1;
+  __shared__ uint32_t s_b, s_in0, s_in1;
+  __shared__ uint64_t outb[UM * W];
+  const int tid = threadIdx.x;
+  const int64_t n = a.n_chunks;
+  if (tid == 0) {
+    const uint32_t w = blockIdx.x;
+    uint32_t lo = 0, hi = kBuckets;  // last b with unit_start[b] <= w
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.unit_start[mid] <= w) lo = mid;
+      else hi = mid;
+    }
+    while (lo + 1 < (uint32_t)kBuckets && a.unit_start[lo + 1] <= w) ++lo;  // skip empty buckets
+    const uint32_t b = lo, u = w - a.unit_start[b];
+    const uint32_t* pre = a.prefT + (int64_t)b * (n + 1);
+    const int64_t c0 = lower_bound_u32(pre, 0, n, (uint64_t)u * H);
+    const int64_t c1 = lower_bound_u32(pre, c0, n, (uint64_t)(u + 1) * H);
+    s_b = b;
+    s_c0 = c0;
+    s_c1 = c1;
+    s_in0 = pre[c0];
+    s_in1 = pre[c1];
+  }
+  const int S = 1 << a.s;
+  for (int i = tid; i <= S; i += kThreads) sh[i] = 0;
+  __syncthreads();
+  const uint32_t b = s_b;
+  const int64_t c0 = s_c0, c1 = s_c1;
+  const uint32_t n_in = s_in1 - s_in0;
+  const uint16_t* lenb = a.lenT + (int64_t)b * n;
+  const uint16_t* offb = a.offT + (int64_t)b * n;
+
+  uint64_t r0[KB], r1[KB];
+  uint32_t base_w = 0;
+  for (int64_t cw = c0; cw < c1; cw += kThreads) {
+    const int64_t c = cw + tid;
+    const uint32_t len = c < c1 ? lenb[c] : 0u;
+    uint32_t wtot;
+    const uint32_t pos = block_excl_scan(len, s_wave, wtot);
+    sw_pos[tid] = pos;
+    sw_c[tid] = (uint32_t)(c - cw);
+    sw_off[tid] = c < c1 ? offb[c] : 0;
+    __syncthreads();
+    const uint32_t nwin = (uint32_t)min((int64_t)kThreads, c1 - cw);
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const uint32_t i = (uint32_t)k * kThreads + tid;
+      if (i >= base_w && i < base_w + wtot) {
+        const uint32_t li = i - base_w;
+        const uint32_t j = seg_of(sw_pos, nwin, li);
+        const int64_t chunk = cw + sw_c[j];
+        const int64_t rec = chunk * M::kTile + sw_off[j] + (li - sw_pos[j]);
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + rec * W;
+        r0[k] = src[0];
+        if (HASHED) r1[k] = src[1];
+      }
+    }
+    base_w += wtot;
+    __syncthreads();
+  }
+  uint32_t rank[KB];
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const uint32_t i = (uint32_t)k * kThreads + tid;
+    if (i < n_in) {
+      const uint32_t sb = sub_of(HASHED ? r0[k] : (r0[k] >> 8), a.s);
+      rank[k] = atomicAdd(&sh[sb], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t tot;
+  const uint32_t v = tid < S ? sh[tid] : 0u;
+  const uint32_t ex = block_excl_scan(v, s_wave, tot);
+  uint16_t* hrow = a.histB + (int64_t)blockIdx.x * a.hstride;
+  if (tid < S) {
+    sh[tid] = ex;
+    hrow[tid] = (uint16_t)ex;
+  }
+  if (tid == 0) hrow[S] = (uint16_t)n_in;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const uint32_t i = (uint32_t)k * kThreads + tid;
+    if (i < n_in) {
+      const uint32_t sb = sub_of(HASHED ? r0[k] : (r0[k] >> 8), a.s);
+      const uint32_t pos = sh[sb] + rank[k];
+      outb[pos * W] = r0[k];
+      if (HASHED) outb[pos * W + 1] = r1[k];
+    }
+  }
+  __syncthreads();
+  const uint64_t obase = a.bucket_base[b] + s_in0;
+  uint64_t* dst = reinterpret_cast<uint64_t*>(a.recsB) + obase * W;
+  for (uint32_t q = tid; q < n_in * W; q += kThreads) dst[q] = outb[q];
+  if (tid == 0) a.unit_out[blockIdx.x] = obase;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase C: count one partition in LDS
+// ------------------------------------------------------------------------------------------------
+struct CArgs {
+  const uint8_t* recsB;
+  const uint16_t* histB;
+  int32_t hstride;
+  int32_t s;
+  const unsigned long long* unit_out;
+  const uint32_t* unit_start;
+  const unsigned long long* bucket_base;
+  const uint8_t* arena;
+  int32_t types[kMaxKeys];
+  int32_t n_keys;
+  int32_t want_cand;
+  double num_rows;
+  const FEntry* entries;  // nullptr: the first pass over every partition
+  unsigned long long* part_groups;
+  unsigned long long* part_unique;
+  double* part_entropy;
+  unsigned long long* part_off;  // materialised groups of partition p start here
+  FEntry* ovf_out;
+  unsigned int* ovf_n;
+  Group* cand;
+  Group* groups;  // materialise every group (nullptr: statistics only)
+  unsigned long long* counters;
+};
+
+template <bool HASHED>
+__global__ void __launch_bounds__(kThreads) freq_phaseC(CArgs a) {
+  using M = FM<HASHED>;
+  constexpr int KT = M::kTableC, W = M::kRB / 8;
+  __shared__ uint64_t tkey[KT], tcnt[KT];
+  __shared__ uint64_t trep[HASHED ? KT : 1];
+  __shared__ uint32_t sw_pos[kThreads];
+  __shared__ uint64_t sw_base[kThreads];
+  __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ uint64_t s_red[kThreads / 64];
+  __shared__ double s_redf[kThreads / 64];
+  __shared__ uint32_t s_occ, s_ovf;
+  __shared__ unsigned long long s_spec_cnt, s_gbase;
+  __shared__ uint64_t s_spec_rep;
+
+  const int tid = threadIdx.x;
+  const uint32_t S = 1u << a.s;
+  uint32_t p, f = 0, fv = 0;
+  if (a.entries) {
+    const FEntry e = a.entries[blockIdx.x];
+    p = e.p;
+    f = e.f;
+    fv = e.v;
+  } else {
+    // XCD-aware: workgroup g runs on XCD g % 8; every partition of bucket b runs on XCD b % 8,
+    // so the bucket's unit histograms are read from one L2
+    const uint32_t g = blockIdx.x, xcd = g & 7u, k = g >> 3;
+    const uint32_t b = xcd + 8u * (k >> a.s);
+    p = (b << a.s) | (k & (S - 1));
+  }
+  const uint32_t b = p >> a.s, sb = p & (S - 1);
+  for (int i = tid; i < KT; i += kThreads) {
+    tkey[i] = kEmptyKey;
+    tcnt[i] = 0;
+    if (HASHED) trep[i] = kNotReady;
+  }
+  if (tid == 0) {
+    s_occ = 0;
+    s_ovf = 0;
+    s_spec_cnt = 0;
+    s_spec_rep = kNotReady;
+  }
+  __syncthreads();
+  const uint32_t fmask = (1u << f) - 1u;
+  const uint32_t u0 = a.unit_start[b], u1 = a.unit_start[b + 1];
+  uint64_t my_off = 0;
+  unsigned long long collisions = 0;
+
+  // Returns false when the record must wait: its group's slot is claimed but the claimer has not
+  // published the representative yet (hashed mode).  Waiting is a retry after the next block
+  // barrier, never a spin, so lanes of one wave can never wait on each other.
+  auto insert = [&](uint64_t h, uint64_t c, uint64_t rep) -> bool {
+    if (h == kEmptyKey) {  // the table's empty marker: its own cell
+      if constexpr (HASHED) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&s_spec_rep, kNotReady, rep);
+        if (prev != kNotReady && prev != rep &&
+            !enc_equal(reinterpret_cast<const uint32_t*>(a.arena + prev),
+                       reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys))
+          ++collisions;
+      }
+      atomicAdd(&s_spec_cnt, (unsigned long long)c);
+      return true;
+    }
+    uint32_t slot = HASHED ? (uint32_t)(((uint64_t)(uint32_t)h * KT) >> 32) : ((uint32_t)h & (KT - 1));
+    for (int probe = 0; probe < KT; ++probe) {
+      uint64_t k = lds_load(&tkey[slot]);
+      bool claimed = false;
+      if (k == kEmptyKey) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&tkey[slot], kEmptyKey, h);
+        if (prev == kEmptyKey) claimed = true;
+        else k = prev;
+      }
+      if (claimed) {
+        if (HASHED) lds_store(&trep[slot], rep);
+        atomicAdd((unsigned long long*)&tcnt[slot], (unsigned long long)c);
+        if (atomicAdd(&s_occ, 1u) >= (uint32_t)(KT * 7 / 8)) s_ovf = 1;
+        return true;
+      }
+      if (k == h) {
+        bool same = true;
+        if constexpr (HASHED) {
+          const uint64_t r2 = lds_load(&trep[slot]);
+          if (r2 == kNotReady) return false;
+          if (r2 != rep)
+            same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
+                             reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
+          if (!same) ++collisions;  // two keys on one 64-bit hash: kept as two groups
+        }
+        if (same) {
+          atomicAdd((unsigned long long*)&tcnt[slot], (unsigned long long)c);
+          return true;
+        }
+      }
+      slot = slot + 1 == (uint32_t)KT ? 0u : slot + 1;
+    }
+    s_ovf = 1;  // table full
+    return true;
+  };
+
+  for (uint32_t uw = u0; uw < u1; uw += kThreads) {
+    const uint32_t u = uw + tid;
+    uint32_t len = 0;
+    uint64_t base = 0;
+    if (u < u1) {
+      const uint16_t* hr = a.histB + (int64_t)u * a.hstride;
+      const uint32_t lo = hr[sb], hi = hr[sb + 1];
+      len = hi - lo;
+      base = a.unit_out[u] + lo;
+      my_off += lo;
+    }
+    uint32_t wtot;
+    const uint32_t pos = block_excl_scan(len, s_wave, wtot);
+    sw_pos[tid] = pos;
+    sw_base[tid] = base;
+    __syncthreads();
+    const uint32_t nwin = min((uint32_t)kThreads, u1 - uw);
+    for (uint32_t it = 0; it * kThreads < wtot; ++it) {
+      const uint32_t li = it * kThreads + tid;
+      uint64_t h = 0, c = 0, rep = 0;
+      bool pending = false;
+      if (li < wtot && !s_ovf) {
+        const uint32_t j = seg_of(sw_pos, nwin, li);
+        const uint64_t idx = sw_base[j] + (li - sw_pos[j]);
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + idx * W;
+        if constexpr (HASHED) {
+          h = src[0];
+          const uint64_t rc = src[1];
+          c = code_count((uint32_t)(rc & 0xff));
+          rep = rc >> 8;
+        } else {
+          const uint64_t r = src[0];
+          h = xrec_h(r, b);
+          c = code_count((uint32_t)(r & 0xff));
+        }
+        pending = f == 0 || ((uint32_t)(h >> kFilterShift) & fmask) == fv;
+      }
+      if constexpr (HASHED) {
+        while (__syncthreads_or(pending ? 1 : 0)) {
+          if (pending) pending = !insert(h, c, rep);
+        }
+      } else {
+        if (pending) insert(h, c, rep);
+      }
+    }
+    __syncthreads();
+  }
+  if (collisions) atomicAdd(&a.counters[C_COLLISIONS], collisions);
+  __syncthreads();
+  if (s_ovf) {
+    if (tid == 0) {
+      const unsigned int q = atomicAdd(a.ovf_n, 2u);
+      a.ovf_out[q] = FEntry{p, f + 1, fv, 0};
+      a.ovf_out[q + 1] = FEntry{p, f + 1, fv | (1u << f), 0};
+    }
+    return;
+  }
+  // statistics of the partition
+  uint32_t g = 0;
+  uint64_t un = 0;
+  double e = 0.0;
+  for (int sl = tid; sl < KT; sl += kThreads) {
+    if (tkey[sl] == kEmptyKey) continue;
+    const uint64_t c = tcnt[sl];
+    ++g;
+    un += c == 1;
+    const double pr = (double)c / a.num_rows;
+    e += -pr * log(pr);
+  }
+  if (tid == 0 && s_spec_cnt) {
+    const uint64_t c = s_spec_cnt;
+    ++g;
+    un += c == 1;
+    const double pr = (double)c / a.num_rows;
+    e += -pr * log(pr);
+  }
+  uint32_t gtot;
+  const uint32_t gex = block_excl_scan(g, s_wave, gtot);
+  const uint64_t utot = block_sum_u64(un, s_red);
+  const double etot = block_sum_f64(e, s_redf);
+  const uint64_t off_sum = block_sum_u64(my_off, s_red);
+  if (tid == 0) {
+    s_gbase = gtot ? atomicAdd(&a.part_groups[p], (unsigned long long)gtot) : 0ULL;
+    if (utot) atomicAdd(&a.part_unique[p], (unsigned long long)utot);
+    if (etot != 0.0) atomicAdd(&a.part_entropy[p], etot);
+  }
+  __syncthreads();
+  if (a.groups) {
+    if (tid == 0) a.part_off[p] = a.bucket_base[b] + off_sum;
+    Group* out = a.groups + a.bucket_base[b] + off_sum + s_gbase + gex;
+    uint32_t q = 0;
+    for (int sl = tid; sl < KT; sl += kThreads) {
+      if (tkey[sl] == kEmptyKey) continue;
+      out[q++] = Group{tkey[sl], tcnt[sl], HASHED ? trep[sl] : 0};
+    }
+    if (tid == 0 && s_spec_cnt) out[q++] = Group{kEmptyKey, s_spec_cnt, HASHED ? s_spec_rep : 0};
+  }
+  if (a.want_cand && a.entries == nullptr) {
+    // top kCand groups of the partition by count (Histogram's rdd.top, per partition)
+    uint64_t tc[kCand];
+    int ts[kCand];
+#pragma unroll
+    for (int q = 0; q < kCand; ++q) {
+      tc[q] = 0;
+      ts[q] = -1;
+    }
+    auto offer = [&](uint64_t c, int sl) {  // insertion with static indices (no scratch)
+#pragma unroll
+      for (int q = 0; q < kCand; ++q) {
+        if (c > tc[q]) {
+          const uint64_t tc2 = tc[q];
+          const int ts2 = ts[q];
+          tc[q] = c;
+          ts[q] = sl;
+          c = tc2;
+          sl = ts2;
+        }
+      }
+    };
+    for (int sl = tid; sl < KT; sl += kThreads)
+      if (tkey[sl] != kEmptyKey) offer(tcnt[sl], sl);
+    if (tid == 0 && s_spec_cnt) offer(s_spec_cnt, KT);  // KT stands for the special cell
+    for (int r = 0; r < kCand; ++r) {
+      const uint64_t mine = tc[0];
+      // block max (count), ties to the lowest thread
+      uint64_t best = mine;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(best, o);
+        best = y > best ? y : best;
+      }
+      if (__lane_id() == 0) s_red[tid >> 6] = best;
+      __syncthreads();
+      uint64_t gbest = 0;
+      for (int w = 0; w < kThreads / 64; ++w) gbest = s_red[w] > gbest ? s_red[w] : gbest;
+      __syncthreads();
+      if (tid == 0) s_occ = ~0u;
+      __syncthreads();
+      if (gbest && mine == gbest) atomicMin(&s_occ, (uint32_t)tid);
+      __syncthreads();
+      Group* cslot = a.cand + (uint64_t)p * kCand + r;
+      if (gbest == 0) {
+        if (tid == 0) *cslot = Group{0, 0, 0};
+      } else if ((uint32_t)tid == s_occ) {
+        const int sl = ts[0];
+        if (sl == KT) *cslot = Group{kEmptyKey, s_spec_cnt, HASHED ? s_spec_rep : 0};
+        else *cslot = Group{tkey[sl], tcnt[sl], HASHED ? trep[sl] : 0};
+#pragma unroll
+        for (int q = 0; q + 1 < kCand; ++q) {  // pop the head
+          tc[q] = tc[q + 1];
+          ts[q] = ts[q + 1];
+        }
+        tc[kCand - 1] = 0;
+        ts[kCand - 1] = -1;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Fixed-order sum of the per-partition statistics: out = {groups, unique, entropy bits}.
+__global__ void __launch_bounds__(kThreads) freq_reduce(const unsigned long long* pg,
+                                                        const unsigned long long* pu,
+                                                        const double* pe, int64_t n,
+                                                        unsigned long long* out) {
+  __shared__ uint64_t s_red[kThreads / 64];
+  __shared__ double s_redf[kThreads / 64];
+  const int64_t per = (n + kThreads - 1) / kThreads;
+  const int64_t lo = threadIdx.x * per, hi = min(lo + per, n);
+  uint64_t g = 0, u = 0;
+  double e = 0.0;
+  for (int64_t i = lo; i < hi; ++i) {
+    g += pg[i];
+    u += pu[i];
+    e += pe[i];
+  }
+  g = block_sum_u64(g, s_red);
+  u = block_sum_u64(u, s_red);
+  e = block_sum_f64(e, s_redf);
+  if (threadIdx.x == 0) {
+    out[0] = g;
+    out[1] = u;
+    out[2] = __builtin_bit_cast(unsigned long long, e);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Selection over Group arrays (Histogram top-N), export and repartition helpers
+// ------------------------------------------------------------------------------------------------
+// hist[k] += #groups with lo <= count < hi falling in bin (count - lo) / width; width == 0
+// selects power-of-two bins (bin = floor(log2(count)))
+__global__ void freq_group_hist(const Group* g, int64_t n, uint64_t lo, uint64_t hi,
+                                uint64_t width, unsigned long long* hist) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = g[i].count;
+    if (c == 0 || c < lo || c >= hi) continue;
+    const uint64_t bin = width ? (c - lo) / width : (uint64_t)(63 - __builtin_clzll(c));
+    atomicAdd(&hist[bin], 1ULL);
+  }
+}
+// every group with count >= hi_take, and groups with lo_tie <= count < hi_take up to `cap`
+__global__ void freq_group_select(const Group* g, int64_t n, uint64_t hi_take, uint64_t lo_tie,
+                                  unsigned long long cap, Group* out, unsigned long long* n_take,
+                                  unsigned long long* n_tie, Group* out_tie) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const Group x = g[i];
+    if (x.count == 0) continue;
+    if (x.count >= hi_take) {
+      out[atomicAdd(n_take, 1ULL)] = x;
+    } else if (x.count >= lo_tie) {
+      const unsigned long long q = atomicAdd(n_tie, 1ULL);
+      if (q < cap) out_tie[q] = x;
+    }
+  }
+}
+// partitions whose candidate list is full (more groups than kCand) and whose last candidate
+// beats `tau`: their unlisted groups could outrank the selection
+__global__ void freq_cand_check(const Group* cand, const unsigned long long* part_groups, int64_t P,
+                                uint64_t tau, unsigned long long* bad) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    if (part_groups[p] > (unsigned long long)kCand && cand[p * kCand + kCand - 1].count > tau)
+      atomicAdd(bad, 1ULL);
+  }
+}
+
+struct PartTypes {
   int32_t types[kMaxKeys];
   int32_t n_keys;
   int32_t exact;
@@ -508,120 +976,79 @@ struct PartArgs {
   uint32_t pad;
 };
 
-// pass 1: records and var bytes per owner
-__global__ void __launch_bounds__(256) freq_part_count_kernel(const uint64_t* keys, const uint64_t* reps,
-                                                              const uint8_t* arena, uint64_t cap,
-                                                              PartArgs a,
-                                                              unsigned long long* n_rec,
-                                                              unsigned long long* n_var) {
+// Owner rank of a group for the multi-GPU repartition: the high hash bits, so every owner gets a
+// contiguous hash range (and the owner's own partitions stay uniformly loaded).
+DQ_DEV uint32_t owner_of(uint64_t h, uint32_t parts) {
+  return (uint32_t)(((h >> 40) * (uint64_t)parts) >> 24);
+}
+
+__global__ void __launch_bounds__(256) freq_owner_count(const Group* g, int64_t n,
+                                                        const uint8_t* arena, PartTypes t,
+                                                        unsigned long long* n_rec,
+                                                        unsigned long long* n_var) {
   __shared__ unsigned long long lr[kMaxParts], lv[kMaxParts];
   for (int i = threadIdx.x; i < kMaxParts; i += blockDim.x) lr[i] = lv[i] = 0;
   __syncthreads();
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t k = keys[s];
-    if (k == kEmpty) continue;
-    uint32_t o = owner_of(k, a.exact, a.parts);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const Group x = g[i];
+    const uint32_t o = owner_of(x.h, t.parts);
     atomicAdd(&lr[o], 1ULL);
-    if (!a.exact) atomicAdd(&lv[o], (enc_record_size(arena + reps[s], a.types, a.n_keys) + 7) & ~7ULL);
+    if (!t.exact)
+      atomicAdd(&lv[o],
+                (unsigned long long)((enc_size(reinterpret_cast<const uint32_t*>(arena + x.rep),
+                                               t.types, t.n_keys) + 7u) & ~7u));
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < a.parts; i += blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < t.parts; i += blockDim.x) {
     if (lr[i]) atomicAdd(&n_rec[i], lr[i]);
     if (lv[i]) atomicAdd(&n_var[i], lv[i]);
   }
 }
 
-// pass 2: scatter into the owner segments (rec_base / var_base = exclusive prefix sums of pass 1)
-__global__ void __launch_bounds__(256) freq_part_scatter_kernel(
-    const uint64_t* keys, const uint64_t* counts, const uint64_t* reps, const uint8_t* arena,
-    uint64_t cap, PartArgs a, const unsigned long long* rec_base, const unsigned long long* var_base,
-    unsigned long long* rec_cur, unsigned long long* var_cur, FreqRecord* out_rec, uint8_t* out_var) {
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < cap;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    uint64_t k = keys[s];
-    if (k == kEmpty) continue;
-    uint32_t o = owner_of(k, a.exact, a.parts);
-    unsigned long long i = atomicAdd(&rec_cur[o], 1ULL);
-    FreqRecord r{k, counts[s], 0};
-    if (!a.exact) {
-      const uint8_t* enc = arena + reps[s];
-      uint64_t size = enc_record_size(enc, a.types, a.n_keys);
-      unsigned long long off = atomicAdd(&var_cur[o], (size + 7) & ~7ULL);
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(enc);
+// dq_freq_record per group (exact: the value, fmix_inv(h); hashed: h and the encoded key copied
+// into the owner's var segment)
+__global__ void __launch_bounds__(256) freq_owner_scatter(
+    const Group* g, int64_t n, const uint8_t* arena, PartTypes t,
+    const unsigned long long* rec_base, const unsigned long long* var_base,
+    unsigned long long* rec_cur, unsigned long long* var_cur, RecIn* out_rec, uint8_t* out_var) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const Group x = g[i];
+    const uint32_t o = owner_of(x.h, t.parts);
+    const unsigned long long q = atomicAdd(&rec_cur[o], 1ULL);
+    RecIn r{t.exact ? fmix_inv(x.h) : x.h, x.count, 0};
+    if (!t.exact) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(arena + x.rep);
+      const uint32_t size = enc_size(src, t.types, t.n_keys);
+      const unsigned long long off = atomicAdd(&var_cur[o], (unsigned long long)((size + 7u) & ~7u));
       uint32_t* dst = reinterpret_cast<uint32_t*>(out_var + var_base[o] + off);
-      for (uint64_t q = 0; q < size / 4; ++q) dst[q] = src[q];
+      for (uint32_t w = 0; w < size / 4; ++w) dst[w] = src[w];
+      if (size & 4u) dst[size / 4] = 0;  // 8-byte padding
       r.enc_off = off;
     }
-    out_rec[rec_base[o] + i] = r;
+    out_rec[rec_base[o] + q] = r;
   }
 }
 
-struct SrcSegs {
-  int64_t rec_start[kMaxParts + 1];  // records of source j: [rec_start[j], rec_start[j+1])
-  int64_t var_base[kMaxParts];       // byte offset of source j's var segment
-  int32_t n_src;
-};
-
-DQ_DEV const uint8_t* record_enc(const FreqRecord& r, int64_t i, const uint8_t* var,
-                                 const SrcSegs& segs) {
-  int j = 0;
-  while (j + 1 < segs.n_src && i >= segs.rec_start[j + 1]) ++j;
-  return var + segs.var_base[j] + r.enc_off;
+// hashed merge: the appended chunks' records point into the appended arena bytes
+__global__ void freq_rebase(uint64_t* recs, const uint16_t* hist, int64_t chunk0, int tile,
+                            uint64_t delta) {
+  const int64_t c = chunk0 + blockIdx.x;
+  const uint32_t n = hist[c * kHistRow + kBuckets];
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) recs[(c * tile + i) * 2 + 1] += delta << 8;
 }
 
-// Re-inserts received groups with their counts (the final aggregate after the Exchange).
-__global__ void __launch_bounds__(256) freq_insert_records_kernel(FreqDev f, const FreqRecord* rec,
-                                                                  const uint8_t* var, SrcSegs segs,
-                                                                  PartArgs a) {
-  const int64_t n = segs.rec_start[segs.n_src];
-  unsigned long long created = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    FreqRecord r = rec[i];
-    if (f.exact) {
-      created += insert_global(f, r.key, r.count, RowSrc{0});
-    } else {
-      const uint8_t* enc = record_enc(r, i, var, segs);
-      created += insert_global(f, r.key, r.count,
-                               ArenaSrc{enc, enc_record_size(enc, a.types, a.n_keys)});
-    }
+// compact the materialised groups: partition p's g_p groups start at src_off[p], go to dst_off[p]
+__global__ void freq_compact(const Group* src, const unsigned long long* src_off,
+                             const unsigned long long* cnt, const unsigned long long* dst_off,
+                             int64_t P, Group* dst) {
+  for (int64_t p = blockIdx.x; p < P; p += gridDim.x) {
+    const uint64_t n = cnt[p];
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[dst_off[p] + i] = src[src_off[p] + i];
   }
-  wave_count(&f.counters[C_OCCUPIED], created);
 }
 
-// Hashed mode: every received group must carry the same encoded key as the group it landed in, so
-// a 64-bit hash collision between groups of different ranks is detected, never merged.
-__global__ void __launch_bounds__(256) freq_verify_records_kernel(FreqDev f, const FreqRecord* rec,
-                                                                  const uint8_t* var, SrcSegs segs,
-                                                                  PartArgs a) {
-  const int64_t n = segs.rec_start[segs.n_src];
-  unsigned long long bad = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    FreqRecord r = rec[i];
-    const uint32_t* enc = reinterpret_cast<const uint32_t*>(record_enc(r, i, var, segs));
-    int64_t slot = find_slot(f, r.key);
-    if (slot < 0 || f.reps[slot] == ~0ULL) {
-      ++bad;
-      continue;
-    }
-    const uint32_t* have = reinterpret_cast<const uint32_t*>(f.arena + f.reps[slot]);
-    uint64_t size = enc_record_size(reinterpret_cast<const uint8_t*>(enc), a.types, a.n_keys);
-    for (uint64_t q = 0; q < size / 4; ++q)
-      if (have[q] != enc[q]) {
-        ++bad;
-        break;
-      }
-  }
-  if (bad) atomicAdd(&f.counters[C_COLLISIONS], bad);
-}
-
-__global__ void fill_u64(uint64_t* p, uint64_t n, uint64_t v) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (uint64_t)gridDim.x * blockDim.x)
-    p[i] = v;
-}
 
 }  // namespace dq
 
@@ -636,15 +1063,45 @@ struct dq_freq {
   std::vector<int32_t> types;
   bool exact = false;
   int mode_null_as_group = -1;  // fixed by the first add
-  uint64_t cap = 0;             // slots (power of two)
-  DevBuf<uint64_t> keys, counts, reps;
-  DevBuf<uint8_t> arena;
-  DevBuf<uint64_t> arena_cursor;
-  DevBuf<unsigned long long> counters;
-  uint64_t h_counters[C_N] = {0, 0, 0, 0, 0, 0};
+  int tile = 0, rb = 0;
+  // the table: bucket-sorted chunk regions (phase A output) + their histograms
+  DevBuf<uint8_t> recs;
+  DevBuf<uint16_t> hist;
+  int64_t n_chunks = 0;
+  DevBuf<uint8_t> arena;                 // hashed: encoded keys
+  DevBuf<unsigned long long> dev_words;  // counters[C_N], then the arena cursor
+  uint64_t h_counters[C_N] = {0, 0, 0};
   uint64_t arena_used = 0;
   int64_t num_rows = 0;
   hipStream_t stream = nullptr;
+  // finalize cache (phase B)
+  bool b_valid = false;
+  int s_bits = 0;
+  uint64_t R = 0;
+  uint32_t n_units = 0;
+  std::vector<unsigned long long> h_bucket_base = std::vector<unsigned long long>(kBuckets + 1, 0);
+  std::vector<uint32_t> h_unit_start = std::vector<uint32_t>(kBuckets + 1, 0);
+  DevBuf<uint16_t> lenT, offT, histB;
+  DevBuf<uint32_t> prefT, unit_start;
+  DevBuf<unsigned long long> totals, bucket_base, unit_out;
+  DevBuf<uint8_t> recsB;
+  // (phase C)
+  bool c_valid = false, c_groups = false, c_cand = false;
+  double c_num_rows = -1.0;
+  DevBuf<unsigned long long> part_groups, part_unique, part_off;
+  DevBuf<double> part_entropy;
+  DevBuf<Group> cand, groups, compact;
+  int64_t n_compact = -1;
+  DevBuf<FEntry> ovf_a, ovf_b;
+  DevBuf<unsigned int> ovf_n;
+  DevBuf<unsigned long long> red;
+  uint64_t st_groups = 0, st_unique = 0;
+  double st_entropy = 0.0;
+  bool recounted = false;
+  // last top-k (dq_freq_topk is called twice: sizes, then data)
+  int topk_k = -1;
+  std::vector<int64_t> topk_counts, topk_offs;
+  std::vector<uint8_t> topk_bytes;
 };
 
 static unsigned grid_for(uint64_t n, unsigned cap = 4096) {
@@ -654,68 +1111,450 @@ static unsigned grid_for(uint64_t n, unsigned cap = 4096) {
   return (unsigned)g;
 }
 
-static FreqDev dev_view(dq_freq* f) {
-  FreqDev d;
-  memset(&d, 0, sizeof(d));
-  d.keys = f->keys.p;
-  d.counts = f->counts.p;
-  d.reps = f->exact ? nullptr : f->reps.p;
-  d.mask = f->cap - 1;
-  d.arena = f->arena.p;
-  d.arena_cursor = f->arena_cursor.p;
-  d.arena_cap = f->arena.p ? f->arena.n : 0;
-  d.counters = f->counters.p;
-  d.n_keys = f->n_keys;
-  d.exact = f->exact ? 1 : 0;
-  d.null_as_group = f->mode_null_as_group > 0 ? 1 : 0;
-  // key types are needed by every kernel that sizes an encoded key (rehash / merge re-inserts)
-  for (int k = 0; k < f->n_keys; ++k) d.cols[k].type = f->types[k];
-  return d;
+static void invalidate(dq_freq* f) {
+  f->b_valid = false;
+  f->c_valid = f->c_groups = f->c_cand = false;
+  f->n_compact = -1;
+  f->topk_k = -1;
+}
+
+// Grows `b` to at least `need` elements keeping the first `used` (stream-ordered copy).
+template <typename T>
+static hipError_t grow_keep(DevBuf<T>& b, size_t used, size_t need, hipStream_t st) {
+  if (need <= b.n && b.p) return hipSuccess;
+  DevBuf<T> nb;
+  hipError_t e = nb.ensure(std::max(need, b.n * 2));
+  if (e != hipSuccess) return e;
+  if (used) {
+    e = hipMemcpyAsync(nb.p, b.p, used * sizeof(T), hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return e;
+    e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+  }
+  b.swap(nb);
+  return hipSuccess;
+}
+
+static dq_status ensure_chunks(dq_freq* f, int64_t add) {
+  const int64_t need = f->n_chunks + add;
+  HIP_TRY(grow_keep(f->recs, (size_t)f->n_chunks * f->tile * f->rb, (size_t)need * f->tile * f->rb,
+                    f->stream));
+  HIP_TRY(grow_keep(f->hist, (size_t)f->n_chunks * kHistRow, (size_t)need * kHistRow, f->stream));
+  return DQ_OK;
 }
 
 static dq_status pull_counters(dq_freq* f) {
   HIP_TRY(hipStreamSynchronize(f->stream));
-  unsigned long long c[C_N];
-  HIP_TRY(hipMemcpy(c, f->counters.p, sizeof(c), hipMemcpyDeviceToHost));
-  for (int k = 0; k < C_N; ++k) f->h_counters[k] = c[k];
-  uint64_t cur = 0;
-  if (!f->exact) HIP_TRY(hipMemcpy(&cur, f->arena_cursor.p, 8, hipMemcpyDeviceToHost));
-  f->arena_used = cur;
+  unsigned long long w[C_N + 1];
+  HIP_TRY(hipMemcpy(w, f->dev_words.p, sizeof(w), hipMemcpyDeviceToHost));
+  for (int k = 0; k < C_N; ++k) f->h_counters[k] = w[k];
+  f->arena_used = w[C_N];
   return DQ_OK;
 }
 
-// Grows the slot arrays to `new_cap` and re-inserts every group.
-static dq_status rehash(dq_freq* f, uint64_t new_cap) {
-  DevBuf<uint64_t> ok, oc, orp;
-  ok.swap(f->keys);
-  oc.swap(f->counts);
-  orp.swap(f->reps);
-  uint64_t old_cap = f->cap;
-  DevBuf<uint8_t> oarena;
-  oarena.swap(f->arena);
-  HIP_TRY(f->keys.ensure(new_cap));
-  HIP_TRY(f->counts.ensure(new_cap));
-  if (!f->exact) HIP_TRY(f->reps.ensure(new_cap));
-  hipLaunchKernelGGL(fill_u64, dim3(grid_for(new_cap)), dim3(256), 0, f->stream, f->keys.p, new_cap,
-                     kEmpty);
-  HIP_TRY(hipMemsetAsync(f->counts.p, 0, new_cap * 8, f->stream));
-  f->cap = new_cap;
-  if (!f->exact) {
-    HIP_TRY(f->arena.ensure(std::max<uint64_t>(oarena.n, 64)));
-    HIP_TRY(hipMemsetAsync(f->arena_cursor.p, 0, 8, f->stream));
+static dq_status push_counters(dq_freq* f) {
+  HIP_TRY(hipStreamSynchronize(f->stream));
+  unsigned long long w[C_N + 1];
+  for (int k = 0; k < C_N; ++k) w[k] = f->h_counters[k];
+  w[C_N] = f->arena_used;
+  HIP_TRY(hipMemcpy(f->dev_words.p, w, sizeof(w), hipMemcpyHostToDevice));
+  return DQ_OK;
+}
+
+template <bool HASHED>
+static void launch_phaseA(dq_freq* f, const AArgs& a, int64_t chunks, bool from_rec) {
+  if (from_rec)
+    hipLaunchKernelGGL((freq_phaseA<HASHED, true>), dim3((unsigned)chunks), dim3(kThreads), 0,
+                       f->stream, a);
+  else
+    hipLaunchKernelGGL((freq_phaseA<HASHED, false>), dim3((unsigned)chunks), dim3(kThreads), 0,
+                       f->stream, a);
+}
+
+static AArgs base_args(dq_freq* f) {
+  AArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int k = 0; k < f->n_keys; ++k) {
+    a.types[k] = f->types[k];
+    a.ks.cols[k].type = f->types[k];
   }
-  // occupied is recounted by the re-insert
-  HIP_TRY(hipMemsetAsync(f->counters.p + C_OCCUPIED, 0, 8, f->stream));
-  if (old_cap) {
-    FreqDev d = dev_view(f);
-    hipLaunchKernelGGL(freq_merge_kernel, dim3(grid_for(old_cap)), dim3(256), 0, f->stream, d, ok.p,
-                       oc.p, f->exact ? nullptr : orp.p, oarena.p, old_cap, f->n_keys);
+  a.n_keys = f->n_keys;
+  a.ks.n_keys = f->n_keys;
+  a.ks.null_as_group = f->mode_null_as_group > 0 ? 1 : 0;
+  a.recs = f->recs.p + (size_t)f->n_chunks * f->tile * f->rb;
+  a.hist = f->hist.p + (size_t)f->n_chunks * kHistRow;
+  a.arena = f->arena.p;
+  a.arena_cursor = f->dev_words.p + C_N;
+  a.counters = f->dev_words.p;
+  return a;
+}
+
+// ---- finalize: phase B ------------------------------------------------------------------------
+static dq_status finalize_b(dq_freq* f) {
+  if (f->b_valid) return DQ_OK;
+  const int64_t n = f->n_chunks;
+  std::fill(f->h_bucket_base.begin(), f->h_bucket_base.end(), 0ULL);
+  std::fill(f->h_unit_start.begin(), f->h_unit_start.end(), 0u);
+  f->R = 0;
+  f->s_bits = 0;
+  f->n_units = 0;
+  if (n == 0) {
+    f->b_valid = true;
+    return DQ_OK;
+  }
+  HIP_TRY(f->lenT.ensure((size_t)kBuckets * n));
+  HIP_TRY(f->offT.ensure((size_t)kBuckets * n));
+  HIP_TRY(f->prefT.ensure((size_t)kBuckets * (n + 1)));
+  HIP_TRY(f->totals.ensure(kBuckets));
+  hipLaunchKernelGGL(freq_hist_transpose, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, f->stream,
+                     f->hist.p, n, f->lenT.p, f->offT.p);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(freq_bucket_scan, dim3(kBuckets), dim3(kThreads), 0, f->stream, f->lenT.p, n,
+                     f->prefT.p, f->totals.p);
+  HIP_TRY(hipGetLastError());
+  std::vector<unsigned long long> tot(kBuckets);
+  HIP_TRY(hipStreamSynchronize(f->stream));
+  HIP_TRY(hipMemcpy(tot.data(), f->totals.p, kBuckets * 8, hipMemcpyDeviceToHost));
+  uint64_t R = 0;
+  for (auto t : tot) R += t;
+  const int target = f->exact ? FM<false>::kTarget : FM<true>::kTarget;
+  int s = 0;
+  while (s < kMaxSubBits && ((uint64_t)kBuckets << s) * (uint64_t)target < R) ++s;
+  const uint64_t H = (uint64_t)f->tile / 2;
+  uint32_t u = 0;
+  for (int b = 0; b < kBuckets; ++b) {
+    f->h_unit_start[b] = u;
+    f->h_bucket_base[b + 1] = f->h_bucket_base[b] + tot[b];
+    u += (uint32_t)((tot[b] + H - 1) / H);
+  }
+  f->h_unit_start[kBuckets] = u;
+  f->R = R;
+  f->s_bits = s;
+  f->n_units = u;
+  HIP_TRY(f->unit_start.ensure(kBuckets + 1));
+  HIP_TRY(f->bucket_base.ensure(kBuckets + 1));
+  HIP_TRY(hipMemcpy(f->unit_start.p, f->h_unit_start.data(), (kBuckets + 1) * 4,
+                    hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(f->bucket_base.p, f->h_bucket_base.data(), (kBuckets + 1) * 8,
+                    hipMemcpyHostToDevice));
+  if (u) {
+    const int hs = (1 << s) + 1;
+    HIP_TRY(f->recsB.ensure(std::max<uint64_t>(R, 1) * f->rb));
+    HIP_TRY(f->histB.ensure((size_t)u * hs));
+    HIP_TRY(f->unit_out.ensure(u));
+    BArgs a;
+    a.recs = f->recs.p;
+    a.lenT = f->lenT.p;
+    a.offT = f->offT.p;
+    a.prefT = f->prefT.p;
+    a.n_chunks = n;
+    a.unit_start = f->unit_start.p;
+    a.bucket_base = f->bucket_base.p;
+    a.s = s;
+    a.hstride = hs;
+    a.recsB = f->recsB.p;
+    a.histB = f->histB.p;
+    a.unit_out = f->unit_out.p;
+    if (f->exact)
+      hipLaunchKernelGGL(freq_phaseB<false>, dim3(u), dim3(kThreads), 0, f->stream, a);
+    else
+      hipLaunchKernelGGL(freq_phaseB<true>, dim3(u), dim3(kThreads), 0, f->stream, a);
     HIP_TRY(hipGetLastError());
   }
+  f->b_valid = true;
+  return DQ_OK;
+}
+
+// ---- finalize: phase C ------------------------------------------------------------------------
+static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
+  dq_status st = finalize_b(f);
+  if (st != DQ_OK) return st;
+  const double nr = (double)f->num_rows;
+  if (f->c_valid && f->c_num_rows == nr && (!want_groups || f->c_groups) && (!want_cand || f->c_cand))
+    return DQ_OK;
+  want_groups = want_groups || (f->c_valid && f->c_groups);
+  want_cand = want_cand || (f->c_valid && f->c_cand);
+  const int64_t P = (int64_t)kBuckets << f->s_bits;
+  HIP_TRY(f->part_groups.ensure(P));
+  HIP_TRY(f->part_unique.ensure(P));
+  HIP_TRY(f->part_off.ensure(P));
+  HIP_TRY(f->part_entropy.ensure(P));
+  HIP_TRY(f->red.ensure(3));
+  HIP_TRY(f->ovf_n.ensure(1));
+  HIP_TRY(hipMemsetAsync(f->part_groups.p, 0, P * 8, f->stream));
+  HIP_TRY(hipMemsetAsync(f->part_unique.p, 0, P * 8, f->stream));
+  HIP_TRY(hipMemsetAsync(f->part_off.p, 0, P * 8, f->stream));
+  HIP_TRY(hipMemsetAsync(f->part_entropy.p, 0, P * 8, f->stream));
+  if (want_groups) HIP_TRY(f->groups.ensure(std::max<uint64_t>(f->R, 1)));
+  if (want_cand) {
+    HIP_TRY(f->cand.ensure((size_t)P * kCand));
+    HIP_TRY(hipMemsetAsync(f->cand.p, 0, (size_t)P * kCand * sizeof(Group), f->stream));
+  }
+  f->recounted = false;
+  if (f->R) {
+    CArgs a;
+    memset(&a, 0, sizeof(a));
+    a.recsB = f->recsB.p;
+    a.histB = f->histB.p;
+    a.hstride = (1 << f->s_bits) + 1;
+    a.s = f->s_bits;
+    a.unit_out = f->unit_out.p;
+    a.unit_start = f->unit_start.p;
+    a.bucket_base = f->bucket_base.p;
+    a.arena = f->arena.p;
+    for (int k = 0; k < f->n_keys; ++k) a.types[k] = f->types[k];
+    a.n_keys = f->n_keys;
+    a.want_cand = want_cand ? 1 : 0;
+    a.num_rows = nr;
+    a.part_groups = f->part_groups.p;
+    a.part_unique = f->part_unique.p;
+    a.part_entropy = f->part_entropy.p;
+    a.part_off = f->part_off.p;
+    a.cand = want_cand ? f->cand.p : nullptr;
+    a.groups = want_groups ? f->groups.p : nullptr;
+    a.counters = f->dev_words.p;
+    HIP_TRY(f->ovf_a.ensure(2 * P));
+    HIP_TRY(hipMemsetAsync(f->ovf_n.p, 0, 4, f->stream));
+    a.entries = nullptr;
+    a.ovf_out = f->ovf_a.p;
+    a.ovf_n = f->ovf_n.p;
+    unsigned grid = (unsigned)P;
+    for (int round = 0; round < 24; ++round) {
+      if (f->exact)
+        hipLaunchKernelGGL(freq_phaseC<false>, dim3(grid), dim3(kThreads), 0, f->stream, a);
+      else
+        hipLaunchKernelGGL(freq_phaseC<true>, dim3(grid), dim3(kThreads), 0, f->stream, a);
+      HIP_TRY(hipGetLastError());
+      unsigned int m = 0;
+      HIP_TRY(hipStreamSynchronize(f->stream));
+      HIP_TRY(hipMemcpy(&m, f->ovf_n.p, 4, hipMemcpyDeviceToHost));
+      if (m == 0) break;
+      if (round == 23) return fail(DQ_ERR_OUT_OF_MEMORY, "frequency partition does not fit");
+      // recount the overflowing partitions over disjoint hash subsets
+      f->recounted = true;
+      f->ovf_a.swap(f->ovf_b);  // ovf_b = this round's entries
+      HIP_TRY(f->ovf_a.ensure(2 * (size_t)m));
+      HIP_TRY(hipMemsetAsync(f->ovf_n.p, 0, 4, f->stream));
+      a.entries = f->ovf_b.p;
+      a.ovf_out = f->ovf_a.p;
+      grid = m;
+    }
+  }
+  hipLaunchKernelGGL(freq_reduce, dim3(1), dim3(kThreads), 0, f->stream, f->part_groups.p,
+                     f->part_unique.p, f->part_entropy.p, P, f->red.p);
+  HIP_TRY(hipGetLastError());
+  unsigned long long r[3];
   HIP_TRY(hipStreamSynchronize(f->stream));
+  HIP_TRY(hipMemcpy(r, f->red.p, sizeof(r), hipMemcpyDeviceToHost));
+  f->st_groups = r[0];
+  f->st_unique = r[1];
+  f->st_entropy = __builtin_bit_cast(double, r[2]);
+  f->c_valid = true;
+  f->c_num_rows = nr;
+  f->c_groups = want_groups;
+  f->c_cand = want_cand;
+  f->n_compact = -1;
   return pull_counters(f);
 }
 
+// The materialised groups, compacted: f->compact[0 .. f->n_compact).
+static dq_status compact_groups(dq_freq* f) {
+  dq_status st = finalize_c(f, true, false);
+  if (st != DQ_OK) return st;
+  if (f->n_compact >= 0) return DQ_OK;
+  const int64_t P = (int64_t)kBuckets << f->s_bits;
+  std::vector<unsigned long long> cnt(P), dst(P);
+  HIP_TRY(hipMemcpy(cnt.data(), f->part_groups.p, P * 8, hipMemcpyDeviceToHost));
+  unsigned long long tot = 0;
+  for (int64_t p = 0; p < P; ++p) {
+    dst[p] = tot;
+    tot += cnt[p];
+  }
+  HIP_TRY(f->compact.ensure(std::max<unsigned long long>(tot, 1)));
+  if (tot) {
+    DevBuf<unsigned long long> d;
+    HIP_TRY(d.ensure(P));
+    HIP_TRY(hipMemcpy(d.p, dst.data(), P * 8, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(freq_compact, dim3((unsigned)std::min<int64_t>(P, 65536)), dim3(256), 0,
+                       f->stream, f->groups.p, f->part_off.p, f->part_groups.p, d.p, P,
+                       f->compact.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(f->stream));
+  }
+  f->n_compact = (int64_t)tot;
+  return DQ_OK;
+}
+
+static PartTypes part_types(const dq_freq* f, int parts) {
+  PartTypes t;
+  memset(&t, 0, sizeof(t));
+  for (int k = 0; k < f->n_keys; ++k) t.types[k] = f->types[k];
+  t.n_keys = f->n_keys;
+  t.exact = f->exact ? 1 : 0;
+  t.parts = (uint32_t)parts;
+  return t;
+}
+
+// Records (+ var bytes) of `n` device groups cut into `parts` owner segments.
+static dq_status owner_sizes(dq_freq* f, const Group* g, int64_t n, int parts,
+                             std::vector<unsigned long long>& rec, std::vector<unsigned long long>& var) {
+  DevBuf<unsigned long long> cnt;
+  HIP_TRY(cnt.ensure(2 * kMaxParts));
+  HIP_TRY(hipMemsetAsync(cnt.p, 0, 2 * kMaxParts * 8, f->stream));
+  if (n)
+    hipLaunchKernelGGL(freq_owner_count, dim3(grid_for(n)), dim3(256), 0, f->stream, g, n,
+                       f->arena.p, part_types(f, parts), cnt.p, cnt.p + kMaxParts);
+  HIP_TRY(hipGetLastError());
+  std::vector<unsigned long long> h(2 * kMaxParts);
+  HIP_TRY(hipStreamSynchronize(f->stream));
+  HIP_TRY(hipMemcpy(h.data(), cnt.p, h.size() * 8, hipMemcpyDeviceToHost));
+  rec.assign(h.begin(), h.begin() + parts);
+  var.assign(h.begin() + kMaxParts, h.begin() + kMaxParts + parts);
+  return DQ_OK;
+}
+
+static dq_status owner_scatter(dq_freq* f, const Group* g, int64_t n, int parts, RecIn* out_rec,
+                               uint8_t* out_var, const std::vector<unsigned long long>& rec,
+                               const std::vector<unsigned long long>& var) {
+  std::vector<unsigned long long> base(4 * kMaxParts, 0);
+  unsigned long long tr = 0, tv = 0;
+  for (int i = 0; i < parts; ++i) {
+    base[i] = tr;
+    base[kMaxParts + i] = tv;
+    tr += rec[i];
+    tv += var[i];
+  }
+  if (!tr) return DQ_OK;
+  DevBuf<unsigned long long> d;
+  HIP_TRY(d.ensure(base.size()));
+  HIP_TRY(hipMemcpy(d.p, base.data(), base.size() * 8, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(freq_owner_scatter, dim3(grid_for(n)), dim3(256), 0, f->stream, g, n,
+                     f->arena.p, part_types(f, parts), d.p, d.p + kMaxParts, d.p + 2 * kMaxParts,
+                     d.p + 3 * kMaxParts, out_rec, out_var);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(f->stream));
+  return DQ_OK;
+}
+
+// Encoded keys (export format) of device groups, assembled on the host.
+static dq_status encode_groups(dq_freq* f, const Group* g, int64_t n, std::vector<int64_t>& counts,
+                               std::vector<int64_t>& offs, std::vector<uint8_t>& bytes) {
+  auto put32 = [&](uint32_t v) {
+    for (int b = 0; b < 4; ++b) bytes.push_back((uint8_t)(v >> (8 * b)));
+  };
+  if (n == 0) return DQ_OK;
+  std::vector<unsigned long long> rec, var;
+  dq_status st = owner_sizes(f, g, n, 1, rec, var);
+  if (st != DQ_OK) return st;
+  DevBuf<RecIn> dr;
+  DevBuf<uint8_t> dv;
+  HIP_TRY(dr.ensure(rec[0]));
+  HIP_TRY(dv.ensure(std::max<unsigned long long>(var[0], 1)));
+  st = owner_scatter(f, g, n, 1, dr.p, dv.p, rec, var);
+  if (st != DQ_OK) return st;
+  std::vector<RecIn> hr(rec[0]);
+  std::vector<uint8_t> hv(var[0]);
+  HIP_TRY(hipMemcpy(hr.data(), dr.p, rec[0] * sizeof(RecIn), hipMemcpyDeviceToHost));
+  if (var[0]) HIP_TRY(hipMemcpy(hv.data(), dv.p, var[0], hipMemcpyDeviceToHost));
+  for (const RecIn& r : hr) {
+    offs.push_back((int64_t)bytes.size());
+    counts.push_back((int64_t)r.count);
+    if (f->exact) {
+      put32(1);
+      put32((uint32_t)r.key);
+      put32((uint32_t)(r.key >> 32));
+    } else {
+      const uint8_t* e = hv.data() + r.enc_off;
+      const uint32_t sz = enc_size(reinterpret_cast<const uint32_t*>(e), f->types.data(), f->n_keys);
+      bytes.insert(bytes.end(), e, e + sz);
+    }
+  }
+  return DQ_OK;
+}
+
+static void put_null_group(dq_freq* f, std::vector<int64_t>& counts, std::vector<int64_t>& offs,
+                           std::vector<uint8_t>& bytes) {
+  offs.push_back((int64_t)bytes.size());
+  counts.push_back((int64_t)f->h_counters[C_NULL_GROUP]);
+  for (int b = 0; b < 4; ++b) bytes.push_back(0);  // tag 0 = NULL
+}
+
+// Top `k` groups by count of a device Group array (count 0 entries are holes): the count range
+// holding the k-th largest is narrowed with histograms until it is one value (ties are
+// arbitrary, like rdd.top) or small enough to bring to the host.
+static dq_status select_top(dq_freq* f, const Group* arr, int64_t n, int k, std::vector<Group>& out) {
+  out.clear();
+  if (n == 0 || k <= 0) return DQ_OK;
+  constexpr int kBins = 1024;
+  constexpr uint64_t kSmall = 4096;
+  DevBuf<unsigned long long> hist;
+  HIP_TRY(hist.ensure(kBins + 2));
+  std::vector<unsigned long long> hb(kBins);
+  auto run_hist = [&](uint64_t lo, uint64_t hi, uint64_t width, int nb) -> dq_status {
+    HIP_TRY(hipMemsetAsync(hist.p, 0, kBins * 8, f->stream));
+    hipLaunchKernelGGL(freq_group_hist, dim3(grid_for(n)), dim3(256), 0, f->stream, arr, n, lo, hi,
+                       width, hist.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(f->stream));
+    HIP_TRY(hipMemcpy(hb.data(), hist.p, nb * 8, hipMemcpyDeviceToHost));
+    return DQ_OK;
+  };
+  // round 0: powers of two (width 0 selects log2 bins)
+  dq_status st = run_hist(1, ~0ULL, 0, 64);
+  if (st != DQ_OK) return st;
+  uint64_t total = 0;
+  for (int j = 0; j < 64; ++j) total += hb[j];
+  uint64_t lo, hi, above = 0, inbin;
+  if (total <= (uint64_t)k) {
+    lo = 1;
+    hi = 1;  // take everything
+    inbin = 0;
+  } else {
+    int j = 63;
+    while (above + hb[j] < (uint64_t)k) above += hb[j--];
+    lo = 1ULL << j;
+    hi = j == 63 ? ~0ULL : (1ULL << (j + 1));
+    inbin = hb[j];
+    while (inbin > kSmall && hi - lo > 1) {
+      const uint64_t width = (hi - lo + kBins - 1) / kBins;
+      const int nb = (int)((hi - lo + width - 1) / width);
+      st = run_hist(lo, hi, width, nb);
+      if (st != DQ_OK) return st;
+      int i = nb - 1;
+      while (above + hb[i] < (uint64_t)k) above += hb[i--];
+      const uint64_t lo2 = lo + (uint64_t)i * width;
+      hi = std::min(lo2 + width, hi);
+      lo = lo2;
+      inbin = hb[i];
+    }
+  }
+  const uint64_t cap = hi - lo == 1 ? (uint64_t)k - above : inbin;
+  DevBuf<Group> take, tie;
+  DevBuf<unsigned long long> nt;
+  HIP_TRY(take.ensure(std::max<uint64_t>(total <= (uint64_t)k ? total : above, 1)));
+  HIP_TRY(tie.ensure(std::max<uint64_t>(cap, 1)));
+  HIP_TRY(nt.ensure(2));
+  HIP_TRY(hipMemsetAsync(nt.p, 0, 16, f->stream));
+  hipLaunchKernelGGL(freq_group_select, dim3(grid_for(n)), dim3(256), 0, f->stream, arr, n, hi, lo,
+                     (unsigned long long)cap, take.p, nt.p, nt.p + 1, tie.p);
+  HIP_TRY(hipGetLastError());
+  unsigned long long cnts[2];
+  HIP_TRY(hipStreamSynchronize(f->stream));
+  HIP_TRY(hipMemcpy(cnts, nt.p, 16, hipMemcpyDeviceToHost));
+  const uint64_t nt_take = cnts[0], nt_tie = std::min<uint64_t>(cnts[1], cap);
+  out.resize(nt_take + nt_tie);
+  if (nt_take) HIP_TRY(hipMemcpy(out.data(), take.p, nt_take * sizeof(Group), hipMemcpyDeviceToHost));
+  if (nt_tie)
+    HIP_TRY(hipMemcpy(out.data() + nt_take, tie.p, nt_tie * sizeof(Group), hipMemcpyDeviceToHost));
+  std::stable_sort(out.begin(), out.end(),
+                   [](const Group& x, const Group& y) { return x.count > y.count; });
+  if (out.size() > (size_t)k) out.resize(k);
+  return DQ_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------------
 extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_types,
                                     int64_t capacity_hint, dq_freq** out) {
   if (!out || !key_types || n_keys <= 0) return fail(DQ_ERR_INVALID_ARGUMENT, "bad arguments");
@@ -728,40 +1567,30 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
   for (int t : f->types)
     if (t < DQ_BOOL || t > DQ_UTF8) return fail(DQ_ERR_INVALID_ARGUMENT, "bad key type %d", t);
   f->exact = n_keys == 1 && f->types[0] != DQ_UTF8;
-  if (n_keys > 1)
-    for (int t : f->types)
-      if (t != DQ_UTF8)
-        return fail(DQ_ERR_UNSUPPORTED,
-                    "grouping on several columns is implemented for string columns only");
+  f->tile = f->exact ? FM<false>::kTile : FM<true>::kTile;
+  f->rb = f->exact ? FM<false>::kRB : FM<true>::kRB;
   HIP_TRY(hipSetDevice(device));
-  HIP_TRY(f->counters.ensure(C_N));
-  HIP_TRY(hipMemset(f->counters.p, 0, C_N * 8));
-  HIP_TRY(f->arena_cursor.ensure(1));
-  HIP_TRY(hipMemset(f->arena_cursor.p, 0, 8));
-  uint64_t cap = 1024;
-  while (cap < (uint64_t)std::max<int64_t>(0, capacity_hint) * 2) cap <<= 1;
-  dq_status st = rehash(f.get(), cap);
-  if (st != DQ_OK) return st;
+  HIP_TRY(f->dev_words.ensure(C_N + 1));
+  HIP_TRY(hipMemset(f->dev_words.p, 0, (C_N + 1) * 8));
+  if (capacity_hint > 0) {
+    dq_status st = ensure_chunks(f.get(), (capacity_hint + f->tile - 1) / f->tile);
+    if (st != DQ_OK) return st;
+  }
   *out = f.release();
   return DQ_OK;
 }
 
-// Empties the table but keeps its capacity (slot arrays and arena), like a Spark task reusing its
-// aggregation buffer: repeated group-bys of the same shape pay no device allocation.
 extern "C" dq_status dq_freq_reset(dq_freq* f, void* hip_stream) {
   if (!f) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   HIP_TRY(hipSetDevice(f->device));
   f->stream = reinterpret_cast<hipStream_t>(hip_stream);
-  hipLaunchKernelGGL(fill_u64, dim3(grid_for(f->cap)), dim3(256), 0, f->stream, f->keys.p, f->cap,
-                     kEmpty);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemsetAsync(f->counts.p, 0, f->cap * 8, f->stream));
-  HIP_TRY(hipMemsetAsync(f->counters.p, 0, C_N * 8, f->stream));
-  HIP_TRY(hipMemsetAsync(f->arena_cursor.p, 0, 8, f->stream));
+  HIP_TRY(hipMemsetAsync(f->dev_words.p, 0, (C_N + 1) * 8, f->stream));
   for (int k = 0; k < C_N; ++k) f->h_counters[k] = 0;
   f->arena_used = 0;
   f->num_rows = 0;
+  f->n_chunks = 0;
   f->mode_null_as_group = -1;
+  invalidate(f);
   return DQ_OK;
 }
 
@@ -776,112 +1605,70 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
                                         int null_as_group, void* hip_stream) {
   if (!f || !keys) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   if (n_keys != f->n_keys) return fail(DQ_ERR_INVALID_ARGUMENT, "expected %d key columns", f->n_keys);
-  int mode = null_as_group ? 1 : 0;
+  const int mode = null_as_group ? 1 : 0;
   if (f->mode_null_as_group >= 0 && f->mode_null_as_group != mode)
     return fail(DQ_ERR_STATE, "null_as_group must be the same for every batch");
-  f->mode_null_as_group = mode;
   if (mode && f->n_keys != 1) return fail(DQ_ERR_UNSUPPORTED, "NULL-as-group needs one key column");
-  int64_t rows = keys[0].length;
+  const int64_t rows = keys[0].length;
   for (int k = 0; k < n_keys; ++k) {
     if (keys[k].type != f->types[k]) return fail(DQ_ERR_WRONG_TYPE, "key %d has the wrong type", k);
     if (keys[k].length != rows) return fail(DQ_ERR_INVALID_ARGUMENT, "key columns differ in length");
     if (rows > 0 && !keys[k].values) return fail(DQ_ERR_INVALID_ARGUMENT, "key %d has no values", k);
+    if (rows > 0 && keys[k].type == DQ_UTF8 && !keys[k].data)
+      return fail(DQ_ERR_INVALID_ARGUMENT, "utf8 key %d has no character data", k);
   }
+  f->mode_null_as_group = mode;
   HIP_TRY(hipSetDevice(f->device));
   f->stream = reinterpret_cast<hipStream_t>(hip_stream);
   f->num_rows += rows;
+  invalidate(f);
   if (rows == 0) return DQ_OK;
-  // capacity: keep the load factor <= 1/2 even if every row is a new group
-  uint64_t need = 2 * (f->h_counters[C_OCCUPIED] + (uint64_t)rows);
-  if (need > f->cap) {
-    uint64_t cap = f->cap;
-    while (cap < need) cap <<= 1;
-    dq_status st = rehash(f, cap);
-    if (st != DQ_OK) return st;
-  }
+  const int64_t chunks = (rows + f->tile - 1) / f->tile;
+  dq_status st = ensure_chunks(f, chunks);
+  if (st != DQ_OK) return st;
   if (!f->exact) {
-    // arena: worst case every row a new group
-    uint64_t extra = 0;
+    // arena room for the worst case (every row its own record), see row_enc_size
+    uint64_t bound = 0;
     for (int k = 0; k < n_keys; ++k) {
-      extra += (uint64_t)rows * 12;
       if (keys[k].type == DQ_UTF8) {
-        int32_t last = 0;
+        int32_t first = 0, last = 0;
+        HIP_TRY(hipMemcpy(&first, keys[k].values, 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(&last, reinterpret_cast<const int32_t*>(keys[k].values) + rows, 4,
                           hipMemcpyDeviceToHost));
-        int32_t first = 0;
-        HIP_TRY(hipMemcpy(&first, keys[k].values, 4, hipMemcpyDeviceToHost));
-        extra += (uint64_t)(last - first) + (uint64_t)rows * 3;
+        if (last < first) return fail(DQ_ERR_INVALID_ARGUMENT, "utf8 key %d has bad offsets", k);
+        bound += (uint64_t)rows * (8 + 3 + kNullValueLen + 3) + (uint64_t)(last - first);
+      } else {
+        bound += (uint64_t)rows * 12;
       }
     }
-    uint64_t want = f->arena_used + extra + 64;
-    if (want > f->arena.n) {
-      // grow, keeping the existing bytes
-      DevBuf<uint8_t> bigger;
-      HIP_TRY(bigger.ensure(std::max<uint64_t>(want, f->arena.n * 2)));
-      if (f->arena_used)
-        HIP_TRY(hipMemcpyAsync(bigger.p, f->arena.p, f->arena_used, hipMemcpyDeviceToDevice, f->stream));
-      HIP_TRY(hipStreamSynchronize(f->stream));
-      f->arena.swap(bigger);
-    }
+    HIP_TRY(grow_keep(f->arena, f->arena_used, f->arena_used + bound + 64, f->stream));
   }
-  FreqDev d = dev_view(f);
+  AArgs a = base_args(f);
   for (int k = 0; k < n_keys; ++k)
-    d.cols[k] = KeyCol{keys[k].type, 0, keys[k].validity, keys[k].values, keys[k].data};
-  unsigned grid = grid_for((uint64_t)rows, 2048);
-  int64_t chunk = (rows + grid - 1) / grid;
-  hipLaunchKernelGGL(freq_insert_kernel, dim3(grid), dim3(256), 0, f->stream, d, rows, chunk);
+    a.ks.cols[k] = KeyCol{keys[k].type, 0, keys[k].validity, keys[k].values, keys[k].data};
+  a.n_items = rows;
+  a.tile_items = f->tile;
+  if (f->exact) launch_phaseA<false>(f, a, chunks, false);
+  else launch_phaseA<true>(f, a, chunks, false);
   HIP_TRY(hipGetLastError());
-  if (!f->exact) {
-    hipLaunchKernelGGL(freq_verify_kernel, dim3(grid_for((uint64_t)rows, 4096)), dim3(256), 0,
-                       f->stream, d, rows);
-    HIP_TRY(hipGetLastError());
-  }
-  dq_status st = pull_counters(f);
-  if (st != DQ_OK) return st;
-  if (f->h_counters[C_ARENA_OVF])
-    return fail(DQ_ERR_OUT_OF_MEMORY, "frequency table arena overflow");
-  if (f->h_counters[C_COLLISIONS])
-    return fail(DQ_ERR_UNSUPPORTED,
-                "64-bit key-hash collision between distinct groups detected (%llu rows)",
-                (unsigned long long)f->h_counters[C_COLLISIONS]);
-  return DQ_OK;
+  f->n_chunks += chunks;
+  return pull_counters(f);
 }
 
 extern "C" dq_status dq_freq_summarize(dq_freq* f, dq_freq_summary* out) {
   if (!f || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   HIP_TRY(hipSetDevice(f->device));
-  const unsigned G = grid_for(f->cap, 8192);  // >= 32 blocks per CU: enough loads in flight
-  DevBuf<int64_t> pi;
-  DevBuf<double> pd;
-  HIP_TRY(pi.ensure(2 * G));
-  HIP_TRY(pd.ensure(G));
-  const double n = (double)f->num_rows;
-  hipLaunchKernelGGL(freq_summary_kernel, dim3(G), dim3(256), 0, f->stream, f->keys.p, f->counts.p,
-                     f->cap, n, pi.p, pd.p);
-  HIP_TRY(hipGetLastError());
-  std::vector<int64_t> hi(2 * G);
-  std::vector<double> hd(G);
-  HIP_TRY(hipStreamSynchronize(f->stream));
-  HIP_TRY(hipMemcpy(hi.data(), pi.p, hi.size() * 8, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(hd.data(), pd.p, hd.size() * 8, hipMemcpyDeviceToHost));
-  dq_status st = pull_counters(f);
+  dq_status st = finalize_c(f, false, false);
   if (st != DQ_OK) return st;
-  int64_t g = 0, u = 0;
-  double e = 0.0;
-  for (unsigned b = 0; b < G; ++b) {
-    g += hi[2 * b];
-    u += hi[2 * b + 1];
-    e += hd[b];
-  }
-  auto extra_group = [&](uint64_t c) {
-    if (!c) return;
+  int64_t g = (int64_t)f->st_groups, u = (int64_t)f->st_unique;
+  double e = f->st_entropy;
+  const uint64_t c = f->h_counters[C_NULL_GROUP];
+  if (c) {  // exact-mode NULL group (Histogram on a fixed-width column)
     ++g;
     u += c == 1;
-    double p = (double)c / n;
+    const double p = (double)c / (double)f->num_rows;
     e += -p * std::log(p);
-  };
-  extra_group(f->h_counters[C_SENTINEL]);
-  extra_group(f->h_counters[C_NULL_GROUP]);
+  }
   out->num_rows = f->num_rows;
   out->n_groups = g;
   out->n_unique = u;
@@ -893,99 +1680,124 @@ extern "C" dq_status dq_freq_summarize(dq_freq* f, dq_freq_summary* out) {
 extern "C" dq_status dq_freq_num_groups(dq_freq* f, int64_t* n) {
   if (!f || !n) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   HIP_TRY(hipSetDevice(f->device));
-  dq_status st = pull_counters(f);
+  dq_status st = finalize_c(f, false, false);
   if (st != DQ_OK) return st;
-  *n = (int64_t)(f->h_counters[C_OCCUPIED] + (f->h_counters[C_SENTINEL] ? 1 : 0) +
-                 (f->h_counters[C_NULL_GROUP] ? 1 : 0));
+  *n = (int64_t)(f->st_groups + (f->h_counters[C_NULL_GROUP] ? 1 : 0));
   return DQ_OK;
 }
 
-// Exports every group: counts, and the encoded key of each group (see encode_row: per key column a
-// u32 tag 0 = NULL / 1 = value, then 8 little-endian value bytes or a u32 length + bytes padded to
-// 4).  key_offsets has n + 1 entries.  Pass key_bytes_out = NULL to query the byte size only.
-extern "C" dq_status dq_freq_export(dq_freq* f, int64_t* counts_out, int64_t* key_offsets_out,
-                                    uint8_t* key_bytes_out, int64_t capacity,
-                                    int64_t key_bytes_capacity, int64_t* key_bytes_needed) {
-  if (!f) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
-  int64_t n = 0;
-  dq_status st = dq_freq_num_groups(f, &n);
-  if (st != DQ_OK) return st;
-  const uint64_t occ = f->h_counters[C_OCCUPIED];
-  std::vector<uint64_t> hk(occ), hc(occ), hr(f->exact ? 0 : occ);
-  if (occ) {
-    DevBuf<uint64_t> ok, oc, orp;
-    DevBuf<unsigned long long> cur;
-    HIP_TRY(ok.ensure(occ));
-    HIP_TRY(oc.ensure(occ));
-    if (!f->exact) HIP_TRY(orp.ensure(occ));
-    HIP_TRY(cur.ensure(1));
-    HIP_TRY(hipMemsetAsync(cur.p, 0, 8, f->stream));
-    hipLaunchKernelGGL(freq_compact_kernel, dim3(grid_for(f->cap)), dim3(256), 0, f->stream,
-                       f->keys.p, f->counts.p, f->exact ? nullptr : f->reps.p, f->cap, cur.p, ok.p,
-                       oc.p, f->exact ? nullptr : orp.p);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(f->stream));
-    HIP_TRY(hipMemcpy(hk.data(), ok.p, occ * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(hc.data(), oc.p, occ * 8, hipMemcpyDeviceToHost));
-    if (!f->exact) HIP_TRY(hipMemcpy(hr.data(), orp.p, occ * 8, hipMemcpyDeviceToHost));
-  }
-  std::vector<uint8_t> arena;
-  if (!f->exact && f->arena_used) {
-    arena.resize(f->arena_used);
-    HIP_TRY(hipMemcpy(arena.data(), f->arena.p, f->arena_used, hipMemcpyDeviceToHost));
-  }
-  // assemble encoded keys
-  std::vector<int64_t> counts;
-  std::vector<uint8_t> bytes;
-  std::vector<int64_t> offs;
-  auto put32 = [&](uint32_t v) {
-    for (int b = 0; b < 4; ++b) bytes.push_back((uint8_t)(v >> (8 * b)));
-  };
-  auto put_exact = [&](bool null, uint64_t v, uint64_t c) {
-    offs.push_back((int64_t)bytes.size());
-    counts.push_back((int64_t)c);
-    put32(null ? 0 : 1);
-    if (!null) {
-      put32((uint32_t)v);
-      put32((uint32_t)(v >> 32));
-    }
-  };
-  for (uint64_t i = 0; i < occ; ++i) {
-    if (f->exact) {
-      put_exact(false, hk[i], hc[i]);
-    } else {
-      offs.push_back((int64_t)bytes.size());
-      counts.push_back((int64_t)hc[i]);
-      const uint8_t* enc = arena.data() + hr[i];
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(enc);
-      uint64_t size = 0;
-      for (int q = 0; q < f->n_keys; ++q) {
-        uint32_t tag = w[size / 4];
-        size += 4;
-        if (!tag) continue;
-        if (f->types[q] == DQ_UTF8) size += 4 + ((w[size / 4] + 3) & ~3u);
-        else size += 8;
-      }
-      bytes.insert(bytes.end(), enc, enc + size);
-    }
-  }
-  if (f->h_counters[C_SENTINEL]) put_exact(false, kEmpty, f->h_counters[C_SENTINEL]);
-  if (f->h_counters[C_NULL_GROUP]) put_exact(true, 0, f->h_counters[C_NULL_GROUP]);
-  offs.push_back((int64_t)bytes.size());
+extern "C" int64_t dq_freq_num_rows(const dq_freq* f) { return f ? f->num_rows : -1; }
+
+static dq_status copy_out(const std::vector<int64_t>& counts, const std::vector<int64_t>& offs,
+                          const std::vector<uint8_t>& bytes, int64_t* counts_out,
+                          int64_t* key_offsets_out, uint8_t* key_bytes_out, int64_t capacity,
+                          int64_t key_bytes_capacity, int64_t* key_bytes_needed) {
   if (key_bytes_needed) *key_bytes_needed = (int64_t)bytes.size();
   if (!key_bytes_out) return DQ_OK;
   if (capacity < (int64_t)counts.size() || key_bytes_capacity < (int64_t)bytes.size())
     return fail(DQ_ERR_INVALID_ARGUMENT, "export buffers too small");
-  if (counts_out) memcpy(counts_out, counts.data(), counts.size() * 8);
+  if (counts_out && !counts.empty()) memcpy(counts_out, counts.data(), counts.size() * 8);
   if (key_offsets_out) memcpy(key_offsets_out, offs.data(), offs.size() * 8);
-  memcpy(key_bytes_out, bytes.data(), bytes.size());
+  if (!bytes.empty()) memcpy(key_bytes_out, bytes.data(), bytes.size());
   return DQ_OK;
 }
 
-// dst += src (FrequenciesAndNumRows.sum, GroupingAnalyzers.scala:128-148): counts of equal keys
-// add, numRows add.
-extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src) {
-  if (!dst || !src) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+extern "C" dq_status dq_freq_export(dq_freq* f, int64_t* counts_out, int64_t* key_offsets_out,
+                                    uint8_t* key_bytes_out, int64_t capacity,
+                                    int64_t key_bytes_capacity, int64_t* key_bytes_needed) {
+  if (!f) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  HIP_TRY(hipSetDevice(f->device));
+  dq_status st = compact_groups(f);
+  if (st != DQ_OK) return st;
+  std::vector<int64_t> counts, offs;
+  std::vector<uint8_t> bytes;
+  st = encode_groups(f, f->compact.p, f->n_compact, counts, offs, bytes);
+  if (st != DQ_OK) return st;
+  if (f->h_counters[C_NULL_GROUP]) put_null_group(f, counts, offs, bytes);
+  offs.push_back((int64_t)bytes.size());
+  return copy_out(counts, offs, bytes, counts_out, key_offsets_out, key_bytes_out, capacity,
+                  key_bytes_capacity, key_bytes_needed);
+}
+
+// Histogram's details: rdd.top(maxDetailBins)(OrderByAbsoluteCount) (Histogram.scala:78).
+extern "C" dq_status dq_freq_topk(dq_freq* f, int k, int64_t* counts_out, int64_t* key_offsets_out,
+                                  uint8_t* key_bytes_out, int64_t key_bytes_capacity, int64_t* n_out,
+                                  int64_t* key_bytes_needed) {
+  if (!f || !n_out || k < 0) return fail(DQ_ERR_INVALID_ARGUMENT, "bad arguments");
+  HIP_TRY(hipSetDevice(f->device));
+  if (f->topk_k != k || !f->c_valid) {
+    dq_status st = finalize_c(f, false, true);
+    if (st != DQ_OK) return st;
+    const int64_t P = (int64_t)kBuckets << f->s_bits;
+    std::vector<Group> top;
+    bool exact_path = f->recounted;
+    if (!exact_path) {
+      st = select_top(f, f->cand.p, P * kCand, k, top);
+      if (st != DQ_OK) return st;
+      const uint64_t tau = top.size() == (size_t)k && k > 0 ? top.back().count : 0;
+      DevBuf<unsigned long long> bad;
+      HIP_TRY(bad.ensure(1));
+      HIP_TRY(hipMemsetAsync(bad.p, 0, 8, f->stream));
+      hipLaunchKernelGGL(freq_cand_check, dim3(grid_for(P)), dim3(256), 0, f->stream, f->cand.p,
+                         f->part_groups.p, P, tau, bad.p);
+      HIP_TRY(hipGetLastError());
+      unsigned long long nb = 0;
+      HIP_TRY(hipStreamSynchronize(f->stream));
+      HIP_TRY(hipMemcpy(&nb, bad.p, 8, hipMemcpyDeviceToHost));
+      exact_path = nb != 0;
+    }
+    if (exact_path) {  // select over every group
+      st = compact_groups(f);
+      if (st != DQ_OK) return st;
+      st = select_top(f, f->compact.p, f->n_compact, k, top);
+      if (st != DQ_OK) return st;
+    }
+    // the exact-mode NULL group competes like any other
+    const uint64_t nullg = f->h_counters[C_NULL_GROUP];
+    f->topk_counts.clear();
+    f->topk_offs.clear();
+    f->topk_bytes.clear();
+    DevBuf<Group> dg;
+    HIP_TRY(dg.ensure(std::max<size_t>(top.size(), 1)));
+    if (!top.empty())
+      HIP_TRY(hipMemcpy(dg.p, top.data(), top.size() * sizeof(Group), hipMemcpyHostToDevice));
+    std::vector<int64_t> c1, o1;
+    std::vector<uint8_t> b1;
+    st = encode_groups(f, dg.p, (int64_t)top.size(), c1, o1, b1);
+    if (st != DQ_OK) return st;
+    // owner_scatter keeps no order: restore count order, placing the NULL group
+    std::vector<size_t> idx(c1.size());
+    for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return c1[x] > c1[y]; });
+    o1.push_back((int64_t)b1.size());
+    bool null_done = nullg == 0;
+    auto emit_null = [&]() {
+      put_null_group(f, f->topk_counts, f->topk_offs, f->topk_bytes);
+      null_done = true;
+    };
+    for (size_t i : idx) {
+      if ((int)f->topk_counts.size() >= k) break;
+      if (!null_done && (int64_t)nullg > c1[i]) emit_null();
+      if ((int)f->topk_counts.size() >= k) break;
+      f->topk_offs.push_back((int64_t)f->topk_bytes.size());
+      f->topk_counts.push_back(c1[i]);
+      f->topk_bytes.insert(f->topk_bytes.end(), b1.begin() + o1[i], b1.begin() + o1[i + 1]);
+    }
+    if (!null_done && (int)f->topk_counts.size() < k) emit_null();
+    f->topk_offs.push_back((int64_t)f->topk_bytes.size());
+    f->topk_k = k;
+  }
+  *n_out = (int64_t)f->topk_counts.size();
+  return copy_out(f->topk_counts, f->topk_offs, f->topk_bytes, counts_out, key_offsets_out,
+                  key_bytes_out, *n_out, key_bytes_capacity, key_bytes_needed);
+}
+
+// dst += src (FrequenciesAndNumRows.sum, GroupingAnalyzers.scala:128-148): the source's chunks
+// are appended, so equal keys meet in the next finalize and their counts add; numRows add.
+extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src_c) {
+  if (!dst || !src_c) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  dq_freq* src = const_cast<dq_freq*>(src_c);
+  if (dst == src) return fail(DQ_ERR_INVALID_ARGUMENT, "cannot merge a table into itself");
   if (dst->n_keys != src->n_keys || dst->types != src->types)
     return fail(DQ_ERR_STATE, "frequency tables group on different key types");
   if (dst->device != src->device) return fail(DQ_ERR_UNSUPPORTED, "tables on different devices");
@@ -993,83 +1805,44 @@ extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src) {
       dst->mode_null_as_group != src->mode_null_as_group)
     return fail(DQ_ERR_STATE, "frequency tables differ in NULL handling");
   HIP_TRY(hipSetDevice(dst->device));
-  dq_freq* s = const_cast<dq_freq*>(src);
-  HIP_TRY(hipStreamSynchronize(s->stream));
-  dq_status st = pull_counters(s);
+  HIP_TRY(hipStreamSynchronize(src->stream));
+  dq_status st = pull_counters(src);
   if (st != DQ_OK) return st;
-  if (dst->mode_null_as_group < 0) dst->mode_null_as_group = s->mode_null_as_group;
-  uint64_t need = 2 * (dst->h_counters[C_OCCUPIED] + s->h_counters[C_OCCUPIED]) + 2;
-  if (need > dst->cap) {
-    uint64_t cap = dst->cap;
-    while (cap < need) cap <<= 1;
-    st = rehash(dst, cap);
-    if (st != DQ_OK) return st;
-  }
-  if (!dst->exact) {
-    uint64_t want = dst->arena_used + s->arena_used + 64;
-    if (want > dst->arena.n) {
-      DevBuf<uint8_t> bigger;
-      HIP_TRY(bigger.ensure(want));
-      if (dst->arena_used)
-        HIP_TRY(hipMemcpy(bigger.p, dst->arena.p, dst->arena_used, hipMemcpyDeviceToDevice));
-      dst->arena.swap(bigger);
-    }
-  }
-  FreqDev d = dev_view(dst);
-  for (int k = 0; k < dst->n_keys; ++k) d.cols[k].type = dst->types[k];
-  hipLaunchKernelGGL(freq_merge_kernel, dim3(grid_for(s->cap)), dim3(256), 0, dst->stream, d,
-                     s->keys.p, s->counts.p, s->exact ? nullptr : s->reps.p, s->arena.p, s->cap,
-                     dst->n_keys);
-  HIP_TRY(hipGetLastError());
-  // special cells
-  unsigned long long add[C_N] = {0, 0, 0, 0, 0, 0};
-  HIP_TRY(hipStreamSynchronize(dst->stream));
   st = pull_counters(dst);
   if (st != DQ_OK) return st;
-  add[C_NULL_ROWS] = dst->h_counters[C_NULL_ROWS] + s->h_counters[C_NULL_ROWS];
-  add[C_NULL_GROUP] = dst->h_counters[C_NULL_GROUP] + s->h_counters[C_NULL_GROUP];
-  add[C_SENTINEL] = dst->h_counters[C_SENTINEL] + s->h_counters[C_SENTINEL];
-  add[C_OCCUPIED] = dst->h_counters[C_OCCUPIED];
-  add[C_COLLISIONS] = dst->h_counters[C_COLLISIONS];
-  add[C_ARENA_OVF] = dst->h_counters[C_ARENA_OVF];
-  HIP_TRY(hipMemcpy(dst->counters.p, add, sizeof(add), hipMemcpyHostToDevice));
-  dst->num_rows += s->num_rows;
-  return pull_counters(dst);
+  if (dst->mode_null_as_group < 0) dst->mode_null_as_group = src->mode_null_as_group;
+  const int64_t nc = src->n_chunks;
+  if (nc) {
+    st = ensure_chunks(dst, nc);
+    if (st != DQ_OK) return st;
+    const size_t region = (size_t)dst->tile * dst->rb;
+    HIP_TRY(hipMemcpyAsync(dst->recs.p + (size_t)dst->n_chunks * region, src->recs.p, nc * region,
+                           hipMemcpyDeviceToDevice, dst->stream));
+    HIP_TRY(hipMemcpyAsync(dst->hist.p + (size_t)dst->n_chunks * kHistRow, src->hist.p,
+                           (size_t)nc * kHistRow * 2, hipMemcpyDeviceToDevice, dst->stream));
+    if (!dst->exact) {
+      HIP_TRY(grow_keep(dst->arena, dst->arena_used, dst->arena_used + src->arena_used + 64,
+                        dst->stream));
+      if (src->arena_used)
+        HIP_TRY(hipMemcpyAsync(dst->arena.p + dst->arena_used, src->arena.p, src->arena_used,
+                               hipMemcpyDeviceToDevice, dst->stream));
+      hipLaunchKernelGGL(freq_rebase, dim3((unsigned)nc), dim3(256), 0, dst->stream,
+                         reinterpret_cast<uint64_t*>(dst->recs.p), dst->hist.p, dst->n_chunks,
+                         dst->tile, (uint64_t)dst->arena_used);
+      HIP_TRY(hipGetLastError());
+      dst->arena_used += src->arena_used;
+    }
+    dst->n_chunks += nc;
+  }
+  for (int k = 0; k < C_N; ++k) dst->h_counters[k] += src->h_counters[k];
+  dst->num_rows += src->num_rows;
+  invalidate(dst);
+  return push_counters(dst);
 }
-
-extern "C" int64_t dq_freq_num_rows(const dq_freq* f) { return f ? f->num_rows : -1; }
 
 // ------------------------------------------------------------------------------------------------
-// Hash repartition for the multi-GPU frequency path (see the kernels above)
+// Multi-GPU repartition (records of materialised groups; see the header)
 // ------------------------------------------------------------------------------------------------
-static PartArgs part_args(const dq_freq* f, int n_parts) {
-  PartArgs a;
-  memset(&a, 0, sizeof(a));
-  for (int k = 0; k < f->n_keys; ++k) a.types[k] = f->types[k];
-  a.n_keys = f->n_keys;
-  a.exact = f->exact ? 1 : 0;
-  a.parts = (uint32_t)n_parts;
-  return a;
-}
-
-// Per-owner record counts and var bytes (device counting pass).
-static dq_status part_sizes(dq_freq* f, int n_parts, std::vector<unsigned long long>& rec,
-                            std::vector<unsigned long long>& var) {
-  DevBuf<unsigned long long> cnt;
-  HIP_TRY(cnt.ensure(2 * kMaxParts));
-  HIP_TRY(hipMemsetAsync(cnt.p, 0, 2 * kMaxParts * 8, f->stream));
-  hipLaunchKernelGGL(freq_part_count_kernel, dim3(grid_for(f->cap)), dim3(256), 0, f->stream,
-                     f->keys.p, f->exact ? nullptr : f->reps.p, f->arena.p, f->cap,
-                     part_args(f, n_parts), cnt.p, cnt.p + kMaxParts);
-  HIP_TRY(hipGetLastError());
-  std::vector<unsigned long long> h(2 * kMaxParts);
-  HIP_TRY(hipStreamSynchronize(f->stream));
-  HIP_TRY(hipMemcpy(h.data(), cnt.p, h.size() * 8, hipMemcpyDeviceToHost));
-  rec.assign(h.begin(), h.begin() + n_parts);
-  var.assign(h.begin() + kMaxParts, h.begin() + kMaxParts + n_parts);
-  return DQ_OK;
-}
-
 extern "C" dq_status dq_freq_partition_sizes(dq_freq* f, int n_parts, int64_t* rec_counts,
                                              int64_t* var_bytes, int64_t* special) {
   if (!f || !rec_counts || !var_bytes || !special)
@@ -1077,16 +1850,16 @@ extern "C" dq_status dq_freq_partition_sizes(dq_freq* f, int n_parts, int64_t* r
   if (n_parts < 1 || n_parts > kMaxParts)
     return fail(DQ_ERR_UNSUPPORTED, "n_parts must be in [1, %d]", kMaxParts);
   HIP_TRY(hipSetDevice(f->device));
-  dq_status st = pull_counters(f);
+  dq_status st = compact_groups(f);
   if (st != DQ_OK) return st;
   std::vector<unsigned long long> rec, var;
-  st = part_sizes(f, n_parts, rec, var);
+  st = owner_sizes(f, f->compact.p, f->n_compact, n_parts, rec, var);
   if (st != DQ_OK) return st;
   for (int i = 0; i < n_parts; ++i) {
     rec_counts[i] = (int64_t)rec[i];
     var_bytes[i] = (int64_t)var[i];
   }
-  special[0] = (int64_t)f->h_counters[C_SENTINEL];
+  special[0] = 0;
   special[1] = (int64_t)f->h_counters[C_NULL_GROUP];
   special[2] = (int64_t)f->h_counters[C_NULL_ROWS];
   return DQ_OK;
@@ -1100,29 +1873,19 @@ extern "C" dq_status dq_freq_partition(dq_freq* f, int n_parts, dq_freq_record* 
   HIP_TRY(hipSetDevice(f->device));
   HIP_TRY(hipStreamSynchronize(f->stream));
   f->stream = reinterpret_cast<hipStream_t>(hip_stream);
-  std::vector<unsigned long long> rec, var_n;
-  dq_status st = part_sizes(f, n_parts, rec, var_n);
+  dq_status st = compact_groups(f);
   if (st != DQ_OK) return st;
-  unsigned long long total_rec = 0, total_var = 0;
-  std::vector<unsigned long long> base(4 * kMaxParts, 0);  // rec_base, var_base, rec_cur, var_cur
+  std::vector<unsigned long long> rec, var_n;
+  st = owner_sizes(f, f->compact.p, f->n_compact, n_parts, rec, var_n);
+  if (st != DQ_OK) return st;
+  unsigned long long tr = 0, tv = 0;
   for (int i = 0; i < n_parts; ++i) {
-    base[i] = total_rec;
-    base[kMaxParts + i] = total_var;
-    total_rec += rec[i];
-    total_var += var_n[i];
+    tr += rec[i];
+    tv += var_n[i];
   }
-  if (total_rec == 0) return DQ_OK;
-  if (!records || (total_var && !var)) return fail(DQ_ERR_INVALID_ARGUMENT, "null output buffer");
-  DevBuf<unsigned long long> dbase;
-  HIP_TRY(dbase.ensure(base.size()));
-  HIP_TRY(hipMemcpyAsync(dbase.p, base.data(), base.size() * 8, hipMemcpyHostToDevice, f->stream));
-  hipLaunchKernelGGL(freq_part_scatter_kernel, dim3(grid_for(f->cap)), dim3(256), 0, f->stream,
-                     f->keys.p, f->counts.p, f->exact ? nullptr : f->reps.p, f->arena.p, f->cap,
-                     part_args(f, n_parts), dbase.p, dbase.p + kMaxParts, dbase.p + 2 * kMaxParts,
-                     dbase.p + 3 * kMaxParts, reinterpret_cast<FreqRecord*>(records), var);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(f->stream));  // dbase is freed on return
-  return DQ_OK;
+  if (tr && (!records || (tv && !var))) return fail(DQ_ERR_INVALID_ARGUMENT, "null output buffer");
+  return owner_scatter(f, f->compact.p, f->n_compact, n_parts, reinterpret_cast<RecIn*>(records),
+                       var, rec, var_n);
 }
 
 extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record* records,
@@ -1135,78 +1898,60 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
     return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   if (n_src < 1 || n_src > kMaxParts)
     return fail(DQ_ERR_UNSUPPORTED, "n_src must be in [1, %d]", kMaxParts);
-  int mode = null_as_group ? 1 : 0;
+  const int mode = null_as_group ? 1 : 0;
   if (f->mode_null_as_group >= 0 && f->mode_null_as_group != mode)
     return fail(DQ_ERR_STATE, "null_as_group must be the same for every batch");
   f->mode_null_as_group = mode;
   HIP_TRY(hipSetDevice(f->device));
   HIP_TRY(hipStreamSynchronize(f->stream));
   f->stream = reinterpret_cast<hipStream_t>(hip_stream);
-  SrcSegs segs;
-  memset(&segs, 0, sizeof(segs));
-  segs.n_src = n_src;
+  AArgs a = base_args(f);
   int64_t total_rec = 0, total_var = 0;
+  a.segs.n_src = n_src;
   for (int j = 0; j < n_src; ++j) {
     if (src_records[j] < 0 || src_var_bytes[j] < 0 || (src_var_bytes[j] & 7))
       return fail(DQ_ERR_INVALID_ARGUMENT, "bad segment sizes for source %d", j);
-    segs.rec_start[j] = total_rec;
-    segs.var_base[j] = total_var;
+    a.segs.rec_start[j] = total_rec;
+    a.segs.var_base[j] = total_var;
     total_rec += src_records[j];
     total_var += src_var_bytes[j];
   }
-  segs.rec_start[n_src] = total_rec;
+  a.segs.rec_start[n_src] = total_rec;
   if (total_rec && !records) return fail(DQ_ERR_INVALID_ARGUMENT, "null records");
   if (!f->exact && total_var && !var) return fail(DQ_ERR_INVALID_ARGUMENT, "null var bytes");
   dq_status st = pull_counters(f);
   if (st != DQ_OK) return st;
-  uint64_t need = 2 * (f->h_counters[C_OCCUPIED] + (uint64_t)total_rec) + 2;
-  if (need > f->cap) {
-    uint64_t cap = f->cap;
-    while (cap < need) cap <<= 1;
-    st = rehash(f, cap);
-    if (st != DQ_OK) return st;
-  }
-  if (!f->exact) {
-    uint64_t want = f->arena_used + (uint64_t)total_var + 64;
-    if (want > f->arena.n) {
-      DevBuf<uint8_t> bigger;
-      HIP_TRY(bigger.ensure(std::max<uint64_t>(want, f->arena.n * 2)));
-      if (f->arena_used)
-        HIP_TRY(hipMemcpyAsync(bigger.p, f->arena.p, f->arena_used, hipMemcpyDeviceToDevice, f->stream));
-      HIP_TRY(hipStreamSynchronize(f->stream));
-      f->arena.swap(bigger);
-    }
-  }
-  FreqDev d = dev_view(f);
-  for (int k = 0; k < f->n_keys; ++k) d.cols[k].type = f->types[k];
-  const PartArgs a = part_args(f, n_src);
-  const auto* rec = reinterpret_cast<const FreqRecord*>(records);
+  invalidate(f);
   if (total_rec) {
-    unsigned grid = grid_for((uint64_t)total_rec);
-    hipLaunchKernelGGL(freq_insert_records_kernel, dim3(grid), dim3(256), 0, f->stream, d, rec, var,
-                       segs, a);
-    HIP_TRY(hipGetLastError());
+    const int64_t per = f->tile / 32;  // a record's count becomes at most 32 records
+    const int64_t chunks = (total_rec + per - 1) / per;
+    st = ensure_chunks(f, chunks);
+    if (st != DQ_OK) return st;
+    a = [&] {
+      AArgs b = base_args(f);
+      b.segs = a.segs;
+      return b;
+    }();
     if (!f->exact) {
-      hipLaunchKernelGGL(freq_verify_records_kernel, dim3(grid), dim3(256), 0, f->stream, d, rec,
-                         var, segs, a);
-      HIP_TRY(hipGetLastError());
+      const uint64_t base = (f->arena_used + 7) & ~7ULL;
+      HIP_TRY(grow_keep(f->arena, f->arena_used, base + total_var + 64, f->stream));
+      if (total_var)
+        HIP_TRY(hipMemcpyAsync(f->arena.p + base, var, total_var, hipMemcpyDeviceToDevice, f->stream));
+      a.arena = f->arena.p;
+      a.var_arena_base = base;
+      f->arena_used = base + total_var;
     }
+    a.rin = reinterpret_cast<const RecIn*>(records);
+    a.n_items = total_rec;
+    a.tile_items = per;
+    if (f->exact) launch_phaseA<false>(f, a, chunks, true);
+    else launch_phaseA<true>(f, a, chunks, true);
+    HIP_TRY(hipGetLastError());
+    f->n_chunks += chunks;
   }
-  st = pull_counters(f);
-  if (st != DQ_OK) return st;
-  unsigned long long c[C_N];
-  for (int k = 0; k < C_N; ++k) c[k] = f->h_counters[k];
-  c[C_SENTINEL] += (unsigned long long)special[0];
-  c[C_NULL_GROUP] += (unsigned long long)special[1];
-  c[C_NULL_ROWS] += (unsigned long long)special[2];
-  HIP_TRY(hipMemcpy(f->counters.p, c, sizeof(c), hipMemcpyHostToDevice));
+  f->h_counters[C_NULL_GROUP] += (uint64_t)special[1];
+  f->h_counters[C_NULL_ROWS] += (uint64_t)special[2];
+  if (special[0]) return fail(DQ_ERR_INVALID_ARGUMENT, "special[0] is no longer used (must be 0)");
   f->num_rows += num_rows;
-  st = pull_counters(f);
-  if (st != DQ_OK) return st;
-  if (f->h_counters[C_ARENA_OVF]) return fail(DQ_ERR_OUT_OF_MEMORY, "frequency table arena overflow");
-  if (f->h_counters[C_COLLISIONS])
-    return fail(DQ_ERR_UNSUPPORTED,
-                "64-bit key-hash collision between distinct groups detected (%llu groups)",
-                (unsigned long long)f->h_counters[C_COLLISIONS]);
-  return DQ_OK;
+  return push_counters(f);
 }

@@ -1,0 +1,319 @@
+// freq_codec.h -- group-key codec of the hash group-by (freq.hip), host + device.
+//
+// Everything here is DQ_HD so that the exact code the kernels run can be exercised on the CPU
+// (tests/test_freq_codec.py builds tools/freq_codec_check.cpp against this header under ASan).
+//
+// Two key modes (FrequencyBasedAnalyzer.computeFrequencies, GroupingAnalyzers.scala:53-80):
+//   * exact  -- one fixed-width key column: the group is the value widened to 64 bits and its
+//               64-bit hash h = fmix_bij(value) is a BIJECTION (murmur3's fmix64), so h alone is
+//               the group and the value is recovered with fmix_inv;
+//   * hashed -- strings and multi-column keys: h = a 64-bit hash of the composite key, and the
+//               group is the encoded key (below), which is compared byte for byte whenever two
+//               rows or records meet on the same h (a hash collision never merges groups).
+// Encoded key: per key column a u32 tag (0 = NULL, 1 = value) and then either 8 little-endian
+// bytes (the value widened to 64 bits) or, for utf8, a u32 byte length and the bytes zero-padded
+// to a multiple of 4.  Histogram (null_as_group, one utf8 key) reads a NULL as the string
+// "NullValue", exactly as the reference's na.fill (Histogram.scala:59-66), so a real "NullValue"
+// string and NULL are one group there as well.
+#pragma once
+
+#include <stdint.h>
+
+#include "engine.h"
+
+namespace dq {
+
+constexpr int kMaxKeys = 8;
+
+struct KeyCol {
+  int32_t type;
+  int32_t pad;
+  const uint8_t* valid;
+  const void* values;
+  const uint8_t* data;
+};
+
+struct KeySet {
+  KeyCol cols[kMaxKeys];
+  int32_t n_keys;
+  int32_t null_as_group;
+};
+
+DQ_HD uint32_t kbit(const uint8_t* bm, int64_t r) {
+  return bm ? ((bm[r >> 3] >> (r & 7)) & 1u) : 1u;
+}
+
+DQ_HD uint64_t kwiden(int type, const void* v, int64_t r) {
+  switch (type) {
+    case DQ_INT8: return (uint64_t)(int64_t) reinterpret_cast<const int8_t*>(v)[r];
+    case DQ_INT16: return (uint64_t)(int64_t) reinterpret_cast<const int16_t*>(v)[r];
+    case DQ_INT32: return (uint64_t)(int64_t) reinterpret_cast<const int32_t*>(v)[r];
+    case DQ_INT64: return (uint64_t) reinterpret_cast<const int64_t*>(v)[r];
+    case DQ_FLOAT32: {
+      uint32_t b;
+      __builtin_memcpy(&b, reinterpret_cast<const float*>(v) + r, 4);
+      return b;
+    }
+    case DQ_FLOAT64: {
+      uint64_t b;
+      __builtin_memcpy(&b, reinterpret_cast<const double*>(v) + r, 8);
+      return b;
+    }
+    case DQ_BOOL: return kbit(reinterpret_cast<const uint8_t*>(v), r);
+    default: return 0;
+  }
+}
+
+// murmur3 fmix64: xor-shifts by >= 32 and odd multiplies, each invertible, so the map is a
+// bijection of uint64; fmix_inv undoes it (the multipliers' inverses mod 2^64).
+constexpr uint64_t kFmixC1 = 0xff51afd7ed558ccdULL, kFmixC1Inv = 0x4f74430c22a54005ULL;
+constexpr uint64_t kFmixC2 = 0xc4ceb9fe1a85ec53ULL, kFmixC2Inv = 0x9cb4b2f8129337dbULL;
+DQ_HD uint64_t fmix_bij(uint64_t k) {
+  k ^= k >> 33;
+  k *= kFmixC1;
+  k ^= k >> 33;
+  k *= kFmixC2;
+  k ^= k >> 33;
+  return k;
+}
+DQ_HD uint64_t fmix_inv(uint64_t k) {
+  k ^= k >> 33;
+  k *= kFmixC2Inv;
+  k ^= k >> 33;
+  k *= kFmixC1Inv;
+  k ^= k >> 33;
+  return k;
+}
+
+// Byte reader for xxh_bytes valid on host and device (unaligned loads within the string).
+struct MemBytes {
+  const uint8_t* p;
+  DQ_HD uint64_t u64(int64_t o) const {
+    uint64_t v;
+    __builtin_memcpy(&v, p + o, 8);
+    return v;
+  }
+  DQ_HD uint32_t u32(int64_t o) const {
+    uint32_t v;
+    __builtin_memcpy(&v, p + o, 4);
+    return v;
+  }
+  DQ_HD uint32_t u8(int64_t o) const { return p[o]; }
+};
+
+// "NullValue" (Histogram.NullFieldReplacement, Histogram.scala:108) as constants: a string view
+// with p == nullptr IS this literal, so no code path needs memory for it.
+constexpr int32_t kNullValueLen = 9;
+constexpr uint64_t kNullValueLo = 0x756c61566c6c754eULL;  // "NullValu", little-endian
+constexpr uint32_t kNullValueHi = 0x65u;                   // "e"
+constexpr uint64_t kNullValueXxh17 = 0xf45f7c0db790929eULL; // XXH64("NullValue", seed 17)
+
+struct SView {
+  const uint8_t* p;  // nullptr: the "NullValue" literal
+  int32_t len;
+};
+DQ_HD uint32_t sv_byte(const SView& v, int32_t q) {
+  if (v.p) return v.p[q];
+  return q < 8 ? (uint32_t)(kNullValueLo >> (8 * q)) & 0xffu : (q == 8 ? kNullValueHi : 0u);
+}
+
+enum RowKind : int32_t { ROW_SKIP = 0, ROW_KEY = 1, ROW_NULL_GROUP = 2 };
+
+// utf8 key column k at row r; a NULL in Histogram mode is the "NullValue" literal.
+DQ_HD bool key_str(const KeySet& ks, int k, int64_t r, SView& v) {
+  const KeyCol& c = ks.cols[k];
+  if (!kbit(c.valid, r)) {
+    if (!ks.null_as_group) return false;
+    v.p = nullptr;
+    v.len = kNullValueLen;
+    return true;
+  }
+  const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
+  const int32_t s = off[r];
+  v.p = c.data + s;
+  v.len = off[r + 1] - s;
+  return true;
+}
+
+// What row r contributes: a keyed row, a row of the exact-mode NULL group (Histogram on a
+// fixed-width column), or nothing (a NULL key in a grouping: GroupingAnalyzers.scala:62-65).
+DQ_HD int row_kind(const KeySet& ks, int64_t r, bool exact) {
+  if (exact) {
+    if (kbit(ks.cols[0].valid, r)) return ROW_KEY;
+    return ks.null_as_group ? ROW_NULL_GROUP : ROW_SKIP;
+  }
+  for (int k = 0; k < ks.n_keys; ++k) {
+    const KeyCol& c = ks.cols[k];
+    if (!kbit(c.valid, r)) {
+      if (!(ks.null_as_group && c.type == DQ_UTF8)) return ROW_SKIP;
+    }
+  }
+  return ROW_KEY;
+}
+
+// Histogram groups cast(col as string) (Histogram.scala:63): every NaN prints as "NaN", so in
+// Histogram mode NaN payloads fold into the canonical NaN (a grouping keeps Spark 2.2's binary
+// key equality).
+DQ_HD uint64_t exact_key(const KeySet& ks, int64_t r) {
+  const KeyCol& c = ks.cols[0];
+  uint64_t v = kwiden(c.type, c.values, r);
+  if (ks.null_as_group) {
+    if (c.type == DQ_FLOAT64 && (v & 0x7fffffffffffffffULL) > 0x7ff0000000000000ULL)
+      v = 0x7ff8000000000000ULL;
+    if (c.type == DQ_FLOAT32 && (v & 0x7fffffffULL) > 0x7f800000ULL) v = 0x7fc00000ULL;
+  }
+  return v;
+}
+DQ_HD uint64_t row_hash_exact(const KeySet& ks, int64_t r) { return fmix_bij(exact_key(ks, r)); }
+
+// Composite 64-bit hash of a keyed row (hashed mode): per column XXH64 with a per-column seed,
+// folded with an XXH64 merge step, then fmix.
+DQ_HD uint64_t row_hash_hashed(const KeySet& ks, int64_t r) {
+  uint64_t h = 0x243F6A8885A308D3ULL;
+  for (int k = 0; k < ks.n_keys; ++k) {
+    const KeyCol& c = ks.cols[k];
+    uint64_t ch;
+    if (c.type == DQ_UTF8) {
+      SView v;
+      key_str(ks, k, r, v);
+      ch = v.p ? xxh_bytes(MemBytes{v.p}, (int64_t)v.len, 17 + k) : kNullValueXxh17;
+    } else {
+      ch = xxh_long(kwiden(c.type, c.values, r), 17 + k);
+    }
+    h = rotl64(h ^ ch, 27) * P1 + P4;
+  }
+  return fmix_bij(h);
+}
+
+DQ_HD uint32_t pad4(uint32_t n) { return (n + 3u) & ~3u; }
+
+DQ_HD uint32_t row_enc_size(const KeySet& ks, int64_t r) {
+  uint32_t n = 0;
+  for (int k = 0; k < ks.n_keys; ++k) {
+    const KeyCol& c = ks.cols[k];
+    n += 4;
+    if (c.type == DQ_UTF8) {
+      SView v;
+      if (key_str(ks, k, r, v)) n += 4 + pad4((uint32_t)v.len);
+    } else if (kbit(c.valid, r)) {
+      n += 8;
+    }
+  }
+  return n;
+}
+
+// Writes the encoded key of row r at dst (4-byte aligned, row_enc_size(ks, r) bytes).
+DQ_HD void row_encode(const KeySet& ks, int64_t r, uint32_t* dst) {
+  for (int k = 0; k < ks.n_keys; ++k) {
+    const KeyCol& c = ks.cols[k];
+    if (c.type == DQ_UTF8) {
+      SView v;
+      if (!key_str(ks, k, r, v)) {
+        *dst++ = 0;
+        continue;
+      }
+      *dst++ = 1;
+      *dst++ = (uint32_t)v.len;
+      for (int32_t q = 0; q < v.len; q += 4) {
+        uint32_t w = 0;
+        for (int b = 0; b < 4 && q + b < v.len; ++b) w |= sv_byte(v, q + b) << (8 * b);
+        *dst++ = w;
+      }
+    } else if (!kbit(c.valid, r)) {
+      *dst++ = 0;
+    } else {
+      const uint64_t v = kwiden(c.type, c.values, r);
+      *dst++ = 1;
+      *dst++ = (uint32_t)v;
+      *dst++ = (uint32_t)(v >> 32);
+    }
+  }
+}
+
+// Are two keyed rows (of the same batch) the same group?
+DQ_HD bool rows_equal(const KeySet& ks, int64_t r1, int64_t r2) {
+  for (int k = 0; k < ks.n_keys; ++k) {
+    const KeyCol& c = ks.cols[k];
+    if (c.type == DQ_UTF8) {
+      SView a, b;
+      const bool v1 = key_str(ks, k, r1, a), v2 = key_str(ks, k, r2, b);
+      if (v1 != v2) return false;
+      if (!v1) continue;
+      if (a.len != b.len) return false;
+      if (a.p && b.p) {
+        for (int32_t q = 0; q < a.len; ++q)
+          if (a.p[q] != b.p[q]) return false;
+      } else {
+        for (int32_t q = 0; q < a.len; ++q)
+          if (sv_byte(a, q) != sv_byte(b, q)) return false;
+      }
+    } else {
+      const uint32_t v1 = kbit(c.valid, r1), v2 = kbit(c.valid, r2);
+      if (v1 != v2) return false;
+      if (v1 && kwiden(c.type, c.values, r1) != kwiden(c.type, c.values, r2)) return false;
+    }
+  }
+  return true;
+}
+
+// Size in bytes of an encoded key.
+DQ_HD uint32_t enc_size(const uint32_t* enc, const int32_t* types, int n_keys) {
+  uint32_t w = 0;
+  for (int k = 0; k < n_keys; ++k) {
+    const uint32_t tag = enc[w++];
+    if (!tag) continue;
+    if (types[k] == DQ_UTF8) w += 1 + pad4(enc[w]) / 4;
+    else w += 2;
+  }
+  return 4 * w;
+}
+
+DQ_HD bool enc_equal(const uint32_t* a, const uint32_t* b, const int32_t* types, int n_keys) {
+  const uint32_t n = enc_size(a, types, n_keys);
+  if (enc_size(b, types, n_keys) != n) return false;
+  for (uint32_t q = 0; q < n / 4; ++q)
+    if (a[q] != b[q]) return false;
+  return true;
+}
+
+// Hash of an encoded key: the same value row_hash_hashed gives for the row it encodes.
+DQ_HD uint64_t enc_hash(const uint32_t* enc, const int32_t* types, int n_keys) {
+  uint64_t h = 0x243F6A8885A308D3ULL;
+  uint32_t w = 0;
+  for (int k = 0; k < n_keys; ++k) {
+    const uint32_t tag = enc[w++];
+    uint64_t ch;
+    if (types[k] == DQ_UTF8) {
+      const uint32_t len = tag ? enc[w++] : 0;
+      ch = xxh_bytes(MemBytes{reinterpret_cast<const uint8_t*>(enc + w)}, (int64_t)len, 17 + k);
+      w += pad4(len) / 4;
+    } else {
+      uint64_t v = 0;
+      if (tag) {
+        v = (uint64_t)enc[w] | ((uint64_t)enc[w + 1] << 32);
+        w += 2;
+      }
+      ch = xxh_long(v, 17 + k);
+    }
+    h = rotl64(h ^ ch, 27) * P1 + P4;
+  }
+  return fmix_bij(h);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Records: how the group-by carries (group, count) pairs between its passes.
+//   exact  record (8 B):  (h << 8) | code        -- the top 8 bits of h are implied by the bucket
+//   hashed record (16 B): {h, (rep << 8) | code} -- rep = arena offset of the encoded key
+// `code` carries a count as one base-4 digit: count = (code & 3) << 2 * (code >> 2); a count c
+// travels as one record per non-zero base-4 digit of c (at most 32), and every pass SUMS counts.
+// ------------------------------------------------------------------------------------------------
+DQ_HD uint64_t code_count(uint32_t code) {
+  return (uint64_t)(code & 3u) << (2u * (code >> 2));
+}
+DQ_HD int count_digits(uint64_t c) {
+  int n = 0;
+  for (; c; c >>= 2) n += (c & 3) != 0;
+  return n;
+}
+
+}  // namespace dq

@@ -304,9 +304,18 @@ int64_t dq_freq_num_rows(const dq_freq* freq);
 dq_status dq_freq_export(dq_freq* freq, int64_t* counts_out, int64_t* key_offsets_out,
                          uint8_t* key_bytes_out, int64_t capacity, int64_t key_bytes_capacity,
                          int64_t* key_bytes_needed);
+/* The k groups with the largest counts, in descending count order (ties in any order), in the
+ * export format: Histogram's details, rdd.top(maxDetailBins)(OrderByAbsoluteCount)
+ * (Histogram.scala:78-79; numberOfBins is dq_freq_num_groups).  Only these k keys leave the
+ * device.  Call with key_bytes_out = NULL for *n_out and *key_bytes_needed; counts_out[k] and
+ * key_offsets_out[k + 1] must hold k entries. */
+dq_status dq_freq_topk(dq_freq* freq, int k, int64_t* counts_out, int64_t* key_offsets_out,
+                       uint8_t* key_bytes_out, int64_t key_bytes_capacity, int64_t* n_out,
+                       int64_t* key_bytes_needed);
 /* dst += src: the null-safe full-outer-join merge of two frequency states
  * (FrequenciesAndNumRows.sum, GroupingAnalyzers.scala:128-148): counts of equal keys add and
- * numRows add. */
+ * numRows add.  Keys are compared as encoded keys, so a 64-bit hash collision between the two
+ * tables' groups never merges them. */
 dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src);
 
 /* ------------------------------------------------------------------------------------------------
@@ -319,16 +328,17 @@ dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src);
  * the segments with an all-to-all (RCCL over xGMI) and each owner re-inserts what it received with
  * dq_freq_add_records_device, which adds counts of equal keys exactly like FrequenciesAndNumRows.sum
  * (GroupingAnalyzers.scala:128-148).  Records are device memory; var holds the encoded keys of
- * hashed-mode tables (string / multi-column / NULL-group keys), 8-byte aligned per group.
+ * hashed-mode tables (string / multi-column keys), 8-byte aligned per group.
  * ---------------------------------------------------------------------------------------------- */
 typedef struct dq_freq_record {
-  uint64_t key;     /* exact mode: the widened key value; hashed mode: the 64-bit group hash      */
+  uint64_t key;     /* exact mode (one fixed-width key): the widened key value; hashed mode
+                       (strings / several keys / Histogram on strings): the 64-bit group hash      */
   uint64_t count;   /* rows in the group                                                          */
   uint64_t enc_off; /* hashed mode: byte offset of the encoded key within the segment's var bytes */
 } dq_freq_record;
-/* Per owner: rec_counts[n_parts] records and var_bytes[n_parts] bytes.  special[3] = the groups
- * kept outside the slot table, which the caller routes to ONE owner: {count of the key equal to
- * INT64_MIN in exact mode, count of the NULL group (Histogram), rows skipped for a NULL key}. */
+/* Per owner: rec_counts[n_parts] records and var_bytes[n_parts] bytes.  special[3] = the counts
+ * kept outside the records, which the caller routes to ONE owner: {0 (unused), rows of the
+ * fixed-width NULL group (Histogram), rows skipped for a NULL key}. */
 dq_status dq_freq_partition_sizes(dq_freq* freq, int n_parts, int64_t* rec_counts,
                                   int64_t* var_bytes, int64_t* special);
 /* Writes the owner segments back to back (segment j at the exclusive prefix sums of the sizes
@@ -336,8 +346,9 @@ dq_status dq_freq_partition_sizes(dq_freq* freq, int n_parts, int64_t* rec_count
 dq_status dq_freq_partition(dq_freq* freq, int n_parts, dq_freq_record* records, uint8_t* var,
                             void* hip_stream);
 /* Inserts n_src received segments laid back to back (src_records[j] records, src_var_bytes[j]
- * var bytes each), adds num_rows to the table's numRows and special[3] to its outside-table groups.
- * A 64-bit hash collision between distinct groups is detected (DQ_ERR_UNSUPPORTED), never merged. */
+ * var bytes each), adds num_rows to the table's numRows and special[3] to its outside-record
+ * counts.  Groups with equal keys add their counts; equal hashes with different encoded keys stay
+ * separate groups. */
 dq_status dq_freq_add_records_device(dq_freq* freq, const dq_freq_record* records,
                                      const uint8_t* var, int n_src, const int64_t* src_records,
                                      const int64_t* src_var_bytes, int64_t num_rows,

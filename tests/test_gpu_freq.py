@@ -53,15 +53,15 @@ def test_frequency_family_matches_oracle(n, batch, gpu_device):
     t = _table(n, seed=n + 1)
     df = Table.from_arrow(t, device=gpu_device, max_batch_rows=batch)
     ot = _otable(t)
-    cases = [("id",), ("s",), ("u",), ("s", "u")]
-    analyzers = [Uniqueness(("id", "s"))]
+    # ("id", "s") mixes a fixed-width and a string key: AnalyzerTests.scala:87-94 pins
+    # Uniqueness(Seq("unique", "nonUnique")) over such keys
+    cases = [("id",), ("s",), ("u",), ("s", "u"), ("id", "s"), ("u", "id", "s")]
+    analyzers = []
     for cols in cases:
         analyzers += [Uniqueness(cols), Distinctness(cols), UniqueValueRatio(cols),
                       CountDistinct(cols)]
     analyzers += [Entropy("id"), Entropy("s")]
     ctx = AnalysisRunner.do_analysis_run(df, analyzers)
-    # multi-column keys with a fixed-width column are not implemented: a loud failure metric
-    assert ctx.metric(Uniqueness(("id", "s"))).value.is_failure
     for cols in cases:
         freq = O.frequencies(ot, list(cols))
         exp = {Uniqueness(cols): O.uniqueness(freq, n), Distinctness(cols): O.distinctness(freq, n),
@@ -123,7 +123,7 @@ def _repartition(t, cols, parts, device, null_as_group=False):
 
 
 @pytest.mark.parametrize("parts", [1, 2, 3, 8])
-@pytest.mark.parametrize("cols", [("id",), ("s",), ("u",), ("s", "u")])
+@pytest.mark.parametrize("cols", [("id",), ("s",), ("u",), ("s", "u"), ("id", "s")])
 def test_repartition_matches_single_table(parts, cols, gpu_device):
     from oracle import deequ_oracle as O
     n = 30_000
@@ -155,6 +155,8 @@ def test_repartition_histogram_null_group(col, gpu_device):
     vals = t.column(col).to_pylist()
     exp = {}
     for v in vals:
+        if v is None and col == "s":   # na.fill("NullValue"): one group with the real string
+            v = "NullValue"
         exp[(v,)] = exp.get((v,), 0) + 1
     owners = _repartition(t, [col], 4, gpu_device, null_as_group=True)
     got = {}
@@ -182,3 +184,73 @@ def test_reset_table_equals_fresh_table(cols, gpu_device):
         ft.add([b[c] for c in cols])
     assert ft.num_rows == 7_000
     assert dict(ft.export()) == O.frequencies(_otable(t2), list(cols))
+
+
+def _freq_table(t, cols, device, null_as_group=False):
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    df = Table.from_arrow(t, device=device, max_batch_rows=7_000)
+    ft = FrequencyTable(list(cols), [df.schema[c].dtype for c in cols], 0)
+    for b in df.batches:
+        ft.add([b[c] for c in cols], null_as_group=null_as_group)
+    return ft
+
+
+@pytest.mark.parametrize("cols", [("id",), ("s",), ("u",), ("s", "u"), ("id", "s")])
+def test_merged_tables_equal_whole_table(cols, gpu_device):
+    """FrequenciesAndNumRows.sum (GroupingAnalyzers.scala:128-148) on the device: random row
+    splits, one table per part, merged with dq_freq_merge == the whole table (counts, numRows)."""
+    from oracle import deequ_oracle as O
+    n = 25_000
+    t = _table(n, seed=41 + len(cols))
+    rng = np.random.default_rng(len(cols))
+    cuts = sorted(rng.choice(np.arange(1, n), 3, replace=False).tolist())
+    bounds = [0] + cuts + [n]
+    parts = [_freq_table(t.slice(bounds[i], bounds[i + 1] - bounds[i]), cols, gpu_device)
+             for i in range(len(bounds) - 1)]
+    merged = parts[0]
+    for p in parts[1:]:
+        merged = merged.merged(p)
+    assert merged.num_rows == n
+    freq = O.frequencies(_otable(t), list(cols))
+    assert dict(merged.export()) == freq
+    s = merged.summarize()
+    assert s.n_groups == len(freq) and s.n_unique == sum(1 for c in freq.values() if c == 1)
+    assert _rel_close(s.entropy, O.entropy(freq, n))
+
+
+def test_merge_keeps_hash_collisions_apart_and_handles_histogram_nulls(gpu_device):
+    """Histogram tables (NULL group) merge; a string table merged with itself doubles counts."""
+    t = _table(12_000, seed=5, null_rate=0.2)
+    for col in ("id", "s"):
+        a = _freq_table(t, [col], gpu_device, null_as_group=True)
+        b = _freq_table(t, [col], gpu_device, null_as_group=True)
+        got = dict(a.merged(b).export())
+        exp = {}
+        for v in t.column(col).to_pylist():
+            if v is None and col == "s":
+                v = "NullValue"
+            exp[(v,)] = exp.get((v,), 0) + 2
+        assert got == exp, col
+
+
+@pytest.mark.parametrize("n,k", [(1, 10), (5000, 3), (40_000, 1000), (200_000, 1000)])
+@pytest.mark.parametrize("col", ["id", "s", "u"])
+def test_topk_matches_oracle_order(n, k, col, gpu_device):
+    """dq_freq_topk == rdd.top(k)(OrderByAbsoluteCount) up to ties: the multiset of returned counts
+    is the oracle's k largest, and every returned key carries its exact count."""
+    from oracle import deequ_oracle as O
+    t = _table(n, seed=n + 3)
+    ft = _freq_table(t, [col], gpu_device, null_as_group=True)
+    got = ft.topk(k)
+    vals = t.column(col).to_pylist()
+    exp = {}
+    for v in vals:
+        if v is None and col != "id":
+            v = "NullValue"
+        exp[v] = exp.get(v, 0) + 1
+    want = sorted(exp.values(), reverse=True)[:k]
+    assert [c for _, c in got] == want
+    for (key,), c in got:
+        assert exp[key] == c
+    assert ft.count() == len(exp)

@@ -2,12 +2,12 @@
 """Single-GPU measurements of BASELINE.json configs[2] and configs[3] (the default bench.py line is
 configs[1], S10).  Not part of the driver's bench contract; the JSON lines land in profiles/.
 
-  c3: Uniqueness + Distinctness + Entropy + Histogram-style grouping on the high-cardinality int64
-      `id` (exact-mode hash group-by, ~N groups) and the 3-value string `priority` (hashed mode,
-      LDS-resident groups).  One step = both group-bys over the table resident in HBM + the one
-      aggregation over each frequency table (dq_freq_summarize).
-      B_alg = key bytes read once (SURVEY §8(d)): id validity + values (8.125 B/row);
-      priority validity + offsets + bytes.  Hash-table traffic excluded.
+  c3: Uniqueness + Distinctness + Entropy + Histogram on the high-cardinality int64 `id` (exact
+      mode, ~N groups) and the 3-value string `priority` (hashed mode).  One step = the two
+      groupings (+ the one aggregation over each frequency table, dq_freq_summarize) and the two
+      Histogram group-bys (+ dq_freq_topk(1000) and the bin count), over the table resident in HBM.
+      B_alg = key bytes read once per group-by (SURVEY §8(d)): id validity + values (8.125 B/row);
+      priority validity + offsets + bytes; x2 (grouping + histogram).  Partition traffic excluded.
   c4: ApproxCountDistinct(id) (HLL++, P = 9) + Correlation(id, score) on an Item table with an
       fp64 `score` column.  One step = the fused scan (HLL launch + co-moment launch + finalize).
       B_alg = id validity + values + score validity + values = 16.25 B/row.
@@ -50,27 +50,38 @@ def main():
         from deequ_amd.analyzers.grouping import FrequencyTable
 
         # one table per grouping, created once with its capacity and reset every step (the
-        # aggregation buffer is reused; the step still clears it, inserts every row, summarizes)
-        tables = {"id": FrequencyTable(["id"], [N.INT64], 0, capacity_hint=rows),
-                  "priority": FrequencyTable(["priority"], [N.UTF8], 0)}
+        # aggregation buffer is reused; the step still clears it, inserts every row, summarizes).
+        # Uniqueness/Distinctness/Entropy share one grouping per column (AnalysisRunner.scala:
+        # 165-180); Histogram runs its own group-by with NULL as a group (Histogram.scala:54-69)
+        # and takes the device top-1000 + the bin count.
+        tables = {("id", False): FrequencyTable(["id"], [N.INT64], 0, capacity_hint=rows),
+                  ("priority", False): FrequencyTable(["priority"], [N.UTF8], 0),
+                  ("id", True): FrequencyTable(["id"], [N.INT64], 0, capacity_hint=rows),
+                  ("priority", True): FrequencyTable(["priority"], [N.UTF8], 0)}
 
         def step():
             out = {}
-            for col, ft in tables.items():
+            for (col, hist), ft in tables.items():
                 ft.reset()
                 for b in table.batches:
-                    ft.add([b[col]])
-                s = ft.summarize()
-                out[col] = (s.n_groups, s.n_unique, s.entropy)
+                    ft.add([b[col]], null_as_group=hist)
+                if hist:
+                    top = ft.topk(1000)
+                    out["Histogram(" + col + ")"] = (ft.count(), len(top), top[0][1])
+                else:
+                    s = ft.summarize()
+                    out[col] = (s.n_groups, s.n_unique, s.entropy)
             return out
         b_alg = 0
         for b in table.batches:
             m = b["id"].length
-            b_alg += nb(m) + 8 * m + nb(m) + 4 * (m + 1) + int(b["priority"].values[m].item())
-        kernel = "dq::freq_insert_kernel (+ freq_verify_kernel for priority, freq_summary_kernel)"
-        desc = ("Uniqueness/Distinctness/Entropy grouping on int64 id (~N groups, exact mode) and "
-                "string priority (3 groups, hashed mode) over a synthetic Item table, 5% nulls "
-                "(BASELINE.json configs[2], 1 GPU)")
+            # each group-by reads its key column once: 2 groupings + 2 histograms
+            b_alg += 2 * (nb(m) + 8 * m + nb(m) + 4 * (m + 1) + int(b["priority"].values[m].item()))
+        kernel = ("dq::freq_phaseA (per batch) + freq_phaseB + freq_phaseC (per table): "
+                  "radix-partitioned group-by")
+        desc = ("Uniqueness/Distinctness/Entropy grouping + Histogram (top-1000 + bins) on int64 id "
+                "(~N groups, exact mode) and string priority (3 groups, hashed mode) over a "
+                "synthetic Item table, 5% nulls (BASELINE.json configs[2], 1 GPU)")
         metric_unit = "rows/s"
     else:
         from deequ_amd import _native as N
