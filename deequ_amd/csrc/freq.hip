@@ -34,6 +34,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -50,14 +52,15 @@ constexpr int kBucketBits = 9;
 constexpr int kBuckets = 1 << kBucketBits;
 constexpr int kHistRow = kBuckets + 1;  // u16 exclusive bucket prefix of a chunk + its total
 constexpr int kThreads = 1024;
-constexpr int kMaxSubBits = 9;
+constexpr int kMaxSubBits = 10;
 constexpr int kFilterShift = 32;        // hash bits that split an overflowing partition
 constexpr int kCand = 4;                // top groups kept per partition for Histogram
+constexpr int kSmallCounts = 64;        // phase C histograms group counts below this
 constexpr int kMaxParts = 64;
 constexpr uint64_t kEmptyKey = ~0ULL;
 constexpr uint64_t kNotReady = ~0ULL;
 
-enum Counter { C_NULL_ROWS = 0, C_NULL_GROUP, C_COLLISIONS, C_N };
+enum Counter { C_NULL_ROWS = 0, C_NULL_GROUP, C_COLLISIONS, C_DBG_NOTREADY, C_DBG_DIFF, C_DBG_FULL, C_DBG_BYPASS, C_N };
 
 template <bool HASHED>
 struct FM;
@@ -66,25 +69,19 @@ struct FM<false> {
   static constexpr int kTile = 8192;    // rows (and at most records) per phase-A chunk
   static constexpr int kRB = 8;         // bytes per record
   static constexpr int kDedupe = 2048;  // phase-A LDS table slots
-  static constexpr int kTableC = 8192;  // phase-C LDS table slots
-  static constexpr int kTarget = 4000;  // groups per final partition the sizing aims at
+  static constexpr int kTableC = 4096;  // phase-C LDS table slots (two workgroups per CU)
+  static constexpr int kTarget = 2000;  // records per final partition the sizing aims at
 };
 template <>
 struct FM<true> {
   static constexpr int kTile = 4096;
   static constexpr int kRB = 16;
   static constexpr int kDedupe = 1024;
-  static constexpr int kTableC = 4608;
-  static constexpr int kTarget = 2500;
+  static constexpr int kTableC = 2560;
+  static constexpr int kTarget = 1200;
 };
-template <bool HASHED>
-constexpr int unit_half() {
-  return FM<HASHED>::kTile / 2;
-}
-template <bool HASHED>
-constexpr int unit_max() {  // a unit: whole chunk segments starting inside one half-tile window
-  return unit_half<HASHED>() + FM<HASHED>::kTile;
-}
+// records per phase-B unit (whole chunk segments of one bucket; ~32 records per partition run)
+constexpr int kUnitTiles = 2;
 
 struct RecIn {  // == dq_freq_record
   uint64_t key;
@@ -216,12 +213,19 @@ DQ_DEV uint64_t xrec_h(uint64_t rec, uint32_t b) {
 
 // ------------------------------------------------------------------------------------------------
 // Phase A: rows (or received records) -> bucket-sorted chunk regions
+//
+// Each workgroup takes `tiles_per_wg` consecutive tiles.  Its LDS dedupe table persists across
+// those tiles, so a low-cardinality key (priority: 3 groups) leaves the workgroup as a handful of
+// records for its whole range, written at the end into the workgroup's own extra chunk
+// (n_tiles + blockIdx.x).  Round 0 of every 8th tile measures the table's hit rate; below 1/16
+// the table is bypassed (high cardinality: it would only cost probes).  Every tile's other rows
+// are counting-sorted by bucket into the tile's chunk region.
 // ------------------------------------------------------------------------------------------------
 struct AArgs {
   KeySet ks;
   int32_t types[kMaxKeys];
   int32_t n_keys;
-  int32_t pad;
+  int32_t tiles_per_wg;
   int64_t n_items;
   int64_t tile_items;
   const RecIn* rin;
@@ -234,10 +238,19 @@ struct AArgs {
   unsigned long long* counters;
 };
 
+// Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
+// the LDS must allow two workgroups per CU (<= 80 KB).
+template <bool HASHED, bool FROM_REC>
+struct AKeys {
+  static constexpr int kDedupe = FROM_REC ? (HASHED ? 128 : 256) : (HASHED ? 256 : 512);
+  // a workgroup's rows: counts < 4^(kTile / kDedupe), so the digits of every entry fit
+  static constexpr int kTilesPerWg = FROM_REC ? 1 : (HASHED ? 15 : 16);
+};
+
 template <bool HASHED, bool FROM_REC>
 __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
   using M = FM<HASHED>;
-  constexpr int T = M::kTile, D = M::kDedupe, W = M::kRB / 8;
+  constexpr int T = M::kTile, D = AKeys<HASHED, FROM_REC>::kDedupe, W = M::kRB / 8;
   constexpr int ROUNDS = FROM_REC ? 1 : T / kThreads;
   __shared__ uint32_t bh[kBuckets], bcur[kBuckets];
   __shared__ uint64_t dkey[D], dcnt[D];
@@ -246,152 +259,62 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
   __shared__ uint64_t s_red[kThreads / 64];
   __shared__ uint32_t s_hits, s_bypass;
   __shared__ unsigned long long s_arena_base, s_arena_cur;
-  __shared__ uint64_t sortbuf[T * W];
+  // the tile's rows, hashed: exact h per row; hashed (h, row index or arena offset) per row.  The
+  // round loops read it back with dynamic indices (no unrolling: the kernel stays small enough for
+  // the instruction cache).
+  __shared__ uint64_t stash[T * W];
+  __shared__ uint64_t scnt[FROM_REC ? kThreads : 1];
 
   const int tid = threadIdx.x;
-  const int64_t chunk = blockIdx.x;
-  const int64_t i0 = chunk * a.tile_items;
-  const int64_t i1 = min(i0 + a.tile_items, a.n_items);
-  for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
+  const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
+  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
+  const int64_t t1 = min(t0 + (int64_t)a.tiles_per_wg, n_tiles);
   for (int i = tid; i < D; i += kThreads) {
     dkey[i] = kEmptyKey;
     dcnt[i] = 0;
     if (HASHED) drep[i] = kNotReady;
   }
-  if (tid == 0) {
-    s_hits = 0;
-    s_bypass = 0;
-    s_arena_cur = 0;
-  }
-  __syncthreads();
-
-  uint64_t rh[ROUNDS], rcnt[ROUNDS], rrep[ROUNDS];
-  bool raw[ROUNDS];
+  for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
+  if (tid == 0) s_bypass = 0;
   unsigned long long nulls = 0, nullg = 0;
-#pragma unroll
-  for (int j = 0; j < ROUNDS; ++j) {
-    raw[j] = false;
-    rh[j] = rcnt[j] = rrep[j] = 0;
-    const int64_t i = i0 + (int64_t)j * kThreads + tid;
-    if (i < i1) {
-      uint64_t h = 0, c = 1, rep = 0;
-      bool keyed = true;
-      if constexpr (FROM_REC) {
-        const RecIn r = a.rin[i];
-        c = r.count;
-        h = HASHED ? r.key : fmix_bij(r.key);
-        if (HASHED) rep = a.var_arena_base + (uint64_t)seg_var_base(a.segs, i) + r.enc_off;
-        keyed = c != 0;
-      } else {
-        const int kind = row_kind(a.ks, i, !HASHED);
-        if (kind == ROW_SKIP) {
-          ++nulls;
-          keyed = false;
-        } else if (kind == ROW_NULL_GROUP) {
-          ++nullg;
-          keyed = false;
-        } else {
-          h = HASHED ? row_hash_hashed(a.ks, i) : row_hash_exact(a.ks, i);
-          rep = (uint64_t)(i - i0);
-        }
-      }
-      if (keyed) {
-        bool done = false;
-        if (!s_bypass && h != kEmptyKey) {
-          uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
-          for (int pr = 0; pr < 4 && !done; ++pr) {
-            uint64_t k = lds_load(&dkey[slot]);
-            bool claimed = false;
-            if (k == kEmptyKey) {
-              const uint64_t prev = atomicCAS((unsigned long long*)&dkey[slot], kEmptyKey, h);
-              if (prev == kEmptyKey) claimed = true;
-              else k = prev;
-            }
-            if (claimed) {
-              if (HASHED) lds_store(&drep[slot], rep);
-              atomicAdd((unsigned long long*)&dcnt[slot], c);
-              done = true;
-            } else if (k == h) {
-              bool same = true;
-              if constexpr (HASHED) {
-                const uint64_t r2 = lds_load(&drep[slot]);
-                if (r2 == kNotReady) break;  // being claimed right now: keep the row raw
-                if (r2 != rep) {
-                  if constexpr (FROM_REC)
-                    same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
-                                     reinterpret_cast<const uint32_t*>(a.arena + rep), a.types,
-                                     a.n_keys);
-                  else
-                    same = rows_equal(a.ks, i0 + (int64_t)r2, i0 + (int64_t)rep);
-                }
-              }
-              if (same) {
-                atomicAdd((unsigned long long*)&dcnt[slot], c);
-                if (j == 0) atomicAdd(&s_hits, 1u);
-                done = true;
-              }
-            }
-            slot = (slot + 1) & (D - 1);
-          }
-        }
-        if (!done) {
-          raw[j] = true;
-          rh[j] = h;
-          rcnt[j] = c;
-          rrep[j] = rep;
-          const uint32_t b = bucket_of(h);
-          for_digits(c, [&](uint32_t) { atomicAdd(&bh[b], 1u); });
-        }
+  unsigned long long dbg_nr = 0, dbg_diff = 0, dbg_full = 0, dbg_bypass = 0;
+
+  // Counting sort of a chunk's records: bucket counts are in bh; begin_chunk scans them, writes
+  // the chunk's histogram row and reserves the chunk's arena bytes; records then go straight to
+  // their place in the chunk region (a 64 KB region: the runs meet in L2).
+  auto begin_chunk = [&](int64_t chunk, uint64_t arena_need) {
+    __syncthreads();
+    uint32_t total;
+    const uint32_t mine = tid < kBuckets ? bh[tid] : 0u;
+    const uint32_t ex = block_excl_scan(mine, s_wave, total);
+    uint16_t* hrow = a.hist + chunk * kHistRow;
+    if (tid < kBuckets) {
+      bcur[tid] = ex;
+      hrow[tid] = (uint16_t)ex;
+    }
+    if (tid == 0) hrow[kBuckets] = (uint16_t)total;
+    if constexpr (HASHED && !FROM_REC) {
+      const uint64_t all = block_sum_u64(arena_need, s_red);
+      if (tid == 0) {
+        s_arena_base = all ? atomicAdd(a.arena_cursor, (unsigned long long)all) : 0ULL;
+        s_arena_cur = 0;
       }
     }
-    if (!FROM_REC && ROUNDS > 1 && j == 0) {
-      __syncthreads();
-      // fewer than 1/16 of the first kThreads rows repeated a key: high cardinality, so the
-      // LDS table would only cost probes for the rest of the chunk
-      if (tid == 0) s_bypass = s_hits * 16u < (uint32_t)kThreads ? 1u : 0u;
-      __syncthreads();
-    }
-  }
-  __syncthreads();
-
-  // records of the collapsed groups count into the bucket histogram
-  for (int sl = tid; sl < D; sl += kThreads) {
-    const uint64_t k = dkey[sl];
-    if (k == kEmptyKey) continue;
-    const uint32_t b = bucket_of(k);
-    for_digits(dcnt[sl], [&](uint32_t) { atomicAdd(&bh[b], 1u); });
-  }
-  __syncthreads();
-  uint32_t total;
-  const uint32_t mine = tid < kBuckets ? bh[tid] : 0u;
-  const uint32_t ex = block_excl_scan(mine, s_wave, total);
-  uint16_t* hrow = a.hist + chunk * kHistRow;
-  if (tid < kBuckets) {
-    bcur[tid] = ex;
-    hrow[tid] = (uint16_t)ex;
-  }
-  if (tid == 0) hrow[kBuckets] = (uint16_t)total;
-
-  // hashed rows: one arena allocation per chunk for the encoded keys of its records
-  if constexpr (HASHED && !FROM_REC) {
-    uint64_t need = 0;
-#pragma unroll
-    for (int j = 0; j < ROUNDS; ++j)
-      if (raw[j]) need += row_enc_size(a.ks, i0 + (int64_t)rrep[j]);
-    for (int sl = tid; sl < D; sl += kThreads)
-      if (dkey[sl] != kEmptyKey) need += row_enc_size(a.ks, i0 + (int64_t)drep[sl]);
-    const uint64_t all = block_sum_u64(need, s_red);
-    if (tid == 0) s_arena_base = all ? atomicAdd(a.arena_cursor, (unsigned long long)all) : 0ULL;
-  }
-  __syncthreads();
-
-  auto put = [&](uint64_t h, uint32_t code, uint64_t rep) {
+    __syncthreads();
+  };
+  auto end_chunk = [&]() {
+    __syncthreads();
+    for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
+    __syncthreads();
+  };
+  auto put = [&](int64_t chunk, uint64_t h, uint32_t code, uint64_t rep) {
     const uint32_t pos = atomicAdd(&bcur[bucket_of(h)], 1u);
+    uint64_t* out = reinterpret_cast<uint64_t*>(a.recs) + (chunk * (int64_t)T + pos) * W;
     if constexpr (HASHED) {
-      sortbuf[2 * pos] = h;
-      sortbuf[2 * pos + 1] = (rep << 8) | code;
+      out[0] = h;
+      out[1] = (rep << 8) | code;
     } else {
-      sortbuf[pos] = (h << 8) | code;
+      out[0] = (h << 8) | code;
     }
   };
   auto arena_rep = [&](int64_t row) -> uint64_t {  // hashed rows: copy the key into the arena
@@ -400,28 +323,188 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
     row_encode(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
     return off;
   };
-#pragma unroll
-  for (int j = 0; j < ROUNDS; ++j) {
-    if (!raw[j]) continue;
-    uint64_t rep = rrep[j];
-    if constexpr (HASHED && !FROM_REC) rep = arena_rep(i0 + (int64_t)rrep[j]);
-    const uint64_t h = rh[j];
-    for_digits(rcnt[j], [&](uint32_t code) { put(h, code, rep); });
+  // LDS dedupe: 0 = not counted (table full), 1 = claimed a new slot, 2 = added to an existing
+  // slot, 3 = the key's slot is being claimed: retry after the next barrier
+  auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep) -> int {
+    if (h == kEmptyKey) return 0;
+    uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
+    for (int pr = 0; pr < 4; ++pr) {
+      uint64_t k = lds_load(&dkey[slot]);
+      bool claimed = false;
+      if (k == kEmptyKey) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&dkey[slot], kEmptyKey, h);
+        if (prev == kEmptyKey) claimed = true;
+        else k = prev;
+      }
+      if (claimed) {
+        if (HASHED) lds_store(&drep[slot], rep);
+        atomicAdd((unsigned long long*)&dcnt[slot], c);
+        return 1;
+      }
+      if (k == h) {
+        bool same = true;
+        if constexpr (HASHED) {
+          const uint64_t r2 = lds_load(&drep[slot]);
+          if (r2 == kNotReady) {  // being claimed right now (another lane / wave)
+            dbg_nr++;
+            return 3;
+          }
+          if (r2 != rep) {
+            if constexpr (FROM_REC)
+              same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
+                               reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
+            else
+              same = rows_equal(a.ks, (int64_t)r2, (int64_t)rep);
+          }
+          if (!same) dbg_diff++;
+        }
+        if (same) {
+          atomicAdd((unsigned long long*)&dcnt[slot], c);
+          return 2;
+        }
+      }
+      slot = (slot + 1) & (D - 1);
+    }
+    dbg_full++;
+    return 0;
+  };
+
+  __syncthreads();
+  for (int64_t t = t0; t < t1; ++t) {
+    const int64_t i0 = t * a.tile_items;
+    const int64_t i1 = min(i0 + a.tile_items, a.n_items);
+    const bool probe = ((t - t0) & 7) == 0;
+    if (tid == 0) s_hits = 0;
+    uint32_t keyed = 0, raw = 0;  // bit j: round j
+    // 1. load + hash
+#pragma unroll 1
+    for (int j = 0; j < ROUNDS; ++j) {
+      const int64_t i = i0 + (int64_t)j * kThreads + tid;
+      const int q = j * kThreads + tid;
+      if (i >= i1) continue;
+      if constexpr (FROM_REC) {
+        const RecIn r = a.rin[i];
+        scnt[tid] = r.count;
+        stash[q * W] = HASHED ? r.key : fmix_bij(r.key);
+        if (HASHED) stash[q * W + 1] = a.var_arena_base + (uint64_t)seg_var_base(a.segs, i) + r.enc_off;
+        if (r.count) keyed |= 1u << j;
+      } else {
+        const int kind = row_kind(a.ks, i, !HASHED);
+        if (kind == ROW_SKIP) {
+          ++nulls;
+        } else if (kind == ROW_NULL_GROUP) {
+          ++nullg;
+        } else {
+          keyed |= 1u << j;
+          stash[q * W] = HASHED ? row_hash_hashed(a.ks, i) : row_hash_exact(a.ks, i);
+          if (HASHED) stash[q * W + 1] = (uint64_t)i;  // the row until it is encoded
+        }
+      }
+    }
+    __syncthreads();
+    // 2. dedupe (round 0 of a probing tile measures the hit rate).  A hashed key whose slot is
+    // claimed but not yet published by its claimer (another lane or wave) is retried after a
+    // block barrier -- never a spin, lanes of one wave would wait on each other -- once per tile
+    // (and right after round 0 when probing), so the rounds themselves run barrier-free.
+    uint32_t wait = 0;  // bit j: round j must retry
+    auto count_raw = [&](int j, uint64_t h, uint64_t c) {
+      raw |= 1u << j;
+      const uint32_t b = bucket_of(h);
+      for_digits(c, [&](uint32_t) { atomicAdd(&bh[b], 1u); });
+    };
+    auto retry = [&](uint32_t rounds_mask, uint32_t& hits) {
+      if constexpr (HASHED) {
+        uint32_t w = wait & rounds_mask;
+        while (__syncthreads_or(w ? 1 : 0)) {
+#pragma unroll 1
+          for (int j = 0; j < ROUNDS; ++j) {
+            if (!((w >> j) & 1u)) continue;
+            const int q = j * kThreads + tid;
+            const uint64_t h = stash[q * W], rep = stash[q * W + 1];
+            const uint64_t c = FROM_REC ? scnt[tid] : 1;
+            const int res = dedupe(h, c, rep);
+            if (res == 3) continue;
+            w &= ~(1u << j);
+            if (res == 2) ++hits;
+            if (!res) count_raw(j, h, c);
+          }
+        }
+        wait &= ~rounds_mask;
+      }
+    };
+#pragma unroll 1
+    for (int j = 0; j < ROUNDS; ++j) {
+      const int q = j * kThreads + tid;
+      const bool on = probe && j == 0 ? true : !s_bypass;
+      uint32_t hits = 0;
+      if ((keyed >> j) & 1u) {
+        const uint64_t h = stash[q * W];
+        const uint64_t rep = HASHED ? stash[q * W + 1] : 0;
+        const uint64_t c = FROM_REC ? scnt[tid] : 1;
+        const int res = on ? dedupe(h, c, rep) : 0;
+        if (res == 3) wait |= 1u << j;
+        else if (res == 2) ++hits;
+        else if (!res) count_raw(j, h, c);
+      }
+      if (probe && j == 0) {
+        retry(1u, hits);
+        const uint32_t wh = wave_sum(hits);  // every lane: the shuffles need the whole wave
+        if (__lane_id() == 0 && wh) atomicAdd(&s_hits, wh);
+        __syncthreads();
+        if (tid == 0) s_bypass = s_hits * 16u < (uint32_t)kThreads ? 1u : 0u;
+        __syncthreads();
+        if (tid == 0) dbg_bypass += s_bypass;
+      }
+    }
+    {
+      uint32_t hits = 0;
+      retry(~0u, hits);
+    }
+    uint64_t need = 0;
+    if constexpr (HASHED && !FROM_REC) {
+#pragma unroll 1
+      for (int j = 0; j < ROUNDS; ++j)
+        if ((raw >> j) & 1u) need += row_enc_size(a.ks, (int64_t)stash[(j * kThreads + tid) * W + 1]);
+    }
+    // 3. counting sort of the raw rows into the tile's chunk
+    begin_chunk(t, need);
+#pragma unroll 1
+    for (int j = 0; j < ROUNDS; ++j) {
+      if (!((raw >> j) & 1u)) continue;
+      const int q = j * kThreads + tid;
+      const uint64_t h = stash[q * W];
+      uint64_t rep = HASHED ? stash[q * W + 1] : 0;
+      if constexpr (HASHED && !FROM_REC) rep = arena_rep((int64_t)rep);
+      for_digits(FROM_REC ? scnt[tid] : 1, [&](uint32_t code) { put(t, h, code, rep); });
+    }
+    end_chunk();
   }
+  // the collapsed groups of the whole range -> this workgroup's own chunk
+  uint64_t need = 0;
+  for (int sl = tid; sl < D; sl += kThreads) {
+    const uint64_t k = dkey[sl];
+    if (k == kEmptyKey) continue;
+    const uint32_t b = bucket_of(k);
+    for_digits(dcnt[sl], [&](uint32_t) { atomicAdd(&bh[b], 1u); });
+    if constexpr (HASHED && !FROM_REC) need += row_enc_size(a.ks, (int64_t)drep[sl]);
+  }
+  const int64_t fchunk = n_tiles + blockIdx.x;
+  begin_chunk(fchunk, need);
   for (int sl = tid; sl < D; sl += kThreads) {
     const uint64_t k = dkey[sl];
     if (k == kEmptyKey) continue;
     uint64_t rep = HASHED ? drep[sl] : 0;
-    if constexpr (HASHED && !FROM_REC) rep = arena_rep(i0 + (int64_t)drep[sl]);
-    for_digits(dcnt[sl], [&](uint32_t code) { put(k, code, rep); });
+    if constexpr (HASHED && !FROM_REC) rep = arena_rep((int64_t)rep);
+    for_digits(dcnt[sl], [&](uint32_t code) { put(fchunk, k, code, rep); });
   }
-  __syncthreads();
-  uint64_t* out = reinterpret_cast<uint64_t*>(a.recs) + chunk * (int64_t)T * W;
-  for (uint32_t q = tid; q < total * W; q += kThreads) out[q] = sortbuf[q];
   if (!FROM_REC) {
     wave_count(&a.counters[C_NULL_ROWS], nulls);
     wave_count(&a.counters[C_NULL_GROUP], nullg);
   }
+  wave_count(&a.counters[C_DBG_NOTREADY], dbg_nr);
+  wave_count(&a.counters[C_DBG_DIFF], dbg_diff);
+  wave_count(&a.counters[C_DBG_FULL], dbg_full);
+  wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -478,8 +561,34 @@ __global__ void __launch_bounds__(kThreads) freq_bucket_scan(const uint16_t* len
   }
 }
 
+// unit_c0[unit_start[b] + u] = first chunk whose bucket-b prefix reaches u*H (the unit's first
+// chunk), unit_b[unit] = b; units without a chunk start keep c0 = n (empty).
+__global__ void __launch_bounds__(256) freq_unit_map(const uint32_t* prefT, int64_t n,
+                                                     const uint32_t* unit_start, uint32_t H,
+                                                     uint32_t* unit_c0, uint16_t* unit_b) {
+  const int b = blockIdx.y;
+  const uint32_t ub = unit_start[b], U = unit_start[b + 1] - ub;
+  const uint32_t* pre = prefT + (int64_t)b * (n + 1);
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+       c += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t uprev = c ? (int64_t)(pre[c - 1] / H) : -1;
+    const int64_t ucur = min((int64_t)(pre[c] / H), (int64_t)U - 1);
+    for (int64_t u = uprev + 1; u <= ucur; ++u) unit_c0[ub + u] = (uint32_t)c;
+  }
+  if (blockIdx.x == 0)
+    for (uint32_t u = threadIdx.x; u < U; u += blockDim.x) unit_b[ub + u] = (uint16_t)b;
+}
+
 // ------------------------------------------------------------------------------------------------
-// Phase B: a bucket's unit -> sorted by the next s hash bits
+// Phase B: a bucket's records -> partition-contiguous records (radix scatter by the next s bits)
+//
+// A bucket's records are cut into units of whole chunk segments (~2 tiles each).  B1 counts each
+// unit's records per sub-bucket, B2 turns the counts into each unit's offsets inside every
+// partition (a scan over the bucket's units per sub-bucket) and the partitions' sizes, and B3
+// re-reads the unit and writes every record to its final place: a partition's records end up in
+// one contiguous range, written as runs of ~32 records per (unit, partition) whose neighbours
+// come from the neighbouring units of the same XCD (units are handed out XCD-contiguously, so a
+// partition's runs meet in one L2).
 // ------------------------------------------------------------------------------------------------
 struct BArgs {
   const uint8_t* recs;
@@ -488,142 +597,163 @@ struct BArgs {
   const uint32_t* prefT;
   int64_t n_chunks;
   const uint32_t* unit_start;
-  const unsigned long long* bucket_base;
+  const uint32_t* unit_c0;
+  const uint16_t* unit_b;
   int32_t s;
-  int32_t hstride;
+  uint32_t n_units;
+  uint32_t* uhist;                        // [unit][S]: counts (B1) -> offsets in the partition (B2)
+  unsigned long long* part_base;          // [P + 1]
   uint8_t* recsB;
-  uint16_t* histB;
-  unsigned long long* unit_out;
 };
 
-DQ_DEV int64_t lower_bound_u32(const uint32_t* a, int64_t lo, int64_t hi, uint64_t x) {
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if ((uint64_t)a[mid] < x) lo = mid + 1;
-    else hi = mid;
+struct UnitLds {
+  uint32_t sw_pos[kThreads];
+  uint32_t sw_c[kThreads];
+  uint16_t sw_off[kThreads];
+  uint32_t s_wave[kThreads / 64];
+  uint32_t s_b;
+  int64_t s_c0, s_c1;
+};
+
+DQ_DEV void unit_range(const BArgs& a, uint32_t w, UnitLds& L) {
+  if (threadIdx.x == 0) {
+    const int64_t n = a.n_chunks;
+    const uint32_t b = a.unit_b[w];
+    L.s_b = b;
+    L.s_c0 = min((int64_t)a.unit_c0[w], n);
+    L.s_c1 = w + 1 < a.unit_start[b + 1] ? min((int64_t)a.unit_c0[w + 1], n) : n;
   }
-  return lo;
+  __syncthreads();
 }
 
-template <bool HASHED>
-__global__ void __launch_bounds__(kThreads) freq_phaseB(BArgs a) {
-  using M = FM<HASHED>;
-  constexpr int W = M::kRB / 8, H = unit_half<HASHED>(), UM = unit_max<HASHED>();
-  constexpr int KB = (UM + kThreads - 1) / kThreads;
-  __shared__ uint32_t sw_pos[kThreads];
-  __shared__ uint32_t sw_c[kThreads];
-  __shared__ uint16_t sw_off[kThreads];
-  __shared__ uint32_t sh[kBuckets + 1];
-  __shared__ uint32_t s_wave[kThreads / 64];
-  __shared__ int64_t s_c0, s_c1;
-  __shared__ uint32_t s_b, s_in0, s_in1;
-  __shared__ uint64_t outb[UM * W];
+// Calls f(record pointer) for every record of the unit (chunk segments of bucket s_b in
+// [s_c0, s_c1)).  Every thread of the block must call it.
+template <bool HASHED, typename F>
+DQ_DEV void for_unit_records(const BArgs& a, UnitLds& L, F&& f) {
+  constexpr int W = FM<HASHED>::kRB / 8;
   const int tid = threadIdx.x;
-  const int64_t n = a.n_chunks;
-  if (tid == 0) {
-    const uint32_t w = blockIdx.x;
-    uint32_t lo = 0, hi = kBuckets;  // last b with unit_start[b] <= w
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (a.unit_start[mid] <= w) lo = mid;
-      else hi = mid;
-    }
-    while (lo + 1 < (uint32_t)kBuckets && a.unit_start[lo + 1] <= w) ++lo;  // skip empty buckets
-    const uint32_t b = lo, u = w - a.unit_start[b];
-    const uint32_t* pre = a.prefT + (int64_t)b * (n + 1);
-    const int64_t c0 = lower_bound_u32(pre, 0, n, (uint64_t)u * H);
-    const int64_t c1 = lower_bound_u32(pre, c0, n, (uint64_t)(u + 1) * H);
-    s_b = b;
-    s_c0 = c0;
-    s_c1 = c1;
-    s_in0 = pre[c0];
-    s_in1 = pre[c1];
-  }
-  const int S = 1 << a.s;
-  for (int i = tid; i <= S; i += kThreads) sh[i] = 0;
-  __syncthreads();
-  const uint32_t b = s_b;
-  const int64_t c0 = s_c0, c1 = s_c1;
-  const uint32_t n_in = s_in1 - s_in0;
-  const uint16_t* lenb = a.lenT + (int64_t)b * n;
-  const uint16_t* offb = a.offT + (int64_t)b * n;
-
-  uint64_t r0[KB], r1[KB];
-  uint32_t base_w = 0;
+  const int64_t n = a.n_chunks, c0 = L.s_c0, c1 = L.s_c1;
+  const uint16_t* lenb = a.lenT + (int64_t)L.s_b * n;
+  const uint16_t* offb = a.offT + (int64_t)L.s_b * n;
   for (int64_t cw = c0; cw < c1; cw += kThreads) {
     const int64_t c = cw + tid;
     const uint32_t len = c < c1 ? lenb[c] : 0u;
     uint32_t wtot;
-    const uint32_t pos = block_excl_scan(len, s_wave, wtot);
-    sw_pos[tid] = pos;
-    sw_c[tid] = (uint32_t)(c - cw);
-    sw_off[tid] = c < c1 ? offb[c] : 0;
+    const uint32_t pos = block_excl_scan(len, L.s_wave, wtot);
+    L.sw_pos[tid] = pos;
+    L.sw_c[tid] = (uint32_t)(c - cw);
+    L.sw_off[tid] = c < c1 ? offb[c] : 0;
     __syncthreads();
     const uint32_t nwin = (uint32_t)min((int64_t)kThreads, c1 - cw);
-#pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      const uint32_t i = (uint32_t)k * kThreads + tid;
-      if (i >= base_w && i < base_w + wtot) {
-        const uint32_t li = i - base_w;
-        const uint32_t j = seg_of(sw_pos, nwin, li);
-        const int64_t chunk = cw + sw_c[j];
-        const int64_t rec = chunk * M::kTile + sw_off[j] + (li - sw_pos[j]);
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + rec * W;
-        r0[k] = src[0];
-        if (HASHED) r1[k] = src[1];
-      }
+    for (uint32_t li = tid; li < wtot; li += kThreads) {
+      const uint32_t j = seg_of(L.sw_pos, nwin, li);
+      const int64_t rec = (cw + L.sw_c[j]) * FM<HASHED>::kTile + L.sw_off[j] + (li - L.sw_pos[j]);
+      f(reinterpret_cast<const uint64_t*>(a.recs) + rec * W);
     }
-    base_w += wtot;
     __syncthreads();
   }
-  uint32_t rank[KB];
-#pragma unroll
-  for (int k = 0; k < KB; ++k) {
-    const uint32_t i = (uint32_t)k * kThreads + tid;
-    if (i < n_in) {
-      const uint32_t sb = sub_of(HASHED ? r0[k] : (r0[k] >> 8), a.s);
-      rank[k] = atomicAdd(&sh[sb], 1u);
+}
+
+DQ_DEV uint32_t rec_sub(const uint64_t* r, int s, bool hashed) {
+  return sub_of(hashed ? r[0] : (r[0] >> 8), s);
+}
+
+// B1: per unit, records per sub-bucket
+template <bool HASHED>
+__global__ void __launch_bounds__(kThreads) freq_phaseB_count(BArgs a) {
+  __shared__ UnitLds L;
+  __shared__ uint32_t sh[1 << kMaxSubBits];
+  const int S = 1 << a.s;
+  for (int i = threadIdx.x; i < S; i += kThreads) sh[i] = 0;
+  unit_range(a, blockIdx.x, L);
+  for_unit_records<HASHED>(a, L, [&](const uint64_t* r) { atomicAdd(&sh[rec_sub(r, a.s, HASHED)], 1u); });
+  uint32_t* row = a.uhist + (int64_t)blockIdx.x * S;
+  for (int i = threadIdx.x; i < S; i += kThreads) row[i] = sh[i];
+}
+
+// B2: per bucket, each unit's offset inside every partition, and the partitions' sizes
+__global__ void __launch_bounds__(kThreads) freq_phaseB_scan(BArgs a) {
+  const uint32_t b = blockIdx.x, S = 1u << a.s;
+  const uint32_t u0 = a.unit_start[b], u1 = a.unit_start[b + 1];
+  for (uint32_t sb = threadIdx.x; sb < S; sb += kThreads) {
+    uint64_t run = 0;
+    for (uint32_t u = u0; u < u1; ++u) {
+      uint32_t* cell = a.uhist + (int64_t)u * S + sb;
+      const uint32_t v = *cell;
+      *cell = (uint32_t)run;
+      run += v;
     }
+    a.part_base[(uint64_t)b * S + sb] = run;  // sizes; freq_part_scan makes them offsets
   }
-  __syncthreads();
-  uint32_t tot;
-  const uint32_t v = tid < S ? sh[tid] : 0u;
-  const uint32_t ex = block_excl_scan(v, s_wave, tot);
-  uint16_t* hrow = a.histB + (int64_t)blockIdx.x * a.hstride;
-  if (tid < S) {
-    sh[tid] = ex;
-    hrow[tid] = (uint16_t)ex;
-  }
-  if (tid == 0) hrow[S] = (uint16_t)n_in;
-  __syncthreads();
+}
+
+// exclusive scan of the P partition sizes in place; part_base[P] = total
+__global__ void __launch_bounds__(kThreads) freq_part_scan(unsigned long long* v, int64_t P) {
+  __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ uint64_t s_red[kThreads / 64];
+  const int64_t per = (P + kThreads - 1) / kThreads;
+  const int64_t lo = threadIdx.x * per, hi = min(lo + per, P);
+  uint64_t sum = 0;
+  for (int64_t i = lo; i < hi; ++i) sum += v[i];
+  // exclusive scan of the per-thread sums (64-bit: two 32-bit halves are not enough in general)
+  const int lane = __lane_id(), wave = threadIdx.x >> 6;
+  uint64_t x = sum;
 #pragma unroll
-  for (int k = 0; k < KB; ++k) {
-    const uint32_t i = (uint32_t)k * kThreads + tid;
-    if (i < n_in) {
-      const uint32_t sb = sub_of(HASHED ? r0[k] : (r0[k] >> 8), a.s);
-      const uint32_t pos = sh[sb] + rank[k];
-      outb[pos * W] = r0[k];
-      if (HASHED) outb[pos * W + 1] = r1[k];
-    }
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
   }
+  if (lane == 63) s_red[wave] = x;
   __syncthreads();
-  const uint64_t obase = a.bucket_base[b] + s_in0;
-  uint64_t* dst = reinterpret_cast<uint64_t*>(a.recsB) + obase * W;
-  for (uint32_t q = tid; q < n_in * W; q += kThreads) dst[q] = outb[q];
-  if (tid == 0) a.unit_out[blockIdx.x] = obase;
+  uint64_t base = 0;
+  for (int w = 0; w < wave; ++w) base += s_red[w];
+  uint64_t run = base + x - sum;
+  for (int64_t i = lo; i < hi; ++i) {
+    const uint64_t t = v[i];
+    v[i] = run;
+    run += t;
+  }
+  if (threadIdx.x == kThreads - 1) v[P] = run;
+  (void)s_wave;
+}
+
+// B3: scatter every record of the unit to its partition
+template <bool HASHED>
+__global__ void __launch_bounds__(kThreads) freq_phaseB_scatter(BArgs a) {
+  constexpr int W = FM<HASHED>::kRB / 8;
+  __shared__ UnitLds L;
+  __shared__ unsigned long long cur[1 << kMaxSubBits];
+  // XCD-contiguous units: workgroup g runs on XCD g % 8; XCD x takes units [x*q, (x+1)*q)
+  const uint32_t g = blockIdx.x, q = (a.n_units + 7) / 8;
+  const uint32_t w = (g & 7u) * q + (g >> 3);
+  if (w >= a.n_units) return;
+  const int S = 1 << a.s;
+  unit_range(a, w, L);
+  const uint32_t* row = a.uhist + (int64_t)w * S;
+  for (int i = threadIdx.x; i < S; i += kThreads)
+    cur[i] = a.part_base[(uint64_t)L.s_b * S + i] + row[i];
+  __syncthreads();
+  uint64_t* out = reinterpret_cast<uint64_t*>(a.recsB);
+  for_unit_records<HASHED>(a, L, [&](const uint64_t* r) {
+    const unsigned long long pos = atomicAdd(&cur[rec_sub(r, a.s, HASHED)], 1ULL);
+    out[pos * W] = r[0];
+    if (HASHED) out[pos * W + 1] = r[1];
+  });
 }
 
 // ------------------------------------------------------------------------------------------------
-// Phase C: count one partition in LDS
+// Phase C: count partitions in LDS
+//
+// Persistent: workgroup w takes work items w, w + grid, ...  (a work item is a partition, or on a
+// recount one hash subset of one), and the loads of the next item's first records are in flight
+// while the current item's statistics are reduced, so the chain of dependent HBM round trips that
+// bounded one-partition-per-workgroup launches is hidden.
 // ------------------------------------------------------------------------------------------------
 struct CArgs {
   const uint8_t* recsB;
-  const uint16_t* histB;
-  int32_t hstride;
+  const unsigned long long* part_base;  // partition p's records: [part_base[p], part_base[p + 1])
   int32_t s;
-  const unsigned long long* unit_out;
-  const uint32_t* unit_start;
-  const unsigned long long* bucket_base;
+  int32_t n_work;                       // partitions (first pass) or entries (recount)
   const uint8_t* arena;
   int32_t types[kMaxKeys];
   int32_t n_keys;
@@ -641,263 +771,349 @@ struct CArgs {
   unsigned long long* counters;
 };
 
+constexpr int kPF = 2;        // records per thread loaded ahead
+constexpr int kCThreads = 512;  // phase-C workgroup: two per CU by LDS, 128 VGPRs per lane
+
 template <bool HASHED>
-__global__ void __launch_bounds__(kThreads) freq_phaseC(CArgs a) {
+struct CItem {
+  uint32_t p, f, fv;
+  uint64_t r0, r1;
+  uint64_t h[kPF], c[kPF], rep[kPF];
+  uint32_t pending;
+};
+
+template <bool HASHED>
+DQ_DEV void c_decode(const CArgs& a, const uint64_t* src, uint64_t li, uint32_t b, uint64_t& h,
+                     uint64_t& c, uint64_t& rep) {
+  constexpr int W = FM<HASHED>::kRB / 8;
+  if constexpr (HASHED) {
+    h = src[li * W];
+    const uint64_t rc = src[li * W + 1];
+    c = code_count((uint32_t)(rc & 0xff));
+    rep = rc >> 8;
+  } else {
+    const uint64_t r = src[li];
+    h = xrec_h(r, b);
+    c = code_count((uint32_t)(r & 0xff));
+    rep = 0;
+  }
+}
+
+// Work item wi: its partition / subset and the first kPF * kCThreads of its records.
+template <bool HASHED>
+DQ_DEV void c_fetch(const CArgs& a, int wi, CItem<HASHED>& it) {
+  constexpr int W = FM<HASHED>::kRB / 8;
+  it.pending = 0;
+  if (wi >= a.n_work) return;
+  it.f = it.fv = 0;
+  if (a.entries) {
+    const FEntry e = a.entries[wi];
+    it.p = e.p;
+    it.f = e.f;
+    it.fv = e.v;
+  } else {
+    it.p = (uint32_t)wi;
+  }
+  it.r0 = a.part_base[it.p];
+  it.r1 = a.part_base[it.p + 1];
+  const uint32_t b = it.p >> a.s;
+  const uint64_t n = it.r1 - it.r0;
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + it.r0 * W;
+  const uint32_t fmask = (1u << it.f) - 1u;
+#pragma unroll
+  for (int q = 0; q < kPF; ++q) {
+    const uint64_t li = (uint64_t)q * kCThreads + threadIdx.x;
+    it.h[q] = it.c[q] = it.rep[q] = 0;
+    if (li < n) {
+      c_decode<HASHED>(a, src, li, b, it.h[q], it.c[q], it.rep[q]);
+      if (it.f == 0 || ((uint32_t)(it.h[q] >> kFilterShift) & fmask) == it.fv) it.pending |= 1u << q;
+    }
+  }
+}
+
+template <bool HASHED>
+__global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
   using M = FM<HASHED>;
   constexpr int KT = M::kTableC, W = M::kRB / 8;
   __shared__ uint64_t tkey[KT], tcnt[KT];
   __shared__ uint64_t trep[HASHED ? KT : 1];
-  __shared__ uint32_t sw_pos[kThreads];
-  __shared__ uint64_t sw_base[kThreads];
-  __shared__ uint32_t s_wave[kThreads / 64];
-  __shared__ uint64_t s_red[kThreads / 64];
-  __shared__ double s_redf[kThreads / 64];
-  __shared__ uint32_t s_occ, s_ovf;
+  __shared__ uint32_t s_wave[kCThreads / 64];
+  __shared__ uint64_t s_red[kCThreads / 64];
+  __shared__ double s_redf[kCThreads / 64];
+  __shared__ uint32_t s_ovf;
   __shared__ unsigned long long s_spec_cnt, s_gbase;
   __shared__ uint64_t s_spec_rep;
+  __shared__ uint32_t s_chist[kSmallCounts];
+  __shared__ uint64_t s_cc[kCThreads / 64 * kCand];
+  __shared__ int32_t s_cs[kCThreads / 64 * kCand];
 
   const int tid = threadIdx.x;
-  const uint32_t S = 1u << a.s;
-  uint32_t p, f = 0, fv = 0;
-  if (a.entries) {
-    const FEntry e = a.entries[blockIdx.x];
-    p = e.p;
-    f = e.f;
-    fv = e.v;
-  } else {
-    // XCD-aware: workgroup g runs on XCD g % 8; every partition of bucket b runs on XCD b % 8,
-    // so the bucket's unit histograms are read from one L2
-    const uint32_t g = blockIdx.x, xcd = g & 7u, k = g >> 3;
-    const uint32_t b = xcd + 8u * (k >> a.s);
-    p = (b << a.s) | (k & (S - 1));
-  }
-  const uint32_t b = p >> a.s, sb = p & (S - 1);
-  for (int i = tid; i < KT; i += kThreads) {
-    tkey[i] = kEmptyKey;
-    tcnt[i] = 0;
-    if (HASHED) trep[i] = kNotReady;
-  }
-  if (tid == 0) {
-    s_occ = 0;
-    s_ovf = 0;
-    s_spec_cnt = 0;
-    s_spec_rep = kNotReady;
-  }
-  __syncthreads();
-  const uint32_t fmask = (1u << f) - 1u;
-  const uint32_t u0 = a.unit_start[b], u1 = a.unit_start[b + 1];
-  uint64_t my_off = 0;
   unsigned long long collisions = 0;
+  CItem<HASHED> cur;
+  c_fetch<HASHED>(a, blockIdx.x, cur);
 
-  // Returns false when the record must wait: its group's slot is claimed but the claimer has not
-  // published the representative yet (hashed mode).  Waiting is a retry after the next block
-  // barrier, never a spin, so lanes of one wave can never wait on each other.
-  auto insert = [&](uint64_t h, uint64_t c, uint64_t rep) -> bool {
-    if (h == kEmptyKey) {  // the table's empty marker: its own cell
-      if constexpr (HASHED) {
-        const uint64_t prev = atomicCAS((unsigned long long*)&s_spec_rep, kNotReady, rep);
-        if (prev != kNotReady && prev != rep &&
-            !enc_equal(reinterpret_cast<const uint32_t*>(a.arena + prev),
-                       reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys))
-          ++collisions;
-      }
-      atomicAdd(&s_spec_cnt, (unsigned long long)c);
-      return true;
+  for (int wi = blockIdx.x; wi < a.n_work; wi += gridDim.x) {
+    for (int i = tid; i < KT; i += kCThreads) {
+      tkey[i] = kEmptyKey;
+      tcnt[i] = 0;
+      if (HASHED) trep[i] = kNotReady;
     }
-    uint32_t slot = HASHED ? (uint32_t)(((uint64_t)(uint32_t)h * KT) >> 32) : ((uint32_t)h & (KT - 1));
-    for (int probe = 0; probe < KT; ++probe) {
-      uint64_t k = lds_load(&tkey[slot]);
-      bool claimed = false;
-      if (k == kEmptyKey) {
-        const uint64_t prev = atomicCAS((unsigned long long*)&tkey[slot], kEmptyKey, h);
-        if (prev == kEmptyKey) claimed = true;
-        else k = prev;
-      }
-      if (claimed) {
-        if (HASHED) lds_store(&trep[slot], rep);
-        atomicAdd((unsigned long long*)&tcnt[slot], (unsigned long long)c);
-        if (atomicAdd(&s_occ, 1u) >= (uint32_t)(KT * 7 / 8)) s_ovf = 1;
+    if (tid == 0) {
+      s_ovf = 0;
+      s_spec_cnt = 0;
+      s_spec_rep = kNotReady;
+    }
+    if (tid < kSmallCounts) s_chist[tid] = 0;
+    __syncthreads();
+    const uint32_t p = cur.p, b = p >> a.s, f = cur.f, fv = cur.fv;
+    const uint32_t fmask = (1u << f) - 1u;
+    const uint64_t r0 = cur.r0, nrec = cur.r1 - cur.r0;
+    uint32_t claims = 0;  // slots this thread claimed (load check after the inserts)
+
+    // Returns false when the record must wait: its group's slot is claimed but the claimer has
+    // not published the representative yet (hashed mode).  Waiting is a retry after the next
+    // block barrier, never a spin, so lanes of one wave can never wait on each other.
+    auto insert = [&](uint64_t h, uint64_t c, uint64_t rep) -> bool {
+      if (h == kEmptyKey) {  // the table's empty marker: its own cell
+        if constexpr (HASHED) {
+          const uint64_t prev = atomicCAS((unsigned long long*)&s_spec_rep, kNotReady, rep);
+          if (prev != kNotReady && prev != rep &&
+              !enc_equal(reinterpret_cast<const uint32_t*>(a.arena + prev),
+                         reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys))
+            ++collisions;
+        }
+        atomicAdd(&s_spec_cnt, (unsigned long long)c);
         return true;
       }
-      if (k == h) {
-        bool same = true;
-        if constexpr (HASHED) {
-          const uint64_t r2 = lds_load(&trep[slot]);
-          if (r2 == kNotReady) return false;
-          if (r2 != rep)
-            same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
-                             reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
-          if (!same) ++collisions;  // two keys on one 64-bit hash: kept as two groups
+      uint32_t slot = HASHED ? (uint32_t)(((uint64_t)(uint32_t)h * KT) >> 32) : ((uint32_t)h & (KT - 1));
+      for (int probe = 0; probe < KT; ++probe) {
+        uint64_t k = lds_load(&tkey[slot]);
+        bool claimed = false;
+        if (k == kEmptyKey) {
+          const uint64_t prev = atomicCAS((unsigned long long*)&tkey[slot], kEmptyKey, h);
+          if (prev == kEmptyKey) claimed = true;
+          else k = prev;
         }
-        if (same) {
+        if (claimed) {
+          if (HASHED) lds_store(&trep[slot], rep);
           atomicAdd((unsigned long long*)&tcnt[slot], (unsigned long long)c);
+          ++claims;
           return true;
         }
-      }
-      slot = slot + 1 == (uint32_t)KT ? 0u : slot + 1;
-    }
-    s_ovf = 1;  // table full
-    return true;
-  };
-
-  for (uint32_t uw = u0; uw < u1; uw += kThreads) {
-    const uint32_t u = uw + tid;
-    uint32_t len = 0;
-    uint64_t base = 0;
-    if (u < u1) {
-      const uint16_t* hr = a.histB + (int64_t)u * a.hstride;
-      const uint32_t lo = hr[sb], hi = hr[sb + 1];
-      len = hi - lo;
-      base = a.unit_out[u] + lo;
-      my_off += lo;
-    }
-    uint32_t wtot;
-    const uint32_t pos = block_excl_scan(len, s_wave, wtot);
-    sw_pos[tid] = pos;
-    sw_base[tid] = base;
-    __syncthreads();
-    const uint32_t nwin = min((uint32_t)kThreads, u1 - uw);
-    for (uint32_t it = 0; it * kThreads < wtot; ++it) {
-      const uint32_t li = it * kThreads + tid;
-      uint64_t h = 0, c = 0, rep = 0;
-      bool pending = false;
-      if (li < wtot && !s_ovf) {
-        const uint32_t j = seg_of(sw_pos, nwin, li);
-        const uint64_t idx = sw_base[j] + (li - sw_pos[j]);
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + idx * W;
-        if constexpr (HASHED) {
-          h = src[0];
-          const uint64_t rc = src[1];
-          c = code_count((uint32_t)(rc & 0xff));
-          rep = rc >> 8;
-        } else {
-          const uint64_t r = src[0];
-          h = xrec_h(r, b);
-          c = code_count((uint32_t)(r & 0xff));
+        if (k == h) {
+          bool same = true;
+          if constexpr (HASHED) {
+            const uint64_t r2 = lds_load(&trep[slot]);
+            if (r2 == kNotReady) return false;
+            if (r2 != rep)
+              same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
+                               reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
+            if (!same) ++collisions;  // two keys on one 64-bit hash: kept as two groups
+          }
+          if (same) {
+            atomicAdd((unsigned long long*)&tcnt[slot], (unsigned long long)c);
+            return true;
+          }
         }
-        pending = f == 0 || ((uint32_t)(h >> kFilterShift) & fmask) == fv;
+        slot = slot + 1 == (uint32_t)KT ? 0u : slot + 1;
       }
+      s_ovf = 1;  // table full
+      return true;
+    };
+    auto insert_all = [&](uint64_t* h, uint64_t* c, uint64_t* rep, uint32_t pending) {
       if constexpr (HASHED) {
         while (__syncthreads_or(pending ? 1 : 0)) {
-          if (pending) pending = !insert(h, c, rep);
+#pragma unroll
+          for (int q = 0; q < kPF; ++q)
+            if ((pending >> q) & 1u)
+              if (insert(h[q], c[q], rep[q])) pending &= ~(1u << q);
         }
       } else {
-        if (pending) insert(h, c, rep);
+#pragma unroll
+        for (int q = 0; q < kPF; ++q)
+          if ((pending >> q) & 1u) insert(h[q], c[q], rep[q]);
+        __syncthreads();
+      }
+    };
+    // the prefetched first records, then the rest of a long partition
+    insert_all(cur.h, cur.c, cur.rep, cur.pending);
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + r0 * W;
+    for (uint64_t base = (uint64_t)kPF * kCThreads; base < nrec; base += (uint64_t)kPF * kCThreads) {
+      uint64_t h[kPF], c[kPF], rep[kPF];
+      uint32_t pending = 0;
+      const bool go = !s_ovf;
+#pragma unroll
+      for (int q = 0; q < kPF; ++q) {
+        const uint64_t li = base + (uint64_t)q * kCThreads + tid;
+        h[q] = c[q] = rep[q] = 0;
+        if (li < nrec && go) {
+          c_decode<HASHED>(a, src, li, b, h[q], c[q], rep[q]);
+          if (f == 0 || ((uint32_t)(h[q] >> kFilterShift) & fmask) == fv) pending |= 1u << q;
+        }
+      }
+      insert_all(h, c, rep, pending);
+    }
+    // next work item's first records: in flight while this one is reduced
+    c_fetch<HASHED>(a, wi + gridDim.x, cur);
+    uint32_t all_claims;
+    block_excl_scan(claims, s_wave, all_claims);
+    if (tid == 0 && all_claims > (uint32_t)(KT * 7 / 8)) s_ovf = 1;  // too full: recount
+    __syncthreads();
+    if (s_ovf) {
+      if (tid == 0) {
+        const unsigned int q = atomicAdd(a.ovf_n, 2u);
+        a.ovf_out[q] = FEntry{p, f + 1, fv, 0};
+        a.ovf_out[q + 1] = FEntry{p, f + 1, fv | (1u << f), 0};
+      }
+      __syncthreads();
+      continue;
+    }
+    // statistics; the entropy term -p ln p depends on the count alone, so small counts are
+    // histogrammed and each distinct one takes ONE log (unique keys: one per partition)
+    uint32_t g = 0;
+    uint64_t un = 0;
+    double e = 0.0;
+    auto term = [&](uint64_t c) {
+      const double pr = (double)c / a.num_rows;
+      return -pr * log(pr);
+    };
+    for (int sl = tid; sl < KT; sl += kCThreads) {
+      if (tkey[sl] == kEmptyKey) continue;
+      const uint64_t c = tcnt[sl];
+      ++g;
+      if (c == 1) ++un;  // the common count: a register, not an LDS atomic on one address
+      else if (c < kSmallCounts) atomicAdd(&s_chist[c], 1u);
+      else e += term(c);
+    }
+    if (tid == 0 && s_spec_cnt) {
+      const uint64_t c = s_spec_cnt;
+      ++g;
+      if (c == 1) ++un;
+      else if (c < kSmallCounts) atomicAdd(&s_chist[c], 1u);
+      else e += term(c);
+    }
+    uint32_t gtot;
+    const uint32_t gex = block_excl_scan(g, s_wave, gtot);  // (its barriers order s_chist too)
+    const uint64_t utot = block_sum_u64(un, s_red);
+    if (tid > 1 && tid < kSmallCounts && s_chist[tid]) e += (double)s_chist[tid] * term(tid);
+    if (tid == 0 && utot) e += (double)utot * term(1);
+    const double etot = block_sum_f64(e, s_redf);
+    const bool sub = f != 0;  // a recount subset: several work items add to one partition
+    if (tid == 0) {
+      if (a.groups) {
+        a.part_off[p] = r0;
+        s_gbase = sub ? atomicAdd(&a.part_groups[p], (unsigned long long)gtot) : 0ULL;
+      }
+      if (!a.groups || !sub) {
+        if (sub) atomicAdd(&a.part_groups[p], (unsigned long long)gtot);
+        else a.part_groups[p] = gtot;
+      }
+      if (sub) {
+        if (utot) atomicAdd(&a.part_unique[p], (unsigned long long)utot);
+        if (etot != 0.0) atomicAdd(&a.part_entropy[p], etot);
+      } else {
+        a.part_unique[p] = utot;
+        a.part_entropy[p] = etot;
+      }
+    }
+    if (a.groups) {
+      __syncthreads();
+      Group* out = a.groups + r0 + s_gbase + gex;
+      uint32_t q = 0;
+      for (int sl = tid; sl < KT; sl += kCThreads) {
+        if (tkey[sl] == kEmptyKey) continue;
+        out[q++] = Group{tkey[sl], tcnt[sl], HASHED ? trep[sl] : 0};
+      }
+      if (tid == 0 && s_spec_cnt) out[q++] = Group{kEmptyKey, s_spec_cnt, HASHED ? s_spec_rep : 0};
+    }
+    if (a.want_cand && !sub) {
+      // top kCand groups of the partition by count (Histogram's rdd.top, per partition): a
+      // thread's top kCand, a wave's by shuffles, the block's by wave 0 over the waves' lists
+      uint64_t tc[kCand];
+      int ts[kCand];
+#pragma unroll
+      for (int q = 0; q < kCand; ++q) {
+        tc[q] = 0;
+        ts[q] = -1;
+      }
+      auto offer = [&](uint64_t c, int sl) {  // insertion with static indices (no scratch)
+#pragma unroll
+        for (int q = 0; q < kCand; ++q) {
+          if (c > tc[q]) {
+            const uint64_t tc2 = tc[q];
+            const int ts2 = ts[q];
+            tc[q] = c;
+            ts[q] = sl;
+            c = tc2;
+            sl = ts2;
+          }
+        }
+      };
+      for (int sl = tid; sl < KT; sl += kCThreads)
+        if (tkey[sl] != kEmptyKey) offer(tcnt[sl], sl);
+      if (tid == 0 && s_spec_cnt) offer(s_spec_cnt, KT);  // KT stands for the special cell
+      // wave: kCand rounds of max over the lanes' heads
+      const int lane = __lane_id(), wave = tid >> 6;
+#pragma unroll
+      for (int r = 0; r < kCand; ++r) {
+        uint64_t best = tc[0];
+        int bl = lane;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const uint64_t y = __shfl_xor(best, o);
+          const int yl = __shfl_xor(bl, o);
+          if (y > best || (y == best && yl < bl)) {
+            best = y;
+            bl = yl;
+          }
+        }
+        const int bs = __shfl(ts[0], bl);
+        if (lane == 0) {
+          s_cc[wave * kCand + r] = best;
+          s_cs[wave * kCand + r] = best ? bs : -1;
+        }
+        if (lane == bl) {
+#pragma unroll
+          for (int q = 0; q + 1 < kCand; ++q) {
+            tc[q] = tc[q + 1];
+            ts[q] = ts[q + 1];
+          }
+          tc[kCand - 1] = 0;
+          ts[kCand - 1] = -1;
+        }
+      }
+      __syncthreads();
+      if (wave == 0) {  // kCThreads / 64 * kCand candidates, one per lane
+        constexpr int kN = kCThreads / 64 * kCand;
+        uint64_t mc = lane < kN ? s_cc[lane] : 0;
+        const int ms = lane < kN ? s_cs[lane] : -1;
+#pragma unroll
+        for (int r = 0; r < kCand; ++r) {
+          uint64_t best = mc;
+          int bl = lane;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t y = __shfl_xor(best, o);
+            const int yl = __shfl_xor(bl, o);
+            if (y > best || (y == best && yl < bl)) {
+              best = y;
+              bl = yl;
+            }
+          }
+          const int sl = __shfl(ms, bl);
+          if (lane == 0) {
+            Group* cslot = a.cand + (uint64_t)p * kCand + r;
+            if (best == 0) *cslot = Group{0, 0, 0};
+            else if (sl == KT) *cslot = Group{kEmptyKey, s_spec_cnt, HASHED ? s_spec_rep : 0};
+            else *cslot = Group{tkey[sl], tcnt[sl], HASHED ? trep[sl] : 0};
+          }
+          if (lane == bl) mc = 0;
+        }
       }
     }
     __syncthreads();
   }
   if (collisions) atomicAdd(&a.counters[C_COLLISIONS], collisions);
-  __syncthreads();
-  if (s_ovf) {
-    if (tid == 0) {
-      const unsigned int q = atomicAdd(a.ovf_n, 2u);
-      a.ovf_out[q] = FEntry{p, f + 1, fv, 0};
-      a.ovf_out[q + 1] = FEntry{p, f + 1, fv | (1u << f), 0};
-    }
-    return;
-  }
-  // statistics of the partition
-  uint32_t g = 0;
-  uint64_t un = 0;
-  double e = 0.0;
-  for (int sl = tid; sl < KT; sl += kThreads) {
-    if (tkey[sl] == kEmptyKey) continue;
-    const uint64_t c = tcnt[sl];
-    ++g;
-    un += c == 1;
-    const double pr = (double)c / a.num_rows;
-    e += -pr * log(pr);
-  }
-  if (tid == 0 && s_spec_cnt) {
-    const uint64_t c = s_spec_cnt;
-    ++g;
-    un += c == 1;
-    const double pr = (double)c / a.num_rows;
-    e += -pr * log(pr);
-  }
-  uint32_t gtot;
-  const uint32_t gex = block_excl_scan(g, s_wave, gtot);
-  const uint64_t utot = block_sum_u64(un, s_red);
-  const double etot = block_sum_f64(e, s_redf);
-  const uint64_t off_sum = block_sum_u64(my_off, s_red);
-  if (tid == 0) {
-    s_gbase = gtot ? atomicAdd(&a.part_groups[p], (unsigned long long)gtot) : 0ULL;
-    if (utot) atomicAdd(&a.part_unique[p], (unsigned long long)utot);
-    if (etot != 0.0) atomicAdd(&a.part_entropy[p], etot);
-  }
-  __syncthreads();
-  if (a.groups) {
-    if (tid == 0) a.part_off[p] = a.bucket_base[b] + off_sum;
-    Group* out = a.groups + a.bucket_base[b] + off_sum + s_gbase + gex;
-    uint32_t q = 0;
-    for (int sl = tid; sl < KT; sl += kThreads) {
-      if (tkey[sl] == kEmptyKey) continue;
-      out[q++] = Group{tkey[sl], tcnt[sl], HASHED ? trep[sl] : 0};
-    }
-    if (tid == 0 && s_spec_cnt) out[q++] = Group{kEmptyKey, s_spec_cnt, HASHED ? s_spec_rep : 0};
-  }
-  if (a.want_cand && a.entries == nullptr) {
-    // top kCand groups of the partition by count (Histogram's rdd.top, per partition)
-    uint64_t tc[kCand];
-    int ts[kCand];
-#pragma unroll
-    for (int q = 0; q < kCand; ++q) {
-      tc[q] = 0;
-      ts[q] = -1;
-    }
-    auto offer = [&](uint64_t c, int sl) {  // insertion with static indices (no scratch)
-#pragma unroll
-      for (int q = 0; q < kCand; ++q) {
-        if (c > tc[q]) {
-          const uint64_t tc2 = tc[q];
-          const int ts2 = ts[q];
-          tc[q] = c;
-          ts[q] = sl;
-          c = tc2;
-          sl = ts2;
-        }
-      }
-    };
-    for (int sl = tid; sl < KT; sl += kThreads)
-      if (tkey[sl] != kEmptyKey) offer(tcnt[sl], sl);
-    if (tid == 0 && s_spec_cnt) offer(s_spec_cnt, KT);  // KT stands for the special cell
-    for (int r = 0; r < kCand; ++r) {
-      const uint64_t mine = tc[0];
-      // block max (count), ties to the lowest thread
-      uint64_t best = mine;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t y = __shfl_xor(best, o);
-        best = y > best ? y : best;
-      }
-      if (__lane_id() == 0) s_red[tid >> 6] = best;
-      __syncthreads();
-      uint64_t gbest = 0;
-      for (int w = 0; w < kThreads / 64; ++w) gbest = s_red[w] > gbest ? s_red[w] : gbest;
-      __syncthreads();
-      if (tid == 0) s_occ = ~0u;
-      __syncthreads();
-      if (gbest && mine == gbest) atomicMin(&s_occ, (uint32_t)tid);
-      __syncthreads();
-      Group* cslot = a.cand + (uint64_t)p * kCand + r;
-      if (gbest == 0) {
-        if (tid == 0) *cslot = Group{0, 0, 0};
-      } else if ((uint32_t)tid == s_occ) {
-        const int sl = ts[0];
-        if (sl == KT) *cslot = Group{kEmptyKey, s_spec_cnt, HASHED ? s_spec_rep : 0};
-        else *cslot = Group{tkey[sl], tcnt[sl], HASHED ? trep[sl] : 0};
-#pragma unroll
-        for (int q = 0; q + 1 < kCand; ++q) {  // pop the head
-          tc[q] = tc[q + 1];
-          ts[q] = ts[q + 1];
-        }
-        tc[kCand - 1] = 0;
-        ts[kCand - 1] = -1;
-      }
-      __syncthreads();
-    }
-  }
 }
 
 // Fixed-order sum of the per-partition statistics: out = {groups, unique, entropy bits}.
@@ -931,15 +1147,22 @@ __global__ void __launch_bounds__(kThreads) freq_reduce(const unsigned long long
 // ------------------------------------------------------------------------------------------------
 // hist[k] += #groups with lo <= count < hi falling in bin (count - lo) / width; width == 0
 // selects power-of-two bins (bin = floor(log2(count)))
-__global__ void freq_group_hist(const Group* g, int64_t n, uint64_t lo, uint64_t hi,
-                                uint64_t width, unsigned long long* hist) {
+__global__ void __launch_bounds__(256) freq_group_hist(const Group* g, int64_t n, uint64_t lo,
+                                                       uint64_t hi, uint64_t width,
+                                                       unsigned long long* hist) {
+  __shared__ unsigned int lh[1024];
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) lh[i] = 0;
+  __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t c = g[i].count;
     if (c == 0 || c < lo || c >= hi) continue;
     const uint64_t bin = width ? (c - lo) / width : (uint64_t)(63 - __builtin_clzll(c));
-    atomicAdd(&hist[bin], 1ULL);
+    atomicAdd(&lh[bin], 1u);
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x)
+    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
 }
 // every group with count >= hi_take, and groups with lo_tie <= count < hi_take up to `cap`
 __global__ void freq_group_select(const Group* g, int64_t n, uint64_t hi_take, uint64_t lo_tie,
@@ -1070,7 +1293,7 @@ struct dq_freq {
   int64_t n_chunks = 0;
   DevBuf<uint8_t> arena;                 // hashed: encoded keys
   DevBuf<unsigned long long> dev_words;  // counters[C_N], then the arena cursor
-  uint64_t h_counters[C_N] = {0, 0, 0};
+  uint64_t h_counters[C_N] = {0};
   uint64_t arena_used = 0;
   int64_t num_rows = 0;
   hipStream_t stream = nullptr;
@@ -1081,9 +1304,10 @@ struct dq_freq {
   uint32_t n_units = 0;
   std::vector<unsigned long long> h_bucket_base = std::vector<unsigned long long>(kBuckets + 1, 0);
   std::vector<uint32_t> h_unit_start = std::vector<uint32_t>(kBuckets + 1, 0);
-  DevBuf<uint16_t> lenT, offT, histB;
-  DevBuf<uint32_t> prefT, unit_start;
-  DevBuf<unsigned long long> totals, bucket_base, unit_out;
+  DevBuf<uint16_t> lenT, offT;
+  DevBuf<uint32_t> prefT, unit_start, unit_c0, uhist;
+  DevBuf<uint16_t> unit_b;
+  DevBuf<unsigned long long> totals, part_base;
   DevBuf<uint8_t> recsB;
   // (phase C)
   bool c_valid = false, c_groups = false, c_cand = false;
@@ -1161,13 +1385,27 @@ static dq_status push_counters(dq_freq* f) {
   return DQ_OK;
 }
 
+// Chunks one phase-A launch over n items writes: one per tile + one per workgroup.
+static int64_t phaseA_chunks(bool hashed, bool from_rec, int64_t n_items, int64_t tile_items,
+                             int64_t* n_wg_out) {
+  const int tpw = from_rec ? 1 : (hashed ? AKeys<true, false>::kTilesPerWg
+                                         : AKeys<false, false>::kTilesPerWg);
+  const int64_t tiles = (n_items + tile_items - 1) / tile_items;
+  const int64_t n_wg = (tiles + tpw - 1) / tpw;
+  if (n_wg_out) *n_wg_out = n_wg;
+  return tiles + n_wg;
+}
+
 template <bool HASHED>
-static void launch_phaseA(dq_freq* f, const AArgs& a, int64_t chunks, bool from_rec) {
+static void launch_phaseA(dq_freq* f, AArgs a, bool from_rec) {
+  int64_t n_wg = 0;
+  phaseA_chunks(HASHED, from_rec, a.n_items, a.tile_items, &n_wg);
+  a.tiles_per_wg = from_rec ? AKeys<HASHED, true>::kTilesPerWg : AKeys<HASHED, false>::kTilesPerWg;
   if (from_rec)
-    hipLaunchKernelGGL((freq_phaseA<HASHED, true>), dim3((unsigned)chunks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((freq_phaseA<HASHED, true>), dim3((unsigned)n_wg), dim3(kThreads), 0,
                        f->stream, a);
   else
-    hipLaunchKernelGGL((freq_phaseA<HASHED, false>), dim3((unsigned)chunks), dim3(kThreads), 0,
+    hipLaunchKernelGGL((freq_phaseA<HASHED, false>), dim3((unsigned)n_wg), dim3(kThreads), 0,
                        f->stream, a);
 }
 
@@ -1198,7 +1436,9 @@ static dq_status finalize_b(dq_freq* f) {
   f->R = 0;
   f->s_bits = 0;
   f->n_units = 0;
+  HIP_TRY(f->part_base.ensure(kBuckets + 1));
   if (n == 0) {
+    HIP_TRY(hipMemsetAsync(f->part_base.p, 0, (kBuckets + 1) * 8, f->stream));
     f->b_valid = true;
     return DQ_OK;
   }
@@ -1217,10 +1457,13 @@ static dq_status finalize_b(dq_freq* f) {
   HIP_TRY(hipMemcpy(tot.data(), f->totals.p, kBuckets * 8, hipMemcpyDeviceToHost));
   uint64_t R = 0;
   for (auto t : tot) R += t;
-  const int target = f->exact ? FM<false>::kTarget : FM<true>::kTarget;
+  int target = f->exact ? FM<false>::kTarget : FM<true>::kTarget;
+  // test hook: a small target forces deep partitioning (all s) on small inputs, a huge one the
+  // recount path of overflowing partitions
+  if (const char* e = getenv("DQ_FREQ_PARTITION_TARGET")) target = std::max(1, atoi(e));
   int s = 0;
   while (s < kMaxSubBits && ((uint64_t)kBuckets << s) * (uint64_t)target < R) ++s;
-  const uint64_t H = (uint64_t)f->tile / 2;
+  const uint64_t H = (uint64_t)f->tile * kUnitTiles;
   uint32_t u = 0;
   for (int b = 0; b < kBuckets; ++b) {
     f->h_unit_start[b] = u;
@@ -1231,36 +1474,66 @@ static dq_status finalize_b(dq_freq* f) {
   f->R = R;
   f->s_bits = s;
   f->n_units = u;
+  if (getenv("DQ_FREQ_DEBUG")) {
+    fprintf(stderr, "dq_freq phase A: notready=%llu diff=%llu full=%llu bypass_tiles=%llu\n",
+            (unsigned long long)f->h_counters[C_DBG_NOTREADY],
+            (unsigned long long)f->h_counters[C_DBG_DIFF], (unsigned long long)f->h_counters[C_DBG_FULL],
+            (unsigned long long)f->h_counters[C_DBG_BYPASS]);
+    uint32_t nonempty = 0;
+    for (auto t : tot) nonempty += t != 0;
+    fprintf(stderr, "dq_freq finalize: %s chunks=%lld records=%llu s=%d units=%u buckets=%u\n",
+            f->exact ? "exact" : "hashed", (long long)n, (unsigned long long)R, s, u, nonempty);
+  }
+  const int64_t P = (int64_t)kBuckets << s;
+  HIP_TRY(f->part_base.ensure(P + 1));
   HIP_TRY(f->unit_start.ensure(kBuckets + 1));
-  HIP_TRY(f->bucket_base.ensure(kBuckets + 1));
   HIP_TRY(hipMemcpy(f->unit_start.p, f->h_unit_start.data(), (kBuckets + 1) * 4,
                     hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(f->bucket_base.p, f->h_bucket_base.data(), (kBuckets + 1) * 8,
-                    hipMemcpyHostToDevice));
-  if (u) {
-    const int hs = (1 << s) + 1;
-    HIP_TRY(f->recsB.ensure(std::max<uint64_t>(R, 1) * f->rb));
-    HIP_TRY(f->histB.ensure((size_t)u * hs));
-    HIP_TRY(f->unit_out.ensure(u));
-    BArgs a;
-    a.recs = f->recs.p;
-    a.lenT = f->lenT.p;
-    a.offT = f->offT.p;
-    a.prefT = f->prefT.p;
-    a.n_chunks = n;
-    a.unit_start = f->unit_start.p;
-    a.bucket_base = f->bucket_base.p;
-    a.s = s;
-    a.hstride = hs;
-    a.recsB = f->recsB.p;
-    a.histB = f->histB.p;
-    a.unit_out = f->unit_out.p;
-    if (f->exact)
-      hipLaunchKernelGGL(freq_phaseB<false>, dim3(u), dim3(kThreads), 0, f->stream, a);
-    else
-      hipLaunchKernelGGL(freq_phaseB<true>, dim3(u), dim3(kThreads), 0, f->stream, a);
-    HIP_TRY(hipGetLastError());
+  if (u == 0) {
+    HIP_TRY(hipMemsetAsync(f->part_base.p, 0, (P + 1) * 8, f->stream));
+    f->b_valid = true;
+    return DQ_OK;
   }
+  const int S = 1 << s;
+  HIP_TRY(f->recsB.ensure(std::max<uint64_t>(R, 1) * f->rb));
+  HIP_TRY(f->unit_c0.ensure(u));
+  HIP_TRY(f->unit_b.ensure(u));
+  HIP_TRY(f->uhist.ensure((size_t)u * S));
+  HIP_TRY(hipMemsetAsync(f->unit_c0.p, 0xFF, (size_t)u * 4, f->stream));
+  hipLaunchKernelGGL(freq_unit_map, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 64), kBuckets),
+                     dim3(256), 0, f->stream, f->prefT.p, n, f->unit_start.p, (uint32_t)H,
+                     f->unit_c0.p, f->unit_b.p);
+  HIP_TRY(hipGetLastError());
+  BArgs a;
+  memset(&a, 0, sizeof(a));
+  a.recs = f->recs.p;
+  a.lenT = f->lenT.p;
+  a.offT = f->offT.p;
+  a.prefT = f->prefT.p;
+  a.n_chunks = n;
+  a.unit_start = f->unit_start.p;
+  a.unit_c0 = f->unit_c0.p;
+  a.unit_b = f->unit_b.p;
+  a.s = s;
+  a.n_units = u;
+  a.uhist = f->uhist.p;
+  a.part_base = f->part_base.p;
+  a.recsB = f->recsB.p;
+  if (f->exact)
+    hipLaunchKernelGGL(freq_phaseB_count<false>, dim3(u), dim3(kThreads), 0, f->stream, a);
+  else
+    hipLaunchKernelGGL(freq_phaseB_count<true>, dim3(u), dim3(kThreads), 0, f->stream, a);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(freq_phaseB_scan, dim3(kBuckets), dim3(kThreads), 0, f->stream, a);
+  HIP_TRY(hipGetLastError());
+  hipLaunchKernelGGL(freq_part_scan, dim3(1), dim3(kThreads), 0, f->stream, f->part_base.p, P);
+  HIP_TRY(hipGetLastError());
+  const unsigned grid = (u + 7) / 8 * 8;
+  if (f->exact)
+    hipLaunchKernelGGL(freq_phaseB_scatter<false>, dim3(grid), dim3(kThreads), 0, f->stream, a);
+  else
+    hipLaunchKernelGGL(freq_phaseB_scatter<true>, dim3(grid), dim3(kThreads), 0, f->stream, a);
+  HIP_TRY(hipGetLastError());
   f->b_valid = true;
   return DQ_OK;
 }
@@ -1295,12 +1568,8 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     CArgs a;
     memset(&a, 0, sizeof(a));
     a.recsB = f->recsB.p;
-    a.histB = f->histB.p;
-    a.hstride = (1 << f->s_bits) + 1;
+    a.part_base = f->part_base.p;
     a.s = f->s_bits;
-    a.unit_out = f->unit_out.p;
-    a.unit_start = f->unit_start.p;
-    a.bucket_base = f->bucket_base.p;
     a.arena = f->arena.p;
     for (int k = 0; k < f->n_keys; ++k) a.types[k] = f->types[k];
     a.n_keys = f->n_keys;
@@ -1318,12 +1587,16 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     a.entries = nullptr;
     a.ovf_out = f->ovf_a.p;
     a.ovf_n = f->ovf_n.p;
-    unsigned grid = (unsigned)P;
+    a.n_work = (int32_t)P;
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, f->device);
+    const unsigned persistent = (unsigned)std::max(1, cus * 2);
+    unsigned grid = (unsigned)std::min<int64_t>(P, persistent);
     for (int round = 0; round < 24; ++round) {
       if (f->exact)
-        hipLaunchKernelGGL(freq_phaseC<false>, dim3(grid), dim3(kThreads), 0, f->stream, a);
+        hipLaunchKernelGGL(freq_phaseC<false>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else
-        hipLaunchKernelGGL(freq_phaseC<true>, dim3(grid), dim3(kThreads), 0, f->stream, a);
+        hipLaunchKernelGGL(freq_phaseC<true>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
       HIP_TRY(hipGetLastError());
       unsigned int m = 0;
       HIP_TRY(hipStreamSynchronize(f->stream));
@@ -1337,7 +1610,8 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       HIP_TRY(hipMemsetAsync(f->ovf_n.p, 0, 4, f->stream));
       a.entries = f->ovf_b.p;
       a.ovf_out = f->ovf_a.p;
-      grid = m;
+      a.n_work = (int32_t)m;
+      grid = std::min<unsigned>(m, persistent);
     }
   }
   hipLaunchKernelGGL(freq_reduce, dim3(1), dim3(kThreads), 0, f->stream, f->part_groups.p,
@@ -1623,7 +1897,7 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
   f->num_rows += rows;
   invalidate(f);
   if (rows == 0) return DQ_OK;
-  const int64_t chunks = (rows + f->tile - 1) / f->tile;
+  const int64_t chunks = phaseA_chunks(!f->exact, false, rows, f->tile, nullptr);
   dq_status st = ensure_chunks(f, chunks);
   if (st != DQ_OK) return st;
   if (!f->exact) {
@@ -1648,8 +1922,8 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     a.ks.cols[k] = KeyCol{keys[k].type, 0, keys[k].validity, keys[k].values, keys[k].data};
   a.n_items = rows;
   a.tile_items = f->tile;
-  if (f->exact) launch_phaseA<false>(f, a, chunks, false);
-  else launch_phaseA<true>(f, a, chunks, false);
+  if (f->exact) launch_phaseA<false>(f, a, false);
+  else launch_phaseA<true>(f, a, false);
   HIP_TRY(hipGetLastError());
   f->n_chunks += chunks;
   return pull_counters(f);
@@ -1924,7 +2198,7 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
   invalidate(f);
   if (total_rec) {
     const int64_t per = f->tile / 32;  // a record's count becomes at most 32 records
-    const int64_t chunks = (total_rec + per - 1) / per;
+    const int64_t chunks = phaseA_chunks(!f->exact, true, total_rec, per, nullptr);
     st = ensure_chunks(f, chunks);
     if (st != DQ_OK) return st;
     a = [&] {
@@ -1944,8 +2218,8 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
     a.rin = reinterpret_cast<const RecIn*>(records);
     a.n_items = total_rec;
     a.tile_items = per;
-    if (f->exact) launch_phaseA<false>(f, a, chunks, true);
-    else launch_phaseA<true>(f, a, chunks, true);
+    if (f->exact) launch_phaseA<false>(f, a, true);
+    else launch_phaseA<true>(f, a, true);
     HIP_TRY(hipGetLastError());
     f->n_chunks += chunks;
   }

@@ -230,6 +230,32 @@ DQ_HD void row_encode(const KeySet& ks, int64_t r, uint32_t* dst) {
   }
 }
 
+// n bytes at a and b equal?  8-, 4-, 2-, 1-byte unaligned loads, never past either string.
+DQ_HD bool bytes_equal(const uint8_t* a, const uint8_t* b, int32_t n) {
+  int32_t q = 0;
+  for (; q + 8 <= n; q += 8) {
+    uint64_t x, y;
+    __builtin_memcpy(&x, a + q, 8);
+    __builtin_memcpy(&y, b + q, 8);
+    if (x != y) return false;
+  }
+  if (q + 4 <= n) {
+    uint32_t x, y;
+    __builtin_memcpy(&x, a + q, 4);
+    __builtin_memcpy(&y, b + q, 4);
+    if (x != y) return false;
+    q += 4;
+  }
+  if (q + 2 <= n) {
+    uint16_t x, y;
+    __builtin_memcpy(&x, a + q, 2);
+    __builtin_memcpy(&y, b + q, 2);
+    if (x != y) return false;
+    q += 2;
+  }
+  return q == n || a[q] == b[q];
+}
+
 // Are two keyed rows (of the same batch) the same group?
 DQ_HD bool rows_equal(const KeySet& ks, int64_t r1, int64_t r2) {
   for (int k = 0; k < ks.n_keys; ++k) {
@@ -241,8 +267,7 @@ DQ_HD bool rows_equal(const KeySet& ks, int64_t r1, int64_t r2) {
       if (!v1) continue;
       if (a.len != b.len) return false;
       if (a.p && b.p) {
-        for (int32_t q = 0; q < a.len; ++q)
-          if (a.p[q] != b.p[q]) return false;
+        if (!bytes_equal(a.p, b.p, a.len)) return false;
       } else {
         for (int32_t q = 0; q < a.len; ++q)
           if (sv_byte(a, q) != sv_byte(b, q)) return false;

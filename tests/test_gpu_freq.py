@@ -254,3 +254,30 @@ def test_topk_matches_oracle_order(n, k, col, gpu_device):
     for (key,), c in got:
         assert exp[key] == c
     assert ft.count() == len(exp)
+
+
+@pytest.mark.parametrize("target", ["1", "7", "1000000000"])
+def test_partition_depths_and_recount(target, gpu_device, monkeypatch):
+    """The partition sizing at both extremes: target 1 drives s to its maximum (10 sub-bucket
+    bits) on a small table, and a huge target keeps s = 0 so that 600K distinct keys overflow the
+    512 partitions' LDS tables and take the recount path.  Results must not change."""
+    from oracle import deequ_oracle as O
+    monkeypatch.setenv("DQ_FREQ_PARTITION_TARGET", target)
+    n = 600_000 if target == "1000000000" else 60_000
+    rng = np.random.default_rng(int(target) % 97)
+    ids = rng.permutation(n).astype(np.int64)
+    ids[: n // 10] = ids[n // 10: n // 5]          # some repeats
+    words = np.array([f"w{v}" for v in ids])
+    t = pa.table({"id": pa.array(ids), "s": pa.array(words)})
+    for cols in (("id",), ("s",)):
+        ft = _freq_table(t, list(cols), gpu_device)
+        s = ft.summarize()
+        exp = {}
+        for v in t.column(cols[0]).to_pylist():
+            exp[v] = exp.get(v, 0) + 1
+        assert s.n_groups == len(exp)
+        assert s.n_unique == sum(1 for c in exp.values() if c == 1)
+        got = {k[0]: c for k, c in ft.export()}
+        assert got == exp
+        top = ft.topk(5)
+        assert [c for _, c in top] == sorted(exp.values(), reverse=True)[:5]
