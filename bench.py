@@ -93,10 +93,26 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: relaunch under torch.distributed.run as a CHILD process, before this
+        # process touches the GPU, and exit with its code
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+               str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and int(os.environ.get("RANK", "0")) == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)",
+              file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -190,6 +206,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / PEAK_HBM,
                 "traffic": load_traffic(args.rows, b_alg),
+                "traffic_source": "profiles/traffic_s10.json: HBM bytes per scan launch from a "
+                                  "separate rocprofv3 --pmc pass on this workload (not this run)",
                 "algorithmic_bytes_per_launch": b_alg,
                 "scan_ms": scan_ms,
                 "kernel": "dq::scan_mixed_kernel (+ finalize1/finalize2)",

@@ -133,6 +133,33 @@ class FrequencyTable:
         return out
 
 
+class KeyedFrequencies:
+    """The grouping of one column read off its Histogram-mode table (NULL as a group): the keyed
+    groups only, as ``SELECT col, COUNT(*) ... WHERE col IS NOT NULL GROUP BY col`` would give
+    (GroupingAnalyzers.scala:62-65).  Valid when the two group-bys put the same non-NULL rows in
+    the same groups -- see Histogram.table_serves_grouping."""
+
+    def __init__(self, table: FrequencyTable):
+        self.table = table
+        self.key_columns = table.key_columns
+        self.key_types = table.key_types
+
+    @property
+    def num_rows(self) -> int:
+        return self.table.num_rows
+
+    def summarize(self) -> N.dq_freq_summary:
+        s = N.dq_freq_summary()
+        N.check(N.lib.dq_freq_summarize_keys(self.table.handle, ctypes.byref(s)))
+        return s
+
+    def export(self) -> List[Tuple[tuple, int]]:
+        return [(k, c) for k, c in self.table.export() if k != (None,)]
+
+    def count(self) -> int:
+        return int(self.summarize().n_groups)
+
+
 def _decode_fixed(t: int, v: int):
     if t == N.FLOAT64:
         return struct.unpack("<d", struct.pack("<Q", v))[0]
@@ -464,9 +491,27 @@ class Histogram(Analyzer):
     def preconditions(self):
         return [self._param_check, Preconditions.has_column(self.column)]
 
+    @staticmethod
+    def table_serves_grouping(data, column: str) -> bool:
+        """Can this column's Histogram table also serve its grouping (Uniqueness, Distinctness,
+        Entropy, ... on [column])?  Integral and boolean columns always: their NULL rows form a
+        separate group the keyed view drops.  A string column only without NULLs (a NULL would
+        merge with a "NullValue" string).  Floating-point never: Histogram folds NaN payloads
+        (cast to string), the grouping does not."""
+        dtype = data.schema[column].dtype
+        if dtype in (N.BOOL, N.INT8, N.INT16, N.INT32, N.INT64):
+            return True
+        if dtype == N.UTF8:
+            return all(b[column].validity is None for b in data.batches)  # no bitmap: no NULLs
+        return False
+
     def compute_state_from(self, data):
-        total = data.count()
+        from ..distributed import compute_frequencies_distributed, is_distributed
         dtype = data.schema[self.column].dtype
+        if is_distributed(data):  # each rank's partial groupBy, repartitioned by owner rank
+            st = compute_frequencies_distributed(data, [self.column], null_as_group=True)
+            return HistogramState(st.frequencies, st.num_rows, dtype, self.binning_udf)
+        total = data.count()
         table = FrequencyTable([self.column], [dtype], data.device_index())
         for batch in data.batches:
             table.add([batch[self.column]], null_as_group=True)
@@ -495,7 +540,7 @@ class Histogram(Analyzer):
         return HistogramMetric(self.column, Failure(wrap_if_necessary(exception)))
 
 
-__all__ = ["FrequencyTable", "FrequenciesAndNumRows", "compute_frequencies",
+__all__ = ["FrequencyTable", "KeyedFrequencies", "FrequenciesAndNumRows", "compute_frequencies",
            "FrequencyBasedAnalyzer", "ScanShareableFrequencyBasedAnalyzer", "Uniqueness",
            "Distinctness", "UniqueValueRatio", "CountDistinct", "Entropy", "Histogram",
            "HistogramState", "java_double_to_string", "java_float_to_string", "cast_to_string"]

@@ -334,6 +334,10 @@ struct TaskPlan {
   StrIn str;
   int out = 0;
   int hll_out = -1;
+  // TK_COMOMENTS fused with an ApproxCountDistinct of one of its columns (BC_CORR_HLL): the HLL
+  // task's register file and which column it hashes (0 = col, 1 = col2)
+  int fused_hll = -1, hll_side = 0;
+  bool carried = false;  // TK_HLL whose rows a fused co-moment task hashes: no items of its own
 };
 
 struct MatExpr {
@@ -369,7 +373,7 @@ static int body_class(const dq_plan* p, const TaskPlan& t) {
     case TK_VALIDITY:
     case TK_BOOLMAP: return BC_BITS;
     case TK_STR_IN: return BC_STR_IN;
-    case TK_COMOMENTS: return BC_CORR;
+    case TK_COMOMENTS: return t.fused_hll >= 0 ? BC_CORR_HLL : BC_CORR;
     default: return BC_HLL;
   }
 }
@@ -575,6 +579,23 @@ extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
     if (s.task >= 0) s.task = remap[s.task];
   for (const TaskPlan& t : p->tasks)
     if (t.kind == TK_HLL || t.kind == TK_COMOMENTS) p->full = true;
+  // ApproxCountDistinct(c) beside Correlation(c, d) or (d, c) under the same where: one pass reads
+  // both columns and feeds the co-moments and c's HLL registers (BC_CORR_HLL).  8-byte columns
+  // only (the vector path both bodies share).  DQ_NO_FUSE=1 keeps two passes (A/B measurement).
+  if (!getenv("DQ_NO_FUSE")) {
+    auto wide = [&](int col) { return p->types[col] == DQ_INT64 || p->types[col] == DQ_FLOAT64; };
+    for (TaskPlan& h : p->tasks) {
+      if (h.kind != TK_HLL || !wide(h.col)) continue;
+      for (TaskPlan& c : p->tasks) {
+        if (c.kind != TK_COMOMENTS || c.fused_hll >= 0 || c.where != h.where) continue;
+        if (!wide(c.col) || !wide(c.col2) || (c.col != h.col && c.col2 != h.col)) continue;
+        c.fused_hll = h.hll_out;
+        c.hll_side = c.col == h.col ? 0 : 1;
+        h.carried = true;
+        break;
+      }
+    }
+  }
   // each workgroup keeps every HLL task's 512 registers in LDS (2 KiB per task)
   if (p->n_hll > 32)
     return fail(DQ_ERR_UNSUPPORTED, "%d ApproxCountDistinct aggregations in one plan (max 32)",
@@ -607,9 +628,12 @@ extern "C" dq_status dq_plan_explain(const dq_plan* plan, char* buf, size_t buf_
     s += line;
   }
   for (const TaskPlan& t : plan->tasks) {
-    snprintf(line, sizeof(line), "task[%d] %s col=%d col2=%d where=%d preds=%d list=%zu%s\n", t.out,
+    char fused[64] = "";
+    if (t.fused_hll >= 0) snprintf(fused, sizeof(fused), " +hll[%d] of col%s", t.fused_hll, t.hll_side ? "2" : "");
+    if (t.carried) snprintf(fused, sizeof(fused), " (rows hashed by a fused co-moment pass)");
+    snprintf(line, sizeof(line), "task[%d] %s col=%d col2=%d where=%d preds=%d list=%zu%s%s\n", t.out,
              kind_name(t.kind), t.col, t.col2, t.where, t.n_preds, t.str.list.size(),
-             t.bool_expr >= 0 ? " (expr bitmap)" : "");
+             t.bool_expr >= 0 ? " (expr bitmap)" : "", fused);
     s += line;
   }
   snprintf(line, sizeof(line), "launches per batch: %d\n", dq_plan_launches_per_batch(plan));
@@ -625,15 +649,17 @@ extern "C" int dq_plan_launches_per_batch(const dq_plan* plan) {
   int classes = 0, hll = 0;
   for (int c = 0; c < kBodyClasses; ++c) {
     bool used = false;
-    for (const TaskPlan& t : plan->tasks) used = used || body_class(plan, t) == c;
-    if (c == BC_HLL) hll = used ? 1 : 0;
+    for (const TaskPlan& t : plan->tasks) used = used || (body_class(plan, t) == c && !t.carried);
+    if (c == BC_HLL || c == BC_CORR_HLL) hll += used ? 1 : 0;
     else classes += used ? 1 : 0;
   }
   // two or more body classes share one mixed launch (dq_scan_device_batches); HLL joins it when
   // its LDS registers fit (kMixedHllMax)
-  if (hll && plan->n_hll <= kMixedHllMax && classes >= 1) {
+  bool hll_alone = false;  // an unfused HLL task (it may join the mixed launch)
+  for (const TaskPlan& t : plan->tasks) hll_alone = hll_alone || (t.kind == TK_HLL && !t.carried);
+  if (hll_alone && plan->n_hll <= kMixedHllMax && classes >= 1) {
     classes += 1;
-    hll = 0;
+    hll -= 1;
   }
   if (classes >= 2 && !getenv("DQ_NO_MIXED")) classes = 1;
   // expression bitmaps + the scan launches + the two finalize launches
@@ -709,7 +735,7 @@ static dq_status upload_host(dq_state* s) {
     HIP_TRY(hipMemcpy(s->d_acc.p, s->acc.data(), s->acc.size() * sizeof(Acc), hipMemcpyHostToDevice));
   if (!s->hll.empty())
     HIP_TRY(hipMemcpy(s->d_hll.p, s->hll.data(), s->hll.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(s->d_queue.p, 0, kQueues * sizeof(uint32_t)));
+  HIP_TRY(hipMemset(s->d_queue.p, 0, kQueueWords * sizeof(uint32_t)));
   HIP_TRY(hipMemset(s->d_hll_stage.p, 0, s->d_hll_stage.n * sizeof(uint32_t)));
   s->host_dirty = false;
   return DQ_OK;
@@ -746,7 +772,7 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
   HIP_TRY(s->d_acc.ensure(nt));
   HIP_TRY(s->d_hll.ensure(std::max(1, plan->n_hll) * (size_t)kHllM));
   HIP_TRY(s->d_hll_stage.ensure(std::max(1, plan->n_hll) * (size_t)kHllM));
-  HIP_TRY(s->d_queue.ensure(kQueues));
+  HIP_TRY(s->d_queue.ensure(kQueueWords));
   HIP_TRY(s->d_partial.ensure(1024));
   HIP_TRY(s->d_partial2.ensure(nt * (size_t)kFinParts));
   for (int k = 0; k < 2; ++k) HIP_TRY(hipEventCreateWithFlags(&s->ev[k], hipEventDisableTiming));
@@ -999,7 +1025,8 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
       t.kind = tp.kind;
       t.body = body_class(plan, tp);
       t.out = tp.out;
-      t.hll_out = tp.hll_out;
+      t.hll_out = tp.kind == TK_COMOMENTS ? tp.fused_hll : tp.hll_out;
+      t.hll_side = tp.hll_side;
       t.batch = b;
       t.rows = rows[b];
       t.w_val = mat_val(tp.where, b);
@@ -1075,7 +1102,8 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
       int64_t item_rows = pow2_at_least((int64_t)(kItemBytes / std::max(bpr, 1e-3)));
       item_rows = std::max<int64_t>(kItemAlign, std::min<int64_t>(item_rows, (int64_t)1 << 22));
       t.item_rows = item_rows;
-      t.n_items = rows[b] > 0 ? (rows[b] + item_rows - 1) / item_rows : 0;
+      // a carried HLL task keeps its (empty) descriptors: finalize finds the task through them
+      t.n_items = rows[b] > 0 && !tp.carried ? (rows[b] + item_rows - 1) / item_rows : 0;
       t.item_begin = total_items;
       total_items += t.n_items;
       td[d] = t;
@@ -1095,7 +1123,8 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
   {
     std::vector<ScanLaunch> plain, hll;
     for (const ScanLaunch& L : launches)
-      (L.body == BC_HLL && !s->mix_hll ? hll : plain).push_back(L);
+      // the fused body keeps HLL registers in LDS too, and the mixed kernel has no such body
+      ((L.body == BC_HLL && !s->mix_hll) || L.body == BC_CORR_HLL ? hll : plain).push_back(L);
     if (plain.size() >= 2 && !getenv("DQ_NO_MIXED")) {
       std::vector<uint32_t> sig;
       for (const ScanLaunch& L : plain) {

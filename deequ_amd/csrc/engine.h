@@ -58,7 +58,8 @@ struct NumPred {
 struct TaskDesc {
   int32_t kind, type, type2, n_preds;
   int32_t out;            // logical task = accumulator index
-  int32_t hll_out;        // HLL register-file index of the logical task (TK_HLL), else -1
+  int32_t hll_out;        // HLL register-file index of the logical task (TK_HLL) or of the HLL
+                          // task a BC_CORR_HLL descriptor also fills, else -1
   int32_t batch;          // batch index of this descriptor
   int32_t negate;         // TK_STR_IN: NOT IN
   int32_t null_is_true;   // TK_STR_IN: IS NULL OR ...
@@ -66,6 +67,7 @@ struct TaskDesc {
   int32_t vec_ok;         // buffers aligned for the vector path
   int32_t list_small;     // TK_STR_IN: <= 8 entries, each <= 7 bytes (packed-key compare path)
   int32_t body;           // scan body class (kernels.h BodyClass)
+  int32_t hll_side;       // BC_CORR_HLL: the column the fused HLL task hashes (0 = x, 1 = y)
   uint64_t list_lenmask;  // TK_STR_IN small lists: bit L set when an entry has length L
   // TK_STR_IN small lists: entry k as (bytes, zero-padded) | length << 56; unused = 0xFE << 56
   // (a row of 8+ bytes keys to ~0, so it matches neither an entry nor an unused slot)

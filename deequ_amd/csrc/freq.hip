@@ -255,6 +255,11 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
   __shared__ uint32_t bh[kBuckets], bcur[kBuckets];
   __shared__ uint64_t dkey[D], dcnt[D];
   __shared__ uint64_t drep[HASHED ? D : 1];
+  // one-column utf8 keys: the short forms (str_short_key) of the slots' keys and the tile's rows,
+  // so most hits are decided in LDS instead of re-reading both strings
+  constexpr bool SK = HASHED && !FROM_REC;
+  __shared__ uint64_t dsk[SK ? D : 1];
+  __shared__ uint64_t ssk[SK ? T : 1];
   __shared__ uint32_t s_wave[kThreads / 64];
   __shared__ uint64_t s_red[kThreads / 64];
   __shared__ uint32_t s_hits, s_bypass;
@@ -325,7 +330,8 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
   };
   // LDS dedupe: 0 = not counted (table full), 1 = claimed a new slot, 2 = added to an existing
   // slot, 3 = the key's slot is being claimed: retry after the next barrier
-  auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep) -> int {
+  const bool one_str = a.ks.n_keys == 1 && a.ks.cols[0].type == DQ_UTF8;  // block-uniform
+  auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep, uint64_t sk) -> int {
     if (h == kEmptyKey) return 0;
     uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
     for (int pr = 0; pr < 4; ++pr) {
@@ -337,6 +343,10 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
         else k = prev;
       }
       if (claimed) {
+        if constexpr (SK) {
+          lds_store(&dsk[slot], sk);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // dsk before drep
+        }
         if (HASHED) lds_store(&drep[slot], rep);
         atomicAdd((unsigned long long*)&dcnt[slot], c);
         return 1;
@@ -350,7 +360,11 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
             return 3;
           }
           if (r2 != rep) {
-            if constexpr (FROM_REC)
+            if constexpr (SK) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const uint64_t sk2 = SK ? lds_load(&dsk[slot]) : kNoShort;
+            if (sk != kNoShort || sk2 != kNoShort)
+              same = sk == sk2;
+            else if constexpr (FROM_REC)
               same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
                                reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
             else
@@ -388,6 +402,16 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
         stash[q * W] = HASHED ? r.key : fmix_bij(r.key);
         if (HASHED) stash[q * W + 1] = a.var_arena_base + (uint64_t)seg_var_base(a.segs, i) + r.enc_off;
         if (r.count) keyed |= 1u << j;
+      } else if (SK && one_str) {  // one utf8 column: no per-column loops
+        SView v;
+        if (!key_str(a.ks, 0, i, v)) {
+          ++nulls;
+        } else {
+          keyed |= 1u << j;
+          stash[q * W] = str_row_hash(v);
+          stash[q * W + 1] = (uint64_t)i;
+          ssk[q] = str_short_key(v);
+        }
       } else {
         const int kind = row_kind(a.ks, i, !HASHED);
         if (kind == ROW_SKIP) {
@@ -398,6 +422,7 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
           keyed |= 1u << j;
           stash[q * W] = HASHED ? row_hash_hashed(a.ks, i) : row_hash_exact(a.ks, i);
           if (HASHED) stash[q * W + 1] = (uint64_t)i;  // the row until it is encoded
+          if constexpr (SK) ssk[q] = kNoShort;
         }
       }
     }
@@ -422,7 +447,7 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
             const int q = j * kThreads + tid;
             const uint64_t h = stash[q * W], rep = stash[q * W + 1];
             const uint64_t c = FROM_REC ? scnt[tid] : 1;
-            const int res = dedupe(h, c, rep);
+            const int res = dedupe(h, c, rep, SK ? ssk[q] : kNoShort);
             if (res == 3) continue;
             w &= ~(1u << j);
             if (res == 2) ++hits;
@@ -441,7 +466,7 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
         const uint64_t h = stash[q * W];
         const uint64_t rep = HASHED ? stash[q * W + 1] : 0;
         const uint64_t c = FROM_REC ? scnt[tid] : 1;
-        const int res = on ? dedupe(h, c, rep) : 0;
+        const int res = on ? dedupe(h, c, rep, SK ? ssk[q] : kNoShort) : 0;
         if (res == 3) wait |= 1u << j;
         else if (res == 2) ++hits;
         else if (!res) count_raw(j, h, c);
@@ -1948,6 +1973,19 @@ extern "C" dq_status dq_freq_summarize(dq_freq* f, dq_freq_summary* out) {
   out->n_unique = u;
   out->n_null_key_rows = (int64_t)f->h_counters[C_NULL_ROWS];
   out->entropy = e;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_freq_summarize_keys(dq_freq* f, dq_freq_summary* out) {
+  if (!f || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  HIP_TRY(hipSetDevice(f->device));
+  dq_status st = finalize_c(f, false, false);
+  if (st != DQ_OK) return st;
+  out->num_rows = f->num_rows;
+  out->n_groups = (int64_t)f->st_groups;
+  out->n_unique = (int64_t)f->st_unique;
+  out->n_null_key_rows = (int64_t)(f->h_counters[C_NULL_ROWS] + f->h_counters[C_NULL_GROUP]);
+  out->entropy = f->st_entropy;
   return DQ_OK;
 }
 

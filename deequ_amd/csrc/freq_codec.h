@@ -168,21 +168,41 @@ DQ_HD uint64_t row_hash_exact(const KeySet& ks, int64_t r) { return fmix_bij(exa
 
 // Composite 64-bit hash of a keyed row (hashed mode): per column XXH64 with a per-column seed,
 // folded with an XXH64 merge step, then fmix.
+constexpr uint64_t kRowHashSeed = 0x243F6A8885A308D3ULL;
+DQ_HD uint64_t fold_col_hash(uint64_t h, uint64_t ch) { return rotl64(h ^ ch, 27) * P1 + P4; }
+DQ_HD uint64_t str_col_hash(const SView& v, int k) {
+  return v.p ? xxh_bytes(MemBytes{v.p}, (int64_t)v.len, 17 + k) : kNullValueXxh17;
+}
+
 DQ_HD uint64_t row_hash_hashed(const KeySet& ks, int64_t r) {
-  uint64_t h = 0x243F6A8885A308D3ULL;
+  uint64_t h = kRowHashSeed;
   for (int k = 0; k < ks.n_keys; ++k) {
     const KeyCol& c = ks.cols[k];
     uint64_t ch;
     if (c.type == DQ_UTF8) {
       SView v;
       key_str(ks, k, r, v);
-      ch = v.p ? xxh_bytes(MemBytes{v.p}, (int64_t)v.len, 17 + k) : kNullValueXxh17;
+      ch = str_col_hash(v, k);
     } else {
       ch = xxh_long(kwiden(c.type, c.values, r), 17 + k);
     }
-    h = rotl64(h ^ ch, 27) * P1 + P4;
+    h = fold_col_hash(h, ch);
   }
   return fmix_bij(h);
+}
+
+// The row hash of a one-column utf8 key (row_hash_hashed with n_keys == 1).
+DQ_HD uint64_t str_row_hash(const SView& v) { return fmix_bij(fold_col_hash(kRowHashSeed, str_col_hash(v, 0))); }
+
+// Short form of a one-column utf8 key of at most 7 bytes: its bytes and its length in one word,
+// so two short keys are equal iff their words are; kNoShort for every other key (the 9-byte
+// "NullValue" literal included), which is never equal to a short key.
+constexpr uint64_t kNoShort = ~0ULL;
+DQ_HD uint64_t str_short_key(const SView& v) {
+  if (!v.p || v.len > 7) return kNoShort;
+  uint64_t w = 0;
+  for (int32_t q = 0; q < v.len; ++q) w |= (uint64_t)v.p[q] << (8 * q);
+  return w | ((uint64_t)v.len << 56);
 }
 
 DQ_HD uint32_t pad4(uint32_t n) { return (n + 3u) & ~3u; }

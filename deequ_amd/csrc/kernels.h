@@ -101,12 +101,20 @@ enum BodyClass : int32_t {
   BC_STR_IN,
   BC_CORR,
   BC_HLL,
+  BC_CORR_HLL,  // TK_COMOMENTS task that also fills an HLL task's registers from one of its columns
   kBodyClasses
 };
 // A launch of the mixed kernel: every non-HLL body class in one grid, items taken in an
 // interleaved order so latency-bound bodies (string gathers) overlap bandwidth-bound ones.
 constexpr int kBodyMixed = kBodyClasses;
-constexpr int kQueues = kBodyClasses + 1;  // one work counter per launch kind
+constexpr int kQueues = kBodyClasses + 1;  // one work queue per launch kind
+// A queue is kQueueHeads head words, one per XCD, each on its own 128-byte line: the items of a
+// launch are cut into kQueueHeads contiguous slices and a wave dequeues from the slice of its
+// workgroup's XCD first (one device-scope head saturates at ~88 dequeues/us with 256 CUs pulling;
+// MI355X_MICROARCH.md "dequeue"), then drains the other slices in turn.
+constexpr int kQueueHeads = 8;
+constexpr int kQueueStride = 32;  // u32 words between heads
+constexpr int kQueueWords = kQueues * kQueueHeads * kQueueStride;
 
 // One scan launch: the items [item_lo, item_hi) of every task of body class `body`.
 struct ScanLaunch {
@@ -127,7 +135,7 @@ constexpr int kMixedHllMax = 0;
 // Fused scan over n_desc (task, batch) descriptors numbered class-major then task-major (each
 // logical task owns one contiguous range of work items), one launch per entry of `launches`, then
 // the two finalize launches that fold the item partials into acc[n_tasks] / hll_acc.
-// queues[kQueues] must be 0 on entry (finalize re-arms them), `partial` holds one record per
+// queues[kQueueWords] must be 0 on entry (finalize re-arms them), `partial` holds one record per
 // item, `partial2` n_tasks * kFinParts, `hll_stage` n_hll * kHllM zeroed u32 registers (finalize
 // clears them again).
 hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const ScanLaunch* launches,

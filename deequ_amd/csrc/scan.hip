@@ -528,26 +528,9 @@ DQ_DEV double as_f64(uint64_t bits, bool is_long) {
   return is_long ? (double)(int64_t)bits : __builtin_bit_cast(double, bits);
 }
 
-DQ_DEV void corr_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int64_t& n, double* c) {
-  const int l = lane_id();
-  const uint64_t* X = reinterpret_cast<const uint64_t*>(t.values) + r0 + 2 * l;
-  const uint64_t* Y = reinterpret_cast<const uint64_t*>(t.values2) + r0 + 2 * l;
-  uint4 qx[8], qy[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    qx[k] = ld16(X + 128 * k);
-    qy[k] = ld16(Y + 128 * k);
-  }
-  const int64_t w0 = (r0 >> 5) + (l >> 4);
-  const uint32_t sh = (uint32_t)(2 * l) & 31u;
-  uint32_t sel = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int64_t w = w0 + 4 * k;
-    uint32_t s = bits32(t.valid, w) & bits32(t.valid2, w);
-    if (t.w_val) s &= bits32(t.w_val, w) & bits32(t.w_vld, w);
-    sel |= ((s >> sh) & 3u) << (2 * k);
-  }
+// The co-moments of a lane's 16 rows (bit i of sel: row i selected) merged into (n, c).
+DQ_DEV void corr_fold16(const uint4* qx, const uint4* qy, uint32_t sel, bool xl, bool yl, int64_t& n,
+                        double* c) {
   const int nb = __popc(sel);
   if (!nb) return;
   double xs[16], ys[16];
@@ -587,7 +570,37 @@ DQ_DEV void corr_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int64_t
   n += nb;
 }
 
-DQ_DEV void corr_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& acc) {
+DQ_DEV void corr_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int64_t& n, double* c) {
+  const int l = lane_id();
+  const uint64_t* X = reinterpret_cast<const uint64_t*>(t.values) + r0 + 2 * l;
+  const uint64_t* Y = reinterpret_cast<const uint64_t*>(t.values2) + r0 + 2 * l;
+  uint4 qx[8], qy[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    qx[k] = ld16(X + 128 * k);
+    qy[k] = ld16(Y + 128 * k);
+  }
+  const int64_t w0 = (r0 >> 5) + (l >> 4);
+  const uint32_t sh = (uint32_t)(2 * l) & 31u;
+  uint32_t sel = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t w = w0 + 4 * k;
+    uint32_t s = bits32(t.valid, w) & bits32(t.valid2, w);
+    if (t.w_val) s &= bits32(t.w_val, w) & bits32(t.w_vld, w);
+    sel |= ((s >> sh) & 3u) << (2 * k);
+  }
+  corr_fold16(qx, qy, sel, xl, yl, n, c);
+}
+
+DQ_DEV void hll_update(uint32_t* regs, uint64_t h);
+DQ_DEV void corr_hll_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int64_t& n, double* c,
+                            uint32_t* regs);
+
+// HLL = true (BC_CORR_HLL): the same pass also feeds the rows of column t.hll_side into the HLL
+// registers `regs` of the fused ApproxCountDistinct task.
+template <bool HLL>
+DQ_DEV void corr_rows(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& acc, uint32_t* regs) {
   const int l = lane_id();
   int64_t n = 0;
   double c[5] = {0, 0, 0, 0, 0};  // xAvg, yAvg, ck, xMk, yMk
@@ -596,7 +609,10 @@ DQ_DEV void corr_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
   const bool y8 = t.type2 == DQ_INT64 || t.type2 == DQ_FLOAT64;
   if (t.vec_ok && x8 && y8) {
     const bool xl = t.type == DQ_INT64, yl = t.type2 == DQ_INT64;
-    for (; r_fast + 1024 <= r_end; r_fast += 1024) corr_chunk8(t, r_fast, xl, yl, n, c);
+    for (; r_fast + 1024 <= r_end; r_fast += 1024) {
+      if constexpr (HLL) corr_hll_chunk8(t, r_fast, xl, yl, n, c, regs);
+      else corr_chunk8(t, r_fast, xl, yl, n, c);
+    }
   }
   for (int64_t r0 = r_fast; r0 < r_end; r0 += 512) {
     double xs[8], ys[8];
@@ -610,13 +626,18 @@ DQ_DEV void corr_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
         xs[i] = 0.0;
         ys[i] = 0.0;
         if (r < r_end) {
-          uint32_t s = bit1(t.valid, r) & bit1(t.valid2, r);
-          if (t.w_val) s &= bit1(t.w_val, r) & bit1(t.w_vld, r);
+          const uint32_t wm = t.w_val ? bit1(t.w_val, r) & bit1(t.w_vld, r) : 1u;
+          const uint32_t s = bit1(t.valid, r) & bit1(t.valid2, r) & wm;
           if (s) {
             xs[i] = load_f64(t.type, t.values, r);
             ys[i] = load_f64(t.type2, t.values2, r);
           }
           sel |= s << i;
+          if constexpr (HLL) {
+            const bool hy = t.hll_side != 0;
+            if (bit1(hy ? t.valid2 : t.valid, r) & wm)
+              hll_update(regs, hash_row(hy ? t.type2 : t.type, hy ? t.values2 : t.values, nullptr, r));
+          }
         }
       }
     }
@@ -650,6 +671,9 @@ DQ_DEV void corr_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
   }
   acc.i[0] = n;
   for (int f = 0; f < 5; ++f) acc.d[f] = c[f];
+}
+DQ_DEV void corr_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& acc) {
+  corr_rows<false>(t, r_begin, r_end, acc, nullptr);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -711,6 +735,77 @@ DQ_DEV void hll_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint32_t
   }
 }
 
+// BC_CORR_HLL vector path: ApproxCountDistinct(x) + Correlation(x, y) (BASELINE.json configs[3])
+// read x and y once.  Loads and co-moments as corr_chunk8; the HLL rows are the non-NULL rows of
+// column t.hll_side (and where), hashed as hll_chunk8 does.
+DQ_DEV void corr_hll_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int64_t& n, double* c,
+                            uint32_t* regs) {
+  const int l = lane_id();
+  const uint64_t* X = reinterpret_cast<const uint64_t*>(t.values) + r0 + 2 * l;
+  const uint64_t* Y = reinterpret_cast<const uint64_t*>(t.values2) + r0 + 2 * l;
+  uint4 qx[8], qy[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    qx[k] = ld16(X + 128 * k);
+    qy[k] = ld16(Y + 128 * k);
+  }
+  const bool hy = t.hll_side != 0;
+  const bool hdbl = (hy ? t.type2 : t.type) == DQ_FLOAT64;
+  const int64_t w0 = (r0 >> 5) + (l >> 4);
+  const uint32_t sh = (uint32_t)(2 * l) & 31u;
+  uint32_t sel = 0, hsel = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t w = w0 + 4 * k;
+    const uint32_t vx = bits32(t.valid, w), vy = bits32(t.valid2, w);
+    const uint32_t wm = t.w_val ? bits32(t.w_val, w) & bits32(t.w_vld, w) : ~0u;
+    sel |= (((vx & vy & wm) >> sh) & 3u) << (2 * k);
+    hsel |= ((((hy ? vy : vx) & wm) >> sh) & 3u) << (2 * k);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint4 q = hy ? qy[k] : qx[k];
+    uint64_t x0 = (uint64_t)q.x | ((uint64_t)q.y << 32);
+    uint64_t x1 = (uint64_t)q.z | ((uint64_t)q.w << 32);
+    if (hdbl) {  // doubleToLongBits: every NaN hashes as the canonical one
+      if (__builtin_bit_cast(double, x0) != __builtin_bit_cast(double, x0)) x0 = 0x7ff8000000000000ULL;
+      if (__builtin_bit_cast(double, x1) != __builtin_bit_cast(double, x1)) x1 = 0x7ff8000000000000ULL;
+    }
+    const uint64_t h0 = xxh_long(x0, 42), h1 = xxh_long(x1, 42);
+    if ((hsel >> (2 * k)) & 1u) hll_update(regs, h0);
+    if ((hsel >> (2 * k + 1)) & 1u) hll_update(regs, h1);
+  }
+  corr_fold16(qx, qy, sel, xl, yl, n, c);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Work queue: kQueueHeads head words per launch kind (kernels.h).  Items [lo, hi) are cut into
+// kQueueHeads contiguous slices; a wave pulls from its home slice (the workgroup's XCD under the
+// round-robin dispatch -- for speed only, any placement is correct), then from the others in
+// turn.  Every call either returns an item or moves to the next slice, so a wave ends after at
+// most kQueueHeads empty pulls, and a queue that was not re-armed just ends every wave.
+// ------------------------------------------------------------------------------------------------
+DQ_DEV bool queue_next(uint32_t* heads, uint32_t lo, uint32_t hi, int home, int& step,
+                       uint32_t& item) {
+  const uint32_t n = hi - lo;
+  while (step < kQueueHeads) {
+    const int x = (home + step) % kQueueHeads;
+    const uint32_t b = lo + (uint32_t)((uint64_t)n * x / kQueueHeads);
+    const uint32_t e = lo + (uint32_t)((uint64_t)n * (x + 1) / kQueueHeads);
+    uint32_t v = 0;
+    if (b < e) {
+      if (lane_id() == 0) v = atomicAdd(&heads[x * kQueueStride], 1u);
+      v = __builtin_amdgcn_readfirstlane(v);
+      if (v < e - b) {
+        item = b + v;
+        return true;
+      }
+    }
+    ++step;
+  }
+  return false;
+}
+
 // ------------------------------------------------------------------------------------------------
 // The scan kernels (persistent; waves pull items from a queue)
 // ------------------------------------------------------------------------------------------------
@@ -726,17 +821,15 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const TaskDesc* __restrict
                                                       Acc* __restrict__ partial,
                                                       uint32_t* __restrict__ hll_stage, int n_hll) {
   extern __shared__ uint32_t hll_lds[];
-  if constexpr (BC == BC_HLL) {
+  constexpr bool kRegs = BC == BC_HLL || BC == BC_CORR_HLL;  // HLL registers in LDS
+  if constexpr (kRegs) {
     for (int i = threadIdx.x; i < n_hll * kHllM; i += kBlock) hll_lds[i] = 0;
     __syncthreads();
   }
   const int l = lane_id();
-  // a wave never runs more items than exist: the loop ends even if the queue was not re-armed
-  for (uint32_t guard = item_lo; guard <= item_hi; ++guard) {
-    uint32_t item = 0;
-    if (l == 0) item = item_lo + atomicAdd(queue, 1u);
-    item = __builtin_amdgcn_readfirstlane(item);
-    if (item >= item_hi) break;
+  int step = 0;
+  uint32_t item = 0;
+  while (queue_next(queue, item_lo, item_hi, (int)(blockIdx.x % kQueueHeads), step, item)) {
     // descriptor = the last one whose first item is <= item (empty descriptors share their
     // first item with the next non-empty one, so they are never selected)
     int lo = 0, hi = n_desc - 1;
@@ -759,18 +852,19 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const TaskDesc* __restrict
     if constexpr (BC == BC_BITS) bits_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_STR_IN) str_in_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_CORR) corr_item(t, r_begin, r_end, a);
+    if constexpr (BC == BC_CORR_HLL) corr_rows<true>(t, r_begin, r_end, a, hll_lds + t.hll_out * kHllM);
     if constexpr (BC == BC_HLL) {
       hll_item(t, r_begin, r_end, hll_lds + t.hll_out * kHllM);
     } else {
       constexpr int kind = BC <= BC_NUM_F64 ? TK_NUMERIC
                            : BC == BC_BITS  ? TK_VALIDITY
-                           : BC == BC_CORR  ? TK_COMOMENTS
+                           : BC == BC_CORR || BC == BC_CORR_HLL ? TK_COMOMENTS
                                             : TK_STR_IN;
       wave_reduce(kind, a);
       if (l == 0) partial[item] = a;
     }
   }
-  if constexpr (BC == BC_HLL) {
+  if constexpr (kRegs) {
     __syncthreads();
     for (int i = threadIdx.x; i < n_hll * kHllM; i += kBlock) {
       const uint32_t v = hll_lds[i];
@@ -778,6 +872,10 @@ __global__ void __launch_bounds__(kBlock) scan_kernel(const TaskDesc* __restrict
     }
   }
 }
+
+// HLL never rides in the mixed launch (kernels.h kMixedHllMax): its XXH64 body compiled in here
+// cost 48 bytes of spilled constants per lane.
+static_assert(kMixedHllMax == 0, "scan_mixed_kernel has no HLL body");
 
 // Mixed launch: the items of every non-HLL body class in one grid.  Queue position q runs item
 // order[q]; the host interleaves the classes' items in proportion to their counts, so at any time
@@ -797,11 +895,9 @@ scan_mixed_kernel(const TaskDesc* __restrict__ tasks, int n_desc, uint32_t n_ord
     __syncthreads();
   }
   const int l = lane_id();
-  for (uint32_t guard = 0; guard <= n_order; ++guard) {
-    uint32_t q = 0;
-    if (l == 0) q = atomicAdd(queue, 1u);
-    q = __builtin_amdgcn_readfirstlane(q);
-    if (q >= n_order) break;
+  int step = 0;
+  uint32_t q = 0;
+  while (queue_next(queue, 0, n_order, (int)(blockIdx.x % kQueueHeads), step, q)) {
     const uint32_t item = order[q];
     int lo = 0, hi = n_desc - 1;
     while (lo < hi) {
@@ -824,7 +920,6 @@ scan_mixed_kernel(const TaskDesc* __restrict__ tasks, int n_desc, uint32_t n_ord
       case BC_BITS: bits_item(t, r_begin, r_end, a); break;
       case BC_STR_IN: str_in_item(t, r_begin, r_end, a); break;
       case BC_CORR: corr_item(t, r_begin, r_end, a); break;
-      case BC_HLL: hll_item(t, r_begin, r_end, mix_lds + t.hll_out * kHllM); continue;
       default: break;
     }
     wave_reduce(t.kind, a);
@@ -910,19 +1005,23 @@ __global__ void __launch_bounds__(64) finalize2_kernel(const TaskDesc* __restric
     for (int f = 0; f < kFinParts; ++f) acc_merge(kind, r, partial2[(int64_t)task * kFinParts + f]);
     acc[task] = r;
   }
-  if (task == 0 && threadIdx.x < kQueues) queue[threadIdx.x] = 0u;
+  if (task == 0)
+    for (int i = threadIdx.x; i < kQueues * kQueueHeads; i += blockDim.x) queue[i * kQueueStride] = 0u;
 }
 
 // ------------------------------------------------------------------------------------------------
 // Host-side launchers
 // ------------------------------------------------------------------------------------------------
-size_t scan_lds_bytes(int body, int n_hll) { return body == BC_HLL ? (size_t)n_hll * kHllM * 4 : 0; }
+size_t scan_lds_bytes(int body, int n_hll) {
+  return body == BC_HLL || body == BC_CORR_HLL ? (size_t)n_hll * kHllM * 4 : 0;
+}
 
 template <int BC>
 static void launch_body(const ScanLaunch& L, const TaskDesc* tasks, int n_desc, int n_hll,
                         uint32_t* queues, Acc* partial, uint32_t* hll_stage, hipStream_t stream) {
   hipLaunchKernelGGL(scan_kernel<BC>, dim3(L.grid), dim3(kBlock), scan_lds_bytes(BC, n_hll), stream,
-                     tasks, n_desc, L.item_lo, L.item_hi, queues + BC, partial, hll_stage, n_hll);
+                     tasks, n_desc, L.item_lo, L.item_hi, queues + BC * kQueueHeads * kQueueStride,
+                     partial, hll_stage, n_hll);
 }
 
 template <int BC>
@@ -945,7 +1044,8 @@ hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const Sca
       const int mix_hll = L.lds_hll;
       hipLaunchKernelGGL(scan_mixed_kernel, dim3(L.grid), dim3(kBlock),
                          (size_t)mix_hll * kHllM * 4, stream, tasks, n_desc, L.item_hi, L.order,
-                         queues + kBodyMixed, partial, hll_stage, mix_hll);
+                         queues + kBodyMixed * kQueueHeads * kQueueStride, partial, hll_stage,
+                         mix_hll);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       continue;
@@ -961,6 +1061,7 @@ hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const Sca
       case BC_STR_IN: launch_body<BC_STR_IN>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       case BC_CORR: launch_body<BC_CORR>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       case BC_HLL: launch_body<BC_HLL>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
+      case BC_CORR_HLL: launch_body<BC_CORR_HLL>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       default: return hipErrorInvalidValue;
     }
     hipError_t e = hipGetLastError();
@@ -987,6 +1088,7 @@ int scan_max_blocks_per_cu(int body, int n_hll) {
     case BC_STR_IN: return occupancy_of<BC_STR_IN>(n_hll);
     case BC_CORR: return occupancy_of<BC_CORR>(n_hll);
     case BC_HLL: return occupancy_of<BC_HLL>(n_hll);
+    case BC_CORR_HLL: return occupancy_of<BC_CORR_HLL>(n_hll);
     case kBodyMixed: {
       int n = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_mixed_kernel, kBlock,

@@ -107,15 +107,24 @@ def freq_partition(table, n_parts: int, stream=None):
     return rec, var, rc, vb, sp
 
 
+def _comm_device(dev):
+    """Where a collective's tensors live: the GPU over RCCL, the host over gloo (CPU tests and the
+    two-ranks-on-one-GPU test)."""
+    import torch.distributed as dist
+    return dev if dist.get_backend() == "nccl" else "cpu"
+
+
 def exchange_segments(rec, var, rec_counts, var_bytes):
     """All-to-all of owner segments (segment j of every rank goes to rank j): one all-to-all of the
     sizes, then one of the fixed records and one of the encoded keys.  Over RCCL each peer pair has
     its own xGMI link, so the exchange runs on all 7 links at once.  Returns the received
-    (records, var, src_rec_counts, src_var_bytes), sources in rank order."""
+    (records, var, src_rec_counts, src_var_bytes) on the device, sources in rank order."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size()
-    dev = rec.device
+    home = rec.device
+    dev = _comm_device(home)
+    rec, var = rec.to(dev), var.to(dev)
     sizes = torch.from_numpy(np.stack([rec_counts, var_bytes], 1).reshape(-1).copy()).to(dev)
     got = torch.empty_like(sizes)
     dist.all_to_all_single(got, sizes)
@@ -129,7 +138,7 @@ def exchange_segments(rec, var, rec_counts, var_bytes):
     if int(np.sum(var_bytes)) or int(src_vb.sum()):
         dist.all_to_all_single(recv_var, var, output_split_sizes=src_vb.tolist(),
                                input_split_sizes=np.asarray(var_bytes).tolist())
-    return recv_rec, recv_var, src_rc, src_vb
+    return recv_rec.to(home), recv_var.to(home), src_rc, src_vb
 
 
 def freq_add_records(table, rec, var, src_rc, src_vb, num_rows: int, special,
@@ -158,7 +167,8 @@ def freq_repartition(local, null_as_group: bool = False):
     world, rank = dist.get_world_size(), dist.get_rank()
     rec, var, rc, vb, sp = freq_partition(local, world)
     recv_rec, recv_var, src_rc, src_vb = exchange_segments(rec, var, rc, vb)
-    tot = torch.tensor([local.num_rows, *sp.tolist()], dtype=torch.int64, device=rec.device)
+    tot = torch.tensor([local.num_rows, *sp.tolist()], dtype=torch.int64,
+                       device=_comm_device(rec.device))
     dist.all_reduce(tot)
     tot = tot.cpu().numpy()
     owned = FrequencyTable(local.key_columns, local.key_types, local.device,
@@ -205,11 +215,44 @@ class DistributedFrequencies:
     def count(self) -> int:
         return int(self.summarize().n_groups)
 
+    def export(self):
+        """Every group of every rank (each group lives on exactly one), rank order."""
+        import torch.distributed as dist
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, self.owned.export())
+        return [g for p in parts for g in p]
 
-def compute_frequencies_distributed(data_shard, grouping_columns):
+    def topk(self, k: int):
+        """Global top-k by count: each group lives on one rank, so the k largest are among the
+        union of the ranks' local top-k (Histogram.scala:78, ties in any order)."""
+        import torch.distributed as dist
+        parts = [None] * dist.get_world_size()
+        dist.all_gather_object(parts, self.owned.topk(k))
+        merged = [g for p in parts for g in p]
+        merged.sort(key=lambda g: -g[1])
+        return merged[:k]
+
+
+def is_distributed(data=None) -> bool:
+    """A row-sharded run: a process group of more than one rank is initialised (and the table was
+    not marked rank-local with ``data.rank_local = True``).  The runners then compute every metric
+    over the union of the ranks' shards."""
+    try:
+        import torch.distributed as dist
+    except ImportError:  # pragma: no cover
+        return False
+    if getattr(data, "rank_local", False):
+        return False
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def compute_frequencies_distributed(data_shard, grouping_columns, null_as_group: bool = False):
     """FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:53-80) over a row-sharded
     table: local partial aggregate on each rank's shard, then freq_repartition."""
-    from .analyzers.grouping import FrequenciesAndNumRows, compute_frequencies
-    local = compute_frequencies(data_shard, grouping_columns).frequencies
-    owned = freq_repartition(local)
+    from .analyzers.grouping import FrequenciesAndNumRows, FrequencyTable
+    types = [data_shard.schema[c].dtype for c in grouping_columns]
+    local = FrequencyTable(grouping_columns, types, data_shard.device_index())
+    for batch in data_shard.batches:
+        local.add([batch[c] for c in grouping_columns], null_as_group=null_as_group)
+    owned = freq_repartition(local, null_as_group)
     return FrequenciesAndNumRows(DistributedFrequencies(owned), owned.num_rows)

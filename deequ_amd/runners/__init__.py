@@ -9,16 +9,19 @@ shareable analyzer, a failing ``from_aggregation_result`` fails only its analyze
 """
 from __future__ import annotations
 
+import dataclasses
 import json
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
 from ..analyzers.base import (Analyzer, GroupingAnalyzer, Preconditions, ScanShareableAnalyzer)
-from ..analyzers.grouping import (FrequenciesAndNumRows, ScanShareableFrequencyBasedAnalyzer,
-                                  compute_frequencies, frequency_row)
+from ..analyzers.grouping import (FrequenciesAndNumRows, Histogram, KeyedFrequencies,
+                                  ScanShareableFrequencyBasedAnalyzer, compute_frequencies,
+                                  frequency_row)
 from ..analyzers.scan import Size
 from ..exceptions import ReusingNotPossibleResultsMissingException
 from ..metrics import DoubleMetric
+from ..distributed import compute_frequencies_distributed, is_distributed, run_scan_distributed
 from .engine import run_scan
 
 
@@ -109,7 +112,16 @@ class AnalysisRunner:
         precondition_failures = _precondition_failure_metrics(failed, schema)
         grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]
         scanning = [a for a in passed if a not in grouping]
-        non_grouped = _run_scanning_analyzers(data, scanning, aggregate_with, save_states_with)
+        shared = _histogram_tables_for_groupings(data, grouping, scanning, aggregate_with,
+                                                 save_states_with)
+        hist_metrics = {}
+        for h in scanning:
+            if isinstance(h, Histogram) and h.column in shared:
+                hist_metrics[h] = h.compute_metric_from(
+                    dataclasses.replace(shared[h.column], binning_udf=h.binning_udf))
+        scanning = [a for a in scanning if a not in hist_metrics]
+        non_grouped = _run_scanning_analyzers(data, scanning, aggregate_with, save_states_with) + \
+            AnalyzerContext(hist_metrics)
 
         num_rows = None
         size_metric = non_grouped.metric(Size())
@@ -121,8 +133,12 @@ class AnalysisRunner:
         for a in grouping:
             groups.setdefault(tuple(sorted(a.grouping_columns())), []).append(a)
         for cols, group in groups.items():
+            state = None
+            if len(cols) == 1 and cols[0] in shared:
+                hs = shared[cols[0]]
+                state = FrequenciesAndNumRows(KeyedFrequencies(hs.frequencies), hs.num_rows)
             n, metrics = _run_grouping_analyzers(data, list(cols), group, aggregate_with,
-                                                 save_states_with, num_rows)
+                                                 save_states_with, num_rows, state)
             grouped = grouped + metrics
             if num_rows is None:
                 num_rows = n
@@ -190,7 +206,9 @@ def _run_scanning_analyzers(data, analyzers: Sequence[Analyzer], aggregate_with,
             offsets = [0]
             for a in shareable:
                 offsets.append(offsets[-1] + len(a.aggregation_functions()))
-            row = run_scan(data, aggregations)  # ONE fused pass (the reference's single Spark job)
+            # ONE fused pass (the reference's single Spark job); over a row-sharded table, every
+            # rank's pass + the all-gather and rank-ordered merge of the states
+            row = (run_scan_distributed if is_distributed(data) else run_scan)(data, aggregations)
             for a, off in zip(shareable, offsets):
                 try:
                     results[a] = a.metric_from_aggregation_result(row, off, aggregate_with,
@@ -205,16 +223,43 @@ def _run_scanning_analyzers(data, analyzers: Sequence[Analyzer], aggregate_with,
     return AnalyzerContext(results)
 
 
+def _histogram_tables_for_groupings(data, grouping, scanning, aggregate_with,
+                                    save_states_with) -> Dict[str, object]:
+    """Histogram(c) and the grouping of [c] (Uniqueness, Entropy, ...) are two group-bys of the
+    same column in the reference (AnalysisRunner.scala:249-277 and 321-323).  Where the Histogram
+    table also yields the grouping exactly (Histogram.table_serves_grouping: the same non-NULL
+    groups), the column is grouped once and both read that table: column -> HistogramState.
+    Not done when states are aggregated or persisted, which keep their own tables."""
+    if aggregate_with is not None or save_states_with is not None or is_distributed(data):
+        return {}
+    grouped = {tuple(a.grouping_columns()) for a in grouping}
+    out: Dict[str, object] = {}
+    for h in scanning:
+        if not isinstance(h, Histogram) or h.column in out or (h.column,) not in grouped:
+            continue
+        if not Histogram.table_serves_grouping(data, h.column):
+            continue
+        try:
+            out[h.column] = h.compute_state_from(data)
+        except Exception:  # noqa: BLE001 -- both analyzers then run (and fail) on their own
+            pass
+    return out
+
+
 def _run_grouping_analyzers(data, grouping_columns, analyzers, aggregate_with, save_states_with,
-                            num_rows_of_data):
+                            num_rows_of_data, state=None):
     """AnalysisRunner.runGroupingAnalyzers (AnalysisRunner.scala:249-277).  The reference's
     groupBy is lazy, so a failure of the grouping surfaces inside the one aggregation over the
     frequencies, whose try fails every analyzer of the grouping (:490-505); the engine's eager
     group-by error is mapped the same way."""
-    try:
-        state = compute_frequencies(data, grouping_columns)
-    except Exception as e:  # noqa: BLE001
-        return None, AnalyzerContext({a: a.to_failure_metric(e) for a in analyzers})
+    if state is None:
+        try:
+            if is_distributed(data):  # local partial groupBy + hash repartition by owner rank
+                state = compute_frequencies_distributed(data, grouping_columns)
+            else:
+                state = compute_frequencies(data, grouping_columns)
+        except Exception as e:  # noqa: BLE001
+            return None, AnalyzerContext({a: a.to_failure_metric(e) for a in analyzers})
     sample = analyzers[0]
     if aggregate_with is not None:
         prev = aggregate_with.load(sample)

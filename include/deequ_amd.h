@@ -291,6 +291,11 @@ typedef struct dq_freq_summary {
   double entropy;
 } dq_freq_summary;
 dq_status dq_freq_summarize(dq_freq* freq, dq_freq_summary* out);
+/* The same aggregation over the keyed groups only: a fixed-width table built with NULL as a group
+ * (Histogram mode) summarised as the grouping of that column would be, its NULL rows dropped
+ * (GroupingAnalyzers.scala:62-65).  Lets one group-by serve Histogram(col) and the
+ * Uniqueness/Distinctness/Entropy grouping of col.  n_null_key_rows counts the NULL rows. */
+dq_status dq_freq_summarize_keys(dq_freq* freq, dq_freq_summary* out);
 
 /* Number of groups currently in the table (NULL group and every distinct key). */
 dq_status dq_freq_num_groups(dq_freq* freq, int64_t* n_groups);

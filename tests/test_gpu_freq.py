@@ -281,3 +281,37 @@ def test_partition_depths_and_recount(target, gpu_device, monkeypatch):
         assert got == exp
         top = ft.topk(5)
         assert [c for _, c in top] == sorted(exp.values(), reverse=True)[:5]
+
+
+@pytest.mark.parametrize("col,nulls", [("id", 0.05), ("id", 0.0), ("s", 0.0)])
+def test_histogram_table_serves_grouping(col, nulls, gpu_device):
+    """The runner groups a column once for Histogram(col) and its grouping analyzers when
+    Histogram.table_serves_grouping holds: the keyed view of the Histogram-mode table
+    (dq_freq_summarize_keys) must equal the grouping table bit for bit, and the metrics of the
+    shared run must equal the oracle's."""
+    from deequ_amd.analyzers import Distinctness, Entropy, Histogram, Uniqueness
+    from deequ_amd.analyzers.grouping import KeyedFrequencies
+    from deequ_amd.runners import AnalysisRunner
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    n = 30_000
+    t = _table(n, seed=77, null_rate=nulls)
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=7_000)
+    assert Histogram.table_serves_grouping(df, col)
+    grouping = _freq_table(t, [col], gpu_device)
+    keyed = KeyedFrequencies(_freq_table(t, [col], gpu_device, null_as_group=True))
+    a, b = grouping.summarize(), keyed.summarize()
+    for f in ("num_rows", "n_groups", "n_unique", "n_null_key_rows"):
+        assert getattr(a, f) == getattr(b, f), f
+    assert a.entropy == b.entropy
+    assert dict(keyed.export()) == dict(grouping.export())
+    assert keyed.count() == grouping.count()
+    suite = [Uniqueness([col]), Distinctness([col]), Entropy(col), Histogram(col)]
+    ctx = AnalysisRunner.do_analysis_run(df, suite)
+    freq = O.frequencies(_otable(t), [col])
+    assert ctx.metric(Uniqueness([col])).value.get() == O.uniqueness(freq, n)
+    assert ctx.metric(Distinctness([col])).value.get() == O.distinctness(freq, n)
+    assert _rel_close(ctx.metric(Entropy(col)).value.get(), O.entropy(freq, n))
+    hist = ctx.metric(Histogram(col)).value.get()
+    exp_bins = len(freq) + (1 if nulls and col == "id" else 0)
+    assert hist.number_of_bins == exp_bins

@@ -210,3 +210,44 @@ def s10_suite():
                        "priority IS NULL OR priority IN ('high','low')"),
             Sum("numViews"), Mean("numViews"), StandardDeviation("numViews"),
             Minimum("numViews"), Maximum("numViews")]
+
+
+@pytest.mark.parametrize("n,null_rate,batch", [(1000, 0.0, None), (50_000, 0.05, 8192),
+                                               (70_001, 0.3, None)])
+def test_fused_hll_and_comoments_match_oracle(n, null_rate, batch, gpu_device):
+    """ApproxCountDistinct(x) beside Correlation(x, y) (BASELINE.json configs[3]) runs as ONE pass
+    (BC_CORR_HLL): the HLL registers must equal the oracle's bit for bit, with the HLL column as
+    either side of the correlation, NaNs in the hashed doubles, NULLs, where filters and row
+    counts off the 1024-row vector chunk."""
+    from deequ_amd.analyzers import ApproxCountDistinct, Correlation
+    from deequ_amd.runners.engine import get_plan, run_scan
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    t = random_table(n, n + 7, null_rate)
+    vals = t.column("b").to_pylist()
+    nulls = np.array([v is None for v in vals])
+    b = np.array([0.0 if v is None else v for v in vals])
+    b[::97] = np.nan                                       # NaN payloads hash as the canonical NaN
+    b[1::97] = np.frombuffer(np.uint64(0x7ff0000000000123).tobytes(), np.float64)[0]
+    t = t.set_column(1, "b", pa.array(b, mask=nulls, type=pa.float64()))
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=batch)
+    ot = oracle_of(t)
+    where = "c > -20"
+    cases = [(ApproxCountDistinct("a"), Correlation("a", "b")),
+             (ApproxCountDistinct("b"), Correlation("a", "b")),
+             (ApproxCountDistinct("a", where), Correlation("b", "a", where))]
+    for hll, corr in cases:
+        aggs = hll.aggregation_functions() + corr.aggregation_functions()
+        explain = get_plan(df.schema, aggs).explain()
+        assert "+hll[" in explain, explain                 # the plan did fuse the two
+        row = run_scan(df, aggs)
+        st = hll.from_aggregation_result(row, 0)
+        assert list(st.words) == O.agg_hll(ot, hll.column, hll.where), str(hll)
+        cst = corr.from_aggregation_result(row, len(hll.aggregation_functions()))
+        exp = O.agg_corr(ot, corr.first_column, corr.second_column, corr.where)
+        if exp[0] == 0:
+            assert cst is None
+        else:
+            assert cst.n == exp[0]
+            ref = exp[3] / math.sqrt(exp[4] * exp[5]) if exp[4] * exp[5] > 0 else float("nan")
+            assert rel_close(cst.metric_value(), ref, 1e-10)

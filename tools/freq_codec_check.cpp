@@ -124,6 +124,11 @@ static void check_table(const std::vector<HostCol>& cols, int64_t n, int null_as
     enc[r].pop_back();
     CHECK(enc_size(enc[r].data(), types, ks.n_keys) == sz, "enc_size row %lld", (long long)r);
     h[r] = row_hash_hashed(ks, r);
+    if (ks.n_keys == 1 && types[0] == DQ_UTF8) {  // phase A's one-column fast path
+      SView v;
+      CHECK(key_str(ks, 0, r, v), "key_str on a keyed row");
+      CHECK(str_row_hash(v) == h[r], "str_row_hash != row_hash_hashed, row %lld", (long long)r);
+    }
     CHECK(enc_hash(enc[r].data(), types, ks.n_keys) == h[r], "enc_hash != row hash, row %lld",
           (long long)r);
   }
@@ -139,6 +144,15 @@ static void check_table(const std::vector<HostCol>& cols, int64_t n, int null_as
           (long long)b, (int)eq, (int)enc_eq);
     CHECK(eq == enc_equal(enc[a].data(), enc[b].data(), types, ks.n_keys), "enc_equal");
     if (eq) CHECK(h[a] == h[b], "equal rows, different hashes");
+    if (ks.n_keys == 1 && types[0] == DQ_UTF8) {  // short forms decide equality when either is short
+      SView va, vb;
+      key_str(ks, 0, a, va);
+      key_str(ks, 0, b, vb);
+      const uint64_t sa = str_short_key(va), sb = str_short_key(vb);
+      if (sa != kNoShort || sb != kNoShort)
+        CHECK((sa == sb) == eq, "short keys of rows %lld, %lld disagree with rows_equal", (long long)a,
+              (long long)b);
+    }
   }
 }
 
@@ -158,7 +172,8 @@ int main() {
   // seeded 5000-row tables
   const int64_t n = 5000;
   std::mt19937_64 g(11);
-  const char* words[] = {"high", "low", "medium", "", "NullValue", "Thingy qqqqqqqqqqqqqqqqqqqqqqqqqqqqqq"};
+  const char* words[] = {"high", "low", "medium", "", "NullValue", "Thingy qqqqqqqqqqqqqqqqqqqqqqqqqqqqqq",
+                         "1234567", "12345678", "abc\0", "abc"};
   std::vector<int64_t> ids(n);
   std::vector<int32_t> i32(n);
   std::vector<double> dbl(n);
@@ -169,7 +184,10 @@ int main() {
     i32[r] = (int32_t)(g() % 7) - 3;
     const double dv[] = {0.0, -0.0, 1.5, -2.25, 1e300};
     dbl[r] = dv[g() % 5];
-    s[r] = words[g() % 6];
+    {
+      const int w = (int)(g() % 10);  // word 8 holds an embedded NUL byte
+      s[r] = w == 8 ? std::string("abc\0", 4) : std::string(words[w]);
+    }
     u[r] = "u" + std::to_string(g() % n);
     n1[r] = g() % 20 == 0;
     n2[r] = g() % 20 == 0;
