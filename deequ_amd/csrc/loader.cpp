@@ -1,17 +1,24 @@
 // loader.cpp -- columnar handoff: host-resident Arrow batches (what a Spark partition exports
 // through the Arrow C Data Interface) staged into HBM for the device entry points.
 //
-// Two device staging slots alternate.  Batch k's buffers are copied H2D on the loader's own copy
-// stream while batch k-1 is scanned on the caller's stream; a slot is refilled only after the
-// work that read it (recorded by dq_loader_release) has finished, and the scan of a slot waits
-// for its copy.  So PCIe transfer and the HBM-bound scan overlap, and the caller's stream sees the
-// usual stream order.  The reference's equivalent is Spark feeding UnsafeRows of a partition into
-// the aggregation iterator (AnalysisRunner.scala:303); ownership stays with the caller exactly as
-// there (the loader never frees or retains the host buffers after dq_loader_stage returns).
+// Two staging slots alternate, each a pinned host buffer plus a device buffer.  dq_loader_stage
+// copies the caller's (pageable) buffers into the slot's pinned buffer on the host -- several
+// threads for large batches -- and queues one DMA per column buffer from there on the loader's own
+// copy stream; the scan of the slot waits for its DMA on the caller's stream.  So batch k's DMA
+// overlaps batch k-1's HBM-bound scan, and a DMA from pinned memory runs at the link rate instead
+// of the driver's pageable bounce path.  A slot is refilled only after its previous DMA has drained
+// (host wait, before the pinned buffer is overwritten) and the work that read its device buffer
+// (recorded by dq_loader_release) has finished.
+//
+// Buffer lifetime: the caller's host buffers are read only inside dq_loader_stage (and
+// dq_scan_host / dq_freq_add_host): they may be freed or reused as soon as the call returns.  The
+// reference's equivalent is Spark feeding UnsafeRows of a partition into the aggregation iterator
+// (AnalysisRunner.scala:303); ownership stays with the caller exactly as there.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "engine.h"
@@ -23,10 +30,32 @@ namespace {
 
 struct Slot {
   DevBuf<uint8_t> buf;
+  uint8_t* pinned = nullptr;  // hipHostMalloc'd staging copy of the batch
+  size_t pinned_n = 0;
   hipEvent_t copied = nullptr;
   hipEvent_t consumed = nullptr;
   bool used = false;
+  bool dma = false;  // a DMA from `pinned` was queued
 };
+
+// memcpy of large buffers split over a few host threads (one thread streams ~10 GB/s, below the
+// host link's rate)
+void host_copy(uint8_t* dst, const void* src, size_t bytes) {
+  constexpr size_t kPerThread = (size_t)16 << 20;
+  const size_t nt = std::min<size_t>(8, bytes / kPerThread);
+  if (nt <= 1) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (bytes + nt - 1) / nt;
+  for (size_t t = 0; t < nt; ++t) {
+    const size_t lo = t * per, hi = std::min(bytes, lo + per);
+    if (lo < hi)
+      th.emplace_back([=] { memcpy(dst + lo, static_cast<const uint8_t*>(src) + lo, hi - lo); });
+  }
+  for (auto& x : th) x.join();
+}
 
 size_t fixed_width(int t) {
   switch (t) {
@@ -50,6 +79,7 @@ struct dq_loader {
   int staged = -1;
   ~dq_loader() {
     for (Slot& s : slot) {
+      if (s.pinned) (void)hipHostFree(s.pinned);
       if (s.copied) (void)hipEventDestroy(s.copied);
       if (s.consumed) (void)hipEventDestroy(s.consumed);
     }
@@ -121,20 +151,31 @@ extern "C" dq_status dq_loader_stage(dq_loader* l, const dq_column* host_cols, i
   const int k = l->next;
   l->next ^= 1;
   Slot& s = l->slot[k];
+  if (s.dma) HIP_TRY(hipEventSynchronize(s.copied));  // the pinned buffer is about to be rewritten
   if (s.used) {
     if (s.buf.n < total) HIP_TRY(hipEventSynchronize(s.consumed));  // about to free it
     else HIP_TRY(hipStreamWaitEvent(l->copy, s.consumed, 0));
   }
   if (s.buf.n < total) HIP_TRY(s.buf.ensure(total + total / 8));
+  if (s.pinned_n < total) {
+    if (s.pinned) HIP_TRY(hipHostFree(s.pinned));
+    s.pinned = nullptr;
+    s.pinned_n = 0;
+    HIP_TRY(hipHostMalloc((void**)&s.pinned, total + total / 8, hipHostMallocDefault));
+    s.pinned_n = total + total / 8;
+  }
   uint8_t* p = s.buf.p;
+  uint8_t* hp = s.pinned;
   for (int c = 0; c < n_cols; ++c) {
     const dq_column& h = host_cols[c];
     dq_column d = h;
     auto put = [&](const void* src, size_t bytes, const void** dst_field) -> hipError_t {
       if (!bytes) return hipSuccess;
-      hipError_t e = hipMemcpyAsync(p, src, bytes, hipMemcpyHostToDevice, l->copy);
+      host_copy(hp, src, bytes);
+      hipError_t e = hipMemcpyAsync(p, hp, bytes, hipMemcpyHostToDevice, l->copy);
       *dst_field = p;
       p += round_up(bytes);
+      hp += round_up(bytes);
       return e;
     };
     const void* vp = nullptr;
@@ -151,6 +192,7 @@ extern "C" dq_status dq_loader_stage(dq_loader* l, const dq_column* host_cols, i
     dev_cols[c] = d;
   }
   HIP_TRY(hipEventRecord(s.copied, l->copy));
+  s.dma = true;
   HIP_TRY(hipStreamWaitEvent(stream, s.copied, 0));
   l->staged = k;
   return DQ_OK;

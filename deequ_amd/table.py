@@ -112,13 +112,22 @@ class Table:
         return int(d.split(":")[1]) if ":" in d else 0
 
     def select_rows(self, start: int, stop: int) -> "Table":
-        """Row slice [start, stop) on batch boundaries (used to shard a table across ranks)."""
+        """Rows [start, stop) as views of this table's device buffers (used to shard a table across
+        ranks).  A batch that straddles a bound is cut; a cut must fall on a multiple of 8 rows
+        (bitmaps are byte-addressed views) or ValueError is raised -- rows are never dropped."""
+        start, stop = max(0, start), min(self.num_rows, stop)
         out, pos = [], 0
         for b in self.batches:
             n = next(iter(b.values())).length if b else 0
-            if pos >= start and pos + n <= stop:
-                out.append(b)
+            lo, hi = max(start, pos), min(stop, pos + n)
+            if lo < hi:
+                if lo == pos and hi == pos + n:
+                    out.append(b)
+                else:
+                    out.append({k: _slice_column(c, lo - pos, hi - pos) for k, c in b.items()})
             pos += n
+        if not out:
+            out.append({f.name: _empty_column(f.dtype, self.device) for f in self.schema.fields})
         return Table(self.schema, out, self.device)
 
     # -------------------------------------------------------------------------------------------
@@ -165,6 +174,23 @@ class Table:
         return Table.from_arrow(pa.Table.from_arrays(arrays, names=names), device=device)
 
 
+def _slice_column(c: ColumnBatch, lo: int, hi: int) -> ColumnBatch:
+    """Rows [lo, hi) of a device column as views (no copy)."""
+    if lo % 8 and lo != hi:
+        raise ValueError(f"row slice starts at row {lo} of a batch: cuts must fall on a multiple "
+                         f"of 8 rows (bitmap views are byte-addressed)")
+    m = hi - lo
+    validity = c.validity[lo // 8:] if c.validity is not None else None
+    if c.dtype == N.BOOL:
+        values = c.values[lo // 8:]
+    elif c.dtype == N.UTF8:
+        values = c.values[lo:]  # absolute offsets into the same character buffer
+    else:
+        values = c.values[lo:]
+    # null_count of a view is not recounted (it stays informational: the bitmap is the truth)
+    return ColumnBatch(c.dtype, m, validity, values, c.data, 0)
+
+
 def _to_device(np_buf: np.ndarray, device: str):
     import torch
     t = torch.from_numpy(np.ascontiguousarray(np_buf))
@@ -192,7 +218,11 @@ def _bits(buf, offset: int, length: int) -> Optional[np.ndarray]:
     return np.concatenate([out, np.zeros(pad + 16, np.uint8)])
 
 
-def _array_to_device(arr, dtype: int, device: str) -> ColumnBatch:
+def array_to_host(arr, dtype: int):
+    """Arrow array -> (validity, values, data) numpy buffers in the engine's column layout: bitmaps
+    re-based to bit 0, string offsets re-based to 0, every buffer zero-padded to a multiple of 16
+    bytes (+16) so the vector loads of a batch tail stay inside it.  validity is None without
+    NULLs, data None for fixed-width columns."""
     n = len(arr)
     bufs = arr.buffers()
     validity = _bits(bufs[0], arr.offset, n) if arr.null_count else None
@@ -200,8 +230,7 @@ def _array_to_device(arr, dtype: int, device: str) -> ColumnBatch:
         values = _bits(bufs[1], arr.offset, n)
         if values is None:
             values = np.zeros(16, np.uint8)
-        return ColumnBatch(dtype, n, _to_device(validity, device) if validity is not None else None,
-                           _to_device(values, device), None, arr.null_count)
+        return validity, values, None
     if dtype == N.UTF8:
         import pyarrow as pa
         if str(arr.type) == "large_string":
@@ -214,11 +243,16 @@ def _array_to_device(arr, dtype: int, device: str) -> ColumnBatch:
         offs = (offs - base).astype(np.int32)
         data = np.concatenate([data, np.zeros(16 + (-len(data)) % 16, np.uint8)])
         offs = np.concatenate([offs, np.zeros((-len(offs)) % 4 + 4, np.int32)])
-        return ColumnBatch(dtype, n, _to_device(validity, device) if validity is not None else None,
-                           _to_device(offs, device), _to_device(data, device), arr.null_count)
+        return validity, offs, data
     npt = _NP_OF[dtype]
     vals = np.frombuffer(bufs[1], dtype=npt)[arr.offset: arr.offset + n]
     pad = (-len(vals)) % (16 // np.dtype(npt).itemsize) + 16 // np.dtype(npt).itemsize
     vals = np.concatenate([vals, np.zeros(pad, npt)])
-    return ColumnBatch(dtype, n, _to_device(validity, device) if validity is not None else None,
-                       _to_device(vals, device), None, arr.null_count)
+    return validity, vals, None
+
+
+def _array_to_device(arr, dtype: int, device: str) -> ColumnBatch:
+    validity, values, data = array_to_host(arr, dtype)
+    return ColumnBatch(dtype, len(arr), _to_device(validity, device) if validity is not None else None,
+                       _to_device(values, device),
+                       _to_device(data, device) if data is not None else None, arr.null_count)

@@ -365,15 +365,19 @@ dq_status dq_freq_add_records_device(dq_freq* freq, const dq_freq_record* record
  * In the reference a Spark partition's rows stream through the aggregation iterator of the one
  * `data.agg(...)` job (AnalysisRunner.scala:303) and of the grouping job
  * (GroupingAnalyzers.scala:62-77).  Here a partition arrives as host Arrow buffers
- * (dq_column_from_arrow), is copied into one of two device staging slots on the loader's copy
- * stream, and is scanned on the caller's stream; the copy of batch k+1 overlaps the scan of
- * batch k.  The caller keeps the host buffers valid until the call returns (the loader retains
- * nothing of them afterwards).  One loader per thread / stream, like a dq_state.
+ * (dq_column_from_arrow), is copied into one of two pinned staging buffers (host threads), DMA'd
+ * into the slot's device buffer on the loader's copy stream, and scanned on the caller's stream;
+ * the DMA of batch k+1 overlaps the scan of batch k.  Lifetime: the loader reads the caller's host
+ * buffers only inside dq_loader_stage / dq_scan_host / dq_freq_add_host -- they may be freed or
+ * reused as soon as the call returns (unlike the device entry points' buffers, which must stay
+ * valid until dq_state_sync / dq_freq_summarize).  One loader per thread / stream, like a
+ * dq_state.
  * ---------------------------------------------------------------------------------------------- */
 typedef struct dq_loader dq_loader;
 dq_status dq_loader_create(int device, dq_loader** out);
 void dq_loader_destroy(dq_loader* loader);
-/* Stages one host batch: enqueues its H2D copies and makes `hip_stream` wait for them; writes the
+/* Stages one host batch: copies it into the slot's pinned buffer, enqueues the DMA and makes
+ * `hip_stream` wait for it; writes the
  * device-pointer columns to dev_cols[n_cols].  Every staged batch must be released (below) after
  * the work that reads dev_cols has been enqueued on `hip_stream`. */
 dq_status dq_loader_stage(dq_loader* loader, const dq_column* host_cols, int n_cols,
