@@ -36,7 +36,7 @@ ERR_INVALID_ARGUMENT, ERR_NO_SUCH_COLUMN, ERR_WRONG_TYPE, ERR_OUT_OF_MEMORY, ERR
 
 
 class dq_column(Structure):
-    _fields_ = [("type", c_int32), ("reserved", c_int32), ("length", c_int64),
+    _fields_ = [("type", c_int32), ("data_bytes", c_int32), ("length", c_int64),
                 ("validity", c_void_p), ("values", c_void_p), ("data", c_void_p)]
 
 

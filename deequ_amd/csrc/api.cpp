@@ -1402,7 +1402,7 @@ extern "C" dq_status dq_column_from_arrow(const struct ArrowArray* array,
   int64_t need = type == DQ_UTF8 ? 3 : 2;
   if (array->n_buffers < need) return fail(DQ_ERR_INVALID_ARGUMENT, "too few Arrow buffers");
   out->type = type;
-  out->reserved = 0;
+  out->data_bytes = 0;  // unknown: the Arrow C Data Interface carries no buffer sizes
   out->length = array->length;
   out->validity = array->null_count == 0 ? nullptr : static_cast<const uint8_t*>(array->buffers[0]);
   out->values = array->buffers[1];

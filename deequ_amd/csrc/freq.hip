@@ -32,6 +32,8 @@
 // appends one's chunks to the other's.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -74,7 +76,7 @@ struct FM<false> {
 };
 template <>
 struct FM<true> {
-  static constexpr int kTile = 4096;
+  static constexpr int kTile = 2048;
   static constexpr int kRB = 16;
   static constexpr int kDedupe = 1024;
   static constexpr int kTableC = 2560;
@@ -236,6 +238,7 @@ struct AArgs {
   uint8_t* arena;
   unsigned long long* arena_cursor;
   unsigned long long* counters;
+  unsigned long long* dbg_clock;  // DQ_FREQ_DEBUG=2: workgroup 0's phase timestamps (wall clock)
 };
 
 // Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
@@ -245,10 +248,16 @@ struct AKeys {
   static constexpr int kDedupe = FROM_REC ? (HASHED ? 128 : 256) : (HASHED ? 256 : 512);
   // a workgroup's rows: counts < 4^(kTile / kDedupe), so the digits of every entry fit
   static constexpr int kTilesPerWg = FROM_REC ? 1 : (HASHED ? 15 : 16);
+  // the string rows: 512-thread workgroups, two per CU (LDS <= 80 KB, <= 128 VGPRs), so one
+  // workgroup's load latency overlaps the other's hashing and dedupe between their barriers
+  static constexpr int kThreads = HASHED && !FROM_REC ? 512 : 1024;
+  static constexpr int kMinWaves = HASHED && !FROM_REC ? 4 : 1;  // per SIMD: two workgroups
 };
 
 template <bool HASHED, bool FROM_REC>
-__global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
+__global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
+                                  (AKeys<HASHED, FROM_REC>::kMinWaves)) freq_phaseA(AArgs a) {
+  constexpr int kThreads = AKeys<HASHED, FROM_REC>::kThreads;
   using M = FM<HASHED>;
   constexpr int T = M::kTile, D = AKeys<HASHED, FROM_REC>::kDedupe, W = M::kRB / 8;
   constexpr int ROUNDS = FROM_REC ? 1 : T / kThreads;
@@ -258,8 +267,8 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
   // one-column utf8 keys: the short forms (str_short_key) of the slots' keys and the tile's rows,
   // so most hits are decided in LDS instead of re-reading both strings
   constexpr bool SK = HASHED && !FROM_REC;
-  __shared__ uint64_t dsk[SK ? D : 1];
-  __shared__ uint64_t ssk[SK ? T : 1];
+  __shared__ uint64_t dsk0[SK ? D : 1], dsk1[SK ? D : 1];
+  __shared__ uint64_t ssk0[SK ? T : 1], ssk1[SK ? T : 1];
   __shared__ uint32_t s_wave[kThreads / 64];
   __shared__ uint64_t s_red[kThreads / 64];
   __shared__ uint32_t s_hits, s_bypass;
@@ -331,7 +340,7 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
   // LDS dedupe: 0 = not counted (table full), 1 = claimed a new slot, 2 = added to an existing
   // slot, 3 = the key's slot is being claimed: retry after the next barrier
   const bool one_str = a.ks.n_keys == 1 && a.ks.cols[0].type == DQ_UTF8;  // block-uniform
-  auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep, uint64_t sk) -> int {
+  auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep, uint64_t k0, uint64_t k1) -> int {
     if (h == kEmptyKey) return 0;
     uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
     for (int pr = 0; pr < 4; ++pr) {
@@ -344,8 +353,9 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
       }
       if (claimed) {
         if constexpr (SK) {
-          lds_store(&dsk[slot], sk);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // dsk before drep
+          lds_store(&dsk0[slot], k0);
+          lds_store(&dsk1[slot], k1);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the short key before drep
         }
         if (HASHED) lds_store(&drep[slot], rep);
         atomicAdd((unsigned long long*)&dcnt[slot], c);
@@ -361,9 +371,9 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
           }
           if (r2 != rep) {
             if constexpr (SK) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const uint64_t sk2 = SK ? lds_load(&dsk[slot]) : kNoShort;
-            if (sk != kNoShort || sk2 != kNoShort)
-              same = sk == sk2;
+            const uint64_t b1 = SK ? lds_load(&dsk1[slot]) : kNoShort;
+            if (k1 != kNoShort || b1 != kNoShort)
+              same = k1 == b1 && k0 == lds_load(&dsk0[slot]);
             else if constexpr (FROM_REC)
               same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
                                reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
@@ -383,50 +393,176 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
     return 0;
   };
 
+  // DQ_FREQ_DEBUG=2: workgroup 0 stamps each tile's phases (wall clock, after the barriers)
+  auto mark = [&](int64_t t, int k) {
+    if (a.dbg_clock && blockIdx.x == 0 && tid == 0 && t - t0 < 16)
+      a.dbg_clock[(t - t0) * 8 + k] = wall_clock64();
+  };
   __syncthreads();
   for (int64_t t = t0; t < t1; ++t) {
+    mark(t, 0);
     const int64_t i0 = t * a.tile_items;
     const int64_t i1 = min(i0 + a.tile_items, a.n_items);
     const bool probe = ((t - t0) & 7) == 0;
     if (tid == 0) s_hits = 0;
     uint32_t keyed = 0, raw = 0;  // bit j: round j
-    // 1. load + hash
+    // 1. load + hash.  The row paths issue every round's loads before any value is used (one
+    // memory latency per tile instead of one per round); records and multi-column keys loop.
+    if constexpr (FROM_REC) {
 #pragma unroll 1
-    for (int j = 0; j < ROUNDS; ++j) {
-      const int64_t i = i0 + (int64_t)j * kThreads + tid;
-      const int q = j * kThreads + tid;
-      if (i >= i1) continue;
-      if constexpr (FROM_REC) {
+      for (int j = 0; j < ROUNDS; ++j) {
+        const int64_t i = i0 + (int64_t)j * kThreads + tid;
+        const int q = j * kThreads + tid;
+        if (i >= i1) continue;
         const RecIn r = a.rin[i];
         scnt[tid] = r.count;
         stash[q * W] = HASHED ? r.key : fmix_bij(r.key);
         if (HASHED) stash[q * W + 1] = a.var_arena_base + (uint64_t)seg_var_base(a.segs, i) + r.enc_off;
         if (r.count) keyed |= 1u << j;
-      } else if (SK && one_str) {  // one utf8 column: no per-column loops
-        SView v;
-        if (!key_str(a.ks, 0, i, v)) {
-          ++nulls;
-        } else {
+      }
+    } else if constexpr (!HASHED) {  // one fixed-width column
+      // branch-free loads (an out-of-tile lane re-reads the tile's last row): a divergent branch
+      // around a load makes the compiler wait for it before the join
+      const KeyCol& c = a.ks.cols[0];
+      int64_t ic[ROUNDS];
+      uint32_t ok = 0;
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        const int64_t i = i0 + (int64_t)j * kThreads + tid;
+        ok |= (i < i1 ? 1u : 0u) << j;
+        ic[j] = i < i1 ? i : i1 - 1;
+      }
+      uint32_t vb = ~0u;
+      if (c.valid) {
+        uint32_t byte[ROUNDS];
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) byte[j] = c.valid[ic[j] >> 3];
+        vb = 0;
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) vb |= ((byte[j] >> (ic[j] & 7)) & 1u) << j;
+      }
+      uint64_t v[ROUNDS];
+      auto load_all = [&](auto type_tag) {
+        constexpr int TY = decltype(type_tag)::value;
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) v[j] = kwiden(TY, c.values, ic[j]);
+      };
+      switch (c.type) {  // block-uniform: one unrolled load loop per width
+        case DQ_INT8: load_all(std::integral_constant<int, DQ_INT8>{}); break;
+        case DQ_INT16: load_all(std::integral_constant<int, DQ_INT16>{}); break;
+        case DQ_INT32: load_all(std::integral_constant<int, DQ_INT32>{}); break;
+        case DQ_FLOAT32: load_all(std::integral_constant<int, DQ_FLOAT32>{}); break;
+        case DQ_FLOAT64: load_all(std::integral_constant<int, DQ_FLOAT64>{}); break;
+        case DQ_BOOL: load_all(std::integral_constant<int, DQ_BOOL>{}); break;
+        default: load_all(std::integral_constant<int, DQ_INT64>{}); break;
+      }
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        if (!((ok >> j) & 1u)) continue;
+        if ((vb >> j) & 1u) {
           keyed |= 1u << j;
-          stash[q * W] = str_row_hash(v);
-          stash[q * W + 1] = (uint64_t)i;
-          ssk[q] = str_short_key(v);
-        }
-      } else {
-        const int kind = row_kind(a.ks, i, !HASHED);
-        if (kind == ROW_SKIP) {
-          ++nulls;
-        } else if (kind == ROW_NULL_GROUP) {
+          stash[(j * kThreads + tid) * W] = fmix_bij(exact_canon(a.ks, v[j]));
+        } else if (a.ks.null_as_group) {
           ++nullg;
         } else {
+          ++nulls;
+        }
+      }
+    } else if (one_str) {  // one utf8 column: offsets, then <= 16 bytes per row, then hash
+      const KeyCol& c = a.ks.cols[0];
+      const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
+      int64_t ic[ROUNDS];
+      uint32_t ok = 0;
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        const int64_t i = i0 + (int64_t)j * kThreads + tid;
+        ok |= (i < i1 ? 1u : 0u) << j;
+        ic[j] = i < i1 ? i : i1 - 1;
+      }
+      int32_t s0[ROUNDS], len[ROUNDS];
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        s0[j] = off[ic[j]];
+        len[j] = off[ic[j] + 1];
+      }
+      uint32_t byte[ROUNDS];  // validity bytes, in flight with the offsets
+      if (c.valid) {
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) byte[j] = c.valid[ic[j] >> 3];
+      }
+      // <= 16 bytes per row as aligned dwords: dword k is read at min(k, last) so every read
+      // holds a byte of the string (no read reaches a page the string does not lie on); rows
+      // that are NULL, empty or longer read the first offset instead (always mapped)
+      uint32_t d[ROUNDS][5];
+      int sh[ROUNDS];
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        len[j] -= s0[j];
+        // (Arrow keeps a NULL slot's offsets monotonic, so its range is inside the buffer too)
+        const bool reg = len[j] > 0 && len[j] <= 16;
+        const uint8_t* p = reg ? c.data + s0[j] : reinterpret_cast<const uint8_t*>(off);
+        const uint32_t* q =
+            reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+        sh[j] = (int)(reinterpret_cast<uintptr_t>(p) & 3u);
+        const int last = reg ? ((sh[j] + len[j] + 3) >> 2) - 1 : 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) d[j][k] = q[k < last ? k : last];
+      }
+      uint32_t vb = ~0u;
+      if (c.valid) {
+        vb = 0;
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) vb |= ((byte[j] >> (ic[j] & 7)) & 1u) << j;
+      }
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        if (!((ok >> j) & 1u)) continue;
+        const int64_t i = ic[j];
+        const int q = j * kThreads + tid;
+        uint64_t h, k0 = 0, k1 = kNoShort;
+        if ((vb >> j) & 1u) {
+          if (len[j] <= 16) {
+            uint64_t w0, w1;
+            str16_from_dwords(d[j], sh[j], len[j], w0, w1);
+            h = str_row_hash_reg(w0, w1, len[j]);
+            str_short_key_reg(w0, w1, len[j], k0, k1);
+          } else {
+            h = str_row_hash(SView{c.data + s0[j], len[j]});
+          }
+        } else if (a.ks.null_as_group) {  // Histogram: NULL is the "NullValue" literal
+          h = str_row_hash(SView{nullptr, kNullValueLen});
+          str_short_key(SView{nullptr, kNullValueLen}, k0, k1);
+        } else {
+          ++nulls;
+          continue;
+        }
+        keyed |= 1u << j;
+        stash[q * W] = h;
+        stash[q * W + 1] = (uint64_t)i;
+        if constexpr (SK) {
+          ssk0[q] = k0;
+          ssk1[q] = k1;
+        }
+      }
+    } else {  // several key columns
+#pragma unroll 1
+      for (int j = 0; j < ROUNDS; ++j) {
+        const int64_t i = i0 + (int64_t)j * kThreads + tid;
+        const int q = j * kThreads + tid;
+        if (i >= i1) continue;
+        const int kind = row_kind(a.ks, i, false);
+        if (kind == ROW_SKIP) {
+          ++nulls;
+        } else {
           keyed |= 1u << j;
-          stash[q * W] = HASHED ? row_hash_hashed(a.ks, i) : row_hash_exact(a.ks, i);
-          if (HASHED) stash[q * W + 1] = (uint64_t)i;  // the row until it is encoded
-          if constexpr (SK) ssk[q] = kNoShort;
+          stash[q * W] = row_hash_hashed(a.ks, i);
+          stash[q * W + 1] = (uint64_t)i;  // the row until it is encoded
+          if constexpr (SK) ssk1[q] = kNoShort;
         }
       }
     }
     __syncthreads();
+    mark(t, 1);
     // 2. dedupe (round 0 of a probing tile measures the hit rate).  A hashed key whose slot is
     // claimed but not yet published by its claimer (another lane or wave) is retried after a
     // block barrier -- never a spin, lanes of one wave would wait on each other -- once per tile
@@ -447,7 +583,7 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
             const int q = j * kThreads + tid;
             const uint64_t h = stash[q * W], rep = stash[q * W + 1];
             const uint64_t c = FROM_REC ? scnt[tid] : 1;
-            const int res = dedupe(h, c, rep, SK ? ssk[q] : kNoShort);
+            const int res = dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort);
             if (res == 3) continue;
             w &= ~(1u << j);
             if (res == 2) ++hits;
@@ -466,7 +602,7 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
         const uint64_t h = stash[q * W];
         const uint64_t rep = HASHED ? stash[q * W + 1] : 0;
         const uint64_t c = FROM_REC ? scnt[tid] : 1;
-        const int res = on ? dedupe(h, c, rep, SK ? ssk[q] : kNoShort) : 0;
+        const int res = on ? dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort) : 0;
         if (res == 3) wait |= 1u << j;
         else if (res == 2) ++hits;
         else if (!res) count_raw(j, h, c);
@@ -485,6 +621,8 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
       uint32_t hits = 0;
       retry(~0u, hits);
     }
+    __syncthreads();
+    mark(t, 2);
     uint64_t need = 0;
     if constexpr (HASHED && !FROM_REC) {
 #pragma unroll 1
@@ -493,6 +631,7 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
     }
     // 3. counting sort of the raw rows into the tile's chunk
     begin_chunk(t, need);
+    mark(t, 3);
 #pragma unroll 1
     for (int j = 0; j < ROUNDS; ++j) {
       if (!((raw >> j) & 1u)) continue;
@@ -503,6 +642,7 @@ __global__ void __launch_bounds__(kThreads) freq_phaseA(AArgs a) {
       for_digits(FROM_REC ? scnt[tid] : 1, [&](uint32_t code) { put(t, h, code, rep); });
     }
     end_chunk();
+    mark(t, 4);
   }
   // the collapsed groups of the whole range -> this workgroup's own chunk
   uint64_t need = 0;
@@ -1320,6 +1460,11 @@ struct dq_freq {
   DevBuf<unsigned long long> dev_words;  // counters[C_N], then the arena cursor
   uint64_t h_counters[C_N] = {0};
   uint64_t arena_used = 0;
+  // phase A launches leave the device counters and arena cursor ahead of the host copies: they
+  // are read back only when needed (finalize, merge, arena growth), so batches queue back to back
+  bool counters_stale = false;
+  uint64_t arena_hi = 0;  // upper bound of the arena bytes in use (arena_used at the last read-back
+                          // + the worst case of every batch added since)
   int64_t num_rows = 0;
   hipStream_t stream = nullptr;
   // finalize cache (phase B)
@@ -1398,8 +1543,11 @@ static dq_status pull_counters(dq_freq* f) {
   HIP_TRY(hipMemcpy(w, f->dev_words.p, sizeof(w), hipMemcpyDeviceToHost));
   for (int k = 0; k < C_N; ++k) f->h_counters[k] = w[k];
   f->arena_used = w[C_N];
+  f->arena_hi = f->arena_used;
+  f->counters_stale = false;
   return DQ_OK;
 }
+static dq_status sync_counters(dq_freq* f) { return f->counters_stale ? pull_counters(f) : DQ_OK; }
 
 static dq_status push_counters(dq_freq* f) {
   HIP_TRY(hipStreamSynchronize(f->stream));
@@ -1407,6 +1555,8 @@ static dq_status push_counters(dq_freq* f) {
   for (int k = 0; k < C_N; ++k) w[k] = f->h_counters[k];
   w[C_N] = f->arena_used;
   HIP_TRY(hipMemcpy(f->dev_words.p, w, sizeof(w), hipMemcpyHostToDevice));
+  f->arena_hi = f->arena_used;
+  f->counters_stale = false;
   return DQ_OK;
 }
 
@@ -1426,12 +1576,42 @@ static void launch_phaseA(dq_freq* f, AArgs a, bool from_rec) {
   int64_t n_wg = 0;
   phaseA_chunks(HASHED, from_rec, a.n_items, a.tile_items, &n_wg);
   a.tiles_per_wg = from_rec ? AKeys<HASHED, true>::kTilesPerWg : AKeys<HASHED, false>::kTilesPerWg;
+  static int dbg = [] {
+    const char* e = getenv("DQ_FREQ_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  unsigned long long* clk = nullptr;
+  if (dbg >= 2 && hipMalloc(&clk, 16 * 8 * sizeof(unsigned long long)) == hipSuccess)
+    (void)hipMemset(clk, 0, 16 * 8 * sizeof(unsigned long long));
+  else
+    clk = nullptr;
+  a.dbg_clock = clk;
   if (from_rec)
-    hipLaunchKernelGGL((freq_phaseA<HASHED, true>), dim3((unsigned)n_wg), dim3(kThreads), 0,
+    hipLaunchKernelGGL((freq_phaseA<HASHED, true>), dim3((unsigned)n_wg),
+                       dim3(AKeys<HASHED, true>::kThreads), 0,
                        f->stream, a);
   else
-    hipLaunchKernelGGL((freq_phaseA<HASHED, false>), dim3((unsigned)n_wg), dim3(kThreads), 0,
+    hipLaunchKernelGGL((freq_phaseA<HASHED, false>), dim3((unsigned)n_wg),
+                       dim3(AKeys<HASHED, false>::kThreads), 0,
                        f->stream, a);
+  if (clk) {  // per-tile phase times of workgroup 0, us (the wall clock ticks at 100 MHz)
+    unsigned long long h[16 * 8];
+    (void)hipStreamSynchronize(f->stream);
+    (void)hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(clk);
+    double acc[4] = {0, 0, 0, 0};
+    int nt = 0;
+    for (int t = 0; t < 16; ++t) {
+      if (!h[t * 8 + 4]) break;
+      for (int k = 0; k < 4; ++k) acc[k] += (double)(h[t * 8 + k + 1] - h[t * 8 + k]) / 100.0;
+      ++nt;
+    }
+    if (nt)
+      fprintf(stderr, "dq_freq phase A%s%s wg0 per tile (us): load+hash %.2f dedupe %.2f begin %.2f "
+              "put+end %.2f (%d tiles)\n", HASHED ? " hashed" : " exact",
+              a.ks.null_as_group ? " (histogram)" : "", acc[0] / nt, acc[1] / nt, acc[2] / nt,
+              acc[3] / nt, nt);
+  }
 }
 
 static AArgs base_args(dq_freq* f) {
@@ -1454,6 +1634,8 @@ static AArgs base_args(dq_freq* f) {
 
 // ---- finalize: phase B ------------------------------------------------------------------------
 static dq_status finalize_b(dq_freq* f) {
+  dq_status cs = sync_counters(f);
+  if (cs != DQ_OK) return cs;
   if (f->b_valid) return DQ_OK;
   const int64_t n = f->n_chunks;
   std::fill(f->h_bucket_base.begin(), f->h_bucket_base.end(), 0ULL);
@@ -1886,6 +2068,8 @@ extern "C" dq_status dq_freq_reset(dq_freq* f, void* hip_stream) {
   HIP_TRY(hipMemsetAsync(f->dev_words.p, 0, (C_N + 1) * 8, f->stream));
   for (int k = 0; k < C_N; ++k) f->h_counters[k] = 0;
   f->arena_used = 0;
+  f->arena_hi = 0;
+  f->counters_stale = false;
   f->num_rows = 0;
   f->n_chunks = 0;
   f->mode_null_as_group = -1;
@@ -1926,21 +2110,32 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
   dq_status st = ensure_chunks(f, chunks);
   if (st != DQ_OK) return st;
   if (!f->exact) {
-    // arena room for the worst case (every row its own record), see row_enc_size
+    // arena room for the worst case (every row its own record), see row_enc_size; a utf8 key's
+    // character bytes come from its data_bytes hint, else from its offsets (a device read)
     uint64_t bound = 0;
     for (int k = 0; k < n_keys; ++k) {
       if (keys[k].type == DQ_UTF8) {
-        int32_t first = 0, last = 0;
-        HIP_TRY(hipMemcpy(&first, keys[k].values, 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(&last, reinterpret_cast<const int32_t*>(keys[k].values) + rows, 4,
-                          hipMemcpyDeviceToHost));
-        if (last < first) return fail(DQ_ERR_INVALID_ARGUMENT, "utf8 key %d has bad offsets", k);
-        bound += (uint64_t)rows * (8 + 3 + kNullValueLen + 3) + (uint64_t)(last - first);
+        int64_t bytes = keys[k].data_bytes;
+        if (bytes <= 0) {
+          int32_t first = 0, last = 0;
+          HIP_TRY(hipMemcpy(&first, keys[k].values, 4, hipMemcpyDeviceToHost));
+          HIP_TRY(hipMemcpy(&last, reinterpret_cast<const int32_t*>(keys[k].values) + rows, 4,
+                            hipMemcpyDeviceToHost));
+          if (last < first) return fail(DQ_ERR_INVALID_ARGUMENT, "utf8 key %d has bad offsets", k);
+          bytes = last - first;
+        }
+        bound += (uint64_t)rows * (8 + 3 + kNullValueLen + 3) + (uint64_t)bytes;
       } else {
         bound += (uint64_t)rows * 12;
       }
     }
-    HIP_TRY(grow_keep(f->arena, f->arena_used, f->arena_used + bound + 64, f->stream));
+    if (f->arena.n < f->arena_hi + bound + 64) {  // may not fit: learn the true use, then grow
+      dq_status cs = pull_counters(f);
+      if (cs != DQ_OK) return cs;
+      if (f->arena.n < f->arena_used + bound + 64)  // room for a few batches per read-back
+        HIP_TRY(grow_keep(f->arena, f->arena_used, f->arena_used + 4 * bound + 64, f->stream));
+    }
+    f->arena_hi += bound;
   }
   AArgs a = base_args(f);
   for (int k = 0; k < n_keys; ++k)
@@ -1951,7 +2146,8 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
   else launch_phaseA<true>(f, a, false);
   HIP_TRY(hipGetLastError());
   f->n_chunks += chunks;
-  return pull_counters(f);
+  f->counters_stale = true;  // read back at finalize / merge / arena growth
+  return DQ_OK;
 }
 
 extern "C" dq_status dq_freq_summarize(dq_freq* f, dq_freq_summary* out) {

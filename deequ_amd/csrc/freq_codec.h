@@ -101,6 +101,20 @@ struct MemBytes {
   DQ_HD uint32_t u8(int64_t o) const { return p[o]; }
 };
 
+// Byte reader over up to 16 bytes held in two registers (w0 = bytes 0..7, w1 = bytes 8..15,
+// little-endian): xxh_bytes of a short string whose bytes were loaded ahead of the hashing.
+struct RegBytes {
+  uint64_t w0, w1;
+  DQ_HD uint64_t at(int64_t o) const {  // bytes o .. o + 7 (zero past byte 15), 0 <= o <= 15
+    if (o == 0) return w0;
+    if (o < 8) return (w0 >> (8 * o)) | (w1 << (64 - 8 * o));
+    return w1 >> (8 * (o - 8));
+  }
+  DQ_HD uint64_t u64(int64_t o) const { return at(o); }
+  DQ_HD uint32_t u32(int64_t o) const { return (uint32_t)at(o); }
+  DQ_HD uint32_t u8(int64_t o) const { return (uint32_t)(at(o) & 0xffu); }
+};
+
 // "NullValue" (Histogram.NullFieldReplacement, Histogram.scala:108) as constants: a string view
 // with p == nullptr IS this literal, so no code path needs memory for it.
 constexpr int32_t kNullValueLen = 9;
@@ -154,15 +168,18 @@ DQ_HD int row_kind(const KeySet& ks, int64_t r, bool exact) {
 // Histogram groups cast(col as string) (Histogram.scala:63): every NaN prints as "NaN", so in
 // Histogram mode NaN payloads fold into the canonical NaN (a grouping keeps Spark 2.2's binary
 // key equality).
-DQ_HD uint64_t exact_key(const KeySet& ks, int64_t r) {
-  const KeyCol& c = ks.cols[0];
-  uint64_t v = kwiden(c.type, c.values, r);
+DQ_HD uint64_t exact_canon(const KeySet& ks, uint64_t v) {
+  const int t = ks.cols[0].type;
   if (ks.null_as_group) {
-    if (c.type == DQ_FLOAT64 && (v & 0x7fffffffffffffffULL) > 0x7ff0000000000000ULL)
+    if (t == DQ_FLOAT64 && (v & 0x7fffffffffffffffULL) > 0x7ff0000000000000ULL)
       v = 0x7ff8000000000000ULL;
-    if (c.type == DQ_FLOAT32 && (v & 0x7fffffffULL) > 0x7f800000ULL) v = 0x7fc00000ULL;
+    if (t == DQ_FLOAT32 && (v & 0x7fffffffULL) > 0x7f800000ULL) v = 0x7fc00000ULL;
   }
   return v;
+}
+DQ_HD uint64_t exact_key(const KeySet& ks, int64_t r) {
+  const KeyCol& c = ks.cols[0];
+  return exact_canon(ks, kwiden(c.type, c.values, r));
 }
 DQ_HD uint64_t row_hash_exact(const KeySet& ks, int64_t r) { return fmix_bij(exact_key(ks, r)); }
 
@@ -193,17 +210,79 @@ DQ_HD uint64_t row_hash_hashed(const KeySet& ks, int64_t r) {
 
 // The row hash of a one-column utf8 key (row_hash_hashed with n_keys == 1).
 DQ_HD uint64_t str_row_hash(const SView& v) { return fmix_bij(fold_col_hash(kRowHashSeed, str_col_hash(v, 0))); }
-
-// Short form of a one-column utf8 key of at most 7 bytes: its bytes and its length in one word,
-// so two short keys are equal iff their words are; kNoShort for every other key (the 9-byte
-// "NullValue" literal included), which is never equal to a short key.
-constexpr uint64_t kNoShort = ~0ULL;
-DQ_HD uint64_t str_short_key(const SView& v) {
-  if (!v.p || v.len > 7) return kNoShort;
-  uint64_t w = 0;
-  for (int32_t q = 0; q < v.len; ++q) w |= (uint64_t)v.p[q] << (8 * q);
-  return w | ((uint64_t)v.len << 56);
+// The same for a non-NULL string of len <= 16 bytes already in registers.
+DQ_HD uint64_t str_row_hash_reg(uint64_t w0, uint64_t w1, int32_t len) {
+  return fmix_bij(fold_col_hash(kRowHashSeed, xxh_bytes(RegBytes{w0, w1}, (int64_t)len, 17)));
 }
+
+// Short form of a one-column utf8 key of at most 15 bytes: (k0, k1) = its bytes 0..7 and
+// 8..14 with the length in k1's top byte (zero for such a string), so two short keys are equal
+// iff both words are.  Every other key has k1 = kNoShort (top byte 0xFF), never equal to a short
+// key.  A NULL in Histogram mode is the 9-byte "NullValue" literal and gets that string's short
+// form, so it meets a real "NullValue" string in LDS (Histogram.scala:59-66).
+constexpr uint64_t kNoShort = ~0ULL;
+constexpr int32_t kShortMax = 15;
+DQ_HD void str_short_key_reg(uint64_t w0, uint64_t w1, int32_t len, uint64_t& k0, uint64_t& k1) {
+  if (len > kShortMax) {
+    k0 = 0;
+    k1 = kNoShort;
+    return;
+  }
+  k0 = w0;
+  k1 = w1 | ((uint64_t)len << 56);
+}
+DQ_HD void str_short_key(const SView& v, uint64_t& k0, uint64_t& k1) {
+  if (!v.p) {
+    str_short_key_reg(kNullValueLo, kNullValueHi, kNullValueLen, k0, k1);
+    return;
+  }
+  if (v.len > kShortMax) {
+    k0 = 0;
+    k1 = kNoShort;
+    return;
+  }
+  uint64_t w0 = 0, w1 = 0;
+  for (int32_t q = 0; q < v.len; ++q) {
+    if (q < 8) w0 |= (uint64_t)v.p[q] << (8 * q);
+    else w1 |= (uint64_t)v.p[q] << (8 * (q - 8));
+  }
+  str_short_key_reg(w0, w1, v.len, k0, k1);
+}
+
+// A string of len <= 16 bytes from the aligned dwords d[0..4] that hold it, starting sh (0..3)
+// bytes into d[0]: (w0, w1) little-endian, zero past its end.
+DQ_HD void str16_from_dwords(const uint32_t* d, int sh, int32_t len, uint64_t& w0, uint64_t& w1) {
+  uint64_t lo = (uint64_t)d[0] | ((uint64_t)d[1] << 32);
+  uint64_t mid = (uint64_t)d[2] | ((uint64_t)d[3] << 32);
+  if (sh) {
+    lo = (lo >> (8 * sh)) | (mid << (64 - 8 * sh));
+    mid = (mid >> (8 * sh)) | ((uint64_t)d[4] << (64 - 8 * sh));
+  }
+  if (len <= 0) {
+    lo = mid = 0;
+  } else if (len < 8) {
+    lo &= (1ULL << (8 * len)) - 1;
+    mid = 0;
+  } else if (len < 16) {
+    mid &= (1ULL << (8 * (len - 8))) - 1;
+  }
+  w0 = lo;
+  w1 = mid;
+}
+
+// Bytes [p, p + len) of a string, len <= 16: reads the aligned dwords that overlap it (each holds
+// a byte of the string, so no read reaches a page the string does not lie on).
+DQ_HD void load_str16(const uint8_t* p, int32_t len, uint64_t& w0, uint64_t& w1) {
+  w0 = w1 = 0;
+  if (len <= 0) return;
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+  const int sh = (int)(reinterpret_cast<uintptr_t>(p) & 3u);
+  const int last = ((sh + len + 3) >> 2) - 1;  // 0..4
+  uint32_t d[5];
+  for (int k = 0; k < 5; ++k) d[k] = q[k < last ? k : last];
+  str16_from_dwords(d, sh, len, w0, w1);
+}
+
 
 DQ_HD uint32_t pad4(uint32_t n) { return (n + 3u) & ~3u; }
 

@@ -32,6 +32,8 @@ class HostColumn:
         c.validity = self.validity.ctypes.data if self.validity is not None else None
         c.values = self.values.ctypes.data
         c.data = self.data.ctypes.data if self.data is not None else None
+        if self.data is not None and self.data.nbytes < (1 << 31):
+            c.data_bytes = self.data.nbytes
         return c
 
     def nbytes(self) -> int:

@@ -77,6 +77,8 @@ class ColumnBatch:
         c.validity = self.validity.data_ptr() if self.validity is not None else None
         c.values = self.values.data_ptr() if self.values is not None else None
         c.data = self.data.data_ptr() if self.data is not None else None
+        if self.data is not None and self.data.numel() < (1 << 31):
+            c.data_bytes = self.data.numel()  # an upper bound of the string bytes (padding incl.)
         return c
 
     def nbytes(self) -> int:

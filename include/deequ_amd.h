@@ -71,7 +71,9 @@ typedef enum dq_type {
 
 typedef struct dq_column {
   int32_t type;            /* dq_type                                                         */
-  int32_t reserved;
+  int32_t data_bytes;      /* DQ_UTF8: optional size hint, >= offsets[length] - offsets[0] (the
+                              group-by then sizes its key arena without reading the offsets
+                              back); 0 = unknown.  Ignored for other types.                  */
   int64_t length;          /* rows                                                            */
   const uint8_t* validity; /* LSB-first bitmap (1 = valid), NULL when the column has no nulls */
   const void* values;      /* fixed-width values; for DQ_UTF8 the int32 offsets               */

@@ -32,8 +32,10 @@ def _table(seed, null_rates):
     def mask(r):
         return rng.random(n) < r
     return pa.table({
-        "item": pa.array([f"B00{v:07d}" for v in rng.integers(0, 800, n)], mask=mask(null_rates[0])),
-        "value": pa.array(att[rng.integers(0, len(att), n)], mask=mask(null_rates[1])),
+        "item": pa.array([f"B00{v:07d}" for v in rng.integers(0, 800, n)], mask=mask(null_rates[0]),
+                         type=pa.string()),
+        "value": pa.array(att[rng.integers(0, len(att), n)], mask=mask(null_rates[1]),
+                          type=pa.string()),
         "numbersA": pa.array(rng.random(n), mask=mask(null_rates[2]), type=pa.float64()),
         "numbersB": pa.array(rng.random(n), mask=mask(null_rates[3]), type=pa.float64()),
         "count": pa.array(rng.integers(-5, 40, n), mask=mask(null_rates[4]), type=pa.int64()),
@@ -92,7 +94,10 @@ def test_partition_states_merge_to_the_whole_table(seed, null_rates, cuts, gpu_d
                 states.append(a.compute_state_from(p))
             except Exception:  # noqa: BLE001 -- a failing state fails the whole run as well
                 states.append(None)
-        merged = a.compute_metric_from(merge_states(*states))
+        try:  # Analyzer.calculate's try (Analyzer.scala:88-103) around computeMetricFrom
+            merged = a.compute_metric_from(merge_states(*states))
+        except Exception as e:  # noqa: BLE001
+            merged = a.to_failure_metric(e)
         direct = a.calculate(whole)
         assert _same(_value(merged), _value(direct)), (str(a), bounds, _value(merged),
                                                        _value(direct))

@@ -128,6 +128,22 @@ static void check_table(const std::vector<HostCol>& cols, int64_t n, int null_as
       SView v;
       CHECK(key_str(ks, 0, r, v), "key_str on a keyed row");
       CHECK(str_row_hash(v) == h[r], "str_row_hash != row_hash_hashed, row %lld", (long long)r);
+      if (v.p && v.len <= 16) {  // phase A's register path: aligned-dword loads, then hash
+        for (int shift = 0; shift < 4; ++shift) {
+          // the device reads whole aligned dwords: give the copy the room a page would
+          alignas(8) uint8_t room[40] = {0};
+          memset(room, 0xEE, sizeof(room));
+          memcpy(room + 4 + shift, v.p, v.len);
+          uint64_t w0 = 0, w1 = 0;
+          load_str16(room + 4 + shift, v.len, w0, w1);
+          CHECK(str_row_hash_reg(w0, w1, v.len) == h[r], "str_row_hash_reg row %lld shift %d",
+                (long long)r, shift);
+          uint64_t a0, a1, b0, b1;
+          str_short_key_reg(w0, w1, v.len, a0, a1);
+          str_short_key(v, b0, b1);
+          CHECK(a0 == b0 && a1 == b1, "str_short_key_reg row %lld", (long long)r);
+        }
+      }
     }
     CHECK(enc_hash(enc[r].data(), types, ks.n_keys) == h[r], "enc_hash != row hash, row %lld",
           (long long)r);
@@ -148,10 +164,12 @@ static void check_table(const std::vector<HostCol>& cols, int64_t n, int null_as
       SView va, vb;
       key_str(ks, 0, a, va);
       key_str(ks, 0, b, vb);
-      const uint64_t sa = str_short_key(va), sb = str_short_key(vb);
-      if (sa != kNoShort || sb != kNoShort)
-        CHECK((sa == sb) == eq, "short keys of rows %lld, %lld disagree with rows_equal", (long long)a,
-              (long long)b);
+      uint64_t a0, a1, b0, b1;
+      str_short_key(va, a0, a1);
+      str_short_key(vb, b0, b1);
+      if (a1 != kNoShort || b1 != kNoShort)
+        CHECK((a0 == b0 && a1 == b1) == eq, "short keys of rows %lld, %lld disagree with rows_equal",
+              (long long)a, (long long)b);
     }
   }
 }
@@ -173,7 +191,8 @@ int main() {
   const int64_t n = 5000;
   std::mt19937_64 g(11);
   const char* words[] = {"high", "low", "medium", "", "NullValue", "Thingy qqqqqqqqqqqqqqqqqqqqqqqqqqqqqq",
-                         "1234567", "12345678", "abc\0", "abc"};
+                         "1234567", "12345678", "abc\0", "abc", "0123456789abcdef", "0123456789abcde",
+                         "0123456789abcdefg"};
   std::vector<int64_t> ids(n);
   std::vector<int32_t> i32(n);
   std::vector<double> dbl(n);
@@ -185,7 +204,7 @@ int main() {
     const double dv[] = {0.0, -0.0, 1.5, -2.25, 1e300};
     dbl[r] = dv[g() % 5];
     {
-      const int w = (int)(g() % 10);  // word 8 holds an embedded NUL byte
+      const int w = (int)(g() % 13);  // word 8 holds an embedded NUL byte
       s[r] = w == 8 ? std::string("abc\0", 4) : std::string(words[w]);
     }
     u[r] = "u" + std::to_string(g() % n);
