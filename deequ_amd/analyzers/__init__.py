@@ -8,6 +8,7 @@ from .grouping import (CountDistinct, Distinctness, Entropy, FrequenciesAndNumRo
                        compute_frequencies)
 from .scan import (ApproxCountDistinct, ApproxCountDistinctState, Completeness, Compliance,
                    Correlation, CorrelationState, MaxState, Maximum, Mean, MeanState, MinState,
-                   Minimum, NumMatches, Size, StandardDeviation, StandardDeviationState, Sum,
-                   SumState)
+                   Minimum, NumMatches, PatternMatch, Patterns, Size, StandardDeviation,
+                   StandardDeviationState, Sum, SumState)
+from .quantile import ApproxQuantile, ApproxQuantileState, QuantileSummaries
 from .state_provider import InMemoryStateProvider, StateLoader, StatePersister

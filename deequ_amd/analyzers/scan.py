@@ -97,6 +97,59 @@ class Compliance(StandardScanShareableAnalyzer):
 
 
 # ------------------------------------------------------------------------------------------------
+# PatternMatch (PatternMatch.scala:41-53)
+# ------------------------------------------------------------------------------------------------
+class Patterns:
+    """PatternMatch.scala:56-72 (Java regex syntax, compiled by deequ_amd/regex.py)."""
+    EMAIL = (r"""(?:[a-z0-9!#$%&'*+/=?^_`{|}~-]+(?:\.[a-z0-9!#$%&'*+/=?^_`{|}~-]+)*|"(?:[\x01-\x08\x0b"""
+             r"""\x0c\x0e-\x1f\x21\x23-\x5b\x5d-\x7f]|\\[\x01-\x09\x0b\x0c\x0e-\x7f])*")@(?:(?:[a-z0-9]"""
+             r"""(?:[a-z0-9-]*[a-z0-9])?\.)+[a-z0-9](?:[a-z0-9-]*[a-z0-9])?|\[(?:(?:25[0-5]|2[0-4][0-9]|"""
+             r"""[01]?[0-9][0-9]?)\.){3}(?:25[0-5]|2[0-4][0-9]|[01]?[0-9][0-9]?|[a-z0-9-]*[a-z0-9]:(?:"""
+             r"""[\x01-\x08\x0b\x0c\x0e-\x1f\x21-\x5a\x53-\x7f]|\\[\x01-\x09\x0b\x0c\x0e-\x7f])+)\])""")
+    URL = r"(https?|ftp)://[^\s/$.?#].[^\s]*"
+    SOCIAL_SECURITY_NUMBER_US = (
+        r"((?!219-09-9999|078-05-1120)(?!666|000|9\d{2})\d{3}-(?!00)\d{2}-(?!0{4})\d{4})|"
+        r"((?!219 09 9999|078 05 1120)(?!666|000|9\d{2})\d{3} (?!00)\d{2} (?!0{4})\d{4})|"
+        r"((?!219099999|078051120)(?!666|000|9\d{2})\d{3}(?!00)\d{2}(?!0{4})\d{4})")
+    CREDITCARD = (r"\b(?:3[47]\d{2}([\ \-]?)\d{6}\1\d|(?:(?:4\d|5[1-5]|65)\d{2}|6011)([\ \-]?)"
+                  r"\d{4}\2\d{4}\2)\d{4}\b")
+
+
+def _sql_string(s: str) -> str:
+    return "'" + s.replace("\\", "\\\\").replace("'", "''") + "'"
+
+
+@dataclass(frozen=True)
+class PatternMatch(StandardScanShareableAnalyzer):
+    """Fraction of rows (where `where` holds) whose first regex find() match in `column` is
+    non-empty: sum(when(regexp_extract(col, p, 0) != "", 1).otherwise(0)) / count(*).  The
+    pattern compiles to a byte automaton the device runs per row (XI_REGEX); an unsupported
+    pattern is a failure metric, never a different answer."""
+    column: str
+    pattern: str
+    where: Optional[str] = None
+    _options = ("where",)
+    _name = "PatternMatch"
+
+    def _instance(self):
+        return self.column
+
+    def aggregation_functions(self):
+        from ..sqlexpr import FIND_NONEMPTY
+        col = "`" + self.column.replace("`", "``") + "`"
+        return [AggSpec(N.AGG_COUNT_TRUE, expr=f"{FIND_NONEMPTY}({col}, {_sql_string(self.pattern)})",
+                        where=self.where),
+                conditional_count(self.where)]
+
+    def from_aggregation_result(self, result, offset):
+        return if_no_nulls_in(result, offset, 2, lambda: NumMatchesAndCount(
+            int(result[offset]), int(result[offset + 1])))
+
+    def preconditions(self):
+        return [Preconditions.has_column(self.column)] + super().preconditions()
+
+
+# ------------------------------------------------------------------------------------------------
 # Sum (Sum.scala:25-52)
 # ------------------------------------------------------------------------------------------------
 @dataclass(frozen=True)

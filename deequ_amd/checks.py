@@ -15,9 +15,9 @@ from dataclasses import dataclass, field
 from enum import Enum
 from typing import Any, Callable, List, Optional, Sequence
 
-from .analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlation, Distinctness,
-                        Entropy, Histogram, Maximum, Mean, Minimum, Size, StandardDeviation, Sum,
-                        UniqueValueRatio, Uniqueness)
+from .analyzers import (ApproxCountDistinct, ApproxQuantile, Completeness, Compliance, Correlation, Distinctness,
+                        Entropy, Histogram, Maximum, Mean, Minimum, PatternMatch, Patterns, Size,
+                        StandardDeviation, Sum, UniqueValueRatio, Uniqueness)
 from .analyzers.grouping import java_double_to_string
 
 
@@ -304,33 +304,38 @@ class Check:
         pred = f"{column} IS NULL OR ({column} {left} {lo} AND {column} {right} {hi})"
         return self.satisfies(pred, f"{column} between {lo} and {hi}", hint=hint)
 
-    # -- config-5 operators not built yet: loud failures -----------
     def has_pattern(self, column: str, pattern: str, assertion=None, name=None,
                     hint=None) -> "Check":
-        label = name or f"PatternMatchConstraint({column}, {pattern})"
-        return self.add_constraint(UnsupportedConstraint(label, "PatternMatch"))
+        """Check.scala:560-571 -> patternMatchConstraint (Constraint.scala:291-311)."""
+        assertion = assertion or IS_ONE
 
-    def contains_url(self, column: str, assertion=None, hint=None) -> "Check":
-        return self.add_constraint(UnsupportedConstraint(f"containsURL({column})",
-                                                         "PatternMatch(URL)"))
-
-    def contains_email(self, column: str, assertion=None, hint=None) -> "Check":
-        return self.add_constraint(UnsupportedConstraint(f"containsEmail({column})",
-                                                         "PatternMatch(EMAIL)"))
+        def make(w):
+            c = AnalysisBasedConstraint(PatternMatch(column, pattern, w), assertion, hint=hint)
+            return NamedConstraint(c, name or f"PatternMatchConstraint({column}, {pattern})")
+        return self._add_filterable(make)
 
     def contains_credit_card_number(self, column: str, assertion=None, hint=None) -> "Check":
-        return self.add_constraint(UnsupportedConstraint(
-            f"containsCreditCardNumber({column})", "PatternMatch(CREDITCARD)"))
+        return self.has_pattern(column, Patterns.CREDITCARD, assertion,
+                                f"containsCreditCardNumber({column})", hint)
+
+    def contains_email(self, column: str, assertion=None, hint=None) -> "Check":
+        return self.has_pattern(column, Patterns.EMAIL, assertion, f"containsEmail({column})", hint)
+
+    def contains_url(self, column: str, assertion=None, hint=None) -> "Check":
+        return self.has_pattern(column, Patterns.URL, assertion, f"containsURL({column})", hint)
 
     def contains_social_security_number(self, column: str, assertion=None,
                                         hint=None) -> "Check":
-        return self.add_constraint(UnsupportedConstraint(
-            f"containsSocialSecurityNumber({column})", "PatternMatch(SSN)"))
+        return self.has_pattern(column, Patterns.SOCIAL_SECURITY_NUMBER_US, assertion,
+                                f"containsSocialSecurityNumber({column})", hint)
 
-    def has_approx_quantile(self, column: str, quantile: float, assertion=None,
+    # -- operators not built yet: loud failures ------------------------------------------------
+    def has_approx_quantile(self, column: str, quantile: float, assertion,
                             hint=None) -> "Check":
-        return self.add_constraint(UnsupportedConstraint(
-            f"ApproxQuantileConstraint(ApproxQuantile({column},{quantile}))", "ApproxQuantile"))
+        """Check.scala:391-398 -> approxQuantileConstraint (Constraint.scala:368-381)."""
+        a = ApproxQuantile(column, quantile)
+        return self.add_constraint(NamedConstraint(AnalysisBasedConstraint(a, assertion, hint=hint),
+                                                   f"ApproxQuantileConstraint({a})"))
 
     def has_data_type(self, column: str, data_type=None, assertion=None, hint=None) -> "Check":
         return self.add_constraint(UnsupportedConstraint(f"DataTypeConstraint({column})",

@@ -125,6 +125,33 @@ static bool parse_node(const int64_t* w, int n, int& pos, std::unique_ptr<Node>&
     case DQ_X_EQ_NULL_SAFE:
       if (!child() || !child()) return false;
       break;
+    case DQ_X_REGEX: {
+      if (pos + 1 >= n) return false;
+      node->i = w[pos++];  // null_mode
+      const int64_t nb = w[pos++];
+      const int64_t nw = (nb + 7) / 8;
+      if (nb < 16 + 256 || pos + nw > n) return false;
+      node->s.assign(reinterpret_cast<const char*>(&w[pos]), (size_t)nb);
+      pos += (int)nw;
+      // validate the automaton's shape before any device code indexes it
+      int32_t hd[4];
+      memcpy(hd, node->s.data(), 16);
+      const int64_t ns = hd[0], nc = hd[1], st = hd[2];
+      if (ns < 1 || ns > 65535 || nc < 2 || nc > 257 || st < 0 || st >= ns) return false;
+      const int64_t need = 16 + 256 + ((ns + 3) & ~3LL) + 2 * ns * nc;
+      if (nb != need) return false;
+      const uint8_t* cls = reinterpret_cast<const uint8_t*>(node->s.data()) + 16;
+      for (int b = 0; b < 256; ++b)
+        if (cls[b] >= nc - 1) return false;
+      const uint16_t* nx = reinterpret_cast<const uint16_t*>(node->s.data() + 16 + 256 + ((ns + 3) & ~3LL));
+      for (int64_t k = 0; k < ns * nc; ++k) {
+        uint16_t v;
+        memcpy(&v, nx + k, 2);
+        if (v >= ns) return false;
+      }
+      if (!child()) return false;
+      break;
+    }
     case DQ_X_IN: {
       if (pos >= n) return false;
       int64_t items = w[pos++];
@@ -177,6 +204,12 @@ static void compile_postfix(const Node& n, std::vector<XInstr>& prog, std::strin
     case DQ_X_OR: ins = {XI_OR, 0, 0}; break;
     case DQ_X_IN: ins = {XI_IN, (int32_t)n.kids.size() - 1, 0}; break;
     case DQ_X_CAST_F64: ins = {XI_CAST_F64, 0, 0}; break;
+    case DQ_X_REGEX: {
+      while (pool.size() % 8) pool.push_back('\0');
+      ins = {XI_REGEX, (int32_t)n.i, (int64_t)pool.size()};
+      pool += n.s;
+      break;
+    }
     default: ins = {XI_CMP, n.op, 0}; break;
   }
   prog.push_back(ins);
@@ -789,7 +822,8 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
   // pool offsets in the programs are relative to each expression's own pool
   for (size_t k = 0; k < plan->mat.size(); ++k)
     for (size_t q = 0; q < plan->mat[k].prog.size(); ++q)
-      if (prog[s->prog_off[k] + q].op == XI_STR) prog[s->prog_off[k] + q].imm += s->pool_off[k];
+      if (prog[s->prog_off[k] + q].op == XI_STR || prog[s->prog_off[k] + q].op == XI_REGEX)
+        prog[s->prog_off[k] + q].imm += s->pool_off[k];
   HIP_TRY(s->d_prog.ensure(std::max<size_t>(1, prog.size())));
   if (!prog.empty())
     HIP_TRY(hipMemcpy(s->d_prog.p, prog.data(), prog.size() * sizeof(XInstr), hipMemcpyHostToDevice));

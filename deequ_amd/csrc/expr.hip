@@ -260,6 +260,46 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
             }
             break;
           }
+          case XI_REGEX: {  // find() over x's text with a compiled automaton (regex.py)
+            V& a = st[sp - 1];
+            if (a.tag == 0 || a.tag == 3) {  // NULL (a double never gets here: the planner
+              if (ins.a) a = V{1, 0, 0, 0.0, nullptr};  // refuses it); null_mode 1 -> FALSE
+              else a = V{0, 0, 0, 0.0, nullptr};
+              break;
+            }
+            const uint8_t* blob = pool + ins.imm;
+            const int32_t ns = reinterpret_cast<const int32_t*>(blob)[0];
+            const int32_t nc = reinterpret_cast<const int32_t*>(blob)[1];
+            uint32_t q = (uint32_t)reinterpret_cast<const int32_t*>(blob)[2];
+            const uint8_t* cls = blob + 16;
+            const uint8_t* status = blob + 16 + 256;
+            const uint16_t* nx = reinterpret_cast<const uint16_t*>(blob + 16 + 256 + ((ns + 3) & ~3));
+            if (a.tag == 4) {
+              DevBytes rd{a.p};
+              for (int32_t k = 0; k < a.len && !status[q]; ++k) q = nx[q * nc + cls[rd.u8(k)]];
+            } else {  // Spark's cast to string: decimal integer, or true / false
+              char buf[24];
+              int nb = 0;
+              if (a.tag == 1) {
+                const char* t = a.i ? "true" : "false";
+                for (; t[nb]; ++nb) buf[nb] = t[nb];
+              } else {
+                uint64_t m = a.i < 0 ? 0ULL - (uint64_t)a.i : (uint64_t)a.i;
+                char tmp[20];
+                int nd = 0;
+                do {
+                  tmp[nd++] = (char)('0' + m % 10);
+                  m /= 10;
+                } while (m);
+                if (a.i < 0) buf[nb++] = '-';
+                while (nd) buf[nb++] = tmp[--nd];
+              }
+              for (int k = 0; k < nb && !status[q]; ++k) q = nx[q * nc + cls[(uint8_t)buf[k]]];
+            }
+            if (!status[q]) q = nx[q * nc + nc - 1];  // end of text
+            a = V{1, 0, status[q] == 1 ? 1 : 0, 0.0, nullptr};
+            break;
+          }
           default: break;
         }
       }

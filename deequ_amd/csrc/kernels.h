@@ -76,7 +76,8 @@ enum XiOp : int32_t {
   XI_OR,
   XI_CMP,        // a = dq_xop comparison
   XI_IN,         // a = number of list items
-  XI_CAST_F64
+  XI_CAST_F64,
+  XI_REGEX       // a = null_mode, imm = offset of the automaton in the pool
 };
 
 struct XInstr {

@@ -1,0 +1,129 @@
+// quantile.hip -- the device half of ApproxQuantile (ApproxQuantile.scala:41-104).
+//
+// The reference feeds every non-NULL value, as a double, into Spark's ApproximatePercentile
+// (QuantileSummaries, Greenwald-Khanna with relativeError).  Here the values of all batches are
+// gathered as doubles, sorted on the device (rocPRIM radix sort: the order is Java's
+// Double.compare once NaNs are canonical, -0.0 before 0.0), and handed to the host as either every
+// value (few enough that the host replays Spark's own insert + compress exactly) or values at
+// evenly spaced exact ranks (a GK summary whose error is far inside relativeError).  The summary
+// arithmetic -- insert, compress, merge, query -- is host code (deequ_amd/analyzers/quantile.py).
+#include <hip/hip_runtime.h>
+
+#include <cstring>  // rocprim headers use memset without including it
+
+#include <rocprim/rocprim.hpp>
+
+#include <vector>
+
+#include "device_util.h"
+#include "kernels.h"
+
+using namespace dq;
+
+namespace {
+
+constexpr int kGatherThreads = 256;
+
+// Non-NULL values of one batch -> doubles at out[*cursor ...] (order irrelevant: sorted next).
+__global__ void __launch_bounds__(kGatherThreads)
+quantile_gather(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
+                int64_t rows, double* __restrict__ out, unsigned long long* __restrict__ cursor) {
+  const int64_t stride = (int64_t)gridDim.x * kGatherThreads;
+  for (int64_t r0 = (int64_t)blockIdx.x * kGatherThreads; r0 < rows; r0 += stride) {
+    const int64_t r = r0 + threadIdx.x;
+    bool keep = false;
+    double v = 0.0;
+    if (r < rows && bit1(valid, r)) {
+      keep = true;
+      v = load_f64(type, values, r);
+      if (v != v) v = __builtin_nan("");  // Double.compare: every NaN is the canonical one
+    }
+    const uint64_t m = __ballot(keep);
+    unsigned long long base = 0;
+    if (__lane_id() == 0 && m) base = atomicAdd(cursor, (unsigned long long)__popcll(m));
+    base = __shfl(base, 0);
+    if (keep) out[base + __popcll(m & ((1ULL << __lane_id()) - 1))] = v;
+  }
+}
+
+// out[j] = sorted[floor(j * (count - 1) / (n - 1))], j < n: the min, the max and evenly spaced
+// exact ranks between
+__global__ void quantile_pick(const double* __restrict__ sorted, int64_t count, int64_t n,
+                              double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int64_t r = n > 1 ? (int64_t)(((__int128)j * (count - 1)) / (n - 1)) : 0;
+  out[j] = sorted[r];
+}
+
+struct DevMem {
+  void* p = nullptr;
+  ~DevMem() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+}  // namespace
+
+extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int n_batches,
+                                      int64_t max_values, double* out, int64_t* n_out,
+                                      int64_t* count_out, void* hip_stream) {
+  if (!n_out || !count_out || (n_batches > 0 && !batches) || n_batches < 0 || max_values < 2)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "bad argument to dq_sorted_sample");
+  hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
+  HIP_TRY(hipSetDevice(device));
+  int64_t rows = 0;
+  for (int b = 0; b < n_batches; ++b) {
+    const dq_column& c = batches[b];
+    if (c.type == DQ_UTF8 || c.type == DQ_BOOL || c.type < DQ_BOOL || c.type > DQ_UTF8)
+      return fail(DQ_ERR_WRONG_TYPE, "ApproxQuantile needs a numeric column");
+    if (b && c.type != batches[0].type) return fail(DQ_ERR_WRONG_TYPE, "batches differ in type");
+    if (c.length < 0 || (c.length > 0 && !c.values))
+      return fail(DQ_ERR_INVALID_ARGUMENT, "batch %d has no values", b);
+    rows += c.length;
+  }
+  *n_out = 0;
+  *count_out = 0;
+  if (rows == 0) return DQ_OK;
+  DevMem keys, sorted, cur, tmp, picks;
+  HIP_TRY(hipMalloc(&keys.p, (size_t)rows * 8));
+  HIP_TRY(hipMalloc(&sorted.p, (size_t)rows * 8));
+  HIP_TRY(hipMalloc(&cur.p, 8));
+  HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
+  auto* kp = static_cast<double*>(keys.p);
+  auto* cp = static_cast<unsigned long long*>(cur.p);
+  for (int b = 0; b < n_batches; ++b) {
+    const dq_column& c = batches[b];
+    if (!c.length) continue;
+    const int64_t blocks = std::min<int64_t>((c.length + kGatherThreads - 1) / kGatherThreads, 8192);
+    hipLaunchKernelGGL(quantile_gather, dim3((unsigned)blocks), dim3(kGatherThreads), 0, stream,
+                       c.type, c.validity, c.values, c.length, kp, cp);
+    HIP_TRY(hipGetLastError());
+  }
+  unsigned long long count = 0;
+  HIP_TRY(hipMemcpyAsync(&count, cp, 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  *count_out = (int64_t)count;
+  if (!count) return DQ_OK;
+  size_t tmp_bytes = 0;
+  HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, kp, static_cast<double*>(sorted.p),
+                                   (size_t)count, 0, 64, stream));
+  HIP_TRY(hipMalloc(&tmp.p, std::max<size_t>(tmp_bytes, 16)));
+  HIP_TRY(rocprim::radix_sort_keys(tmp.p, tmp_bytes, kp, static_cast<double*>(sorted.p),
+                                   (size_t)count, 0, 64, stream));
+  const int64_t n = (int64_t)count <= max_values ? (int64_t)count : max_values;
+  *n_out = n;
+  if (!out) return DQ_OK;  // size query only
+  if (n == (int64_t)count) {
+    HIP_TRY(hipMemcpyAsync(out, sorted.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
+  } else {
+    HIP_TRY(hipMalloc(&picks.p, (size_t)n * 8));
+    hipLaunchKernelGGL(quantile_pick, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                       static_cast<const double*>(sorted.p), (int64_t)count, n,
+                       static_cast<double*>(picks.p));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
+  }
+  HIP_TRY(hipStreamSynchronize(stream));
+  return DQ_OK;
+}

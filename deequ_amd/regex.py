@@ -1,0 +1,986 @@
+"""Java regular expressions -> byte DFAs for the device (PatternMatch, PatternMatch.scala:41-53).
+
+PatternMatch counts a row when ``regexp_extract(col, pattern, 0) != ""``: Java's first
+``Matcher.find()`` match exists and is non-empty.  For a pattern that cannot match the empty string
+(every pattern of ``Patterns``, PatternMatch.scala:57-72) that is "some substring matches", a
+regular property of the row's UTF-8 bytes, so the pattern compiles to ONE deterministic automaton
+over bytes the device runs per row (deequ_amd/csrc/expr.hip, XI_REGEX): no backtracking, no
+per-row allocation.
+
+Language model.  The automaton reads the whole row and then an end-of-text symbol (EOT, class
+256), and accepts iff the row is in  Sigma* P Sigma* EOT.  Lookaheads and word boundaries are
+compiled in continuation-passing style: ``(?!X)`` at a point whose continuation (the rest of the
+pattern, then Sigma* EOT) is C becomes  C minus (X Sigma* EOT), a product construction on the two
+DFAs.  The DFA's states from which every input is accepted / rejected are marked so the device
+stops early.
+
+Supported Java syntax: literals and escapes (\\t \\n \\r \\f \\a \\e \\xhh \\uhhhh \\0o \\cX and
+escaped metacharacters), ``.`` (any code point but the Java line terminators), classes with ranges,
+negation, nested escapes and \\d \\D \\s \\S \\w \\W (ASCII, as Java without UNICODE_CHARACTER_CLASS),
+groups ( ), (?: ), alternation, greedy / lazy quantifiers * + ? {n} {n,} {n,m}, lookaheads (?= )
+(?! ), back-references to groups with a finite language (expanded: the CREDITCARD separators),
+^ / \\A at the start, $ / \\z at the end, \\b at the start or end of the pattern.  Rejected (a
+PatternNotSupported error, never a silently different answer): patterns that can match the empty
+string, possessive quantifiers, lookbehind, inline flags, \\b / anchors elsewhere, and automata above
+``MAX_STATES``.  Known approximation: \\b treats every non-ASCII code point as a word character
+(Java's \\b uses Character.isLetterOrDigit).
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass
+from typing import Dict, FrozenSet, List, Optional, Sequence, Tuple
+
+EOT = 256
+NSYM = 257
+MAX_STATES = 4096
+MAX_CP = 0x10FFFF
+
+
+class PatternNotSupported(ValueError):
+    pass
+
+
+# ------------------------------------------------------------------------------------------------
+# Character sets: sorted disjoint code point intervals
+# ------------------------------------------------------------------------------------------------
+def cs_norm(r: Sequence[Tuple[int, int]]) -> Tuple[Tuple[int, int], ...]:
+    out: List[List[int]] = []
+    for a, b in sorted(r):
+        if out and a <= out[-1][1] + 1:
+            out[-1][1] = max(out[-1][1], b)
+        else:
+            out.append([a, b])
+    return tuple((a, b) for a, b in out)
+
+
+def cs_neg(r) -> Tuple[Tuple[int, int], ...]:
+    out, lo = [], 0
+    for a, b in cs_norm(r):
+        if a > lo:
+            out.append((lo, a - 1))
+        lo = b + 1
+    if lo <= MAX_CP:
+        out.append((lo, MAX_CP))
+    return tuple(out)
+
+
+DIGIT = ((48, 57),)
+WORD = cs_norm([(48, 57), (65, 90), (95, 95), (97, 122)])
+SPACE = cs_norm([(9, 13), (32, 32)])  # [ \t\n\x0B\f\r]
+LINE_TERMINATORS = cs_norm([(10, 10), (13, 13), (0x85, 0x85), (0x2028, 0x2029)])
+DOT = cs_neg(LINE_TERMINATORS)
+ANY = ((0, MAX_CP),)
+
+
+# ------------------------------------------------------------------------------------------------
+# AST
+# ------------------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class Chars:
+    ranges: Tuple[Tuple[int, int], ...]
+
+
+@dataclass(frozen=True)
+class Seq:
+    items: Tuple
+
+
+@dataclass(frozen=True)
+class Alt:
+    options: Tuple
+
+
+@dataclass(frozen=True)
+class Repeat:
+    node: object
+    lo: int
+    hi: Optional[int]  # None = unbounded
+
+
+@dataclass(frozen=True)
+class Group:
+    node: object
+    index: Optional[int]  # capturing group number, None for (?: )
+
+
+@dataclass(frozen=True)
+class Look:
+    node: object
+    negative: bool
+
+
+@dataclass(frozen=True)
+class BackRef:
+    index: int
+
+
+@dataclass(frozen=True)
+class Anchor:
+    kind: str  # "^", "$", "\\b"
+
+
+EMPTY = Seq(())
+
+
+class _Parser:
+    def __init__(self, pattern: str):
+        self.s = pattern
+        self.i = 0
+        self.groups = 0
+
+    def error(self, msg):
+        raise PatternNotSupported(f"{msg} at position {self.i} of /{self.s}/")
+
+    def peek(self):
+        return self.s[self.i] if self.i < len(self.s) else None
+
+    def take(self):
+        c = self.s[self.i]
+        self.i += 1
+        return c
+
+    def parse(self):
+        node = self.alt()
+        if self.i != len(self.s):
+            self.error("unbalanced ')'")
+        return node
+
+    def alt(self):
+        opts = [self.seq()]
+        while self.peek() == "|":
+            self.take()
+            opts.append(self.seq())
+        return opts[0] if len(opts) == 1 else Alt(tuple(opts))
+
+    def seq(self):
+        items = []
+        while self.peek() is not None and self.peek() not in "|)":
+            items.append(self.quantified())
+        return items[0] if len(items) == 1 else Seq(tuple(items))
+
+    def quantified(self):
+        atom = self.atom()
+        while True:
+            c = self.peek()
+            if c == "*":
+                self.take()
+                lo, hi = 0, None
+            elif c == "+":
+                self.take()
+                lo, hi = 1, None
+            elif c == "?":
+                self.take()
+                lo, hi = 0, 1
+            elif c == "{" and self._is_counted():
+                lo, hi = self._counted()
+            else:
+                return atom
+            if isinstance(atom, (Anchor, Look)):
+                self.error("quantified assertion")
+            if self.peek() == "?":  # lazy: same language (find() semantics on non-empty matches)
+                self.take()
+            elif self.peek() == "+":
+                self.error("possessive quantifier")
+            atom = Repeat(atom, lo, hi)
+
+    def _is_counted(self):
+        j = self.i + 1
+        while j < len(self.s) and (self.s[j].isdigit() or self.s[j] == ","):
+            j += 1
+        return j < len(self.s) and self.s[j] == "}" and j > self.i + 1 and self.s[self.i + 1].isdigit()
+
+    def _counted(self):
+        self.take()
+        j = self.s.index("}", self.i)
+        body = self.s[self.i:j]
+        self.i = j + 1
+        if "," in body:
+            a, b = body.split(",", 1)
+            return int(a), (int(b) if b else None)
+        return int(body), int(body)
+
+    def atom(self):
+        c = self.take()
+        if c == "(":
+            if self.s.startswith("?:", self.i):
+                self.i += 2
+                node = Group(self.alt(), None)
+            elif self.s.startswith("?!", self.i) or self.s.startswith("?=", self.i):
+                neg = self.s[self.i + 1] == "!"
+                self.i += 2
+                node = Look(self.alt(), neg)
+            elif self.peek() == "?":
+                self.error("unsupported group construct (lookbehind, named group or inline flag)")
+            else:
+                self.groups += 1
+                idx = self.groups
+                node = Group(self.alt(), idx)
+            if self.peek() != ")":
+                self.error("missing ')'")
+            self.take()
+            return node
+        if c == "[":
+            return Chars(self.char_class())
+        if c == ".":
+            return Chars(DOT)
+        if c == "^":
+            return Anchor("^")
+        if c == "$":
+            return Anchor("$")
+        if c == "\\":
+            return self.escape(in_class=False)
+        if c in "*+?":
+            self.error("dangling quantifier")
+        return Chars(((ord(c), ord(c)),))
+
+    def escape(self, in_class: bool):
+        if self.peek() is None:
+            self.error("trailing backslash")
+        c = self.take()
+        simple = {"t": 9, "n": 10, "r": 13, "f": 12, "a": 7, "e": 27}
+        if c in simple:
+            v = simple[c]
+            return Chars(((v, v),)) if not in_class else ((v, v),)
+        classes = {"d": DIGIT, "D": cs_neg(DIGIT), "s": SPACE, "S": cs_neg(SPACE), "w": WORD,
+                   "W": cs_neg(WORD)}
+        if c in classes:
+            return Chars(classes[c]) if not in_class else classes[c]
+        if c == "x":
+            v = int(self.s[self.i:self.i + 2], 16)
+            self.i += 2
+        elif c == "u":
+            v = int(self.s[self.i:self.i + 4], 16)
+            self.i += 4
+        elif c == "0":
+            j = self.i
+            while j < len(self.s) and j < self.i + 3 and self.s[j] in "01234567":
+                j += 1
+            v = int(self.s[self.i:j] or "0", 8)
+            self.i = j
+        elif c == "c":
+            v = ord(self.take()) ^ 64
+        elif c.isdigit() and not in_class:
+            return BackRef(int(c))
+        elif c in "bB" and not in_class:
+            if c == "B":
+                self.error("\\B")
+            return Anchor("\\b")
+        elif c in "AzZ" and not in_class:
+            return Anchor("^" if c == "A" else "$")
+        elif c.isalnum():
+            self.error(f"unsupported escape \\{c}")
+        else:
+            v = ord(c)
+        return Chars(((v, v),)) if not in_class else ((v, v),)
+
+    def char_class(self):
+        neg = False
+        if self.peek() == "^":
+            self.take()
+            neg = True
+        ranges: List[Tuple[int, int]] = []
+        first = True
+        while True:
+            c = self.peek()
+            if c is None:
+                self.error("missing ']'")
+            if c == "]" and not first:
+                self.take()
+                break
+            first = False
+            if c == "[":
+                self.error("nested character class")
+            if c == "&" and self.s.startswith("&&", self.i):
+                self.error("class intersection")
+            self.take()
+            if c == "\\":
+                lo_set = self.escape(in_class=True)
+            else:
+                lo_set = ((ord(c), ord(c)),)
+            if (len(lo_set) == 1 and lo_set[0][0] == lo_set[0][1] and self.peek() == "-"
+                    and self.i + 1 < len(self.s) and self.s[self.i + 1] != "]"):
+                self.take()
+                d = self.take()
+                if d == "\\":
+                    hi_set = self.escape(in_class=True)
+                    if len(hi_set) != 1 or hi_set[0][0] != hi_set[0][1]:
+                        self.error("class range to a class")
+                    hi = hi_set[0][0]
+                else:
+                    hi = ord(d)
+                if hi < lo_set[0][0]:
+                    self.error("inverted class range")
+                ranges.append((lo_set[0][0], hi))
+            else:
+                ranges.extend(lo_set)
+        r = cs_norm(ranges)
+        return cs_neg(r) if neg else r
+
+
+# ------------------------------------------------------------------------------------------------
+# AST analysis and rewriting
+# ------------------------------------------------------------------------------------------------
+def nullable(n) -> bool:
+    if isinstance(n, Chars):
+        return False
+    if isinstance(n, Seq):
+        return all(nullable(x) for x in n.items)
+    if isinstance(n, Alt):
+        return any(nullable(x) for x in n.options)
+    if isinstance(n, Repeat):
+        return n.lo == 0 or nullable(n.node)
+    if isinstance(n, Group):
+        return nullable(n.node)
+    if isinstance(n, (Look, Anchor)):
+        return True
+    if isinstance(n, BackRef):
+        return True  # conservatively (the group may match "")
+    raise TypeError(n)
+
+
+def finite_strings(n, limit=64) -> Optional[List[str]]:
+    """The finite language of a lookaround-free node, or None (infinite / too many)."""
+    if isinstance(n, Chars):
+        total = sum(b - a + 1 for a, b in n.ranges)
+        if total > limit:
+            return None
+        return [chr(c) for a, b in n.ranges for c in range(a, b + 1)]
+    if isinstance(n, Seq):
+        out = [""]
+        for x in n.items:
+            part = finite_strings(x, limit)
+            if part is None:
+                return None
+            out = [a + b for a in out for b in part]
+            if len(out) > limit:
+                return None
+        return out
+    if isinstance(n, Alt):
+        out = []
+        for x in n.options:
+            part = finite_strings(x, limit)
+            if part is None:
+                return None
+            out += part
+        return list(dict.fromkeys(out)) if len(out) <= limit else None
+    if isinstance(n, Group):
+        return finite_strings(n.node, limit)
+    if isinstance(n, Repeat):
+        if n.hi is None:
+            return None
+        base = finite_strings(n.node, limit)
+        if base is None:
+            return None
+        out, cur = [], [""]
+        for k in range(n.hi + 1):
+            if k >= n.lo:
+                out += cur
+            cur = [a + b for a in cur for b in base]
+            if len(out) > limit or len(cur) > limit * limit:
+                return None
+        return list(dict.fromkeys(out))
+    return None
+
+
+def _literal(s: str):
+    return Seq(tuple(Chars(((ord(c), ord(c)),)) for c in s))
+
+
+def _subst(n, index: int, value: str):
+    """Group `index` -> the literal `value`, \\index -> the same literal."""
+    if isinstance(n, Group):
+        if n.index == index:
+            return Group(_literal(value), None)
+        return Group(_subst(n.node, index, value), n.index)
+    if isinstance(n, BackRef):
+        return _literal(value) if n.index == index else n
+    if isinstance(n, Seq):
+        return Seq(tuple(_subst(x, index, value) for x in n.items))
+    if isinstance(n, Alt):
+        return Alt(tuple(_subst(x, index, value) for x in n.options))
+    if isinstance(n, Repeat):
+        return Repeat(_subst(n.node, index, value), n.lo, n.hi)
+    if isinstance(n, Look):
+        return Look(_subst(n.node, index, value), n.negative)
+    return n
+
+
+def _find_group(n, index):
+    if isinstance(n, Group):
+        if n.index == index:
+            return n
+        return _find_group(n.node, index)
+    for attr in ("items", "options"):
+        if hasattr(n, attr):
+            for x in getattr(n, attr):
+                g = _find_group(x, index)
+                if g is not None:
+                    return g
+    if isinstance(n, (Repeat, Look)):
+        return _find_group(n.node, index)
+    return None
+
+
+def _backrefs(n) -> List[int]:
+    if isinstance(n, BackRef):
+        return [n.index]
+    out = []
+    for attr in ("items", "options"):
+        if hasattr(n, attr):
+            for x in getattr(n, attr):
+                out += _backrefs(x)
+    if isinstance(n, (Repeat, Look, Group)):
+        out += _backrefs(n.node)
+    return out
+
+
+def expand_backrefs(n):
+    """A back-reference to a group with a small finite language (CREDITCARD's separator) becomes a
+    union over that language of the pattern with group and reference both set to the value."""
+    refs = sorted(set(_backrefs(n)))
+    for k in refs:
+        g = _find_group(n, k)
+        if g is None:
+            raise PatternNotSupported(f"back-reference \\{k} to a missing group")
+        values = finite_strings(g.node, 16)
+        if values is None:
+            raise PatternNotSupported(f"back-reference \\{k} to a group with an unbounded language")
+        n = Alt(tuple(_subst(n, k, v) for v in values))
+    return n
+
+
+# ------------------------------------------------------------------------------------------------
+# Automata over bytes + EOT
+# ------------------------------------------------------------------------------------------------
+def _utf8_ranges(lo: int, hi: int) -> List[List[Tuple[int, int]]]:
+    """Code points [lo, hi] as a union of byte-range sequences (UTF-8, no surrogate check)."""
+    out = []
+    bounds = [(0, 0x7F, 1), (0x80, 0x7FF, 2), (0x800, 0xFFFF, 3), (0x10000, MAX_CP, 4)]
+    for blo, bhi, n in bounds:
+        a, b = max(lo, blo), min(hi, bhi)
+        if a <= b:
+            out += _split(a, b, n)
+    return out
+
+
+def _enc(c: int, n: int) -> List[int]:
+    if n == 1:
+        return [c]
+    if n == 2:
+        return [0xC0 | (c >> 6), 0x80 | (c & 0x3F)]
+    if n == 3:
+        return [0xE0 | (c >> 12), 0x80 | ((c >> 6) & 0x3F), 0x80 | (c & 0x3F)]
+    return [0xF0 | (c >> 18), 0x80 | ((c >> 12) & 0x3F), 0x80 | ((c >> 6) & 0x3F), 0x80 | (c & 0x3F)]
+
+
+def _split(a: int, b: int, n: int) -> List[List[Tuple[int, int]]]:
+    if n == 1:
+        return [[(a, b)]]
+    # split so that all but the first byte span full continuation ranges
+    for k in range(1, n):
+        m = (1 << (6 * k)) - 1
+        if (a & ~m) != (b & ~m):
+            if a & m:
+                return _split(a, a | m, n) + _split((a | m) + 1, b, n)
+            if (b & m) != m:
+                return _split(a, (b & ~m) - 1, n) + _split(b & ~m, b, n)
+    ea, eb = _enc(a, n), _enc(b, n)
+    return [[(x, y) for x, y in zip(ea, eb)]]
+
+
+class NFA:
+    """Thompson-style NFA: trans[s] = list of (symbol bitmask, t); eps[s] = list of t."""
+
+    def __init__(self):
+        self.trans: List[List[Tuple[int, int]]] = []
+        self.eps: List[List[int]] = []
+
+    def new(self) -> int:
+        self.trans.append([])
+        self.eps.append([])
+        return len(self.trans) - 1
+
+
+def _mask(lo: int, hi: int) -> int:
+    return ((1 << (hi + 1)) - 1) ^ ((1 << lo) - 1)
+
+
+ALL_BYTES = _mask(0, 255)
+
+
+class DFA:
+    def __init__(self, nxt: List[List[int]], accept: List[bool], start: int):
+        self.nxt = nxt        # nxt[state][symbol], symbol in 0..256
+        self.accept = accept
+        self.start = start
+
+    @property
+    def n(self):
+        return len(self.nxt)
+
+
+def determinize(nfa: NFA, start: int, finals: FrozenSet[int], univ: int = -1) -> DFA:
+    """Subset construction.  `univ` (optional) is a state whose language is everything (Sigma* EOT):
+    a subset containing it is that state alone, which keeps the search automaton from tracking
+    candidates once one has matched."""
+    def closure(states):
+        stack, seen = list(states), set(states)
+        while stack:
+            s = stack.pop()
+            for t in nfa.eps[s]:
+                if t not in seen:
+                    seen.add(t)
+                    stack.append(t)
+        return frozenset(seen)
+
+    u0 = closure([univ]) if univ >= 0 else None
+
+    def canon(t):
+        return u0 if u0 is not None and univ in t else t
+
+    s0 = canon(closure([start]))
+    index: Dict[FrozenSet[int], int] = {s0: 0}
+    order = [s0]
+    nxt: List[List[int]] = []
+    accept: List[bool] = []
+    i = 0
+    while i < len(order):
+        cur = order[i]
+        i += 1
+        accept.append(bool(cur & finals))
+        # group the outgoing transitions by symbol
+        moves: Dict[int, set] = {}
+        edges = [(m, t) for s in cur for m, t in nfa.trans[s]]
+        row = [0] * NSYM
+        if edges:
+            # symbols in play: split by distinct masks
+            syms = 0
+            for m, _ in edges:
+                syms |= m
+            for sym in range(NSYM):
+                if not (syms >> sym) & 1:
+                    continue
+                tgt = frozenset(t for m, t in edges if (m >> sym) & 1)
+                moves.setdefault(sym, tgt)
+        targets: Dict[FrozenSet[int], int] = {}
+        for sym in range(NSYM):
+            tgt = moves.get(sym)
+            if not tgt:
+                tset = frozenset()
+            else:
+                tset = targets.get(tgt)
+                if tset is None:
+                    tset = canon(closure(tgt))
+                    targets[tgt] = tset
+            if tset not in index:
+                if len(order) >= MAX_STATES:
+                    raise PatternNotSupported(f"automaton exceeds {MAX_STATES} states")
+                index[tset] = len(order)
+                order.append(tset)
+            row[sym] = index[tset]
+        nxt.append(row)
+    return DFA(nxt, accept, 0)
+
+
+def dfa_to_nfa(d: DFA, nfa: NFA, univ: int) -> Tuple[int, int]:
+    """Embeds a DFA (a language of whole remaining texts, EOT included) into an NFA; returns
+    (start, final) with eps from accepting states.  States from which every text is accepted
+    become the shared universal state `univ`; states from which none is are dropped."""
+    n = d.n
+    bad = [not d.accept[d.nxt[q][EOT]] for q in range(n)]  # some text (here: the empty one) fails
+    live = [d.accept[q] for q in range(n)]
+    changed = True
+    while changed:
+        changed = False
+        for q in range(n):
+            if not bad[q] and any(bad[d.nxt[q][b]] for b in range(256)):
+                bad[q] = changed = True
+            if not live[q] and any(live[t] for t in d.nxt[q]):
+                live[q] = changed = True
+    final = nfa.new()
+    base = {}
+    for q in range(n):
+        if not live[q]:
+            continue
+        base[q] = univ if not bad[q] else nfa.new()
+    for q, node in base.items():
+        if node == univ:
+            continue
+        by_t: Dict[int, int] = {}
+        for sym, t in enumerate(d.nxt[q]):
+            if t in base:
+                by_t[t] = by_t.get(t, 0) | (1 << sym)
+        for t, m in by_t.items():
+            nfa.trans[node].append((m, base[t]))
+        if d.accept[q]:
+            nfa.eps[node].append(final)
+    if d.start not in base:  # the empty language: a start state with no way out
+        return nfa.new(), final
+    return base[d.start], final
+
+
+def product(a: DFA, b: DFA, op) -> DFA:
+    index = {(a.start, b.start): 0}
+    order = [(a.start, b.start)]
+    nxt, acc = [], []
+    i = 0
+    while i < len(order):
+        x, y = order[i]
+        i += 1
+        acc.append(op(a.accept[x], b.accept[y]))
+        row = []
+        for sym in range(NSYM):
+            p = (a.nxt[x][sym], b.nxt[y][sym])
+            if p not in index:
+                if len(order) >= MAX_STATES:
+                    raise PatternNotSupported(f"automaton exceeds {MAX_STATES} states")
+                index[p] = len(order)
+                order.append(p)
+            row.append(index[p])
+        nxt.append(row)
+    return DFA(nxt, acc, 0)
+
+
+def minimize(d: DFA) -> DFA:
+    """Moore partition refinement (small automata)."""
+    part = [1 if a else 0 for a in d.accept]
+    while True:
+        sig = {}
+        newp = []
+        for s in range(d.n):
+            key = (part[s], tuple(part[t] for t in d.nxt[s]))
+            if key not in sig:
+                sig[key] = len(sig)
+            newp.append(sig[key])
+        if len(sig) == len(set(part)):
+            part = newp
+            break
+        part = newp
+    k = max(part) + 1
+    nxt = [None] * k
+    acc = [False] * k
+    for s in range(d.n):
+        p = part[s]
+        if nxt[p] is None:
+            nxt[p] = [part[t] for t in d.nxt[s]]
+            acc[p] = d.accept[s]
+    return DFA(nxt, acc, part[d.start])
+
+
+class _Compiler:
+    """Thompson construction in continuation-passing style: build(node, s, cont) compiles `node`
+    from state s and calls cont(t) exactly once with the state after it (alternatives and
+    optional repetitions meet in a join state first), so the rest of the pattern is compiled once.
+    A lookahead instead compiles its continuation from a fresh state and records itself; after the
+    whole graph exists, lookaheads are resolved right to left: the continuation's DFA (rest of the
+    pattern, Sigma*, EOT) combined with X Sigma* EOT (minus for (?! ), intersection for (?= )),
+    embedded between s and the final state."""
+
+    def __init__(self):
+        self.nfa = NFA()
+        self.final = -1
+        self._univ = -1
+        self.pending: List[Tuple[int, int, object]] = []
+
+    @property
+    def univ(self) -> int:
+        """Sigma* EOT -> final (created on first use, after `final`)."""
+        if self._univ < 0:
+            u = self.nfa.new()
+            self.nfa.trans[u].append((ALL_BYTES, u))
+            self.nfa.trans[u].append((1 << EOT, self.final))
+            self._univ = u
+        return self._univ
+
+    def chars(self, ranges, s: int, t: int):
+        """s --(one code point in ranges)--> t."""
+        for seq in (x for a, b in ranges for x in _utf8_ranges(a, b)):
+            cur = s
+            for k, (lo, hi) in enumerate(seq):
+                nx = t if k == len(seq) - 1 else self.nfa.new()
+                self.nfa.trans[cur].append((_mask(lo, hi), nx))
+                cur = nx
+
+    def anything(self, s: int) -> int:
+        """s --(any bytes)*--> returned state (Sigma* over bytes)."""
+        t = self.nfa.new()
+        self.nfa.eps[s].append(t)
+        self.nfa.trans[t].append((ALL_BYTES, t))
+        return t
+
+    def join(self, cont):
+        j = self.nfa.new()
+        return j, (lambda x: self.nfa.eps[x].append(j))
+
+    def build(self, node, s: int, cont) -> None:
+        if isinstance(node, Chars):
+            m = self.nfa.new()
+            self.chars(node.ranges, s, m)
+            cont(m)
+        elif isinstance(node, Seq):
+            def go(i, st):
+                if i == len(node.items):
+                    cont(st)
+                else:
+                    self.build(node.items[i], st, lambda x: go(i + 1, x))
+            go(0, s)
+        elif isinstance(node, Alt):
+            j, to_j = self.join(cont)
+            for o in node.options:
+                self.build(o, s, to_j)
+            cont(j)
+        elif isinstance(node, Group):
+            self.build(node.node, s, cont)
+        elif isinstance(node, Repeat):
+            if _has_look(node.node):
+                raise PatternNotSupported("lookaround inside a quantifier")
+            j, to_j = self.join(cont)
+
+            def rep(k, st):
+                if k < node.lo:
+                    self.build(node.node, st, lambda x: rep(k + 1, x))
+                elif node.hi is None:
+                    loop = self.nfa.new()
+                    self.nfa.eps[st].append(loop)
+                    self.build(node.node, loop, lambda x: self.nfa.eps[x].append(loop))
+                    to_j(loop)
+                else:
+                    to_j(st)
+                    if k < node.hi:
+                        self.build(node.node, st, lambda x: rep(k + 1, x))
+            rep(0, s)
+            cont(j)
+        elif isinstance(node, Look):
+            mark = self.nfa.new()
+            self.pending.append((s, mark, node))  # before cont: lookaheads after it come later
+            cont(mark)
+        elif isinstance(node, Anchor):
+            raise PatternNotSupported(f"anchor {node.kind} inside the pattern")
+        elif isinstance(node, BackRef):
+            raise PatternNotSupported("back-reference")
+        else:
+            raise TypeError(node)
+
+    def resolve_lookaheads(self):
+        for s, mark, node in reversed(self.pending):
+            d_cont = minimize(determinize(self.nfa, mark, frozenset([self.final]), self.univ))
+            x = _Compiler()
+            xs = x.nfa.new()
+            x.final = x.nfa.new()
+            x.build(node.node, xs, lambda st: x.nfa.eps[st].append(x.univ))
+            x.resolve_lookaheads()
+            d_x = minimize(determinize(x.nfa, xs, frozenset([x.final]), x.univ))
+            op = (lambda p, q: p and not q) if node.negative else (lambda p, q: p and q)
+            d = minimize(product(d_cont, d_x, op))
+            st, fi = dfa_to_nfa(d, self.nfa, self.univ)
+            self.nfa.eps[s].append(st)
+            self.nfa.eps[fi].append(self.final)
+        self.pending = []
+
+
+def _has_look(n) -> bool:
+    if isinstance(n, (Look, Anchor)):
+        return True
+    for attr in ("items", "options"):
+        if hasattr(n, attr):
+            if any(_has_look(x) for x in getattr(n, attr)):
+                return True
+    if isinstance(n, (Repeat, Group)):
+        return _has_look(n.node)
+    return False
+
+
+def _first_last_word(node, last: bool) -> Optional[bool]:
+    """Whether the first (last) code point of every match is a word character (True), never one
+    (False), or either (None)."""
+    if isinstance(node, Chars):
+        inside = all(any(a <= lo and hi <= b for a, b in WORD) for lo, hi in node.ranges)
+        outside = all(all(hi < a or lo > b for a, b in WORD) for lo, hi in node.ranges)
+        return True if inside else (False if outside else None)
+    if isinstance(node, Seq):
+        items = list(reversed(node.items)) if last else list(node.items)
+        for x in items:
+            if isinstance(x, (Look, Anchor)):
+                continue
+            r = _first_last_word(x, last)
+            if nullable(x):
+                return None
+            return r
+        return None
+    if isinstance(node, Alt):
+        rs = {_first_last_word(o, last) for o in node.options}
+        return rs.pop() if len(rs) == 1 else None
+    if isinstance(node, (Group,)):
+        return _first_last_word(node.node, last)
+    if isinstance(node, Repeat):
+        return _first_last_word(node.node, last) if node.lo > 0 else None
+    return None
+
+
+@dataclass
+class CompiledRegex:
+    pattern: str
+    n_states: int
+    n_classes: int           # byte classes + the EOT class (the last one)
+    start: int
+    byte_class: bytes        # 256 entries
+    accept: bytes            # per state: 0 = undecided, 1 = accepted (sticky), 2 = rejected (dead)
+    next: List[int]          # n_states * n_classes, row-major
+
+    def blob(self) -> bytes:
+        """Device layout (expr.hip XI_REGEX): int32 n_states, n_classes, start, 0; byte_class[256];
+        status[n_states] (padded to 4); uint16 next[n_states * n_classes]."""
+        head = struct.pack("<4i", self.n_states, self.n_classes, self.start, 0)
+        acc = self.accept + b"\0" * ((-len(self.accept)) % 4)
+        nx = struct.pack(f"<{len(self.next)}H", *self.next)
+        return head + self.byte_class + acc + nx
+
+    def matches(self, s: str) -> bool:
+        """Host run of the same automaton (tests of the compiler itself)."""
+        st = self.start
+        for b in s.encode("utf-8"):
+            if self.accept[st]:
+                break
+            st = self.next[st * self.n_classes + self.byte_class[b]]
+        if not self.accept[st]:
+            st = self.next[st * self.n_classes + self.n_classes - 1]
+        return self.accept[st] == 1
+
+
+def compile_java_regex(pattern: str) -> CompiledRegex:
+    """Java regex -> DFA over UTF-8 bytes with PatternMatch's find-non-empty semantics."""
+    ast = _Parser(pattern).parse()
+    items = list(ast.items) if isinstance(ast, Seq) else [ast]
+    start_anchor = end_anchor = None
+    if items and isinstance(items[0], Anchor):
+        start_anchor = items.pop(0).kind
+    if items and isinstance(items[-1], Anchor):
+        end_anchor = items.pop().kind
+    body = expand_backrefs(Seq(tuple(items)))
+    if _has_anchor(body):
+        raise PatternNotSupported("anchors or \\b inside the pattern")
+    if nullable(body):
+        raise PatternNotSupported(
+            "a pattern that can match the empty string (PatternMatch counts non-empty first "
+            "matches; Java's choice between an empty and a non-empty match is not modelled)")
+    c = _Compiler()
+    s0 = c.nfa.new()
+    c.final = c.nfa.new()
+    non_word = cs_norm([r for r in cs_neg(WORD) if r[1] < 0x80])  # non-ASCII counts as word
+    # prefix: Sigma*, honouring a leading ^ or \b
+    if start_anchor == "^":
+        p = s0
+    elif start_anchor == "\\b":
+        first = _first_last_word(body, last=False)
+        if first is None:
+            raise PatternNotSupported("\\b before a pattern that may start with either class")
+        if first:  # previous code point is a non-word one, or the match starts the row
+            p = c.nfa.new()
+            c.nfa.eps[s0].append(p)
+            any_ = c.anything(s0)
+            c.chars(non_word, any_, p)
+        else:
+            p = c.nfa.new()
+            any_ = c.anything(s0)
+            c.chars(cs_norm(WORD + ((0x80, MAX_CP),)), any_, p)
+    else:
+        p = c.anything(s0)
+
+    def tail(st):
+        if end_anchor == "$":
+            # Java's $ also matches before a final line terminator
+            c.nfa.trans[st].append((1 << EOT, c.final))
+            m = c.nfa.new()
+            c.chars(LINE_TERMINATORS, st, m)
+            c.nfa.trans[m].append((1 << EOT, c.final))
+        elif end_anchor == "\\b":
+            last = _first_last_word(body, last=True)
+            if last is None:
+                raise PatternNotSupported("\\b after a pattern that may end with either class")
+            c.nfa.trans[st].append((1 << EOT, c.final) if last else (0, c.final))
+            m = c.nfa.new()
+            c.chars(non_word if last else cs_norm(WORD + ((0x80, MAX_CP),)), st, m)
+            c.nfa.eps[m].append(c.univ)
+        else:
+            c.nfa.eps[st].append(c.univ)
+
+    c.build(body, p, tail)
+    c.resolve_lookaheads()
+    d = minimize(determinize(c.nfa, s0, frozenset([c.final]), c.univ))
+    return _finish(pattern, d)
+
+
+def _has_anchor(n) -> bool:
+    if isinstance(n, Anchor):
+        return True
+    for attr in ("items", "options"):
+        if hasattr(n, attr) and any(_has_anchor(x) for x in getattr(n, attr)):
+            return True
+    if isinstance(n, (Repeat, Group, Look)):
+        return _has_anchor(n.node)
+    return False
+
+
+def _finish(pattern: str, d: DFA) -> CompiledRegex:
+    # status: 1 = every continuation accepts (sticky accept), 2 = none does (dead)
+    n = d.n
+    can_accept = [d.accept[s] for s in range(n)]
+    changed = True
+    while changed:  # states that reach an accepting state
+        changed = False
+        for s in range(n):
+            if not can_accept[s] and any(can_accept[t] for t in d.nxt[s]):
+                can_accept[s] = changed = True
+    can_reject = [not d.accept[s] for s in range(n)]
+    changed = True
+    while changed:
+        changed = False
+        for s in range(n):
+            if not can_reject[s] and any(can_reject[t] for t in d.nxt[s]):
+                can_reject[s] = changed = True
+    # acceptance happens only on EOT; a state whose EOT successor accepts and from which no input
+    # can lead to rejection accepts already
+    status = bytearray(n)
+    for s in range(n):
+        if not can_accept[s]:
+            status[s] = 2
+        elif not can_reject[s]:
+            status[s] = 1
+    # byte classes: bytes with identical columns
+    cols: Dict[Tuple[int, ...], int] = {}
+    byte_class = bytearray(256)
+    reps = []
+    for b in range(256):
+        col = tuple(d.nxt[s][b] for s in range(n))
+        if col not in cols:
+            cols[col] = len(cols)
+            reps.append(b)
+        byte_class[b] = cols[col]
+    nc = len(cols) + 1
+    nxt = []
+    for s in range(n):
+        nxt += [d.nxt[s][b] for b in reps] + [d.nxt[s][EOT]]
+    # EOT always leads to an accepting (status 1 after EOT) or a rejecting state: map the EOT
+    # successor's acceptance through its status
+    for s in range(n):
+        t = d.nxt[s][EOT]
+        if d.accept[t]:
+            status[t] = 1
+    if n > 65535:
+        raise PatternNotSupported("automaton too large")
+    return CompiledRegex(pattern, n, nc, d.start, bytes(byte_class), bytes(status), nxt)
+
+
+def nullable_pattern(pattern: str) -> bool:
+    ast = _Parser(pattern).parse()
+    return nullable(ast)
+
+
+def accept_all(pattern: str) -> CompiledRegex:
+    """Every text matches (RLIKE with a pattern that matches the empty string)."""
+    return CompiledRegex(pattern, 1, 2, 0, bytes(256), bytes([1]), [0, 0])
+
+
+__all__ = ["compile_java_regex", "CompiledRegex", "PatternNotSupported", "nullable_pattern",
+           "accept_all"]

@@ -82,7 +82,12 @@ class Node:
     ltype: Optional[str] = None  # literal type: int, float, str, bool, null
 
 
-_KW = {"AND", "OR", "NOT", "IS", "NULL", "IN", "TRUE", "FALSE", "BETWEEN", "CAST", "AS"}
+_KW = {"AND", "OR", "NOT", "IS", "NULL", "IN", "TRUE", "FALSE", "BETWEEN", "CAST", "AS", "RLIKE"}
+
+# The engine's spelling of PatternMatch's counted expression,
+# when(regexp_extract(x, pattern, 0) != "", 1).otherwise(0) (PatternMatch.scala:44-46): TRUE when
+# Java's first find() match exists and is non-empty, FALSE otherwise (a NULL x included).
+FIND_NONEMPTY = "dq_find_nonempty"
 
 
 class _Parser:
@@ -160,6 +165,16 @@ class _Parser:
             self.i += 1
             return Node("isnotnull" if neg else "isnull", [left])
         neg = False
+        if self.kw("NOT") and self.kw("RLIKE", 1):
+            self.i += 1
+            neg = True
+        if self.kw("RLIKE"):  # x RLIKE 'java regex': find() anywhere, NULL on NULL
+            self.i += 1
+            pat = self.primary()
+            if pat.op != "lit" or pat.ltype != "str":
+                raise SqlError("RLIKE needs a string literal pattern")
+            n = Node("regex", [left], name="rlike", value=pat.value)
+            return Node("not", [n]) if neg else n
         if self.kw("NOT") and (self.kw("IN", 1) or self.kw("BETWEEN", 1)):
             self.i += 1
             neg = True
@@ -224,6 +239,15 @@ class _Parser:
                 return Node("cast", [inner], name=ty)
             if u in _KW:
                 raise SqlError(f"unexpected keyword {t.text}")
+            if self.sym("(") and t.text.lower() == FIND_NONEMPTY:
+                self.expect_sym("(")
+                x = self.or_()
+                self.expect_sym(",")
+                pat = self.primary()
+                self.expect_sym(")")
+                if pat.op != "lit" or pat.ltype != "str":
+                    raise SqlError(f"{FIND_NONEMPTY} needs a string literal pattern")
+                return Node("regex", [x], name="nonempty", value=pat.value)
             if self.sym("("):
                 raise SqlError(f"function {t.text}() is not supported by the engine")
             return Node("col", name=t.text)
@@ -361,7 +385,39 @@ class _Emitter:
             for i in items:
                 self.emit(i, target)
             return
+        if n.op == "regex":
+            tx = self.type_of(n.kids[0])
+            if tx == "float":
+                raise SqlError("a regex over a floating-point column needs Java's Double.toString, "
+                               "which the engine does not implement")
+            if tx not in ("str", "int", "bool", "null"):
+                raise SqlError(f"cannot match a regex against a {tx} value")
+            blob = _compiled_regex(n.value, n.name == "rlike")
+            w += [N.X_REGEX, 1 if n.name == "nonempty" else 0, len(blob)]
+            padded = blob + b"\0" * ((-len(blob)) % 8)
+            w += list(struct.unpack(f"<{len(padded) // 8}q", padded))
+            self.emit(n.kids[0])
+            return
         raise SqlError(f"unsupported expression node {n.op}")
+
+
+_REGEX_CACHE = {}
+
+
+def _compiled_regex(pattern: str, any_match: bool) -> bytes:
+    """The automaton blob of a Java regex (deequ_amd/regex.py).  RLIKE (any_match) is find()
+    including an empty match: a pattern that can match the empty string then matches every row."""
+    from .regex import PatternNotSupported, accept_all, compile_java_regex, nullable_pattern
+    key = (pattern, any_match)
+    if key not in _REGEX_CACHE:
+        try:
+            if any_match and nullable_pattern(pattern):
+                _REGEX_CACHE[key] = accept_all(pattern).blob()
+            else:
+                _REGEX_CACHE[key] = compile_java_regex(pattern).blob()
+        except PatternNotSupported as e:
+            raise SqlError(f"regex /{pattern}/: {e}") from e
+    return _REGEX_CACHE[key]
 
 
 def _common_cmp_type(ta: str, tb: str) -> Optional[str]:

@@ -146,7 +146,16 @@ typedef enum dq_xop {
   DQ_X_GE = 17,
   DQ_X_EQ_NULL_SAFE = 18, /* <=> */
   DQ_X_IN = 19,        /* [op, n, x, item_1 .. item_n]      x IN (items)                          */
-  DQ_X_CAST_F64 = 20   /* [op, x]                           CAST(x AS DOUBLE) (string: parse)    */
+  DQ_X_CAST_F64 = 20,  /* [op, x]                           CAST(x AS DOUBLE) (string: parse)    */
+  DQ_X_REGEX = 21      /* [op, null_mode, nbytes, ceil(n/8) words, x]  regex find() over x's text:
+                          the words pack an automaton (deequ_amd/regex.py CompiledRegex.blob):
+                          int32 n_states, n_classes, start, 0; u8 byte_class[256]; u8
+                          status[n_states] (1 accept, 2 reject, padded to 4); u16
+                          next[n_states * n_classes], the last class being end-of-text.  x is
+                          a string (integral / boolean x are formatted as Spark's cast to
+                          string).  A NULL x gives NULL (null_mode 0, RLIKE) or FALSE
+                          (null_mode 1: when(regexp_extract(x, p, 0) != "", 1).otherwise(0),
+                          PatternMatch.scala:44-46).                                           */
 } dq_xop;
 
 typedef struct dq_expr {
@@ -391,6 +400,17 @@ dq_status dq_scan_host(dq_loader* loader, const dq_plan* plan, const dq_column* 
 /* stage + dq_freq_add_device + release. */
 dq_status dq_freq_add_host(dq_loader* loader, dq_freq* freq, const dq_column* host_keys, int n_keys,
                            int null_as_group, void* hip_stream);
+
+/* ------------------------------------------------------------------------------------------------
+ * ApproxQuantile (ApproxQuantile.scala:41-104): the device sorts the non-NULL values of a numeric
+ * column (all batches, cast to double as ApproximatePercentile does; NaNs canonical, so the order
+ * is Java's Double.compare) and returns either every value (when count <= max_values; the host
+ * then replays Spark's QuantileSummaries exactly) or max_values of them at the exact ranks
+ * floor(j * (count - 1) / (max_values - 1)).  out holds max_values doubles (host memory);
+ * *n_out = values written, *count_out = non-NULL values.  Synchronous on hip_stream.
+ * ---------------------------------------------------------------------------------------------- */
+dq_status dq_sorted_sample(int device, const dq_column* batches, int n_batches, int64_t max_values,
+                           double* out, int64_t* n_out, int64_t* count_out, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -654,3 +654,126 @@ def histogram(t: OTable, column: str) -> Tuple[Dict[str, int], int]:
             s = str(int(v))
         out[s] = out.get(s, 0) + 1
     return out, t.n
+
+
+# ------------------------------------------------------------------------------------------------
+# PatternMatch (M/analyzers/PatternMatch.scala:41-53): Java's Pattern.find() restated with
+# Python's backtracking `re` (same leftmost-first semantics), the pattern translated from Java
+# syntax where the two differ.  Test infrastructure only.
+# ------------------------------------------------------------------------------------------------
+def java_regex_to_python(pattern: str) -> str:
+    """Java -> Python `re`: `.` outside a class excludes every Java line terminator (Python's
+    excludes only \\n); everything else used by Patterns is common syntax (re.ASCII gives Java's
+    ASCII \\d \\w \\s)."""
+    out, i, in_class = [], 0, False
+    while i < len(pattern):
+        c = pattern[i]
+        if c == "\\":
+            out.append(pattern[i:i + 2])
+            i += 2
+            continue
+        if in_class:
+            if c == "]" and not (out and out[-1] in ("[", "[^")):
+                in_class = False
+            out.append(c)
+        elif c == "[":
+            in_class = True
+            if pattern.startswith("[^", i):
+                out.append("[^")
+                i += 2
+                continue
+            out.append(c)
+        elif c == ".":
+            out.append("[^\\n\\r\\u0085\\u2028\\u2029]")
+        else:
+            out.append(c)
+        i += 1
+    return "".join(out)
+
+
+def regex_find_nonempty(value, pattern: str) -> bool:
+    """regexp_extract(value, pattern, 0) != "" (a NULL value gives False: otherwise(0))."""
+    import re
+    if value is None:
+        return False
+    m = re.search(java_regex_to_python(pattern), str(value), re.ASCII)
+    return bool(m) and m.group(0) != ""
+
+
+def agg_pattern_match(t: OTable, column: str, pattern: str, where: Optional[str]):
+    """(sum of matches over the where-rows, conditionalCount(where)) -- the PatternMatch state."""
+    vals = _sel(t, column, where)
+    n = agg_conditional_count(t, where)
+    if not n:
+        return None
+    pred = parse_predicate(where) if where else None
+    hits = 0
+    for i, r in enumerate(t.rows()):
+        if pred is not None and eval_predicate(pred, r) is not True:
+            continue
+        v = vals[i]
+        if t.types[column] == "boolean" and v is not None:
+            v = "true" if v else "false"
+        hits += regex_find_nonempty(v, pattern)
+    return hits, n
+
+
+# ------------------------------------------------------------------------------------------------
+# ApproxQuantile (M/analyzers/ApproxQuantile.scala:41-104) -> Spark 2.2 ApproximatePercentile:
+# QuantileSummaries(relativeError) fed one value at a time; below its 50000-value head buffer the
+# summary is one sorted-buffer insert followed by compress, then query.  Restated for tests.
+# ------------------------------------------------------------------------------------------------
+def spark_approx_quantile(values, quantile: float, relative_error: float = 0.01):
+    """The reference's result for at most 50000 non-NULL values (None when there are none)."""
+    import math
+    # Java's Double.compare order: -0.0 before 0.0, NaN after everything
+    xs = sorted((float(v) for v in values if v is not None),
+                key=lambda x: (math.isnan(x), 0.0 if math.isnan(x) else x, math.copysign(1.0, x)))
+    n = len(xs)
+    if n == 0:
+        return None
+    assert n <= 50000, "beyond one head buffer the result depends on Spark's row order"
+    # insert: (value, g, delta); delta = floor(2 eps i) except the first and the last
+    s = [(x, 1, 0 if i in (0, n - 1) else int(math.floor(2 * relative_error * (i + 1))))
+         for i, x in enumerate(xs)]
+    # compress from the right with threshold 2 eps n, keeping the minimum
+    thr = 2 * relative_error * n
+    head = s[-1]
+    kept = []
+    for i in range(n - 2, 0, -1):
+        if s[i][1] + head[1] + head[2] < thr:
+            head = (head[0], head[1] + s[i][1], head[2])
+        else:
+            kept.append(head)
+            head = s[i]
+    kept.append(head)
+    kept.reverse()
+    if n > 1 and s[0][0] <= head[0]:
+        kept.insert(0, s[0])
+    if quantile <= relative_error:
+        return kept[0][0]
+    if quantile >= 1 - relative_error:
+        return kept[-1][0]
+    rank = math.ceil(quantile * n)
+    err = math.ceil(relative_error * n)
+    lo = 0
+    for v, g, d in kept[1:-1]:
+        lo += g
+        if lo + d - err <= rank <= lo + err:
+            return v
+    return kept[-1][0]
+
+
+def quantile_rank_error(values, quantile: float, result: float) -> int:
+    """How many ranks `result` is from the target rank ceil(q n) of the sorted non-NULL values
+    (0 when a copy of `result` sits at the target rank)."""
+    import bisect
+    import math
+    xs = sorted(float(v) for v in values if v is not None)
+    n = len(xs)
+    target = max(1, math.ceil(quantile * n))
+    lo = bisect.bisect_left(xs, result) + 1   # 1-based rank range of `result`
+    hi = bisect.bisect_right(xs, result)
+    if lo <= target <= hi:
+        return 0
+    return min(abs(target - lo), abs(target - hi))

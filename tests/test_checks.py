@@ -63,10 +63,28 @@ def test_where_replaces_last_constraint_and_predicates():
 
 
 def test_unsupported_operator_fails_loudly():
-    check = Check(CheckLevel.Warning, "d").contains_url("description", lambda v: v >= 0.5)
+    check = Check(CheckLevel.Warning, "d").has_data_type("description")
     r = check.evaluate(AnalyzerContext({}))
     assert r.status == CheckStatus.Warning
     assert "not implemented" in r.constraint_results[0].message
+
+
+def test_pattern_and_quantile_checks_require_their_analyzers():
+    """Check.scala:560-642 / 391-398: containsURL & co. are hasPattern with the Patterns regexes
+    and their own names; hasApproxQuantile names ApproxQuantileConstraint(ApproxQuantile(...))."""
+    from deequ_amd.analyzers import ApproxQuantile, PatternMatch, Patterns
+    check = (Check(CheckLevel.Warning, "d").contains_url("description", lambda v: v >= 0.5)
+             .contains_email("e").contains_credit_card_number("c")
+             .contains_social_security_number("s").has_pattern("p", r"\d+")
+             .has_approx_quantile("n", 0.5, lambda v: v <= 10))
+    assert check.required_analyzers() == [
+        PatternMatch("description", Patterns.URL), PatternMatch("e", Patterns.EMAIL),
+        PatternMatch("c", Patterns.CREDITCARD), PatternMatch("s", Patterns.SOCIAL_SECURITY_NUMBER_US),
+        PatternMatch("p", r"\d+"), ApproxQuantile("n", 0.5)]
+    names = [str(c) for c in check.constraints]
+    assert names == ["containsURL(description)", "containsEmail(e)", "containsCreditCardNumber(c)",
+                     "containsSocialSecurityNumber(s)", "PatternMatchConstraint(p, \\d+)",
+                     "ApproxQuantileConstraint(ApproxQuantile(n,0.5,0.01))"]
 
 
 def test_suite_status_is_the_worst_check():
@@ -81,8 +99,9 @@ def test_suite_status_is_the_worst_check():
 
 @pytest.mark.gpu
 def test_basic_example_end_to_end(gpu_device):
-    """M/examples/BasicExample.scala:25-76 on the GPU: isComplete(name) = 0.8 fails, every other
-    integrity constraint passes, so the suite status is Error."""
+    """M/examples/BasicExample.scala:25-76 on the GPU, both checks: isComplete(name) = 0.8 fails
+    (Error), containsURL(description) = 0.4 fails (Warning), the median of numViews is 5.0 and every
+    other constraint passes; the suite status is Error."""
     import pyarrow as pa
 
     from deequ_amd import Table
@@ -98,12 +117,25 @@ def test_basic_example_end_to_end(gpu_device):
     integrity = (Check(CheckLevel.Error, "integrity checks").has_size(lambda n: n == 5)
                  .is_complete("id").is_unique("id").is_complete("name")
                  .is_contained_in("priority", ["high", "low"]).is_non_negative("numViews"))
-    res = VerificationSuite().on_data(df).add_check(integrity).run()
+    distribution = (Check(CheckLevel.Warning, "distribution checks")
+                    .contains_url("description", lambda v: v >= 0.5)
+                    .has_approx_quantile("numViews", 0.5, lambda v: v <= 10))
+    res = VerificationSuite().on_data(df).add_check(integrity).add_check(distribution).run()
     assert res.status == CheckStatus.Error
+    assert res.check_results[integrity].status == CheckStatus.Error
+    assert res.check_results[distribution].status == CheckStatus.Warning
     statuses = [(str(c.constraint), c.status, c.message)
                 for c in res.check_results[integrity].constraint_results]
     failed = [s for s in statuses if s[1] != ConstraintStatus.Success]
     assert failed == [("CompletenessConstraint(Completeness(name,None))",
                        ConstraintStatus.Failure,
                        "Value: 0.8 does not meet the constraint requirement!")]
+    url, median = res.check_results[distribution].constraint_results
+    assert str(url.constraint) == "containsURL(description)"
+    assert url.status == ConstraintStatus.Failure
+    assert url.message == "Value: 0.4 does not meet the constraint requirement!"
+    assert str(median.constraint) == "ApproxQuantileConstraint(ApproxQuantile(numViews,0.5,0.01))"
+    assert median.status == ConstraintStatus.Success
     assert res.metrics[Uniqueness(["id"])].value.get() == 1.0
+    from deequ_amd.analyzers import ApproxQuantile
+    assert res.metrics[ApproxQuantile("numViews", 0.5)].value.get() == 5.0

@@ -1,0 +1,79 @@
+"""The Java-regex -> byte-DFA compiler (deequ_amd/regex.py) against the ORACLE's restatement of
+Pattern.find() (oracle/deequ_oracle.py regex_find_nonempty, Python `re`), and the reference's own
+PatternMatch known answers (AnalyzerTests.scala:595-688).  Host runs of the compiled automaton
+(CompiledRegex.matches, the same table the device walks); no GPU."""
+import random
+
+import pytest
+
+from deequ_amd.analyzers import Patterns
+from deequ_amd.regex import PatternNotSupported, compile_java_regex
+from oracle.deequ_oracle import regex_find_nonempty
+
+KNOWN = [  # AnalyzerTests.scala:595-688
+    (r"\d", ["1", "a"], 1),
+    (Patterns.EMAIL, ["someone@somewhere.org", "someone@else"], 1),
+    (Patterns.CREDITCARD, ["378282246310005", "6011111111111117", "6011 1111 1111 1117",
+                           "6011-1111-1111-1117", "5555555555554444", "5555 5555 5555 4444",
+                           "5555-5555-5555-4444", "4111111111111111", "4111 1111 1111 1111",
+                           "4111-1111-1111-1111", "0000111122223333", "000011112222333",
+                           "00001111222233"], 10),
+    (Patterns.URL, ["http://foo.com/blah_blah", "http://foo.com/blah_blah_(wikipedia)",
+                    "http://foo.bar/?q=Test%20URL-encoded%20stuff", "http://\u27a1.ws/\u4a39",
+                    "http://\u2318.ws/", "http://\u263a.damowmow.com/", "http://\u4f8b\u5b50.\u6d4b\u8bd5",
+                    "https://foo_bar.example.com/", "http://userid@example.com:8080",
+                    "http://foo.com/blah_(wikipedia)#cite-1", "http://../", "h://test",
+                    "http://.www.foo.bar/"], 10),
+    (Patterns.SOCIAL_SECURITY_NUMBER_US, ["111-05-1130", "111051130", "111-05-000", "111-00-000",
+                                          "000-05-1130", "666-05-1130", "900-05-1130",
+                                          "999-05-1130"], 2),
+]
+
+
+@pytest.mark.parametrize("pattern,rows,expected", KNOWN)
+def test_reference_known_answers(pattern, rows, expected):
+    c = compile_java_regex(pattern)
+    assert sum(c.matches(r) for r in rows) == expected
+    assert sum(regex_find_nonempty(r, pattern) for r in rows) == expected  # the oracle too
+
+
+def _random_strings(rng, alphabet, n, max_len):
+    return ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, max_len))) for _ in range(n)]
+
+
+FUZZ = [
+    (Patterns.SOCIAL_SECURITY_NUMBER_US, "0123456789- 9", 14),
+    (Patterns.CREDITCARD, "01345679 -x", 22),
+    (Patterns.URL, "hftps:/.?#$ a\t\u00e9", 14),
+    (Patterns.EMAIL, "ab.@-_[]\"\\1:9", 14),
+    (r"a(?!b)c|x{2,3}y?", "abcxy", 8),
+    (r"(?:ab|a)(?=c)\w", "abcz_", 7),
+    (r"[^\s]+@[\w.]+\.(com|org)$", "a@b.com org\n", 16),
+    (r"^\d{2,4}-[A-F]+", "0123-ABFG", 9),
+    (r"(x|y)\1z", "xyz", 6),
+    (r"\bcat\b", "cat s_", 9),
+    (r"caf\u00e9|na.ve|\u4f8b+", "cafe\u00e9nav\u00efi\u4f8b\r", 8),
+]
+
+
+@pytest.mark.parametrize("pattern,alphabet,max_len", FUZZ)
+def test_automaton_matches_java_find_semantics(pattern, alphabet, max_len):
+    rng = random.Random(hash(pattern) & 0xFFFF)
+    c = compile_java_regex(pattern)
+    for s in _random_strings(rng, alphabet, 3000, max_len):
+        assert c.matches(s) == regex_find_nonempty(s, pattern), (pattern, s)
+
+
+@pytest.mark.parametrize("pattern", [r"a*", r"(?<=a)b", r"(?i)abc", r"a++", r"x\Bz", r"(a|)"])
+def test_unsupported_patterns_are_refused(pattern):
+    with pytest.raises(PatternNotSupported):
+        compile_java_regex(pattern)
+
+
+def test_blob_layout():
+    c = compile_java_regex(r"\d")
+    b = c.blob()
+    import struct
+    ns, nc, start, zero = struct.unpack_from("<4i", b)
+    assert (ns, nc, start, zero) == (c.n_states, c.n_classes, c.start, 0)
+    assert len(b) == 16 + 256 + ((ns + 3) & ~3) + 2 * ns * nc
