@@ -899,6 +899,22 @@ static bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintp
 
 
 
+namespace dq {
+// What a plan reads of each column: 0 nothing, 1 the validity bitmap only (Completeness: a
+// TK_VALIDITY task), 2 every buffer.  The columnar loader stages only that (loader.cpp).
+void plan_column_needs(const dq_plan* plan, std::vector<int>& need) {
+  need.assign(plan->types.size(), 0);
+  for (const TaskPlan& t : plan->tasks) {
+    const int v = t.kind == TK_VALIDITY ? 1 : 2;
+    if (t.col >= 0) need[t.col] = std::max(need[t.col], v);
+    if (t.col2 >= 0) need[t.col2] = std::max(need[t.col2], v);
+  }
+  for (const MatExpr& m : plan->mat)
+    for (const XInstr& ins : m.prog)
+      if (ins.op == XI_COL) need[ins.a] = 2;
+}
+}  // namespace dq
+
 // Validates one batch against the plan and returns its row count (-1 on error).
 static int64_t batch_rows(const dq_plan* plan, const dq_column* cols, const std::vector<int>& ref,
                           dq_status& st) {

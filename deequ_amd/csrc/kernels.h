@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <utility>
+#include <vector>
 
 #include "engine.h"
 
@@ -144,5 +145,7 @@ hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const Sca
                        uint32_t* hll_stage, Acc* acc, uint8_t* hll_acc, hipStream_t stream);
 size_t scan_lds_bytes(int body, int n_hll);
 int scan_max_blocks_per_cu(int body, int n_hll);
+// Per column of a plan: 0 not read, 1 validity bitmap only, 2 every buffer (api.cpp).
+void plan_column_needs(const dq_plan* plan, std::vector<int>& need);
 
 }  // namespace dq

@@ -116,8 +116,10 @@ extern "C" void dq_loader_destroy(dq_loader* l) {
   delete l;
 }
 
-extern "C" dq_status dq_loader_stage(dq_loader* l, const dq_column* host_cols, int n_cols,
-                                     dq_column* dev_cols, void* hip_stream) {
+// need (optional, per column): 0 stage nothing, 1 the validity bitmap only, 2 every buffer; an
+// unstaged values / data buffer is given a non-null device address that nothing reads.
+static dq_status stage(dq_loader* l, const dq_column* host_cols, int n_cols, dq_column* dev_cols,
+                       void* hip_stream, const int* need) {
   if (!l || (n_cols > 0 && (!host_cols || !dev_cols)) || n_cols < 0)
     return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   if (l->staged >= 0) return fail(DQ_ERR_STATE, "previous staged batch was not released");
@@ -130,8 +132,11 @@ extern "C" dq_status dq_loader_stage(dq_loader* l, const dq_column* host_cols, i
     const dq_column& h = host_cols[c];
     if (h.length < 0) return fail(DQ_ERR_INVALID_ARGUMENT, "column %d: negative length", c);
     const size_t n = (size_t)h.length;
-    nv[c] = h.validity ? (n + 7) / 8 : 0;
-    if (h.type == DQ_UTF8) {
+    const int nd = need ? need[c] : 2;
+    nv[c] = h.validity && nd >= 1 ? (n + 7) / 8 : 0;
+    if (nd < 2) {  // unread values / data are never touched (not even the offsets)
+      nval[c] = ndat[c] = 0;
+    } else if (h.type == DQ_UTF8) {
       nval[c] = h.values ? 4 * (n + 1) : 0;
       const int32_t* off = static_cast<const int32_t*>(h.values);
       const int32_t end = off ? off[n] : 0;
@@ -148,6 +153,7 @@ extern "C" dq_status dq_loader_stage(dq_loader* l, const dq_column* host_cols, i
     }
     total += round_up(nv[c]) + round_up(nval[c]) + round_up(ndat[c]);
   }
+  total = std::max<size_t>(total, 256);  // the stand-in address of unstaged buffers
   const int k = l->next;
   l->next ^= 1;
   Slot& s = l->slot[k];
@@ -184,11 +190,17 @@ extern "C" dq_status dq_loader_stage(dq_loader* l, const dq_column* host_cols, i
     HIP_TRY(put(h.validity, nv[c], &vp));
     HIP_TRY(put(h.values, nval[c], &valp));
     HIP_TRY(put(h.data, ndat[c], &dp));
-    d.validity = static_cast<const uint8_t*>(h.validity ? vp : nullptr);
-    d.values = h.values ? valp : nullptr;
-    d.data = static_cast<const uint8_t*>(h.data ? dp : nullptr);
-    if (h.type == DQ_UTF8 && h.data && ndat[c] == 0) d.data = s.buf.p;  // empty strings only
-    if (h.values && nval[c] == 0) d.values = s.buf.p;                   // zero-row column
+    const int nd = need ? need[c] : 2;
+    d.validity = static_cast<const uint8_t*>(h.validity && nd >= 1 ? vp : nullptr);
+    if (nd == 2) {
+      d.values = h.values ? valp : nullptr;
+      d.data = static_cast<const uint8_t*>(h.data ? dp : nullptr);
+    } else {  // a stand-in address: the plan reads neither
+      d.values = s.buf.p;
+      d.data = h.type == DQ_UTF8 ? s.buf.p : nullptr;
+    }
+    if (nd == 2 && h.type == DQ_UTF8 && h.data && ndat[c] == 0) d.data = s.buf.p;  // empty strings
+    if (nd == 2 && h.values && nval[c] == 0) d.values = s.buf.p;                   // zero-row column
     dev_cols[c] = d;
   }
   HIP_TRY(hipEventRecord(s.copied, l->copy));
@@ -196,6 +208,11 @@ extern "C" dq_status dq_loader_stage(dq_loader* l, const dq_column* host_cols, i
   HIP_TRY(hipStreamWaitEvent(stream, s.copied, 0));
   l->staged = k;
   return DQ_OK;
+}
+
+extern "C" dq_status dq_loader_stage(dq_loader* l, const dq_column* host_cols, int n_cols,
+                                     dq_column* dev_cols, void* hip_stream) {
+  return stage(l, host_cols, n_cols, dev_cols, hip_stream, nullptr);
 }
 
 extern "C" dq_status dq_loader_release(dq_loader* l, void* hip_stream) {
@@ -212,7 +229,11 @@ extern "C" dq_status dq_loader_release(dq_loader* l, void* hip_stream) {
 extern "C" dq_status dq_scan_host(dq_loader* l, const dq_plan* plan, const dq_column* host_cols,
                                   int n_cols, dq_state* state, void* hip_stream) {
   std::vector<dq_column> dev(std::max(0, n_cols));
-  dq_status st = dq_loader_stage(l, host_cols, n_cols, dev.data(), hip_stream);
+  if (!plan) return fail(DQ_ERR_INVALID_ARGUMENT, "null plan");
+  std::vector<int> need;  // only what the plan reads crosses the host link
+  plan_column_needs(plan, need);
+  if ((int)need.size() != n_cols) return fail(DQ_ERR_INVALID_ARGUMENT, "plan has %d columns", (int)need.size());
+  dq_status st = stage(l, host_cols, n_cols, dev.data(), hip_stream, need.data());
   if (st != DQ_OK) return st;
   st = dq_scan_device(plan, dev.data(), n_cols, state, hip_stream);
   dq_status rs = dq_loader_release(l, hip_stream);

@@ -814,8 +814,10 @@ DQ_DEV bool queue_next(uint32_t* heads, uint32_t lo, uint32_t hi, int home, int&
 // body needs, not the maximum over all bodies.  A suite is one launch per class it uses (S10: the
 // validity, numeric-int64 and string-IN classes) plus the two finalize launches; items of all
 // batches of a class run in the same launch.
+// The fused HLL + co-moment body (BC_CORR_HLL) is bound by its 64-bit multiplies as much as by
+// HBM: it is held to 128 VGPRs so four waves per SIMD hide the loads behind the hashing.
 template <int BC>
-__global__ void __launch_bounds__(kBlock) scan_kernel(const TaskDesc* __restrict__ tasks, int n_desc,
+__global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? 4 : 1)) scan_kernel(const TaskDesc* __restrict__ tasks, int n_desc,
                                                       uint32_t item_lo, uint32_t item_hi,
                                                       uint32_t* __restrict__ queue,
                                                       Acc* __restrict__ partial,

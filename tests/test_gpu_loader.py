@@ -29,13 +29,15 @@ def _table(n, seed):
         "b": pa.array(rng.normal(5.0, 2.0, n), mask=mask(), type=pa.float64()),
         "s": pa.array([None if m else v for v, m in
                        zip(words[rng.integers(0, len(words), n)], mask())], type=pa.string()),
+        # read by Completeness only: the loader stages its validity bitmap alone
+        "c": pa.array([None if m else f"v{k}" for k, m in enumerate(mask())], type=pa.string()),
     })
 
 
 def _otable(t):
     from oracle.deequ_oracle import OTable
     return OTable({k: t.column(k).to_pylist() for k in t.column_names},
-                  {"a": "long", "b": "double", "s": "string"})
+                  {"a": "long", "b": "double", "s": "string", "c": "string"})
 
 
 def _clobbered(batch):
@@ -55,8 +57,8 @@ def _clobber(batch):
 
 @pytest.mark.parametrize("n,batch", [(30_000, 7_000), (100_003, 16_384)])
 def test_scan_host_matches_oracle_and_outlives_host_buffers(n, batch, gpu_device):
-    from deequ_amd.analyzers import (ApproxCountDistinct, Compliance, Maximum, Mean, Size,
-                                     StandardDeviation, Sum)
+    from deequ_amd.analyzers import (ApproxCountDistinct, Completeness, Compliance, Maximum, Mean,
+                                     Size, StandardDeviation, Sum)
     from deequ_amd.loader import HostLoader, HostTable
     from deequ_amd.runners.engine import get_plan, read_row
     from deequ_amd import _native as N
@@ -65,7 +67,7 @@ def test_scan_host_matches_oracle_and_outlives_host_buffers(n, batch, gpu_device
     ht = HostTable.from_arrow(t, max_batch_rows=batch)
     assert len(ht.batches) > 2
     suite = [Size(), Sum("a"), Mean("b"), Maximum("b"), StandardDeviation("a"),
-             Compliance("in", "s IN ('high','low')"), ApproxCountDistinct("s")]
+             Compliance("in", "s IN ('high','low')"), ApproxCountDistinct("s"), Completeness("c")]
     specs = [s for a in suite for s in a.aggregation_functions()]
     plan = get_plan(ht.schema, specs)
     state = plan.state(0)
@@ -90,6 +92,7 @@ def test_scan_host_matches_oracle_and_outlives_host_buffers(n, batch, gpu_device
     assert got[suite[5]].num_matches == O.agg_compliance(ot, "s IN ('high','low')", None)
     assert list(got[suite[6]].words) == O.agg_hll(ot, "s", None)
     assert _close(got[suite[3]].max_value, O.agg_max(ot, "b", None))
+    assert got[suite[7]].num_matches == O.agg_sum_notnull(ot, "c", None)
 
 
 @pytest.mark.parametrize("cols,null_as_group", [(("a",), False), (("s",), False), (("a", "s"), False),
