@@ -27,7 +27,7 @@ INTEGRAL_TYPES = {INT8, INT16, INT32, INT64}
 
 # dq_agg_kind
 (AGG_COUNT_ALL, AGG_COUNT_NOTNULL, AGG_COUNT_TRUE, AGG_SUM, AGG_MIN, AGG_MAX, AGG_STDDEV_POP,
- AGG_CORR, AGG_HLL) = range(1, 10)
+ AGG_CORR, AGG_HLL, AGG_DTYPE) = range(1, 11)
 
 # dq_status
 DQ_OK = 0
@@ -111,6 +111,9 @@ def _load() -> ctypes.CDLL:
         "dq_freq_add_device": (c_int, [c_void_p, POINTER(dq_column), c_int, c_int, c_void_p]),
         "dq_freq_summarize": (c_int, [c_void_p, POINTER(dq_freq_summary)]),
         "dq_freq_summarize_keys": (c_int, [c_void_p, POINTER(dq_freq_summary)]),
+        "dq_freq_marginal": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
+        "dq_freq_mutual_information": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int),
+                                               c_void_p]),
         "dq_sorted_sample": (c_int, [c_int, POINTER(dq_column), c_int, c_int64, c_void_p,
                                      POINTER(c_int64), POINTER(c_int64), c_void_p]),
         "dq_freq_num_groups": (c_int, [c_void_p, POINTER(c_int64)]),
@@ -152,7 +155,7 @@ EXPORTED = [
     "dq_state_destroy", "dq_state_reset", "dq_scan_device", "dq_scan_device_batches",
     "dq_state_sync", "dq_state_get", "dq_state_merge", "dq_state_serialized_size",
     "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_freq_create",
-    "dq_freq_destroy", "dq_freq_reset", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_summarize_keys", "dq_sorted_sample", "dq_freq_num_groups",
+    "dq_freq_destroy", "dq_freq_reset", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_summarize_keys", "dq_sorted_sample", "dq_freq_marginal", "dq_freq_mutual_information", "dq_freq_num_groups",
     "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge", "dq_freq_topk", "dq_loader_create",
     "dq_loader_destroy", "dq_loader_stage", "dq_loader_release", "dq_scan_host",
     "dq_freq_add_host", "dq_freq_partition_sizes", "dq_freq_partition",

@@ -4,11 +4,13 @@ from .base import (AggSpec, Analyzer, DoubleValuedState, GroupingAnalyzer, NumMa
                    merge_states)
 from .grouping import (CountDistinct, Distinctness, Entropy, FrequenciesAndNumRows,
                        FrequencyBasedAnalyzer, FrequencyTable, Histogram, HistogramState,
+                       MutualInformation,
                        ScanShareableFrequencyBasedAnalyzer, UniqueValueRatio, Uniqueness,
                        compute_frequencies)
 from .scan import (ApproxCountDistinct, ApproxCountDistinctState, Completeness, Compliance,
                    Correlation, CorrelationState, MaxState, Maximum, Mean, MeanState, MinState,
                    Minimum, NumMatches, PatternMatch, Patterns, Size, StandardDeviation,
                    StandardDeviationState, Sum, SumState)
+from .datatype import DataType, DataTypeHistogram, DataTypeInstances, determine_type
 from .quantile import ApproxQuantile, ApproxQuantileState, QuantileSummaries
 from .state_provider import InMemoryStateProvider, StateLoader, StatePersister

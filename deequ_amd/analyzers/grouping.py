@@ -126,6 +126,16 @@ class FrequencyTable:
                 key.append(_decode_fixed(t, v))
         return tuple(key)
 
+    def marginal(self, key_index: int, stream=None) -> "FrequencyTable":
+        """The one-key table of key column `key_index`'s marginal counts over this multi-key
+        table's groups (dq_freq_marginal); numRows is this table's."""
+        out = FrequencyTable([self.key_columns[key_index]], [self.key_types[key_index]], self.device)
+        if stream is None:
+            import torch
+            stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        N.check(N.lib.dq_freq_marginal(self.handle, key_index, out.handle, stream))
+        return out
+
     def merged(self, other: "FrequencyTable") -> "FrequencyTable":
         out = FrequencyTable(self.key_columns, self.key_types, self.device)
         N.check(N.lib.dq_freq_merge(out.handle, self.handle))
@@ -370,6 +380,65 @@ class Entropy(ScanShareableFrequencyBasedAnalyzer):
         return [FreqAgg("entropy")]
 
 
+@dataclass(frozen=True)
+class MutualInformation(FrequencyBasedAnalyzer):
+    """MutualInformation.scala:35-97: sum over the joint groups of
+    (pxy/n) ln((pxy/n) / ((px/n)(py/n))), the marginals re-aggregated from the joint table
+    (dq_freq_mutual_information: marginals and the join on the device, the reference's per-group
+    arithmetic, a fixed-order sum)."""
+    columns: Tuple[str, ...]
+    _name = "MutualInformation"
+
+    def __init__(self, columns, column_b: Optional[str] = None):
+        cols = (columns, column_b) if column_b is not None else _cols(columns)
+        object.__setattr__(self, "columns", tuple(cols))
+
+    def _columns(self):
+        return list(self.columns)
+
+    def preconditions(self):
+        return [Preconditions.exactly_n_columns(list(self.columns), 2)] + super().preconditions()
+
+    def _instance(self):
+        return ",".join(self.columns)
+
+    def compute_metric_from(self, state):
+        if state is None:
+            return metric_from_empty(self, self._name, self._instance(), entity_from(self.columns))
+        joint = state.frequencies
+        if isinstance(joint, FrequencyTable):  # the reference's per-group terms, on the device
+            mi, null = ctypes.c_double(), ctypes.c_int()
+            import torch
+            stream = ctypes.c_void_p(torch.cuda.current_stream(joint.device).cuda_stream)
+            N.check(N.lib.dq_freq_mutual_information(joint.handle, ctypes.byref(mi),
+                                                     ctypes.byref(null), stream))
+            if null.value:  # sum over no joint groups is NULL
+                return metric_from_empty(self, self._name, self._instance(),
+                                         entity_from(self.columns))
+            return metric_from_value(mi.value, self._name, self._instance(),
+                                     entity_from(self.columns))
+        # a repartitioned (multi-GPU) joint table: H(X) + H(Y) - H(X,Y), the same sum regrouped,
+        # from the three distributed entropies (a value's groups may sit on several ranks)
+        s = joint.summarize()
+        if s.n_groups == 0:
+            return metric_from_empty(self, self._name, self._instance(), entity_from(self.columns))
+        hx = _marginal_entropy(joint, 0)
+        hy = _marginal_entropy(joint, 1)
+        return metric_from_value(hx + hy - s.entropy, self._name, self._instance(),
+                                 entity_from(self.columns))
+
+    def to_failure_metric(self, exception):
+        return metric_from_failure(exception, self._name, self._instance(),
+                                   entity_from(self.columns))
+
+
+def _marginal_entropy(joint, k: int) -> float:
+    from ..distributed import DistributedFrequencies, freq_repartition
+    if isinstance(joint, DistributedFrequencies):  # a value's groups may sit on several ranks
+        return DistributedFrequencies(freq_repartition(joint.owned.marginal(k))).summarize().entropy
+    return joint.marginal(k).summarize().entropy
+
+
 # ------------------------------------------------------------------------------------------------
 # Histogram (Histogram.scala:41-116)
 # ------------------------------------------------------------------------------------------------
@@ -540,7 +609,7 @@ class Histogram(Analyzer):
         return HistogramMetric(self.column, Failure(wrap_if_necessary(exception)))
 
 
-__all__ = ["FrequencyTable", "KeyedFrequencies", "FrequenciesAndNumRows", "compute_frequencies",
+__all__ = ["FrequencyTable", "KeyedFrequencies", "FrequenciesAndNumRows", "MutualInformation", "compute_frequencies",
            "FrequencyBasedAnalyzer", "ScanShareableFrequencyBasedAnalyzer", "Uniqueness",
            "Distinctness", "UniqueValueRatio", "CountDistinct", "Entropy", "Histogram",
            "HistogramState", "java_double_to_string", "java_float_to_string", "cast_to_string"]

@@ -15,10 +15,21 @@ from dataclasses import dataclass, field
 from enum import Enum
 from typing import Any, Callable, List, Optional, Sequence
 
-from .analyzers import (ApproxCountDistinct, ApproxQuantile, Completeness, Compliance, Correlation, Distinctness,
+from .analyzers import (ApproxCountDistinct, ApproxQuantile, Completeness, DataType,
+                        MutualInformation, Compliance, Correlation, Distinctness,
                         Entropy, Histogram, Maximum, Mean, Minimum, PatternMatch, Patterns, Size,
                         StandardDeviation, Sum, UniqueValueRatio, Uniqueness)
 from .analyzers.grouping import java_double_to_string
+
+
+class ConstrainableDataTypes(Enum):
+    """Constraint.scala ConstrainableDataTypes"""
+    Null = 0
+    Fractional = 1
+    Integral = 2
+    Boolean = 3
+    String = 4
+    Numeric = 5
 
 
 class CheckLevel(Enum):
@@ -78,6 +89,13 @@ class AnalysisBasedConstraint(Constraint):
         self.value_picker = value_picker
         self.hint = hint
 
+    def __str__(self):  # the Scala case class's toString
+        picker = "Some(<function1>)" if self.value_picker else "None"
+        hint = f"Some({self.hint})" if self.hint is not None else "None"
+        return f"AnalysisBasedConstraint({self.analyzer},<function1>,{picker},{hint})"
+
+    __repr__ = __str__
+
     def evaluate(self, metric_map) -> ConstraintResult:
         metric = metric_map.get(self.analyzer)
         if metric is None:
@@ -114,25 +132,6 @@ class NamedConstraint(Constraint):
     def evaluate(self, metric_map) -> ConstraintResult:
         r = self.inner.evaluate(metric_map)
         return ConstraintResult(self, r.status, r.message, r.metric)
-
-    def __str__(self):
-        return self.name
-
-    __repr__ = __str__
-
-
-class UnsupportedConstraint(Constraint):
-    """A constraint over an analyzer this engine does not implement yet.  It never silently
-    passes and never falls back to a CPU path: it evaluates to a Failure naming the operator."""
-
-    def __init__(self, name: str, operator: str):
-        self.name = name
-        self.operator = operator
-
-    def evaluate(self, metric_map) -> ConstraintResult:
-        return ConstraintResult(self, ConstraintStatus.Failure,
-                                f"{self.operator} is not implemented by deequ_amd yet "
-                                f"(config-5 operator, SURVEY.md §8(f))")
 
     def __str__(self):
         return self.name
@@ -329,7 +328,6 @@ class Check:
         return self.has_pattern(column, Patterns.SOCIAL_SECURITY_NUMBER_US, assertion,
                                 f"containsSocialSecurityNumber({column})", hint)
 
-    # -- operators not built yet: loud failures ------------------------------------------------
     def has_approx_quantile(self, column: str, quantile: float, assertion,
                             hint=None) -> "Check":
         """Check.scala:391-398 -> approxQuantileConstraint (Constraint.scala:368-381)."""
@@ -337,14 +335,28 @@ class Check:
         return self.add_constraint(NamedConstraint(AnalysisBasedConstraint(a, assertion, hint=hint),
                                                    f"ApproxQuantileConstraint({a})"))
 
-    def has_data_type(self, column: str, data_type=None, assertion=None, hint=None) -> "Check":
-        return self.add_constraint(UnsupportedConstraint(f"DataTypeConstraint({column})",
-                                                         "DataType"))
+    def has_data_type(self, column: str, data_type: "ConstrainableDataTypes", assertion=None,
+                      hint=None) -> "Check":
+        """Check.scala:653-661 -> dataTypeConstraint (Constraint.scala:549-579): the ratio of
+        `data_type` in DataType(column)'s distribution (0.0 when absent); Numeric = Fractional +
+        Integral.  The reference leaves this constraint unnamed."""
+        assertion = assertion or IS_ONE
 
-    def has_mutual_information(self, column_a: str, column_b: str, assertion=None,
+        def pick(dist):
+            def ratio(k):
+                v = dist.values.get(k)
+                return v.ratio if v is not None else 0.0
+            if data_type == ConstrainableDataTypes.Numeric:
+                return ratio("Fractional") + ratio("Integral")
+            return ratio({ConstrainableDataTypes.Null: "Unknown"}.get(data_type, data_type.name))
+        return self.add_constraint(AnalysisBasedConstraint(DataType(column), assertion, pick, hint))
+
+    def has_mutual_information(self, column_a: str, column_b: str, assertion,
                                hint=None) -> "Check":
-        return self.add_constraint(UnsupportedConstraint(
-            f"MutualInformationConstraint({column_a},{column_b})", "MutualInformation"))
+        """Check.scala:371-379 -> mutualInformationConstraint (Constraint.scala:344-357)."""
+        mi = MutualInformation([column_a, column_b])
+        return self.add_constraint(NamedConstraint(AnalysisBasedConstraint(mi, assertion, hint=hint),
+                                                   f"MutualInformationConstraint({mi})"))
 
     # -- evaluation --------------------------------------------------------------------------
     def evaluate(self, context) -> CheckResult:

@@ -406,6 +406,7 @@ static int body_class(const dq_plan* p, const TaskPlan& t) {
     case TK_VALIDITY:
     case TK_BOOLMAP: return BC_BITS;
     case TK_STR_IN: return BC_STR_IN;
+    case TK_DTYPE: return BC_DTYPE;
     case TK_COMOMENTS: return t.fused_hll >= 0 ? BC_CORR_HLL : BC_CORR;
     default: return BC_HLL;
   }
@@ -578,6 +579,13 @@ extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
         s.task = find_or_add_task(p.get(), TK_HLL, a.col, -1, w);
         break;
       }
+      case DQ_AGG_DTYPE: {
+        if ((st = check_col(a.col)) != DQ_OK) return st;
+        if ((st = where_of(a, w)) != DQ_OK) return st;
+        s.src = SRC_TASK;
+        s.task = find_or_add_task(p.get(), TK_DTYPE, a.col, -1, w);
+        break;
+      }
       default: return fail(DQ_ERR_INVALID_ARGUMENT, "unknown aggregation kind %d", a.kind);
     }
     p->slots.push_back(s);
@@ -647,6 +655,7 @@ static const char* kind_name(int k) {
     case TK_BOOLMAP: return "boolmap";
     case TK_COMOMENTS: return "comoments";
     case TK_HLL: return "hll";
+    case TK_DTYPE: return "dtype";
     default: return "?";
   }
 }
@@ -1325,6 +1334,9 @@ extern "C" dq_status dq_state_get(const dq_state* s, int agg_index, dq_value* ou
       break;
     case DQ_AGG_HLL:
       pack_hll(&s->hll[(size_t)tp.hll_out * kHllM], out->words);
+      break;
+    case DQ_AGG_DTYPE:  // the UDAF's buffer is never NULL (StatefulDataType.initialize)
+      for (int q = 0; q < 5; ++q) out->words[q] = (uint64_t)a.i[q];
       break;
     default: break;
   }

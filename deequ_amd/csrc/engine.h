@@ -23,7 +23,8 @@ enum TaskKind : int32_t {
   TK_STR_IN = 3,     // [col IS NULL OR] col [NOT] IN ('a','b',...) on a utf8 column
   TK_BOOLMAP = 4,    // counts over a materialised predicate bitmap (generic predicates / where)
   TK_COMOMENTS = 5,  // two numeric columns: (n, xAvg, yAvg, ck, xMk, yMk)
-  TK_HLL = 6         // HLL++ registers (P = 9, 512 registers) of one column
+  TK_HLL = 6,        // HLL++ registers (P = 9, 512 registers) of one column
+  TK_DTYPE = 7       // DataType: counts of NULL / Fractional / Integral / Boolean / String values
 };
 
 constexpr int kMaxPreds = 3;          // fused predicates per TK_NUMERIC task
@@ -101,6 +102,7 @@ struct TaskDesc {
 //   TK_VALIDITY : i0 count
 //   TK_STR_IN / TK_BOOLMAP : i0 TRUE count, i1 non-NULL count
 //   TK_COMOMENTS: i0 n; d0 xAvg, d1 yAvg, d2 ck, d3 xMk, d4 yMk
+//   TK_DTYPE    : i0 NULL, i1 Fractional, i2 Integral, i3 Boolean, i4 String
 struct alignas(16) Acc {
   int64_t i[10];
   double d[6];
@@ -188,6 +190,9 @@ DQ_HD void acc_merge(int kind, Acc& a, const Acc& b) {
       a.i[0] += b.i[0];
       break;
     }
+    case TK_DTYPE:
+      for (int k = 0; k < 5; ++k) a.i[k] += b.i[k];
+      break;
     default:
       a.i[0] += b.i[0];
       a.i[1] += b.i[1];

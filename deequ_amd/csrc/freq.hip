@@ -1866,6 +1866,108 @@ static dq_status compact_groups(dq_freq* f) {
   return DQ_OK;
 }
 
+// The marginal of key column k over a hashed table's groups, as records for a one-key table:
+// column k's part of a group's encoded key IS the one-column encoding of that value, so a
+// record points into the same arena (enc_off), and carries the group's count.  Exact output
+// (fixed-width column): key = the value.  Hashed output (utf8): key = the one-column row hash.
+__global__ void freq_project(const Group* __restrict__ g, int64_t n, const uint8_t* __restrict__ arena,
+                             PartTypes t, int k, RecIn* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* enc = reinterpret_cast<const uint32_t*>(arena + g[i].rep);
+  uint32_t w = 0;
+  for (int c = 0; c < k; ++c) {  // skip the columns before k
+    const uint32_t tag = enc[w++];
+    if (!tag) continue;
+    if (t.types[c] == DQ_UTF8) w += 1 + pad4(enc[w]) / 4;
+    else w += 2;
+  }
+  RecIn r;
+  r.count = g[i].count;
+  r.enc_off = g[i].rep + 4ull * w;
+  if (t.types[k] == DQ_UTF8) {
+    const uint32_t len = enc[w + 1];
+    r.key = str_row_hash(SView{reinterpret_cast<const uint8_t*>(enc + w + 2), (int32_t)len});
+  } else {
+    r.key = (uint64_t)enc[w + 1] | ((uint64_t)enc[w + 2] << 32);
+  }
+  out[i] = r;
+}
+
+// ---- MutualInformation (MutualInformation.scala:41-84) -----------------------------------------
+// Column k's part of an encoded multi-key group key.
+DQ_DEV const uint32_t* enc_part(const uint32_t* enc, const PartTypes& t, int k) {
+  uint32_t w = 0;
+  for (int c = 0; c < k; ++c) {
+    const uint32_t tag = enc[w++];
+    if (!tag) continue;
+    if (t.types[c] == DQ_UTF8) w += 1 + pad4(enc[w]) / 4;
+    else w += 2;
+  }
+  return enc + w;
+}
+
+// Open-addressing index over a one-key table's groups: slot -> group index + 1 (0 = empty).
+struct Lookup {
+  const Group* g;
+  const uint32_t* slots;
+  uint64_t mask;
+  const uint8_t* arena;
+  int32_t type;
+  int32_t exact;
+};
+
+__global__ void freq_lookup_build(const Group* __restrict__ g, int64_t n, uint64_t mask,
+                                  uint32_t* __restrict__ slots) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t s = g[i].h & mask;
+  while (atomicCAS(&slots[s], 0u, (uint32_t)(i + 1)) != 0u) s = (s + 1) & mask;
+}
+
+// The count of the marginal group whose key is the one-column encoding `part`.
+DQ_DEV uint64_t lookup_count(const Lookup& L, const uint32_t* part) {
+  uint64_t h;
+  if (L.exact) {
+    h = fmix_bij((uint64_t)part[1] | ((uint64_t)part[2] << 32));
+  } else {
+    h = str_row_hash(SView{reinterpret_cast<const uint8_t*>(part + 2), (int32_t)part[1]});
+  }
+  for (uint64_t s = h & L.mask;; s = (s + 1) & L.mask) {
+    const uint32_t idx = L.slots[s];
+    if (!idx) return 0;  // not reachable: every joint value has its marginal group
+    const Group& m = L.g[idx - 1];
+    if (m.h != h) continue;
+    if (L.exact) return m.count;
+    const int32_t ty = DQ_UTF8;
+    if (enc_equal(reinterpret_cast<const uint32_t*>(L.arena + m.rep), part, &ty, 1)) return m.count;
+  }
+}
+
+// terms[i] = (pxy/n) ln((pxy/n) / ((px/n)(py/n))), the reference's UDF (MutualInformation.scala:
+// 61-64) with its operation order, per joint group
+__global__ void freq_mi_terms(const Group* __restrict__ gj, int64_t n, const uint8_t* __restrict__ arena,
+                              PartTypes t, Lookup X, Lookup Y, double total, double* __restrict__ terms) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* enc = reinterpret_cast<const uint32_t*>(arena + gj[i].rep);
+  const double px = (double)lookup_count(X, enc_part(enc, t, 0));
+  const double py = (double)lookup_count(Y, enc_part(enc, t, 1));
+  const double pxy = (double)gj[i].count;
+  terms[i] = (pxy / total) * log((pxy / total) / ((px / total) * (py / total)));
+}
+
+// Fixed-order sum: block b adds its strided share in index order, then a fixed tree.
+__global__ void __launch_bounds__(256) freq_sum_f64(const double* __restrict__ x, int64_t n,
+                                                    double* __restrict__ partial) {
+  __shared__ double s_red[256 / 64];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    acc += x[i];
+  acc = block_sum_f64(acc, s_red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = acc;
+}
+
 static PartTypes part_types(const dq_freq* f, int parts) {
   PartTypes t;
   memset(&t, 0, sizeof(t));
@@ -2183,6 +2285,97 @@ extern "C" dq_status dq_freq_summarize_keys(dq_freq* f, dq_freq_summary* out) {
   out->n_null_key_rows = (int64_t)(f->h_counters[C_NULL_ROWS] + f->h_counters[C_NULL_GROUP]);
   out->entropy = f->st_entropy;
   return DQ_OK;
+}
+
+extern "C" dq_status dq_freq_marginal(dq_freq* joint, int key_index, dq_freq* out,
+                                     void* hip_stream) {
+  if (!joint || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (joint->exact || joint->n_keys < 2) return fail(DQ_ERR_INVALID_ARGUMENT, "not a multi-key table");
+  if (key_index < 0 || key_index >= joint->n_keys) return fail(DQ_ERR_INVALID_ARGUMENT, "bad key index");
+  if (out->n_keys != 1 || out->types[0] != joint->types[key_index])
+    return fail(DQ_ERR_WRONG_TYPE, "the marginal table must have one key of the column's type");
+  if (joint->mode_null_as_group > 0) return fail(DQ_ERR_UNSUPPORTED, "marginal of a Histogram table");
+  HIP_TRY(hipSetDevice(joint->device));
+  dq_status st = compact_groups(joint);
+  if (st != DQ_OK) return st;
+  const int64_t n = joint->n_compact;
+  DevBuf<RecIn> rec;
+  HIP_TRY(rec.ensure(std::max<int64_t>(n, 1)));
+  if (n) {
+    hipLaunchKernelGGL(freq_project, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, joint->stream,
+                       joint->compact.p, n, joint->arena.p, part_types(joint, 1), key_index, rec.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(joint->stream));
+  }
+  const int64_t rc[1] = {n};
+  const int64_t vb[1] = {(int64_t)((joint->arena_used + 7) & ~7ULL)};
+  const int64_t special[3] = {0, 0, (int64_t)joint->h_counters[C_NULL_ROWS]};
+  st = dq_freq_add_records_device(out, reinterpret_cast<const dq_freq_record*>(rec.p),
+                                  joint->arena.p, 1, rc, vb, joint->num_rows, special, 0, hip_stream);
+  if (st != DQ_OK) return st;
+  HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(hip_stream)));
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int* is_null,
+                                               void* hip_stream) {
+  if (!joint || !mi || !is_null) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (joint->exact || joint->n_keys != 2)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "MutualInformation needs a two-key grouping table");
+  HIP_TRY(hipSetDevice(joint->device));
+  dq_status st = compact_groups(joint);
+  if (st != DQ_OK) return st;
+  const int64_t n = joint->n_compact;
+  *mi = 0.0;
+  *is_null = n == 0 ? 1 : 0;  // sum over no joint groups is NULL
+  if (!n) return DQ_OK;
+  hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
+  dq_freq* marg[2] = {nullptr, nullptr};
+  DevBuf<uint32_t> slots[2];
+  Lookup L[2];
+  dq_status res = DQ_OK;
+  for (int k = 0; k < 2 && res == DQ_OK; ++k) {
+    const int32_t ty = joint->types[k];
+    res = dq_freq_create(joint->device, 1, &ty, 0, &marg[k]);
+    if (res == DQ_OK) res = dq_freq_marginal(joint, k, marg[k], hip_stream);
+    if (res == DQ_OK) res = compact_groups(marg[k]);
+    if (res != DQ_OK) break;
+    const int64_t m = marg[k]->n_compact;
+    uint64_t cap = 2;
+    while (cap < (uint64_t)(2 * m)) cap <<= 1;
+    if (slots[k].ensure(cap) != hipSuccess || hipMemsetAsync(slots[k].p, 0, cap * 4, stream) != hipSuccess) {
+      res = fail(DQ_ERR_OUT_OF_MEMORY, "marginal index");
+      break;
+    }
+    if (m)
+      hipLaunchKernelGGL(freq_lookup_build, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
+                         marg[k]->compact.p, m, cap - 1, slots[k].p);
+    L[k] = Lookup{marg[k]->compact.p, slots[k].p, cap - 1, marg[k]->arena.p, ty, marg[k]->exact ? 1 : 0};
+  }
+  if (res == DQ_OK) {
+    DevBuf<double> terms, partial;
+    constexpr int kSumBlocks = 1024;
+    if (terms.ensure(n) != hipSuccess || partial.ensure(kSumBlocks) != hipSuccess) {
+      res = fail(DQ_ERR_OUT_OF_MEMORY, "MutualInformation terms");
+    } else {
+      hipLaunchKernelGGL(freq_mi_terms, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                         joint->compact.p, n, joint->arena.p, part_types(joint, 1), L[0], L[1],
+                         (double)joint->num_rows, terms.p);
+      hipLaunchKernelGGL(freq_sum_f64, dim3(kSumBlocks), dim3(256), 0, stream, terms.p, n, partial.p);
+      std::vector<double> h(kSumBlocks);
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(h.data(), partial.p, kSumBlocks * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+          hipStreamSynchronize(stream) != hipSuccess) {
+        res = fail(DQ_ERR_DEVICE, "MutualInformation launch failed");
+      } else {
+        double sum = 0.0;
+        for (double v : h) sum += v;
+        *mi = sum;
+      }
+    }
+  }
+  for (dq_freq* m : marg) dq_freq_destroy(m);
+  return res;
 }
 
 extern "C" dq_status dq_freq_num_groups(dq_freq* f, int64_t* n) {

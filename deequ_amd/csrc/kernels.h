@@ -101,6 +101,7 @@ enum BodyClass : int32_t {
   BC_NUM_F64,
   BC_BITS,     // TK_VALIDITY, TK_BOOLMAP
   BC_STR_IN,
+  BC_DTYPE,     // TK_DTYPE
   BC_CORR,
   BC_HLL,
   BC_CORR_HLL,  // TK_COMOMENTS task that also fills an HLL task's registers from one of its columns

@@ -517,6 +517,61 @@ DQ_DEV void str_in_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& 
 }
 
 // ------------------------------------------------------------------------------------------------
+// TK_DTYPE (DataType, StatefulDataType.scala:36-69): each value of when(where, col) as a string is
+// NULL, else the first of FRACTIONAL ^(-|\+)? ?\d*\.\d*$, INTEGRAL ^(-|\+)? ?\d*$ (which matches
+// ""), BOOLEAN ^(true|false)$ it fully matches, else STRING.  Non-string columns are classified
+// as their cast to string: integers are Integral, booleans Boolean, and a double / float prints
+// with a '.' (Fractional) exactly when it is finite and 0 or 1e-3 <= |x| < 1e7 (Java's
+// Double/Float.toString switch to E-notation, or NaN / Infinity, are String).
+// ------------------------------------------------------------------------------------------------
+enum DtypeClass { DT_NULL = 0, DT_FRACTIONAL, DT_INTEGRAL, DT_BOOLEAN, DT_STRING };
+
+DQ_DEV int dtype_of_string(const uint8_t* p, int32_t n) {
+  DevBytes b{p};
+  int32_t i = 0;
+  if (i < n && (b.u8(i) == '-' || b.u8(i) == '+')) ++i;
+  if (i < n && b.u8(i) == ' ') ++i;
+  while (i < n && b.u8(i) - '0' < 10u) ++i;
+  if (i == n) return DT_INTEGRAL;  // no '.': FRACTIONAL fails, INTEGRAL matches
+  if (b.u8(i) == '.') {
+    ++i;
+    while (i < n && b.u8(i) - '0' < 10u) ++i;
+    if (i == n) return DT_FRACTIONAL;
+  }
+  if (n == 4 && b.u8(0) == 't' && b.u8(1) == 'r' && b.u8(2) == 'u' && b.u8(3) == 'e') return DT_BOOLEAN;
+  if (n == 5 && b.u8(0) == 'f' && b.u8(1) == 'a' && b.u8(2) == 'l' && b.u8(3) == 's' && b.u8(4) == 'e')
+    return DT_BOOLEAN;
+  return DT_STRING;
+}
+
+DQ_DEV void dtype_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& acc) {
+  int64_t c[5] = {0, 0, 0, 0, 0};
+  const int32_t* off = reinterpret_cast<const int32_t*>(t.values);
+  for (int64_t r = r_begin + lane_id(); r < r_end; r += 64) {
+    const uint32_t w = t.w_val ? bit1(t.w_val, r) & bit1(t.w_vld, r) : 1u;
+    int k;
+    if (!w || !bit1(t.valid, r)) {
+      k = DT_NULL;
+    } else if (t.type == DQ_UTF8) {
+      const int32_t s = off[r];
+      k = dtype_of_string(t.data + s, off[r + 1] - s);
+    } else if (t.type == DQ_BOOL) {
+      k = DT_BOOLEAN;
+    } else if (t.type == DQ_FLOAT64 || t.type == DQ_FLOAT32) {
+      const double x = load_f64(t.type, t.values, r);
+      const double ax = x < 0 ? -x : x;
+      k = (x == x && (ax == 0.0 || (ax >= 1e-3 && ax < 1e7))) ? DT_FRACTIONAL : DT_STRING;
+    } else {
+      k = DT_INTEGRAL;
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) c[q] += k == q;
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) acc.i[q] = c[q];
+}
+
+// ------------------------------------------------------------------------------------------------
 // TK_COMOMENTS (Correlation): rows where x and y are both non-NULL (and where is TRUE).
 // Lane l owns rows r0 + 128k + 2l + {0, 1} (k < 4) of a 512-row step.
 // ------------------------------------------------------------------------------------------------
@@ -853,6 +908,7 @@ __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? 4 : 1)) scan_kern
     if constexpr (BC == BC_NUM_F64) num_item<double>(t, r_begin, r_end, a);
     if constexpr (BC == BC_BITS) bits_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_STR_IN) str_in_item(t, r_begin, r_end, a);
+    if constexpr (BC == BC_DTYPE) dtype_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_CORR) corr_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_CORR_HLL) corr_rows<true>(t, r_begin, r_end, a, hll_lds + t.hll_out * kHllM);
     if constexpr (BC == BC_HLL) {
@@ -860,6 +916,7 @@ __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? 4 : 1)) scan_kern
     } else {
       constexpr int kind = BC <= BC_NUM_F64 ? TK_NUMERIC
                            : BC == BC_BITS  ? TK_VALIDITY
+                           : BC == BC_DTYPE ? TK_DTYPE
                            : BC == BC_CORR || BC == BC_CORR_HLL ? TK_COMOMENTS
                                             : TK_STR_IN;
       wave_reduce(kind, a);
@@ -921,6 +978,7 @@ scan_mixed_kernel(const TaskDesc* __restrict__ tasks, int n_desc, uint32_t n_ord
       case BC_NUM_F64: num_item<double>(t, r_begin, r_end, a); break;
       case BC_BITS: bits_item(t, r_begin, r_end, a); break;
       case BC_STR_IN: str_in_item(t, r_begin, r_end, a); break;
+      case BC_DTYPE: dtype_item(t, r_begin, r_end, a); break;
       case BC_CORR: corr_item(t, r_begin, r_end, a); break;
       default: break;
     }
@@ -1061,6 +1119,7 @@ hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const Sca
       case BC_NUM_F64: launch_body<BC_NUM_F64>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       case BC_BITS: launch_body<BC_BITS>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       case BC_STR_IN: launch_body<BC_STR_IN>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
+      case BC_DTYPE: launch_body<BC_DTYPE>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       case BC_CORR: launch_body<BC_CORR>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       case BC_HLL: launch_body<BC_HLL>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       case BC_CORR_HLL: launch_body<BC_CORR_HLL>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
@@ -1088,6 +1147,7 @@ int scan_max_blocks_per_cu(int body, int n_hll) {
     case BC_NUM_F64: return occupancy_of<BC_NUM_F64>(n_hll);
     case BC_BITS: return occupancy_of<BC_BITS>(n_hll);
     case BC_STR_IN: return occupancy_of<BC_STR_IN>(n_hll);
+    case BC_DTYPE: return occupancy_of<BC_DTYPE>(n_hll);
     case BC_CORR: return occupancy_of<BC_CORR>(n_hll);
     case BC_HLL: return occupancy_of<BC_HLL>(n_hll);
     case BC_CORR_HLL: return occupancy_of<BC_CORR_HLL>(n_hll);

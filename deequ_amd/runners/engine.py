@@ -162,6 +162,8 @@ def decode_value(kind: int, v: "N.dq_value"):
         return (float(v.f64[0]), float(v.f64[1]), float(v.f64[2]))
     if kind == N.AGG_CORR:
         return tuple(float(v.f64[k]) for k in range(6))
+    if kind == N.AGG_DTYPE:
+        return tuple(int(v.words[q]) for q in range(5))
     if kind == N.AGG_HLL:
         return tuple(int(w) - (1 << 64) if w >= (1 << 63) else int(w) for w in v.words)
     raise ValueError(kind)

@@ -179,7 +179,9 @@ typedef enum dq_agg_kind {
   DQ_AGG_MAX = 6,           /* max(when(where, col))                        Maximum.scala:36       */
   DQ_AGG_STDDEV_POP = 7,    /* stateful_stddev_pop(when(where, col))        StandardDeviation:49   */
   DQ_AGG_CORR = 8,          /* stateful_corr(when(where,x), when(where,y))  Correlation.scala:81   */
-  DQ_AGG_HLL = 9            /* stateful_approx_count_distinct(...)          ApproxCountDistinct:43 */
+  DQ_AGG_HLL = 9,           /* stateful_approx_count_distinct(...)          ApproxCountDistinct:43 */
+  DQ_AGG_DTYPE = 10         /* stateful_datatype(when(where, col))           DataType.scala:171-173:
+                               words[0..4] = NULL, Fractional, Integral, Boolean, String counts   */
 } dq_agg_kind;
 
 typedef struct dq_agg {
@@ -307,6 +309,18 @@ dq_status dq_freq_summarize(dq_freq* freq, dq_freq_summary* out);
  * (GroupingAnalyzers.scala:62-65).  Lets one group-by serve Histogram(col) and the
  * Uniqueness/Distinctness/Entropy grouping of col.  n_null_key_rows counts the NULL rows. */
 dq_status dq_freq_summarize_keys(dq_freq* freq, dq_freq_summary* out);
+
+/* The marginal of key column key_index of a multi-key grouping table, added into `out` (a table
+ * with one key of that column's type): every group of `joint` contributes its count to the group
+ * of its key_index value, and out's numRows grows by joint's.  MutualInformation
+ * (MutualInformation.scala:41-70) needs these marginals of the joint frequencies. */
+dq_status dq_freq_marginal(dq_freq* joint, int key_index, dq_freq* out, void* hip_stream);
+
+/* MutualInformation (MutualInformation.scala:41-84) of a two-key grouping table: the sum over its
+ * groups of (pxy/n) ln((pxy/n) / ((px/n)(py/n))), n = numRows, px / py the marginal counts
+ * (re-aggregated from the joint table on the device and joined by key).  *is_null = 1 when the
+ * table has no groups (the reference's sum is then NULL -> empty state). */
+dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int* is_null, void* hip_stream);
 
 /* Number of groups currently in the table (NULL group and every distinct key). */
 dq_status dq_freq_num_groups(dq_freq* freq, int64_t* n_groups);

@@ -777,3 +777,59 @@ def quantile_rank_error(values, quantile: float, result: float) -> int:
     if lo <= target <= hi:
         return 0
     return min(abs(target - lo), abs(target - hi))
+
+
+# ------------------------------------------------------------------------------------------------
+# DataType (M/analyzers/catalyst/StatefulDataType.scala:36-69): Scala `x match { case R(_) => }`
+# is a full match; each value of when(where, col) cast to string is classified in order.
+# ------------------------------------------------------------------------------------------------
+def datatype_counts(t: OTable, column: str, where: Optional[str]) -> Tuple[int, ...]:
+    """(NULL, Fractional, Integral, Boolean, String) counts."""
+    import re
+    frac = re.compile(r"(-|\+)? ?[0-9]*\.[0-9]*")
+    integral = re.compile(r"(-|\+)? ?[0-9]*")
+    boolean = re.compile(r"(true|false)")
+    ty = t.types[column]
+    out = [0, 0, 0, 0, 0]
+    for v in _sel(t, column, where):
+        if v is None:
+            out[0] += 1
+            continue
+        if ty == "string":
+            s = v
+        elif ty == "boolean":
+            s = "true" if v else "false"
+        elif ty in ("double", "float"):
+            s = java_double_to_string(float(v))
+        else:
+            s = str(int(v))
+        if frac.fullmatch(s):
+            out[1] += 1
+        elif integral.fullmatch(s):
+            out[2] += 1
+        elif boolean.fullmatch(s):
+            out[3] += 1
+        else:
+            out[4] += 1
+    return tuple(out)
+
+
+# ------------------------------------------------------------------------------------------------
+# MutualInformation (M/analyzers/MutualInformation.scala:41-84): joint frequencies (both keys
+# non-NULL), marginals re-aggregated from them, joined, summed per joint group.
+# ------------------------------------------------------------------------------------------------
+def mutual_information(t: OTable, c1: str, c2: str) -> Optional[float]:
+    import math
+    joint = frequencies(t, [c1, c2])
+    if not joint:
+        return None
+    px: Dict = {}
+    py: Dict = {}
+    for (x, y), c in joint.items():
+        px[x] = px.get(x, 0) + c
+        py[y] = py.get(y, 0) + c
+    total = t.n
+    acc = 0.0
+    for (x, y), c in joint.items():
+        acc += (c / total) * math.log((c / total) / ((px[x] / total) * (py[y] / total)))
+    return acc

@@ -62,11 +62,28 @@ def test_where_replaces_last_constraint_and_predicates():
     assert a.predicate == "x IS NULL OR (x > 1.0 AND x < 2.0)"
 
 
-def test_unsupported_operator_fails_loudly():
-    check = Check(CheckLevel.Warning, "d").has_data_type("description")
-    r = check.evaluate(AnalyzerContext({}))
-    assert r.status == CheckStatus.Warning
-    assert "not implemented" in r.constraint_results[0].message
+def test_data_type_and_mutual_information_checks():
+    """Check.scala:653-661 (unnamed: the AnalysisBasedConstraint's own toString) and :371-379."""
+    from deequ_amd.analyzers import DataType, MutualInformation
+    from deequ_amd.checks import ConstrainableDataTypes
+    from deequ_amd.metrics import Distribution, DistributionValue, HistogramMetric
+    check = (Check(CheckLevel.Error, "t").has_data_type("c", ConstrainableDataTypes.Numeric,
+                                                       lambda v: v >= 0.5)
+             .has_mutual_information("a", "b", lambda v: v > 0.1))
+    assert check.required_analyzers() == [DataType("c"), MutualInformation(["a", "b"])]
+    assert str(check.constraints[0]) == \
+        "AnalysisBasedConstraint(DataType(c,None),<function1>,Some(<function1>),None)"
+    assert str(check.constraints[1]) == "MutualInformationConstraint(MutualInformation(List(a, b)))"
+    dist = Distribution({"Unknown": DistributionValue(1, 0.25), "Fractional": DistributionValue(1, 0.25),
+                         "Integral": DistributionValue(1, 0.25), "Boolean": DistributionValue(0, 0.0),
+                         "String": DistributionValue(1, 0.25)}, 5)
+    ctx = AnalyzerContext({DataType("c"): HistogramMetric("c", Success(dist)),
+                           MutualInformation(["a", "b"]): DoubleMetric(Entity.Mutlicolumn,
+                                                                      "MutualInformation", "a,b",
+                                                                      Success(0.05))})
+    r = check.evaluate(ctx)
+    assert [c.status for c in r.constraint_results] == [ConstraintStatus.Success,
+                                                        ConstraintStatus.Failure]
 
 
 def test_pattern_and_quantile_checks_require_their_analyzers():
