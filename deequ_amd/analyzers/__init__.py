@@ -12,5 +12,5 @@ from .scan import (ApproxCountDistinct, ApproxCountDistinctState, Completeness, 
                    Minimum, NumMatches, PatternMatch, Patterns, Size, StandardDeviation,
                    StandardDeviationState, Sum, SumState)
 from .datatype import DataType, DataTypeHistogram, DataTypeInstances, determine_type
-from .quantile import ApproxQuantile, ApproxQuantileState, QuantileSummaries
+from .quantile import ApproxQuantile, ApproxQuantiles, ApproxQuantileState, QuantileSummaries
 from .state_provider import InMemoryStateProvider, StateLoader, StatePersister

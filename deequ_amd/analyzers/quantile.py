@@ -208,9 +208,57 @@ class ApproxQuantile(Analyzer):
                                    entity_from([self.column]))
 
 
+@dataclass(frozen=True)
+class ApproxQuantiles(Analyzer):
+    """ApproxQuantiles.scala:39-101: several quantiles of one column from one summary, as a
+    KeyedDoubleMetric keyed by the quantile's Scala toString.  Unlike ApproxQuantile an all-NULL
+    column is not an empty state: getPercentiles of an empty digest is empty, so the metric is
+    a Success of an empty map."""
+    column: str
+    quantiles: Tuple[float, ...]
+    relative_error: float = 0.01
+
+    def __init__(self, column, quantiles, relative_error: float = 0.01):
+        object.__setattr__(self, "column", column)
+        object.__setattr__(self, "quantiles", tuple(float(q) for q in quantiles))
+        object.__setattr__(self, "relative_error", relative_error)
+
+    def __str__(self):
+        qs = ", ".join(_scala_double(q) for q in self.quantiles)
+        return f"ApproxQuantiles({self.column},List({qs}),{_scala_double(self.relative_error)})"
+
+    def _param_check(self, _schema):
+        for q in self.quantiles:
+            ApproxQuantile(self.column, q, self.relative_error)._param_check(_schema)
+        ApproxQuantile(self.column, 0.5, self.relative_error)._param_check(_schema)
+
+    def preconditions(self):
+        return [self._param_check, Preconditions.has_column(self.column),
+                Preconditions.is_numeric(self.column)]
+
+    def compute_state_from(self, data):
+        s = ApproxQuantile(self.column, 0.5, self.relative_error).compute_state_from(data)
+        return s if s is not None else ApproxQuantileState(
+            QuantileSummaries(self.relative_error, [], 0))
+
+    def compute_metric_from(self, state):
+        from ..metrics import Entity, KeyedDoubleMetric, Success
+        if state is None:
+            return self.to_failure_metric(empty_state_exception(self))
+        s = state.summaries
+        vals = {} if s.count == 0 else {_scala_double(q): s.query(q) for q in self.quantiles}
+        return KeyedDoubleMetric(Entity.Column, "ApproxQuantiles", self.column, Success(vals))
+
+    def to_failure_metric(self, exception):
+        from ..exceptions import wrap_if_necessary
+        from ..metrics import Entity, Failure, KeyedDoubleMetric
+        return KeyedDoubleMetric(Entity.Column, "ApproxQuantiles", self.column,
+                                 Failure(wrap_if_necessary(exception)))
+
+
 def _scala_double(x: float) -> str:
     from .grouping import java_double_to_string
     return java_double_to_string(float(x))
 
 
-__all__ = ["ApproxQuantile", "ApproxQuantileState", "QuantileSummaries", "quantile_summaries"]
+__all__ = ["ApproxQuantile", "ApproxQuantiles", "ApproxQuantileState", "QuantileSummaries", "quantile_summaries"]

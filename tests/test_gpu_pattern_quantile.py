@@ -102,3 +102,16 @@ def test_approx_quantile_of_all_null_column_is_empty(gpu_device):
     from deequ_amd.analyzers import ApproxQuantile
     df = _df({"x": pa.array([None, None], pa.float64())}, gpu_device)
     assert ApproxQuantile("x", 0.5).calculate(df).value.is_failure
+
+
+def test_approx_quantiles_keyed_metric(gpu_device):
+    """ApproxQuantiles.scala:76-88: one summary, one entry per quantile keyed by its toString;
+    an all-NULL column gives an empty map (not a failure)."""
+    from deequ_amd.analyzers import ApproxQuantiles
+    df = _df({"att1": pa.array([1, 2, 3, 4, 5, 6], pa.int64()),
+              "n": pa.array([None] * 6, pa.float64())}, gpu_device)
+    m = ApproxQuantiles("att1", [0.5, 0.25, 1.0]).calculate(df)
+    assert m.value.get() == {"0.5": 3.0, "0.25": 2.0, "1.0": 6.0}
+    assert [x.name for x in m.flatten()] == ["ApproxQuantiles-0.5", "ApproxQuantiles-0.25",
+                                             "ApproxQuantiles-1.0"]
+    assert ApproxQuantiles("n", [0.5]).calculate(df).value.get() == {}
