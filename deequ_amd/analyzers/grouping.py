@@ -76,6 +76,13 @@ class FrequencyTable:
         N.check(N.lib.dq_freq_num_groups(self.handle, ctypes.byref(n)))
         return int(n.value)
 
+    def null_literal(self) -> Tuple[int, int]:
+        """(rows of the NULL group, count of the "NullValue" string group) of a Histogram table
+        (dq_freq_null_literal); the second is 0 unless the key is one string column."""
+        nullg, lit = ctypes.c_int64(), ctypes.c_int64()
+        N.check(N.lib.dq_freq_null_literal(self.handle, ctypes.byref(nullg), ctypes.byref(lit)))
+        return int(nullg.value), int(lit.value)
+
     def export(self) -> List[Tuple[tuple, int]]:
         """All groups as (key tuple, count); a NULL key component is None."""
         n = self.count()
@@ -513,6 +520,26 @@ def _python_dtype(value, column_dtype: int) -> int:
     return column_dtype
 
 
+def _fold_null_group(frequencies, dtype: int, k: int):
+    """Histogram's details and numberOfBins from a table whose NULL rows form a group kept apart:
+    na.fill("NullValue") (Histogram.scala:59-66) makes them one group with any real "NullValue"
+    string, so that group's count is the sum of both (dq_freq_null_literal) and it is placed by
+    that count among the device top-N (ties in any order, like rdd.top)."""
+    nullg, lit = frequencies.null_literal()
+    raw = frequencies.topk(k + 2)  # up to two raw entries fold into one
+    top = []
+    for (key,), c in raw:
+        if key is None or (dtype == N.UTF8 and key == NULL_FIELD_REPLACEMENT):
+            continue
+        top.append((cast_to_string(key, dtype), c))
+    folded = nullg + lit
+    if folded:
+        at = next((i for i, (_, c) in enumerate(top) if c < folded), len(top))
+        top.insert(at, (NULL_FIELD_REPLACEMENT, folded))
+    bins = frequencies.count() - (1 if nullg and lit else 0)
+    return top[:k], bins
+
+
 @dataclass
 class HistogramState(FrequenciesAndNumRows):
     dtype: int = N.UTF8
@@ -563,16 +590,13 @@ class Histogram(Analyzer):
     @staticmethod
     def table_serves_grouping(data, column: str) -> bool:
         """Can this column's Histogram table also serve its grouping (Uniqueness, Distinctness,
-        Entropy, ... on [column])?  Integral and boolean columns always: their NULL rows form a
-        separate group the keyed view drops.  A string column only without NULLs (a NULL would
-        merge with a "NullValue" string).  Floating-point never: Histogram folds NaN payloads
-        (cast to string), the grouping does not."""
+        Entropy, ... on [column])?  Integral, boolean and string columns: their NULL rows form a
+        separate group that the keyed view drops (a string column's NULL group is folded into the
+        "NullValue" string only when Histogram reads the table, _fold_null_group).
+        Floating-point never: Histogram folds NaN payloads (cast to string), the grouping does
+        not."""
         dtype = data.schema[column].dtype
-        if dtype in (N.BOOL, N.INT8, N.INT16, N.INT32, N.INT64):
-            return True
-        if dtype == N.UTF8:
-            return all(b[column].validity is None for b in data.batches)  # no bitmap: no NULLs
-        return False
+        return dtype in (N.BOOL, N.INT8, N.INT16, N.INT32, N.INT64, N.UTF8)
 
     def compute_state_from(self, data):
         from ..distributed import compute_frequencies_distributed, is_distributed
@@ -592,9 +616,7 @@ class Histogram(Analyzer):
         try:
             if state.binning_udf is None:
                 # device top-N: only max_detail_bins groups reach the host (Histogram.scala:78-79)
-                top = [(cast_to_string(key, state.dtype), c)
-                       for (key,), c in state.frequencies.topk(self.max_detail_bins)]
-                bins = state.frequencies.count()
+                top, bins = _fold_null_group(state.frequencies, state.dtype, self.max_detail_bins)
             else:
                 groups = state.string_groups()
                 # rdd.top(maxDetailBins)(OrderByAbsoluteCount): ties are arbitrary in the reference

@@ -529,9 +529,12 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
           } else {
             h = str_row_hash(SView{c.data + s0[j], len[j]});
           }
-        } else if (a.ks.null_as_group) {  // Histogram: NULL is the "NullValue" literal
-          h = str_row_hash(SView{nullptr, kNullValueLen});
-          str_short_key(SView{nullptr, kNullValueLen}, k0, k1);
+        } else if (a.ks.null_as_group) {
+          // Histogram: the NULL rows are one group kept apart (C_NULL_GROUP), so this table also
+          // serves the column's grouping; the caller folds it into the "NullValue" string group
+          // (Histogram.scala:59-66) with the literal's count from phase C (dq_freq_null_literal)
+          ++nullg;
+          continue;
         } else {
           ++nulls;
           continue;
@@ -934,7 +937,18 @@ struct CArgs {
   Group* cand;
   Group* groups;  // materialise every group (nullptr: statistics only)
   unsigned long long* counters;
+  // Histogram on a string column: the count of the "NullValue" string group is added to
+  // *lit_count (nullptr: no probe); lit_h is that key's row hash
+  uint64_t lit_h;
+  unsigned long long* lit_count;
 };
+
+// Is the encoded one-column utf8 key at p the 9-byte string "NullValue"?
+DQ_DEV bool enc_is_null_literal(const uint8_t* p) {
+  const uint32_t* e = reinterpret_cast<const uint32_t*>(p);
+  return e[0] == 1u && e[1] == (uint32_t)kNullValueLen && e[2] == (uint32_t)kNullValueLo &&
+         e[3] == (uint32_t)(kNullValueLo >> 32) && e[4] == kNullValueHi;
+}
 
 constexpr int kPF = 2;        // records per thread loaded ahead
 constexpr int kCThreads = 512;  // phase-C workgroup: two per CU by LDS, 128 VGPRs per lane
@@ -1145,6 +1159,9 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     for (int sl = tid; sl < KT; sl += kCThreads) {
       if (tkey[sl] == kEmptyKey) continue;
       const uint64_t c = tcnt[sl];
+      if constexpr (HASHED)
+        if (a.lit_count && tkey[sl] == a.lit_h && enc_is_null_literal(a.arena + trep[sl]))
+          atomicAdd(a.lit_count, (unsigned long long)c);
       ++g;
       if (c == 1) ++un;  // the common count: a register, not an LDS atomic on one address
       else if (c < kSmallCounts) atomicAdd(&s_chist[c], 1u);
@@ -1491,6 +1508,7 @@ struct dq_freq {
   DevBuf<unsigned long long> red;
   uint64_t st_groups = 0, st_unique = 0;
   double st_entropy = 0.0;
+  uint64_t st_literal = 0;  // Histogram on a string: count of the "NullValue" string group
   bool recounted = false;
   // last top-k (dq_freq_topk is called twice: sizes, then data)
   int topk_k = -1;
@@ -1503,6 +1521,12 @@ static unsigned grid_for(uint64_t n, unsigned cap = 4096) {
   if (g < 1) g = 1;
   if (g > cap) g = cap;
   return (unsigned)g;
+}
+
+// A Histogram table over one string column: its NULL rows are kept apart from a "NullValue"
+// string group that phase C probes for.
+static bool has_null_literal(const dq_freq* f) {
+  return !f->exact && f->n_keys == 1 && f->types[0] == DQ_UTF8 && f->mode_null_as_group > 0;
 }
 
 static void invalidate(dq_freq* f) {
@@ -1759,7 +1783,8 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
   HIP_TRY(f->part_unique.ensure(P));
   HIP_TRY(f->part_off.ensure(P));
   HIP_TRY(f->part_entropy.ensure(P));
-  HIP_TRY(f->red.ensure(3));
+  HIP_TRY(f->red.ensure(4));
+  HIP_TRY(hipMemsetAsync(f->red.p + 3, 0, 8, f->stream));
   HIP_TRY(f->ovf_n.ensure(1));
   HIP_TRY(hipMemsetAsync(f->part_groups.p, 0, P * 8, f->stream));
   HIP_TRY(hipMemsetAsync(f->part_unique.p, 0, P * 8, f->stream));
@@ -1789,6 +1814,10 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     a.cand = want_cand ? f->cand.p : nullptr;
     a.groups = want_groups ? f->groups.p : nullptr;
     a.counters = f->dev_words.p;
+    if (has_null_literal(f)) {
+      a.lit_h = str_row_hash(SView{nullptr, kNullValueLen});
+      a.lit_count = f->red.p + 3;
+    }
     HIP_TRY(f->ovf_a.ensure(2 * P));
     HIP_TRY(hipMemsetAsync(f->ovf_n.p, 0, 4, f->stream));
     a.entries = nullptr;
@@ -1824,12 +1853,13 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
   hipLaunchKernelGGL(freq_reduce, dim3(1), dim3(kThreads), 0, f->stream, f->part_groups.p,
                      f->part_unique.p, f->part_entropy.p, P, f->red.p);
   HIP_TRY(hipGetLastError());
-  unsigned long long r[3];
+  unsigned long long r[4];
   HIP_TRY(hipStreamSynchronize(f->stream));
   HIP_TRY(hipMemcpy(r, f->red.p, sizeof(r), hipMemcpyDeviceToHost));
   f->st_groups = r[0];
   f->st_unique = r[1];
   f->st_entropy = __builtin_bit_cast(double, r[2]);
+  f->st_literal = r[3];
   f->c_valid = true;
   f->c_num_rows = nr;
   f->c_groups = want_groups;
@@ -2384,6 +2414,17 @@ extern "C" dq_status dq_freq_num_groups(dq_freq* f, int64_t* n) {
   dq_status st = finalize_c(f, false, false);
   if (st != DQ_OK) return st;
   *n = (int64_t)(f->st_groups + (f->h_counters[C_NULL_GROUP] ? 1 : 0));
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_freq_null_literal(dq_freq* f, int64_t* null_group_rows,
+                                          int64_t* literal_count) {
+  if (!f || !null_group_rows || !literal_count) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  HIP_TRY(hipSetDevice(f->device));
+  dq_status st = finalize_c(f, false, false);
+  if (st != DQ_OK) return st;
+  *null_group_rows = (int64_t)f->h_counters[C_NULL_GROUP];
+  *literal_count = has_null_literal(f) ? (int64_t)f->st_literal : 0;
   return DQ_OK;
 }
 

@@ -215,6 +215,17 @@ class DistributedFrequencies:
     def count(self) -> int:
         return int(self.summarize().n_groups)
 
+    def null_literal(self):
+        """(NULL-group rows, "NullValue" string count) summed over the ranks: each lives on one."""
+        import torch
+        import torch.distributed as dist
+        nullg, lit = self.owned.null_literal()
+        dev = "cpu" if dist.get_backend() == "gloo" else f"cuda:{self.owned.device}"
+        t = torch.tensor([nullg, lit], dtype=torch.int64, device=dev)
+        dist.all_reduce(t)
+        a, b = (int(v) for v in t.cpu().tolist())
+        return a, b
+
     def export(self):
         """Every group of every rank (each group lives on exactly one), rank order."""
         import torch.distributed as dist

@@ -286,8 +286,11 @@ void dq_freq_destroy(dq_freq* freq);
  * (GroupingAnalyzers.scala:70, a fresh HashAggregate buffer per task). */
 dq_status dq_freq_reset(dq_freq* freq, void* hip_stream);
 /* Inserts one batch: rows where any key is NULL are skipped but counted in numRows
- * (GroupingAnalyzers.scala:62-77).  Histogram mode (null_as_group != 0) instead maps a NULL key
- * to its own group, like na.fill("NullValue") (Histogram.scala:59-66). */
+ * (GroupingAnalyzers.scala:62-77).  Histogram mode (null_as_group != 0, one key column) instead
+ * counts the NULL rows as one group kept apart from every keyed group (export / top-k report it
+ * with tag 0); na.fill("NullValue") (Histogram.scala:59-66) folds it into a "NullValue" string
+ * group, which the caller does with dq_freq_null_literal.  Kept apart, the same table also serves
+ * the column's grouping (dq_freq_summarize_keys). */
 dq_status dq_freq_add_device(dq_freq* freq, const dq_column* keys, int n_keys, int null_as_group,
                              void* hip_stream);
 
@@ -304,7 +307,7 @@ typedef struct dq_freq_summary {
   double entropy;
 } dq_freq_summary;
 dq_status dq_freq_summarize(dq_freq* freq, dq_freq_summary* out);
-/* The same aggregation over the keyed groups only: a fixed-width table built with NULL as a group
+/* The same aggregation over the keyed groups only: a table built with NULL as a group
  * (Histogram mode) summarised as the grouping of that column would be, its NULL rows dropped
  * (GroupingAnalyzers.scala:62-65).  Lets one group-by serve Histogram(col) and the
  * Uniqueness/Distinctness/Entropy grouping of col.  n_null_key_rows counts the NULL rows. */
@@ -324,6 +327,11 @@ dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int* is_null, v
 
 /* Number of groups currently in the table (NULL group and every distinct key). */
 dq_status dq_freq_num_groups(dq_freq* freq, int64_t* n_groups);
+/* Histogram's NULL fold (Histogram.scala:59-66, na.fill("NullValue") before the groupBy): the rows
+ * of the NULL group, and the count of the string group "NullValue" of a one-utf8-key Histogram
+ * table (0 for every other table).  Histogram's group "NullValue" has their sum as its count;
+ * numberOfBins is dq_freq_num_groups minus 1 when both are non-zero. */
+dq_status dq_freq_null_literal(dq_freq* freq, int64_t* null_group_rows, int64_t* literal_count);
 /* Rows added so far (nulls included): the numRows of FrequenciesAndNumRows. */
 int64_t dq_freq_num_rows(const dq_freq* freq);
 /* Exports every group (unordered): counts_out[n], key_offsets_out[n + 1] and the encoded keys:
@@ -336,7 +344,8 @@ dq_status dq_freq_export(dq_freq* freq, int64_t* counts_out, int64_t* key_offset
                          int64_t* key_bytes_needed);
 /* The k groups with the largest counts, in descending count order (ties in any order), in the
  * export format: Histogram's details, rdd.top(maxDetailBins)(OrderByAbsoluteCount)
- * (Histogram.scala:78-79; numberOfBins is dq_freq_num_groups).  Only these k keys leave the
+ * (Histogram.scala:78-79; numberOfBins is dq_freq_num_groups; see dq_freq_null_literal for the
+ * NULL fold of a string column).  Only these k keys leave the
  * device.  Call with key_bytes_out = NULL for *n_out and *key_bytes_needed; counts_out[k] and
  * key_offsets_out[k + 1] must hold k entries. */
 dq_status dq_freq_topk(dq_freq* freq, int k, int64_t* counts_out, int64_t* key_offsets_out,
@@ -368,7 +377,7 @@ typedef struct dq_freq_record {
 } dq_freq_record;
 /* Per owner: rec_counts[n_parts] records and var_bytes[n_parts] bytes.  special[3] = the counts
  * kept outside the records, which the caller routes to ONE owner: {0 (unused), rows of the
- * fixed-width NULL group (Histogram), rows skipped for a NULL key}. */
+ * NULL group (Histogram), rows skipped for a NULL key}. */
 dq_status dq_freq_partition_sizes(dq_freq* freq, int n_parts, int64_t* rec_counts,
                                   int64_t* var_bytes, int64_t* special);
 /* Writes the owner segments back to back (segment j at the exclusive prefix sums of the sizes

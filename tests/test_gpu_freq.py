@@ -150,21 +150,25 @@ def test_repartition_matches_single_table(parts, cols, gpu_device):
 
 @pytest.mark.parametrize("col", ["id", "s"])
 def test_repartition_histogram_null_group(col, gpu_device):
-    """Histogram mode (NULL is its own group, Histogram.scala:59-66) through the repartition."""
+    """Histogram mode (NULL is its own group, Histogram.scala:59-66) through the repartition: the
+    NULL group stays apart from a real "NullValue" string (folded only when Histogram reads it)."""
     t = _table(20_000, seed=3, null_rate=0.1)
     vals = t.column(col).to_pylist()
     exp = {}
     for v in vals:
-        if v is None and col == "s":   # na.fill("NullValue"): one group with the real string
-            v = "NullValue"
         exp[(v,)] = exp.get((v,), 0) + 1
     owners = _repartition(t, [col], 4, gpu_device, null_as_group=True)
     got = {}
+    nullg = lit = 0
     for owned in owners:
         for key, cnt in owned.export():
             assert key not in got
             got[key] = cnt
+        a, b = owned.null_literal()
+        nullg, lit = nullg + a, lit + b
     assert got == exp
+    assert nullg == exp[(None,)]
+    assert lit == (exp.get(("NullValue",), 0) if col == "s" else 0)
 
 
 @pytest.mark.parametrize("cols", [("id",), ("s",)])
@@ -225,35 +229,43 @@ def test_merge_keeps_hash_collisions_apart_and_handles_histogram_nulls(gpu_devic
     for col in ("id", "s"):
         a = _freq_table(t, [col], gpu_device, null_as_group=True)
         b = _freq_table(t, [col], gpu_device, null_as_group=True)
-        got = dict(a.merged(b).export())
+        m = a.merged(b)
+        got = dict(m.export())
         exp = {}
         for v in t.column(col).to_pylist():
-            if v is None and col == "s":
-                v = "NullValue"
             exp[(v,)] = exp.get((v,), 0) + 2
         assert got == exp, col
+        assert m.null_literal() == (exp[(None,)], exp.get(("NullValue",), 0) if col == "s" else 0)
 
 
 @pytest.mark.parametrize("n,k", [(1, 10), (5000, 3), (40_000, 1000), (200_000, 1000)])
 @pytest.mark.parametrize("col", ["id", "s", "u"])
 def test_topk_matches_oracle_order(n, k, col, gpu_device):
     """dq_freq_topk == rdd.top(k)(OrderByAbsoluteCount) up to ties: the multiset of returned counts
-    is the oracle's k largest, and every returned key carries its exact count."""
-    from oracle import deequ_oracle as O
+    is the oracle's k largest, and every returned key carries its exact count.  Raw table: the
+    NULL group apart; Histogram's view (_fold_null_group): NULL folded into "NullValue"."""
+    from deequ_amd import _native as N
+    from deequ_amd.analyzers.grouping import _fold_null_group, cast_to_string
     t = _table(n, seed=n + 3)
     ft = _freq_table(t, [col], gpu_device, null_as_group=True)
     got = ft.topk(k)
     vals = t.column(col).to_pylist()
-    exp = {}
+    raw, exp = {}, {}
     for v in vals:
-        if v is None and col != "id":
-            v = "NullValue"
-        exp[v] = exp.get(v, 0) + 1
-    want = sorted(exp.values(), reverse=True)[:k]
-    assert [c for _, c in got] == want
+        raw[v] = raw.get(v, 0) + 1
+        f = "NullValue" if v is None and col != "id" else v
+        exp[f] = exp.get(f, 0) + 1
+    assert [c for _, c in got] == sorted(raw.values(), reverse=True)[:k]
     for (key,), c in got:
-        assert exp[key] == c
-    assert ft.count() == len(exp)
+        assert raw[key] == c
+    assert ft.count() == len(raw)
+    dtype = N.INT64 if col == "id" else N.UTF8
+    top, bins = _fold_null_group(ft, dtype, k)
+    assert bins == len(exp)
+    assert [c for _, c in top] == sorted(exp.values(), reverse=True)[:k]
+    str_exp = {cast_to_string(key, dtype): c for key, c in exp.items()}
+    for key, c in top:
+        assert str_exp[key] == c
 
 
 @pytest.mark.parametrize("target", ["1", "7", "1000000000"])
@@ -315,3 +327,33 @@ def test_histogram_table_serves_grouping(col, nulls, gpu_device):
     hist = ctx.metric(Histogram(col)).value.get()
     exp_bins = len(freq) + (1 if nulls and col == "id" else 0)
     assert hist.number_of_bins == exp_bins
+
+
+@pytest.mark.parametrize("k", [1, 2, 1000])
+def test_histogram_shares_string_table_with_grouping(k, gpu_device):
+    """Histogram("s") and the grouping of ["s"] read ONE group-by of a string column with NULLs
+    and real "NullValue" strings (runners._histogram_tables_for_groupings): the grouping drops the
+    NULL rows (GroupingAnalyzers.scala:62-65), Histogram folds them into "NullValue"
+    (Histogram.scala:59-66) -- both equal to the oracle's."""
+    from deequ_amd.analyzers import CountDistinct, Entropy, Histogram, Uniqueness
+    from deequ_amd.runners import AnalysisRunner
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    n = 30_000
+    t = _table(n, seed=77, null_rate=0.3)   # NULL rows outnumber every string: the fold ranks first
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=8192)
+    ot = _otable(t)
+    h = Histogram("s", max_detail_bins=k)
+    ctx = AnalysisRunner.do_analysis_run(df, [h, Uniqueness(["s"]), Entropy("s"), CountDistinct(["s"])])
+    freq = O.frequencies(ot, ["s"])
+    assert ctx.metric(Uniqueness(["s"])).value.get() == O.uniqueness(freq, n)
+    assert ctx.metric(CountDistinct(["s"])).value.get() == O.count_distinct(freq)
+    assert _rel_close(ctx.metric(Entropy("s")).value.get(), O.entropy(freq, n))
+    hist, _ = O.histogram(ot, "s")
+    dist = ctx.metric(h).value.get()
+    assert dist.number_of_bins == len(hist)
+    want = sorted(hist.values(), reverse=True)[:k]
+    got = sorted((v.absolute for v in dist.values.values()), reverse=True)
+    assert got == want
+    for key, v in dist.values.items():
+        assert hist[key] == v.absolute and v.ratio == v.absolute / n

@@ -112,8 +112,7 @@ def test_freq_add_host_matches_oracle(cols, null_as_group, gpu_device):
     if null_as_group:
         exp = {}
         for v in t.column(cols[0]).to_pylist():
-            k = ("NullValue" if v is None else v,)
-            exp[k] = exp.get(k, 0) + 1
+            exp[(v,)] = exp.get((v,), 0) + 1  # the NULL group kept apart (tag 0)
     else:
         exp = O.frequencies(_otable(t), list(cols))
     assert dict(ft.export()) == exp

@@ -18,10 +18,10 @@ def test_integral_and_boolean_columns_always_share():
         assert Histogram.table_serves_grouping(_data(t, [True, False]), "c")
 
 
-def test_strings_share_only_without_nulls():
+def test_strings_share_with_or_without_nulls():
+    # the NULL rows are a group kept apart in the table; Histogram folds it into "NullValue"
     assert Histogram.table_serves_grouping(_data(N.UTF8, [False, False]), "c")
-    # a NULL would merge with a literal "NullValue" in the Histogram table
-    assert not Histogram.table_serves_grouping(_data(N.UTF8, [False, True]), "c")
+    assert Histogram.table_serves_grouping(_data(N.UTF8, [False, True]), "c")
 
 
 def test_floating_point_never_shares():
