@@ -13,4 +13,4 @@ from .scan import (ApproxCountDistinct, ApproxCountDistinctState, Completeness, 
                    StandardDeviationState, Sum, SumState)
 from .datatype import DataType, DataTypeHistogram, DataTypeInstances, determine_type
 from .quantile import ApproxQuantile, ApproxQuantiles, ApproxQuantileState, QuantileSummaries
-from .state_provider import InMemoryStateProvider, StateLoader, StatePersister
+from .state_provider import HdfsStateProvider, InMemoryStateProvider, StateLoader, StatePersister

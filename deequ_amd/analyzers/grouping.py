@@ -143,6 +143,41 @@ class FrequencyTable:
         N.check(N.lib.dq_freq_marginal(self.handle, key_index, out.handle, stream))
         return out
 
+    @staticmethod
+    def encode_key(key: tuple, key_types: Sequence[int]) -> bytes:
+        """A group key in the dq_freq_export format (per column: u32 tag, then 8 value bytes or a
+        u32 length + the UTF-8 bytes padded to 4)."""
+        out = []
+        for v, t in zip(key, key_types):
+            if v is None:
+                out.append(struct.pack("<I", 0))
+            elif t == N.UTF8:
+                b = v.encode("utf-8")
+                out.append(struct.pack("<II", 1, len(b)) + b + b"\0" * ((-len(b)) % 4))
+            else:
+                out.append(struct.pack("<I", 1) + struct.pack("<Q", _encode_fixed(t, v)))
+        return b"".join(out)
+
+    @staticmethod
+    def from_groups(key_columns, key_types, device: int, groups, num_rows: int,
+                    null_key_rows: int = 0, null_as_group: bool = False,
+                    stream=None) -> "FrequencyTable":
+        """A table holding the given (key tuple, count) groups (dq_freq_import, the inverse of
+        export): how a persisted frequency state is loaded back (StateProvider.scala:270-278)."""
+        ft = FrequencyTable(list(key_columns), list(key_types), device)
+        keys = [FrequencyTable.encode_key(k, key_types) for k, _ in groups]
+        offs = np.zeros(len(keys) + 1, np.int64)
+        offs[1:] = np.cumsum([len(k) for k in keys]) if keys else []
+        raw = np.frombuffer(b"".join(keys) or b"\0", np.uint8).copy()
+        counts = np.ascontiguousarray([c for _, c in groups] or [0], np.int64)
+        if stream is None:
+            import torch
+            stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+        N.check(N.lib.dq_freq_import(ft.handle, counts.ctypes.data, offs.ctypes.data,
+                                     raw.ctypes.data, len(keys), int(num_rows), int(null_key_rows),
+                                     1 if null_as_group else 0, stream))
+        return ft
+
     def merged(self, other: "FrequencyTable") -> "FrequencyTable":
         out = FrequencyTable(self.key_columns, self.key_types, self.device)
         N.check(N.lib.dq_freq_merge(out.handle, self.handle))
@@ -175,6 +210,17 @@ class KeyedFrequencies:
 
     def count(self) -> int:
         return int(self.summarize().n_groups)
+
+
+def _encode_fixed(t: int, v) -> int:
+    """The widened 64-bit pattern of a fixed-width key (the inverse of _decode_fixed)."""
+    if t == N.FLOAT64:
+        return struct.unpack("<Q", struct.pack("<d", v))[0]
+    if t == N.FLOAT32:
+        return struct.unpack("<I", struct.pack("<f", v))[0]
+    if t == N.BOOL:
+        return 1 if v else 0
+    return int(v) & 0xFFFFFFFFFFFFFFFF
 
 
 def _decode_fixed(t: int, v: int):
@@ -525,8 +571,8 @@ def _fold_null_group(frequencies, dtype: int, k: int):
     na.fill("NullValue") (Histogram.scala:59-66) makes them one group with any real "NullValue"
     string, so that group's count is the sum of both (dq_freq_null_literal) and it is placed by
     that count among the device top-N (ties in any order, like rdd.top)."""
-    nullg, lit = frequencies.null_literal()
     raw = frequencies.topk(k + 2)  # up to two raw entries fold into one
+    nullg, lit = frequencies.null_literal()  # (after topk: the same finalize serves both)
     top = []
     for (key,), c in raw:
         if key is None or (dtype == N.UTF8 and key == NULL_FIELD_REPLACEMENT):
@@ -559,9 +605,23 @@ class HistogramState(FrequenciesAndNumRows):
             out[s] = out.get(s, 0) + cnt
         return out
 
+    def as_string_table(self) -> "HistogramState":
+        """The same state keyed by the cast-to-string values, NULL -> "NullValue" (the reference's
+        own state: a persisted Histogram state loads back like this)."""
+        if self.dtype == N.UTF8 and self.binning_udf is None:
+            return self
+        groups = [((k,), c) for k, c in self.string_groups().items()]
+        col = self.frequencies.key_columns[0]
+        ft = FrequencyTable.from_groups([col], [N.UTF8], self.frequencies.device, groups,
+                                        self.frequencies.num_rows, null_as_group=True)
+        return HistogramState(ft, self.num_rows, N.UTF8, None)
+
     def sum(self, other):
-        return HistogramState(self.frequencies.merged(other.frequencies),
-                              self.num_rows + other.num_rows, self.dtype, self.binning_udf)
+        a, b = self, other
+        if a.dtype != b.dtype or (a.binning_udf is None) != (b.binning_udf is None):
+            a, b = a.as_string_table(), b.as_string_table()  # e.g. one side loaded from disk
+        return HistogramState(a.frequencies.merged(b.frequencies),
+                              a.num_rows + b.num_rows, a.dtype, a.binning_udf)
 
 
 @dataclass(frozen=True)

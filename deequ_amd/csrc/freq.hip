@@ -56,7 +56,7 @@ constexpr int kHistRow = kBuckets + 1;  // u16 exclusive bucket prefix of a chun
 constexpr int kThreads = 1024;
 constexpr int kMaxSubBits = 10;
 constexpr int kFilterShift = 32;        // hash bits that split an overflowing partition
-constexpr int kCand = 4;                // top groups kept per partition for Histogram
+constexpr int kCand = 2;                // top groups kept per partition for Histogram
 constexpr int kSmallCounts = 64;        // phase C histograms group counts below this
 constexpr int kMaxParts = 64;
 constexpr uint64_t kEmptyKey = ~0ULL;
@@ -950,30 +950,30 @@ DQ_DEV bool enc_is_null_literal(const uint8_t* p) {
          e[3] == (uint32_t)(kNullValueLo >> 32) && e[4] == kNullValueHi;
 }
 
-constexpr int kPF = 2;        // records per thread loaded ahead
 constexpr int kCThreads = 512;  // phase-C workgroup: two per CU by LDS, 128 VGPRs per lane
+// records per thread loaded ahead: exact partitions (~kTarget records) arrive whole
+template <bool HASHED>
+constexpr int kPF = HASHED ? 2 : 4;
 
+// A work item and the raw words of its first kPF * kCThreads records (decoded at insert time,
+// so the prefetch holds one word per exact record).
 template <bool HASHED>
 struct CItem {
   uint32_t p, f, fv;
   uint64_t r0, r1;
-  uint64_t h[kPF], c[kPF], rep[kPF];
-  uint32_t pending;
+  uint64_t w[kPF<HASHED>][FM<HASHED>::kRB / 8];
+  uint32_t valid;
 };
 
 template <bool HASHED>
-DQ_DEV void c_decode(const CArgs& a, const uint64_t* src, uint64_t li, uint32_t b, uint64_t& h,
-                     uint64_t& c, uint64_t& rep) {
-  constexpr int W = FM<HASHED>::kRB / 8;
+DQ_DEV void c_decode(const uint64_t* w, uint32_t b, uint64_t& h, uint64_t& c, uint64_t& rep) {
   if constexpr (HASHED) {
-    h = src[li * W];
-    const uint64_t rc = src[li * W + 1];
-    c = code_count((uint32_t)(rc & 0xff));
-    rep = rc >> 8;
+    h = w[0];
+    c = code_count((uint32_t)(w[1] & 0xff));
+    rep = w[1] >> 8;
   } else {
-    const uint64_t r = src[li];
-    h = xrec_h(r, b);
-    c = code_count((uint32_t)(r & 0xff));
+    h = xrec_h(w[0], b);
+    c = code_count((uint32_t)(w[0] & 0xff));
     rep = 0;
   }
 }
@@ -982,7 +982,7 @@ DQ_DEV void c_decode(const CArgs& a, const uint64_t* src, uint64_t li, uint32_t 
 template <bool HASHED>
 DQ_DEV void c_fetch(const CArgs& a, int wi, CItem<HASHED>& it) {
   constexpr int W = FM<HASHED>::kRB / 8;
-  it.pending = 0;
+  it.valid = 0;
   if (wi >= a.n_work) return;
   it.f = it.fv = 0;
   if (a.entries) {
@@ -995,17 +995,17 @@ DQ_DEV void c_fetch(const CArgs& a, int wi, CItem<HASHED>& it) {
   }
   it.r0 = a.part_base[it.p];
   it.r1 = a.part_base[it.p + 1];
-  const uint32_t b = it.p >> a.s;
   const uint64_t n = it.r1 - it.r0;
   const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + it.r0 * W;
-  const uint32_t fmask = (1u << it.f) - 1u;
 #pragma unroll
-  for (int q = 0; q < kPF; ++q) {
+  for (int q = 0; q < kPF<HASHED>; ++q) {
     const uint64_t li = (uint64_t)q * kCThreads + threadIdx.x;
-    it.h[q] = it.c[q] = it.rep[q] = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) it.w[q][k] = 0;
     if (li < n) {
-      c_decode<HASHED>(a, src, li, b, it.h[q], it.c[q], it.rep[q]);
-      if (it.f == 0 || ((uint32_t)(it.h[q] >> kFilterShift) & fmask) == it.fv) it.pending |= 1u << q;
+#pragma unroll
+      for (int k = 0; k < W; ++k) it.w[q][k] = src[li * W + k];
+      it.valid |= 1u << q;
     }
   }
 }
@@ -1016,7 +1016,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
   constexpr int KT = M::kTableC, W = M::kRB / 8;
   __shared__ uint64_t tkey[KT], tcnt[KT];
   __shared__ uint64_t trep[HASHED ? KT : 1];
-  __shared__ uint32_t s_wave[kCThreads / 64];
+  __shared__ uint32_t s_wg[kCThreads / 64], s_wc[kCThreads / 64];
   __shared__ uint64_t s_red[kCThreads / 64];
   __shared__ double s_redf[kCThreads / 64];
   __shared__ uint32_t s_ovf;
@@ -1099,56 +1099,65 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       s_ovf = 1;  // table full
       return true;
     };
-    auto insert_all = [&](uint64_t* h, uint64_t* c, uint64_t* rep, uint32_t pending) {
+    constexpr int PF = kPF<HASHED>;
+    // decodes the valid records of w[PF][W] (raw words) and inserts those of this item's hash
+    // subset
+    auto insert_all = [&](uint64_t (*w)[W], uint32_t valid) {
+      uint32_t pending = 0;
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        if (!((valid >> q) & 1u)) continue;
+        uint64_t h, c, rep;
+        c_decode<HASHED>(w[q], b, h, c, rep);
+        if (f == 0 || ((uint32_t)(h >> kFilterShift) & fmask) == fv) pending |= 1u << q;
+      }
       if constexpr (HASHED) {
         while (__syncthreads_or(pending ? 1 : 0)) {
 #pragma unroll
-          for (int q = 0; q < kPF; ++q)
-            if ((pending >> q) & 1u)
-              if (insert(h[q], c[q], rep[q])) pending &= ~(1u << q);
+          for (int q = 0; q < PF; ++q) {
+            if (!((pending >> q) & 1u)) continue;
+            uint64_t h, c, rep;
+            c_decode<HASHED>(w[q], b, h, c, rep);
+            if (insert(h, c, rep)) pending &= ~(1u << q);
+          }
         }
       } else {
 #pragma unroll
-        for (int q = 0; q < kPF; ++q)
-          if ((pending >> q) & 1u) insert(h[q], c[q], rep[q]);
+        for (int q = 0; q < PF; ++q) {
+          if (!((pending >> q) & 1u)) continue;
+          uint64_t h, c, rep;
+          c_decode<HASHED>(w[q], b, h, c, rep);
+          insert(h, c, rep);
+        }
         __syncthreads();
       }
     };
     // the prefetched first records, then the rest of a long partition
-    insert_all(cur.h, cur.c, cur.rep, cur.pending);
+    insert_all(cur.w, cur.valid);
     const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + r0 * W;
-    for (uint64_t base = (uint64_t)kPF * kCThreads; base < nrec; base += (uint64_t)kPF * kCThreads) {
-      uint64_t h[kPF], c[kPF], rep[kPF];
-      uint32_t pending = 0;
+    for (uint64_t base = (uint64_t)PF * kCThreads; base < nrec; base += (uint64_t)PF * kCThreads) {
+      uint64_t w[PF][W];
+      uint32_t valid = 0;
       const bool go = !s_ovf;
 #pragma unroll
-      for (int q = 0; q < kPF; ++q) {
+      for (int q = 0; q < PF; ++q) {
         const uint64_t li = base + (uint64_t)q * kCThreads + tid;
-        h[q] = c[q] = rep[q] = 0;
+#pragma unroll
+        for (int k = 0; k < W; ++k) w[q][k] = 0;
         if (li < nrec && go) {
-          c_decode<HASHED>(a, src, li, b, h[q], c[q], rep[q]);
-          if (f == 0 || ((uint32_t)(h[q] >> kFilterShift) & fmask) == fv) pending |= 1u << q;
+#pragma unroll
+          for (int k = 0; k < W; ++k) w[q][k] = src[li * W + k];
+          valid |= 1u << q;
         }
       }
-      insert_all(h, c, rep, pending);
+      insert_all(w, valid);
     }
     // next work item's first records: in flight while this one is reduced
     c_fetch<HASHED>(a, wi + gridDim.x, cur);
-    uint32_t all_claims;
-    block_excl_scan(claims, s_wave, all_claims);
-    if (tid == 0 && all_claims > (uint32_t)(KT * 7 / 8)) s_ovf = 1;  // too full: recount
-    __syncthreads();
-    if (s_ovf) {
-      if (tid == 0) {
-        const unsigned int q = atomicAdd(a.ovf_n, 2u);
-        a.ovf_out[q] = FEntry{p, f + 1, fv, 0};
-        a.ovf_out[q + 1] = FEntry{p, f + 1, fv | (1u << f), 0};
-      }
-      __syncthreads();
-      continue;
-    }
     // statistics; the entropy term -p ln p depends on the count alone, so small counts are
-    // histogrammed and each distinct one takes ONE log (unique keys: one per partition)
+    // histogrammed and each distinct one takes ONE log (unique keys: one per partition).  The
+    // table-load check, #groups, Σ[c==1] and the groups' output offsets come out of ONE exchange of
+    // per-wave sums (one barrier), the entropy out of a second; both in a fixed order.
     uint32_t g = 0;
     uint64_t un = 0;
     double e = 0.0;
@@ -1174,14 +1183,50 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       else if (c < kSmallCounts) atomicAdd(&s_chist[c], 1u);
       else e += term(c);
     }
-    uint32_t gtot;
-    const uint32_t gex = block_excl_scan(g, s_wave, gtot);  // (its barriers order s_chist too)
-    const uint64_t utot = block_sum_u64(un, s_red);
+    const int lane = __lane_id(), wave = tid >> 6;
+    constexpr int NW = kCThreads / 64;
+    uint32_t gin = g;  // inclusive prefix of g over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(gin, o);
+      if (lane >= o) gin += y;
+    }
+    const uint32_t wclaims = wave_sum(claims);
+    const uint64_t wun = wave_sum(un);
+    if (lane == 63) {
+      s_wg[wave] = gin;
+      s_wc[wave] = wclaims;
+      s_red[wave] = wun;
+    }
+    __syncthreads();
+    uint32_t gtot = 0, gex = gin - g, all_claims = 0;
+    uint64_t utot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      gtot += s_wg[w];
+      if (w < wave) gex += s_wg[w];
+      all_claims += s_wc[w];
+      utot += s_red[w];
+    }
+    if (s_ovf || all_claims > (uint32_t)(KT * 7 / 8)) {  // too full: recount (block-uniform)
+      if (tid == 0) {
+        const unsigned int q = atomicAdd(a.ovf_n, 2u);
+        a.ovf_out[q] = FEntry{p, f + 1, fv, 0};
+        a.ovf_out[q + 1] = FEntry{p, f + 1, fv | (1u << f), 0};
+      }
+      __syncthreads();
+      continue;
+    }
     if (tid > 1 && tid < kSmallCounts && s_chist[tid]) e += (double)s_chist[tid] * term(tid);
     if (tid == 0 && utot) e += (double)utot * term(1);
-    const double etot = block_sum_f64(e, s_redf);
+    e = wave_sum(e);
+    if (lane == 0) s_redf[wave] = e;
+    __syncthreads();
     const bool sub = f != 0;  // a recount subset: several work items add to one partition
     if (tid == 0) {
+      double etot = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) etot += s_redf[w];
       if (a.groups) {
         a.part_off[p] = r0;
         s_gbase = sub ? atomicAdd(&a.part_groups[p], (unsigned long long)gtot) : 0ULL;
@@ -1235,7 +1280,6 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
         if (tkey[sl] != kEmptyKey) offer(tcnt[sl], sl);
       if (tid == 0 && s_spec_cnt) offer(s_spec_cnt, KT);  // KT stands for the special cell
       // wave: kCand rounds of max over the lanes' heads
-      const int lane = __lane_id(), wave = tid >> 6;
 #pragma unroll
       for (int r = 0; r < kCand; ++r) {
         uint64_t best = tc[0];
@@ -2459,6 +2503,68 @@ extern "C" dq_status dq_freq_export(dq_freq* f, int64_t* counts_out, int64_t* ke
   offs.push_back((int64_t)bytes.size());
   return copy_out(counts, offs, bytes, counts_out, key_offsets_out, key_bytes_out, capacity,
                   key_bytes_capacity, key_bytes_needed);
+}
+
+// The inverse of dq_freq_export (a persisted frequency state loaded back, StateProvider.scala:
+// 231-237, 270-278): each group becomes one record -- exact mode: the widened value; hashed mode:
+// the encoded key's row hash (enc_hash, the value the row path computes) with the key in the
+// var bytes -- and goes through the records path of the repartition.  A one-key group with tag
+// 0 is the NULL group of a Histogram table.
+extern "C" dq_status dq_freq_import(dq_freq* f, const int64_t* counts, const int64_t* key_offsets,
+                                    const uint8_t* key_bytes, int64_t n_groups, int64_t num_rows,
+                                    int64_t null_key_rows, int null_as_group, void* hip_stream) {
+  if (!f || n_groups < 0 || num_rows < 0 || null_key_rows < 0)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "bad arguments");
+  if (n_groups && (!counts || !key_offsets || !key_bytes))
+    return fail(DQ_ERR_INVALID_ARGUMENT, "null group buffers");
+  std::vector<RecIn> rec;
+  std::vector<uint8_t> var;
+  rec.reserve((size_t)n_groups);
+  int64_t special[3] = {0, 0, null_key_rows};
+  const int64_t total = n_groups ? key_offsets[n_groups] : 0;
+  for (int64_t g = 0; g < n_groups; ++g) {
+    const int64_t o0 = key_offsets[g], o1 = key_offsets[g + 1];
+    if (o0 < 0 || o1 < o0 || o1 > total || (o0 & 3) || (o1 - o0) < 4)
+      return fail(DQ_ERR_INVALID_ARGUMENT, "bad key offsets at group %lld", (long long)g);
+    if (counts[g] <= 0) return fail(DQ_ERR_INVALID_ARGUMENT, "group %lld has count <= 0", (long long)g);
+    const uint32_t* enc = reinterpret_cast<const uint32_t*>(key_bytes + o0);
+    const int64_t sz = (int64_t)enc_size(enc, f->types.data(), f->n_keys);
+    if (sz != o1 - o0) return fail(DQ_ERR_INVALID_ARGUMENT, "group %lld: malformed key", (long long)g);
+    if (f->n_keys == 1 && enc[0] == 0) {  // the NULL group (Histogram tables only)
+      if (!null_as_group) return fail(DQ_ERR_INVALID_ARGUMENT, "NULL key outside a Histogram table");
+      special[1] += counts[g];
+      continue;
+    }
+    RecIn r;
+    r.count = (uint64_t)counts[g];
+    if (f->exact) {
+      r.key = (uint64_t)enc[1] | ((uint64_t)enc[2] << 32);
+      r.enc_off = 0;
+    } else {
+      r.key = enc_hash(enc, f->types.data(), f->n_keys);
+      r.enc_off = var.size();
+      var.insert(var.end(), key_bytes + o0, key_bytes + o1);
+      var.resize((var.size() + 7) & ~(size_t)7, 0);
+    }
+    rec.push_back(r);
+  }
+  HIP_TRY(hipSetDevice(f->device));
+  hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+  DevBuf<RecIn> drec;
+  DevBuf<uint8_t> dvar;
+  HIP_TRY(drec.ensure(std::max<size_t>(rec.size(), 1)));
+  HIP_TRY(dvar.ensure(std::max<size_t>(var.size(), 8)));
+  if (!rec.empty())
+    HIP_TRY(hipMemcpyAsync(drec.p, rec.data(), rec.size() * sizeof(RecIn), hipMemcpyHostToDevice, st));
+  if (!var.empty()) HIP_TRY(hipMemcpyAsync(dvar.p, var.data(), var.size(), hipMemcpyHostToDevice, st));
+  const int64_t rc[1] = {(int64_t)rec.size()};
+  const int64_t vb[1] = {(int64_t)var.size()};
+  dq_status s = dq_freq_add_records_device(f, reinterpret_cast<const dq_freq_record*>(drec.p),
+                                           dvar.p, 1, rc, vb, num_rows, special, null_as_group,
+                                           hip_stream);
+  if (s != DQ_OK) return s;
+  HIP_TRY(hipStreamSynchronize(st));  // the staging buffers die here
+  return DQ_OK;
 }
 
 // Histogram's details: rdd.top(maxDetailBins)(OrderByAbsoluteCount) (Histogram.scala:78).

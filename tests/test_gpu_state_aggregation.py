@@ -123,3 +123,48 @@ def test_saved_partition_states_run_on_aggregated_states(gpu_device):
     direct = AnalysisRunner.run(whole, analysis)
     for a in analysis.analyzers:
         assert _same(_value(agg.metric(a)), _value(direct.metric(a))), str(a)
+
+
+def test_states_persisted_to_disk_run_on_aggregated_states(gpu_device, tmp_path):
+    """The same with HdfsStateProvider (StateProvider.scala:71-294, StateProviderTest.scala
+    "restore their state from the filesystem"): every partition's states go through the
+    reference's on-disk layouts -- big-endian .bin files, frequency tables as Parquet (Histogram's
+    cast to string) -- and load back into metrics equal to one run over the whole table."""
+    from deequ_amd.analyzers import HdfsStateProvider
+    from deequ_amd.runners import Analysis, AnalysisRunner
+    from deequ_amd.table import Table
+    t = _table(23, (0.1, 0.2, 0.0, 0.1, 0.05))
+    analysis = Analysis(_analyzers())
+    providers = []
+    for i, (lo, hi) in enumerate([(0, 1200), (1200, N_ROWS)]):
+        prov = HdfsStateProvider(str(tmp_path / f"part{i}"))
+        AnalysisRunner.run(Table.from_arrow(t.slice(lo, hi - lo), device=gpu_device), analysis,
+                           save_states_with=prov)
+        providers.append(prov)
+    whole = Table.from_arrow(t, device=gpu_device)
+    agg = AnalysisRunner.run_on_aggregated_states(whole.schema, analysis, providers)
+    direct = AnalysisRunner.run(whole, analysis)
+    for a in analysis.analyzers:
+        assert _same(_value(agg.metric(a)), _value(direct.metric(a))), str(a)
+
+
+def test_frequency_states_round_trip_through_parquet(gpu_device, tmp_path):
+    """persist -> load of FrequenciesAndNumRows / Histogram states: the loaded table holds the same
+    groups and numRows (assertCorrectlyRestoresFrequencyBasedState, StateProviderTest.scala)."""
+    from deequ_amd.analyzers import Entropy, HdfsStateProvider, Histogram, Uniqueness
+    from deequ_amd.table import Table
+    t = _table(29, (0.1, 0.2, 0.0, 0.0, 0.1))
+    data = Table.from_arrow(t, device=gpu_device)
+    prov = HdfsStateProvider(str(tmp_path / "st"))
+    for a in [Uniqueness(["item"]), Uniqueness(["item", "count"]), Entropy("value"),
+              Histogram("value"), Histogram("count")]:
+        st = a.compute_state_from(data)
+        prov.persist(a, st)
+        back = prov.load(a)
+        assert back.num_rows == st.num_rows, str(a)
+        if isinstance(a, Histogram):
+            assert back.string_groups() == st.string_groups(), str(a)
+            assert _same(_value(a.compute_metric_from(back)), _value(a.compute_metric_from(st)))
+        else:
+            assert dict(back.frequencies.export()) == dict(st.frequencies.export()), str(a)
+            assert _same(_value(a.compute_metric_from(back)), _value(a.compute_metric_from(st)))

@@ -7,8 +7,8 @@ configs[1], S10).  Not part of the driver's bench contract; the JSON lines land 
       groupings (+ the one aggregation over each frequency table, dq_freq_summarize) and the two
       Histogram group-bys (+ dq_freq_topk(1000) and the bin count), over the table resident in HBM.
       B_alg = key bytes read once per group-by (SURVEY §8(d)): id validity + values (8.125 B/row);
-      priority validity + offsets + bytes, x2 (grouping + histogram; id's Histogram table serves
-      its grouping, so id is read once).  Partition traffic excluded.
+      priority validity + offsets + bytes (each column's Histogram table serves its grouping, so
+      each column is read once).  Partition traffic excluded.
   c4: ApproxCountDistinct(id) (HLL++, P = 9) + Correlation(id, score) on an Item table with an
       fp64 `score` column.  One step = the fused scan (HLL launch + co-moment launch + finalize).
       B_alg = id validity + values + score validity + values = 16.25 B/row.
@@ -54,16 +54,15 @@ def main():
         # The group-bys AnalysisRunner plans for this suite (runners/__init__.py): Uniqueness/
         # Distinctness/Entropy share one grouping per column (AnalysisRunner.scala:165-180);
         # Histogram groups with NULL as a group (Histogram.scala:54-69) and takes the device
-        # top-1000 + the bin count.  For the int64 `id` one Histogram-mode table serves both (its
-        # keyed groups are the grouping: dq_freq_summarize_keys); `priority` has NULLs, so its
-        # grouping and its Histogram are two group-bys.  Tables are created once with their
-        # capacity and reset every step (the step still clears, inserts every row, aggregates).
-        # --runner times AnalysisRunner.do_analysis_run itself (tables allocated per run).
-        tables = {("id", True): FrequencyTable(["id"], [N.INT64], 0, capacity_hint=rows),
-                  ("priority", False): FrequencyTable(["priority"], [N.UTF8], 0),
-                  ("priority", True): FrequencyTable(["priority"], [N.UTF8], 0)}
+        # top-1000 + the bin count.  One Histogram-mode table per column serves both (its NULL
+        # rows are a group kept apart: the keyed groups are the grouping, dq_freq_summarize_keys,
+        # and Histogram folds the NULL group into "NullValue", _fold_null_group).  Tables are
+        # created once with their capacity and reset every step (the step still clears, inserts
+        # every row, aggregates).  --runner times AnalysisRunner.do_analysis_run itself.
+        tables = {"id": (FrequencyTable(["id"], [N.INT64], 0, capacity_hint=rows), N.INT64),
+                  "priority": (FrequencyTable(["priority"], [N.UTF8], 0), N.UTF8)}
         from deequ_amd.analyzers import Distinctness, Entropy, Histogram, Uniqueness
-        from deequ_amd.analyzers.grouping import KeyedFrequencies
+        from deequ_amd.analyzers.grouping import KeyedFrequencies, _fold_null_group
         from deequ_amd.runners import AnalysisRunner
         suite = [a for c in ("id", "priority")
                  for a in (Uniqueness([c]), Distinctness([c]), Entropy(c), Histogram(c))]
@@ -71,24 +70,22 @@ def main():
         def step():
             if args.runner:
                 ctx = AnalysisRunner.do_analysis_run(table, suite)
-                return {str(a): ctx.metric(a).value for a in suite[:4]}
+                return {str(a): ctx.metric(a).value for a in suite}
             out = {}
-            for (col, hist), ft in tables.items():
+            for col, (ft, dtype) in tables.items():
                 ft.reset()
                 for b in table.batches:
-                    ft.add([b[col]], null_as_group=hist)
-                if hist:
-                    top = ft.topk(1000)
-                    out["Histogram(" + col + ")"] = (ft.count(), len(top), top[0][1])
-                if col == "id" or not hist:
-                    s = (KeyedFrequencies(ft) if hist else ft).summarize()
-                    out[col] = (s.n_groups, s.n_unique, s.entropy)
+                    ft.add([b[col]], null_as_group=True)
+                top, bins = _fold_null_group(ft, dtype, 1000)
+                out["Histogram(" + col + ")"] = (bins, len(top), top[0])
+                s = KeyedFrequencies(ft).summarize()
+                out[col] = (s.n_groups, s.n_unique, s.entropy)
             return out
         b_alg = 0
         for b in table.batches:
             m = b["id"].length
-            # each group-by reads its key column once: id once, priority twice
-            b_alg += nb(m) + 8 * m + 2 * (nb(m) + 4 * (m + 1) + int(b["priority"].values[m].item()))
+            # each group-by reads its key column once
+            b_alg += nb(m) + 8 * m + (nb(m) + 4 * (m + 1) + int(b["priority"].values[m].item()))
         kernel = ("dq::freq_phaseA (per batch) + freq_phaseB + freq_phaseC (per table): "
                   "radix-partitioned group-by")
         desc = ("Uniqueness/Distinctness/Entropy grouping + Histogram (top-1000 + bins) on int64 id "
