@@ -393,6 +393,17 @@ dq_status dq_freq_add_records_device(dq_freq* freq, const dq_freq_record* record
                                      const int64_t* src_var_bytes, int64_t num_rows,
                                      const int64_t* special, int null_as_group, void* hip_stream);
 
+/* Spark 2.2 Cast(StringType -> LongType | DoubleType) of a utf8 column, on the device: the
+ * ColumnProfiler's cast of string columns inferred numeric (profiles/ColumnProfiler.scala:311-320,
+ * 389-405).  to_type DQ_INT64 follows UTF8String.toLong (sign, digits, '.' + digits truncated);
+ * DQ_FLOAT64 follows java.lang.Double.parseDouble over decimal strings.  A string that does not
+ * convert is NULL in validity_out (LSB-first, (length + 7) / 8 bytes); values_out holds length
+ * int64 / double.  *n_unsupported counts strings parseDouble would read that are not converted
+ * here exactly (exponents, NaN/Infinity, hex, > 19 significant digits ...): those rows are NULL and
+ * the caller must treat a non-zero count as a failure.  Synchronises `hip_stream`. */
+dq_status dq_cast_utf8(const dq_column* in, int to_type, void* values_out, uint8_t* validity_out,
+                       int64_t* n_unsupported, void* hip_stream);
+
 /* ------------------------------------------------------------------------------------------------
  * Columnar handoff: host-resident Arrow batches -> HBM (the JNI shim's entry).
  *
