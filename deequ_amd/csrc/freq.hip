@@ -624,8 +624,15 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
       uint32_t hits = 0;
       retry(~0u, hits);
     }
-    __syncthreads();
+    const bool any_raw = __syncthreads_or(raw ? 1 : 0);
     mark(t, 2);
+    if (!any_raw) {  // every row collapsed into the dedupe table: an empty chunk, no sort
+      uint16_t* hrow = a.hist + t * kHistRow;
+      for (int i = tid; i < kHistRow; i += kThreads) hrow[i] = 0;
+      mark(t, 3);
+      mark(t, 4);
+      continue;
+    }
     uint64_t need = 0;
     if constexpr (HASHED && !FROM_REC) {
 #pragma unroll 1

@@ -150,3 +150,29 @@ def _to_list(col, dt):
     v = col.values.cpu().numpy().view(dt)[: col.length]
     bits = np.unpackbits(col.validity.cpu().numpy(), bitorder="little")[: col.length]
     return [x.item() if b else None for x, b in zip(v, bits)]
+
+
+def test_success_metrics_json_known_answer(gpu_device):
+    """SimpleResultSerdeTest (T/repository/AnalysisResultSerdeTest.scala:176-222): the success
+    metrics of an analysis over getDfFull as JSON rows with the dataset date and the tag."""
+    import json
+    from deequ_amd.analyzers import Completeness, Distinctness, MutualInformation, Size, Uniqueness
+    from deequ_amd.repository import AnalysisResult, ResultKey, success_metrics_as_json
+    from deequ_amd.runners import Analysis
+    from deequ_amd.table import Table
+    df = Table.from_pydict({"item": ["1", "2", "3", "4"], "att1": ["a", "a", "a", "b"],
+                            "att2": ["c", "c", "c", "d"]},
+                           {"item": "string", "att1": "string", "att2": "string"}, device=gpu_device)
+    ctx = Analysis([Size(), Distinctness("item"), Completeness("att1"), Uniqueness("att1"),
+                    Distinctness("att1"), Completeness("att2"), Uniqueness("att2"),
+                    MutualInformation("att1", "att2")]).run(df)
+    got = json.loads(success_metrics_as_json(AnalysisResult(ResultKey(1507975810, {"Region": "EU"}),
+                                                             ctx)))
+    exp = [("Column", "att2", "Completeness", 1.0), ("Column", "att1", "Completeness", 1.0),
+           ("Column", "att2", "Uniqueness", 0.25), ("Column", "item", "Distinctness", 1.0),
+           ("Dataset", "*", "Size", 4.0), ("Column", "att1", "Uniqueness", 0.25),
+           ("Column", "att1", "Distinctness", 0.5),
+           ("Mutlicolumn", "att1,att2", "MutualInformation", 0.5623351446188083)]
+    want = sorted({"dataset_date": 1507975810, "entity": e, "region": "EU", "instance": i,
+                   "name": n, "value": v}.items() for e, i, n, v in exp)
+    assert sorted(sorted(r.items()) for r in got) == sorted(sorted(w) for w in want)
