@@ -100,6 +100,7 @@ def murmur3_string_hash(s: str, seed: int) -> int:
 # sample, big-endian (java.nio.ByteBuffer), of the compressed summary.
 # ------------------------------------------------------------------------------------------------
 COMPRESS_THRESHOLD = 10000  # QuantileSummaries.defaultCompressThreshold
+COUNT_COL = "com_amazon_deequ_dq_metrics_count"  # Analyzers.COUNT_COL (Analyzer.scala:338-339)
 
 
 def digest_to_bytes(summaries) -> bytes:
@@ -218,7 +219,12 @@ class HdfsStateProvider(StateLoader, StatePersister):
             arrays = [pa.array([k[i] for k, _ in groups], type=_ARROW[t])
                       for i, t in enumerate(state.frequencies.key_types)]
             counts = [c for _, c in groups]
-        table = pa.table(arrays + [pa.array(counts, type=pa.int64())], names=cols + ["count"])
+        # the frequency DataFrame's count column: Analyzers.COUNT_COL for a grouping
+        # (GroupingAnalyzers.scala:71), Spark's `.count()` for Histogram (Histogram.scala:66)
+        count_col = "count" if isinstance(state, G.HistogramState) else COUNT_COL
+        if count_col in cols:  # Spark's Parquet writer refuses duplicate column names
+            raise ValueError(f"Found duplicate column(s) in the data schema: `{count_col}`")
+        table = pa.table(arrays + [pa.array(counts, type=pa.int64())], names=cols + [count_col])
         os.makedirs(path)
         pq.write_table(table, os.path.join(path, "part-00000.snappy.parquet"), compression="snappy")
         open(os.path.join(path, "_SUCCESS"), "wb").close()
@@ -274,11 +280,12 @@ class HdfsStateProvider(StateLoader, StatePersister):
         from .. import _native as N
         (num_rows,) = struct.unpack(">q", self._read(self._path(ident, "-num_rows.bin"))[:8])
         table = pq.read_table(self._path(ident, "-frequencies.pqt"))
-        names = [n for n in table.column_names if n != "count"]
+        hist = isinstance(analyzer, G.Histogram)
+        count_col = "count" if hist else COUNT_COL
+        names = [n for n in table.column_names if n != count_col]
         types = [_from_arrow(table.schema.field(n).type) for n in names]
         keys = list(zip(*[table.column(n).to_pylist() for n in names])) if names else []
-        counts = table.column("count").to_pylist()
-        hist = isinstance(analyzer, G.Histogram)
+        counts = table.column(count_col).to_pylist()
         ft = G.FrequencyTable.from_groups(names, types, self.device, list(zip(keys, counts)),
                                           num_rows=num_rows, null_as_group=hist)
         if hist:
