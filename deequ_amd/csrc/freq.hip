@@ -254,7 +254,9 @@ struct AKeys {
   static constexpr int kMinWaves = HASHED && !FROM_REC ? 4 : 1;  // per SIMD: two workgroups
 };
 
-template <bool HASHED, bool FROM_REC>
+// STR1: the key is one utf8 column (its own instantiation: the generic multi-column path would
+// otherwise hold registers the string path needs, and spill)
+template <bool HASHED, bool FROM_REC, bool STR1 = false>
 __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
                                   (AKeys<HASHED, FROM_REC>::kMinWaves)) freq_phaseA(AArgs a) {
   constexpr int kThreads = AKeys<HASHED, FROM_REC>::kThreads;
@@ -291,7 +293,11 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
   if (tid == 0) s_bypass = 0;
   unsigned long long nulls = 0, nullg = 0;
-  unsigned long long dbg_nr = 0, dbg_diff = 0, dbg_full = 0, dbg_bypass = 0;
+  // debug event counts (rare events) in LDS: dedupe is an out-of-line lambda, and locals it
+  // updated through its captures lived in scratch
+  __shared__ uint32_t s_dbg[3];  // not-ready retries, hash collisions, table full
+  if (tid < 3) s_dbg[tid] = 0;
+  unsigned long long dbg_bypass = 0;
 
   // Counting sort of a chunk's records: bucket counts are in bh; begin_chunk scans them, writes
   // the chunk's histogram row and reserves the chunk's arena bytes; records then go straight to
@@ -339,7 +345,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   };
   // LDS dedupe: 0 = not counted (table full), 1 = claimed a new slot, 2 = added to an existing
   // slot, 3 = the key's slot is being claimed: retry after the next barrier
-  const bool one_str = a.ks.n_keys == 1 && a.ks.cols[0].type == DQ_UTF8;  // block-uniform
+  static_assert(!STR1 || (HASHED && !FROM_REC), "STR1 is the row path of a utf8 key");
   auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep, uint64_t k0, uint64_t k1) -> int {
     if (h == kEmptyKey) return 0;
     uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
@@ -366,7 +372,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         if constexpr (HASHED) {
           const uint64_t r2 = lds_load(&drep[slot]);
           if (r2 == kNotReady) {  // being claimed right now (another lane / wave)
-            dbg_nr++;
+            atomicAdd(&s_dbg[0], 1u);
             return 3;
           }
           if (r2 != rep) {
@@ -380,7 +386,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
             else
               same = rows_equal(a.ks, (int64_t)r2, (int64_t)rep);
           }
-          if (!same) dbg_diff++;
+          if (!same) atomicAdd(&s_dbg[1], 1u);
         }
         if (same) {
           atomicAdd((unsigned long long*)&dcnt[slot], c);
@@ -389,7 +395,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
       }
       slot = (slot + 1) & (D - 1);
     }
-    dbg_full++;
+    atomicAdd(&s_dbg[2], 1u);
     return 0;
   };
 
@@ -462,13 +468,13 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         if ((vb >> j) & 1u) {
           keyed |= 1u << j;
           stash[(j * kThreads + tid) * W] = fmix_bij(exact_canon(a.ks, v[j]));
-        } else if (a.ks.null_as_group) {
-          ++nullg;
         } else {
-          ++nulls;
+          const unsigned long long ng = a.ks.null_as_group ? 1ULL : 0ULL;
+          nullg += ng;
+          nulls += 1ULL - ng;
         }
       }
-    } else if (one_str) {  // one utf8 column: offsets, then <= 16 bytes per row, then hash
+    } else if constexpr (STR1) {  // one utf8 column: offsets, then <= 16 bytes per row, then hash
       const KeyCol& c = a.ks.cols[0];
       const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
       int64_t ic[ROUNDS];
@@ -529,14 +535,15 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
           } else {
             h = str_row_hash(SView{c.data + s0[j], len[j]});
           }
-        } else if (a.ks.null_as_group) {
-          // Histogram: the NULL rows are one group kept apart (C_NULL_GROUP), so this table also
-          // serves the column's grouping; the caller folds it into the "NullValue" string group
-          // (Histogram.scala:59-66) with the literal's count from phase C (dq_freq_null_literal)
-          ++nullg;
-          continue;
         } else {
-          ++nulls;
+          // a NULL row.  Histogram: the NULL rows are one group kept apart (C_NULL_GROUP), so
+          // this table also serves the column's grouping; the caller folds it into the
+          // "NullValue" string group (Histogram.scala:59-66) with the literal's count from phase
+          // C (dq_freq_null_literal).  (Counted without a branch: selecting between the two
+          // counters made the compiler address them in scratch.)
+          const unsigned long long ng = a.ks.null_as_group ? 1ULL : 0ULL;
+          nullg += ng;
+          nulls += 1ULL - ng;
           continue;
         }
         keyed |= 1u << j;
@@ -676,9 +683,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     wave_count(&a.counters[C_NULL_ROWS], nulls);
     wave_count(&a.counters[C_NULL_GROUP], nullg);
   }
-  wave_count(&a.counters[C_DBG_NOTREADY], dbg_nr);
-  wave_count(&a.counters[C_DBG_DIFF], dbg_diff);
-  wave_count(&a.counters[C_DBG_FULL], dbg_full);
+  __syncthreads();
+  if (tid < 3 && s_dbg[tid]) atomicAdd(&a.counters[C_DBG_NOTREADY + tid], (unsigned long long)s_dbg[tid]);
   wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
 }
 
@@ -985,23 +991,38 @@ DQ_DEV void c_decode(const uint64_t* w, uint32_t b, uint64_t& h, uint64_t& c, ui
   }
 }
 
-// Work item wi: its partition / subset and the first kPF * kCThreads of its records.
+// A work item's partition / hash subset and its record range, loaded one item ahead of its
+// records (so fetching the records of the next item is one HBM round trip, not two).
+struct CBounds {
+  uint32_t p, f, fv;
+  uint64_t r0, r1;
+};
+DQ_DEV void c_bounds(const CArgs& a, int wi, CBounds& bd) {
+  if (wi >= a.n_work) return;
+  bd.f = bd.fv = 0;
+  if (a.entries) {
+    const FEntry e = a.entries[wi];
+    bd.p = e.p;
+    bd.f = e.f;
+    bd.fv = e.v;
+  } else {
+    bd.p = (uint32_t)wi;
+  }
+  bd.r0 = a.part_base[bd.p];
+  bd.r1 = a.part_base[bd.p + 1];
+}
+
+// Work item wi (bounds bd): the raw words of its first kPF * kCThreads records.
 template <bool HASHED>
-DQ_DEV void c_fetch(const CArgs& a, int wi, CItem<HASHED>& it) {
+DQ_DEV void c_fetch(const CArgs& a, int wi, const CBounds& bd, CItem<HASHED>& it) {
   constexpr int W = FM<HASHED>::kRB / 8;
   it.valid = 0;
   if (wi >= a.n_work) return;
-  it.f = it.fv = 0;
-  if (a.entries) {
-    const FEntry e = a.entries[wi];
-    it.p = e.p;
-    it.f = e.f;
-    it.fv = e.v;
-  } else {
-    it.p = (uint32_t)wi;
-  }
-  it.r0 = a.part_base[it.p];
-  it.r1 = a.part_base[it.p + 1];
+  it.p = bd.p;
+  it.f = bd.f;
+  it.fv = bd.fv;
+  it.r0 = bd.r0;
+  it.r1 = bd.r1;
   const uint64_t n = it.r1 - it.r0;
   const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + it.r0 * W;
 #pragma unroll
@@ -1017,44 +1038,55 @@ DQ_DEV void c_fetch(const CArgs& a, int wi, CItem<HASHED>& it) {
   }
 }
 
+// Per work item: the inserts, then ONE pass over the LDS table that reads every slot once for
+// the statistics, the Histogram candidates (kept in registers) and the lit probe, and clears it
+// for the next item (when the groups are materialised, the output pass clears instead).  The
+// flags and the special cell the inserts update are double-buffered by item parity, so they are
+// reset for item i + 1 while item i runs, between two of its barriers: three barriers per item.
 template <bool HASHED>
 __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
   using M = FM<HASHED>;
-  constexpr int KT = M::kTableC, W = M::kRB / 8;
+  constexpr int KT = M::kTableC, W = M::kRB / 8, NW = kCThreads / 64;
   __shared__ uint64_t tkey[KT], tcnt[KT];
   __shared__ uint64_t trep[HASHED ? KT : 1];
-  __shared__ uint32_t s_wg[kCThreads / 64], s_wc[kCThreads / 64];
-  __shared__ uint64_t s_red[kCThreads / 64];
-  __shared__ double s_redf[kCThreads / 64];
-  __shared__ uint32_t s_ovf;
-  __shared__ unsigned long long s_spec_cnt, s_gbase;
-  __shared__ uint64_t s_spec_rep;
-  __shared__ uint32_t s_chist[kSmallCounts];
-  __shared__ uint64_t s_cc[kCThreads / 64 * kCand];
-  __shared__ int32_t s_cs[kCThreads / 64 * kCand];
+  __shared__ uint32_t s_wg[NW], s_wc[NW];
+  __shared__ uint64_t s_red[NW];
+  __shared__ double s_redf[NW];
+  __shared__ uint32_t s_ovf[2];
+  __shared__ unsigned long long s_spec_cnt[2], s_gbase;
+  __shared__ uint64_t s_spec_rep[2];
+  __shared__ uint32_t s_chist[2][kSmallCounts];
+  __shared__ uint64_t s_cc[NW * kCand], s_ck[NW * kCand], s_cr[NW * kCand];
 
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
   unsigned long long collisions = 0;
+  for (int i = tid; i < KT; i += kCThreads) {
+    tkey[i] = kEmptyKey;
+    tcnt[i] = 0;
+    if (HASHED) trep[i] = kNotReady;
+  }
+  if (tid < 2) {
+    s_ovf[tid] = 0;
+    s_spec_cnt[tid] = 0;
+    s_spec_rep[tid] = kNotReady;
+  }
+  if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
+  CBounds nb;
   CItem<HASHED> cur;
-  c_fetch<HASHED>(a, blockIdx.x, cur);
+  c_bounds(a, blockIdx.x, nb);
+  c_fetch<HASHED>(a, blockIdx.x, nb, cur);
+  c_bounds(a, blockIdx.x + gridDim.x, nb);
+  __syncthreads();
 
-  for (int wi = blockIdx.x; wi < a.n_work; wi += gridDim.x) {
-    for (int i = tid; i < KT; i += kCThreads) {
-      tkey[i] = kEmptyKey;
-      tcnt[i] = 0;
-      if (HASHED) trep[i] = kNotReady;
-    }
-    if (tid == 0) {
-      s_ovf = 0;
-      s_spec_cnt = 0;
-      s_spec_rep = kNotReady;
-    }
-    if (tid < kSmallCounts) s_chist[tid] = 0;
-    __syncthreads();
+  uint32_t par = 0;
+  for (int wi = blockIdx.x; wi < a.n_work; wi += gridDim.x, par ^= 1u) {
     const uint32_t p = cur.p, b = p >> a.s, f = cur.f, fv = cur.fv;
     const uint32_t fmask = (1u << f) - 1u;
     const uint64_t r0 = cur.r0, nrec = cur.r1 - cur.r0;
     uint32_t claims = 0;  // slots this thread claimed (load check after the inserts)
+    uint32_t* ovf = &s_ovf[par];
+    unsigned long long* spec_cnt = &s_spec_cnt[par];
+    uint64_t* spec_rep = &s_spec_rep[par];
 
     // Returns false when the record must wait: its group's slot is claimed but the claimer has
     // not published the representative yet (hashed mode).  Waiting is a retry after the next
@@ -1062,13 +1094,13 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     auto insert = [&](uint64_t h, uint64_t c, uint64_t rep) -> bool {
       if (h == kEmptyKey) {  // the table's empty marker: its own cell
         if constexpr (HASHED) {
-          const uint64_t prev = atomicCAS((unsigned long long*)&s_spec_rep, kNotReady, rep);
+          const uint64_t prev = atomicCAS((unsigned long long*)spec_rep, kNotReady, rep);
           if (prev != kNotReady && prev != rep &&
               !enc_equal(reinterpret_cast<const uint32_t*>(a.arena + prev),
                          reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys))
             ++collisions;
         }
-        atomicAdd(&s_spec_cnt, (unsigned long long)c);
+        atomicAdd(spec_cnt, (unsigned long long)c);
         return true;
       }
       uint32_t slot = HASHED ? (uint32_t)(((uint64_t)(uint32_t)h * KT) >> 32) : ((uint32_t)h & (KT - 1));
@@ -1103,12 +1135,12 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
         }
         slot = slot + 1 == (uint32_t)KT ? 0u : slot + 1;
       }
-      s_ovf = 1;  // table full
+      *ovf = 1;  // table full
       return true;
     };
     constexpr int PF = kPF<HASHED>;
     // decodes the valid records of w[PF][W] (raw words) and inserts those of this item's hash
-    // subset
+    // subset; ends with a block barrier
     auto insert_all = [&](uint64_t (*w)[W], uint32_t valid) {
       uint32_t pending = 0;
 #pragma unroll
@@ -1139,13 +1171,13 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
         __syncthreads();
       }
     };
-    // the prefetched first records, then the rest of a long partition
+    // the prefetched first records, then the rest of a long partition            [barrier 1]
     insert_all(cur.w, cur.valid);
     const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + r0 * W;
     for (uint64_t base = (uint64_t)PF * kCThreads; base < nrec; base += (uint64_t)PF * kCThreads) {
       uint64_t w[PF][W];
       uint32_t valid = 0;
-      const bool go = !s_ovf;
+      const bool go = !*ovf;
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
         const uint64_t li = base + (uint64_t)q * kCThreads + tid;
@@ -1159,39 +1191,74 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       }
       insert_all(w, valid);
     }
-    // next work item's first records: in flight while this one is reduced
-    c_fetch<HASHED>(a, wi + gridDim.x, cur);
-    // statistics; the entropy term -p ln p depends on the count alone, so small counts are
-    // histogrammed and each distinct one takes ONE log (unique keys: one per partition).  The
-    // table-load check, #groups, Σ[c==1] and the groups' output offsets come out of ONE exchange of
-    // per-wave sums (one barrier), the entropy out of a second; both in a fixed order.
+    // the table is final.  Next item's records (bounds already here) and the bounds after it are
+    // in flight while this one is reduced; the other parity's flags are reset for it.
+    c_fetch<HASHED>(a, wi + gridDim.x, nb, cur);
+    c_bounds(a, wi + 2 * gridDim.x, nb);
+    if (tid == 0) {
+      s_ovf[par ^ 1u] = 0;
+      s_spec_cnt[par ^ 1u] = 0;
+      s_spec_rep[par ^ 1u] = kNotReady;
+    }
+    if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
+    const bool overflow = *ovf != 0;
+    const uint64_t sc = *spec_cnt, sr = HASHED ? *spec_rep : 0;
+
+    // statistics: -p ln p depends on the count alone, so small counts are histogrammed and each
+    // distinct one takes ONE log (unique keys: one per partition)
+    const bool keep = a.groups != nullptr;  // the output pass reads the table, then clears it
+    const bool cand = a.want_cand && f == 0;
     uint32_t g = 0;
     uint64_t un = 0;
     double e = 0.0;
+    uint64_t tc[kCand], tk[kCand], tr[kCand];
+#pragma unroll
+    for (int q = 0; q < kCand; ++q) tc[q] = tk[q] = tr[q] = 0;
     auto term = [&](uint64_t c) {
       const double pr = (double)c / a.num_rows;
       return -pr * log(pr);
     };
-    for (int sl = tid; sl < KT; sl += kCThreads) {
-      if (tkey[sl] == kEmptyKey) continue;
-      const uint64_t c = tcnt[sl];
-      if constexpr (HASHED)
-        if (a.lit_count && tkey[sl] == a.lit_h && enc_is_null_literal(a.arena + trep[sl]))
-          atomicAdd(a.lit_count, (unsigned long long)c);
+    auto count_group = [&](uint64_t c) {
       ++g;
       if (c == 1) ++un;  // the common count: a register, not an LDS atomic on one address
-      else if (c < kSmallCounts) atomicAdd(&s_chist[c], 1u);
+      else if (c < kSmallCounts) atomicAdd(&s_chist[par][c], 1u);
       else e += term(c);
+    };
+    auto offer = [&](uint64_t c, uint64_t k, uint64_t r) {  // insertion, static indices
+#pragma unroll
+      for (int q = 0; q < kCand; ++q) {
+        if (c > tc[q]) {
+          const uint64_t c2 = tc[q], k2 = tk[q], r2 = tr[q];
+          tc[q] = c;
+          tk[q] = k;
+          tr[q] = r;
+          c = c2;
+          k = k2;
+          r = r2;
+        }
+      }
+    };
+    for (int sl = tid; sl < KT; sl += kCThreads) {
+      const uint64_t k = tkey[sl];
+      if (k == kEmptyKey) continue;
+      const uint64_t c = tcnt[sl];
+      const uint64_t r = HASHED ? trep[sl] : 0;
+      if (!keep) {
+        tkey[sl] = kEmptyKey;
+        tcnt[sl] = 0;
+        if (HASHED) trep[sl] = kNotReady;
+      }
+      if (overflow) continue;
+      if constexpr (HASHED)
+        if (a.lit_count && k == a.lit_h && enc_is_null_literal(a.arena + r))
+          atomicAdd(a.lit_count, (unsigned long long)c);
+      count_group(c);
+      if (cand) offer(c, k, r);
     }
-    if (tid == 0 && s_spec_cnt) {
-      const uint64_t c = s_spec_cnt;
-      ++g;
-      if (c == 1) ++un;
-      else if (c < kSmallCounts) atomicAdd(&s_chist[c], 1u);
-      else e += term(c);
+    if (tid == 0 && sc && !overflow) {
+      count_group(sc);
+      if (cand) offer(sc, kEmptyKey, sr);
     }
-    const int lane = __lane_id(), wave = tid >> 6;
-    constexpr int NW = kCThreads / 64;
     uint32_t gin = g;  // inclusive prefix of g over the wave
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1205,7 +1272,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       s_wc[wave] = wclaims;
       s_red[wave] = wun;
     }
-    __syncthreads();
+    __syncthreads();  //                                                            [barrier 2]
     uint32_t gtot = 0, gex = gin - g, all_claims = 0;
     uint64_t utot = 0;
 #pragma unroll
@@ -1215,78 +1282,29 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       all_claims += s_wc[w];
       utot += s_red[w];
     }
-    if (s_ovf || all_claims > (uint32_t)(KT * 7 / 8)) {  // too full: recount (block-uniform)
+    if (overflow || all_claims > (uint32_t)(KT * 7 / 8)) {  // too full: recount (block-uniform)
       if (tid == 0) {
         const unsigned int q = atomicAdd(a.ovf_n, 2u);
         a.ovf_out[q] = FEntry{p, f + 1, fv, 0};
         a.ovf_out[q + 1] = FEntry{p, f + 1, fv | (1u << f), 0};
       }
-      __syncthreads();
+      if (keep) {  // the output pass would have cleared the table
+        for (int sl = tid; sl < KT; sl += kCThreads) {
+          tkey[sl] = kEmptyKey;
+          tcnt[sl] = 0;
+          if (HASHED) trep[sl] = kNotReady;
+        }
+        __syncthreads();
+      }
       continue;
     }
-    if (tid > 1 && tid < kSmallCounts && s_chist[tid]) e += (double)s_chist[tid] * term(tid);
+    if (tid > 1 && tid < kSmallCounts && s_chist[par][tid])
+      e += (double)s_chist[par][tid] * term(tid);
     if (tid == 0 && utot) e += (double)utot * term(1);
     e = wave_sum(e);
     if (lane == 0) s_redf[wave] = e;
-    __syncthreads();
-    const bool sub = f != 0;  // a recount subset: several work items add to one partition
-    if (tid == 0) {
-      double etot = 0.0;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) etot += s_redf[w];
-      if (a.groups) {
-        a.part_off[p] = r0;
-        s_gbase = sub ? atomicAdd(&a.part_groups[p], (unsigned long long)gtot) : 0ULL;
-      }
-      if (!a.groups || !sub) {
-        if (sub) atomicAdd(&a.part_groups[p], (unsigned long long)gtot);
-        else a.part_groups[p] = gtot;
-      }
-      if (sub) {
-        if (utot) atomicAdd(&a.part_unique[p], (unsigned long long)utot);
-        if (etot != 0.0) atomicAdd(&a.part_entropy[p], etot);
-      } else {
-        a.part_unique[p] = utot;
-        a.part_entropy[p] = etot;
-      }
-    }
-    if (a.groups) {
-      __syncthreads();
-      Group* out = a.groups + r0 + s_gbase + gex;
-      uint32_t q = 0;
-      for (int sl = tid; sl < KT; sl += kCThreads) {
-        if (tkey[sl] == kEmptyKey) continue;
-        out[q++] = Group{tkey[sl], tcnt[sl], HASHED ? trep[sl] : 0};
-      }
-      if (tid == 0 && s_spec_cnt) out[q++] = Group{kEmptyKey, s_spec_cnt, HASHED ? s_spec_rep : 0};
-    }
-    if (a.want_cand && !sub) {
-      // top kCand groups of the partition by count (Histogram's rdd.top, per partition): a
-      // thread's top kCand, a wave's by shuffles, the block's by wave 0 over the waves' lists
-      uint64_t tc[kCand];
-      int ts[kCand];
-#pragma unroll
-      for (int q = 0; q < kCand; ++q) {
-        tc[q] = 0;
-        ts[q] = -1;
-      }
-      auto offer = [&](uint64_t c, int sl) {  // insertion with static indices (no scratch)
-#pragma unroll
-        for (int q = 0; q < kCand; ++q) {
-          if (c > tc[q]) {
-            const uint64_t tc2 = tc[q];
-            const int ts2 = ts[q];
-            tc[q] = c;
-            ts[q] = sl;
-            c = tc2;
-            sl = ts2;
-          }
-        }
-      };
-      for (int sl = tid; sl < KT; sl += kCThreads)
-        if (tkey[sl] != kEmptyKey) offer(tcnt[sl], sl);
-      if (tid == 0 && s_spec_cnt) offer(s_spec_cnt, KT);  // KT stands for the special cell
-      // wave: kCand rounds of max over the lanes' heads
+    if (cand) {
+      // the wave's top kCand: kCand rounds of max over the lanes' heads
 #pragma unroll
       for (int r = 0; r < kCand; ++r) {
         uint64_t best = tc[0];
@@ -1300,51 +1318,82 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
             bl = yl;
           }
         }
-        const int bs = __shfl(ts[0], bl);
+        const uint64_t bk = __shfl(tk[0], bl), br = __shfl(tr[0], bl);
         if (lane == 0) {
           s_cc[wave * kCand + r] = best;
-          s_cs[wave * kCand + r] = best ? bs : -1;
+          s_ck[wave * kCand + r] = bk;
+          s_cr[wave * kCand + r] = br;
         }
         if (lane == bl) {
 #pragma unroll
           for (int q = 0; q + 1 < kCand; ++q) {
             tc[q] = tc[q + 1];
-            ts[q] = ts[q + 1];
+            tk[q] = tk[q + 1];
+            tr[q] = tr[q + 1];
           }
           tc[kCand - 1] = 0;
-          ts[kCand - 1] = -1;
-        }
-      }
-      __syncthreads();
-      if (wave == 0) {  // kCThreads / 64 * kCand candidates, one per lane
-        constexpr int kN = kCThreads / 64 * kCand;
-        uint64_t mc = lane < kN ? s_cc[lane] : 0;
-        const int ms = lane < kN ? s_cs[lane] : -1;
-#pragma unroll
-        for (int r = 0; r < kCand; ++r) {
-          uint64_t best = mc;
-          int bl = lane;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) {
-            const uint64_t y = __shfl_xor(best, o);
-            const int yl = __shfl_xor(bl, o);
-            if (y > best || (y == best && yl < bl)) {
-              best = y;
-              bl = yl;
-            }
-          }
-          const int sl = __shfl(ms, bl);
-          if (lane == 0) {
-            Group* cslot = a.cand + (uint64_t)p * kCand + r;
-            if (best == 0) *cslot = Group{0, 0, 0};
-            else if (sl == KT) *cslot = Group{kEmptyKey, s_spec_cnt, HASHED ? s_spec_rep : 0};
-            else *cslot = Group{tkey[sl], tcnt[sl], HASHED ? trep[sl] : 0};
-          }
-          if (lane == bl) mc = 0;
         }
       }
     }
-    __syncthreads();
+    const bool sub = f != 0;  // a recount subset: several work items add to one partition
+    if (tid == 0 && keep) {
+      a.part_off[p] = r0;
+      s_gbase = sub ? atomicAdd(&a.part_groups[p], (unsigned long long)gtot) : 0ULL;
+    }
+    __syncthreads();  //                                                            [barrier 3]
+    if (tid == 0) {
+      double etot = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) etot += s_redf[w];
+      if (!keep || !sub) {
+        if (sub) atomicAdd(&a.part_groups[p], (unsigned long long)gtot);
+        else a.part_groups[p] = gtot;
+      }
+      if (sub) {
+        if (utot) atomicAdd(&a.part_unique[p], (unsigned long long)utot);
+        if (etot != 0.0) atomicAdd(&a.part_entropy[p], etot);
+      } else {
+        a.part_unique[p] = utot;
+        a.part_entropy[p] = etot;
+      }
+    }
+    if (cand && wave == 0) {  // the block's top kCand over the waves' lists, one per lane
+      constexpr int kN = NW * kCand;
+      uint64_t mc = lane < kN ? s_cc[lane] : 0;
+#pragma unroll
+      for (int r = 0; r < kCand; ++r) {
+        uint64_t best = mc;
+        int bl = lane;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const uint64_t y = __shfl_xor(best, o);
+          const int yl = __shfl_xor(bl, o);
+          if (y > best || (y == best && yl < bl)) {
+            best = y;
+            bl = yl;
+          }
+        }
+        if (lane == 0) {
+          Group* cslot = a.cand + (uint64_t)p * kCand + r;
+          *cslot = best ? Group{s_ck[bl], best, HASHED ? s_cr[bl] : 0} : Group{0, 0, 0};
+        }
+        if (lane == bl) mc = 0;
+      }
+    }
+    if (keep) {  // materialise the groups, clearing the table
+      Group* out = a.groups + r0 + s_gbase + gex;
+      uint32_t q = 0;
+      for (int sl = tid; sl < KT; sl += kCThreads) {
+        const uint64_t k = tkey[sl];
+        if (k == kEmptyKey) continue;
+        out[q++] = Group{k, tcnt[sl], HASHED ? trep[sl] : 0};
+        tkey[sl] = kEmptyKey;
+        tcnt[sl] = 0;
+        if (HASHED) trep[sl] = kNotReady;
+      }
+      if (tid == 0 && sc) out[q++] = Group{kEmptyKey, sc, HASHED ? sr : 0};
+      __syncthreads();
+    }
   }
   if (collisions) atomicAdd(&a.counters[C_COLLISIONS], collisions);
 }
@@ -1664,6 +1713,10 @@ static void launch_phaseA(dq_freq* f, AArgs a, bool from_rec) {
   if (from_rec)
     hipLaunchKernelGGL((freq_phaseA<HASHED, true>), dim3((unsigned)n_wg),
                        dim3(AKeys<HASHED, true>::kThreads), 0,
+                       f->stream, a);
+  else if (HASHED && a.ks.n_keys == 1 && a.ks.cols[0].type == DQ_UTF8)
+    hipLaunchKernelGGL((freq_phaseA<HASHED, false, HASHED>), dim3((unsigned)n_wg),
+                       dim3(AKeys<HASHED, false>::kThreads), 0,
                        f->stream, a);
   else
     hipLaunchKernelGGL((freq_phaseA<HASHED, false>), dim3((unsigned)n_wg),
