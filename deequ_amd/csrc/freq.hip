@@ -117,25 +117,23 @@ DQ_DEV void lds_store(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// ockl wavefront reductions / scans: DPP row and broadcast steps, no LDS round trips (the
+// __shfl_* forms are ds_bpermute, a few hundred cycles for a 6-step 64-bit chain)
+extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
+extern "C" __device__ uint64_t __ockl_wfred_add_u64(uint64_t);
+extern "C" __device__ double __ockl_wfred_add_f64(double);
+extern "C" __device__ uint64_t __ockl_wfred_max_u64(uint64_t);
+extern "C" __device__ uint32_t __ockl_wfscan_add_u32(uint32_t, bool);
+
 // Exclusive scan of one u32 per thread over the workgroup; returns the thread's prefix and sets
 // `total`.  Every thread of the block must call it.
 DQ_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
   const int lane = __lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
+  const uint32_t x = __ockl_wfscan_add_u32(v, true);
   if (lane == 63) s_wave[wave] = x;
   __syncthreads();
   if (wave == 0) {
-    uint32_t w = lane < nw ? s_wave[lane] : 0u;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(w, o);
-      if (lane >= o) w += y;
-    }
+    const uint32_t w = __ockl_wfscan_add_u32(lane < nw ? s_wave[lane] : 0u, true);
     if (lane < nw) s_wave[lane] = w;
   }
   __syncthreads();
@@ -147,9 +145,9 @@ DQ_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
 
 template <typename T>
 DQ_DEV T wave_sum(T v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  if constexpr (std::is_same_v<T, double>) return __ockl_wfred_add_f64(v);
+  else if constexpr (sizeof(T) == 8) return (T)__ockl_wfred_add_u64((uint64_t)v);
+  else return (T)__ockl_wfred_add_u32((uint32_t)v);
 }
 
 // Fixed-order block sums (every thread calls; the result is valid in every thread).
@@ -954,6 +952,7 @@ struct CArgs {
   // *lit_count (nullptr: no probe); lit_h is that key's row hash
   uint64_t lit_h;
   unsigned long long* lit_count;
+  unsigned long long* dbg_clock;  // DQ_FREQ_DEBUG=2: workgroup 0's per-item stamps (wall clock)
 };
 
 // Is the encoded one-column utf8 key at p the 9-byte string "NullValue"?
@@ -1056,7 +1055,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
   __shared__ unsigned long long s_spec_cnt[2], s_gbase;
   __shared__ uint64_t s_spec_rep[2];
   __shared__ uint32_t s_chist[2][kSmallCounts];
-  __shared__ uint64_t s_cc[NW * kCand], s_ck[NW * kCand], s_cr[NW * kCand];
+  // Histogram candidates: packed (count << 16 | tid << 1 | q) maxima, top-1 then top-2
+  __shared__ unsigned long long s_top[2][2];
 
   const int tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
   unsigned long long collisions = 0;
@@ -1069,6 +1069,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     s_ovf[tid] = 0;
     s_spec_cnt[tid] = 0;
     s_spec_rep[tid] = kNotReady;
+    s_top[tid][0] = s_top[tid][1] = 0;
   }
   if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
   CBounds nb;
@@ -1079,7 +1080,13 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
   __syncthreads();
 
   uint32_t par = 0;
-  for (int wi = blockIdx.x; wi < a.n_work; wi += gridDim.x, par ^= 1u) {
+  int item = 0;
+  auto mark = [&](int k) {
+    if (a.dbg_clock && blockIdx.x == 0 && tid == 0 && item < 16)
+      a.dbg_clock[item * 4 + k] = wall_clock64();
+  };
+  for (int wi = blockIdx.x; wi < a.n_work; wi += gridDim.x, par ^= 1u, ++item) {
+    mark(0);
     const uint32_t p = cur.p, b = p >> a.s, f = cur.f, fv = cur.fv;
     const uint32_t fmask = (1u << f) - 1u;
     const uint64_t r0 = cur.r0, nrec = cur.r1 - cur.r0;
@@ -1191,6 +1198,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       }
       insert_all(w, valid);
     }
+    mark(1);
     // the table is final.  Next item's records (bounds already here) and the bounds after it are
     // in flight while this one is reduced; the other parity's flags are reset for it.
     c_fetch<HASHED>(a, wi + gridDim.x, nb, cur);
@@ -1199,6 +1207,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       s_ovf[par ^ 1u] = 0;
       s_spec_cnt[par ^ 1u] = 0;
       s_spec_rep[par ^ 1u] = kNotReady;
+      s_top[par ^ 1u][0] = s_top[par ^ 1u][1] = 0;
     }
     if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
     const bool overflow = *ovf != 0;
@@ -1238,6 +1247,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
         }
       }
     };
+#pragma unroll
     for (int sl = tid; sl < KT; sl += kCThreads) {
       const uint64_t k = tkey[sl];
       if (k == kEmptyKey) continue;
@@ -1259,20 +1269,24 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       count_group(sc);
       if (cand) offer(sc, kEmptyKey, sr);
     }
-    uint32_t gin = g;  // inclusive prefix of g over the wave
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(gin, o);
-      if (lane >= o) gin += y;
-    }
-    const uint32_t wclaims = wave_sum(claims);
-    const uint64_t wun = wave_sum(un);
+    const uint32_t gin = __ockl_wfscan_add_u32(g, true);  // inclusive prefix over the wave
+    const uint32_t wclaims = __ockl_wfred_add_u32(claims);
+    const uint64_t wun = __ockl_wfred_add_u64(un);
     if (lane == 63) {
       s_wg[wave] = gin;
       s_wc[wave] = wclaims;
       s_red[wave] = wun;
     }
+    // Histogram candidates, round 1: the block's largest (count, tid, q)
+    auto pack = [&](int q) -> uint64_t {
+      return tc[q] ? (tc[q] << 16) | ((uint64_t)tid << 1) | (uint64_t)q : 0ULL;
+    };
+    if (cand) {
+      const uint64_t w1 = __ockl_wfred_max_u64(pack(0));
+      if (lane == 0 && w1) atomicMax(&s_top[par][0], (unsigned long long)w1);
+    }
     __syncthreads();  //                                                            [barrier 2]
+    mark(2);
     uint32_t gtot = 0, gex = gin - g, all_claims = 0;
     uint64_t utot = 0;
 #pragma unroll
@@ -1301,39 +1315,14 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     if (tid > 1 && tid < kSmallCounts && s_chist[par][tid])
       e += (double)s_chist[par][tid] * term(tid);
     if (tid == 0 && utot) e += (double)utot * term(1);
-    e = wave_sum(e);
+    e = __ockl_wfred_add_f64(e);
     if (lane == 0) s_redf[wave] = e;
-    if (cand) {
-      // the wave's top kCand: kCand rounds of max over the lanes' heads
-#pragma unroll
-      for (int r = 0; r < kCand; ++r) {
-        uint64_t best = tc[0];
-        int bl = lane;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const uint64_t y = __shfl_xor(best, o);
-          const int yl = __shfl_xor(bl, o);
-          if (y > best || (y == best && yl < bl)) {
-            best = y;
-            bl = yl;
-          }
-        }
-        const uint64_t bk = __shfl(tk[0], bl), br = __shfl(tr[0], bl);
-        if (lane == 0) {
-          s_cc[wave * kCand + r] = best;
-          s_ck[wave * kCand + r] = bk;
-          s_cr[wave * kCand + r] = br;
-        }
-        if (lane == bl) {
-#pragma unroll
-          for (int q = 0; q + 1 < kCand; ++q) {
-            tc[q] = tc[q + 1];
-            tk[q] = tk[q + 1];
-            tr[q] = tr[q + 1];
-          }
-          tc[kCand - 1] = 0;
-        }
-      }
+    uint64_t top1 = 0;
+    if (cand) {  // round 2: the largest of the rest (the top-1 owner offers its second)
+      top1 = s_top[par][0];
+      const uint64_t mine = top1 && top1 == pack(0) ? pack(1) : pack(0);
+      const uint64_t w2 = __ockl_wfred_max_u64(mine);
+      if (lane == 0 && w2) atomicMax(&s_top[par][1], (unsigned long long)w2);
     }
     const bool sub = f != 0;  // a recount subset: several work items add to one partition
     if (tid == 0 && keep) {
@@ -1341,6 +1330,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       s_gbase = sub ? atomicAdd(&a.part_groups[p], (unsigned long long)gtot) : 0ULL;
     }
     __syncthreads();  //                                                            [barrier 3]
+    mark(3);
     if (tid == 0) {
       double etot = 0.0;
 #pragma unroll
@@ -1357,27 +1347,18 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
         a.part_entropy[p] = etot;
       }
     }
-    if (cand && wave == 0) {  // the block's top kCand over the waves' lists, one per lane
-      constexpr int kN = NW * kCand;
-      uint64_t mc = lane < kN ? s_cc[lane] : 0;
+    if (cand) {  // each winner's owner writes it; an empty place is written by thread 0
+      static_assert(kCand == 2, "two candidate rounds");
 #pragma unroll
       for (int r = 0; r < kCand; ++r) {
-        uint64_t best = mc;
-        int bl = lane;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const uint64_t y = __shfl_xor(best, o);
-          const int yl = __shfl_xor(bl, o);
-          if (y > best || (y == best && yl < bl)) {
-            best = y;
-            bl = yl;
-          }
+        const uint64_t t = r ? s_top[par][1] : top1;
+        Group* cslot = a.cand + (uint64_t)p * kCand + r;
+        if (!t) {
+          if (tid == 0) *cslot = Group{0, 0, 0};
+        } else if ((int)((t >> 1) & 511u) == tid) {
+          const int q = (int)(t & 1u);
+          *cslot = Group{q ? tk[1] : tk[0], q ? tc[1] : tc[0], HASHED ? (q ? tr[1] : tr[0]) : 0};
         }
-        if (lane == 0) {
-          Group* cslot = a.cand + (uint64_t)p * kCand + r;
-          *cslot = best ? Group{s_ck[bl], best, HASHED ? s_cr[bl] : 0} : Group{0, 0, 0};
-        }
-        if (lane == bl) mc = 0;
       }
     }
     if (keep) {  // materialise the groups, clearing the table
@@ -1928,6 +1909,16 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     a.ovf_out = f->ovf_a.p;
     a.ovf_n = f->ovf_n.p;
     a.n_work = (int32_t)P;
+    static int dbg = [] {
+      const char* e = getenv("DQ_FREQ_DEBUG");
+      return e ? atoi(e) : 0;
+    }();
+    unsigned long long* clk = nullptr;
+    if (dbg >= 2 && hipMalloc(&clk, 16 * 4 * sizeof(unsigned long long)) == hipSuccess)
+      (void)hipMemset(clk, 0, 16 * 4 * sizeof(unsigned long long));
+    else
+      clk = nullptr;
+    a.dbg_clock = clk;
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, f->device);
     const unsigned persistent = (unsigned)std::max(1, cus * 2);
@@ -1941,8 +1932,31 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       unsigned int m = 0;
       HIP_TRY(hipStreamSynchronize(f->stream));
       HIP_TRY(hipMemcpy(&m, f->ovf_n.p, 4, hipMemcpyDeviceToHost));
+      if (clk) {  // per-item phase times of workgroup 0, us (the wall clock ticks at 100 MHz)
+        unsigned long long h[16 * 4];
+        (void)hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost);
+        double acc[4] = {0, 0, 0, 0};
+        int ni = 0;
+        for (int i = 0; i + 1 < 16; ++i) {
+          if (!h[(i + 1) * 4]) break;
+          acc[0] += (double)(h[i * 4 + 1] - h[i * 4]) / 100.0;
+          acc[1] += (double)(h[i * 4 + 2] - h[i * 4 + 1]) / 100.0;
+          acc[2] += (double)(h[i * 4 + 3] - h[i * 4 + 2]) / 100.0;
+          acc[3] += (double)(h[(i + 1) * 4] - h[i * 4 + 3]) / 100.0;
+          ++ni;
+        }
+        if (ni)
+          fprintf(stderr, "dq_freq phase C%s wg0 per item (us): inserts %.2f stats %.2f "
+                  "entropy+cand %.2f tail %.2f (%d items, grid %u, round %d)\n",
+                  f->exact ? " exact" : " hashed", acc[0] / ni, acc[1] / ni, acc[2] / ni,
+                  acc[3] / ni, ni, grid, round);
+        (void)hipMemset(clk, 0, sizeof(h));
+      }
       if (m == 0) break;
-      if (round == 23) return fail(DQ_ERR_OUT_OF_MEMORY, "frequency partition does not fit");
+      if (round == 23) {
+        if (clk) (void)hipFree(clk);
+        return fail(DQ_ERR_OUT_OF_MEMORY, "frequency partition does not fit");
+      }
       // recount the overflowing partitions over disjoint hash subsets
       f->recounted = true;
       f->ovf_a.swap(f->ovf_b);  // ovf_b = this round's entries
@@ -1953,6 +1967,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       a.n_work = (int32_t)m;
       grid = std::min<unsigned>(m, persistent);
     }
+    if (clk) (void)hipFree(clk);
   }
   hipLaunchKernelGGL(freq_reduce, dim3(1), dim3(kThreads), 0, f->stream, f->part_groups.p,
                      f->part_unique.p, f->part_entropy.p, P, f->red.p);
