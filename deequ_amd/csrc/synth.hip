@@ -150,3 +150,32 @@ extern "C" int dq_synth_strings(uint64_t seed, uint64_t row0, int64_t n, const i
                      name_off, name_data, prio_off, prio_data);
   return (int)hipGetLastError();
 }
+
+// configs[4]'s URL-bearing text: row r of `out` = a prefix + row r of `src`; the prefix carries an
+// https URL when bit 62 of r * 0x9E3779B97F4A7C15 is set (about half the rows), else none.
+// out_off holds the caller's offsets (it knows both lengths).
+namespace {
+__constant__ const char kUrlPrefix[] = "see https://www.example.com/item/";  // 33 bytes
+__constant__ const char kPlainPrefix[] = "no link: ";                        // 9 bytes
+__global__ void gen_describe(uint64_t row0, int64_t n, const int32_t* src_off, const uint8_t* src,
+                             const int32_t* out_off, uint8_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool url = (((row0 + (uint64_t)i) * 0x9E3779B97F4A7C15ULL) >> 62) & 1ULL;
+  const char* pre = url ? kUrlPrefix : kPlainPrefix;
+  const int plen = url ? 33 : 9;
+  uint8_t* o = out + out_off[i];
+  for (int k = 0; k < plen; ++k) o[k] = (uint8_t)pre[k];
+  const int32_t s = src_off[i], len = src_off[i + 1] - s;
+  for (int k = 0; k < len; ++k) o[plen + k] = src[s + k];
+}
+}  // namespace
+
+extern "C" int dq_synth_describe(uint64_t row0, int64_t n, const int32_t* src_off,
+                                 const uint8_t* src, const int32_t* out_off, uint8_t* out,
+                                 void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(gen_describe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, row0, n, src_off, src, out_off, out);
+  return (int)hipGetLastError();
+}

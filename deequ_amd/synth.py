@@ -227,3 +227,57 @@ def item_buffers_numpy(n: int, seed: int = 7, start: int = 0) -> dict:
     codes = np.repeat(code, lens)
     out["priority_data"] = np.concatenate([table[codes, within], np.zeros(16, np.uint8)])
     return out
+
+
+def profiling_table_device(n: int, batch_rows: int = 1 << 26, device: str = "cuda:0") -> Table:
+    """BASELINE configs[4]'s table: 20 mixed columns generated in HBM -- 10 numeric (id; numViews
+    of five Item tables with different seeds; score of four) and 10 strings (name and priority of
+    three Item tables; four `description` columns = name + a prefix that carries an https URL in
+    about half the rows, the containsURL workload).  Every column has ~5 % NULLs."""
+    import torch
+    lib = _synth_lib()
+    if not hasattr(lib, "_describe_ready"):
+        vp = ctypes.c_void_p
+        lib.dq_synth_describe.argtypes = [ctypes.c_uint64, ctypes.c_int64, vp, vp, vp, vp, vp]
+        lib.dq_synth_describe.restype = ctypes.c_int
+        lib._describe_ready = True
+    parts = [item_table_device(n, seed=100 + k, batch_rows=batch_rows, device=device, extra=True)
+             for k in range(5)]
+    dev = torch.device(device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    fields = [StructField("id", N.INT64)]
+    fields += [StructField(f"numViews_{k}", N.INT64) for k in range(5)]
+    fields += [StructField(f"score_{k}", N.FLOAT64) for k in range(4)]
+    fields += [StructField(f"name_{k}", N.UTF8) for k in range(3)]
+    fields += [StructField(f"priority_{k}", N.UTF8) for k in range(3)]
+    fields += [StructField(f"description_{k}", N.UTF8) for k in range(4)]
+    batches = []
+    pos = 0
+    for bi in range(len(parts[0].batches)):
+        b = {"id": parts[0].batches[bi]["id"]}
+        for k in range(5):
+            b[f"numViews_{k}"] = parts[k].batches[bi]["numViews"]
+        for k in range(4):
+            b[f"score_{k}"] = parts[k].batches[bi]["score"]
+        for k in range(3):
+            b[f"name_{k}"] = parts[k].batches[bi]["name"]
+            b[f"priority_{k}"] = parts[k].batches[bi]["priority"]
+        for k in range(4):
+            src = parts[k + 1].batches[bi]["name"]
+            m = src.length
+            rows = torch.arange(pos, pos + m, dtype=torch.int64, device=dev)
+            url = ((rows * -7046029254386353131) >> 62) & 1  # bit 62 of r * 0x9E3779B97F4A7C15
+            lens = (src.values[1: m + 1] - src.values[:m]).to(torch.int64) + torch.where(
+                url.bool(), torch.tensor(33, device=dev), torch.tensor(9, device=dev))
+            off = torch.zeros(m + 4, dtype=torch.int32, device=dev)
+            off[1: m + 1] = torch.cumsum(lens, 0).to(torch.int32)
+            data = torch.zeros(int(off[m].item()) + 16, dtype=torch.uint8, device=dev)
+            rc = lib.dq_synth_describe(pos, m, src.values.data_ptr(), src.data.data_ptr(),
+                                       off.data_ptr(), data.data_ptr(), stream)
+            if rc:
+                raise RuntimeError(f"dq_synth_describe failed ({rc})")
+            b[f"description_{k}"] = ColumnBatch(N.UTF8, m, src.validity, off, data)
+        batches.append(b)
+        pos += parts[0].batches[bi]["id"].length
+    torch.cuda.synchronize(dev)
+    return Table(StructType(fields), batches, device)

@@ -13,7 +13,16 @@ configs[1], S10).  Not part of the driver's bench contract; the JSON lines land 
       fp64 `score` column.  One step = the fused scan (HLL launch + co-moment launch + finalize).
       B_alg = id validity + values + score validity + values = 16.25 B/row.
 
-Usage: python tools/bench_workloads.py c3|c4 [--rows N] [--steps K] [--warmup W]
+  c5: BASELINE configs[4], the full profiling suite: every analyzer on 20 mixed columns (10 numeric,
+      10 strings incl. four URL-bearing description columns; deequ_amd.synth.profiling_table_device)
+      through AnalysisRunner -- one fused scan (Size, Completeness, Compliance, Sum, Mean,
+      StandardDeviation, Minimum, Maximum, Correlation, ApproxCountDistinct, DataType,
+      PatternMatch(URL)), one group-by per column for Uniqueness / Distinctness / UniqueValueRatio /
+      CountDistinct / Entropy / Histogram (shared except on doubles), the MutualInformation joints,
+      and one device sort per ApproxQuantile.  One step = one do_analysis_run.  B_alg = every
+      buffer of the table once.
+
+Usage: python tools/bench_workloads.py c3|c4|c5 [--rows N] [--steps K] [--warmup W]
 """
 import argparse
 import ctypes
@@ -29,7 +38,7 @@ PEAK = 8.0e12
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("workload", choices=["c3", "c4"])
+    ap.add_argument("workload", choices=["c3", "c4", "c5"])
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
@@ -39,9 +48,14 @@ def main():
     import torch
     dev = "cuda:0"
     from deequ_amd.synth import item_table_device
-    rows = args.rows or (1_000_000_000 if args.workload == "c3" else 1_250_000_000)
-    table = item_table_device(rows, seed=9, batch_rows=args.batch_rows, device=dev,
-                              extra=args.workload == "c4")
+    rows = args.rows or {"c3": 1_000_000_000, "c4": 1_250_000_000, "c5": 250_000_000}[args.workload]
+    if args.workload == "c5":
+        from deequ_amd.synth import profiling_table_device
+        # description strings average ~40 B: 2^25-row batches keep int32 offsets in range
+        table = profiling_table_device(rows, batch_rows=min(args.batch_rows, 1 << 25), device=dev)
+    else:
+        table = item_table_device(rows, seed=9, batch_rows=args.batch_rows, device=dev,
+                                  extra=args.workload == "c4")
     stream = torch.cuda.current_stream(dev)
     e0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     e1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -91,6 +105,45 @@ def main():
         desc = ("Uniqueness/Distinctness/Entropy grouping + Histogram (top-1000 + bins) on int64 id "
                 "(~N groups, exact mode) and string priority (3 groups, hashed mode) over a "
                 "synthetic Item table, 5% nulls (BASELINE.json configs[2], 1 GPU)")
+        metric_unit = "rows/s"
+    elif args.workload == "c5":
+        from deequ_amd import analyzers as A
+        from deequ_amd.runners import AnalysisRunner
+        num = ["id"] + [f"numViews_{k}" for k in range(5)] + [f"score_{k}" for k in range(4)]
+        strs = ([f"name_{k}" for k in range(3)] + [f"priority_{k}" for k in range(3)]
+                + [f"description_{k}" for k in range(4)])
+        suite = [A.Size()]
+        for c in num + strs:
+            suite += [A.Completeness(c), A.ApproxCountDistinct(c), A.Uniqueness([c]),
+                      A.Distinctness([c]), A.UniqueValueRatio([c]), A.CountDistinct([c]),
+                      A.Entropy(c), A.Histogram(c)]
+        for c in num:
+            suite += [A.Sum(c), A.Mean(c), A.StandardDeviation(c), A.Minimum(c), A.Maximum(c),
+                      A.Compliance(f"{c} non-negative", f"{c} >= 0"), A.ApproxQuantile(c, 0.5)]
+        for c in strs:
+            suite += [A.DataType(c), A.PatternMatch(c, A.Patterns.URL)]
+        suite += [A.Correlation("numViews_0", "score_0"), A.Correlation("numViews_1", "score_1"),
+                  A.Correlation("id", "numViews_2"),
+                  A.MutualInformation("priority_0", "priority_1"),
+                  A.MutualInformation("name_0", "priority_2")]
+
+        def step():
+            ctx = AnalysisRunner.do_analysis_run(table, suite)
+            bad = [str(a) for a in suite if not ctx.metric(a).value.is_success]
+            if bad:
+                raise RuntimeError(f"failed metrics: {bad[:5]}")
+            return {"metrics": len(suite),
+                    "Histogram(priority_0)": ctx.metric(A.Histogram("priority_0")).value.get().number_of_bins,
+                    "PatternMatch(description_0)": ctx.metric(A.PatternMatch("description_0", A.Patterns.URL)).value.get(),
+                    "Uniqueness(id)": ctx.metric(A.Uniqueness(["id"])).value.get()}
+        b_alg = 0
+        for b in table.batches:
+            for c in b.values():
+                b_alg += c.nbytes()
+        kernel = "whole suite (fused scan + 20 group-bys + 10 quantile sorts + MI joints)"
+        desc = ("every analyzer on 20 mixed columns (10 numeric, 10 string incl. containsURL over "
+                "URL-bearing text), synthetic, 5% nulls (BASELINE.json configs[4], per-GPU shard, "
+                "1 GPU)")
         metric_unit = "rows/s"
     else:
         from deequ_amd import _native as N
