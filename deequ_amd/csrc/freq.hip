@@ -344,7 +344,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   // LDS dedupe: 0 = not counted (table full), 1 = claimed a new slot, 2 = added to an existing
   // slot, 3 = the key's slot is being claimed: retry after the next barrier
   static_assert(!STR1 || (HASHED && !FROM_REC), "STR1 is the row path of a utf8 key");
-  auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep, uint64_t k0, uint64_t k1) -> int {
+  // defer: a hit (2) only reports its slot in hit_slot; the caller adds the count (wave-aggregated)
+  auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep, uint64_t k0, uint64_t k1, bool defer,
+                    uint32_t& hit_slot) -> int {
     if (h == kEmptyKey) return 0;
     uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
     for (int pr = 0; pr < 4; ++pr) {
@@ -387,7 +389,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
           if (!same) atomicAdd(&s_dbg[1], 1u);
         }
         if (same) {
-          atomicAdd((unsigned long long*)&dcnt[slot], c);
+          if (defer) hit_slot = slot;
+          else atomicAdd((unsigned long long*)&dcnt[slot], c);
           return 2;
         }
       }
@@ -591,7 +594,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
             const int q = j * kThreads + tid;
             const uint64_t h = stash[q * W], rep = stash[q * W + 1];
             const uint64_t c = FROM_REC ? scnt[tid] : 1;
-            const int res = dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort);
+            uint32_t unused = 0;
+            const int res = dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort, false,
+                                   unused);
             if (res == 3) continue;
             w &= ~(1u << j);
             if (res == 2) ++hits;
@@ -605,15 +610,30 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     for (int j = 0; j < ROUNDS; ++j) {
       const int q = j * kThreads + tid;
       const bool on = probe && j == 0 ? true : !s_bypass;
-      uint32_t hits = 0;
+      uint32_t hits = 0, hslot = 0;
+      int res = -1;
       if ((keyed >> j) & 1u) {
         const uint64_t h = stash[q * W];
         const uint64_t rep = HASHED ? stash[q * W + 1] : 0;
         const uint64_t c = FROM_REC ? scnt[tid] : 1;
-        const int res = on ? dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort) : 0;
+        res = on ? dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort, !FROM_REC, hslot)
+                 : 0;
         if (res == 3) wait |= 1u << j;
         else if (res == 2) ++hits;
         else if (!res) count_raw(j, h, c);
+      }
+      if constexpr (!FROM_REC) {
+        // the hits' counts (1 per row): one LDS atomic per distinct slot of the wave instead of
+        // one per lane (a low-cardinality key puts every lane on a handful of addresses)
+        uint64_t m = __ballot(res == 2);
+        while (m) {
+          const int leader = __builtin_ctzll(m);
+          const uint32_t ls = (uint32_t)__builtin_amdgcn_readlane((int)hslot, leader);
+          const uint64_t same = __ballot(res == 2 && hslot == ls);
+          if (__lane_id() == leader)
+            atomicAdd((unsigned long long*)&dcnt[ls], (unsigned long long)__popcll(same));
+          m &= ~same;
+        }
       }
       if (probe && j == 0) {
         retry(1u, hits);
@@ -1779,7 +1799,11 @@ static dq_status finalize_b(dq_freq* f) {
   if (const char* e = getenv("DQ_FREQ_PARTITION_TARGET")) target = std::max(1, atoi(e));
   int s = 0;
   while (s < kMaxSubBits && ((uint64_t)kBuckets << s) * (uint64_t)target < R) ++s;
-  const uint64_t H = (uint64_t)f->tile * kUnitTiles;
+  static const int unit_tiles = [] {  // DQ_FREQ_UNIT_TILES: A/B hook for the phase-B unit size
+    const char* e = getenv("DQ_FREQ_UNIT_TILES");
+    return e ? std::max(1, atoi(e)) : kUnitTiles;
+  }();
+  const uint64_t H = (uint64_t)f->tile * unit_tiles;
   uint32_t u = 0;
   for (int b = 0; b < kBuckets; ++b) {
     f->h_unit_start[b] = u;

@@ -112,13 +112,29 @@ class AnalysisRunner:
         precondition_failures = _precondition_failure_metrics(failed, schema)
         grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]
         scanning = [a for a in passed if a not in grouping]
-        shared = _histogram_tables_for_groupings(data, grouping, scanning, aggregate_with,
-                                                 save_states_with)
+        groups: Dict[tuple, List[Analyzer]] = {}
+        for a in grouping:
+            groups.setdefault(tuple(sorted(a.grouping_columns())), []).append(a)
+        # columns grouped once for Histogram and their grouping: one column at a time, so that
+        # only one such table is alive (the reference unpersists each grouping's frequencies,
+        # AnalysisRunner.scala:531)
         hist_metrics = {}
-        for h in scanning:
-            if isinstance(h, Histogram) and h.column in shared:
+        grouped = AnalyzerContext.empty()
+        for col in _histogram_columns_for_groupings(data, grouping, scanning, aggregate_with,
+                                                    save_states_with):
+            hists = [h for h in scanning if isinstance(h, Histogram) and h.column == col]
+            try:
+                hs = hists[0].compute_state_from(data)
+            except Exception:  # noqa: BLE001 -- both analyzers then run (and fail) on their own
+                continue
+            for h in hists:
                 hist_metrics[h] = h.compute_metric_from(
-                    dataclasses.replace(shared[h.column], binning_udf=h.binning_udf))
+                    dataclasses.replace(hs, binning_udf=h.binning_udf))
+            state = FrequenciesAndNumRows(KeyedFrequencies(hs.frequencies), hs.num_rows)
+            _, metrics = _run_grouping_analyzers(data, [col], groups.pop((col,)), aggregate_with,
+                                                 save_states_with, None, state)
+            grouped = grouped + metrics
+            del hs, state
         scanning = [a for a in scanning if a not in hist_metrics]
         non_grouped = _run_scanning_analyzers(data, scanning, aggregate_with, save_states_with) + \
             AnalyzerContext(hist_metrics)
@@ -128,17 +144,9 @@ class AnalysisRunner:
         if size_metric is not None and size_metric.value.is_success:
             num_rows = int(size_metric.value.get())
 
-        grouped = AnalyzerContext.empty()
-        groups: Dict[tuple, List[Analyzer]] = {}
-        for a in grouping:
-            groups.setdefault(tuple(sorted(a.grouping_columns())), []).append(a)
         for cols, group in groups.items():
-            state = None
-            if len(cols) == 1 and cols[0] in shared:
-                hs = shared[cols[0]]
-                state = FrequenciesAndNumRows(KeyedFrequencies(hs.frequencies), hs.num_rows)
             n, metrics = _run_grouping_analyzers(data, list(cols), group, aggregate_with,
-                                                 save_states_with, num_rows, state)
+                                                 save_states_with, num_rows, None)
             grouped = grouped + metrics
             if num_rows is None:
                 num_rows = n
@@ -223,26 +231,22 @@ def _run_scanning_analyzers(data, analyzers: Sequence[Analyzer], aggregate_with,
     return AnalyzerContext(results)
 
 
-def _histogram_tables_for_groupings(data, grouping, scanning, aggregate_with,
-                                    save_states_with) -> Dict[str, object]:
+def _histogram_columns_for_groupings(data, grouping, scanning, aggregate_with,
+                                     save_states_with) -> List[str]:
     """Histogram(c) and the grouping of [c] (Uniqueness, Entropy, ...) are two group-bys of the
     same column in the reference (AnalysisRunner.scala:249-277 and 321-323).  Where the Histogram
     table also yields the grouping exactly (Histogram.table_serves_grouping: the same non-NULL
-    groups), the column is grouped once and both read that table: column -> HistogramState.
-    Not done when states are aggregated or persisted, which keep their own tables."""
+    groups), the column is grouped once and both read that table.  Not done when states are
+    aggregated or persisted, which keep their own tables."""
     if aggregate_with is not None or save_states_with is not None or is_distributed(data):
-        return {}
-    grouped = {tuple(a.grouping_columns()) for a in grouping}
-    out: Dict[str, object] = {}
+        return []
+    grouped = {tuple(sorted(a.grouping_columns())) for a in grouping}
+    out: List[str] = []
     for h in scanning:
         if not isinstance(h, Histogram) or h.column in out or (h.column,) not in grouped:
             continue
-        if not Histogram.table_serves_grouping(data, h.column):
-            continue
-        try:
-            out[h.column] = h.compute_state_from(data)
-        except Exception:  # noqa: BLE001 -- both analyzers then run (and fail) on their own
-            pass
+        if Histogram.table_serves_grouping(data, h.column):
+            out.append(h.column)
     return out
 
 

@@ -332,7 +332,7 @@ def test_histogram_table_serves_grouping(col, nulls, gpu_device):
 @pytest.mark.parametrize("k", [1, 2, 1000])
 def test_histogram_shares_string_table_with_grouping(k, gpu_device):
     """Histogram("s") and the grouping of ["s"] read ONE group-by of a string column with NULLs
-    and real "NullValue" strings (runners._histogram_tables_for_groupings): the grouping drops the
+    and real "NullValue" strings (runners._histogram_columns_for_groupings): the grouping drops the
     NULL rows (GroupingAnalyzers.scala:62-65), Histogram folds them into "NullValue"
     (Histogram.scala:59-66) -- both equal to the oracle's."""
     from deequ_amd.analyzers import CountDistinct, Entropy, Histogram, Uniqueness

@@ -1,10 +1,10 @@
 """Host logic of the runner's one-group-by-for-two plan (runners/__init__.py
-_histogram_tables_for_groupings): which columns' Histogram tables may serve their grouping."""
+_histogram_columns_for_groupings): which columns' Histogram tables may serve their grouping."""
 from types import SimpleNamespace
 
 from deequ_amd import _native as N
 from deequ_amd.analyzers import Entropy, Histogram, Uniqueness
-from deequ_amd.runners import _histogram_tables_for_groupings
+from deequ_amd.runners import _histogram_columns_for_groupings
 
 
 def _data(dtype, bitmaps):
@@ -33,11 +33,13 @@ def test_floating_point_never_shares():
 def test_no_sharing_when_states_are_aggregated_or_saved():
     data = _data(N.INT64, [False])
     grouping, scanning = [Uniqueness(["c"]), Entropy("c")], [Histogram("c")]
-    assert _histogram_tables_for_groupings(data, grouping, scanning, object(), None) == {}
-    assert _histogram_tables_for_groupings(data, grouping, scanning, None, object()) == {}
+    assert _histogram_columns_for_groupings(data, grouping, scanning, object(), None) == []
+    assert _histogram_columns_for_groupings(data, grouping, scanning, None, object()) == []
 
 
 def test_no_sharing_without_a_grouping_of_that_column():
     data = _data(N.INT64, [False])
-    assert _histogram_tables_for_groupings(data, [Uniqueness(["c", "d"])], [Histogram("c")],
-                                           None, None) == {}
+    assert _histogram_columns_for_groupings(data, [Uniqueness(["c", "d"])], [Histogram("c")],
+                                            None, None) == []
+    assert _histogram_columns_for_groupings(data, [Uniqueness(["c"])], [Histogram("c")],
+                                            None, None) == ["c"]

@@ -129,9 +129,10 @@ def main():
 
         def step():
             ctx = AnalysisRunner.do_analysis_run(table, suite)
-            bad = [str(a) for a in suite if not ctx.metric(a).value.is_success]
+            bad = [(str(a), repr(ctx.metric(a).value.failed)[:300]) for a in suite
+                   if not ctx.metric(a).value.is_success]
             if bad:
-                raise RuntimeError(f"failed metrics: {bad[:5]}")
+                raise RuntimeError(f"failed metrics: {bad[:3]}")
             return {"metrics": len(suite),
                     "Histogram(priority_0)": ctx.metric(A.Histogram("priority_0")).value.get().number_of_bins,
                     "PatternMatch(description_0)": ctx.metric(A.PatternMatch("description_0", A.Patterns.URL)).value.get(),
