@@ -1537,6 +1537,17 @@ __global__ void __launch_bounds__(256) freq_owner_scatter(
   }
 }
 
+// the largest count_digits of n received records (sizes the records path's tiles)
+__global__ void __launch_bounds__(256) freq_max_digits(const RecIn* __restrict__ r, int64_t n,
+                                                       unsigned int* out) {
+  int m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    m = max(m, count_digits(r[i].count));
+  m = (int)__ockl_wfred_max_u64((uint64_t)m);
+  if (__lane_id() == 0 && m) atomicMax(out, (unsigned int)m);
+}
+
 // hashed merge: the appended chunks' records point into the appended arena bytes
 __global__ void freq_rebase(uint64_t* recs, const uint16_t* hist, int64_t chunk0, int tile,
                             uint64_t delta) {
@@ -2870,7 +2881,24 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
   if (st != DQ_OK) return st;
   invalidate(f);
   if (total_rec) {
-    const int64_t per = f->tile / 32;  // a record's count becomes at most 32 records
+    // a record's count becomes count_digits(count) <= 32 records: tiles of tile / max digits
+    // records never overflow a chunk (a 32x bound sized a marginal of 1e8 groups at 60+ GB)
+    int maxd = 32;
+    {
+      DevBuf<unsigned int> md;
+      HIP_TRY(md.ensure(1));
+      HIP_TRY(hipMemsetAsync(md.p, 0, 4, f->stream));
+      hipLaunchKernelGGL(freq_max_digits, dim3(grid_for(total_rec)), dim3(256), 0, f->stream,
+                         reinterpret_cast<const RecIn*>(records), total_rec, md.p);
+      HIP_TRY(hipGetLastError());
+      unsigned int h = 32;
+      HIP_TRY(hipMemcpyAsync(&h, md.p, 4, hipMemcpyDeviceToHost, f->stream));
+      HIP_TRY(hipStreamSynchronize(f->stream));
+      maxd = std::max(1, (int)std::min(h, 32u));
+    }
+    // (and at most one record per thread: the records path runs one round per tile)
+    const int64_t per = std::min<int64_t>(f->tile / maxd, AKeys<false, true>::kThreads);
+    static_assert(AKeys<false, true>::kThreads == AKeys<true, true>::kThreads, "one round");
     const int64_t chunks = phaseA_chunks(!f->exact, true, total_rec, per, nullptr);
     st = ensure_chunks(f, chunks);
     if (st != DQ_OK) return st;
