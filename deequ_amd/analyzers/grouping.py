@@ -251,7 +251,8 @@ def compute_frequencies(data, grouping_columns: Sequence[str],
                         num_rows: Optional[int] = None) -> FrequenciesAndNumRows:
     """FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:53-80)."""
     types = [data.schema[c].dtype for c in grouping_columns]
-    table = FrequencyTable(grouping_columns, types, data.device_index())
+    table = FrequencyTable(grouping_columns, types, data.device_index(),
+                           capacity_hint=data.num_rows)  # sized once: no growth copies
     for batch in data.batches:
         table.add([batch[c] for c in grouping_columns])
     n = num_rows if num_rows is not None else data.count()
@@ -665,7 +666,7 @@ class Histogram(Analyzer):
             st = compute_frequencies_distributed(data, [self.column], null_as_group=True)
             return HistogramState(st.frequencies, st.num_rows, dtype, self.binning_udf)
         total = data.count()
-        table = FrequencyTable([self.column], [dtype], data.device_index())
+        table = FrequencyTable([self.column], [dtype], data.device_index(), capacity_hint=total)
         for batch in data.batches:
             table.add([batch[self.column]], null_as_group=True)
         return HistogramState(table, total, dtype, self.binning_udf)

@@ -1471,3 +1471,103 @@ extern "C" dq_status dq_column_from_arrow(const struct ArrowArray* array,
   out->data = type == DQ_UTF8 ? static_cast<const uint8_t*>(array->buffers[2]) : nullptr;
   return DQ_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Device memory cache (kernels.h)
+// ------------------------------------------------------------------------------------------------
+#include <mutex>
+
+namespace dq {
+namespace {
+constexpr int kPoolDevices = 64;
+constexpr size_t kPoolRound = 256;                 // small blocks: 256-B granules
+constexpr size_t kPoolBig = 2ULL << 20;            // >= 2 MiB: 2-MiB granules
+constexpr size_t kPoolKeep = 64ULL << 30;          // at most this much cached per device
+struct DevPool {
+  std::mutex m;
+  std::multimap<size_t, void*> free_blocks[kPoolDevices];
+  size_t cached[kPoolDevices] = {0};
+};
+DevPool& dev_pool() {
+  static DevPool* pool = new DevPool;  // lives to process exit (the driver reclaims the memory)
+  return *pool;
+}
+size_t pool_round(size_t b) {
+  const size_t g = b >= kPoolBig ? kPoolBig : kPoolRound;
+  return (b + g - 1) / g * g;
+}
+void release_cached(int dev) {  // caller holds the lock; dev is the current device
+  DevPool& pool = dev_pool();
+  for (auto& kv : pool.free_blocks[dev]) (void)hipFree(kv.second);
+  pool.free_blocks[dev].clear();
+  pool.cached[dev] = 0;
+}
+}  // namespace
+
+hipError_t dev_alloc(void** out, size_t bytes, size_t* got, int* device) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  *device = dev;
+  const size_t want = pool_round(bytes ? bytes : 1);
+  DevPool& pool = dev_pool();
+  if (dev >= 0 && dev < kPoolDevices) {
+    std::lock_guard<std::mutex> lock(pool.m);
+    auto& fl = pool.free_blocks[dev];
+    auto it = fl.lower_bound(want);
+    if (it != fl.end() && it->first <= 2 * want) {
+      *out = it->second;
+      *got = it->first;
+      pool.cached[dev] -= it->first;
+      fl.erase(it);
+      return hipSuccess;
+    }
+  }
+  hipError_t e = hipMalloc(out, want);
+  if (e == hipErrorOutOfMemory && dev >= 0 && dev < kPoolDevices) {
+    (void)hipGetLastError();
+    {
+      std::lock_guard<std::mutex> lock(pool.m);
+      release_cached(dev);
+    }
+    e = hipMalloc(out, want);
+  }
+  *got = e == hipSuccess ? want : 0;
+  return e;
+}
+
+void dev_free(void* p, size_t bytes, int dev) {
+  if (!p) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (dev != cur) (void)hipSetDevice(dev);
+  (void)hipDeviceSynchronize();  // as hipFree: no kernel may still use the block
+  DevPool& pool = dev_pool();
+  bool kept = false;
+  if (dev >= 0 && dev < kPoolDevices && bytes) {
+    std::lock_guard<std::mutex> lock(pool.m);
+    if (pool.cached[dev] + bytes <= kPoolKeep) {
+      pool.free_blocks[dev].emplace(bytes, p);
+      pool.cached[dev] += bytes;
+      kept = true;
+    }
+  }
+  if (!kept) (void)hipFree(p);
+  if (dev != cur) (void)hipSetDevice(cur);
+}
+
+}  // namespace dq
+
+extern "C" void dq_release_cached_memory(void) {
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  int n = 0;
+  (void)hipGetDeviceCount(&n);
+  dq::DevPool& pool = dq::dev_pool();
+  std::lock_guard<std::mutex> lock(pool.m);
+  for (int d = 0; d < n && d < dq::kPoolDevices; ++d) {
+    if (pool.free_blocks[d].empty()) continue;
+    (void)hipSetDevice(d);
+    dq::release_cached(d);
+  }
+  (void)hipSetDevice(cur);
+}

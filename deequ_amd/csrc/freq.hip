@@ -616,25 +616,12 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         const uint64_t h = stash[q * W];
         const uint64_t rep = HASHED ? stash[q * W + 1] : 0;
         const uint64_t c = FROM_REC ? scnt[tid] : 1;
-        res = on ? dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort, !FROM_REC, hslot)
-                 : 0;
+        res = on ? dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort, false, hslot) : 0;
         if (res == 3) wait |= 1u << j;
         else if (res == 2) ++hits;
         else if (!res) count_raw(j, h, c);
       }
-      if constexpr (!FROM_REC) {
-        // the hits' counts (1 per row): one LDS atomic per distinct slot of the wave instead of
-        // one per lane (a low-cardinality key puts every lane on a handful of addresses)
-        uint64_t m = __ballot(res == 2);
-        while (m) {
-          const int leader = __builtin_ctzll(m);
-          const uint32_t ls = (uint32_t)__builtin_amdgcn_readlane((int)hslot, leader);
-          const uint64_t same = __ballot(res == 2 && hslot == ls);
-          if (__lane_id() == leader)
-            atomicAdd((unsigned long long*)&dcnt[ls], (unsigned long long)__popcll(same));
-          m &= ~same;
-        }
-      }
+
       if (probe && j == 0) {
         retry(1u, hits);
         const uint32_t wh = wave_sum(hits);  // every lane: the shuffles need the whole wave
@@ -2339,8 +2326,10 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(f->dev_words.ensure(C_N + 1));
   HIP_TRY(hipMemset(f->dev_words.p, 0, (C_N + 1) * 8));
-  if (capacity_hint > 0) {
-    dq_status st = ensure_chunks(f.get(), (capacity_hint + f->tile - 1) / f->tile);
+  if (capacity_hint > 0) {  // the chunks phase A writes for that many rows (+ per-batch rounding)
+    const int64_t chunks = phaseA_chunks(!f->exact, false, capacity_hint, f->tile, nullptr) +
+                           2 * (capacity_hint >> 24) + 16;
+    dq_status st = ensure_chunks(f.get(), chunks);
     if (st != DQ_OK) return st;
   }
   *out = f.release();

@@ -24,32 +24,51 @@ dq_status fail(dq_status code, const char* fmt, ...);
     }                                                                                        \
   } while (0)
 
+// Device memory cache (api.cpp).  A group-by allocates gigabytes per table; hipMalloc/hipFree of
+// such blocks, once per table and per growth step, cost more than the table's kernels when a run
+// builds twenty tables (configs[4]).  Freed blocks are kept per device and handed out again to
+// requests they cover within 2x; the device is synchronised on free, as hipFree does, so a block
+// is never reused while a kernel still reads it.  On hipMalloc failure the cache is released and
+// the allocation retried.
+hipError_t dev_alloc(void** p, size_t bytes, size_t* got, int* device);
+void dev_free(void* p, size_t bytes, int device);
+
 // Device buffer that grows on demand (contents are not preserved across growth).
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  size_t bytes = 0;
+  int dev = -1;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() {
-    if (p) (void)hipFree(p);
+    if (p) dev_free(p, bytes, dev);
   }
   hipError_t ensure(size_t count) {
     if (count <= n && p) return hipSuccess;
     if (p) {
-      (void)hipFree(p);
+      dev_free(p, bytes, dev);
       p = nullptr;
-      n = 0;
+      n = bytes = 0;
     }
     if (count == 0) count = 1;
-    hipError_t e = hipMalloc(&p, count * sizeof(T));
-    if (e == hipSuccess) n = count;
+    void* q = nullptr;
+    size_t got = 0;
+    hipError_t e = dev_alloc(&q, count * sizeof(T), &got, &dev);
+    if (e == hipSuccess) {
+      p = static_cast<T*>(q);
+      bytes = got;
+      n = got / sizeof(T);
+    }
     return e;
   }
   void swap(DevBuf& o) {
     std::swap(p, o.p);
     std::swap(n, o.n);
+    std::swap(bytes, o.bytes);
+    std::swap(dev, o.dev);
   }
 };
 

@@ -393,6 +393,11 @@ dq_status dq_freq_add_records_device(dq_freq* freq, const dq_freq_record* record
                                      const int64_t* src_var_bytes, int64_t num_rows,
                                      const int64_t* special, int null_as_group, void* hip_stream);
 
+/* Returns the device blocks the engine keeps cached for reuse (every dq_* buffer is handed back
+ * to a per-device cache when freed, so building many tables does not hipMalloc / hipFree
+ * gigabytes each time) to the HIP runtime. */
+void dq_release_cached_memory(void);
+
 /* Spark 2.2 Cast(StringType -> LongType | DoubleType) of a utf8 column, on the device: the
  * ColumnProfiler's cast of string columns inferred numeric (profiles/ColumnProfiler.scala:311-320,
  * 389-405).  to_type DQ_INT64 follows UTF8String.toLong (sign, digits, '.' + digits truncated);

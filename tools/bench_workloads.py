@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch-rows", type=int, default=1 << 26)
     ap.add_argument("--runner", action="store_true", help="c3: time AnalysisRunner itself")
+    ap.add_argument("--pyprof", action="store_true", help="cProfile one extra step (stderr)")
     args = ap.parse_args()
     import torch
     dev = "cuda:0"
@@ -175,6 +176,18 @@ def main():
 
     for _ in range(args.warmup):
         res = step()
+    if args.pyprof:
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        step()
+        torch.cuda.synchronize(dev)
+        pr.disable()
+        buf = io.StringIO()
+        pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(40)
+        print(buf.getvalue(), file=sys.stderr)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
