@@ -696,13 +696,39 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
 // ------------------------------------------------------------------------------------------------
 // Finalize: transpose the chunk histograms, scan them per bucket
 // ------------------------------------------------------------------------------------------------
+// Non-empty chunks, in order: a low-cardinality key leaves almost every tile's chunk empty (its
+// rows collapse in phase A's LDS table), and finalize then runs over the non-empty ones only.
+// C1 counts per 1024 chunks, freq_part_scan turns the counts into offsets, C2 writes the ids.
+__global__ void __launch_bounds__(kThreads) freq_chunk_count(const uint16_t* hist, int64_t n,
+                                                             unsigned long long* bcount) {
+  __shared__ uint32_t s_wave[kThreads / 64];
+  const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const uint32_t f = c < n && hist[c * kHistRow + kBuckets] != 0 ? 1u : 0u;
+  uint32_t tot;
+  block_excl_scan(f, s_wave, tot);
+  if (threadIdx.x == 0) bcount[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(kThreads) freq_chunk_ids(const uint16_t* hist, int64_t n,
+                                                           const unsigned long long* boff,
+                                                           uint32_t* ids) {
+  __shared__ uint32_t s_wave[kThreads / 64];
+  const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const uint32_t f = c < n && hist[c * kHistRow + kBuckets] != 0 ? 1u : 0u;
+  uint32_t tot;
+  const uint32_t pos = block_excl_scan(f, s_wave, tot);
+  if (f) ids[boff[blockIdx.x] + pos] = (uint32_t)c;
+}
+
+// cmap (optional): the chunk each of the n rows stands for (the non-empty chunks, in order)
 __global__ void __launch_bounds__(256) freq_hist_transpose(const uint16_t* hist, int64_t n,
-                                                           uint16_t* lenT, uint16_t* offT) {
+                                                           const uint32_t* cmap, uint16_t* lenT,
+                                                           uint16_t* offT) {
   __shared__ uint16_t tile[64][kHistRow + 1];
   const int64_t c0 = (int64_t)blockIdx.x * 64;
   for (int idx = threadIdx.x; idx < 64 * kHistRow; idx += 256) {
     const int cc = idx / kHistRow, b = idx % kHistRow;
-    tile[cc][b] = c0 + cc < n ? hist[(c0 + cc) * kHistRow + b] : 0;
+    const int64_t c = c0 + cc;
+    tile[cc][b] = c < n ? hist[(cmap ? (int64_t)cmap[c] : c) * kHistRow + b] : 0;
   }
   __syncthreads();
   for (int idx = threadIdx.x; idx < kBuckets * 64; idx += 256) {
@@ -778,6 +804,7 @@ __global__ void __launch_bounds__(256) freq_unit_map(const uint32_t* prefT, int6
 // ------------------------------------------------------------------------------------------------
 struct BArgs {
   const uint8_t* recs;
+  const uint32_t* chunk_id;  // chunk of each (compacted) chunk row, or nullptr: the identity
   const uint16_t* lenT;
   const uint16_t* offT;
   const uint32_t* prefT;
@@ -827,13 +854,13 @@ DQ_DEV void for_unit_records(const BArgs& a, UnitLds& L, F&& f) {
     uint32_t wtot;
     const uint32_t pos = block_excl_scan(len, L.s_wave, wtot);
     L.sw_pos[tid] = pos;
-    L.sw_c[tid] = (uint32_t)(c - cw);
+    L.sw_c[tid] = c < c1 ? (a.chunk_id ? a.chunk_id[c] : (uint32_t)c) : 0u;  // the chunk itself
     L.sw_off[tid] = c < c1 ? offb[c] : 0;
     __syncthreads();
     const uint32_t nwin = (uint32_t)min((int64_t)kThreads, c1 - cw);
     for (uint32_t li = tid; li < wtot; li += kThreads) {
       const uint32_t j = seg_of(L.sw_pos, nwin, li);
-      const int64_t rec = (cw + L.sw_c[j]) * FM<HASHED>::kTile + L.sw_off[j] + (li - L.sw_pos[j]);
+      const int64_t rec = (int64_t)L.sw_c[j] * FM<HASHED>::kTile + L.sw_off[j] + (li - L.sw_pos[j]);
       f(reinterpret_cast<const uint64_t*>(a.recs) + rec * W);
     }
     __syncthreads();
@@ -1591,6 +1618,8 @@ struct dq_freq {
   std::vector<unsigned long long> h_bucket_base = std::vector<unsigned long long>(kBuckets + 1, 0);
   std::vector<uint32_t> h_unit_start = std::vector<uint32_t>(kBuckets + 1, 0);
   DevBuf<uint16_t> lenT, offT;
+  DevBuf<uint32_t> chunk_id;               // the non-empty chunks (finalize over those only)
+  DevBuf<unsigned long long> chunk_boff;
   DevBuf<uint32_t> prefT, unit_start, unit_c0, uhist;
   DevBuf<uint16_t> unit_b;
   DevBuf<unsigned long long> totals, part_base;
@@ -1764,7 +1793,29 @@ static dq_status finalize_b(dq_freq* f) {
   dq_status cs = sync_counters(f);
   if (cs != DQ_OK) return cs;
   if (f->b_valid) return DQ_OK;
-  const int64_t n = f->n_chunks;
+  const int64_t n_all = f->n_chunks;
+  // the non-empty chunks (only when that saves a good part of the finalize)
+  int64_t n = n_all;
+  const uint32_t* cmap = nullptr;
+  if (n_all >= 4 * kThreads) {
+    const int64_t nb = (n_all + kThreads - 1) / kThreads;
+    HIP_TRY(f->chunk_id.ensure(n_all));
+    HIP_TRY(f->chunk_boff.ensure(nb + 1));
+    hipLaunchKernelGGL(freq_chunk_count, dim3((unsigned)nb), dim3(kThreads), 0, f->stream,
+                       f->hist.p, n_all, f->chunk_boff.p);
+    hipLaunchKernelGGL(freq_part_scan, dim3(1), dim3(kThreads), 0, f->stream, f->chunk_boff.p, nb);
+    HIP_TRY(hipGetLastError());
+    unsigned long long m = 0;
+    HIP_TRY(hipMemcpyAsync(&m, f->chunk_boff.p + nb, 8, hipMemcpyDeviceToHost, f->stream));
+    HIP_TRY(hipStreamSynchronize(f->stream));
+    if ((int64_t)m * 4 < n_all * 3) {
+      hipLaunchKernelGGL(freq_chunk_ids, dim3((unsigned)nb), dim3(kThreads), 0, f->stream, f->hist.p,
+                         n_all, f->chunk_boff.p, f->chunk_id.p);
+      HIP_TRY(hipGetLastError());
+      n = (int64_t)m;
+      cmap = f->chunk_id.p;
+    }
+  }
   std::fill(f->h_bucket_base.begin(), f->h_bucket_base.end(), 0ULL);
   std::fill(f->h_unit_start.begin(), f->h_unit_start.end(), 0u);
   f->R = 0;
@@ -1781,7 +1832,7 @@ static dq_status finalize_b(dq_freq* f) {
   HIP_TRY(f->prefT.ensure((size_t)kBuckets * (n + 1)));
   HIP_TRY(f->totals.ensure(kBuckets));
   hipLaunchKernelGGL(freq_hist_transpose, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, f->stream,
-                     f->hist.p, n, f->lenT.p, f->offT.p);
+                     f->hist.p, n, cmap, f->lenT.p, f->offT.p);
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(freq_bucket_scan, dim3(kBuckets), dim3(kThreads), 0, f->stream, f->lenT.p, n,
                      f->prefT.p, f->totals.p);
@@ -1845,6 +1896,7 @@ static dq_status finalize_b(dq_freq* f) {
   BArgs a;
   memset(&a, 0, sizeof(a));
   a.recs = f->recs.p;
+  a.chunk_id = cmap;
   a.lenT = f->lenT.p;
   a.offT = f->offT.p;
   a.prefT = f->prefT.p;
