@@ -1413,18 +1413,21 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
   if (collisions) atomicAdd(&a.counters[C_COLLISIONS], collisions);
 }
 
-// Fixed-order sum of the per-partition statistics: out = {groups, unique, entropy bits}.
-__global__ void __launch_bounds__(kThreads) freq_reduce(const unsigned long long* pg,
-                                                        const unsigned long long* pu,
-                                                        const double* pe, int64_t n,
-                                                        unsigned long long* out) {
+// Multi-block fixed-order reduction of the per-partition statistics: block b sums its contiguous
+// range (coalesced: consecutive threads read consecutive partitions), freq_reduce_final adds the
+// blocks' partials in block order.  out = {groups, unique, entropy bits}.
+constexpr int kRedBlocks = 256;
+__global__ void __launch_bounds__(kThreads) freq_reduce_part(const unsigned long long* pg,
+                                                             const unsigned long long* pu,
+                                                             const double* pe, int64_t n,
+                                                             unsigned long long* part) {
   __shared__ uint64_t s_red[kThreads / 64];
   __shared__ double s_redf[kThreads / 64];
-  const int64_t per = (n + kThreads - 1) / kThreads;
-  const int64_t lo = threadIdx.x * per, hi = min(lo + per, n);
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(lo + per, n);
   uint64_t g = 0, u = 0;
   double e = 0.0;
-  for (int64_t i = lo; i < hi; ++i) {
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
     g += pg[i];
     u += pu[i];
     e += pe[i];
@@ -1433,11 +1436,71 @@ __global__ void __launch_bounds__(kThreads) freq_reduce(const unsigned long long
   u = block_sum_u64(u, s_red);
   e = block_sum_f64(e, s_redf);
   if (threadIdx.x == 0) {
-    out[0] = g;
-    out[1] = u;
-    out[2] = __builtin_bit_cast(unsigned long long, e);
+    part[blockIdx.x * 3] = g;
+    part[blockIdx.x * 3 + 1] = u;
+    part[blockIdx.x * 3 + 2] = __builtin_bit_cast(unsigned long long, e);
   }
 }
+__global__ void freq_reduce_final(const unsigned long long* part, int nb, unsigned long long* out) {
+  if (threadIdx.x != 0) return;
+  uint64_t g = 0, u = 0;
+  double e = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    g += part[b * 3];
+    u += part[b * 3 + 1];
+    e += __builtin_bit_cast(double, part[b * 3 + 2]);
+  }
+  out[0] = g;
+  out[1] = u;
+  out[2] = __builtin_bit_cast(unsigned long long, e);
+}
+
+// Multi-block exclusive scan of u64 values in place, v[n] = total (large n; freq_part_scan is the
+// one-block form): S1 block sums of kScanTile values, freq_part_scan over the sums, S2 scans each
+// tile from its offset.
+constexpr int kScanPer = 4;
+constexpr int64_t kScanTile = (int64_t)kThreads * kScanPer;
+__global__ void __launch_bounds__(kThreads) scan_u64_sums(const unsigned long long* v, int64_t n,
+                                                          unsigned long long* bsum) {
+  __shared__ uint64_t s_red[kThreads / 64];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
+  uint64_t t = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k)
+    if (base + k < n) t += v[base + k];
+  t = block_sum_u64(t, s_red);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = t;
+}
+__global__ void __launch_bounds__(kThreads) scan_u64_apply(unsigned long long* v, int64_t n,
+                                                           const unsigned long long* boff) {
+  __shared__ uint64_t s_red[kThreads / 64];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanPer;
+  uint64_t x[kScanPer], t = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    x[k] = base + k < n ? v[base + k] : 0;
+    t += x[k];
+  }
+  // exclusive prefix of t over the block: wave prefix (64-bit) + the waves before
+  const int lane = __lane_id(), wave = threadIdx.x >> 6;
+  uint64_t inc = t;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) s_red[wave] = inc;
+  __syncthreads();
+  uint64_t run = boff[blockIdx.x] + inc - t;
+  for (int w = 0; w < wave; ++w) run += s_red[w];
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    if (base + k < n) v[base + k] = run;
+    run += x[k];
+  }
+  if (base <= n - 1 && n - 1 < base + kScanPer) v[n] = run;  // the thread holding the last value
+}
+
 
 // ------------------------------------------------------------------------------------------------
 // Selection over Group arrays (Histogram top-N), export and repartition helpers
@@ -1619,7 +1682,7 @@ struct dq_freq {
   std::vector<uint32_t> h_unit_start = std::vector<uint32_t>(kBuckets + 1, 0);
   DevBuf<uint16_t> lenT, offT;
   DevBuf<uint32_t> chunk_id;               // the non-empty chunks (finalize over those only)
-  DevBuf<unsigned long long> chunk_boff;
+  DevBuf<unsigned long long> chunk_boff, scan_tmp;
   DevBuf<uint32_t> prefT, unit_start, unit_c0, uhist;
   DevBuf<uint16_t> unit_b;
   DevBuf<unsigned long long> totals, part_base;
@@ -1916,7 +1979,17 @@ static dq_status finalize_b(dq_freq* f) {
   HIP_TRY(hipGetLastError());
   hipLaunchKernelGGL(freq_phaseB_scan, dim3(kBuckets), dim3(kThreads), 0, f->stream, a);
   HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(freq_part_scan, dim3(1), dim3(kThreads), 0, f->stream, f->part_base.p, P);
+  if (P <= 4 * kScanTile) {
+    hipLaunchKernelGGL(freq_part_scan, dim3(1), dim3(kThreads), 0, f->stream, f->part_base.p, P);
+  } else {
+    const int64_t nb = (P + kScanTile - 1) / kScanTile;
+    HIP_TRY(f->scan_tmp.ensure(nb + 1));
+    hipLaunchKernelGGL(scan_u64_sums, dim3((unsigned)nb), dim3(kThreads), 0, f->stream,
+                       f->part_base.p, P, f->scan_tmp.p);
+    hipLaunchKernelGGL(freq_part_scan, dim3(1), dim3(kThreads), 0, f->stream, f->scan_tmp.p, nb);
+    hipLaunchKernelGGL(scan_u64_apply, dim3((unsigned)nb), dim3(kThreads), 0, f->stream,
+                       f->part_base.p, P, f->scan_tmp.p);
+  }
   HIP_TRY(hipGetLastError());
   const unsigned grid = (u + 7) / 8 * 8;
   if (f->exact)
@@ -2043,8 +2116,14 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     }
     if (clk) (void)hipFree(clk);
   }
-  hipLaunchKernelGGL(freq_reduce, dim3(1), dim3(kThreads), 0, f->stream, f->part_groups.p,
-                     f->part_unique.p, f->part_entropy.p, P, f->red.p);
+  HIP_TRY(f->scan_tmp.ensure(kRedBlocks * 3));
+  {
+    const unsigned nbr = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kRedBlocks, (P + kThreads - 1) / kThreads));
+    hipLaunchKernelGGL(freq_reduce_part, dim3(nbr), dim3(kThreads), 0, f->stream, f->part_groups.p,
+                       f->part_unique.p, f->part_entropy.p, P, f->scan_tmp.p);
+    hipLaunchKernelGGL(freq_reduce_final, dim3(1), dim3(64), 0, f->stream, f->scan_tmp.p, (int)nbr,
+                       f->red.p);
+  }
   HIP_TRY(hipGetLastError());
   unsigned long long r[4];
   HIP_TRY(hipStreamSynchronize(f->stream));
