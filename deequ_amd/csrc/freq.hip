@@ -300,7 +300,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   // Counting sort of a chunk's records: bucket counts are in bh; begin_chunk scans them, writes
   // the chunk's histogram row and reserves the chunk's arena bytes; records then go straight to
   // their place in the chunk region (a 64 KB region: the runs meet in L2).
-  auto begin_chunk = [&](int64_t chunk, uint64_t arena_need) {
+  auto begin_chunk = [&](int64_t chunk, uint64_t arena_need) -> uint32_t {
     __syncthreads();
     uint32_t total;
     const uint32_t mine = tid < kBuckets ? bh[tid] : 0u;
@@ -319,6 +319,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
       }
     }
     __syncthreads();
+    return total;
   };
   auto end_chunk = [&]() {
     __syncthreads();
@@ -652,16 +653,42 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         if ((raw >> j) & 1u) need += row_enc_size(a.ks, (int64_t)stash[(j * kThreads + tid) * W + 1]);
     }
     // 3. counting sort of the raw rows into the tile's chunk
-    begin_chunk(t, need);
+    const uint32_t ctotal = begin_chunk(t, need);
     mark(t, 3);
+    if constexpr (!HASHED && !FROM_REC) {
+      // exact rows (count 1: one record each): sorted in LDS over the stash, then written out as
+      // one contiguous 16-byte-store stream (scattered 8-byte global stores were ~half the tile)
+      uint64_t rv[ROUNDS];
+      uint32_t pv[ROUNDS];
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        if (!((raw >> j) & 1u)) continue;
+        const uint64_t h = stash[j * kThreads + tid];
+        pv[j] = atomicAdd(&bcur[bucket_of(h)], 1u);
+        rv[j] = (h << 8) | 1u;  // the count-1 digit code (for_digits(1))
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j)
+        if ((raw >> j) & 1u) stash[pv[j]] = rv[j];
+      __syncthreads();
+      uint64_t* out = reinterpret_cast<uint64_t*>(a.recs) + t * (int64_t)T;
+      const uint32_t pairs = ctotal >> 1;
+      for (uint32_t i = tid; i < pairs; i += kThreads) {
+        const ulonglong2 v = make_ulonglong2(stash[2 * i], stash[2 * i + 1]);
+        reinterpret_cast<ulonglong2*>(out)[i] = v;
+      }
+      if ((ctotal & 1u) && tid == 0) out[ctotal - 1] = stash[ctotal - 1];
+    } else {
 #pragma unroll 1
-    for (int j = 0; j < ROUNDS; ++j) {
-      if (!((raw >> j) & 1u)) continue;
-      const int q = j * kThreads + tid;
-      const uint64_t h = stash[q * W];
-      uint64_t rep = HASHED ? stash[q * W + 1] : 0;
-      if constexpr (HASHED && !FROM_REC) rep = arena_rep((int64_t)rep);
-      for_digits(FROM_REC ? scnt[tid] : 1, [&](uint32_t code) { put(t, h, code, rep); });
+      for (int j = 0; j < ROUNDS; ++j) {
+        if (!((raw >> j) & 1u)) continue;
+        const int q = j * kThreads + tid;
+        const uint64_t h = stash[q * W];
+        uint64_t rep = HASHED ? stash[q * W + 1] : 0;
+        if constexpr (HASHED && !FROM_REC) rep = arena_rep((int64_t)rep);
+        for_digits(FROM_REC ? scnt[tid] : 1, [&](uint32_t code) { put(t, h, code, rep); });
+      }
     }
     end_chunk();
     mark(t, 4);
