@@ -957,28 +957,94 @@ __global__ void __launch_bounds__(kThreads) freq_part_scan(unsigned long long* v
   (void)s_wave;
 }
 
-// B3: scatter every record of the unit to its partition
+// B3: scatter every record of the unit to its partition, staged in LDS: each round of up to SUB
+// records is counting-sorted by sub-bucket in LDS, then written out in staged order, so the lanes
+// of a wave write runs of neighbouring addresses (a sub-bucket's records of the round) instead of
+// 64 scattered 8-byte stores to 64 partitions.
 template <bool HASHED>
 __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter(BArgs a) {
   constexpr int W = FM<HASHED>::kRB / 8;
+  constexpr int SUB = 8192 / W;  // records per round (64 KB staged)
+  constexpr int PER = SUB / kThreads;
+  constexpr int SMAX = 1 << kMaxSubBits;
   __shared__ UnitLds L;
-  __shared__ unsigned long long cur[1 << kMaxSubBits];
+  __shared__ unsigned long long cur[SMAX];  // the unit's next output position per sub-bucket
+  __shared__ unsigned long long gbs[SMAX];  // this round's output base per sub-bucket
+  __shared__ uint32_t hcnt[SMAX];           // this round's count, then local base, per sub-bucket
+  __shared__ uint64_t staged[SUB * W];
+  __shared__ uint16_t ssb[SUB];
   // XCD-contiguous units: workgroup g runs on XCD g % 8; XCD x takes units [x*q, (x+1)*q)
   const uint32_t g = blockIdx.x, q = (a.n_units + 7) / 8;
   const uint32_t w = (g & 7u) * q + (g >> 3);
   if (w >= a.n_units) return;
   const int S = 1 << a.s;
+  const int tid = threadIdx.x;
   unit_range(a, w, L);
   const uint32_t* row = a.uhist + (int64_t)w * S;
-  for (int i = threadIdx.x; i < S; i += kThreads)
-    cur[i] = a.part_base[(uint64_t)L.s_b * S + i] + row[i];
-  __syncthreads();
+  for (int i = tid; i < S; i += kThreads) cur[i] = a.part_base[(uint64_t)L.s_b * S + i] + row[i];
   uint64_t* out = reinterpret_cast<uint64_t*>(a.recsB);
-  for_unit_records<HASHED>(a, L, [&](const uint64_t* r) {
-    const unsigned long long pos = atomicAdd(&cur[rec_sub(r, a.s, HASHED)], 1ULL);
-    out[pos * W] = r[0];
-    if (HASHED) out[pos * W + 1] = r[1];
-  });
+  const int64_t n = a.n_chunks, c0 = L.s_c0, c1 = L.s_c1;
+  const uint16_t* lenb = a.lenT + (int64_t)L.s_b * n;
+  const uint16_t* offb = a.offT + (int64_t)L.s_b * n;
+  for (int64_t cw = c0; cw < c1; cw += kThreads) {  // windows of chunk segments
+    const int64_t c = cw + tid;
+    const uint32_t len = c < c1 ? lenb[c] : 0u;
+    uint32_t wtot;
+    const uint32_t pos = block_excl_scan(len, L.s_wave, wtot);
+    L.sw_pos[tid] = pos;
+    L.sw_c[tid] = c < c1 ? (a.chunk_id ? a.chunk_id[c] : (uint32_t)c) : 0u;
+    L.sw_off[tid] = c < c1 ? offb[c] : 0;
+    const uint32_t nwin = (uint32_t)min((int64_t)kThreads, c1 - cw);
+    for (uint32_t base = 0; base < wtot; base += SUB) {
+      const uint32_t nr = min((uint32_t)SUB, wtot - base);
+      for (int i = tid; i < S; i += kThreads) hcnt[i] = 0;
+      __syncthreads();
+      uint64_t rv[PER][W];
+      uint32_t sbv[PER], lpos[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint32_t r = (uint32_t)k * kThreads + tid;
+        sbv[k] = 0;
+        if (r >= nr) continue;
+        const uint32_t li = base + r;
+        const uint32_t j = seg_of(L.sw_pos, nwin, li);
+        const int64_t rec = (int64_t)L.sw_c[j] * FM<HASHED>::kTile + L.sw_off[j] + (li - L.sw_pos[j]);
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + rec * W;
+#pragma unroll
+        for (int x = 0; x < W; ++x) rv[k][x] = src[x];
+        sbv[k] = rec_sub(rv[k], a.s, HASHED);
+        lpos[k] = atomicAdd(&hcnt[sbv[k]], 1u);
+      }
+      __syncthreads();
+      const uint32_t cnt = tid < S ? hcnt[tid] : 0u;
+      uint32_t tot;
+      const uint32_t ex = block_excl_scan(cnt, L.s_wave, tot);  // (barriers: every count is read)
+      if (tid < S) {
+        hcnt[tid] = ex;
+        gbs[tid] = cur[tid];
+        cur[tid] += cnt;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const uint32_t r = (uint32_t)k * kThreads + tid;
+        if (r >= nr) continue;
+        const uint32_t slot = hcnt[sbv[k]] + lpos[k];
+#pragma unroll
+        for (int x = 0; x < W; ++x) staged[slot * W + x] = rv[k][x];
+        ssb[slot] = (uint16_t)sbv[k];
+      }
+      __syncthreads();
+      for (uint32_t i = tid; i < nr; i += kThreads) {
+        const uint32_t sb = ssb[i];
+        const unsigned long long d = gbs[sb] + (i - hcnt[sb]);
+#pragma unroll
+        for (int x = 0; x < W; ++x) out[d * W + x] = staged[i * W + x];
+      }
+      __syncthreads();
+    }
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
