@@ -1,0 +1,58 @@
+"""Per-kernel summary of the configs[2] PMC passes (tools/gpu_pmc_c3.sh, 1e8 rows, one step).
+
+Usage: python tools/summarize_c3_pmc.py TAG
+  reads  gpurun_out/{pmcf,pmcw,pmc,pmc2}_c3_TAG/*_counter_collection.csv
+  writes profiles/TAG/c3_counters.json: per dq:: kernel, the summed counters over its dispatches,
+         HBM bytes (FETCH_SIZE KiB x 1024, reported raw and x2 per MI355X_MICROARCH.md §HBM --
+         the halving is calibrated only for 16-B-per-lane streaming reads; these kernels read
+         8-B records, so both are given), WRITE_SIZE bytes, and the SQ wave-state fractions.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1]
+    src = os.path.join(ROOT, "gpurun_out")
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for pas in ("pmcf", "pmcw", "pmc", "pmc2"):
+        for path in glob.glob(os.path.join(src, f"{pas}_c3_{tag}", "*_counter_collection.csv")):
+            for r in csv.DictReader(open(path)):
+                if not r["Kernel_Name"].startswith(("dq::", "void dq::")):
+                    continue
+                k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+                acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                disp[k].add((pas, r["Dispatch_Id"]))
+    out = {}
+    for k, c in acc.items():
+        d = {name: v for name, v in c.items()}
+        if "FETCH_SIZE" in c:
+            d["fetch_bytes_raw"] = c["FETCH_SIZE"] * 1024
+            d["fetch_bytes_x2"] = 2 * c["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in c:
+            d["write_bytes"] = c["WRITE_SIZE"] * 1024
+        if c.get("SQ_WAVE_CYCLES"):
+            for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if n in c:
+                    d[n + "_frac"] = c[n] / c["SQ_WAVE_CYCLES"]
+        out[k] = d
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    json.dump({"tag": tag, "workload": "c3 --rows 100000000 --steps 1 --warmup 0",
+               "kernels": out}, open(os.path.join(dst, "c3_counters.json"), "w"), indent=1)
+    for k in sorted(out, key=lambda k: -out[k].get("fetch_bytes_raw", 0)):
+        d = out[k]
+        print(k[:48].ljust(48), {x: round(d[x] / 1e9, 3) for x in ("fetch_bytes_raw", "write_bytes")
+                                 if x in d},
+              {x: round(d[x], 2) for x in d if x.endswith("_frac")})
+
+
+if __name__ == "__main__":
+    main()
