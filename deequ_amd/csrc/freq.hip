@@ -287,6 +287,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     dkey[i] = kEmptyKey;
     dcnt[i] = 0;
     if (HASHED) drep[i] = kNotReady;
+    if (SK) dsk1[i] = kShortNotReady;
   }
   for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
   if (tid == 0) s_bypass = 0;
@@ -337,9 +338,10 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     }
   };
   auto arena_rep = [&](int64_t row) -> uint64_t {  // hashed rows: copy the key into the arena
-    const uint32_t sz = row_enc_size(a.ks, row);
+    const uint32_t sz = STR1 ? str1_enc_size(a.ks, row) : row_enc_size(a.ks, row);
     const uint64_t off = s_arena_base + atomicAdd(&s_arena_cur, (unsigned long long)sz);
-    row_encode(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
+    if constexpr (STR1) str1_encode(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
+    else row_encode(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
     return off;
   };
   // LDS dedupe: 0 = not counted (table full), 1 = claimed a new slot, 2 = added to an existing
@@ -352,6 +354,13 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
     for (int pr = 0; pr < 4; ++pr) {
       uint64_t k = lds_load(&dkey[slot]);
+      // short utf8 keys: the slot's short form is read beside its key, so a hit costs two LDS
+      // round trips (key + dsk1, then dsk0) instead of four.  A claimer writes the key, dsk0,
+      // then (released) dsk1, and every field is written once: a dsk1 other than
+      // kShortNotReady is final, and dsk0 read after it (acquire) is too.
+      const uint64_t b1 = SK ? __hip_atomic_load(&dsk1[slot], __ATOMIC_ACQUIRE,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+      const uint64_t b0 = SK ? lds_load(&dsk0[slot]) : 0;
       bool claimed = false;
       if (k == kEmptyKey) {
         const uint64_t prev = atomicCAS((unsigned long long*)&dkey[slot], kEmptyKey, h);
@@ -361,7 +370,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
       if (claimed) {
         if constexpr (SK) {
           lds_store(&dsk0[slot], k0);
-          lds_store(&dsk1[slot], k1);
+          __hip_atomic_store(&dsk1[slot], k1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the short key before drep
         }
         if (HASHED) lds_store(&drep[slot], rep);
@@ -371,21 +380,27 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
       if (k == h) {
         bool same = true;
         if constexpr (HASHED) {
-          const uint64_t r2 = lds_load(&drep[slot]);
-          if (r2 == kNotReady) {  // being claimed right now (another lane / wave)
+          if (SK && b1 == kShortNotReady) {  // being claimed right now (another lane / wave)
             atomicAdd(&s_dbg[0], 1u);
             return 3;
           }
-          if (r2 != rep) {
-            if constexpr (SK) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            const uint64_t b1 = SK ? lds_load(&dsk1[slot]) : kNoShort;
-            if (k1 != kNoShort || b1 != kNoShort)
-              same = k1 == b1 && k0 == lds_load(&dsk0[slot]);
-            else if constexpr (FROM_REC)
-              same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
-                               reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
-            else
-              same = rows_equal(a.ks, (int64_t)r2, (int64_t)rep);
+          if (SK && (k1 != kNoShort || b1 != kNoShort)) {
+            same = k1 == b1 && k0 == b0;
+          } else {
+            const uint64_t r2 = lds_load(&drep[slot]);
+            if (r2 == kNotReady) {  // being claimed right now (another lane / wave)
+              atomicAdd(&s_dbg[0], 1u);
+              return 3;
+            }
+            if (r2 != rep) {
+              if constexpr (FROM_REC)
+                same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
+                                 reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
+              else if constexpr (STR1)
+                same = str1_rows_equal(a.ks, (int64_t)r2, (int64_t)rep);
+              else
+                same = rows_equal(a.ks, (int64_t)r2, (int64_t)rep);
+            }
           }
           if (!same) atomicAdd(&s_dbg[1], 1u);
         }
@@ -535,7 +550,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
             h = str_row_hash_reg(w0, w1, len[j]);
             str_short_key_reg(w0, w1, len[j], k0, k1);
           } else {
-            h = str_row_hash(SView{c.data + s0[j], len[j]});
+            h = str_row_hash_long(c.data + s0[j], len[j]);
           }
         } else {
           // a NULL row.  Histogram: the NULL rows are one group kept apart (C_NULL_GROUP), so
@@ -650,7 +665,10 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     if constexpr (HASHED && !FROM_REC) {
 #pragma unroll 1
       for (int j = 0; j < ROUNDS; ++j)
-        if ((raw >> j) & 1u) need += row_enc_size(a.ks, (int64_t)stash[(j * kThreads + tid) * W + 1]);
+        if ((raw >> j) & 1u) {
+          const int64_t row = (int64_t)stash[(j * kThreads + tid) * W + 1];
+          need += STR1 ? str1_enc_size(a.ks, row) : row_enc_size(a.ks, row);
+        }
     }
     // 3. counting sort of the raw rows into the tile's chunk
     const uint32_t ctotal = begin_chunk(t, need);
@@ -700,7 +718,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     if (k == kEmptyKey) continue;
     const uint32_t b = bucket_of(k);
     for_digits(dcnt[sl], [&](uint32_t) { atomicAdd(&bh[b], 1u); });
-    if constexpr (HASHED && !FROM_REC) need += row_enc_size(a.ks, (int64_t)drep[sl]);
+    if constexpr (HASHED && !FROM_REC)
+      need += STR1 ? str1_enc_size(a.ks, (int64_t)drep[sl]) : row_enc_size(a.ks, (int64_t)drep[sl]);
   }
   const int64_t fchunk = n_tiles + blockIdx.x;
   begin_chunk(fchunk, need);
@@ -866,11 +885,13 @@ DQ_DEV void unit_range(const BArgs& a, uint32_t w, UnitLds& L) {
   __syncthreads();
 }
 
-// Calls f(record pointer) for every record of the unit (chunk segments of bucket s_b in
-// [s_c0, s_c1)).  Every thread of the block must call it.
+// Calls f(record words) for every record of the unit (chunk segments of bucket s_b in
+// [s_c0, s_c1)).  Every thread of the block must call it.  Each thread loads PB records before
+// it uses any (one HBM round trip per PB records; an out-of-range lane re-reads the window's last
+// record and drops it).
 template <bool HASHED, typename F>
 DQ_DEV void for_unit_records(const BArgs& a, UnitLds& L, F&& f) {
-  constexpr int W = FM<HASHED>::kRB / 8;
+  constexpr int W = FM<HASHED>::kRB / 8, PB = 8;
   const int tid = threadIdx.x;
   const int64_t n = a.n_chunks, c0 = L.s_c0, c1 = L.s_c1;
   const uint16_t* lenb = a.lenT + (int64_t)L.s_b * n;
@@ -885,10 +906,21 @@ DQ_DEV void for_unit_records(const BArgs& a, UnitLds& L, F&& f) {
     L.sw_off[tid] = c < c1 ? offb[c] : 0;
     __syncthreads();
     const uint32_t nwin = (uint32_t)min((int64_t)kThreads, c1 - cw);
-    for (uint32_t li = tid; li < wtot; li += kThreads) {
-      const uint32_t j = seg_of(L.sw_pos, nwin, li);
-      const int64_t rec = (int64_t)L.sw_c[j] * FM<HASHED>::kTile + L.sw_off[j] + (li - L.sw_pos[j]);
-      f(reinterpret_cast<const uint64_t*>(a.recs) + rec * W);
+    for (uint32_t base = 0; base < wtot; base += (uint32_t)PB * kThreads) {
+      uint64_t rv[PB][W];
+#pragma unroll
+      for (int k = 0; k < PB; ++k) {
+        uint32_t li = base + (uint32_t)k * kThreads + tid;
+        li = li < wtot ? li : wtot - 1;
+        const uint32_t j = seg_of(L.sw_pos, nwin, li);
+        const int64_t rec = (int64_t)L.sw_c[j] * FM<HASHED>::kTile + L.sw_off[j] + (li - L.sw_pos[j]);
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + rec * W;
+#pragma unroll
+        for (int x = 0; x < W; ++x) rv[k][x] = src[x];
+      }
+#pragma unroll
+      for (int k = 0; k < PB; ++k)
+        if (base + (uint32_t)k * kThreads + tid < wtot) f(rv[k]);
     }
     __syncthreads();
   }
@@ -961,10 +993,12 @@ __global__ void __launch_bounds__(kThreads) freq_part_scan(unsigned long long* v
 // records is counting-sorted by sub-bucket in LDS, then written out in staged order, so the lanes
 // of a wave write runs of neighbouring addresses (a sub-bucket's records of the round) instead of
 // 64 scattered 8-byte stores to 64 partitions.
-template <bool HASHED>
+// SUBB: staged bytes' worth of 8-byte words per round (8192: 64 KB staged, one workgroup per
+// CU; 4096: 32 KB, two per CU so one's loads overlap the other's sort and stores)
+template <bool HASHED, int SUBB = 8192>
 __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter(BArgs a) {
   constexpr int W = FM<HASHED>::kRB / 8;
-  constexpr int SUB = 8192 / W;  // records per round (64 KB staged)
+  constexpr int SUB = SUBB / W;  // records per round
   constexpr int PER = SUB / kThreads;
   constexpr int SMAX = 1 << kMaxSubBits;
   __shared__ UnitLds L;
@@ -1164,6 +1198,13 @@ DQ_DEV void c_fetch(const CArgs& a, int wi, const CBounds& bd, CItem<HASHED>& it
   }
 }
 
+// -(c/n) ln(c/n), out of line: the statistics pass calls it from every unrolled slot, and inlined
+// copies of log() there made phase C several times larger than the instruction cache holds
+__device__ __attribute__((noinline)) double entropy_term(uint64_t c, double n) {
+  const double pr = (double)c / n;
+  return -pr * log(pr);
+}
+
 // Per work item: the inserts, then ONE pass over the LDS table that reads every slot once for
 // the statistics, the Histogram candidates (kept in registers) and the lit probe, and clears it
 // for the next item (when the groups are materialised, the output pass clears instead).  The
@@ -1199,11 +1240,19 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     s_top[tid][0] = s_top[tid][1] = 0;
   }
   if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
+  // exact mode fetches records two items ahead: item i + 2's loads are in flight through all of
+  // item i + 1 (one item's inserts and reduction are shorter than an HBM round trip under load).
+  // Hashed mode has no registers for it and fetches one item ahead.
+  constexpr int kAhead = HASHED ? 1 : 2;
   CBounds nb;
-  CItem<HASHED> cur;
+  CItem<HASHED> cur, nxt;
   c_bounds(a, blockIdx.x, nb);
   c_fetch<HASHED>(a, blockIdx.x, nb, cur);
   c_bounds(a, blockIdx.x + gridDim.x, nb);
+  if constexpr (kAhead == 2) {
+    c_fetch<HASHED>(a, blockIdx.x + gridDim.x, nb, nxt);
+    c_bounds(a, blockIdx.x + 2 * gridDim.x, nb);
+  }
   __syncthreads();
 
   uint32_t par = 0;
@@ -1239,13 +1288,10 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       }
       uint32_t slot = HASHED ? (uint32_t)(((uint64_t)(uint32_t)h * KT) >> 32) : ((uint32_t)h & (KT - 1));
       for (int probe = 0; probe < KT; ++probe) {
-        uint64_t k = lds_load(&tkey[slot]);
-        bool claimed = false;
-        if (k == kEmptyKey) {
-          const uint64_t prev = atomicCAS((unsigned long long*)&tkey[slot], kEmptyKey, h);
-          if (prev == kEmptyKey) claimed = true;
-          else k = prev;
-        }
+        // compare-and-swap first: it returns the slot's key, so a claim (most records of a
+        // mostly-unique key) costs one LDS round trip instead of a load and then the swap
+        const uint64_t k = atomicCAS((unsigned long long*)&tkey[slot], kEmptyKey, h);
+        const bool claimed = k == kEmptyKey;
         if (claimed) {
           if (HASHED) lds_store(&trep[slot], rep);
           atomicAdd((unsigned long long*)&tcnt[slot], (unsigned long long)c);
@@ -1328,8 +1374,14 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     mark(1);
     // the table is final.  Next item's records (bounds already here) and the bounds after it are
     // in flight while this one is reduced; the other parity's flags are reset for it.
-    c_fetch<HASHED>(a, wi + gridDim.x, nb, cur);
-    c_bounds(a, wi + 2 * gridDim.x, nb);
+    if constexpr (kAhead == 2) {
+      cur = nxt;
+      c_fetch<HASHED>(a, wi + 2 * gridDim.x, nb, nxt);
+      c_bounds(a, wi + 3 * gridDim.x, nb);
+    } else {
+      c_fetch<HASHED>(a, wi + gridDim.x, nb, cur);
+      c_bounds(a, wi + 2 * gridDim.x, nb);
+    }
     if (tid == 0) {
       s_ovf[par ^ 1u] = 0;
       s_spec_cnt[par ^ 1u] = 0;
@@ -1350,10 +1402,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     uint64_t tc[kCand], tk[kCand], tr[kCand];
 #pragma unroll
     for (int q = 0; q < kCand; ++q) tc[q] = tk[q] = tr[q] = 0;
-    auto term = [&](uint64_t c) {
-      const double pr = (double)c / a.num_rows;
-      return -pr * log(pr);
-    };
+    auto term = [&](uint64_t c) { return entropy_term(c, a.num_rows); };
     auto count_group = [&](uint64_t c) {
       ++g;
       if (c == 1) ++un;  // the common count: a register, not an LDS atomic on one address
@@ -1390,7 +1439,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
         if (a.lit_count && k == a.lit_h && enc_is_null_literal(a.arena + r))
           atomicAdd(a.lit_count, (unsigned long long)c);
       count_group(c);
-      if (cand) offer(c, k, r);
+      // (a branch, not selects: with mostly-unique keys nearly every slot fails the first test)
+      if (cand && c > tc[kCand - 1]) offer(c, k, r);
     }
     if (tid == 0 && sc && !overflow) {
       count_group(sc);
@@ -2085,10 +2135,21 @@ static dq_status finalize_b(dq_freq* f) {
   }
   HIP_TRY(hipGetLastError());
   const unsigned grid = (u + 7) / 8 * 8;
-  if (f->exact)
-    hipLaunchKernelGGL(freq_phaseB_scatter<false>, dim3(grid), dim3(kThreads), 0, f->stream, a);
-  else
-    hipLaunchKernelGGL(freq_phaseB_scatter<true>, dim3(grid), dim3(kThreads), 0, f->stream, a);
+  static const int bsub = [] {  // DQ_FREQ_BSUB: A/B hook for the phase-B3 round size
+    const char* e = getenv("DQ_FREQ_BSUB");
+    return e && atoi(e) == 8192 ? 8192 : 4096;
+  }();
+  if (f->exact) {
+    if (bsub == 8192)
+      hipLaunchKernelGGL((freq_phaseB_scatter<false, 8192>), dim3(grid), dim3(kThreads), 0, f->stream, a);
+    else
+      hipLaunchKernelGGL((freq_phaseB_scatter<false, 4096>), dim3(grid), dim3(kThreads), 0, f->stream, a);
+  } else {
+    if (bsub == 8192)
+      hipLaunchKernelGGL((freq_phaseB_scatter<true, 8192>), dim3(grid), dim3(kThreads), 0, f->stream, a);
+    else
+      hipLaunchKernelGGL((freq_phaseB_scatter<true, 4096>), dim3(grid), dim3(kThreads), 0, f->stream, a);
+  }
   HIP_TRY(hipGetLastError());
   f->b_valid = true;
   return DQ_OK;

@@ -101,26 +101,11 @@ struct MemBytes {
   DQ_HD uint32_t u8(int64_t o) const { return p[o]; }
 };
 
-// Byte reader over up to 16 bytes held in two registers (w0 = bytes 0..7, w1 = bytes 8..15,
-// little-endian): xxh_bytes of a short string whose bytes were loaded ahead of the hashing.
-struct RegBytes {
-  uint64_t w0, w1;
-  DQ_HD uint64_t at(int64_t o) const {  // bytes o .. o + 7 (zero past byte 15), 0 <= o <= 15
-    if (o == 0) return w0;
-    if (o < 8) return (w0 >> (8 * o)) | (w1 << (64 - 8 * o));
-    return w1 >> (8 * (o - 8));
-  }
-  DQ_HD uint64_t u64(int64_t o) const { return at(o); }
-  DQ_HD uint32_t u32(int64_t o) const { return (uint32_t)at(o); }
-  DQ_HD uint32_t u8(int64_t o) const { return (uint32_t)(at(o) & 0xffu); }
-};
-
 // "NullValue" (Histogram.NullFieldReplacement, Histogram.scala:108) as constants: a string view
 // with p == nullptr IS this literal, so no code path needs memory for it.
 constexpr int32_t kNullValueLen = 9;
 constexpr uint64_t kNullValueLo = 0x756c61566c6c754eULL;  // "NullValu", little-endian
 constexpr uint32_t kNullValueHi = 0x65u;                   // "e"
-constexpr uint64_t kNullValueXxh17 = 0xf45f7c0db790929eULL; // XXH64("NullValue", seed 17)
 
 struct SView {
   const uint8_t* p;  // nullptr: the "NullValue" literal
@@ -187,8 +172,37 @@ DQ_HD uint64_t row_hash_exact(const KeySet& ks, int64_t r) { return fmix_bij(exa
 // folded with an XXH64 merge step, then fmix.
 constexpr uint64_t kRowHashSeed = 0x243F6A8885A308D3ULL;
 DQ_HD uint64_t fold_col_hash(uint64_t h, uint64_t ch) { return rotl64(h ^ ch, 27) * P1 + P4; }
+// Column hash of a string of at most 16 bytes held in (w0, w1) (little-endian, zero past its
+// end): two odd multiplies, no loop and no data-dependent branch, so the lanes of a wave hashing
+// strings of different lengths never diverge.  For a fixed (w1, len) the map w0 -> hash is a
+// bijection; the row hash (fold_col_hash, fmix_bij) adds the avalanche.  (Only the group-by uses
+// it: the value is internal to the frequency table, never a reference-visible hash.)
+constexpr int32_t kHash16Max = 16;
+DQ_HD uint64_t str_hash16(uint64_t w0, uint64_t w1, int32_t len, uint64_t seed) {
+  const uint64_t a = rotl64(w0 * P1 + seed, 31);
+  const uint64_t b = (w1 + (uint64_t)len * P5) * P2;
+  return a ^ b;
+}
+// (w0, w1) of a string of at most 16 bytes in memory, bytewise (a host build reads no byte past
+// the string)
+DQ_HD void mem_str16(const uint8_t* p, int32_t len, uint64_t& w0, uint64_t& w1) {
+  w0 = w1 = 0;
+  for (int32_t q = 0; q < len; ++q) {
+    if (q < 8) w0 |= (uint64_t)p[q] << (8 * q);
+    else w1 |= (uint64_t)p[q] << (8 * (q - 8));
+  }
+}
+DQ_HD uint64_t str_bytes_hash(const uint8_t* p, int32_t len, int k) {
+  if (len <= kHash16Max) {
+    uint64_t w0, w1;
+    mem_str16(p, len, w0, w1);
+    return str_hash16(w0, w1, len, 17 + k);
+  }
+  return xxh_bytes(MemBytes{p}, (int64_t)len, 17 + k);
+}
 DQ_HD uint64_t str_col_hash(const SView& v, int k) {
-  return v.p ? xxh_bytes(MemBytes{v.p}, (int64_t)v.len, 17 + k) : kNullValueXxh17;
+  return v.p ? str_bytes_hash(v.p, v.len, k)
+             : str_hash16(kNullValueLo, kNullValueHi, kNullValueLen, 17 + k);
 }
 
 DQ_HD uint64_t row_hash_hashed(const KeySet& ks, int64_t r) {
@@ -210,9 +224,15 @@ DQ_HD uint64_t row_hash_hashed(const KeySet& ks, int64_t r) {
 
 // The row hash of a one-column utf8 key (row_hash_hashed with n_keys == 1).
 DQ_HD uint64_t str_row_hash(const SView& v) { return fmix_bij(fold_col_hash(kRowHashSeed, str_col_hash(v, 0))); }
+// The same, out of line, for phase A's strings longer than 16 bytes (rare in a wave; one copy of
+// the XXH64 loop instead of one per unrolled round)
+__host__ __device__ __attribute__((noinline)) uint64_t str_row_hash_long(const uint8_t* p,
+                                                                         int32_t len) {
+  return str_row_hash(SView{p, len});
+}
 // The same for a non-NULL string of len <= 16 bytes already in registers.
 DQ_HD uint64_t str_row_hash_reg(uint64_t w0, uint64_t w1, int32_t len) {
-  return fmix_bij(fold_col_hash(kRowHashSeed, xxh_bytes(RegBytes{w0, w1}, (int64_t)len, 17)));
+  return fmix_bij(fold_col_hash(kRowHashSeed, str_hash16(w0, w1, len, 17)));
 }
 
 // Short form of a one-column utf8 key of at most 15 bytes: (k0, k1) = its bytes 0..7 and
@@ -221,6 +241,7 @@ DQ_HD uint64_t str_row_hash_reg(uint64_t w0, uint64_t w1, int32_t len) {
 // key.  A NULL in Histogram mode is the 9-byte "NullValue" literal and gets that string's short
 // form, so it meets a real "NullValue" string in LDS (Histogram.scala:59-66).
 constexpr uint64_t kNoShort = ~0ULL;
+constexpr uint64_t kShortNotReady = 0xFEULL << 56;  // top byte 0xFE: never a short form
 constexpr int32_t kShortMax = 15;
 DQ_HD void str_short_key_reg(uint64_t w0, uint64_t w1, int32_t len, uint64_t& k0, uint64_t& k1) {
   if (len > kShortMax) {
@@ -380,6 +401,33 @@ DQ_HD bool rows_equal(const KeySet& ks, int64_t r1, int64_t r2) {
   return true;
 }
 
+// The same three for a key of one utf8 column at a non-NULL row (phase A's one-string-column
+// path): what the generic forms compute for such a row, without their per-type code.
+DQ_HD SView str1_view(const KeySet& ks, int64_t r) {
+  const int32_t* off = reinterpret_cast<const int32_t*>(ks.cols[0].values);
+  const int32_t s = off[r];
+  return SView{ks.cols[0].data + s, off[r + 1] - s};
+}
+DQ_HD uint32_t str1_enc_size(const KeySet& ks, int64_t r) {
+  return 8 + pad4((uint32_t)str1_view(ks, r).len);
+}
+DQ_HD void str1_encode(const KeySet& ks, int64_t r, uint32_t* dst) {
+  const SView v = str1_view(ks, r);
+  dst[0] = 1;
+  dst[1] = (uint32_t)v.len;
+  for (int32_t q = 0; q < v.len; q += 4) {
+    uint32_t w = 0;
+    for (int b = 0; b < 4 && q + b < v.len; ++b) w |= (uint32_t)v.p[q + b] << (8 * b);
+    dst[2 + q / 4] = w;
+  }
+}
+// (out of line: only long strings get here, so one copy instead of one per call site)
+__host__ __device__ __attribute__((noinline)) bool str1_rows_equal(const KeySet& ks, int64_t r1,
+                                                                   int64_t r2) {
+  const SView a = str1_view(ks, r1), b = str1_view(ks, r2);
+  return a.len == b.len && bytes_equal(a.p, b.p, a.len);
+}
+
 // Size in bytes of an encoded key.
 DQ_HD uint32_t enc_size(const uint32_t* enc, const int32_t* types, int n_keys) {
   uint32_t w = 0;
@@ -409,7 +457,7 @@ DQ_HD uint64_t enc_hash(const uint32_t* enc, const int32_t* types, int n_keys) {
     uint64_t ch;
     if (types[k] == DQ_UTF8) {
       const uint32_t len = tag ? enc[w++] : 0;
-      ch = xxh_bytes(MemBytes{reinterpret_cast<const uint8_t*>(enc + w)}, (int64_t)len, 17 + k);
+      ch = str_bytes_hash(reinterpret_cast<const uint8_t*>(enc + w), (int32_t)len, k);
       w += pad4(len) / 4;
     } else {
       uint64_t v = 0;
