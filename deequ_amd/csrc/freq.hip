@@ -1313,7 +1313,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
             return true;
           }
         }
-        slot = slot + 1 == (uint32_t)KT ? 0u : slot + 1;
+        if constexpr ((KT & (KT - 1)) == 0) slot = (slot + 1) & (KT - 1);
+        else slot = slot + 1 == (uint32_t)KT ? 0u : slot + 1;
       }
       *ovf = 1;  // table full
       return true;
