@@ -622,13 +622,49 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         wait &= ~rounds_mask;
       }
     };
+    // One-string-column keys: a batched first probe of every round's home slot, with all rounds'
+    // LDS reads in flight together (two LDS round trips for the thread's rows instead of two per
+    // row in sequence), counts the rows whose short key already sits in its home slot -- nearly
+    // every row of a low-cardinality column; the rest take the full dedupe below.  (Not on
+    // probing tiles, whose round 0 decides the bypass for the rest.)
+    uint32_t fast = 0;  // bit j: round j was counted here
+    if constexpr (STR1) {
+      if (!probe && !s_bypass) {
+        uint64_t hk[ROUNDS], kk[ROUNDS], b1[ROUNDS], b0[ROUNDS], k0v[ROUNDS], k1v[ROUNDS];
+        uint32_t sl[ROUNDS];
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) {
+          const int q = j * kThreads + tid;
+          hk[j] = stash[q * W];
+          sl[j] = (uint32_t)(hk[j] >> 20) & (D - 1);
+          kk[j] = lds_load(&dkey[sl[j]]);
+          b1[j] = lds_load(&dsk1[sl[j]]);
+          k0v[j] = ssk0[q];
+          k1v[j] = ssk1[q];
+        }
+        // dsk1 is written (released) after dsk0: a final dsk1 read before this fence makes the
+        // dsk0 read after it final too
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) b0[j] = lds_load(&dsk0[sl[j]]);
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) {
+          const bool hit = ((keyed >> j) & 1u) && hk[j] != kEmptyKey && kk[j] == hk[j] &&
+                           k1v[j] != kNoShort && b1[j] == k1v[j] && b0[j] == k0v[j];
+          if (hit) {
+            atomicAdd((unsigned long long*)&dcnt[sl[j]], 1ULL);
+            fast |= 1u << j;
+          }
+        }
+      }
+    }
 #pragma unroll 1
     for (int j = 0; j < ROUNDS; ++j) {
       const int q = j * kThreads + tid;
       const bool on = probe && j == 0 ? true : !s_bypass;
       uint32_t hits = 0, hslot = 0;
       int res = -1;
-      if ((keyed >> j) & 1u) {
+      if (((keyed & ~fast) >> j) & 1u) {
         const uint64_t h = stash[q * W];
         const uint64_t rep = HASHED ? stash[q * W + 1] : 0;
         const uint64_t c = FROM_REC ? scnt[tid] : 1;
