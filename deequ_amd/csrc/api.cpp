@@ -724,6 +724,12 @@ struct dq_state {
   int64_t rows = 0;
   bool host_dirty = false;   // host mirror newer than device (after merge / deserialize / reset)
   bool synced = true;        // host mirror reflects every scanned batch
+  // pinned staging of the host mirror: resets upload it and syncs read it back with async copies
+  // on the state's stream and one stream synchronisation, instead of pageable hipMemcpy calls
+  // that each block the host
+  void* h_pin = nullptr;
+  size_t h_pin_cap = 0;
+  bool pin_pending = false;  // an async copy from h_pin may still be queued
   // device
   DevBuf<Acc> d_acc, d_partial, d_partial2;
   DevBuf<uint8_t> d_hll;
@@ -770,15 +776,52 @@ static void host_reset(dq_state* s) {
   s->synced = true;
 }
 
+// Pinned staging of at least `bytes` (the caller has set the device).
+static dq_status pin_ensure(dq_state* s, size_t bytes) {
+  if (s->h_pin_cap >= bytes) return DQ_OK;
+  if (s->pin_pending) {
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    s->pin_pending = false;
+  }
+  if (s->h_pin) (void)hipHostFree(s->h_pin);
+  s->h_pin = nullptr;
+  s->h_pin_cap = 0;
+  HIP_TRY(hipHostMalloc(&s->h_pin, bytes, hipHostMallocDefault));
+  s->h_pin_cap = bytes;
+  return DQ_OK;
+}
+
 static dq_status upload_host(dq_state* s) {
   if (!s->host_dirty || s->device < 0) return DQ_OK;
   HIP_TRY(hipSetDevice(s->device));
-  if (!s->acc.empty())
-    HIP_TRY(hipMemcpy(s->d_acc.p, s->acc.data(), s->acc.size() * sizeof(Acc), hipMemcpyHostToDevice));
-  if (!s->hll.empty())
-    HIP_TRY(hipMemcpy(s->d_hll.p, s->hll.data(), s->hll.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemset(s->d_queue.p, 0, kQueueWords * sizeof(uint32_t)));
-  HIP_TRY(hipMemset(s->d_hll_stage.p, 0, s->d_hll_stage.n * sizeof(uint32_t)));
+  const size_t ab = s->acc.size() * sizeof(Acc), hb = s->hll.size();
+  if (!s->stream_set) {  // no stream yet: blocking copies (the first scan may use any stream)
+    if (ab) HIP_TRY(hipMemcpy(s->d_acc.p, s->acc.data(), ab, hipMemcpyHostToDevice));
+    if (hb) HIP_TRY(hipMemcpy(s->d_hll.p, s->hll.data(), hb, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(s->d_queue.p, 0, kQueueWords * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(s->d_hll_stage.p, 0, s->d_hll_stage.n * sizeof(uint32_t)));
+    s->host_dirty = false;
+    return DQ_OK;
+  }
+  // on the state's stream, ordered before the next scan: no host wait
+  if (s->pin_pending) HIP_TRY(hipStreamSynchronize(s->stream));  // h_pin is about to be rewritten
+  s->pin_pending = false;
+  {
+    const dq_status ps = pin_ensure(s, ab + hb);
+    if (ps != DQ_OK) return ps;
+  }
+  uint8_t* pin = static_cast<uint8_t*>(s->h_pin);
+  if (ab) {
+    memcpy(pin, s->acc.data(), ab);
+    HIP_TRY(hipMemcpyAsync(s->d_acc.p, pin, ab, hipMemcpyHostToDevice, s->stream));
+  }
+  if (hb) {
+    memcpy(pin + ab, s->hll.data(), hb);
+    HIP_TRY(hipMemcpyAsync(s->d_hll.p, pin + ab, hb, hipMemcpyHostToDevice, s->stream));
+  }
+  s->pin_pending = ab + hb > 0;
+  HIP_TRY(hipMemsetAsync(s->d_queue.p, 0, kQueueWords * sizeof(uint32_t), s->stream));
+  HIP_TRY(hipMemsetAsync(s->d_hll_stage.p, 0, s->d_hll_stage.n * sizeof(uint32_t), s->stream));
   s->host_dirty = false;
   return DQ_OK;
 }
@@ -888,6 +931,7 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
 extern "C" void dq_state_destroy(dq_state* state) {
   if (!state) return;
   if (state->stream_set && state->device >= 0) (void)hipStreamSynchronize(state->stream);
+  if (state->h_pin) (void)hipHostFree(state->h_pin);
   delete state;
 }
 
@@ -1251,11 +1295,19 @@ extern "C" dq_status dq_state_sync(dq_state* s) {
   if (!s) return fail(DQ_ERR_INVALID_ARGUMENT, "null state");
   if (s->synced || s->device < 0) return DQ_OK;
   HIP_TRY(hipSetDevice(s->device));
+  // both read-backs queued behind the scan on its stream, one host wait
+  const size_t ab = s->acc.size() * sizeof(Acc), hb = s->hll.size();
+  {
+    const dq_status ps = pin_ensure(s, ab + hb);
+    if (ps != DQ_OK) return ps;
+  }
+  uint8_t* pin = static_cast<uint8_t*>(s->h_pin);
+  if (ab) HIP_TRY(hipMemcpyAsync(pin, s->d_acc.p, ab, hipMemcpyDeviceToHost, s->stream));
+  if (hb) HIP_TRY(hipMemcpyAsync(pin + ab, s->d_hll.p, hb, hipMemcpyDeviceToHost, s->stream));
   HIP_TRY(hipStreamSynchronize(s->stream));
-  if (!s->acc.empty())
-    HIP_TRY(hipMemcpy(s->acc.data(), s->d_acc.p, s->acc.size() * sizeof(Acc), hipMemcpyDeviceToHost));
-  if (!s->hll.empty())
-    HIP_TRY(hipMemcpy(s->hll.data(), s->d_hll.p, s->hll.size(), hipMemcpyDeviceToHost));
+  s->pin_pending = false;
+  if (ab) memcpy(s->acc.data(), pin, ab);
+  if (hb) memcpy(s->hll.data(), pin + ab, hb);
   s->synced = true;
   return DQ_OK;
 }

@@ -119,14 +119,25 @@ def get_plan(schema, specs: Sequence[AggSpec]) -> Plan:
 
 
 def column_array(table, plan: Plan):
-    """dq_column[n_batches][n_cols] for every batch of the table."""
+    """dq_column[n_batches][n_cols] for every batch of the table.  Built once per (table, plan)
+    and kept on the table, keyed by the batch objects (a batch's buffers do not change once
+    built): rebuilding the ctypes descriptors of every column of every batch cost tens of
+    microseconds per scan."""
     n_cols = len(plan.types)
     n_b = len(table.batches)
+    cache = table.__dict__.setdefault("_column_arrays", {})
+    key = (id(plan), n_cols)
+    hit = cache.get(key)
+    # (the entry holds the plan and the batches themselves, so their ids cannot be reused)
+    if (hit is not None and hit[0] is plan and len(hit[2]) == n_b
+            and all(x is y for x, y in zip(hit[2], table.batches))):
+        return hit[1], n_cols, n_b
     arr = (N.dq_column * max(1, n_b * n_cols))()
     names = table.schema.field_names
     for b, batch in enumerate(table.batches):
         for c, name in enumerate(names):
             arr[b * n_cols + c] = batch[name].to_c()
+    cache[key] = (plan, arr, tuple(table.batches))
     return arr, n_cols, n_b
 
 
