@@ -994,24 +994,35 @@ scan_mixed_kernel(const TaskDesc* __restrict__ tasks, int n_desc, uint32_t n_ord
   }
 }
 
-// Item range [lo, hi) of logical task `task` (descriptors are numbered task-major).
-DQ_DEV void task_range(const TaskDesc* tasks, int n_desc, int task, int64_t& lo, int64_t& hi,
-                       int& kind, int& hll_out) {
-  lo = -1;
-  hi = -1;
-  kind = 0;
-  hll_out = -1;
-  for (int d = 0; d < n_desc; ++d) {
+// Item range [lo, hi) of logical task `task` (descriptors are numbered task-major), kind and HLL
+// register file, with the block's threads reading the descriptors in parallel (every thread of the
+// block must call it): a one-thread walk is a chain of dependent scalar loads, tens of
+// microseconds per finalize launch at S10's 60 descriptors.
+DQ_DEV void task_range_block(const TaskDesc* tasks, int n_desc, int task, int64_t& lo, int64_t& hi,
+                             int& kind, int& hll_out) {
+  __shared__ unsigned long long s_lo, s_hi;
+  __shared__ int s_kind, s_hll;
+  if (threadIdx.x == 0) {
+    s_lo = ~0ULL;
+    s_hi = 0;
+    s_kind = 0;
+    s_hll = -1;
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < n_desc; d += blockDim.x) {
     const TaskDesc& t = tasks[d];
     if (t.out != task) continue;
-    if (lo < 0) {
-      lo = t.item_begin;
-      kind = t.kind;
-      hll_out = t.hll_out;
-    }
-    hi = t.item_begin + t.n_items;
+    atomicMin(&s_lo, (unsigned long long)t.item_begin);
+    atomicMax(&s_hi, (unsigned long long)(t.item_begin + t.n_items));
+    s_kind = t.kind;  // (one value per task: every descriptor of the task carries it)
+    s_hll = t.hll_out;
   }
-  if (lo < 0) lo = hi = 0;
+  __syncthreads();
+  lo = s_lo == ~0ULL ? 0 : (int64_t)s_lo;
+  hi = s_lo == ~0ULL ? 0 : (int64_t)s_hi;
+  kind = s_kind;
+  hll_out = s_hll;
+  __syncthreads();  // (the shared cells may be reused by a later call)
 }
 
 // Stage 1: workgroup (task, f) merges slice f of the task's item partials; thread i takes items
@@ -1024,7 +1035,7 @@ __global__ void __launch_bounds__(kBlock) finalize1_kernel(const TaskDesc* __res
   const int task = blockIdx.x, f = blockIdx.y;
   int64_t lo, hi;
   int kind, hll_out;
-  task_range(tasks, n_desc, task, lo, hi, kind, hll_out);
+  task_range_block(tasks, n_desc, task, lo, hi, kind, hll_out);
   Acc a;
   acc_init(kind, a);
   if (kind != TK_HLL) {
@@ -1052,7 +1063,7 @@ __global__ void __launch_bounds__(64) finalize2_kernel(const TaskDesc* __restric
   const int task = blockIdx.x;
   int64_t lo, hi;
   int kind, hll_out;
-  task_range(tasks, n_desc, task, lo, hi, kind, hll_out);
+  task_range_block(tasks, n_desc, task, lo, hi, kind, hll_out);
   if (kind == TK_HLL) {
     for (int reg = threadIdx.x; reg < kHllM; reg += blockDim.x) {
       const int64_t i = (int64_t)hll_out * kHllM + reg;
@@ -1060,10 +1071,20 @@ __global__ void __launch_bounds__(64) finalize2_kernel(const TaskDesc* __restric
       hll_acc[i] = (uint8_t)(v > m ? v : m);
       hll_stage[i] = 0;
     }
-  } else if (kind != 0 && threadIdx.x == 0) {
-    Acc r = acc[task];
-    for (int f = 0; f < kFinParts; ++f) acc_merge(kind, r, partial2[(int64_t)task * kFinParts + f]);
-    acc[task] = r;
+  } else if (kind != 0) {  // (block-uniform) the slices in a fixed tree, then into the running
+    __shared__ Acc sh2[kFinParts];  // accumulator: parallel, and the same order on every run
+    static_assert(kFinParts <= 64 && (kFinParts & (kFinParts - 1)) == 0, "one wave, power of 2");
+    if (threadIdx.x < kFinParts) sh2[threadIdx.x] = partial2[(int64_t)task * kFinParts + threadIdx.x];
+    __syncthreads();
+    for (int s = kFinParts / 2; s > 0; s >>= 1) {
+      if (threadIdx.x < s) acc_merge(kind, sh2[threadIdx.x], sh2[threadIdx.x + s]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      Acc r = acc[task];
+      acc_merge(kind, r, sh2[0]);
+      acc[task] = r;
+    }
   }
   if (task == 0)
     for (int i = threadIdx.x; i < kQueues * kQueueHeads; i += blockDim.x) queue[i * kQueueStride] = 0u;
