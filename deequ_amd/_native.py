@@ -99,6 +99,7 @@ def _load() -> ctypes.CDLL:
                                            c_void_p]),
         "dq_state_sync": (c_int, [c_void_p]),
         "dq_state_get": (c_int, [c_void_p, c_int, POINTER(dq_value)]),
+        "dq_state_get_all": (c_int, [c_void_p, c_int, POINTER(dq_value)]),
         "dq_state_merge": (c_int, [c_void_p, c_void_p]),
         "dq_state_serialized_size": (c_int64, [c_void_p]),
         "dq_state_serialize": (c_int, [c_void_p, c_void_p, c_int64]),
@@ -158,7 +159,7 @@ EXPORTED = [
     "dq_last_error", "dq_version", "dq_device_count", "dq_column_from_arrow", "dq_plan_create",
     "dq_plan_destroy", "dq_plan_explain", "dq_plan_launches_per_batch", "dq_state_create",
     "dq_state_destroy", "dq_state_reset", "dq_scan_device", "dq_scan_device_batches",
-    "dq_state_sync", "dq_state_get", "dq_state_merge", "dq_state_serialized_size",
+    "dq_state_sync", "dq_state_get", "dq_state_get_all", "dq_state_merge", "dq_state_serialized_size",
     "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_freq_create",
     "dq_freq_destroy", "dq_freq_reset", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_summarize_keys", "dq_sorted_sample", "dq_freq_marginal", "dq_freq_mutual_information", "dq_freq_num_groups", "dq_freq_null_literal", "dq_freq_import", "dq_cast_utf8", "dq_release_cached_memory",
     "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge", "dq_freq_topk", "dq_loader_create",

@@ -1395,6 +1395,15 @@ extern "C" dq_status dq_state_get(const dq_state* s, int agg_index, dq_value* ou
   return DQ_OK;
 }
 
+extern "C" dq_status dq_state_get_all(const dq_state* s, int n, dq_value* out) {
+  if (!s || (!out && n > 0)) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  for (int k = 0; k < n; ++k) {
+    const dq_status st = dq_state_get(s, k, out + k);
+    if (st != DQ_OK) return st;
+  }
+  return DQ_OK;
+}
+
 extern "C" dq_status dq_state_merge(dq_state* dst, const dq_state* src) {
   if (!dst || !src) return fail(DQ_ERR_INVALID_ARGUMENT, "null state");
   if (dst->plan != src->plan) return fail(DQ_ERR_STATE, "states belong to different plans");

@@ -156,12 +156,12 @@ def scan_into(table, plan: Plan, state, stream=None) -> None:
 
 def read_row(plan: Plan, state) -> List[object]:
     N.check(N.lib.dq_state_sync(state))
-    row: List[object] = []
-    v = N.dq_value()
-    for i, spec in enumerate(plan.specs):
-        N.check(N.lib.dq_state_get(state, i, ctypes.byref(v)))
-        row.append(decode_value(spec.kind, v))
-    return row
+    n = len(plan.specs)
+    vals = plan.__dict__.get("_values")
+    if vals is None or len(vals) != max(1, n):
+        vals = plan.__dict__["_values"] = (N.dq_value * max(1, n))()
+    N.check(N.lib.dq_state_get_all(state, n, vals))
+    return [decode_value(spec.kind, vals[i]) for i, spec in enumerate(plan.specs)]
 
 
 def decode_value(kind: int, v: "N.dq_value"):

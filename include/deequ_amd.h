@@ -249,6 +249,9 @@ typedef struct dq_value {
   uint64_t words[52];
 } dq_value;
 dq_status dq_state_get(const dq_state* state, int agg_index, dq_value* out);
+/* dq_state_get for aggregations 0 .. n-1 into out[0 .. n-1] in one call (the per-step result
+ * read-out of a scan: one foreign call instead of one per aggregation). */
+dq_status dq_state_get_all(const dq_state* state, int n, dq_value* out);
 
 /* dst += src for two synced states of one plan: Spark's partial-aggregation merge of every
  * aggregation buffer -- what happens between the partitions of ONE Spark job, and here between
