@@ -347,9 +347,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   // LDS dedupe: 0 = not counted (table full), 1 = claimed a new slot, 2 = added to an existing
   // slot, 3 = the key's slot is being claimed: retry after the next barrier
   static_assert(!STR1 || (HASHED && !FROM_REC), "STR1 is the row path of a utf8 key");
-  // defer: a hit (2) only reports its slot in hit_slot; the caller adds the count (wave-aggregated)
-  auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep, uint64_t k0, uint64_t k1, bool defer,
-                    uint32_t& hit_slot) -> int {
+  auto dedupe = [&](uint64_t h, uint64_t c, uint64_t rep, uint64_t k0, uint64_t k1) -> int {
     if (h == kEmptyKey) return 0;
     uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
     for (int pr = 0; pr < 4; ++pr) {
@@ -405,8 +403,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
           if (!same) atomicAdd(&s_dbg[1], 1u);
         }
         if (same) {
-          if (defer) hit_slot = slot;
-          else atomicAdd((unsigned long long*)&dcnt[slot], c);
+          atomicAdd((unsigned long long*)&dcnt[slot], c);
           return 2;
         }
       }
@@ -610,9 +607,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
             const int q = j * kThreads + tid;
             const uint64_t h = stash[q * W], rep = stash[q * W + 1];
             const uint64_t c = FROM_REC ? scnt[tid] : 1;
-            uint32_t unused = 0;
-            const int res = dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort, false,
-                                   unused);
+            const int res = dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort);
             if (res == 3) continue;
             w &= ~(1u << j);
             if (res == 2) ++hits;
@@ -662,13 +657,13 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     for (int j = 0; j < ROUNDS; ++j) {
       const int q = j * kThreads + tid;
       const bool on = probe && j == 0 ? true : !s_bypass;
-      uint32_t hits = 0, hslot = 0;
+      uint32_t hits = 0;
       int res = -1;
       if (((keyed & ~fast) >> j) & 1u) {
         const uint64_t h = stash[q * W];
         const uint64_t rep = HASHED ? stash[q * W + 1] : 0;
         const uint64_t c = FROM_REC ? scnt[tid] : 1;
-        res = on ? dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort, false, hslot) : 0;
+        res = on ? dedupe(h, c, rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort) : 0;
         if (res == 3) wait |= 1u << j;
         else if (res == 2) ++hits;
         else if (!res) count_raw(j, h, c);
