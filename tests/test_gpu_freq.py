@@ -357,3 +357,36 @@ def test_histogram_shares_string_table_with_grouping(k, gpu_device):
     assert got == want
     for key, v in dist.values.items():
         assert hist[key] == v.absolute and v.ratio == v.absolute / n
+
+
+@pytest.mark.parametrize("distinct", [40, 5000])
+def test_short_string_keys_of_every_length(distinct, gpu_device):
+    """One utf8 key column whose values have every length 0..24, embedded NUL bytes and shared
+    prefixes ("a", "a\\0", "a\\0\\0", ...): the branch-free hash of strings <= 16 bytes, the
+    short-key LDS comparisons and the batched first probe of the one-string phase A must keep
+    every distinct string its own group.  60k rows span many phase-A tiles per workgroup, so the
+    low-cardinality case runs the non-probing tiles' fast path.  Bar: exported frequencies equal
+    the oracle's exactly."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    rng = np.random.default_rng(distinct)
+    base = ["", "a", "a\x00", "a\x00\x00", "\x00", "\x00a", "ab" * 4, "ab" * 4 + "\x00",
+            "x" * 15, "x" * 16, "x" * 17, "y" * 24, "NullValue"]
+    vocab = list(base)
+    while len(vocab) < distinct:
+        k = int(rng.integers(0, 25))
+        vocab.append("".join(chr(int(c)) for c in rng.integers(0, 3, k)))  # bytes 0..2
+    vocab = sorted(set(vocab))
+    n = 60_000
+    vals = [vocab[i] for i in rng.integers(0, len(vocab), n)]
+    mask = rng.random(n) < 0.03
+    t = pa.table({"s": pa.array([None if m else v for v, m in zip(vals, mask)],
+                                type=pa.string())})
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=1 << 14)
+    ft = FrequencyTable(["s"], [df.schema["s"].dtype], 0, capacity_hint=n)
+    for b in df.batches:
+        ft.add([b["s"]])
+    ot = O.OTable({"s": t.column("s").to_pylist()}, {"s": "string"})
+    assert dict(ft.export()) == O.frequencies(ot, ["s"])
+    assert ft.num_rows == n
