@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 from ctypes import (POINTER, Structure, c_char, c_char_p, c_double, c_int, c_int32, c_int64,
-                    c_size_t, c_uint8, c_uint64, c_void_p)
+                    c_float, c_size_t, c_uint8, c_uint64, c_void_p)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DQ_LIB_PATH: diagnostic A/B builds only (tools/); the product loads the in-tree library
@@ -106,6 +106,8 @@ def _load() -> ctypes.CDLL:
         "dq_state_deserialize": (c_int, [c_void_p, c_void_p, c_int64]),
         "dq_hll_count": (c_double, [POINTER(c_uint64), POINTER(c_int)]),
         "dq_xxhash64": (c_uint64, [c_void_p, c_int64, c_uint64]),
+        "dq_java_double_to_string": (c_int, [c_double, c_char_p]),
+        "dq_java_float_to_string": (c_int, [c_float, c_char_p]),
         "dq_freq_create": (c_int, [c_int, c_int, POINTER(c_int32), c_int64, POINTER(c_void_p)]),
         "dq_freq_destroy": (None, [c_void_p]),
         "dq_freq_reset": (c_int, [c_void_p, c_void_p]),
@@ -160,7 +162,7 @@ EXPORTED = [
     "dq_plan_destroy", "dq_plan_explain", "dq_plan_launches_per_batch", "dq_state_create",
     "dq_state_destroy", "dq_state_reset", "dq_scan_device", "dq_scan_device_batches",
     "dq_state_sync", "dq_state_get", "dq_state_get_all", "dq_state_merge", "dq_state_serialized_size",
-    "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_freq_create",
+    "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_java_double_to_string", "dq_java_float_to_string", "dq_freq_create",
     "dq_freq_destroy", "dq_freq_reset", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_summarize_keys", "dq_sorted_sample", "dq_freq_marginal", "dq_freq_mutual_information", "dq_freq_num_groups", "dq_freq_null_literal", "dq_freq_import", "dq_cast_utf8", "dq_release_cached_memory",
     "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge", "dq_freq_topk", "dq_loader_create",
     "dq_loader_destroy", "dq_loader_stage", "dq_loader_release", "dq_scan_host",
@@ -190,3 +192,41 @@ def hll_count(words) -> tuple:
 def xxhash64(data: bytes, seed: int = 42) -> int:
     buf = ctypes.create_string_buffer(data, len(data))
     return int(lib.dq_xxhash64(buf, len(data), seed))
+
+
+def java_double_to_string(d: float) -> str:
+    """Double.toString(d) -- the formatter the device uses (jfmt.h), run on the host."""
+    buf = ctypes.create_string_buffer(32)
+    n = lib.dq_java_double_to_string(d, buf)
+    return buf.raw[:n].decode("ascii")
+
+
+def java_float_to_string(f: float) -> str:
+    """Float.toString(f) -- the formatter the device uses (jfmt.h), run on the host."""
+    buf = ctypes.create_string_buffer(32)
+    n = lib.dq_java_float_to_string(f, buf)
+    return buf.raw[:n].decode("ascii")
+
+
+def release_cached_memory() -> None:
+    """Frees the engine's cached device blocks (dev_alloc's pool) and torch's cached blocks, so
+    either allocator can reclaim memory the other one holds idle."""
+    lib.dq_release_cached_memory()
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+
+
+def retry_on_oom(fn, *args, **kwargs):
+    """Runs an idempotent device allocation / call; when torch or the engine runs out of device
+    memory, releases both caches and runs it once more (the second failure propagates)."""
+    import torch
+    try:
+        return fn(*args, **kwargs)
+    except torch.OutOfMemoryError:
+        pass
+    except EngineError as e:
+        if e.code != ERR_OUT_OF_MEMORY:
+            raise
+    release_cached_memory()
+    return fn(*args, **kwargs)

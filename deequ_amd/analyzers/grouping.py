@@ -501,43 +501,15 @@ MAXIMUM_ALLOWED_DETAIL_BINS = 1000
 
 
 def java_double_to_string(d: float) -> str:
-    """Java Double.toString formatting (Spark 2.2 Cast(DoubleType -> StringType)) using the
-    shortest round-trip digits."""
-    if math.isnan(d):
-        return "NaN"
-    if math.isinf(d):
-        return "Infinity" if d > 0 else "-Infinity"
-    if d == 0.0:
-        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
-    return _java_fmt(repr(float(d)), abs(d))
+    """Java Double.toString (Spark 2.2 Cast(DoubleType -> StringType)): the formatter the device
+    runs for PatternMatch over a double column (csrc/jfmt.h: shortest round-trip digits, Java's
+    plain / E-notation layout).  JDK 8's few non-shortest outputs are parity unpinned (jfmt.h)."""
+    return N.java_double_to_string(float(d))
 
 
 def java_float_to_string(f: float) -> str:
-    if math.isnan(f):
-        return "NaN"
-    if math.isinf(f):
-        return "Infinity" if f > 0 else "-Infinity"
-    if f == 0.0:
-        return "-0.0" if math.copysign(1.0, f) < 0 else "0.0"
-    digits = np.format_float_scientific(np.float32(f), unique=True, trim="-")
-    return _java_fmt(digits, abs(f))
-
-
-def _java_fmt(py: str, mag: float) -> str:
-    from decimal import Decimal
-    dec = Decimal(py)
-    sign = "-" if dec < 0 else ""
-    dec = abs(dec)
-    t = dec.as_tuple()
-    digits = "".join(map(str, t.digits)).rstrip("0") or "0"
-    exp10 = t.exponent + len(t.digits) - 1  # exponent of the leading digit
-    if 1e-3 <= mag < 1e7:
-        s = format(dec.normalize(), "f")
-        if "." not in s:
-            s += ".0"
-        return sign + s
-    mant = digits[0] + "." + (digits[1:] or "0")
-    return f"{sign}{mant}E{exp10}"
+    """Java Float.toString (Cast(FloatType -> StringType)), the device formatter on the host."""
+    return N.java_float_to_string(float(f))
 
 
 def cast_to_string(value, dtype: int) -> str:

@@ -131,27 +131,37 @@ class ApproxQuantileState(State):
 
 
 def quantile_summaries(data, column: str, relative_error: float) -> QuantileSummaries:
-    """The summary of `column`'s non-NULL values over every batch of a device table."""
+    """The summary of `column`'s non-NULL values over every batch of a device table.
+
+    The device returns every sorted value when they fit Spark's head buffer, when relativeError is
+    0 (accuracy 1/0.0 = Infinity: Spark keeps every sample and answers the exact order statistic,
+    ApproxQuantile.scala:39-41) or when 2/eps + 1 ranks would cover every value; otherwise
+    max(HEAD_SIZE, 2/eps + 1) evenly spaced exact order statistics, thinned here to 2/eps + 1."""
     import torch
     batches = [b[column] for b in data.batches]
     arr = (N.dq_column * max(1, len(batches)))(*[c.to_c() for c in batches])
+    total = sum(int(arr[i].length) for i in range(len(batches)))
     device = data.device_index()
-    few = HEAD_SIZE
-    ranks = max(3, int(math.ceil(2.0 / relative_error)) + 1) if relative_error > 0 else few
-    cap = max(few, ranks)
-    out = np.empty(cap, np.float64)
+    ranks = int(math.ceil(2.0 / relative_error)) + 1 if relative_error > 0 else None
+    want = total if ranks is None else max(HEAD_SIZE, ranks)
+    want = max(2, min(want, total))
+    out = np.empty(want, np.float64)
     n_out, count = ctypes.c_int64(), ctypes.c_int64()
     stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
-    # one call: every value when count <= HEAD_SIZE, else `ranks` evenly spaced order statistics
-    N.check(N.lib.dq_sorted_sample(device, arr, len(batches), few, out.ctypes.data,
-                                   ctypes.byref(n_out), ctypes.byref(count), stream))
+    N.retry_on_oom(lambda: N.check(N.lib.dq_sorted_sample(
+        device, arr, len(batches), want, out.ctypes.data, ctypes.byref(n_out),
+        ctypes.byref(count), stream)))
     n, cnt = int(n_out.value), int(count.value)
     if cnt == 0:
         return QuantileSummaries(relative_error, [], 0)
     if n == cnt:
-        return QuantileSummaries.from_sorted(out[:n], relative_error)
-    # too many values for an exact replay: thin the HEAD_SIZE evenly spaced order statistics to
-    # `ranks` of them (still exact ranks of the full column)
+        if cnt <= HEAD_SIZE:  # one head buffer: Spark's own insert + compress, replayed
+            return QuantileSummaries.from_sorted(out[:n], relative_error)
+        # every value as a sample of g = 1, delta = 0: the exact summary (Spark's at eps = 0)
+        s = QuantileSummaries(relative_error, list(zip(out[:n].tolist(), [1] * n, [0] * n)), cnt)
+        return s.compress() if relative_error > 0 else s
+    # n >= 2/eps + 1 evenly spaced order statistics: thin to 2/eps + 1 of them (exact ranks of the
+    # full column, gaps <= eps * cnt)
     idx = [(j * (n - 1)) // (ranks - 1) for j in range(ranks)] if ranks < n else list(range(n))
     picked = out[idx]
     full_ranks = [(i * (cnt - 1)) // (n - 1) for i in idx]

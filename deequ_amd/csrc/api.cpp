@@ -17,6 +17,7 @@
 
 #include "engine.h"
 #include "kernels.h"
+#include "jfmt.h"
 
 using namespace dq;
 
@@ -1506,6 +1507,13 @@ extern "C" uint64_t dq_xxhash64(const void* data, int64_t nbytes, uint64_t seed)
   return xxh_bytes(rd, nbytes, seed);
 }
 
+extern "C" int dq_java_double_to_string(double value, char* buf) {
+  return jfmt::double_to_java(value, buf);
+}
+extern "C" int dq_java_float_to_string(float value, char* buf) {
+  return jfmt::float_to_java(value, buf);
+}
+
 extern "C" dq_status dq_column_from_arrow(const struct ArrowArray* array,
                                           const struct ArrowSchema* schema, dq_column* out) {
   if (!array || !schema || !out || !schema->format)
@@ -1543,7 +1551,7 @@ namespace {
 constexpr int kPoolDevices = 64;
 constexpr size_t kPoolRound = 256;                 // small blocks: 256-B granules
 constexpr size_t kPoolBig = 2ULL << 20;            // >= 2 MiB: 2-MiB granules
-constexpr size_t kPoolKeep = 64ULL << 30;          // at most this much cached per device
+constexpr size_t kPoolKeep = 32ULL << 30;          // at most this much cached per device
 struct DevPool {
   std::mutex m;
   std::multimap<size_t, void*> free_blocks[kPoolDevices];

@@ -6,6 +6,7 @@
 
 #include "device_util.h"
 #include "kernels.h"
+#include "jfmt.h"
 
 namespace dq {
 
@@ -172,6 +173,7 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
               v.i = bit1(reinterpret_cast<const uint8_t*>(c.values), r);
             } else if (is_float_type(c.type)) {
               v.tag = 3;
+              v.len = c.type == DQ_FLOAT32;  // the cast to string prints a float as Float.toString
               v.d = load_f64(c.type, c.values, r);
             } else {
               v.tag = 2;
@@ -262,8 +264,8 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
           }
           case XI_REGEX: {  // find() over x's text with a compiled automaton (regex.py)
             V& a = st[sp - 1];
-            if (a.tag == 0 || a.tag == 3) {  // NULL (a double never gets here: the planner
-              if (ins.a) a = V{1, 0, 0, 0.0, nullptr};  // refuses it); null_mode 1 -> FALSE
+            if (a.tag == 0) {  // NULL: null_mode 1 (PatternMatch's otherwise(0)) -> FALSE
+              if (ins.a) a = V{1, 0, 0, 0.0, nullptr};
               else a = V{0, 0, 0, 0.0, nullptr};
               break;
             }
@@ -277,10 +279,12 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
             if (a.tag == 4) {
               DevBytes rd{a.p};
               for (int32_t k = 0; k < a.len && !status[q]; ++k) q = nx[q * nc + cls[rd.u8(k)]];
-            } else {  // Spark's cast to string: decimal integer, or true / false
-              char buf[24];
+            } else {  // Spark's cast to string: decimal integer, true / false, Double.toString
+              char buf[jfmt::kMaxChars];
               int nb = 0;
-              if (a.tag == 1) {
+              if (a.tag == 3) {
+                nb = a.len ? jfmt::float_to_java((float)a.d, buf) : jfmt::double_to_java(a.d, buf);
+              } else if (a.tag == 1) {
                 const char* t = a.i ? "true" : "false";
                 for (; t[nb]; ++nb) buf[nb] = t[nb];
               } else {

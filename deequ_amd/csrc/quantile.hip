@@ -56,13 +56,6 @@ __global__ void quantile_pick(const double* __restrict__ sorted, int64_t count, 
   out[j] = sorted[r];
 }
 
-struct DevMem {
-  void* p = nullptr;
-  ~DevMem() {
-    if (p) (void)hipFree(p);
-  }
-};
-
 }  // namespace
 
 extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int n_batches,
@@ -85,13 +78,16 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   *n_out = 0;
   *count_out = 0;
   if (rows == 0) return DQ_OK;
-  DevMem keys, sorted, cur, tmp, picks;
-  HIP_TRY(hipMalloc(&keys.p, (size_t)rows * 8));
-  HIP_TRY(hipMalloc(&sorted.p, (size_t)rows * 8));
-  HIP_TRY(hipMalloc(&cur.p, 8));
+  // through the engine's device cache (dev_alloc): reused across columns, released on OOM
+  DevBuf<double> keys, sorted, picks;
+  DevBuf<unsigned long long> cur;
+  DevBuf<uint8_t> tmp;
+  HIP_TRY(keys.ensure((size_t)rows));
+  HIP_TRY(sorted.ensure((size_t)rows));
+  HIP_TRY(cur.ensure(1));
   HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
-  auto* kp = static_cast<double*>(keys.p);
-  auto* cp = static_cast<unsigned long long*>(cur.p);
+  double* kp = keys.p;
+  unsigned long long* cp = cur.p;
   for (int b = 0; b < n_batches; ++b) {
     const dq_column& c = batches[b];
     if (!c.length) continue;
@@ -106,21 +102,18 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   *count_out = (int64_t)count;
   if (!count) return DQ_OK;
   size_t tmp_bytes = 0;
-  HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, kp, static_cast<double*>(sorted.p),
-                                   (size_t)count, 0, 64, stream));
-  HIP_TRY(hipMalloc(&tmp.p, std::max<size_t>(tmp_bytes, 16)));
-  HIP_TRY(rocprim::radix_sort_keys(tmp.p, tmp_bytes, kp, static_cast<double*>(sorted.p),
-                                   (size_t)count, 0, 64, stream));
+  HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, kp, sorted.p, (size_t)count, 0, 64, stream));
+  HIP_TRY(tmp.ensure(std::max<size_t>(tmp_bytes, 16)));
+  HIP_TRY(rocprim::radix_sort_keys(tmp.p, tmp_bytes, kp, sorted.p, (size_t)count, 0, 64, stream));
   const int64_t n = (int64_t)count <= max_values ? (int64_t)count : max_values;
   *n_out = n;
   if (!out) return DQ_OK;  // size query only
   if (n == (int64_t)count) {
     HIP_TRY(hipMemcpyAsync(out, sorted.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
   } else {
-    HIP_TRY(hipMalloc(&picks.p, (size_t)n * 8));
+    HIP_TRY(picks.ensure((size_t)n));
     hipLaunchKernelGGL(quantile_pick, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                       static_cast<const double*>(sorted.p), (int64_t)count, n,
-                       static_cast<double*>(picks.p));
+                       sorted.p, (int64_t)count, n, picks.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
   }

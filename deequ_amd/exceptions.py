@@ -47,7 +47,12 @@ class HllBiasTablesUnavailableException(MetricCalculationRuntimeException):
     """ApproxCountDistinct's estimate fell in HLL++'s empirical-bias range (raw estimate E < 5M and
     no linear counting): the reference subtracts estimateBias(E) from Spark's RAW_ESTIMATE_DATA /
     BIAS_DATA tables (StatefulHyperloglogPlus.scala:235-237, 257-295), which are not available to
-    this engine.  Raised instead of returning a value that would differ from deequ's."""
+    this engine.  Raised instead of returning a value that would differ from deequ's.
+
+    In that range the sketch's linear counting already estimates more than LINEAR_COUNTING_FLOOR
+    distinct values (HyperLogLogPlusPlus.THRESHOLDS(P - 4) for P = 9): consumers that only compare
+    the count with a smaller bound (the ColumnProfiler's histogram threshold) can still decide."""
+    LINEAR_COUNTING_FLOOR = 400
 
 
 class AnalysisException(Exception):

@@ -25,7 +25,7 @@ from . import _native as N
 from .analyzers import (ApproxCountDistinct, ApproxQuantiles, Completeness, DataType, Histogram,
                         Maximum, Mean, Minimum, Size, StandardDeviation, Sum)
 from .analyzers.datatype import DataTypeInstances, determine_type
-from .exceptions import ReusingNotPossibleResultsMissingException
+from .exceptions import HllBiasTablesUnavailableException, ReusingNotPossibleResultsMissingException
 from .metrics import Distribution, DistributionValue, HistogramMetric, Success
 from .runners import AnalysisRunBuilder, AnalyzerContext
 
@@ -36,7 +36,7 @@ DEFAULT_CARDINALITY_THRESHOLD = 120
 class StandardColumnProfile:
     column: str
     completeness: float
-    approximate_num_distinct_values: int
+    approximate_num_distinct_values: Optional[int]  # None: HLL++ bias range, no tables
     data_type: DataTypeInstances
     is_data_type_inferred: bool
     type_counts: Dict[str, int]
@@ -86,7 +86,7 @@ class _GenericStatistics:
     inferred_types: Dict[str, DataTypeInstances]
     known_types: Dict[str, DataTypeInstances]
     type_detection_histograms: Dict[str, Dict[str, int]]
-    approximate_num_distincts: Dict[str, int]
+    approximate_num_distincts: Dict[str, Optional[int]]
     completenesses: Dict[str, float]
 
     def type_of(self, column: str) -> DataTypeInstances:
@@ -207,7 +207,11 @@ def _extract_generic_statistics(columns, schema, results) -> _GenericStatistics:
             inferred[a.column] = determine_type(dist)
             hists[a.column] = {k: v.absolute for k, v in dist.values.items()}
         elif isinstance(a, ApproxCountDistinct):
-            distincts[a.column] = int(m.value.get())  # Double.toLong truncates
+            if not m.value.is_success and isinstance(m.value.failed,
+                                                     HllBiasTablesUnavailableException):
+                distincts[a.column] = None  # unavailable: HLL++ bias range (see below)
+            else:
+                distincts[a.column] = int(m.value.get())  # Double.toLong truncates
         elif isinstance(a, Completeness):
             compl[a.column] = m.value.get()
     known = {f.name: _known_type(f.dtype) for f in schema.fields
@@ -222,9 +226,10 @@ def _cast_column(data, name: str, to_type: int):
     batches = []
     for b in data.batches:
         c = b[name]
-        values = torch.empty(max(c.length, 1), dtype=torch.int64 if to_type == N.INT64
-                             else torch.float64, device=data.device)
-        validity = torch.empty(max((c.length + 7) // 8, 1), dtype=torch.uint8, device=data.device)
+        values = N.retry_on_oom(torch.empty, max(c.length, 1), device=data.device,
+                                dtype=torch.int64 if to_type == N.INT64 else torch.float64)
+        validity = N.retry_on_oom(torch.empty, max((c.length + 7) // 8, 1), dtype=torch.uint8,
+                                  device=data.device)
         bad = ctypes.c_int64()
         stream = ctypes.c_void_p(torch.cuda.current_stream(data.device).cuda_stream)
         col = c.to_c()
@@ -280,9 +285,25 @@ def _extract_numeric_statistics(results) -> _NumericStatistics:
 
 
 def _target_columns_for_histograms(schema, generic, threshold) -> List[str]:
+    """getHistogramsOfLowCardinalityColumns' selection (ColumnProfiler.scala:416-433).  A column
+    whose ApproxCountDistinct fell in the HLL++ bias range has no number here (Spark's bias tables
+    are missing, HllBiasTablesUnavailableException), but there linear counting already puts it
+    above LINEAR_COUNTING_FLOOR distinct values: it is not a target for any threshold below that,
+    and a larger threshold cannot be decided without the tables (raised, never guessed)."""
     strings = {f.name for f in schema.fields if f.dtype == N.UTF8}
-    return [c for c, n in generic.approximate_num_distincts.items()
-            if c in strings and generic.type_of(c) == DataTypeInstances.String and n <= threshold]
+    out = []
+    for c, n in generic.approximate_num_distincts.items():
+        if c not in strings or generic.type_of(c) != DataTypeInstances.String:
+            continue
+        if n is None:
+            if threshold >= HllBiasTablesUnavailableException.LINEAR_COUNTING_FLOOR:
+                raise HllBiasTablesUnavailableException(
+                    f"column {c}: its approximate distinct count lies in the HLL++ bias-correction "
+                    f"range, so it cannot be compared with a histogram threshold of {threshold}")
+            continue
+        if n <= threshold:
+            out.append(c)
+    return out
 
 
 def _compute_histograms(data, targets) -> Dict[str, Distribution]:

@@ -19,13 +19,24 @@ escaped metacharacters), ``.`` (any code point but the Java line terminators), c
 negation, nested escapes and \\d \\D \\s \\S \\w \\W (ASCII, as Java without UNICODE_CHARACTER_CLASS),
 groups ( ), (?: ), alternation, greedy / lazy quantifiers * + ? {n} {n,} {n,m}, lookaheads (?= )
 (?! ), back-references to groups with a finite language (expanded: the CREDITCARD separators),
-^ / \\A at the start, $ / \\z at the end, \\b at the start or end of the pattern.  Rejected (a
-PatternNotSupported error, never a silently different answer): patterns that can match the empty
-string, possessive quantifiers, lookbehind, inline flags, \\b / anchors elsewhere, and automata above
-``MAX_STATES``.  Known approximation: \\b treats every non-ASCII code point as a word character
-(Java's \\b uses Character.isLetterOrDigit).
+^ / \\A at the start; $ / \\Z (end, or before one final line terminator, "\\r\\n" included) and
+\\z (strict end) at the end; \\b at the start or end of the pattern.  Rejected (a PatternNotSupported
+error, never a silently different answer): patterns that can match the empty string, possessive
+quantifiers, lookbehind, inline flags, \\b / anchors elsewhere, $ after a pattern that may end in
+"\\r" (Java's $ never matches between "\\r\\n"), and automata above ``MAX_STATES``.
+
+\\b is Java's Bound: a word character is '_' or Character.isLetterOrDigit (categories L* and Nd),
+taken from Python's Unicode database.  Exact for U+0000-U+07FF and the punctuation / symbol blocks
+U+2000-U+2BFF, U+3000-U+303F, U+FF00-U+FFEF (the em dash and the euro sign are boundaries, as in
+Java); other code points from U+0800 up count as word characters (overwhelmingly letters: CJK,
+Indic, Hangul ...), which keeps the byte automaton small.  Parity unpinned: those other blocks,
+JDK 8's Unicode 6.2 tables vs Python's, and Java's rule that a combining mark (Mn) after a base
+character is a word character.
 """
 from __future__ import annotations
+
+import functools
+import unicodedata
 
 import struct
 from dataclasses import dataclass
@@ -71,6 +82,29 @@ SPACE = cs_norm([(9, 13), (32, 32)])  # [ \t\n\x0B\f\r]
 LINE_TERMINATORS = cs_norm([(10, 10), (13, 13), (0x85, 0x85), (0x2028, 0x2029)])
 DOT = cs_neg(LINE_TERMINATORS)
 ANY = ((0, MAX_CP),)
+# \b's word characters are decided exactly in these blocks (see the module docstring)
+_BOUND_EXACT = ((0, 0x7FF), (0x2000, 0x2BFF), (0x3000, 0x303F), (0xFF00, 0xFFEF))
+
+
+@functools.lru_cache(maxsize=1)
+def bound_word_chars() -> Tuple[Tuple[int, int], ...]:
+    """Java's Bound.isWord: '_' or Character.isLetterOrDigit, exact in _BOUND_EXACT, and every
+    other code point from U+0800 up counted as a word character."""
+    out, start = [], None
+    for cp in range(MAX_CP + 1):
+        if any(a <= cp <= b for a, b in _BOUND_EXACT):
+            cat = unicodedata.category(chr(cp))
+            w = cp == 95 or cat[0] == "L" or cat == "Nd"
+        else:
+            w = cp >= 0x800 and not 0xD800 <= cp <= 0xDFFF
+        if w and start is None:
+            start = cp
+        elif not w and start is not None:
+            out.append((start, cp - 1))
+            start = None
+    if start is not None:
+        out.append((start, MAX_CP))
+    return cs_norm(out)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -267,7 +301,7 @@ class _Parser:
                 self.error("\\B")
             return Anchor("\\b")
         elif c in "AzZ" and not in_class:
-            return Anchor("^" if c == "A" else "$")
+            return Anchor({"A": "^", "Z": "$", "z": "\\z"}[c])
         elif c.isalnum():
             self.error(f"unsupported escape \\{c}")
         else:
@@ -791,12 +825,35 @@ def _has_look(n) -> bool:
     return False
 
 
-def _first_last_word(node, last: bool) -> Optional[bool]:
-    """Whether the first (last) code point of every match is a word character (True), never one
-    (False), or either (None)."""
+def _may_end_with(node, cp: int) -> bool:
+    """Whether some match of `node` can end with code point `cp`."""
     if isinstance(node, Chars):
-        inside = all(any(a <= lo and hi <= b for a, b in WORD) for lo, hi in node.ranges)
-        outside = all(all(hi < a or lo > b for a, b in WORD) for lo, hi in node.ranges)
+        return any(a <= cp <= b for a, b in node.ranges)
+    if isinstance(node, Seq):
+        for x in reversed(node.items):
+            if isinstance(x, (Look, Anchor)):
+                continue
+            if _may_end_with(x, cp):
+                return True
+            if not nullable(x):
+                return False
+        return False
+    if isinstance(node, Alt):
+        return any(_may_end_with(o, cp) for o in node.options)
+    if isinstance(node, Group):
+        return _may_end_with(node.node, cp)
+    if isinstance(node, Repeat):
+        return node.hi != 0 and _may_end_with(node.node, cp)
+    return False
+
+
+def _first_last_word(node, last: bool) -> Optional[bool]:
+    """Whether the first (last) code point of every match is a \\b word character (True), never
+    one (False), or either (None)."""
+    if isinstance(node, Chars):
+        word = bound_word_chars()
+        inside = all(any(a <= lo and hi <= b for a, b in word) for lo, hi in node.ranges)
+        outside = all(all(hi < a or lo > b for a, b in word) for lo, hi in node.ranges)
         return True if inside else (False if outside else None)
     if isinstance(node, Seq):
         items = list(reversed(node.items)) if last else list(node.items)
@@ -867,7 +924,10 @@ def compile_java_regex(pattern: str) -> CompiledRegex:
     c = _Compiler()
     s0 = c.nfa.new()
     c.final = c.nfa.new()
-    non_word = cs_norm([r for r in cs_neg(WORD) if r[1] < 0x80])  # non-ASCII counts as word
+    bound_word = bound_word_chars() if "\\b" in (start_anchor, end_anchor) else WORD
+    non_word = cs_neg(bound_word)
+    if end_anchor == "$" and _may_end_with(body, 13):
+        raise PatternNotSupported("$ after a pattern that may end in \\r")
     # prefix: Sigma*, honouring a leading ^ or \b
     if start_anchor == "^":
         p = s0
@@ -883,24 +943,30 @@ def compile_java_regex(pattern: str) -> CompiledRegex:
         else:
             p = c.nfa.new()
             any_ = c.anything(s0)
-            c.chars(cs_norm(WORD + ((0x80, MAX_CP),)), any_, p)
+            c.chars(bound_word, any_, p)
     else:
         p = c.anything(s0)
 
     def tail(st):
-        if end_anchor == "$":
-            # Java's $ also matches before a final line terminator
+        if end_anchor == "\\z":
+            c.nfa.trans[st].append((1 << EOT, c.final))
+        elif end_anchor == "$":
+            # Java's $ (\Z) also matches before a final line terminator, "\r\n" included
             c.nfa.trans[st].append((1 << EOT, c.final))
             m = c.nfa.new()
             c.chars(LINE_TERMINATORS, st, m)
             c.nfa.trans[m].append((1 << EOT, c.final))
+            cr, crlf = c.nfa.new(), c.nfa.new()
+            c.chars(((13, 13),), st, cr)
+            c.chars(((10, 10),), cr, crlf)
+            c.nfa.trans[crlf].append((1 << EOT, c.final))
         elif end_anchor == "\\b":
             last = _first_last_word(body, last=True)
             if last is None:
                 raise PatternNotSupported("\\b after a pattern that may end with either class")
             c.nfa.trans[st].append((1 << EOT, c.final) if last else (0, c.final))
             m = c.nfa.new()
-            c.chars(non_word if last else cs_norm(WORD + ((0x80, MAX_CP),)), st, m)
+            c.chars(non_word if last else bound_word, st, m)
             c.nfa.eps[m].append(c.univ)
         else:
             c.nfa.eps[st].append(c.univ)

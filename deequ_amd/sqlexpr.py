@@ -387,10 +387,9 @@ class _Emitter:
             return
         if n.op == "regex":
             tx = self.type_of(n.kids[0])
-            if tx == "float":
-                raise SqlError("a regex over a floating-point column needs Java's Double.toString, "
-                               "which the engine does not implement")
-            if tx not in ("str", "int", "bool", "null"):
+            # a non-string operand is matched as Spark's cast to string: decimal integers,
+            # true / false, Double.toString / Float.toString (csrc/jfmt.h, on the device)
+            if tx not in ("str", "int", "float", "bool", "null"):
                 raise SqlError(f"cannot match a regex against a {tx} value")
             blob = _compiled_regex(n.value, n.name == "rlike")
             w += [N.X_REGEX, 1 if n.name == "nonempty" else 0, len(blob)]

@@ -196,7 +196,7 @@ def _slice_column(c: ColumnBatch, lo: int, hi: int) -> ColumnBatch:
 def _to_device(np_buf: np.ndarray, device: str):
     import torch
     t = torch.from_numpy(np.ascontiguousarray(np_buf))
-    return t.to(device)
+    return N.retry_on_oom(t.to, device)
 
 
 def _empty_column(dtype: int, device: str) -> ColumnBatch:

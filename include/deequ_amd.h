@@ -273,6 +273,12 @@ dq_status dq_state_deserialize(dq_state* state, const void* buf, int64_t buf_len
 double dq_hll_count(const uint64_t* words, int* bias_corrected);
 /* Spark XxHash64Function.hash(v, type, 42) for one value (host reference of the device hash). */
 uint64_t dq_xxhash64(const void* data, int64_t nbytes, uint64_t seed);
+/* Java's Double.toString / Float.toString of one value (Spark 2.2 Cast(Double|FloatType ->
+ * StringType), the text PatternMatch.scala:44-48 and Histogram.scala:59-66 see for a floating-point
+ * column): the device formatter of jfmt.h, run on the host.  Writes at most 26 bytes, no NUL;
+ * returns the length. */
+int dq_java_double_to_string(double value, char* buf);
+int dq_java_float_to_string(float value, char* buf);
 
 /* ------------------------------------------------------------------------------------------------
  * Frequency path: hash group-by (FrequencyBasedAnalyzer.computeFrequencies) on the GPU.

@@ -610,31 +610,64 @@ def entropy(freq, num_rows):
     return total
 
 
+def _java_layout(sign: str, digits: str, e10: int) -> str:
+    """java.lang.Double.toString's layout of a shortest digit string whose leading digit has
+    exponent e10: plain ddd.ddd for e10 in [-3, 6], else d.dddE<e10>; one fraction digit at least."""
+    digits = digits.rstrip("0") or "0"
+    if 0 <= e10 < 7:
+        ip = (digits + "0" * 7)[:e10 + 1]
+        return sign + ip + "." + (digits[e10 + 1:] or "0")
+    if -3 <= e10 < 0:
+        return sign + "0." + "0" * (-e10 - 1) + digits
+    return sign + digits[0] + "." + (digits[1:] or "0") + "E" + str(e10)
+
+
 def java_double_to_string(d: float) -> str:
+    """Double.toString (Spark 2.2 Cast(DoubleType -> StringType)): Python's repr gives the shortest
+    round-trip digits (David Gay's dtoa), laid out as Java does.  Double.MIN_VALUE prints 4.9E-324
+    (FloatingDecimal's two-digit estimate); JDK 8's other non-shortest outputs are unpinned."""
     if math.isnan(d):
         return "NaN"
     if math.isinf(d):
         return "Infinity" if d > 0 else "-Infinity"
     if d == 0.0:
         return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
-    r = repr(d)
-    mant, _, exp = r.partition("e")
-    digits = mant.replace("-", "").replace(".", "").lstrip("0").rstrip("0") or "0"
-    a = abs(d)
-    if 1e-3 <= a < 1e7:
-        s = ("%.17f" % a).rstrip("0")
-        # shortest: rebuild from repr digits
-        from decimal import Decimal
-        s = format(Decimal(repr(a)).normalize(), "f")
-        if "." not in s:
-            s += ".0"
-        return ("-" if d < 0 else "") + s
+    if abs(d) == 5e-324:
+        return ("-" if d < 0 else "") + "4.9E-324"
     from decimal import Decimal
-    dec = Decimal(repr(a))
-    t = dec.as_tuple()
-    e10 = t.exponent + len(t.digits) - 1
-    ds = "".join(map(str, t.digits)).rstrip("0") or "0"
-    return ("-" if d < 0 else "") + ds[0] + "." + (ds[1:] or "0") + "E" + str(e10)
+    t = Decimal(repr(abs(d))).as_tuple()
+    return _java_layout("-" if d < 0 else "", "".join(map(str, t.digits)),
+                        t.exponent + len(t.digits) - 1)
+
+
+def java_float_to_string(f: float) -> str:
+    """Float.toString (Cast(FloatType -> StringType)): numpy's shortest float32 digits (Dragon4
+    unique mode), Java's layout; Float.MIN_VALUE prints 1.4E-45."""
+    import numpy as np
+    if math.isnan(f):
+        return "NaN"
+    if math.isinf(f):
+        return "Infinity" if f > 0 else "-Infinity"
+    if f == 0.0:
+        return "-0.0" if math.copysign(1.0, f) < 0 else "0.0"
+    if abs(f) == float(np.float32(1e-45)):
+        return ("-" if f < 0 else "") + "1.4E-45"
+    sci = np.format_float_scientific(np.float32(abs(f)), unique=True, trim="-")
+    mant, _, exp = sci.partition("e")
+    return _java_layout("-" if f < 0 else "", mant.replace(".", ""), int(exp))
+
+
+def java_to_string(v, ty: str) -> str:
+    """Spark's cast to string of a non-NULL value of oracle type `ty`."""
+    if ty == "string":
+        return v
+    if ty == "boolean":
+        return "true" if v else "false"
+    if ty == "double":
+        return java_double_to_string(float(v))
+    if ty == "float":
+        return java_float_to_string(float(v))
+    return str(int(v))
 
 
 def histogram(t: OTable, column: str) -> Tuple[Dict[str, int], int]:
@@ -642,16 +675,7 @@ def histogram(t: OTable, column: str) -> Tuple[Dict[str, int], int]:
     ty = t.types[column]
     out: Dict[str, int] = {}
     for v in t.columns[column]:
-        if v is None:
-            s = "NullValue"
-        elif ty == "string":
-            s = v
-        elif ty == "boolean":
-            s = "true" if v else "false"
-        elif ty in ("double", "float"):
-            s = java_double_to_string(float(v))
-        else:
-            s = str(int(v))
+        s = "NullValue" if v is None else java_to_string(v, ty)
         out[s] = out.get(s, 0) + 1
     return out, t.n
 
@@ -661,15 +685,54 @@ def histogram(t: OTable, column: str) -> Tuple[Dict[str, int], int]:
 # Python's backtracking `re` (same leftmost-first semantics), the pattern translated from Java
 # syntax where the two differ.  Test infrastructure only.
 # ------------------------------------------------------------------------------------------------
+_JAVA_DOLLAR = "(?:\\Z|(?=\\r\\n\\Z)|(?<!\\r)(?=\\n\\Z)|(?=[\\r\\x85\\u2028\\u2029]\\Z))"
+
+
+def _java_word_class() -> str:
+    """Java's Bound.isWord (Pattern.java, JDK 8): '_' or Character.isLetterOrDigit -- Unicode
+    categories L* and Nd -- as a Python character class over every code point."""
+    import unicodedata
+    parts, start = [], None
+    for cp in range(0x110000):
+        cat = unicodedata.category(chr(cp))
+        w = cp == 95 or cat[0] == "L" or cat == "Nd"
+        if w and start is None:
+            start = cp
+        elif not w and start is not None:
+            parts.append((start, cp - 1))
+            start = None
+    if start is not None:
+        parts.append((start, 0x10FFFF))
+    esc = lambda c: "\\U%08x" % c  # noqa: E731
+    return "[" + "".join(esc(a) if a == b else esc(a) + "-" + esc(b) for a, b in parts) + "]"
+
+
+_JAVA_WORD = None
+
+
 def java_regex_to_python(pattern: str) -> str:
-    """Java -> Python `re`: `.` outside a class excludes every Java line terminator (Python's
-    excludes only \\n); everything else used by Patterns is common syntax (re.ASCII gives Java's
-    ASCII \\d \\w \\s)."""
+    """Java -> Python `re` (used with re.ASCII, which gives Java's ASCII \\d \\w \\s):
+    `.` outside a class excludes every Java line terminator (Python's excludes only \\n); `$` and
+    `\\Z` are Java's Dollar (end, or before one final terminator, "\\r\\n" included, never
+    between "\\r\\n"); `\\z` is the strict end; `\\b` is Java's Bound over Unicode letters and
+    digits (Python's ASCII \\b would call every non-ASCII code point a non-word one)."""
+    global _JAVA_WORD
     out, i, in_class = [], 0, False
     while i < len(pattern):
         c = pattern[i]
         if c == "\\":
-            out.append(pattern[i:i + 2])
+            e = pattern[i:i + 2]
+            if not in_class and e == "\\b":
+                if _JAVA_WORD is None:
+                    _JAVA_WORD = _java_word_class()
+                w = _JAVA_WORD
+                out.append(f"(?:(?<!{w})(?={w})|(?<={w})(?!{w}))")
+            elif not in_class and e == "\\Z":
+                out.append(_JAVA_DOLLAR)
+            elif not in_class and e == "\\z":
+                out.append("\\Z")
+            else:
+                out.append(e)
             i += 2
             continue
         if in_class:
@@ -685,6 +748,8 @@ def java_regex_to_python(pattern: str) -> str:
             out.append(c)
         elif c == ".":
             out.append("[^\\n\\r\\u0085\\u2028\\u2029]")
+        elif c == "$":
+            out.append(_JAVA_DOLLAR)
         else:
             out.append(c)
         i += 1
@@ -712,9 +777,8 @@ def agg_pattern_match(t: OTable, column: str, pattern: str, where: Optional[str]
         if pred is not None and eval_predicate(pred, r) is not True:
             continue
         v = vals[i]
-        if t.types[column] == "boolean" and v is not None:
-            v = "true" if v else "false"
-        hits += regex_find_nonempty(v, pattern)
+        hits += regex_find_nonempty(None if v is None else java_to_string(v, t.types[column]),
+                                    pattern)
     return hits, n
 
 
@@ -795,14 +859,7 @@ def datatype_counts(t: OTable, column: str, where: Optional[str]) -> Tuple[int, 
         if v is None:
             out[0] += 1
             continue
-        if ty == "string":
-            s = v
-        elif ty == "boolean":
-            s = "true" if v else "false"
-        elif ty in ("double", "float"):
-            s = java_double_to_string(float(v))
-        else:
-            s = str(int(v))
+        s = java_to_string(v, ty)
         if frac.fullmatch(s):
             out[1] += 1
         elif integral.fullmatch(s):

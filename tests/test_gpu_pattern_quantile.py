@@ -26,15 +26,54 @@ def test_pattern_match_known_answers(gpu_device):
 
 
 def test_pattern_match_integral_and_null_rows(gpu_device):
-    """An integral column is matched as Spark's cast to string; NULL rows count in the
-    denominator only (AnalyzerTests.scala:597-601 uses a double column: Java's Double.toString is
-    not on the device, so such a column is a failure metric, never a different number)."""
+    """A non-string column is matched as Spark's cast to string; NULL rows count in the
+    denominator only.  The double column is AnalyzerTests.scala:597-601 (Success(0.75)): the
+    device prints each double with Java's Double.toString (csrc/jfmt.h) before the walk."""
     from deequ_amd.analyzers import PatternMatch
     df = _df({"i": pa.array([11, None, -32, 4], pa.int64()),
-              "d": pa.array([1.1, None, 3.2, 4.4], pa.float64())}, gpu_device)
+              "d": pa.array([1.1, None, 3.2, 4.4], pa.float64()),
+              "f": pa.array([1.1, None, 3.2, 4.4], pa.float32())}, gpu_device)
     assert PatternMatch("i", r"\d\d").calculate(df).value.get() == 0.5
     assert PatternMatch("i", r"^-").calculate(df).value.get() == 0.25
-    assert PatternMatch("d", r"\d\.\d").calculate(df).value.is_failure
+    assert PatternMatch("d", r"\d\.\d").calculate(df).value.get() == 0.75
+    assert PatternMatch("f", r"^\d\.\d$").calculate(df).value.get() == 0.75
+
+
+@pytest.mark.parametrize("pattern", [r"\d\.\d", r"E-\d+$", r"^-?\d+\.0$", r"\.\d{6,}",
+                                     r"^(NaN|-?Infinity)$", r"^-0\.0$", r"9{3}"])
+@pytest.mark.parametrize("dtype", ["double", "float"])
+def test_pattern_match_floating_point_columns_match_oracle(pattern, dtype, gpu_device):
+    """Doubles / floats of every layout Java prints (plain, E-notation both signs, NaN, +-Infinity,
+    +-0.0, subnormals, integers) matched as their Double / Float.toString text, row for row
+    against the oracle's independent restatement (Python repr digits + Java's layout)."""
+    import struct
+    from deequ_amd.analyzers import PatternMatch
+    from oracle.deequ_oracle import OTable, agg_pattern_match
+    rng = random.Random(hash((pattern, dtype)) & 0xFFFF)
+    specials = [0.0, -0.0, float("nan"), float("inf"), float("-inf"), 1e7, 9999999.0, 0.001,
+                0.00099, 1e-300, 5e-324, 1.5e300, -2.5, 100.0]
+    n = 20_000
+    vals = []
+    for i in range(n):
+        u = rng.random()
+        if u < 0.05:
+            vals.append(None)
+        elif u < 0.15:
+            vals.append(rng.choice(specials))
+        elif u < 0.45:
+            vals.append(struct.unpack("<d", struct.pack("<Q", rng.getrandbits(64)))[0])
+        elif u < 0.75:
+            vals.append(round(rng.uniform(-1e8, 1e8), rng.randint(0, 7)))
+        else:
+            vals.append(float(rng.randint(-10**6, 10**6)) * 10.0 ** rng.randint(-8, 8))
+    if dtype == "float":
+        vals = [None if v is None else float(np.float32(v)) for v in vals]
+    pa_type = pa.float64() if dtype == "double" else pa.float32()
+    df = _df({"x": pa.array(vals, pa_type)}, gpu_device, batch=8192)
+    got = PatternMatch("x", pattern).calculate(df).value.get()
+    ot = OTable({"x": vals}, {"x": dtype})
+    hits, cnt = agg_pattern_match(ot, "x", pattern, None)
+    assert got == hits / cnt, (pattern, got, hits, cnt)
 
 
 @pytest.mark.parametrize("pattern", [r"(https?|ftp)://[^\s/$.?#].[^\s]*", r"\d{3}-\d{2}",
@@ -115,3 +154,23 @@ def test_approx_quantiles_keyed_metric(gpu_device):
     assert [x.name for x in m.flatten()] == ["ApproxQuantiles-0.5", "ApproxQuantiles-0.25",
                                              "ApproxQuantiles-1.0"]
     assert ApproxQuantiles("n", [0.5]).calculate(df).value.get() == {}
+
+
+@pytest.mark.parametrize("eps", [0.0, 1e-6, 1e-5])
+def test_approx_quantile_small_relative_error_beyond_the_head_buffer(eps, gpu_device):
+    """relativeError 0 gives the exact quantile (ApproxQuantile.scala:39-41: accuracy 1/0.0, Spark
+    keeps every sample, query returns sampled(ceil(q n)) of the sorted values); 1e-6 / 1e-5 must
+    stay within eps * n ranks although 2/eps + 1 exceeds Spark's 50000-value head buffer."""
+    from deequ_amd.analyzers import ApproxQuantile
+    from oracle.deequ_oracle import quantile_rank_error
+    n = 120_007
+    vals = np.random.default_rng(17).normal(0, 5, n)
+    df = _df({"x": pa.array(vals)}, gpu_device, 1 << 15)
+    srt = np.sort(vals)
+    for q in (0.0, 0.01, 0.25, 0.5, 0.99, 1.0):
+        got = ApproxQuantile("x", q, eps).calculate(df).value.get()
+        if eps == 0.0:
+            exp = srt[0] if q <= 0 else srt[-1] if q >= 1 else srt[min(math.ceil(q * n), n - 1)]
+            assert got == exp, (q, got, exp)
+        else:
+            assert quantile_rank_error(vals, q, got) <= math.ceil(eps * n), (eps, q, got)

@@ -176,3 +176,26 @@ def test_success_metrics_json_known_answer(gpu_device):
     want = sorted({"dataset_date": 1507975810, "entity": e, "region": "EU", "instance": i,
                    "name": n, "value": v}.items() for e, i, n, v in exp)
     assert sorted(sorted(r.items()) for r in got) == sorted(sorted(w) for w in want)
+
+
+def test_profile_of_a_column_in_the_hll_bias_range(gpu_device):
+    """About 1000 distinct values put ApproxCountDistinct in HLL++'s bias-correction range (Spark's
+    BIAS_DATA tables are absent): the profile still completes, the column's distinct count is
+    reported as unavailable (None) instead of a different number, it is not a histogram target
+    at the default threshold (linear counting already exceeds 400), and a low-cardinality column
+    next to it is profiled as usual."""
+    from deequ_amd.profiles import ColumnProfiler
+    from deequ_amd.table import Table
+    n = 5000
+    df = Table.from_pydict({"ids": [f"k{i % 1000}" for i in range(n)],
+                            "low": ["ab"[i % 2] for i in range(n)]},
+                           {"ids": "string", "low": "string"}, device=gpu_device)
+    p = ColumnProfiler.profile(df)
+    assert p.num_records == n
+    assert p.profiles["ids"].approximate_num_distinct_values is None
+    assert p.profiles["ids"].histogram is None
+    assert p.profiles["low"].approximate_num_distinct_values == 2
+    assert set(p.profiles["low"].histogram.values) == {"a", "b"}
+    from deequ_amd.exceptions import HllBiasTablesUnavailableException
+    with pytest.raises(HllBiasTablesUnavailableException):
+        ColumnProfiler.profile(df, low_cardinality_histogram_threshold=500)

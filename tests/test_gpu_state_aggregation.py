@@ -88,12 +88,18 @@ def test_partition_states_merge_to_the_whole_table(seed, null_rates, cuts, gpu_d
              for lo, hi in zip(bounds[:-1], bounds[1:])]
     whole = Table.from_arrow(t, device=gpu_device, max_batch_rows=1000)
     for a in _analyzers():
-        states = []
+        states, error = [], None
         for p in parts:
             try:
                 states.append(a.compute_state_from(p))
-            except Exception:  # noqa: BLE001 -- a failing state fails the whole run as well
-                states.append(None)
+            except Exception as e:  # noqa: BLE001 -- the reference fails the analyzer
+                error = e
+                break
+        if error is not None:  # a throwing partition is a failure metric, never a dropped state
+            merged = a.to_failure_metric(error)
+            assert not a.calculate(whole).value.is_success, (str(a), bounds, repr(error))
+            assert not merged.value.is_success
+            continue
         try:  # Analyzer.calculate's try (Analyzer.scala:88-103) around computeMetricFrom
             merged = a.compute_metric_from(merge_states(*states))
         except Exception as e:  # noqa: BLE001

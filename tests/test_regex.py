@@ -53,6 +53,13 @@ FUZZ = [
     (r"(x|y)\1z", "xyz", 6),
     (r"\bcat\b", "cat s_", 9),
     (r"caf\u00e9|na.ve|\u4f8b+", "cafe\u00e9nav\u00efi\u4f8b\r", 8),
+    # \b next to non-ASCII letters (a word character for Java) and punctuation / currency (not)
+    (r"\bab\d\b", "ab1 \u00e9\u20ac\u2014\u00b7\u03b1_x", 8),
+    (Patterns.CREDITCARD, "41 -\u00e9\u20ac\u2014\u00d7", 24),
+    # Java's $ / \Z before a final "\r\n" or one terminator (never between "\r\n"), \z strict
+    (r"a\d$", "a1\r\n\u2028x", 7),
+    (r"a\d\Z", "a1\r\n\u0085", 7),
+    (r"a\d\z", "a1\r\n", 6),
 ]
 
 
@@ -64,7 +71,8 @@ def test_automaton_matches_java_find_semantics(pattern, alphabet, max_len):
         assert c.matches(s) == regex_find_nonempty(s, pattern), (pattern, s)
 
 
-@pytest.mark.parametrize("pattern", [r"a*", r"(?<=a)b", r"(?i)abc", r"a++", r"x\Bz", r"(a|)"])
+@pytest.mark.parametrize("pattern", [r"a*", r"(?<=a)b", r"(?i)abc", r"a++", r"x\Bz", r"(a|)",
+                                     r"a\s$"])
 def test_unsupported_patterns_are_refused(pattern):
     with pytest.raises(PatternNotSupported):
         compile_java_regex(pattern)
