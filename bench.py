@@ -52,33 +52,42 @@ def algorithmic_bytes(table) -> int:
     return total
 
 
+def available_cpus() -> tuple:
+    """(CPUs this process may run on, CPUs of the host): the affinity mask, capped by a cgroup v2
+    `cpu.max` quota when one is set (a GPU box's share of a larger host)."""
+    host = os.cpu_count() or 1
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n, host
+
+
 def cpu_baseline(rows: int, seed: int, min_seconds: float = 10.0):
-    """oracle/oracle.c S10 (Spark local[T] execution model) on a bounded sample."""
+    """oracle/oracle.c S10 as ONE pass per partition (the reference's single Spark job, local[T]
+    with T = every CPU this process may use) on a bounded sample."""
     from deequ_amd.synth import item_buffers_numpy
     from oracle import c_oracle as C
-    threads = min(16, os.cpu_count() or 1)
+    threads, host = available_cpus()
     buf = item_buffers_numpy(rows, seed)
     n = buf["n"]
-
-    def once():
-        C.numeric_i64(buf["numViews"], buf["numViews_valid"], op=17, lit=0, threads=threads)
-        C.validity_count(buf["id_valid"], n, threads)
-        C.validity_count(buf["name_valid"], n, threads)
-        C.str_in(buf["priority_offsets"], buf["priority_data"], buf["priority_valid"], n,
-                 ["high", "low"], True, threads)
-
-    once()
+    res = C.s10_fused(buf, threads=threads)
+    assert res.rows == n
     reps, t0 = 0, time.perf_counter()
     while True:
-        once()
+        C.s10_fused(buf, threads=threads)
         reps += 1
         el = time.perf_counter() - t0
         if el >= min_seconds or reps >= 5000:
             break
     return {"value": reps * n / el, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"S10 over {n} synthetic Item rows x {reps} passes ({el:.1f} s), "
-                      f"CPU restatement of Spark 2.2 deequ semantics (oracle/oracle.c, OpenMP, "
-                      f"{threads} threads = Spark local[{threads}] partitions) -- not Spark"}
+            "sample": f"S10 over {n} synthetic Item rows x {reps} passes ({el:.1f} s): one fused "
+                      f"pass per partition, CPU restatement of Spark 2.2 deequ semantics "
+                      f"(oracle/oracle.c, OpenMP, {threads} threads = Spark local[{threads}], every "
+                      f"CPU this process may use; the host has {host}) -- not Spark"}
 
 
 def h2d_inclusive(plan, state, seed: int, batch_rows: int = 1 << 24, passes: int = 8):
@@ -220,6 +229,7 @@ def main():
     # sanity: the row must be a valid S10 result
     assert row[0] == args.rows * world or world > 1 or row[0] == args.rows
 
+    traffic, traffic_src = load_traffic(args.rows, b_alg)
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -251,9 +261,8 @@ def main():
                 "peak": PEAK_HBM / 1e9,
                 "unit": "GB/s",
                 "frac": achieved / PEAK_HBM,
-                "traffic": load_traffic(args.rows, b_alg),
-                "traffic_source": "profiles/traffic_s10.json: HBM bytes per scan launch from a "
-                                  "separate rocprofv3 --pmc pass on this workload (not this run)",
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": b_alg,
                 "scan_ms": scan_ms,
                 "kernel": "dq::scan_mixed_kernel (+ finalize1/finalize2)",
@@ -261,24 +270,45 @@ def main():
         }
         if world == 1 and not args.no_h2d:
             out["h2d_inclusive"] = h2d_inclusive(plan, state, args.seed)
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.seed)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
+SCAN_SOURCES = ("scan.hip", "kernels.h", "engine.h", "device_util.h", "stream_load.h")
+
+
+def scan_source_hash() -> str:
+    """sha256 (16 hex digits) of the sources the scan kernel is compiled from: a PMC traffic
+    figure only describes the build whose sources hash the same."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in SCAN_SOURCES:
+        h.update(open(os.path.join(ROOT, "deequ_amd", "csrc", name), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def load_traffic(rows: int, b_alg: int):
-    """HBM bytes per scan launch from the committed rocprofv3 PMC pass (profiles/), if one was
-    recorded for this workload size; else null."""
+    """(HBM bytes per scan launch, source) from the committed rocprofv3 PMC passes
+    (profiles/traffic_s10.json) when they were recorded for this workload size AND this build of
+    the scan kernel (source hash); else (None, why)."""
     path = os.path.join(ROOT, "profiles", "traffic_s10.json")
     try:
         d = json.load(open(path))
-        if int(d.get("rows_per_gpu", -1)) == rows:
-            return d["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        pass
-    return None
+    except (OSError, ValueError):
+        return None, "no profiles/traffic_s10.json"
+    if int(d.get("rows_per_gpu", -1)) != rows:
+        return None, f"profiles/traffic_s10.json is for {d.get('rows_per_gpu')} rows per GPU"
+    if d.get("scan_source_sha") != scan_source_hash():
+        return None, (f"profiles/traffic_s10.json ({d.get('tag')}) was measured on another build "
+                      f"of the scan kernel (source hash {d.get('scan_source_sha')} != "
+                      f"{scan_source_hash()})")
+    return d["hbm_bytes_per_launch"], (
+        f"profiles/traffic_s10.json ({d.get('tag')}, scan source hash {d['scan_source_sha']}): "
+        "HBM bytes per scan launch from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+        "of this command (FETCH_SIZE x 2 on gfx950, KiB units), not this run")
 
 
 if __name__ == "__main__":

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <tuple>
@@ -1514,11 +1515,92 @@ extern "C" int dq_java_float_to_string(float value, char* buf) {
   return jfmt::float_to_java(value, buf);
 }
 
+// Bitmaps re-based for sliced Arrow arrays, owned by the library until dq_column_release.
+namespace {
+struct OwnedBitmap {
+  int device;  // -1: host malloc
+  size_t bytes;
+};
+std::mutex& owned_mutex() {
+  static std::mutex m;
+  return m;
+}
+std::map<const void*, OwnedBitmap>& owned_bitmaps() {
+  static auto* m = new std::map<const void*, OwnedBitmap>;
+  return *m;
+}
+
+// A bitmap of `rows` bits starting at bit `bit` of `src`, as a pointer to bit 0: aliases src when
+// the offset is whole bytes, else a re-based copy in src's memory space (device or host).
+dq_status bitmap_at(const uint8_t* src, int64_t bit, int64_t rows, const uint8_t** out) {
+  if (bit % 8 == 0 || rows == 0) {
+    *out = src + bit / 8;
+    return DQ_OK;
+  }
+  hipPointerAttribute_t attr{};
+  const bool on_device = hipPointerGetAttributes(&attr, src) == hipSuccess &&
+                         attr.type == hipMemoryTypeDevice;
+  (void)hipGetLastError();  // an unregistered host pointer leaves an error behind
+  const size_t n = (size_t)(rows + 7) / 8;
+  if (on_device) {
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(attr.device));
+    void* p = nullptr;
+    size_t got = 0;
+    int dev = 0;
+    hipError_t e = dev_alloc(&p, n + 16, &got, &dev);
+    if (e == hipSuccess) e = hipMemsetAsync(p, 0, got, nullptr);
+    if (e == hipSuccess) e = launch_bitmap_rebase(src, bit, rows, static_cast<uint8_t*>(p), nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    (void)hipSetDevice(cur);
+    if (e != hipSuccess) {
+      if (p) dev_free(p, got, dev);
+      return fail(e == hipErrorOutOfMemory ? DQ_ERR_OUT_OF_MEMORY : DQ_ERR_DEVICE,
+                  "re-basing a sliced bitmap: %s", hipGetErrorString(e));
+    }
+    std::lock_guard<std::mutex> lock(owned_mutex());
+    owned_bitmaps()[p] = OwnedBitmap{dev, got};
+    *out = static_cast<const uint8_t*>(p);
+    return DQ_OK;
+  }
+  auto* h = static_cast<uint8_t*>(std::calloc(n + 16, 1));
+  if (!h) return fail(DQ_ERR_OUT_OF_MEMORY, "re-basing a sliced bitmap");
+  const int64_t last = (bit + rows - 1) / 8;
+  const unsigned sh = (unsigned)(bit & 7);
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t j = bit / 8 + (int64_t)i;
+    unsigned v = src[j] >> sh;
+    if (j + 1 <= last) v |= (unsigned)src[j + 1] << (8 - sh);
+    h[i] = (uint8_t)v;
+  }
+  std::lock_guard<std::mutex> lock(owned_mutex());
+  owned_bitmaps()[h] = OwnedBitmap{-1, n + 16};
+  *out = h;
+  return DQ_OK;
+}
+
+void release_owned(const void* p) {
+  if (!p) return;
+  OwnedBitmap b{};
+  {
+    std::lock_guard<std::mutex> lock(owned_mutex());
+    auto it = owned_bitmaps().find(p);
+    if (it == owned_bitmaps().end()) return;
+    b = it->second;
+    owned_bitmaps().erase(it);
+  }
+  if (b.device < 0) std::free(const_cast<void*>(p));
+  else dev_free(const_cast<void*>(p), b.bytes, b.device);
+}
+}  // namespace
+
 extern "C" dq_status dq_column_from_arrow(const struct ArrowArray* array,
                                           const struct ArrowSchema* schema, dq_column* out) {
   if (!array || !schema || !out || !schema->format)
     return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
-  if (array->offset != 0) return fail(DQ_ERR_UNSUPPORTED, "arrays with a non-zero offset");
+  if (array->offset < 0 || array->length < 0)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "negative Arrow offset or length");
   std::string f(schema->format);
   int type = 0;
   if (f == "b") type = DQ_BOOL;
@@ -1532,13 +1614,41 @@ extern "C" dq_status dq_column_from_arrow(const struct ArrowArray* array,
   else return fail(DQ_ERR_UNSUPPORTED, "Arrow format '%s'", schema->format);
   int64_t need = type == DQ_UTF8 ? 3 : 2;
   if (array->n_buffers < need) return fail(DQ_ERR_INVALID_ARGUMENT, "too few Arrow buffers");
-  out->type = type;
-  out->data_bytes = 0;  // unknown: the Arrow C Data Interface carries no buffer sizes
-  out->length = array->length;
-  out->validity = array->null_count == 0 ? nullptr : static_cast<const uint8_t*>(array->buffers[0]);
-  out->values = array->buffers[1];
-  out->data = type == DQ_UTF8 ? static_cast<const uint8_t*>(array->buffers[2]) : nullptr;
+  const int64_t off = array->offset, n = array->length;
+  dq_column c{};
+  c.type = type;
+  c.data_bytes = 0;  // unknown: the Arrow C Data Interface carries no buffer sizes
+  c.length = n;
+  const auto* valid = static_cast<const uint8_t*>(array->buffers[0]);
+  if (array->null_count != 0 && valid) {
+    dq_status st = bitmap_at(valid, off, n, &c.validity);
+    if (st != DQ_OK) return st;
+  }
+  const auto* vals = static_cast<const uint8_t*>(array->buffers[1]);
+  if (type == DQ_BOOL) {
+    const uint8_t* v = nullptr;
+    dq_status st = vals ? bitmap_at(vals, off, n, &v) : DQ_OK;
+    if (st != DQ_OK) {
+      release_owned(c.validity);
+      return st;
+    }
+    c.values = v;
+  } else if (type == DQ_UTF8) {  // offsets stay absolute into the (unsliced) character buffer
+    c.values = vals ? vals + 4 * off : nullptr;
+    c.data = static_cast<const uint8_t*>(array->buffers[2]);
+  } else {
+    const int64_t w = type == DQ_INT8 ? 1 : type == DQ_INT16 ? 2
+                    : (type == DQ_INT32 || type == DQ_FLOAT32) ? 4 : 8;
+    c.values = vals ? vals + w * off : nullptr;
+  }
+  *out = c;
   return DQ_OK;
+}
+
+extern "C" void dq_column_release(dq_column* col) {
+  if (!col) return;
+  release_owned(col->validity);
+  if (col->type == DQ_BOOL) release_owned(col->values);
 }
 
 // ------------------------------------------------------------------------------------------------

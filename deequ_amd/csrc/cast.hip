@@ -161,7 +161,33 @@ __global__ void __launch_bounds__(kCastThreads) cast_utf8_kernel(
   if (bad) atomicAdd(n_unsupported, (unsigned long long)bad);
 }
 
+// Arrow bitmap at bit offset `bit` -> LSB-first bitmap at bit 0 (one thread per output byte).
+// Reads only bytes that hold bits of rows [bit, bit + rows).
+__global__ void __launch_bounds__(kCastThreads)
+bitmap_rebase_kernel(const uint8_t* __restrict__ src, int64_t bit, int64_t rows,
+                     uint8_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * kCastThreads + threadIdx.x;
+  const int64_t n_out = (rows + 7) / 8;
+  if (i >= n_out) return;
+  const int64_t last_src = (bit + rows - 1) / 8;  // last source byte holding a row's bit
+  const int64_t j = bit / 8 + i;
+  const uint32_t sh = (uint32_t)(bit & 7);
+  uint32_t v = src[j] >> sh;
+  if (sh && j + 1 <= last_src) v |= (uint32_t)src[j + 1] << (8 - sh);
+  dst[i] = (uint8_t)v;
+}
+
 }  // namespace
+
+hipError_t launch_bitmap_rebase(const uint8_t* src, int64_t bit, int64_t rows, uint8_t* dst,
+                                hipStream_t stream) {
+  const int64_t n_out = (rows + 7) / 8;
+  if (n_out <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bitmap_rebase_kernel, dim3((unsigned)((n_out + kCastThreads - 1) / kCastThreads)),
+                     dim3(kCastThreads), 0, stream, src, bit, rows, dst);
+  return hipGetLastError();
+}
+
 }  // namespace dq
 
 using namespace dq;

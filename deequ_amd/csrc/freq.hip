@@ -45,6 +45,7 @@
 #include "engine.h"
 #include "freq_codec.h"
 #include "kernels.h"
+#include "stream_load.h"
 
 namespace dq {
 
@@ -237,6 +238,11 @@ struct AArgs {
   unsigned long long* arena_cursor;
   unsigned long long* counters;
   unsigned long long* dbg_clock;  // DQ_FREQ_DEBUG=2: workgroup 0's phase timestamps (wall clock)
+  // the small-key path (freq_phaseA_small) tried this batch first when fast_epoch != 0:
+  // fast_words = {epoch of the last batch it could not take, its NULL rows, its NULL-group rows}
+  unsigned long long* fast_words;
+  uint64_t fast_epoch;
+  int32_t vec_ok;  // offsets / validity aligned for the 16-byte / dword streaming loads
 };
 
 // Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
@@ -280,6 +286,19 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   __shared__ uint64_t scnt[FROM_REC ? kThreads : 1];
 
   const int tid = threadIdx.x;
+  if constexpr (STR1) {
+    if (a.fast_epoch) {  // freq_phaseA_small ran first: it either took the batch or gave it up
+      const bool taken = a.fast_words[0] != a.fast_epoch;
+      if (blockIdx.x == 0 && tid == 0) {  // its NULL counts count only if its output stands
+        if (taken) {
+          a.counters[C_NULL_ROWS] += a.fast_words[1];
+          a.counters[C_NULL_GROUP] += a.fast_words[2];
+        }
+        a.fast_words[1] = a.fast_words[2] = 0;
+      }
+      if (taken) return;
+    }
+  }
   const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
   const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
   const int64_t t1 = min(t0 + (int64_t)a.tiles_per_wg, n_tiles);
@@ -768,6 +787,266 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   __syncthreads();
   if (tid < 3 && s_dbg[tid]) atomicAdd(&a.counters[C_DBG_NOTREADY + tid], (unsigned long long)s_dbg[tid]);
   wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase A, small keys: a one-utf8-column key whose strings are at most 7 bytes long and that takes
+// few distinct values (priority: 3) -- the common low-cardinality case -- counted at streaming
+// speed, without hashing, LDS tables or barriers per tile.
+//
+// A string of at most 7 bytes is its own exact 64-bit key: bytes | length << 56.  Each wave walks
+// 1024-row steps like the scan's TK_STR_IN body (16-byte offset loads, one unaligned 8-byte load
+// per string, the validity slice redistributed across the wave) and keeps up to kSmallCand
+// candidate keys, wave-uniform, with one u32 counter per candidate per lane: a row costs a few
+// compares and adds in registers.  A key not among the candidates joins them (a wave-uniform loop,
+// once per new key per wave).  A string longer than 7 bytes, or a (kSmallCand + 1)-th key in a
+// wave, gives the batch up: the wave stores the batch's epoch in fast_words[0] and every wave
+// stops at its next step, and the general phase A (launched right behind, freq_phaseA<STR1>)
+// sees the epoch and does the batch itself.  Otherwise the general kernel returns at once and this
+// kernel's output stands: every tile chunk of the workgroup empty, and the workgroup's groups in
+// its own chunk (n_tiles + blockIdx.x), exactly the layout phase A leaves for collapsed keys --
+// records {h, arena offset << 8 | count digit} with the row hash of freq_codec.h and the key
+// encoded in the arena as str1_encode would.
+// ------------------------------------------------------------------------------------------------
+constexpr int kSmallCand = 8;
+constexpr int kSmallThreads = 256;
+constexpr uint64_t kLongKey = ~0ULL;
+
+DQ_DEV uint64_t small_key(uint64_t v, int32_t len) {
+  if (len > 7) return kLongKey;
+  const uint64_t m = len > 0 ? (~0ULL >> (64 - 8 * len)) : 0ULL;
+  return (v & m) | ((uint64_t)len << 56);
+}
+
+__global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
+  constexpr int NW = kSmallThreads / 64;
+  __shared__ uint64_t s_key[NW * kSmallCand], s_cnt[NW * kSmallCand];
+  __shared__ uint32_t s_nc[NW];
+  __shared__ uint64_t g_key[NW * kSmallCand], g_cnt[NW * kSmallCand], g_off[NW * kSmallCand];
+  __shared__ uint32_t g_rec[NW * kSmallCand];  // records (count digits) per group
+  __shared__ uint32_t s_ng;
+  const int tid = threadIdx.x, lane = (int)__lane_id(), wave = tid >> 6;
+  const KeyCol& c = a.ks.cols[0];
+  const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
+  const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
+  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
+  const int64_t t1 = min(t0 + (int64_t)a.tiles_per_wg, n_tiles);
+  for (int64_t i = t0 * kHistRow + tid; i < t1 * kHistRow; i += kSmallThreads) a.hist[i] = 0;
+  const int64_t r_begin = t0 * a.tile_items, r_end = min(t1 * a.tile_items, a.n_items);
+  const int32_t dlen = off[a.n_items];
+
+  uint64_t cand[kSmallCand];
+  uint32_t cnt[kSmallCand];
+#pragma unroll
+  for (int k = 0; k < kSmallCand; ++k) {
+    cand[k] = kLongKey;
+    cnt[k] = 0;
+  }
+  int nc = 0;
+  bool gave_up = false;
+  unsigned long long nulls = 0;
+  // count the rows of `pend` (bit i: key[i]) that match a candidate; returns the rest.  Each row
+  // finds its candidate index (unused candidates hold kLongKey, which no counted row has) and adds
+  // one to that index's byte of a packed per-lane counter word (<= 16 per byte per call).
+  auto count = [&](const uint64_t* key, uint32_t pend) -> uint32_t {
+    uint64_t packed = 0;
+    uint32_t miss = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      int idx = kSmallCand;
+#pragma unroll
+      for (int k = 0; k < kSmallCand; ++k) idx = key[i] == cand[k] ? k : idx;
+      const bool p = (pend >> i) & 1u;
+      packed += (p && idx < kSmallCand) ? (1ULL << (8 * idx)) : 0ULL;
+      miss |= (p && idx == kSmallCand ? 1u : 0u) << i;
+    }
+#pragma unroll
+    for (int k = 0; k < kSmallCand; ++k) cnt[k] += (uint32_t)(packed >> (8 * k)) & 0xffu;
+    return miss;
+  };
+  // rows whose key is not yet a candidate: add their keys (wave-uniform), then count them
+  auto admit = [&](const uint64_t* key, uint32_t pend) {
+    while (true) {
+      const uint64_t any = __ballot(pend != 0);
+      if (!any) break;
+      const int src = __builtin_ctzll(any);
+      uint64_t fk = 0;
+#pragma unroll
+      for (int i = 15; i >= 0; --i)
+        if ((pend >> i) & 1u) fk = key[i];
+      const uint64_t nk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(fk >> 32), src) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)fk, src);
+      if (nc == kSmallCand || nk == kLongKey) {
+        gave_up = true;
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < kSmallCand; ++k)
+        if (k == nc) cand[k] = nk;
+      ++nc;
+      pend = count(key, pend);
+    }
+  };
+
+  const bool vec = a.vec_ok != 0;
+  for (int64_t r0 = r_begin + (int64_t)wave * kWaveRows; r0 < r_end && !gave_up;
+       r0 += (int64_t)NW * kWaveRows) {
+    if (__hip_atomic_load(&a.fast_words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        a.fast_epoch) {
+      gave_up = true;  // another wave gave the batch up
+      break;
+    }
+    uint64_t key[16];
+    uint32_t vb = 0;
+    if (vec && r0 + kWaveRows <= r_end) {
+      // lane l owns rows r0 + 256 g + 4 l + j
+      int32_t o[4][5];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint4 u = ld16(off + r0 + 256 * g + 4 * lane);
+        o[g][0] = (int32_t)u.x;
+        o[g][1] = (int32_t)u.y;
+        o[g][2] = (int32_t)u.z;
+        o[g][3] = (int32_t)u.w;
+        const int32_t last = ldg_i32(off + r0 + 256 * g + 256);
+        const int32_t nxt = __shfl_down((int32_t)u.x, 1);
+        o[g][4] = lane == 63 ? last : nxt;
+      }
+      if (c.valid) {
+        ChunkBits cb;
+        cb.load(c.valid, r0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) vb |= cb.get(256 * g + 4 * lane, 4) << (4 * g);
+      } else {
+        vb = 0xffffu;
+      }
+      const int32_t step_end = __shfl(o[3][4], 63);
+      if ((int64_t)step_end + 8 <= (int64_t)dlen) {
+        uint64_t v[16];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[4 * g + j] = ldg64_unaligned(c.data + o[g][j]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) key[4 * g + j] = small_key(v[4 * g + j], o[g][j + 1] - o[g][j]);
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int32_t len = o[g][j + 1] - o[g][j];
+            uint64_t w0 = 0, w1 = 0;
+            if (len > 0 && len <= 7) load_str16(c.data + o[g][j], len, w0, w1);
+            key[4 * g + j] = small_key(w0, len);
+          }
+      }
+    } else {  // batch tail or unaligned buffers: lane l owns rows r0 + 64 i + l, bounds-checked
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t r = r0 + 64 * i + lane;
+        key[i] = kLongKey;
+        if (r < r_end && kbit(c.valid, r)) {
+          vb |= 1u << i;
+          const int32_t s0 = off[r], len = off[r + 1] - s0;
+          uint64_t w0 = 0, w1 = 0;
+          if (len > 0 && len <= 7) load_str16(c.data + s0, len, w0, w1);
+          key[i] = small_key(w0, len);
+        }
+      }
+      uint32_t in = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) in |= (r0 + 64 * i + lane < r_end ? 1u : 0u) << i;
+      nulls += __popc(in & ~vb);
+      uint32_t pend = count(key, vb);
+      if (__ballot(pend != 0)) admit(key, pend);
+      continue;
+    }
+    nulls += 16 - __popc(vb);
+    uint32_t pend = count(key, vb);
+    if (__ballot(pend != 0)) admit(key, pend);
+  }
+  if (gave_up && lane == 0)
+    __hip_atomic_store(&a.fast_words[0], (unsigned long long)a.fast_epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (__syncthreads_or(gave_up ? 1 : 0)) return;  // every wave of the workgroup returns here
+  // the wave's candidates and counts -> LDS; thread 0 merges the waves' lists
+  if (lane == 0) s_nc[wave] = (uint32_t)nc;
+#pragma unroll
+  for (int k = 0; k < kSmallCand; ++k) {
+    const uint64_t tot = wave_sum((uint64_t)cnt[k]);
+    if (lane == 0 && k < nc) {
+      s_key[wave * kSmallCand + k] = cand[k];
+      s_cnt[wave * kSmallCand + k] = tot;
+    }
+  }
+  nulls = wave_sum(nulls);
+  if (lane == 0 && nulls)
+    atomicAdd(&a.fast_words[a.ks.null_as_group ? 2 : 1], nulls);
+  __syncthreads();
+  if (tid == 0) {  // <= NW * kSmallCand groups: merged, encoded, hashed, placed by one thread
+    uint32_t ng = 0;
+    for (int w = 0; w < NW; ++w)
+      for (uint32_t k = 0; k < s_nc[w]; ++k) {
+        const uint64_t key = s_key[w * kSmallCand + k], ct = s_cnt[w * kSmallCand + k];
+        if (!ct) continue;
+        uint32_t g = 0;
+        while (g < ng && g_key[g] != key) ++g;
+        if (g == ng) {
+          g_key[ng] = key;
+          g_cnt[ng++] = 0;
+        }
+        g_cnt[g] += ct;
+      }
+    uint64_t bytes = 0;
+    for (uint32_t g = 0; g < ng; ++g) bytes += 8 + pad4((uint32_t)(g_key[g] >> 56));
+    uint64_t at = bytes ? atomicAdd(a.arena_cursor, (unsigned long long)bytes) : 0ULL;
+    for (uint32_t g = 0; g < ng; ++g) {  // str1_encode of the key: {1, len, bytes as LE words}
+      const uint32_t len = (uint32_t)(g_key[g] >> 56);
+      const uint64_t w0 = g_key[g] & ((1ULL << 56) - 1);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(a.arena + at);
+      dst[0] = 1;
+      dst[1] = len;
+      if (len > 0) dst[2] = (uint32_t)w0;
+      if (len > 4) dst[3] = (uint32_t)(w0 >> 32);
+      g_off[g] = at;
+      at += 8 + pad4(len);
+      g_key[g] = str_row_hash_reg(w0, 0, (int32_t)len);  // from here on: the group's row hash
+      uint32_t nd = 0;
+      for (uint64_t x = g_cnt[g]; x; x >>= 2) nd += (x & 3) ? 1u : 0u;
+      g_rec[g] = nd;
+    }
+    s_ng = ng;
+  }
+  __syncthreads();
+  // the workgroup's chunk: records bucket-sorted (groups of one bucket in group order), its
+  // histogram row the exclusive prefix of the records per bucket
+  const uint32_t ng = s_ng;
+  const int64_t fchunk = n_tiles + blockIdx.x;
+  uint16_t* hrow = a.hist + fchunk * kHistRow;
+  for (int b = tid; b <= kBuckets; b += kSmallThreads) {
+    uint32_t before = 0;
+    for (uint32_t g = 0; g < ng; ++g)
+      if (b == kBuckets || bucket_of(g_key[g]) < (uint32_t)b) before += g_rec[g];
+    hrow[b] = (uint16_t)before;
+  }
+  if (tid < (int)ng) {
+    const uint32_t g = (uint32_t)tid, bg = bucket_of(g_key[g]);
+    uint32_t pos = 0;
+    for (uint32_t q = 0; q < ng; ++q) {
+      const uint32_t bq = bucket_of(g_key[q]);
+      if (bq < bg || (bq == bg && q < g)) pos += g_rec[q];
+    }
+    uint64_t* out = reinterpret_cast<uint64_t*>(a.recs) + (fchunk * (int64_t)FM<true>::kTile + pos) * 2;
+    const uint64_t h = g_key[g], rep = g_off[g];
+    uint32_t d = 0;
+    for_digits(g_cnt[g], [&](uint32_t code) {
+      out[2 * d] = h;
+      out[2 * d + 1] = (rep << 8) | code;
+      ++d;
+    });
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1848,6 +2127,16 @@ struct dq_freq {
                           // + the worst case of every batch added since)
   int64_t num_rows = 0;
   hipStream_t stream = nullptr;
+  // the small-key phase A (freq_phaseA_small): the epoch of its last attempt, and a pinned copy of
+  // the epoch it last gave up (copied back asynchronously: a table it gave up on stops trying)
+  uint64_t fast_epoch = 0;
+  bool fast_off = false;
+  struct PinnedWord {
+    unsigned long long* p = nullptr;
+    ~PinnedWord() {
+      if (p) (void)hipHostFree(p);
+    }
+  } fast_seen;
   // finalize cache (phase B)
   bool b_valid = false;
   int s_bits = 0;
@@ -2006,6 +2295,41 @@ static void launch_phaseA(dq_freq* f, AArgs a, bool from_rec) {
               a.ks.null_as_group ? " (histogram)" : "", acc[0] / nt, acc[1] / nt, acc[2] / nt,
               acc[3] / nt, nt);
   }
+}
+
+// The small-key phase A over one batch of a one-utf8-column key, before the general one (which
+// returns at once when this one took the batch).  Tried while the batch's strings average at most
+// 8 bytes (its data_bytes hint) and until the table sees it give a batch up.
+static bool small_keys_worth_trying(dq_freq* f, const dq_column& k, int64_t rows) {
+  static const bool enabled = [] {
+    const char* e = getenv("DQ_FREQ_SMALL");
+    return !e || atoi(e) != 0;
+  }();
+  if (!enabled || f->exact || f->n_keys != 1 || f->types[0] != DQ_UTF8 || rows < 4096) return false;
+  if (f->fast_off) return false;
+  if (f->fast_seen.p && f->fast_epoch && *(volatile unsigned long long*)f->fast_seen.p == f->fast_epoch) {
+    f->fast_off = true;  // the last attempt gave its batch up: long strings or many keys
+    return false;
+  }
+  return k.data_bytes > 0 && (int64_t)k.data_bytes <= 8 * rows;
+}
+
+static dq_status launch_phaseA_small(dq_freq* f, AArgs& a) {
+  if (!f->fast_seen.p) {
+    HIP_TRY(hipHostMalloc((void**)&f->fast_seen.p, 8, hipHostMallocDefault));
+    *f->fast_seen.p = 0;
+  }
+  int64_t n_wg = 0;
+  phaseA_chunks(true, false, a.n_items, a.tile_items, &n_wg);
+  a.tiles_per_wg = AKeys<true, false>::kTilesPerWg;
+  a.fast_words = f->dev_words.p + C_N + 1;
+  a.fast_epoch = ++f->fast_epoch;
+  const KeyCol& c = a.ks.cols[0];
+  a.vec_ok = (reinterpret_cast<uintptr_t>(c.values) & 15u) == 0 &&
+             (reinterpret_cast<uintptr_t>(c.valid) & 3u) == 0;
+  hipLaunchKernelGGL(freq_phaseA_small, dim3((unsigned)n_wg), dim3(kSmallThreads), 0, f->stream, a);
+  HIP_TRY(hipGetLastError());
+  return DQ_OK;
 }
 
 static AArgs base_args(dq_freq* f) {
@@ -2641,8 +2965,8 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
   f->tile = f->exact ? FM<false>::kTile : FM<true>::kTile;
   f->rb = f->exact ? FM<false>::kRB : FM<true>::kRB;
   HIP_TRY(hipSetDevice(device));
-  HIP_TRY(f->dev_words.ensure(C_N + 1));
-  HIP_TRY(hipMemset(f->dev_words.p, 0, (C_N + 1) * 8));
+  HIP_TRY(f->dev_words.ensure(C_N + 4));  // counters, arena cursor, small-key words (3)
+  HIP_TRY(hipMemset(f->dev_words.p, 0, (C_N + 4) * 8));
   if (capacity_hint > 0) {  // the chunks phase A writes for that many rows (+ per-batch rounding)
     const int64_t chunks = phaseA_chunks(!f->exact, false, capacity_hint, f->tile, nullptr) +
                            2 * (capacity_hint >> 24) + 16;
@@ -2657,7 +2981,7 @@ extern "C" dq_status dq_freq_reset(dq_freq* f, void* hip_stream) {
   if (!f) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   HIP_TRY(hipSetDevice(f->device));
   f->stream = reinterpret_cast<hipStream_t>(hip_stream);
-  HIP_TRY(hipMemsetAsync(f->dev_words.p, 0, (C_N + 1) * 8, f->stream));
+  HIP_TRY(hipMemsetAsync(f->dev_words.p, 0, (C_N + 4) * 8, f->stream));
   for (int k = 0; k < C_N; ++k) f->h_counters[k] = 0;
   f->arena_used = 0;
   f->arena_hi = 0;
@@ -2721,6 +3045,10 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
         bound += (uint64_t)rows * 12;
       }
     }
+    // + what a small-key attempt that gives the batch up may have reserved
+    int64_t n_wg_a = 0;
+    phaseA_chunks(true, false, rows, f->tile, &n_wg_a);
+    bound += (uint64_t)n_wg_a * (kSmallThreads / 64) * kSmallCand * 16;
     if (f->arena.n < f->arena_hi + bound + 64) {  // may not fit: learn the true use, then grow
       dq_status cs = pull_counters(f);
       if (cs != DQ_OK) return cs;
@@ -2734,9 +3062,16 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     a.ks.cols[k] = KeyCol{keys[k].type, 0, keys[k].validity, keys[k].values, keys[k].data};
   a.n_items = rows;
   a.tile_items = f->tile;
+  const bool small = small_keys_worth_trying(f, keys[0], rows);
+  if (small) {
+    dq_status ss = launch_phaseA_small(f, a);
+    if (ss != DQ_OK) return ss;
+  }
   if (f->exact) launch_phaseA<false>(f, a, false);
   else launch_phaseA<true>(f, a, false);
   HIP_TRY(hipGetLastError());
+  if (small)  // the host learns (late, without a wait) whether the attempt gave the batch up
+    HIP_TRY(hipMemcpyAsync(f->fast_seen.p, a.fast_words, 8, hipMemcpyDeviceToHost, f->stream));
   f->n_chunks += chunks;
   f->counters_stale = true;  // read back at finalize / merge / arena growth
   return DQ_OK;

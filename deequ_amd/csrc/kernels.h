@@ -108,6 +108,9 @@ struct XInstr {
 
 constexpr int kMaxStack = 16;
 
+// Arrow bitmap at a bit offset -> bitmap at bit 0 (cast.hip; sliced Arrow arrays at the ABI).
+hipError_t launch_bitmap_rebase(const uint8_t* src, int64_t bit, int64_t rows, uint8_t* dst,
+                                hipStream_t stream);
 hipError_t launch_expr(const XInstr* prog, int n_instr, const DevCol* cols, const uint8_t* pool,
                        int64_t rows, uint64_t* out_val, uint64_t* out_vld, hipStream_t stream);
 // Body classes of the scan: one kernel instantiation each (scan.hip).

@@ -40,6 +40,68 @@ class HostColumn:
         return sum(b.nbytes for b in (self.validity, self.values, self.data) if b is not None)
 
 
+class ArrowSchemaC(ctypes.Structure):
+    pass
+
+
+class ArrowArrayC(ctypes.Structure):
+    pass
+
+
+ArrowSchemaC._fields_ = [("format", ctypes.c_char_p), ("name", ctypes.c_char_p),
+                         ("metadata", ctypes.c_char_p), ("flags", ctypes.c_int64),
+                         ("n_children", ctypes.c_int64),
+                         ("children", ctypes.POINTER(ctypes.POINTER(ArrowSchemaC))),
+                         ("dictionary", ctypes.POINTER(ArrowSchemaC)),
+                         ("release", ctypes.CFUNCTYPE(None, ctypes.POINTER(ArrowSchemaC))),
+                         ("private_data", ctypes.c_void_p)]
+ArrowArrayC._fields_ = [("length", ctypes.c_int64), ("null_count", ctypes.c_int64),
+                        ("offset", ctypes.c_int64), ("n_buffers", ctypes.c_int64),
+                        ("n_children", ctypes.c_int64),
+                        ("buffers", ctypes.POINTER(ctypes.c_void_p)),
+                        ("children", ctypes.POINTER(ctypes.POINTER(ArrowArrayC))),
+                        ("dictionary", ctypes.POINTER(ArrowArrayC)),
+                        ("release", ctypes.CFUNCTYPE(None, ctypes.POINTER(ArrowArrayC))),
+                        ("private_data", ctypes.c_void_p)]
+
+
+class ArrowColumn:
+    """One host pyarrow array handed to the engine through the Arrow C Data Interface, as the JNI
+    shim hands a Spark partition's export: exported with _export_to_c and
+    imported by dq_column_from_arrow, which honours ArrowArray.offset (sliced arrays).  Keeps the
+    export alive until the engine column is released."""
+
+    def __init__(self, arr):
+        self.array = ArrowArrayC()
+        self.schema = ArrowSchemaC()
+        arr._export_to_c(ctypes.addressof(self.array), ctypes.addressof(self.schema))
+        self.column = N.dq_column()
+        try:
+            N.check(N.lib.dq_column_from_arrow(ctypes.addressof(self.array),
+                                               ctypes.addressof(self.schema),
+                                               ctypes.byref(self.column)))
+        except Exception:
+            self._release_export()
+            raise
+        self.dtype = int(self.column.type)
+        self.length = int(self.column.length)
+
+    def to_c(self) -> N.dq_column:
+        return self.column
+
+    def _release_export(self):
+        for s in (self.array, self.schema):
+            if s.release:
+                s.release(ctypes.byref(s))
+
+    def __del__(self):
+        try:
+            N.lib.dq_column_release(ctypes.byref(self.column))
+            self._release_export()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
 class HostTable:
     """Record batches of host columns (the host counterpart of table.Table)."""
 
@@ -79,6 +141,21 @@ class HostTable:
                 v, vals, d = array_to_host(arr, f.dtype)
                 cols[f.name] = HostColumn(f.dtype, len(arr), v, vals, d)
             out.append(cols)
+        return HostTable(StructType(fields), out)
+
+    @staticmethod
+    def from_arrow_c(batches, schema=None) -> "HostTable":
+        """Record batches (or sliced ones) imported through the Arrow C Data Interface, buffers
+        aliased where the engine can (ArrowColumn): the JNI shim's path."""
+        import pyarrow as pa
+        batches = list(batches)
+        schema = schema or batches[0].schema
+        fields = []
+        for f in schema:
+            if f.type == pa.large_string():
+                raise TypeError(f"column {f.name}: large_string has 64-bit offsets")
+            fields.append(StructField(f.name, _ARROW_TO_DQ[str(f.type)]))
+        out = [{f.name: ArrowColumn(rb.column(i)) for i, f in enumerate(fields)} for rb in batches]
         return HostTable(StructType(fields), out)
 
 
@@ -148,4 +225,4 @@ def compute_frequencies_host(host_table: HostTable, columns: Sequence[str], devi
     return table
 
 
-__all__ = ["HostColumn", "HostTable", "HostLoader", "run_scan_host", "compute_frequencies_host"]
+__all__ = ["ArrowColumn", "HostColumn", "HostTable", "HostLoader", "run_scan_host", "compute_frequencies_host"]

@@ -111,12 +111,19 @@ struct ArrowArray {
 };
 #endif
 
-/* Converts one Arrow C Data Interface array (primitive or utf8, offset 0) into a dq_column that
+/* Converts one Arrow C Data Interface array (primitive or utf8, any offset) into a dq_column that
  * aliases the same buffers.  The JNI shim calls this on each exported
- * DataFrame-partition column.  Buffers may be host or device pointers; the caller says which by
- * the entry point it hands the column to. */
+ * DataFrame-partition column (a sliced partition carries a non-zero ArrowArray.offset).  Values and
+ * utf8 offsets are aliased at the slice's first row (utf8 offsets stay absolute into the character
+ * buffer); a validity bitmap (or boolean values) whose offset is not a whole number of bytes is
+ * copied, re-based to bit 0, into the memory space it came from (device or host), and owned by the
+ * library until dq_column_release.  Buffers may be host or device pointers; the caller says which
+ * by the entry point it hands the column to. */
 dq_status dq_column_from_arrow(const struct ArrowArray* array, const struct ArrowSchema* schema,
                                dq_column* out);
+/* Frees what dq_column_from_arrow allocated for `col` (re-based bitmaps); a no-op for a column
+ * that only aliases Arrow buffers. */
+void dq_column_release(dq_column* col);
 
 /* ------------------------------------------------------------------------------------------------
  * Expressions (SQL predicates of `where` filters and Compliance / Check constraints).

@@ -17,6 +17,12 @@ class OrNumeric(ctypes.Structure):
                 ("pred_nonnull", ctypes.c_int64)]
 
 
+class OrS10(ctypes.Structure):
+    _fields_ = [("rows", ctypes.c_int64), ("id_nonnull", ctypes.c_int64),
+                ("name_nonnull", ctypes.c_int64), ("prio_true", ctypes.c_int64),
+                ("views", OrNumeric)]
+
+
 def lib():
     global _LIB
     if _LIB is None:
@@ -27,6 +33,8 @@ def lib():
         L = ctypes.CDLL(path)
         vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
         L.or_numeric_i64.argtypes = [vp, vp, i64, i32, i64, i32, ctypes.POINTER(OrNumeric)]
+        L.or_s10_fused.argtypes = [vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, i32, i32,
+                                   ctypes.POINTER(OrS10)]
         L.or_validity_count.argtypes = [vp, i64, i32]
         L.or_validity_count.restype = i64
         L.or_str_in.argtypes = [vp, vp, vp, i64, vp, vp, i32, i32, i32, ctypes.POINTER(i64),
@@ -89,3 +97,16 @@ def freq_i64(values, valid_bits, num_rows):
     lib().or_freq_i64(_p(values), _p(valid_bits), len(values), num_rows, ctypes.byref(g),
                       ctypes.byref(u), ctypes.byref(e))
     return int(g.value), int(u.value), float(e.value)
+
+
+def s10_fused(buf: dict, items=("high", "low"), threads: int = 1) -> OrS10:
+    """S10 as one pass over item_buffers_numpy()'s buffers (the reference's one Spark job)."""
+    lb = b"".join(i.encode() for i in items)
+    lo = np.array([0] + list(np.cumsum([len(i.encode()) for i in items])), np.int32)
+    lbuf = np.frombuffer(lb + b"\0", np.uint8)
+    out = OrS10()
+    lib().or_s10_fused(_p(buf["id_valid"]), _p(buf["name_valid"]), _p(buf["numViews"]),
+                       _p(buf["numViews_valid"]), _p(buf["priority_offsets"]),
+                       _p(buf["priority_data"]), _p(buf["priority_valid"]), buf["n"], _p(lbuf),
+                       _p(lo), len(items), threads, ctypes.byref(out))
+    return out

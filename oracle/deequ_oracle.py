@@ -886,7 +886,8 @@ def mutual_information(t: OTable, c1: str, c2: str) -> Optional[float]:
         px[x] = px.get(x, 0) + c
         py[y] = py.get(y, 0) + c
     total = t.n
-    acc = 0.0
-    for (x, y), c in joint.items():
-        acc += (c / total) * math.log((c / total) / ((px[x] / total) * (py[y] / total)))
-    return acc
+    # Spark sums the per-group terms in partition order, which no fixed order reproduces: the
+    # oracle takes the exactly rounded sum of the same terms (fsum), the reference point every
+    # summation order is within its own rounding error of
+    return math.fsum((c / total) * math.log((c / total) / ((px[x] / total) * (py[y] / total)))
+                     for (x, y), c in joint.items())

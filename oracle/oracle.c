@@ -145,6 +145,77 @@ void or_str_in(const int32_t* off, const uint8_t* data, const uint8_t* valid, in
   *nn_out = nn;
 }
 
+/* ------------------------------------------------------- S10 as ONE pass (bench baseline) --- */
+/* The reference runs a suite as one Spark job (AnalysisRunner.scala:279-326): each task walks its
+ * partition once and updates every aggregate of the suite per row.  Same here for S10: Size,
+ * Completeness(id), Completeness(name), Compliance(numViews >= 0), Compliance(priority IS NULL OR
+ * priority IN (list)), Sum / Mean / StdDev / Min / Max(numViews); partitions merged in order. */
+typedef struct {
+  int64_t rows, id_nonnull, name_nonnull, prio_true;
+  or_numeric views;
+} or_s10;
+
+void or_s10_fused(const uint8_t* id_valid, const uint8_t* name_valid, const int64_t* views,
+                  const uint8_t* views_valid, const int32_t* prio_off, const uint8_t* prio_data,
+                  const uint8_t* prio_valid, int64_t n, const uint8_t* list_bytes,
+                  const int32_t* list_off, int n_list, int nthreads, or_s10* out) {
+  if (nthreads < 1) nthreads = 1;
+  or_s10* parts = (or_s10*)calloc((size_t)nthreads, sizeof(or_s10));
+#pragma omp parallel for num_threads(nthreads) schedule(static, 1)
+  for (int p = 0; p < nthreads; ++p) {
+    int64_t r0 = n * p / nthreads, r1 = n * (p + 1) / nthreads;
+    or_s10 s;
+    memset(&s, 0, sizeof(s));
+    s.views.min = INT64_MAX;
+    s.views.max = INT64_MIN;
+    for (int64_t r = r0; r < r1; ++r) {
+      s.rows += 1;
+      s.id_nonnull += bit(id_valid, r);
+      s.name_nonnull += bit(name_valid, r);
+      if (bit(views_valid, r)) {
+        int64_t x = views[r];
+        s.views.count += 1;
+        s.views.sum_long = (int64_t)((uint64_t)s.views.sum_long + (uint64_t)x);
+        if (x < s.views.min) s.views.min = x;
+        if (x > s.views.max) s.views.max = x;
+        double xd = (double)x;
+        double n2 = s.views.n + 1.0, delta = xd - s.views.avg, delta_n = delta / n2;
+        s.views.avg += delta_n;
+        s.views.m2 += delta * (delta - delta_n);
+        s.views.n = n2;
+        s.views.pred_nonnull += 1;
+        s.views.pred_true += x >= 0;
+      }
+      if (!bit(prio_valid, r)) {
+        s.prio_true += 1;
+      } else {
+        int32_t st = prio_off[r], len = prio_off[r + 1] - st;
+        for (int j = 0; j < n_list; ++j) {
+          int32_t ls = list_off[j], ll = list_off[j + 1] - ls;
+          if (ll == len && memcmp(prio_data + st, list_bytes + ls, (size_t)len) == 0) {
+            s.prio_true += 1;
+            break;
+          }
+        }
+      }
+    }
+    parts[p] = s;
+  }
+  or_s10 acc;
+  memset(&acc, 0, sizeof(acc));
+  acc.views.min = INT64_MAX;
+  acc.views.max = INT64_MIN;
+  for (int p = 0; p < nthreads; ++p) {
+    acc.rows += parts[p].rows;
+    acc.id_nonnull += parts[p].id_nonnull;
+    acc.name_nonnull += parts[p].name_nonnull;
+    acc.prio_true += parts[p].prio_true;
+    numeric_merge(&acc.views, &parts[p].views);
+  }
+  *out = acc;
+  free(parts);
+}
+
 /* ---------------------------------------------------------------- XXH64 ------------------- */
 #define XP1 0x9E3779B185EBCA87ULL
 #define XP2 0xC2B2AE3D27D4EB4FULL

@@ -117,3 +117,50 @@ def test_approx_count_distinct_in_bias_range_is_a_failure_not_a_wrong_number():
     small = tuple(O.hll_words(O.hll_registers(list(range(50)), "long")))
     assert ApproxCountDistinct("c").compute_metric_from(ApproxCountDistinctState(small)).value.get() \
         == O.hll_count(small)[0]
+
+
+@pytest.mark.parametrize("offset", [0, 8, 3, 13])
+def test_sliced_arrow_arrays_import_at_their_offset(offset):
+    """dq_column_from_arrow honours ArrowArray.offset (a sliced Spark partition export): values
+    and utf8 offsets aliased at the first row, bitmaps at a bit offset re-based to bit 0 (host
+    buffers here; the device path is in test_gpu_loader.py)."""
+    import ctypes
+
+    import numpy as np
+    import pyarrow as pa
+
+    from deequ_amd.loader import ArrowColumn
+    rng = np.random.default_rng(offset)
+    n = 200
+    mask = rng.random(n) < 0.3
+    cases = [pa.array(rng.integers(-99, 99, n), mask=mask, type=pa.int64()),
+             pa.array(rng.normal(size=n).astype(np.float32), mask=mask, type=pa.float32()),
+             pa.array(rng.integers(-9, 9, n).astype(np.int16), mask=mask, type=pa.int16()),
+             pa.array(rng.random(n) < 0.5, mask=mask, type=pa.bool_()),
+             pa.array([None if m else "x" * (k % 5) for k, m in enumerate(mask)], pa.string())]
+    length = n - offset - 7
+    for arr in cases:
+        sl = arr.slice(offset, length)
+        col = ArrowColumn(sl)
+        c = col.to_c()
+        assert c.length == length
+        bits = lambda ptr, k: np.unpackbits(  # noqa: E731
+            np.frombuffer(ctypes.string_at(ptr, (k + 7) // 8), np.uint8), bitorder="little")[:k]
+        valid = np.array([x is not None for x in sl.to_pylist()])
+        assert (bits(c.validity, length).astype(bool) == valid).all(), str(arr.type)
+        if pa.types.is_boolean(arr.type):
+            got = bits(c.values, length).astype(bool)
+            exp = np.array([bool(x) for x in sl.fill_null(False).to_pylist()])
+            assert (got[valid] == exp[valid]).all()
+        elif pa.types.is_string(arr.type):
+            offs = np.frombuffer(ctypes.string_at(c.values, 4 * (length + 1)), np.int32)
+            data = ctypes.string_at(c.data, int(offs[-1]))
+            got = [data[offs[k]:offs[k + 1]].decode() for k in range(length)]
+            assert [g for g, v in zip(got, valid) if v] == [x for x in sl.to_pylist() if x is not None]
+        else:
+            npt = arr.type.to_pandas_dtype()
+            w = np.dtype(npt).itemsize
+            got = np.frombuffer(ctypes.string_at(c.values, w * length), npt)
+            exp = np.asarray(arr.to_numpy(zero_copy_only=False))[offset:offset + length]
+            assert (got[valid] == exp[valid]).all()
+        del col

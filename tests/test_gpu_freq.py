@@ -390,3 +390,71 @@ def test_short_string_keys_of_every_length(distinct, gpu_device):
     ot = O.OTable({"s": t.column("s").to_pylist()}, {"s": "string"})
     assert dict(ft.export()) == O.frequencies(ot, ["s"])
     assert ft.num_rows == n
+
+
+@pytest.mark.parametrize("distinct,poison", [(1, None), (3, None), (8, None), (3, "long"),
+                                             (12, None), (3, "late_long")])
+@pytest.mark.parametrize("nulls", [0.0, 0.1])
+def test_small_key_phase_a_matches_oracle(distinct, poison, nulls, gpu_device):
+    """One utf8 key of strings <= 7 bytes with few values (freq_phaseA_small: exact packed keys,
+    per-lane counters).  8 values fit a wave's candidates; 12 do not, and a string longer than 7
+    bytes anywhere in a batch ("long": mid-table, "late_long": the last rows of the last batch)
+    makes the kernel give that batch up to the general phase A -- batches before it keep the small
+    kernel's output.  Empty strings, embedded NULs and a ragged last batch included.  Bar: the
+    grouping's frequencies and the Histogram / grouping metrics of a shared run equal the
+    oracle's."""
+    from deequ_amd.analyzers import CountDistinct, Entropy, Histogram, Uniqueness
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.runners import AnalysisRunner
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    rng = np.random.default_rng(distinct * 7 + (poison is not None))
+    vocab = ["", "a", "a\x00", "\x00", "high", "low", "medium", "zzzzzzz", "b\x00\x00c",
+             "q1", "q2", "q3"][:distinct]
+    n = 200_003
+    vals = [vocab[i] for i in rng.integers(0, len(vocab), n)]
+    if poison == "long":
+        vals[100_000] = "eight+1ch"
+    elif poison == "late_long":
+        vals[n - 3] = "a much longer string"
+    mask = rng.random(n) < nulls
+    t = pa.table({"s": pa.array([None if m else v for v, m in zip(vals, mask)], pa.string())})
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=1 << 16)
+    assert len(df.batches) == 4
+    ot = O.OTable({"s": t.column("s").to_pylist()}, {"s": "string"})
+    freq = O.frequencies(ot, ["s"])
+    ft = FrequencyTable(["s"], [df.schema["s"].dtype], 0, capacity_hint=n)
+    for b in df.batches:
+        ft.add([b["s"]])
+    assert dict(ft.export()) == freq
+    assert ft.num_rows == n
+    h = Histogram("s")
+    ctx = AnalysisRunner.do_analysis_run(df, [h, Uniqueness(["s"]), Entropy("s"),
+                                              CountDistinct(["s"])])
+    assert ctx.metric(Uniqueness(["s"])).value.get() == O.uniqueness(freq, n)
+    assert ctx.metric(CountDistinct(["s"])).value.get() == O.count_distinct(freq)
+    assert _rel_close(ctx.metric(Entropy("s")).value.get(), O.entropy(freq, n))
+    hist, _ = O.histogram(ot, "s")
+    dist = ctx.metric(h).value.get()
+    assert dist.number_of_bins == len(hist)
+    assert {k: v.absolute for k, v in dist.values.items()} == hist
+
+
+def test_small_key_phase_a_on_unaligned_and_sliced_batches(gpu_device):
+    """The small-key kernel's bounds-checked path: a batch whose validity bitmap is not dword
+    aligned (a row slice of a device table, 8 rows in) and whose length is not a multiple of the
+    1024-row step."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    rng = np.random.default_rng(5)
+    vocab = ["x", "yy", "", "zzz"]
+    n = 70_001
+    vals = [None if rng.random() < 0.05 else vocab[i] for i in rng.integers(0, 4, n)]
+    t = pa.table({"s": pa.array(vals, pa.string())})
+    df = Table.from_arrow(t, device=gpu_device).select_rows(8, n - 5)
+    ft = FrequencyTable(["s"], [df.schema["s"].dtype], 0)
+    for b in df.batches:
+        ft.add([b["s"]])
+    ot = O.OTable({"s": vals[8:n - 5]}, {"s": "string"})
+    assert dict(ft.export()) == O.frequencies(ot, ["s"])

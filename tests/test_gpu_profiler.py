@@ -190,7 +190,7 @@ def test_profile_of_a_column_in_the_hll_bias_range(gpu_device):
     df = Table.from_pydict({"ids": [f"k{i % 1000}" for i in range(n)],
                             "low": ["ab"[i % 2] for i in range(n)]},
                            {"ids": "string", "low": "string"}, device=gpu_device)
-    p = ColumnProfiler.profile(df)
+    p = ColumnProfiler.profile(df, ["ids", "low"])
     assert p.num_records == n
     assert p.profiles["ids"].approximate_num_distinct_values is None
     assert p.profiles["ids"].histogram is None
@@ -198,4 +198,4 @@ def test_profile_of_a_column_in_the_hll_bias_range(gpu_device):
     assert set(p.profiles["low"].histogram.values) == {"a", "b"}
     from deequ_amd.exceptions import HllBiasTablesUnavailableException
     with pytest.raises(HllBiasTablesUnavailableException):
-        ColumnProfiler.profile(df, low_cardinality_histogram_threshold=500)
+        ColumnProfiler.profile(df, ["ids", "low"], low_cardinality_histogram_threshold=500)

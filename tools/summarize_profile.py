@@ -83,7 +83,10 @@ def main():
             summary["traffic_over_algorithmic"] = d["hbm_bytes_per_dispatch"] / b_alg
     json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     if dominant and kernels[dominant]["hbm_bytes_per_dispatch"]:
+        sys.path.insert(0, ROOT)
+        from bench import scan_source_hash
         json.dump({"tag": tag, "rows_per_gpu": rows, "kernel": dominant,
+                   "scan_source_sha": scan_source_hash(),
                    "hbm_bytes_per_launch": kernels[dominant]["hbm_bytes_per_dispatch"],
                    "source": f"profiles/{tag}/dq_counters.csv (2 x FETCH_SIZE + WRITE_SIZE, KiB)"},
                   open(os.path.join(ROOT, "profiles", "traffic_s10.json"), "w"), indent=1)
