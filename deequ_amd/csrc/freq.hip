@@ -811,6 +811,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
 constexpr int kSmallCand = 8;
 constexpr int kSmallThreads = 256;
 constexpr uint64_t kLongKey = ~0ULL;
+// an unused candidate: length byte 0xFE, which neither a short key (<= 7) nor kLongKey (0xFF) has,
+// so a long string never matches a free slot and is always seen as a miss
+constexpr uint64_t kFreeCand = 0xFEULL << 56;
 
 DQ_DEV uint64_t small_key(uint64_t v, int32_t len) {
   if (len > 7) return kLongKey;
@@ -839,14 +842,14 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   uint32_t cnt[kSmallCand];
 #pragma unroll
   for (int k = 0; k < kSmallCand; ++k) {
-    cand[k] = kLongKey;
+    cand[k] = kFreeCand;
     cnt[k] = 0;
   }
   int nc = 0;
   bool gave_up = false;
   unsigned long long nulls = 0;
   // count the rows of `pend` (bit i: key[i]) that match a candidate; returns the rest.  Each row
-  // finds its candidate index (unused candidates hold kLongKey, which no counted row has) and adds
+  // finds its candidate index (unused candidates hold kFreeCand, which no row's key equals) and adds
   // one to that index's byte of a packed per-lane counter word (<= 16 per byte per call).
   auto count = [&](const uint64_t* key, uint32_t pend) -> uint32_t {
     uint64_t packed = 0;
