@@ -821,6 +821,35 @@ DQ_DEV uint64_t small_key(uint64_t v, int32_t len) {
   return (v & m) | ((uint64_t)len << 56);
 }
 
+// The loads of one 1024-row step that do not depend on the character data: four 16-byte offset
+// loads per lane (+ each 256-row group's closing offset) and the step's validity bitmap slice.
+struct StrOffsets {
+  int4 q[4];
+  int32_t last[4];
+  ChunkBits c;
+  DQ_DEV void load(const int32_t* off, const uint8_t* valid, int64_t r0, int l) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint4 u = ld16(off + r0 + 256 * g + 4 * l);
+      q[g] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
+      last[g] = ldg_i32(off + r0 + 256 * g + 256);
+    }
+    if (valid) c.load(valid, r0);
+  }
+  // o[g][0..4]: the offsets of lane l's rows 256 g + 4 l .. + 3 and the one after them
+  DQ_DEV void offsets(int32_t (&o)[4][5], int l) const {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int32_t nxt = __shfl_down(q[g].x, 1);
+      o[g][0] = q[g].x;
+      o[g][1] = q[g].y;
+      o[g][2] = q[g].z;
+      o[g][3] = q[g].w;
+      o[g][4] = l == 63 ? last[g] : nxt;
+    }
+  }
+};
+
 __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   constexpr int NW = kSmallThreads / 64;
   __shared__ uint64_t s_key[NW * kSmallCand], s_cnt[NW * kSmallCand];
@@ -892,49 +921,45 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   };
 
   const bool vec = a.vec_ok != 0;
-  for (int64_t r0 = r_begin + (int64_t)wave * kWaveRows; r0 < r_end && !gave_up;
-       r0 += (int64_t)NW * kWaveRows) {
-    if (__hip_atomic_load(&a.fast_words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        a.fast_epoch) {
-      gave_up = true;  // another wave gave the batch up
-      break;
-    }
-    uint64_t key[16];
-    uint32_t vb = 0;
-    if (vec && r0 + kWaveRows <= r_end) {
-      // lane l owns rows r0 + 256 g + 4 l + j
+  const int64_t stride = (int64_t)NW * kWaveRows;
+  int64_t r0 = r_begin + (int64_t)wave * kWaveRows;
+  if (vec) {
+    // software pipeline (as the scan's str_in_item): the next step's offsets and validity are in
+    // flight while this step's strings load and count.  Lane l owns rows r0 + 256 g + 4 l + j.
+    StrOffsets cur;
+    if (r0 + kWaveRows <= r_end) cur.load(off, c.valid, r0, lane);
+    for (int step = 0; r0 + kWaveRows <= r_end; r0 += stride, ++step) {
+      // another wave may have given the batch up: polled every 4th step, the load in flight with
+      // the step's own
+      const bool poll = (step & 3) == 3;
+      unsigned long long flag = 0;
+      if (poll)
+        flag = __hip_atomic_load(&a.fast_words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool more = r0 + stride + kWaveRows <= r_end;
       int32_t o[4][5];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint4 u = ld16(off + r0 + 256 * g + 4 * lane);
-        o[g][0] = (int32_t)u.x;
-        o[g][1] = (int32_t)u.y;
-        o[g][2] = (int32_t)u.z;
-        o[g][3] = (int32_t)u.w;
-        const int32_t last = ldg_i32(off + r0 + 256 * g + 256);
-        const int32_t nxt = __shfl_down((int32_t)u.x, 1);
-        o[g][4] = lane == 63 ? last : nxt;
-      }
+      cur.offsets(o, lane);
+      uint32_t vb = 0xffffu;
       if (c.valid) {
-        ChunkBits cb;
-        cb.load(c.valid, r0);
+        vb = 0;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) vb |= cb.get(256 * g + 4 * lane, 4) << (4 * g);
-      } else {
-        vb = 0xffffu;
+        for (int g = 0; g < 4; ++g) vb |= cur.c.get(256 * g + 4 * lane, 4) << (4 * g);
       }
-      const int32_t step_end = __shfl(o[3][4], 63);
-      if ((int64_t)step_end + 8 <= (int64_t)dlen) {
+      const int32_t step_end = cur.last[3];
+      uint64_t key[16];
+      if ((int64_t)step_end + 8 <= (int64_t)dlen) {  // every string has 8 readable bytes
         uint64_t v[16];
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[4 * g + j] = ldg64_unaligned(c.data + o[g][j]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) cur.load(off, c.valid, r0 + stride, lane);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
           for (int j = 0; j < 4; ++j) key[4 * g + j] = small_key(v[4 * g + j], o[g][j + 1] - o[g][j]);
-      } else {
+      } else {  // the batch's last strings: loads that stay inside the data buffer
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
@@ -944,30 +969,41 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
             if (len > 0 && len <= 7) load_str16(c.data + o[g][j], len, w0, w1);
             key[4 * g + j] = small_key(w0, len);
           }
+        if (more) cur.load(off, c.valid, r0 + stride, lane);
       }
-    } else {  // batch tail or unaligned buffers: lane l owns rows r0 + 64 i + l, bounds-checked
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int64_t r = r0 + 64 * i + lane;
-        key[i] = kLongKey;
-        if (r < r_end && kbit(c.valid, r)) {
-          vb |= 1u << i;
-          const int32_t s0 = off[r], len = off[r + 1] - s0;
-          uint64_t w0 = 0, w1 = 0;
-          if (len > 0 && len <= 7) load_str16(c.data + s0, len, w0, w1);
-          key[i] = small_key(w0, len);
-        }
-      }
-      uint32_t in = 0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) in |= (r0 + 64 * i + lane < r_end ? 1u : 0u) << i;
-      nulls += __popc(in & ~vb);
-      uint32_t pend = count(key, vb);
+      nulls += 16 - __popc(vb);
+      const uint32_t pend = count(key, vb);
       if (__ballot(pend != 0)) admit(key, pend);
-      continue;
+      if (gave_up || (poll && flag == a.fast_epoch)) {
+        gave_up = true;
+        break;
+      }
     }
-    nulls += 16 - __popc(vb);
-    uint32_t pend = count(key, vb);
+  }
+  // batch tail or unaligned buffers: lane l owns rows r0 + 64 i + l, bounds-checked
+  for (; r0 < r_end && !gave_up; r0 += stride) {
+    if (__hip_atomic_load(&a.fast_words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        a.fast_epoch) {
+      gave_up = true;  // another wave gave the batch up
+      break;
+    }
+    uint64_t key[16];
+    uint32_t vb = 0, in = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t r = r0 + 64 * i + lane;
+      key[i] = kLongKey;
+      in |= (r < r_end ? 1u : 0u) << i;
+      if (r < r_end && kbit(c.valid, r)) {
+        vb |= 1u << i;
+        const int32_t s0 = off[r], len = off[r + 1] - s0;
+        uint64_t w0 = 0, w1 = 0;
+        if (len > 0 && len <= 7) load_str16(c.data + s0, len, w0, w1);
+        key[i] = small_key(w0, len);
+      }
+    }
+    nulls += __popc(in & ~vb);
+    const uint32_t pend = count(key, vb);
     if (__ballot(pend != 0)) admit(key, pend);
   }
   if (gave_up && lane == 0)
