@@ -118,7 +118,7 @@ def _load() -> ctypes.CDLL:
         "dq_freq_marginal": (c_int, [c_void_p, c_int, c_void_p, c_void_p]),
         "dq_freq_mutual_information": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int),
                                                c_void_p]),
-        "dq_sorted_sample": (c_int, [c_int, POINTER(dq_column), c_int, c_int64, c_void_p,
+        "dq_sorted_sample": (c_int, [c_int, POINTER(dq_column), c_int, c_int64, c_int64, c_void_p,
                                      POINTER(c_int64), POINTER(c_int64), c_void_p]),
         "dq_freq_num_groups": (c_int, [c_void_p, POINTER(c_int64)]),
         "dq_freq_null_literal": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64)]),

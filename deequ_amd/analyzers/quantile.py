@@ -135,21 +135,22 @@ def quantile_summaries(data, column: str, relative_error: float) -> QuantileSumm
 
     The device returns every sorted value when they fit Spark's head buffer, when relativeError is
     0 (accuracy 1/0.0 = Infinity: Spark keeps every sample and answers the exact order statistic,
-    ApproxQuantile.scala:39-41) or when 2/eps + 1 ranks would cover every value; otherwise
-    max(HEAD_SIZE, 2/eps + 1) evenly spaced exact order statistics, thinned here to 2/eps + 1."""
+    ApproxQuantile.scala:39-41) or when 2/eps + 1 ranks would cover every value; otherwise only the
+    2/eps + 1 evenly spaced exact order statistics the summary keeps (so no more than those cross
+    the link or pass through host code)."""
     import torch
     batches = [b[column] for b in data.batches]
     arr = (N.dq_column * max(1, len(batches)))(*[c.to_c() for c in batches])
     total = sum(int(arr[i].length) for i in range(len(batches)))
     device = data.device_index()
     ranks = int(math.ceil(2.0 / relative_error)) + 1 if relative_error > 0 else None
-    want = total if ranks is None else max(HEAD_SIZE, ranks)
-    want = max(2, min(want, total))
-    out = np.empty(want, np.float64)
+    head = total if ranks is None else max(HEAD_SIZE, ranks)
+    picks = 2 if ranks is None else ranks
+    out = np.empty(max(2, min(max(head, picks), total)), np.float64)
     n_out, count = ctypes.c_int64(), ctypes.c_int64()
     stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
     N.retry_on_oom(lambda: N.check(N.lib.dq_sorted_sample(
-        device, arr, len(batches), want, out.ctypes.data, ctypes.byref(n_out),
+        device, arr, len(batches), head, picks, out.ctypes.data, ctypes.byref(n_out),
         ctypes.byref(count), stream)))
     n, cnt = int(n_out.value), int(count.value)
     if cnt == 0:
@@ -160,15 +161,9 @@ def quantile_summaries(data, column: str, relative_error: float) -> QuantileSumm
         # every value as a sample of g = 1, delta = 0: the exact summary (Spark's at eps = 0)
         s = QuantileSummaries(relative_error, list(zip(out[:n].tolist(), [1] * n, [0] * n)), cnt)
         return s.compress() if relative_error > 0 else s
-    # n >= 2/eps + 1 evenly spaced order statistics: thin to 2/eps + 1 of them (exact ranks of the
-    # full column, gaps <= eps * cnt)
-    idx = [(j * (n - 1)) // (ranks - 1) for j in range(ranks)] if ranks < n else list(range(n))
-    picked = out[idx]
-    full_ranks = [(i * (cnt - 1)) // (n - 1) for i in idx]
-    samples: List[Sample] = [(float(picked[0]), 1, 0)]
-    for j in range(1, len(idx)):
-        samples.append((float(picked[j]), full_ranks[j] - full_ranks[j - 1], 0))
-    return QuantileSummaries(relative_error, samples, cnt).compress()
+    # 2/eps + 1 order statistics at the exact ranks floor(j (cnt - 1) / (n - 1)): rank gaps
+    # <= eps * cnt / 2
+    return QuantileSummaries.from_ranks(out[:n], cnt, relative_error)
 
 
 @dataclass(frozen=True)

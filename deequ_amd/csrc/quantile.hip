@@ -23,26 +23,58 @@ using namespace dq;
 namespace {
 
 constexpr int kGatherThreads = 256;
+constexpr int kGatherWaves = kGatherThreads / 64;
+constexpr int kGatherRounds = 16;  // rows per thread per block step: 4096 rows a step
+
+static_assert(kGatherRounds * kGatherWaves == 64, "one wave scans the step's counts");
 
 // Non-NULL values of one batch -> doubles at out[*cursor ...] (order irrelevant: sorted next).
+// A block step covers 4096 rows (round i: rows r0 + 256 i + tid, coalesced); the kept rows of a
+// step are placed by one exclusive scan over its (round, wave) ballot counts and ONE cursor
+// atomic per step -- one per wave (a same-address atomic every 64 rows) serialised the kernel.
 __global__ void __launch_bounds__(kGatherThreads)
 quantile_gather(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
                 int64_t rows, double* __restrict__ out, unsigned long long* __restrict__ cursor) {
-  const int64_t stride = (int64_t)gridDim.x * kGatherThreads;
-  for (int64_t r0 = (int64_t)blockIdx.x * kGatherThreads; r0 < rows; r0 += stride) {
-    const int64_t r = r0 + threadIdx.x;
-    bool keep = false;
-    double v = 0.0;
-    if (r < rows && bit1(valid, r)) {
-      keep = true;
-      v = load_f64(type, values, r);
-      if (v != v) v = __builtin_nan("");  // Double.compare: every NaN is the canonical one
+  __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
+  __shared__ unsigned long long s_base;
+  const int tid = threadIdx.x, lane = (int)__lane_id(), wave = tid >> 6;
+  const uint64_t lt = lane ? (~0ULL >> (64 - lane)) : 0ULL;  // lanes below this one
+  constexpr int64_t kStep = (int64_t)kGatherRounds * kGatherThreads;
+  for (int64_t r0 = (int64_t)blockIdx.x * kStep; r0 < rows; r0 += (int64_t)gridDim.x * kStep) {
+    double v[kGatherRounds];
+    uint64_t m[kGatherRounds];
+#pragma unroll
+    for (int i = 0; i < kGatherRounds; ++i) {
+      const int64_t r = r0 + (int64_t)i * kGatherThreads + tid;
+      const bool keep = r < rows && bit1(valid, r);
+      v[i] = keep ? load_f64(type, values, r) : 0.0;
+      if (v[i] != v[i]) v[i] = __builtin_nan("");  // Double.compare: every NaN is the canonical one
+      m[i] = __ballot(keep);
+      if (lane == 0) s_cnt[i * kGatherWaves + wave] = (uint32_t)__popcll(m[i]);
     }
-    const uint64_t m = __ballot(keep);
-    unsigned long long base = 0;
-    if (__lane_id() == 0 && m) base = atomicAdd(cursor, (unsigned long long)__popcll(m));
-    base = __shfl(base, 0);
-    if (keep) out[base + __popcll(m & ((1ULL << __lane_id()) - 1))] = v;
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the 64 (round, wave) counts, round-major
+      const uint32_t c = s_cnt[tid];
+      uint32_t x = c;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+      }
+      const uint32_t total = __shfl(x, 63);
+      unsigned long long base = 0;
+      if (lane == 63 && total) base = atomicAdd(cursor, (unsigned long long)total);
+      base = __shfl(base, 63);
+      s_cnt[tid] = x - c;
+      if (lane == 0) s_base = base;
+    }
+    __syncthreads();
+    const unsigned long long base = s_base;
+#pragma unroll
+    for (int i = 0; i < kGatherRounds; ++i)
+      if ((m[i] >> lane) & 1u)
+        out[base + s_cnt[i * kGatherWaves + wave] + __popcll(m[i] & lt)] = v[i];
+    __syncthreads();  // s_cnt / s_base are rewritten by the next step
   }
 }
 
@@ -59,9 +91,11 @@ __global__ void quantile_pick(const double* __restrict__ sorted, int64_t count, 
 }  // namespace
 
 extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int n_batches,
-                                      int64_t max_values, double* out, int64_t* n_out,
+                                      int64_t head_values, int64_t max_values, double* out,
+                                      int64_t* n_out,
                                       int64_t* count_out, void* hip_stream) {
-  if (!n_out || !count_out || (n_batches > 0 && !batches) || n_batches < 0 || max_values < 2)
+  if (!n_out || !count_out || (n_batches > 0 && !batches) || n_batches < 0 || max_values < 2 ||
+      head_values < 0)
     return fail(DQ_ERR_INVALID_ARGUMENT, "bad argument to dq_sorted_sample");
   hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
   HIP_TRY(hipSetDevice(device));
@@ -91,7 +125,8 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   for (int b = 0; b < n_batches; ++b) {
     const dq_column& c = batches[b];
     if (!c.length) continue;
-    const int64_t blocks = std::min<int64_t>((c.length + kGatherThreads - 1) / kGatherThreads, 8192);
+    const int64_t step = (int64_t)kGatherRounds * kGatherThreads;
+    const int64_t blocks = std::min<int64_t>((c.length + step - 1) / step, 2048);
     hipLaunchKernelGGL(quantile_gather, dim3((unsigned)blocks), dim3(kGatherThreads), 0, stream,
                        c.type, c.validity, c.values, c.length, kp, cp);
     HIP_TRY(hipGetLastError());
@@ -105,7 +140,7 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, kp, sorted.p, (size_t)count, 0, 64, stream));
   HIP_TRY(tmp.ensure(std::max<size_t>(tmp_bytes, 16)));
   HIP_TRY(rocprim::radix_sort_keys(tmp.p, tmp_bytes, kp, sorted.p, (size_t)count, 0, 64, stream));
-  const int64_t n = (int64_t)count <= max_values ? (int64_t)count : max_values;
+  const int64_t n = (int64_t)count <= std::max(head_values, max_values) ? (int64_t)count : max_values;
   *n_out = n;
   if (!out) return DQ_OK;  // size query only
   if (n == (int64_t)count) {

@@ -459,13 +459,15 @@ dq_status dq_freq_add_host(dq_loader* loader, dq_freq* freq, const dq_column* ho
 /* ------------------------------------------------------------------------------------------------
  * ApproxQuantile (ApproxQuantile.scala:41-104): the device sorts the non-NULL values of a numeric
  * column (all batches, cast to double as ApproximatePercentile does; NaNs canonical, so the order
- * is Java's Double.compare) and returns either every value (when count <= max_values; the host
+ * is Java's Double.compare) and returns either every value (when count <= head_values; the host
  * then replays Spark's QuantileSummaries exactly) or max_values of them at the exact ranks
- * floor(j * (count - 1) / (max_values - 1)).  out holds max_values doubles (host memory);
- * *n_out = values written, *count_out = non-NULL values.  Synchronous on hip_stream.
+ * floor(j * (count - 1) / (max_values - 1)).  out holds max(head_values, max_values) doubles (host
+ * memory; min(..., rows) suffices); *n_out = values written, *count_out = non-NULL values.
+ * Synchronous on hip_stream.
  * ---------------------------------------------------------------------------------------------- */
-dq_status dq_sorted_sample(int device, const dq_column* batches, int n_batches, int64_t max_values,
-                           double* out, int64_t* n_out, int64_t* count_out, void* hip_stream);
+dq_status dq_sorted_sample(int device, const dq_column* batches, int n_batches, int64_t head_values,
+                           int64_t max_values, double* out, int64_t* n_out, int64_t* count_out,
+                           void* hip_stream);
 
 #ifdef __cplusplus
 }
