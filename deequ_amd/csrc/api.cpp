@@ -751,6 +751,13 @@ struct dq_state {
   std::vector<int> prog_off;    // per mat expr: offset into d_prog
   DevBuf<uint8_t> d_pool;
   std::vector<int64_t> pool_off;
+  // per mat expr: PatternMatch over a utf8 column runs regex_find_kernel on a fused table in
+  // d_pool (col < 0: the interpreter)
+  struct RegexRun {
+    int col = -1, null_mode = 0, ns = 0, start = 0;
+    int64_t table_off = 0;
+  };
+  std::vector<RegexRun> rx;
   DevBuf<DevCol> d_cols[2];
   DevCol* h_cols[2] = {nullptr, nullptr};
   size_t h_cols_cap[2] = {0, 0};
@@ -828,6 +835,45 @@ static dq_status upload_host(dq_state* s) {
   return DQ_OK;
 }
 
+// The fused automaton of a regex blob (regex.py CompiledRegex.blob: int32 n_states, n_classes,
+// start, 0; u8 class[256]; u8 status[n_states] padded to 4; u16 next[n_states * n_classes], the
+// last class being end-of-text): u8 successor[state][byte] with the classes folded in and terminal
+// states (status 1 sticky accept, 2 dead) made self-loops, then one flag byte per state -- bit 0:
+// accepted once the end-of-text symbol is read from it, bit 1: terminal.  False when the automaton
+// does not fit u8 states (the interpreter walks it instead).
+static bool build_regex_table(const std::string& pool, int64_t at, std::vector<uint8_t>& tab,
+                              int* ns_out, int* start_out) {
+  if (at < 0 || (size_t)at + 16 + 256 > pool.size()) return false;
+  const uint8_t* blob = reinterpret_cast<const uint8_t*>(pool.data()) + at;
+  int32_t head[4];
+  memcpy(head, blob, sizeof(head));
+  const int ns = head[0], nc = head[1], start = head[2];
+  if (ns < 1 || ns > kRegexMaxStates || nc < 2 || start < 0 || start >= ns) return false;
+  const size_t nx_at = 16 + 256 + (size_t)((ns + 3) & ~3);
+  if ((size_t)at + nx_at + (size_t)ns * nc * 2 > pool.size()) return false;
+  const uint8_t* cls = blob + 16;
+  const uint8_t* status = blob + 16 + 256;
+  auto nx = [&](int q, int c) {
+    uint16_t v;
+    memcpy(&v, blob + nx_at + ((size_t)q * nc + c) * 2, 2);
+    return (int)v;
+  };
+  tab.assign((size_t)ns * 257, 0);
+  for (int q = 0; q < ns; ++q) {
+    for (int b = 0; b < 256; ++b) {
+      const int t = status[q] ? q : nx(q, cls[b]);
+      if (t < 0 || t >= ns || cls[b] >= nc - 1) return false;
+      tab[(size_t)q * 256 + b] = (uint8_t)t;
+    }
+    const int e = status[q] ? q : nx(q, nc - 1);
+    if (e < 0 || e >= ns) return false;
+    tab[(size_t)ns * 256 + q] = (uint8_t)((status[e] == 1 ? 1u : 0u) | (status[q] ? 2u : 0u));
+  }
+  *ns_out = ns;
+  *start_out = start;
+  return true;
+}
+
 extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state** out) {
   if (!plan || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   *out = nullptr;
@@ -872,6 +918,20 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
     while (pool.size() % 16) pool.push_back('\0');
     s->pool_off.push_back((int64_t)pool.size());
     pool += m.pool;
+  }
+  // PatternMatch over a utf8 column: its fused automaton table appended to the pool
+  s->rx.assign(plan->mat.size(), dq_state::RegexRun{});
+  for (size_t k = 0; k < plan->mat.size(); ++k) {
+    std::vector<uint8_t> tab;
+    int ns = 0, start = 0;
+    const std::vector<XInstr>& pr = plan->mat[k].prog;
+    if (pr.size() == 2 && pr[0].op == XI_COL && pr[1].op == XI_REGEX && pr[0].a >= 0 &&
+        pr[0].a < (int)plan->types.size() && plan->types[pr[0].a] == DQ_UTF8 &&
+        build_regex_table(plan->mat[k].pool, pr[1].imm, tab, &ns, &start)) {
+      while (pool.size() % 16) pool.push_back('\0');
+      s->rx[k] = dq_state::RegexRun{pr[0].a, pr[1].a, ns, start, (int64_t)pool.size()};
+      pool.append(reinterpret_cast<const char*>(tab.data()), tab.size());
+    }
   }
   // pool offsets in the programs are relative to each expression's own pool
   for (size_t k = 0; k < plan->mat.size(); ++k)
@@ -1087,9 +1147,17 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
       for (int b = 0; b < n_batches; ++b) {
         uint64_t* val = s->d_bitmaps.p + (2 * k) * s->bitmap_words + bm_off[b];
         uint64_t* vld = s->d_bitmaps.p + (2 * k + 1) * s->bitmap_words + bm_off[b];
-        HIP_TRY(launch_expr(s->d_prog.p + s->prog_off[k], (int)plan->mat[k].prog.size(),
-                            s->d_cols[slot].p + (size_t)b * ncol, s->d_pool.p, rows[b], val, vld,
-                            stream));
+        const dq_state::RegexRun& rx = s->rx[k];
+        if (rx.col >= 0) {
+          const dq_column& col = cols[(size_t)b * n_cols + rx.col];
+          HIP_TRY(launch_regex(col.validity, reinterpret_cast<const int32_t*>(col.values), col.data,
+                               rows[b], s->d_pool.p + rx.table_off, rx.ns, rx.start, rx.null_mode,
+                               val, vld, stream));
+        } else {
+          HIP_TRY(launch_expr(s->d_prog.p + s->prog_off[k], (int)plan->mat[k].prog.size(),
+                              s->d_cols[slot].p + (size_t)b * ncol, s->d_pool.p, rows[b], val, vld,
+                              stream));
+        }
       }
     }
   }

@@ -321,6 +321,102 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------------
+// PatternMatch over a utf8 column (the program [XI_COL c, XI_REGEX]): its own kernel instead of the
+// interpreter walk.  The automaton arrives fused (RegexTable, built on the host by
+// build_regex_table): one u8 successor per (state, byte) -- the byte classes folded in, terminal
+// states (sticky accept / dead) made self-loops -- then per state bit 0 = accepted after the
+// end-of-text symbol, bit 1 = terminal.  The block stages it in LDS with 16-byte copies, so a byte
+// costs one dependent LDS read.  A lane walks two rows (rows r and r + 64 of a 128-row pair of
+// bitmap words: two independent chains in flight), loading each string 16 bytes at a time with one
+// unaligned load; a row stops at its end or in a terminal state, the wave when every row has.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint4 ldg128_unaligned(const uint8_t* p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4), aligned(1)));
+  const v4u v = *(const __attribute__((address_space(1))) v4u*)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+struct RxRow {
+  int64_t pos, end;  // byte range left to walk in the data buffer
+  uint32_t q;
+  DQ_DEV bool active(const uint8_t* fin) const { return pos < end && !(fin[q] & 2u); }
+  // the next (at most) 16 bytes of the row
+  DQ_DEV void chunk(const uint8_t* data, int64_t data_len, uint32_t (&w)[4]) const {
+    if (pos + 16 <= data_len) {
+      const uint4 u = ldg128_unaligned(data + pos);
+      w[0] = u.x;
+      w[1] = u.y;
+      w[2] = u.z;
+      w[3] = u.w;
+    } else {  // the buffer's last bytes: no read past its end
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = 0;
+      for (int j = 0; j < 16 && pos + j < end; ++j) w[j >> 2] |= (uint32_t)data[pos + j] << (8 * (j & 3));
+    }
+  }
+};
+
+__global__ void __launch_bounds__(kBlock)
+regex_find_kernel(const uint8_t* __restrict__ valid, const int32_t* __restrict__ off,
+                  const uint8_t* __restrict__ data, int64_t rows, const uint8_t* __restrict__ table,
+                  int32_t ns, int32_t start, int32_t null_mode, uint64_t* __restrict__ out_val,
+                  uint64_t* __restrict__ out_vld) {
+  extern __shared__ uint4 rx_lds[];
+  uint8_t* T = reinterpret_cast<uint8_t*>(rx_lds);
+  const uint8_t* fin = T + (size_t)ns * 256;
+  const int n16 = (ns * 257 + 15) / 16;
+  for (int i = threadIdx.x; i < n16; i += kBlock) rx_lds[i] = reinterpret_cast<const uint4*>(table)[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
+  const int64_t n_words = (rows + 63) >> 6;
+  const int64_t data_len = rows ? (int64_t)off[rows] : 0;
+  for (int64_t w = 2 * wave; w < n_words; w += 2 * n_waves) {
+    RxRow rr[2];
+    bool vld[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t r = (w + h) * 64 + lane;
+      vld[h] = r < rows && bit1(valid, r);
+      rr[h].q = (uint32_t)start;
+      rr[h].pos = vld[h] ? off[r] : 0;
+      rr[h].end = vld[h] ? off[r + 1] : 0;
+    }
+    while (__ballot(rr[0].active(fin) || rr[1].active(fin))) {
+      uint32_t c[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (rr[h].active(fin)) rr[h].chunk(data, data_len, c[h]);
+        else c[h][0] = c[h][1] = c[h][2] = c[h][3] = 0;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t b = (c[h][j >> 2] >> (8 * (j & 3))) & 0xffu;
+          const uint32_t nq = T[rr[h].q * 256u + b];
+          rr[h].q = rr[h].pos + j < rr[h].end ? nq : rr[h].q;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) rr[h].pos = rr[h].pos + 16 < rr[h].end ? rr[h].pos + 16 : rr[h].end;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // NULL: null_mode 1 (PatternMatch's otherwise(0)) -> FALSE, else NULL
+      const bool res_valid = (w + h) * 64 + lane < rows && (vld[h] || null_mode);
+      const bool truth = vld[h] && (fin[rr[h].q] & 1u);
+      const uint64_t bv = __ballot(truth), bn = __ballot(res_valid);
+      if (lane == 0 && w + h < n_words) {
+        out_val[w + h] = bv;
+        out_vld[w + h] = bn;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Host-side launchers
 // ------------------------------------------------------------------------------------------------
 hipError_t launch_expr(const XInstr* prog, int n_instr, const DevCol* cols, const uint8_t* pool,
@@ -331,6 +427,20 @@ hipError_t launch_expr(const XInstr* prog, int n_instr, const DevCol* cols, cons
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(expr_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, stream, prog, n_instr,
                      cols, pool, rows, out_val, out_vld);
+  return hipGetLastError();
+}
+
+hipError_t launch_regex(const uint8_t* valid, const int32_t* offsets, const uint8_t* data,
+                        int64_t rows, const uint8_t* table, int ns, int start, int null_mode,
+                        uint64_t* out_val, uint64_t* out_vld, hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  if (ns < 1 || ns > kRegexMaxStates) return hipErrorInvalidValue;
+  const int64_t pairs = ((rows + 63) / 64 + 1) / 2;
+  int64_t blocks = (pairs + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  const size_t lds = ((size_t)ns * 257 + 15) / 16 * 16;
+  hipLaunchKernelGGL(regex_find_kernel, dim3((unsigned)blocks), dim3(kBlock), lds, stream, valid,
+                     offsets, data, rows, table, ns, start, null_mode, out_val, out_vld);
   return hipGetLastError();
 }
 

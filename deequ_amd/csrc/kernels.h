@@ -113,6 +113,12 @@ hipError_t launch_bitmap_rebase(const uint8_t* src, int64_t bit, int64_t rows, u
                                 hipStream_t stream);
 hipError_t launch_expr(const XInstr* prog, int n_instr, const DevCol* cols, const uint8_t* pool,
                        int64_t rows, uint64_t* out_val, uint64_t* out_vld, hipStream_t stream);
+// PatternMatch over a utf8 column with a fused automaton table (expr.hip): ns * 256 u8 successors
+// then ns flag bytes (bit 0 accepted after end of text, bit 1 terminal), 16-byte aligned.
+constexpr int kRegexMaxStates = 255;
+hipError_t launch_regex(const uint8_t* valid, const int32_t* offsets, const uint8_t* data,
+                        int64_t rows, const uint8_t* table, int ns, int start, int null_mode,
+                        uint64_t* out_val, uint64_t* out_vld, hipStream_t stream);
 // Body classes of the scan: one kernel instantiation each (scan.hip).
 enum BodyClass : int32_t {
   BC_NUM_I8 = 0,

@@ -174,3 +174,39 @@ def test_approx_quantile_small_relative_error_beyond_the_head_buffer(eps, gpu_de
             assert got == exp, (q, got, exp)
         else:
             assert quantile_rank_error(vals, q, got) <= math.ceil(eps * n), (eps, q, got)
+
+
+@pytest.mark.parametrize("name", ["URL", "EMAIL", "SOCIAL_SECURITY_NUMBER_US", "CREDITCARD"])
+def test_pattern_match_library_patterns_on_long_rows(name, gpu_device):
+    """The fused-table regex kernel (regex_find_kernel: 16-byte chunks, two rows per lane, early
+    stop in terminal states) on the reference's own patterns (PatternMatch.scala:56-72) over rows
+    of 0..90 bytes that plant matches, near-misses and non-ASCII bytes at every chunk offset, the
+    last rows ending at the data buffer's end (the bounds-checked chunk path); NULL rows count as
+    non-matching rows.  Bar: (matches, rows) equal the oracle's java.util.regex find()."""
+    from deequ_amd.analyzers import Patterns, PatternMatch
+    from oracle.deequ_oracle import OTable, agg_pattern_match
+    pattern = getattr(Patterns, name)
+    rng = random.Random(name)
+    plants = {"URL": ["https://a.b/c", "ftp://x.y", "http:// no", "https://", "http://é.fr/x"],
+              "EMAIL": ["a.b@c.de", "x@[192.168.0.1]", "no@", "@x.y", "\"q\"@h.io"],
+              "SOCIAL_SECURITY_NUMBER_US": ["123-45-6789", "078-05-1120", "666-12-3456",
+                                            "123 45 6789", "123456789", "12-345-6789"],
+              "CREDITCARD": ["4111 1111 1111 1111", "4111-1111-1111-1111", "378282246310005",
+                             "6011000990139424", "4111 1111-1111 1111", "x4111111111111111"]}[name]
+    filler = "abc xyz 0123456789 .-@:/é"
+    n = 20_011
+    vals = []
+    for _ in range(n):
+        if rng.random() < 0.05:
+            vals.append(None)
+            continue
+        s = "".join(rng.choice(filler) for _ in range(rng.randint(0, 70)))
+        if rng.random() < 0.5:
+            at = rng.randint(0, len(s))
+            s = s[:at] + rng.choice(plants) + s[at:]
+        vals.append(s)
+    df = _df({"s": pa.array(vals, pa.string())}, gpu_device, 6000)
+    ot = OTable({"s": vals}, {"s": "string"})
+    st = PatternMatch("s", pattern).compute_state_from(df)
+    hits, cnt = agg_pattern_match(ot, "s", pattern, None)
+    assert (st.num_matches, st.count) == (hits, cnt), name
