@@ -57,7 +57,7 @@ constexpr int kHistRow = kBuckets + 1;  // u16 exclusive bucket prefix of a chun
 constexpr int kThreads = 1024;
 constexpr int kMaxSubBits = 10;
 constexpr int kFilterShift = 32;        // hash bits that split an overflowing partition
-constexpr int kCand = 2;                // top groups kept per partition for Histogram
+constexpr int kCand = 4;                // top groups kept per partition for Histogram
 constexpr int kSmallCounts = 64;        // phase C histograms group counts below this
 constexpr int kMaxParts = 64;
 constexpr uint64_t kEmptyKey = ~0ULL;
@@ -1572,8 +1572,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
   __shared__ unsigned long long s_spec_cnt[2], s_gbase;
   __shared__ uint64_t s_spec_rep[2];
   __shared__ uint32_t s_chist[2][kSmallCounts];
-  // Histogram candidates: packed (count << 16 | tid << 1 | q) maxima, top-1 then top-2
-  __shared__ unsigned long long s_top[2][2];
+  // Histogram candidates: packed (count << 16 | tid << 2 | q) maxima, top-1 .. top-kCand
+  __shared__ unsigned long long s_top[2][kCand];
 
   const int tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
   unsigned long long collisions = 0;
@@ -1586,7 +1586,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     s_ovf[tid] = 0;
     s_spec_cnt[tid] = 0;
     s_spec_rep[tid] = kNotReady;
-    s_top[tid][0] = s_top[tid][1] = 0;
+#pragma unroll
+    for (int r = 0; r < kCand; ++r) s_top[tid][r] = 0;
   }
   if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
   // exact mode fetches records two items ahead: item i + 2's loads are in flight through all of
@@ -1736,7 +1737,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       s_ovf[par ^ 1u] = 0;
       s_spec_cnt[par ^ 1u] = 0;
       s_spec_rep[par ^ 1u] = kNotReady;
-      s_top[par ^ 1u][0] = s_top[par ^ 1u][1] = 0;
+#pragma unroll
+      for (int r = 0; r < kCand; ++r) s_top[par ^ 1u][r] = 0;
     }
     if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
     const bool overflow = *ovf != 0;
@@ -1805,9 +1807,14 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       s_red[wave] = wun;
     }
     // Histogram candidates, round 1: the block's largest (count, tid, q)
+    static_assert(kCThreads <= 1024 && kCand <= 4, "candidate packing: tid in 10 bits, q in 2");
     auto pack = [&](int q) -> uint64_t {
-      return tc[q] ? (tc[q] << 16) | ((uint64_t)tid << 1) | (uint64_t)q : 0ULL;
+      uint64_t c = 0;
+#pragma unroll
+      for (int i = 0; i < kCand; ++i) c = i == q ? tc[i] : c;
+      return c ? (c << 16) | ((uint64_t)tid << 2) | (uint64_t)q : 0ULL;
     };
+    int taken = 0;  // this thread's candidates already placed (they leave in count order)
     if (cand) {
       const uint64_t w1 = __ockl_wfred_max_u64(pack(0));
       if (lane == 0 && w1) atomicMax(&s_top[par][0], (unsigned long long)w1);
@@ -1844,11 +1851,10 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     if (tid == 0 && utot) e += (double)utot * term(1);
     e = __ockl_wfred_add_f64(e);
     if (lane == 0) s_redf[wave] = e;
-    uint64_t top1 = 0;
     if (cand) {  // round 2: the largest of the rest (the top-1 owner offers its second)
-      top1 = s_top[par][0];
-      const uint64_t mine = top1 && top1 == pack(0) ? pack(1) : pack(0);
-      const uint64_t w2 = __ockl_wfred_max_u64(mine);
+      const uint64_t top1 = s_top[par][0];
+      taken = top1 && top1 == pack(0) ? 1 : 0;
+      const uint64_t w2 = __ockl_wfred_max_u64(pack(taken));
       if (lane == 0 && w2) atomicMax(&s_top[par][1], (unsigned long long)w2);
     }
     const bool sub = f != 0;  // a recount subset: several work items add to one partition
@@ -1874,17 +1880,34 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
         a.part_entropy[p] = etot;
       }
     }
-    if (cand) {  // each winner's owner writes it; an empty place is written by thread 0
-      static_assert(kCand == 2, "two candidate rounds");
+    if (cand) {
+      // rounds 3 .. kCand (their own barriers; cand is block-uniform): the winner of each round
+      // advances past the candidate it placed
+#pragma unroll
+      for (int r = 2; r < kCand; ++r) {
+        const uint64_t prev = s_top[par][r - 1];
+        if (prev && prev == pack(taken)) ++taken;
+        const uint64_t w = __ockl_wfred_max_u64(pack(taken));
+        if (lane == 0 && w) atomicMax(&s_top[par][r], (unsigned long long)w);
+        __syncthreads();
+      }
+      // each winner's owner writes it; an empty place is written by thread 0
 #pragma unroll
       for (int r = 0; r < kCand; ++r) {
-        const uint64_t t = r ? s_top[par][1] : top1;
+        const uint64_t t = s_top[par][r];
         Group* cslot = a.cand + (uint64_t)p * kCand + r;
         if (!t) {
           if (tid == 0) *cslot = Group{0, 0, 0};
-        } else if ((int)((t >> 1) & 511u) == tid) {
-          const int q = (int)(t & 1u);
-          *cslot = Group{q ? tk[1] : tk[0], q ? tc[1] : tc[0], HASHED ? (q ? tr[1] : tr[0]) : 0};
+        } else if ((int)((t >> 2) & 1023u) == tid) {
+          const int q = (int)(t & 3u);
+          uint64_t gk = 0, gc = 0, gr = 0;
+#pragma unroll
+          for (int i = 0; i < kCand; ++i) {
+            gk = i == q ? tk[i] : gk;
+            gc = i == q ? tc[i] : gc;
+            gr = i == q ? tr[i] : gr;
+          }
+          *cslot = Group{gk, gc, HASHED ? gr : 0};
         }
       }
     }
