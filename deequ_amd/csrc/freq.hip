@@ -243,6 +243,7 @@ struct AArgs {
   unsigned long long* fast_words;
   uint64_t fast_epoch;
   int32_t vec_ok;  // offsets / validity aligned for the 16-byte / dword streaming loads
+  int32_t fast_poll;  // steps between polls of the give-up word (0: never)
 };
 
 // Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
@@ -815,10 +816,11 @@ constexpr uint64_t kLongKey = ~0ULL;
 // so a long string never matches a free slot and is always seen as a miss
 constexpr uint64_t kFreeCand = 0xFEULL << 56;
 
-DQ_DEV uint64_t small_key(uint64_t v, int32_t len) {
-  if (len > 7) return kLongKey;
-  const uint64_t m = len > 0 ? (~0ULL >> (64 - 8 * len)) : 0ULL;
-  return (v & m) | ((uint64_t)len << 56);
+DQ_DEV uint64_t small_key(uint64_t v, int32_t len) {  // branch-free: selects, no exec masking
+  const uint32_t sh = 8u * ((uint32_t)len & 7u);
+  const uint64_t m = sh ? (~0ULL >> (64u - sh)) : 0ULL;
+  const uint64_t k = (v & m) | ((uint64_t)(uint32_t)len << 56);
+  return len > 7 ? kLongKey : k;
 }
 
 // The loads of one 1024-row step that do not depend on the character data: four 16-byte offset
@@ -834,7 +836,7 @@ struct StrOffsets {
       q[g] = make_int4((int)u.x, (int)u.y, (int)u.z, (int)u.w);
       last[g] = ldg_i32(off + r0 + 256 * g + 256);
     }
-    if (valid) c.load(valid, r0);
+    c.load(valid, r0);  // (never null here)
   }
   // o[g][0..4]: the offsets of lane l's rows 256 g + 4 l .. + 3 and the one after them
   DQ_DEV void offsets(int32_t (&o)[4][5], int l) const {
@@ -926,24 +928,26 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   if (vec) {
     // software pipeline (as the scan's str_in_item): the next step's offsets and validity are in
     // flight while this step's strings load and count.  Lane l owns rows r0 + 256 g + 4 l + j.
+    // Every load of a step is unconditional (the last step re-reads itself, a missing validity
+    // bitmap reads the offsets and is ignored), so the compiler counts the loads in flight exactly
+    // and waits for each string load alone -- a conditional prefetch made it wait for the next
+    // step's offsets before the last string of this one.
+    const uint8_t* vsrc = c.valid ? c.valid : reinterpret_cast<const uint8_t*>(off);
     StrOffsets cur;
-    if (r0 + kWaveRows <= r_end) cur.load(off, c.valid, r0, lane);
-    for (int step = 0; r0 + kWaveRows <= r_end; r0 += stride, ++step) {
-      // another wave may have given the batch up: polled every 4th step, the load in flight with
-      // the step's own
-      const bool poll = (step & 3) == 3;
+    if (r0 + kWaveRows <= r_end) cur.load(off, vsrc, r0, lane);
+    while (r0 + kWaveRows <= r_end && !gave_up) {
+      // another wave may have given the batch up (read with the step's loads, checked at its end;
+      // a.fast_poll: every that many steps, 0 never -- a wave that gives up stops alone)
       unsigned long long flag = 0;
-      if (poll)
+      if (a.fast_poll && (r0 / stride) % a.fast_poll == 0)
         flag = __hip_atomic_load(&a.fast_words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool more = r0 + stride + kWaveRows <= r_end;
+      const int64_t rn = r0 + stride + kWaveRows <= r_end ? r0 + stride : r0;
       int32_t o[4][5];
       cur.offsets(o, lane);
-      uint32_t vb = 0xffffu;
-      if (c.valid) {
-        vb = 0;
+      uint32_t vb = 0;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) vb |= cur.c.get(256 * g + 4 * lane, 4) << (4 * g);
-      }
+      for (int g = 0; g < 4; ++g) vb |= cur.c.get(256 * g + 4 * lane, 4) << (4 * g);
+      if (!c.valid) vb = 0xffffu;
       const int32_t step_end = cur.last[3];
       uint64_t key[16];
       if ((int64_t)step_end + 8 <= (int64_t)dlen) {  // every string has 8 readable bytes
@@ -953,7 +957,7 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[4 * g + j] = ldg64_unaligned(c.data + o[g][j]);
         __builtin_amdgcn_sched_barrier(0);
-        if (more) cur.load(off, c.valid, r0 + stride, lane);
+        cur.load(off, vsrc, rn, lane);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int g = 0; g < 4; ++g)
@@ -969,15 +973,13 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
             if (len > 0 && len <= 7) load_str16(c.data + o[g][j], len, w0, w1);
             key[4 * g + j] = small_key(w0, len);
           }
-        if (more) cur.load(off, c.valid, r0 + stride, lane);
+        cur.load(off, vsrc, rn, lane);
       }
       nulls += 16 - __popc(vb);
       const uint32_t pend = count(key, vb);
       if (__ballot(pend != 0)) admit(key, pend);
-      if (gave_up || (poll && flag == a.fast_epoch)) {
-        gave_up = true;
-        break;
-      }
+      if (flag == a.fast_epoch) gave_up = true;
+      r0 += stride;
     }
   }
   // batch tail or unaligned buffers: lane l owns rows r0 + 64 i + l, bounds-checked
@@ -1882,9 +1884,12 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     }
     if (cand) {
       // rounds 3 .. kCand (their own barriers; cand is block-uniform): the winner of each round
-      // advances past the candidate it placed
+      // advances past the candidate it placed.  Skipped when the second candidate's count is at
+      // most 1 (every later one is too: mostly-unique keys pay no extra barriers); the check
+      // (freq_cand_check) then sees two filled places.
+      const bool more_rounds = (s_top[par][1] >> 16) > 1;
 #pragma unroll
-      for (int r = 2; r < kCand; ++r) {
+      for (int r = 2; r < kCand && more_rounds; ++r) {
         const uint64_t prev = s_top[par][r - 1];
         if (prev && prev == pack(taken)) ++taken;
         const uint64_t w = __ockl_wfred_max_u64(pack(taken));
@@ -2056,13 +2061,16 @@ __global__ void freq_group_select(const Group* g, int64_t n, uint64_t hi_take, u
     }
   }
 }
-// partitions whose candidate list is full (more groups than kCand) and whose last candidate
-// beats `tau`: their unlisted groups could outrank the selection
+// partitions with groups beyond their listed candidates whose last candidate beats `tau`: their
+// unlisted groups could outrank the selection
 __global__ void freq_cand_check(const Group* cand, const unsigned long long* part_groups, int64_t P,
                                 uint64_t tau, unsigned long long* bad) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
        p += (int64_t)gridDim.x * blockDim.x) {
-    if (part_groups[p] > (unsigned long long)kCand && cand[p * kCand + kCand - 1].count > tau)
+    int filled = 0;  // places hold the partition's top groups in count order, empty ones last
+    for (int r = 0; r < kCand; ++r) filled += cand[p * kCand + r].count ? 1 : 0;
+    if (part_groups[p] > (unsigned long long)filled &&
+        (!filled || cand[p * kCand + filled - 1].count > tau))
       atomicAdd(bad, 1ULL);
   }
 }
@@ -2387,6 +2395,11 @@ static dq_status launch_phaseA_small(dq_freq* f, AArgs& a) {
   a.fast_words = f->dev_words.p + C_N + 1;
   a.fast_epoch = ++f->fast_epoch;
   const KeyCol& c = a.ks.cols[0];
+  static const int poll = [] {  // DQ_FREQ_POLL: A/B hook for the give-up poll interval
+    const char* e = getenv("DQ_FREQ_POLL");
+    return e ? atoi(e) : 0;
+  }();
+  a.fast_poll = poll;
   a.vec_ok = (reinterpret_cast<uintptr_t>(c.values) & 15u) == 0 &&
              (reinterpret_cast<uintptr_t>(c.valid) & 3u) == 0;
   hipLaunchKernelGGL(freq_phaseA_small, dim3((unsigned)n_wg), dim3(kSmallThreads), 0, f->stream, a);

@@ -238,7 +238,7 @@ def test_merge_keeps_hash_collisions_apart_and_handles_histogram_nulls(gpu_devic
         assert m.null_literal() == (exp[(None,)], exp.get(("NullValue",), 0) if col == "s" else 0)
 
 
-@pytest.mark.parametrize("n,k", [(1, 10), (5000, 3), (40_000, 1000), (200_000, 1000)])
+@pytest.mark.parametrize("n,k", [(1, 10), (5000, 3), (3000, 2000), (40_000, 1000), (200_000, 1000)])
 @pytest.mark.parametrize("col", ["id", "s", "u"])
 def test_topk_matches_oracle_order(n, k, col, gpu_device):
     """dq_freq_topk == rdd.top(k)(OrderByAbsoluteCount) up to ties: the multiset of returned counts
