@@ -143,6 +143,8 @@ def _load() -> ctypes.CDLL:
                                      c_void_p]),
         "dq_freq_partition_sizes": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
         "dq_freq_partition": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
+        "dq_key_partition": (c_int, [POINTER(dq_column), c_int, c_int, c_int, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]),
         "dq_freq_add_records_device": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                                c_void_p, c_int64, c_void_p, c_int, c_void_p]),
     }
@@ -168,7 +170,7 @@ EXPORTED = [
     "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge", "dq_freq_topk", "dq_loader_create",
     "dq_loader_destroy", "dq_loader_stage", "dq_loader_release", "dq_scan_host",
     "dq_freq_add_host", "dq_freq_partition_sizes", "dq_freq_partition",
-    "dq_freq_add_records_device",
+    "dq_freq_add_records_device", "dq_key_partition",
 ]
 FREQ_RECORD_BYTES = 24  # sizeof(dq_freq_record)
 

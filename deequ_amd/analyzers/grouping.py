@@ -85,6 +85,10 @@ class FrequencyTable:
 
     def export(self) -> List[Tuple[tuple, int]]:
         """All groups as (key tuple, count); a NULL key component is None."""
+        return self.decode_groups(*self.export_raw())
+
+    def export_raw(self):
+        """dq_freq_export's arrays: (counts[n], key offsets[n + 1], encoded key bytes)."""
         n = self.count()
         need = ctypes.c_int64()
         N.check(N.lib.dq_freq_export(self.handle, None, None, None, 0, 0, ctypes.byref(need)))
@@ -93,15 +97,15 @@ class FrequencyTable:
         raw = np.zeros(max(1, need.value), np.uint8)
         N.check(N.lib.dq_freq_export(self.handle, counts.ctypes.data, offs.ctypes.data,
                                      raw.ctypes.data, n, need.value, ctypes.byref(need)))
-        data = raw.tobytes()
-        out = []
-        for g in range(n):
-            out.append((self._decode(data, int(offs[g])), int(counts[g])))
-        return out
+        return counts[:n], offs[:n + 1], raw[:need.value]
 
     def topk(self, k: int) -> List[Tuple[tuple, int]]:
         """The k largest groups by count, descending (dq_freq_topk: only these keys leave the
         device; rdd.top(maxDetailBins) in Histogram.scala:78, ties in any order)."""
+        return self.decode_groups(*self.topk_raw(k))
+
+    def topk_raw(self, k: int):
+        """dq_freq_topk's arrays: (counts[n], key offsets[n + 1], encoded key bytes)."""
         n, need = ctypes.c_int64(), ctypes.c_int64()
         N.check(N.lib.dq_freq_topk(self.handle, k, None, None, None, 0, ctypes.byref(n),
                                    ctypes.byref(need)))
@@ -111,8 +115,11 @@ class FrequencyTable:
         N.check(N.lib.dq_freq_topk(self.handle, k, counts.ctypes.data, offs.ctypes.data,
                                    raw.ctypes.data, need.value, ctypes.byref(n),
                                    ctypes.byref(need)))
-        data = raw.tobytes()
-        return [(self._decode(data, int(offs[g])), int(counts[g])) for g in range(n.value)]
+        return counts[:n.value], offs[:n.value + 1], raw[:need.value]
+
+    def decode_groups(self, counts, offs, raw) -> List[Tuple[tuple, int]]:
+        data = bytes(raw)
+        return [(self._decode(data, int(offs[g])), int(counts[g])) for g in range(len(counts))]
 
     def _decode(self, data: bytes, pos: int) -> tuple:
         key = []

@@ -193,12 +193,19 @@ class ApproxQuantile(Analyzer):
     def compute_state_from(self, data):
         from ..distributed import is_distributed
         s = quantile_summaries(data, self.column, self.relative_error)
-        if is_distributed(data):  # every rank's summary, merged in rank order
-            import torch.distributed as dist
-            parts = [None] * dist.get_world_size()
-            dist.all_gather_object(parts, (s.sampled, s.count))
+        if is_distributed(data):  # every rank's summary (arrays, one device gather), rank order
+            from ..distributed import all_gather_varbytes
+            m = len(s.sampled)
+            v = np.array([x[0] for x in s.sampled], np.float64)
+            gd = np.array([[x[1], x[2]] for x in s.sampled], np.int64).reshape(m, 2)
+            blob = np.array([s.count, m], np.int64).tobytes() + v.tobytes() + gd.tobytes()
+            parts = all_gather_varbytes(blob, f"cuda:{data.device_index()}")
             s = QuantileSummaries(self.relative_error, [], 0)
-            for sampled, cnt in parts:
+            for b in parts:
+                cnt, m = (int(x) for x in np.frombuffer(b, np.int64, 2))
+                v = np.frombuffer(b, np.float64, m, 16)
+                gd = np.frombuffer(b, np.int64, 2 * m, 16 + 8 * m).reshape(m, 2)
+                sampled = [(float(v[i]), int(gd[i, 0]), int(gd[i, 1])) for i in range(m)]
                 s = s.merge(QuantileSummaries(self.relative_error, sampled, cnt))
         return ApproxQuantileState(s) if s.count else None
 

@@ -3646,3 +3646,161 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
   f->num_rows += num_rows;
   return push_counters(f);
 }
+
+// ------------------------------------------------------------------------------------------------
+// Multi-GPU raw-key repartition: a one-column fixed-width key of high
+// cardinality (a unique id) is exchanged as its raw values, before any local count -- one
+// group-by per row on its owner rank and 1-8 bytes per row over xGMI, instead of a local group-by,
+// 24-byte records and a second group-by.  The owner is a function of the key the table counts
+// (fmix of the canonical widened value, freq_codec.h), so every rank sends equal keys to one owner;
+// NULL rows stay home as a count.
+// ------------------------------------------------------------------------------------------------
+namespace dq {
+
+constexpr int kKeyPartThreads = 256;
+constexpr int kKeyPartRows = 16 * kKeyPartThreads;  // rows per block step
+
+DQ_DEV uint32_t raw_owner(int type, const void* values, int64_t r, int null_as_group, int parts) {
+  KeySet ks;
+  ks.n_keys = 1;
+  ks.null_as_group = null_as_group;
+  ks.cols[0].type = type;
+  const uint64_t h = fmix_bij(exact_canon(ks, kwiden(type, values, r)));
+  return (uint32_t)(((h & 0xFFFFFFULL) * (uint64_t)parts) >> 24);  // low bits: the owner's keys
+                                                                   // still fill every bucket
+}
+
+__global__ void __launch_bounds__(kKeyPartThreads)
+key_owner_count(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
+                int64_t rows, int null_as_group, int parts, unsigned long long* __restrict__ counts,
+                unsigned long long* __restrict__ nulls) {
+  __shared__ uint32_t s_cnt[kMaxParts];
+  for (int i = threadIdx.x; i < parts; i += kKeyPartThreads) s_cnt[i] = 0;
+  __syncthreads();
+  unsigned long long nn = 0;
+  for (int64_t r = (int64_t)blockIdx.x * kKeyPartThreads + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * kKeyPartThreads) {
+    if (!kbit(valid, r)) {
+      ++nn;
+      continue;
+    }
+    atomicAdd(&s_cnt[raw_owner(type, values, r, null_as_group, parts)], 1u);
+  }
+  nn = wave_sum(nn);
+  if (__lane_id() == 0 && nn) atomicAdd(nulls, nn);
+  __syncthreads();
+  for (int i = threadIdx.x; i < parts; i += kKeyPartThreads)
+    if (s_cnt[i]) atomicAdd(&counts[i], (unsigned long long)s_cnt[i]);
+}
+
+// Each block step of kKeyPartRows rows counts its rows per owner in LDS, reserves its run in every
+// owner segment with one atomic per owner, then writes every row's value into its run (the runs of
+// a step are contiguous per owner, so the stores of a wave land in a few neighbouring lines).
+__global__ void __launch_bounds__(kKeyPartThreads)
+key_owner_scatter(int type, int elem, const uint8_t* __restrict__ valid,
+                  const void* __restrict__ values, int64_t rows, int null_as_group, int parts,
+                  unsigned long long* __restrict__ cursor, uint8_t* __restrict__ out) {
+  __shared__ uint32_t s_cnt[kMaxParts], s_pos[kMaxParts];
+  __shared__ unsigned long long s_base[kMaxParts];
+  for (int64_t r0 = (int64_t)blockIdx.x * kKeyPartRows; r0 < rows;
+       r0 += (int64_t)gridDim.x * kKeyPartRows) {
+    for (int i = threadIdx.x; i < parts; i += kKeyPartThreads) s_cnt[i] = s_pos[i] = 0;
+    __syncthreads();
+    uint32_t own[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int64_t r = r0 + (int64_t)k * kKeyPartThreads + threadIdx.x;
+      own[k] = ~0u;
+      if (r < rows && kbit(valid, r)) {
+        own[k] = raw_owner(type, values, r, null_as_group, parts);
+        atomicAdd(&s_cnt[own[k]], 1u);
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < parts; i += kKeyPartThreads)
+      s_base[i] = s_cnt[i] ? atomicAdd(&cursor[i], (unsigned long long)s_cnt[i]) : 0ULL;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (own[k] == ~0u) continue;
+      const int64_t r = r0 + (int64_t)k * kKeyPartThreads + threadIdx.x;
+      const uint64_t at = s_base[own[k]] + atomicAdd(&s_pos[own[k]], 1u);
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(values) + r * elem;
+      uint8_t* dst = out + at * elem;
+      switch (elem) {
+        case 1: *dst = *src; break;
+        case 2: *reinterpret_cast<uint16_t*>(dst) = *reinterpret_cast<const uint16_t*>(src); break;
+        case 4: *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(src); break;
+        default: *reinterpret_cast<uint64_t*>(dst) = *reinterpret_cast<const uint64_t*>(src); break;
+      }
+    }
+    __syncthreads();  // s_cnt / s_pos / s_base are reset by the next step
+  }
+}
+
+}  // namespace dq
+
+static int raw_key_elem(int type) {
+  switch (type) {
+    case DQ_INT8: return 1;
+    case DQ_INT16: return 2;
+    case DQ_INT32: case DQ_FLOAT32: return 4;
+    case DQ_INT64: case DQ_FLOAT64: return 8;
+    default: return 0;  // bool (bit-packed) and strings: the records path
+  }
+}
+
+extern "C" dq_status dq_key_partition(const dq_column* batches, int n_batches, int n_parts,
+                                      int null_as_group, uint8_t* out, int64_t* counts_out,
+                                      int64_t* null_rows_out, void* hip_stream) {
+  using namespace dq;
+  if ((n_batches > 0 && !batches) || n_batches < 0 || !counts_out || !null_rows_out)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_parts < 1 || n_parts > kMaxParts)
+    return fail(DQ_ERR_UNSUPPORTED, "n_parts must be in [1, %d]", kMaxParts);
+  int64_t rows = 0;
+  int type = n_batches ? batches[0].type : DQ_INT64;
+  const int elem = raw_key_elem(type);
+  if (!elem) return fail(DQ_ERR_WRONG_TYPE, "raw-key repartition needs a fixed-width key");
+  for (int b = 0; b < n_batches; ++b) {
+    if (batches[b].type != type) return fail(DQ_ERR_WRONG_TYPE, "batches differ in type");
+    if (batches[b].length < 0 || (batches[b].length && !batches[b].values))
+      return fail(DQ_ERR_INVALID_ARGUMENT, "batch %d has no values", b);
+    rows += batches[b].length;
+  }
+  if (rows && !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null output buffer");
+  hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
+  DevBuf<unsigned long long> cnt;
+  HIP_TRY(cnt.ensure(2 * kMaxParts + 1));
+  HIP_TRY(hipMemsetAsync(cnt.p, 0, (2 * kMaxParts + 1) * 8, stream));
+  for (int b = 0; b < n_batches; ++b) {
+    const dq_column& c = batches[b];
+    if (!c.length) continue;
+    const unsigned grid = (unsigned)std::min<int64_t>((c.length + kKeyPartRows - 1) / kKeyPartRows * 4, 4096);
+    hipLaunchKernelGGL(key_owner_count, dim3(grid), dim3(kKeyPartThreads), 0, stream, type,
+                       c.validity, c.values, c.length, null_as_group, n_parts, cnt.p,
+                       cnt.p + 2 * kMaxParts);
+    HIP_TRY(hipGetLastError());
+  }
+  unsigned long long h[2 * kMaxParts + 1];
+  HIP_TRY(hipMemcpyAsync(h, cnt.p, sizeof(h), hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  unsigned long long base = 0;
+  for (int j = 0; j < n_parts; ++j) {  // segment cursors: the exclusive prefix of the counts
+    counts_out[j] = (int64_t)h[j];
+    h[kMaxParts + j] = base;
+    base += h[j];
+  }
+  *null_rows_out = (int64_t)h[2 * kMaxParts];
+  HIP_TRY(hipMemcpyAsync(cnt.p + kMaxParts, h + kMaxParts, kMaxParts * 8, hipMemcpyHostToDevice, stream));
+  for (int b = 0; b < n_batches; ++b) {
+    const dq_column& c = batches[b];
+    if (!c.length) continue;
+    const unsigned grid = (unsigned)std::min<int64_t>((c.length + kKeyPartRows - 1) / kKeyPartRows, 4096);
+    hipLaunchKernelGGL(key_owner_scatter, dim3(grid), dim3(kKeyPartThreads), 0, stream, type, elem,
+                       c.validity, c.values, c.length, null_as_group, n_parts, cnt.p + kMaxParts, out);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipStreamSynchronize(stream));  // the cursors' buffer dies here
+  return DQ_OK;
+}

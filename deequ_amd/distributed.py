@@ -107,6 +107,43 @@ def freq_partition(table, n_parts: int, stream=None):
     return rec, var, rc, vb, sp
 
 
+def all_gather_varbytes(payload: bytes, device=None) -> List[bytes]:
+    """Every rank's byte string (sizes may differ): one all-gather of the sizes, then one of the
+    payloads padded to the largest -- tensors, on the device over RCCL, never pickled objects."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    sizes = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(sizes, n)
+    sizes = sizes.cpu().tolist()
+    width = max(1, max(sizes))
+    t = torch.zeros(width, dtype=torch.uint8)
+    if payload:
+        t[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
+    t = t.to(dev)
+    out = torch.empty(world * width, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(out, t)
+    host = out.cpu().numpy()
+    return [host[r * width: r * width + sizes[r]].tobytes() for r in range(world)]
+
+
+def _pack_groups(counts, offs, raw) -> bytes:
+    """(counts, key offsets, encoded keys) of dq_freq_topk / dq_freq_export as one byte string."""
+    head = np.array([len(counts), len(raw)], np.int64)
+    return (head.tobytes() + np.asarray(counts, np.int64).tobytes()
+            + np.asarray(offs, np.int64).tobytes() + np.asarray(raw, np.uint8).tobytes())
+
+
+def _unpack_groups(b: bytes):
+    n, nraw = (int(v) for v in np.frombuffer(b, np.int64, 2))
+    counts = np.frombuffer(b, np.int64, n, 16)
+    offs = np.frombuffer(b, np.int64, n + 1, 16 + 8 * n)
+    raw = np.frombuffer(b, np.uint8, nraw, 16 + 8 * n + 8 * (n + 1))
+    return counts, offs, raw
+
+
 def _comm_device(dev):
     """Where a collective's tensors live: the GPU over RCCL, the host over gloo (CPU tests and the
     two-ranks-on-one-GPU test)."""
@@ -228,19 +265,18 @@ class DistributedFrequencies:
 
     def export(self):
         """Every group of every rank (each group lives on exactly one), rank order."""
-        import torch.distributed as dist
-        parts = [None] * dist.get_world_size()
-        dist.all_gather_object(parts, self.owned.export())
-        return [g for p in parts for g in p]
+        parts = all_gather_varbytes(_pack_groups(*self.owned.export_raw()),
+                                    f"cuda:{self.owned.device}")
+        return [g for p in parts for g in self.owned.decode_groups(*_unpack_groups(p))]
 
     def topk(self, k: int):
         """Global top-k by count: each group lives on one rank, so the k largest are among the
-        union of the ranks' local top-k (Histogram.scala:78, ties in any order)."""
-        import torch.distributed as dist
-        parts = [None] * dist.get_world_size()
-        dist.all_gather_object(parts, self.owned.topk(k))
-        merged = [g for p in parts for g in p]
-        merged.sort(key=lambda g: -g[1])
+        union of the ranks' local top-k (Histogram.scala:78, ties in any order).  Each rank's k
+        groups travel as dq_freq_topk's arrays in one device all-gather."""
+        parts = all_gather_varbytes(_pack_groups(*self.owned.topk_raw(k)),
+                                    f"cuda:{self.owned.device}")
+        merged = [g for p in parts for g in self.owned.decode_groups(*_unpack_groups(p))]
+        merged.sort(key=lambda g: -g[1])  # stable: ties keep rank order
         return merged[:k]
 
 
@@ -257,11 +293,99 @@ def is_distributed(data=None) -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
+RAW_KEY_ELEM = {N.INT8: 1, N.INT16: 2, N.INT32: 4, N.INT64: 8, N.FLOAT32: 4, N.FLOAT64: 8}
+RAW_SAMPLE_ROWS = 1 << 20
+RAW_MIN_DISTINCT = 0.5  # sampled groups per non-NULL row at or above which raw keys travel
+
+
+def _raw_keys_pay(data_shard, column, dtype) -> bool:
+    """Whether the raw-key exchange beats partial aggregation: the groups per non-NULL row of the
+    first RAW_SAMPLE_ROWS rows of every rank's first batch, summed over the ranks (one all-reduce,
+    so every rank takes the same path).  A unique id samples ~1.0, a low-cardinality key ~0."""
+    import torch
+    import torch.distributed as dist
+    from .analyzers.grouping import FrequencyTable
+    from .table import ColumnBatch
+    groups = rows = 0
+    if data_shard.batches and data_shard.batches[0][column].length:
+        c = data_shard.batches[0][column]
+        m = min(c.length, RAW_SAMPLE_ROWS)
+        t = FrequencyTable([column], [dtype], data_shard.device_index(), capacity_hint=m)
+        t.add([ColumnBatch(dtype, m, c.validity, c.values)])
+        s = t.summarize()
+        groups, rows = int(s.n_groups), int(s.num_rows - s.n_null_key_rows)
+    v = torch.tensor([groups, rows], dtype=torch.int64,
+                     device=_comm_device(f"cuda:{data_shard.device_index()}"))
+    dist.all_reduce(v)
+    g, r = (int(x) for x in v.cpu().tolist())
+    return r > 0 and g >= RAW_MIN_DISTINCT * r
+
+
+def raw_key_repartition(data_shard, column, dtype, null_as_group: bool = False):
+    """The Exchange of a high-cardinality one-column fixed-width key as raw values: every rank cuts
+    its rows into owner segments on the device (dq_key_partition), the segments meet in one
+    all-to-all (1-8 bytes per row over xGMI), and each owner counts what it received in ONE
+    group-by.  NULL rows stay home as counts; numRows and the NULL counts are summed in one
+    all-reduce and the NULL group lives on rank 0, as in freq_repartition."""
+    import torch
+    import torch.distributed as dist
+    from .analyzers.grouping import FrequencyTable
+    from .table import ColumnBatch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    dev = f"cuda:{data_shard.device_index()}"
+    elem = RAW_KEY_ELEM[dtype]
+    cols = [b[column] for b in data_shard.batches]
+    rows = sum(c.length for c in cols)
+    arr = (N.dq_column * max(1, len(cols)))(*[c.to_c() for c in cols])
+    out = torch.empty(max(1, rows * elem), dtype=torch.uint8, device=dev)
+    counts = np.zeros(world, np.int64)
+    nulls = ctypes.c_int64()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    N.check(N.lib.dq_key_partition(arr, len(cols), world, 1 if null_as_group else 0,
+                                   out.data_ptr(), counts.ctypes.data, ctypes.byref(nulls), stream))
+    cdev = _comm_device(dev)
+    sizes = torch.from_numpy(counts.copy()).to(cdev)
+    got = torch.empty_like(sizes)
+    dist.all_to_all_single(got, sizes)
+    src = got.cpu().numpy()
+    sent = out[: int(counts.sum()) * elem].to(cdev)
+    recv = torch.empty(max(1, int(src.sum()) * elem), dtype=torch.uint8, device=cdev)
+    dist.all_to_all_single(recv[: int(src.sum()) * elem], sent,
+                           output_split_sizes=(src * elem).tolist(),
+                           input_split_sizes=(counts * elem).tolist())
+    recv = recv.to(dev)
+    del out, sent
+    n_recv = int(src.sum())
+    owned = FrequencyTable([column], [dtype], data_shard.device_index(), capacity_hint=n_recv)
+    step = 1 << 26
+    for lo in range(0, n_recv, step):
+        m = min(step, n_recv - lo)
+        owned.add([ColumnBatch(dtype, m, None, recv[lo * elem: (lo + m) * elem])],
+                  null_as_group=null_as_group)
+    tot = torch.tensor([rows, nulls.value], dtype=torch.int64, device=cdev)
+    dist.all_reduce(tot)
+    tot_rows, tot_nulls = (int(v) for v in tot.cpu().tolist())
+    special = np.zeros(3, np.int64)
+    if rank == 0:
+        special[1 if null_as_group else 2] = tot_nulls
+    zero = np.zeros(1, np.int64)
+    N.check(N.lib.dq_freq_add_records_device(
+        owned.handle, None, None, 1, zero.ctypes.data, zero.ctypes.data, tot_rows - n_recv,
+        special.ctypes.data, 1 if null_as_group else 0, stream))
+    return owned
+
+
 def compute_frequencies_distributed(data_shard, grouping_columns, null_as_group: bool = False):
     """FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:53-80) over a row-sharded
-    table: local partial aggregate on each rank's shard, then freq_repartition."""
+    table: a one-column fixed-width key of high cardinality travels as raw values
+    (raw_key_repartition); every other key is aggregated locally first (the partial aggregate of
+    each rank's shard), then freq_repartition exchanges the groups."""
     from .analyzers.grouping import FrequenciesAndNumRows, FrequencyTable
     types = [data_shard.schema[c].dtype for c in grouping_columns]
+    if len(grouping_columns) == 1 and types[0] in RAW_KEY_ELEM and \
+            _raw_keys_pay(data_shard, grouping_columns[0], types[0]):
+        owned = raw_key_repartition(data_shard, grouping_columns[0], types[0], null_as_group)
+        return FrequenciesAndNumRows(DistributedFrequencies(owned), owned.num_rows)
     local = FrequencyTable(grouping_columns, types, data_shard.device_index())
     for batch in data_shard.batches:
         local.add([batch[c] for c in grouping_columns], null_as_group=null_as_group)

@@ -409,6 +409,18 @@ dq_status dq_freq_add_records_device(dq_freq* freq, const dq_freq_record* record
                                      const int64_t* src_var_bytes, int64_t num_rows,
                                      const int64_t* special, int null_as_group, void* hip_stream);
 
+/* Raw-key repartition (the same Exchange, for a one-column fixed-width key of high cardinality:
+ * int8..int64, float, double).  Exchanging the rows' raw values before any local count costs one
+ * group-by per row on the owner and 1-8 bytes per row over the link, where partitioning a partial
+ * table costs a group-by on every rank, 24-byte records and a second group-by.  Writes the non-NULL
+ * values of all batches into out (device, (rows of all batches) x element size bytes), owner j's
+ * segment at the exclusive prefix of counts_out[0..n_parts); the owner is a function of the key the
+ * table counts (NaN payloads canonical under null_as_group, as in dq_freq_add_device), so equal
+ * keys of every rank meet on one owner.  NULL rows stay home: *null_rows_out.  Synchronous. */
+dq_status dq_key_partition(const dq_column* batches, int n_batches, int n_parts, int null_as_group,
+                           uint8_t* out, int64_t* counts_out, int64_t* null_rows_out,
+                           void* hip_stream);
+
 /* Returns the device blocks the engine keeps cached for reuse (every dq_* buffer is handed back
  * to a per-device cache when freed, so building many tables does not hipMalloc / hipFree
  * gigabytes each time) to the HIP runtime. */

@@ -185,3 +185,50 @@ def test_gloo_world3_frequency_segment_exchange():
             assert rc[src] == n
         assert rec == exp_rec
         assert var == exp_var
+
+
+def _varbytes_worker(rank, world, port, out_q):
+    """Each rank gathers a ragged byte string (empty on rank 1) and a packed group list through the
+    product's device-gather helpers (deequ_amd.distributed.all_gather_varbytes, _pack_groups)."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from deequ_amd.distributed import _pack_groups, _unpack_groups, all_gather_varbytes
+        payload = b"" if rank == 1 else bytes(range(rank * 7 % 251)) * (rank + 1)
+        got = all_gather_varbytes(payload)
+        counts = np.arange(rank + 2, dtype=np.int64) * 10 + rank
+        offs = np.arange(rank + 3, dtype=np.int64) * 12
+        raw = np.full(12 * (rank + 2), rank, np.uint8)
+        groups = [tuple(a.tolist() for a in _unpack_groups(b))
+                  for b in all_gather_varbytes(_pack_groups(counts, offs, raw))]
+        out_q.put((rank, got, groups))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world3_varbytes_gather():
+    """The tensor all-gather that carries Histogram's per-rank top-k, frequency exports and
+    quantile summaries (instead of pickled objects): ragged and empty payloads arrive intact, in
+    rank order, on every rank."""
+    import torch.multiprocessing as mp
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_varbytes_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (got, groups) for r, got, groups in (q.get(timeout=180) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = [b"" if r == 1 else bytes(range(r * 7 % 251)) * (r + 1) for r in range(world)]
+    for r in range(world):
+        got, groups = res[r]
+        assert got == exp
+        for src, (counts, offs, raw) in enumerate(groups):
+            assert counts == (np.arange(src + 2) * 10 + src).tolist()
+            assert offs == (np.arange(src + 3) * 12).tolist()
+            assert raw == [src] * (12 * (src + 2))

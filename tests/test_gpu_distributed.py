@@ -48,3 +48,29 @@ def test_two_ranks_reproduce_one_rank(gpu_device, tmp_path):
                     assert v[2][key] == c, (k, key)
         else:
             assert close(g, v), (k, g, v)
+
+
+def test_two_ranks_match_the_oracle(gpu_device, tmp_path):
+    """The same two-rank run against the oracle (not only against the engine's one-rank run):
+    every grouping metric -- including the unique int64 / int32 ids that take the raw-key exchange
+    (dq_key_partition) and the low-cardinality keys that take the partial-aggregate exchange --
+    Histogram bins and counts, and the scan metrics.  Bar: counts and bins exact, fp64 1e-12."""
+    sys.path.insert(0, HERE)
+    from dist_suite import close, oracle_metrics, table
+    exp = oracle_metrics(table())
+    out = tmp_path / "ranks.json"
+    port = _port()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "workers", "dist_ranks.py"),
+                               str(r), "2", str(port), str(out)], env=env)
+             for r in range(2)]
+    codes = [p.wait(timeout=240) for p in procs]
+    assert codes == [0, 0], codes
+    got = json.loads(out.read_text())
+    for k, v in exp.items():
+        g = got[k]
+        if isinstance(v, list):  # Histogram: bins, and the top counts (ties in any order)
+            assert g[0] == v[0], k
+            assert g[1] == v[1][:len(g[1])], k
+        else:
+            assert close(g, v), (k, g, v)
