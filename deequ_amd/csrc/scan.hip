@@ -379,7 +379,9 @@ struct StrStep {
       }
       last[g] = ldg_i32(off + r0 + 256 * g + 256);
     }
-    if (t.valid) c.load(t.valid, r0);
+    // (unconditional: without a validity bitmap it reads the offsets and is ignored, so the loads
+    // of a step are a fixed count the compiler can wait on one by one)
+    c.load(t.valid ? t.valid : reinterpret_cast<const uint8_t*>(off), r0);
   }
 };
 
@@ -390,11 +392,14 @@ DQ_DEV void str_in_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& 
   int64_t ct = 0, cn = 0;
   int64_t r0 = r_begin;
   if (t.vec_ok && r0 + kWaveRows <= r_end) {
-    // software pipeline: step k+1's offsets and bitmaps are in flight while step k's strings load
+    // software pipeline: step k+1's offsets and bitmaps are in flight while step k's strings
+    // load.  The prefetch is unconditional (the last step re-reads itself): with a conditional one
+    // the compiler could not count the loads in flight and waited for the prefetch before the
+    // step's last strings.
     StrStep cur;
     cur.load(t, off, r0, l);
     for (; r0 + kWaveRows <= r_end; r0 += kWaveRows) {
-      const bool more = r0 + 2 * kWaveRows <= r_end;
+      const int64_t rn = r0 + 2 * kWaveRows <= r_end ? r0 + kWaveRows : r0;
       uint32_t vb = 0xffffu, wt = 0xffffu;
       if (t.valid) {
         vb = 0;
@@ -434,7 +439,7 @@ DQ_DEV void str_in_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& 
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[4 * g + j] = ldg64_unaligned(t.data + o[g][j]);
         __builtin_amdgcn_sched_barrier(0);
-        if (more) cur.load(t, off, r0 + kWaveRows, l);
+        cur.load(t, off, rn, l);
         __builtin_amdgcn_sched_barrier(0);
         uint32_t hits = 0;
 #pragma unroll
@@ -446,7 +451,7 @@ DQ_DEV void str_in_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& 
         ct += __popc((t.negate ? ~hits : hits) & sel) + __popc(nulls);
         cn += __popc(sel) + __popc(nulls);
       } else {
-        if (more) cur.load(t, off, r0 + kWaveRows, l);
+        cur.load(t, off, rn, l);
 #pragma unroll
         for (int g = 0; g < 4; ++g) str_in_rows(t, o[g], vb >> (4 * g), wt >> (4 * g), dlen, ct, cn);
       }
