@@ -244,6 +244,9 @@ struct AArgs {
   uint64_t fast_epoch;
   int32_t vec_ok;  // offsets / validity aligned for the 16-byte / dword streaming loads
   int32_t fast_poll;  // steps between polls of the give-up word (0: never)
+  // the batch's groups merged across workgroups (freq_phaseA_small): kBatchSlots keys (+1, 0 =
+  // free), their counts, then the workgroups' arrival counter; zeroed before the launch
+  unsigned long long* batch_tab;
 };
 
 // Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
@@ -811,6 +814,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
 // ------------------------------------------------------------------------------------------------
 constexpr int kSmallCand = 8;
 constexpr int kSmallThreads = 256;
+constexpr int kBatchSlots = 64;
+constexpr int kBatchTabWords = 2 * kBatchSlots + 1;
 constexpr uint64_t kLongKey = ~0ULL;
 // an unused candidate: length byte 0xFE, which neither a short key (<= 7) nor kLongKey (0xFF) has,
 // so a long string never matches a free slot and is always seen as a miss
@@ -856,8 +861,10 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   constexpr int NW = kSmallThreads / 64;
   __shared__ uint64_t s_key[NW * kSmallCand], s_cnt[NW * kSmallCand];
   __shared__ uint32_t s_nc[NW];
-  __shared__ uint64_t g_key[NW * kSmallCand], g_cnt[NW * kSmallCand], g_off[NW * kSmallCand];
-  __shared__ uint32_t g_rec[NW * kSmallCand];  // records (count digits) per group
+  // the workgroup's groups (+ the batch table's, for the last workgroup)
+  __shared__ uint64_t g_key[NW * kSmallCand + kBatchSlots], g_cnt[NW * kSmallCand + kBatchSlots],
+      g_off[NW * kSmallCand + kBatchSlots];
+  __shared__ uint32_t g_rec[NW * kSmallCand + kBatchSlots];  // records (count digits) per group
   __shared__ uint32_t s_ng;
   const int tid = threadIdx.x, lane = (int)__lane_id(), wave = tid >> 6;
   const KeyCol& c = a.ks.cols[0];
@@ -1026,7 +1033,12 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   if (lane == 0 && nulls)
     atomicAdd(&a.fast_words[a.ks.null_as_group ? 2 : 1], nulls);
   __syncthreads();
-  if (tid == 0) {  // <= NW * kSmallCand groups: merged, encoded, hashed, placed by one thread
+  // thread 0: the waves' lists merged (<= NW * kSmallCand groups), then added into the batch's
+  // device table (a batch of a 3-value column then leaves 3 records, not 3 per workgroup: phase C
+  // would otherwise count ~2000 records of one key per partition, a serial chain of LDS atomics
+  // on one slot); a group the full table cannot take stays in this workgroup's own records.  The
+  // last workgroup to arrive writes the table's groups as its records too.
+  if (tid == 0) {
     uint32_t ng = 0;
     for (int w = 0; w < NW; ++w)
       for (uint32_t k = 0; k < s_nc[w]; ++k) {
@@ -1040,6 +1052,40 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
         }
         g_cnt[g] += ct;
       }
+    unsigned long long* tkeys = a.batch_tab;
+    unsigned long long* tcnts = a.batch_tab + kBatchSlots;
+    uint32_t kept = 0;  // groups the table did not take, compacted to the front
+    for (uint32_t g = 0; g < ng; ++g) {
+      const unsigned long long tag = (unsigned long long)g_key[g] + 1ULL;  // never 0
+      uint32_t slot = (uint32_t)(fmix_bij(g_key[g]) & (kBatchSlots - 1));
+      bool placed = false;
+      for (int probe = 0; probe < kBatchSlots && !placed; ++probe, slot = (slot + 1) & (kBatchSlots - 1)) {
+        const unsigned long long prev = atomicCAS(&tkeys[slot], 0ULL, tag);
+        if (prev == 0ULL || prev == tag) {
+          atomicAdd(&tcnts[slot], (unsigned long long)g_cnt[g]);
+          placed = true;
+        }
+      }
+      if (!placed) {
+        g_key[kept] = g_key[g];
+        g_cnt[kept++] = g_cnt[g];
+      }
+    }
+    __threadfence();
+    const unsigned long long arrived =
+        atomicAdd(&a.batch_tab[2 * kBatchSlots], 1ULL);  // after this workgroup's adds
+    const bool last = arrived == (unsigned long long)gridDim.x - 1;
+    if (last) {  // every workgroup's adds are in: the table's groups join this one's records
+      __threadfence();
+      for (int slot = 0; slot < kBatchSlots; ++slot) {
+        const unsigned long long tag =
+            __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!tag) continue;
+        g_key[kept] = tag - 1ULL;
+        g_cnt[kept++] = __hip_atomic_load(&tcnts[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    ng = kept;
     uint64_t bytes = 0;
     for (uint32_t g = 0; g < ng; ++g) bytes += 8 + pad4((uint32_t)(g_key[g] >> 56));
     uint64_t at = bytes ? atomicAdd(a.arena_cursor, (unsigned long long)bytes) : 0ULL;
@@ -2188,6 +2234,7 @@ struct dq_freq {
   int64_t n_chunks = 0;
   DevBuf<uint8_t> arena;                 // hashed: encoded keys
   DevBuf<unsigned long long> dev_words;  // counters[C_N], then the arena cursor
+  DevBuf<unsigned long long> batch_tab;  // freq_phaseA_small's cross-workgroup group table
   uint64_t h_counters[C_N] = {0};
   uint64_t arena_used = 0;
   // phase A launches leave the device counters and arena cursor ahead of the host copies: they
@@ -2393,6 +2440,9 @@ static dq_status launch_phaseA_small(dq_freq* f, AArgs& a) {
   phaseA_chunks(true, false, a.n_items, a.tile_items, &n_wg);
   a.tiles_per_wg = AKeys<true, false>::kTilesPerWg;
   a.fast_words = f->dev_words.p + C_N + 1;
+  HIP_TRY(f->batch_tab.ensure(kBatchTabWords));
+  HIP_TRY(hipMemsetAsync(f->batch_tab.p, 0, kBatchTabWords * 8, f->stream));
+  a.batch_tab = f->batch_tab.p;
   a.fast_epoch = ++f->fast_epoch;
   const KeyCol& c = a.ks.cols[0];
   static const int poll = [] {  // DQ_FREQ_POLL: A/B hook for the give-up poll interval
@@ -3123,7 +3173,7 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     // + what a small-key attempt that gives the batch up may have reserved
     int64_t n_wg_a = 0;
     phaseA_chunks(true, false, rows, f->tile, &n_wg_a);
-    bound += (uint64_t)n_wg_a * (kSmallThreads / 64) * kSmallCand * 16;
+    bound += (uint64_t)n_wg_a * (kSmallThreads / 64) * kSmallCand * 16 + kBatchSlots * 16;
     if (f->arena.n < f->arena_hi + bound + 64) {  // may not fit: learn the true use, then grow
       dq_status cs = pull_counters(f);
       if (cs != DQ_OK) return cs;

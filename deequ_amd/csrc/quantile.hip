@@ -2,17 +2,23 @@
 //
 // The reference feeds every non-NULL value, as a double, into Spark's ApproximatePercentile
 // (QuantileSummaries, Greenwald-Khanna with relativeError).  Here the values of all batches are
-// gathered as doubles, sorted on the device (rocPRIM radix sort: the order is Java's
-// Double.compare once NaNs are canonical, -0.0 before 0.0), and handed to the host as either every
-// value (few enough that the host replays Spark's own insert + compress exactly) or values at
-// evenly spaced exact ranks (a GK summary whose error is far inside relativeError).  The summary
-// arithmetic -- insert, compress, merge, query -- is host code (deequ_amd/analyzers/quantile.py).
+// gathered as order-preserving 64-bit keys (Java's Double.compare order as unsigned order: NaNs
+// canonical and largest, -0.0 before 0.0) and handed to the host as either
+//   * every value, sorted (rocPRIM radix sort) -- few enough that the host replays Spark's own
+//     insert + compress exactly, or relativeError 0 (the exact summary); or
+//   * the values at m evenly spaced exact ranks floor(j (n - 1) / (m - 1)) (a GK summary whose
+//     error is far inside relativeError), found by a radix SELECT: a few histogram passes over the
+//     keys narrow every rank to one bin, and only the bins that hold a rank are compacted and
+//     sorted -- instead of sorting every value.
+// The summary arithmetic -- insert, compress, merge, query -- is host code
+// (deequ_amd/analyzers/quantile.py).
 #include <hip/hip_runtime.h>
 
 #include <cstring>  // rocprim headers use memset without including it
 
 #include <rocprim/rocprim.hpp>
 
+#include <algorithm>
 #include <vector>
 
 #include "device_util.h"
@@ -25,31 +31,34 @@ namespace {
 constexpr int kGatherThreads = 256;
 constexpr int kGatherWaves = kGatherThreads / 64;
 constexpr int kGatherRounds = 16;  // rows per thread per block step: 4096 rows a step
+constexpr int64_t kGatherStep = (int64_t)kGatherRounds * kGatherThreads;
 
 static_assert(kGatherRounds * kGatherWaves == 64, "one wave scans the step's counts");
 
-// Non-NULL values of one batch -> doubles at out[*cursor ...] (order irrelevant: sorted next).
-// A block step covers 4096 rows (round i: rows r0 + 256 i + tid, coalesced); the kept rows of a
-// step are placed by one exclusive scan over its (round, wave) ballot counts and ONE cursor
-// atomic per step -- one per wave (a same-address atomic every 64 rows) serialised the kernel.
-__global__ void __launch_bounds__(kGatherThreads)
-quantile_gather(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
-                int64_t rows, double* __restrict__ out, unsigned long long* __restrict__ cursor) {
-  __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
-  __shared__ unsigned long long s_base;
-  const int tid = threadIdx.x, lane = (int)__lane_id(), wave = tid >> 6;
-  const uint64_t lt = lane ? (~0ULL >> (64 - lane)) : 0ULL;  // lanes below this one
-  constexpr int64_t kStep = (int64_t)kGatherRounds * kGatherThreads;
-  for (int64_t r0 = (int64_t)blockIdx.x * kStep; r0 < rows; r0 += (int64_t)gridDim.x * kStep) {
-    double v[kGatherRounds];
+// Double.compare order as unsigned order (the canonical NaN is the largest key)
+DQ_HD uint64_t ordered_key(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  return (b >> 63) ? ~b : (b | (1ULL << 63));
+}
+DQ_HD double from_ordered(uint64_t k) {
+  return __builtin_bit_cast(double, (k >> 63) ? (k & ~(1ULL << 63)) : ~k);
+}
+
+// A block step of 4096 items (round i: item base + 256 i + tid) keeps the items whose bit is set
+// in keep[i]; their values land at out[*cursor ...] in (round, wave, lane) order of the step,
+// placed by one exclusive scan over the step's 64 (round, wave) ballot counts and ONE cursor
+// atomic per step (one atomic per wave on one address serialised the kernel).
+struct StepPlacer {
+  uint32_t* s_cnt;  // kGatherRounds * kGatherWaves
+  unsigned long long* s_base;
+  DQ_DEV void place(const bool (&keep)[kGatherRounds], const uint64_t (&v)[kGatherRounds],
+                    uint64_t* __restrict__ out, unsigned long long* __restrict__ cursor) {
+    const int tid = threadIdx.x, lane = (int)__lane_id(), wave = tid >> 6;
+    const uint64_t lt = lane ? (~0ULL >> (64 - lane)) : 0ULL;  // lanes below this one
     uint64_t m[kGatherRounds];
 #pragma unroll
     for (int i = 0; i < kGatherRounds; ++i) {
-      const int64_t r = r0 + (int64_t)i * kGatherThreads + tid;
-      const bool keep = r < rows && bit1(valid, r);
-      v[i] = keep ? load_f64(type, values, r) : 0.0;
-      if (v[i] != v[i]) v[i] = __builtin_nan("");  // Double.compare: every NaN is the canonical one
-      m[i] = __ballot(keep);
+      m[i] = __ballot(keep[i]);
       if (lane == 0) s_cnt[i * kGatherWaves + wave] = (uint32_t)__popcll(m[i]);
     }
     __syncthreads();
@@ -66,34 +75,262 @@ quantile_gather(int type, const uint8_t* __restrict__ valid, const void* __restr
       if (lane == 63 && total) base = atomicAdd(cursor, (unsigned long long)total);
       base = __shfl(base, 63);
       s_cnt[tid] = x - c;
-      if (lane == 0) s_base = base;
+      if (lane == 0) *s_base = base;
     }
     __syncthreads();
-    const unsigned long long base = s_base;
+    const unsigned long long base = *s_base;
 #pragma unroll
     for (int i = 0; i < kGatherRounds; ++i)
-      if ((m[i] >> lane) & 1u)
-        out[base + s_cnt[i * kGatherWaves + wave] + __popcll(m[i] & lt)] = v[i];
+      if ((m[i] >> lane) & 1u) out[base + s_cnt[i * kGatherWaves + wave] + __popcll(m[i] & lt)] = v[i];
     __syncthreads();  // s_cnt / s_base are rewritten by the next step
+  }
+};
+
+// Non-NULL values of one batch -> ordered keys at out[*cursor ...] (order irrelevant).
+__global__ void __launch_bounds__(kGatherThreads)
+quantile_gather(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
+                int64_t rows, uint64_t* __restrict__ out, unsigned long long* __restrict__ cursor) {
+  __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
+  __shared__ unsigned long long s_base;
+  StepPlacer pl{s_cnt, &s_base};
+  for (int64_t r0 = (int64_t)blockIdx.x * kGatherStep; r0 < rows; r0 += (int64_t)gridDim.x * kGatherStep) {
+    bool keep[kGatherRounds];
+    uint64_t v[kGatherRounds];
+#pragma unroll
+    for (int i = 0; i < kGatherRounds; ++i) {
+      const int64_t r = r0 + (int64_t)i * kGatherThreads + threadIdx.x;
+      keep[i] = r < rows && bit1(valid, r);
+      double d = keep[i] ? load_f64(type, values, r) : 0.0;
+      if (d != d) d = __builtin_nan("");  // Double.compare: every NaN is the canonical one
+      v[i] = ordered_key(d);
+    }
+    pl.place(keep, v, out, cursor);
   }
 }
 
-// out[j] = sorted[floor(j * (count - 1) / (n - 1))], j < n: the min, the max and evenly spaced
-// exact ranks between
-__global__ void quantile_pick(const double* __restrict__ sorted, int64_t count, int64_t n,
-                              double* __restrict__ out) {
+// ---- radix select -----------------------------------------------------------------------------
+// A pass counts the keys whose top `bits` bits equal one of the A active prefixes (sorted, unique)
+// by their next D bits: hist[a << D | digit], A << D <= kSelBins, privatised in LDS per block.
+constexpr int kSelBins = 8192;  // 32 KB of LDS counters (+ 16 KB of prefixes at most)
+constexpr int kSelMaxTargets = 2048;
+
+DQ_DEV int find_prefix(const uint64_t* act, int A, uint64_t p) {
+  int lo = 0, hi = A;  // first index with act[i] >= p
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (act[mid] < p) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < A && act[lo] == p ? lo : -1;
+}
+
+__global__ void __launch_bounds__(256)
+select_hist(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __restrict__ active, int A,
+            int bits, int D, unsigned int* __restrict__ hist) {
+  extern __shared__ uint64_t sel_lds[];
+  uint64_t* s_act = sel_lds;                                            // A
+  unsigned int* s_hist = reinterpret_cast<unsigned int*>(sel_lds + A);  // A << D
+  const int nb = A << D;
+  for (int i = threadIdx.x; i < A; i += 256) s_act[i] = active[i];
+  for (int i = threadIdx.x; i < nb; i += 256) s_hist[i] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const uint64_t k = keys[i];
+    int a = 0;
+    if (bits) {
+      a = find_prefix(s_act, A, k >> (64 - bits));
+      if (a < 0) continue;
+    }
+    const uint32_t d = (uint32_t)((k << bits) >> (64 - D));
+    atomicAdd(&s_hist[(a << D) | (int)d], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += 256)
+    if (s_hist[i]) atomicAdd(&hist[i], s_hist[i]);
+}
+
+// The keys whose top `bits` bits are one of the A prefixes -> out[*cursor ...].
+__global__ void __launch_bounds__(kGatherThreads)
+select_compact(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __restrict__ active,
+               int A, int bits, uint64_t* __restrict__ out, unsigned long long* __restrict__ cursor) {
+  extern __shared__ uint64_t sel_lds[];
+  __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
+  __shared__ unsigned long long s_base;
+  for (int i = threadIdx.x; i < A; i += kGatherThreads) sel_lds[i] = active[i];
+  __syncthreads();
+  StepPlacer pl{s_cnt, &s_base};
+  for (int64_t i0 = (int64_t)blockIdx.x * kGatherStep; i0 < n; i0 += (int64_t)gridDim.x * kGatherStep) {
+    bool keep[kGatherRounds];
+    uint64_t v[kGatherRounds];
+#pragma unroll
+    for (int r = 0; r < kGatherRounds; ++r) {
+      const int64_t i = i0 + (int64_t)r * kGatherThreads + threadIdx.x;
+      v[r] = i < n ? keys[i] : 0ULL;
+      keep[r] = i < n && find_prefix(sel_lds, A, v[r] >> (64 - bits)) >= 0;
+    }
+    pl.place(keep, v, out, cursor);
+  }
+}
+
+// out[j] = from_ordered(keys[idx[j]])
+__global__ void select_pick(const uint64_t* __restrict__ keys, const int64_t* __restrict__ idx,
+                            int64_t m, double* __restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const int64_t r = n > 1 ? (int64_t)(((__int128)j * (count - 1)) / (n - 1)) : 0;
-  out[j] = sorted[r];
+  if (j < m) out[j] = from_ordered(keys[idx[j]]);
+}
+
+// out[j] = from_ordered(sorted[j])
+__global__ void keys_to_doubles(const uint64_t* __restrict__ sorted, int64_t n, double* __restrict__ out) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+    out[j] = from_ordered(sorted[j]);
+}
+
+unsigned grid_of(int64_t n, int64_t per_block, int64_t cap) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + per_block - 1) / per_block, cap));
+}
+
+hipError_t sort_keys(const uint64_t* in, uint64_t* out, size_t n, DevBuf<uint8_t>& tmp,
+                     hipStream_t stream) {
+  size_t tmp_bytes = 0;
+  hipError_t e = rocprim::radix_sort_keys(nullptr, tmp_bytes, in, out, n, 0, 64, stream);
+  if (e != hipSuccess) return e;
+  e = tmp.ensure(std::max<size_t>(tmp_bytes, 16));
+  if (e != hipSuccess) return e;
+  return rocprim::radix_sort_keys(tmp.p, tmp_bytes, in, out, n, 0, 64, stream);
+}
+
+// The values at the exact ranks rank[0..m) (ascending) of the n keys at `keys`, into out_dev[m]
+// (doubles).  Histogram passes narrow every rank to a bin of the keys' top bits; once the bins
+// that hold a rank hold few keys (or every bit is decided) those keys are compacted and sorted.
+dq_status radix_select(uint64_t* keys, int64_t n, const std::vector<int64_t>& rank, double* out_dev,
+                       hipStream_t stream) {
+  const int m = (int)rank.size();
+  // keys sorted at the end: always when this few; and up to kStallBudget when a pass stopped
+  // narrowing (a bin of one repeated value -- integers of a narrow range -- never shrinks: more
+  // passes over it only spend bits)
+  constexpr int64_t kSortBudget = 1 << 24, kStallBudget = 1 << 26;
+  int64_t T_prev = n;
+  struct Target {
+    uint64_t prefix;
+    int64_t q;  // rank among the keys with this prefix
+  };
+  std::vector<Target> tg(m);
+  for (int j = 0; j < m; ++j) tg[j] = Target{0, rank[j]};
+  DevBuf<uint64_t> buf[2], act;
+  DevBuf<unsigned int> hist;
+  DevBuf<unsigned long long> cur;
+  DevBuf<uint8_t> tmp;
+  DevBuf<int64_t> didx;
+  HIP_TRY(cur.ensure(1));
+  const uint64_t* src = keys;
+  int64_t M = n;
+  int which = 0;
+  int bits = 0;
+  std::vector<uint64_t> prefixes, sp;  // (alive until the copies from them have run)
+  std::vector<unsigned int> h;
+  while (true) {
+    prefixes.clear();
+    for (const Target& t : tg) prefixes.push_back(t.prefix);
+    std::sort(prefixes.begin(), prefixes.end());
+    prefixes.erase(std::unique(prefixes.begin(), prefixes.end()), prefixes.end());
+    const int A = (int)prefixes.size();
+    int D = 1;
+    while (D < 64 - bits && ((int64_t)A << (D + 1)) <= kSelBins) ++D;
+    const int nb = A << D;
+    HIP_TRY(act.ensure(A));
+    HIP_TRY(hipMemcpyAsync(act.p, prefixes.data(), A * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hist.ensure(nb));
+    HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)nb * 4, stream));
+    const size_t lds = (size_t)A * 8 + (size_t)nb * 4;
+    // (a few blocks per CU: each flushes up to kSelBins counters)
+    hipLaunchKernelGGL(select_hist, dim3(grid_of(M, 256 * 64, 512)), dim3(256), lds, stream, src,
+                       M, act.p, A, bits, D, hist.p);
+    HIP_TRY(hipGetLastError());
+    h.resize(nb);
+    HIP_TRY(hipMemcpyAsync(h.data(), hist.p, (size_t)nb * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    // every target: the bin of its prefix that holds its rank
+    for (Target& t : tg) {
+      const int a = (int)(std::lower_bound(prefixes.begin(), prefixes.end(), t.prefix) - prefixes.begin());
+      int64_t below = 0;
+      int d = 0;
+      for (; d < (1 << D); ++d) {
+        const int64_t c = h[((size_t)a << D) | d];
+        if (t.q < below + c) break;
+        below += c;
+      }
+      if (d == (1 << D)) return fail(DQ_ERR_STATE, "radix select lost a rank (counts changed under it)");
+      t.prefix = (t.prefix << D) | (uint64_t)d;
+      t.q -= below;
+    }
+    const int nbits = bits + D;
+    // the bins that now hold a rank, and the keys in them
+    std::vector<std::pair<uint64_t, int64_t>> sel;  // (prefix, keys), ascending
+    for (const Target& t : tg) sel.push_back({t.prefix, 0});
+    std::sort(sel.begin(), sel.end());
+    sel.erase(std::unique(sel.begin(), sel.end()), sel.end());
+    int64_t T = 0;
+    for (auto& s : sel) {
+      const uint64_t parent = s.first >> D;  // (0, the only prefix, on the first pass)
+      const int a = (int)(std::lower_bound(prefixes.begin(), prefixes.end(), parent) - prefixes.begin());
+      s.second = h[((size_t)a << D) | (s.first & ((1ULL << D) - 1))];
+      T += s.second;
+    }
+    bits = nbits;
+    if (bits == 64) {  // every bit decided: the prefix IS the key
+      std::vector<double> v(m);
+      for (int j = 0; j < m; ++j) v[j] = from_ordered(tg[j].prefix);
+      HIP_TRY(hipMemcpyAsync(out_dev, v.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
+      return DQ_OK;
+    }
+    const bool finish = T <= kSortBudget || (T <= kStallBudget && 2 * T > T_prev);
+    T_prev = T;
+    if (!finish && T > M / 2) continue;  // narrowing did not pay for a copy yet
+    // compact the selected bins' keys (into the buffer src is not)
+    sp.resize(sel.size());
+    for (size_t i = 0; i < sel.size(); ++i) sp[i] = sel[i].first;
+    const int S = (int)sp.size();
+    HIP_TRY(act.ensure(S));
+    HIP_TRY(hipMemcpyAsync(act.p, sp.data(), (size_t)S * 8, hipMemcpyHostToDevice, stream));
+    DevBuf<uint64_t>& dst = buf[which];
+    HIP_TRY(dst.ensure((size_t)std::max<int64_t>(T, 1)));
+    HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
+    hipLaunchKernelGGL(select_compact, dim3(grid_of(M, kGatherStep, 2048)), dim3(kGatherThreads),
+                       (size_t)S * 8, stream, src, M, act.p, S, bits, dst.p, cur.p);
+    HIP_TRY(hipGetLastError());
+    src = dst.p;
+    M = T;
+    which ^= 1;
+    if (!finish) continue;
+    // sort the compacted keys; a target's key sits at (keys of the bins before its own) + q
+    DevBuf<uint64_t>& sorted = buf[which];
+    HIP_TRY(sorted.ensure((size_t)std::max<int64_t>(T, 1)));
+    HIP_TRY(sort_keys(src, sorted.p, (size_t)T, tmp, stream));
+    std::vector<int64_t> idx(m);
+    for (int j = 0; j < m; ++j) {
+      int64_t before = 0;
+      for (const auto& s : sel) {
+        if (s.first == tg[j].prefix) break;
+        before += s.second;
+      }
+      idx[j] = before + tg[j].q;
+    }
+    HIP_TRY(didx.ensure(m));
+    HIP_TRY(hipMemcpyAsync(didx.p, idx.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream));
+    hipLaunchKernelGGL(select_pick, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
+                       sorted.p, didx.p, (int64_t)m, out_dev);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(stream));  // the host vectors above die here
+    return DQ_OK;
+  }
 }
 
 }  // namespace
 
 extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int n_batches,
                                       int64_t head_values, int64_t max_values, double* out,
-                                      int64_t* n_out,
-                                      int64_t* count_out, void* hip_stream) {
+                                      int64_t* n_out, int64_t* count_out, void* hip_stream) {
   if (!n_out || !count_out || (n_batches > 0 && !batches) || n_batches < 0 || max_values < 2 ||
       head_values < 0)
     return fail(DQ_ERR_INVALID_ARGUMENT, "bad argument to dq_sorted_sample");
@@ -113,45 +350,55 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   *count_out = 0;
   if (rows == 0) return DQ_OK;
   // through the engine's device cache (dev_alloc): reused across columns, released on OOM
-  DevBuf<double> keys, sorted, picks;
+  DevBuf<uint64_t> keys, sorted;
+  DevBuf<double> picks;
   DevBuf<unsigned long long> cur;
   DevBuf<uint8_t> tmp;
   HIP_TRY(keys.ensure((size_t)rows));
-  HIP_TRY(sorted.ensure((size_t)rows));
   HIP_TRY(cur.ensure(1));
   HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
-  double* kp = keys.p;
-  unsigned long long* cp = cur.p;
   for (int b = 0; b < n_batches; ++b) {
     const dq_column& c = batches[b];
     if (!c.length) continue;
-    const int64_t step = (int64_t)kGatherRounds * kGatherThreads;
-    const int64_t blocks = std::min<int64_t>((c.length + step - 1) / step, 2048);
-    hipLaunchKernelGGL(quantile_gather, dim3((unsigned)blocks), dim3(kGatherThreads), 0, stream,
-                       c.type, c.validity, c.values, c.length, kp, cp);
+    hipLaunchKernelGGL(quantile_gather, dim3(grid_of(c.length, kGatherStep, 2048)),
+                       dim3(kGatherThreads), 0, stream, c.type, c.validity, c.values, c.length,
+                       keys.p, cur.p);
     HIP_TRY(hipGetLastError());
   }
   unsigned long long count = 0;
-  HIP_TRY(hipMemcpyAsync(&count, cp, 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipMemcpyAsync(&count, cur.p, 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   *count_out = (int64_t)count;
   if (!count) return DQ_OK;
-  size_t tmp_bytes = 0;
-  HIP_TRY(rocprim::radix_sort_keys(nullptr, tmp_bytes, kp, sorted.p, (size_t)count, 0, 64, stream));
-  HIP_TRY(tmp.ensure(std::max<size_t>(tmp_bytes, 16)));
-  HIP_TRY(rocprim::radix_sort_keys(tmp.p, tmp_bytes, kp, sorted.p, (size_t)count, 0, 64, stream));
   const int64_t n = (int64_t)count <= std::max(head_values, max_values) ? (int64_t)count : max_values;
   *n_out = n;
   if (!out) return DQ_OK;  // size query only
-  if (n == (int64_t)count) {
-    HIP_TRY(hipMemcpyAsync(out, sorted.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
-  } else {
-    HIP_TRY(picks.ensure((size_t)n));
-    hipLaunchKernelGGL(quantile_pick, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                       sorted.p, (int64_t)count, n, picks.p);
+  HIP_TRY(picks.ensure((size_t)n));
+  if (n == (int64_t)count) {  // every value, sorted
+    HIP_TRY(sorted.ensure((size_t)count));
+    HIP_TRY(sort_keys(keys.p, sorted.p, (size_t)count, tmp, stream));
+    hipLaunchKernelGGL(keys_to_doubles, dim3(grid_of(n, 256 * 16, 4096)), dim3(256), 0, stream,
+                       sorted.p, n, picks.p);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
+  } else {  // the values at the ranks floor(j (count - 1) / (n - 1))
+    std::vector<int64_t> rank(n);
+    for (int64_t j = 0; j < n; ++j) rank[j] = (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1));
+    if (n <= kSelMaxTargets) {
+      const dq_status st = radix_select(keys.p, (int64_t)count, rank, picks.p, stream);
+      if (st != DQ_OK) return st;
+    } else {  // many ranks: one sort, then the picks
+      HIP_TRY(sorted.ensure((size_t)count));
+      HIP_TRY(sort_keys(keys.p, sorted.p, (size_t)count, tmp, stream));
+      DevBuf<int64_t> didx;
+      HIP_TRY(didx.ensure((size_t)n));
+      HIP_TRY(hipMemcpyAsync(didx.p, rank.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream));
+      hipLaunchKernelGGL(select_pick, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                         sorted.p, didx.p, n, picks.p);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipStreamSynchronize(stream));  // rank dies here
+    }
   }
+  HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   return DQ_OK;
 }

@@ -458,3 +458,35 @@ def test_small_key_phase_a_on_unaligned_and_sliced_batches(gpu_device):
         ft.add([b["s"]])
     ot = O.OTable({"s": vals[8:n - 5]}, {"s": "string"})
     assert dict(ft.export()) == O.frequencies(ot, ["s"])
+
+
+def test_small_key_batch_table_overflow(gpu_device):
+    """freq_phaseA_small merges the workgroups' groups in a 64-slot device table per batch; keys
+    beyond its capacity stay in the workgroups' own records (and the last workgroup to arrive writes
+    the table's).  Rows draw from 5 keys of a window that moves every 30720 rows (one workgroup's
+    range), so every wave stays within its 8 candidates while the batch holds ~170 distinct keys.
+    Bar: frequencies and Histogram equal the oracle's."""
+    from deequ_amd.analyzers import Histogram
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.runners import AnalysisRunner
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    rng = np.random.default_rng(17)
+    n = 1 << 20
+    region = np.arange(n) // 30720
+    pick = region * 5 + rng.integers(0, 5, n)
+    vals = [None if rng.random() < 0.02 else f"k{p:03d}" for p in pick.tolist()]
+    t = pa.table({"s": pa.array(vals, pa.string())})
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=1 << 19)
+    ft = FrequencyTable(["s"], [df.schema["s"].dtype], 0, capacity_hint=n)
+    for b in df.batches:
+        ft.add([b["s"]])
+    ot = O.OTable({"s": vals}, {"s": "string"})
+    freq = O.frequencies(ot, ["s"])
+    assert len(freq) > 64
+    assert dict(ft.export()) == freq
+    ctx = AnalysisRunner.do_analysis_run(df, [Histogram("s")])
+    hist, _ = O.histogram(ot, "s")
+    dist = ctx.metric(Histogram("s")).value.get()
+    assert dist.number_of_bins == len(hist)
+    assert {k: v.absolute for k, v in dist.values.items()} == hist

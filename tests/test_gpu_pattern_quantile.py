@@ -210,3 +210,52 @@ def test_pattern_match_library_patterns_on_long_rows(name, gpu_device):
     st = PatternMatch("s", pattern).compute_state_from(df)
     hits, cnt = agg_pattern_match(ot, "s", pattern, None)
     assert (st.num_matches, st.count) == (hits, cnt), name
+
+
+def _ordered(x: np.ndarray) -> np.ndarray:
+    """Java's Double.compare order as unsigned order (canonical NaN largest, -0.0 < 0.0)."""
+    x = np.where(np.isnan(x), np.float64("nan"), x)
+    b = x.view(np.uint64)
+    return np.where(b >> np.uint64(63), ~b, b | np.uint64(1 << 63))
+
+
+@pytest.mark.parametrize("dist", ["uniform", "exponential_ints", "constant", "specials", "two_values"])
+@pytest.mark.parametrize("m", [2, 201, 2001, 2500])
+def test_sorted_sample_exact_ranks_by_radix_select(dist, m, gpu_device):
+    """dq_sorted_sample's picks (radix select for m <= 2048 ranks, one sort beyond) are the values
+    at the exact ranks floor(j (n - 1) / (m - 1)) of the non-NULL values in Double.compare order, for
+    spread doubles, integers crowded into a few exponents (numViews-like: every histogram pass
+    narrows a little), a constant column (every bit decided before the bins shrink), special values
+    (NaN payloads, +-0.0, +-Infinity) and two values.  Bar: bit-exact."""
+    import ctypes
+    import torch
+    from deequ_amd import _native as N
+    rng = np.random.default_rng(len(dist) * 31 + m)
+    n = 700_001
+    if dist == "uniform":
+        x = rng.random(n) * 2e6 - 1e6
+    elif dist == "exponential_ints":
+        x = np.floor(rng.exponential(1000.0, n)) * np.where(rng.random(n) < 0.01, -1, 1)
+    elif dist == "constant":
+        x = np.full(n, 42.5)
+    elif dist == "specials":
+        x = rng.choice(np.array([np.nan, -0.0, 0.0, np.inf, -np.inf, 1.5, -1.5]), n)
+        x[:3] = np.frombuffer(np.array([0x7ff0000000000001, 0xfff8000000000000, 0x7ff8000000000abc],
+                                       np.uint64).tobytes(), np.float64)
+    else:
+        x = np.where(rng.random(n) < 0.3, -7.0, 9.0)
+    valid = rng.random(n) > 0.05
+    t = pa.table({"x": pa.array(x, mask=~valid, type=pa.float64())})
+    df = _df({"x": t.column("x")}, gpu_device, 1 << 18)
+    cols = [b["x"] for b in df.batches]
+    arr = (N.dq_column * len(cols))(*[c.to_c() for c in cols])
+    out = np.zeros(m, np.float64)
+    n_out, count = ctypes.c_int64(), ctypes.c_int64()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(df.device_index()).cuda_stream)
+    N.check(N.lib.dq_sorted_sample(df.device_index(), arr, len(cols), 0, m, out.ctypes.data,
+                                   ctypes.byref(n_out), ctypes.byref(count), stream))
+    keys = np.sort(_ordered(x[valid]))
+    cnt = len(keys)
+    assert count.value == cnt and n_out.value == m
+    ranks = [(j * (cnt - 1)) // (m - 1) for j in range(m)]
+    assert _ordered(out).tolist() == keys[ranks].tolist(), dist
