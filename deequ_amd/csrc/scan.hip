@@ -434,10 +434,18 @@ DQ_DEV void str_in_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& 
         SmallList sl;
         sl.load(t);
         uint64_t v[16];
+#if DQ_STRIN_CONTIG  // diagnostic build only (wrong matches): the same bytes as compact loads
+        {
+          const uint8_t* base = t.data + __shfl(o[0][0], 0);  // the step's first byte
+#pragma unroll
+          for (int i = 0; i < 16; ++i) v[i] = ldg64_unaligned(base + 4 * (64 * i + l));
+        }
+#else
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[4 * g + j] = ldg64_unaligned(t.data + o[g][j]);
+#endif
         __builtin_amdgcn_sched_barrier(0);
         cur.load(t, off, rn, l);
         __builtin_amdgcn_sched_barrier(0);
