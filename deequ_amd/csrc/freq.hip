@@ -247,6 +247,8 @@ struct AArgs {
   // the batch's groups merged across workgroups (freq_phaseA_small): kBatchSlots keys (+1, 0 =
   // free), their counts, then the workgroups' arrival counter; zeroed before the launch
   unsigned long long* batch_tab;
+  // freq_phaseA_small: general-kernel workgroups (tile ranges + chunk) per small-kernel workgroup
+  int32_t small_merge;
 };
 
 // Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
@@ -816,6 +818,10 @@ constexpr int kSmallCand = 8;
 constexpr int kSmallThreads = 256;
 constexpr int kBatchSlots = 64;
 constexpr int kBatchTabWords = 2 * kBatchSlots + 1;
+// one table per XCD class of workgroups (blockIdx % 8): 8x less contention on its slots and its
+// arrival counter (2000+ workgroups adding into one table serialised the kernel's tail), 8 records
+// per group per batch instead of one
+constexpr int kBatchTabs = 8;
 constexpr uint64_t kLongKey = ~0ULL;
 // an unused candidate: length byte 0xFE, which neither a short key (<= 7) nor kLongKey (0xFF) has,
 // so a long string never matches a free slot and is always seen as a miss
@@ -870,9 +876,17 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   const KeyCol& c = a.ks.cols[0];
   const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
   const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
-  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
-  const int64_t t1 = min(t0 + (int64_t)a.tiles_per_wg, n_tiles);
+  // this workgroup stands for the general kernel's workgroups [v0, v1): their tiles, and their
+  // chunks n_tiles + v -- the first holds this workgroup's records, the others stay empty (fewer,
+  // longer workgroups: the per-workgroup tail -- merge, table adds, records -- amortised)
+  const int64_t n_vwg = (n_tiles + a.tiles_per_wg - 1) / a.tiles_per_wg;
+  const int64_t v0 = (int64_t)blockIdx.x * a.small_merge;
+  const int64_t v1 = min(v0 + (int64_t)a.small_merge, n_vwg);
+  const int64_t t0 = v0 * a.tiles_per_wg;
+  const int64_t t1 = min(v1 * (int64_t)a.tiles_per_wg, n_tiles);
   for (int64_t i = t0 * kHistRow + tid; i < t1 * kHistRow; i += kSmallThreads) a.hist[i] = 0;
+  for (int64_t i = (n_tiles + v0 + 1) * kHistRow + tid; i < (n_tiles + v1) * kHistRow; i += kSmallThreads)
+    a.hist[i] = 0;
   const int64_t r_begin = t0 * a.tile_items, r_end = min(t1 * a.tile_items, a.n_items);
   const int32_t dlen = off[a.n_items];
 
@@ -1033,11 +1047,15 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   if (lane == 0 && nulls)
     atomicAdd(&a.fast_words[a.ks.null_as_group ? 2 : 1], nulls);
   __syncthreads();
-  // thread 0: the waves' lists merged (<= NW * kSmallCand groups), then added into the batch's
-  // device table (a batch of a 3-value column then leaves 3 records, not 3 per workgroup: phase C
-  // would otherwise count ~2000 records of one key per partition, a serial chain of LDS atomics
-  // on one slot); a group the full table cannot take stays in this workgroup's own records.  The
-  // last workgroup to arrive writes the table's groups as its records too.
+  // The waves' lists merged (<= NW * kSmallCand groups, thread 0, LDS only), then added into the
+  // batch's device table, one thread per group (a batch of a 3-value column then leaves 3 records,
+  // not 3 per workgroup: phase C would otherwise count ~2000 records of one key per partition, a
+  // serial chain of LDS atomics on one slot); a group the full table cannot take stays in this
+  // workgroup's own records.  The last workgroup to arrive writes the table's groups as its
+  // records too.
+  __shared__ uint32_t s_ng0, s_last;
+  __shared__ uint32_t s_placed[NW * kSmallCand];
+  __shared__ uint64_t s_tkey[kBatchSlots], s_tcnt[kBatchSlots];
   if (tid == 0) {
     uint32_t ng = 0;
     for (int w = 0; w < NW; ++w)
@@ -1052,40 +1070,55 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
         }
         g_cnt[g] += ct;
       }
-    unsigned long long* tkeys = a.batch_tab;
-    unsigned long long* tcnts = a.batch_tab + kBatchSlots;
-    uint32_t kept = 0;  // groups the table did not take, compacted to the front
-    for (uint32_t g = 0; g < ng; ++g) {
-      const unsigned long long tag = (unsigned long long)g_key[g] + 1ULL;  // never 0
-      uint32_t slot = (uint32_t)(fmix_bij(g_key[g]) & (kBatchSlots - 1));
-      bool placed = false;
-      for (int probe = 0; probe < kBatchSlots && !placed; ++probe, slot = (slot + 1) & (kBatchSlots - 1)) {
-        const unsigned long long prev = atomicCAS(&tkeys[slot], 0ULL, tag);
-        if (prev == 0ULL || prev == tag) {
-          atomicAdd(&tcnts[slot], (unsigned long long)g_cnt[g]);
-          placed = true;
-        }
+    s_ng0 = ng;
+  }
+  __syncthreads();
+  const int tab = (int)(blockIdx.x % kBatchTabs);
+  unsigned long long* tkeys = a.batch_tab + (size_t)tab * kBatchTabWords;
+  unsigned long long* tcnts = tkeys + kBatchSlots;
+  if (tid < (int)s_ng0) {  // group tid into the table (CAS on its key, then add its count)
+    const unsigned long long tag = (unsigned long long)g_key[tid] + 1ULL;  // never 0
+    uint32_t slot = (uint32_t)(fmix_bij(g_key[tid]) & (kBatchSlots - 1));
+    uint32_t placed = 0;
+    for (int probe = 0; probe < kBatchSlots && !placed; ++probe, slot = (slot + 1) & (kBatchSlots - 1)) {
+      const unsigned long long prev = atomicCAS(&tkeys[slot], 0ULL, tag);
+      if (prev == 0ULL || prev == tag) {
+        atomicAdd(&tcnts[slot], (unsigned long long)g_cnt[tid]);
+        placed = 1;
       }
-      if (!placed) {
+    }
+    s_placed[tid] = placed;
+    __threadfence();  // this thread's adds complete before the workgroup arrives
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned long long arrived = atomicAdd(&tkeys[2 * kBatchSlots], 1ULL);
+    const unsigned int members = (gridDim.x - (unsigned)tab + kBatchTabs - 1) / kBatchTabs;
+    s_last = arrived == (unsigned long long)members - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  const bool last = s_last != 0;
+  if (last && tid < kBatchSlots) {  // every workgroup's adds are in: read the table
+    __threadfence();
+    s_tkey[tid] = __hip_atomic_load(&tkeys[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tcnt[tid] = __hip_atomic_load(&tcnts[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t ng0 = s_ng0;
+    uint32_t kept = 0;  // groups the table did not take, compacted to the front
+    for (uint32_t g = 0; g < ng0; ++g)
+      if (!s_placed[g]) {
         g_key[kept] = g_key[g];
         g_cnt[kept++] = g_cnt[g];
       }
-    }
-    __threadfence();
-    const unsigned long long arrived =
-        atomicAdd(&a.batch_tab[2 * kBatchSlots], 1ULL);  // after this workgroup's adds
-    const bool last = arrived == (unsigned long long)gridDim.x - 1;
-    if (last) {  // every workgroup's adds are in: the table's groups join this one's records
-      __threadfence();
+    if (last)  // the table's groups join this workgroup's records
       for (int slot = 0; slot < kBatchSlots; ++slot) {
-        const unsigned long long tag =
-            __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!tag) continue;
-        g_key[kept] = tag - 1ULL;
-        g_cnt[kept++] = __hip_atomic_load(&tcnts[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!s_tkey[slot]) continue;
+        g_key[kept] = s_tkey[slot] - 1ULL;
+        g_cnt[kept++] = s_tcnt[slot];
       }
-    }
-    ng = kept;
+    uint32_t ng = kept;
     uint64_t bytes = 0;
     for (uint32_t g = 0; g < ng; ++g) bytes += 8 + pad4((uint32_t)(g_key[g] >> 56));
     uint64_t at = bytes ? atomicAdd(a.arena_cursor, (unsigned long long)bytes) : 0ULL;
@@ -1110,7 +1143,7 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   // the workgroup's chunk: records bucket-sorted (groups of one bucket in group order), its
   // histogram row the exclusive prefix of the records per bucket
   const uint32_t ng = s_ng;
-  const int64_t fchunk = n_tiles + blockIdx.x;
+  const int64_t fchunk = n_tiles + v0;
   uint16_t* hrow = a.hist + fchunk * kHistRow;
   for (int b = tid; b <= kBuckets; b += kSmallThreads) {
     uint32_t before = 0;
@@ -2440,8 +2473,8 @@ static dq_status launch_phaseA_small(dq_freq* f, AArgs& a) {
   phaseA_chunks(true, false, a.n_items, a.tile_items, &n_wg);
   a.tiles_per_wg = AKeys<true, false>::kTilesPerWg;
   a.fast_words = f->dev_words.p + C_N + 1;
-  HIP_TRY(f->batch_tab.ensure(kBatchTabWords));
-  HIP_TRY(hipMemsetAsync(f->batch_tab.p, 0, kBatchTabWords * 8, f->stream));
+  HIP_TRY(f->batch_tab.ensure(kBatchTabs * kBatchTabWords));
+  HIP_TRY(hipMemsetAsync(f->batch_tab.p, 0, kBatchTabs * kBatchTabWords * 8, f->stream));
   a.batch_tab = f->batch_tab.p;
   a.fast_epoch = ++f->fast_epoch;
   const KeyCol& c = a.ks.cols[0];
@@ -2452,7 +2485,17 @@ static dq_status launch_phaseA_small(dq_freq* f, AArgs& a) {
   a.fast_poll = poll;
   a.vec_ok = (reinterpret_cast<uintptr_t>(c.values) & 15u) == 0 &&
              (reinterpret_cast<uintptr_t>(c.valid) & 3u) == 0;
-  hipLaunchKernelGGL(freq_phaseA_small, dim3((unsigned)n_wg), dim3(kSmallThreads), 0, f->stream, a);
+  static const int cus = [] {
+    int n = 0, d = 0;
+    (void)hipGetDevice(&d);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0 ? n : 256;
+  }();
+  // about three workgroups per CU (the kernel's occupancy), each standing for several of the
+  // general kernel's
+  const int64_t slots = 3LL * cus;
+  a.small_merge = (int32_t)std::max<int64_t>(1, (n_wg + slots - 1) / slots);
+  const int64_t grid = (n_wg + a.small_merge - 1) / a.small_merge;
+  hipLaunchKernelGGL(freq_phaseA_small, dim3((unsigned)grid), dim3(kSmallThreads), 0, f->stream, a);
   HIP_TRY(hipGetLastError());
   return DQ_OK;
 }
@@ -3173,7 +3216,7 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     // + what a small-key attempt that gives the batch up may have reserved
     int64_t n_wg_a = 0;
     phaseA_chunks(true, false, rows, f->tile, &n_wg_a);
-    bound += (uint64_t)n_wg_a * (kSmallThreads / 64) * kSmallCand * 16 + kBatchSlots * 16;
+    bound += (uint64_t)n_wg_a * (kSmallThreads / 64) * kSmallCand * 16 + kBatchTabs * kBatchSlots * 16;
     if (f->arena.n < f->arena_hi + bound + 64) {  // may not fit: learn the true use, then grow
       dq_status cs = pull_counters(f);
       if (cs != DQ_OK) return cs;
