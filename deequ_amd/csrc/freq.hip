@@ -1710,7 +1710,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
         if constexpr (HASHED) {
           const uint64_t prev = atomicCAS((unsigned long long*)spec_rep, kNotReady, rep);
           if (prev != kNotReady && prev != rep &&
-              !enc_equal(reinterpret_cast<const uint32_t*>(a.arena + prev),
+              !enc_equal_arena(reinterpret_cast<const uint32_t*>(a.arena + prev),
                          reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys))
             ++collisions;
         }
@@ -1735,7 +1735,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
             const uint64_t r2 = lds_load(&trep[slot]);
             if (r2 == kNotReady) return false;
             if (r2 != rep)
-              same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
+              same = enc_equal_arena(reinterpret_cast<const uint32_t*>(a.arena + r2),
                                reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
             if (!same) ++collisions;  // two keys on one 64-bit hash: kept as two groups
           }
@@ -2920,7 +2920,7 @@ DQ_DEV uint64_t lookup_count(const Lookup& L, const uint32_t* part) {
     if (m.h != h) continue;
     if (L.exact) return m.count;
     const int32_t ty = DQ_UTF8;
-    if (enc_equal(reinterpret_cast<const uint32_t*>(L.arena + m.rep), part, &ty, 1)) return m.count;
+    if (enc_equal_arena(reinterpret_cast<const uint32_t*>(L.arena + m.rep), part, &ty, 1)) return m.count;
   }
 }
 

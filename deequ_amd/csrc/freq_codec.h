@@ -448,6 +448,36 @@ DQ_HD bool enc_equal(const uint32_t* a, const uint32_t* b, const int32_t* types,
   return true;
 }
 
+// enc_equal for the device's arena (phase C's hash hits, MutualInformation's lookups): the same
+// answer with few dependent round trips.  The encoding is self-delimiting, so two keys are equal
+// iff the first enc_size(a) bytes of both are; the words of a 4-word chunk are loaded together
+// (one round trip per chunk, where enc_equal's early-exit loop took one per word).  The first
+// chunk is read unconditionally: every arena keeps >= 64 bytes past its last entry (grow_keep's
+// callers), so 16 bytes from any entry's start are mapped.
+__device__ inline bool enc_equal_arena(const uint32_t* a, const uint32_t* b, const int32_t* types,
+                                       int n_keys) {
+  uint32_t wa[4], wb[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    wa[k] = a[k];
+    wb[k] = b[k];
+  }
+  uint32_t n;  // words of a's encoding
+  if (n_keys == 1 && types[0] == DQ_UTF8) n = wa[0] ? 2 + pad4(wa[1]) / 4 : 1;
+  else n = enc_size(a, types, n_keys) / 4;
+  uint32_t x = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x |= (uint32_t)k < n ? wa[k] ^ wb[k] : 0u;
+  if (x) return false;
+  for (uint32_t q = 4; q < n; q += 4) {
+    x = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) x |= q + k < n ? a[q + k] ^ b[q + k] : 0u;
+    if (x) return false;
+  }
+  return true;
+}
+
 // Hash of an encoded key: the same value row_hash_hashed gives for the row it encodes.
 DQ_HD uint64_t enc_hash(const uint32_t* enc, const int32_t* types, int n_keys) {
   uint64_t h = 0x243F6A8885A308D3ULL;

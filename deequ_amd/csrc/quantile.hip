@@ -35,10 +35,6 @@ constexpr int64_t kGatherStep = (int64_t)kGatherRounds * kGatherThreads;
 
 static_assert(kGatherRounds * kGatherWaves == 64, "one wave scans the step's counts");
 
-constexpr int kSelBins = 8192;  // radix-select LDS counters per pass: 32 KB (+ 16 KB of prefixes)
-constexpr int kFirstD = 13;     // the first pass (in the gather): the keys' top 13 bits
-static_assert((1 << kFirstD) == kSelBins, "the gather's histogram is the select's first pass");
-
 // Double.compare order as unsigned order (the canonical NaN is the largest key)
 DQ_HD uint64_t ordered_key(double v) {
   const uint64_t b = __builtin_bit_cast(uint64_t, v);
@@ -90,20 +86,12 @@ struct StepPlacer {
   }
 };
 
-// Non-NULL values of one batch -> ordered keys at out[*cursor ...] (order irrelevant).  HIST: also
-// the radix select's first pass, the keys counted by their top kFirstD bits (hist[kSelBins]).
-template <bool HIST>
+// Non-NULL values of one batch -> ordered keys at out[*cursor ...] (order irrelevant).
 __global__ void __launch_bounds__(kGatherThreads)
 quantile_gather(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
-                int64_t rows, uint64_t* __restrict__ out, unsigned long long* __restrict__ cursor,
-                unsigned int* __restrict__ hist) {
+                int64_t rows, uint64_t* __restrict__ out, unsigned long long* __restrict__ cursor) {
   __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
   __shared__ unsigned long long s_base;
-  __shared__ uint32_t s_hist[HIST ? kSelBins : 1];
-  if constexpr (HIST) {
-    for (int i = threadIdx.x; i < kSelBins; i += kGatherThreads) s_hist[i] = 0;
-    __syncthreads();
-  }
   StepPlacer pl{s_cnt, &s_base};
   for (int64_t r0 = (int64_t)blockIdx.x * kGatherStep; r0 < rows; r0 += (int64_t)gridDim.x * kGatherStep) {
     bool keep[kGatherRounds];
@@ -115,22 +103,19 @@ quantile_gather(int type, const uint8_t* __restrict__ valid, const void* __restr
       double d = keep[i] ? load_f64(type, values, r) : 0.0;
       if (d != d) d = __builtin_nan("");  // Double.compare: every NaN is the canonical one
       v[i] = ordered_key(d);
-      if constexpr (HIST)
-        if (keep[i]) atomicAdd(&s_hist[(uint32_t)(v[i] >> (64 - kFirstD))], 1u);
     }
     pl.place(keep, v, out, cursor);
-  }
-  if constexpr (HIST) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < kSelBins; i += kGatherThreads)
-      if (s_hist[i]) atomicAdd(&hist[i], s_hist[i]);
   }
 }
 
 // ---- radix select -----------------------------------------------------------------------------
 // A pass counts the keys whose top `bits` bits equal one of the A active prefixes (sorted, unique)
 // by their next D bits: hist[a << D | digit], A << D <= kSelBins, privatised in LDS per block.
+constexpr int kSelBins = 8192;  // 32 KB of LDS counters (+ 16 KB of prefixes at most)
 constexpr int kSelMaxTargets = 2048;
+// passes whose prefixes are at most kMapBits long find a key's prefix through a direct LDS map
+// (prefix -> active index, 16 KB) instead of a binary search over the prefixes
+constexpr int kMapBits = 13;
 
 DQ_DEV int find_prefix(const uint64_t* act, int A, uint64_t p) {
   int lo = 0, hi = A;  // first index with act[i] >= p
@@ -142,6 +127,14 @@ DQ_DEV int find_prefix(const uint64_t* act, int A, uint64_t p) {
   return lo < A && act[lo] == p ? lo : -1;
 }
 
+// The active index of every prefix of `bits` <= kMapBits bits (-1: not active), in LDS.
+DQ_DEV void build_prefix_map(const uint64_t* act, int A, int bits, int16_t* map) {
+  for (int i = threadIdx.x; i < (1 << bits); i += blockDim.x) map[i] = -1;
+  __syncthreads();
+  for (int i = threadIdx.x; i < A; i += blockDim.x) map[act[i]] = (int16_t)i;
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(256)
 select_hist(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __restrict__ active, int A,
             int bits, int D, unsigned int* __restrict__ hist) {
@@ -149,18 +142,33 @@ select_hist(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __rest
   uint64_t* s_act = sel_lds;                                            // A
   unsigned int* s_hist = reinterpret_cast<unsigned int*>(sel_lds + A);  // A << D
   const int nb = A << D;
+  int16_t* s_map = reinterpret_cast<int16_t*>(s_hist + nb);  // 1 << bits, when bits <= kMapBits
+  const bool mapped = bits > 0 && bits <= kMapBits;
   for (int i = threadIdx.x; i < A; i += 256) s_act[i] = active[i];
   for (int i = threadIdx.x; i < nb; i += 256) s_hist[i] = 0;
   __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const uint64_t k = keys[i];
-    int a = 0;
-    if (bits) {
-      a = find_prefix(s_act, A, k >> (64 - bits));
-      if (a < 0) continue;
+  if (mapped) build_prefix_map(s_act, A, bits, s_map);
+  // 8 keys per thread per step, all loads in flight before the first is counted
+  constexpr int kU = 8;
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 * kU; i0 < n; i0 += (int64_t)gridDim.x * 256 * kU) {
+    uint64_t kk[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t i = i0 + (int64_t)u * 256 + threadIdx.x;
+      kk[u] = i < n ? keys[i] : 0ULL;
     }
-    const uint32_t d = (uint32_t)((k << bits) >> (64 - D));
-    atomicAdd(&s_hist[(a << D) | (int)d], 1u);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (i0 + (int64_t)u * 256 + threadIdx.x >= n) continue;
+      const uint64_t k = kk[u];
+      int a = 0;
+      if (bits) {
+        a = mapped ? (int)s_map[k >> (64 - bits)] : find_prefix(s_act, A, k >> (64 - bits));
+        if (a < 0) continue;
+      }
+      const uint32_t d = (uint32_t)((k << bits) >> (64 - D));
+      atomicAdd(&s_hist[(a << D) | (int)d], 1u);
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nb; i += 256)
@@ -174,8 +182,11 @@ select_compact(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __r
   extern __shared__ uint64_t sel_lds[];
   __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
   __shared__ unsigned long long s_base;
+  int16_t* s_map = reinterpret_cast<int16_t*>(sel_lds + A);  // 1 << bits, when bits <= kMapBits
+  const bool mapped = bits <= kMapBits;
   for (int i = threadIdx.x; i < A; i += kGatherThreads) sel_lds[i] = active[i];
   __syncthreads();
+  if (mapped) build_prefix_map(sel_lds, A, bits, s_map);
   StepPlacer pl{s_cnt, &s_base};
   for (int64_t i0 = (int64_t)blockIdx.x * kGatherStep; i0 < n; i0 += (int64_t)gridDim.x * kGatherStep) {
     bool keep[kGatherRounds];
@@ -184,7 +195,8 @@ select_compact(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __r
     for (int r = 0; r < kGatherRounds; ++r) {
       const int64_t i = i0 + (int64_t)r * kGatherThreads + threadIdx.x;
       v[r] = i < n ? keys[i] : 0ULL;
-      keep[r] = i < n && find_prefix(sel_lds, A, v[r] >> (64 - bits)) >= 0;
+      keep[r] = i < n && (mapped ? s_map[v[r] >> (64 - bits)] >= 0
+                                 : find_prefix(sel_lds, A, v[r] >> (64 - bits)) >= 0);
     }
     pl.place(keep, v, out, cursor);
   }
@@ -221,7 +233,7 @@ hipError_t sort_keys(const uint64_t* in, uint64_t* out, size_t n, DevBuf<uint8_t
 // (doubles).  Histogram passes narrow every rank to a bin of the keys' top bits; once the bins
 // that hold a rank hold few keys (or every bit is decided) those keys are compacted and sorted.
 dq_status radix_select(uint64_t* keys, int64_t n, const std::vector<int64_t>& rank, double* out_dev,
-                       const unsigned int* first_hist, hipStream_t stream) {
+                       hipStream_t stream) {
   const int m = (int)rank.size();
   // keys sorted at the end: always when this few; and up to kStallBudget when a pass stopped
   // narrowing (a bin of one repeated value -- integers of a narrow range -- never shrinks: more
@@ -257,20 +269,15 @@ dq_status radix_select(uint64_t* keys, int64_t n, const std::vector<int64_t>& ra
     const int nb = A << D;
     HIP_TRY(act.ensure(A));
     HIP_TRY(hipMemcpyAsync(act.p, prefixes.data(), A * 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hist.ensure(nb));
+    HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)nb * 4, stream));
+    const size_t lds = (size_t)A * 8 + (size_t)nb * 4 + (bits && bits <= kMapBits ? 2u << bits : 0u);
+    // (a few blocks per CU: each flushes up to kSelBins counters)
+    hipLaunchKernelGGL(select_hist, dim3(grid_of(M, 256 * 64, 1024)), dim3(256), lds, stream, src,
+                       M, act.p, A, bits, D, hist.p);
+    HIP_TRY(hipGetLastError());
     h.resize(nb);
-    if (bits == 0 && first_hist) {  // the gather counted the first pass
-      if (D != kFirstD) return fail(DQ_ERR_STATE, "radix select: first pass width");
-      HIP_TRY(hipMemcpyAsync(h.data(), first_hist, (size_t)nb * 4, hipMemcpyDeviceToHost, stream));
-    } else {
-      HIP_TRY(hist.ensure(nb));
-      HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)nb * 4, stream));
-      const size_t lds = (size_t)A * 8 + (size_t)nb * 4;
-      // (a few blocks per CU: each flushes up to kSelBins counters)
-      hipLaunchKernelGGL(select_hist, dim3(grid_of(M, 256 * 64, 512)), dim3(256), lds, stream, src,
-                         M, act.p, A, bits, D, hist.p);
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(h.data(), hist.p, (size_t)nb * 4, hipMemcpyDeviceToHost, stream));
-    }
+    HIP_TRY(hipMemcpyAsync(h.data(), hist.p, (size_t)nb * 4, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     // every target: the bin of its prefix that holds its rank
     for (Target& t : tg) {
@@ -320,7 +327,8 @@ dq_status radix_select(uint64_t* keys, int64_t n, const std::vector<int64_t>& ra
     HIP_TRY(dst.ensure((size_t)std::max<int64_t>(T, 1)));
     HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
     hipLaunchKernelGGL(select_compact, dim3(grid_of(M, kGatherStep, 2048)), dim3(kGatherThreads),
-                       (size_t)S * 8, stream, src, M, act.p, S, bits, dst.p, cur.p);
+                       (size_t)S * 8 + (bits <= kMapBits ? 2u << bits : 0u), stream, src, M, act.p, S,
+                       bits, dst.p, cur.p);
     HIP_TRY(hipGetLastError());
     src = dst.p;
     M = T;
@@ -380,24 +388,12 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   HIP_TRY(keys.ensure((size_t)rows));
   HIP_TRY(cur.ensure(1));
   HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
-  // more rows than values handed over whole: the gather also counts the select's first pass
-  const bool select_likely = rows > std::max(head_values, max_values) && max_values <= kSelMaxTargets;
-  DevBuf<unsigned int> first;
-  if (select_likely) {
-    HIP_TRY(first.ensure(kSelBins));
-    HIP_TRY(hipMemsetAsync(first.p, 0, kSelBins * 4, stream));
-  }
   for (int b = 0; b < n_batches; ++b) {
     const dq_column& c = batches[b];
     if (!c.length) continue;
-    if (select_likely)  // (a few blocks per CU: each flushes up to kSelBins counters)
-      hipLaunchKernelGGL(quantile_gather<true>, dim3(grid_of(c.length, kGatherStep, 512)),
-                         dim3(kGatherThreads), 0, stream, c.type, c.validity, c.values, c.length,
-                         keys.p, cur.p, first.p);
-    else
-      hipLaunchKernelGGL(quantile_gather<false>, dim3(grid_of(c.length, kGatherStep, 2048)),
-                         dim3(kGatherThreads), 0, stream, c.type, c.validity, c.values, c.length,
-                         keys.p, cur.p, nullptr);
+    hipLaunchKernelGGL(quantile_gather, dim3(grid_of(c.length, kGatherStep, 2048)),
+                       dim3(kGatherThreads), 0, stream, c.type, c.validity, c.values, c.length,
+                       keys.p, cur.p);
     HIP_TRY(hipGetLastError());
   }
   unsigned long long count = 0;
@@ -419,8 +415,7 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
     std::vector<int64_t> rank(n);
     for (int64_t j = 0; j < n; ++j) rank[j] = (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1));
     if (n <= kSelMaxTargets) {
-      const dq_status st = radix_select(keys.p, (int64_t)count, rank, picks.p,
-                                        select_likely ? first.p : nullptr, stream);
+      const dq_status st = radix_select(keys.p, (int64_t)count, rank, picks.p, stream);
       if (st != DQ_OK) return st;
     } else {  // many ranks: one sort, then the picks
       HIP_TRY(sorted.ensure((size_t)count));
