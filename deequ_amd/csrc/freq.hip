@@ -365,9 +365,31 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   auto arena_rep = [&](int64_t row) -> uint64_t {  // hashed rows: copy the key into the arena
     const uint32_t sz = STR1 ? str1_enc_size(a.ks, row) : row_enc_size(a.ks, row);
     const uint64_t off = s_arena_base + atomicAdd(&s_arena_cur, (unsigned long long)sz);
-    if constexpr (STR1) str1_encode(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
-    else row_encode(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
+    if constexpr (STR1) {
+      const SView v = str1_view(a.ks, row);
+      str1_encode_copy(v.p, v.len, reinterpret_cast<uint32_t*>(a.arena + off));
+    } else {
+      row_encode(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
+    }
     return off;
+  };
+  // one-column utf8: a key of at most 15 bytes is encoded from its short form in LDS (k1 !=
+  // kNoShort), with no global reads; a longer one through arena_rep
+  auto enc_size_sk = [&](int64_t row, uint64_t k1) -> uint32_t {
+    if constexpr (STR1)
+      if (k1 != kNoShort) return 8 + pad4(str1_short_len(k1));
+    return STR1 ? str1_enc_size(a.ks, row) : row_enc_size(a.ks, row);
+  };
+  auto arena_rep_sk = [&](int64_t row, uint64_t k0, uint64_t k1) -> uint64_t {
+    if constexpr (STR1) {
+      if (k1 != kNoShort) {
+        const uint64_t off = s_arena_base +
+            atomicAdd(&s_arena_cur, (unsigned long long)(8 + pad4(str1_short_len(k1))));
+        str1_encode_short(k0, k1, reinterpret_cast<uint32_t*>(a.arena + off));
+        return off;
+      }
+    }
+    return arena_rep(row);
   };
   // LDS dedupe: 0 = not counted (table full), 1 = claimed a new slot, 2 = added to an existing
   // slot, 3 = the key's slot is being claimed: retry after the next barrier
@@ -722,8 +744,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
 #pragma unroll 1
       for (int j = 0; j < ROUNDS; ++j)
         if ((raw >> j) & 1u) {
-          const int64_t row = (int64_t)stash[(j * kThreads + tid) * W + 1];
-          need += STR1 ? str1_enc_size(a.ks, row) : row_enc_size(a.ks, row);
+          const int q = j * kThreads + tid;
+          const int64_t row = (int64_t)stash[q * W + 1];
+          need += enc_size_sk(row, SK ? ssk1[q] : kNoShort);
         }
     }
     // 3. counting sort of the raw rows into the tile's chunk
@@ -760,7 +783,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         const int q = j * kThreads + tid;
         const uint64_t h = stash[q * W];
         uint64_t rep = HASHED ? stash[q * W + 1] : 0;
-        if constexpr (HASHED && !FROM_REC) rep = arena_rep((int64_t)rep);
+        if constexpr (HASHED && !FROM_REC)
+          rep = arena_rep_sk((int64_t)rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort);
         for_digits(FROM_REC ? scnt[tid] : 1, [&](uint32_t code) { put(t, h, code, rep); });
       }
     }
@@ -774,8 +798,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     if (k == kEmptyKey) continue;
     const uint32_t b = bucket_of(k);
     for_digits(dcnt[sl], [&](uint32_t) { atomicAdd(&bh[b], 1u); });
-    if constexpr (HASHED && !FROM_REC)
-      need += STR1 ? str1_enc_size(a.ks, (int64_t)drep[sl]) : row_enc_size(a.ks, (int64_t)drep[sl]);
+    if constexpr (HASHED && !FROM_REC) need += enc_size_sk((int64_t)drep[sl], SK ? dsk1[sl] : kNoShort);
   }
   const int64_t fchunk = n_tiles + blockIdx.x;
   begin_chunk(fchunk, need);
@@ -783,7 +806,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     const uint64_t k = dkey[sl];
     if (k == kEmptyKey) continue;
     uint64_t rep = HASHED ? drep[sl] : 0;
-    if constexpr (HASHED && !FROM_REC) rep = arena_rep((int64_t)rep);
+    if constexpr (HASHED && !FROM_REC)
+      rep = arena_rep_sk((int64_t)rep, SK ? dsk0[sl] : 0, SK ? dsk1[sl] : kNoShort);
     for_digits(dcnt[sl], [&](uint32_t code) { put(fchunk, k, code, rep); });
   }
   if (!FROM_REC) {

@@ -421,6 +421,42 @@ DQ_HD void str1_encode(const KeySet& ks, int64_t r, uint32_t* dst) {
     dst[2 + q / 4] = w;
   }
 }
+// str1_encode of a key whose short form (str_short_key_reg: bytes 0..7 in k0, bytes 8..14 and the
+// length in k1, zero past the end) is at hand: no reads.
+DQ_HD uint32_t str1_short_len(uint64_t k1) { return (uint32_t)(k1 >> 56); }
+DQ_HD void str1_encode_short(uint64_t k0, uint64_t k1, uint32_t* dst) {
+  const uint32_t len = str1_short_len(k1);
+  const uint32_t w[4] = {(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1,
+                         (uint32_t)(k1 >> 32) & 0xFFFFFFu};
+  dst[0] = 1;
+  dst[1] = len;
+  for (uint32_t q = 0; 4 * q < len; ++q) dst[2 + q] = w[q];
+}
+// str1_encode of the string p[0, len) from aligned dword loads, up to 9 in flight (every dword read
+// holds a byte of the string), instead of one dependent load per byte.
+__device__ inline void str1_encode_copy(const uint8_t* p, int32_t len, uint32_t* dst) {
+  dst[0] = 1;
+  dst[1] = (uint32_t)len;
+  const uintptr_t ad = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(ad & 3u) * 8u;
+  const int32_t nsrc = ((int32_t)(ad & 3u) + len + 3) >> 2;  // source dwords with string bytes
+  const int32_t nw = (len + 3) >> 2;
+  for (int32_t q0 = 0; q0 < nw; q0 += 8) {
+    uint32_t d[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) d[k] = q0 + k < nsrc ? src[q0 + k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int32_t q = q0 + k;
+      if (q >= nw) break;
+      uint32_t w = sh ? (d[k] >> sh) | (d[k + 1] << (32u - sh)) : d[k];
+      const int32_t nb = len - 4 * q;  // bytes of the string in this word
+      if (nb < 4) w &= (1u << (8 * nb)) - 1u;
+      dst[2 + q] = w;
+    }
+  }
+}
 // (out of line: only long strings get here, so one copy instead of one per call site)
 __host__ __device__ __attribute__((noinline)) bool str1_rows_equal(const KeySet& ks, int64_t r1,
                                                                    int64_t r2) {

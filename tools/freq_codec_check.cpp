@@ -142,6 +142,14 @@ static void check_table(const std::vector<HostCol>& cols, int64_t n, int null_as
           str_short_key_reg(w0, w1, v.len, a0, a1);
           str_short_key(v, b0, b1);
           CHECK(a0 == b0 && a1 == b1, "str_short_key_reg row %lld", (long long)r);
+          if (a1 != kNoShort) {  // phase A encodes a short key from its short form
+            std::vector<uint32_t> e(enc[r].size() + 1, 0xDEADBEEFu);
+            str1_encode_short(a0, a1, e.data());
+            CHECK(e.back() == 0xDEADBEEFu, "str1_encode_short wrote past the key (row %lld)",
+                  (long long)r);
+            e.pop_back();
+            CHECK(e == enc[r], "str1_encode_short != row_encode, row %lld", (long long)r);
+          }
         }
       }
     }
