@@ -807,8 +807,9 @@ static dq_status upload_host(dq_state* s) {
   if (!s->stream_set) {  // no stream yet: blocking copies (the first scan may use any stream)
     if (ab) HIP_TRY(hipMemcpy(s->d_acc.p, s->acc.data(), ab, hipMemcpyHostToDevice));
     if (hb) HIP_TRY(hipMemcpy(s->d_hll.p, s->hll.data(), hb, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(s->d_queue.p, 0, kQueueWords * sizeof(uint32_t)));
-    HIP_TRY(hipMemset(s->d_hll_stage.p, 0, s->d_hll_stage.n * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(s->d_queue.p, 0, kQueueWords * sizeof(uint32_t), nullptr));
+    HIP_TRY(hipMemsetAsync(s->d_hll_stage.p, 0, s->d_hll_stage.n * sizeof(uint32_t), nullptr));
+    HIP_TRY(hipStreamSynchronize(nullptr));  // the first scan may run on a non-blocking stream
     s->host_dirty = false;
     return DQ_OK;
   }

@@ -3158,7 +3158,9 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
   f->rb = f->exact ? FM<false>::kRB : FM<true>::kRB;
   HIP_TRY(hipSetDevice(device));
   HIP_TRY(f->dev_words.ensure(C_N + 4));  // counters, arena cursor, small-key words (3)
-  HIP_TRY(hipMemset(f->dev_words.p, 0, (C_N + 4) * 8));
+  // stream-ordered and waited for: the table's later work may run on a non-blocking stream
+  HIP_TRY(hipMemsetAsync(f->dev_words.p, 0, (C_N + 4) * 8, nullptr));
+  HIP_TRY(hipStreamSynchronize(nullptr));
   if (capacity_hint > 0) {  // the chunks phase A writes for that many rows (+ per-batch rounding)
     const int64_t chunks = phaseA_chunks(!f->exact, false, capacity_hint, f->tile, nullptr) +
                            2 * (capacity_hint >> 24) + 16;

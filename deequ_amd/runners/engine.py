@@ -76,6 +76,7 @@ class Plan:
         N.check(N.lib.dq_plan_create(ctypes.byref(desc), ctypes.byref(handle)))
         self.handle = handle
         self._states: Dict[int, ctypes.c_void_p] = {}
+        self.lock = threading.Lock()  # one run_scan at a time per cached state
 
     def __del__(self):
         try:
@@ -185,7 +186,8 @@ def run_scan(table, specs: Sequence[AggSpec]) -> List[object]:
     if not specs:
         return []
     plan = get_plan(table.schema, specs)
-    state = plan.state(table.device_index())
-    N.check(N.lib.dq_state_reset(state))
-    scan_into(table, plan, state)
-    return read_row(plan, state)
+    with plan.lock:
+        state = plan.state(table.device_index())
+        N.check(N.lib.dq_state_reset(state))
+        scan_into(table, plan, state)
+        return read_row(plan, state)
