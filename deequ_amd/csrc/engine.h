@@ -286,6 +286,65 @@ DQ_HD uint64_t xxh_bytes(const Reader& rd, int64_t len, uint64_t seed) {
   return xxh_fmix(h);
 }
 
+// XXH64.hashUnsafeBytes (xxh_bytes above) of a string of len <= 64 bytes held in registers:
+// w[j] = its bytes [4j, 4j + 4).  Every step of xxh_bytes is unrolled with compile-time register
+// indices, taken under its own condition on len, so no register array is indexed at run time.
+DQ_HD uint64_t xxh_bytes_regs64(const uint32_t (&w)[16], int32_t len, uint64_t seed) {
+  auto w64 = [&](int j) { return (uint64_t)w[2 * j] | ((uint64_t)w[2 * j + 1] << 32); };
+  uint64_t h;
+  const int ns = len >> 5;  // 32-byte stripes: 0, 1 or 2
+  if (ns) {
+    uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+    v1 = xxh_round(v1, w64(0));
+    v2 = xxh_round(v2, w64(1));
+    v3 = xxh_round(v3, w64(2));
+    v4 = xxh_round(v4, w64(3));
+    if (ns > 1) {
+      v1 = xxh_round(v1, w64(4));
+      v2 = xxh_round(v2, w64(5));
+      v3 = xxh_round(v3, w64(6));
+      v4 = xxh_round(v4, w64(7));
+    }
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = xxh_merge_round(h, v1);
+    h = xxh_merge_round(h, v2);
+    h = xxh_merge_round(h, v3);
+    h = xxh_merge_round(h, v4);
+  } else {
+    h = seed + P5;
+  }
+  h += (uint64_t)len;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {  // the 8-byte words after the stripes
+    if (j >= 4 * ns && 8 * j + 8 <= len) {
+      h ^= xxh_round(0, w64(j));
+      h = rotl64(h, 27) * P1 + P4;
+    }
+  }
+  const int nw = len >> 3;
+  if ((len & 7) >= 4) {  // one 4-byte word at 8 * nw
+    uint32_t d = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d = j == nw ? w[2 * j] : d;
+    h ^= (uint64_t)d * P1;
+    h = rotl64(h, 23) * P2 + P3;
+  }
+  const int nb = len & 3;
+  if (nb) {  // the last len % 4 bytes, from the dword at 4 * (len / 4)
+    uint32_t d = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) d = j == (len >> 2) ? w[j] : d;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      if (b < nb) {
+        h ^= (uint64_t)((d >> (8 * b)) & 0xffu) * P5;
+        h = rotl64(h, 11) * P1;
+      }
+    }
+  }
+  return xxh_fmix(h);
+}
+
 struct HostBytes {
   const uint8_t* p;
   DQ_HD uint64_t u64(int64_t o) const {

@@ -739,7 +739,52 @@ DQ_DEV void hll_chunk8(const TaskDesc& t, int64_t r0, bool dbl, uint32_t* regs) 
   }
 }
 
+// TK_HLL over a utf8 column: lane l takes row r0 + l of each 64-row step.  A string of at most 64
+// bytes is read as the aligned dwords that hold it -- all issued before any is used, as many as
+// the wave's longest such string needs (each dword holds a byte of the string, so none leaves
+// its buffer) -- and hashed from registers; longer strings take xxh_bytes' loop.
+DQ_DEV void hll_str_rows(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint32_t* regs) {
+  const int l = lane_id();
+  const int32_t* off = reinterpret_cast<const int32_t*>(t.values);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += 64) {
+    const int64_t r = r0 + l;
+    uint32_t ok = 0;
+    int32_t s = 0, e = 0;
+    if (r < r_end) {
+      ok = bit1(t.valid, r);
+      if (t.w_val) ok &= bit1(t.w_val, r) & bit1(t.w_vld, r);
+      s = off[r];
+      e = off[r + 1];
+    }
+    const int32_t len = e - s;
+    const bool reg = ok && len <= 64;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(t.data + s);
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const uint32_t sh = (uint32_t)(a & 3);
+    const int nd = reg && len > 0 ? (int)((sh + (uint32_t)len + 3) >> 2) : 0;  // dwords: <= 17
+    int ndw = nd;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) ndw = max(ndw, __shfl_xor(ndw, o));
+    ndw = __builtin_amdgcn_readfirstlane(ndw);
+    uint32_t dw[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+      dw[k] = 0;
+      if (k < ndw) dw[k] = nd ? base[min(k, nd - 1)] : 0u;
+    }
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(dw[j + 1], dw[j], sh);
+    if (reg) hll_update(regs, xxh_bytes_regs64(w, len, 42));
+    if (ok && !reg) hll_update(regs, xxh_bytes(UBytes{t.data + s}, (int64_t)len, 42));
+  }
+}
+
 DQ_DEV void hll_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint32_t* regs) {
+  if (t.type == DQ_UTF8) {
+    hll_str_rows(t, r_begin, r_end, regs);
+    return;
+  }
   const int l = lane_id();
   int64_t r_fast = r_begin;
   if (t.vec_ok && (t.type == DQ_INT64 || t.type == DQ_FLOAT64)) {

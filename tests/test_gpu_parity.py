@@ -251,3 +251,31 @@ def test_fused_hll_and_comoments_match_oracle(n, null_rate, batch, gpu_device):
             assert cst.n == exp[0]
             ref = exp[3] / math.sqrt(exp[4] * exp[5]) if exp[4] * exp[5] > 0 else float("nan")
             assert rel_close(cst.metric_value(), ref, 1e-10)
+
+
+@pytest.mark.parametrize("n,batch", [(5_000, None), (40_000, 6_000)])
+def test_hll_strings_of_every_length_match_oracle(n, batch, gpu_device):
+    """TK_HLL over utf8: strings of 0..100 bytes (the register path takes <= 64, longer ones
+    xxh_bytes' loop), multibyte characters, NULLs and a where filter; registers bit-exact."""
+    from deequ_amd import Table
+    from deequ_amd.analyzers import ApproxCountDistinct
+    from oracle import deequ_oracle as O
+    rng = np.random.default_rng(n)
+    alphabet = list("abcXYZ019 _-") + ["é", "ß", "€", "漢"]
+    vals = []
+    for i in range(n):
+        if rng.random() < 0.05:
+            vals.append(None)
+            continue
+        target = int(rng.integers(0, 101))
+        s = ""
+        while len(s.encode()) < target:
+            s += alphabet[int(rng.integers(0, len(alphabet)))]
+        vals.append(s)
+    ks = rng.integers(0, 3, n).astype(np.int32)
+    t = pa.table({"s": pa.array(vals, type=pa.string()), "k": pa.array(ks, type=pa.int32())})
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=batch)
+    ot = O.OTable({"s": vals, "k": ks.tolist()}, {"s": "string", "k": "int"})
+    for w in (None, "k > 0"):
+        st = _state_of(df, ApproxCountDistinct("s", w))
+        assert list(st.words) == O.agg_hll(ot, "s", w), w

@@ -188,15 +188,36 @@ def main():
         buf = io.StringIO()
         pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(40)
         print(buf.getvalue(), file=sys.stderr)
+    import gc
+    gc_log = []  # (generation, seconds) of every collection, and the host time of each step
+    gc_t = {}
+
+    def on_gc(phase, info):
+        if phase == "start":
+            gc_t["t"] = time.perf_counter()
+        else:
+            gc_log.append((info["generation"], time.perf_counter() - gc_t.get("t", time.perf_counter()),
+                           info.get("collected", 0)))
+    gc.callbacks.append(on_gc)
+    step_host = []
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
         e0[i].record(stream)
+        n_gc = len(gc_log)
+        ts = time.perf_counter()
         res = step()
+        step_host.append((time.perf_counter() - ts, gc_log[n_gc:]))
         e1[i].record(stream)
     torch.cuda.synchronize(dev)
     el = (time.perf_counter() - t0) / args.steps
-    dev_ms = sum(a.elapsed_time(b) for a, b in zip(e0, e1)) / args.steps
+    per_step = [a.elapsed_time(b) for a, b in zip(e0, e1)]
+    print("device ms per step: " + " ".join(f"{x:.1f}" for x in per_step), file=sys.stderr)
+    for i, (h, gcs) in enumerate(step_host):
+        print(f"step {i}: host {h * 1e3:.1f} ms, {len(gcs)} gc collections, "
+              f"{sum(d for _, d, _ in gcs) * 1e3:.1f} ms, gen2: " +
+              ", ".join(f"{d * 1e3:.1f} ms" for g, d, _ in gcs if g == 2), file=sys.stderr)
+    dev_ms = sum(per_step) / args.steps
     achieved = b_alg / (dev_ms * 1e-3)
     print(json.dumps({
         "workload": args.workload, "desc": desc, "rows": rows, "unit": metric_unit,

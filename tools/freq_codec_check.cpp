@@ -182,6 +182,37 @@ static void check_table(const std::vector<HostCol>& cols, int64_t n, int null_as
   }
 }
 
+// TK_HLL's register path for utf8 (scan.hip hll_str_rows): the aligned dwords that hold a string
+// of <= 64 bytes (the last one repeated up to 17), realigned by alignbyte, hashed by
+// xxh_bytes_regs64 -- equal to xxh_bytes (Spark's hashUnsafeBytes) at every length and alignment.
+static void check_hll_regs() {
+  std::mt19937_64 g(5);
+  for (int len = 0; len <= 64; ++len) {
+    for (int shift = 0; shift < 4; ++shift) {
+      for (int rep = 0; rep < 20; ++rep) {
+        alignas(8) uint8_t room[96];
+        memset(room, 0xEE, sizeof(room));
+        uint8_t* p = room + 4 + shift;
+        for (int k = 0; k < len; ++k) p[k] = (uint8_t)g();
+        const uint64_t want = xxh_bytes(HostBytes{p}, len, 42);
+        const uint32_t* base = reinterpret_cast<const uint32_t*>(room + 4);
+        const int nd = len > 0 ? (shift + len + 3) >> 2 : 0;
+        uint32_t dw[17];
+        for (int k = 0; k < 17; ++k) {
+          dw[k] = 0;
+          if (nd) memcpy(&dw[k], base + (k < nd - 1 ? k : nd - 1), 4);
+        }
+        uint32_t w[16];
+        for (int j = 0; j < 16; ++j) {  // __builtin_amdgcn_alignbyte(dw[j + 1], dw[j], shift)
+          const uint64_t both = ((uint64_t)dw[j + 1] << 32) | dw[j];
+          w[j] = (uint32_t)(both >> (8 * shift));
+        }
+        CHECK(xxh_bytes_regs64(w, len, 42) == want, "xxh_bytes_regs64 len %d shift %d", len, shift);
+      }
+    }
+  }
+}
+
 int main() {
   // fmix is a bijection with the stated inverse
   std::mt19937_64 rng(7);
@@ -190,6 +221,7 @@ int main() {
     CHECK(fmix_inv(fmix_bij(x)) == x, "fmix_inv");
   }
   CHECK(code_count((2u << 2) | 3u) == 48, "code_count");
+  check_hll_regs();
   // the round-1 fault input: one row, (int64 INT64_MIN, "high")
   for (int nag = 0; nag < 1; ++nag) {
     std::vector<HostCol> c = {int64_col({INT64_MIN}, {false}), str_col({"high"}, {false})};
