@@ -14,6 +14,8 @@ import functools
 import gc
 import json
 import os
+import sys
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -239,6 +241,12 @@ def _histogram_and_grouping_job(data, col, hists, group, aggregate_with, save_st
     return AnalyzerContext(hist_metrics), metrics
 
 
+def _job_name(job) -> str:
+    if job.func is _run_scanning_analyzers:
+        return "scan " + ",".join(type(a).__name__ for a in job.args[1])
+    return f"{job.func.__name__} {job.args[1]}"
+
+
 def _job_weight(job) -> int:
     """Submission order of the jobs: groupings over several columns first, then one-column
     groupings and Histograms, then the scans (ties keep their order)."""
@@ -282,7 +290,14 @@ def _run_jobs(data, jobs, workers: int) -> list:
     for the caller's stream (the table's buffers), and the caller's stream waits for all of them
     at the end."""
     if workers <= 1 or len(jobs) <= 1:
-        return [job() for job in jobs]
+        if not os.environ.get("DQ_RUN_TRACE"):
+            return [job() for job in jobs]
+        out = []
+        for job in jobs:  # DQ_RUN_TRACE=1: each job's wall time on stderr
+            t0 = time.perf_counter()
+            out.append(job())
+            print(f"[dq run] {time.perf_counter() - t0:9.4f} s {_job_name(job)}", file=sys.stderr)
+        return out
     import queue
     from concurrent.futures import ThreadPoolExecutor
     import torch

@@ -207,14 +207,14 @@ def main():
         n_gc = len(gc_log)
         ts = time.perf_counter()
         res = step()
-        step_host.append((time.perf_counter() - ts, gc_log[n_gc:]))
+        step_host.append((time.perf_counter() - ts, gc_log[n_gc:], torch.cuda.mem_get_info(dev)[0]))
         e1[i].record(stream)
     torch.cuda.synchronize(dev)
     el = (time.perf_counter() - t0) / args.steps
     per_step = [a.elapsed_time(b) for a, b in zip(e0, e1)]
     print("device ms per step: " + " ".join(f"{x:.1f}" for x in per_step), file=sys.stderr)
-    for i, (h, gcs) in enumerate(step_host):
-        print(f"step {i}: host {h * 1e3:.1f} ms, {len(gcs)} gc collections, "
+    for i, (h, gcs, free) in enumerate(step_host):
+        print(f"step {i}: host {h * 1e3:.1f} ms, free {free / 2**30:.1f} GiB, {len(gcs)} gc collections, "
               f"{sum(d for _, d, _ in gcs) * 1e3:.1f} ms, gen2: " +
               ", ".join(f"{d * 1e3:.1f} ms" for g, d, _ in gcs if g == 2), file=sys.stderr)
     dev_ms = sum(per_step) / args.steps
