@@ -1723,6 +1723,7 @@ extern "C" void dq_column_release(dq_column* col) {
 // ------------------------------------------------------------------------------------------------
 // Device memory cache (kernels.h)
 // ------------------------------------------------------------------------------------------------
+#include <chrono>
 #include <mutex>
 
 namespace dq {
@@ -1730,7 +1731,34 @@ namespace {
 constexpr int kPoolDevices = 64;
 constexpr size_t kPoolRound = 256;                 // small blocks: 256-B granules
 constexpr size_t kPoolBig = 2ULL << 20;            // >= 2 MiB: 2-MiB granules
-constexpr size_t kPoolKeep = 32ULL << 30;          // at most this much cached per device
+// At most a third of the device's memory is cached (96 GB of an MI355X's 288).  Measured on
+// configs[4]: with a 32 GB cap the larger freed blocks went back to the driver,
+// hipFree of 4-8 GB took 0.1-0.3 s, and about one hipMalloc of such a size in twenty waited
+// ~6 s (the driver clearing freed memory); with 96 GB every block is reused.
+size_t pool_keep(int dev) {  // the caller holds the pool lock; DQ_POOL_KEEP_GB overrides
+  static const long long env_gb = [] {
+    const char* e = getenv("DQ_POOL_KEEP_GB");
+    return e ? atoll(e) : -1LL;
+  }();
+  if (env_gb >= 0) return (size_t)env_gb << 30;
+  static size_t keep[kPoolDevices] = {0};
+  if (!keep[dev]) {
+    size_t free_b = 0, total_b = 0;
+    keep[dev] = hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b ? total_b / 3
+                                                                           : (32ULL << 30);
+  }
+  return keep[dev];
+}
+int pool_debug() {  // DQ_POOL_DEBUG=1: every hipMalloc / hipFree of the cache taking >= 50 ms
+  static const int d = [] {
+    const char* e = getenv("DQ_POOL_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  return d;
+}
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
 struct DevPool {
   std::mutex m;
   std::multimap<size_t, void*> free_blocks[kPoolDevices];
@@ -1770,7 +1798,11 @@ hipError_t dev_alloc(void** out, size_t bytes, size_t* got, int* device) {
       return hipSuccess;
     }
   }
+  auto t0 = std::chrono::steady_clock::now();
   hipError_t e = hipMalloc(out, want);
+  if (pool_debug() && ms_since(t0) >= 50.0)
+    fprintf(stderr, "dq pool: hipMalloc(%.2f GB) took %.1f ms (cached %.2f GB)\n", want / 1e9,
+            ms_since(t0), pool.cached[dev] / 1e9);
   if (e == hipErrorOutOfMemory && dev >= 0 && dev < kPoolDevices) {
     (void)hipGetLastError();
     {
@@ -1793,13 +1825,18 @@ void dev_free(void* p, size_t bytes, int dev) {
   bool kept = false;
   if (dev >= 0 && dev < kPoolDevices && bytes) {
     std::lock_guard<std::mutex> lock(pool.m);
-    if (pool.cached[dev] + bytes <= kPoolKeep) {
+    if (pool.cached[dev] + bytes <= pool_keep(dev)) {
       pool.free_blocks[dev].emplace(bytes, p);
       pool.cached[dev] += bytes;
       kept = true;
     }
   }
-  if (!kept) (void)hipFree(p);
+  if (!kept) {
+    auto t0 = std::chrono::steady_clock::now();
+    (void)hipFree(p);
+    if (pool_debug() && ms_since(t0) >= 50.0)
+      fprintf(stderr, "dq pool: hipFree(%.2f GB) took %.1f ms\n", bytes / 1e9, ms_since(t0));
+  }
   if (dev != cur) (void)hipSetDevice(cur);
 }
 

@@ -35,6 +35,7 @@
 #include <type_traits>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -3326,6 +3327,11 @@ extern "C" dq_status dq_freq_marginal(dq_freq* joint, int key_index, dq_freq* ou
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(joint->stream));
   }
+  static const int dbg = [] {
+    const char* e = getenv("DQ_FREQ_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
   const int64_t rc[1] = {n};
   const int64_t vb[1] = {(int64_t)((joint->arena_used + 7) & ~7ULL)};
   const int64_t special[3] = {0, 0, (int64_t)joint->h_counters[C_NULL_ROWS]};
@@ -3333,6 +3339,9 @@ extern "C" dq_status dq_freq_marginal(dq_freq* joint, int key_index, dq_freq* ou
                                   joint->arena.p, 1, rc, vb, joint->num_rows, special, 0, hip_stream);
   if (st != DQ_OK) return st;
   HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(hip_stream)));
+  if (dbg)
+    fprintf(stderr, "dq_freq marginal %d: records added in %.2f ms\n", key_index,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return DQ_OK;
 }
 
@@ -3349,6 +3358,19 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
   *is_null = n == 0 ? 1 : 0;  // sum over no joint groups is NULL
   if (!n) return DQ_OK;
   hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
+  static const int dbg = [] {  // DQ_FREQ_DEBUG: the MI pass's steps, timed (synchronising)
+    const char* e = getenv("DQ_FREQ_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  auto t_last = std::chrono::steady_clock::now();
+  auto stamp = [&](const char* what) {
+    if (!dbg) return;
+    (void)hipStreamSynchronize(stream);
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "dq_freq MI %s: %.2f ms\n", what,
+            std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
   dq_freq* marg[2] = {nullptr, nullptr};
   DevBuf<uint32_t> slots[2];
   Lookup L[2];
@@ -3356,8 +3378,11 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
   for (int k = 0; k < 2 && res == DQ_OK; ++k) {
     const int32_t ty = joint->types[k];
     res = dq_freq_create(joint->device, 1, &ty, 0, &marg[k]);
+    stamp(k ? "marginal 1 create" : "marginal 0 create");
     if (res == DQ_OK) res = dq_freq_marginal(joint, k, marg[k], hip_stream);
+    stamp(k ? "marginal 1 records" : "marginal 0 records");
     if (res == DQ_OK) res = compact_groups(marg[k]);
+    stamp(k ? "marginal 1 groups" : "marginal 0 groups");
     if (res != DQ_OK) break;
     const int64_t m = marg[k]->n_compact;
     uint64_t cap = 2;
@@ -3370,6 +3395,7 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
       hipLaunchKernelGGL(freq_lookup_build, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
                          marg[k]->compact.p, m, cap - 1, slots[k].p);
     L[k] = Lookup{marg[k]->compact.p, slots[k].p, cap - 1, marg[k]->arena.p, ty, marg[k]->exact ? 1 : 0};
+    stamp(k ? "marginal 1 index" : "marginal 0 index");
   }
   if (res == DQ_OK) {
     DevBuf<double> terms, partial;
@@ -3380,6 +3406,7 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
       hipLaunchKernelGGL(freq_mi_terms, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                          joint->compact.p, n, joint->arena.p, part_types(joint, 1), L[0], L[1],
                          (double)joint->num_rows, terms.p);
+      stamp("terms");
       hipLaunchKernelGGL(freq_sum_f64, dim3(kSumBlocks), dim3(256), 0, stream, terms.p, n, partial.p);
       std::vector<double> h(kSumBlocks);
       if (hipGetLastError() != hipSuccess ||
@@ -3393,7 +3420,9 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
       }
     }
   }
+  stamp("sum");
   for (dq_freq* m : marg) dq_freq_destroy(m);
+  stamp("destroy");
   return res;
 }
 
@@ -3712,9 +3741,23 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
   a.segs.rec_start[n_src] = total_rec;
   if (total_rec && !records) return fail(DQ_ERR_INVALID_ARGUMENT, "null records");
   if (!f->exact && total_var && !var) return fail(DQ_ERR_INVALID_ARGUMENT, "null var bytes");
+  static const int dbg = [] {  // DQ_FREQ_DEBUG: the steps below, timed (synchronising)
+    const char* e = getenv("DQ_FREQ_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  auto t_last = std::chrono::steady_clock::now();
+  auto stamp = [&](const char* what) {
+    if (!dbg) return;
+    (void)hipStreamSynchronize(f->stream);
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "dq_freq add_records %s: %.2f ms\n", what,
+            std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
   dq_status st = pull_counters(f);
   if (st != DQ_OK) return st;
   invalidate(f);
+  stamp("counters");
   if (total_rec) {
     // a record's count becomes count_digits(count) <= 32 records: tiles of tile / max digits
     // records never overflow a chunk (a 32x bound sized a marginal of 1e8 groups at 60+ GB)
@@ -3735,8 +3778,10 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
     const int64_t per = std::min<int64_t>(f->tile / maxd, AKeys<false, true>::kThreads);
     static_assert(AKeys<false, true>::kThreads == AKeys<true, true>::kThreads, "one round");
     const int64_t chunks = phaseA_chunks(!f->exact, true, total_rec, per, nullptr);
+    stamp("max digits");
     st = ensure_chunks(f, chunks);
     if (st != DQ_OK) return st;
+    stamp("chunks");
     a = [&] {
       AArgs b = base_args(f);
       b.segs = a.segs;
@@ -3751,12 +3796,14 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
       a.var_arena_base = base;
       f->arena_used = base + total_var;
     }
+    stamp("arena");
     a.rin = reinterpret_cast<const RecIn*>(records);
     a.n_items = total_rec;
     a.tile_items = per;
     if (f->exact) launch_phaseA<false>(f, a, true);
     else launch_phaseA<true>(f, a, true);
     HIP_TRY(hipGetLastError());
+    stamp("phase A");
     f->n_chunks += chunks;
   }
   f->h_counters[C_NULL_GROUP] += (uint64_t)special[1];
