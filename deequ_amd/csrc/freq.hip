@@ -2295,6 +2295,7 @@ struct dq_freq {
   DevBuf<unsigned long long> batch_tab;  // freq_phaseA_small's cross-workgroup group table
   uint64_t h_counters[C_N] = {0};
   uint64_t arena_used = 0;
+  uint64_t rec_var_base = 0;  // arena offset of the last dq_freq_add_records_device's var bytes
   // phase A launches leave the device counters and arena cursor ahead of the host copies: they
   // are read back only when needed (finalize, merge, arena growth), so batches queue back to back
   bool counters_stale = false;
@@ -2871,6 +2872,25 @@ static dq_status compact_groups(dq_freq* f) {
   return DQ_OK;
 }
 
+// str_row_hash of an arena-encoded utf8 part (tag, length, bytes zero-padded to 4): the bytes
+// start dword-aligned, so a key of <= 16 bytes is read as its dwords (no byte loop), masked to its
+// length, and hashed from registers (str_row_hash_reg == str_row_hash for such keys).
+DQ_DEV uint64_t enc_str_hash(const uint32_t* part) {
+  const int32_t len = (int32_t)part[1];
+  if (len > 16) return str_row_hash(SView{reinterpret_cast<const uint8_t*>(part + 2), len});
+  const int nd = (len + 3) >> 2;
+  uint32_t d[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = k < nd ? part[2 + k] : 0u;
+  const uint32_t tail = (uint32_t)len & 3u;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (tail && k == nd - 1) d[k] &= (1u << (8 * tail)) - 1u;
+  const uint64_t w0 = (uint64_t)d[0] | ((uint64_t)d[1] << 32);
+  const uint64_t w1 = (uint64_t)d[2] | ((uint64_t)d[3] << 32);
+  return str_row_hash_reg(w0, w1, len);
+}
+
 // The marginal of key column k over a hashed table's groups, as records for a one-key table:
 // column k's part of a group's encoded key IS the one-column encoding of that value, so a
 // record points into the same arena (enc_off), and carries the group's count.  Exact output
@@ -2891,8 +2911,7 @@ __global__ void freq_project(const Group* __restrict__ g, int64_t n, const uint8
   r.count = g[i].count;
   r.enc_off = g[i].rep + 4ull * w;
   if (t.types[k] == DQ_UTF8) {
-    const uint32_t len = enc[w + 1];
-    r.key = str_row_hash(SView{reinterpret_cast<const uint8_t*>(enc + w + 2), (int32_t)len});
+    r.key = enc_str_hash(enc + w);
   } else {
     r.key = (uint64_t)enc[w + 1] | ((uint64_t)enc[w + 2] << 32);
   }
@@ -2920,6 +2939,9 @@ struct Lookup {
   const uint8_t* arena;
   int32_t type;
   int32_t exact;
+  // a marginal group's rep = rep_base + the joint-arena offset of the key part it was made
+  // from (dq_freq_marginal copies the joint arena): a part at that offset IS the group's key
+  uint64_t rep_base;
 };
 
 __global__ void freq_lookup_build(const Group* __restrict__ g, int64_t n, uint64_t mask,
@@ -2930,20 +2952,21 @@ __global__ void freq_lookup_build(const Group* __restrict__ g, int64_t n, uint64
   while (atomicCAS(&slots[s], 0u, (uint32_t)(i + 1)) != 0u) s = (s + 1) & mask;
 }
 
-// The count of the marginal group whose key is the one-column encoding `part`.
-DQ_DEV uint64_t lookup_count(const Lookup& L, const uint32_t* part) {
+// The count of the marginal group whose key is the one-column encoding `part`, at offset
+// part_off of the joint arena.
+DQ_DEV uint64_t lookup_count(const Lookup& L, const uint32_t* part, uint64_t part_off) {
   uint64_t h;
   if (L.exact) {
     h = fmix_bij((uint64_t)part[1] | ((uint64_t)part[2] << 32));
   } else {
-    h = str_row_hash(SView{reinterpret_cast<const uint8_t*>(part + 2), (int32_t)part[1]});
+    h = enc_str_hash(part);
   }
   for (uint64_t s = h & L.mask;; s = (s + 1) & L.mask) {
     const uint32_t idx = L.slots[s];
     if (!idx) return 0;  // not reachable: every joint value has its marginal group
     const Group& m = L.g[idx - 1];
     if (m.h != h) continue;
-    if (L.exact) return m.count;
+    if (L.exact || m.rep == L.rep_base + part_off) return m.count;  // (its own record: no compare)
     const int32_t ty = DQ_UTF8;
     if (enc_equal_arena(reinterpret_cast<const uint32_t*>(L.arena + m.rep), part, &ty, 1)) return m.count;
   }
@@ -2956,8 +2979,10 @@ __global__ void freq_mi_terms(const Group* __restrict__ gj, int64_t n, const uin
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t* enc = reinterpret_cast<const uint32_t*>(arena + gj[i].rep);
-  const double px = (double)lookup_count(X, enc_part(enc, t, 0));
-  const double py = (double)lookup_count(Y, enc_part(enc, t, 1));
+  const uint32_t* ex = enc_part(enc, t, 0);
+  const uint32_t* ey = enc_part(enc, t, 1);
+  const double px = (double)lookup_count(X, ex, gj[i].rep + 4ull * (uint64_t)(ex - enc));
+  const double py = (double)lookup_count(Y, ey, gj[i].rep + 4ull * (uint64_t)(ey - enc));
   const double pxy = (double)gj[i].count;
   terms[i] = (pxy / total) * log((pxy / total) / ((px / total) * (py / total)));
 }
@@ -3394,7 +3419,8 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
     if (m)
       hipLaunchKernelGGL(freq_lookup_build, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
                          marg[k]->compact.p, m, cap - 1, slots[k].p);
-    L[k] = Lookup{marg[k]->compact.p, slots[k].p, cap - 1, marg[k]->arena.p, ty, marg[k]->exact ? 1 : 0};
+    L[k] = Lookup{marg[k]->compact.p, slots[k].p, cap - 1, marg[k]->arena.p, ty, marg[k]->exact ? 1 : 0,
+                  marg[k]->rec_var_base};
     stamp(k ? "marginal 1 index" : "marginal 0 index");
   }
   if (res == DQ_OK) {
@@ -3794,6 +3820,7 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
         HIP_TRY(hipMemcpyAsync(f->arena.p + base, var, total_var, hipMemcpyDeviceToDevice, f->stream));
       a.arena = f->arena.p;
       a.var_arena_base = base;
+      f->rec_var_base = base;
       f->arena_used = base + total_var;
     }
     stamp("arena");
