@@ -254,6 +254,69 @@ struct AArgs {
 
 // Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
 // the LDS must allow two workgroups per CU (<= 80 KB).
+// Device forms of row_hash_hashed / row_encode (freq_codec.h) for phase A's multi-column keys: a
+// utf8 value of at most 16 bytes is read once, as the aligned dwords that hold it (load_str16:
+// every read holds a byte of the string), instead of byte by byte.  Same results: load_str16 and
+// the byte path give the same words (tools/freq_codec_check.cpp).
+DQ_DEV uint64_t row_hash_hashed_dw(const KeySet& ks, int64_t r) {
+  uint64_t h = kRowHashSeed;
+  for (int k = 0; k < ks.n_keys; ++k) {
+    const KeyCol& c = ks.cols[k];
+    uint64_t ch;
+    if (c.type == DQ_UTF8) {
+      SView v;
+      key_str(ks, k, r, v);
+      if (v.p && v.len <= kHash16Max) {
+        uint64_t w0, w1;
+        load_str16(v.p, v.len, w0, w1);
+        ch = str_hash16(w0, w1, v.len, 17 + k);
+      } else {
+        ch = str_col_hash(v, k);
+      }
+    } else {
+      ch = xxh_long(kwiden(c.type, c.values, r), 17 + k);
+    }
+    h = fold_col_hash(h, ch);
+  }
+  return fmix_bij(h);
+}
+
+DQ_DEV void row_encode_dw(const KeySet& ks, int64_t r, uint32_t* dst) {
+  for (int k = 0; k < ks.n_keys; ++k) {
+    const KeyCol& c = ks.cols[k];
+    if (c.type == DQ_UTF8) {
+      SView v;
+      if (!key_str(ks, k, r, v)) {
+        *dst++ = 0;
+        continue;
+      }
+      *dst++ = 1;
+      *dst++ = (uint32_t)v.len;
+      if (v.p && v.len <= kHash16Max) {
+        uint64_t w0, w1;
+        load_str16(v.p, v.len, w0, w1);
+        const uint32_t d[4] = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (4 * q < v.len) *dst++ = d[q];
+      } else {
+        for (int32_t q = 0; q < v.len; q += 4) {
+          uint32_t w = 0;
+          for (int b = 0; b < 4 && q + b < v.len; ++b) w |= sv_byte(v, q + b) << (8 * b);
+          *dst++ = w;
+        }
+      }
+    } else if (!kbit(c.valid, r)) {
+      *dst++ = 0;
+    } else {
+      const uint64_t v = kwiden(c.type, c.values, r);
+      *dst++ = 1;
+      *dst++ = (uint32_t)v;
+      *dst++ = (uint32_t)(v >> 32);
+    }
+  }
+}
+
 template <bool HASHED, bool FROM_REC>
 struct AKeys {
   static constexpr int kDedupe = FROM_REC ? (HASHED ? 128 : 256) : (HASHED ? 256 : 512);
@@ -370,7 +433,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
       const SView v = str1_view(a.ks, row);
       str1_encode_copy(v.p, v.len, reinterpret_cast<uint32_t*>(a.arena + off));
     } else {
-      row_encode(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
+      row_encode_dw(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
     }
     return off;
   };
@@ -627,7 +690,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
           ++nulls;
         } else {
           keyed |= 1u << j;
-          stash[q * W] = row_hash_hashed(a.ks, i);
+          stash[q * W] = row_hash_hashed_dw(a.ks, i);
           stash[q * W + 1] = (uint64_t)i;  // the row until it is encoded
           if constexpr (SK) ssk1[q] = kNoShort;
         }
