@@ -503,8 +503,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
             }
             if (r2 != rep) {
               if constexpr (FROM_REC)
-                same = enc_equal(reinterpret_cast<const uint32_t*>(a.arena + r2),
-                                 reinterpret_cast<const uint32_t*>(a.arena + rep), a.types, a.n_keys);
+                same = enc_equal_arena(reinterpret_cast<const uint32_t*>(a.arena + r2),
+                                       reinterpret_cast<const uint32_t*>(a.arena + rep), a.types,
+                                       a.n_keys);
               else if constexpr (STR1)
                 same = str1_rows_equal(a.ks, (int64_t)r2, (int64_t)rep);
               else
