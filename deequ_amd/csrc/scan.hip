@@ -513,9 +513,65 @@ DQ_DEV int dtype_of_string(const uint8_t* p, int32_t n) {
   return DT_STRING;
 }
 
+// A string whose first byte is none of - + space digit . t f is STRING (no pattern above can
+// match it); only the others take dtype_of_string's walk.
+DQ_DEV bool dtype_needs_walk(uint32_t c0) {
+  return c0 - '0' < 10u || c0 == '-' || c0 == '+' || c0 == ' ' || c0 == '.' || c0 == 't' ||
+         c0 == 'f';
+}
+
+// utf8 columns: lane l classifies rows r0 + 64j + l (j < 4) of each 256-row step, with the four
+// rows' offsets and then their first data dwords loaded together (one round trip each for the
+// step, not per row); most strings are decided by their first byte.
+DQ_DEV void dtype_str_rows(const TaskDesc& t, int64_t r_begin, int64_t r_end, int64_t (&c)[5]) {
+  const int l = lane_id();
+  const int32_t* off = reinterpret_cast<const int32_t*>(t.values);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += 256) {
+    int32_t s[4], n[4];
+    uint32_t ok = 0, in = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t r = r0 + 64 * j + l;
+      s[j] = n[j] = 0;
+      if (r < r_end) {
+        in |= 1u << j;
+        uint32_t v = bit1(t.valid, r);
+        if (t.w_val) v &= bit1(t.w_val, r) & bit1(t.w_vld, r);
+        ok |= v << j;
+        s[j] = off[r];
+        n[j] = off[r + 1] - s[j];
+      }
+    }
+    uint32_t d[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // the dword holding each string's first byte
+      const uintptr_t a = reinterpret_cast<uintptr_t>(t.data + s[j]);
+      d[j] = ((ok >> j) & 1u) && n[j] > 0 ? *reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3)) >> (8 * (a & 3))
+                                          : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!((in >> j) & 1u)) continue;
+      int k;
+      if (!((ok >> j) & 1u)) k = DT_NULL;
+      else if (n[j] == 0) k = DT_INTEGRAL;  // "" matches INTEGRAL's pattern
+      else if (dtype_needs_walk(d[j] & 0xffu)) k = dtype_of_string(t.data + s[j], n[j]);
+      else k = DT_STRING;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) c[q] += k == q;
+    }
+  }
+}
+
 DQ_DEV void dtype_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& acc) {
   int64_t c[5] = {0, 0, 0, 0, 0};
   const int32_t* off = reinterpret_cast<const int32_t*>(t.values);
+  if (t.type == DQ_UTF8) {
+    dtype_str_rows(t, r_begin, r_end, c);
+#pragma unroll
+    for (int q = 0; q < 5; ++q) acc.i[q] = c[q];
+    return;
+  }
   for (int64_t r = r_begin + lane_id(); r < r_end; r += 64) {
     const uint32_t w = t.w_val ? bit1(t.w_val, r) & bit1(t.w_vld, r) : 1u;
     int k;
