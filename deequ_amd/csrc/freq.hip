@@ -2360,6 +2360,10 @@ struct dq_freq {
   uint64_t h_counters[C_N] = {0};
   uint64_t arena_used = 0;
   uint64_t rec_var_base = 0;  // arena offset of the last dq_freq_add_records_device's var bytes
+  // a table built from another table's records may read that table's arena in place instead of
+  // a copy (MutualInformation's marginals, which die before their joint table): then the keys live
+  // here and the table takes no further adds
+  const uint8_t* arena_view = nullptr;
   // phase A launches leave the device counters and arena cursor ahead of the host copies: they
   // are read back only when needed (finalize, merge, arena growth), so batches queue back to back
   bool counters_stale = false;
@@ -2590,6 +2594,8 @@ static dq_status launch_phaseA_small(dq_freq* f, AArgs& a) {
   return DQ_OK;
 }
 
+static const uint8_t* arena_of(const dq_freq* f) { return f->arena_view ? f->arena_view : f->arena.p; }
+
 static AArgs base_args(dq_freq* f) {
   AArgs a;
   memset(&a, 0, sizeof(a));
@@ -2602,7 +2608,7 @@ static AArgs base_args(dq_freq* f) {
   a.ks.null_as_group = f->mode_null_as_group > 0 ? 1 : 0;
   a.recs = f->recs.p + (size_t)f->n_chunks * f->tile * f->rb;
   a.hist = f->hist.p + (size_t)f->n_chunks * kHistRow;
-  a.arena = f->arena.p;
+  a.arena = const_cast<uint8_t*>(arena_of(f));
   a.arena_cursor = f->dev_words.p + C_N;
   a.counters = f->dev_words.p;
   return a;
@@ -2802,7 +2808,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     a.recsB = f->recsB.p;
     a.part_base = f->part_base.p;
     a.s = f->s_bits;
-    a.arena = f->arena.p;
+    a.arena = arena_of(f);
     for (int k = 0; k < f->n_keys; ++k) a.types[k] = f->types[k];
     a.n_keys = f->n_keys;
     a.want_cand = want_cand ? 1 : 0;
@@ -3080,7 +3086,7 @@ static dq_status owner_sizes(dq_freq* f, const Group* g, int64_t n, int parts,
   HIP_TRY(hipMemsetAsync(cnt.p, 0, 2 * kMaxParts * 8, f->stream));
   if (n)
     hipLaunchKernelGGL(freq_owner_count, dim3(grid_for(n)), dim3(256), 0, f->stream, g, n,
-                       f->arena.p, part_types(f, parts), cnt.p, cnt.p + kMaxParts);
+                       arena_of(f), part_types(f, parts), cnt.p, cnt.p + kMaxParts);
   HIP_TRY(hipGetLastError());
   std::vector<unsigned long long> h(2 * kMaxParts);
   HIP_TRY(hipStreamSynchronize(f->stream));
@@ -3106,7 +3112,7 @@ static dq_status owner_scatter(dq_freq* f, const Group* g, int64_t n, int parts,
   HIP_TRY(d.ensure(base.size()));
   HIP_TRY(hipMemcpy(d.p, base.data(), base.size() * 8, hipMemcpyHostToDevice));
   hipLaunchKernelGGL(freq_owner_scatter, dim3(grid_for(n)), dim3(256), 0, f->stream, g, n,
-                     f->arena.p, part_types(f, parts), d.p, d.p + kMaxParts, d.p + 2 * kMaxParts,
+                     arena_of(f), part_types(f, parts), d.p, d.p + kMaxParts, d.p + 2 * kMaxParts,
                      d.p + 3 * kMaxParts, out_rec, out_var);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(f->stream));
@@ -3288,6 +3294,7 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
                                         int null_as_group, void* hip_stream) {
   if (!f || !keys) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   if (n_keys != f->n_keys) return fail(DQ_ERR_INVALID_ARGUMENT, "expected %d key columns", f->n_keys);
+  if (f->arena_view) return fail(DQ_ERR_STATE, "a table reading another table's keys takes no adds");
   const int mode = null_as_group ? 1 : 0;
   if (f->mode_null_as_group >= 0 && f->mode_null_as_group != mode)
     return fail(DQ_ERR_STATE, "null_as_group must be the same for every batch");
@@ -3396,8 +3403,21 @@ extern "C" dq_status dq_freq_summarize_keys(dq_freq* f, dq_freq_summary* out) {
   return DQ_OK;
 }
 
+static dq_status marginal_of(dq_freq* joint, int key_index, dq_freq* out, void* hip_stream,
+                             bool borrow);
+static dq_status add_records(dq_freq* f, const dq_freq_record* records, const uint8_t* var,
+                             int n_src, const int64_t* src_records, const int64_t* src_var_bytes,
+                             int64_t num_rows, const int64_t* special, int null_as_group,
+                             void* hip_stream, bool borrow);
+
 extern "C" dq_status dq_freq_marginal(dq_freq* joint, int key_index, dq_freq* out,
                                      void* hip_stream) {
+  return marginal_of(joint, key_index, out, hip_stream, false);
+}
+
+// borrow: the marginal reads the joint table's arena in place (it must die first)
+static dq_status marginal_of(dq_freq* joint, int key_index, dq_freq* out, void* hip_stream,
+                             bool borrow) {
   if (!joint || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   if (joint->exact || joint->n_keys < 2) return fail(DQ_ERR_INVALID_ARGUMENT, "not a multi-key table");
   if (key_index < 0 || key_index >= joint->n_keys) return fail(DQ_ERR_INVALID_ARGUMENT, "bad key index");
@@ -3412,7 +3432,7 @@ extern "C" dq_status dq_freq_marginal(dq_freq* joint, int key_index, dq_freq* ou
   HIP_TRY(rec.ensure(std::max<int64_t>(n, 1)));
   if (n) {
     hipLaunchKernelGGL(freq_project, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, joint->stream,
-                       joint->compact.p, n, joint->arena.p, part_types(joint, 1), key_index, rec.p);
+                       joint->compact.p, n, arena_of(joint), part_types(joint, 1), key_index, rec.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(joint->stream));
   }
@@ -3424,8 +3444,8 @@ extern "C" dq_status dq_freq_marginal(dq_freq* joint, int key_index, dq_freq* ou
   const int64_t rc[1] = {n};
   const int64_t vb[1] = {(int64_t)((joint->arena_used + 7) & ~7ULL)};
   const int64_t special[3] = {0, 0, (int64_t)joint->h_counters[C_NULL_ROWS]};
-  st = dq_freq_add_records_device(out, reinterpret_cast<const dq_freq_record*>(rec.p),
-                                  joint->arena.p, 1, rc, vb, joint->num_rows, special, 0, hip_stream);
+  st = add_records(out, reinterpret_cast<const dq_freq_record*>(rec.p), arena_of(joint), 1, rc, vb,
+                   joint->num_rows, special, 0, hip_stream, borrow && !out->exact);
   if (st != DQ_OK) return st;
   HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(hip_stream)));
   if (dbg)
@@ -3468,7 +3488,7 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
     const int32_t ty = joint->types[k];
     res = dq_freq_create(joint->device, 1, &ty, 0, &marg[k]);
     stamp(k ? "marginal 1 create" : "marginal 0 create");
-    if (res == DQ_OK) res = dq_freq_marginal(joint, k, marg[k], hip_stream);
+    if (res == DQ_OK) res = marginal_of(joint, k, marg[k], hip_stream, true);
     stamp(k ? "marginal 1 records" : "marginal 0 records");
     if (res == DQ_OK) res = compact_groups(marg[k]);
     stamp(k ? "marginal 1 groups" : "marginal 0 groups");
@@ -3483,7 +3503,7 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
     if (m)
       hipLaunchKernelGGL(freq_lookup_build, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
                          marg[k]->compact.p, m, cap - 1, slots[k].p);
-    L[k] = Lookup{marg[k]->compact.p, slots[k].p, cap - 1, marg[k]->arena.p, ty, marg[k]->exact ? 1 : 0,
+    L[k] = Lookup{marg[k]->compact.p, slots[k].p, cap - 1, arena_of(marg[k]), ty, marg[k]->exact ? 1 : 0,
                   marg[k]->rec_var_base};
     stamp(k ? "marginal 1 index" : "marginal 0 index");
   }
@@ -3494,7 +3514,7 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
       res = fail(DQ_ERR_OUT_OF_MEMORY, "MutualInformation terms");
     } else {
       hipLaunchKernelGGL(freq_mi_terms, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                         joint->compact.p, n, joint->arena.p, part_types(joint, 1), L[0], L[1],
+                         joint->compact.p, n, arena_of(joint), part_types(joint, 1), L[0], L[1],
                          (double)joint->num_rows, terms.p);
       stamp("terms");
       hipLaunchKernelGGL(freq_sum_f64, dim3(kSumBlocks), dim3(256), 0, stream, terms.p, n, partial.p);
@@ -3710,6 +3730,7 @@ extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src_c) {
   if (!dst || !src_c) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   dq_freq* src = const_cast<dq_freq*>(src_c);
   if (dst == src) return fail(DQ_ERR_INVALID_ARGUMENT, "cannot merge a table into itself");
+  if (dst->arena_view) return fail(DQ_ERR_STATE, "a table reading another table's keys takes no adds");
   if (dst->n_keys != src->n_keys || dst->types != src->types)
     return fail(DQ_ERR_STATE, "frequency tables group on different key types");
   if (dst->device != src->device) return fail(DQ_ERR_UNSUPPORTED, "tables on different devices");
@@ -3736,7 +3757,7 @@ extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src_c) {
       HIP_TRY(grow_keep(dst->arena, dst->arena_used, dst->arena_used + src->arena_used + 64,
                         dst->stream));
       if (src->arena_used)
-        HIP_TRY(hipMemcpyAsync(dst->arena.p + dst->arena_used, src->arena.p, src->arena_used,
+        HIP_TRY(hipMemcpyAsync(dst->arena.p + dst->arena_used, arena_of(src), src->arena_used,
                                hipMemcpyDeviceToDevice, dst->stream));
       hipLaunchKernelGGL(freq_rebase, dim3((unsigned)nc), dim3(256), 0, dst->stream,
                          reinterpret_cast<uint64_t*>(dst->recs.p), dst->hist.p, dst->n_chunks,
@@ -3800,14 +3821,32 @@ extern "C" dq_status dq_freq_partition(dq_freq* f, int n_parts, dq_freq_record* 
                        var, rec, var_n);
 }
 
+static dq_status add_records(dq_freq* f, const dq_freq_record* records, const uint8_t* var,
+                             int n_src, const int64_t* src_records, const int64_t* src_var_bytes,
+                             int64_t num_rows, const int64_t* special, int null_as_group,
+                             void* hip_stream, bool borrow);
+
 extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record* records,
                                                 const uint8_t* var, int n_src,
                                                 const int64_t* src_records,
                                                 const int64_t* src_var_bytes, int64_t num_rows,
                                                 const int64_t* special, int null_as_group,
                                                 void* hip_stream) {
+  return add_records(f, records, var, n_src, src_records, src_var_bytes, num_rows, special,
+                     null_as_group, hip_stream, false);
+}
+
+// borrow: read the var bytes in place (arena_view) instead of copying them into the table's
+// arena -- only for a fresh hashed table that dies before the var bytes do
+static dq_status add_records(dq_freq* f, const dq_freq_record* records, const uint8_t* var,
+                             int n_src, const int64_t* src_records, const int64_t* src_var_bytes,
+                             int64_t num_rows, const int64_t* special, int null_as_group,
+                             void* hip_stream, bool borrow) {
   if (!f || !src_records || !src_var_bytes || !special)
     return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  if (f->arena_view) return fail(DQ_ERR_STATE, "a table reading another table's keys takes no adds");
+  if (borrow && (f->exact || f->arena_used || f->n_chunks))
+    return fail(DQ_ERR_STATE, "only a fresh hashed table can borrow var bytes");
   if (n_src < 1 || n_src > kMaxParts)
     return fail(DQ_ERR_UNSUPPORTED, "n_src must be in [1, %d]", kMaxParts);
   const int mode = null_as_group ? 1 : 0;
@@ -3877,7 +3916,13 @@ extern "C" dq_status dq_freq_add_records_device(dq_freq* f, const dq_freq_record
       b.segs = a.segs;
       return b;
     }();
-    if (!f->exact) {
+    if (!f->exact && borrow) {  // (the var bytes' owner keeps >= 64 bytes past its last key)
+      f->arena_view = var;
+      a.arena = const_cast<uint8_t*>(var);
+      a.var_arena_base = 0;
+      f->rec_var_base = 0;
+      f->arena_used = total_var;
+    } else if (!f->exact) {
       const uint64_t base = (f->arena_used + 7) & ~7ULL;
       HIP_TRY(grow_keep(f->arena, f->arena_used, base + total_var + 64, f->stream));
       if (total_var)
