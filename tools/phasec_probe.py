@@ -2,7 +2,7 @@
 1.25e8 rows) with DQ_FREQ_DEBUG=2 phase timings (phase A tiles, phase C items of workgroup 0)
 and the device time of its finalize.
 
-Usage: DQ_FREQ_DEBUG=2 python tools/phasec_probe.py [rows] [column]
+Usage: DQ_FREQ_DEBUG=2 python tools/phasec_probe.py [rows] [column]  (configs[4] columns too)
 """
 import os
 import sys
@@ -17,8 +17,11 @@ def main():
     rows = int(sys.argv[1]) if len(sys.argv) > 1 else 125_000_000
     col = sys.argv[2] if len(sys.argv) > 2 else "name"
     from deequ_amd.analyzers.grouping import FrequencyTable
-    from deequ_amd.synth import item_table_device
-    t = item_table_device(rows, seed=101, device="cuda:0")
+    from deequ_amd.synth import item_table_device, profiling_table_device
+    if col in ("name", "priority", "id", "numViews"):
+        t = item_table_device(rows, seed=101, device="cuda:0")
+    else:  # a configs[4] column (description_0, name_0, ...)
+        t = profiling_table_device(rows, batch_rows=1 << 25, device="cuda:0")
     torch.cuda.synchronize()
     for rep in range(2):
         ft = FrequencyTable([col], [t.schema[col].dtype], 0, capacity_hint=rows)
