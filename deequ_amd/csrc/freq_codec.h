@@ -489,15 +489,15 @@ DQ_HD bool enc_equal(const uint32_t* a, const uint32_t* b, const int32_t* types,
 // iff the first enc_size(a) bytes of both are; the words of a 4-word chunk are loaded together
 // (one round trip per chunk, where enc_equal's early-exit loop took one per word).  The first
 // chunk is read unconditionally: every arena keeps >= 64 bytes past its last entry (grow_keep's
-// callers, and a borrowed arena is another table's), so 32 bytes from any entry's start are
+// callers, and a borrowed arena is another table's), so 64 bytes from any entry's start are
 // mapped.
 __device__ inline bool enc_equal_arena(const uint32_t* a, const uint32_t* b, const int32_t* types,
                                        int n_keys) {
-  // the first 8 words of both keys in one round trip (a one-column utf8 key of <= 24 bytes
+  // the first 16 words of both keys in one round trip (a one-column utf8 key of <= 56 bytes
   // is decided by it), then 8 words per round
-  uint32_t wa[8], wb[8];
+  uint32_t wa[16], wb[16];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < 16; ++k) {
     wa[k] = a[k];
     wb[k] = b[k];
   }
@@ -506,9 +506,9 @@ __device__ inline bool enc_equal_arena(const uint32_t* a, const uint32_t* b, con
   else n = enc_size(a, types, n_keys) / 4;
   uint32_t x = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) x |= (uint32_t)k < n ? wa[k] ^ wb[k] : 0u;
+  for (int k = 0; k < 16; ++k) x |= (uint32_t)k < n ? wa[k] ^ wb[k] : 0u;
   if (x) return false;
-  for (uint32_t q = 8; q < n; q += 8) {
+  for (uint32_t q = 16; q < n; q += 8) {
     x = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) x |= q + k < n ? a[q + k] ^ b[q + k] : 0u;
