@@ -3274,6 +3274,8 @@ extern "C" dq_status dq_freq_reset(dq_freq* f, void* hip_stream) {
   HIP_TRY(hipMemsetAsync(f->dev_words.p, 0, (C_N + 4) * 8, f->stream));
   for (int k = 0; k < C_N; ++k) f->h_counters[k] = 0;
   f->arena_used = 0;
+  f->arena_view = nullptr;  // (a reset table owns its keys again)
+  f->rec_var_base = 0;
   f->arena_hi = 0;
   f->counters_stale = false;
   f->num_rows = 0;
