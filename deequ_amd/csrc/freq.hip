@@ -250,6 +250,14 @@ struct AArgs {
   unsigned long long* batch_tab;
   // freq_phaseA_small: general-kernel workgroups (tile ranges + chunk) per small-kernel workgroup
   int32_t small_merge;
+  // exact rows, bucket pieces (pstart != nullptr): the batch's records go to one region of
+  // n_items records at `recs`, bucket-major; workgroup w's records of bucket b fill the piece that
+  // starts at tot-prefix(b) + ph[w][b] (freq_prepass_x / freq_prepass_scan), and the workgroup
+  // writes its pieces' starts and lengths (rows of the table's piece arrays)
+  const uint32_t* ph;    // [n_wg][kBuckets]: exclusive prefix over workgroups, per bucket
+  const uint32_t* ptot;  // [kBuckets]: the batch's rows per bucket
+  uint32_t* pstart;      // [n_wg][kBuckets]
+  uint32_t* plen;        // [n_wg][kBuckets]
 };
 
 // Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
@@ -882,6 +890,81 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   __syncthreads();
   if (tid < 3 && s_dbg[tid]) atomicAdd(&a.counters[C_DBG_NOTREADY + tid], (unsigned long long)s_dbg[tid]);
   wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase A0, exact rows: the rows of each phase-A workgroup per bucket, so that phase A can write
+// the batch bucket-major (bucket b of the batch is one contiguous region when no rows collapse in
+// the dedupe table, and phase B then reads whole buckets as streams instead of gathering 128-byte
+// chunk segments).  Same tile ranges and the same hash as freq_phaseA<false, false>; only
+// non-NULL rows are keyed.
+// ------------------------------------------------------------------------------------------------
+constexpr int kPreThreads = 1024;
+__global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t* ph) {
+  constexpr int ROUNDS = FM<false>::kTile / kPreThreads;
+  __shared__ uint32_t bh[kBuckets];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kBuckets; i += kPreThreads) bh[i] = 0;
+  __syncthreads();
+  const KeyCol& c = a.ks.cols[0];
+  const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
+  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
+  const int64_t t1 = min(t0 + (int64_t)a.tiles_per_wg, n_tiles);
+  auto tile_loop = [&](auto type_tag) {
+    constexpr int TY = decltype(type_tag)::value;
+    for (int64_t t = t0; t < t1; ++t) {
+      const int64_t i0 = t * a.tile_items, i1 = min(i0 + a.tile_items, a.n_items);
+      int64_t ic[ROUNDS];
+      uint32_t ok = 0, vb = ~0u;
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        const int64_t i = i0 + (int64_t)j * kPreThreads + tid;
+        ok |= (i < i1 ? 1u : 0u) << j;
+        ic[j] = i < i1 ? i : i1 - 1;
+      }
+      if (c.valid) {
+        uint32_t byte[ROUNDS];
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) byte[j] = c.valid[ic[j] >> 3];
+        vb = 0;
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) vb |= ((byte[j] >> (ic[j] & 7)) & 1u) << j;
+      }
+      uint64_t v[ROUNDS];
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) v[j] = kwiden(TY, c.values, ic[j]);
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j)
+        if ((ok & vb) >> j & 1u) atomicAdd(&bh[bucket_of(fmix_bij(exact_canon(a.ks, v[j])))], 1u);
+    }
+  };
+  switch (c.type) {  // block-uniform: one unrolled load loop per width
+    case DQ_INT8: tile_loop(std::integral_constant<int, DQ_INT8>{}); break;
+    case DQ_INT16: tile_loop(std::integral_constant<int, DQ_INT16>{}); break;
+    case DQ_INT32: tile_loop(std::integral_constant<int, DQ_INT32>{}); break;
+    case DQ_FLOAT32: tile_loop(std::integral_constant<int, DQ_FLOAT32>{}); break;
+    case DQ_FLOAT64: tile_loop(std::integral_constant<int, DQ_FLOAT64>{}); break;
+    case DQ_BOOL: tile_loop(std::integral_constant<int, DQ_BOOL>{}); break;
+    default: tile_loop(std::integral_constant<int, DQ_INT64>{}); break;
+  }
+  __syncthreads();
+  for (int i = tid; i < kBuckets; i += kPreThreads) ph[(int64_t)blockIdx.x * kBuckets + i] = bh[i];
+}
+
+// Per bucket (one block each): ph[*][b] -> its exclusive prefix over the workgroups, tot[b] = sum.
+__global__ void __launch_bounds__(256) freq_prepass_scan(uint32_t* ph, int64_t n_wg, uint32_t* tot) {
+  __shared__ uint32_t s_wave[4];
+  const int b = blockIdx.x;
+  uint32_t carry = 0;
+  for (int64_t w0 = 0; w0 < n_wg; w0 += 256) {
+    const int64_t w = w0 + threadIdx.x;
+    const uint32_t v = w < n_wg ? ph[w * kBuckets + b] : 0u;
+    uint32_t t;
+    const uint32_t ex = block_excl_scan(v, s_wave, t);
+    if (w < n_wg) ph[w * kBuckets + b] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) tot[b] = carry;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2102,6 +2185,415 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
   if (collisions) atomicAdd(&a.counters[C_COLLISIONS], collisions);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Phase C, exact mode (one fixed-width key: the hash is the key, no arena, no representative).
+//
+// The generic kernel above spends most of its issue slots on per-partition work that does not
+// depend on the records: a pass over all kTableC slots (empty ones included), a 4-deep candidate
+// insertion per occupied slot, three barriers.  Here every claim appends its slot to an LDS list
+// (one LDS atomic per wave and insert round), so the statistics pass visits the partition's groups
+// only, and the work per partition is:
+//   inserts: the first probe of all of a thread's records in flight together (linear probing
+//            after that);                                                        [barrier 1]
+//   stats:   over the list -- Σ[c==1] in a register, counts 2..63 into an LDS histogram (one log
+//            per distinct count), larger counts' terms summed; each slot is cleared as it is read;
+//            Histogram candidates: the first kCand groups of the list, plus a per-lane top-kCand of
+//            the groups with count > 1;                                          [barrier 2]
+// and the partition's statistics and candidates are written by wave 0 during the NEXT item, right
+// after that item's loads are issued.  (Global stores count in vmcnt like loads, so a store issued
+// at the end of an item made the next item's wait for its prefetched records a wait for the store
+// too: a full store round trip per item.  Every vector-memory operation of an item is now issued
+// at its start, one item before anything waits for it.)
+// Only when a partition's largest count exceeds 1 AND Histogram wants candidates do kCand more
+// rounds (with barriers) pick its exact top kCand; a mostly-unique key never takes them.
+// Entropy stays deterministic: count-1 groups are counted, counts < kSmallCounts histogrammed, and
+// the partials are added in a fixed order.  Same outputs as freq_phaseC<false>.
+// DBG: DQ_FREQ_DEBUG=2's instantiation, workgroup 0 stamps each item's phases (wall clock).
+// ------------------------------------------------------------------------------------------------
+// PK: packed slots, for tables partitioned to the full kMaxSubBits (a partition then fixes the
+// top kBucketBits + kMaxSubBits = 19 hash bits): one u64 per slot = count << 45 | the key's low 45
+// hash bits, so a claim installs key AND count in one CAS, a duplicate adds count << 45, and the
+// table holds 8192 slots in the LDS of 4096 two-word slots (load ~0.22 instead of ~0.44: fewer
+// probe rounds, the wave's longest probe sequence bounding every round).  A count field can only
+// overflow when some record carries a count >= 128 or the partition has more than 4096 records;
+// such an item is handed on (an ovf entry of the whole partition, f = 0) to the two-word kernel.
+template <bool DBG, bool PK>
+__global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
+  constexpr int KT = PK ? 8192 : FM<false>::kTableC, NW = kCThreads / 64, PF = kPF<false>;
+  constexpr int KL = PK ? 2 * PF * kCThreads : KT;  // list capacity
+  constexpr uint64_t M45 = (1ULL << 45) - 1;
+  __shared__ uint64_t tkey[KT], tcnt[PK ? 1 : KT];
+  __shared__ uint16_t list[KL];
+  __shared__ uint32_t s_n[2], s_ovf[2];
+  __shared__ unsigned long long s_spec[2];
+  __shared__ uint32_t s_chist[2][kSmallCounts];
+  __shared__ unsigned long long s_wun[2][NW], s_wmax[2][NW];
+  __shared__ double s_went[2][NW];
+  __shared__ double s_term[kSmallCounts];
+  __shared__ uint64_t s_fk[2][kCand], s_fc[2][kCand];  // the list's first groups
+  __shared__ unsigned long long s_top[kCand];
+  __shared__ unsigned long long s_gbase;
+  // an item's outputs, written during the next item: partition, first group slot, #groups, flags
+  __shared__ uint32_t s_tp[2], s_tg[2], s_tfl[2];
+  __shared__ uint64_t s_tr0[2];
+  enum { TF_VALID = 1, TF_SUB = 2, TF_CANDFAST = 4 };
+
+  const int tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
+  for (int i = tid; i < KT; i += kCThreads) {
+    tkey[i] = kEmptyKey;
+    if (!PK) tcnt[i] = 0;
+  }
+  if (tid < 2) {
+    s_n[tid] = 0;
+    s_ovf[tid] = 0;
+    s_spec[tid] = 0;
+    s_tfl[tid] = 0;
+  }
+  if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
+  if (tid < kSmallCounts) s_term[tid] = tid ? entropy_term((uint64_t)tid, a.num_rows) : 0.0;
+  if (tid < kCand) s_top[tid] = 0;
+  const bool keep = a.groups != nullptr;
+
+  // Wave 0: the statistics and candidates of the item of parity q (its words stay untouched until
+  // the item after next resets them, behind that item's barrier 1).
+  auto tail = [&](uint32_t q) {
+    const uint32_t fl = s_tfl[q];
+    if (!(fl & TF_VALID)) return;
+    const uint32_t p = s_tp[q], gtot = s_tg[q];
+    const bool sub = (fl & TF_SUB) != 0;
+    if ((fl & TF_CANDFAST) && lane < kCand)  // every count is 1: the list's first groups
+      a.cand[(uint64_t)p * kCand + lane] =
+          (uint32_t)lane < gtot ? Group{s_fk[q][lane], s_fc[q][lane], 0} : Group{0, 0, 0};
+    const uint32_t hc = lane > 1 ? s_chist[q][lane] : 0u;
+    double t = hc ? (double)hc * s_term[lane] : 0.0;
+    t = __ockl_wfred_add_f64(t);
+    if (lane == 0) {
+      uint64_t utot = 0;
+      double etot = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        utot += s_wun[q][w];
+        etot += s_went[q][w];
+      }
+      etot += t;
+      if (utot) etot += (double)utot * s_term[1];
+      if (sub) {
+        if (!keep) atomicAdd(&a.part_groups[p], (unsigned long long)gtot);
+        if (utot) atomicAdd(&a.part_unique[p], (unsigned long long)utot);
+        if (etot != 0.0) atomicAdd(&a.part_entropy[p], etot);
+      } else {
+        a.part_groups[p] = gtot;
+        a.part_unique[p] = utot;
+        a.part_entropy[p] = etot;
+      }
+      if (keep) a.part_off[p] = s_tr0[q];
+    }
+  };
+
+  // One item ahead, issued at the top of an item and taken over at its end: the records of item
+  // i + 1 and the bounds of item i + 2 are in flight through all of item i.
+  CBounds nb;
+  CItem<false> cur;
+  c_bounds(a, blockIdx.x, nb);
+  c_fetch<false>(a, blockIdx.x, nb, cur);
+  c_bounds(a, blockIdx.x + gridDim.x, nb);
+  __syncthreads();
+
+  uint32_t par = 0;
+  int item = 0;
+  auto mark = [&](int kk) {
+    if constexpr (DBG)
+      if (blockIdx.x == 0 && tid == 0 && item < 16) a.dbg_clock[item * 8 + kk] = wall_clock64();
+  };
+  for (int wi = blockIdx.x; wi < a.n_work; wi += gridDim.x, par ^= 1u, ++item) {
+    mark(0);
+    const uint32_t p = cur.p, b = p >> a.s, f = cur.f, fv = cur.fv;
+    const uint32_t fmask = (1u << f) - 1u;
+    const uint64_t r0 = cur.r0, nrec = cur.r1 - cur.r0;
+    CItem<false> pf;
+    CBounds nb2;
+
+    // Decodes one round of (at most PF) raw records per thread, then inserts them and appends the
+    // claimed slots to the list.  Every thread calls it (the list append is wave-aggregated).
+    // `issue` runs between the two, behind scheduling barriers: the first round issues the next
+    // item's loads and the last item's stores there, after the only wait for this item's words.
+    auto insert_round = [&](const uint64_t (*w)[1], uint32_t valid, auto&& issue) {
+      uint64_t h[PF], c[PF], old[PF];
+      uint32_t slot[PF], todo = 0;
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        h[q] = xrec_h(w[q][0], b);
+        c[q] = code_count((uint32_t)(w[q][0] & 0xff));
+        slot[q] = (uint32_t)h[q] & (KT - 1);
+        const bool in = ((valid >> q) & 1u) && (f == 0 || ((uint32_t)(h[q] >> kFilterShift) & fmask) == fv);
+        if constexpr (PK) {
+          if (in && c[q] >= 128) s_ovf[par] = 1;  // a count field could overflow: hand it on
+          if (in) todo |= 1u << q;
+          h[q] = (c[q] << 45) | (h[q] & M45);  // the packed word
+        } else {
+          if (in && h[q] == kEmptyKey) atomicAdd(&s_spec[par], (unsigned long long)c[q]);
+          else if (in) todo |= 1u << q;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mark(4);
+      issue();
+      mark(5);
+      __builtin_amdgcn_sched_barrier(0);
+      // Probe rounds with every pending record's CAS in flight together (a wave takes as many
+      // rounds as its longest probe sequence, not the sum over its records); double hashing (an
+      // odd step from high hash bits) keeps those sequences short.
+      uint32_t step[PF];
+#pragma unroll
+      for (int q = 0; q < PF; ++q) step[q] = ((uint32_t)(h[q] >> 40) | 1u) & (KT - 1);
+      uint32_t mine = 0;
+      for (int pr = 0; todo && pr < KT; ++pr) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q)
+          old[q] = (todo >> q) & 1u ? atomicCAS((unsigned long long*)&tkey[slot[q]], kEmptyKey, h[q]) : 0ULL;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          if (!((todo >> q) & 1u)) continue;
+          const bool claimed = old[q] == kEmptyKey;
+          const bool match = PK ? ((old[q] ^ h[q]) & M45) == 0 : old[q] == h[q];
+          if (claimed || match) {
+            if constexpr (PK) {
+              if (!claimed) atomicAdd((unsigned long long*)&tkey[slot[q]], (unsigned long long)(c[q] << 45));
+            } else {
+              atomicAdd((unsigned long long*)&tcnt[slot[q]], (unsigned long long)c[q]);
+            }
+            if (claimed) mine |= 1u << q;
+            todo &= ~(1u << q);
+          } else {
+            slot[q] = (slot[q] + step[q]) & (KT - 1);
+          }
+        }
+      }
+      if (todo) s_ovf[par] = 1;  // the table is full
+      const uint32_t nm = (uint32_t)__builtin_popcount(mine);
+      const uint32_t incl = __ockl_wfscan_add_u32(nm, true);
+      const uint32_t wtot = __builtin_amdgcn_readlane(incl, 63);
+      if (wtot) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&s_n[par], wtot);
+        uint32_t pos = __builtin_amdgcn_readlane(base, 0) + incl - nm;
+#pragma unroll
+        for (int q = 0; q < PF; ++q)
+          if ((mine >> q) & 1u) list[pos++] = (uint16_t)slot[q];
+      }
+      mark(6);
+    };
+    const bool too_long = PK && nrec > (uint64_t)KL;  // (handed on whole, see `overflow`)
+    insert_round(cur.w, too_long ? 0u : cur.valid, [&]() {
+      c_fetch<false>(a, wi + gridDim.x, nb, pf);
+      c_bounds(a, wi + 2 * gridDim.x, nb2);
+      if (wave == 0) tail(par ^ 1u);
+    });
+    if (nrec > (uint64_t)PF * kCThreads && !too_long) {  // the rest of a long partition (rare)
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + r0;
+      for (uint64_t base = (uint64_t)PF * kCThreads; base < nrec; base += (uint64_t)PF * kCThreads) {
+        uint64_t w[PF][1];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          const uint64_t li = base + (uint64_t)q * kCThreads + tid;
+          w[q][0] = li < nrec ? src[li] : 0ULL;
+          valid |= (li < nrec ? 1u : 0u) << q;
+        }
+        insert_round(w, valid, []() {});
+      }
+    }
+    __syncthreads();  //                                                            [barrier 1]
+    mark(1);
+    const uint32_t n = s_n[par];
+    const uint64_t sc = s_spec[par];
+    // PK: any count field at risk, or a partition longer than the list: the two-word kernel
+    const bool overflow = s_ovf[par] != 0 || n > (uint32_t)(KT * 7 / 8) ||
+                          (PK && nrec > (uint64_t)KL);
+    const bool sub = f != 0;  // a recount subset: several work items add to one partition
+    const bool cand = a.want_cand && f == 0 && !overflow;
+    // the other parity's words, for item + 1 (the last item's tail has read them)
+    if (tid == 0) {
+      s_n[par ^ 1u] = 0;
+      s_ovf[par ^ 1u] = 0;
+      s_spec[par ^ 1u] = 0;
+      s_tfl[par ^ 1u] = 0;
+    }
+    if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
+    if (tid < kCand) s_top[tid] = 0;
+    const uint32_t gtot = n + (sc ? 1u : 0u);
+    uint64_t gbase = 0;
+    if (keep && sub && !overflow) {  // block-uniform
+      if (tid == 0) s_gbase = atomicAdd(&a.part_groups[p], (unsigned long long)gtot);
+      __syncthreads();
+      gbase = s_gbase;
+    }
+    const uint64_t obase = r0 + gbase;
+
+    // statistics over the list, clearing the table
+    uint64_t un = 0, mx = 0;
+    double e = 0.0;
+    uint64_t tc[kCand], tk[kCand];  // this lane's top groups with count > 1
+#pragma unroll
+    for (int q = 0; q < kCand; ++q) tc[q] = tk[q] = 0;
+    uint64_t k1 = 0;  // a count-1 group of this lane (k1c: present)
+    bool k1c = false;
+    auto stat = [&](uint32_t i, uint64_t k, uint64_t c) {
+      if (keep) a.groups[obase + i] = Group{k, c, 0};
+      if (c == 1) ++un;
+      else if (c < kSmallCounts) atomicAdd(&s_chist[par][c], 1u);
+      else e += entropy_term(c, a.num_rows);
+      mx = c > mx ? c : mx;
+      if (cand) {
+        if (i < (uint32_t)kCand) {
+          s_fk[par][i] = k;
+          s_fc[par][i] = c;
+        }
+        if (c == 1) {
+          if (!k1c) k1 = k;
+          k1c = true;
+        } else if (c > tc[kCand - 1]) {
+#pragma unroll
+          for (int q = 0; q < kCand; ++q) {
+            if (c > tc[q]) {
+              const uint64_t c2 = tc[q], k2 = tk[q];
+              tc[q] = c;
+              tk[q] = k;
+              c = c2;
+              k = k2;
+            }
+          }
+        }
+      }
+    };
+    {  // the first 4 entries per thread with all their LDS reads in flight, then the rest
+      constexpr int U = 4;
+      uint32_t sl[U];
+      uint64_t kv[U], cv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = tid + (uint32_t)u * kCThreads;
+        sl[u] = i < n ? list[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kv[u] = tkey[sl[u]];
+        cv[u] = PK ? 0 : tcnt[sl[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = tid + (uint32_t)u * kCThreads;
+        if (i < n) {
+          tkey[sl[u]] = kEmptyKey;
+          if (!PK) tcnt[sl[u]] = 0;
+        }
+        if (PK) {  // unpack: the partition's 19 fixed hash bits over the key's 45
+          cv[u] = kv[u] >> 45;
+          kv[u] = ((uint64_t)p << 45) | (kv[u] & M45);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = tid + (uint32_t)u * kCThreads;
+        if (i < n && !overflow) stat(i, kv[u], cv[u]);
+      }
+      for (uint32_t i = tid + (uint32_t)U * kCThreads; i < n; i += kCThreads) {
+        const uint32_t s = list[i];
+        uint64_t kk = tkey[s], c = PK ? 0 : tcnt[s];
+        tkey[s] = kEmptyKey;
+        if (!PK) tcnt[s] = 0;
+        if (PK) {
+          c = kk >> 45;
+          kk = ((uint64_t)p << 45) | (kk & M45);
+        }
+        if (!overflow) stat(i, kk, c);
+      }
+    }
+    if (tid == 0 && sc && !overflow) stat(n, kEmptyKey, sc);
+    {
+      const uint64_t wun = __ockl_wfred_add_u64(un);
+      const double we = __ockl_wfred_add_f64(e);
+      const uint64_t wmx = __ockl_wfred_max_u64(mx);
+      if (lane == 0) {
+        s_wun[par][wave] = wun;
+        s_went[par][wave] = we;
+        s_wmax[par][wave] = wmx;
+      }
+    }
+    __syncthreads();  //                                                            [barrier 2]
+    mark(2);
+    if (overflow) {  // recount over two hash subsets (the table is clear already)
+      if (tid == 0 && PK) {  // the whole partition, again, by the two-word kernel
+        const unsigned int q = atomicAdd(a.ovf_n, 1u);
+        a.ovf_out[q] = FEntry{p, 0, 0, 0};
+      } else if (tid == 0) {
+        const unsigned int q = atomicAdd(a.ovf_n, 2u);
+        a.ovf_out[q] = FEntry{p, f + 1, fv, 0};
+        a.ovf_out[q + 1] = FEntry{p, f + 1, fv | (1u << f), 0};
+      }
+    } else {
+      uint64_t M = 0;
+      if (cand) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) M = s_wmax[par][w] > M ? s_wmax[par][w] : M;
+      }
+      if (cand && M > 1) {
+        // exact top kCand: each lane offers its groups with count > 1 in count order, then its
+        // count-1 group; rounds of packed block maxima (count << 16 | tid << 2 | q)
+        int taken = 0;
+        auto pack = [&]() -> uint64_t {
+          uint64_t c = 0;
+#pragma unroll
+          for (int i = 0; i < kCand; ++i) c = i == taken ? tc[i] : c;
+          if (c) return (c << 16) | ((uint64_t)tid << 2) | (uint64_t)taken;
+          return k1c ? (1ULL << 16) | ((uint64_t)tid << 2) | 3ULL : 0ULL;
+        };
+        static_assert(kCThreads <= 1024 && kCand == 4, "candidate packing");
+#pragma unroll
+        for (int r = 0; r < kCand; ++r) {
+          const uint64_t mine = pack();
+          const uint64_t wm = __ockl_wfred_max_u64(mine);
+          if (lane == 0 && wm) atomicMax(&s_top[r], (unsigned long long)wm);
+          __syncthreads();
+          const uint64_t t = s_top[r];
+          if (t && t == mine) {  // this thread's offer won the round
+            const int q = (int)(t & 3u);
+            const bool one = (uint32_t)(t >> 16) == 1u && !(taken < kCand && tc[taken]);
+            uint64_t kk = 0, cc = 0;
+#pragma unroll
+            for (int i = 0; i < kCand; ++i) {
+              kk = i == q ? tk[i] : kk;
+              cc = i == q ? tc[i] : cc;
+            }
+            if (one) {
+              kk = k1;
+              cc = 1;
+              k1c = false;
+            } else {
+              ++taken;
+            }
+            a.cand[(uint64_t)p * kCand + r] = Group{kk, cc, 0};
+          } else if (!t && tid == 0) {
+            a.cand[(uint64_t)p * kCand + r] = Group{0, 0, 0};
+          }
+        }
+      }
+      if (tid == 0) {  // this item's outputs, for the next item's wave 0
+        s_tp[par] = p;
+        s_tg[par] = gtot;
+        s_tr0[par] = r0;
+        s_tfl[par] = TF_VALID | (sub ? TF_SUB : 0u) | (cand && M <= 1 ? TF_CANDFAST : 0u);
+      }
+    }
+    mark(3);
+    cur = pf;
+    nb = nb2;
+  }
+  // the last item's outputs (its words were set before its barrier 2... and s_tfl after it)
+  __syncthreads();
+  if (wave == 0) tail(par ^ 1u);
+}
+
 // Multi-block fixed-order reduction of the per-partition statistics: block b sums its contiguous
 // range (coalesced: consecutive threads read consecutive partitions), freq_reduce_final adds the
 // blocks' partials in block order.  out = {groups, unique, entropy bits}.
@@ -2835,8 +3327,8 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       return e ? atoi(e) : 0;
     }();
     unsigned long long* clk = nullptr;
-    if (dbg >= 2 && hipMalloc(&clk, 16 * 4 * sizeof(unsigned long long)) == hipSuccess)
-      (void)hipMemset(clk, 0, 16 * 4 * sizeof(unsigned long long));
+    if (dbg >= 2 && hipMalloc(&clk, 16 * 8 * sizeof(unsigned long long)) == hipSuccess)
+      (void)hipMemset(clk, 0, 16 * 8 * sizeof(unsigned long long));
     else
       clk = nullptr;
     a.dbg_clock = clk;
@@ -2844,8 +3336,26 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, f->device);
     const unsigned persistent = (unsigned)std::max(1, cus * 2);
     unsigned grid = (unsigned)std::min<int64_t>(P, persistent);
+    static const bool old_c = [] {  // DQ_FREQ_OLDC=1: A/B hook, the generic exact kernel
+      const char* e = getenv("DQ_FREQ_OLDC");
+      return e && atoi(e) != 0;
+    }();
+    static const bool no_pk = [] {  // DQ_FREQ_NOPK=1: A/B hook, no packed-slot first pass
+      const char* e = getenv("DQ_FREQ_NOPK");
+      return e && atoi(e) != 0;
+    }();
     for (int round = 0; round < 24; ++round) {
-      if (f->exact)
+      // packed slots: the first pass of a table partitioned to the full depth (19 fixed bits)
+      const bool pk = round == 0 && f->s_bits == kMaxSubBits && !no_pk;
+      if (f->exact && !old_c && clk && pk)
+        hipLaunchKernelGGL((freq_phaseC_x<true, true>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
+      else if (f->exact && !old_c && clk)
+        hipLaunchKernelGGL((freq_phaseC_x<true, false>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
+      else if (f->exact && !old_c && pk)
+        hipLaunchKernelGGL((freq_phaseC_x<false, true>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
+      else if (f->exact && !old_c)
+        hipLaunchKernelGGL((freq_phaseC_x<false, false>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
+      else if (f->exact)
         hipLaunchKernelGGL(freq_phaseC<false>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else
         hipLaunchKernelGGL(freq_phaseC<true>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
@@ -2853,7 +3363,28 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       unsigned int m = 0;
       HIP_TRY(hipStreamSynchronize(f->stream));
       HIP_TRY(hipMemcpy(&m, f->ovf_n.p, 4, hipMemcpyDeviceToHost));
-      if (clk) {  // per-item phase times of workgroup 0, us (the wall clock ticks at 100 MHz)
+      if (clk && f->exact && !old_c) {  // freq_phaseC_x: 8 stamps per item
+        unsigned long long h[16 * 8];
+        (void)hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost);
+        double acc[7] = {0, 0, 0, 0, 0, 0, 0};
+        int ni = 0;
+        // 0 top, 4 decoded (top wait), 5 issued (+ tail), 6 inserted, 1 barrier 1, 2 barrier 2, 3 end
+        const int order[8] = {0, 4, 5, 6, 1, 2, 3, 8};
+        for (int i = 0; i + 1 < 16; ++i) {
+          if (!h[(i + 1) * 8]) break;
+          for (int q = 0; q < 7; ++q) {
+            const unsigned long long t1 = order[q + 1] == 8 ? h[(i + 1) * 8] : h[i * 8 + order[q + 1]];
+            acc[q] += (double)(t1 - h[i * 8 + order[q]]) / 100.0;
+          }
+          ++ni;
+        }
+        if (ni)
+          fprintf(stderr, "dq_freq phase C_x wg0 per item (us): wait+decode %.2f issue+tail %.2f "
+                  "cas+append %.2f barrier1 %.2f stats %.2f cand %.2f gap %.2f (%d items)\n",
+                  acc[0] / ni, acc[1] / ni, acc[2] / ni, acc[3] / ni, acc[4] / ni, acc[5] / ni,
+                  acc[6] / ni, ni);
+        (void)hipMemset(clk, 0, sizeof(h));
+      } else if (clk) {  // per-item phase times of workgroup 0, us (the wall clock ticks at 100 MHz)
         unsigned long long h[16 * 4];
         (void)hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost);
         double acc[4] = {0, 0, 0, 0};
@@ -2879,7 +3410,8 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
         return fail(DQ_ERR_OUT_OF_MEMORY, "frequency partition does not fit");
       }
       // recount the overflowing partitions over disjoint hash subsets
-      f->recounted = true;
+      // (a packed-slot first pass hands whole partitions on: no hash subsets yet)
+      if (!(round == 0 && f->s_bits == kMaxSubBits && !no_pk && f->exact && !old_c)) f->recounted = true;
       f->ovf_a.swap(f->ovf_b);  // ovf_b = this round's entries
       HIP_TRY(f->ovf_a.ensure(2 * (size_t)m));
       HIP_TRY(hipMemsetAsync(f->ovf_n.p, 0, 4, f->stream));

@@ -295,6 +295,35 @@ def test_partition_depths_and_recount(target, gpu_device, monkeypatch):
         assert [c for _, c in top] == sorted(exp.values(), reverse=True)[:5]
 
 
+@pytest.mark.parametrize("heavy", [0.02, 0.3])
+def test_packed_phase_c_hands_on_heavy_partitions(heavy, gpu_device, monkeypatch):
+    """Exact mode partitioned to the full depth (s = 10) counts in packed slots (count << 45 |
+    key); a partition holding a record whose count is >= 128 (a heavy key collapsed in phase A)
+    or more than 4096 records is handed on whole to the two-word kernel.  Mixed heavy keys and
+    unique keys must give the oracle's groups, statistics and top-k either way."""
+    monkeypatch.setenv("DQ_FREQ_PARTITION_TARGET", "1")
+    n = 200_000
+    rng = np.random.default_rng(5)
+    ids = rng.permutation(n).astype(np.int64) * 3
+    hv = rng.random(n) < heavy
+    ids[hv] = rng.choice(np.array([7, 11, 13], dtype=np.int64), size=int(hv.sum()))
+    t = pa.table({"id": pa.array(ids)})
+    ft = _freq_table(t, ["id"], gpu_device)
+    exp = {}
+    for v in ids.tolist():
+        exp[v] = exp.get(v, 0) + 1
+    s = ft.summarize()
+    assert s.n_groups == len(exp)
+    assert s.n_unique == sum(1 for c in exp.values() if c == 1)
+    ent = -sum((c / n) * math.log(c / n) for c in exp.values())
+    assert abs(s.entropy - ent) <= 1e-12 * abs(ent)
+    top = ft.topk(6)
+    assert [c for _, c in top] == sorted(exp.values(), reverse=True)[:6]
+    for (key,), c in top:
+        assert exp[key] == c
+    assert {k[0]: c for k, c in ft.export()} == exp
+
+
 @pytest.mark.parametrize("col,nulls", [("id", 0.05), ("id", 0.0), ("s", 0.0)])
 def test_histogram_table_serves_grouping(col, nulls, gpu_device):
     """The runner groups a column once for Histogram(col) and its grouping analyzers when
