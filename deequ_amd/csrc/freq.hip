@@ -362,6 +362,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   // the instruction cache).
   __shared__ uint64_t stash[T * W];
   __shared__ uint64_t scnt[FROM_REC ? kThreads : 1];
+  // exact rows into bucket pieces (a.pstart): each bucket's next record slot in the batch region
+  constexpr bool XP = !HASHED && !FROM_REC;
+  __shared__ uint32_t wcur[XP ? kBuckets : 1];
 
   const int tid = threadIdx.x;
   if constexpr (STR1) {
@@ -388,6 +391,27 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   }
   for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
   if (tid == 0) s_bypass = 0;
+  const bool pieces = XP && a.pstart != nullptr;
+  if constexpr (XP) {
+    if (pieces) {
+      // bucket b of the batch starts at the prefix of the batch's bucket totals; this workgroup's
+      // piece of it at the prefix of the earlier workgroups' rows of b (freq_prepass_scan)
+      uint32_t all;
+      const uint32_t tot = tid < kBuckets ? a.ptot[tid] : 0u;
+      const uint32_t bb = block_excl_scan(tot, s_wave, all);
+      if (tid < kBuckets) {
+        const uint32_t st = bb + a.ph[(int64_t)blockIdx.x * kBuckets + tid];
+        wcur[tid] = st;
+        a.pstart[(int64_t)blockIdx.x * kBuckets + tid] = st;
+      }
+      // the batch's chunk rows (tiles and workgroup chunks) hold no records: empty histograms
+      const int64_t nt = (a.n_items + a.tile_items - 1) / a.tile_items;
+      const int64_t r1 = min((int64_t)(blockIdx.x + 1) * a.tiles_per_wg, nt);
+      for (int64_t r = (int64_t)blockIdx.x * a.tiles_per_wg; r < r1; ++r)
+        for (int i = tid; i < kHistRow; i += kThreads) a.hist[r * kHistRow + i] = 0;
+      for (int i = tid; i < kHistRow; i += kThreads) a.hist[(nt + blockIdx.x) * kHistRow + i] = 0;
+    }
+  }
   unsigned long long nulls = 0, nullg = 0;
   // debug event counts (rare events) in LDS: dedupe is an out-of-line lambda, and locals it
   // updated through its captures lived in scratch
@@ -807,7 +831,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     mark(t, 2);
     if (!any_raw) {  // every row collapsed into the dedupe table: an empty chunk, no sort
       uint16_t* hrow = a.hist + t * kHistRow;
-      for (int i = tid; i < kHistRow; i += kThreads) hrow[i] = 0;
+      if (!pieces)
+        for (int i = tid; i < kHistRow; i += kThreads) hrow[i] = 0;
       mark(t, 3);
       mark(t, 4);
       continue;
@@ -823,6 +848,46 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         }
     }
     // 3. counting sort of the raw rows into the tile's chunk
+    if constexpr (XP) {
+      if (pieces) {
+        // ... or, bucket pieces: sorted in LDS by bucket, then written to each bucket's next
+        // slots in the batch region (runs of ~16 records per bucket and tile, each continuing
+        // the workgroup's piece of that bucket)
+        __syncthreads();
+        uint32_t ctotal;
+        const uint32_t cnt = tid < kBuckets ? bh[tid] : 0u;
+        const uint32_t ex = block_excl_scan(cnt, s_wave, ctotal);
+        if (tid < kBuckets) bcur[tid] = ex;
+        __syncthreads();
+        mark(t, 3);
+        uint32_t pv[ROUNDS];
+        uint64_t hv[ROUNDS];
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) {
+          if (!((raw >> j) & 1u)) continue;
+          hv[j] = stash[j * kThreads + tid];
+          pv[j] = atomicAdd(&bcur[bucket_of(hv[j])], 1u);
+        }
+        __syncthreads();
+        if (tid < kBuckets) {  // bcur: the bucket's region slot minus its first sorted position
+          const uint32_t c = bh[tid], st = bcur[tid] - c;
+          bcur[tid] = wcur[tid] - st;
+          wcur[tid] += c;
+        }
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j)
+          if ((raw >> j) & 1u) stash[pv[j]] = hv[j];
+        __syncthreads();
+        uint64_t* out = reinterpret_cast<uint64_t*>(a.recs);
+        for (uint32_t i = tid; i < ctotal; i += kThreads) {
+          const uint64_t hh = stash[i];
+          out[(uint32_t)(bcur[bucket_of(hh)] + i)] = (hh << 8) | 1u;  // the count-1 digit code
+        }
+        end_chunk();
+        mark(t, 4);
+        continue;
+      }
+    }
     const uint32_t ctotal = begin_chunk(t, need);
     mark(t, 3);
     if constexpr (!HASHED && !FROM_REC) {
@@ -863,6 +928,28 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     }
     end_chunk();
     mark(t, 4);
+  }
+  if constexpr (XP) {
+    if (pieces) {  // the collapsed groups into their buckets' pieces, then the pieces' lengths
+      uint64_t* out = reinterpret_cast<uint64_t*>(a.recs);
+      __syncthreads();
+      for (int sl = tid; sl < D; sl += kThreads) {
+        const uint64_t k = dkey[sl];
+        if (k == kEmptyKey) continue;
+        const uint32_t b = bucket_of(k);
+        for_digits(dcnt[sl], [&](uint32_t code) { out[atomicAdd(&wcur[b], 1u)] = (k << 8) | code; });
+      }
+      __syncthreads();
+      if (tid < kBuckets)
+        a.plen[(int64_t)blockIdx.x * kBuckets + tid] =
+            wcur[tid] - a.pstart[(int64_t)blockIdx.x * kBuckets + tid];
+      wave_count(&a.counters[C_NULL_ROWS], nulls);
+      wave_count(&a.counters[C_NULL_GROUP], nullg);
+      __syncthreads();
+      if (tid < 3 && s_dbg[tid]) atomicAdd(&a.counters[C_DBG_NOTREADY + tid], (unsigned long long)s_dbg[tid]);
+      wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
+      return;
+    }
   }
   // the collapsed groups of the whole range -> this workgroup's own chunk
   uint64_t need = 0;
@@ -1367,73 +1454,111 @@ __global__ void __launch_bounds__(kThreads) freq_chunk_ids(const uint16_t* hist,
   if (f) ids[boff[blockIdx.x] + pos] = (uint32_t)c;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Segments.  Phase B reads each bucket as a list of segments (record ranges of `recs`): the
+// bucket's part of every non-empty chunk (hashed mode, records path: runs of a few records) and
+// every bucket piece of the exact batches (runs of ~250 records, adjacent ones contiguous).  One
+// array pair per bucket, J columns: segS = first record, segP = length, then (freq_seg_scan) the
+// list compacted -- empty segments dropped, contiguous neighbours merged (an exact batch's bucket
+// is then ONE segment) -- with segP the exclusive record prefix and nseg the count.
+// ------------------------------------------------------------------------------------------------
 // cmap (optional): the chunk each of the n rows stands for (the non-empty chunks, in order)
 __global__ void __launch_bounds__(256) freq_hist_transpose(const uint16_t* hist, int64_t n,
-                                                           const uint32_t* cmap, uint16_t* lenT,
-                                                           uint16_t* offT) {
-  __shared__ uint16_t tile[64][kHistRow + 1];
+                                                           const uint32_t* cmap, int tile, int64_t J,
+                                                           unsigned long long* segS, uint32_t* segP) {
+  __shared__ uint16_t tl[64][kHistRow + 1];
+  __shared__ uint32_t tc[64];
   const int64_t c0 = (int64_t)blockIdx.x * 64;
   for (int idx = threadIdx.x; idx < 64 * kHistRow; idx += 256) {
     const int cc = idx / kHistRow, b = idx % kHistRow;
     const int64_t c = c0 + cc;
-    tile[cc][b] = c < n ? hist[(cmap ? (int64_t)cmap[c] : c) * kHistRow + b] : 0;
+    tl[cc][b] = c < n ? hist[(cmap ? (int64_t)cmap[c] : c) * kHistRow + b] : 0;
+  }
+  if (threadIdx.x < 64) {
+    const int64_t c = c0 + threadIdx.x;
+    tc[threadIdx.x] = c < n ? (cmap ? cmap[c] : (uint32_t)c) : 0u;
   }
   __syncthreads();
   for (int idx = threadIdx.x; idx < kBuckets * 64; idx += 256) {
     const int b = idx / 64, cc = idx % 64;
     if (c0 + cc < n) {
-      lenT[(int64_t)b * n + c0 + cc] = (uint16_t)(tile[cc][b + 1] - tile[cc][b]);
-      offT[(int64_t)b * n + c0 + cc] = tile[cc][b];
+      segS[(int64_t)b * J + c0 + cc] = (unsigned long long)tc[cc] * (unsigned)tile + tl[cc][b];
+      segP[(int64_t)b * (J + 1) + c0 + cc] = (uint32_t)(tl[cc][b + 1] - tl[cc][b]);
     }
   }
 }
 
-// prefT[b][0..n] = exclusive prefix of lenT[b][*] (prefT[b][n] = bucket total)
-__global__ void __launch_bounds__(kThreads) freq_bucket_scan(const uint16_t* lenT, int64_t n,
-                                                             uint32_t* prefT,
-                                                             unsigned long long* totals) {
+// The bucket pieces of n_prow piece rows -> columns [col0, col0 + n_prow).
+__global__ void __launch_bounds__(256) freq_piece_transpose(const uint32_t* pstart, const uint32_t* plen,
+                                                            const unsigned long long* pbase, int64_t n_prow,
+                                                            int64_t col0, int64_t J,
+                                                            unsigned long long* segS, uint32_t* segP) {
+  const int64_t total = n_prow * kBuckets;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i % n_prow, b = i / n_prow;  // consecutive threads: consecutive columns
+    const int64_t src = r * kBuckets + b;
+    segS[b * J + col0 + r] = pbase[r] + pstart[src];
+    segP[b * (J + 1) + col0 + r] = plen[src];
+  }
+}
+
+// Per bucket (one block each): compacts the bucket's J segments in place -- drops the empty ones,
+// merges a segment into its predecessor entry when it starts where that one ends -- and turns the
+// lengths into the exclusive record prefix (segP[nseg] = the bucket's records).
+__global__ void __launch_bounds__(kThreads) freq_seg_scan(unsigned long long* segS, uint32_t* segP,
+                                                          int64_t J, uint32_t* nseg,
+                                                          unsigned long long* totals) {
   __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ unsigned long long s_end[kThreads];  // each entry's end (start + length), or ~0
+  __shared__ unsigned long long s_carry_end;
   const int b = blockIdx.x;
-  const uint16_t* len = lenT + (int64_t)b * n;
-  uint32_t* pre = prefT + (int64_t)b * (n + 1);
-  uint32_t carry = 0;
-  constexpr int PER = 8;
-  for (int64_t base = 0; base < n; base += (int64_t)kThreads * PER) {
-    uint32_t v[PER], sum = 0;
-    const int64_t my = base + (int64_t)threadIdx.x * PER;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      v[k] = my + k < n ? len[my + k] : 0u;
-      sum += v[k];
+  unsigned long long* S = segS + (int64_t)b * J;
+  uint32_t* P = segP + (int64_t)b * (J + 1);
+  uint32_t carry_m = 0, carry_r = 0;
+  if (threadIdx.x == 0) s_carry_end = ~0ULL;
+  for (int64_t base = 0; base < J; base += kThreads) {
+    const int64_t j = base + threadIdx.x;
+    const bool in = j < J;
+    const uint32_t len = in ? P[j] : 0u;
+    const unsigned long long st = in ? S[j] : 0ULL;
+    s_end[threadIdx.x] = len ? st + len : ~0ULL;
+    __syncthreads();
+    const unsigned long long prev_end = threadIdx.x ? s_end[threadIdx.x - 1] : s_carry_end;
+    const uint32_t fresh = len && prev_end != st ? 1u : 0u;  // starts a compacted segment
+    uint32_t tm, tr;
+    const uint32_t m = block_excl_scan(fresh, s_wave, tm) + carry_m;
+    const uint32_t r = block_excl_scan(len, s_wave, tr) + carry_r;
+    // (every read of this round is done: the barriers of the scans)
+    if (fresh) {
+      S[m] = st;
+      P[m] = r;
     }
-    uint32_t tot;
-    uint32_t ex = block_excl_scan(sum, s_wave, tot) + carry;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      if (my + k < n) pre[my + k] = ex;
-      ex += v[k];
-    }
-    carry += tot;
+    if (threadIdx.x == kThreads - 1) s_carry_end = s_end[kThreads - 1];
+    carry_m += tm;
+    carry_r += tr;
+    __syncthreads();
   }
   if (threadIdx.x == 0) {
-    pre[n] = carry;
-    totals[b] = carry;
+    P[carry_m] = carry_r;
+    nseg[b] = carry_m;
+    totals[b] = carry_r;
   }
 }
 
-// unit_c0[unit_start[b] + u] = first chunk whose bucket-b prefix reaches u*H (the unit's first
-// chunk), unit_b[unit] = b; units without a chunk start keep c0 = n (empty).
-__global__ void __launch_bounds__(256) freq_unit_map(const uint32_t* prefT, int64_t n,
+// unit_c0[unit_start[b] + u] = the compacted segment holding the bucket's record u*H (units are
+// record ranges [u*H, (u+1)*H) of the bucket), unit_b[unit] = b.
+__global__ void __launch_bounds__(256) freq_unit_map(const uint32_t* segP, int64_t J, const uint32_t* nseg,
                                                      const uint32_t* unit_start, uint32_t H,
                                                      uint32_t* unit_c0, uint16_t* unit_b) {
   const int b = blockIdx.y;
   const uint32_t ub = unit_start[b], U = unit_start[b + 1] - ub;
-  const uint32_t* pre = prefT + (int64_t)b * (n + 1);
+  const uint32_t* P = segP + (int64_t)b * (J + 1);
+  const int64_t n = nseg[b];
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
        c += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t uprev = c ? (int64_t)(pre[c - 1] / H) : -1;
-    const int64_t ucur = min((int64_t)(pre[c] / H), (int64_t)U - 1);
-    for (int64_t u = uprev + 1; u <= ucur; ++u) unit_c0[ub + u] = (uint32_t)c;
+    const uint64_t lo = P[c], hi = P[c + 1];
+    for (uint64_t u = (lo + H - 1) / H; u * H < hi && u < U; ++u) unit_c0[ub + u] = (uint32_t)c;
   }
   if (blockIdx.x == 0)
     for (uint32_t u = threadIdx.x; u < U; u += blockDim.x) unit_b[ub + u] = (uint16_t)b;
@@ -1442,21 +1567,21 @@ __global__ void __launch_bounds__(256) freq_unit_map(const uint32_t* prefT, int6
 // ------------------------------------------------------------------------------------------------
 // Phase B: a bucket's records -> partition-contiguous records (radix scatter by the next s bits)
 //
-// A bucket's records are cut into units of whole chunk segments (~2 tiles each).  B1 counts each
-// unit's records per sub-bucket, B2 turns the counts into each unit's offsets inside every
+// A bucket's records are cut into units of H records (ranges of its segment list).  B1 counts
+// each unit's records per sub-bucket, B2 turns the counts into each unit's offsets inside every
 // partition (a scan over the bucket's units per sub-bucket) and the partitions' sizes, and B3
 // re-reads the unit and writes every record to its final place: a partition's records end up in
-// one contiguous range, written as runs of ~32 records per (unit, partition) whose neighbours
-// come from the neighbouring units of the same XCD (units are handed out XCD-contiguously, so a
-// partition's runs meet in one L2).
+// one contiguous range, written as runs of (records per unit / 2^s) per (unit, partition) whose
+// neighbours come from the neighbouring units of the same XCD (units are handed out
+// XCD-contiguously, so a partition's runs meet in one L2).
 // ------------------------------------------------------------------------------------------------
 struct BArgs {
   const uint8_t* recs;
-  const uint32_t* chunk_id;  // chunk of each (compacted) chunk row, or nullptr: the identity
-  const uint16_t* lenT;
-  const uint16_t* offT;
-  const uint32_t* prefT;
-  int64_t n_chunks;
+  const unsigned long long* segS;  // [kBuckets][J] compacted segment starts
+  const uint32_t* segP;            // [kBuckets][J + 1] their exclusive record prefix
+  const uint32_t* nseg;            // [kBuckets]
+  int64_t J;
+  uint32_t H;                      // records per unit
   const uint32_t* unit_start;
   const uint32_t* unit_c0;
   const uint16_t* unit_b;
@@ -1468,55 +1593,74 @@ struct BArgs {
 };
 
 struct UnitLds {
-  uint32_t sw_pos[kThreads];
-  uint32_t sw_c[kThreads];
-  uint16_t sw_off[kThreads];
+  uint32_t sw_pos[kThreads];             // window-local prefix of the segments' records in the unit
+  unsigned long long sw_s[kThreads];     // record index of each window segment's first such record
   uint32_t s_wave[kThreads / 64];
-  uint32_t s_b;
+  uint32_t s_b, s_lo, s_hi;
   int64_t s_c0, s_c1;
 };
 
 DQ_DEV void unit_range(const BArgs& a, uint32_t w, UnitLds& L) {
   if (threadIdx.x == 0) {
-    const int64_t n = a.n_chunks;
     const uint32_t b = a.unit_b[w];
+    const int64_t n = a.nseg[b];
+    const uint32_t* P = a.segP + (int64_t)b * (a.J + 1);
+    const uint32_t lo = (w - a.unit_start[b]) * a.H;
     L.s_b = b;
+    L.s_lo = lo;
+    L.s_hi = (uint32_t)min((uint64_t)lo + a.H, (uint64_t)P[n]);
     L.s_c0 = min((int64_t)a.unit_c0[w], n);
-    L.s_c1 = w + 1 < a.unit_start[b + 1] ? min((int64_t)a.unit_c0[w + 1], n) : n;
+    L.s_c1 = w + 1 < a.unit_start[b + 1] ? min((int64_t)a.unit_c0[w + 1] + 1, n) : n;
   }
   __syncthreads();
 }
 
-// Calls f(record words) for every record of the unit (chunk segments of bucket s_b in
-// [s_c0, s_c1)).  Every thread of the block must call it.  Each thread loads PB records before
-// it uses any (one HBM round trip per PB records; an out-of-range lane re-reads the window's last
-// record and drops it).
+// Loads the window of segments [cw, cw + kThreads) of the unit: each one's records inside the
+// unit's range, as an exclusive prefix (sw_pos) and a first record (sw_s).  Returns the window's
+// records; every thread of the block must call it.
+DQ_DEV uint32_t unit_window(const BArgs& a, UnitLds& L, int64_t cw, uint32_t& nwin) {
+  const int tid = threadIdx.x;
+  const int64_t c = cw + tid, c1 = L.s_c1;
+  uint32_t len = 0;
+  unsigned long long st = 0;
+  if (c < c1) {
+    const uint32_t* P = a.segP + (int64_t)L.s_b * (a.J + 1);
+    const uint32_t ps = P[c], pe = P[c + 1];
+    const uint32_t a0 = max(ps, L.s_lo), a1 = min(pe, L.s_hi);
+    len = a1 > a0 ? a1 - a0 : 0u;
+    st = a.segS[(int64_t)L.s_b * a.J + c] + (a0 - ps);
+  }
+  uint32_t wtot;
+  const uint32_t pos = block_excl_scan(len, L.s_wave, wtot);
+  L.sw_pos[tid] = pos;
+  L.sw_s[tid] = st;
+  nwin = (uint32_t)min((int64_t)kThreads, c1 - cw);
+  __syncthreads();
+  return wtot;
+}
+
+DQ_DEV int64_t window_rec(const UnitLds& L, uint32_t nwin, uint32_t li) {
+  const uint32_t j = seg_of(L.sw_pos, nwin, li);
+  return (int64_t)L.sw_s[j] + (li - L.sw_pos[j]);
+}
+
+// Calls f(record words) for every record of the unit.  Every thread of the block must call it.
+// Each thread loads PB records before it uses any (one HBM round trip per PB records; an
+// out-of-range lane re-reads the window's last record and drops it).
 template <bool HASHED, typename F>
 DQ_DEV void for_unit_records(const BArgs& a, UnitLds& L, F&& f) {
   constexpr int W = FM<HASHED>::kRB / 8, PB = 8;
   const int tid = threadIdx.x;
-  const int64_t n = a.n_chunks, c0 = L.s_c0, c1 = L.s_c1;
-  const uint16_t* lenb = a.lenT + (int64_t)L.s_b * n;
-  const uint16_t* offb = a.offT + (int64_t)L.s_b * n;
-  for (int64_t cw = c0; cw < c1; cw += kThreads) {
-    const int64_t c = cw + tid;
-    const uint32_t len = c < c1 ? lenb[c] : 0u;
-    uint32_t wtot;
-    const uint32_t pos = block_excl_scan(len, L.s_wave, wtot);
-    L.sw_pos[tid] = pos;
-    L.sw_c[tid] = c < c1 ? (a.chunk_id ? a.chunk_id[c] : (uint32_t)c) : 0u;  // the chunk itself
-    L.sw_off[tid] = c < c1 ? offb[c] : 0;
-    __syncthreads();
-    const uint32_t nwin = (uint32_t)min((int64_t)kThreads, c1 - cw);
+  for (int64_t cw = L.s_c0; cw < L.s_c1; cw += kThreads) {
+    uint32_t nwin;
+    const uint32_t wtot = unit_window(a, L, cw, nwin);
     for (uint32_t base = 0; base < wtot; base += (uint32_t)PB * kThreads) {
       uint64_t rv[PB][W];
 #pragma unroll
       for (int k = 0; k < PB; ++k) {
         uint32_t li = base + (uint32_t)k * kThreads + tid;
         li = li < wtot ? li : wtot - 1;
-        const uint32_t j = seg_of(L.sw_pos, nwin, li);
-        const int64_t rec = (int64_t)L.sw_c[j] * FM<HASHED>::kTile + L.sw_off[j] + (li - L.sw_pos[j]);
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + rec * W;
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + window_rec(L, nwin, li) * W;
 #pragma unroll
         for (int x = 0; x < W; ++x) rv[k][x] = src[x];
       }
@@ -1619,18 +1763,9 @@ __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter(BArgs a) {
   const uint32_t* row = a.uhist + (int64_t)w * S;
   for (int i = tid; i < S; i += kThreads) cur[i] = a.part_base[(uint64_t)L.s_b * S + i] + row[i];
   uint64_t* out = reinterpret_cast<uint64_t*>(a.recsB);
-  const int64_t n = a.n_chunks, c0 = L.s_c0, c1 = L.s_c1;
-  const uint16_t* lenb = a.lenT + (int64_t)L.s_b * n;
-  const uint16_t* offb = a.offT + (int64_t)L.s_b * n;
-  for (int64_t cw = c0; cw < c1; cw += kThreads) {  // windows of chunk segments
-    const int64_t c = cw + tid;
-    const uint32_t len = c < c1 ? lenb[c] : 0u;
-    uint32_t wtot;
-    const uint32_t pos = block_excl_scan(len, L.s_wave, wtot);
-    L.sw_pos[tid] = pos;
-    L.sw_c[tid] = c < c1 ? (a.chunk_id ? a.chunk_id[c] : (uint32_t)c) : 0u;
-    L.sw_off[tid] = c < c1 ? offb[c] : 0;
-    const uint32_t nwin = (uint32_t)min((int64_t)kThreads, c1 - cw);
+  for (int64_t cw = L.s_c0; cw < L.s_c1; cw += kThreads) {  // windows of segments
+    uint32_t nwin;
+    const uint32_t wtot = unit_window(a, L, cw, nwin);
     for (uint32_t base = 0; base < wtot; base += SUB) {
       const uint32_t nr = min((uint32_t)SUB, wtot - base);
       for (int i = tid; i < S; i += kThreads) hcnt[i] = 0;
@@ -1642,10 +1777,7 @@ __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter(BArgs a) {
         const uint32_t r = (uint32_t)k * kThreads + tid;
         sbv[k] = 0;
         if (r >= nr) continue;
-        const uint32_t li = base + r;
-        const uint32_t j = seg_of(L.sw_pos, nwin, li);
-        const int64_t rec = (int64_t)L.sw_c[j] * FM<HASHED>::kTile + L.sw_off[j] + (li - L.sw_pos[j]);
-        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + rec * W;
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + window_rec(L, nwin, base + r) * W;
 #pragma unroll
         for (int x = 0; x < W; ++x) rv[k][x] = src[x];
         sbv[k] = rec_sub(rv[k], a.s, HASHED);
@@ -1680,6 +1812,78 @@ __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter(BArgs a) {
       __syncthreads();
     }
     __syncthreads();
+  }
+}
+
+// B3, whole units: a unit of at most PER * kThreads records is loaded into registers, counted,
+// placed in LDS in sub-bucket order and written out once, so each (unit, partition) run leaves as
+// one stream of ~H / 2^s records (the round-based kernel above wrote it in ~H / SUB pieces, each
+// a partial line the L2 had to merge).
+template <bool HASHED, int PER>
+__global__ void __launch_bounds__(kThreads) freq_phaseB_scatter_u(BArgs a) {
+  constexpr int W = FM<HASHED>::kRB / 8;
+  constexpr int SMAX = 1 << kMaxSubBits;
+  constexpr uint32_t NR = (uint32_t)PER * kThreads;
+  __shared__ UnitLds L;
+  __shared__ unsigned long long gbs[SMAX];  // the unit's output base per sub-bucket
+  __shared__ uint32_t hcnt[SMAX];           // the unit's count, then its local base, per sub-bucket
+  __shared__ uint64_t staged[NR * W];
+  // XCD-contiguous units: workgroup g runs on XCD g % 8; XCD x takes units [x*q, (x+1)*q)
+  const uint32_t g = blockIdx.x, q = (a.n_units + 7) / 8;
+  const uint32_t w = (g & 7u) * q + (g >> 3);
+  if (w >= a.n_units) return;
+  const int S = 1 << a.s;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < S; i += kThreads) hcnt[i] = 0;
+  unit_range(a, w, L);
+  const uint32_t nrec = L.s_hi - L.s_lo;  // <= NR (the host sizes units so)
+  uint64_t rv[PER][W];
+  uint32_t done = 0;
+  for (int64_t cw = L.s_c0; cw < L.s_c1; cw += kThreads) {  // windows of segments (usually one)
+    uint32_t nwin;
+    const uint32_t wtot = unit_window(a, L, cw, nwin);
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t r = (uint32_t)j * kThreads + tid;
+      if (r >= done && r < done + wtot) {
+        const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + window_rec(L, nwin, r - done) * W;
+#pragma unroll
+        for (int x = 0; x < W; ++x) rv[j][x] = src[x];
+      }
+    }
+    done += wtot;
+    __syncthreads();
+  }
+  uint32_t lpos[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if ((uint32_t)j * kThreads + tid < nrec) lpos[j] = atomicAdd(&hcnt[rec_sub(rv[j], a.s, HASHED)], 1u);
+  __syncthreads();
+  const uint32_t cnt = tid < S ? hcnt[tid] : 0u;
+  uint32_t tot;
+  const uint32_t ex = block_excl_scan(cnt, L.s_wave, tot);  // (barriers: every count is read)
+  if (tid < S) {
+    hcnt[tid] = ex;
+    gbs[tid] = a.part_base[(uint64_t)L.s_b * S + tid] + a.uhist[(int64_t)w * S + tid];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    if ((uint32_t)j * kThreads + tid >= nrec) continue;
+    const uint32_t slot = hcnt[rec_sub(rv[j], a.s, HASHED)] + lpos[j];
+#pragma unroll
+    for (int x = 0; x < W; ++x) staged[slot * W + x] = rv[j][x];
+  }
+  __syncthreads();
+  uint64_t* out = reinterpret_cast<uint64_t*>(a.recsB);
+  for (uint32_t i = tid; i < nrec; i += kThreads) {
+    uint64_t r[W];
+#pragma unroll
+    for (int x = 0; x < W; ++x) r[x] = staged[i * W + x];
+    const uint32_t sb = rec_sub(r, a.s, HASHED);
+    const unsigned long long d = gbs[sb] + (i - hcnt[sb]);
+#pragma unroll
+    for (int x = 0; x < W; ++x) out[d * W + x] = r[x];
   }
 }
 
@@ -2846,6 +3050,13 @@ struct dq_freq {
   DevBuf<uint8_t> recs;
   DevBuf<uint16_t> hist;
   int64_t n_chunks = 0;
+  // exact rows: batch regions written bucket-major (freq_prepass_x), one piece row per phase-A
+  // workgroup: piece (r, b) = records [pbase[r] + pstart[r][b], + plen[r][b]) of `recs`
+  DevBuf<uint32_t> pstart, plen;
+  std::vector<unsigned long long> h_pbase;
+  int64_t n_prow = 0;
+  DevBuf<uint32_t> ph, ptot;  // the pre-pass's per-workgroup bucket counts (scratch)
+  DevBuf<unsigned long long> pbase;
   DevBuf<uint8_t> arena;                 // hashed: encoded keys
   DevBuf<unsigned long long> dev_words;  // counters[C_N], then the arena cursor
   DevBuf<unsigned long long> batch_tab;  // freq_phaseA_small's cross-workgroup group table
@@ -2880,10 +3091,11 @@ struct dq_freq {
   uint32_t n_units = 0;
   std::vector<unsigned long long> h_bucket_base = std::vector<unsigned long long>(kBuckets + 1, 0);
   std::vector<uint32_t> h_unit_start = std::vector<uint32_t>(kBuckets + 1, 0);
-  DevBuf<uint16_t> lenT, offT;
+  DevBuf<unsigned long long> segS;         // phase B's segments per bucket (freq_seg_scan)
+  DevBuf<uint32_t> segP, nseg;
   DevBuf<uint32_t> chunk_id;               // the non-empty chunks (finalize over those only)
   DevBuf<unsigned long long> chunk_boff, scan_tmp;
-  DevBuf<uint32_t> prefT, unit_start, unit_c0, uhist;
+  DevBuf<uint32_t> unit_start, unit_c0, uhist;
   DevBuf<uint16_t> unit_b;
   DevBuf<unsigned long long> totals, part_base;
   DevBuf<uint8_t> recsB;
@@ -3106,6 +3318,42 @@ static AArgs base_args(dq_freq* f) {
   return a;
 }
 
+// Exact rows written bucket-major per batch (DQ_FREQ_PIECES=0: the per-tile chunk layout).
+static bool pieces_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DQ_FREQ_PIECES");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// Pre-pass (rows per workgroup and bucket), its scan, and phase A into bucket pieces; the batch's
+// region is the `chunks` chunk slots at f->n_chunks (tiles + workgroup chunks >= rows records).
+static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
+  int64_t n_wg = 0;
+  phaseA_chunks(false, false, a.n_items, a.tile_items, &n_wg);
+  a.tiles_per_wg = AKeys<false, false>::kTilesPerWg;
+  HIP_TRY(f->ph.ensure((size_t)n_wg * kBuckets));
+  HIP_TRY(f->ptot.ensure(kBuckets));
+  const size_t rows_need = (size_t)(f->n_prow + n_wg) * kBuckets;
+  HIP_TRY(grow_keep(f->pstart, (size_t)f->n_prow * kBuckets, rows_need, f->stream));
+  HIP_TRY(grow_keep(f->plen, (size_t)f->n_prow * kBuckets, rows_need, f->stream));
+  hipLaunchKernelGGL(freq_prepass_x, dim3((unsigned)n_wg), dim3(kPreThreads), 0, f->stream, a, f->ph.p);
+  hipLaunchKernelGGL(freq_prepass_scan, dim3(kBuckets), dim3(256), 0, f->stream, f->ph.p, n_wg, f->ptot.p);
+  HIP_TRY(hipGetLastError());
+  a.ph = f->ph.p;
+  a.ptot = f->ptot.p;
+  a.pstart = f->pstart.p + (size_t)f->n_prow * kBuckets;
+  a.plen = f->plen.p + (size_t)f->n_prow * kBuckets;
+  launch_phaseA<false>(f, a, false);
+  HIP_TRY(hipGetLastError());
+  const unsigned long long base = (unsigned long long)f->n_chunks * f->tile;
+  for (int64_t w = 0; w < n_wg; ++w) f->h_pbase.push_back(base);
+  f->n_prow += n_wg;
+  (void)chunks;
+  return DQ_OK;
+}
+
 // ---- finalize: phase B ------------------------------------------------------------------------
 static dq_status finalize_b(dq_freq* f) {
   dq_status cs = sync_counters(f);
@@ -3140,20 +3388,33 @@ static dq_status finalize_b(dq_freq* f) {
   f->s_bits = 0;
   f->n_units = 0;
   HIP_TRY(f->part_base.ensure(kBuckets + 1));
-  if (n == 0) {
+  const int64_t J = n + f->n_prow;  // segment columns: chunks, then bucket pieces
+  if (J == 0) {
     HIP_TRY(hipMemsetAsync(f->part_base.p, 0, (kBuckets + 1) * 8, f->stream));
     f->b_valid = true;
     return DQ_OK;
   }
-  HIP_TRY(f->lenT.ensure((size_t)kBuckets * n));
-  HIP_TRY(f->offT.ensure((size_t)kBuckets * n));
-  HIP_TRY(f->prefT.ensure((size_t)kBuckets * (n + 1)));
+  HIP_TRY(f->segS.ensure((size_t)kBuckets * J));
+  HIP_TRY(f->segP.ensure((size_t)kBuckets * (J + 1)));
+  HIP_TRY(f->nseg.ensure(kBuckets));
   HIP_TRY(f->totals.ensure(kBuckets));
-  hipLaunchKernelGGL(freq_hist_transpose, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, f->stream,
-                     f->hist.p, n, cmap, f->lenT.p, f->offT.p);
-  HIP_TRY(hipGetLastError());
-  hipLaunchKernelGGL(freq_bucket_scan, dim3(kBuckets), dim3(kThreads), 0, f->stream, f->lenT.p, n,
-                     f->prefT.p, f->totals.p);
+  if (n) {
+    hipLaunchKernelGGL(freq_hist_transpose, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, f->stream,
+                       f->hist.p, n, cmap, f->tile, J, f->segS.p, f->segP.p);
+    HIP_TRY(hipGetLastError());
+  }
+  if (f->n_prow) {
+    HIP_TRY(f->pbase.ensure(f->n_prow));
+    HIP_TRY(hipMemcpyAsync(f->pbase.p, f->h_pbase.data(), f->n_prow * 8, hipMemcpyHostToDevice,
+                           f->stream));
+    const int64_t tot = f->n_prow * kBuckets;
+    hipLaunchKernelGGL(freq_piece_transpose, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 8192)),
+                       dim3(256), 0, f->stream, f->pstart.p, f->plen.p, f->pbase.p, f->n_prow, n, J,
+                       f->segS.p, f->segP.p);
+    HIP_TRY(hipGetLastError());
+  }
+  hipLaunchKernelGGL(freq_seg_scan, dim3(kBuckets), dim3(kThreads), 0, f->stream, f->segS.p, f->segP.p,
+                     J, f->nseg.p, f->totals.p);
   HIP_TRY(hipGetLastError());
   std::vector<unsigned long long> tot(kBuckets);
   HIP_TRY(hipStreamSynchronize(f->stream));
@@ -3188,8 +3449,13 @@ static dq_status finalize_b(dq_freq* f) {
             (unsigned long long)f->h_counters[C_DBG_BYPASS]);
     uint32_t nonempty = 0;
     for (auto t : tot) nonempty += t != 0;
-    fprintf(stderr, "dq_freq finalize: %s chunks=%lld records=%llu s=%d units=%u buckets=%u\n",
-            f->exact ? "exact" : "hashed", (long long)n, (unsigned long long)R, s, u, nonempty);
+    std::vector<uint32_t> ns(kBuckets);
+    (void)hipMemcpy(ns.data(), f->nseg.p, kBuckets * 4, hipMemcpyDeviceToHost);
+    uint64_t segs = 0;
+    for (auto v : ns) segs += v;
+    fprintf(stderr, "dq_freq finalize: %s chunks=%lld piece_rows=%lld segments=%llu records=%llu s=%d "
+            "units=%u buckets=%u\n", f->exact ? "exact" : "hashed", (long long)n, (long long)f->n_prow,
+            (unsigned long long)segs, (unsigned long long)R, s, u, nonempty);
   }
   const int64_t P = (int64_t)kBuckets << s;
   HIP_TRY(f->part_base.ensure(P + 1));
@@ -3206,19 +3472,19 @@ static dq_status finalize_b(dq_freq* f) {
   HIP_TRY(f->unit_c0.ensure(u));
   HIP_TRY(f->unit_b.ensure(u));
   HIP_TRY(f->uhist.ensure((size_t)u * S));
-  HIP_TRY(hipMemsetAsync(f->unit_c0.p, 0xFF, (size_t)u * 4, f->stream));
-  hipLaunchKernelGGL(freq_unit_map, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 64), kBuckets),
-                     dim3(256), 0, f->stream, f->prefT.p, n, f->unit_start.p, (uint32_t)H,
+  HIP_TRY(hipMemsetAsync(f->unit_c0.p, 0, (size_t)u * 4, f->stream));
+  hipLaunchKernelGGL(freq_unit_map, dim3((unsigned)std::min<int64_t>((J + 255) / 256, 64), kBuckets),
+                     dim3(256), 0, f->stream, f->segP.p, J, f->nseg.p, f->unit_start.p, (uint32_t)H,
                      f->unit_c0.p, f->unit_b.p);
   HIP_TRY(hipGetLastError());
   BArgs a;
   memset(&a, 0, sizeof(a));
   a.recs = f->recs.p;
-  a.chunk_id = cmap;
-  a.lenT = f->lenT.p;
-  a.offT = f->offT.p;
-  a.prefT = f->prefT.p;
-  a.n_chunks = n;
+  a.segS = f->segS.p;
+  a.segP = f->segP.p;
+  a.nseg = f->nseg.p;
+  a.J = J;
+  a.H = (uint32_t)H;
   a.unit_start = f->unit_start.p;
   a.unit_c0 = f->unit_c0.p;
   a.unit_b = f->unit_b.p;
@@ -3247,11 +3513,16 @@ static dq_status finalize_b(dq_freq* f) {
   }
   HIP_TRY(hipGetLastError());
   const unsigned grid = (u + 7) / 8 * 8;
-  static const int bsub = [] {  // DQ_FREQ_BSUB: A/B hook for the phase-B3 round size
+  static const int bsub = [] {  // DQ_FREQ_BSUB: A/B hook for the phase-B3 round size (0: whole units)
     const char* e = getenv("DQ_FREQ_BSUB");
-    return e && atoi(e) == 8192 ? 8192 : 4096;
+    return e ? atoi(e) : 0;
   }();
-  if (f->exact) {
+  constexpr uint64_t kUnitX = 16 * kThreads, kUnitH = 4 * kThreads;  // whole-unit capacities
+  if (bsub == 0 && f->exact && H <= kUnitX) {
+    hipLaunchKernelGGL((freq_phaseB_scatter_u<false, 16>), dim3(grid), dim3(kThreads), 0, f->stream, a);
+  } else if (bsub == 0 && !f->exact && H <= kUnitH) {
+    hipLaunchKernelGGL((freq_phaseB_scatter_u<true, 4>), dim3(grid), dim3(kThreads), 0, f->stream, a);
+  } else if (f->exact) {
     if (bsub == 8192)
       hipLaunchKernelGGL((freq_phaseB_scatter<false, 8192>), dim3(grid), dim3(kThreads), 0, f->stream, a);
     else
@@ -3812,6 +4083,9 @@ extern "C" dq_status dq_freq_reset(dq_freq* f, void* hip_stream) {
   f->counters_stale = false;
   f->num_rows = 0;
   f->n_chunks = 0;
+  f->n_prow = 0;
+  f->h_pbase.clear();
+  f->fast_off = false;  // (a reset table may see keys the small-key path takes again)
   f->mode_null_as_group = -1;
   invalidate(f);
   return DQ_OK;
@@ -3892,8 +4166,14 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     dq_status ss = launch_phaseA_small(f, a);
     if (ss != DQ_OK) return ss;
   }
-  if (f->exact) launch_phaseA<false>(f, a, false);
-  else launch_phaseA<true>(f, a, false);
+  if (f->exact && pieces_enabled()) {
+    dq_status ps = launch_pieces(f, a, chunks);
+    if (ps != DQ_OK) return ps;
+  } else if (f->exact) {
+    launch_phaseA<false>(f, a, false);
+  } else {
+    launch_phaseA<true>(f, a, false);
+  }
   HIP_TRY(hipGetLastError());
   if (small)  // the host learns (late, without a wait) whether the attempt gave the batch up
     HIP_TRY(hipMemcpyAsync(f->fast_seen.p, a.fast_words, 8, hipMemcpyDeviceToHost, f->stream));
@@ -4298,6 +4578,18 @@ extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src_c) {
                          dst->tile, (uint64_t)dst->arena_used);
       HIP_TRY(hipGetLastError());
       dst->arena_used += src->arena_used;
+    }
+    if (src->n_prow) {  // the source's bucket pieces, their regions moved with its chunks
+      const size_t need = (size_t)(dst->n_prow + src->n_prow) * kBuckets;
+      HIP_TRY(grow_keep(dst->pstart, (size_t)dst->n_prow * kBuckets, need, dst->stream));
+      HIP_TRY(grow_keep(dst->plen, (size_t)dst->n_prow * kBuckets, need, dst->stream));
+      HIP_TRY(hipMemcpyAsync(dst->pstart.p + (size_t)dst->n_prow * kBuckets, src->pstart.p,
+                             (size_t)src->n_prow * kBuckets * 4, hipMemcpyDeviceToDevice, dst->stream));
+      HIP_TRY(hipMemcpyAsync(dst->plen.p + (size_t)dst->n_prow * kBuckets, src->plen.p,
+                             (size_t)src->n_prow * kBuckets * 4, hipMemcpyDeviceToDevice, dst->stream));
+      const unsigned long long shift = (unsigned long long)dst->n_chunks * dst->tile;
+      for (unsigned long long b : src->h_pbase) dst->h_pbase.push_back(b + shift);
+      dst->n_prow += src->n_prow;
     }
     dst->n_chunks += nc;
   }

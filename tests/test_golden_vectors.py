@@ -171,7 +171,7 @@ def test_hip_scan_reproduces_golden_vectors(name, gpu_device):
                 assert got is None, key
             else:
                 assert got[0] == exp[0], key
-                assert all(_close(float(g), float(e), 1e-11) for g, e in zip(got[1:], exp[1:])), \
+                assert all(_close(float(g), float(e)) for g, e in zip(got[1:], exp[1:])), \
                     (key, got, exp)
         else:
             assert _same(got, exp), (key, got, exp)

@@ -315,7 +315,7 @@ def test_packed_phase_c_hands_on_heavy_partitions(heavy, gpu_device, monkeypatch
     s = ft.summarize()
     assert s.n_groups == len(exp)
     assert s.n_unique == sum(1 for c in exp.values() if c == 1)
-    ent = -sum((c / n) * math.log(c / n) for c in exp.values())
+    ent = -math.fsum((c / n) * math.log(c / n) for c in exp.values())
     assert abs(s.entropy - ent) <= 1e-12 * abs(ent)
     top = ft.topk(6)
     assert [c for _, c in top] == sorted(exp.values(), reverse=True)[:6]

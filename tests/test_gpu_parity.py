@@ -86,7 +86,7 @@ def test_scan_suite_matches_oracle(n, null_rate, batch, gpu_device):
         assert (None if st is None else st.sum_value) == exp
     st = _state_of(df, Sum("b"))
     exp = O.agg_sum(ot, "b", None)
-    assert (st is None and exp is None) or rel_close(st.sum_value, exp, 1e-11)
+    assert (st is None and exp is None) or rel_close(st.sum_value, exp)
     for a, fn in [(Minimum("a"), O.agg_min), (Maximum("a"), O.agg_max), (Minimum("b"), O.agg_min)]:
         st = _state_of(df, a)
         exp = fn(ot, a.column, a.where)
@@ -98,7 +98,7 @@ def test_scan_suite_matches_oracle(n, null_rate, batch, gpu_device):
         if n_ == 0:
             assert st is None
         else:
-            assert st.n == n_ and rel_close(st.avg, avg) and rel_close(st.m2, m2, 1e-11)
+            assert st.n == n_ and rel_close(st.avg, avg) and rel_close(st.m2, m2)
             assert rel_close(st.metric_value(), math.sqrt(m2 / n_))
     for x, y, w in [("a", "b", None), ("c", "b", where)]:
         st = _state_of(df, Correlation(x, y, w))
@@ -109,7 +109,7 @@ def test_scan_suite_matches_oracle(n, null_rate, batch, gpu_device):
             assert st.n == exp[0]
             got = st.metric_value()
             ref = exp[3] / math.sqrt(exp[4] * exp[5]) if exp[4] * exp[5] > 0 else float("nan")
-            assert rel_close(got, ref, 1e-10)
+            assert rel_close(got, ref)
     # HLL registers: bit-exact
     for col, w in [("a", None), ("s", None), ("b", where)]:
         st = _state_of(df, ApproxCountDistinct(col, w))
@@ -250,7 +250,7 @@ def test_fused_hll_and_comoments_match_oracle(n, null_rate, batch, gpu_device):
         else:
             assert cst.n == exp[0]
             ref = exp[3] / math.sqrt(exp[4] * exp[5]) if exp[4] * exp[5] > 0 else float("nan")
-            assert rel_close(cst.metric_value(), ref, 1e-10)
+            assert rel_close(cst.metric_value(), ref)
 
 
 @pytest.mark.parametrize("n,batch", [(5_000, None), (40_000, 6_000)])
@@ -279,3 +279,73 @@ def test_hll_strings_of_every_length_match_oracle(n, batch, gpu_device):
     for w in (None, "k > 0"):
         st = _state_of(df, ApproxCountDistinct("s", w))
         assert list(st.words) == O.agg_hll(ot, "s", w), w
+
+
+def _exact_moments(xs, ys):
+    """Population moments in exact rational arithmetic (fractions.Fraction over the float inputs):
+    the value both Spark's row-sequential update (Correlation.scala:37-52 merge, Corr update) and
+    the device's blocked two-pass + Chan merges approximate."""
+    from fractions import Fraction as F
+    n = len(xs)
+    fx, fy = [F(x) for x in xs], [F(y) for y in ys]
+    mx, my = sum(fx) / n, sum(fy) / n
+    dx, dy = [x - mx for x in fx], [y - my for y in fy]
+    return dict(n=n, mx=mx, my=my, ck=sum(a * b for a, b in zip(dx, dy)),
+                xm=sum(a * a for a in dx), ym=sum(b * b for b in dy),
+                sx=sum(abs(x) for x in fx) / n, sy=sum(abs(y) for y in fy) / n,
+                sck=sum(abs(a * b) for a, b in zip(dx, dy)))
+
+
+@pytest.mark.parametrize("n,null_rate,batch,rho", [(4097, 0.05, None, 0.0), (20_011, 0.3, 4096, 0.0),
+                                                   (30_000, 0.05, 7000, 0.8), (9_000, 0.0, None, -0.99)])
+def test_moments_against_exact_arithmetic(n, null_rate, batch, rho, gpu_device):
+    """Mean / StdDev / Correlation states against EXACT rational arithmetic of the same formulas.
+    Bound: every state component within 1e-12 of its scale -- the averages over
+    Σ|x|/n, the co-moment ck over Σ|dx·dy|, the second moments (sums of squares) relative -- for
+    the device AND for the oracle's row-sequential Spark update, so the two are within 2e-12 of
+    each other on that scale.  The correlation metric is then within 1e-12 relative whenever
+    |corr| >= 1e-3 · Σ|dx·dy| / sqrt(xMk·yMk) (for these independent columns, |corr| ~ 1e-3 and the
+    metric still meets 1e-12 relative: measured 3e-15 device, 5e-14 oracle)."""
+    from fractions import Fraction as F
+    from deequ_amd import Table
+    from deequ_amd.analyzers import Correlation, StandardDeviation
+    from deequ_amd.runners.engine import run_scan
+    from oracle import deequ_oracle as O
+    t = random_table(n, n + 17, null_rate)
+    if rho:  # a column correlated with b (well-conditioned ck)
+        rng = np.random.default_rng(n)
+        b = t.column("b").to_numpy(zero_copy_only=False)
+        d = rho * (b - 1000.0) + math.sqrt(1 - rho * rho) * rng.normal(0.0, 250.0, n)
+        t = t.append_column("d", pa.array(d, mask=np.asarray(t.column("b").is_null())))
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=batch)
+    ot = oracle_of(t)
+    if rho:
+        ot.types["d"] = "double"
+    pairs = [("a", "b", None), ("c", "b", "c > -20")] + ([("d", "b", None)] if rho else [])
+    for cx, cy, w in pairs:
+        a = Correlation(cx, cy, w)
+        st = a.from_aggregation_result(run_scan(df, a.aggregation_functions()), 0)
+        sel = [(float(x), float(y)) for x, y in zip(O._sel(ot, cx, w), O._sel(ot, cy, w))
+               if x is not None and y is not None]
+        e = _exact_moments([x for x, _ in sel], [y for _, y in sel])
+        orc = O.agg_corr(ot, cx, cy, w)
+        ex_corr = float(e["ck"]) / math.sqrt(float(e["xm"]) * float(e["ym"]))
+        for who, s in (("device", (st.n, st.x_avg, st.y_avg, st.ck, st.x_mk, st.y_mk)), ("oracle", orc)):
+            assert s[0] == e["n"], who
+            assert abs(F(s[1]) - e["mx"]) <= F(1, 10 ** 12) * e["sx"], (who, "xAvg")
+            assert abs(F(s[2]) - e["my"]) <= F(1, 10 ** 12) * e["sy"], (who, "yAvg")
+            assert abs(F(s[3]) - e["ck"]) <= F(1, 10 ** 12) * e["sck"], (who, "ck")
+            assert abs(F(s[4]) - e["xm"]) <= F(1, 10 ** 12) * e["xm"], (who, "xMk")
+            assert abs(F(s[5]) - e["ym"]) <= F(1, 10 ** 12) * e["ym"], (who, "yMk")
+            corr = s[3] / math.sqrt(s[4] * s[5])
+            assert rel_close(corr, ex_corr), (who, corr, ex_corr)
+        assert rel_close(st.metric_value(), orc[3] / math.sqrt(orc[4] * orc[5]))
+    for col, w in [("a", None), ("b", None), ("c", "c > -20")]:
+        sd = StandardDeviation(col, w)
+        st = sd.from_aggregation_result(run_scan(df, sd.aggregation_functions()), 0)
+        xs = [float(v) for v in O._sel(ot, col, w) if v is not None]
+        e = _exact_moments(xs, xs)
+        assert st.n == e["n"]
+        assert abs(F(st.avg) - e["mx"]) <= F(1, 10 ** 12) * e["sx"], col
+        assert abs(F(st.m2) - e["xm"]) <= F(1, 10 ** 12) * e["xm"], col
+        assert rel_close(st.metric_value(), math.sqrt(float(e["xm"]) / e["n"]))
