@@ -23,7 +23,7 @@ INTEGRAL_TYPES = {INT8, INT16, INT32, INT64}
 
 # dq_xop
 (X_COL, X_NULL, X_BOOL, X_I64, X_F64, X_STR, X_IS_NULL, X_IS_NOT_NULL, X_NOT, X_AND, X_OR, X_EQ,
- X_NE, X_LT, X_LE, X_GT, X_GE, X_EQ_NULL_SAFE, X_IN, X_CAST_F64, X_REGEX) = range(1, 22)
+ X_NE, X_LT, X_LE, X_GT, X_GE, X_EQ_NULL_SAFE, X_IN, X_CAST_F64, X_REGEX, X_CAST_F32) = range(1, 23)
 
 # dq_agg_kind
 (AGG_COUNT_ALL, AGG_COUNT_NOTNULL, AGG_COUNT_TRUE, AGG_SUM, AGG_MIN, AGG_MAX, AGG_STDDEV_POP,

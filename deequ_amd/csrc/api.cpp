@@ -114,6 +114,7 @@ static bool parse_node(const int64_t* w, int n, int& pos, std::unique_ptr<Node>&
     case DQ_X_IS_NOT_NULL:
     case DQ_X_NOT:
     case DQ_X_CAST_F64:
+    case DQ_X_CAST_F32:
       if (!child()) return false;
       break;
     case DQ_X_AND:
@@ -206,6 +207,7 @@ static void compile_postfix(const Node& n, std::vector<XInstr>& prog, std::strin
     case DQ_X_OR: ins = {XI_OR, 0, 0}; break;
     case DQ_X_IN: ins = {XI_IN, (int32_t)n.kids.size() - 1, 0}; break;
     case DQ_X_CAST_F64: ins = {XI_CAST_F64, 0, 0}; break;
+    case DQ_X_CAST_F32: ins = {XI_CAST_F64, 1, 0}; break;  // a = 1: round to float
     case DQ_X_REGEX: {
       while (pool.size() % 8) pool.push_back('\0');
       ins = {XI_REGEX, (int32_t)n.i, (int64_t)pool.size()};

@@ -250,16 +250,21 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
             st[sp++] = res;
             break;
           }
-          case XI_CAST_F64: {
+          case XI_CAST_F64: {  // ins.a = 1: CAST AS FLOAT (rounded to float, prints as Float.toString)
             V& a = st[sp - 1];
+            const bool to_f32 = ins.a != 0;
             if (a.tag == 2 || a.tag == 1) {
-              a.d = (double)a.i;
+              a.d = to_f32 ? (double)(float)a.i : (double)a.i;  // (float)long: one rounding
               a.tag = 3;
             } else if (a.tag == 4) {
               double d;
               if (parse_f64(a.p, a.len, d)) a = V{3, 0, 0, d, nullptr};
               else a = V{0, 0, 0, 0.0, nullptr};
+            } else if (a.tag == 3 && to_f32) {
+              a.d = (double)(float)a.d;
             }
+            // the type of the result decides how a regex prints it (Double / Float.toString)
+            if (a.tag == 3) a.len = to_f32 ? 1 : 0;
             break;
           }
           case XI_REGEX: {  // find() over x's text with a compiled automaton (regex.py)

@@ -126,7 +126,7 @@ static dq_status stage(dq_loader* l, const dq_column* host_cols, int n_cols, dq_
   hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
   HIP_TRY(hipSetDevice(l->device));
   // layout of the slot: per column validity | values | data, each 256-byte aligned
-  std::vector<size_t> nv(n_cols), nval(n_cols), ndat(n_cols);
+  std::vector<size_t> nv(n_cols), nval(n_cols), ndat(n_cols), dlo(n_cols, 0);
   size_t total = 0;
   for (int c = 0; c < n_cols; ++c) {
     const dq_column& h = host_cols[c];
@@ -140,8 +140,13 @@ static dq_status stage(dq_loader* l, const dq_column* host_cols, int n_cols, dq_
       nval[c] = h.values ? 4 * (n + 1) : 0;
       const int32_t* off = static_cast<const int32_t*>(h.values);
       const int32_t end = off ? off[n] : 0;
-      if (end < 0) return fail(DQ_ERR_INVALID_ARGUMENT, "column %d: negative string offset", c);
-      ndat[c] = h.data ? (size_t)end : 0;
+      if (end < 0 || (off && off[0] < 0) || (off && off[0] > end))
+        return fail(DQ_ERR_INVALID_ARGUMENT, "column %d: bad string offsets", c);
+      // a sliced array (off[0] > 0): only the bytes from off[0] (rounded down to 256, keeping the
+      // staged pointer's alignment) cross the link; the device data pointer is moved back by as
+      // much, so the offsets stay absolute and every string still starts inside the staged bytes
+      dlo[c] = off ? (size_t)off[0] & ~(size_t)255 : 0;
+      ndat[c] = h.data ? (size_t)end - dlo[c] : 0;
     } else if (h.type == DQ_BOOL) {
       nval[c] = h.values ? (n + 7) / 8 : 0;
       ndat[c] = 0;
@@ -189,7 +194,8 @@ static dq_status stage(dq_loader* l, const dq_column* host_cols, int n_cols, dq_
     const void* valp = nullptr;
     HIP_TRY(put(h.validity, nv[c], &vp));
     HIP_TRY(put(h.values, nval[c], &valp));
-    HIP_TRY(put(h.data, ndat[c], &dp));
+    HIP_TRY(put(h.data ? static_cast<const uint8_t*>(h.data) + dlo[c] : nullptr, ndat[c], &dp));
+    if (dp) dp = static_cast<const uint8_t*>(dp) - dlo[c];
     const int nd = need ? need[c] : 2;
     d.validity = static_cast<const uint8_t*>(h.validity && nd >= 1 ? vp : nullptr);
     if (nd == 2) {

@@ -137,7 +137,7 @@ DQ_DEV void build_prefix_map(const uint64_t* act, int A, int bits, int16_t* map)
 
 __global__ void __launch_bounds__(256)
 select_hist(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __restrict__ active, int A,
-            int bits, int D, unsigned int* __restrict__ hist) {
+            int bits, int D, unsigned long long* __restrict__ hist) {
   extern __shared__ uint64_t sel_lds[];
   uint64_t* s_act = sel_lds;                                            // A
   unsigned int* s_hist = reinterpret_cast<unsigned int*>(sel_lds + A);  // A << D
@@ -172,7 +172,7 @@ select_hist(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __rest
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nb; i += 256)
-    if (s_hist[i]) atomicAdd(&hist[i], s_hist[i]);
+    if (s_hist[i]) atomicAdd(&hist[i], (unsigned long long)s_hist[i]);  // (u64: a bin may pass 2^32 keys)
 }
 
 // The keys whose top `bits` bits are one of the A prefixes -> out[*cursor ...].
@@ -247,7 +247,7 @@ dq_status radix_select(uint64_t* keys, int64_t n, const std::vector<int64_t>& ra
   std::vector<Target> tg(m);
   for (int j = 0; j < m; ++j) tg[j] = Target{0, rank[j]};
   DevBuf<uint64_t> buf[2], act;
-  DevBuf<unsigned int> hist;
+  DevBuf<unsigned long long> hist;
   DevBuf<unsigned long long> cur;
   DevBuf<uint8_t> tmp;
   DevBuf<int64_t> didx;
@@ -257,7 +257,7 @@ dq_status radix_select(uint64_t* keys, int64_t n, const std::vector<int64_t>& ra
   int which = 0;
   int bits = 0;
   std::vector<uint64_t> prefixes, sp;  // (alive until the copies from them have run)
-  std::vector<unsigned int> h;
+  std::vector<unsigned long long> h;
   while (true) {
     prefixes.clear();
     for (const Target& t : tg) prefixes.push_back(t.prefix);
@@ -270,14 +270,14 @@ dq_status radix_select(uint64_t* keys, int64_t n, const std::vector<int64_t>& ra
     HIP_TRY(act.ensure(A));
     HIP_TRY(hipMemcpyAsync(act.p, prefixes.data(), A * 8, hipMemcpyHostToDevice, stream));
     HIP_TRY(hist.ensure(nb));
-    HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)nb * 4, stream));
+    HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)nb * 8, stream));
     const size_t lds = (size_t)A * 8 + (size_t)nb * 4 + (bits && bits <= kMapBits ? 2u << bits : 0u);
     // (a few blocks per CU: each flushes up to kSelBins counters)
     hipLaunchKernelGGL(select_hist, dim3(grid_of(M, 256 * 64, 1024)), dim3(256), lds, stream, src,
                        M, act.p, A, bits, D, hist.p);
     HIP_TRY(hipGetLastError());
     h.resize(nb);
-    HIP_TRY(hipMemcpyAsync(h.data(), hist.p, (size_t)nb * 4, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(h.data(), hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     // every target: the bin of its prefix that holds its rank
     for (Target& t : tg) {

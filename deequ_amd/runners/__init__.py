@@ -12,6 +12,7 @@ from __future__ import annotations
 import dataclasses
 import functools
 import gc
+import threading
 import json
 import os
 import sys
@@ -67,6 +68,30 @@ class AnalyzerContext:
         return json.dumps(AnalyzerContext.success_metrics_as_rows(ctx, for_analyzers))
 
 
+# Runs may overlap (threads): only the outermost one pauses the cyclic GC and restores its
+# previous state, so an inner run ending never re-enables collection under an outer one.
+_gc_lock = threading.Lock()
+_gc_depth = 0
+_gc_was_enabled = False
+
+
+def _gc_pause_enter():
+    global _gc_depth, _gc_was_enabled
+    with _gc_lock:
+        if _gc_depth == 0:
+            _gc_was_enabled = gc.isenabled()
+            gc.disable()
+        _gc_depth += 1
+
+
+def _gc_pause_exit():
+    global _gc_depth
+    with _gc_lock:
+        _gc_depth -= 1
+        if _gc_depth == 0 and _gc_was_enabled:
+            gc.enable()
+
+
 @dataclass
 class AnalysisRunnerRepositoryOptions:
     metrics_repository: object = None
@@ -98,14 +123,12 @@ class AnalysisRunner:
         a run leaves only a few dozen cycles, which the next collection after it frees."""
         if not analyzers:
             return AnalyzerContext.empty()
-        collecting = gc.isenabled()
-        gc.disable()
+        _gc_pause_enter()
         try:
             return AnalysisRunner._do_analysis_run(data, analyzers, aggregate_with,
                                                    save_states_with, repository_options)
         finally:
-            if collecting:
-                gc.enable()
+            _gc_pause_exit()
 
     @staticmethod
     def _do_analysis_run(data, analyzers, aggregate_with, save_states_with, repository_options):

@@ -342,7 +342,11 @@ class _Emitter:
         if n.op == "cast":
             if n.name not in ("DOUBLE", "FLOAT"):
                 raise SqlError(f"CAST AS {n.name} is not supported by the engine")
-            w.append(N.X_CAST_F64)
+            if n.name == "FLOAT" and self.type_of(n.kids[0]) == "str":
+                # Spark parses with Float.parseFloat (one rounding to float); parse-to-double and
+                # then round would round twice -- refused rather than restated approximately
+                raise SqlError("CAST(string AS FLOAT) is not supported by the engine")
+            w.append(N.X_CAST_F32 if n.name == "FLOAT" else N.X_CAST_F64)
             self.emit(n.kids[0])
             return
         if n.op in ("isnull", "isnotnull", "not"):

@@ -153,8 +153,9 @@ typedef enum dq_xop {
   DQ_X_GE = 17,
   DQ_X_EQ_NULL_SAFE = 18, /* <=> */
   DQ_X_IN = 19,        /* [op, n, x, item_1 .. item_n]      x IN (items)                          */
-  DQ_X_CAST_F64 = 20,  /* [op, x]                           CAST(x AS DOUBLE) (string: parse)    */
-  DQ_X_REGEX = 21      /* [op, null_mode, nbytes, ceil(n/8) words, x]  regex find() over x's text:
+  DQ_X_CAST_F64 = 20,  /* [op, x]                           CAST(x AS DOUBLE) (string: parse); a  */
+                       /*   float32 value is widened exactly and prints as Double.toString after */
+  DQ_X_REGEX = 21,     /* [op, null_mode, nbytes, ceil(n/8) words, x]  regex find() over x's text:
                           the words pack an automaton (deequ_amd/regex.py CompiledRegex.blob):
                           int32 n_states, n_classes, start, 0; u8 byte_class[256]; u8
                           status[n_states] (1 accept, 2 reject, padded to 4); u16
@@ -163,6 +164,10 @@ typedef enum dq_xop {
                           string).  A NULL x gives NULL (null_mode 0, RLIKE) or FALSE
                           (null_mode 1: when(regexp_extract(x, p, 0) != "", 1).otherwise(0),
                           PatternMatch.scala:44-46).                                           */
+  DQ_X_CAST_F32 = 22   /* [op, x]  CAST(x AS FLOAT): an integral x rounds to the nearest float,
+                          a double one too (Spark's Cast to FloatType, `.toFloat`); the value
+                          then prints as Float.toString.  (A string x is refused by the host
+                          compiler: Float.parseFloat's direct rounding is not restated.)       */
 } dq_xop;
 
 typedef struct dq_expr {

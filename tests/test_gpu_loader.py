@@ -119,7 +119,7 @@ def test_freq_add_host_matches_oracle(cols, null_as_group, gpu_device):
     assert ft.num_rows == t.num_rows
 
 
-@pytest.mark.parametrize("offset", [0, 8, 5])
+@pytest.mark.parametrize("offset", [0, 8, 5, 3000])
 def test_sliced_arrow_export_scans_like_the_unsliced_copy(offset, gpu_device):
     """A Spark partition exported through the Arrow C Data Interface may be a slice (non-zero
     ArrowArray.offset): imported by dq_column_from_arrow (HostTable.from_arrow_c) and scanned by
@@ -132,7 +132,10 @@ def test_sliced_arrow_export_scans_like_the_unsliced_copy(offset, gpu_device):
     t = _table(n + 64, offset + 1)
     f = pa.array(np.arange(n + 64) % 3 == 0, mask=np.arange(n + 64) % 7 == 0)
     t = t.append_column("f", f)
-    sliced = [rb.slice(offset, n // 2) for rb in t.to_batches(max_chunksize=(n + 64) // 2)]
+    # (offset 3000: the strings start ~30 KB into the data buffer; the loader stages only the
+    # bytes from the slice's first offset, rounded down to 256)
+    sliced = [rb.slice(offset, min(n // 2, rb.num_rows - offset))
+              for rb in t.to_batches(max_chunksize=(n + 64) // 2)]
     copies = [pa.Table.from_batches([rb]).combine_chunks().to_batches()[0] for rb in sliced]
     copies = [pa.RecordBatch.from_arrays([pa.array(c.to_pylist(), c.type) for c in rb.columns],
                                          schema=rb.schema) for rb in copies]

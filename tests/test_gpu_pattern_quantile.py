@@ -259,3 +259,41 @@ def test_sorted_sample_exact_ranks_by_radix_select(dist, m, gpu_device):
     assert count.value == cnt and n_out.value == m
     ranks = [(j * (cnt - 1)) // (m - 1) for j in range(m)]
     assert _ordered(out).tolist() == keys[ranks].tolist(), dist
+
+
+@pytest.mark.parametrize("expr,ty", [("CAST(f AS DOUBLE) RLIKE '^0\\\\.1000000'", "widen"),
+                                     ("CAST(d AS FLOAT) RLIKE '^0\\\\.1$'", "narrow"),
+                                     ("CAST(f AS DOUBLE) RLIKE 'E'", "widen"),
+                                     ("CAST(i AS FLOAT) RLIKE '\\\\.0$'", "int2f"),
+                                     ("f RLIKE '^0\\\\.1$'", "float")])
+def test_regex_over_casts_prints_the_cast_type(expr, ty, gpu_device):
+    """x RLIKE p matches Spark's cast of x to string, so the printed form follows the type of x:
+    CAST(float32 AS DOUBLE) prints Double.toString of the exactly widened value ("0.10000000149011612"),
+    CAST(double AS FLOAT) rounds to float and prints Float.toString ("0.1"), CAST(long AS FLOAT)
+    rounds the integer once.  Expected values from the oracle's Java formatting and java find()."""
+    from deequ_amd import Table
+    from deequ_amd.analyzers import Compliance
+    from oracle.deequ_oracle import java_double_to_string, java_float_to_string, regex_find_nonempty
+    rng = np.random.default_rng(11)
+    n = 5000
+    f = (rng.integers(0, 40, n) / 10.0).astype(np.float32)
+    f[::7] = np.float32(1e-9)
+    d = rng.integers(0, 40, n) / 10.0
+    i = rng.integers(-(1 << 60), 1 << 60, n)
+    i[::5] = rng.integers(-100, 100, n)[::5]
+    t = pa.table({"f": pa.array(f, type=pa.float32()), "d": pa.array(d), "i": pa.array(i)})
+    df = Table.from_arrow(t, device=gpu_device)
+    pat = expr.split("RLIKE ")[1].strip("'").replace("\\\\", "\\")
+    exp = 0
+    for k in range(n):
+        if ty == "widen":
+            txt = java_double_to_string(float(f[k]))
+        elif ty == "narrow":
+            txt = java_float_to_string(float(np.float32(d[k])))
+        elif ty == "int2f":
+            txt = java_float_to_string(float(np.float32(int(i[k]))))
+        else:
+            txt = java_float_to_string(float(f[k]))
+        exp += 1 if regex_find_nonempty(txt, pat) else 0
+    got = Compliance("c", expr).calculate(df).value.get()
+    assert got == exp / n, (expr, got, exp / n)

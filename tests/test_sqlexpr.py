@@ -52,3 +52,13 @@ def test_errors(bad):
 def test_parse_tree_shapes():
     n = parse("a > 1 AND NOT b IS NULL OR c = 'x'")
     assert n.op == "or" and n.kids[0].op == "and"
+
+
+def test_cast_as_float_and_double_opcodes():
+    """CAST AS FLOAT is its own opcode (rounds to float, prints as Float.toString); CAST AS DOUBLE
+    widens (prints as Double.toString); a string cast to FLOAT is refused (Float.parseFloat's one
+    rounding is not restated)."""
+    assert comp("CAST(price AS FLOAT) > 1.5")[:2] == [N.X_GT, N.X_CAST_F32]
+    assert comp("CAST(att1 AS DOUBLE) > 1.5")[:2] == [N.X_GT, N.X_CAST_F64]
+    with pytest.raises(SqlError):
+        comp("CAST(item AS FLOAT) > 1.5")
