@@ -43,6 +43,8 @@ def lib():
         L.or_xxh64.restype = ctypes.c_uint64
         L.or_hll.argtypes = [i32, vp, vp, vp, i64, i32, vp]
         L.or_corr.argtypes = [vp, vp, vp, vp, i64, i32, vp]
+        L.or_freq.argtypes = [i32, vp, vp, vp, i64, i32, i64, i32, i32, vp, vp, vp,
+                              ctypes.POINTER(ctypes.c_int)]
         L.or_freq_i64.argtypes = [vp, vp, i64, i64, ctypes.POINTER(i64), ctypes.POINTER(i64),
                                   ctypes.POINTER(ctypes.c_double)]
         _LIB = L
@@ -90,6 +92,26 @@ def corr(x, vx, y, vy, threads=1):
     out = np.zeros(6, np.float64)
     lib().or_corr(_p(x), _p(vx), _p(y), _p(vy), len(x), threads, _p(out))
     return tuple(float(v) for v in out)
+
+
+class OrFreqOut(ctypes.Structure):
+    _fields_ = [("groups", ctypes.c_int64), ("unique", ctypes.c_int64), ("null_rows", ctypes.c_int64),
+                ("entropy", ctypes.c_double)]
+
+
+def freq(kind, values, data, valid_bits, n, num_rows, null_as_group=False, k=0, threads=1):
+    """or_freq: the frequency family over one key column (kind "long": int64 values; "string":
+    int32 offsets + bytes), hash-partitioned on `threads` OpenMP threads.  Returns (OrFreqOut,
+    top-k counts, top-k rows (-1: the NULL group))."""
+    out = OrFreqOut()
+    kk = max(int(k), 0)
+    tc = np.zeros(max(kk, 1), np.int64)
+    tr = np.zeros(max(kk, 1), np.int64)
+    nt = ctypes.c_int()
+    lib().or_freq(0 if kind == "long" else 1, _p(values), _p(data), _p(valid_bits), int(n),
+                  1 if null_as_group else 0, int(num_rows), kk, int(threads), ctypes.byref(out),
+                  _p(tc), _p(tr), ctypes.byref(nt))
+    return out, tc[:nt.value], tr[:nt.value]
 
 
 def freq_i64(values, valid_bits, num_rows):

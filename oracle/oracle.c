@@ -391,3 +391,220 @@ void or_freq_i64(const int64_t* v, const uint8_t* valid, int64_t n, int64_t num_
   *ent = e;
   free(buf);
 }
+
+/* ------------------------------------------------- frequency family, hash-partitioned (CPU) ----
+ * computeFrequencies (M/analyzers/GroupingAnalyzers.scala:53-80: where all keys are not null,
+ * groupBy(keys).agg(count)) and the one aggregation over the frequency table that Uniqueness /
+ * Distinctness / UniqueValueRatio / CountDistinct / Entropy share (AnalysisRunner.scala:490-500;
+ * Σ[c==1], count(*), Σ -(c/numRows) ln(c/numRows), Entropy.scala:33-40), plus Histogram's
+ * top-k (Histogram.scala:54-79: NULL is a group of its own when null_as_group, its key
+ * "NullValue"; rdd.top(k) by count, ties in any order).
+ * Execution = Spark local[N]'s hash Exchange + HashAggregate: every thread hash-partitions its
+ * contiguous row range into P shuffle partitions (count, then scatter of row ids), then each
+ * partition is aggregated in an open-addressing table; partition partials are combined in
+ * partition order.  type 0: int64 keys; type 1: utf8 (int32 offsets + bytes), equal keys compared
+ * byte for byte.  topk_rows: a row of each top group (-1: the NULL group).
+ */
+typedef struct {
+  int64_t groups, unique, null_rows;
+  double entropy;
+} or_freq_out;
+
+static inline uint64_t or_mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+typedef struct {
+  int64_t c, row;
+} or_top;
+
+/* min-heap of the k largest counts */
+static void top_push(or_top* h, int* nh, int k, int64_t c, int64_t row) {
+  if (k <= 0) return;
+  if (*nh < k) {
+    int i = (*nh)++;
+    h[i].c = c;
+    h[i].row = row;
+    while (i > 0 && h[(i - 1) / 2].c > h[i].c) {
+      or_top t = h[i];
+      h[i] = h[(i - 1) / 2];
+      h[(i - 1) / 2] = t;
+      i = (i - 1) / 2;
+    }
+    return;
+  }
+  if (c <= h[0].c) return;
+  h[0].c = c;
+  h[0].row = row;
+  for (int i = 0;;) {
+    int l = 2 * i + 1, r = l + 1, m = i;
+    if (l < *nh && h[l].c < h[m].c) m = l;
+    if (r < *nh && h[r].c < h[m].c) m = r;
+    if (m == i) break;
+    or_top t = h[i];
+    h[i] = h[m];
+    h[m] = t;
+    i = m;
+  }
+}
+
+static int top_cmp_desc(const void* a, const void* b) {
+  int64_t x = ((const or_top*)a)->c, y = ((const or_top*)b)->c;
+  return (x < y) - (x > y);
+}
+
+static inline uint64_t key_hash(int type, const void* values, const uint8_t* data, int64_t r) {
+  if (type == 0) return or_mix64((uint64_t)((const int64_t*)values)[r]);
+  const int32_t* off = (const int32_t*)values;
+  return or_xxh64(data + off[r], off[r + 1] - off[r], 0);
+}
+
+static inline int key_eq(int type, const void* values, const uint8_t* data, int64_t a, int64_t b) {
+  if (type == 0) return ((const int64_t*)values)[a] == ((const int64_t*)values)[b];
+  const int32_t* off = (const int32_t*)values;
+  const int32_t la = off[a + 1] - off[a], lb = off[b + 1] - off[b];
+  return la == lb && memcmp(data + off[a], data + off[b], (size_t)la) == 0;
+}
+
+void or_freq(int type, const void* values, const uint8_t* data, const uint8_t* valid, int64_t n,
+             int null_as_group, int64_t num_rows, int k, int nthreads, or_freq_out* out,
+             int64_t* topk_counts, int64_t* topk_rows, int* n_top) {
+  const int P = 256;  /* shuffle partitions */
+  const double nr = (double)num_rows;
+  int64_t* cnt = (int64_t*)calloc((size_t)nthreads * P + 1, sizeof(int64_t));
+  uint64_t* hs = (uint64_t*)malloc((size_t)(n > 0 ? n : 1) * 8);
+  int64_t* rows = (int64_t*)malloc((size_t)(n > 0 ? n : 1) * 8);
+  int64_t nulls = 0;
+  /* the shuffle write: hash every keyed row, count per (thread, partition), scatter row ids */
+#pragma omp parallel num_threads(nthreads) reduction(+ : nulls)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t r0 = n * t / nthreads, r1 = n * (t + 1) / nthreads;
+    int64_t* c = cnt + (size_t)t * P;
+    for (int64_t r = r0; r < r1; ++r) {
+      if (!bit(valid, r)) {
+        ++nulls;
+        hs[r] = 0;
+        continue;
+      }
+      hs[r] = key_hash(type, values, data, r);
+      ++c[hs[r] >> 56];
+    }
+  }
+  /* offsets: partition-major, thread order inside a partition */
+  int64_t* base = (int64_t*)malloc(((size_t)nthreads * P + 1) * sizeof(int64_t));
+  int64_t acc = 0;
+  for (int p = 0; p < P; ++p)
+    for (int t = 0; t < nthreads; ++t) {
+      base[(size_t)t * P + p] = acc;
+      acc += cnt[(size_t)t * P + p];
+    }
+  int64_t* pbeg = (int64_t*)malloc((size_t)(P + 1) * sizeof(int64_t));
+  for (int p = 0; p < P; ++p) pbeg[p] = base[p];
+  pbeg[P] = acc;
+#pragma omp parallel num_threads(nthreads)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t r0 = n * t / nthreads, r1 = n * (t + 1) / nthreads;
+    int64_t* b = base + (size_t)t * P;
+    for (int64_t r = r0; r < r1; ++r)
+      if (bit(valid, r)) rows[b[hs[r] >> 56]++] = r;
+  }
+  /* the shuffle read + final aggregation, one partition at a time per thread */
+  int64_t* pg = (int64_t*)calloc(P, sizeof(int64_t));
+  int64_t* pu = (int64_t*)calloc(P, sizeof(int64_t));
+  double* pe = (double*)calloc(P, sizeof(double));
+  or_top* ptop = (or_top*)malloc((size_t)P * (k > 0 ? k : 1) * sizeof(or_top));
+  int* pnt = (int*)calloc(P, sizeof(int));
+  int64_t lit_count = 0, lit_row = -1;  /* (one partition holds it: no race) */
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+  for (int p = 0; p < P; ++p) {
+    const int64_t m = pbeg[p + 1] - pbeg[p];
+    size_t cap = 16;
+    while (cap < (size_t)m * 2) cap <<= 1;
+    int64_t* trow = (int64_t*)malloc(cap * sizeof(int64_t));
+    int64_t* tcnt = (int64_t*)malloc(cap * sizeof(int64_t));
+    for (size_t i = 0; i < cap; ++i) trow[i] = -1;
+    for (int64_t i = pbeg[p]; i < pbeg[p + 1]; ++i) {
+      const int64_t r = rows[i];
+      size_t s = (size_t)(hs[r] & (cap - 1));
+      for (;;) {
+        if (trow[s] < 0) {
+          trow[s] = r;
+          tcnt[s] = 1;
+          break;
+        }
+        if (hs[trow[s]] == hs[r] && key_eq(type, values, data, trow[s], r)) {
+          ++tcnt[s];
+          break;
+        }
+        s = (s + 1) & (cap - 1);
+      }
+    }
+    int64_t g = 0, u = 0;
+    double e = 0.0;
+    for (size_t s = 0; s < cap; ++s) {
+      if (trow[s] < 0) continue;
+      const int64_t c = tcnt[s];
+      if (type == 1 && null_as_group) {  /* a real "NullValue": merged with the NULL group */
+        const int32_t* off = (const int32_t*)values;
+        const int64_t r = trow[s];
+        if (off[r + 1] - off[r] == 9 && memcmp(data + off[r], "NullValue", 9) == 0) {
+          lit_count = c;
+          lit_row = r;
+          continue;
+        }
+      }
+      ++g;
+      u += c == 1;
+      const double pr = (double)c / nr;
+      e += -pr * log(pr);
+      top_push(ptop + (size_t)p * k, &pnt[p], k, c, trow[s]);
+    }
+    pg[p] = g;
+    pu[p] = u;
+    pe[p] = e;
+    free(trow);
+    free(tcnt);
+  }
+  or_freq_out o = {0, 0, nulls, 0.0};
+  or_top* heap = (or_top*)malloc((size_t)(k > 0 ? k : 1) * sizeof(or_top));
+  int nh = 0;
+  for (int p = 0; p < P; ++p) {
+    o.groups += pg[p];
+    o.unique += pu[p];
+    o.entropy += pe[p];
+    for (int i = 0; i < pnt[p]; ++i) top_push(heap, &nh, k, ptop[(size_t)p * k + i].c, ptop[(size_t)p * k + i].row);
+  }
+  if (null_as_group && nulls + lit_count) {  /* Histogram: the NULL group ("NullValue") */
+    const int64_t c = nulls + lit_count;
+    ++o.groups;
+    o.unique += c == 1;
+    const double pr = (double)c / nr;
+    o.entropy += -pr * log(pr);
+    top_push(heap, &nh, k, c, nulls ? -1 : lit_row);
+  }
+  qsort(heap, (size_t)nh, sizeof(or_top), top_cmp_desc);
+  for (int i = 0; i < nh; ++i) {
+    topk_counts[i] = heap[i].c;
+    topk_rows[i] = heap[i].row;
+  }
+  *n_top = nh;
+  *out = o;
+  free(heap);
+  free(pg);
+  free(pu);
+  free(pe);
+  free(ptop);
+  free(pnt);
+  free(pbeg);
+  free(base);
+  free(rows);
+  free(hs);
+  free(cnt);
+}

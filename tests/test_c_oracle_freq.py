@@ -1,0 +1,58 @@
+"""The C/OpenMP frequency restatement (oracle/oracle.c or_freq, the configs[2] / configs[4] CPU
+baseline) against the pure-Python oracle: groups, Σ[c==1], entropy and Histogram's top-k, over
+int64 and utf8 keys, NULLs skipped (grouping) or a group of their own merged with a real
+"NullValue" string (Histogram.scala:59-66).  CPU only."""
+import math
+
+import numpy as np
+import pyarrow as pa
+import pytest
+
+from oracle import c_oracle as C
+from oracle import deequ_oracle as O
+
+
+def _buffers(arr):
+    arr = arr.combine_chunks() if isinstance(arr, pa.ChunkedArray) else arr
+    bufs = arr.buffers()
+    n = len(arr)
+    valid = (np.frombuffer(bufs[0], np.uint8).copy() if bufs[0] is not None
+             else np.full((n + 7) // 8, 0xFF, np.uint8))
+    if pa.types.is_string(arr.type):
+        off = np.frombuffer(bufs[1], np.int32)[: n + 1].copy()
+        data = np.frombuffer(bufs[2], np.uint8).copy() if bufs[2] is not None else np.zeros(1, np.uint8)
+        return off, data, valid
+    return np.frombuffer(bufs[1], np.int64)[:n].copy(), None, valid
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+@pytest.mark.parametrize("kind", ["long", "string"])
+def test_c_frequency_family_matches_python_oracle(kind, threads):
+    rng = np.random.default_rng(7 + threads)
+    n = 30_000
+    ids = rng.integers(0, n // 3, n)
+    mask = rng.random(n) < 0.05
+    if kind == "long":
+        arr = pa.array(ids, mask=mask, type=pa.int64())
+    else:
+        words = np.array([f"w{v}" for v in ids], dtype=object)
+        words[::97] = "NullValue"
+        arr = pa.array([None if m else str(w) for w, m in zip(words, mask)], type=pa.string())
+    t = O.OTable({"k": arr.to_pylist()}, {"k": kind})
+    values, data, valid = _buffers(arr)
+    out, _, _ = C.freq(kind, values, data, valid, n, n, threads=threads)
+    freq = O.frequencies(t, ["k"])
+    assert out.groups == len(freq)
+    assert out.unique == sum(1 for c in freq.values() if c == 1)
+    assert out.null_rows == int(mask.sum())
+    ent = -math.fsum((c / n) * math.log(c / n) for c in freq.values())
+    assert abs(out.entropy - ent) <= 1e-12 * ent
+    # Histogram: NULL -> "NullValue" (merged with a real one), top-k by count
+    hout, tc, tr = C.freq(kind, values, data, valid, n, n, null_as_group=True, k=50, threads=threads)
+    hist, _ = O.histogram(t, "k")
+    assert hout.groups == len(hist)
+    assert list(tc) == sorted(hist.values(), reverse=True)[:50]
+    vals = arr.to_pylist()
+    for c, r in zip(tc, tr):
+        key = "NullValue" if r < 0 or vals[r] is None else O.java_to_string(vals[r], kind)
+        assert hist[key] == c

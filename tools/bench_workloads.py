@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--batch-rows", type=int, default=1 << 26)
     ap.add_argument("--runner", action="store_true", help="c3: time AnalysisRunner itself")
     ap.add_argument("--pyprof", action="store_true", help="cProfile one extra step (stderr)")
+    ap.add_argument("--cpu-baseline", action="store_true",
+                    help="also time the C/OpenMP restatement (oracle/oracle.c) on a bounded sample")
+    ap.add_argument("--cpu-rows", type=int, default=1 << 25, help="rows of that sample")
     args = ap.parse_args()
     import torch
     dev = "cuda:0"
@@ -219,7 +222,9 @@ def main():
               ", ".join(f"{d * 1e3:.1f} ms" for g, d, _ in gcs if g == 2), file=sys.stderr)
     dev_ms = sum(per_step) / args.steps
     achieved = b_alg / (dev_ms * 1e-3)
+    cpu = cpu_baseline(args, table) if args.cpu_baseline else None
     print(json.dumps({
+        "cpu_baseline": cpu,
         "workload": args.workload, "desc": desc, "rows": rows, "unit": metric_unit,
         "value": rows / el, "ms_per_step": el * 1e3, "device_ms_per_step": dev_ms,
         "steps": args.steps, "warmup": args.warmup,
@@ -228,6 +233,67 @@ def main():
                      "kernel": kernel},
         "result": repr(res)[:300],
     }), flush=True)
+
+
+def _host_column(col, n):
+    """The first n rows of a device column as host numpy buffers (values, data, validity)."""
+    import numpy as np
+    vb = (n + 7) // 8
+    valid = (col.validity[:vb].cpu().numpy().copy() if col.validity is not None
+             else np.full(vb, 0xFF, np.uint8))
+    if col.data is not None:  # utf8
+        off = col.values[: n + 1].cpu().numpy().astype(np.int32)
+        data = col.data[: int(off[-1])].cpu().numpy().copy()
+        return off, data if len(data) else np.zeros(1, np.uint8), valid
+    return col.values[:n].cpu().numpy().copy(), None, valid
+
+
+def cpu_baseline(args, table, min_seconds: float = 10.0):
+    """The same workload's semantics restated in C/OpenMP (oracle/oracle.c: or_freq = the hash
+    Exchange + HashAggregate of Spark local[T], or_hll / or_corr = the partial + final
+    aggregation) on a bounded sample: the first rows of the table's first batch, repeated until
+    `min_seconds` of CPU work.  kind "port": a CPU restatement of Spark 2.2 deequ -- not Spark."""
+    sys.path.insert(0, ROOT)
+    from bench import available_cpus
+    from oracle import c_oracle as C
+    threads, host = available_cpus()
+    b0 = table.batches[0]
+    first = next(iter(b0.values()))
+    n = min(args.cpu_rows, first.length)
+    if args.workload == "c3":
+        cols = {c: _host_column(b0[c], n) for c in ("id", "priority")}
+
+        def one():
+            for c, kind in (("id", "long"), ("priority", "string")):
+                v, d, m = cols[c]
+                C.freq(kind, v, d, m, n, n, null_as_group=True, k=1000, threads=threads)
+        what = ("Uniqueness/Distinctness/Entropy + Histogram top-1000 of id and priority: "
+                "or_freq (hash-partitioned count, 256 shuffle partitions)")
+    elif args.workload == "c4":
+        import numpy as np
+        idv, _, idm = _host_column(b0["id"], n)
+        sv, _, sm = _host_column(b0["score"], n)
+        sv = sv.view(np.float64)
+
+        def one():
+            C.hll(5, idv, None, idm, n, threads)
+            C.corr(idv, idm, sv, sm, threads)
+        what = "ApproxCountDistinct(id) + Correlation(id, score): or_hll + or_corr"
+    else:
+        return None
+    one()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= min_seconds or reps >= 1000:
+            break
+    return {"value": reps * n / el, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"{what} over the first {n} rows of the same synthetic table x {reps} passes "
+                      f"({el:.1f} s), oracle/oracle.c, OpenMP, {threads} threads = Spark "
+                      f"local[{threads}] (every CPU this process may use; the host has {host}) "
+                      f"-- a CPU restatement of Spark 2.2 deequ semantics, not Spark"}
 
 
 if __name__ == "__main__":
