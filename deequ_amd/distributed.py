@@ -14,6 +14,34 @@ import numpy as np
 
 from . import _native as N
 
+# Bytes this rank moved through collectives since the last reset_comm_bytes(): sent to and
+# received from OTHER ranks (over RCCL: the xGMI traffic; a rank's own segment never leaves it).
+# All-to-all: the off-rank splits; all-gather / all-reduce: the payload to / from each peer.
+COMM_BYTES = {"sent": 0, "recv": 0}
+
+
+def reset_comm_bytes() -> None:
+    COMM_BYTES["sent"] = COMM_BYTES["recv"] = 0
+
+
+def _count_a2a(in_splits, out_splits, rank: int) -> None:
+    COMM_BYTES["sent"] += int(sum(int(v) for j, v in enumerate(in_splits) if j != rank))
+    COMM_BYTES["recv"] += int(sum(int(v) for j, v in enumerate(out_splits) if j != rank))
+
+
+def _count_reduce(t) -> None:
+    """A ring all-reduce of tensor t: 2 (world - 1) / world of its bytes each way."""
+    import torch.distributed as dist
+    w = dist.get_world_size()
+    b = 2 * (w - 1) * t.numel() * t.element_size() // w
+    COMM_BYTES["sent"] += b
+    COMM_BYTES["recv"] += b
+
+
+def _count_gather(nbytes: int, world: int, others_bytes: int = None) -> None:
+    COMM_BYTES["sent"] += int(nbytes) * (world - 1)
+    COMM_BYTES["recv"] += int(nbytes) * (world - 1) if others_bytes is None else int(others_bytes)
+
 
 def serialize_state(plan, state) -> bytes:
     size = int(N.lib.dq_state_serialized_size(plan.handle))
@@ -50,6 +78,7 @@ def all_gather_bytes(payload: bytes, device=None) -> List[bytes]:
         t = t.to(device)
     out = torch.empty(world * t.numel(), dtype=torch.uint8, device=t.device)
     dist.all_gather_into_tensor(out, t)
+    _count_gather(t.numel(), world)
     host = out.cpu().numpy()
     n = len(payload)
     return [host[r * n:(r + 1) * n].tobytes() for r in range(world)]
@@ -117,6 +146,7 @@ def all_gather_varbytes(payload: bytes, device=None) -> List[bytes]:
     n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
     sizes = torch.empty(world, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(sizes, n)
+    _count_gather(n.numel() * n.element_size(), dist.get_world_size())
     sizes = sizes.cpu().tolist()
     width = max(1, max(sizes))
     t = torch.zeros(width, dtype=torch.uint8)
@@ -125,6 +155,7 @@ def all_gather_varbytes(payload: bytes, device=None) -> List[bytes]:
     t = t.to(dev)
     out = torch.empty(world * width, dtype=torch.uint8, device=dev)
     dist.all_gather_into_tensor(out, t)
+    _count_gather(width, world)
     host = out.cpu().numpy()
     return [host[r * width: r * width + sizes[r]].tobytes() for r in range(world)]
 
@@ -171,10 +202,14 @@ def exchange_segments(rec, var, rec_counts, var_bytes):
     recv_rec = torch.empty(int(src_rc.sum()) * rb, dtype=torch.uint8, device=dev)
     dist.all_to_all_single(recv_rec, rec, output_split_sizes=(src_rc * rb).tolist(),
                            input_split_sizes=(np.asarray(rec_counts) * rb).tolist())
+    me = dist.get_rank()
+    _count_a2a(np.asarray(rec_counts) * rb, src_rc * rb, me)
+    _count_a2a([16] * world, [16] * world, me)  # the sizes
     recv_var = torch.empty(int(src_vb.sum()), dtype=torch.uint8, device=dev)
     if int(np.sum(var_bytes)) or int(src_vb.sum()):
         dist.all_to_all_single(recv_var, var, output_split_sizes=src_vb.tolist(),
                                input_split_sizes=np.asarray(var_bytes).tolist())
+        _count_a2a(np.asarray(var_bytes), src_vb, me)
     return recv_rec.to(home), recv_var.to(home), src_rc, src_vb
 
 
@@ -207,6 +242,7 @@ def freq_repartition(local, null_as_group: bool = False):
     tot = torch.tensor([local.num_rows, *sp.tolist()], dtype=torch.int64,
                        device=_comm_device(rec.device))
     dist.all_reduce(tot)
+    _count_reduce(tot)
     tot = tot.cpu().numpy()
     owned = FrequencyTable(local.key_columns, local.key_types, local.device,
                            capacity_hint=int(src_rc.sum()))
@@ -237,9 +273,11 @@ class DistributedFrequencies:
         ints = torch.tensor([s.n_groups, s.n_unique, s.n_null_key_rows], dtype=torch.int64,
                             device=dev)
         dist.all_reduce(ints)
+        _count_reduce(ints)
         ent = torch.tensor([s.entropy], dtype=torch.float64, device=dev)
         parts = torch.empty(dist.get_world_size(), dtype=torch.float64, device=dev)
         dist.all_gather_into_tensor(parts, ent)
+        _count_gather(ent.numel() * ent.element_size(), dist.get_world_size())
         out = N.dq_freq_summary()
         out.num_rows = s.num_rows
         out.n_groups, out.n_unique, out.n_null_key_rows = (int(v) for v in ints.cpu().tolist())
@@ -260,6 +298,7 @@ class DistributedFrequencies:
         dev = "cpu" if dist.get_backend() == "gloo" else f"cuda:{self.owned.device}"
         t = torch.tensor([nullg, lit], dtype=torch.int64, device=dev)
         dist.all_reduce(t)
+        _count_reduce(t)
         a, b = (int(v) for v in t.cpu().tolist())
         return a, b
 
@@ -317,6 +356,7 @@ def _raw_keys_pay(data_shard, column, dtype) -> bool:
     v = torch.tensor([groups, rows], dtype=torch.int64,
                      device=_comm_device(f"cuda:{data_shard.device_index()}"))
     dist.all_reduce(v)
+    _count_reduce(v)
     g, r = (int(x) for x in v.cpu().tolist())
     return r > 0 and g >= RAW_MIN_DISTINCT * r
 
@@ -353,6 +393,8 @@ def raw_key_repartition(data_shard, column, dtype, null_as_group: bool = False):
     dist.all_to_all_single(recv[: int(src.sum()) * elem], sent,
                            output_split_sizes=(src * elem).tolist(),
                            input_split_sizes=(counts * elem).tolist())
+    _count_a2a(counts * elem, src * elem, rank)
+    _count_a2a([8] * world, [8] * world, rank)  # the sizes
     recv = recv.to(dev)
     del out, sent
     n_recv = int(src.sum())
@@ -364,6 +406,7 @@ def raw_key_repartition(data_shard, column, dtype, null_as_group: bool = False):
                   null_as_group=null_as_group)
     tot = torch.tensor([rows, nulls.value], dtype=torch.int64, device=cdev)
     dist.all_reduce(tot)
+    _count_reduce(tot)
     tot_rows, tot_nulls = (int(v) for v in tot.cpu().tolist())
     special = np.zeros(3, np.int64)
     if rank == 0:

@@ -229,7 +229,8 @@ def item_buffers_numpy(n: int, seed: int = 7, start: int = 0) -> dict:
     return out
 
 
-def profiling_table_device(n: int, batch_rows: int = 1 << 26, device: str = "cuda:0") -> Table:
+def profiling_table_device(n: int, batch_rows: int = 1 << 26, device: str = "cuda:0",
+                           start: int = 0) -> Table:
     """BASELINE configs[4]'s table: 20 mixed columns generated in HBM -- 10 numeric (id; numViews
     of five Item tables with different seeds; score of four) and 10 strings (name and priority of
     three Item tables; four `description` columns = name + a prefix that carries an https URL in
@@ -241,8 +242,8 @@ def profiling_table_device(n: int, batch_rows: int = 1 << 26, device: str = "cud
         lib.dq_synth_describe.argtypes = [ctypes.c_uint64, ctypes.c_int64, vp, vp, vp, vp, vp]
         lib.dq_synth_describe.restype = ctypes.c_int
         lib._describe_ready = True
-    parts = [item_table_device(n, seed=100 + k, batch_rows=batch_rows, device=device, extra=True)
-             for k in range(5)]
+    parts = [item_table_device(n, seed=100 + k, batch_rows=batch_rows, device=device, extra=True,
+                               start=start) for k in range(5)]
     dev = torch.device(device)
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     fields = [StructField("id", N.INT64)]
@@ -252,7 +253,7 @@ def profiling_table_device(n: int, batch_rows: int = 1 << 26, device: str = "cud
     fields += [StructField(f"priority_{k}", N.UTF8) for k in range(3)]
     fields += [StructField(f"description_{k}", N.UTF8) for k in range(4)]
     batches = []
-    pos = 0
+    pos = start  # (rows [start, start + n): a rank's shard of the same table)
     for bi in range(len(parts[0].batches)):
         b = {"id": parts[0].batches[bi]["id"]}
         for k in range(5):

@@ -22,7 +22,14 @@ configs[1], S10).  Not part of the driver's bench contract; the JSON lines land 
       and one device sort per ApproxQuantile.  One step = one do_analysis_run.  B_alg = every
       buffer of the table once.
 
-Usage: python tools/bench_workloads.py c3|c4|c5 [--rows N] [--steps K] [--warmup W]
+  --gpus N (N > 1): the same workload on N ranks, one per GPU (relaunched under
+      torch.distributed.run), weak scaling: --rows per GPU, each rank a row shard of one table,
+      through the product's distributed paths; rank 0 prints whole-job rows/s over the slowest
+      rank, each rank's ms per step, and each rank's collective bytes per step (run_distributed).
+  --cpu-baseline: the C/OpenMP restatement (oracle/oracle.c) timed on a bounded sample.
+
+Usage: python tools/bench_workloads.py c3|c4|c5 [--rows N] [--steps K] [--warmup W] [--gpus N]
+       [--cpu-baseline]
 """
 import argparse
 import ctypes
@@ -48,8 +55,29 @@ def main():
     ap.add_argument("--cpu-baseline", action="store_true",
                     help="also time the C/OpenMP restatement (oracle/oracle.c) on a bounded sample")
     ap.add_argument("--cpu-rows", type=int, default=1 << 25, help="rows of that sample")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU (weak scaling: --rows per GPU, row shards of one table)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal on a one-GPU box: every rank on cuda:0, collectives over gloo")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: relaunch under torch.distributed.run as a CHILD process, before this
+        # process touches the GPU, and exit with its code (as bench.py does)
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+               str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
     import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        return run_distributed(args, world, rank, local)
     dev = "cuda:0"
     from deequ_amd.synth import item_table_device
     # c5: the per-GPU shard of 1e9 rows over 8 GPUs (20 columns, ~280 B/row with the strings)
@@ -115,23 +143,7 @@ def main():
     elif args.workload == "c5":
         from deequ_amd import analyzers as A
         from deequ_amd.runners import AnalysisRunner
-        num = ["id"] + [f"numViews_{k}" for k in range(5)] + [f"score_{k}" for k in range(4)]
-        strs = ([f"name_{k}" for k in range(3)] + [f"priority_{k}" for k in range(3)]
-                + [f"description_{k}" for k in range(4)])
-        suite = [A.Size()]
-        for c in num + strs:
-            suite += [A.Completeness(c), A.ApproxCountDistinct(c), A.Uniqueness([c]),
-                      A.Distinctness([c]), A.UniqueValueRatio([c]), A.CountDistinct([c]),
-                      A.Entropy(c), A.Histogram(c)]
-        for c in num:
-            suite += [A.Sum(c), A.Mean(c), A.StandardDeviation(c), A.Minimum(c), A.Maximum(c),
-                      A.Compliance(f"{c} non-negative", f"{c} >= 0"), A.ApproxQuantile(c, 0.5)]
-        for c in strs:
-            suite += [A.DataType(c), A.PatternMatch(c, A.Patterns.URL)]
-        suite += [A.Correlation("numViews_0", "score_0"), A.Correlation("numViews_1", "score_1"),
-                  A.Correlation("id", "numViews_2"),
-                  A.MutualInformation("priority_0", "priority_1"),
-                  A.MutualInformation("name_0", "priority_2")]
+        suite = c5_suite()
 
         def step():
             ctx = AnalysisRunner.do_analysis_run(table, suite)
@@ -233,6 +245,125 @@ def main():
                      "kernel": kernel},
         "result": repr(res)[:300],
     }), flush=True)
+
+
+def gather_rank_stats(seconds: float, sent: int, recv: int, device: str):
+    """Every rank's (seconds, collective bytes sent, received), on every rank: one all-gather of
+    three values per rank (on the device over RCCL, host tensors over gloo)."""
+    import torch
+    import torch.distributed as dist
+    from deequ_amd.distributed import _comm_device
+    dev = _comm_device(device)
+    t = torch.tensor([float(seconds), float(sent), float(recv)], dtype=torch.float64, device=dev)
+    out = torch.empty(dist.get_world_size() * 3, dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, t)
+    v = out.cpu().numpy().reshape(-1, 3)
+    return v[:, 0].tolist(), [int(x) for x in v[:, 1]], [int(x) for x in v[:, 2]]
+
+
+def dist_report(workload: str, per_rank_s, steps: int, rows_per_rank: int, sent, recv,
+                backend: str) -> dict:
+    """The JSON line of an N-rank run: whole-job rows/s over the slowest rank's time (max over
+    ranks), each rank's time per step, and each rank's collective bytes per step (over RCCL the
+    xGMI traffic to / from the other ranks)."""
+    world = len(per_rank_s)
+    t = max(per_rank_s)
+    return {"workload": workload, "n_gpus": world, "scaling": "weak", "rows_per_gpu": rows_per_rank,
+            "rows": rows_per_rank * world, "unit": "rows/s", "steps": steps,
+            "value": rows_per_rank * world * steps / t, "ms_per_step": t / steps * 1e3,
+            "per_rank_ms_per_step": [s / steps * 1e3 for s in per_rank_s],
+            "collective_bytes_per_step": {"sent": [b / steps for b in sent],
+                                          "recv": [b / steps for b in recv], "backend": backend}}
+
+
+def run_distributed(args, world: int, rank: int, local: int):
+    """configs[2] / [3] / [4] on `world` ranks, one per GPU: each rank generates its shard (rows
+    [rank * R, (rank + 1) * R) of the same synthetic table, R = --rows) and runs the workload
+    through the product's distributed paths -- the scan's state all-gather + rank-ordered merge
+    (run_scan_distributed), the groupings' raw-key or partial-aggregate all-to-all
+    (compute_frequencies_distributed, via AnalysisRunner) -- K timed steps bracketed by a barrier
+    and a device sync on both sides; rank 0 prints one JSON line (dist_report)."""
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if args.share_gpu:  # (RCCL takes one rank per device: the rehearsal meets over gloo)
+        local = 0
+    torch.cuda.set_device(local)
+    dist.init_process_group("gloo" if args.share_gpu else "nccl", rank=rank, world_size=world)
+    dev = f"cuda:{local}"
+    from deequ_amd import distributed as D
+    from deequ_amd.runners import AnalysisRunner
+    rows = args.rows or {"c3": 1_000_000_000, "c4": 1_250_000_000, "c5": 125_000_000}[args.workload]
+    if args.workload == "c5":
+        from deequ_amd.synth import profiling_table_device
+        table = profiling_table_device(rows, batch_rows=min(args.batch_rows, 1 << 25), device=dev,
+                                       start=rank * rows)
+        torch.cuda.empty_cache()
+        suite = c5_suite()
+    else:
+        from deequ_amd.synth import item_table_device
+        table = item_table_device(rows, seed=9, batch_rows=args.batch_rows, device=dev,
+                                  extra=args.workload == "c4", start=rank * rows)
+    if args.workload == "c3":
+        from deequ_amd.analyzers import Distinctness, Entropy, Histogram, Uniqueness
+        suite = [a for c in ("id", "priority")
+                 for a in (Uniqueness([c]), Distinctness([c]), Entropy(c), Histogram(c))]
+    if args.workload == "c4":
+        from deequ_amd.analyzers import ApproxCountDistinct, Correlation
+        suite = [ApproxCountDistinct("id"), Correlation("id", "score")]
+        specs = [s for a in suite for s in a.aggregation_functions()]
+
+        def step():
+            return D.run_scan_distributed(table, specs)
+    else:
+        def step():
+            ctx = AnalysisRunner.do_analysis_run(table, suite)
+            bad = [str(a) for a in suite if not ctx.metric(a).value.is_success]
+            if bad:
+                raise RuntimeError(f"failed metrics: {bad[:3]}")
+            return len(suite)
+    for _ in range(args.warmup):
+        step()
+    D.reset_comm_bytes()
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    el = time.perf_counter() - t0
+    secs, sent, recv = gather_rank_stats(el, D.COMM_BYTES["sent"], D.COMM_BYTES["recv"], dev)
+    if rank == 0:
+        out = dist_report(args.workload, secs, args.steps, rows, sent, recv, dist.get_backend())
+        out["desc"] = (f"BASELINE.json configs[{ {'c3': 2, 'c4': 3, 'c5': 4}[args.workload] }] on "
+                       f"{world} GPUs, {rows} synthetic rows per GPU (weak scaling)")
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0
+
+
+def c5_suite():
+    from deequ_amd import analyzers as A
+    num = ["id"] + [f"numViews_{k}" for k in range(5)] + [f"score_{k}" for k in range(4)]
+    strs = ([f"name_{k}" for k in range(3)] + [f"priority_{k}" for k in range(3)]
+            + [f"description_{k}" for k in range(4)])
+    suite = [A.Size()]
+    for c in num + strs:
+        suite += [A.Completeness(c), A.ApproxCountDistinct(c), A.Uniqueness([c]),
+                  A.Distinctness([c]), A.UniqueValueRatio([c]), A.CountDistinct([c]),
+                  A.Entropy(c), A.Histogram(c)]
+    for c in num:
+        suite += [A.Sum(c), A.Mean(c), A.StandardDeviation(c), A.Minimum(c), A.Maximum(c),
+                  A.Compliance(f"{c} non-negative", f"{c} >= 0"), A.ApproxQuantile(c, 0.5)]
+    for c in strs:
+        suite += [A.DataType(c), A.PatternMatch(c, A.Patterns.URL)]
+    suite += [A.Correlation("numViews_0", "score_0"), A.Correlation("numViews_1", "score_1"),
+              A.Correlation("id", "numViews_2"),
+              A.MutualInformation("priority_0", "priority_1"),
+              A.MutualInformation("name_0", "priority_2")]
+    return suite
 
 
 def _host_column(col, n):
