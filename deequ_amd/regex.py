@@ -20,10 +20,20 @@ negation, nested escapes and \\d \\D \\s \\S \\w \\W (ASCII, as Java without UNI
 groups ( ), (?: ), alternation, greedy / lazy quantifiers * + ? {n} {n,} {n,m}, lookaheads (?= )
 (?! ), back-references to groups with a finite language (expanded: the CREDITCARD separators),
 ^ / \\A at the start; $ / \\Z (end, or before one final line terminator, "\\r\\n" included) and
-\\z (strict end) at the end; \\b at the start or end of the pattern.  Rejected (a PatternNotSupported
-error, never a silently different answer): patterns that can match the empty string, possessive
-quantifiers, lookbehind, inline flags, \\b / anchors elsewhere, $ after a pattern that may end in
-"\\r" (Java's $ never matches between "\\r\\n"), and automata above ``MAX_STATES``.
+\\z (strict end) at the end; \\b at the start or end of the pattern; the case flag (?i) (?-i)
+(?i: ) (?-i: ) anywhere (ASCII case folding, Java without UNICODE_CASE; to the end of the
+enclosing group, alternatives included).
+
+Nullable patterns (``\\d*``, ``(?i)x?y*``, ``[0-9]*(\\.[0-9]+)?``): the empty match at offset 0
+always exists, so find()'s first match starts there and the row counts iff Java's PREFERRED
+match at offset 0 is non-empty -- compiled from a priority-ordered thread automaton
+(``compile_nullable``: alternation order, greedy / lazy preference, Java's rule that an iteration
+consuming nothing ends its loop), with no anchor but a leading ^.
+
+Rejected (a PatternNotSupported error, never a silently different answer): nullable patterns with
+a lookaround, back-reference or trailing anchor, possessive quantifiers, lookbehind, flags other
+than i, \\b / anchors elsewhere, $ after a pattern that may end in "\\r" (Java's $ never matches
+between "\\r\\n"), and automata above ``MAX_STATES``.
 
 \\b is Java's Bound: a word character is '_' or Character.isLetterOrDigit (categories L* and Nd),
 taken from Python's Unicode database.  Exact for U+0000-U+07FF and the punctuation / symbol blocks
@@ -130,6 +140,7 @@ class Repeat:
     node: object
     lo: int
     hi: Optional[int]  # None = unbounded
+    greedy: bool = True  # (lazy *? +? ?? {n,m}?: the same language, another match preference)
 
 
 @dataclass(frozen=True)
@@ -162,6 +173,7 @@ class _Parser:
         self.s = pattern
         self.i = 0
         self.groups = 0
+        self.ci = False  # CASE_INSENSITIVE ((?i)): ASCII letters only, as Java without UNICODE_CASE
 
     def error(self, msg):
         raise PatternNotSupported(f"{msg} at position {self.i} of /{self.s}/")
@@ -190,7 +202,9 @@ class _Parser:
     def seq(self):
         items = []
         while self.peek() is not None and self.peek() not in "|)":
-            items.append(self.quantified())
+            node = self.quantified()
+            if node is not EMPTY:  # (an inline flag)
+                items.append(node)
         return items[0] if len(items) == 1 else Seq(tuple(items))
 
     def quantified(self):
@@ -212,11 +226,13 @@ class _Parser:
                 return atom
             if isinstance(atom, (Anchor, Look)):
                 self.error("quantified assertion")
-            if self.peek() == "?":  # lazy: same language (find() semantics on non-empty matches)
+            greedy = True
+            if self.peek() == "?":  # lazy: the same language, shortest first
                 self.take()
+                greedy = False
             elif self.peek() == "+":
                 self.error("possessive quantifier")
-            atom = Repeat(atom, lo, hi)
+            atom = Repeat(atom, lo, hi, greedy)
 
     def _is_counted(self):
         j = self.i + 1
@@ -234,12 +250,29 @@ class _Parser:
             return int(a), (int(b) if b else None)
         return int(body), int(body)
 
+    def _group_body(self):
+        """A group's alternatives; an inline flag inside applies up to the group's end."""
+        saved = self.ci
+        node = self.alt()
+        self.ci = saved
+        return node
+
     def atom(self):
         c = self.take()
         if c == "(":
-            if self.s.startswith("?:", self.i):
+            flags = self._inline_flags()
+            if flags is not None:  # (?i) (?-i): up to the end of the enclosing group
+                on, scoped = flags
+                if not scoped:
+                    self.ci = on
+                    return EMPTY
+                saved = self.ci
+                self.ci = on
+                node = Group(self._group_body(), None)
+                self.ci = saved
+            elif self.s.startswith("?:", self.i):
                 self.i += 2
-                node = Group(self.alt(), None)
+                node = Group(self._group_body(), None)
             elif self.s.startswith("?!", self.i) or self.s.startswith("?=", self.i):
                 neg = self.s[self.i + 1] == "!"
                 self.i += 2
@@ -249,7 +282,7 @@ class _Parser:
             else:
                 self.groups += 1
                 idx = self.groups
-                node = Group(self.alt(), idx)
+                node = Group(self._group_body(), idx)
             if self.peek() != ")":
                 self.error("missing ')'")
             self.take()
@@ -266,7 +299,33 @@ class _Parser:
             return self.escape(in_class=False)
         if c in "*+?":
             self.error("dangling quantifier")
-        return Chars(((ord(c), ord(c)),))
+        return Chars(self.fold(((ord(c), ord(c)),)))
+
+    def _inline_flags(self):
+        """At '(' : (?i) / (?-i) -> (on, False); (?i: / (?-i: -> (on, True), consumed; else
+        None.  Other flags (d m s u x U, and combinations) are not supported."""
+        for text, on, scoped in (("?i)", True, False), ("?-i)", False, False),
+                                 ("?i:", True, True), ("?-i:", False, True)):
+            if self.s.startswith(text, self.i):
+                self.i += len(text)
+                return on, scoped
+        j = self.i
+        if self.s.startswith("?", j) and j + 1 < len(self.s) and (self.s[j + 1].isalpha()
+                                                                  or self.s[j + 1] == "-"):
+            self.error("inline flags other than (?i) / (?-i)")
+        return None
+
+    def fold(self, ranges):
+        """Under (?i): the ranges plus the other case of every ASCII letter in them."""
+        if not self.ci:
+            return ranges
+        extra = []
+        for a, b in ranges:
+            for lo, hi, d in ((65, 90, 32), (97, 122, -32)):
+                x, y = max(a, lo), min(b, hi)
+                if x <= y:
+                    extra.append((x + d, y + d))
+        return cs_norm(list(ranges) + extra)
 
     def escape(self, in_class: bool):
         if self.peek() is None:
@@ -306,7 +365,7 @@ class _Parser:
             self.error(f"unsupported escape \\{c}")
         else:
             v = ord(c)
-        return Chars(((v, v),)) if not in_class else ((v, v),)
+        return Chars(self.fold(((v, v),))) if not in_class else ((v, v),)
 
     def char_class(self):
         neg = False
@@ -348,7 +407,7 @@ class _Parser:
                 ranges.append((lo_set[0][0], hi))
             else:
                 ranges.extend(lo_set)
-        r = cs_norm(ranges)
+        r = self.fold(cs_norm(ranges))  # (case folded before the negation, as Java)
         return cs_neg(r) if neg else r
 
 
@@ -914,13 +973,18 @@ def compile_java_regex(pattern: str) -> CompiledRegex:
         start_anchor = items.pop(0).kind
     if items and isinstance(items[-1], Anchor):
         end_anchor = items.pop().kind
+    if nullable(Seq(tuple(items))) and start_anchor in (None, "^") and end_anchor is None:
+        # the empty match at offset 0 always succeeds, so find()'s first match starts there:
+        # whether it is the non-empty one depends on the match PREFERENCE (greedy / lazy,
+        # alternation order), modelled by an ordered-thread automaton
+        return compile_nullable(pattern, Seq(tuple(items)))
     body = expand_backrefs(Seq(tuple(items)))
     if _has_anchor(body):
         raise PatternNotSupported("anchors or \\b inside the pattern")
     if nullable(body):
         raise PatternNotSupported(
-            "a pattern that can match the empty string (PatternMatch counts non-empty first "
-            "matches; Java's choice between an empty and a non-empty match is not modelled)")
+            "a pattern that can match the empty string next to an anchor, a lookaround or a "
+            "back-reference (the first match need not start at offset 0)")
     c = _Compiler()
     s0 = c.nfa.new()
     c.final = c.nfa.new()
@@ -974,6 +1038,192 @@ def compile_java_regex(pattern: str) -> CompiledRegex:
     c.build(body, p, tail)
     c.resolve_lookaheads()
     d = minimize(determinize(c.nfa, s0, frozenset([c.final]), c.univ))
+    return _finish(pattern, d)
+
+
+# ------------------------------------------------------------------------------------------------
+# Nullable patterns: Java's preferred match at offset 0
+#
+# A pattern that can match the empty string (and has no anchor but a leading ^, no lookaround, no
+# back-reference) always matches at offset 0, so find()'s first match starts there, and the row
+# counts iff that match -- the one Java's backtracking prefers -- is non-empty.  Preference is the
+# order of Java's backtracking: alternatives left to right, a greedy quantifier's next iteration
+# before its exit, a lazy one's exit first, an iteration that consumed nothing not repeated.  A
+# leftmost-first Pike program (byte instructions, SPLIT with a preferred branch) simulated with
+# threads in priority order finds exactly that match (RE2's leftmost-first semantics, which are
+# Perl's and Java's for these constructs); the simulation's states -- the ordered list of live
+# threads and whether a match has been recorded at offset 0, later, or not yet -- are finite, and
+# become the states of the byte DFA the device runs (the same table format as every pattern).
+# ------------------------------------------------------------------------------------------------
+_P_BYTE, _P_SPLIT, _P_MATCH, _P_ENTER, _P_BACK = 0, 1, 2, 3, 4
+
+
+class _Prog:
+    """BYTE(mask, next) | SPLIT(preferred, other) | MATCH | ENTER(loop, next) -- an iteration of a
+    loop begins | BACK(loop, progressed, empty) -- it ends: continue at `progressed` if it consumed
+    input, else at `empty` (Java Pattern.Loop / LazyLoop: an iteration that consumed nothing ends
+    the loop, whatever the count)."""
+
+    def __init__(self):
+        self.op: List[int] = []
+        self.arg: List[list] = []
+        self.n_loops = 0
+
+    def emit(self, op, *arg) -> int:
+        self.op.append(op)
+        self.arg.append(list(arg))
+        return len(self.op) - 1
+
+    def choice(self, body: int, exit_: int, greedy: bool) -> int:
+        return self.emit(_P_SPLIT, *((body, exit_) if greedy else (exit_, body)))
+
+
+def _prog_build(prog: _Prog, node, nxt: int) -> int:
+    """Compiles `node` to continue at pc `nxt`; returns its entry pc (built back to front, so
+    every successor exists when an instruction is emitted)."""
+    if isinstance(node, Chars):
+        entries = []
+        for a, b in node.ranges:
+            for seq in _utf8_ranges(a, b):
+                pc = nxt
+                for lo, hi in reversed(seq):
+                    pc = prog.emit(_P_BYTE, _mask(lo, hi), pc)
+                entries.append(pc)
+        if not entries:  # an empty class matches nothing
+            return prog.emit(_P_BYTE, 0, nxt)
+        pc = entries[-1]
+        for e in reversed(entries[:-1]):  # disjoint byte sequences: the order is immaterial
+            pc = prog.emit(_P_SPLIT, e, pc)
+        return pc
+    if isinstance(node, Seq):
+        pc = nxt
+        for x in reversed(node.items):
+            pc = _prog_build(prog, x, pc)
+        return pc
+    if isinstance(node, Alt):
+        entries = [_prog_build(prog, o, nxt) for o in node.options]
+        pc = entries[-1]
+        for e in reversed(entries[:-1]):
+            pc = prog.emit(_P_SPLIT, e, pc)  # the left alternative first
+        return pc
+    if isinstance(node, Group):
+        return _prog_build(prog, node.node, nxt)
+    if isinstance(node, Repeat):
+        return _prog_repeat(prog, node, nxt)
+    raise PatternNotSupported(f"{type(node).__name__} in a pattern that can match the empty string")
+
+
+def _prog_repeat(prog: _Prog, node: Repeat, exit_: int) -> int:
+    """x{lo,hi} as lo mandatory copies then the optional part (a loop for hi=None, hi-lo nested
+    optional copies otherwise).  A body that can match the empty string is bracketed by
+    ENTER/BACK so that an empty iteration leaves the repeat (to `exit_`), as in Java."""
+    guard = nullable(node.node)
+    lid = prog.n_loops
+    prog.n_loops += 1
+
+    def copy(progressed: int) -> int:
+        if not guard:
+            return _prog_build(prog, node.node, progressed)
+        back = prog.emit(_P_BACK, lid, progressed, exit_)
+        return prog.emit(_P_ENTER, lid, _prog_build(prog, node.node, back))
+
+    if node.hi is None:
+        loop = prog.emit(_P_SPLIT, -1, -1)
+        body = copy(loop)
+        prog.arg[loop] = [body, exit_] if node.greedy else [exit_, body]
+        pc = loop
+    else:
+        pc = exit_
+        for _ in range(node.hi - node.lo):
+            pc = prog.choice(copy(pc), exit_, node.greedy)
+    for _ in range(node.lo):
+        pc = copy(pc)
+    return pc
+
+
+def _threads(prog: _Prog, pcs) -> Tuple[int, ...]:
+    """The priority-ordered epsilon closure of `pcs` (each started with no loop entered at this
+    position): SPLITs take the preferred branch first; a BACK whose loop was ENTERed on the same
+    path at this position (the iteration consumed nothing) takes its `empty` exit; BYTE and MATCH
+    pcs are kept at their first, highest-priority, occurrence."""
+    out: List[int] = []
+    kept = set()
+    seen = set()
+    for start in pcs:
+        stack = [(start, frozenset())]
+        while stack:
+            q, entered = stack.pop()
+            op = prog.op[q]
+            if op in (_P_BYTE, _P_MATCH):
+                if q not in kept:
+                    kept.add(q)
+                    out.append(q)
+                continue
+            if (q, entered) in seen:
+                continue
+            seen.add((q, entered))
+            arg = prog.arg[q]
+            if op == _P_SPLIT:
+                stack.append((arg[1], entered))
+                stack.append((arg[0], entered))  # (popped first: the preferred branch)
+            elif op == _P_ENTER:
+                stack.append((arg[1], entered | {arg[0]}))
+            else:  # BACK
+                stack.append((arg[2] if arg[0] in entered else arg[1], entered))
+    return tuple(out)
+
+
+def compile_nullable(pattern: str, ast) -> CompiledRegex:
+    """The byte DFA of "Java's preferred match at offset 0 is non-empty" (see above)."""
+    if _has_look(ast) or _backrefs(ast):
+        raise PatternNotSupported("a lookaround or back-reference in a pattern that can match "
+                                  "the empty string")
+    prog = _Prog()
+    match = prog.emit(_P_MATCH)
+    start = _prog_build(prog, ast, match)
+    # DFA states: (threads, at0, best) -- best: 0 none yet, 1 the empty match, 2 a non-empty one
+    ACC, REJ = 0, 1
+    states: Dict[Tuple, int] = {}
+    table: List[List[int]] = [[ACC] * NSYM, [REJ] * NSYM]
+    accept = [True, False]
+    work: List[Tuple] = []
+
+    def intern(key) -> int:
+        threads, at0, best = key
+        if not threads:  # decided
+            return ACC if best == 2 else REJ
+        if key not in states:
+            states[key] = len(table)
+            table.append([REJ] * NSYM)
+            accept.append(False)
+            work.append(key)
+            if len(table) > MAX_STATES:
+                raise PatternNotSupported(f"automaton exceeds {MAX_STATES} states")
+        return states[key]
+
+    def step(threads, at0, best, byte):
+        """One position: threads in priority order; a MATCH records the match and cuts every
+        lower-priority thread; BYTE threads that take `byte` (None: end of text) advance."""
+        nxt = []
+        for q in threads:
+            if prog.op[q] == _P_MATCH:
+                best = 1 if at0 else 2
+                break
+            if byte is not None and (prog.arg[q][0] >> byte) & 1:
+                nxt.append(prog.arg[q][1])
+        return _threads(prog, nxt), best
+
+    s0 = intern((_threads(prog, [start]), True, 0))
+    while work:
+        key = work.pop()
+        threads, at0, best = key
+        row = table[states[key]]
+        for byte in range(256):
+            t2, b2 = step(threads, at0, best, byte)
+            row[byte] = intern((t2, False, b2))
+        _, b_end = step(threads, at0, best, None)
+        row[EOT] = ACC if b_end == 2 else REJ
+    d = minimize(DFA(table, accept, s0))
     return _finish(pattern, d)
 
 

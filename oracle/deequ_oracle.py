@@ -718,8 +718,31 @@ def java_regex_to_python(pattern: str) -> str:
     digits (Python's ASCII \\b would call every non-ASCII code point a non-word one)."""
     global _JAVA_WORD
     out, i, in_class = [], 0, False
+    # Java's inline (?i) / (?-i) applies to the end of the enclosing group, alternatives included
+    # (Python's applies to the whole pattern): restated as scoped (?i:...) groups closed at each
+    # '|' and ')' of that group and re-opened after a '|'.  (?i) is ASCII-only in Java without
+    # UNICODE_CASE, as in Python under re.ASCII.
+    scopes = [[]]
     while i < len(pattern):
         c = pattern[i]
+        if not in_class:
+            m = re.match(r"\(\?(-?)i\)", pattern[i:])
+            if m:
+                opener = "(?-i:" if m.group(1) else "(?i:"
+                out.append(opener)
+                scopes[-1].append(opener)
+                i += m.end()
+                continue
+            if c == "(":
+                scopes.append([])
+            elif c == ")" and len(scopes) > 1:
+                out.append(")" * len(scopes.pop()))
+            elif c == "|":
+                out.append(")" * len(scopes[-1]))
+                out.append("|")
+                out.extend(scopes[-1])
+                i += 1
+                continue
         if c == "\\":
             e = pattern[i:i + 2]
             if not in_class and e == "\\b":
@@ -753,6 +776,7 @@ def java_regex_to_python(pattern: str) -> str:
         else:
             out.append(c)
         i += 1
+    out.append(")" * len(scopes[0]))
     return "".join(out)
 
 

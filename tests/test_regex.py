@@ -3,6 +3,7 @@ Pattern.find() (oracle/deequ_oracle.py regex_find_nonempty, Python `re`), and th
 PatternMatch known answers (AnalyzerTests.scala:595-688).  Host runs of the compiled automaton
 (CompiledRegex.matches, the same table the device walks); no GPU."""
 import random
+import zlib
 
 import pytest
 
@@ -65,14 +66,54 @@ FUZZ = [
 
 @pytest.mark.parametrize("pattern,alphabet,max_len", FUZZ)
 def test_automaton_matches_java_find_semantics(pattern, alphabet, max_len):
-    rng = random.Random(hash(pattern) & 0xFFFF)
+    rng = random.Random(zlib.crc32(pattern.encode()))
     c = compile_java_regex(pattern)
     for s in _random_strings(rng, alphabet, 3000, max_len):
         assert c.matches(s) == regex_find_nonempty(s, pattern), (pattern, s)
 
 
-@pytest.mark.parametrize("pattern", [r"a*", r"(?<=a)b", r"(?i)abc", r"a++", r"x\Bz", r"(a|)",
-                                     r"a\s$"])
+# Patterns that can match the empty string: the row counts iff Java's PREFERRED match at offset 0
+# is non-empty (greedy / lazy, alternation order, an empty iteration ending its loop), and the case
+# flag (?i) scoped to its group
+NULLABLE = [
+    (r"\d*", "12a 3", 7),
+    (r"\d*?", "12a", 5),
+    (r"(?i)http", "hHtTpPs:", 7),
+    (r"(?i)ab*|c", "aAbBcC", 6),
+    (r"a(?i)b|c", "aAbBcC", 6),
+    (r"x(?i:y)z", "xXyYzZ", 6),
+    (r"(?i)[^a-c]x", "aAbBxXdD", 6),
+    (r"[0-9]*(\.[0-9]+)?", "12.3.a", 8),
+    (r"(a|ab)*c?", "abc", 8),
+    (r"(ab|a)*?b?", "abc", 8),
+    (r"(?:a??)+b?", "abx", 6),
+    (r"(a?){2,}b?", "abx", 6),
+    (r"(a?){1,3}?b", "abx", 6),
+    (r"(|a)b?", "abx", 5),
+    (r"^\s*\w*", " \tab_1-", 8),
+    (r"(?:x|\u00e9)*y?", "x\u00e9y\u00c9", 6),
+]
+
+
+@pytest.mark.parametrize("pattern,alphabet,max_len", NULLABLE)
+def test_nullable_patterns_match_javas_preferred_match(pattern, alphabet, max_len):
+    rng = random.Random(zlib.crc32(pattern.encode()))
+    c = compile_java_regex(pattern)
+    for s in [""] + _random_strings(rng, alphabet, 3000, max_len):
+        assert c.matches(s) == regex_find_nonempty(s, pattern), (pattern, s)
+
+
+def test_nullable_known_answers():
+    # Java: "12ab".find(\d*) -> "12"; "ab12" -> "" at 0; lazy \d*? -> "" always
+    assert [compile_java_regex(r"\d*").matches(s) for s in ["12ab", "ab12", ""]] == [True, False, False]
+    assert not compile_java_regex(r"\d*?").matches("123")
+    assert [compile_java_regex(r"(?i)http").matches(s) for s in ["HTTP", "xHtTp", "htp"]] == [True, True, False]
+    # an empty first iteration ends Java's loop: (?:a??)+ prefers "" and never iterates again
+    assert not compile_java_regex(r"(?:a??)+b?").matches("ab")
+
+
+@pytest.mark.parametrize("pattern", [r"(?<=a)b", r"a++", r"x\Bz", r"a\s$", r"a*$", r"(?s)a",
+                                     r"(?=x)a*", r"(a?)\1"])
 def test_unsupported_patterns_are_refused(pattern):
     with pytest.raises(PatternNotSupported):
         compile_java_regex(pattern)

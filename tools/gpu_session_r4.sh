@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-4 session: the whole -m gpu suite, then the multi-GPU harness rehearsed as 2 ranks on one
+# GPU (gloo), and the configs[2] / configs[3] lines with their CPU baselines.  TAG names outputs.
+set -o pipefail
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+O=gpurun_out
+T=${TAG:-s}
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests_$T.log 2>&1 &&
+timeout -k 10 300 python -u tools/bench_workloads.py c3 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c3_$T.json 2>&1 &&
+timeout -k 10 300 python -u tools/bench_workloads.py c4 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c4_$T.json 2>&1 &&
+timeout -k 10 400 python -u tools/bench_workloads.py c3 --steps 3 --cpu-baseline > $O/wl_c3_$T.json 2>&1 &&
+timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 5 --cpu-baseline > $O/wl_c4_$T.json 2>&1
