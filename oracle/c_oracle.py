@@ -47,6 +47,9 @@ def lib():
                               ctypes.POINTER(ctypes.c_int)]
         L.or_freq_i64.argtypes = [vp, vp, i64, i64, ctypes.POINTER(i64), ctypes.POINTER(i64),
                                   ctypes.POINTER(ctypes.c_double)]
+        L.or_numeric_f64.argtypes = [vp, vp, i64, ctypes.c_double, i32, ctypes.POINTER(OrNumericD)]
+        L.or_dfa_count.argtypes = [vp, vp, vp, i64, vp, vp, vp, i32, i32, i32]
+        L.or_dfa_count.restype = i64
         _LIB = L
     return _LIB
 
@@ -132,3 +135,25 @@ def s10_fused(buf: dict, items=("high", "low"), threads: int = 1) -> OrS10:
                        _p(buf["priority_data"]), _p(buf["priority_valid"]), buf["n"], _p(lbuf),
                        _p(lo), len(items), threads, ctypes.byref(out))
     return out
+
+
+class OrNumericD(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_int64), ("sum", ctypes.c_double), ("min", ctypes.c_double),
+                ("max", ctypes.c_double), ("n", ctypes.c_double), ("avg", ctypes.c_double),
+                ("m2", ctypes.c_double), ("pred_true", ctypes.c_int64)]
+
+
+def numeric_f64(values, valid_bits, lit: float = 0.0, threads: int = 1) -> OrNumericD:
+    out = OrNumericD()
+    lib().or_numeric_f64(_p(values), _p(valid_bits), len(values), float(lit), int(threads),
+                         ctypes.byref(out))
+    return out
+
+
+def dfa_count(offsets, data, valid_bits, n, compiled, threads: int = 1) -> int:
+    """Matching non-NULL rows of a utf8 column under a CompiledRegex (deequ_amd/regex.py) table."""
+    bc = np.frombuffer(compiled.byte_class, np.uint8)
+    st = np.frombuffer(compiled.accept, np.uint8)
+    nx = np.asarray(compiled.next, np.uint16)
+    return int(lib().or_dfa_count(_p(offsets), _p(data), _p(valid_bits), int(n), _p(bc), _p(st),
+                                  _p(nx), compiled.n_classes, compiled.start, int(threads)))

@@ -608,3 +608,80 @@ void or_freq(int type, const void* values, const uint8_t* data, const uint8_t* v
   free(hs);
   free(cnt);
 }
+
+/* ------------------------------------------- configs[4] baseline helpers (cpu_baseline) ---- */
+/* Double column: count, Sum (double), Min, Max, CentralMomentAgg (n, avg, m2) and `x >= lit`
+ * (M/analyzers/Sum.scala:35, Minimum.scala:36, Maximum.scala:36, StandardDeviation.scala:37-44,
+ * Compliance.scala:47-49), partition partials merged in partition order. */
+typedef struct {
+  int64_t count;
+  double sum, min, max, n, avg, m2;
+  int64_t pred_true;
+} or_numeric_d;
+
+void or_numeric_f64(const double* v, const uint8_t* valid, int64_t n, double lit, int nthreads,
+                    or_numeric_d* out) {
+  if (nthreads < 1) nthreads = 1;
+  or_numeric_d* parts = (or_numeric_d*)calloc((size_t)nthreads, sizeof(or_numeric_d));
+#pragma omp parallel for num_threads(nthreads) schedule(static, 1)
+  for (int p = 0; p < nthreads; ++p) {
+    int64_t r0 = n * p / nthreads, r1 = n * (p + 1) / nthreads;
+    or_numeric_d s;
+    memset(&s, 0, sizeof(s));
+    s.min = INFINITY;
+    s.max = -INFINITY;
+    for (int64_t r = r0; r < r1; ++r) {
+      if (!bit(valid, r)) continue;
+      const double x = v[r];
+      s.count += 1;
+      s.sum += x;
+      s.min = x < s.min ? x : s.min;
+      s.max = x > s.max ? x : s.max;
+      double n2 = s.n + 1.0, delta = x - s.avg, delta_n = delta / n2;
+      s.avg += delta_n;
+      s.m2 += delta * (delta - delta_n);
+      s.n = n2;
+      s.pred_true += x >= lit;
+    }
+    parts[p] = s;
+  }
+  or_numeric_d a;
+  memset(&a, 0, sizeof(a));
+  a.min = INFINITY;
+  a.max = -INFINITY;
+  for (int p = 0; p < nthreads; ++p) {
+    const or_numeric_d* b = &parts[p];
+    if (!b->count) continue;
+    double nn = a.n + b->n, delta = b->avg - a.avg, delta_n = nn == 0.0 ? 0.0 : delta / nn;
+    a.avg += delta_n * b->n;
+    a.m2 += b->m2 + delta * delta_n * a.n * b->n;
+    a.n = nn;
+    a.count += b->count;
+    a.sum += b->sum;
+    a.min = b->min < a.min ? b->min : a.min;
+    a.max = b->max > a.max ? b->max : a.max;
+    a.pred_true += b->pred_true;
+  }
+  *out = a;
+  free(parts);
+}
+
+/* PatternMatch's per-row test as a walk of a byte DFA (the table layout of CompiledRegex.blob:
+ * byte_class[256], status per state 0 undecided / 1 accepted / 2 rejected, u16 next[state][class],
+ * the last class = end of text): the count of matching non-NULL rows.  A timing baseline for the
+ * regex scan (a DFA walk is the fastest CPU form of it; Spark runs java.util.regex per row). */
+int64_t or_dfa_count(const int32_t* off, const uint8_t* data, const uint8_t* valid, int64_t n,
+                     const uint8_t* byte_class, const uint8_t* status, const uint16_t* next,
+                     int n_classes, int start, int nthreads) {
+  int64_t hits = 0;
+#pragma omp parallel for num_threads(nthreads) reduction(+ : hits) schedule(static)
+  for (int64_t r = 0; r < n; ++r) {
+    if (!bit(valid, r)) continue;
+    int st = start;
+    for (int32_t i = off[r]; i < off[r + 1] && !status[st]; ++i)
+      st = next[st * n_classes + byte_class[data[i]]];
+    if (!status[st]) st = next[st * n_classes + n_classes - 1];
+    hits += status[st] == 1;
+  }
+  return hits;
+}

@@ -56,3 +56,39 @@ def test_c_frequency_family_matches_python_oracle(kind, threads):
     for c, r in zip(tc, tr):
         key = "NullValue" if r < 0 or vals[r] is None else O.java_to_string(vals[r], kind)
         assert hist[key] == c
+
+
+@pytest.mark.parametrize("threads", [1, 5])
+def test_c_double_column_aggregates_match_python_oracle(threads):
+    """or_numeric_f64 (the configs[4] CPU baseline's double columns) against the Python oracle."""
+    rng = np.random.default_rng(threads)
+    n = 20_000
+    vals = rng.normal(3.0, 7.0, n)
+    mask = rng.random(n) < 0.05
+    arr = pa.array(vals, mask=mask, type=pa.float64())
+    v = np.frombuffer(arr.buffers()[1], np.float64)[:n].copy()
+    valid = np.frombuffer(arr.buffers()[0], np.uint8).copy()
+    got = C.numeric_f64(v, valid, 0.0, threads)
+    py = [None if m else float(x) for x, m in zip(vals, mask)]
+    t = O.OTable({"x": py}, {"x": "double"})
+    nn, avg, m2 = O.agg_stddev(t, "x", None)
+    assert got.count == sum(x is not None for x in py)
+    assert got.min == O.agg_min(t, "x", None) and got.max == O.agg_max(t, "x", None)
+    assert abs(got.sum - math.fsum(x for x in py if x is not None)) <= 1e-9 * abs(got.sum)
+    assert got.n == nn and abs(got.avg - avg) <= 1e-12 * abs(avg) and abs(got.m2 - m2) <= 1e-12 * m2
+    assert got.pred_true == sum(1 for x in py if x is not None and x >= 0.0)
+
+
+@pytest.mark.parametrize("pattern", [r"(https?|ftp)://[^\s/$.?#].[^\s]*", r"\d*", r"(?i)ab+"])
+def test_c_dfa_walk_counts_like_the_python_oracle(pattern):
+    """or_dfa_count (the PatternMatch timing baseline) walks the compiled table: the same hits as
+    the oracle's Java find() restatement."""
+    import random
+    from deequ_amd.regex import compile_java_regex
+    rng = random.Random(3)
+    alpha = list("abAB09 :/.htpsé") + ["http://", "ftp://"]
+    rows = [None if rng.random() < 0.05 else
+            "".join(rng.choice(alpha) for _ in range(rng.randint(0, 12))) for _ in range(5000)]
+    off, data, valid = _buffers(pa.array(rows, pa.string()))
+    got = C.dfa_count(off, data, valid, len(rows), compile_java_regex(pattern), threads=3)
+    assert got == sum(O.regex_find_nonempty(r, pattern) for r in rows if r is not None)

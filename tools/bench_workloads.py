@@ -410,8 +410,42 @@ def cpu_baseline(args, table, min_seconds: float = 10.0):
             C.hll(5, idv, None, idm, n, threads)
             C.corr(idv, idm, sv, sm, threads)
         what = "ApproxCountDistinct(id) + Correlation(id, score): or_hll + or_corr"
-    else:
-        return None
+    else:  # c5
+        import numpy as np
+        from deequ_amd.analyzers import Patterns
+        from deequ_amd.regex import compile_java_regex
+        url = compile_java_regex(Patterns.URL)
+        names = [f.name for f in table.schema.fields]
+        cols = {c: _host_column(b0[c], n) for c in names}
+        ints = [c for c in names if c == "id" or c.startswith("numViews")]
+        dbls = [c for c in names if c.startswith("score")]
+        strs = [c for c in names if c not in ints and c not in dbls]
+
+        def one():
+            for c in ints:
+                v, _, m = cols[c]
+                C.numeric_i64(v, m, 17, 0, threads)          # Size..Max, Compliance(>= 0)
+                C.hll(5, v, None, m, n, threads)
+                C.freq("long", v, None, m, n, n, True, 1000, threads)
+                np.sort(v)                                   # ApproxQuantile (sort stand-in)
+            for c in dbls:
+                v, _, m = cols[c]
+                d = v.view(np.float64)
+                C.numeric_f64(d, m, 0.0, threads)
+                C.hll(7, d, None, m, n, threads)
+                C.freq("long", v, None, m, n, n, True, 1000, threads)  # on the value bits
+                np.sort(d)
+            for c in strs:
+                o, d, m = cols[c]
+                C.hll(8, o, d, m, n, threads)
+                C.freq("string", o, d, m, n, n, True, 1000, threads)
+                C.dfa_count(o, d, m, n, url, threads)
+            for x, y in (("numViews_0", "score_0"), ("numViews_1", "score_1")):
+                C.corr(cols[x][0], cols[x][2], cols[y][0].view(np.float64), cols[y][2], threads)
+        what = ("configs[4] minus DataType and MutualInformation: per numeric column the scan "
+                "aggregates (or_numeric_i64/_f64), or_hll, or_freq (Uniqueness..Histogram) and a "
+                "numpy sort for ApproxQuantile; per string column or_hll, or_freq and the URL "
+                "PatternMatch as a DFA walk (or_dfa_count); two Correlations")
     one()
     reps, t0 = 0, time.perf_counter()
     while True:
