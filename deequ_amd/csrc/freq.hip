@@ -1038,6 +1038,210 @@ __global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t*
   for (int i = tid; i < kBuckets; i += kPreThreads) ph[(int64_t)blockIdx.x * kBuckets + i] = bh[i];
 }
 
+// ------------------------------------------------------------------------------------------------
+// Phase A, exact rows into bucket pieces (the pieces layout of freq_phaseA<false, false> with
+// a.pstart set; same tile ranges, dedupe table and bypass probing, same records).  A lean kernel
+// of its own: 512 threads x 16 rounds per 8192-row tile and ~80 KB of LDS, so TWO workgroups
+// share a CU and one's loads overlap the other's sort and stores (the generic kernel, 1024 threads
+// at 128 VGPRs with spills, ran one workgroup per CU with every phase behind a barrier).  The
+// bucket-counting atomic returns the row's rank in its bucket, so the counting sort takes one LDS
+// atomic per row instead of two.
+// ------------------------------------------------------------------------------------------------
+constexpr int kAXThreads = 512;
+// row base + r of a fixed-width column, the base (wave-uniform) applied to the pointer
+template <int TY>
+DQ_DEV uint64_t kload_at(const void* v, int64_t base, int r) {
+  if constexpr (TY == DQ_BOOL) {
+    return kwiden(TY, v, base + r);
+  } else {
+    constexpr int W = TY == DQ_INT8 ? 1 : TY == DQ_INT16 ? 2 : (TY == DQ_INT32 || TY == DQ_FLOAT32) ? 4 : 8;
+    return kwiden(TY, reinterpret_cast<const char*>(v) + base * W, r);
+  }
+}
+template <int TY>
+__global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4 waves per SIMD: two workgroups per CU
+  constexpr int T = FM<false>::kTile, R = T / kAXThreads, D = AKeys<false, false>::kDedupe;
+  static_assert(R <= 32, "round bits");
+  __shared__ uint32_t bh[kBuckets];     // counts of the tile's raw rows, then their sorted starts
+  __shared__ uint32_t gdel[kBuckets];   // region slot of a sorted position, minus that position
+  __shared__ uint32_t wcur[kBuckets];   // each bucket's next region slot (the workgroup's piece)
+  __shared__ unsigned long long dkey[D], dcnt[D];
+  __shared__ uint64_t stash[T];
+  __shared__ uint32_t s_wave[kAXThreads / 64];
+  __shared__ uint32_t s_hits, s_bypass, s_full;
+  const int tid = threadIdx.x;
+  const KeyCol& c = a.ks.cols[0];
+  const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
+  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
+  const int64_t t1 = min(t0 + (int64_t)a.tiles_per_wg, n_tiles);
+  for (int i = tid; i < D; i += kAXThreads) {
+    dkey[i] = kEmptyKey;
+    dcnt[i] = 0;
+  }
+  {
+    uint32_t all;
+    const uint32_t bb = block_excl_scan(a.ptot[tid], s_wave, all);  // (kAXThreads == kBuckets)
+    const uint32_t st = bb + a.ph[(int64_t)blockIdx.x * kBuckets + tid];
+    wcur[tid] = st;
+    a.pstart[(int64_t)blockIdx.x * kBuckets + tid] = st;
+    bh[tid] = 0;
+    // the batch's chunk rows hold no records: empty histograms
+    for (int64_t r = t0; r < t1; ++r)
+      for (int i = tid; i < kHistRow; i += kAXThreads) a.hist[r * kHistRow + i] = 0;
+    for (int i = tid; i < kHistRow; i += kAXThreads) a.hist[(n_tiles + blockIdx.x) * kHistRow + i] = 0;
+  }
+  if (tid == 0) {
+    s_bypass = 0;
+    s_full = 0;
+  }
+  unsigned long long nulls = 0, nullg = 0, dbg_bypass = 0;
+  uint64_t* out = reinterpret_cast<uint64_t*>(a.recs);
+  // the full-tile loads: 8-byte-aligned bitmap words, tiles on 64-row boundaries
+  const bool full_ok = (reinterpret_cast<uintptr_t>(c.valid) & 7u) == 0 && (a.tile_items & 63) == 0;
+  // 1 claimed, 2 added, 0 table full (the row stays raw)
+  auto dedupe = [&](uint64_t h) -> int {
+    uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
+    for (int pr = 0; pr < 4; ++pr) {
+      unsigned long long k = lds_load(reinterpret_cast<const uint64_t*>(&dkey[slot]));
+      if (k == kEmptyKey) {
+        const unsigned long long prev = atomicCAS(&dkey[slot], kEmptyKey, (unsigned long long)h);
+        if (prev == kEmptyKey) {
+          atomicAdd(&dcnt[slot], 1ULL);
+          return 1;
+        }
+        k = prev;
+      }
+      if (k == h) {
+        atomicAdd(&dcnt[slot], 1ULL);
+        return 2;
+      }
+      slot = (slot + 1) & (D - 1);
+    }
+    return 0;
+  };
+  __syncthreads();
+  {
+#pragma unroll 1
+    for (int64_t t = t0; t < t1; ++t) {
+      const int64_t i0 = t * a.tile_items, i1 = min(i0 + a.tile_items, a.n_items);
+      const bool probe = ((t - t0) & 7) == 0;
+      // 1. loads, then hash.  A full tile: each round's rows from a uniform base (one offset
+      // register) and each wave's 64 validity bits as one scalar load of a bitmap word.  The last
+      // tile: branch-free clamped loads (an out-of-tile lane re-reads the tile's last row).
+      uint64_t h[R];
+      uint32_t ok = 0, vb = ~0u;
+      if (i1 - i0 == T && full_ok) {
+        ok = (1u << R) - 1u;
+#pragma unroll
+        for (int j = 0; j < R; ++j) h[j] = kload_at<TY>(c.values, i0 + (int64_t)j * kAXThreads, tid);
+        if (c.valid) {
+          const int64_t wrow = i0 + 64 * (int64_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+          vb = 0;
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            const uint64_t w =
+                *reinterpret_cast<const uint64_t*>(c.valid + ((wrow + (int64_t)j * kAXThreads) >> 3));
+            vb |= (uint32_t)((w >> __lane_id()) & 1u) << j;
+          }
+        }
+      } else {
+        int64_t ic[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          const int64_t i = i0 + (int64_t)j * kAXThreads + tid;
+          ok |= (i < i1 ? 1u : 0u) << j;
+          ic[j] = i < i1 ? i : i1 - 1;
+        }
+#pragma unroll
+        for (int j = 0; j < R; ++j) h[j] = kwiden(TY, c.values, ic[j]);
+        if (c.valid) {
+          uint32_t byte[R];
+#pragma unroll
+          for (int j = 0; j < R; ++j) byte[j] = c.valid[ic[j] >> 3];
+          vb = 0;
+#pragma unroll
+          for (int j = 0; j < R; ++j) vb |= ((byte[j] >> (ic[j] & 7)) & 1u) << j;
+        }
+      }
+      const uint32_t keyed = ok & vb;
+      {
+        const unsigned long long nn = (unsigned long long)__builtin_popcount(ok & ~vb);
+        const unsigned long long ng = a.ks.null_as_group ? nn : 0ULL;
+        nullg += ng;
+        nulls += nn - ng;
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) h[j] = fmix_bij(exact_canon(a.ks, h[j]));
+      // 2. dedupe: round 0 of a probing tile measures the hit rate, which decides the bypass
+      uint32_t raw = keyed;
+      if (probe) {
+        if (tid == 0) s_hits = 0;
+        __syncthreads();
+        int res = -1;
+        if (keyed & 1u) {
+          res = dedupe(h[0]);
+          if (res) raw &= ~1u;
+          if (!res) atomicAdd(&s_full, 1u);
+        }
+        const uint32_t wh = (uint32_t)__builtin_popcountll(__ballot(res == 2));  // whole wave
+        if (__lane_id() == 0 && wh) atomicAdd(&s_hits, wh);
+        __syncthreads();
+        if (tid == 0) s_bypass = s_hits * 16u < (uint32_t)kAXThreads ? 1u : 0u;
+        __syncthreads();
+        dbg_bypass += tid == 0 ? s_bypass : 0u;
+      }
+      if (!s_bypass) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          if (!((keyed >> j) & 1u) || (probe && j == 0)) continue;
+          const int res = dedupe(h[j]);
+          if (res) raw &= ~(1u << j);
+          else atomicAdd(&s_full, 1u);
+        }
+      }
+      if (!__syncthreads_or(raw ? 1 : 0)) continue;  // every row collapsed: nothing to write
+      // 3. counting sort by bucket: the counting atomic gives each raw row its rank
+      uint32_t rk[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if ((raw >> j) & 1u) rk[j] = atomicAdd(&bh[bucket_of(h[j])], 1u);
+      __syncthreads();
+      uint32_t ctotal;
+      const uint32_t cnt = bh[tid];
+      const uint32_t ex = block_excl_scan(cnt, s_wave, ctotal);
+      bh[tid] = ex;
+      gdel[tid] = wcur[tid] - ex;
+      wcur[tid] += cnt;
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if ((raw >> j) & 1u) stash[bh[bucket_of(h[j])] + rk[j]] = h[j];
+      __syncthreads();
+      // 4. the sorted tile to each bucket's next slots: runs of ~16 records per bucket
+      for (uint32_t i = tid; i < ctotal; i += kAXThreads) {
+        const uint64_t hh = stash[i];
+        out[(uint32_t)(gdel[bucket_of(hh)] + i)] = (hh << 8) | 1u;  // the count-1 digit code
+      }
+      __syncthreads();
+      bh[tid] = 0;  // (visible after the next tile's barriers)
+    }
+  }
+  // the collapsed groups into their buckets' pieces, then the pieces' lengths
+  __syncthreads();
+  for (int sl = tid; sl < D; sl += kAXThreads) {
+    const uint64_t k = dkey[sl];
+    if (k == kEmptyKey) continue;
+    const uint32_t b = bucket_of(k);
+    for_digits(dcnt[sl], [&](uint32_t code) { out[atomicAdd(&wcur[b], 1u)] = (k << 8) | code; });
+  }
+  __syncthreads();
+  a.plen[(int64_t)blockIdx.x * kBuckets + tid] = wcur[tid] - a.pstart[(int64_t)blockIdx.x * kBuckets + tid];
+  wave_count(&a.counters[C_NULL_ROWS], nulls);
+  wave_count(&a.counters[C_NULL_GROUP], nullg);
+  wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
+  if (tid == 0 && s_full) atomicAdd(&a.counters[C_DBG_FULL], (unsigned long long)s_full);
+}
+
 // Per bucket (one block each): ph[*][b] -> its exclusive prefix over the workgroups, tot[b] = sum.
 __global__ void __launch_bounds__(256) freq_prepass_scan(uint32_t* ph, int64_t n_wg, uint32_t* tot) {
   __shared__ uint32_t s_wave[4];
@@ -3345,7 +3549,28 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
   a.ptot = f->ptot.p;
   a.pstart = f->pstart.p + (size_t)f->n_prow * kBuckets;
   a.plen = f->plen.p + (size_t)f->n_prow * kBuckets;
-  launch_phaseA<false>(f, a, false);
+  static const bool generic = [] {  // DQ_FREQ_GENERIC_A=1: A/B hook, the generic kernel
+    const char* e = getenv("DQ_FREQ_GENERIC_A");
+    return e && atoi(e) != 0;
+  }();
+  if (generic) {
+    launch_phaseA<false>(f, a, false);
+  } else {
+    static_assert(kAXThreads == kBuckets, "one bucket per thread");
+    a.dbg_clock = nullptr;
+    auto go = [&](auto kernel) {
+      hipLaunchKernelGGL(kernel, dim3((unsigned)n_wg), dim3(kAXThreads), 0, f->stream, a);
+    };
+    switch (a.ks.cols[0].type) {  // one kernel per width (one kernel for all spilled heavily)
+      case DQ_INT8: go(freq_phaseA_xp<DQ_INT8>); break;
+      case DQ_INT16: go(freq_phaseA_xp<DQ_INT16>); break;
+      case DQ_INT32: go(freq_phaseA_xp<DQ_INT32>); break;
+      case DQ_FLOAT32: go(freq_phaseA_xp<DQ_FLOAT32>); break;
+      case DQ_FLOAT64: go(freq_phaseA_xp<DQ_FLOAT64>); break;
+      case DQ_BOOL: go(freq_phaseA_xp<DQ_BOOL>); break;
+      default: go(freq_phaseA_xp<DQ_INT64>); break;
+    }
+  }
   HIP_TRY(hipGetLastError());
   const unsigned long long base = (unsigned long long)f->n_chunks * f->tile;
   for (int64_t w = 0; w < n_wg; ++w) f->h_pbase.push_back(base);
