@@ -986,6 +986,16 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
 // chunk segments).  Same tile ranges and the same hash as freq_phaseA<false, false>; only
 // non-NULL rows are keyed.
 // ------------------------------------------------------------------------------------------------
+// row base + r of a fixed-width column, the base (wave-uniform) applied to the pointer
+template <int TY>
+DQ_DEV uint64_t kload_at(const void* v, int64_t base, int r) {
+  if constexpr (TY == DQ_BOOL) {
+    return kwiden(TY, v, base + r);
+  } else {
+    constexpr int W = TY == DQ_INT8 ? 1 : TY == DQ_INT16 ? 2 : (TY == DQ_INT32 || TY == DQ_FLOAT32) ? 4 : 8;
+    return kwiden(TY, reinterpret_cast<const char*>(v) + base * W, r);
+  }
+}
 constexpr int kPreThreads = 1024;
 __global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t* ph) {
   constexpr int ROUNDS = FM<false>::kTile / kPreThreads;
@@ -997,29 +1007,46 @@ __global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t*
   const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
   const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
   const int64_t t1 = min(t0 + (int64_t)a.tiles_per_wg, n_tiles);
+  const bool full_ok = (reinterpret_cast<uintptr_t>(c.valid) & 7u) == 0 && (a.tile_items & 63) == 0;
   auto tile_loop = [&](auto type_tag) {
     constexpr int TY = decltype(type_tag)::value;
     for (int64_t t = t0; t < t1; ++t) {
       const int64_t i0 = t * a.tile_items, i1 = min(i0 + a.tile_items, a.n_items);
-      int64_t ic[ROUNDS];
       uint32_t ok = 0, vb = ~0u;
-#pragma unroll
-      for (int j = 0; j < ROUNDS; ++j) {
-        const int64_t i = i0 + (int64_t)j * kPreThreads + tid;
-        ok |= (i < i1 ? 1u : 0u) << j;
-        ic[j] = i < i1 ? i : i1 - 1;
-      }
-      if (c.valid) {
-        uint32_t byte[ROUNDS];
-#pragma unroll
-        for (int j = 0; j < ROUNDS; ++j) byte[j] = c.valid[ic[j] >> 3];
-        vb = 0;
-#pragma unroll
-        for (int j = 0; j < ROUNDS; ++j) vb |= ((byte[j] >> (ic[j] & 7)) & 1u) << j;
-      }
       uint64_t v[ROUNDS];
+      if (i1 - i0 == FM<false>::kTile && full_ok) {  // as freq_phaseA_xp's full tiles
+        ok = (1u << ROUNDS) - 1u;
 #pragma unroll
-      for (int j = 0; j < ROUNDS; ++j) v[j] = kwiden(TY, c.values, ic[j]);
+        for (int j = 0; j < ROUNDS; ++j) v[j] = kload_at<TY>(c.values, i0 + (int64_t)j * kPreThreads, tid);
+        if (c.valid) {
+          const int64_t wrow = i0 + 64 * (int64_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+          vb = 0;
+#pragma unroll
+          for (int j = 0; j < ROUNDS; ++j) {
+            const uint64_t w =
+                *reinterpret_cast<const uint64_t*>(c.valid + ((wrow + (int64_t)j * kPreThreads) >> 3));
+            vb |= (uint32_t)((w >> __lane_id()) & 1u) << j;
+          }
+        }
+      } else {
+        int64_t ic[ROUNDS];
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) {
+          const int64_t i = i0 + (int64_t)j * kPreThreads + tid;
+          ok |= (i < i1 ? 1u : 0u) << j;
+          ic[j] = i < i1 ? i : i1 - 1;
+        }
+        if (c.valid) {
+          uint32_t byte[ROUNDS];
+#pragma unroll
+          for (int j = 0; j < ROUNDS; ++j) byte[j] = c.valid[ic[j] >> 3];
+          vb = 0;
+#pragma unroll
+          for (int j = 0; j < ROUNDS; ++j) vb |= ((byte[j] >> (ic[j] & 7)) & 1u) << j;
+        }
+#pragma unroll
+        for (int j = 0; j < ROUNDS; ++j) v[j] = kwiden(TY, c.values, ic[j]);
+      }
 #pragma unroll
       for (int j = 0; j < ROUNDS; ++j)
         if ((ok & vb) >> j & 1u) atomicAdd(&bh[bucket_of(fmix_bij(exact_canon(a.ks, v[j])))], 1u);
@@ -1048,16 +1075,7 @@ __global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t*
 // atomic per row instead of two.
 // ------------------------------------------------------------------------------------------------
 constexpr int kAXThreads = 512;
-// row base + r of a fixed-width column, the base (wave-uniform) applied to the pointer
-template <int TY>
-DQ_DEV uint64_t kload_at(const void* v, int64_t base, int r) {
-  if constexpr (TY == DQ_BOOL) {
-    return kwiden(TY, v, base + r);
-  } else {
-    constexpr int W = TY == DQ_INT8 ? 1 : TY == DQ_INT16 ? 2 : (TY == DQ_INT32 || TY == DQ_FLOAT32) ? 4 : 8;
-    return kwiden(TY, reinterpret_cast<const char*>(v) + base * W, r);
-  }
-}
+
 template <int TY>
 __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4 waves per SIMD: two workgroups per CU
   constexpr int T = FM<false>::kTile, R = T / kAXThreads, D = AKeys<false, false>::kDedupe;
