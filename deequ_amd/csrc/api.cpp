@@ -1334,9 +1334,13 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
       }
       launches.clear();
       bool has_hll = false;
-      for (const ScanLaunch& L : plain) has_hll = has_hll || L.body == BC_HLL;
+      uint32_t classes = 0;
+      for (const ScanLaunch& L : plain) {
+        has_hll = has_hll || L.body == BC_HLL;
+        classes |= 1u << L.body;
+      }
       launches.push_back(ScanLaunch{kBodyMixed, s->grid[kBodyMixed], 0, n_order,
-                                    s->d_order[slot].p, has_hll ? s->mix_hll : 0});
+                                    s->d_order[slot].p, has_hll ? s->mix_hll : 0, classes});
       for (const ScanLaunch& L : hll) launches.push_back(L);
     }
   }

@@ -154,7 +154,11 @@ struct ScanLaunch {
   uint32_t item_lo, item_hi;  // kBodyMixed: item_lo = 0, item_hi = entries of `order`
   const uint32_t* order;   // kBodyMixed: queue position -> global item index
   int32_t lds_hll = 0;     // kBodyMixed: HLL tasks whose registers the launch keeps in LDS
+  uint32_t classes = 0;    // kBodyMixed: the body classes of its items (bit per BodyClass)
 };
+// Mixed-kernel instantiations: every class, and BASELINE configs[1]'s three
+constexpr uint32_t kMixedAll = (1u << kBodyClasses) - 1u;
+constexpr uint32_t kMixedS10 = (1u << BC_BITS) | (1u << BC_NUM_I64) | (1u << BC_STR_IN);
 
 // Most HLL tasks whose LDS registers (2 KiB each) ride in the mixed launch.  0 = HLL always keeps
 // its own launch: measured on MI355X at configs[3] (1.25e9 rows), HLL inside the mixed grid took

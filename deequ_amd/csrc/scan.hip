@@ -20,6 +20,8 @@
 // dword load per lane and redistributed with ds_bpermute (no LDS traffic, no barrier).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "device_util.h"
 #include "kernels.h"
 #include "stream_load.h"
@@ -1012,6 +1014,10 @@ static_assert(kMixedHllMax == 0, "scan_mixed_kernel has no HLL body");
 // bound) instead of one class at a time.  The body is chosen per item (a wave-uniform branch on
 // the descriptor).  Inlined side by side the bodies would need ~173 VGPRs (2 waves/SIMD); the
 // kernel is pinned to 3 waves/SIMD (168 VGPRs) like the string body alone.
+// MASK: the body classes compiled in (bit per BodyClass).  kMixedS10 (validity bits, Long
+// columns, string IN: BASELINE configs[1]) leaves out the bodies that spilled 28 bytes per lane
+// into the all-class kernel.
+template <uint32_t MASK>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3, 3)))
 scan_mixed_kernel(const TaskDesc* __restrict__ tasks, int n_desc, uint32_t n_order,
                   const uint32_t* __restrict__ order, uint32_t* __restrict__ queue,
@@ -1039,19 +1045,24 @@ scan_mixed_kernel(const TaskDesc* __restrict__ tasks, int n_desc, uint32_t n_ord
     const int64_t r_end = min(r_begin + t.item_rows, t.rows);
     Acc a;
     acc_init(t.kind, a);
+#define DQ_BODY(BCV, CALL) \
+  case BCV:                \
+    if constexpr ((MASK >> BCV) & 1u) CALL; \
+    break;
     switch (t.body) {
-      case BC_NUM_I8: num_item<int8_t>(t, r_begin, r_end, a); break;
-      case BC_NUM_I16: num_item<int16_t>(t, r_begin, r_end, a); break;
-      case BC_NUM_I32: num_item<int32_t>(t, r_begin, r_end, a); break;
-      case BC_NUM_I64: num_item<int64_t>(t, r_begin, r_end, a); break;
-      case BC_NUM_F32: num_item<float>(t, r_begin, r_end, a); break;
-      case BC_NUM_F64: num_item<double>(t, r_begin, r_end, a); break;
-      case BC_BITS: bits_item(t, r_begin, r_end, a); break;
-      case BC_STR_IN: str_in_item(t, r_begin, r_end, a); break;
-      case BC_DTYPE: dtype_item(t, r_begin, r_end, a); break;
-      case BC_CORR: corr_item(t, r_begin, r_end, a); break;
+      DQ_BODY(BC_NUM_I8, (num_item<int8_t>(t, r_begin, r_end, a)))
+      DQ_BODY(BC_NUM_I16, (num_item<int16_t>(t, r_begin, r_end, a)))
+      DQ_BODY(BC_NUM_I32, (num_item<int32_t>(t, r_begin, r_end, a)))
+      DQ_BODY(BC_NUM_I64, (num_item<int64_t>(t, r_begin, r_end, a)))
+      DQ_BODY(BC_NUM_F32, (num_item<float>(t, r_begin, r_end, a)))
+      DQ_BODY(BC_NUM_F64, (num_item<double>(t, r_begin, r_end, a)))
+      DQ_BODY(BC_BITS, (bits_item(t, r_begin, r_end, a)))
+      DQ_BODY(BC_STR_IN, (str_in_item(t, r_begin, r_end, a)))
+      DQ_BODY(BC_DTYPE, (dtype_item(t, r_begin, r_end, a)))
+      DQ_BODY(BC_CORR, (corr_item(t, r_begin, r_end, a)))
       default: break;
     }
+#undef DQ_BODY
     wave_reduce(t.kind, a);
     if (l == 0) partial[item] = a;
   }
@@ -1193,10 +1204,15 @@ hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const Sca
     if (L.item_hi <= L.item_lo) continue;
     if (L.body == kBodyMixed) {
       const int mix_hll = L.lds_hll;
-      hipLaunchKernelGGL(scan_mixed_kernel, dim3(L.grid), dim3(kBlock),
-                         (size_t)mix_hll * kHllM * 4, stream, tasks, n_desc, L.item_hi, L.order,
-                         queues + kBodyMixed * kQueueHeads * kQueueStride, partial, hll_stage,
-                         mix_hll);
+      auto go = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(L.grid), dim3(kBlock), (size_t)mix_hll * kHllM * 4, stream,
+                           tasks, n_desc, L.item_hi, L.order,
+                           queues + kBodyMixed * kQueueHeads * kQueueStride, partial, hll_stage,
+                           mix_hll);
+      };
+      static const bool all = getenv("DQ_MIXED_ALL") != nullptr;  // A/B hook
+      if ((L.classes & ~kMixedS10) == 0 && !all) go(scan_mixed_kernel<kMixedS10>);
+      else go(scan_mixed_kernel<kMixedAll>);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       continue;
@@ -1244,7 +1260,7 @@ int scan_max_blocks_per_cu(int body, int n_hll) {
     case BC_CORR_HLL: return occupancy_of<BC_CORR_HLL>(n_hll);
     case kBodyMixed: {
       int n = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_mixed_kernel, kBlock,
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_mixed_kernel<kMixedAll>, kBlock,
                                                        (size_t)n_hll * kHllM * 4) != hipSuccess)
         n = 2;
       return n > 0 ? n : 1;

@@ -1,18 +1,26 @@
 #!/bin/bash
-# Round-4 session: the whole -m gpu suite, then the multi-GPU harness rehearsed as 2 ranks on one
-# GPU (gloo), and the configs[2] / configs[3] lines with their CPU baselines.  TAG names outputs.
+# Round-4 sessions; TAG names outputs, PART selects the half.
+#  PART=1: the whole -m gpu suite, S10 bench (A/B of the mixed-kernel mask), configs[2]/[3] lines
+#          with their CPU baselines, and configs[2] with the generic phase-A kernel (A/B).
+#  PART=2: the multi-GPU harness rehearsed as 2 ranks on one GPU, rocprof kernel stats of
+#          configs[2] and configs[4], and the configs[4] line with its CPU baseline.
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 O=gpurun_out
 T=${TAG:-s}
 mkdir -p $O
+if [ "${PART:-1}" = 1 ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests_$T.log 2>&1 &&
-timeout -k 10 300 python -u tools/bench_workloads.py c3 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c3_$T.json 2>&1 &&
-timeout -k 10 300 python -u tools/bench_workloads.py c4 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c4_$T.json 2>&1 &&
+timeout -k 10 120 python -u bench.py > $O/bench_$T.json 2>&1 &&
+DQ_MIXED_ALL=1 timeout -k 10 120 python -u bench.py > $O/bench_all_$T.json 2>&1 &&
 timeout -k 10 400 python -u tools/bench_workloads.py c3 --steps 3 --cpu-baseline > $O/wl_c3_$T.json 2>&1 &&
 DQ_FREQ_GENERIC_A=1 timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 3 > $O/wl_c3_genA_$T.json 2>&1 &&
-timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 5 --cpu-baseline > $O/wl_c4_$T.json 2>&1 &&
+timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 5 --cpu-baseline > $O/wl_c4_$T.json 2>&1
+else
+timeout -k 10 300 python -u tools/bench_workloads.py c3 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c3_$T.json 2>&1 &&
+timeout -k 10 300 python -u tools/bench_workloads.py c4 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c4_$T.json 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_$T -o run -- python3 tools/bench_workloads.py c3 --steps 2 > $O/prof_c3_$T.log 2>&1 &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1 &&
 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 --cpu-baseline --cpu-rows 8388608 > $O/wl_c5_$T.json 2>&1
+fi
