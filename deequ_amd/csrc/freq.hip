@@ -2109,6 +2109,101 @@ __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter_u(BArgs a) {
   }
 }
 
+// B3, whole units, persistent: workgroup g of an XCD takes that XCD's units g, g + G/8, ... and
+// issues the loads of its next unit right after placing the current one in LDS, so they are in
+// flight while the current unit's runs are written (freq_phaseB_scatter_u, one workgroup per CU by
+// LDS and one unit per workgroup, left every load latency exposed).  Same output.
+template <bool HASHED, int PER>
+__global__ void __launch_bounds__(kThreads) freq_phaseB_scatter_p(BArgs a) {
+  constexpr int W = FM<HASHED>::kRB / 8;
+  constexpr int SMAX = 1 << kMaxSubBits;
+  constexpr uint32_t NR = (uint32_t)PER * kThreads;
+  __shared__ UnitLds L;
+  __shared__ unsigned long long gbs[SMAX];
+  __shared__ uint32_t hcnt[SMAX];
+  __shared__ uint64_t staged[NR * W];
+  const uint32_t g = blockIdx.x, per_xcd = gridDim.x / 8u, q = (a.n_units + 7) / 8;
+  const uint32_t x = g & 7u, gl = g >> 3;
+  const uint32_t uend = min((x + 1) * q, a.n_units);
+  uint32_t w = x * q + gl;
+  if (w >= uend) return;  // (workgroup-uniform)
+  const int S = 1 << a.s;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < S; i += kThreads) hcnt[i] = 0;
+  uint64_t rv[PER][W];
+  // the unit's records into rv (the loads are left in flight); returns its record count
+  auto load_unit = [&](uint32_t u) -> uint32_t {
+    unit_range(a, u, L);
+    const uint32_t nrec = L.s_hi - L.s_lo;  // <= NR (the host sizes units so)
+    uint32_t done = 0;
+    for (int64_t cw = L.s_c0; cw < L.s_c1; cw += kThreads) {  // windows of segments (usually one)
+      uint32_t nwin;
+      const uint32_t wtot = unit_window(a, L, cw, nwin);
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const uint32_t r = (uint32_t)j * kThreads + tid;
+        if (r >= done && r < done + wtot) {
+          const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recs) + window_rec(L, nwin, r - done) * W;
+#pragma unroll
+          for (int y = 0; y < W; ++y) rv[j][y] = src[y];
+        }
+      }
+      done += wtot;
+      __syncthreads();
+    }
+    return nrec;
+  };
+  uint32_t nrec = load_unit(w), b = L.s_b;
+  uint64_t* out = reinterpret_cast<uint64_t*>(a.recsB);
+  while (true) {
+    uint32_t lpos[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if ((uint32_t)j * kThreads + tid < nrec) lpos[j] = atomicAdd(&hcnt[rec_sub(rv[j], a.s, HASHED)], 1u);
+    __syncthreads();
+    const uint32_t cnt = tid < S ? hcnt[tid] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(cnt, L.s_wave, tot);  // (barriers: every count is read)
+    if (tid < S) {
+      hcnt[tid] = ex;
+      gbs[tid] = a.part_base[(uint64_t)b * S + tid] + a.uhist[(int64_t)w * S + tid];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if ((uint32_t)j * kThreads + tid >= nrec) continue;
+      const uint32_t slot = hcnt[rec_sub(rv[j], a.s, HASHED)] + lpos[j];
+#pragma unroll
+      for (int y = 0; y < W; ++y) staged[slot * W + y] = rv[j][y];
+    }
+    __syncthreads();
+    // the next unit's loads go out before this unit's stores
+    const uint32_t wn = w + per_xcd;
+    const bool more = wn < uend;
+    uint32_t nrec_n = 0, b_n = 0;
+    if (more) {
+      nrec_n = load_unit(wn);
+      b_n = L.s_b;
+    }
+    for (uint32_t i = tid; i < nrec; i += kThreads) {
+      uint64_t r[W];
+#pragma unroll
+      for (int y = 0; y < W; ++y) r[y] = staged[i * W + y];
+      const uint32_t sb = rec_sub(r, a.s, HASHED);
+      const unsigned long long d = gbs[sb] + (i - hcnt[sb]);
+#pragma unroll
+      for (int y = 0; y < W; ++y) out[d * W + y] = r[y];
+    }
+    if (!more) break;
+    __syncthreads();
+    for (int i = tid; i < S; i += kThreads) hcnt[i] = 0;
+    __syncthreads();
+    w = wn;
+    nrec = nrec_n;
+    b = b_n;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Phase C: count partitions in LDS
 //
@@ -3761,7 +3856,18 @@ static dq_status finalize_b(dq_freq* f) {
     return e ? atoi(e) : 0;
   }();
   constexpr uint64_t kUnitX = 16 * kThreads, kUnitH = 4 * kThreads;  // whole-unit capacities
-  if (bsub == 0 && f->exact && H <= kUnitX) {
+  static const bool b3u = [] {  // DQ_FREQ_B3U=1: A/B hook, one unit per workgroup
+    const char* e = getenv("DQ_FREQ_B3U");
+    return e && atoi(e) != 0;
+  }();
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, f->device);
+  const unsigned pgrid = (unsigned)std::max(8, cus / 8 * 8);  // one per CU (LDS), XCD multiple
+  if (bsub == 0 && f->exact && H <= kUnitX && !b3u) {
+    hipLaunchKernelGGL((freq_phaseB_scatter_p<false, 16>), dim3(pgrid), dim3(kThreads), 0, f->stream, a);
+  } else if (bsub == 0 && !f->exact && H <= kUnitH && !b3u) {
+    hipLaunchKernelGGL((freq_phaseB_scatter_p<true, 4>), dim3(pgrid), dim3(kThreads), 0, f->stream, a);
+  } else if (bsub == 0 && f->exact && H <= kUnitX) {
     hipLaunchKernelGGL((freq_phaseB_scatter_u<false, 16>), dim3(grid), dim3(kThreads), 0, f->stream, a);
   } else if (bsub == 0 && !f->exact && H <= kUnitH) {
     hipLaunchKernelGGL((freq_phaseB_scatter_u<true, 4>), dim3(grid), dim3(kThreads), 0, f->stream, a);

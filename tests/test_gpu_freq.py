@@ -519,3 +519,35 @@ def test_small_key_batch_table_overflow(gpu_device):
     dist = ctx.metric(Histogram("s")).value.get()
     assert dist.number_of_bins == len(hist)
     assert {k: v.absolute for k, v in dist.values.items()} == hist
+
+
+@pytest.mark.parametrize("nulls", [0.0, 0.05])
+def test_exact_bucket_pieces_at_scale(nulls, gpu_device):
+    """12M int64 rows in 4M-row batches: bucket pieces from several batches and workgroups
+    (freq_prepass_x + freq_phaseA_xp), several phase-B units per bucket and per persistent B3
+    workgroup, full-depth partitions (s = 10) in packed phase C -- against numpy's exact counts
+    and the C restatement's entropy."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    n = 12_000_000
+    rng = np.random.default_rng(11)
+    ids = rng.integers(0, 9_000_000, n, dtype=np.int64)      # ~26 % of keys repeated
+    ids[:2000] = 42                                           # one heavy key (collapses in A)
+    mask = rng.random(n) < nulls
+    t = pa.table({"id": pa.array(ids, mask=mask)})
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=4_000_000)
+    ft = FrequencyTable(["id"], [df.schema["id"].dtype], 0)
+    for b in df.batches:
+        ft.add([b["id"]])
+    s = ft.summarize()
+    vals, counts = np.unique(ids[~mask], return_counts=True)
+    assert s.num_rows == n
+    assert s.n_groups == len(vals)
+    assert s.n_unique == int((counts == 1).sum())
+    p = counts / n
+    ent = -math.fsum((p * np.log(p)).tolist())
+    assert abs(s.entropy - ent) <= 1e-12 * abs(ent)
+    top = ft.topk(3)
+    order = np.argsort(-counts, kind="stable")[:3]
+    assert [c for _, c in top] == counts[order].tolist()
+    assert top[0][0][0] == 42
