@@ -914,6 +914,36 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         reinterpret_cast<ulonglong2*>(out)[i] = v;
       }
       if ((ctotal & 1u) && tid == 0) out[ctotal - 1] = stash[ctotal - 1];
+    } else if constexpr (HASHED && !FROM_REC) {
+      // row keys into the arena: each wave reserves its round's bytes with one LDS atomic (a
+      // per-row atomic on the one cursor word serialised every row of the tile)
+#pragma unroll 1
+      for (int j = 0; j < ROUNDS; ++j) {  // (wave-uniform trip count)
+        const bool on = (raw >> j) & 1u;
+        const int q = j * kThreads + tid;
+        const int64_t row = on ? (int64_t)stash[q * W + 1] : 0;
+        const uint64_t k0 = SK && on ? ssk0[q] : 0, k1 = SK && on ? ssk1[q] : kNoShort;
+        const uint32_t sz = on ? enc_size_sk(row, k1) : 0u;
+        const uint32_t incl = __ockl_wfscan_add_u32(sz, true);
+        const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        unsigned long long wbase = 0;
+        if (__lane_id() == 63 && wtot) wbase = atomicAdd(&s_arena_cur, (unsigned long long)wtot);
+        wbase = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(wbase >> 32), 63) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wbase, 63);
+        if (!on) continue;
+        const uint64_t off = s_arena_base + wbase + (incl - sz);
+        if constexpr (STR1) {
+          if (k1 != kNoShort) {
+            str1_encode_short(k0, k1, reinterpret_cast<uint32_t*>(a.arena + off));
+          } else {
+            const SView v = str1_view(a.ks, row);
+            str1_encode_copy(v.p, v.len, reinterpret_cast<uint32_t*>(a.arena + off));
+          }
+        } else {
+          row_encode_dw(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
+        }
+        put(t, stash[q * W], 1u, off);  // (row keys: one record, the count-1 digit code)
+      }
     } else {
 #pragma unroll 1
       for (int j = 0; j < ROUNDS; ++j) {
@@ -921,8 +951,6 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         const int q = j * kThreads + tid;
         const uint64_t h = stash[q * W];
         uint64_t rep = HASHED ? stash[q * W + 1] : 0;
-        if constexpr (HASHED && !FROM_REC)
-          rep = arena_rep_sk((int64_t)rep, SK ? ssk0[q] : 0, SK ? ssk1[q] : kNoShort);
         for_digits(FROM_REC ? scnt[tid] : 1, [&](uint32_t code) { put(t, h, code, rep); });
       }
     }
