@@ -3400,6 +3400,7 @@ struct dq_freq {
   DevBuf<uint32_t> pstart, plen;
   std::vector<unsigned long long> h_pbase;
   int64_t n_prow = 0;
+  int64_t n_empty_chunks = 0;  // chunk rows known empty (bucket-piece batches): finalize skips them
   DevBuf<uint32_t> ph, ptot;  // the pre-pass's per-workgroup bucket counts (scratch)
   DevBuf<unsigned long long> pbase;
   DevBuf<uint8_t> arena;                 // hashed: encoded keys
@@ -3716,7 +3717,7 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
   const unsigned long long base = (unsigned long long)f->n_chunks * f->tile;
   for (int64_t w = 0; w < n_wg; ++w) f->h_pbase.push_back(base);
   f->n_prow += n_wg;
-  (void)chunks;
+  f->n_empty_chunks += chunks;
   return DQ_OK;
 }
 
@@ -3729,7 +3730,9 @@ static dq_status finalize_b(dq_freq* f) {
   // the non-empty chunks (only when that saves a good part of the finalize)
   int64_t n = n_all;
   const uint32_t* cmap = nullptr;
-  if (n_all >= 4 * kThreads) {
+  if (f->n_empty_chunks == n_all) {  // every chunk row empty (bucket pieces): no read-back
+    n = 0;
+  } else if (n_all >= 4 * kThreads) {
     const int64_t nb = (n_all + kThreads - 1) / kThreads;
     HIP_TRY(f->chunk_id.ensure(n_all));
     HIP_TRY(f->chunk_boff.ensure(nb + 1));
@@ -4461,6 +4464,7 @@ extern "C" dq_status dq_freq_reset(dq_freq* f, void* hip_stream) {
   f->num_rows = 0;
   f->n_chunks = 0;
   f->n_prow = 0;
+  f->n_empty_chunks = 0;
   f->h_pbase.clear();
   f->fast_off = false;  // (a reset table may see keys the small-key path takes again)
   f->mode_null_as_group = -1;
@@ -4967,6 +4971,7 @@ extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src_c) {
       const unsigned long long shift = (unsigned long long)dst->n_chunks * dst->tile;
       for (unsigned long long b : src->h_pbase) dst->h_pbase.push_back(b + shift);
       dst->n_prow += src->n_prow;
+      dst->n_empty_chunks += src->n_empty_chunks;
     }
     dst->n_chunks += nc;
   }
