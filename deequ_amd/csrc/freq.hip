@@ -3723,9 +3723,7 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
 
 // ---- finalize: phase B ------------------------------------------------------------------------
 static dq_status finalize_b(dq_freq* f) {
-  dq_status cs = sync_counters(f);
-  if (cs != DQ_OK) return cs;
-  if (f->b_valid) return DQ_OK;
+  if (f->b_valid) return sync_counters(f);
   const int64_t n_all = f->n_chunks;
   // the non-empty chunks (only when that saves a good part of the finalize)
   int64_t n = n_all;
@@ -3761,7 +3759,7 @@ static dq_status finalize_b(dq_freq* f) {
   if (J == 0) {
     HIP_TRY(hipMemsetAsync(f->part_base.p, 0, (kBuckets + 1) * 8, f->stream));
     f->b_valid = true;
-    return DQ_OK;
+    return sync_counters(f);
   }
   HIP_TRY(f->segS.ensure((size_t)kBuckets * J));
   HIP_TRY(f->segP.ensure((size_t)kBuckets * (J + 1)));
@@ -3786,7 +3784,12 @@ static dq_status finalize_b(dq_freq* f) {
                      J, f->nseg.p, f->totals.p);
   HIP_TRY(hipGetLastError());
   std::vector<unsigned long long> tot(kBuckets);
-  HIP_TRY(hipStreamSynchronize(f->stream));
+  if (f->counters_stale) {  // one stream wait for the counters and the bucket totals
+    dq_status cs = pull_counters(f);
+    if (cs != DQ_OK) return cs;
+  } else {
+    HIP_TRY(hipStreamSynchronize(f->stream));
+  }
   HIP_TRY(hipMemcpy(tot.data(), f->totals.p, kBuckets * 8, hipMemcpyDeviceToHost));
   uint64_t R = 0;
   for (auto t : tot) R += t;
@@ -3918,8 +3921,21 @@ static dq_status finalize_b(dq_freq* f) {
   return DQ_OK;
 }
 
+// The partitions' statistics summed in a fixed order into f->red.
+static dq_status launch_reduce(dq_freq* f, int64_t P) {
+  HIP_TRY(f->scan_tmp.ensure(kRedBlocks * 3));
+  const unsigned nbr = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kRedBlocks, (P + kThreads - 1) / kThreads));
+  hipLaunchKernelGGL(freq_reduce_part, dim3(nbr), dim3(kThreads), 0, f->stream, f->part_groups.p,
+                     f->part_unique.p, f->part_entropy.p, P, f->scan_tmp.p);
+  hipLaunchKernelGGL(freq_reduce_final, dim3(1), dim3(64), 0, f->stream, f->scan_tmp.p, (int)nbr,
+                     f->red.p);
+  HIP_TRY(hipGetLastError());
+  return DQ_OK;
+}
+
 // ---- finalize: phase C ------------------------------------------------------------------------
 static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
+  bool reduced = false;  // f->red already holds this pass's sums
   dq_status st = finalize_b(f);
   if (st != DQ_OK) return st;
   const double nr = (double)f->num_rows;
@@ -4011,9 +4027,15 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       else
         hipLaunchKernelGGL(freq_phaseC<true>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
       HIP_TRY(hipGetLastError());
+      if (round == 0) {  // the reduction, queued before the wait: read with ovf_n if none overflow
+        dq_status rs = launch_reduce(f, P);
+        if (rs != DQ_OK) return rs;
+        reduced = true;
+      }
       unsigned int m = 0;
       HIP_TRY(hipStreamSynchronize(f->stream));
       HIP_TRY(hipMemcpy(&m, f->ovf_n.p, 4, hipMemcpyDeviceToHost));
+      if (m) reduced = false;
       if (clk && f->exact && !old_c) {  // freq_phaseC_x: 8 stamps per item
         unsigned long long h[16 * 8];
         (void)hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost);
@@ -4073,15 +4095,10 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     }
     if (clk) (void)hipFree(clk);
   }
-  HIP_TRY(f->scan_tmp.ensure(kRedBlocks * 3));
-  {
-    const unsigned nbr = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kRedBlocks, (P + kThreads - 1) / kThreads));
-    hipLaunchKernelGGL(freq_reduce_part, dim3(nbr), dim3(kThreads), 0, f->stream, f->part_groups.p,
-                       f->part_unique.p, f->part_entropy.p, P, f->scan_tmp.p);
-    hipLaunchKernelGGL(freq_reduce_final, dim3(1), dim3(64), 0, f->stream, f->scan_tmp.p, (int)nbr,
-                       f->red.p);
+  if (!reduced) {
+    dq_status rs = launch_reduce(f, P);
+    if (rs != DQ_OK) return rs;
   }
-  HIP_TRY(hipGetLastError());
   unsigned long long r[4];
   HIP_TRY(hipStreamSynchronize(f->stream));
   HIP_TRY(hipMemcpy(r, f->red.p, sizeof(r), hipMemcpyDeviceToHost));
