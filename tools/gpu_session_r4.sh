@@ -17,7 +17,8 @@ DQ_MIXED_ALL=1 timeout -k 10 120 python -u bench.py > $O/bench_all_$T.json 2>&1 
 timeout -k 10 400 python -u tools/bench_workloads.py c3 --steps 3 --cpu-baseline > $O/wl_c3_$T.json 2>&1 &&
 DQ_FREQ_GENERIC_A=1 timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 3 > $O/wl_c3_genA_$T.json 2>&1 &&
 timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 5 --cpu-baseline > $O/wl_c4_$T.json 2>&1 &&
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1 &&
+DQ_FREQ_DEBUG=2 timeout -k 10 300 python -u tools/bench_workloads.py c5 --steps 1 --warmup 0 > $O/dbg_c5_$T.log 2>&1
 else
 timeout -k 10 300 python -u tools/bench_workloads.py c3 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c3_$T.json 2>&1 &&
 timeout -k 10 300 python -u tools/bench_workloads.py c4 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c4_$T.json 2>&1 &&
