@@ -3143,6 +3143,374 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
   if (wave == 0) tail(par ^ 1u);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Phase C, hashed mode, first pass (freq_phaseC_x's design for 16-byte records): two-word slots,
+// the key's 64-bit row hash and rep << 24 | count, so a claim is one CAS and one store and a
+// duplicate one atomic add; the inserts of all a thread's records are in flight together (double
+// hashing); claimed slots go to an LDS list, so the statistics visit the partition's groups only;
+// the item's outputs are written by wave 0 during the next item.  A record that meets its key's
+// slot claimed but not yet published (value 0) re-probes the same slot next round -- the claimer
+// stores right after its CAS, so no barrier and no spin.  Equal hashes are decided on the arena
+// bytes (enc_equal_arena): a 64-bit collision stays two groups.  A partition this kernel cannot
+// take exactly (a record count >= 2^12, more than kCL records, the key kEmptyKey, a full table)
+// is handed on whole (an ovf entry, f = 0) to freq_phaseC<true>.
+// ------------------------------------------------------------------------------------------------
+// enc_equal_arena with a rolled loop of 4-word rounds (few registers: it sits inside every probe
+// round of freq_phaseC_h); 4 words past a key's end stay inside the arena's 64-byte tail.
+DQ_DEV bool enc_equal_lean(const uint8_t* arena, uint64_t x, uint64_t y, const int32_t* types,
+                           int n_keys) {
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(arena + x);
+  const uint32_t* b = reinterpret_cast<const uint32_t*>(arena + y);
+  const uint32_t n = n_keys == 1 && types[0] == DQ_UTF8 ? (a[0] ? 2 + pad4(a[1]) / 4 : 1u)
+                                                        : enc_size(a, types, n_keys) / 4;
+#pragma unroll 1
+  for (uint32_t q = 0; q < n; q += 4) {
+    uint32_t d = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) d |= q + k < n ? a[q + k] ^ b[q + k] : 0u;
+    if (d) return false;
+  }
+  return true;
+}
+constexpr int kCHT = 4096;   // slots
+constexpr int kCL = 4096;    // list capacity = most records per partition
+template <bool DBG>
+__global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
+  constexpr int KT = kCHT, KL = kCL, NW = kCThreads / 64, PF = kPF<true>;
+  constexpr uint64_t M24 = (1ULL << 24) - 1;
+  __shared__ uint64_t tkey[KT], tval[KT];
+  __shared__ uint16_t list[KL];
+  __shared__ uint32_t s_n[2], s_ovf[2];
+  __shared__ uint32_t s_chist[2][kSmallCounts];
+  __shared__ unsigned long long s_wun[2][NW], s_wmax[2][NW];
+  __shared__ double s_went[2][NW];
+  __shared__ double s_term[kSmallCounts];
+  __shared__ uint64_t s_fk[2][kCand], s_fc[2][kCand], s_fr[2][kCand];
+  __shared__ unsigned long long s_top[kCand];
+  __shared__ uint32_t s_tp[2], s_tg[2], s_tfl[2];
+  __shared__ uint64_t s_tr0[2];
+  enum { TF_VALID = 1, TF_CANDFAST = 4 };
+
+  const int tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
+  unsigned long long collisions = 0;
+  for (int i = tid; i < KT; i += kCThreads) {
+    tkey[i] = kEmptyKey;
+    tval[i] = 0;
+  }
+  if (tid < 2) {
+    s_n[tid] = 0;
+    s_ovf[tid] = 0;
+    s_tfl[tid] = 0;
+  }
+  if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
+  if (tid < kSmallCounts) s_term[tid] = tid ? entropy_term((uint64_t)tid, a.num_rows) : 0.0;
+  if (tid < kCand) s_top[tid] = 0;
+  const bool keep = a.groups != nullptr;
+
+  auto tail = [&](uint32_t q) {  // wave 0: the outputs of the item of parity q
+    const uint32_t fl = s_tfl[q];
+    if (!(fl & TF_VALID)) return;
+    const uint32_t p = s_tp[q], gtot = s_tg[q];
+    if ((fl & TF_CANDFAST) && lane < kCand)
+      a.cand[(uint64_t)p * kCand + lane] = (uint32_t)lane < gtot
+                                               ? Group{s_fk[q][lane], s_fc[q][lane], s_fr[q][lane]}
+                                               : Group{0, 0, 0};
+    const uint32_t hc = lane > 1 ? s_chist[q][lane] : 0u;
+    double t = hc ? (double)hc * s_term[lane] : 0.0;
+    t = __ockl_wfred_add_f64(t);
+    if (lane == 0) {
+      uint64_t utot = 0;
+      double etot = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        utot += s_wun[q][w];
+        etot += s_went[q][w];
+      }
+      etot += t;
+      if (utot) etot += (double)utot * s_term[1];
+      a.part_groups[p] = gtot;
+      a.part_unique[p] = utot;
+      a.part_entropy[p] = etot;
+      if (keep) a.part_off[p] = s_tr0[q];
+    }
+  };
+
+  CBounds nb;
+  CItem<true> cur;
+  c_bounds(a, blockIdx.x, nb);
+  c_fetch<true>(a, blockIdx.x, nb, cur);
+  c_bounds(a, blockIdx.x + gridDim.x, nb);
+  __syncthreads();
+
+  uint32_t par = 0;
+  int item = 0;
+  auto mark = [&](int kk) {
+    if constexpr (DBG)
+      if (blockIdx.x == 0 && tid == 0 && item < 16) a.dbg_clock[item * 8 + kk] = wall_clock64();
+  };
+  for (int wi = blockIdx.x; wi < a.n_work; wi += gridDim.x, par ^= 1u, ++item) {
+    mark(0);
+    const uint32_t p = cur.p;
+    const uint64_t r0 = cur.r0, nrec = cur.r1 - cur.r0;
+    CItem<true> pf;
+    CBounds nb2;
+
+    auto insert_round = [&](const uint64_t (*w)[2], uint32_t valid, auto&& issue) {
+      uint64_t h[PF], v[PF], old[PF];
+      uint32_t slot[PF], step[PF], todo = 0;
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        h[q] = w[q][0];
+        const uint64_t c = code_count((uint32_t)(w[q][1] & 0xff));
+        v[q] = ((w[q][1] >> 8) << 24) | c;  // rep << 24 | count
+        slot[q] = (uint32_t)h[q] & (KT - 1);
+        step[q] = ((uint32_t)(h[q] >> 40) | 1u) & (KT - 1);
+        const bool in = (valid >> q) & 1u;
+        if (in && (c >= (1u << 12) || h[q] == kEmptyKey)) s_ovf[par] = 1;  // hand it on
+        if (in) todo |= 1u << q;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mark(4);
+      issue();
+      mark(5);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t mine = 0;
+      for (int pr = 0; todo && pr < 4 * KT; ++pr) {
+#pragma unroll
+        for (int q = 0; q < PF; ++q)
+          old[q] = (todo >> q) & 1u ? atomicCAS((unsigned long long*)&tkey[slot[q]], kEmptyKey, h[q]) : 0ULL;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          if (!((todo >> q) & 1u)) continue;
+          if (old[q] == kEmptyKey) {  // claimed: publish rep and count (non-zero)
+            __hip_atomic_store(&tval[slot[q]], v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            mine |= 1u << q;
+            todo &= ~(1u << q);
+          } else if (old[q] == h[q]) {
+            const uint64_t sv = __hip_atomic_load(&tval[slot[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (!sv) continue;  // claimed, not yet published: the same slot next round
+            const uint64_t rs = sv >> 24, rm = v[q] >> 24;
+            const bool same = rs == rm || enc_equal_lean(a.arena, rs, rm, a.types, a.n_keys);
+            if (same) {
+              atomicAdd((unsigned long long*)&tval[slot[q]], (unsigned long long)(v[q] & M24));
+              todo &= ~(1u << q);
+            } else {
+              ++collisions;  // two keys on one 64-bit hash: two groups
+              slot[q] = (slot[q] + step[q]) & (KT - 1);
+            }
+          } else {
+            slot[q] = (slot[q] + step[q]) & (KT - 1);
+          }
+        }
+      }
+      if (todo) s_ovf[par] = 1;  // the table is full
+      const uint32_t nm = (uint32_t)__builtin_popcount(mine);
+      const uint32_t incl = __ockl_wfscan_add_u32(nm, true);
+      const uint32_t wtot = __builtin_amdgcn_readlane(incl, 63);
+      if (wtot) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&s_n[par], wtot);
+        uint32_t pos = __builtin_amdgcn_readlane(base, 0) + incl - nm;
+#pragma unroll
+        for (int q = 0; q < PF; ++q)
+          if ((mine >> q) & 1u) list[pos++] = (uint16_t)slot[q];
+      }
+      mark(6);
+    };
+    const bool too_long = nrec > (uint64_t)KL;
+    insert_round(cur.w, too_long ? 0u : cur.valid, [&]() {
+      c_fetch<true>(a, wi + gridDim.x, nb, pf);
+      c_bounds(a, wi + 2 * gridDim.x, nb2);
+      if (wave == 0) tail(par ^ 1u);
+    });
+    if (nrec > (uint64_t)PF * kCThreads && !too_long) {  // the rest of a long partition
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + r0 * 2;
+      for (uint64_t base = (uint64_t)PF * kCThreads; base < nrec; base += (uint64_t)PF * kCThreads) {
+        uint64_t w[PF][2];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          const uint64_t li = base + (uint64_t)q * kCThreads + tid;
+          w[q][0] = li < nrec ? src[li * 2] : 0ULL;
+          w[q][1] = li < nrec ? src[li * 2 + 1] : 0ULL;
+          valid |= (li < nrec ? 1u : 0u) << q;
+        }
+        insert_round(w, valid, []() {});
+      }
+    }
+    __syncthreads();  //                                                            [barrier 1]
+    mark(1);
+    const uint32_t n = s_n[par];
+    const bool overflow = s_ovf[par] != 0 || n > (uint32_t)(KT * 7 / 8) || too_long;
+    const bool cand = a.want_cand && !overflow;
+    if (tid == 0) {
+      s_n[par ^ 1u] = 0;
+      s_ovf[par ^ 1u] = 0;
+      s_tfl[par ^ 1u] = 0;
+    }
+    if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
+    if (tid < kCand) s_top[tid] = 0;
+    const uint32_t gtot = n;
+    const uint64_t obase = r0;
+
+    uint64_t un = 0, mx = 0;
+    double e = 0.0;
+    uint64_t tc[kCand], tk[kCand], tr[kCand];
+#pragma unroll
+    for (int q = 0; q < kCand; ++q) tc[q] = tk[q] = tr[q] = 0;
+    uint64_t k1 = 0, r1 = 0;
+    bool k1c = false;
+    auto stat = [&](uint32_t i, uint64_t k, uint64_t c, uint64_t r) {
+      if (a.lit_count && k == a.lit_h && enc_is_null_literal(a.arena + r))
+        atomicAdd(a.lit_count, (unsigned long long)c);
+      if (keep) a.groups[obase + i] = Group{k, c, r};
+      if (c == 1) ++un;
+      else if (c < kSmallCounts) atomicAdd(&s_chist[par][c], 1u);
+      else e += entropy_term(c, a.num_rows);
+      mx = c > mx ? c : mx;
+      if (cand) {
+        if (i < (uint32_t)kCand) {
+          s_fk[par][i] = k;
+          s_fc[par][i] = c;
+          s_fr[par][i] = r;
+        }
+        if (c == 1) {
+          if (!k1c) {
+            k1 = k;
+            r1 = r;
+          }
+          k1c = true;
+        } else if (c > tc[kCand - 1]) {
+#pragma unroll
+          for (int q = 0; q < kCand; ++q) {
+            if (c > tc[q]) {
+              const uint64_t c2 = tc[q], k2 = tk[q], r2 = tr[q];
+              tc[q] = c;
+              tk[q] = k;
+              tr[q] = r;
+              c = c2;
+              k = k2;
+              r = r2;
+            }
+          }
+        }
+      }
+    };
+    {
+      constexpr int U = 2;
+      uint32_t sl[U];
+      uint64_t kv[U], vv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = tid + (uint32_t)u * kCThreads;
+        sl[u] = i < n ? list[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kv[u] = tkey[sl[u]];
+        vv[u] = tval[sl[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = tid + (uint32_t)u * kCThreads;
+        if (i < n) {
+          tkey[sl[u]] = kEmptyKey;
+          tval[sl[u]] = 0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = tid + (uint32_t)u * kCThreads;
+        if (i < n && !overflow) stat(i, kv[u], vv[u] & M24, vv[u] >> 24);
+      }
+      for (uint32_t i = tid + (uint32_t)U * kCThreads; i < n; i += kCThreads) {
+        const uint32_t s = list[i];
+        const uint64_t kk = tkey[s], vx = tval[s];
+        tkey[s] = kEmptyKey;
+        tval[s] = 0;
+        if (!overflow) stat(i, kk, vx & M24, vx >> 24);
+      }
+    }
+    {
+      const uint64_t wun = __ockl_wfred_add_u64(un);
+      const double we = __ockl_wfred_add_f64(e);
+      const uint64_t wmx = __ockl_wfred_max_u64(mx);
+      if (lane == 0) {
+        s_wun[par][wave] = wun;
+        s_went[par][wave] = we;
+        s_wmax[par][wave] = wmx;
+      }
+    }
+    __syncthreads();  //                                                            [barrier 2]
+    mark(2);
+    if (overflow) {
+      if (tid == 0) {  // the whole partition, again, by the generic kernel
+        const unsigned int q = atomicAdd(a.ovf_n, 1u);
+        a.ovf_out[q] = FEntry{p, 0, 0, 0};
+      }
+    } else {
+      uint64_t M = 0;
+      if (cand) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) M = s_wmax[par][w] > M ? s_wmax[par][w] : M;
+      }
+      if (cand && M > 1) {
+        int taken = 0;
+        auto pack = [&]() -> uint64_t {
+          uint64_t c = 0;
+#pragma unroll
+          for (int i = 0; i < kCand; ++i) c = i == taken ? tc[i] : c;
+          if (c) return (c << 16) | ((uint64_t)tid << 2) | (uint64_t)taken;
+          return k1c ? (1ULL << 16) | ((uint64_t)tid << 2) | 3ULL : 0ULL;
+        };
+        static_assert(kCThreads <= 1024 && kCand == 4, "candidate packing");
+#pragma unroll
+        for (int r = 0; r < kCand; ++r) {
+          const uint64_t mine = pack();
+          const uint64_t wm = __ockl_wfred_max_u64(mine);
+          if (lane == 0 && wm) atomicMax(&s_top[r], (unsigned long long)wm);
+          __syncthreads();
+          const uint64_t t = s_top[r];
+          if (t && t == mine) {
+            const int q = (int)(t & 3u);
+            const bool one = (uint32_t)(t >> 16) == 1u && !(taken < kCand && tc[taken]);
+            uint64_t kk = 0, cc = 0, rr = 0;
+#pragma unroll
+            for (int i = 0; i < kCand; ++i) {
+              kk = i == q ? tk[i] : kk;
+              cc = i == q ? tc[i] : cc;
+              rr = i == q ? tr[i] : rr;
+            }
+            if (one) {
+              kk = k1;
+              cc = 1;
+              rr = r1;
+              k1c = false;
+            } else {
+              ++taken;
+            }
+            a.cand[(uint64_t)p * kCand + r] = Group{kk, cc, rr};
+          } else if (!t && tid == 0) {
+            a.cand[(uint64_t)p * kCand + r] = Group{0, 0, 0};
+          }
+        }
+      }
+      if (tid == 0) {
+        s_tp[par] = p;
+        s_tg[par] = gtot;
+        s_tr0[par] = r0;
+        s_tfl[par] = TF_VALID | (cand && M <= 1 ? TF_CANDFAST : 0u);
+      }
+    }
+    mark(3);
+    cur = pf;
+    nb = nb2;
+  }
+  __syncthreads();
+  if (wave == 0) tail(par ^ 1u);
+  if (collisions) atomicAdd(&a.counters[C_COLLISIONS], collisions);
+}
+
 // Multi-block fixed-order reduction of the per-partition statistics: block b sums its contiguous
 // range (coalesced: consecutive threads read consecutive partitions), freq_reduce_final adds the
 // blocks' partials in block order.  out = {groups, unique, entropy bits}.
@@ -4007,6 +4375,10 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       const char* e = getenv("DQ_FREQ_OLDC");
       return e && atoi(e) != 0;
     }();
+    static const bool old_hc = [] {  // DQ_FREQ_OLDHC=1: A/B hook, the generic hashed kernel
+      const char* e = getenv("DQ_FREQ_OLDHC");
+      return e && atoi(e) != 0;
+    }();
     static const bool no_pk = [] {  // DQ_FREQ_NOPK=1: A/B hook, no packed-slot first pass
       const char* e = getenv("DQ_FREQ_NOPK");
       return e && atoi(e) != 0;
@@ -4024,6 +4396,10 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
         hipLaunchKernelGGL((freq_phaseC_x<false, false>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else if (f->exact)
         hipLaunchKernelGGL(freq_phaseC<false>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
+      else if (round == 0 && !old_hc && clk)
+        hipLaunchKernelGGL(freq_phaseC_h<true>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
+      else if (round == 0 && !old_hc)
+        hipLaunchKernelGGL(freq_phaseC_h<false>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else
         hipLaunchKernelGGL(freq_phaseC<true>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
       HIP_TRY(hipGetLastError());
@@ -4036,7 +4412,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       HIP_TRY(hipStreamSynchronize(f->stream));
       HIP_TRY(hipMemcpy(&m, f->ovf_n.p, 4, hipMemcpyDeviceToHost));
       if (m) reduced = false;
-      if (clk && f->exact && !old_c) {  // freq_phaseC_x: 8 stamps per item
+      if (clk && ((f->exact && !old_c) || (!f->exact && round == 0 && !old_hc))) {  // C_x / C_h: 8 stamps per item
         unsigned long long h[16 * 8];
         (void)hipMemcpy(h, clk, sizeof(h), hipMemcpyDeviceToHost);
         double acc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -4084,7 +4460,10 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       }
       // recount the overflowing partitions over disjoint hash subsets
       // (a packed-slot first pass hands whole partitions on: no hash subsets yet)
-      if (!(round == 0 && f->s_bits == kMaxSubBits && !no_pk && f->exact && !old_c)) f->recounted = true;
+      // (so does the hashed first pass)
+      if (!(round == 0 && f->s_bits == kMaxSubBits && !no_pk && f->exact && !old_c) &&
+          !(round == 0 && !f->exact && !old_hc))
+        f->recounted = true;
       f->ovf_a.swap(f->ovf_b);  // ovf_b = this round's entries
       HIP_TRY(f->ovf_a.ensure(2 * (size_t)m));
       HIP_TRY(hipMemsetAsync(f->ovf_n.p, 0, 4, f->stream));
