@@ -3274,34 +3274,77 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
       issue();
       mark(5);
       __builtin_amdgcn_sched_barrier(0);
-      uint32_t mine = 0;
-      for (int pr = 0; todo && pr < 4 * KT; ++pr) {
+      uint32_t mine = 0, cmp = 0;  // cmp bit q: the hash matched another record's key; compare
+      uint64_t crs[PF];
+      auto probe_rounds = [&]() {
+        for (int pr = 0; todo && pr < 4 * KT; ++pr) {
 #pragma unroll
-        for (int q = 0; q < PF; ++q)
-          old[q] = (todo >> q) & 1u ? atomicCAS((unsigned long long*)&tkey[slot[q]], kEmptyKey, h[q]) : 0ULL;
+          for (int q = 0; q < PF; ++q)
+            old[q] = (todo >> q) & 1u ? atomicCAS((unsigned long long*)&tkey[slot[q]], kEmptyKey, h[q]) : 0ULL;
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-          if (!((todo >> q) & 1u)) continue;
-          if (old[q] == kEmptyKey) {  // claimed: publish rep and count (non-zero)
-            __hip_atomic_store(&tval[slot[q]], v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            mine |= 1u << q;
-            todo &= ~(1u << q);
-          } else if (old[q] == h[q]) {
-            const uint64_t sv = __hip_atomic_load(&tval[slot[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (!sv) continue;  // claimed, not yet published: the same slot next round
-            const uint64_t rs = sv >> 24, rm = v[q] >> 24;
-            const bool same = rs == rm || enc_equal_lean(a.arena, rs, rm, a.types, a.n_keys);
-            if (same) {
-              atomicAdd((unsigned long long*)&tval[slot[q]], (unsigned long long)(v[q] & M24));
+          for (int q = 0; q < PF; ++q) {
+            if (!((todo >> q) & 1u)) continue;
+            if (old[q] == kEmptyKey) {  // claimed: publish rep and count (non-zero)
+              __hip_atomic_store(&tval[slot[q]], v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              mine |= 1u << q;
+              todo &= ~(1u << q);
+            } else if (old[q] == h[q]) {
+              const uint64_t sv = __hip_atomic_load(&tval[slot[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              if (!sv) continue;  // claimed, not yet published: the same slot next round
+              crs[q] = sv >> 24;
+              if (crs[q] == (v[q] >> 24)) {  // (the same arena key: another digit of one group)
+                atomicAdd((unsigned long long*)&tval[slot[q]], (unsigned long long)(v[q] & M24));
+              } else {
+                cmp |= 1u << q;  // decided on the bytes below, every record's loads together
+              }
               todo &= ~(1u << q);
             } else {
-              ++collisions;  // two keys on one 64-bit hash: two groups
               slot[q] = (slot[q] + step[q]) & (KT - 1);
             }
-          } else {
-            slot[q] = (slot[q] + step[q]) & (KT - 1);
           }
         }
+      };
+      probe_rounds();
+      // Equal hashes on different arena keys (duplicates of a key, which phase A wrote once per
+      // row): both keys' first 6 words for every such record in flight at once -- one round trip
+      // per round of inserts instead of a chain per record -- which decide a one-utf8-column key
+      // of <= 16 bytes; a longer key whose first words agree is compared to the end.
+      while (__ballot(cmp != 0)) {
+        uint32_t ka[PF][6], kb[PF][6];
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          const uint32_t* x = reinterpret_cast<const uint32_t*>(a.arena + ((cmp >> q) & 1u ? crs[q] : 0));
+          const uint32_t* y = reinterpret_cast<const uint32_t*>(a.arena + ((cmp >> q) & 1u ? (v[q] >> 24) : 0));
+#pragma unroll
+          for (int k = 0; k < 6; ++k) {
+            ka[q][k] = x[k];
+            kb[q][k] = y[k];
+          }
+        }
+        uint32_t retry = 0;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          if (!((cmp >> q) & 1u)) continue;
+          const uint32_t n = a.n_keys == 1 && a.types[0] == DQ_UTF8
+                                 ? (ka[q][0] ? 2 + pad4(ka[q][1]) / 4 : 1u)
+                                 : enc_size(reinterpret_cast<const uint32_t*>(a.arena + crs[q]), a.types,
+                                            a.n_keys) / 4;
+          uint32_t d = 0;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) d |= (uint32_t)k < n ? ka[q][k] ^ kb[q][k] : 0u;
+          bool same = d == 0;
+          if (same && n > 6) same = enc_equal_lean(a.arena, crs[q], v[q] >> 24, a.types, a.n_keys);
+          if (same) {
+            atomicAdd((unsigned long long*)&tval[slot[q]], (unsigned long long)(v[q] & M24));
+          } else {  // two keys on one 64-bit hash: two groups; probe on from the next slot
+            ++collisions;
+            slot[q] = (slot[q] + step[q]) & (KT - 1);
+            retry |= 1u << q;
+          }
+        }
+        cmp = 0;
+        todo = retry;
+        if (__ballot(todo != 0)) probe_rounds();
       }
       if (todo) s_ovf[par] = 1;  // the table is full
       const uint32_t nm = (uint32_t)__builtin_popcount(mine);
