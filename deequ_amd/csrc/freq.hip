@@ -691,7 +691,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
             h = str_row_hash_reg(w0, w1, len[j]);
             str_short_key_reg(w0, w1, len[j], k0, k1);
           } else {
-            h = str_row_hash_long(c.data + s0[j], len[j]);
+            h = fmix_bij(fold_col_hash(kRowHashSeed, str_hash_long_dev(c.data + s0[j], len[j], 0)));
           }
         } else {
           // a NULL row.  Histogram: the NULL rows are one group kept apart (C_NULL_GROUP), so

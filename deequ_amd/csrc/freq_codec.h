@@ -192,13 +192,33 @@ DQ_HD void mem_str16(const uint8_t* p, int32_t len, uint64_t& w0, uint64_t& w1) 
     else w1 |= (uint64_t)p[q] << (8 * (q - 8));
   }
 }
+// A string longer than 16 bytes: its 16-byte chunks (little-endian words, the last one zero-padded)
+// mixed in order, then an avalanche -- three multiplies per chunk, and chunks a device thread
+// builds from aligned dwords in registers (str_hash_long_dev).  Internal to the frequency table
+// like every group-by hash (XXH64 over the bytes took a dependent chain of loads per 8 bytes).
+DQ_HD uint64_t str_long_chunk(uint64_t acc, uint64_t w0, uint64_t w1) {
+  return rotl64(acc ^ rotl64(w0 * P1, 31) ^ (w1 * P2), 27) * P1 + P4;
+}
+DQ_HD uint64_t str_long_final(uint64_t acc) {
+  acc ^= acc >> 33;
+  acc *= P2;
+  acc ^= acc >> 29;
+  return acc;
+}
+DQ_HD uint64_t str_long_seed(int32_t len, uint64_t seed) { return seed ^ ((uint64_t)len * P5); }
 DQ_HD uint64_t str_bytes_hash(const uint8_t* p, int32_t len, int k) {
   if (len <= kHash16Max) {
     uint64_t w0, w1;
     mem_str16(p, len, w0, w1);
     return str_hash16(w0, w1, len, 17 + k);
   }
-  return xxh_bytes(MemBytes{p}, (int64_t)len, 17 + k);
+  uint64_t acc = str_long_seed(len, 17 + k);
+  for (int32_t o = 0; o < len; o += 16) {
+    uint64_t w0, w1;
+    mem_str16(p + o, len - o < 16 ? len - o : 16, w0, w1);
+    acc = str_long_chunk(acc, w0, w1);
+  }
+  return str_long_final(acc);
 }
 DQ_HD uint64_t str_col_hash(const SView& v, int k) {
   return v.p ? str_bytes_hash(v.p, v.len, k)
@@ -304,6 +324,37 @@ DQ_HD void load_str16(const uint8_t* p, int32_t len, uint64_t& w0, uint64_t& w1)
   str16_from_dwords(d, sh, len, w0, w1);
 }
 
+
+#ifdef __HIPCC__
+// str_bytes_hash(p, len, k) for 16 < len, the string read as aligned dwords: up to 48 bytes with
+// every load in flight together (each dword holds a byte of the string), then 16 bytes per round.
+__device__ inline uint64_t str_hash_long_dev(const uint8_t* p, int32_t len, int k) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+  const int sh = (int)(reinterpret_cast<uintptr_t>(p) & 3u);
+  uint64_t acc = str_long_seed(len, 17 + k);
+  int32_t o = 0;
+  if (len <= 48) {
+    const int last = ((sh + len + 3) >> 2) - 1;  // <= 12
+    uint32_t d[13];
+#pragma unroll
+    for (int j = 0; j < 13; ++j) d[j] = q[j < last ? j : last];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      if (16 * c >= len) break;
+      uint64_t w0, w1;
+      str16_from_dwords(d + 4 * c, sh, len - 16 * c < 16 ? len - 16 * c : 16, w0, w1);
+      acc = str_long_chunk(acc, w0, w1);
+    }
+    return str_long_final(acc);
+  }
+  for (; o < len; o += 16) {
+    uint64_t w0, w1;
+    load_str16(p + o, len - o < 16 ? len - o : 16, w0, w1);
+    acc = str_long_chunk(acc, w0, w1);
+  }
+  return str_long_final(acc);
+}
+#endif
 
 DQ_HD uint32_t pad4(uint32_t n) { return (n + 3u) & ~3u; }
 

@@ -551,3 +551,38 @@ def test_exact_bucket_pieces_at_scale(nulls, gpu_device):
     order = np.argsort(-counts, kind="stable")[:3]
     assert [c for _, c in top] == counts[order].tolist()
     assert top[0][0][0] == 42
+
+
+@pytest.mark.parametrize("batch", [None, 9_000])
+def test_long_string_keys_match_oracle(batch, gpu_device):
+    """One-column and two-column keys over strings of 17..80 bytes (the chunked long-string hash:
+    the device's register path up to 48 bytes, 16 bytes per round beyond), with duplicates within
+    and across batches, and a merge of two tables: groups, Σ[c==1] and entropy vs the oracle."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    rng = np.random.default_rng(21)
+    n = 30_000
+    base = [("https://example.org/" * 4)[: rng.integers(17, 81)] for _ in range(40)]
+    keys = [base[i % 40][:-3] + f"{rng.integers(0, 300):03d}" for i in range(n)]
+    mask = rng.random(n) < 0.04
+    t = pa.table({"l": pa.array([None if m else k for k, m in zip(keys, mask)], pa.string()),
+                  "p": pa.array([["a", "bb", None][i % 3] for i in range(n)], pa.string())})
+    ot = O.OTable({"l": t.column("l").to_pylist(), "p": t.column("p").to_pylist()},
+                  {"l": "string", "p": "string"})
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=batch)
+    for cols in (["l"], ["l", "p"]):
+        exp = O.frequencies(ot, cols)
+        halves = []
+        for lo, hi in ((0, len(df.batches) // 2), (len(df.batches) // 2, len(df.batches))):
+            ft = FrequencyTable(cols, [df.schema[c].dtype for c in cols], 0)
+            for b in df.batches[lo:hi]:
+                ft.add([b[c] for c in cols])
+            halves.append(ft)
+        ft = halves[0].merged(halves[1]) if len(df.batches) > 1 else halves[0]
+        s = ft.summarize()
+        assert s.n_groups == len(exp)
+        assert s.n_unique == sum(1 for c in exp.values() if c == 1)
+        assert dict(ft.export()) == exp
+        ent = O.entropy(exp, n)
+        assert _rel_close(s.entropy, ent)
