@@ -391,6 +391,17 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   }
   for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
   if (tid == 0) s_bypass = 0;
+  if constexpr (STR1) {
+    // the arena bytes of every key this workgroup may encode, reserved once: at most 8 + len + 3
+    // per row (a per-chunk reservation made every workgroup's tiles queue on the one cursor word)
+    if (tid == 0) {
+      const int32_t* off = reinterpret_cast<const int32_t*>(a.ks.cols[0].values);
+      const int64_t r0 = min(t0 * a.tile_items, a.n_items), r1 = min(t1 * a.tile_items, a.n_items);
+      const uint64_t need = r1 > r0 ? (uint64_t)(r1 - r0) * 11 + (uint64_t)(off[r1] - off[r0]) : 0;
+      s_arena_base = need ? atomicAdd(a.arena_cursor, (unsigned long long)need) : 0ULL;
+      s_arena_cur = 0;
+    }
+  }
   const bool pieces = XP && a.pstart != nullptr;
   if constexpr (XP) {
     if (pieces) {
@@ -433,7 +444,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
       hrow[tid] = (uint16_t)ex;
     }
     if (tid == 0) hrow[kBuckets] = (uint16_t)total;
-    if constexpr (HASHED && !FROM_REC) {
+    if constexpr (HASHED && !FROM_REC && !STR1) {
       const uint64_t all = block_sum_u64(arena_need, s_red);
       if (tid == 0) {
         s_arena_base = all ? atomicAdd(a.arena_cursor, (unsigned long long)all) : 0ULL;
