@@ -611,13 +611,14 @@ DQ_DEV double as_f64(uint64_t bits, bool is_long) {
 }
 
 // The co-moments of a lane's 16 rows (bit i of sel: row i selected) merged into (n, c).
+template <int K = 8>
 DQ_DEV void corr_fold16(const uint4* qx, const uint4* qy, uint32_t sel, bool xl, bool yl, int64_t& n,
                         double* c) {
   const int nb = __popc(sel);
   if (!nb) return;
-  double xs[16], ys[16];
+  double xs[2 * K], ys[2 * K];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < K; ++k) {
     xs[2 * k] = as_f64((uint64_t)qx[k].x | ((uint64_t)qx[k].y << 32), xl);
     xs[2 * k + 1] = as_f64((uint64_t)qx[k].z | ((uint64_t)qx[k].w << 32), xl);
     ys[2 * k] = as_f64((uint64_t)qy[k].x | ((uint64_t)qy[k].y << 32), yl);
@@ -625,7 +626,7 @@ DQ_DEV void corr_fold16(const uint4* qx, const uint4* qy, uint32_t sel, bool xl,
   }
   double sx = 0, sy = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < 2 * K; ++i) {
     if ((sel >> i) & 1u) {
       sx += xs[i];
       sy += ys[i];
@@ -636,7 +637,7 @@ DQ_DEV void corr_fold16(const uint4* qx, const uint4* qy, uint32_t sel, bool xl,
   b[1] = sy / nb;
   b[2] = b[3] = b[4] = 0.0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < 2 * K; ++i) {
     if ((sel >> i) & 1u) {
       const double dx = xs[i] - b[0], dy = ys[i] - b[1];
       b[2] += dx * dy;
@@ -676,12 +677,15 @@ DQ_DEV void corr_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int64_t
 }
 
 DQ_DEV void hll_update(uint32_t* regs, uint64_t h);
+template <int K>
 DQ_DEV void corr_hll_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int64_t& n, double* c,
                             uint32_t* regs);
 
 // HLL = true (BC_CORR_HLL): the same pass also feeds the rows of column t.hll_side into the HLL
 // registers `regs` of the fused ApproxCountDistinct task.
-template <bool HLL>
+// K: 16-byte loads per lane and column per chunk (K = 8: 1024 rows per wave; K = 4: 512 rows, half
+// the registers, so more waves per SIMD hide the loads behind the hashing)
+template <bool HLL, int K = 8>
 DQ_DEV void corr_rows(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& acc, uint32_t* regs) {
   const int l = lane_id();
   int64_t n = 0;
@@ -691,9 +695,10 @@ DQ_DEV void corr_rows(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
   const bool y8 = t.type2 == DQ_INT64 || t.type2 == DQ_FLOAT64;
   if (t.vec_ok && x8 && y8) {
     const bool xl = t.type == DQ_INT64, yl = t.type2 == DQ_INT64;
-    for (; r_fast + 1024 <= r_end; r_fast += 1024) {
-      if constexpr (HLL) corr_hll_chunk8(t, r_fast, xl, yl, n, c, regs);
-      else corr_chunk8(t, r_fast, xl, yl, n, c);
+    if constexpr (HLL) {
+      for (; r_fast + 128 * K <= r_end; r_fast += 128 * K) corr_hll_chunk8<K>(t, r_fast, xl, yl, n, c, regs);
+    } else {
+      for (; r_fast + 1024 <= r_end; r_fast += 1024) corr_chunk8(t, r_fast, xl, yl, n, c);
     }
   }
   for (int64_t r0 = r_fast; r0 < r_end; r0 += 512) {
@@ -865,14 +870,15 @@ DQ_DEV void hll_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint32_t
 // BC_CORR_HLL vector path: ApproxCountDistinct(x) + Correlation(x, y) (BASELINE.json configs[3])
 // read x and y once.  Loads and co-moments as corr_chunk8; the HLL rows are the non-NULL rows of
 // column t.hll_side (and where), hashed as hll_chunk8 does.
+template <int K>
 DQ_DEV void corr_hll_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int64_t& n, double* c,
                             uint32_t* regs) {
   const int l = lane_id();
   const uint64_t* X = reinterpret_cast<const uint64_t*>(t.values) + r0 + 2 * l;
   const uint64_t* Y = reinterpret_cast<const uint64_t*>(t.values2) + r0 + 2 * l;
-  uint4 qx[8], qy[8];
+  uint4 qx[K], qy[K];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < K; ++k) {
     qx[k] = ld16(X + 128 * k);
     qy[k] = ld16(Y + 128 * k);
   }
@@ -882,7 +888,7 @@ DQ_DEV void corr_hll_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int
   const uint32_t sh = (uint32_t)(2 * l) & 31u;
   uint32_t sel = 0, hsel = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < K; ++k) {
     const int64_t w = w0 + 4 * k;
     const uint32_t vx = bits32(t.valid, w), vy = bits32(t.valid2, w);
     const uint32_t wm = t.w_val ? bits32(t.w_val, w) & bits32(t.w_vld, w) : ~0u;
@@ -890,7 +896,7 @@ DQ_DEV void corr_hll_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int
     hsel |= ((((hy ? vy : vx) & wm) >> sh) & 3u) << (2 * k);
   }
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < K; ++k) {
     const uint4 q = hy ? qy[k] : qx[k];
     uint64_t x0 = (uint64_t)q.x | ((uint64_t)q.y << 32);
     uint64_t x1 = (uint64_t)q.z | ((uint64_t)q.w << 32);
@@ -902,7 +908,7 @@ DQ_DEV void corr_hll_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int
     if ((hsel >> (2 * k)) & 1u) hll_update(regs, h0);
     if ((hsel >> (2 * k + 1)) & 1u) hll_update(regs, h1);
   }
-  corr_fold16(qx, qy, sel, xl, yl, n, c);
+  corr_fold16<K>(qx, qy, sel, xl, yl, n, c);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -943,8 +949,8 @@ DQ_DEV bool queue_next(uint32_t* heads, uint32_t lo, uint32_t hi, int home, int&
 // batches of a class run in the same launch.
 // The fused HLL + co-moment body (BC_CORR_HLL) is bound by its 64-bit multiplies as much as by
 // HBM: it is held to 128 VGPRs so four waves per SIMD hide the loads behind the hashing.
-template <int BC>
-__global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? 4 : 1)) scan_kernel(const TaskDesc* __restrict__ tasks, int n_desc,
+template <int BC, int K = 8>
+__global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? (K == 8 ? 4 : 5) : 1)) scan_kernel(const TaskDesc* __restrict__ tasks, int n_desc,
                                                       uint32_t item_lo, uint32_t item_hi,
                                                       uint32_t* __restrict__ queue,
                                                       Acc* __restrict__ partial,
@@ -982,7 +988,7 @@ __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? 4 : 1)) scan_kern
     if constexpr (BC == BC_STR_IN) str_in_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_DTYPE) dtype_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_CORR) corr_item(t, r_begin, r_end, a);
-    if constexpr (BC == BC_CORR_HLL) corr_rows<true>(t, r_begin, r_end, a, hll_lds + t.hll_out * kHllM);
+    if constexpr (BC == BC_CORR_HLL) corr_rows<true, K>(t, r_begin, r_end, a, hll_lds + t.hll_out * kHllM);
     if constexpr (BC == BC_HLL) {
       hll_item(t, r_begin, r_end, hll_lds + t.hll_out * kHllM);
     } else {
@@ -1178,20 +1184,35 @@ size_t scan_lds_bytes(int body, int n_hll) {
   return body == BC_HLL || body == BC_CORR_HLL ? (size_t)n_hll * kHllM * 4 : 0;
 }
 
+// DQ_CORR_K=4: A/B hook, the fused co-moment + HLL body on 4-deep chunks at 6 waves per SIMD
+static int corr_k() {
+  static const int k = [] {
+    const char* e = getenv("DQ_CORR_K");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  return k;
+}
+
 template <int BC>
 static void launch_body(const ScanLaunch& L, const TaskDesc* tasks, int n_desc, int n_hll,
                         uint32_t* queues, Acc* partial, uint32_t* hll_stage, hipStream_t stream) {
-  hipLaunchKernelGGL(scan_kernel<BC>, dim3(L.grid), dim3(kBlock), scan_lds_bytes(BC, n_hll), stream,
-                     tasks, n_desc, L.item_lo, L.item_hi, queues + BC * kQueueHeads * kQueueStride,
-                     partial, hll_stage, n_hll);
+  auto go = [&](auto kernel) {
+    hipLaunchKernelGGL(kernel, dim3(L.grid), dim3(kBlock), scan_lds_bytes(BC, n_hll), stream,
+                       tasks, n_desc, L.item_lo, L.item_hi, queues + BC * kQueueHeads * kQueueStride,
+                       partial, hll_stage, n_hll);
+  };
+  if (BC == BC_CORR_HLL && corr_k() == 4) go(scan_kernel<BC, 4>);
+  else go(scan_kernel<BC>);
 }
 
 template <int BC>
 static int occupancy_of(int n_hll) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<BC>, kBlock,
-                                                   scan_lds_bytes(BC, n_hll)) != hipSuccess)
-    n = 2;
+  const hipError_t e =
+      BC == BC_CORR_HLL && corr_k() == 4
+          ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<BC, 4>, kBlock, scan_lds_bytes(BC, n_hll))
+          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_kernel<BC>, kBlock, scan_lds_bytes(BC, n_hll));
+  if (e != hipSuccess) n = 2;
   return n > 0 ? n : 1;
 }
 
