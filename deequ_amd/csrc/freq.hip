@@ -325,6 +325,27 @@ DQ_DEV void row_encode_dw(const KeySet& ks, int64_t r, uint32_t* dst) {
   }
 }
 
+// Short form of a two-utf8-column key whose values are both at most 7 bytes (the MutualInformation
+// joints of low-cardinality string columns): k0, k1 = each value's bytes | its length << 56, an
+// exact key, so phase A's dedupe decides a hit in LDS (dsk0 / dsk1) instead of re-reading both
+// rows' strings; any other key has k1 = kNoShort.  (Keyed rows of a multi-column key have no NULL.)
+DQ_DEV void multi_short_key(const KeySet& ks, int64_t r, uint64_t& k0, uint64_t& k1) {
+  k0 = 0;
+  k1 = kNoShort;
+  if (ks.n_keys != 2 || ks.cols[0].type != DQ_UTF8 || ks.cols[1].type != DQ_UTF8) return;
+  uint64_t w[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    SView v;
+    if (!key_str(ks, k, r, v) || !v.p || v.len > 7) return;
+    uint64_t w0, w1;
+    load_str16(v.p, v.len, w0, w1);
+    w[k] = w0 | ((uint64_t)v.len << 56);
+  }
+  k0 = w[0];
+  k1 = w[1];
+}
+
 template <bool HASHED, bool FROM_REC>
 struct AKeys {
   static constexpr int kDedupe = FROM_REC ? (HASHED ? 128 : 256) : (HASHED ? 256 : 512);
@@ -736,7 +757,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
           keyed |= 1u << j;
           stash[q * W] = row_hash_hashed_dw(a.ks, i);
           stash[q * W + 1] = (uint64_t)i;  // the row until it is encoded
-          if constexpr (SK) ssk1[q] = kNoShort;
+          if constexpr (SK) multi_short_key(a.ks, i, ssk0[q], ssk1[q]);
         }
       }
     }

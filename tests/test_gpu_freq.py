@@ -586,3 +586,36 @@ def test_long_string_keys_match_oracle(batch, gpu_device):
         assert dict(ft.export()) == exp
         ent = O.entropy(exp, n)
         assert _rel_close(s.entropy, ent)
+
+
+@pytest.mark.parametrize("long_frac", [0.0, 0.01])
+def test_two_small_string_columns_dedupe_on_short_forms(long_frac, gpu_device):
+    """A two-column utf8 key whose values are at most 7 bytes (a MutualInformation joint of two
+    low-cardinality columns) dedupes in phase A on its LDS short form; a few longer values take
+    the row compare.  Groups, Σ[c==1] and entropy vs the oracle."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    rng = np.random.default_rng(5)
+    n = 200_000
+    pa_vals = np.array(["high", "low", "medium", "", "x"], dtype=object)
+    pb_vals = np.array(["a", "bb", "ccc", "dddd", "eeeeeee"], dtype=object)
+    a_ = pa_vals[rng.integers(0, 5, n)]
+    b_ = pb_vals[rng.integers(0, 5, n)]
+    longs = rng.random(n) < long_frac
+    b_ = np.where(longs, "a much longer value", b_)
+    ma, mb = rng.random(n) < 0.05, rng.random(n) < 0.05
+    t = pa.table({"a": pa.array([None if m else v for v, m in zip(a_, ma)], pa.string()),
+                  "b": pa.array([None if m else v for v, m in zip(b_, mb)], pa.string())})
+    ot = O.OTable({"a": t.column("a").to_pylist(), "b": t.column("b").to_pylist()},
+                  {"a": "string", "b": "string"})
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=50_000)
+    ft = FrequencyTable(["a", "b"], [df.schema["a"].dtype, df.schema["b"].dtype], 0)
+    for b in df.batches:
+        ft.add([b["a"], b["b"]])
+    exp = O.frequencies(ot, ["a", "b"])
+    s = ft.summarize()
+    assert s.n_groups == len(exp)
+    assert s.n_unique == sum(1 for c in exp.values() if c == 1)
+    assert dict(ft.export()) == exp
+    assert _rel_close(s.entropy, O.entropy(exp, n))
