@@ -3153,9 +3153,13 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
             } else {
               ++taken;
             }
-            a.cand[(uint64_t)p * kCand + r] = Group{kk, cc, 0};
-          } else if (!t && tid == 0) {
-            a.cand[(uint64_t)p * kCand + r] = Group{0, 0, 0};
+            // (written by the next item's tail: a global store here made the next item's wait
+            // for its prefetched records a wait for the store too)
+            s_fk[par][r] = kk;
+            s_fc[par][r] = cc;
+          } else if (!t && tid == 0) {  // no candidate left: an empty place
+            s_fk[par][r] = 0;
+            s_fc[par][r] = 0;
           }
         }
       }
@@ -3163,7 +3167,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
         s_tp[par] = p;
         s_tg[par] = gtot;
         s_tr0[par] = r0;
-        s_tfl[par] = TF_VALID | (sub ? TF_SUB : 0u) | (cand && M <= 1 ? TF_CANDFAST : 0u);
+        s_tfl[par] = TF_VALID | (sub ? TF_SUB : 0u) | (cand ? TF_CANDFAST : 0u);
       }
     }
     mark(3);
@@ -3564,9 +3568,13 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
             } else {
               ++taken;
             }
-            a.cand[(uint64_t)p * kCand + r] = Group{kk, cc, rr};
-          } else if (!t && tid == 0) {
-            a.cand[(uint64_t)p * kCand + r] = Group{0, 0, 0};
+            s_fk[par][r] = kk;  // (written by the next item's tail, as in freq_phaseC_x)
+            s_fc[par][r] = cc;
+            s_fr[par][r] = rr;
+          } else if (!t && tid == 0) {  // no candidate left: an empty place
+            s_fk[par][r] = 0;
+            s_fc[par][r] = 0;
+            s_fr[par][r] = 0;
           }
         }
       }
@@ -3574,7 +3582,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
         s_tp[par] = p;
         s_tg[par] = gtot;
         s_tr0[par] = r0;
-        s_tfl[par] = TF_VALID | (cand && M <= 1 ? TF_CANDFAST : 0u);
+        s_tfl[par] = TF_VALID | (cand ? TF_CANDFAST : 0u);
       }
     }
     mark(3);
