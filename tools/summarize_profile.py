@@ -21,16 +21,22 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _name(kernel: str) -> str:
+    """'void dq::scan_mixed_kernel<200u>(...)' -> 'dq::scan_mixed_kernel<200u>'"""
+    k = kernel.split("(")[0]
+    return k[5:] if k.startswith("void ") else k
+
+
 def per_kernel(path, counter):
     out = {}
     if not os.path.exists(path):
         return out, []
     rows = list(csv.DictReader(open(path)))
-    keep = [r for r in rows if r["Kernel_Name"].startswith("dq::")]
+    keep = [r for r in rows if _name(r["Kernel_Name"]).startswith("dq::")]
     for r in keep:
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0]
+        name = _name(r["Kernel_Name"])
         out.setdefault(name, []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in out.items()}, keep
 
@@ -45,8 +51,8 @@ def main():
     shutil.copy(stats_path, os.path.join(dst, "kernel_stats.csv"))
     stats = {}
     for r in csv.DictReader(open(stats_path)):
-        if r["Name"].startswith("dq::"):
-            stats[r["Name"].split("(")[0]] = {"calls": int(r["Calls"]),
+        if _name(r["Name"]).startswith("dq::"):
+            stats[_name(r["Name"])] = {"calls": int(r["Calls"]),
                                               "avg_ns": float(r["AverageNs"]),
                                               "min_ns": float(r["MinNs"]),
                                               "max_ns": float(r["MaxNs"])}
