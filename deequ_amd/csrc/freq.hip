@@ -418,8 +418,10 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     if (tid == 0) {
       const int32_t* off = reinterpret_cast<const int32_t*>(a.ks.cols[0].values);
       const int64_t r0 = min(t0 * a.tile_items, a.n_items), r1 = min(t1 * a.tile_items, a.n_items);
-      const uint64_t need = r1 > r0 ? (uint64_t)(r1 - r0) * 11 + (uint64_t)(off[r1] - off[r0]) : 0;
-      s_arena_base = need ? atomicAdd(a.arena_cursor, (unsigned long long)need) : 0ULL;
+      // (16-byte aligned keys, str1_enc_size16: at most 8 + len + 3 + 12 bytes each)
+      const uint64_t need = r1 > r0 ? (uint64_t)(r1 - r0) * 23 + (uint64_t)(off[r1] - off[r0]) + 16 : 0;
+      const unsigned long long base = need ? atomicAdd(a.arena_cursor, (unsigned long long)need) : 0ULL;
+      s_arena_base = (base + 15ULL) & ~15ULL;
       s_arena_cur = 0;
     }
   }
@@ -955,7 +957,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         const int q = j * kThreads + tid;
         const int64_t row = on ? (int64_t)stash[q * W + 1] : 0;
         const uint64_t k0 = SK && on ? ssk0[q] : 0, k1 = SK && on ? ssk1[q] : kNoShort;
-        const uint32_t sz = on ? enc_size_sk(row, k1) : 0u;
+        uint32_t sz = on ? enc_size_sk(row, k1) : 0u;
+        if constexpr (STR1) sz = (sz + 15u) & ~15u;  // 16-byte aligned keys: vector stores
         const uint32_t incl = __ockl_wfscan_add_u32(sz, true);
         const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         unsigned long long wbase = 0;
@@ -966,10 +969,10 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         const uint64_t off = s_arena_base + wbase + (incl - sz);
         if constexpr (STR1) {
           if (k1 != kNoShort) {
-            str1_encode_short(k0, k1, reinterpret_cast<uint32_t*>(a.arena + off));
+            str1_encode_short16(k0, k1, reinterpret_cast<uint32_t*>(a.arena + off));
           } else {
             const SView v = str1_view(a.ks, row);
-            str1_encode_copy(v.p, v.len, reinterpret_cast<uint32_t*>(a.arena + off));
+            str1_encode_copy16(v.p, v.len, reinterpret_cast<uint32_t*>(a.arena + off));
           }
         } else {
           row_encode_dw(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
@@ -3346,31 +3349,45 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
       // per round of inserts instead of a chain per record -- which decide a one-utf8-column key
       // of <= 16 bytes; a longer key whose first words agree is compared to the end.
       while (__ballot(cmp != 0)) {
-        uint32_t ka[PF][6], kb[PF][6];
+        // windows of 8 words, every undecided record's loads of a window in flight together
+        uint32_t undecided = cmp, neq = 0, nw[PF];
+        for (uint32_t w0 = 0; __ballot(undecided != 0); w0 += 8) {
+          uint32_t ka[PF][8], kb[PF][8];
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-          const uint32_t* x = reinterpret_cast<const uint32_t*>(a.arena + ((cmp >> q) & 1u ? crs[q] : 0));
-          const uint32_t* y = reinterpret_cast<const uint32_t*>(a.arena + ((cmp >> q) & 1u ? (v[q] >> 24) : 0));
+          for (int q = 0; q < PF; ++q) {
+            const bool on = (undecided >> q) & 1u;
+            const uint32_t* x = reinterpret_cast<const uint32_t*>(a.arena + (on ? crs[q] : 0)) + (on ? w0 : 0);
+            const uint32_t* y = reinterpret_cast<const uint32_t*>(a.arena + (on ? (v[q] >> 24) : 0)) + (on ? w0 : 0);
 #pragma unroll
-          for (int k = 0; k < 6; ++k) {
-            ka[q][k] = x[k];
-            kb[q][k] = y[k];
+            for (int k = 0; k < 8; ++k) {
+              ka[q][k] = x[k];
+              kb[q][k] = y[k];
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < PF; ++q) {
+            if (!((undecided >> q) & 1u)) continue;
+            if (w0 == 0)  // words of the slot's key (self-delimiting encoding)
+              nw[q] = a.n_keys == 1 && a.types[0] == DQ_UTF8
+                          ? (ka[q][0] ? 2 + pad4(ka[q][1]) / 4 : 1u)
+                          : enc_size(reinterpret_cast<const uint32_t*>(a.arena + crs[q]), a.types,
+                                     a.n_keys) / 4;
+            uint32_t d = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d |= w0 + (uint32_t)k < nw[q] ? ka[q][k] ^ kb[q][k] : 0u;
+            if (d) {
+              neq |= 1u << q;
+              undecided &= ~(1u << q);
+            } else if (w0 + 8 >= nw[q]) {
+              undecided &= ~(1u << q);  // equal to the end
+            }
           }
         }
         uint32_t retry = 0;
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
           if (!((cmp >> q) & 1u)) continue;
-          const uint32_t n = a.n_keys == 1 && a.types[0] == DQ_UTF8
-                                 ? (ka[q][0] ? 2 + pad4(ka[q][1]) / 4 : 1u)
-                                 : enc_size(reinterpret_cast<const uint32_t*>(a.arena + crs[q]), a.types,
-                                            a.n_keys) / 4;
-          uint32_t d = 0;
-#pragma unroll
-          for (int k = 0; k < 6; ++k) d |= (uint32_t)k < n ? ka[q][k] ^ kb[q][k] : 0u;
-          bool same = d == 0;
-          if (same && n > 6) same = enc_equal_lean(a.arena, crs[q], v[q] >> 24, a.types, a.n_keys);
-          if (same) {
+          if (!((neq >> q) & 1u)) {
             atomicAdd((unsigned long long*)&tval[slot[q]], (unsigned long long)(v[q] & M24));
           } else {  // two keys on one 64-bit hash: two groups; probe on from the next slot
             ++collisions;
@@ -5012,6 +5029,7 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     int64_t n_wg_a = 0;
     phaseA_chunks(true, false, rows, f->tile, &n_wg_a);
     bound += (uint64_t)n_wg_a * (kSmallThreads / 64) * kSmallCand * 16 + kBatchTabs * kBatchSlots * 16;
+    bound += (uint64_t)n_wg_a * 32;  // (the string phase A's per-workgroup 16-byte alignment)
     if (f->arena.n < f->arena_hi + bound + 64) {  // may not fit: learn the true use, then grow
       dq_status cs = pull_counters(f);
       if (cs != DQ_OK) return cs;

@@ -508,6 +508,54 @@ __device__ inline void str1_encode_copy(const uint8_t* p, int32_t len, uint32_t*
     }
   }
 }
+// The same two encodings with 16-byte stores, at a 16-byte aligned dst with room for the encoding
+// rounded up to 16 bytes (str1_enc_size16): one store instruction per 16 bytes instead of one per
+// word (scattered 4-byte stores made the string path's arena writes the slowest part of a tile).
+DQ_HD uint32_t str1_enc_size16(int32_t len) { return (8u + pad4((uint32_t)len) + 15u) & ~15u; }
+#ifdef __HIPCC__
+__device__ inline void str1_encode_short16(uint64_t k0, uint64_t k1, uint32_t* dst) {
+  const uint32_t len = str1_short_len(k1);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = make_uint4(1u, len, (uint32_t)k0, (uint32_t)(k0 >> 32));
+  if (len > 8) d[1] = make_uint4((uint32_t)k1, (uint32_t)(k1 >> 32) & 0xFFFFFFu, 0u, 0u);
+}
+__device__ inline void str1_encode_copy16(const uint8_t* p, int32_t len, uint32_t* dst) {
+  const uintptr_t ad = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(ad & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(ad & 3u) * 8u;
+  const int32_t nsrc = ((int32_t)(ad & 3u) + len + 3) >> 2;  // source dwords with string bytes
+  const int32_t nw = (len + 3) >> 2;                           // string words of the encoding
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  // word i of the encoding: 0 -> 1, 1 -> len, 2 + q -> string word q
+  auto sword = [&](int32_t q, const uint32_t* dd) -> uint32_t {  // dd: source dwords from q's
+    uint32_t w = sh ? (dd[0] >> sh) | (dd[1] << (32u - sh)) : dd[0];
+    const int32_t nb = len - 4 * q;
+    if (nb < 4) w &= (1u << (8 * nb)) - 1u;
+    return w;
+  };
+  for (int32_t c = 0; 4 * c < 2 + nw; c += 4) {  // 4 stores (16 words) per round of loads
+    uint32_t sd[17];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+      const int32_t j = 4 * c - 2 + k;  // source dword index (string word j needs dwords j, j+1)
+      sd[k] = j >= 0 && j < nsrc ? src[j] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int32_t i0 = 4 * (c + u);  // first encoding word of this store
+      if (i0 >= 2 + nw) break;
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int32_t i = i0 + e;
+        w[e] = i == 0 ? 1u : i == 1 ? (uint32_t)len : (i - 2 < nw ? sword(i - 2, sd + (i - 2 - (4 * c - 2))) : 0u);
+      }
+      d[c + u] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+#endif
+
 // (out of line: only long strings get here, so one copy instead of one per call site)
 __host__ __device__ __attribute__((noinline)) bool str1_rows_equal(const KeySet& ks, int64_t r1,
                                                                    int64_t r2) {
