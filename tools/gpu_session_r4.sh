@@ -25,8 +25,7 @@ timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1 &&
 DQ_FREQ_DEBUG=2 timeout -k 10 300 python -u tools/bench_workloads.py c5 --steps 1 --warmup 0 > $O/dbg_c5_$T.log 2>&1 &&
 timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 3 > $O/wl_c3_$T.json 2>&1 &&
-timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 5 > $O/wl_c4_$T.json 2>&1 &&
-DQ_CORR_K=4 timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 5 > $O/wl_c4k4_$T.json 2>&1
+timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 10 --warmup 3 > $O/wl_c4_$T.json 2>&1
 else
 timeout -k 10 300 python -u tools/bench_workloads.py c3 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c3_$T.json 2>&1 &&
 timeout -k 10 300 python -u tools/bench_workloads.py c4 --rows 100000000 --steps 2 --warmup 1 --gpus 2 --share-gpu > $O/dist_c4_$T.json 2>&1 &&
