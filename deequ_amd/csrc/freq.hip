@@ -2814,8 +2814,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
   __shared__ unsigned long long s_wun[2][NW], s_wmax[2][NW];
   __shared__ double s_went[2][NW];
   __shared__ double s_term[kSmallCounts];
-  __shared__ uint64_t s_fk[2][kCand], s_fc[2][kCand];  // the list's first groups
-  __shared__ unsigned long long s_top[kCand];
+  // each wave's top kCand groups of the item (count 0: none), merged by the next item's tail
+  __shared__ uint64_t s_wk[2][NW][kCand], s_wc[2][NW][kCand];
   __shared__ unsigned long long s_gbase;
   // an item's outputs, written during the next item: partition, first group slot, #groups, flags
   __shared__ uint32_t s_tp[2], s_tg[2], s_tfl[2];
@@ -2835,7 +2835,6 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
   }
   if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
   if (tid < kSmallCounts) s_term[tid] = tid ? entropy_term((uint64_t)tid, a.num_rows) : 0.0;
-  if (tid < kCand) s_top[tid] = 0;
   const bool keep = a.groups != nullptr;
 
   // Wave 0: the statistics and candidates of the item of parity q (its words stay untouched until
@@ -2845,9 +2844,23 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     if (!(fl & TF_VALID)) return;
     const uint32_t p = s_tp[q], gtot = s_tg[q];
     const bool sub = (fl & TF_SUB) != 0;
-    if ((fl & TF_CANDFAST) && lane < kCand)  // every count is 1: the list's first groups
-      a.cand[(uint64_t)p * kCand + lane] =
-          (uint32_t)lane < gtot ? Group{s_fk[q][lane], s_fc[q][lane], 0} : Group{0, 0, 0};
+    if (fl & TF_CANDFAST) {  // the item's top kCand: rounds of wave maxima over the waves' lists
+      static_assert(NW * kCand <= 64, "one wave merges the lists");
+      const bool in = lane < NW * kCand;
+      const int w = in ? lane / kCand : 0, r = lane % kCand;
+      const uint64_t c = in ? s_wc[q][w][r] : 0;
+      uint64_t mine = c ? (c << 8) | (uint64_t)(63 - lane) : 0ULL;  // ties: the lower lane
+#pragma unroll
+      for (int k = 0; k < kCand; ++k) {
+        const uint64_t wm = __ockl_wfred_max_u64(mine);
+        if (wm && wm == mine) {
+          a.cand[(uint64_t)p * kCand + k] = Group{s_wk[q][w][r], c, 0};
+          mine = 0;
+        } else if (!wm && lane == 0) {
+          a.cand[(uint64_t)p * kCand + k] = Group{0, 0, 0};
+        }
+      }
+    }
     const uint32_t hc = lane > 1 ? s_chist[q][lane] : 0u;
     double t = hc ? (double)hc * s_term[lane] : 0.0;
     t = __ockl_wfred_add_f64(t);
@@ -3004,7 +3017,6 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       s_tfl[par ^ 1u] = 0;
     }
     if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
-    if (tid < kCand) s_top[tid] = 0;
     const uint32_t gtot = n + (sc ? 1u : 0u);
     uint64_t gbase = 0;
     if (keep && sub && !overflow) {  // block-uniform
@@ -3029,10 +3041,6 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       else e += entropy_term(c, a.num_rows);
       mx = c > mx ? c : mx;
       if (cand) {
-        if (i < (uint32_t)kCand) {
-          s_fk[par][i] = k;
-          s_fc[par][i] = c;
-        }
         if (c == 1) {
           if (!k1c) k1 = k;
           k1c = true;
@@ -3094,6 +3102,37 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       }
     }
     if (tid == 0 && sc && !overflow) stat(n, kEmptyKey, sc);
+    if (cand) {  // the wave's top kCand: each lane offers its groups with count > 1 in count
+      // order, then its count-1 group; rounds of packed wave maxima, no block barrier
+      int taken = 0;
+#pragma unroll
+      for (int r = 0; r < kCand; ++r) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int i2 = 0; i2 < kCand; ++i2) c = i2 == taken ? tc[i2] : c;
+        const bool one = !c && k1c;
+        const uint64_t mine = c ? (c << 8) | ((uint64_t)lane << 2) | (uint64_t)taken
+                                : (one ? (1ULL << 8) | ((uint64_t)lane << 2) | 3ULL : 0ULL);
+        const uint64_t wm = __ockl_wfred_max_u64(mine);
+        if (wm && wm == mine) {
+          uint64_t kk = k1, cc = 1;
+          if (!one) {
+#pragma unroll
+            for (int i2 = 0; i2 < kCand; ++i2) {
+              kk = i2 == taken ? tk[i2] : kk;
+              cc = i2 == taken ? tc[i2] : cc;
+            }
+            ++taken;
+          } else {
+            k1c = false;
+          }
+          s_wk[par][wave][r] = kk;
+          s_wc[par][wave][r] = cc;
+        } else if (!wm && lane == 0) {
+          s_wc[par][wave][r] = 0;
+        }
+      }
+    }
     {
       const uint64_t wun = __ockl_wfred_add_u64(un);
       const double we = __ockl_wfred_add_f64(e);
@@ -3116,56 +3155,6 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
         a.ovf_out[q + 1] = FEntry{p, f + 1, fv | (1u << f), 0};
       }
     } else {
-      uint64_t M = 0;
-      if (cand) {
-#pragma unroll
-        for (int w = 0; w < NW; ++w) M = s_wmax[par][w] > M ? s_wmax[par][w] : M;
-      }
-      if (cand && M > 1) {
-        // exact top kCand: each lane offers its groups with count > 1 in count order, then its
-        // count-1 group; rounds of packed block maxima (count << 16 | tid << 2 | q)
-        int taken = 0;
-        auto pack = [&]() -> uint64_t {
-          uint64_t c = 0;
-#pragma unroll
-          for (int i = 0; i < kCand; ++i) c = i == taken ? tc[i] : c;
-          if (c) return (c << 16) | ((uint64_t)tid << 2) | (uint64_t)taken;
-          return k1c ? (1ULL << 16) | ((uint64_t)tid << 2) | 3ULL : 0ULL;
-        };
-        static_assert(kCThreads <= 1024 && kCand == 4, "candidate packing");
-#pragma unroll
-        for (int r = 0; r < kCand; ++r) {
-          const uint64_t mine = pack();
-          const uint64_t wm = __ockl_wfred_max_u64(mine);
-          if (lane == 0 && wm) atomicMax(&s_top[r], (unsigned long long)wm);
-          __syncthreads();
-          const uint64_t t = s_top[r];
-          if (t && t == mine) {  // this thread's offer won the round
-            const int q = (int)(t & 3u);
-            const bool one = (uint32_t)(t >> 16) == 1u && !(taken < kCand && tc[taken]);
-            uint64_t kk = 0, cc = 0;
-#pragma unroll
-            for (int i = 0; i < kCand; ++i) {
-              kk = i == q ? tk[i] : kk;
-              cc = i == q ? tc[i] : cc;
-            }
-            if (one) {
-              kk = k1;
-              cc = 1;
-              k1c = false;
-            } else {
-              ++taken;
-            }
-            // (written by the next item's tail: a global store here made the next item's wait
-            // for its prefetched records a wait for the store too)
-            s_fk[par][r] = kk;
-            s_fc[par][r] = cc;
-          } else if (!t && tid == 0) {  // no candidate left: an empty place
-            s_fk[par][r] = 0;
-            s_fc[par][r] = 0;
-          }
-        }
-      }
       if (tid == 0) {  // this item's outputs, for the next item's wave 0
         s_tp[par] = p;
         s_tg[par] = gtot;
@@ -3224,8 +3213,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
   __shared__ unsigned long long s_wun[2][NW], s_wmax[2][NW];
   __shared__ double s_went[2][NW];
   __shared__ double s_term[kSmallCounts];
-  __shared__ uint64_t s_fk[2][kCand], s_fc[2][kCand], s_fr[2][kCand];
-  __shared__ unsigned long long s_top[kCand];
+  // each wave's top kCand groups of the item (count 0: none), merged by the next item's tail
+  __shared__ uint64_t s_wk[2][NW][kCand], s_wc[2][NW][kCand], s_wr[2][NW][kCand];
   __shared__ uint32_t s_tp[2], s_tg[2], s_tfl[2];
   __shared__ uint64_t s_tr0[2];
   enum { TF_VALID = 1, TF_CANDFAST = 4 };
@@ -3243,17 +3232,29 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
   }
   if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
   if (tid < kSmallCounts) s_term[tid] = tid ? entropy_term((uint64_t)tid, a.num_rows) : 0.0;
-  if (tid < kCand) s_top[tid] = 0;
   const bool keep = a.groups != nullptr;
 
   auto tail = [&](uint32_t q) {  // wave 0: the outputs of the item of parity q
     const uint32_t fl = s_tfl[q];
     if (!(fl & TF_VALID)) return;
     const uint32_t p = s_tp[q], gtot = s_tg[q];
-    if ((fl & TF_CANDFAST) && lane < kCand)
-      a.cand[(uint64_t)p * kCand + lane] = (uint32_t)lane < gtot
-                                               ? Group{s_fk[q][lane], s_fc[q][lane], s_fr[q][lane]}
-                                               : Group{0, 0, 0};
+    if (fl & TF_CANDFAST) {  // the item's top kCand: rounds of wave maxima over the waves' lists
+      static_assert(NW * kCand <= 64, "one wave merges the lists");
+      const bool in = lane < NW * kCand;
+      const int w = in ? lane / kCand : 0, r = lane % kCand;
+      const uint64_t c = in ? s_wc[q][w][r] : 0;
+      uint64_t mine = c ? (c << 8) | (uint64_t)(63 - lane) : 0ULL;  // ties: the lower lane
+#pragma unroll
+      for (int k = 0; k < kCand; ++k) {
+        const uint64_t wm = __ockl_wfred_max_u64(mine);
+        if (wm && wm == mine) {
+          a.cand[(uint64_t)p * kCand + k] = Group{s_wk[q][w][r], c, s_wr[q][w][r]};
+          mine = 0;
+        } else if (!wm && lane == 0) {
+          a.cand[(uint64_t)p * kCand + k] = Group{0, 0, 0};
+        }
+      }
+    }
     const uint32_t hc = lane > 1 ? s_chist[q][lane] : 0u;
     double t = hc ? (double)hc * s_term[lane] : 0.0;
     t = __ockl_wfred_add_f64(t);
@@ -3445,7 +3446,6 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
       s_tfl[par ^ 1u] = 0;
     }
     if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
-    if (tid < kCand) s_top[tid] = 0;
     const uint32_t gtot = n;
     const uint64_t obase = r0;
 
@@ -3465,11 +3465,6 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
       else e += entropy_term(c, a.num_rows);
       mx = c > mx ? c : mx;
       if (cand) {
-        if (i < (uint32_t)kCand) {
-          s_fk[par][i] = k;
-          s_fc[par][i] = c;
-          s_fr[par][i] = r;
-        }
         if (c == 1) {
           if (!k1c) {
             k1 = k;
@@ -3527,6 +3522,39 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
         if (!overflow) stat(i, kk, vx & M24, vx >> 24);
       }
     }
+    if (cand) {  // the wave's top kCand: each lane offers its groups with count > 1 in count
+      // order, then its count-1 group; rounds of packed wave maxima, no block barrier
+      int taken = 0;
+#pragma unroll
+      for (int r = 0; r < kCand; ++r) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int i2 = 0; i2 < kCand; ++i2) c = i2 == taken ? tc[i2] : c;
+        const bool one = !c && k1c;
+        const uint64_t mine = c ? (c << 8) | ((uint64_t)lane << 2) | (uint64_t)taken
+                                : (one ? (1ULL << 8) | ((uint64_t)lane << 2) | 3ULL : 0ULL);
+        const uint64_t wm = __ockl_wfred_max_u64(mine);
+        if (wm && wm == mine) {
+          uint64_t kk = k1, cc = 1, rr = r1;
+          if (!one) {
+#pragma unroll
+            for (int i2 = 0; i2 < kCand; ++i2) {
+              kk = i2 == taken ? tk[i2] : kk;
+              cc = i2 == taken ? tc[i2] : cc;
+              rr = i2 == taken ? tr[i2] : rr;
+            }
+            ++taken;
+          } else {
+            k1c = false;
+          }
+          s_wk[par][wave][r] = kk;
+          s_wc[par][wave][r] = cc;
+          s_wr[par][wave][r] = rr;
+        } else if (!wm && lane == 0) {
+          s_wc[par][wave][r] = 0;
+        }
+      }
+    }
     {
       const uint64_t wun = __ockl_wfred_add_u64(un);
       const double we = __ockl_wfred_add_f64(e);
@@ -3545,56 +3573,6 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
         a.ovf_out[q] = FEntry{p, 0, 0, 0};
       }
     } else {
-      uint64_t M = 0;
-      if (cand) {
-#pragma unroll
-        for (int w = 0; w < NW; ++w) M = s_wmax[par][w] > M ? s_wmax[par][w] : M;
-      }
-      if (cand && M > 1) {
-        int taken = 0;
-        auto pack = [&]() -> uint64_t {
-          uint64_t c = 0;
-#pragma unroll
-          for (int i = 0; i < kCand; ++i) c = i == taken ? tc[i] : c;
-          if (c) return (c << 16) | ((uint64_t)tid << 2) | (uint64_t)taken;
-          return k1c ? (1ULL << 16) | ((uint64_t)tid << 2) | 3ULL : 0ULL;
-        };
-        static_assert(kCThreads <= 1024 && kCand == 4, "candidate packing");
-#pragma unroll
-        for (int r = 0; r < kCand; ++r) {
-          const uint64_t mine = pack();
-          const uint64_t wm = __ockl_wfred_max_u64(mine);
-          if (lane == 0 && wm) atomicMax(&s_top[r], (unsigned long long)wm);
-          __syncthreads();
-          const uint64_t t = s_top[r];
-          if (t && t == mine) {
-            const int q = (int)(t & 3u);
-            const bool one = (uint32_t)(t >> 16) == 1u && !(taken < kCand && tc[taken]);
-            uint64_t kk = 0, cc = 0, rr = 0;
-#pragma unroll
-            for (int i = 0; i < kCand; ++i) {
-              kk = i == q ? tk[i] : kk;
-              cc = i == q ? tc[i] : cc;
-              rr = i == q ? tr[i] : rr;
-            }
-            if (one) {
-              kk = k1;
-              cc = 1;
-              rr = r1;
-              k1c = false;
-            } else {
-              ++taken;
-            }
-            s_fk[par][r] = kk;  // (written by the next item's tail, as in freq_phaseC_x)
-            s_fc[par][r] = cc;
-            s_fr[par][r] = rr;
-          } else if (!t && tid == 0) {  // no candidate left: an empty place
-            s_fk[par][r] = 0;
-            s_fc[par][r] = 0;
-            s_fr[par][r] = 0;
-          }
-        }
-      }
       if (tid == 0) {
         s_tp[par] = p;
         s_tg[par] = gtot;
