@@ -4,6 +4,8 @@
 // Analyzer.scala:385-408; Compliance.scala:37-53).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "device_util.h"
 #include "kernels.h"
 #include "jfmt.h"
@@ -342,12 +344,12 @@ __device__ __forceinline__ uint4 ldg128_unaligned(const uint8_t* p) {
 }
 
 struct RxRow {
-  int64_t pos, end;  // byte range left to walk in the data buffer
+  int32_t pos, end;  // byte range left to walk in the data buffer (Arrow utf8: int32 offsets)
   uint32_t q;
   DQ_DEV bool active(const uint8_t* fin) const { return pos < end && !(fin[q] & 2u); }
   // the next (at most) 16 bytes of the row
-  DQ_DEV void chunk(const uint8_t* data, int64_t data_len, uint32_t (&w)[4]) const {
-    if (pos + 16 <= data_len) {
+  DQ_DEV void chunk(const uint8_t* data, int32_t data_len, uint32_t (&w)[4]) const {
+    if ((int64_t)pos + 16 <= (int64_t)data_len) {
       const uint4 u = ldg128_unaligned(data + pos);
       w[0] = u.x;
       w[1] = u.y;
@@ -356,12 +358,14 @@ struct RxRow {
     } else {  // the buffer's last bytes: no read past its end
 #pragma unroll
       for (int k = 0; k < 4; ++k) w[k] = 0;
-      for (int j = 0; j < 16 && pos + j < end; ++j) w[j >> 2] |= (uint32_t)data[pos + j] << (8 * (j & 3));
+      for (int j = 0; j < 16 && j < end - pos; ++j) w[j >> 2] |= (uint32_t)data[pos + j] << (8 * (j & 3));
     }
   }
 };
 
-__global__ void __launch_bounds__(kBlock)
+// HR: rows per lane (independent chains of dependent LDS reads in flight)
+template <int HR>
+__global__ void __launch_bounds__(kBlock, HR == 4 ? 4 : 1)
 regex_find_kernel(const uint8_t* __restrict__ valid, const int32_t* __restrict__ off,
                   const uint8_t* __restrict__ data, int64_t rows, const uint8_t* __restrict__ table,
                   int32_t ns, int32_t start, int32_t null_mode, uint64_t* __restrict__ out_val,
@@ -376,39 +380,45 @@ regex_find_kernel(const uint8_t* __restrict__ valid, const int32_t* __restrict__
   const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
   const int64_t n_waves = ((int64_t)gridDim.x * kBlock) >> 6;
   const int64_t n_words = (rows + 63) >> 6;
-  const int64_t data_len = rows ? (int64_t)off[rows] : 0;
-  for (int64_t w = 2 * wave; w < n_words; w += 2 * n_waves) {
-    RxRow rr[2];
-    bool vld[2];
+  const int32_t data_len = rows ? off[rows] : 0;
+  for (int64_t w = HR * wave; w < n_words; w += HR * n_waves) {
+    RxRow rr[HR];
+    bool vld[HR];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < HR; ++h) {
       const int64_t r = (w + h) * 64 + lane;
       vld[h] = r < rows && bit1(valid, r);
       rr[h].q = (uint32_t)start;
       rr[h].pos = vld[h] ? off[r] : 0;
       rr[h].end = vld[h] ? off[r + 1] : 0;
     }
-    while (__ballot(rr[0].active(fin) || rr[1].active(fin))) {
-      uint32_t c[2][4];
+    auto any_active = [&]() {
+      bool x = false;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < HR; ++h) x = x || rr[h].active(fin);
+      return x;
+    };
+    while (__ballot(any_active())) {
+      uint32_t c[HR][4];
+#pragma unroll
+      for (int h = 0; h < HR; ++h) {
         if (rr[h].active(fin)) rr[h].chunk(data, data_len, c[h]);
         else c[h][0] = c[h][1] = c[h][2] = c[h][3] = 0;
       }
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < HR; ++h) {
           const uint32_t b = (c[h][j >> 2] >> (8 * (j & 3))) & 0xffu;
           const uint32_t nq = T[rr[h].q * 256u + b];
-          rr[h].q = rr[h].pos + j < rr[h].end ? nq : rr[h].q;
+          rr[h].q = j < rr[h].end - rr[h].pos ? nq : rr[h].q;
         }
       }
 #pragma unroll
-      for (int h = 0; h < 2; ++h) rr[h].pos = rr[h].pos + 16 < rr[h].end ? rr[h].pos + 16 : rr[h].end;
+      for (int h = 0; h < HR; ++h) rr[h].pos = rr[h].end - rr[h].pos > 16 ? rr[h].pos + 16 : rr[h].end;
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < HR; ++h) {
       // NULL: null_mode 1 (PatternMatch's otherwise(0)) -> FALSE, else NULL
       const bool res_valid = (w + h) * 64 + lane < rows && (vld[h] || null_mode);
       const bool truth = vld[h] && (fin[rr[h].q] & 1u);
@@ -440,12 +450,20 @@ hipError_t launch_regex(const uint8_t* valid, const int32_t* offsets, const uint
                         uint64_t* out_val, uint64_t* out_vld, hipStream_t stream) {
   if (rows <= 0) return hipSuccess;
   if (ns < 1 || ns > kRegexMaxStates) return hipErrorInvalidValue;
-  const int64_t pairs = ((rows + 63) / 64 + 1) / 2;
-  int64_t blocks = (pairs + 3) / 4;
+  static const int hr = [] {  // DQ_RX_ROWS=2: A/B hook, two rows per lane
+    const char* e = getenv("DQ_RX_ROWS");
+    return e && atoi(e) == 2 ? 2 : 4;
+  }();
+  const int64_t groups = ((rows + 63) / 64 + hr - 1) / hr;
+  int64_t blocks = (groups + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   const size_t lds = ((size_t)ns * 257 + 15) / 16 * 16;
-  hipLaunchKernelGGL(regex_find_kernel, dim3((unsigned)blocks), dim3(kBlock), lds, stream, valid,
-                     offsets, data, rows, table, ns, start, null_mode, out_val, out_vld);
+  if (hr == 2)
+    hipLaunchKernelGGL(regex_find_kernel<2>, dim3((unsigned)blocks), dim3(kBlock), lds, stream, valid,
+                       offsets, data, rows, table, ns, start, null_mode, out_val, out_vld);
+  else
+    hipLaunchKernelGGL(regex_find_kernel<4>, dim3((unsigned)blocks), dim3(kBlock), lds, stream, valid,
+                       offsets, data, rows, table, ns, start, null_mode, out_val, out_vld);
   return hipGetLastError();
 }
 
