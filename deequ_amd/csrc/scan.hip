@@ -889,14 +889,15 @@ DQ_DEV void hll_str_rows_staged(const TaskDesc& t, int64_t r_begin, int64_t r_en
     }
     const int32_t o = (int32_t)((int64_t)s - base);  // the string's LDS byte offset
     const uint32_t sh = (uint32_t)o & 3u;
-    const int nd = ok && len > 0 ? (int)((sh + (uint32_t)len + 3) >> 2) : 0;  // <= 13
+    const int nd = ok && len > 0 && len <= 64 ? (int)((sh + (uint32_t)len + 3) >> 2) : 0;  // <= 17
     uint32_t dw[17];
 #pragma unroll
     for (int k = 0; k < 17; ++k) dw[k] = k < nd ? sd[(o >> 2) + k] : 0u;
     uint32_t w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(dw[j + 1], dw[j], sh);
-    if (ok) hll_update(regs, xxh_bytes_regs64(w, len, 42));
+    if (ok && len <= 64) hll_update(regs, xxh_bytes_regs64(w, len, 42));
+    if (ok && len > 64) hll_update(regs, xxh_bytes(UBytes{t.data + s}, (int64_t)len, 42));
     __builtin_amdgcn_wave_barrier();  // the stage is reused by the next step
   }
 }
