@@ -2820,7 +2820,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
   // an item's outputs, written during the next item: partition, first group slot, #groups, flags
   __shared__ uint32_t s_tp[2], s_tg[2], s_tfl[2];
   __shared__ uint64_t s_tr0[2];
-  enum { TF_VALID = 1, TF_SUB = 2, TF_CANDFAST = 4 };
+  enum { TF_VALID = 1, TF_SUB = 2, TF_CANDFAST = 4, TF_CANDONE = 8 };
 
   const int tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
   for (int i = tid; i < KT; i += kCThreads) {
@@ -2849,15 +2849,24 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       const bool in = lane < NW * kCand;
       const int w = in ? lane / kCand : 0, r = lane % kCand;
       const uint64_t c = in ? s_wc[q][w][r] : 0;
-      uint64_t mine = c ? (c << 8) | (uint64_t)(63 - lane) : 0ULL;  // ties: the lower lane
+      if (fl & TF_CANDONE) {  // every count is 1: the first kCand candidates
+        const uint64_t bal = __ballot(c != 0);
+        const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ULL << lane) - 1ULL));
+        if (c && rank < (uint32_t)kCand)
+          a.cand[(uint64_t)p * kCand + rank] = Group{s_wk[q][w][r], c, 0};
+        if (lane < kCand && (uint32_t)lane >= (uint32_t)__builtin_popcountll(bal))
+          a.cand[(uint64_t)p * kCand + lane] = Group{0, 0, 0};
+      } else {
+        uint64_t mine = c ? (c << 8) | (uint64_t)(63 - lane) : 0ULL;  // ties: the lower lane
 #pragma unroll
-      for (int k = 0; k < kCand; ++k) {
-        const uint64_t wm = __ockl_wfred_max_u64(mine);
-        if (wm && wm == mine) {
-          a.cand[(uint64_t)p * kCand + k] = Group{s_wk[q][w][r], c, 0};
-          mine = 0;
-        } else if (!wm && lane == 0) {
-          a.cand[(uint64_t)p * kCand + k] = Group{0, 0, 0};
+        for (int k = 0; k < kCand; ++k) {
+          const uint64_t wm = __ockl_wfred_max_u64(mine);
+          if (wm && wm == mine) {
+            a.cand[(uint64_t)p * kCand + k] = Group{s_wk[q][w][r], c, 0};
+            mine = 0;
+          } else if (!wm && lane == 0) {
+            a.cand[(uint64_t)p * kCand + k] = Group{0, 0, 0};
+          }
         }
       }
     }
@@ -3102,7 +3111,16 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       }
     }
     if (tid == 0 && sc && !overflow) stat(n, kEmptyKey, sc);
-    if (cand) {  // the wave's top kCand: each lane offers its groups with count > 1 in count
+    const uint64_t wmx1 = __ockl_wfred_max_u64(mx);
+    if (cand && wmx1 <= 1) {  // every count of the wave is 1: its first four count-1 groups
+      const uint64_t bal = __ballot(k1c);
+      const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ULL << lane) - 1ULL));
+      if (k1c && rank < (uint32_t)kCand) {
+        s_wk[par][wave][rank] = k1;
+        s_wc[par][wave][rank] = 1;
+      }
+      if (lane < kCand && (uint32_t)lane >= (uint32_t)__builtin_popcountll(bal)) s_wc[par][wave][lane] = 0;
+    } else if (cand) {  // the wave's top kCand: each lane offers its groups with count > 1 in count
       // order, then its count-1 group; rounds of packed wave maxima, no block barrier
       int taken = 0;
 #pragma unroll
@@ -3136,7 +3154,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     {
       const uint64_t wun = __ockl_wfred_add_u64(un);
       const double we = __ockl_wfred_add_f64(e);
-      const uint64_t wmx = __ockl_wfred_max_u64(mx);
+      const uint64_t wmx = wmx1;
       if (lane == 0) {
         s_wun[par][wave] = wun;
         s_went[par][wave] = we;
@@ -3159,7 +3177,11 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
         s_tp[par] = p;
         s_tg[par] = gtot;
         s_tr0[par] = r0;
-        s_tfl[par] = TF_VALID | (sub ? TF_SUB : 0u) | (cand ? TF_CANDFAST : 0u);
+        uint64_t M = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) M = s_wmax[par][w] > M ? s_wmax[par][w] : M;
+        s_tfl[par] = TF_VALID | (sub ? TF_SUB : 0u) | (cand ? TF_CANDFAST : 0u) |
+                     (cand && M <= 1 ? TF_CANDONE : 0u);
       }
     }
     mark(3);
@@ -3217,7 +3239,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
   __shared__ uint64_t s_wk[2][NW][kCand], s_wc[2][NW][kCand], s_wr[2][NW][kCand];
   __shared__ uint32_t s_tp[2], s_tg[2], s_tfl[2];
   __shared__ uint64_t s_tr0[2];
-  enum { TF_VALID = 1, TF_CANDFAST = 4 };
+  enum { TF_VALID = 1, TF_CANDFAST = 4, TF_CANDONE = 8 };
 
   const int tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
   unsigned long long collisions = 0;
@@ -3243,15 +3265,24 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
       const bool in = lane < NW * kCand;
       const int w = in ? lane / kCand : 0, r = lane % kCand;
       const uint64_t c = in ? s_wc[q][w][r] : 0;
-      uint64_t mine = c ? (c << 8) | (uint64_t)(63 - lane) : 0ULL;  // ties: the lower lane
+      if (fl & TF_CANDONE) {  // every count is 1: the first kCand candidates
+        const uint64_t bal = __ballot(c != 0);
+        const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ULL << lane) - 1ULL));
+        if (c && rank < (uint32_t)kCand)
+          a.cand[(uint64_t)p * kCand + rank] = Group{s_wk[q][w][r], c, s_wr[q][w][r]};
+        if (lane < kCand && (uint32_t)lane >= (uint32_t)__builtin_popcountll(bal))
+          a.cand[(uint64_t)p * kCand + lane] = Group{0, 0, 0};
+      } else {
+        uint64_t mine = c ? (c << 8) | (uint64_t)(63 - lane) : 0ULL;  // ties: the lower lane
 #pragma unroll
-      for (int k = 0; k < kCand; ++k) {
-        const uint64_t wm = __ockl_wfred_max_u64(mine);
-        if (wm && wm == mine) {
-          a.cand[(uint64_t)p * kCand + k] = Group{s_wk[q][w][r], c, s_wr[q][w][r]};
-          mine = 0;
-        } else if (!wm && lane == 0) {
-          a.cand[(uint64_t)p * kCand + k] = Group{0, 0, 0};
+        for (int k = 0; k < kCand; ++k) {
+          const uint64_t wm = __ockl_wfred_max_u64(mine);
+          if (wm && wm == mine) {
+            a.cand[(uint64_t)p * kCand + k] = Group{s_wk[q][w][r], c, s_wr[q][w][r]};
+            mine = 0;
+          } else if (!wm && lane == 0) {
+            a.cand[(uint64_t)p * kCand + k] = Group{0, 0, 0};
+          }
         }
       }
     }
@@ -3522,7 +3553,17 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
         if (!overflow) stat(i, kk, vx & M24, vx >> 24);
       }
     }
-    if (cand) {  // the wave's top kCand: each lane offers its groups with count > 1 in count
+    const uint64_t wmx1 = __ockl_wfred_max_u64(mx);
+    if (cand && wmx1 <= 1) {  // every count of the wave is 1: its first four count-1 groups
+      const uint64_t bal = __ballot(k1c);
+      const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ULL << lane) - 1ULL));
+      if (k1c && rank < (uint32_t)kCand) {
+        s_wk[par][wave][rank] = k1;
+        s_wc[par][wave][rank] = 1;
+        s_wr[par][wave][rank] = r1;
+      }
+      if (lane < kCand && (uint32_t)lane >= (uint32_t)__builtin_popcountll(bal)) s_wc[par][wave][lane] = 0;
+    } else if (cand) {  // the wave's top kCand: each lane offers its groups with count > 1 in count
       // order, then its count-1 group; rounds of packed wave maxima, no block barrier
       int taken = 0;
 #pragma unroll
@@ -3558,7 +3599,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
     {
       const uint64_t wun = __ockl_wfred_add_u64(un);
       const double we = __ockl_wfred_add_f64(e);
-      const uint64_t wmx = __ockl_wfred_max_u64(mx);
+      const uint64_t wmx = wmx1;
       if (lane == 0) {
         s_wun[par][wave] = wun;
         s_went[par][wave] = we;
@@ -3577,7 +3618,10 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
         s_tp[par] = p;
         s_tg[par] = gtot;
         s_tr0[par] = r0;
-        s_tfl[par] = TF_VALID | (cand ? TF_CANDFAST : 0u);
+        uint64_t M = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) M = s_wmax[par][w] > M ? s_wmax[par][w] : M;
+        s_tfl[par] = TF_VALID | (cand ? TF_CANDFAST : 0u) | (cand && M <= 1 ? TF_CANDONE : 0u);
       }
     }
     mark(3);

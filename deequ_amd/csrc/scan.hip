@@ -843,70 +843,9 @@ DQ_DEV void hll_str_rows(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint
   }
 }
 
-// The bytes of a wave's 64 consecutive strings, staged in LDS: the aligned 16-byte blocks that
-// hold [data + lo, data + hi) -- each holds a byte of the buffer, so none leaves its page -- read
-// with coalesced 16-byte loads (lane l takes blocks l, l + 64, ...).  A per-lane gather of a
-// string's dwords touches ~20 cache lines per wave instruction and bounded the string bodies by
-// the texture address path; here a wave instruction reads 1 KiB of consecutive bytes.  Returns
-// the LDS byte offset of data + lo's block, or -1 when the bytes exceed CAP (nothing staged).
-constexpr int kStageBytes = 3072;  // per wave: 64 strings of <= 48 bytes
-DQ_DEV int64_t wave_stage(const uint8_t* data, int32_t lo, int32_t hi, uint4* lds) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(data + lo) & ~(uintptr_t)15;
-  const uintptr_t b = (reinterpret_cast<uintptr_t>(data + hi) + 15) & ~(uintptr_t)15;
-  const int n16 = (int)((b - a) >> 4);
-  if (hi <= lo || n16 * 16 > kStageBytes) return -1;
-  const uint4* src = reinterpret_cast<const uint4*>(a);
-  for (int k = lane_id(); k < n16; k += 64) lds[k] = src[k];  // (wave-local: no barrier needed)
-  __builtin_amdgcn_wave_barrier();
-  return (int64_t)(a - reinterpret_cast<uintptr_t>(data));   // = the block's offset from data
-}
-
-// hll_str_rows with the wave's strings staged in LDS (wave_stage), falling back per step.
-DQ_DEV void hll_str_rows_staged(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint32_t* regs,
-                                uint4* stage) {
-  const int l = lane_id();
-  const int32_t* off = reinterpret_cast<const int32_t*>(t.values);
-  const uint32_t* sd = reinterpret_cast<const uint32_t*>(stage);
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += 64) {
-    const int64_t r = r0 + l;
-    uint32_t ok = 0;
-    int32_t s = 0, e = 0;
-    const int64_t rl = min(r, r_end - 1);
-    s = off[rl];
-    e = off[rl + 1];
-    if (r < r_end) {
-      ok = bit1(t.valid, r);
-      if (t.w_val) ok &= bit1(t.w_val, r) & bit1(t.w_vld, r);
-    }
-    if (r >= r_end) e = s;
-    const int32_t lo = off[r0], hi = off[min(r0 + 64, r_end)];  // (wave-uniform)
-    const int64_t base = wave_stage(t.data, lo, hi, stage);
-    const int32_t len = e - s;
-    if (base < 0) {  // (wave-uniform) too many bytes: the per-lane path for this step
-      if (ok) hll_update(regs, xxh_bytes(UBytes{t.data + s}, (int64_t)len, 42));
-      __builtin_amdgcn_wave_barrier();
-      continue;
-    }
-    const int32_t o = (int32_t)((int64_t)s - base);  // the string's LDS byte offset
-    const uint32_t sh = (uint32_t)o & 3u;
-    const int nd = ok && len > 0 && len <= 64 ? (int)((sh + (uint32_t)len + 3) >> 2) : 0;  // <= 17
-    uint32_t dw[17];
-#pragma unroll
-    for (int k = 0; k < 17; ++k) dw[k] = k < nd ? sd[(o >> 2) + k] : 0u;
-    uint32_t w[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(dw[j + 1], dw[j], sh);
-    if (ok && len <= 64) hll_update(regs, xxh_bytes_regs64(w, len, 42));
-    if (ok && len > 64) hll_update(regs, xxh_bytes(UBytes{t.data + s}, (int64_t)len, 42));
-    __builtin_amdgcn_wave_barrier();  // the stage is reused by the next step
-  }
-}
-
-DQ_DEV void hll_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint32_t* regs,
-                     uint4* stage = nullptr) {
+DQ_DEV void hll_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, uint32_t* regs) {
   if (t.type == DQ_UTF8) {
-    if (stage) hll_str_rows_staged(t, r_begin, r_end, regs, stage);
-    else hll_str_rows(t, r_begin, r_end, regs);
+    hll_str_rows(t, r_begin, r_end, regs);
     return;
   }
   const int l = lane_id();
@@ -1017,8 +956,6 @@ __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? (K == 8 ? 4 : 5) 
                                                       Acc* __restrict__ partial,
                                                       uint32_t* __restrict__ hll_stage, int n_hll) {
   extern __shared__ uint32_t hll_lds[];
-  // BC_HLL: each wave's string bytes (wave_stage)
-  __shared__ uint4 s_stage[BC == BC_HLL ? kBlock / 64 : 1][BC == BC_HLL ? kStageBytes / 16 : 1];
   constexpr bool kRegs = BC == BC_HLL || BC == BC_CORR_HLL;  // HLL registers in LDS
   if constexpr (kRegs) {
     for (int i = threadIdx.x; i < n_hll * kHllM; i += kBlock) hll_lds[i] = 0;
@@ -1053,7 +990,7 @@ __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? (K == 8 ? 4 : 5) 
     if constexpr (BC == BC_CORR) corr_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_CORR_HLL) corr_rows<true, K>(t, r_begin, r_end, a, hll_lds + t.hll_out * kHllM);
     if constexpr (BC == BC_HLL) {
-      hll_item(t, r_begin, r_end, hll_lds + t.hll_out * kHllM, s_stage[threadIdx.x >> 6]);
+      hll_item(t, r_begin, r_end, hll_lds + t.hll_out * kHllM);
     } else {
       constexpr int kind = BC <= BC_NUM_F64 ? TK_NUMERIC
                            : BC == BC_BITS  ? TK_VALIDITY
