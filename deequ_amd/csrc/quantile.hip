@@ -108,6 +108,80 @@ quantile_gather(int type, const uint8_t* __restrict__ valid, const void* __restr
   }
 }
 
+// The first radix pass, fused into the read of the columns: a histogram of the ordered keys' top
+// kQ0Bits bits (no key is written; the keys of the bins that hold a rank are gathered afterwards by
+// quantile_compact0, so the column is read twice and only those keys are written).
+constexpr int kQ0Bits = 13;
+constexpr int kQ0Bins = 1 << kQ0Bits;
+
+__global__ void __launch_bounds__(256)
+quantile_hist0(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
+               int64_t rows, uint32_t* __restrict__ partial) {
+  __shared__ uint32_t s_hist[kQ0Bins];
+  for (int i = threadIdx.x; i < kQ0Bins; i += 256) s_hist[i] = 0;
+  __syncthreads();
+  constexpr int kU = 8;  // rows per thread per step, all loads in flight before the first count
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 * kU; i0 < rows; i0 += (int64_t)gridDim.x * 256 * kU) {
+    uint64_t k[kU];
+    bool ok[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t r = i0 + (int64_t)u * 256 + threadIdx.x;
+      ok[u] = r < rows && bit1(valid, r);
+      double d = ok[u] ? load_f64(type, values, r) : 0.0;
+      if (d != d) d = __builtin_nan("");
+      k[u] = ordered_key(d);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (ok[u]) atomicAdd(&s_hist[k[u] >> (64 - kQ0Bits)], 1u);
+  }
+  __syncthreads();
+  // the block's counts as one coalesced row of partials (a global atomic per bin and block was
+  // millions of atomics on 8192 addresses)
+  uint32_t* row = partial + (size_t)blockIdx.x * kQ0Bins;
+  for (int i = threadIdx.x; i < kQ0Bins; i += 256) row[i] = s_hist[i];
+}
+
+// hist[bin] += the blocks' partial counts of the bin (one thread per bin, rows read coalesced)
+__global__ void __launch_bounds__(256)
+quantile_hist0_sum(const uint32_t* __restrict__ partial, int blocks, unsigned long long* __restrict__ hist) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= kQ0Bins) return;
+  unsigned long long t = 0;
+  for (int b = 0; b < blocks; ++b) t += partial[(size_t)b * kQ0Bins + i];
+  hist[i] += t;
+}
+
+// The non-NULL values of one batch whose key's top kQ0Bits bits are a bin set in `bins` (a
+// kQ0Bins-bit mask) -> ordered keys at out[*cursor ...] (order irrelevant).
+__global__ void __launch_bounds__(kGatherThreads)
+quantile_compact0(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
+                  int64_t rows, const uint32_t* __restrict__ bins, uint64_t* __restrict__ out,
+                  unsigned long long* __restrict__ cursor) {
+  __shared__ uint32_t s_bins[kQ0Bins / 32];
+  __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
+  __shared__ unsigned long long s_base;
+  for (int i = threadIdx.x; i < kQ0Bins / 32; i += kGatherThreads) s_bins[i] = bins[i];
+  __syncthreads();
+  StepPlacer pl{s_cnt, &s_base};
+  for (int64_t r0 = (int64_t)blockIdx.x * kGatherStep; r0 < rows; r0 += (int64_t)gridDim.x * kGatherStep) {
+    bool keep[kGatherRounds];
+    uint64_t v[kGatherRounds];
+#pragma unroll
+    for (int i = 0; i < kGatherRounds; ++i) {
+      const int64_t r = r0 + (int64_t)i * kGatherThreads + threadIdx.x;
+      const bool ok = r < rows && bit1(valid, r);
+      double d = ok ? load_f64(type, values, r) : 0.0;
+      if (d != d) d = __builtin_nan("");
+      v[i] = ordered_key(d);
+      const uint32_t b = (uint32_t)(v[i] >> (64 - kQ0Bits));
+      keep[i] = ok && ((s_bins[b >> 5] >> (b & 31)) & 1u);
+    }
+    pl.place(keep, v, out, cursor);
+  }
+}
+
 // ---- radix select -----------------------------------------------------------------------------
 // A pass counts the keys whose top `bits` bits equal one of the A active prefixes (sorted, unique)
 // by their next D bits: hist[a << D | digit], A << D <= kSelBins, privatised in LDS per block.
@@ -232,20 +306,21 @@ hipError_t sort_keys(const uint64_t* in, uint64_t* out, size_t n, DevBuf<uint8_t
 // The values at the exact ranks rank[0..m) (ascending) of the n keys at `keys`, into out_dev[m]
 // (doubles).  Histogram passes narrow every rank to a bin of the keys' top bits; once the bins
 // that hold a rank hold few keys (or every bit is decided) those keys are compacted and sorted.
-dq_status radix_select(uint64_t* keys, int64_t n, const std::vector<int64_t>& rank, double* out_dev,
-                       hipStream_t stream) {
-  const int m = (int)rank.size();
+struct Target {
+  uint64_t prefix;  // the top `bits` bits of the target's key
+  int64_t q;        // rank among the keys with this prefix
+};
+
+// `keys` (n of them) are exactly the keys whose top `bits0` bits are one of the targets' prefixes
+// (every key when bits0 = 0).
+dq_status radix_select(const uint64_t* keys, int64_t n, std::vector<Target> tg, int bits0,
+                       double* out_dev, hipStream_t stream) {
+  const int m = (int)tg.size();
   // keys sorted at the end: always when this few; and up to kStallBudget when a pass stopped
   // narrowing (a bin of one repeated value -- integers of a narrow range -- never shrinks: more
   // passes over it only spend bits)
   constexpr int64_t kSortBudget = 1 << 24, kStallBudget = 1 << 26;
   int64_t T_prev = n;
-  struct Target {
-    uint64_t prefix;
-    int64_t q;  // rank among the keys with this prefix
-  };
-  std::vector<Target> tg(m);
-  for (int j = 0; j < m; ++j) tg[j] = Target{0, rank[j]};
   DevBuf<uint64_t> buf[2], act;
   DevBuf<unsigned long long> hist;
   DevBuf<unsigned long long> cur;
@@ -255,7 +330,7 @@ dq_status radix_select(uint64_t* keys, int64_t n, const std::vector<int64_t>& ra
   const uint64_t* src = keys;
   int64_t M = n;
   int which = 0;
-  int bits = 0;
+  int bits = bits0;
   std::vector<uint64_t> prefixes, sp;  // (alive until the copies from them have run)
   std::vector<unsigned long long> h;
   while (true) {
@@ -383,43 +458,57 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   // through the engine's device cache (dev_alloc): reused across columns, released on OOM
   DevBuf<uint64_t> keys, sorted;
   DevBuf<double> picks;
-  DevBuf<unsigned long long> cur;
+  DevBuf<unsigned long long> cur, hist;
+  DevBuf<uint32_t> partial, mask;
   DevBuf<uint8_t> tmp;
-  HIP_TRY(keys.ensure((size_t)rows));
-  HIP_TRY(cur.ensure(1));
-  HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
+  // pass 1: the count and the keys' top-kQ0Bits histogram, straight from the columns
+  constexpr int kHistBlocks = 512;
+  HIP_TRY(hist.ensure(kQ0Bins));
+  HIP_TRY(partial.ensure((size_t)kHistBlocks * kQ0Bins));
+  HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)kQ0Bins * 8, stream));
   for (int b = 0; b < n_batches; ++b) {
     const dq_column& c = batches[b];
     if (!c.length) continue;
-    hipLaunchKernelGGL(quantile_gather, dim3(grid_of(c.length, kGatherStep, 2048)),
-                       dim3(kGatherThreads), 0, stream, c.type, c.validity, c.values, c.length,
-                       keys.p, cur.p);
+    const unsigned g = grid_of(c.length, 256 * 8 * 4, kHistBlocks);
+    hipLaunchKernelGGL(quantile_hist0, dim3(g), dim3(256), 0, stream, c.type, c.validity, c.values,
+                       c.length, partial.p);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(quantile_hist0_sum, dim3(kQ0Bins / 256), dim3(256), 0, stream, partial.p, (int)g,
+                       hist.p);
     HIP_TRY(hipGetLastError());
   }
-  unsigned long long count = 0;
-  HIP_TRY(hipMemcpyAsync(&count, cur.p, 8, hipMemcpyDeviceToHost, stream));
+  std::vector<unsigned long long> h0(kQ0Bins);
+  HIP_TRY(hipMemcpyAsync(h0.data(), hist.p, (size_t)kQ0Bins * 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
+  unsigned long long count = 0;
+  for (unsigned long long x : h0) count += x;
   *count_out = (int64_t)count;
   if (!count) return DQ_OK;
   const int64_t n = (int64_t)count <= std::max(head_values, max_values) ? (int64_t)count : max_values;
   *n_out = n;
   if (!out) return DQ_OK;  // size query only
   HIP_TRY(picks.ensure((size_t)n));
-  if (n == (int64_t)count) {  // every value, sorted
+  HIP_TRY(cur.ensure(1));
+  HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
+  if (n == (int64_t)count || n > kSelMaxTargets) {  // every key, gathered and sorted
+    HIP_TRY(keys.ensure((size_t)count));
+    for (int b = 0; b < n_batches; ++b) {
+      const dq_column& c = batches[b];
+      if (!c.length) continue;
+      hipLaunchKernelGGL(quantile_gather, dim3(grid_of(c.length, kGatherStep, 2048)),
+                         dim3(kGatherThreads), 0, stream, c.type, c.validity, c.values, c.length,
+                         keys.p, cur.p);
+      HIP_TRY(hipGetLastError());
+    }
     HIP_TRY(sorted.ensure((size_t)count));
     HIP_TRY(sort_keys(keys.p, sorted.p, (size_t)count, tmp, stream));
-    hipLaunchKernelGGL(keys_to_doubles, dim3(grid_of(n, 256 * 16, 4096)), dim3(256), 0, stream,
-                       sorted.p, n, picks.p);
-    HIP_TRY(hipGetLastError());
-  } else {  // the values at the ranks floor(j (count - 1) / (n - 1))
-    std::vector<int64_t> rank(n);
-    for (int64_t j = 0; j < n; ++j) rank[j] = (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1));
-    if (n <= kSelMaxTargets) {
-      const dq_status st = radix_select(keys.p, (int64_t)count, rank, picks.p, stream);
-      if (st != DQ_OK) return st;
-    } else {  // many ranks: one sort, then the picks
-      HIP_TRY(sorted.ensure((size_t)count));
-      HIP_TRY(sort_keys(keys.p, sorted.p, (size_t)count, tmp, stream));
+    if (n == (int64_t)count) {  // every value, sorted
+      hipLaunchKernelGGL(keys_to_doubles, dim3(grid_of(n, 256 * 16, 4096)), dim3(256), 0, stream,
+                         sorted.p, n, picks.p);
+      HIP_TRY(hipGetLastError());
+    } else {  // many ranks: the picks of the sorted keys
+      std::vector<int64_t> rank(n);
+      for (int64_t j = 0; j < n; ++j) rank[j] = (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1));
       DevBuf<int64_t> didx;
       HIP_TRY(didx.ensure((size_t)n));
       HIP_TRY(hipMemcpyAsync(didx.p, rank.data(), (size_t)n * 8, hipMemcpyHostToDevice, stream));
@@ -428,6 +517,34 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipStreamSynchronize(stream));  // rank dies here
     }
+  } else {  // the values at the ranks floor(j (count - 1) / (n - 1)), by radix select
+    // every rank's bin of pass 1 (ranks ascend, so one sweep), and the bins' keys gathered
+    std::vector<Target> tg(n);
+    std::vector<uint32_t> bm(kQ0Bins / 32, 0u);
+    int64_t below = 0, T = 0;
+    int d = 0;
+    for (int64_t j = 0; j < n; ++j) {
+      const int64_t r = (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1));
+      while (r >= below + (int64_t)h0[d]) below += (int64_t)h0[d++];
+      tg[j] = Target{(uint64_t)d, r - below};
+      if (!((bm[d >> 5] >> (d & 31)) & 1u)) {
+        bm[d >> 5] |= 1u << (d & 31);
+        T += (int64_t)h0[d];
+      }
+    }
+    HIP_TRY(keys.ensure((size_t)T));
+    HIP_TRY(mask.ensure(kQ0Bins / 32));
+    HIP_TRY(hipMemcpyAsync(mask.p, bm.data(), (kQ0Bins / 32) * 4, hipMemcpyHostToDevice, stream));
+    for (int b = 0; b < n_batches; ++b) {
+      const dq_column& c = batches[b];
+      if (!c.length) continue;
+      hipLaunchKernelGGL(quantile_compact0, dim3(grid_of(c.length, kGatherStep, 2048)),
+                         dim3(kGatherThreads), 0, stream, c.type, c.validity, c.values, c.length,
+                         mask.p, keys.p, cur.p);
+      HIP_TRY(hipGetLastError());
+    }
+    const dq_status st = radix_select(keys.p, T, std::move(tg), kQ0Bits, picks.p, stream);
+    if (st != DQ_OK) return st;
   }
   HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));

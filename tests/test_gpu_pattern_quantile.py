@@ -265,6 +265,39 @@ def test_sorted_sample_exact_ranks_by_radix_select(dist, m, gpu_device):
     assert _ordered(out).tolist() == keys[ranks].tolist(), dist
 
 
+@pytest.mark.parametrize("ty", [pa.int64(), pa.int32(), pa.float32()])
+def test_sorted_sample_integral_batches_with_a_null_batch(ty, gpu_device):
+    """The fused first pass (a histogram of the keys' top bits read straight from the columns, then
+    only those bins' keys gathered) over integral / float batches, one of them all NULL: the picks
+    are the exact-rank values, bit-exact."""
+    import ctypes
+    import torch
+    from deequ_amd import _native as N
+    rng = np.random.default_rng(11)
+    n = 300_000
+    x = rng.integers(-5000, 3_000_000, n).astype(np.float64)
+    valid = rng.random(n) > 0.1
+    valid[100_000:150_000] = False  # the second batch of 50_000 rows: every value NULL
+    if ty == pa.float32():
+        x = x.astype(np.float32).astype(np.float64) / 8.0
+    arr_x = x.astype(np.float32) if ty == pa.float32() else x.astype(ty.to_pandas_dtype())
+    t = pa.table({"x": pa.array(arr_x, mask=~valid, type=ty)})
+    df = _df({"x": t.column("x")}, gpu_device, 50_000)
+    cols = [b["x"] for b in df.batches]
+    arr = (N.dq_column * len(cols))(*[c.to_c() for c in cols])
+    m = 201
+    out = np.zeros(m, np.float64)
+    n_out, count = ctypes.c_int64(), ctypes.c_int64()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(df.device_index()).cuda_stream)
+    N.check(N.lib.dq_sorted_sample(df.device_index(), arr, len(cols), 0, m, out.ctypes.data,
+                                   ctypes.byref(n_out), ctypes.byref(count), stream))
+    keys = np.sort(_ordered(arr_x.astype(np.float64)[valid]))
+    cnt = len(keys)
+    assert count.value == cnt and n_out.value == m
+    ranks = [(j * (cnt - 1)) // (m - 1) for j in range(m)]
+    assert _ordered(out).tolist() == keys[ranks].tolist()
+
+
 @pytest.mark.parametrize("expr,ty", [("CAST(f AS DOUBLE) RLIKE '^0\\\\.1000000'", "widen"),
                                      ("CAST(d AS FLOAT) RLIKE '^0\\\\.1$'", "narrow"),
                                      ("CAST(f AS DOUBLE) RLIKE 'E'", "widen"),
