@@ -1,15 +1,21 @@
 // quantile.hip -- the device half of ApproxQuantile (ApproxQuantile.scala:41-104).
 //
 // The reference feeds every non-NULL value, as a double, into Spark's ApproximatePercentile
-// (QuantileSummaries, Greenwald-Khanna with relativeError).  Here the values of all batches are
-// gathered as order-preserving 64-bit keys (Java's Double.compare order as unsigned order: NaNs
-// canonical and largest, -0.0 before 0.0) and handed to the host as either
+// (QuantileSummaries, Greenwald-Khanna with relativeError).  Here the values are order-preserving
+// 64-bit keys (Java's Double.compare order as unsigned order: NaNs canonical and largest, -0.0
+// before 0.0) and the host gets either
 //   * every value, sorted (rocPRIM radix sort) -- few enough that the host replays Spark's own
 //     insert + compress exactly, or relativeError 0 (the exact summary); or
 //   * the values at m evenly spaced exact ranks floor(j (n - 1) / (m - 1)) (a GK summary whose
-//     error is far inside relativeError), found by a radix SELECT: a few histogram passes over the
-//     keys narrow every rank to one bin, and only the bins that hold a rank are compacted and
-//     sorted -- instead of sorting every value.
+//     error is far inside relativeError), found by a radix SELECT straight over the columns:
+//     histogram passes narrow every rank to a bin of the keys' top bits, and only once the bins
+//     that hold a rank are small are their keys compacted (and, when few, sorted).
+// Every pass runs over a fixed row -> block map: a block's histogram lands in a row of per-block
+// partials, so a compaction knows each block's output offset from the pass before it (no
+// cursor atomic: one global atomic per step on one address bound the old gather at ~1.3 TB/s).
+// A pass also takes each active prefix's smallest and largest key, so a rank whose bin holds one
+// distinct value (integers of a narrow range: every further pass would only spend bits) is
+// decided at once.
 // The summary arithmetic -- insert, compress, merge, query -- is host code
 // (deequ_amd/analyzers/quantile.py).
 #include <hip/hip_runtime.h>
@@ -26,14 +32,20 @@
 
 using namespace dq;
 
+extern "C" __device__ uint64_t __ockl_wfred_add_u64(uint64_t);
+extern "C" __device__ uint64_t __ockl_wfred_min_u64(uint64_t);
+extern "C" __device__ uint64_t __ockl_wfred_max_u64(uint64_t);
+
 namespace {
 
-constexpr int kGatherThreads = 256;
-constexpr int kGatherWaves = kGatherThreads / 64;
-constexpr int kGatherRounds = 16;  // rows per thread per block step: 4096 rows a step
-constexpr int64_t kGatherStep = (int64_t)kGatherRounds * kGatherThreads;
-
-static_assert(kGatherRounds * kGatherWaves == 64, "one wave scans the step's counts");
+constexpr int kRsThreads = 256;
+constexpr int kRsK = 16;  // keys per thread per step, all loads in flight before the first is used
+constexpr int64_t kRsStep = (int64_t)kRsThreads * kRsK;
+constexpr int kSelBins = 8192;         // a pass's bins: A active prefixes << D digit bits
+constexpr int kSelMaxTargets = 2048;   // ranks selected (more: one sort of every key)
+constexpr int kMapBits = 13;           // prefixes this short find their index in an LDS map
+constexpr int kKeys = 0;               // source type: an array of keys (every one present)
+constexpr int kTargetBlocks = 1024;    // blocks of a pass over all the sources
 
 // Double.compare order as unsigned order (the canonical NaN is the largest key)
 DQ_HD uint64_t ordered_key(double v) {
@@ -44,152 +56,95 @@ DQ_HD double from_ordered(uint64_t k) {
   return __builtin_bit_cast(double, (k >> 63) ? (k & ~(1ULL << 63)) : ~k);
 }
 
-// A block step of 4096 items (round i: item base + 256 i + tid) keeps the items whose bit is set
-// in keep[i]; their values land at out[*cursor ...] in (round, wave, lane) order of the step,
-// placed by one exclusive scan over the step's 64 (round, wave) ballot counts and ONE cursor
-// atomic per step (one atomic per wave on one address serialised the kernel).
-struct StepPlacer {
-  uint32_t* s_cnt;  // kGatherRounds * kGatherWaves
-  unsigned long long* s_base;
-  DQ_DEV void place(const bool (&keep)[kGatherRounds], const uint64_t (&v)[kGatherRounds],
-                    uint64_t* __restrict__ out, unsigned long long* __restrict__ cursor) {
-    const int tid = threadIdx.x, lane = (int)__lane_id(), wave = tid >> 6;
-    const uint64_t lt = lane ? (~0ULL >> (64 - lane)) : 0ULL;  // lanes below this one
-    uint64_t m[kGatherRounds];
-#pragma unroll
-    for (int i = 0; i < kGatherRounds; ++i) {
-      m[i] = __ballot(keep[i]);
-      if (lane == 0) s_cnt[i * kGatherWaves + wave] = (uint32_t)__popcll(m[i]);
-    }
-    __syncthreads();
-    if (tid < 64) {  // exclusive scan of the 64 (round, wave) counts, round-major
-      const uint32_t c = s_cnt[tid];
-      uint32_t x = c;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
-      }
-      const uint32_t total = __shfl(x, 63);
-      unsigned long long base = 0;
-      if (lane == 63 && total) base = atomicAdd(cursor, (unsigned long long)total);
-      base = __shfl(base, 63);
-      s_cnt[tid] = x - c;
-      if (lane == 0) *s_base = base;
-    }
-    __syncthreads();
-    const unsigned long long base = *s_base;
-#pragma unroll
-    for (int i = 0; i < kGatherRounds; ++i)
-      if ((m[i] >> lane) & 1u) out[base + s_cnt[i * kGatherWaves + wave] + __popcll(m[i] & lt)] = v[i];
-    __syncthreads();  // s_cnt / s_base are rewritten by the next step
-  }
+// One batch of a numeric column, or an array of keys, and its first block in the pass.
+struct Src {
+  const uint8_t* valid;
+  const void* values;
+  int64_t rows;
+  int64_t blk0;
 };
 
-// Non-NULL values of one batch -> ordered keys at out[*cursor ...] (order irrelevant).
-__global__ void __launch_bounds__(kGatherThreads)
-quantile_gather(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
-                int64_t rows, uint64_t* __restrict__ out, unsigned long long* __restrict__ cursor) {
-  __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
-  __shared__ unsigned long long s_base;
-  StepPlacer pl{s_cnt, &s_base};
-  for (int64_t r0 = (int64_t)blockIdx.x * kGatherStep; r0 < rows; r0 += (int64_t)gridDim.x * kGatherStep) {
-    bool keep[kGatherRounds];
-    uint64_t v[kGatherRounds];
-#pragma unroll
-    for (int i = 0; i < kGatherRounds; ++i) {
-      const int64_t r = r0 + (int64_t)i * kGatherThreads + threadIdx.x;
-      keep[i] = r < rows && bit1(valid, r);
-      double d = keep[i] ? load_f64(type, values, r) : 0.0;
-      if (d != d) d = __builtin_nan("");  // Double.compare: every NaN is the canonical one
-      v[i] = ordered_key(d);
-    }
-    pl.place(keep, v, out, cursor);
+// The sources of one launch: up to kMaxSrc batches, their blocks back to back from blk0 of the first
+constexpr int kMaxSrc = 8;
+struct Srcs {
+  Src s[kMaxSrc];
+  int n;
+};
+// this block's source and its block index within it
+DQ_DEV const Src& block_src(const Srcs& ss, int64_t& local) {
+  const int64_t blk = ss.s[0].blk0 + blockIdx.x;
+  int j = 0;
+  while (j + 1 < ss.n && ss.s[j + 1].blk0 <= blk) ++j;
+  local = blk - ss.s[j].blk0;
+  return ss.s[j];
+}
+
+// What a pass bins by: the keys whose top `bits` bits are one of the A (sorted) prefixes, by
+// their next D bits (bin a << D | digit); R rows per block.
+struct Pass {
+  const uint64_t* act;
+  int A, bits, D;
+  int64_t R;
+};
+
+template <int TY> struct Ty { using T = double; };
+template <> struct Ty<kKeys> { using T = uint64_t; };
+template <> struct Ty<DQ_INT8> { using T = int8_t; };
+template <> struct Ty<DQ_INT16> { using T = int16_t; };
+template <> struct Ty<DQ_INT32> { using T = int32_t; };
+template <> struct Ty<DQ_INT64> { using T = int64_t; };
+template <> struct Ty<DQ_FLOAT32> { using T = float; };
+// rows per 16-byte load (VEC: the values are 16-byte aligned)
+template <int TY, bool VEC>
+constexpr int vec_of() {
+  return !VEC ? 1 : sizeof(typename Ty<TY>::T) == 8 ? 2 : sizeof(typename Ty<TY>::T) == 4 ? 4 : 1;
+}
+
+template <int TY>
+DQ_DEV uint64_t to_key(typename Ty<TY>::T v) {
+  if constexpr (TY == kKeys) {
+    return v;
+  } else {
+    double d = (double)v;
+    if (d != d) d = __builtin_nan("");  // Double.compare: every NaN is the canonical one
+    return ordered_key(d);
   }
 }
 
-// The first radix pass, fused into the read of the columns: a histogram of the ordered keys' top
-// kQ0Bits bits (no key is written; the keys of the bins that hold a rank are gathered afterwards by
-// quantile_compact0, so the column is read twice and only those keys are written).
-constexpr int kQ0Bits = 13;
-constexpr int kQ0Bins = 1 << kQ0Bits;
-
-__global__ void __launch_bounds__(256)
-quantile_hist0(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
-               int64_t rows, uint32_t* __restrict__ partial) {
-  __shared__ uint32_t s_hist[kQ0Bins];
-  for (int i = threadIdx.x; i < kQ0Bins; i += 256) s_hist[i] = 0;
-  __syncthreads();
-  constexpr int kU = 8;  // rows per thread per step, all loads in flight before the first count
-  for (int64_t i0 = (int64_t)blockIdx.x * 256 * kU; i0 < rows; i0 += (int64_t)gridDim.x * 256 * kU) {
-    uint64_t k[kU];
-    bool ok[kU];
+// The keys of one step of a block (rows i0 + (u * kRsThreads + tid) * V + j, j < V): each lane's V
+// consecutive rows come with one 16-byte load and one validity byte (V <= 4 rows from an aligned
+// row: their bits share the byte).  ok: present and in range.
+template <int TY, bool VEC>
+DQ_DEV void step_keys(const Src& s, int64_t i0, int64_t r_end, uint64_t (&k)[kRsK], bool (&ok)[kRsK]) {
+  using T = typename Ty<TY>::T;
+  constexpr int V = vec_of<TY, VEC>(), U = kRsK / V;
+  const T* vals = reinterpret_cast<const T*>(s.values);
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t r = i0 + (int64_t)u * 256 + threadIdx.x;
-      ok[u] = r < rows && bit1(valid, r);
-      double d = ok[u] ? load_f64(type, values, r) : 0.0;
-      if (d != d) d = __builtin_nan("");
-      k[u] = ordered_key(d);
+  for (int u = 0; u < U; ++u) {
+    const int64_t r = i0 + ((int64_t)u * kRsThreads + threadIdx.x) * V;
+    const int64_t rc = r < r_end ? r : r_end - 1;  // (in bounds; discarded below)
+    T v[V];
+    if constexpr (V > 1) {
+      if (r + V <= r_end) {
+        const uint4 x = *reinterpret_cast<const uint4*>(vals + r);
+        __builtin_memcpy(v, &x, 16);
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] = vals[r + j < r_end ? r + j : r_end - 1];
+      }
+    } else {
+      v[0] = vals[rc];
     }
+    uint32_t vb = 0xffu;
+    if constexpr (TY != kKeys)
+      if (s.valid) vb = (uint32_t)s.valid[rc >> 3] >> (r & 7);
 #pragma unroll
-    for (int u = 0; u < kU; ++u)
-      if (ok[u]) atomicAdd(&s_hist[k[u] >> (64 - kQ0Bits)], 1u);
-  }
-  __syncthreads();
-  // the block's counts as one coalesced row of partials (a global atomic per bin and block was
-  // millions of atomics on 8192 addresses)
-  uint32_t* row = partial + (size_t)blockIdx.x * kQ0Bins;
-  for (int i = threadIdx.x; i < kQ0Bins; i += 256) row[i] = s_hist[i];
-}
-
-// hist[bin] += the blocks' partial counts of the bin (one thread per bin, rows read coalesced)
-__global__ void __launch_bounds__(256)
-quantile_hist0_sum(const uint32_t* __restrict__ partial, int blocks, unsigned long long* __restrict__ hist) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= kQ0Bins) return;
-  unsigned long long t = 0;
-  for (int b = 0; b < blocks; ++b) t += partial[(size_t)b * kQ0Bins + i];
-  hist[i] += t;
-}
-
-// The non-NULL values of one batch whose key's top kQ0Bits bits are a bin set in `bins` (a
-// kQ0Bins-bit mask) -> ordered keys at out[*cursor ...] (order irrelevant).
-__global__ void __launch_bounds__(kGatherThreads)
-quantile_compact0(int type, const uint8_t* __restrict__ valid, const void* __restrict__ values,
-                  int64_t rows, const uint32_t* __restrict__ bins, uint64_t* __restrict__ out,
-                  unsigned long long* __restrict__ cursor) {
-  __shared__ uint32_t s_bins[kQ0Bins / 32];
-  __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
-  __shared__ unsigned long long s_base;
-  for (int i = threadIdx.x; i < kQ0Bins / 32; i += kGatherThreads) s_bins[i] = bins[i];
-  __syncthreads();
-  StepPlacer pl{s_cnt, &s_base};
-  for (int64_t r0 = (int64_t)blockIdx.x * kGatherStep; r0 < rows; r0 += (int64_t)gridDim.x * kGatherStep) {
-    bool keep[kGatherRounds];
-    uint64_t v[kGatherRounds];
-#pragma unroll
-    for (int i = 0; i < kGatherRounds; ++i) {
-      const int64_t r = r0 + (int64_t)i * kGatherThreads + threadIdx.x;
-      const bool ok = r < rows && bit1(valid, r);
-      double d = ok ? load_f64(type, values, r) : 0.0;
-      if (d != d) d = __builtin_nan("");
-      v[i] = ordered_key(d);
-      const uint32_t b = (uint32_t)(v[i] >> (64 - kQ0Bits));
-      keep[i] = ok && ((s_bins[b >> 5] >> (b & 31)) & 1u);
+    for (int j = 0; j < V; ++j) {
+      ok[u * V + j] = ((vb >> j) & 1u) && r + j < r_end;
+      k[u * V + j] = to_key<TY>(v[j]);
     }
-    pl.place(keep, v, out, cursor);
   }
 }
-
-// ---- radix select -----------------------------------------------------------------------------
-// A pass counts the keys whose top `bits` bits equal one of the A active prefixes (sorted, unique)
-// by their next D bits: hist[a << D | digit], A << D <= kSelBins, privatised in LDS per block.
-constexpr int kSelBins = 8192;  // 32 KB of LDS counters (+ 16 KB of prefixes at most)
-constexpr int kSelMaxTargets = 2048;
-// passes whose prefixes are at most kMapBits long find a key's prefix through a direct LDS map
-// (prefix -> active index, 16 KB) instead of a binary search over the prefixes
-constexpr int kMapBits = 13;
 
 DQ_DEV int find_prefix(const uint64_t* act, int A, uint64_t p) {
   int lo = 0, hi = A;  // first index with act[i] >= p
@@ -201,78 +156,213 @@ DQ_DEV int find_prefix(const uint64_t* act, int A, uint64_t p) {
   return lo < A && act[lo] == p ? lo : -1;
 }
 
-// The active index of every prefix of `bits` <= kMapBits bits (-1: not active), in LDS.
-DQ_DEV void build_prefix_map(const uint64_t* act, int A, int bits, int16_t* map) {
-  for (int i = threadIdx.x; i < (1 << bits); i += blockDim.x) map[i] = -1;
-  __syncthreads();
-  for (int i = threadIdx.x; i < A; i += blockDim.x) map[act[i]] = (int16_t)i;
-  __syncthreads();
+// LDS of a pass: the prefixes, (bits > 0) their min / max keys, (bits <= kMapBits) the prefix map
+struct PassLds {
+  uint64_t* act;
+  unsigned long long *mn, *mx;
+  int16_t* map;
+  bool mapped;
+  DQ_DEV void load(const Pass& p, uint64_t* base, bool minmax) {
+    act = base;
+    mn = reinterpret_cast<unsigned long long*>(base + p.A);
+    mx = mn + p.A;
+    map = reinterpret_cast<int16_t*>(base + p.A + (minmax ? 2 * p.A : 0));
+    mapped = p.bits > 0 && p.bits <= kMapBits;
+    for (int i = threadIdx.x; i < p.A; i += kRsThreads) {
+      act[i] = p.act[i];
+      if (minmax) {
+        mn[i] = ~0ULL;
+        mx[i] = 0ULL;
+      }
+    }
+    if (mapped) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < (1 << p.bits); i += kRsThreads) map[i] = -1;
+      __syncthreads();
+      for (int i = threadIdx.x; i < p.A; i += kRsThreads) map[act[i]] = (int16_t)i;
+    }
+  }
+  DQ_DEV int index(const Pass& p, uint64_t k) const {
+    if (p.bits == 0) return 0;
+    const uint64_t pre = k >> (64 - p.bits);
+    return mapped ? (int)map[pre] : find_prefix(act, p.A, pre);
+  }
+};
+DQ_HD size_t pass_lds_words(const Pass& p, bool minmax) {  // in u64 words, before the bins
+  return (size_t)p.A * (minmax ? 3 : 1) +
+         (p.bits > 0 && p.bits <= kMapBits ? ((2u << p.bits) + 7) / 8 : 0);
+}
+DQ_DEV uint32_t digit_of(const Pass& p, uint64_t k) {
+  return p.D ? (uint32_t)((k << p.bits) >> (64 - p.D)) : 0u;
 }
 
-__global__ void __launch_bounds__(256)
-select_hist(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __restrict__ active, int A,
-            int bits, int D, unsigned long long* __restrict__ hist) {
-  extern __shared__ uint64_t sel_lds[];
-  uint64_t* s_act = sel_lds;                                            // A
-  unsigned int* s_hist = reinterpret_cast<unsigned int*>(sel_lds + A);  // A << D
-  const int nb = A << D;
-  int16_t* s_map = reinterpret_cast<int16_t*>(s_hist + nb);  // 1 << bits, when bits <= kMapBits
-  const bool mapped = bits > 0 && bits <= kMapBits;
-  for (int i = threadIdx.x; i < A; i += 256) s_act[i] = active[i];
-  for (int i = threadIdx.x; i < nb; i += 256) s_hist[i] = 0;
+// A pass's histogram: block g's counts -> partial[g][A << D]; with bits > 0 also each prefix's
+// min / max key -> pmm[g][2A].
+template <int TY, bool VEC>
+__global__ void __launch_bounds__(kRsThreads)
+rs_hist(Srcs ss, Pass p, uint32_t* __restrict__ partial, unsigned long long* __restrict__ pmm) {
+  extern __shared__ uint64_t rs_lds[];
+  int64_t lb;
+  const Src& s = block_src(ss, lb);
+  const bool minmax = p.bits > 0;
+  PassLds L;
+  L.load(p, rs_lds, minmax);
+  const int nb = p.A << p.D;
+  uint32_t* s_hist = reinterpret_cast<uint32_t*>(rs_lds + pass_lds_words(p, minmax));
+  for (int i = threadIdx.x; i < nb; i += kRsThreads) s_hist[i] = 0;
   __syncthreads();
-  if (mapped) build_prefix_map(s_act, A, bits, s_map);
-  // 8 keys per thread per step, all loads in flight before the first is counted
-  constexpr int kU = 8;
-  for (int64_t i0 = (int64_t)blockIdx.x * 256 * kU; i0 < n; i0 += (int64_t)gridDim.x * 256 * kU) {
-    uint64_t kk[kU];
+  const int64_t r_begin = lb * p.R;
+  const int64_t r_end = r_begin + p.R < s.rows ? r_begin + p.R : s.rows;
+  for (int64_t i0 = r_begin; i0 < r_end; i0 += kRsStep) {
+    uint64_t k[kRsK];
+    bool ok[kRsK];
+    step_keys<TY, VEC>(s, i0, r_end, k, ok);
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int64_t i = i0 + (int64_t)u * 256 + threadIdx.x;
-      kk[u] = i < n ? keys[i] : 0ULL;
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      if (i0 + (int64_t)u * 256 + threadIdx.x >= n) continue;
-      const uint64_t k = kk[u];
-      int a = 0;
-      if (bits) {
-        a = mapped ? (int)s_map[k >> (64 - bits)] : find_prefix(s_act, A, k >> (64 - bits));
-        if (a < 0) continue;
+    for (int u = 0; u < kRsK; ++u) {
+      const int a = ok[u] ? L.index(p, k[u]) : -1;
+      if (a >= 0) atomicAdd(&s_hist[(a << p.D) | (int)digit_of(p, k[u])], 1u);
+      if (minmax) {  // a wave whose keys share one prefix (narrow data) reduces before its atomic
+        const int a0 = __builtin_amdgcn_readfirstlane(a);
+        if (__ballot(a == a0) == ~0ULL) {
+          if (a0 >= 0) {
+            const uint64_t lo = __ockl_wfred_min_u64(k[u]), hi = __ockl_wfred_max_u64(k[u]);
+            if (__lane_id() == 0) {
+              atomicMin(&L.mn[a0], (unsigned long long)lo);
+              atomicMax(&L.mx[a0], (unsigned long long)hi);
+            }
+          }
+        } else if (a >= 0) {
+          atomicMin(&L.mn[a], (unsigned long long)k[u]);
+          atomicMax(&L.mx[a], (unsigned long long)k[u]);
+        }
       }
-      const uint32_t d = (uint32_t)((k << bits) >> (64 - D));
-      atomicAdd(&s_hist[(a << D) | (int)d], 1u);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nb; i += 256)
-    if (s_hist[i]) atomicAdd(&hist[i], (unsigned long long)s_hist[i]);  // (u64: a bin may pass 2^32 keys)
+  const int64_t g = s.blk0 + lb;
+  uint32_t* row = partial + (size_t)g * nb;
+  for (int i = threadIdx.x; i < nb; i += kRsThreads) row[i] = s_hist[i];
+  if (minmax) {
+    unsigned long long* mrow = pmm + (size_t)g * 2 * p.A;
+    for (int i = threadIdx.x; i < p.A; i += kRsThreads) {
+      mrow[2 * i] = L.mn[i];
+      mrow[2 * i + 1] = L.mx[i];
+    }
+  }
 }
 
-// The keys whose top `bits` bits are one of the A prefixes -> out[*cursor ...].
-__global__ void __launch_bounds__(kGatherThreads)
-select_compact(const uint64_t* __restrict__ keys, int64_t n, const uint64_t* __restrict__ active,
-               int A, int bits, uint64_t* __restrict__ out, unsigned long long* __restrict__ cursor) {
-  extern __shared__ uint64_t sel_lds[];
-  __shared__ uint32_t s_cnt[kGatherRounds * kGatherWaves];
-  __shared__ unsigned long long s_base;
-  int16_t* s_map = reinterpret_cast<int16_t*>(sel_lds + A);  // 1 << bits, when bits <= kMapBits
-  const bool mapped = bits <= kMapBits;
-  for (int i = threadIdx.x; i < A; i += kGatherThreads) sel_lds[i] = active[i];
+// hist[bin] = sum over the blocks of partial[g][bin]; blockIdx.y takes 32 blocks' rows
+__global__ void __launch_bounds__(256)
+rs_sum(const uint32_t* __restrict__ partial, int64_t G, int nb, unsigned long long* __restrict__ hist) {
+  const int bin = blockIdx.x * 256 + threadIdx.x;
+  if (bin >= nb) return;
+  const int64_t g0 = (int64_t)blockIdx.y * 32, g1 = g0 + 32 < G ? g0 + 32 : G;
+  unsigned long long t = 0;
+  for (int64_t g = g0; g < g1; ++g) t += partial[(size_t)g * nb + bin];
+  if (t) atomicAdd(&hist[bin], t);
+}
+
+// mm[2a] = min, mm[2a + 1] = max over the blocks of prefix a's keys (mm preset to ~0 / 0)
+__global__ void __launch_bounds__(256)
+rs_minmax(const unsigned long long* __restrict__ pmm, int64_t G, int A, unsigned long long* __restrict__ mm) {
+  const int a = blockIdx.x * 256 + threadIdx.x;
+  if (a >= A) return;
+  const int64_t g0 = (int64_t)blockIdx.y * 32, g1 = g0 + 32 < G ? g0 + 32 : G;
+  unsigned long long lo = ~0ULL, hi = 0ULL;
+  for (int64_t g = g0; g < g1; ++g) {
+    const unsigned long long x = pmm[(size_t)g * 2 * A + 2 * a], y = pmm[(size_t)g * 2 * A + 2 * a + 1];
+    lo = x < lo ? x : lo;
+    hi = y > hi ? y : hi;
+  }
+  if (lo != ~0ULL) atomicMin(&mm[2 * a], lo);
+  if (hi) atomicMax(&mm[2 * a + 1], hi);
+}
+
+// kept[g] = block g's keys in the selected bins (sel: an nb-bit mask)
+__global__ void __launch_bounds__(256)
+rs_kept(const uint32_t* __restrict__ partial, int nb, const uint32_t* __restrict__ sel,
+        unsigned long long* __restrict__ kept) {
+  __shared__ unsigned long long s_red[4];
+  const uint32_t* row = partial + (size_t)blockIdx.x * nb;
+  unsigned long long t = 0;
+  for (int i = threadIdx.x; i < nb; i += 256)
+    if ((sel[i >> 5] >> (i & 31)) & 1u) t += row[i];
+  t = (unsigned long long)__ockl_wfred_add_u64((uint64_t)t);
+  if (__lane_id() == 0) s_red[threadIdx.x >> 6] = t;
   __syncthreads();
-  if (mapped) build_prefix_map(sel_lds, A, bits, s_map);
-  StepPlacer pl{s_cnt, &s_base};
-  for (int64_t i0 = (int64_t)blockIdx.x * kGatherStep; i0 < n; i0 += (int64_t)gridDim.x * kGatherStep) {
-    bool keep[kGatherRounds];
-    uint64_t v[kGatherRounds];
+  if (threadIdx.x == 0) kept[blockIdx.x] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+}
+
+// base = exclusive scan of kept[0..G) (one block)
+__global__ void __launch_bounds__(1024) rs_scan(const unsigned long long* __restrict__ kept, int64_t G,
+                                                unsigned long long* __restrict__ base) {
+  __shared__ unsigned long long s_w[16];
+  __shared__ unsigned long long s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < G; c0 += 1024) {
+    const int64_t g = c0 + threadIdx.x;
+    const unsigned long long v = g < G ? kept[g] : 0ULL;
+    unsigned long long x = v;  // inclusive scan in the wave
 #pragma unroll
-    for (int r = 0; r < kGatherRounds; ++r) {
-      const int64_t i = i0 + (int64_t)r * kGatherThreads + threadIdx.x;
-      v[r] = i < n ? keys[i] : 0ULL;
-      keep[r] = i < n && (mapped ? s_map[v[r] >> (64 - bits)] >= 0
-                                 : find_prefix(sel_lds, A, v[r] >> (64 - bits)) >= 0);
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long y = __shfl_up(x, d);
+      if ((int)__lane_id() >= d) x += y;
     }
-    pl.place(keep, v, out, cursor);
+    const int w = threadIdx.x >> 6;
+    if (__lane_id() == 63) s_w[w] = x;
+    __syncthreads();
+    unsigned long long before = s_carry;
+    for (int j = 0; j < w; ++j) before += s_w[j];
+    if (g < G) base[g] = before + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) s_carry = before + x;
+    __syncthreads();
+  }
+}
+
+// The keys in the selected bins of a pass (same blocks and rows as its rs_hist) -> out[base[g] ..]
+template <int TY, bool VEC>
+__global__ void __launch_bounds__(kRsThreads)
+rs_compact(Srcs ss, Pass p, const uint32_t* __restrict__ sel, const unsigned long long* __restrict__ base,
+           uint64_t* __restrict__ out) {
+  extern __shared__ uint64_t rs_lds[];
+  int64_t lb;
+  const Src& s = block_src(ss, lb);
+  __shared__ uint32_t s_cur;
+  PassLds L;
+  L.load(p, rs_lds, false);
+  const int nb = p.A << p.D;
+  uint32_t* s_sel = reinterpret_cast<uint32_t*>(rs_lds + pass_lds_words(p, false));
+  for (int i = threadIdx.x; i < (nb + 31) / 32; i += kRsThreads) s_sel[i] = sel[i];
+  if (threadIdx.x == 0) s_cur = 0;
+  __syncthreads();
+  const unsigned long long ob = base[s.blk0 + lb];
+  const int lane = (int)__lane_id();
+  const uint64_t lt = lane ? (~0ULL >> (64 - lane)) : 0ULL;
+  const int64_t r_begin = lb * p.R;
+  const int64_t r_end = r_begin + p.R < s.rows ? r_begin + p.R : s.rows;
+  for (int64_t i0 = r_begin; i0 < r_end; i0 += kRsStep) {
+    uint64_t k[kRsK];
+    bool ok[kRsK];
+    step_keys<TY, VEC>(s, i0, r_end, k, ok);
+#pragma unroll
+    for (int u = 0; u < kRsK; ++u) {
+      bool keep = false;
+      if (ok[u]) {
+        const int a = L.index(p, k[u]);
+        if (a >= 0) {
+          const uint32_t bin = ((uint32_t)a << p.D) | digit_of(p, k[u]);
+          keep = (s_sel[bin >> 5] >> (bin & 31)) & 1u;
+        }
+      }
+      const uint64_t bal = __ballot(keep);
+      if (!bal) continue;
+      uint32_t off = 0;
+      if (lane == 0) off = atomicAdd(&s_cur, (uint32_t)__builtin_popcountll(bal));
+      off = __shfl(off, 0);
+      if (keep) out[ob + off + (uint32_t)__builtin_popcountll(bal & lt)] = k[u];
+    }
   }
 }
 
@@ -289,10 +379,6 @@ __global__ void keys_to_doubles(const uint64_t* __restrict__ sorted, int64_t n, 
     out[j] = from_ordered(sorted[j]);
 }
 
-unsigned grid_of(int64_t n, int64_t per_block, int64_t cap) {
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + per_block - 1) / per_block, cap));
-}
-
 hipError_t sort_keys(const uint64_t* in, uint64_t* out, size_t n, DevBuf<uint8_t>& tmp,
                      hipStream_t stream) {
   size_t tmp_bytes = 0;
@@ -303,132 +389,241 @@ hipError_t sort_keys(const uint64_t* in, uint64_t* out, size_t n, DevBuf<uint8_t
   return rocprim::radix_sort_keys(tmp.p, tmp_bytes, in, out, n, 0, 64, stream);
 }
 
-// The values at the exact ranks rank[0..m) (ascending) of the n keys at `keys`, into out_dev[m]
-// (doubles).  Histogram passes narrow every rank to a bin of the keys' top bits; once the bins
-// that hold a rank hold few keys (or every bit is decided) those keys are compacted and sorted.
+// The keys a pass runs over: the batches of a column (type TY) or one array of keys, cut into
+// blocks of R rows.
+struct Source {
+  int type;
+  std::vector<Src> parts;
+  int64_t R = kRsStep, G = 0, M = 0;  // rows per block, blocks, keys (non-NULL rows: after pass 0)
+  bool aligned16() const {
+    for (const Src& s : parts)
+      if (reinterpret_cast<uintptr_t>(s.values) & 15) return false;
+    return true;
+  }
+  void cut(int64_t total_rows) {
+    R = std::max<int64_t>(4 * kRsStep, (total_rows / kTargetBlocks + kRsStep - 1) / kRsStep * kRsStep);
+    G = 0;
+    for (Src& s : parts) {
+      s.blk0 = G;
+      G += (s.rows + R - 1) / R;
+    }
+  }
+};
+
+// The sources in launches of at most kMaxSrc batches each (blocks back to back)
+template <class F>
+void for_launches(const Source& src, F&& f) {
+  for (size_t i = 0; i < src.parts.size(); i += kMaxSrc) {
+    Srcs ss;
+    ss.n = (int)std::min<size_t>(kMaxSrc, src.parts.size() - i);
+    int64_t blocks = 0;
+    for (int j = 0; j < ss.n; ++j) {
+      ss.s[j] = src.parts[i + j];
+      blocks += (ss.s[j].rows + src.R - 1) / src.R;
+    }
+    f(ss, (unsigned)blocks);
+  }
+}
+
+template <int TY, bool VEC>
+void launch_hist_t(const Source& src, Pass p, uint32_t* partial, unsigned long long* pmm, hipStream_t st) {
+  p.R = src.R;
+  const size_t lds = pass_lds_words(p, p.bits > 0) * 8 + (size_t)(p.A << p.D) * 4;
+  for_launches(src, [&](const Srcs& ss, unsigned blocks) {
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(rs_hist<TY, VEC>), dim3(blocks), dim3(kRsThreads), lds, st, ss, p, partial, pmm);
+  });
+}
+template <int TY, bool VEC>
+void launch_compact_t(const Source& src, Pass p, const uint32_t* sel, const unsigned long long* base,
+                      uint64_t* out, hipStream_t st) {
+  p.R = src.R;
+  const size_t lds = pass_lds_words(p, false) * 8 + (size_t)(((p.A << p.D) + 31) / 32) * 4;
+  for_launches(src, [&](const Srcs& ss, unsigned blocks) {
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(rs_compact<TY, VEC>), dim3(blocks), dim3(kRsThreads), lds, st, ss, p, sel, base, out);
+  });
+}
+#define RS_DISPATCH_V(fn, V, ...)                              \
+  switch (src.type) {                                          \
+    case kKeys: fn<kKeys, V>(__VA_ARGS__); break;              \
+    case DQ_INT8: fn<DQ_INT8, V>(__VA_ARGS__); break;          \
+    case DQ_INT16: fn<DQ_INT16, V>(__VA_ARGS__); break;        \
+    case DQ_INT32: fn<DQ_INT32, V>(__VA_ARGS__); break;        \
+    case DQ_INT64: fn<DQ_INT64, V>(__VA_ARGS__); break;        \
+    case DQ_FLOAT32: fn<DQ_FLOAT32, V>(__VA_ARGS__); break;    \
+    default: fn<DQ_FLOAT64, V>(__VA_ARGS__); break;            \
+  }
+#define RS_DISPATCH(fn, ...)                    \
+  if (src.aligned16()) {                        \
+    RS_DISPATCH_V(fn, true, __VA_ARGS__)        \
+  } else {                                      \
+    RS_DISPATCH_V(fn, false, __VA_ARGS__)       \
+  }
+
+// One pass over `src`: its bins' counts (host `h`, A << D of them) and, with bits > 0, each
+// prefix's min / max key (host `mm`); the per-block partials stay on the device for a compaction.
+struct Passer {
+  hipStream_t st;
+  DevBuf<uint32_t> partial;
+  DevBuf<unsigned long long> pmm, hist, mm, kept, base;
+  DevBuf<uint64_t> act;
+  DevBuf<uint32_t> sel;
+  std::vector<unsigned long long> h, mmh;
+  dq_status run(const Source& src, const std::vector<uint64_t>& prefixes, int bits, int D, Pass& p) {
+    const int A = (int)prefixes.size(), nb = A << D;
+    HIP_TRY(act.ensure(A));
+    HIP_TRY(hipMemcpyAsync(act.p, prefixes.data(), (size_t)A * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(partial.ensure((size_t)src.G * nb));
+    HIP_TRY(hist.ensure(nb));
+    HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)nb * 8, st));
+    p = Pass{act.p, A, bits, D, src.R};
+    if (bits > 0) {
+      HIP_TRY(pmm.ensure((size_t)src.G * 2 * A));
+      HIP_TRY(mm.ensure((size_t)2 * A));
+      std::vector<unsigned long long> init(2 * (size_t)A);
+      for (int a = 0; a < A; ++a) init[2 * a] = ~0ULL, init[2 * a + 1] = 0ULL;
+      mmh.swap(init);
+      HIP_TRY(hipMemcpyAsync(mm.p, mmh.data(), (size_t)A * 16, hipMemcpyHostToDevice, st));
+    }
+    RS_DISPATCH(launch_hist_t, src, p, partial.p, pmm.p, st);
+    HIP_TRY(hipGetLastError());
+    const unsigned gy = (unsigned)((src.G + 31) / 32);
+    hipLaunchKernelGGL(rs_sum, dim3((unsigned)((nb + 255) / 256), gy), dim3(256), 0, st, partial.p, src.G,
+                       nb, hist.p);
+    HIP_TRY(hipGetLastError());
+    if (bits > 0) {
+      hipLaunchKernelGGL(rs_minmax, dim3((unsigned)((A + 255) / 256), gy), dim3(256), 0, st, pmm.p, src.G,
+                         A, mm.p);
+      HIP_TRY(hipGetLastError());
+    }
+    h.resize(nb);
+    HIP_TRY(hipMemcpyAsync(h.data(), hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, st));
+    if (bits > 0) HIP_TRY(hipMemcpyAsync(mmh.data(), mm.p, (size_t)A * 16, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return DQ_OK;
+  }
+  // the keys of the last pass's selected bins (mask: nb bits) -> dst (T of them)
+  dq_status compact(const Source& src, const Pass& p, const std::vector<uint32_t>& mask, uint64_t* dst) {
+    HIP_TRY(sel.ensure(mask.size()));
+    HIP_TRY(hipMemcpyAsync(sel.p, mask.data(), mask.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(kept.ensure((size_t)src.G));
+    HIP_TRY(base.ensure((size_t)src.G));
+    hipLaunchKernelGGL(rs_kept, dim3((unsigned)src.G), dim3(256), 0, st, partial.p, p.A << p.D, sel.p, kept.p);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(rs_scan, dim3(1), dim3(1024), 0, st, kept.p, src.G, base.p);
+    HIP_TRY(hipGetLastError());
+    RS_DISPATCH(launch_compact_t, src, p, sel.p, base.p, dst, st);
+    HIP_TRY(hipGetLastError());
+    return DQ_OK;
+  }
+};
+
 struct Target {
   uint64_t prefix;  // the top `bits` bits of the target's key
   int64_t q;        // rank among the keys with this prefix
+  int j;            // output index
 };
 
-// `keys` (n of them) are exactly the keys whose top `bits0` bits are one of the targets' prefixes
-// (every key when bits0 = 0).
-dq_status radix_select(const uint64_t* keys, int64_t n, std::vector<Target> tg, int bits0,
-                       double* out_dev, hipStream_t stream) {
-  const int m = (int)tg.size();
-  // keys sorted at the end: always when this few; and up to kStallBudget when a pass stopped
-  // narrowing (a bin of one repeated value -- integers of a narrow range -- never shrinks: more
-  // passes over it only spend bits)
-  constexpr int64_t kSortBudget = 1 << 24, kStallBudget = 1 << 26;
-  int64_t T_prev = n;
-  DevBuf<uint64_t> buf[2], act;
-  DevBuf<unsigned long long> hist;
-  DevBuf<unsigned long long> cur;
+// The values at the exact ranks of `tg`, into res[j].  Pass 0 (one prefix, D0 bits) has run: `h`
+// holds its bins.  Histogram passes narrow every rank to a bin; a rank whose prefix holds one
+// distinct key is decided by the prefix's min = max; once the selected bins are small (or hold
+// at most half of the keys a pass reads) their keys are compacted, and when few enough sorted.
+dq_status radix_select(Source src, Passer& ps, Pass p, std::vector<Target> tg, std::vector<double>& res) {
+  constexpr int64_t kSortBudget = 1 << 20;
+  hipStream_t st = ps.st;
+  DevBuf<uint64_t> buf[2];
   DevBuf<uint8_t> tmp;
   DevBuf<int64_t> didx;
-  HIP_TRY(cur.ensure(1));
-  const uint64_t* src = keys;
-  int64_t M = n;
+  DevBuf<double> dpick;
   int which = 0;
-  int bits = bits0;
-  std::vector<uint64_t> prefixes, sp;  // (alive until the copies from them have run)
-  std::vector<unsigned long long> h;
+  std::vector<uint64_t> cur{0};  // the prefixes of this pass (sorted; pass 0: the empty prefix)
   while (true) {
-    prefixes.clear();
-    for (const Target& t : tg) prefixes.push_back(t.prefix);
-    std::sort(prefixes.begin(), prefixes.end());
-    prefixes.erase(std::unique(prefixes.begin(), prefixes.end()), prefixes.end());
-    const int A = (int)prefixes.size();
-    int D = 1;
-    while (D < 64 - bits && ((int64_t)A << (D + 1)) <= kSelBins) ++D;
-    const int nb = A << D;
-    HIP_TRY(act.ensure(A));
-    HIP_TRY(hipMemcpyAsync(act.p, prefixes.data(), A * 8, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hist.ensure(nb));
-    HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)nb * 8, stream));
-    const size_t lds = (size_t)A * 8 + (size_t)nb * 4 + (bits && bits <= kMapBits ? 2u << bits : 0u);
-    // (a few blocks per CU: each flushes up to kSelBins counters)
-    hipLaunchKernelGGL(select_hist, dim3(grid_of(M, 256 * 64, 1024)), dim3(256), lds, stream, src,
-                       M, act.p, A, bits, D, hist.p);
-    HIP_TRY(hipGetLastError());
-    h.resize(nb);
-    HIP_TRY(hipMemcpyAsync(h.data(), hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    // every target: the bin of its prefix that holds its rank
+    // decided by min = max: the prefix holds one distinct key
+    std::vector<Target> left;
     for (Target& t : tg) {
-      const int a = (int)(std::lower_bound(prefixes.begin(), prefixes.end(), t.prefix) - prefixes.begin());
+      const int a = (int)(std::lower_bound(cur.begin(), cur.end(), t.prefix) - cur.begin());
+      if (p.bits > 0 && ps.mmh[2 * a] == ps.mmh[2 * a + 1]) {
+        res[t.j] = from_ordered(ps.mmh[2 * a]);
+        continue;
+      }
       int64_t below = 0;
       int d = 0;
-      for (; d < (1 << D); ++d) {
-        const int64_t c = h[((size_t)a << D) | d];
+      for (; d < (1 << p.D); ++d) {
+        const int64_t c = (int64_t)ps.h[((size_t)a << p.D) | d];
         if (t.q < below + c) break;
         below += c;
       }
-      if (d == (1 << D)) return fail(DQ_ERR_STATE, "radix select lost a rank (counts changed under it)");
-      t.prefix = (t.prefix << D) | (uint64_t)d;
-      t.q -= below;
+      if (d == (1 << p.D)) return fail(DQ_ERR_STATE, "radix select lost a rank (counts changed under it)");
+      left.push_back(Target{(t.prefix << p.D) | (uint64_t)d, t.q - below, t.j});
     }
-    const int nbits = bits + D;
-    // the bins that now hold a rank, and the keys in them
+    tg.swap(left);
+    const int bits = p.bits + p.D;
+    if (tg.empty()) return DQ_OK;
+    if (bits == 64) {  // every bit decided: the prefix IS the key
+      for (const Target& t : tg) res[t.j] = from_ordered(t.prefix);
+      return DQ_OK;
+    }
+    // the bins that now hold a rank, and their keys
     std::vector<std::pair<uint64_t, int64_t>> sel;  // (prefix, keys), ascending
     for (const Target& t : tg) sel.push_back({t.prefix, 0});
     std::sort(sel.begin(), sel.end());
     sel.erase(std::unique(sel.begin(), sel.end()), sel.end());
     int64_t T = 0;
+    std::vector<uint32_t> mask(((size_t)(p.A << p.D) + 31) / 32, 0u);
     for (auto& s : sel) {
-      const uint64_t parent = s.first >> D;  // (0, the only prefix, on the first pass)
-      const int a = (int)(std::lower_bound(prefixes.begin(), prefixes.end(), parent) - prefixes.begin());
-      s.second = h[((size_t)a << D) | (s.first & ((1ULL << D) - 1))];
+      const int a = (int)(std::lower_bound(cur.begin(), cur.end(), s.first >> p.D) - cur.begin());
+      const uint32_t bin = ((uint32_t)a << p.D) | (uint32_t)(s.first & ((1ULL << p.D) - 1));
+      s.second = (int64_t)ps.h[bin];
+      mask[bin >> 5] |= 1u << (bin & 31);
       T += s.second;
     }
-    bits = nbits;
-    if (bits == 64) {  // every bit decided: the prefix IS the key
-      std::vector<double> v(m);
-      for (int j = 0; j < m; ++j) v[j] = from_ordered(tg[j].prefix);
-      HIP_TRY(hipMemcpyAsync(out_dev, v.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
+    const bool finish = T <= kSortBudget;
+    if (finish || 2 * T <= src.M) {  // compact the selected bins' keys (into the buffer src is not)
+      DevBuf<uint64_t>& dst = buf[which];
+      HIP_TRY(dst.ensure((size_t)std::max<int64_t>(T, 1)));
+      dq_status cs = ps.compact(src, p, mask, dst.p);
+      if (cs != DQ_OK) return cs;
+      Source next;
+      next.type = kKeys;
+      next.parts.push_back(Src{nullptr, dst.p, T, 0});
+      next.cut(T);
+      next.M = T;
+      src = next;
+      which ^= 1;
+    }
+    if (finish) {  // sort them; a target's key sits at (keys of the bins before its own) + q
+      DevBuf<uint64_t>& sorted = buf[which];
+      HIP_TRY(sorted.ensure((size_t)std::max<int64_t>(T, 1)));
+      HIP_TRY(sort_keys(reinterpret_cast<const uint64_t*>(src.parts[0].values), sorted.p, (size_t)T, tmp, st));
+      const int u = (int)tg.size();
+      std::vector<int64_t> idx(u);
+      for (int i = 0; i < u; ++i) {
+        int64_t before = 0;
+        for (const auto& s : sel) {
+          if (s.first == tg[i].prefix) break;
+          before += s.second;
+        }
+        idx[i] = before + tg[i].q;
+      }
+      HIP_TRY(didx.ensure(u));
+      HIP_TRY(dpick.ensure(u));
+      HIP_TRY(hipMemcpyAsync(didx.p, idx.data(), (size_t)u * 8, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(select_pick, dim3((unsigned)((u + 255) / 256)), dim3(256), 0, st, sorted.p, didx.p,
+                         (int64_t)u, dpick.p);
+      HIP_TRY(hipGetLastError());
+      std::vector<double> v(u);
+      HIP_TRY(hipMemcpyAsync(v.data(), dpick.p, (size_t)u * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));  // idx and v die here
+      for (int i = 0; i < u; ++i) res[tg[i].j] = v[i];
       return DQ_OK;
     }
-    const bool finish = T <= kSortBudget || (T <= kStallBudget && 2 * T > T_prev);
-    T_prev = T;
-    if (!finish && T > M / 2) continue;  // narrowing did not pay for a copy yet
-    // compact the selected bins' keys (into the buffer src is not)
-    sp.resize(sel.size());
-    for (size_t i = 0; i < sel.size(); ++i) sp[i] = sel[i].first;
-    const int S = (int)sp.size();
-    HIP_TRY(act.ensure(S));
-    HIP_TRY(hipMemcpyAsync(act.p, sp.data(), (size_t)S * 8, hipMemcpyHostToDevice, stream));
-    DevBuf<uint64_t>& dst = buf[which];
-    HIP_TRY(dst.ensure((size_t)std::max<int64_t>(T, 1)));
-    HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
-    hipLaunchKernelGGL(select_compact, dim3(grid_of(M, kGatherStep, 2048)), dim3(kGatherThreads),
-                       (size_t)S * 8 + (bits <= kMapBits ? 2u << bits : 0u), stream, src, M, act.p, S,
-                       bits, dst.p, cur.p);
-    HIP_TRY(hipGetLastError());
-    src = dst.p;
-    M = T;
-    which ^= 1;
-    if (!finish) continue;
-    // sort the compacted keys; a target's key sits at (keys of the bins before its own) + q
-    DevBuf<uint64_t>& sorted = buf[which];
-    HIP_TRY(sorted.ensure((size_t)std::max<int64_t>(T, 1)));
-    HIP_TRY(sort_keys(src, sorted.p, (size_t)T, tmp, stream));
-    std::vector<int64_t> idx(m);
-    for (int j = 0; j < m; ++j) {
-      int64_t before = 0;
-      for (const auto& s : sel) {
-        if (s.first == tg[j].prefix) break;
-        before += s.second;
-      }
-      idx[j] = before + tg[j].q;
-    }
-    HIP_TRY(didx.ensure(m));
-    HIP_TRY(hipMemcpyAsync(didx.p, idx.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream));
-    hipLaunchKernelGGL(select_pick, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
-                       sorted.p, didx.p, (int64_t)m, out_dev);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(stream));  // the host vectors above die here
-    return DQ_OK;
+    // the next pass: the selected bins' prefixes, as many digit bits as the bins allow
+    cur.clear();
+    for (const auto& s : sel) cur.push_back(s.first);
+    const int A = (int)cur.size();
+    int D = 1;
+    while (D < 64 - bits && ((int64_t)A << (D + 1)) <= kSelBins) ++D;
+    dq_status rs = ps.run(src, cur, bits, D, p);
+    if (rs != DQ_OK) return rs;
   }
 }
 
@@ -455,57 +650,44 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   *n_out = 0;
   *count_out = 0;
   if (rows == 0) return DQ_OK;
-  // through the engine's device cache (dev_alloc): reused across columns, released on OOM
-  DevBuf<uint64_t> keys, sorted;
-  DevBuf<double> picks;
-  DevBuf<unsigned long long> cur, hist;
-  DevBuf<uint32_t> partial, mask;
-  DevBuf<uint8_t> tmp;
-  // pass 1: the count and the keys' top-kQ0Bits histogram, straight from the columns
-  constexpr int kHistBlocks = 512;
-  HIP_TRY(hist.ensure(kQ0Bins));
-  HIP_TRY(partial.ensure((size_t)kHistBlocks * kQ0Bins));
-  HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)kQ0Bins * 8, stream));
-  for (int b = 0; b < n_batches; ++b) {
-    const dq_column& c = batches[b];
-    if (!c.length) continue;
-    const unsigned g = grid_of(c.length, 256 * 8 * 4, kHistBlocks);
-    hipLaunchKernelGGL(quantile_hist0, dim3(g), dim3(256), 0, stream, c.type, c.validity, c.values,
-                       c.length, partial.p);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(quantile_hist0_sum, dim3(kQ0Bins / 256), dim3(256), 0, stream, partial.p, (int)g,
-                       hist.p);
-    HIP_TRY(hipGetLastError());
-  }
-  std::vector<unsigned long long> h0(kQ0Bins);
-  HIP_TRY(hipMemcpyAsync(h0.data(), hist.p, (size_t)kQ0Bins * 8, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
+  // pass 0 over the columns: the count and the keys' top bits (through the engine's device cache:
+  // buffers reused across columns, released on OOM)
+  Source col;
+  col.type = batches[0].type;
+  for (int b = 0; b < n_batches; ++b)
+    if (batches[b].length) col.parts.push_back(Src{batches[b].validity, batches[b].values, batches[b].length, 0});
+  col.cut(rows);
+  Passer ps;
+  ps.st = stream;
+  Pass p;
+  constexpr int kD0 = 13;
+  dq_status st = ps.run(col, std::vector<uint64_t>{0}, 0, kD0, p);
+  if (st != DQ_OK) return st;
   unsigned long long count = 0;
-  for (unsigned long long x : h0) count += x;
+  for (unsigned long long x : ps.h) count += x;
+  col.M = (int64_t)count;
   *count_out = (int64_t)count;
   if (!count) return DQ_OK;
   const int64_t n = (int64_t)count <= std::max(head_values, max_values) ? (int64_t)count : max_values;
   *n_out = n;
   if (!out) return DQ_OK;  // size query only
-  HIP_TRY(picks.ensure((size_t)n));
-  HIP_TRY(cur.ensure(1));
-  HIP_TRY(hipMemsetAsync(cur.p, 0, 8, stream));
-  if (n == (int64_t)count || n > kSelMaxTargets) {  // every key, gathered and sorted
+  if (n == (int64_t)count || n > kSelMaxTargets) {  // every key, compacted and sorted
+    DevBuf<uint64_t> keys, sorted;
+    DevBuf<uint8_t> tmp;
+    DevBuf<double> picks;
     HIP_TRY(keys.ensure((size_t)count));
-    for (int b = 0; b < n_batches; ++b) {
-      const dq_column& c = batches[b];
-      if (!c.length) continue;
-      hipLaunchKernelGGL(quantile_gather, dim3(grid_of(c.length, kGatherStep, 2048)),
-                         dim3(kGatherThreads), 0, stream, c.type, c.validity, c.values, c.length,
-                         keys.p, cur.p);
-      HIP_TRY(hipGetLastError());
-    }
     HIP_TRY(sorted.ensure((size_t)count));
+    HIP_TRY(picks.ensure((size_t)n));
+    const std::vector<uint32_t> all((1 << kD0) / 32, ~0u);  // (alive until the stream syncs below)
+    st = ps.compact(col, p, all, keys.p);
+    if (st != DQ_OK) return st;
     HIP_TRY(sort_keys(keys.p, sorted.p, (size_t)count, tmp, stream));
     if (n == (int64_t)count) {  // every value, sorted
-      hipLaunchKernelGGL(keys_to_doubles, dim3(grid_of(n, 256 * 16, 4096)), dim3(256), 0, stream,
-                         sorted.p, n, picks.p);
+      hipLaunchKernelGGL(keys_to_doubles, dim3((unsigned)std::min<int64_t>((n + 4095) / 4096, 4096)), dim3(256),
+                         0, stream, sorted.p, n, picks.p);
       HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
+      HIP_TRY(hipStreamSynchronize(stream));
     } else {  // many ranks: the picks of the sorted keys
       std::vector<int64_t> rank(n);
       for (int64_t j = 0; j < n; ++j) rank[j] = (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1));
@@ -515,38 +697,18 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
       hipLaunchKernelGGL(select_pick, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                          sorted.p, didx.p, n, picks.p);
       HIP_TRY(hipGetLastError());
+      HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
       HIP_TRY(hipStreamSynchronize(stream));  // rank dies here
     }
-  } else {  // the values at the ranks floor(j (count - 1) / (n - 1)), by radix select
-    // every rank's bin of pass 1 (ranks ascend, so one sweep), and the bins' keys gathered
-    std::vector<Target> tg(n);
-    std::vector<uint32_t> bm(kQ0Bins / 32, 0u);
-    int64_t below = 0, T = 0;
-    int d = 0;
-    for (int64_t j = 0; j < n; ++j) {
-      const int64_t r = (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1));
-      while (r >= below + (int64_t)h0[d]) below += (int64_t)h0[d++];
-      tg[j] = Target{(uint64_t)d, r - below};
-      if (!((bm[d >> 5] >> (d & 31)) & 1u)) {
-        bm[d >> 5] |= 1u << (d & 31);
-        T += (int64_t)h0[d];
-      }
-    }
-    HIP_TRY(keys.ensure((size_t)T));
-    HIP_TRY(mask.ensure(kQ0Bins / 32));
-    HIP_TRY(hipMemcpyAsync(mask.p, bm.data(), (kQ0Bins / 32) * 4, hipMemcpyHostToDevice, stream));
-    for (int b = 0; b < n_batches; ++b) {
-      const dq_column& c = batches[b];
-      if (!c.length) continue;
-      hipLaunchKernelGGL(quantile_compact0, dim3(grid_of(c.length, kGatherStep, 2048)),
-                         dim3(kGatherThreads), 0, stream, c.type, c.validity, c.values, c.length,
-                         mask.p, keys.p, cur.p);
-      HIP_TRY(hipGetLastError());
-    }
-    const dq_status st = radix_select(keys.p, T, std::move(tg), kQ0Bits, picks.p, stream);
-    if (st != DQ_OK) return st;
+    return DQ_OK;
   }
-  HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
+  // the values at the ranks floor(j (count - 1) / (n - 1)), by radix select from pass 0
+  std::vector<Target> tg(n);
+  for (int64_t j = 0; j < n; ++j)
+    tg[j] = Target{0, (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1)), (int)j};
+  std::vector<double> res(n);
+  st = radix_select(col, ps, p, std::move(tg), res);
+  if (st != DQ_OK) return st;
+  memcpy(out, res.data(), (size_t)n * 8);
   return DQ_OK;
 }
