@@ -109,6 +109,7 @@ def _load() -> ctypes.CDLL:
         "dq_column_release": (None, [POINTER(dq_column)]),
         "dq_java_double_to_string": (c_int, [c_double, c_char_p]),
         "dq_java_float_to_string": (c_int, [c_float, c_char_p]),
+        "dq_java_doubles_to_strings": (None, [c_void_p, c_int64, c_int, c_void_p, c_void_p]),
         "dq_freq_create": (c_int, [c_int, c_int, POINTER(c_int32), c_int64, POINTER(c_void_p)]),
         "dq_freq_destroy": (None, [c_void_p]),
         "dq_freq_reset": (c_int, [c_void_p, c_void_p]),
@@ -165,7 +166,7 @@ EXPORTED = [
     "dq_plan_destroy", "dq_plan_explain", "dq_plan_launches_per_batch", "dq_state_create",
     "dq_state_destroy", "dq_state_reset", "dq_scan_device", "dq_scan_device_batches",
     "dq_state_sync", "dq_state_get", "dq_state_get_all", "dq_state_merge", "dq_state_serialized_size",
-    "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_column_release", "dq_java_double_to_string", "dq_java_float_to_string", "dq_freq_create",
+    "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_column_release", "dq_java_double_to_string", "dq_java_float_to_string", "dq_java_doubles_to_strings", "dq_freq_create",
     "dq_freq_destroy", "dq_freq_reset", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_summarize_keys", "dq_sorted_sample", "dq_freq_marginal", "dq_freq_mutual_information", "dq_freq_num_groups", "dq_freq_null_literal", "dq_freq_import", "dq_cast_utf8", "dq_release_cached_memory",
     "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge", "dq_freq_topk", "dq_loader_create",
     "dq_loader_destroy", "dq_loader_stage", "dq_loader_release", "dq_scan_host",
@@ -202,6 +203,19 @@ def java_double_to_string(d: float) -> str:
     buf = ctypes.create_string_buffer(32)
     n = lib.dq_java_double_to_string(d, buf)
     return buf.raw[:n].decode("ascii")
+
+
+def java_doubles_to_strings(values, is_float: bool = False) -> list:
+    """java_double_to_string (java_float_to_string) of many values in one call."""
+    import numpy as np
+    v = np.ascontiguousarray(values, np.float64)
+    n = len(v)
+    out = np.zeros(max(1, n) * 32, np.uint8)
+    lens = np.zeros(max(1, n), np.int32)
+    lib.dq_java_doubles_to_strings(v.ctypes.data, n, 1 if is_float else 0, out.ctypes.data,
+                                   lens.ctypes.data)
+    data = out.tobytes()
+    return [data[32 * i: 32 * i + ln].decode("ascii") for i, ln in enumerate(lens[:n].tolist())]
 
 
 def java_float_to_string(f: float) -> str:

@@ -118,8 +118,38 @@ class FrequencyTable:
         return counts[:n.value], offs[:n.value + 1], raw[:need.value]
 
     def decode_groups(self, counts, offs, raw) -> List[Tuple[tuple, int]]:
+        n = len(counts)
+        if n and len(self.key_types) == 1:
+            return list(zip(self._decode_one_key(n, offs, raw), counts[:n].tolist()))
         data = bytes(raw)
-        return [(self._decode(data, int(offs[g])), int(counts[g])) for g in range(len(counts))]
+        return [(self._decode(data, int(offs[g])), int(counts[g])) for g in range(n)]
+
+    def _decode_one_key(self, n: int, offs, raw) -> list:
+        """The keys of a one-column table's encoded groups, decoded with array operations (the
+        per-key struct unpacking of _decode held Histogram's host side for ~1 ms per 1000 keys).
+        Same values as _decode."""
+        t = self.key_types[0]
+        data = bytes(raw)
+        words = np.frombuffer(data[: len(data) // 4 * 4], np.uint32)
+        at = np.asarray(offs[:n], np.int64) // 4  # encodings start 4-byte aligned
+        last = len(words) - 1
+        tags = words[at]
+        w1 = words[np.minimum(at + 1, last)]
+        if t == N.UTF8:
+            starts = (4 * at + 8).tolist()
+            return [(data[b: b + ln].decode("utf-8", "replace"),) if tg else (None,)
+                    for b, ln, tg in zip(starts, w1.tolist(), tags.tolist())]
+        w2 = words[np.minimum(at + 2, last)]
+        bits = w1.astype(np.uint64) | (w2.astype(np.uint64) << np.uint64(32))
+        if t == N.FLOAT64:
+            vals = bits.view(np.float64).tolist()
+        elif t == N.FLOAT32:
+            vals = w1.view(np.float32).astype(np.float64).tolist()
+        elif t == N.BOOL:
+            vals = (bits != 0).tolist()
+        else:
+            vals = bits.view(np.int64).tolist()
+        return [(v,) if tg else (None,) for v, tg in zip(vals, tags.tolist())]
 
     def _decode(self, data: bytes, pos: int) -> tuple:
         key = []
@@ -553,11 +583,13 @@ def _fold_null_group(frequencies, dtype: int, k: int):
     that count among the device top-N (ties in any order, like rdd.top)."""
     raw = frequencies.topk(k + 2)  # up to two raw entries fold into one
     nullg, lit = frequencies.null_literal()  # (after topk: the same finalize serves both)
-    top = []
-    for (key,), c in raw:
-        if key is None or (dtype == N.UTF8 and key == NULL_FIELD_REPLACEMENT):
-            continue
-        top.append((cast_to_string(key, dtype), c))
+    kept = [(key, c) for (key,), c in raw
+            if not (key is None or (dtype == N.UTF8 and key == NULL_FIELD_REPLACEMENT))]
+    if dtype in (N.FLOAT64, N.FLOAT32):  # Double/Float.toString of every key in one call
+        texts = N.java_doubles_to_strings([k for k, _ in kept], dtype == N.FLOAT32)
+        top = [(s, c) for s, (_, c) in zip(texts, kept)]
+    else:
+        top = [(cast_to_string(k, dtype), c) for k, c in kept]
     folded = nullg + lit
     if folded:
         at = next((i for i, (_, c) in enumerate(top) if c < folded), len(top))

@@ -1589,6 +1589,12 @@ extern "C" int dq_java_double_to_string(double value, char* buf) {
 extern "C" int dq_java_float_to_string(float value, char* buf) {
   return jfmt::float_to_java(value, buf);
 }
+extern "C" void dq_java_doubles_to_strings(const double* values, int64_t n, int is_float, char* out,
+                                           int32_t* lens) {
+  for (int64_t i = 0; i < n; ++i)
+    lens[i] = is_float ? jfmt::float_to_java((float)values[i], out + 32 * i)
+                       : jfmt::double_to_java(values[i], out + 32 * i);
+}
 
 // Bitmaps re-based for sliced Arrow arrays, owned by the library until dq_column_release.
 namespace {

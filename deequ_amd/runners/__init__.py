@@ -138,21 +138,32 @@ class AnalysisRunner:
             previous = opts.metrics_repository.load_by_key(
                 opts.reuse_existing_results_for_key) or AnalyzerContext.empty()
         already = set(previous.metric_map.keys())
-        # dedupe preserving order (case classes: equal analyzers run once)
+        # dedupe preserving order (case classes: equal analyzers run once); by hash, not by list
+        # scans (O(n^2) dataclass comparisons were ~20 ms of host time per configs[4] run)
         to_run: List[Analyzer] = []
-        for a in analyzers:
-            if a not in already and a not in to_run:
-                to_run.append(a)
+        try:
+            seen = set(already)
+            for a in analyzers:
+                if a not in seen:
+                    seen.add(a)
+                    to_run.append(a)
+        except TypeError:  # an analyzer that does not hash: compare by equality
+            to_run = []
+            for a in analyzers:
+                if a not in already and a not in to_run:
+                    to_run.append(a)
         if opts.fail_if_results_for_reusing_missing and to_run:
             raise ReusingNotPossibleResultsMissingException(
                 "Could not find all necessary results in the MetricsRepository, the calculation of "
                 f"the metrics for these analyzers would be needed: {', '.join(map(str, to_run))}")
         schema = data.schema
-        passed = [a for a in to_run if Preconditions.find_first_failing(schema, a.preconditions()) is None]
-        failed = [a for a in to_run if a not in passed]
+        passed, failed = [], []
+        for a in to_run:
+            ok = Preconditions.find_first_failing(schema, a.preconditions()) is None
+            (passed if ok else failed).append(a)
         precondition_failures = _precondition_failure_metrics(failed, schema)
         grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]
-        scanning = [a for a in passed if a not in grouping]
+        scanning = [a for a in passed if not isinstance(a, GroupingAnalyzer)]
         groups: Dict[tuple, List[Analyzer]] = {}
         for a in grouping:
             groups.setdefault(tuple(sorted(a.grouping_columns())), []).append(a)
@@ -168,9 +179,10 @@ class AnalysisRunner:
             hist_jobs.append(functools.partial(_histogram_and_grouping_job, data, col, hists,
                                                groups.pop((col,)), aggregate_with,
                                                save_states_with))
-        scanning = [a for a in scanning if not (isinstance(a, Histogram) and a.column in hist_cols)]
+        hist_set = set(hist_cols)
+        scanning = [a for a in scanning if not (isinstance(a, Histogram) and a.column in hist_set)]
         shareable = [a for a in scanning if isinstance(a, ScanShareableAnalyzer)]
-        others = [a for a in scanning if a not in shareable]
+        others = [a for a in scanning if not isinstance(a, ScanShareableAnalyzer)]
         scan_jobs = [functools.partial(_run_scanning_analyzers, data, shareable, aggregate_with,
                                        save_states_with)] + \
             [functools.partial(_run_scanning_analyzers, data, [a], aggregate_with, save_states_with)

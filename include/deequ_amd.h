@@ -291,6 +291,10 @@ uint64_t dq_xxhash64(const void* data, int64_t nbytes, uint64_t seed);
  * returns the length. */
 int dq_java_double_to_string(double value, char* buf);
 int dq_java_float_to_string(float value, char* buf);
+/* The same for n values at once (Histogram's keys of a floating-point column): value i's text at
+ * out + 32 i, its length in lens[i]; is_float: Float.toString of (float) values[i]. */
+void dq_java_doubles_to_strings(const double* values, int64_t n, int is_float, char* out,
+                                int32_t* lens);
 
 /* ------------------------------------------------------------------------------------------------
  * Frequency path: hash group-by (FrequencyBasedAnalyzer.computeFrequencies) on the GPU.

@@ -70,3 +70,16 @@ def test_formatted_strings_read_back():
     for v in _doubles(rng, 20000):
         if math.isfinite(v):
             assert float(N.java_double_to_string(v)) == v
+
+
+def test_batch_formatter_matches_one_value_calls():
+    """dq_java_doubles_to_strings (Histogram's keys of a floating-point column in one call) gives
+    each value's dq_java_double_to_string / dq_java_float_to_string text."""
+    rng = random.Random(5)
+    vals = [0.0, -0.0, 1.0, 1e7, 1e-3, 123456789.125, float("inf"), float("-inf"), float("nan"),
+            5e-324, 1.7976931348623157e308] + [rng.uniform(-1e9, 1e9) for _ in range(300)]
+    assert N.java_doubles_to_strings(vals) == [N.java_double_to_string(v) for v in vals]
+    with np.errstate(over="ignore"):
+        fl = np.array(vals, np.float64).astype(np.float32).astype(np.float64).tolist()
+    assert N.java_doubles_to_strings(fl, True) == [N.java_float_to_string(v) for v in fl]
+    assert N.java_doubles_to_strings([]) == []
