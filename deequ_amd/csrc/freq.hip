@@ -57,6 +57,7 @@ constexpr int kBuckets = 1 << kBucketBits;
 constexpr int kHistRow = kBuckets + 1;  // u16 exclusive bucket prefix of a chunk + its total
 constexpr int kThreads = 1024;
 constexpr int kMaxSubBits = 10;
+constexpr int kMinPkSubBits = 7;  // packed phase-C slots need a partition of >= 9 + 7 fixed bits
 constexpr int kFilterShift = 32;        // hash bits that split an overflowing partition
 constexpr int kCand = 4;                // top groups kept per partition for Histogram
 constexpr int kSmallCounts = 64;        // phase C histograms group counts below this
@@ -64,7 +65,10 @@ constexpr int kMaxParts = 64;
 constexpr uint64_t kEmptyKey = ~0ULL;
 constexpr uint64_t kNotReady = ~0ULL;
 
-enum Counter { C_NULL_ROWS = 0, C_NULL_GROUP, C_COLLISIONS, C_DBG_NOTREADY, C_DBG_DIFF, C_DBG_FULL, C_DBG_BYPASS, C_N };
+// C_MAXCNT: an upper bound of the count any phase-A record carries (packed phase-C slots at
+// fewer than kMaxSubBits sub-bits need every record count below 2^(s-3); merges add the bounds)
+enum Counter { C_NULL_ROWS = 0, C_NULL_GROUP, C_COLLISIONS, C_DBG_NOTREADY, C_DBG_DIFF, C_DBG_FULL, C_DBG_BYPASS,
+               C_MAXCNT, C_N };
 
 template <bool HASHED>
 struct FM;
@@ -178,6 +182,14 @@ DQ_DEV double block_sum_f64(double v, double* s) {
 DQ_DEV void wave_count(unsigned long long* counter, unsigned long long v) {
   v = wave_sum(v);
   if (__lane_id() == 0 && v) atomicAdd(counter, v);
+}
+extern "C" __device__ uint64_t __ockl_wfred_max_u64(uint64_t);
+// A workgroup's largest record count into an LDS word, only when it could bar packed slots
+// (>= 16 = 2^(7-3)); the workgroup then makes one global atomic (one per wave on one address
+// serialised phase A over records: 9.4 -> 50 ms per configs[4] run)
+DQ_DEV void wave_max_lds(unsigned long long* s_slot, uint64_t v) {
+  v = __ockl_wfred_max_u64(v);
+  if (__lane_id() == 0 && v >= 16) atomicMax(s_slot, (unsigned long long)v);
 }
 
 // last index j in [0, n) with pos[j] <= x (pos non-decreasing, pos[0] = 0 <= x)
@@ -447,10 +459,13 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     }
   }
   unsigned long long nulls = 0, nullg = 0;
+  uint64_t maxcnt = 1;  // the largest count a record of this workgroup carries (row records: 1)
   // debug event counts (rare events) in LDS: dedupe is an out-of-line lambda, and locals it
   // updated through its captures lived in scratch
   __shared__ uint32_t s_dbg[3];  // not-ready retries, hash collisions, table full
+  __shared__ unsigned long long s_maxcnt;
   if (tid < 3) s_dbg[tid] = 0;
+  if (tid == 0) s_maxcnt = 0;
   unsigned long long dbg_bypass = 0;
 
   // Counting sort of a chunk's records: bucket counts are in bh; begin_chunk scans them, writes
@@ -485,9 +500,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   auto put = [&](int64_t chunk, uint64_t h, uint32_t code, uint64_t rep) {
     const uint32_t pos = atomicAdd(&bcur[bucket_of(h)], 1u);
     uint64_t* out = reinterpret_cast<uint64_t*>(a.recs) + (chunk * (int64_t)T + pos) * W;
-    if constexpr (HASHED) {
-      out[0] = h;
-      out[1] = (rep << 8) | code;
+    if constexpr (HASHED) {  // one 16-byte store (records are 16-byte aligned)
+      *reinterpret_cast<ulonglong2*>(out) = make_ulonglong2(h, (rep << 8) | code);
     } else {
       out[0] = (h << 8) | code;
     }
@@ -986,6 +1000,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         const int q = j * kThreads + tid;
         const uint64_t h = stash[q * W];
         uint64_t rep = HASHED ? stash[q * W + 1] : 0;
+        if constexpr (FROM_REC) maxcnt = scnt[tid] > maxcnt ? scnt[tid] : maxcnt;
         for_digits(FROM_REC ? scnt[tid] : 1, [&](uint32_t code) { put(t, h, code, rep); });
       }
     }
@@ -1000,9 +1015,12 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         const uint64_t k = dkey[sl];
         if (k == kEmptyKey) continue;
         const uint32_t b = bucket_of(k);
+        maxcnt = dcnt[sl] > maxcnt ? dcnt[sl] : maxcnt;
         for_digits(dcnt[sl], [&](uint32_t code) { out[atomicAdd(&wcur[b], 1u)] = (k << 8) | code; });
       }
+      wave_max_lds(&s_maxcnt, maxcnt);
       __syncthreads();
+      if (tid == 0 && s_maxcnt) atomicMax(&a.counters[C_MAXCNT], s_maxcnt);
       if (tid < kBuckets)
         a.plen[(int64_t)blockIdx.x * kBuckets + tid] =
             wcur[tid] - a.pstart[(int64_t)blockIdx.x * kBuckets + tid];
@@ -1031,13 +1049,16 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     uint64_t rep = HASHED ? drep[sl] : 0;
     if constexpr (HASHED && !FROM_REC)
       rep = arena_rep_sk((int64_t)rep, SK ? dsk0[sl] : 0, SK ? dsk1[sl] : kNoShort);
+    maxcnt = dcnt[sl] > maxcnt ? dcnt[sl] : maxcnt;
     for_digits(dcnt[sl], [&](uint32_t code) { put(fchunk, k, code, rep); });
   }
+  wave_max_lds(&s_maxcnt, maxcnt);
   if (!FROM_REC) {
     wave_count(&a.counters[C_NULL_ROWS], nulls);
     wave_count(&a.counters[C_NULL_GROUP], nullg);
   }
   __syncthreads();
+  if (tid == 0 && s_maxcnt) atomicMax(&a.counters[C_MAXCNT], s_maxcnt);
   if (tid < 3 && s_dbg[tid]) atomicAdd(&a.counters[C_DBG_NOTREADY + tid], (unsigned long long)s_dbg[tid]);
   wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
 }
@@ -1150,6 +1171,7 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
   __shared__ uint64_t stash[T];
   __shared__ uint32_t s_wave[kAXThreads / 64];
   __shared__ uint32_t s_hits, s_bypass, s_full;
+  __shared__ unsigned long long s_maxcnt;
   const int tid = threadIdx.x;
   const KeyCol& c = a.ks.cols[0];
   const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
@@ -1174,6 +1196,7 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
   if (tid == 0) {
     s_bypass = 0;
     s_full = 0;
+    s_maxcnt = 0;
   }
   unsigned long long nulls = 0, nullg = 0, dbg_bypass = 0;
   uint64_t* out = reinterpret_cast<uint64_t*>(a.recs);
@@ -1309,13 +1332,17 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
   }
   // the collapsed groups into their buckets' pieces, then the pieces' lengths
   __syncthreads();
+  uint64_t maxcnt = 1;
   for (int sl = tid; sl < D; sl += kAXThreads) {
     const uint64_t k = dkey[sl];
     if (k == kEmptyKey) continue;
     const uint32_t b = bucket_of(k);
+    maxcnt = dcnt[sl] > maxcnt ? dcnt[sl] : maxcnt;
     for_digits(dcnt[sl], [&](uint32_t code) { out[atomicAdd(&wcur[b], 1u)] = (k << 8) | code; });
   }
+  wave_max_lds(&s_maxcnt, maxcnt);
   __syncthreads();
+  if (tid == 0 && s_maxcnt) atomicMax(&a.counters[C_MAXCNT], s_maxcnt);
   a.plen[(int64_t)blockIdx.x * kBuckets + tid] = wcur[tid] - a.pstart[(int64_t)blockIdx.x * kBuckets + tid];
   wave_count(&a.counters[C_NULL_ROWS], nulls);
   wave_count(&a.counters[C_NULL_GROUP], nullg);
@@ -2343,19 +2370,25 @@ struct CBounds {
   uint32_t p, f, fv;
   uint64_t r0, r1;
 };
+// (wave-uniform reads of words phase C never writes, through the constant address space: scalar
+// loads, counted by lgkmcnt -- as vector loads, a wait for them in the next item was also a wait
+// for every vector store issued before it)
 DQ_DEV void c_bounds(const CArgs& a, int wi, CBounds& bd) {
   if (wi >= a.n_work) return;
+  using cu64 = const __attribute__((address_space(4))) uint64_t;
+  using cu32 = const __attribute__((address_space(4))) uint32_t;
   bd.f = bd.fv = 0;
   if (a.entries) {
-    const FEntry e = a.entries[wi];
-    bd.p = e.p;
-    bd.f = e.f;
-    bd.fv = e.v;
+    cu32* e = (cu32*)(size_t)(a.entries + wi);
+    bd.p = e[0];
+    bd.f = e[1];
+    bd.fv = e[2];
   } else {
     bd.p = (uint32_t)wi;
   }
-  bd.r0 = a.part_base[bd.p];
-  bd.r1 = a.part_base[bd.p + 1];
+  cu64* pb = (cu64*)(size_t)a.part_base;
+  bd.r0 = pb[bd.p];
+  bd.r1 = pb[bd.p + 1];
 }
 
 // Work item wi (bounds bd): the raw words of its first kPF * kCThreads records.
@@ -2794,18 +2827,23 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
 // the partials are added in a fixed order.  Same outputs as freq_phaseC<false>.
 // DBG: DQ_FREQ_DEBUG=2's instantiation, workgroup 0 stamps each item's phases (wall clock).
 // ------------------------------------------------------------------------------------------------
-// PK: packed slots, for tables partitioned to the full kMaxSubBits (a partition then fixes the
-// top kBucketBits + kMaxSubBits = 19 hash bits): one u64 per slot = count << 45 | the key's low 45
-// hash bits, so a claim installs key AND count in one CAS, a duplicate adds count << 45, and the
+// PK: packed slots, for tables partitioned at least kMinPkSubBits deep (a partition then fixes the
+// top kBucketBits + s >= 16 hash bits): one u64 per slot = count << KB | the key's low KB = 55 - s
+// hash bits, so a claim installs key AND count in one CAS, a duplicate adds count << KB, and the
 // table holds 8192 slots in the LDS of 4096 two-word slots (load ~0.22 instead of ~0.44: fewer
-// probe rounds, the wave's longest probe sequence bounding every round).  A count field can only
-// overflow when some record carries a count >= 128 or the partition has more than 4096 records;
-// such an item is handed on (an ovf entry of the whole partition, f = 0) to the two-word kernel.
+// probe rounds, the wave's longest probe sequence bounding every round).  A count field of 9 + s
+// bits can only overflow when some record carries a count >= 2^(s-3) (128 at s = 10) or the
+// partition has more than 4096 records; such an item is handed on (an ovf entry of the whole
+// partition, f = 0) to the two-word kernel.  (s = 7..9: the configs[4]-sized tables.)
 template <bool DBG, bool PK>
 __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
   constexpr int KT = PK ? 8192 : FM<false>::kTableC, NW = kCThreads / 64, PF = kPF<false>;
   constexpr int KL = PK ? 2 * PF * kCThreads : KT;  // list capacity
-  constexpr uint64_t M45 = (1ULL << 45) - 1;
+  // PK: the partition fixes the hash's top 9 + s bits, the slot keeps the other KB = 55 - s
+  // (45..48 for s = 10..7) under a count field of 9 + s bits
+  const int KB = 55 - (int)a.s;
+  const uint64_t MK = (1ULL << KB) - 1;
+  const uint64_t cmax = 1ULL << (a.s > 3 ? a.s - 3 : 0);  // record counts below this: no overflow
   __shared__ uint64_t tkey[KT], tcnt[PK ? 1 : KT];
   __shared__ uint16_t list[KL];
   __shared__ uint32_t s_n[2], s_ovf[2];
@@ -2839,12 +2877,14 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
 
   // Wave 0: the statistics and candidates of the item of parity q (its words stay untouched until
   // the item after next resets them, behind that item's barrier 1).
-  auto tail = [&](uint32_t q) {
+  // (wv 1 merges the candidates while wv 0 writes the statistics: neither holds up the inserts
+  // that wait at barrier 1 for the slowest wave)
+  auto tail = [&](uint32_t q, int wv) {
     const uint32_t fl = s_tfl[q];
     if (!(fl & TF_VALID)) return;
     const uint32_t p = s_tp[q], gtot = s_tg[q];
     const bool sub = (fl & TF_SUB) != 0;
-    if (fl & TF_CANDFAST) {  // the item's top kCand: rounds of wave maxima over the waves' lists
+    if ((fl & TF_CANDFAST) && wv == 1) {  // the item's top kCand: rounds of wave maxima over the waves' lists
       static_assert(NW * kCand <= 64, "one wave merges the lists");
       const bool in = lane < NW * kCand;
       const int w = in ? lane / kCand : 0, r = lane % kCand;
@@ -2870,9 +2910,10 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
         }
       }
     }
+    if (wv != 0) return;
     const uint32_t hc = lane > 1 ? s_chist[q][lane] : 0u;
     double t = hc ? (double)hc * s_term[lane] : 0.0;
-    t = __ockl_wfred_add_f64(t);
+    t = __ballot(hc != 0) ? __ockl_wfred_add_f64(t) : 0.0;  // (no counts 2..63: nothing to add)
     if (lane == 0) {
       uint64_t utot = 0;
       double etot = 0.0;
@@ -2933,9 +2974,9 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
         slot[q] = (uint32_t)h[q] & (KT - 1);
         const bool in = ((valid >> q) & 1u) && (f == 0 || ((uint32_t)(h[q] >> kFilterShift) & fmask) == fv);
         if constexpr (PK) {
-          if (in && c[q] >= 128) s_ovf[par] = 1;  // a count field could overflow: hand it on
+          if (in && c[q] >= cmax) s_ovf[par] = 1;  // a count field could overflow: hand it on
           if (in) todo |= 1u << q;
-          h[q] = (c[q] << 45) | (h[q] & M45);  // the packed word
+          h[q] = (c[q] << KB) | (h[q] & MK);  // the packed word
         } else {
           if (in && h[q] == kEmptyKey) atomicAdd(&s_spec[par], (unsigned long long)c[q]);
           else if (in) todo |= 1u << q;
@@ -2949,9 +2990,11 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       // Probe rounds with every pending record's CAS in flight together (a wave takes as many
       // rounds as its longest probe sequence, not the sum over its records); double hashing (an
       // odd step from high hash bits) keeps those sequences short.
+      // (PK: the step comes from key bits 32..44 of the packed word -- bits 45 and up are the
+      // count, and records of one key with different counts must walk the same sequence)
       uint32_t step[PF];
 #pragma unroll
-      for (int q = 0; q < PF; ++q) step[q] = ((uint32_t)(h[q] >> 40) | 1u) & (KT - 1);
+      for (int q = 0; q < PF; ++q) step[q] = ((uint32_t)(h[q] >> (PK ? 32 : 40)) | 1u) & (KT - 1);
       uint32_t mine = 0;
       for (int pr = 0; todo && pr < KT; ++pr) {
 #pragma unroll
@@ -2961,10 +3004,10 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
         for (int q = 0; q < PF; ++q) {
           if (!((todo >> q) & 1u)) continue;
           const bool claimed = old[q] == kEmptyKey;
-          const bool match = PK ? ((old[q] ^ h[q]) & M45) == 0 : old[q] == h[q];
+          const bool match = PK ? ((old[q] ^ h[q]) & MK) == 0 : old[q] == h[q];
           if (claimed || match) {
             if constexpr (PK) {
-              if (!claimed) atomicAdd((unsigned long long*)&tkey[slot[q]], (unsigned long long)(c[q] << 45));
+              if (!claimed) atomicAdd((unsigned long long*)&tkey[slot[q]], (unsigned long long)(c[q] << KB));
             } else {
               atomicAdd((unsigned long long*)&tcnt[slot[q]], (unsigned long long)c[q]);
             }
@@ -2993,19 +3036,33 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     insert_round(cur.w, too_long ? 0u : cur.valid, [&]() {
       c_fetch<false>(a, wi + gridDim.x, nb, pf);
       c_bounds(a, wi + 2 * gridDim.x, nb2);
-      if (wave == 0) tail(par ^ 1u);
     });
-    if (nrec > (uint64_t)PF * kCThreads && !too_long) {  // the rest of a long partition (rare)
+    // the last item's outputs, after this wave's inserts (its records are no longer live; the
+    // stores come after the prefetch, so the next item's wait for its records leaves them be)
+    if (wave < 2) tail(par ^ 1u, wave);
+    if (nrec > (uint64_t)PF * kCThreads && !too_long) {  // the rest of a long partition
+      // (a column of heavy values: every workgroup's records of a heavy key land in one
+      // partition) -- the next round's words in flight while this round inserts
       const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + r0;
-      for (uint64_t base = (uint64_t)PF * kCThreads; base < nrec; base += (uint64_t)PF * kCThreads) {
-        uint64_t w[PF][1];
-        uint32_t valid = 0;
+      constexpr uint64_t STEP = (uint64_t)PF * kCThreads;
+      uint64_t wn[PF][1];
+      uint32_t vn = 0;
+      auto load = [&](uint64_t base) {
+        vn = 0;
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
           const uint64_t li = base + (uint64_t)q * kCThreads + tid;
-          w[q][0] = li < nrec ? src[li] : 0ULL;
-          valid |= (li < nrec ? 1u : 0u) << q;
+          wn[q][0] = li < nrec ? src[li] : 0ULL;
+          vn |= (li < nrec ? 1u : 0u) << q;
         }
+      };
+      load(STEP);
+      for (uint64_t base = STEP; base < nrec; base += STEP) {
+        uint64_t w[PF][1];
+#pragma unroll
+        for (int q = 0; q < PF; ++q) w[q][0] = wn[q][0];
+        const uint32_t valid = vn;
+        if (base + STEP < nrec) load(base + STEP);
         insert_round(w, valid, []() {});
       }
     }
@@ -3089,8 +3146,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
           if (!PK) tcnt[sl[u]] = 0;
         }
         if (PK) {  // unpack: the partition's 19 fixed hash bits over the key's 45
-          cv[u] = kv[u] >> 45;
-          kv[u] = ((uint64_t)p << 45) | (kv[u] & M45);
+          cv[u] = kv[u] >> KB;
+          kv[u] = ((uint64_t)p << KB) | (kv[u] & MK);
         }
       }
 #pragma unroll
@@ -3104,8 +3161,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
         tkey[s] = kEmptyKey;
         if (!PK) tcnt[s] = 0;
         if (PK) {
-          c = kk >> 45;
-          kk = ((uint64_t)p << 45) | (kk & M45);
+          c = kk >> KB;
+          kk = ((uint64_t)p << KB) | (kk & MK);
         }
         if (!overflow) stat(i, kk, c);
       }
@@ -3153,7 +3210,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     }
     {
       const uint64_t wun = __ockl_wfred_add_u64(un);
-      const double we = __ockl_wfred_add_f64(e);
+      const double we = __ballot(e != 0.0) ? __ockl_wfred_add_f64(e) : 0.0;
       const uint64_t wmx = wmx1;
       if (lane == 0) {
         s_wun[par][wave] = wun;
@@ -3190,7 +3247,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
   }
   // the last item's outputs (its words were set before its barrier 2... and s_tfl after it)
   __syncthreads();
-  if (wave == 0) tail(par ^ 1u);
+  if (wave < 2) tail(par ^ 1u, wave);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3256,11 +3313,12 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
   if (tid < kSmallCounts) s_term[tid] = tid ? entropy_term((uint64_t)tid, a.num_rows) : 0.0;
   const bool keep = a.groups != nullptr;
 
-  auto tail = [&](uint32_t q) {  // wave 0: the outputs of the item of parity q
+  // waves 0 and 1: the outputs of the item of parity q (wv 1 the candidates, wv 0 the statistics)
+  auto tail = [&](uint32_t q, int wv) {
     const uint32_t fl = s_tfl[q];
     if (!(fl & TF_VALID)) return;
     const uint32_t p = s_tp[q], gtot = s_tg[q];
-    if (fl & TF_CANDFAST) {  // the item's top kCand: rounds of wave maxima over the waves' lists
+    if ((fl & TF_CANDFAST) && wv == 1) {  // the item's top kCand: rounds of wave maxima over the waves' lists
       static_assert(NW * kCand <= 64, "one wave merges the lists");
       const bool in = lane < NW * kCand;
       const int w = in ? lane / kCand : 0, r = lane % kCand;
@@ -3286,9 +3344,10 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
         }
       }
     }
+    if (wv != 0) return;
     const uint32_t hc = lane > 1 ? s_chist[q][lane] : 0u;
     double t = hc ? (double)hc * s_term[lane] : 0.0;
-    t = __ockl_wfred_add_f64(t);
+    t = __ballot(hc != 0) ? __ockl_wfred_add_f64(t) : 0.0;  // (no counts 2..63: nothing to add)
     if (lane == 0) {
       uint64_t utot = 0;
       double etot = 0.0;
@@ -3449,8 +3508,10 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
     insert_round(cur.w, too_long ? 0u : cur.valid, [&]() {
       c_fetch<true>(a, wi + gridDim.x, nb, pf);
       c_bounds(a, wi + 2 * gridDim.x, nb2);
-      if (wave == 0) tail(par ^ 1u);
     });
+    // the last item's outputs, after this wave's inserts (its records are no longer live; the
+    // stores come after the prefetch, so the next item's wait for its records leaves them be)
+    if (wave < 2) tail(par ^ 1u, wave);
     if (nrec > (uint64_t)PF * kCThreads && !too_long) {  // the rest of a long partition
       const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + r0 * 2;
       for (uint64_t base = (uint64_t)PF * kCThreads; base < nrec; base += (uint64_t)PF * kCThreads) {
@@ -3598,7 +3659,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
     }
     {
       const uint64_t wun = __ockl_wfred_add_u64(un);
-      const double we = __ockl_wfred_add_f64(e);
+      const double we = __ballot(e != 0.0) ? __ockl_wfred_add_f64(e) : 0.0;
       const uint64_t wmx = wmx1;
       if (lane == 0) {
         s_wun[par][wave] = wun;
@@ -3629,7 +3690,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
     nb = nb2;
   }
   __syncthreads();
-  if (wave == 0) tail(par ^ 1u);
+  if (wave < 2) tail(par ^ 1u, wave);
   if (collisions) atomicAdd(&a.counters[C_COLLISIONS], collisions);
 }
 
@@ -4428,6 +4489,14 @@ static dq_status launch_reduce(dq_freq* f, int64_t P) {
 }
 
 // ---- finalize: phase C ------------------------------------------------------------------------
+// Packed phase-C slots for this table's first pass: at the full depth always (a partition whose
+// count field could overflow is handed on); at 7..9 sub-bits only when no record count reaches
+// 2^(s-3) (a column of heavy values would hand on nearly every partition: two passes)
+static bool pk_ok(const dq_freq* f) {
+  if (f->s_bits == kMaxSubBits) return true;
+  return f->s_bits >= kMinPkSubBits && f->h_counters[C_MAXCNT] < (1ULL << (f->s_bits - 3));
+}
+
 static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
   bool reduced = false;  // f->red already holds this pass's sums
   dq_status st = finalize_b(f);
@@ -4511,7 +4580,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     }();
     for (int round = 0; round < 24; ++round) {
       // packed slots: the first pass of a table partitioned to the full depth (19 fixed bits)
-      const bool pk = round == 0 && f->s_bits == kMaxSubBits && !no_pk;
+      const bool pk = round == 0 && pk_ok(f) && !no_pk;
       if (f->exact && !old_c && clk && pk)
         hipLaunchKernelGGL((freq_phaseC_x<true, true>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else if (f->exact && !old_c && clk)
@@ -4587,7 +4656,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       // recount the overflowing partitions over disjoint hash subsets
       // (a packed-slot first pass hands whole partitions on: no hash subsets yet)
       // (so does the hashed first pass)
-      if (!(round == 0 && f->s_bits == kMaxSubBits && !no_pk && f->exact && !old_c) &&
+      if (!(round == 0 && pk_ok(f) && !no_pk && f->exact && !old_c) &&
           !(round == 0 && !f->exact && !old_hc))
         f->recounted = true;
       f->ovf_a.swap(f->ovf_b);  // ovf_b = this round's entries
@@ -4693,6 +4762,32 @@ __global__ void freq_project(const Group* __restrict__ g, int64_t n, const uint8
   out[i] = r;
 }
 
+// Both marginals' records of a two-key table's groups in one pass over the groups and the arena
+// (freq_project for key 0 and key 1).
+__global__ void freq_project2(const Group* __restrict__ g, int64_t n, const uint8_t* __restrict__ arena,
+                              PartTypes t, RecIn* __restrict__ out0, RecIn* __restrict__ out1) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Group gi = g[i];
+  const uint32_t* enc = reinterpret_cast<const uint32_t*>(arena + gi.rep);
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    RecIn r;
+    r.count = gi.count;
+    r.enc_off = gi.rep + 4ull * w;
+    const uint32_t tag = enc[w];
+    if (t.types[k] == DQ_UTF8) {
+      r.key = enc_str_hash(enc + w);
+      w += tag ? 2 + pad4(enc[w + 1]) / 4 : 1;
+    } else {
+      r.key = (uint64_t)enc[w + 1] | ((uint64_t)enc[w + 2] << 32);
+      w += tag ? 3 : 1;
+    }
+    (k ? out1 : out0)[i] = r;
+  }
+}
+
 // ---- MutualInformation (MutualInformation.scala:41-84) -----------------------------------------
 // Column k's part of an encoded multi-key group key.
 DQ_DEV const uint32_t* enc_part(const uint32_t* enc, const PartTypes& t, int k) {
@@ -4758,6 +4853,44 @@ __global__ void freq_mi_terms(const Group* __restrict__ gj, int64_t n, const uin
   const uint32_t* ey = enc_part(enc, t, 1);
   const double px = (double)lookup_count(X, ex, gj[i].rep + 4ull * (uint64_t)(ex - enc));
   const double py = (double)lookup_count(Y, ey, gj[i].rep + 4ull * (uint64_t)(ey - enc));
+  const double pxy = (double)gj[i].count;
+  terms[i] = (pxy / total) * log((pxy / total) / ((px / total) * (py / total)));
+}
+
+// A marginal's groups by row hash, for a table with no two keys on one 64-bit hash (its phase C
+// counted no collision): slot = {row hash, count}, count 0 = empty, so a lookup is one probe
+// sequence with no key bytes compared.
+struct CountSlot {
+  unsigned long long h, count;
+};
+__global__ void freq_count_index(const Group* __restrict__ g, int64_t n, uint64_t mask,
+                                 CountSlot* __restrict__ slots) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Group gi = g[i];
+  uint64_t s = gi.h & mask;
+  while (atomicCAS(&slots[s].count, 0ULL, (unsigned long long)gi.count) != 0ULL) s = (s + 1) & mask;
+  slots[s].h = gi.h;
+}
+DQ_DEV uint64_t count_of(const CountSlot* __restrict__ slots, uint64_t mask, uint64_t h) {
+  for (uint64_t s = h & mask;; s = (s + 1) & mask) {
+    const CountSlot c = slots[s];
+    if (c.h == h || c.count == 0) return c.count;  // (count 0: not reachable, every joint value has its group)
+  }
+}
+// freq_mi_terms with both marginals looked up by the row hashes the projection computed (exact
+// keys: the bijective hash of the value), same arithmetic and order
+__global__ void freq_mi_terms_h(const Group* __restrict__ gj, int64_t n, const RecIn* __restrict__ r0,
+                                const RecIn* __restrict__ r1, int exact0, int exact1,
+                                const CountSlot* __restrict__ s0, uint64_t m0,
+                                const CountSlot* __restrict__ s1, uint64_t m1, double total,
+                                double* __restrict__ terms) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h0 = exact0 ? fmix_bij(r0[i].key) : r0[i].key;
+  const uint64_t h1 = exact1 ? fmix_bij(r1[i].key) : r1[i].key;
+  const double px = (double)count_of(s0, m0, h0);
+  const double py = (double)count_of(s1, m1, h1);
   const double pxy = (double)gj[i].count;
   terms[i] = (pxy / total) * log((pxy / total) / ((px / total) * (py / total)));
 }
@@ -5200,29 +5333,65 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
   };
   dq_freq* marg[2] = {nullptr, nullptr};
   DevBuf<uint32_t> slots[2];
+  DevBuf<CountSlot> cslots[2];
+  uint64_t cmask[2] = {0, 0};
   Lookup L[2];
   dq_status res = DQ_OK;
+  // both marginals' records in one pass over the joint groups (kept: the lookups read their hashes)
+  DevBuf<RecIn> rec[2];
+  HIP_TRY(rec[0].ensure(n));
+  HIP_TRY(rec[1].ensure(n));
+  hipLaunchKernelGGL(freq_project2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, joint->stream,
+                     joint->compact.p, n, arena_of(joint), part_types(joint, 1), rec[0].p, rec[1].p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(joint->stream));
+  stamp("project");
+  const char* fl = getenv("DQ_FREQ_MI_LOOKUP");  // =1: the byte-compare lookups (A/B, tests)
+  const bool force_lookup = fl && atoi(fl) != 0;
+  bool by_hash = !force_lookup;  // no marginal has two keys on one 64-bit hash
   for (int k = 0; k < 2 && res == DQ_OK; ++k) {
     const int32_t ty = joint->types[k];
     res = dq_freq_create(joint->device, 1, &ty, 0, &marg[k]);
     stamp(k ? "marginal 1 create" : "marginal 0 create");
-    if (res == DQ_OK) res = marginal_of(joint, k, marg[k], hip_stream, true);
+    if (res == DQ_OK) {
+      const int64_t rc[1] = {n};
+      const int64_t vb[1] = {(int64_t)((joint->arena_used + 7) & ~7ULL)};
+      const int64_t special[3] = {0, 0, (int64_t)joint->h_counters[C_NULL_ROWS]};
+      res = add_records(marg[k], reinterpret_cast<const dq_freq_record*>(rec[k].p), arena_of(joint), 1, rc,
+                        vb, joint->num_rows, special, 0, hip_stream, !marg[k]->exact);
+    }
     stamp(k ? "marginal 1 records" : "marginal 0 records");
     if (res == DQ_OK) res = compact_groups(marg[k]);
     stamp(k ? "marginal 1 groups" : "marginal 0 groups");
     if (res != DQ_OK) break;
+    if (marg[k]->h_counters[C_COLLISIONS]) by_hash = false;
+  }
+  for (int k = 0; k < 2 && res == DQ_OK; ++k) {
+    const int32_t ty = joint->types[k];
     const int64_t m = marg[k]->n_compact;
     uint64_t cap = 2;
     while (cap < (uint64_t)(2 * m)) cap <<= 1;
-    if (slots[k].ensure(cap) != hipSuccess || hipMemsetAsync(slots[k].p, 0, cap * 4, stream) != hipSuccess) {
-      res = fail(DQ_ERR_OUT_OF_MEMORY, "marginal index");
-      break;
+    if (by_hash) {
+      cmask[k] = cap - 1;
+      if (cslots[k].ensure(cap) != hipSuccess ||
+          hipMemsetAsync(cslots[k].p, 0, cap * sizeof(CountSlot), stream) != hipSuccess) {
+        res = fail(DQ_ERR_OUT_OF_MEMORY, "marginal index");
+        break;
+      }
+      if (m)
+        hipLaunchKernelGGL(freq_count_index, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
+                           marg[k]->compact.p, m, cap - 1, cslots[k].p);
+    } else {
+      if (slots[k].ensure(cap) != hipSuccess || hipMemsetAsync(slots[k].p, 0, cap * 4, stream) != hipSuccess) {
+        res = fail(DQ_ERR_OUT_OF_MEMORY, "marginal index");
+        break;
+      }
+      if (m)
+        hipLaunchKernelGGL(freq_lookup_build, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
+                           marg[k]->compact.p, m, cap - 1, slots[k].p);
+      L[k] = Lookup{marg[k]->compact.p, slots[k].p, cap - 1, arena_of(marg[k]), ty, marg[k]->exact ? 1 : 0,
+                    marg[k]->rec_var_base};
     }
-    if (m)
-      hipLaunchKernelGGL(freq_lookup_build, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
-                         marg[k]->compact.p, m, cap - 1, slots[k].p);
-    L[k] = Lookup{marg[k]->compact.p, slots[k].p, cap - 1, arena_of(marg[k]), ty, marg[k]->exact ? 1 : 0,
-                  marg[k]->rec_var_base};
     stamp(k ? "marginal 1 index" : "marginal 0 index");
   }
   if (res == DQ_OK) {
@@ -5231,9 +5400,15 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
     if (terms.ensure(n) != hipSuccess || partial.ensure(kSumBlocks) != hipSuccess) {
       res = fail(DQ_ERR_OUT_OF_MEMORY, "MutualInformation terms");
     } else {
-      hipLaunchKernelGGL(freq_mi_terms, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                         joint->compact.p, n, arena_of(joint), part_types(joint, 1), L[0], L[1],
-                         (double)joint->num_rows, terms.p);
+      if (by_hash)
+        hipLaunchKernelGGL(freq_mi_terms_h, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                           joint->compact.p, n, rec[0].p, rec[1].p, marg[0]->exact ? 1 : 0,
+                           marg[1]->exact ? 1 : 0, cslots[0].p, cmask[0], cslots[1].p, cmask[1],
+                           (double)joint->num_rows, terms.p);
+      else
+        hipLaunchKernelGGL(freq_mi_terms, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                           joint->compact.p, n, arena_of(joint), part_types(joint, 1), L[0], L[1],
+                           (double)joint->num_rows, terms.p);
       stamp("terms");
       hipLaunchKernelGGL(freq_sum_f64, dim3(kSumBlocks), dim3(256), 0, stream, terms.p, n, partial.p);
       std::vector<double> h(kSumBlocks);

@@ -125,6 +125,38 @@ def test_mutual_information_matches_oracle(kinds, gpu_device):
     assert abs(got - exp) <= 1e-12 * max(1.0, abs(exp)), (got, exp)
 
 
+@pytest.mark.parametrize("kinds", [("string", "string"), ("long", "string"), ("double", "long")])
+def test_mutual_information_hash_lookups_equal_byte_lookups(kinds, gpu_device, monkeypatch):
+    """The marginal counts looked up by row hash (no two marginal keys on one 64-bit hash) give
+    the same MI as the lookups that compare key bytes (DQ_FREQ_MI_LOOKUP=1) and the oracle;
+    high-cardinality strings on both sides, ragged batches."""
+    from deequ_amd.analyzers import MutualInformation
+    rng = np.random.default_rng(77)
+    n = 150_001
+
+    def col(kind, card):
+        v = rng.integers(0, card, n)
+        mask = rng.random(n) < 0.05
+        if kind == "string":
+            return pa.array([None if m else f"key-{x}-{x * 7919 % 1000}" for x, m in zip(v, mask)],
+                            pa.string())
+        if kind == "double":
+            return pa.array(v * 0.25, mask=mask, type=pa.float64())
+        return pa.array(v, mask=mask, type=pa.int64())
+    from oracle.deequ_oracle import OTable, mutual_information
+    a, b = col(kinds[0], 60_000), col(kinds[1], 40)
+    df = _df({"a": a, "b": b}, gpu_device, 50_000)
+    fast = MutualInformation("a", "b").calculate(df).value.get()
+    monkeypatch.setenv("DQ_FREQ_MI_LOOKUP", "1")
+    slow = MutualInformation("a", "b").calculate(df).value.get()
+    # (each run builds its own joint table: the groups' order, and so the last bits of the
+    # fixed-order sum, may differ; the terms themselves are the same function of the counts)
+    assert abs(fast - slow) <= 1e-12 * abs(slow), (fast, slow)
+    exp = mutual_information(OTable({"a": a.to_pylist(), "b": b.to_pylist()},
+                                    {"a": kinds[0], "b": kinds[1]}), "a", "b")
+    assert abs(fast - exp) <= 1e-12 * max(1.0, abs(exp)), (fast, exp)
+
+
 def test_mutual_information_of_merged_states(gpu_device):
     """FrequenciesAndNumRows.sum (GroupingAnalyzers.scala:128-148) then MutualInformation."""
     from deequ_amd.analyzers import MutualInformation

@@ -324,6 +324,37 @@ def test_packed_phase_c_hands_on_heavy_partitions(heavy, gpu_device, monkeypatch
     assert {k[0]: c for k, c in ft.export()} == exp
 
 
+@pytest.mark.parametrize("target", ["100", "45", "20", "4"])  # s = 7, 8, 9, 10 sub-bits
+def test_packed_slots_mixed_counts_of_one_key(target, gpu_device, monkeypatch):
+    """Packed phase-C slots (s = 7..10 sub-bits) with one key arriving as records of different
+    counts in one partition (a run of the key collapsed in phase A's LDS table, plus a single
+    copy elsewhere): every record of a key must probe the same slot sequence (the double-hashing
+    step comes from key bits, never from the count field), or a key splits into two groups.
+    Bar: the oracle's group count, unique count, entropy and top counts."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    monkeypatch.setenv("DQ_FREQ_PARTITION_TARGET", target)
+    rng = np.random.default_rng(int(target))
+    keys = rng.permutation(3_000_000).astype(np.int64) * 7 + 1
+    runs = rng.integers(1, 4, len(keys))
+    ids = np.repeat(keys, runs)
+    extra = rng.choice(keys, 1_000_000, replace=False)
+    ids = np.concatenate([ids, extra])
+    df = Table.from_arrow(pa.table({"id": pa.array(ids)}), device=gpu_device, max_batch_rows=1 << 21)
+    ft = FrequencyTable(["id"], [df.schema["id"].dtype], 0)
+    for b in df.batches:
+        ft.add([b["id"]])
+    _, cnt = np.unique(ids, return_counts=True)
+    s = ft.summarize()
+    assert s.n_groups == len(cnt)
+    assert s.n_unique == int((cnt == 1).sum())
+    n = len(ids)
+    ent = -math.fsum(((cnt / n) * np.log(cnt / n)).tolist())
+    assert abs(s.entropy - ent) <= 1e-12 * abs(ent)
+    top = ft.topk(8)
+    assert [c for _, c in top] == sorted(cnt.tolist(), reverse=True)[:8]
+
+
 @pytest.mark.parametrize("col,nulls", [("id", 0.05), ("id", 0.0), ("s", 0.0)])
 def test_histogram_table_serves_grouping(col, nulls, gpu_device):
     """The runner groups a column once for Histogram(col) and its grouping analyzers when
