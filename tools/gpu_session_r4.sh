@@ -61,6 +61,13 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_datatype_mi.py tests/test_g
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1 &&
 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1 &&
 DQ_FREQ_DEBUG=2 timeout -k 10 300 python -u tools/bench_workloads.py c5 --steps 1 --warmup 0 > $O/dbg_c5_$T.log 2>&1
+elif [ "${PART}" = 11 ]; then
+timeout -k 10 400 python -u -m pytest tests/test_gpu_freq.py tests/test_gpu_configs4.py -x -q --timeout 200 --timeout-method thread > $O/gpu_tests_q_$T.log 2>&1 &&
+TAG=$T bash tools/gpu_s10_prof.sh &&
+TAG=$T bash tools/gpu_pmc_c3.sh &&
+timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 10 --warmup 3 > $O/wl_c4_$T.json 2>&1 &&
+timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
+timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1
 elif [ "${PART}" = 3 ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests_$T.log 2>&1 &&
 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1 &&
