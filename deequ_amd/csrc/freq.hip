@@ -2327,6 +2327,9 @@ struct CArgs {
   uint64_t lit_h;
   unsigned long long* lit_count;
   unsigned long long* dbg_clock;  // DQ_FREQ_DEBUG=2: workgroup 0's per-item stamps (wall clock)
+  // 0: groups materialise at their partition's record offset; else work item wi's groups go to
+  // groups[wi * group_stride ..] (dq_freq_topk's recount of a few partitions)
+  uint32_t group_stride;
 };
 
 // Is the encoded one-column utf8 key at p the 9-byte string "NullValue"?
@@ -3090,7 +3093,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       __syncthreads();
       gbase = s_gbase;
     }
-    const uint64_t obase = r0 + gbase;
+    const uint64_t obase = a.group_stride ? (uint64_t)wi * a.group_stride : r0 + gbase;
 
     // statistics over the list, clearing the table
     uint64_t un = 0, mx = 0;
@@ -3280,6 +3283,7 @@ DQ_DEV bool enc_equal_lean(const uint8_t* arena, uint64_t x, uint64_t y, const i
   return true;
 }
 constexpr int kCHT = 4096;   // slots
+constexpr int64_t kTopkRecountMax = 4096;  // dq_freq_topk recounts at most this many partitions
 constexpr int kCL = 4096;    // list capacity = most records per partition
 template <bool DBG>
 __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
@@ -3539,7 +3543,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
     }
     if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
     const uint32_t gtot = n;
-    const uint64_t obase = r0;
+    const uint64_t obase = a.group_stride ? (uint64_t)wi * a.group_stride : r0;
 
     uint64_t un = 0, mx = 0;
     double e = 0.0;
@@ -3824,15 +3828,23 @@ __global__ void freq_group_select(const Group* g, int64_t n, uint64_t hi_take, u
 // partitions with groups beyond their listed candidates whose last candidate beats `tau`: their
 // unlisted groups could outrank the selection
 __global__ void freq_cand_check(const Group* cand, const unsigned long long* part_groups, int64_t P,
-                                uint64_t tau, unsigned long long* bad) {
+                                uint64_t tau, unsigned long long* bad, FEntry* bad_list, int64_t cap) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
        p += (int64_t)gridDim.x * blockDim.x) {
     int filled = 0;  // places hold the partition's top groups in count order, empty ones last
     for (int r = 0; r < kCand; ++r) filled += cand[p * kCand + r].count ? 1 : 0;
     if (part_groups[p] > (unsigned long long)filled &&
-        (!filled || cand[p * kCand + filled - 1].count > tau))
-      atomicAdd(bad, 1ULL);
+        (!filled || cand[p * kCand + filled - 1].count > tau)) {
+      const unsigned long long q = atomicAdd(bad, 1ULL);
+      if ((int64_t)q < cap) bad_list[q] = FEntry{(uint32_t)p, 0, 0, 0};
+    }
   }
+}
+
+// The candidate places of the listed partitions emptied (their every group is selected instead)
+__global__ void freq_cand_clear(Group* cand, const FEntry* list, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n * kCand) cand[(uint64_t)list[i / kCand].p * kCand + i % kCand] = Group{0, 0, 0};
 }
 
 struct PartTypes {
@@ -5545,6 +5557,73 @@ extern "C" dq_status dq_freq_import(dq_freq* f, const int64_t* counts, const int
 }
 
 // Histogram's details: rdd.top(maxDetailBins)(OrderByAbsoluteCount) (Histogram.scala:78).
+// dq_freq_topk when a few partitions may hold unlisted groups that outrank the selection: those
+// partitions are counted again with every group materialised (work items of a phase-C launch,
+// group_stride slots each), and the top k are selected over the other partitions' candidates
+// plus those groups.  done = false: a partition overflowed the first-pass table, so the caller
+// takes the exact path over every group.
+static dq_status topk_recount(dq_freq* f, int k, FEntry* list, int64_t nb, std::vector<Group>& top,
+                              bool& done) {
+  done = false;
+  const int64_t P = (int64_t)kBuckets << f->s_bits;
+  const uint32_t stride = (uint32_t)(f->exact ? FM<false>::kTableC : kCHT) + 1;  // (+ the special group)
+  DevBuf<Group> all;  // [the candidates of every partition | the recounted partitions' groups]
+  const int64_t nc = P * kCand;
+  HIP_TRY(all.ensure((size_t)(nc + nb * (int64_t)stride)));
+  HIP_TRY(hipMemsetAsync(all.p + nc, 0, (size_t)nb * stride * sizeof(Group), f->stream));
+  HIP_TRY(hipMemcpyAsync(all.p, f->cand.p, (size_t)nc * sizeof(Group), hipMemcpyDeviceToDevice, f->stream));
+  hipLaunchKernelGGL(freq_cand_clear, dim3((unsigned)((nb * kCand + 255) / 256)), dim3(256), 0, f->stream,
+                     all.p, list, nb);
+  HIP_TRY(hipGetLastError());
+  CArgs a;
+  memset(&a, 0, sizeof(a));
+  a.recsB = f->recsB.p;
+  a.part_base = f->part_base.p;
+  a.s = f->s_bits;
+  a.arena = arena_of(f);
+  for (int q = 0; q < f->n_keys; ++q) a.types[q] = f->types[q];
+  a.n_keys = f->n_keys;
+  a.want_cand = 0;
+  a.num_rows = (double)f->num_rows;
+  a.entries = list;
+  a.n_work = (int32_t)nb;
+  // the statistics of these partitions are stored again with the same values; the rest of
+  // the table's state stays as the full pass left it
+  a.part_groups = f->part_groups.p;
+  a.part_unique = f->part_unique.p;
+  a.part_entropy = f->part_entropy.p;
+  a.part_off = f->part_off.p;
+  DevBuf<FEntry> ovf;
+  DevBuf<unsigned int> novf;
+  HIP_TRY(ovf.ensure(2 * (size_t)nb));
+  HIP_TRY(novf.ensure(1));
+  HIP_TRY(hipMemsetAsync(novf.p, 0, 4, f->stream));
+  a.ovf_out = ovf.p;
+  a.ovf_n = novf.p;
+  a.groups = all.p + nc;
+  a.group_stride = stride;
+  DevBuf<unsigned long long> scratch_counters;  // (collision counts of a recount: not the table's)
+  HIP_TRY(scratch_counters.ensure(C_N));
+  HIP_TRY(hipMemsetAsync(scratch_counters.p, 0, C_N * 8, f->stream));
+  a.counters = scratch_counters.p;
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, f->device);
+  const unsigned grid = (unsigned)std::min<int64_t>(nb, 2 * cus);
+  if (f->exact)
+    hipLaunchKernelGGL((freq_phaseC_x<false, false>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
+  else
+    hipLaunchKernelGGL(freq_phaseC_h<false>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
+  HIP_TRY(hipGetLastError());
+  unsigned int m = 0;
+  HIP_TRY(hipStreamSynchronize(f->stream));
+  HIP_TRY(hipMemcpy(&m, novf.p, 4, hipMemcpyDeviceToHost));
+  if (m) return DQ_OK;  // (not done)
+  dq_status st = select_top(f, all.p, nc + nb * (int64_t)stride, k, top);
+  if (st != DQ_OK) return st;
+  done = true;
+  return DQ_OK;
+}
+
 extern "C" dq_status dq_freq_topk(dq_freq* f, int k, int64_t* counts_out, int64_t* key_offsets_out,
                                   uint8_t* key_bytes_out, int64_t key_bytes_capacity, int64_t* n_out,
                                   int64_t* key_bytes_needed) {
@@ -5561,15 +5640,25 @@ extern "C" dq_status dq_freq_topk(dq_freq* f, int k, int64_t* counts_out, int64_
       if (st != DQ_OK) return st;
       const uint64_t tau = top.size() == (size_t)k && k > 0 ? top.back().count : 0;
       DevBuf<unsigned long long> bad;
+      DevBuf<FEntry> bad_list;
+      const int64_t cap = kTopkRecountMax;
       HIP_TRY(bad.ensure(1));
+      HIP_TRY(bad_list.ensure(cap));
       HIP_TRY(hipMemsetAsync(bad.p, 0, 8, f->stream));
       hipLaunchKernelGGL(freq_cand_check, dim3(grid_for(P)), dim3(256), 0, f->stream, f->cand.p,
-                         f->part_groups.p, P, tau, bad.p);
+                         f->part_groups.p, P, tau, bad.p, bad_list.p, cap);
       HIP_TRY(hipGetLastError());
       unsigned long long nb = 0;
       HIP_TRY(hipStreamSynchronize(f->stream));
       HIP_TRY(hipMemcpy(&nb, bad.p, 8, hipMemcpyDeviceToHost));
       exact_path = nb != 0;
+      const char* fe = getenv("DQ_FREQ_TOPK_EXACT");  // =1: every group (A/B, tests)
+      if (nb && (int64_t)nb <= cap && !(fe && atoi(fe))) {  // a few partitions: recount just those
+        bool done = false;
+        st = topk_recount(f, k, bad_list.p, (int64_t)nb, top, done);
+        if (st != DQ_OK) return st;
+        exact_path = !done;
+      }
     }
     if (exact_path) {  // select over every group
       st = compact_groups(f);

@@ -324,6 +324,44 @@ def test_packed_phase_c_hands_on_heavy_partitions(heavy, gpu_device, monkeypatch
     assert {k[0]: c for k, c in ft.export()} == exp
 
 
+@pytest.mark.parametrize("kind,target", [("long", None), ("long", "50"), ("string", None),
+                                         ("string", "50")])
+def test_topk_recounts_only_partitions_that_may_hold_outranking_groups(kind, target, gpu_device,
+                                                                        monkeypatch):
+    """dq_freq_topk with a flat count distribution (many groups of similar counts, so partitions
+    hold more groups than their listed candidates): the partitions whose unlisted groups could
+    outrank the selection are counted again with their groups, and the top k come from the
+    other partitions' candidates plus those groups.  Bar: the oracle's top-k counts and each
+    returned key's count, the same as the exact path (DQ_FREQ_TOPK_EXACT=1)."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    if target:
+        monkeypatch.setenv("DQ_FREQ_PARTITION_TARGET", target)
+    rng = np.random.default_rng(3 if kind == "long" else 4)
+    g = 60_000
+    cnt = rng.integers(1, 41, g)
+    keys = rng.permutation(g).astype(np.int64) * 13 + 5
+    ids = rng.permutation(np.repeat(keys, cnt))
+    col = pa.array(ids) if kind == "long" else pa.array([f"k{v}" for v in ids.tolist()])
+    df = Table.from_arrow(pa.table({"c": col}), device=gpu_device, max_batch_rows=1 << 20)
+
+    def top(k):
+        ft = FrequencyTable(["c"], [df.schema["c"].dtype], 0)
+        for b in df.batches:
+            ft.add([b["c"]])
+        return ft.topk(k)
+    exp = dict(zip(keys.tolist(), cnt.tolist()))
+    if kind == "string":
+        exp = {f"k{v}": c for v, c in exp.items()}
+    for k in (1000, 10):
+        got = top(k)
+        assert [c for _, c in got] == sorted(exp.values(), reverse=True)[:k]
+        for (key,), c in got:
+            assert exp[key] == c
+    monkeypatch.setenv("DQ_FREQ_TOPK_EXACT", "1")
+    assert [c for _, c in top(1000)] == sorted(exp.values(), reverse=True)[:1000]
+
+
 @pytest.mark.parametrize("target", ["100", "45", "20", "4"])  # s = 7, 8, 9, 10 sub-bits
 def test_packed_slots_mixed_counts_of_one_key(target, gpu_device, monkeypatch):
     """Packed phase-C slots (s = 7..10 sub-bits) with one key arriving as records of different

@@ -68,6 +68,11 @@ TAG=$T bash tools/gpu_pmc_c3.sh &&
 timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 10 --warmup 3 > $O/wl_c4_$T.json 2>&1 &&
 timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1
+elif [ "${PART}" = 12 ]; then
+timeout -k 10 400 python -u -m pytest tests/test_gpu_freq.py -x -q --timeout 200 --timeout-method thread -k "topk or Histogram or histogram" > $O/gpu_tests_k_$T.log 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1 &&
+timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1 &&
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests_$T.log 2>&1
 elif [ "${PART}" = 3 ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests_$T.log 2>&1 &&
 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1 &&
