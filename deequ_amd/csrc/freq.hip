@@ -41,6 +41,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <array>
+#include <map>
 #include <vector>
 
 #include "engine.h"
@@ -4796,7 +4798,173 @@ __global__ void freq_project2(const Group* __restrict__ g, int64_t n, const uint
       r.key = (uint64_t)enc[w + 1] | ((uint64_t)enc[w + 2] << 32);
       w += tag ? 3 : 1;
     }
-    (k ? out1 : out0)[i] = r;
+    RecIn* o = k ? out1 : out0;  // (nullptr: that side's marginal is built another way)
+    if (o) o[i] = r;
+  }
+}
+
+// ---- small marginals (MutualInformation over a low-cardinality column) ----------------------------
+// One pass over the joint groups aggregates each side's marginal in registers and LDS when the
+// side has at most kSmallMarg distinct values per wave and keys of at most 8 encoded words: a wave
+// keeps its values (row hash + encoded words), matches every group's part against them (hash and
+// words), and sums the joint counts per value with one wave reduction per value.  The host merges
+// the waves' lists by (hash, words).  A side with more values, a longer key or two values on one
+// hash is marked failed and takes the general path (a one-key table of the projected records).
+// Also writes every group's row hash of each side (hk[k][i], the hash its marginal is indexed by).
+constexpr int kSmallMarg = 16;
+struct SmallEntry {
+  unsigned long long h, count;
+  uint32_t w[8];
+};
+// A side's part of an encoded key from the 16 words loaded at the key's start: its word count,
+// its row hash (utf8 <= 16 bytes and fixed-width from the words; longer utf8 from memory) and
+// its first 8 words (a side with a longer key is not aggregated here)
+DQ_DEV void small_part(const uint32_t (&e)[16], uint32_t w, bool utf8, const uint32_t* enc, uint32_t& nw,
+                       uint64_t& h, uint32_t (&pw)[8]) {
+  uint32_t ww[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {  // e[w + j] (w <= 6 for a first side of <= 8 words... else memory)
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v = (uint32_t)q == w + (uint32_t)j ? e[q] : v;
+    ww[j] = w + (uint32_t)j < 16u ? v : enc[w + j];
+  }
+  const uint32_t tag = ww[0];
+  if (utf8) {
+    const uint32_t len = ww[1];
+    nw = tag ? 2u + pad4(len) / 4 : 1u;
+    if (!tag) {
+      h = 0;
+    } else if (len <= 16) {
+      const int nd = (int)((len + 3) >> 2);
+      uint32_t d[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[k] = k < nd ? ww[2 + k] : 0u;
+      const uint32_t tail = len & 3u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (tail && k == nd - 1) d[k] &= (1u << (8 * tail)) - 1u;
+      h = str_row_hash_reg((uint64_t)d[0] | ((uint64_t)d[1] << 32), (uint64_t)d[2] | ((uint64_t)d[3] << 32),
+                           (int32_t)len);
+    } else {
+      h = enc_str_hash(enc + w);
+    }
+  } else {
+    nw = tag ? 3u : 1u;
+    h = tag ? fmix_bij((uint64_t)ww[1] | ((uint64_t)ww[2] << 32)) : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pw[j] = (uint32_t)j < nw ? ww[j] : 0u;
+}
+
+__global__ void __launch_bounds__(256)
+freq_small_marginal(const Group* __restrict__ g, int64_t n, const uint8_t* __restrict__ arena, PartTypes t,
+                    uint32_t try_sides, unsigned long long* __restrict__ hk0, unsigned long long* __restrict__ hk1,
+                    SmallEntry* __restrict__ out, uint32_t* __restrict__ nout, unsigned int* __restrict__ fail) {
+  __shared__ unsigned long long s_h[4][2][kSmallMarg], s_c[4][2][kSmallMarg];
+  __shared__ uint32_t s_w[4][2][kSmallMarg][8];
+  constexpr int U = 2;  // groups per lane per step, every load of the step in flight together
+  const int lane = (int)__lane_id(), wave = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+  int nc[2] = {0, 0};
+  bool dead[2] = {!(try_sides & 1u), !(try_sides & 2u)};
+  for (int64_t base = gw * 64 * U; base < n; base += (int64_t)gridDim.x * 256 * U) {
+    Group gi[U];
+    bool on[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + u * 64 + lane;
+      on[u] = i < n;
+      gi[u] = g[on[u] ? i : n - 1];
+    }
+    uint32_t e[U][16];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t* enc = reinterpret_cast<const uint32_t*>(arena + gi[u].rep);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) e[u][q] = enc[q];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + u * 64 + lane;
+      const uint32_t* enc = reinterpret_cast<const uint32_t*>(arena + gi[u].rep);
+      uint32_t w = 0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        uint32_t nw, pw[8];
+        uint64_t h;
+        small_part(e[u], w, t.types[k] == DQ_UTF8, enc, nw, h, pw);
+        if (on[u]) (k ? hk1 : hk0)[i] = h;
+        if (!dead[k] && __ballot(on[u] && (!pw[0] || nw > 8u))) dead[k] = true;  // NULL part, long key
+        if (!dead[k]) {
+          int m = -1;
+          for (int c = 0; c < nc[k]; ++c) {
+            bool eq = on[u] && m < 0 && s_h[wave][k][c] == h;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) eq = eq && s_w[wave][k][c][j] == pw[j];
+            if (eq) m = c;
+          }
+          while (true) {
+            const uint64_t need = __ballot(on[u] && m < 0);
+            if (!need) break;
+            if (nc[k] == kSmallMarg) {
+              dead[k] = true;
+              break;
+            }
+            const int leader = __builtin_ctzll(need);
+            const uint64_t lh = ((uint64_t)__builtin_amdgcn_readlane((int)(h >> 32), leader) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)h, leader);
+            uint32_t lw[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) lw[j] = (uint32_t)__builtin_amdgcn_readlane((int)pw[j], leader);
+            bool clash = false;  // another value on this hash: not decidable by hash
+            for (int c = 0; c < nc[k]; ++c) clash = clash || s_h[wave][k][c] == lh;
+            if (clash) {
+              dead[k] = true;
+              break;
+            }
+            const int c = nc[k]++;
+            if (lane == 0) {
+              s_h[wave][k][c] = lh;
+              s_c[wave][k][c] = 0;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) s_w[wave][k][c][j] = lw[j];
+            }
+            bool eq = on[u] && m < 0 && h == lh;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) eq = eq && pw[j] == lw[j];
+            if (eq) m = c;
+          }
+          if (!dead[k]) {
+            for (int c = 0; c < nc[k]; ++c) {
+              const uint64_t sum = __ockl_wfred_add_u64(m == c ? gi[u].count : 0ULL);
+              if (lane == 0) s_c[wave][k][c] += sum;
+            }
+          }
+        }
+        w += nw;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int64_t slot = gw * 2 + k;
+    if (dead[k]) {
+      if (lane == 0) {
+        nout[slot] = 0u;
+        if (try_sides & (1u << k)) atomicOr(&fail[k], 1u);
+      }
+      continue;
+    }
+    if (lane < nc[k]) {
+      SmallEntry en;
+      en.h = s_h[wave][k][lane];
+      en.count = s_c[wave][k][lane];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) en.w[j] = s_w[wave][k][lane][j];
+      out[slot * kSmallMarg + lane] = en;
+    }
+    if (lane == 0) nout[slot] = (uint32_t)nc[k];
   }
 }
 
@@ -4884,25 +5052,66 @@ __global__ void freq_count_index(const Group* __restrict__ g, int64_t n, uint64_
   while (atomicCAS(&slots[s].count, 0ULL, (unsigned long long)gi.count) != 0ULL) s = (s + 1) & mask;
   slots[s].h = gi.h;
 }
-DQ_DEV uint64_t count_of(const CountSlot* __restrict__ slots, uint64_t mask, uint64_t h) {
+// Per-partition form (the marginal's phase C partitions, built in LDS, no global atomics):
+// partition p = h >> part_shift owns slots [pbase[p], pbase[p] + 2^plog[p]), probed from h's low
+// bits.  pbase == nullptr: one table of mask + 1 slots.
+struct CountIndex {
+  const CountSlot* slots;
+  uint64_t mask;
+  const unsigned long long* pbase;
+  const uint8_t* plog;
+  int part_shift;
+};
+constexpr int kIdxMaxLog = 12;  // the largest per-partition table built in LDS (64 KB)
+__global__ void __launch_bounds__(256)
+freq_count_index_parts(const Group* __restrict__ groups, const unsigned long long* __restrict__ part_off,
+                       const unsigned long long* __restrict__ part_groups, int64_t P,
+                       const unsigned long long* __restrict__ pbase, const uint8_t* __restrict__ plog,
+                       CountSlot* __restrict__ slots) {
+  __shared__ unsigned long long s_h[1 << kIdxMaxLog], s_c[1 << kIdxMaxLog];
+  for (int64_t p = blockIdx.x; p < P; p += gridDim.x) {
+    const uint32_t R = 1u << plog[p];
+    const uint64_t off = part_off[p], n = part_groups[p];
+    for (uint32_t j = threadIdx.x; j < R; j += 256) s_c[j] = 0;
+    __syncthreads();
+    for (uint64_t i = threadIdx.x; i < n; i += 256) {
+      const Group gi = groups[off + i];
+      uint32_t sl = (uint32_t)gi.h & (R - 1);
+      while (atomicCAS(&s_c[sl], 0ULL, (unsigned long long)gi.count) != 0ULL) sl = (sl + 1) & (R - 1);
+      s_h[sl] = gi.h;
+    }
+    __syncthreads();
+    CountSlot* out = slots + pbase[p];
+    for (uint32_t j = threadIdx.x; j < R; j += 256) out[j] = CountSlot{s_c[j] ? s_h[j] : 0ULL, s_c[j]};
+    __syncthreads();
+  }
+}
+DQ_DEV uint64_t count_of(const CountIndex& x, uint64_t h) {
+  const CountSlot* sl = x.slots;
+  uint64_t mask = x.mask;
+  if (x.pbase) {
+    const uint64_t p = h >> x.part_shift;
+    sl += x.pbase[p];
+    mask = (1ULL << x.plog[p]) - 1;
+  }
   for (uint64_t s = h & mask;; s = (s + 1) & mask) {
-    const CountSlot c = slots[s];
+    const CountSlot c = sl[s];
     if (c.h == h || c.count == 0) return c.count;  // (count 0: not reachable, every joint value has its group)
   }
 }
 // freq_mi_terms with both marginals looked up by the row hashes the projection computed (exact
 // keys: the bijective hash of the value), same arithmetic and order
-__global__ void freq_mi_terms_h(const Group* __restrict__ gj, int64_t n, const RecIn* __restrict__ r0,
-                                const RecIn* __restrict__ r1, int exact0, int exact1,
-                                const CountSlot* __restrict__ s0, uint64_t m0,
-                                const CountSlot* __restrict__ s1, uint64_t m1, double total,
-                                double* __restrict__ terms) {
+// (k0 / k1: each side's key of group i at k[i * stride]: a RecIn's key (stride 3; exact: the
+// value, hashed here) or freq_small_marginal's row hash (stride 1))
+__global__ void freq_mi_terms_h(const Group* __restrict__ gj, int64_t n, const uint64_t* __restrict__ k0,
+                                int st0, const uint64_t* __restrict__ k1, int st1, int exact0, int exact1,
+                                CountIndex x0, CountIndex x1, double total, double* __restrict__ terms) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t h0 = exact0 ? fmix_bij(r0[i].key) : r0[i].key;
-  const uint64_t h1 = exact1 ? fmix_bij(r1[i].key) : r1[i].key;
-  const double px = (double)count_of(s0, m0, h0);
-  const double py = (double)count_of(s1, m1, h1);
+  const uint64_t h0 = exact0 ? fmix_bij(k0[i * st0]) : k0[i * st0];
+  const uint64_t h1 = exact1 ? fmix_bij(k1[i * st1]) : k1[i * st1];
+  const double px = (double)count_of(x0, h0);
+  const double py = (double)count_of(x1, h1);
   const double pxy = (double)gj[i].count;
   terms[i] = (pxy / total) * log((pxy / total) / ((px / total) * (py / total)));
 }
@@ -5349,19 +5558,80 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
   uint64_t cmask[2] = {0, 0};
   Lookup L[2];
   dq_status res = DQ_OK;
-  // both marginals' records in one pass over the joint groups (kept: the lookups read their hashes)
-  DevBuf<RecIn> rec[2];
-  HIP_TRY(rec[0].ensure(n));
-  HIP_TRY(rec[1].ensure(n));
-  hipLaunchKernelGGL(freq_project2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, joint->stream,
-                     joint->compact.p, n, arena_of(joint), part_types(joint, 1), rec[0].p, rec[1].p);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(joint->stream));
-  stamp("project");
   const char* fl = getenv("DQ_FREQ_MI_LOOKUP");  // =1: the byte-compare lookups (A/B, tests)
   const bool force_lookup = fl && atoi(fl) != 0;
+  const char* fsm = getenv("DQ_FREQ_MI_NOSMALL");  // =1: no small-marginal pass (A/B, tests)
+  bool small[2] = {false, false};  // side k's marginal aggregated by freq_small_marginal
+  DevBuf<unsigned long long> hk[2];
+  if (!force_lookup && !(fsm && atoi(fsm))) {
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((n + 511) / 512, 1), 2048);
+    const int64_t nw = (int64_t)grid * 4;
+    DevBuf<SmallEntry> ent;
+    DevBuf<uint32_t> nout;
+    DevBuf<unsigned int> sfail;
+    HIP_TRY(hk[0].ensure(n));
+    HIP_TRY(hk[1].ensure(n));
+    HIP_TRY(ent.ensure((size_t)nw * 2 * kSmallMarg));
+    HIP_TRY(nout.ensure((size_t)nw * 2));
+    HIP_TRY(sfail.ensure(2));
+    HIP_TRY(hipMemsetAsync(sfail.p, 0, 8, stream));
+    hipLaunchKernelGGL(freq_small_marginal, dim3(grid), dim3(256), 0, stream, joint->compact.p, n,
+                       arena_of(joint), part_types(joint, 1), 3u, hk[0].p, hk[1].p, ent.p, nout.p, sfail.p);
+    HIP_TRY(hipGetLastError());
+    unsigned int hf[2];
+    HIP_TRY(hipMemcpyAsync(hf, sfail.p, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (!hf[0] || !hf[1]) {  // merge the waves' lists of each small side by (hash, words)
+      std::vector<uint32_t> hn((size_t)nw * 2);
+      std::vector<SmallEntry> he((size_t)nw * 2 * kSmallMarg);
+      HIP_TRY(hipMemcpy(hn.data(), nout.p, hn.size() * 4, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(he.data(), ent.p, he.size() * sizeof(SmallEntry), hipMemcpyDeviceToHost));
+      for (int k = 0; k < 2; ++k) {
+        if (hf[k]) continue;
+        std::map<uint64_t, std::pair<std::array<uint32_t, 8>, uint64_t>> vals;
+        bool ok = true;
+        for (int64_t gwv = 0; gwv < nw && ok; ++gwv)
+          for (uint32_t c = 0; c < hn[gwv * 2 + k] && ok; ++c) {
+            const SmallEntry& e = he[((size_t)gwv * 2 + k) * kSmallMarg + c];
+            std::array<uint32_t, 8> wv;
+            for (int q = 0; q < 8; ++q) wv[q] = e.w[q];
+            auto it = vals.find(e.h);
+            if (it == vals.end()) vals.emplace(e.h, std::make_pair(wv, (uint64_t)e.count));
+            else if (it->second.first != wv) ok = false;  // two values on one hash
+            else it->second.second += e.count;
+          }
+        if (!ok) continue;
+        uint64_t cap = 2;
+        while (cap < 2 * (uint64_t)vals.size()) cap <<= 1;
+        std::vector<CountSlot> tab(cap, CountSlot{0, 0});
+        for (const auto& kv : vals) {
+          uint64_t sl = kv.first & (cap - 1);
+          while (tab[sl].count) sl = (sl + 1) & (cap - 1);
+          tab[sl] = CountSlot{kv.first, kv.second.second};
+        }
+        HIP_TRY(cslots[k].ensure(cap));
+        HIP_TRY(hipMemcpy(cslots[k].p, tab.data(), cap * sizeof(CountSlot), hipMemcpyHostToDevice));
+        cmask[k] = cap - 1;
+        small[k] = true;
+      }
+    }
+    stamp("small marginals");
+  }
+  // the other sides' records in one pass over the joint groups (kept: the lookups read their keys)
+  DevBuf<RecIn> rec[2];
+  for (int k = 0; k < 2; ++k)
+    if (!small[k]) HIP_TRY(rec[k].ensure(n));
+  if (!small[0] || !small[1]) {
+    hipLaunchKernelGGL(freq_project2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, joint->stream,
+                       joint->compact.p, n, arena_of(joint), part_types(joint, 1),
+                       small[0] ? nullptr : rec[0].p, small[1] ? nullptr : rec[1].p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(joint->stream));
+  }
+  stamp("project");
   bool by_hash = !force_lookup;  // no marginal has two keys on one 64-bit hash
   for (int k = 0; k < 2 && res == DQ_OK; ++k) {
+    if (small[k]) continue;
     const int32_t ty = joint->types[k];
     res = dq_freq_create(joint->device, 1, &ty, 0, &marg[k]);
     stamp(k ? "marginal 1 create" : "marginal 0 create");
@@ -5373,27 +5643,103 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
                         vb, joint->num_rows, special, 0, hip_stream, !marg[k]->exact);
     }
     stamp(k ? "marginal 1 records" : "marginal 0 records");
-    if (res == DQ_OK) res = compact_groups(marg[k]);
+    // (the groups stay where phase C put them, per partition; compacted only for the
+    // byte-compare lookups)
+    if (res == DQ_OK) res = finalize_c(marg[k], true, false);
     stamp(k ? "marginal 1 groups" : "marginal 0 groups");
     if (res != DQ_OK) break;
     if (marg[k]->h_counters[C_COLLISIONS]) by_hash = false;
   }
-  for (int k = 0; k < 2 && res == DQ_OK; ++k) {
-    const int32_t ty = joint->types[k];
-    const int64_t m = marg[k]->n_compact;
-    uint64_t cap = 2;
-    while (cap < (uint64_t)(2 * m)) cap <<= 1;
-    if (by_hash) {
-      cmask[k] = cap - 1;
-      if (cslots[k].ensure(cap) != hipSuccess ||
-          hipMemsetAsync(cslots[k].p, 0, cap * sizeof(CountSlot), stream) != hipSuccess) {
-        res = fail(DQ_ERR_OUT_OF_MEMORY, "marginal index");
+  if (res == DQ_OK && !by_hash && (small[0] || small[1])) {
+    // a general side counted a hash collision: the byte-compare lookups need both sides as
+    // tables, so the small sides are built the general way too
+    for (int k = 0; k < 2 && res == DQ_OK; ++k) {
+      if (!small[k]) continue;
+      small[k] = false;
+      if (rec[k].ensure(n) != hipSuccess) {
+        res = fail(DQ_ERR_OUT_OF_MEMORY, "MutualInformation records");
         break;
       }
-      if (m)
-        hipLaunchKernelGGL(freq_count_index, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
-                           marg[k]->compact.p, m, cap - 1, cslots[k].p);
+      hipLaunchKernelGGL(freq_project, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, joint->stream,
+                         joint->compact.p, n, arena_of(joint), part_types(joint, 1), k, rec[k].p);
+      const int32_t ty = joint->types[k];
+      res = dq_freq_create(joint->device, 1, &ty, 0, &marg[k]);
+      if (res == DQ_OK) {
+        const int64_t rc[1] = {n};
+        const int64_t vb[1] = {(int64_t)((joint->arena_used + 7) & ~7ULL)};
+        const int64_t special[3] = {0, 0, (int64_t)joint->h_counters[C_NULL_ROWS]};
+        res = add_records(marg[k], reinterpret_cast<const dq_freq_record*>(rec[k].p), arena_of(joint), 1,
+                          rc, vb, joint->num_rows, special, 0, hip_stream, !marg[k]->exact);
+      }
+      if (res == DQ_OK) res = compact_groups(marg[k]);
+    }
+  }
+  CountIndex X[2];
+  DevBuf<unsigned long long> pbase[2];
+  DevBuf<uint8_t> plog[2];
+  for (int k = 0; k < 2; ++k) X[k] = CountIndex{cslots[k].p, cmask[k], nullptr, nullptr, 0};
+  for (int k = 0; k < 2 && res == DQ_OK; ++k) {
+    if (small[k]) continue;
+    const int32_t ty = joint->types[k];
+    if (by_hash) {  // per partition, in LDS, when every partition's table fits
+      dq_freq* mg = marg[k];
+      const int64_t P = (int64_t)kBuckets << mg->s_bits;
+      std::vector<unsigned long long> cnt(P), base(P);
+      std::vector<uint8_t> lg(P);
+      if (hipMemcpy(cnt.data(), mg->part_groups.p, P * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+        res = fail(DQ_ERR_DEVICE, "marginal index");
+        break;
+      }
+      unsigned long long tot = 0;
+      bool fits = true;
+      for (int64_t q = 0; q < P; ++q) {
+        int l = 4;
+        while ((1ULL << l) < 2 * cnt[q]) ++l;
+        fits = fits && l <= kIdxMaxLog;
+        lg[q] = (uint8_t)l;
+        base[q] = tot;
+        tot += 1ULL << l;
+      }
+      if (fits) {
+        if (cslots[k].ensure(tot) != hipSuccess || pbase[k].ensure(P) != hipSuccess ||
+            plog[k].ensure(P) != hipSuccess ||
+            hipMemcpy(pbase[k].p, base.data(), P * 8, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(plog[k].p, lg.data(), P, hipMemcpyHostToDevice) != hipSuccess) {
+          res = fail(DQ_ERR_OUT_OF_MEMORY, "marginal index");
+          break;
+        }
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, joint->device);
+        hipLaunchKernelGGL(freq_count_index_parts, dim3((unsigned)std::min<int64_t>(P, 2 * cus)), dim3(256), 0,
+                           mg->stream, mg->groups.p, mg->part_off.p, mg->part_groups.p, P, pbase[k].p,
+                           plog[k].p, cslots[k].p);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(mg->stream) != hipSuccess) {
+          res = fail(DQ_ERR_DEVICE, "marginal index");
+          break;
+        }
+        X[k] = CountIndex{cslots[k].p, 0, pbase[k].p, plog[k].p, 64 - kBucketBits - mg->s_bits};
+      } else {  // one table over the compacted groups
+        res = compact_groups(mg);
+        if (res != DQ_OK) break;
+        const int64_t m = mg->n_compact;
+        uint64_t cap = 2;
+        while (cap < (uint64_t)(2 * m)) cap <<= 1;
+        if (cslots[k].ensure(cap) != hipSuccess ||
+            hipMemsetAsync(cslots[k].p, 0, cap * sizeof(CountSlot), stream) != hipSuccess) {
+          res = fail(DQ_ERR_OUT_OF_MEMORY, "marginal index");
+          break;
+        }
+        if (m)
+          hipLaunchKernelGGL(freq_count_index, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream,
+                             mg->compact.p, m, cap - 1, cslots[k].p);
+        X[k] = CountIndex{cslots[k].p, cap - 1, nullptr, nullptr, 0};
+      }
     } else {
+      res = compact_groups(marg[k]);
+      if (res != DQ_OK) break;
+      const int64_t m = marg[k]->n_compact;
+      uint64_t cap = 2;
+      while (cap < (uint64_t)(2 * m)) cap <<= 1;
       if (slots[k].ensure(cap) != hipSuccess || hipMemsetAsync(slots[k].p, 0, cap * 4, stream) != hipSuccess) {
         res = fail(DQ_ERR_OUT_OF_MEMORY, "marginal index");
         break;
@@ -5412,15 +5758,22 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
     if (terms.ensure(n) != hipSuccess || partial.ensure(kSumBlocks) != hipSuccess) {
       res = fail(DQ_ERR_OUT_OF_MEMORY, "MutualInformation terms");
     } else {
-      if (by_hash)
+      if (by_hash) {
+        const uint64_t* kp[2];
+        int kst[2], kex[2];
+        for (int k = 0; k < 2; ++k) {
+          kp[k] = small[k] ? reinterpret_cast<const uint64_t*>(hk[k].p) : reinterpret_cast<const uint64_t*>(rec[k].p);
+          kst[k] = small[k] ? 1 : (int)(sizeof(RecIn) / 8);
+          kex[k] = small[k] ? 0 : (marg[k]->exact ? 1 : 0);
+        }
         hipLaunchKernelGGL(freq_mi_terms_h, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
-                           joint->compact.p, n, rec[0].p, rec[1].p, marg[0]->exact ? 1 : 0,
-                           marg[1]->exact ? 1 : 0, cslots[0].p, cmask[0], cslots[1].p, cmask[1],
+                           joint->compact.p, n, kp[0], kst[0], kp[1], kst[1], kex[0], kex[1], X[0], X[1],
                            (double)joint->num_rows, terms.p);
-      else
+      } else {
         hipLaunchKernelGGL(freq_mi_terms, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                            joint->compact.p, n, arena_of(joint), part_types(joint, 1), L[0], L[1],
                            (double)joint->num_rows, terms.p);
+      }
       stamp("terms");
       hipLaunchKernelGGL(freq_sum_f64, dim3(kSumBlocks), dim3(256), 0, stream, terms.p, n, partial.p);
       std::vector<double> h(kSumBlocks);

@@ -157,6 +157,40 @@ def test_mutual_information_hash_lookups_equal_byte_lookups(kinds, gpu_device, m
     assert abs(fast - exp) <= 1e-12 * max(1.0, abs(exp)), (fast, exp)
 
 
+@pytest.mark.parametrize("kinds,cards", [(("string", "string"), (50_000, 3)),
+                                         (("string", "string"), (4, 3)),
+                                         (("long", "string"), (7, 60_000)),
+                                         (("double", "long"), (12, 5)),
+                                         (("string", "long"), (20, 9))])
+def test_mutual_information_small_marginals(kinds, cards, gpu_device, monkeypatch):
+    """A side with few values has its marginal aggregated in one pass over the joint groups
+    (freq_small_marginal: per-wave value lists merged by hash and key words); a side with more
+    values than a wave can list takes the general path.  Bar: the oracle within 1e-12, and the
+    same as with the small pass off (DQ_FREQ_MI_NOSMALL=1)."""
+    from deequ_amd.analyzers import MutualInformation
+    from oracle.deequ_oracle import OTable, mutual_information
+    rng = np.random.default_rng(sum(cards))
+    n = 120_001
+
+    def col(kind, card):
+        v = rng.integers(0, card, n)
+        mask = rng.random(n) < 0.05
+        if kind == "string":
+            return pa.array([None if m else f"val-{x}" for x, m in zip(v, mask)], pa.string())
+        if kind == "double":
+            return pa.array(v * 0.5 - 1.0, mask=mask, type=pa.float64())
+        return pa.array(v, mask=mask, type=pa.int64())
+    a, b = col(kinds[0], cards[0]), col(kinds[1], cards[1])
+    df = _df({"a": a, "b": b}, gpu_device, 40_000)
+    got = MutualInformation("a", "b").calculate(df).value.get()
+    exp = mutual_information(OTable({"a": a.to_pylist(), "b": b.to_pylist()},
+                                    {"a": kinds[0], "b": kinds[1]}), "a", "b")
+    assert abs(got - exp) <= 1e-12 * max(1.0, abs(exp)), (got, exp)
+    monkeypatch.setenv("DQ_FREQ_MI_NOSMALL", "1")
+    ref = MutualInformation("a", "b").calculate(df).value.get()
+    assert abs(got - ref) <= 1e-12 * max(1.0, abs(ref)), (got, ref)
+
+
 def test_mutual_information_of_merged_states(gpu_device):
     """FrequenciesAndNumRows.sum (GroupingAnalyzers.scala:128-148) then MutualInformation."""
     from deequ_amd.analyzers import MutualInformation

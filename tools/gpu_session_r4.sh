@@ -73,6 +73,17 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_freq.py -x -q --timeout 200
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1 &&
 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1 &&
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests_$T.log 2>&1
+elif [ "${PART}" = 13 ]; then
+timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1 &&
+DQ_RUN_WORKERS=2 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5w2_$T.json 2>&1 &&
+DQ_RUN_WORKERS=3 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5w3_$T.json 2>&1 &&
+timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 1 --pyprof > $O/pyprof_c5_$T.log 2>&1 &&
+DQ_RUN_TRACE=1 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 1 > $O/trace_c5_$T.log 2>&1
+elif [ "${PART}" = 14 ]; then
+timeout -k 10 400 python -u -m pytest tests/test_gpu_datatype_mi.py tests/test_gpu_configs4.py -x -q --timeout 200 --timeout-method thread > $O/gpu_tests_q_$T.log 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1 &&
+timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1 &&
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests_$T.log 2>&1
 elif [ "${PART}" = 3 ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests_$T.log 2>&1 &&
 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5_$T.json 2>&1 &&
