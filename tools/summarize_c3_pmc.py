@@ -1,8 +1,8 @@
 """Per-kernel summary of the configs[2] PMC passes (tools/gpu_pmc_c3.sh, 1e8 rows, one step).
 
-Usage: python tools/summarize_c3_pmc.py TAG
-  reads  gpurun_out/{pmcf,pmcw,pmc,pmc2}_c3_TAG/*_counter_collection.csv
-  writes profiles/TAG/c3_counters.json: per dq:: kernel, the summed counters over its dispatches,
+Usage: python tools/summarize_c3_pmc.py TAG [WORKLOAD]   (WORKLOAD c3 (default) or c5)
+  reads  gpurun_out/{pmcf,pmcw,pmc,pmc2}_WORKLOAD_TAG/*_counter_collection.csv
+  writes profiles/TAG/WORKLOAD_counters.json: per dq:: kernel, the summed counters over its dispatches,
          HBM bytes (FETCH_SIZE KiB x 1024, reported raw and x2 per MI355X_MICROARCH.md §HBM --
          the halving is calibrated only for 16-B-per-lane streaming reads; these kernels read
          8-B records, so both are given), WRITE_SIZE bytes, and the SQ wave-state fractions.
@@ -19,11 +19,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     tag = sys.argv[1]
+    wl = sys.argv[2] if len(sys.argv) > 2 else "c3"
     src = os.path.join(ROOT, "gpurun_out")
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for pas in ("pmcf", "pmcw", "pmc", "pmc2"):
-        for path in glob.glob(os.path.join(src, f"{pas}_c3_{tag}", "*_counter_collection.csv")):
+        for path in glob.glob(os.path.join(src, f"{pas}_{wl}_{tag}", "*_counter_collection.csv")):
             for r in csv.DictReader(open(path)):
                 if not r["Kernel_Name"].startswith(("dq::", "void dq::")):
                     continue
@@ -45,8 +46,9 @@ def main():
         out[k] = d
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
-    json.dump({"tag": tag, "workload": "c3 --rows 100000000 --steps 1 --warmup 0",
-               "kernels": out}, open(os.path.join(dst, "c3_counters.json"), "w"), indent=1)
+    what = {"c3": "c3 --rows 100000000 --steps 1 --warmup 0", "c5": "c5 --steps 1 --warmup 0"}[wl]
+    json.dump({"tag": tag, "workload": what, "kernels": out},
+              open(os.path.join(dst, f"{wl}_counters.json"), "w"), indent=1)
     for k in sorted(out, key=lambda k: -out[k].get("fetch_bytes_raw", 0)):
         d = out[k]
         print(k[:48].ljust(48), {x: round(d[x] / 1e9, 3) for x in ("fetch_bytes_raw", "write_bytes")
