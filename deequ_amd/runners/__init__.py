@@ -261,9 +261,39 @@ def _histogram_and_grouping_job(data, col, hists, group, aggregate_with, save_st
     """Histogram(col) and the grouping of [col] from one table (_histogram_columns_for_groupings).
     Returns (Histogram metrics, grouping metrics).  If the Histogram table cannot be built, both
     run (and fail) on their own, as in the reference's two group-bys."""
+    st = _histogram_and_grouping_launch(data, col, hists, group, aggregate_with, save_states_with)
+    _histogram_and_grouping_device(st)
+    return _histogram_and_grouping_host(st)
+
+
+# The job in three stages, so that the sequential runner (_run_jobs) can run one job's host-only
+# stage while the device runs the next job's phase A: launch (the table's batches queued),
+# device (every device result the metrics need: finalize, the top-k, the NULL-group counts --
+# afterwards the table's calls answer from its caches), host (decoding and metric objects).
+def _histogram_and_grouping_launch(data, col, hists, group, aggregate_with, save_states_with):
     try:
         hs = hists[0].compute_state_from(data)
     except Exception:  # noqa: BLE001
+        hs = None
+    return (data, col, hists, group, aggregate_with, save_states_with, hs)
+
+
+def _histogram_and_grouping_device(st):
+    hs, hists = st[6], st[2]
+    if hs is None:
+        return
+    try:
+        if hs.binning_udf is None and hists and all(h.binning_udf is None for h in hists):
+            hs.frequencies.topk_raw(max(h.max_detail_bins for h in hists) + 2)
+            hs.frequencies.null_literal()
+            hs.frequencies.count()
+    except Exception:  # noqa: BLE001  (the host stage meets the error again and records it)
+        pass
+
+
+def _histogram_and_grouping_host(st):
+    data, col, hists, group, aggregate_with, save_states_with, hs = st
+    if hs is None:
         return (_run_scanning_analyzers(data, hists, aggregate_with, save_states_with),
                 _run_grouping_analyzers(data, [col], group, aggregate_with, save_states_with,
                                         None, None)[1])
@@ -319,6 +349,29 @@ def _job_workers(data, key_sets, aggregate_with, save_states_with) -> int:
     return workers
 
 
+def _run_jobs_pipelined(jobs) -> list:
+    """One job at a time, except that a Histogram job's host-only stage runs after the next
+    Histogram job's batches are queued, so the device works through that job's phase A
+    meanwhile (the host stage touches only the finished table's caches)."""
+    out = [None] * len(jobs)
+    pending = None  # (index, state) of a Histogram job whose host stage has not run
+    for i, job in enumerate(jobs):
+        if job.func is _histogram_and_grouping_job:
+            st = _histogram_and_grouping_launch(*job.args)
+            if pending is not None:
+                out[pending[0]] = _histogram_and_grouping_host(pending[1])
+            _histogram_and_grouping_device(st)
+            pending = (i, st)
+            continue
+        if pending is not None:
+            out[pending[0]] = _histogram_and_grouping_host(pending[1])
+            pending = None
+        out[i] = job()
+    if pending is not None:
+        out[pending[0]] = _histogram_and_grouping_host(pending[1])
+    return out
+
+
 def _run_jobs(data, jobs, workers: int) -> list:
     """Runs the jobs, `workers` at a time, each on a HIP stream of its own (a thread per job: the
     engine's calls release the GIL), and returns their results in order.  Each stream first waits
@@ -326,7 +379,9 @@ def _run_jobs(data, jobs, workers: int) -> list:
     at the end."""
     if workers <= 1 or len(jobs) <= 1:
         if not os.environ.get("DQ_RUN_TRACE"):
-            return [job() for job in jobs]
+            if is_distributed(data):  # (every rank keeps the plain order of its collectives)
+                return [job() for job in jobs]
+            return _run_jobs_pipelined(jobs)
         out = []
         for job in jobs:  # DQ_RUN_TRACE=1: each job's wall time on stderr
             t0 = time.perf_counter()
