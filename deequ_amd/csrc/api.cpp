@@ -1852,6 +1852,48 @@ void dev_free(void* p, size_t bytes, int dev) {
   if (dev != cur) (void)hipSetDevice(cur);
 }
 
+namespace {
+struct PinnedPool {  // page-locked staging blocks (powers of two >= 4 KB), kept to process exit
+  std::mutex m;
+  std::multimap<size_t, void*> free_blocks;
+};
+PinnedPool& pinned_pool() {
+  static PinnedPool* pool = new PinnedPool;
+  return *pool;
+}
+}  // namespace
+
+hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (!bytes) return hipStreamSynchronize(st);
+  size_t want = 4096;
+  while (want < bytes) want <<= 1;
+  PinnedPool& pool = pinned_pool();
+  void* buf = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(pool.m);
+    auto it = pool.free_blocks.lower_bound(want);
+    if (it != pool.free_blocks.end()) {
+      want = it->first;
+      buf = it->second;
+      pool.free_blocks.erase(it);
+    }
+  }
+  if (!buf && want > (64u << 20)) {  // (large copies: not worth pinning a block for)
+    hipError_t e = hipStreamSynchronize(st);
+    return e != hipSuccess ? e : hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+  }
+  if (!buf) {
+    hipError_t e = hipHostMalloc(&buf, want, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) memcpy(dst, buf, bytes);
+  std::lock_guard<std::mutex> lock(pool.m);
+  pool.free_blocks.emplace(want, buf);
+  return e;
+}
+
 }  // namespace dq
 
 extern "C" void dq_release_cached_memory(void) {

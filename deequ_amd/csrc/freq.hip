@@ -4078,7 +4078,7 @@ static dq_status ensure_chunks(dq_freq* f, int64_t add) {
 static dq_status pull_counters(dq_freq* f) {
   HIP_TRY(hipStreamSynchronize(f->stream));
   unsigned long long w[C_N + 1];
-  HIP_TRY(hipMemcpy(w, f->dev_words.p, sizeof(w), hipMemcpyDeviceToHost));
+  HIP_TRY(d2h(w, f->dev_words.p, sizeof(w), f->stream));
   for (int k = 0; k < C_N; ++k) f->h_counters[k] = w[k];
   f->arena_used = w[C_N];
   f->arena_hi = f->arena_used;
@@ -4304,8 +4304,7 @@ static dq_status finalize_b(dq_freq* f) {
     hipLaunchKernelGGL(freq_part_scan, dim3(1), dim3(kThreads), 0, f->stream, f->chunk_boff.p, nb);
     HIP_TRY(hipGetLastError());
     unsigned long long m = 0;
-    HIP_TRY(hipMemcpyAsync(&m, f->chunk_boff.p + nb, 8, hipMemcpyDeviceToHost, f->stream));
-    HIP_TRY(hipStreamSynchronize(f->stream));
+    HIP_TRY(d2h(&m, f->chunk_boff.p + nb, 8, f->stream));
     if ((int64_t)m * 4 < n_all * 3) {
       hipLaunchKernelGGL(freq_chunk_ids, dim3((unsigned)nb), dim3(kThreads), 0, f->stream, f->hist.p,
                          n_all, f->chunk_boff.p, f->chunk_id.p);
@@ -4355,7 +4354,7 @@ static dq_status finalize_b(dq_freq* f) {
   } else {
     HIP_TRY(hipStreamSynchronize(f->stream));
   }
-  HIP_TRY(hipMemcpy(tot.data(), f->totals.p, kBuckets * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(d2h(tot.data(), f->totals.p, kBuckets * 8, f->stream));
   uint64_t R = 0;
   for (auto t : tot) R += t;
   int target = f->exact ? FM<false>::kTarget : FM<true>::kTarget;
@@ -4387,7 +4386,7 @@ static dq_status finalize_b(dq_freq* f) {
     uint32_t nonempty = 0;
     for (auto t : tot) nonempty += t != 0;
     std::vector<uint32_t> ns(kBuckets);
-    (void)hipMemcpy(ns.data(), f->nseg.p, kBuckets * 4, hipMemcpyDeviceToHost);
+    (void)d2h(ns.data(), f->nseg.p, kBuckets * 4, f->stream);
     uint64_t segs = 0;
     for (auto v : ns) segs += v;
     fprintf(stderr, "dq_freq finalize: %s chunks=%lld piece_rows=%lld segments=%llu records=%llu s=%d "
@@ -4618,8 +4617,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
         reduced = true;
       }
       unsigned int m = 0;
-      HIP_TRY(hipStreamSynchronize(f->stream));
-      HIP_TRY(hipMemcpy(&m, f->ovf_n.p, 4, hipMemcpyDeviceToHost));
+      HIP_TRY(d2h(&m, f->ovf_n.p, 4, f->stream));
       if (m) reduced = false;
       if (clk && ((f->exact && !old_c) || (!f->exact && round == 0 && !old_hc))) {  // C_x / C_h: 8 stamps per item
         unsigned long long h[16 * 8];
@@ -4688,8 +4686,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     if (rs != DQ_OK) return rs;
   }
   unsigned long long r[4];
-  HIP_TRY(hipStreamSynchronize(f->stream));
-  HIP_TRY(hipMemcpy(r, f->red.p, sizeof(r), hipMemcpyDeviceToHost));
+  HIP_TRY(d2h(r, f->red.p, sizeof(r), f->stream));
   f->st_groups = r[0];
   f->st_unique = r[1];
   f->st_entropy = __builtin_bit_cast(double, r[2]);
@@ -4709,7 +4706,7 @@ static dq_status compact_groups(dq_freq* f) {
   if (f->n_compact >= 0) return DQ_OK;
   const int64_t P = (int64_t)kBuckets << f->s_bits;
   std::vector<unsigned long long> cnt(P), dst(P);
-  HIP_TRY(hipMemcpy(cnt.data(), f->part_groups.p, P * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(d2h(cnt.data(), f->part_groups.p, P * 8, f->stream));
   unsigned long long tot = 0;
   for (int64_t p = 0; p < P; ++p) {
     dst[p] = tot;
@@ -5140,6 +5137,11 @@ static PartTypes part_types(const dq_freq* f, int parts) {
 // Records (+ var bytes) of `n` device groups cut into `parts` owner segments.
 static dq_status owner_sizes(dq_freq* f, const Group* g, int64_t n, int parts,
                              std::vector<unsigned long long>& rec, std::vector<unsigned long long>& var) {
+  if (f->exact && parts == 1) {  // one segment of n fixed-size records: nothing to count
+    rec.assign(1, (unsigned long long)n);
+    var.assign(1, 0ULL);
+    return DQ_OK;
+  }
   DevBuf<unsigned long long> cnt;
   HIP_TRY(cnt.ensure(2 * kMaxParts));
   HIP_TRY(hipMemsetAsync(cnt.p, 0, 2 * kMaxParts * 8, f->stream));
@@ -5148,8 +5150,7 @@ static dq_status owner_sizes(dq_freq* f, const Group* g, int64_t n, int parts,
                        arena_of(f), part_types(f, parts), cnt.p, cnt.p + kMaxParts);
   HIP_TRY(hipGetLastError());
   std::vector<unsigned long long> h(2 * kMaxParts);
-  HIP_TRY(hipStreamSynchronize(f->stream));
-  HIP_TRY(hipMemcpy(h.data(), cnt.p, h.size() * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(d2h(h.data(), cnt.p, h.size() * 8, f->stream));
   rec.assign(h.begin(), h.begin() + parts);
   var.assign(h.begin() + kMaxParts, h.begin() + kMaxParts + parts);
   return DQ_OK;
@@ -5169,7 +5170,7 @@ static dq_status owner_scatter(dq_freq* f, const Group* g, int64_t n, int parts,
   if (!tr) return DQ_OK;
   DevBuf<unsigned long long> d;
   HIP_TRY(d.ensure(base.size()));
-  HIP_TRY(hipMemcpy(d.p, base.data(), base.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpyAsync(d.p, base.data(), base.size() * 8, hipMemcpyHostToDevice, f->stream));
   hipLaunchKernelGGL(freq_owner_scatter, dim3(grid_for(n)), dim3(256), 0, f->stream, g, n,
                      arena_of(f), part_types(f, parts), d.p, d.p + kMaxParts, d.p + 2 * kMaxParts,
                      d.p + 3 * kMaxParts, out_rec, out_var);
@@ -5196,8 +5197,8 @@ static dq_status encode_groups(dq_freq* f, const Group* g, int64_t n, std::vecto
   if (st != DQ_OK) return st;
   std::vector<RecIn> hr(rec[0]);
   std::vector<uint8_t> hv(var[0]);
-  HIP_TRY(hipMemcpy(hr.data(), dr.p, rec[0] * sizeof(RecIn), hipMemcpyDeviceToHost));
-  if (var[0]) HIP_TRY(hipMemcpy(hv.data(), dv.p, var[0], hipMemcpyDeviceToHost));
+  HIP_TRY(d2h(hr.data(), dr.p, rec[0] * sizeof(RecIn), f->stream));
+  if (var[0]) HIP_TRY(d2h(hv.data(), dv.p, var[0], f->stream));
   for (const RecIn& r : hr) {
     offs.push_back((int64_t)bytes.size());
     counts.push_back((int64_t)r.count);
@@ -5237,8 +5238,7 @@ static dq_status select_top(dq_freq* f, const Group* arr, int64_t n, int k, std:
     hipLaunchKernelGGL(freq_group_hist, dim3(grid_for(n)), dim3(256), 0, f->stream, arr, n, lo, hi,
                        width, hist.p);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(f->stream));
-    HIP_TRY(hipMemcpy(hb.data(), hist.p, nb * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(d2h(hb.data(), hist.p, nb * 8, f->stream));
     return DQ_OK;
   };
   // round 0: powers of two (width 0 selects log2 bins)
@@ -5281,13 +5281,12 @@ static dq_status select_top(dq_freq* f, const Group* arr, int64_t n, int k, std:
                      (unsigned long long)cap, take.p, nt.p, nt.p + 1, tie.p);
   HIP_TRY(hipGetLastError());
   unsigned long long cnts[2];
-  HIP_TRY(hipStreamSynchronize(f->stream));
-  HIP_TRY(hipMemcpy(cnts, nt.p, 16, hipMemcpyDeviceToHost));
+  HIP_TRY(d2h(cnts, nt.p, 16, f->stream));
   const uint64_t nt_take = cnts[0], nt_tie = std::min<uint64_t>(cnts[1], cap);
   out.resize(nt_take + nt_tie);
-  if (nt_take) HIP_TRY(hipMemcpy(out.data(), take.p, nt_take * sizeof(Group), hipMemcpyDeviceToHost));
+  if (nt_take) HIP_TRY(d2h(out.data(), take.p, nt_take * sizeof(Group), f->stream));
   if (nt_tie)
-    HIP_TRY(hipMemcpy(out.data() + nt_take, tie.p, nt_tie * sizeof(Group), hipMemcpyDeviceToHost));
+    HIP_TRY(d2h(out.data() + nt_take, tie.p, nt_tie * sizeof(Group), f->stream));
   std::stable_sort(out.begin(), out.end(),
                    [](const Group& x, const Group& y) { return x.count > y.count; });
   if (out.size() > (size_t)k) out.resize(k);
@@ -5321,6 +5320,13 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
                            2 * (capacity_hint >> 24) + 16;
     dq_status st = ensure_chunks(f.get(), chunks);
     if (st != DQ_OK) return st;
+    if (f->exact && pieces_enabled()) {  // the pre-pass rows too: growing them waits for the stream
+      int64_t n_wg = 0;
+      phaseA_chunks(false, false, capacity_hint, f->tile, &n_wg);
+      n_wg += 2 * (capacity_hint >> 24) + 16;
+      HIP_TRY(f->pstart.ensure((size_t)n_wg * kBuckets));
+      HIP_TRY(f->plen.ensure((size_t)n_wg * kBuckets));
+    }
   }
   *out = f.release();
   return DQ_OK;
@@ -5579,13 +5585,12 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
                        arena_of(joint), part_types(joint, 1), 3u, hk[0].p, hk[1].p, ent.p, nout.p, sfail.p);
     HIP_TRY(hipGetLastError());
     unsigned int hf[2];
-    HIP_TRY(hipMemcpyAsync(hf, sfail.p, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(d2h(hf, sfail.p, 8, stream));
     if (!hf[0] || !hf[1]) {  // merge the waves' lists of each small side by (hash, words)
       std::vector<uint32_t> hn((size_t)nw * 2);
       std::vector<SmallEntry> he((size_t)nw * 2 * kSmallMarg);
-      HIP_TRY(hipMemcpy(hn.data(), nout.p, hn.size() * 4, hipMemcpyDeviceToHost));
-      HIP_TRY(hipMemcpy(he.data(), ent.p, he.size() * sizeof(SmallEntry), hipMemcpyDeviceToHost));
+      HIP_TRY(d2h(hn.data(), nout.p, hn.size() * 4, stream));
+      HIP_TRY(d2h(he.data(), ent.p, he.size() * sizeof(SmallEntry), stream));
       for (int k = 0; k < 2; ++k) {
         if (hf[k]) continue;
         std::map<uint64_t, std::pair<std::array<uint32_t, 8>, uint64_t>> vals;
@@ -5686,7 +5691,7 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
       const int64_t P = (int64_t)kBuckets << mg->s_bits;
       std::vector<unsigned long long> cnt(P), base(P);
       std::vector<uint8_t> lg(P);
-      if (hipMemcpy(cnt.data(), mg->part_groups.p, P * 8, hipMemcpyDeviceToHost) != hipSuccess) {
+      if (d2h(cnt.data(), mg->part_groups.p, P * 8, mg->stream) != hipSuccess) {
         res = fail(DQ_ERR_DEVICE, "marginal index");
         break;
       }
@@ -5778,8 +5783,7 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
       hipLaunchKernelGGL(freq_sum_f64, dim3(kSumBlocks), dim3(256), 0, stream, terms.p, n, partial.p);
       std::vector<double> h(kSumBlocks);
       if (hipGetLastError() != hipSuccess ||
-          hipMemcpyAsync(h.data(), partial.p, kSumBlocks * 8, hipMemcpyDeviceToHost, stream) != hipSuccess ||
-          hipStreamSynchronize(stream) != hipSuccess) {
+          d2h(h.data(), partial.p, kSumBlocks * 8, stream) != hipSuccess) {
         res = fail(DQ_ERR_DEVICE, "MutualInformation launch failed");
       } else {
         double sum = 0.0;
@@ -5968,8 +5972,7 @@ static dq_status topk_recount(dq_freq* f, int k, FEntry* list, int64_t nb, std::
     hipLaunchKernelGGL(freq_phaseC_h<false>, dim3(grid), dim3(kCThreads), 0, f->stream, a);
   HIP_TRY(hipGetLastError());
   unsigned int m = 0;
-  HIP_TRY(hipStreamSynchronize(f->stream));
-  HIP_TRY(hipMemcpy(&m, novf.p, 4, hipMemcpyDeviceToHost));
+  HIP_TRY(d2h(&m, novf.p, 4, f->stream));
   if (m) return DQ_OK;  // (not done)
   dq_status st = select_top(f, all.p, nc + nb * (int64_t)stride, k, top);
   if (st != DQ_OK) return st;
@@ -6002,8 +6005,7 @@ extern "C" dq_status dq_freq_topk(dq_freq* f, int k, int64_t* counts_out, int64_
                          f->part_groups.p, P, tau, bad.p, bad_list.p, cap);
       HIP_TRY(hipGetLastError());
       unsigned long long nb = 0;
-      HIP_TRY(hipStreamSynchronize(f->stream));
-      HIP_TRY(hipMemcpy(&nb, bad.p, 8, hipMemcpyDeviceToHost));
+      HIP_TRY(d2h(&nb, bad.p, 8, f->stream));
       exact_path = nb != 0;
       const char* fe = getenv("DQ_FREQ_TOPK_EXACT");  // =1: every group (A/B, tests)
       if (nb && (int64_t)nb <= cap && !(fe && atoi(fe))) {  // a few partitions: recount just those
@@ -6027,7 +6029,8 @@ extern "C" dq_status dq_freq_topk(dq_freq* f, int k, int64_t* counts_out, int64_
     DevBuf<Group> dg;
     HIP_TRY(dg.ensure(std::max<size_t>(top.size(), 1)));
     if (!top.empty())
-      HIP_TRY(hipMemcpy(dg.p, top.data(), top.size() * sizeof(Group), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpyAsync(dg.p, top.data(), top.size() * sizeof(Group), hipMemcpyHostToDevice,
+                             f->stream));  // (encode_groups waits for the stream)
     std::vector<int64_t> c1, o1;
     std::vector<uint8_t> b1;
     st = encode_groups(f, dg.p, (int64_t)top.size(), c1, o1, b1);
@@ -6247,8 +6250,7 @@ static dq_status add_records(dq_freq* f, const dq_freq_record* records, const ui
                          reinterpret_cast<const RecIn*>(records), total_rec, md.p);
       HIP_TRY(hipGetLastError());
       unsigned int h = 32;
-      HIP_TRY(hipMemcpyAsync(&h, md.p, 4, hipMemcpyDeviceToHost, f->stream));
-      HIP_TRY(hipStreamSynchronize(f->stream));
+      HIP_TRY(d2h(&h, md.p, 4, f->stream));
       maxd = std::max(1, (int)std::min(h, 32u));
     }
     // (and at most one record per thread: the records path runs one round per tile)
@@ -6433,8 +6435,7 @@ extern "C" dq_status dq_key_partition(const dq_column* batches, int n_batches, i
     HIP_TRY(hipGetLastError());
   }
   unsigned long long h[2 * kMaxParts + 1];
-  HIP_TRY(hipMemcpyAsync(h, cnt.p, sizeof(h), hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
+  HIP_TRY(d2h(h, cnt.p, sizeof(h), stream));
   unsigned long long base = 0;
   for (int j = 0; j < n_parts; ++j) {  // segment cursors: the exclusive prefix of the counts
     counts_out[j] = (int64_t)h[j];

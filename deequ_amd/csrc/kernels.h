@@ -33,6 +33,12 @@ dq_status fail(dq_status code, const char* fmt, ...);
 hipError_t dev_alloc(void** p, size_t bytes, size_t* got, int* device);
 void dev_free(void* p, size_t bytes, int device);
 
+// Device -> host copy of a small result (counts, bounds, a histogram, the top-k records) after
+// the work queued on `st`: stream-ordered into page-locked staging (api.cpp keeps a few blocks),
+// then memcpy'd to `dst`.  A plain hipMemcpy into pageable memory goes through the runtime's own
+// staging: measured ~20 us for 16 bytes and ~100 us for 64 KB, against ~10 us from pinned.
+hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st);
+
 // Device buffer that grows on demand (contents are not preserved across growth).
 template <typename T>
 struct DevBuf {

@@ -496,9 +496,8 @@ struct Passer {
       HIP_TRY(hipGetLastError());
     }
     h.resize(nb);
-    HIP_TRY(hipMemcpyAsync(h.data(), hist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, st));
-    if (bits > 0) HIP_TRY(hipMemcpyAsync(mmh.data(), mm.p, (size_t)A * 16, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(d2h(h.data(), hist.p, (size_t)nb * 8, st));
+    if (bits > 0) HIP_TRY(d2h(mmh.data(), mm.p, (size_t)A * 16, st));
     return DQ_OK;
   }
   // the keys of the last pass's selected bins (mask: nb bits) -> dst (T of them)
@@ -611,8 +610,7 @@ dq_status radix_select(Source src, Passer& ps, Pass p, std::vector<Target> tg, s
                          (int64_t)u, dpick.p);
       HIP_TRY(hipGetLastError());
       std::vector<double> v(u);
-      HIP_TRY(hipMemcpyAsync(v.data(), dpick.p, (size_t)u * 8, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipStreamSynchronize(st));  // idx and v die here
+      HIP_TRY(d2h(v.data(), dpick.p, (size_t)u * 8, st));  // idx and v die here
       for (int i = 0; i < u; ++i) res[tg[i].j] = v[i];
       return DQ_OK;
     }
@@ -686,8 +684,7 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
       hipLaunchKernelGGL(keys_to_doubles, dim3((unsigned)std::min<int64_t>((n + 4095) / 4096, 4096)), dim3(256),
                          0, stream, sorted.p, n, picks.p);
       HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
+      HIP_TRY(d2h(out, picks.p, (size_t)n * 8, stream));
     } else {  // many ranks: the picks of the sorted keys
       std::vector<int64_t> rank(n);
       for (int64_t j = 0; j < n; ++j) rank[j] = (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1));
@@ -697,8 +694,7 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
       hipLaunchKernelGGL(select_pick, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                          sorted.p, didx.p, n, picks.p);
       HIP_TRY(hipGetLastError());
-      HIP_TRY(hipMemcpyAsync(out, picks.p, (size_t)n * 8, hipMemcpyDeviceToHost, stream));
-      HIP_TRY(hipStreamSynchronize(stream));  // rank dies here
+      HIP_TRY(d2h(out, picks.p, (size_t)n * 8, stream));  // rank dies here
     }
     return DQ_OK;
   }

@@ -349,26 +349,39 @@ def _job_workers(data, key_sets, aggregate_with, save_states_with) -> int:
     return workers
 
 
-def _run_jobs_pipelined(jobs) -> list:
+def _run_jobs_pipelined(jobs, trace: bool = False) -> list:
     """One job at a time, except that a Histogram job's host-only stage runs after the next
     Histogram job's batches are queued, so the device works through that job's phase A
-    meanwhile (the host stage touches only the finished table's caches)."""
+    meanwhile (the host stage touches only the finished table's caches).  trace
+    (DQ_RUN_TRACE=2): each stage's wall time on stderr."""
     out = [None] * len(jobs)
     pending = None  # (index, state) of a Histogram job whose host stage has not run
+    clock = time.perf_counter
+
+    def stage(what, i, fn, *a):
+        if not trace:
+            return fn(*a)
+        t0 = clock()
+        r = fn(*a)
+        print(f"[dq run] {1e3 * t0:12.3f} {1e6 * (clock() - t0):9.1f} us {what} "
+              f"{_job_name(jobs[i])}", file=sys.stderr)
+        return r
+
     for i, job in enumerate(jobs):
         if job.func is _histogram_and_grouping_job:
-            st = _histogram_and_grouping_launch(*job.args)
+            st = stage("launch", i, _histogram_and_grouping_launch, *job.args)
             if pending is not None:
-                out[pending[0]] = _histogram_and_grouping_host(pending[1])
-            _histogram_and_grouping_device(st)
+                out[pending[0]] = stage("host", pending[0], _histogram_and_grouping_host,
+                                        pending[1])
+            stage("device", i, _histogram_and_grouping_device, st)
             pending = (i, st)
             continue
         if pending is not None:
-            out[pending[0]] = _histogram_and_grouping_host(pending[1])
+            out[pending[0]] = stage("host", pending[0], _histogram_and_grouping_host, pending[1])
             pending = None
-        out[i] = job()
+        out[i] = stage("job", i, job)
     if pending is not None:
-        out[pending[0]] = _histogram_and_grouping_host(pending[1])
+        out[pending[0]] = stage("host", pending[0], _histogram_and_grouping_host, pending[1])
     return out
 
 
@@ -378,10 +391,11 @@ def _run_jobs(data, jobs, workers: int) -> list:
     for the caller's stream (the table's buffers), and the caller's stream waits for all of them
     at the end."""
     if workers <= 1 or len(jobs) <= 1:
-        if not os.environ.get("DQ_RUN_TRACE"):
+        trace = os.environ.get("DQ_RUN_TRACE", "")
+        if trace in ("", "2"):
             if is_distributed(data):  # (every rank keeps the plain order of its collectives)
                 return [job() for job in jobs]
-            return _run_jobs_pipelined(jobs)
+            return _run_jobs_pipelined(jobs, trace == "2")
         out = []
         for job in jobs:  # DQ_RUN_TRACE=1: each job's wall time on stderr
             t0 = time.perf_counter()
