@@ -284,9 +284,21 @@ def _histogram_and_grouping_device(st):
         return
     try:
         if hs.binning_udf is None and hists and all(h.binning_udf is None for h in hists):
-            hs.frequencies.topk_raw(max(h.max_detail_bins for h in hists) + 2)
-            hs.frequencies.null_literal()
-            hs.frequencies.count()
+            ft = hs.frequencies
+            if os.environ.get("DQ_RUN_TRACE") == "3":  # (the calls' host times)
+                t = [time.perf_counter()]
+                ft.topk_raw(max(h.max_detail_bins for h in hists) + 2)
+                t.append(time.perf_counter())
+                ft.null_literal()
+                t.append(time.perf_counter())
+                ft.count()
+                t.append(time.perf_counter())
+                print("[dq run] device calls us: " + " ".join(
+                    f"{1e6 * (b - a):.1f}" for a, b in zip(t, t[1:])), file=sys.stderr)
+                return
+            ft.topk_raw(max(h.max_detail_bins for h in hists) + 2)
+            ft.null_literal()
+            ft.count()
     except Exception:  # noqa: BLE001  (the host stage meets the error again and records it)
         pass
 
@@ -392,10 +404,10 @@ def _run_jobs(data, jobs, workers: int) -> list:
     at the end."""
     if workers <= 1 or len(jobs) <= 1:
         trace = os.environ.get("DQ_RUN_TRACE", "")
-        if trace in ("", "2"):
+        if trace in ("", "2", "3"):
             if is_distributed(data):  # (every rank keeps the plain order of its collectives)
                 return [job() for job in jobs]
-            return _run_jobs_pipelined(jobs, trace == "2")
+            return _run_jobs_pipelined(jobs, trace in ("2", "3"))
         out = []
         for job in jobs:  # DQ_RUN_TRACE=1: each job's wall time on stderr
             t0 = time.perf_counter()
