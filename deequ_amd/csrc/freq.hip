@@ -43,6 +43,7 @@
 #include <memory>
 #include <array>
 #include <map>
+#include <mutex>
 #include <vector>
 
 #include "engine.h"
@@ -3949,6 +3950,38 @@ using namespace dq;
 // ------------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------------
+
+// 8-byte page-locked words (the small-key phase A's give-up flag) carved from shared 4 KB blocks
+// kept to process exit: a hipHostMalloc + hipHostFree per table cost ~0.1-0.2 ms each at every
+// string Histogram job's boundary.
+struct PinnedWords {
+  std::mutex m;
+  std::vector<unsigned long long*> free_words;
+};
+static PinnedWords& pinned_words() {
+  static PinnedWords* w = new PinnedWords;
+  return *w;
+}
+static hipError_t pinned_word_get(unsigned long long** out) {
+  PinnedWords& w = pinned_words();
+  std::lock_guard<std::mutex> lock(w.m);
+  if (w.free_words.empty()) {
+    void* blk = nullptr;
+    hipError_t e = hipHostMalloc(&blk, 4096, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < 512; ++i) w.free_words.push_back(static_cast<unsigned long long*>(blk) + i);
+  }
+  *out = w.free_words.back();
+  w.free_words.pop_back();
+  return hipSuccess;
+}
+static void pinned_word_put(unsigned long long* p) {
+  (void)hipDeviceSynchronize();  // (as hipHostFree: no copy may still land in the word)
+  PinnedWords& w = pinned_words();
+  std::lock_guard<std::mutex> lock(w.m);
+  w.free_words.push_back(p);
+}
+
 struct dq_freq {
   int device = 0;
   int n_keys = 0;
@@ -3992,7 +4025,7 @@ struct dq_freq {
   struct PinnedWord {
     unsigned long long* p = nullptr;
     ~PinnedWord() {
-      if (p) (void)hipHostFree(p);
+      if (p) pinned_word_put(p);
     }
   } fast_seen;
   // finalize cache (phase B)
@@ -4175,7 +4208,7 @@ static bool small_keys_worth_trying(dq_freq* f, const dq_column& k, int64_t rows
 
 static dq_status launch_phaseA_small(dq_freq* f, AArgs& a) {
   if (!f->fast_seen.p) {
-    HIP_TRY(hipHostMalloc((void**)&f->fast_seen.p, 8, hipHostMallocDefault));
+    HIP_TRY(pinned_word_get(&f->fast_seen.p));
     *f->fast_seen.p = 0;
   }
   int64_t n_wg = 0;
