@@ -361,13 +361,59 @@ def _job_workers(data, key_sets, aggregate_with, save_states_with) -> int:
     return workers
 
 
+def _histogram_scan_launch(data, analyzers, aggregate_with, save_states_with):
+    """A scanning job of one Histogram (a column whose table does not serve its grouping) in the
+    three stages of _histogram_and_grouping_job: Analyzer.calculate, split."""
+    a = analyzers[0]
+    try:
+        for condition in a.preconditions():
+            condition(data.schema)
+        return (a, a.compute_state_from(data), None)
+    except Exception as e:  # noqa: BLE001
+        return (a, None, e)
+
+
+def _histogram_scan_device(st):
+    a, state, err = st
+    if err is not None or state is None or state.binning_udf is not None:
+        return
+    try:
+        state.frequencies.topk_raw(a.max_detail_bins + 2)
+        state.frequencies.null_literal()
+        state.frequencies.count()
+    except Exception:  # noqa: BLE001  (the host stage meets the error again and records it)
+        pass
+
+
+def _histogram_scan_host(st):
+    a, state, err = st
+    if err is None:
+        try:
+            return AnalyzerContext({a: a.calculate_metric(state, None, None)})
+        except Exception as e:  # noqa: BLE001
+            err = e
+    return AnalyzerContext({a: a.to_failure_metric(err)})
+
+
+def _stages_of(job):
+    """(launch, device, host) of a job the sequential runner may overlap, else None."""
+    if job.func is _histogram_and_grouping_job:
+        return (_histogram_and_grouping_launch, _histogram_and_grouping_device,
+                _histogram_and_grouping_host)
+    if (job.func is _run_scanning_analyzers and len(job.args[1]) == 1
+            and isinstance(job.args[1][0], Histogram) and job.args[2] is None
+            and job.args[3] is None):
+        return _histogram_scan_launch, _histogram_scan_device, _histogram_scan_host
+    return None
+
+
 def _run_jobs_pipelined(jobs, trace: bool = False) -> list:
     """One job at a time, except that a Histogram job's host-only stage runs after the next
     Histogram job's batches are queued, so the device works through that job's phase A
     meanwhile (the host stage touches only the finished table's caches).  trace
     (DQ_RUN_TRACE=2): each stage's wall time on stderr."""
     out = [None] * len(jobs)
-    pending = None  # (index, state) of a Histogram job whose host stage has not run
+    pending = None  # (index, host stage, state) of a job whose host stage has not run
     clock = time.perf_counter
 
     def stage(what, i, fn, *a):
@@ -380,20 +426,21 @@ def _run_jobs_pipelined(jobs, trace: bool = False) -> list:
         return r
 
     for i, job in enumerate(jobs):
-        if job.func is _histogram_and_grouping_job:
-            st = stage("launch", i, _histogram_and_grouping_launch, *job.args)
+        stages = _stages_of(job)
+        if stages is not None:
+            launch, device, host = stages
+            st = stage("launch", i, launch, *job.args)
             if pending is not None:
-                out[pending[0]] = stage("host", pending[0], _histogram_and_grouping_host,
-                                        pending[1])
-            stage("device", i, _histogram_and_grouping_device, st)
-            pending = (i, st)
+                out[pending[0]] = stage("host", pending[0], pending[1], pending[2])
+            stage("device", i, device, st)
+            pending = (i, host, st)
             continue
         if pending is not None:
-            out[pending[0]] = stage("host", pending[0], _histogram_and_grouping_host, pending[1])
+            out[pending[0]] = stage("host", pending[0], pending[1], pending[2])
             pending = None
         out[i] = stage("job", i, job)
     if pending is not None:
-        out[pending[0]] = stage("host", pending[0], _histogram_and_grouping_host, pending[1])
+        out[pending[0]] = stage("host", pending[0], pending[1], pending[2])
     return out
 
 
