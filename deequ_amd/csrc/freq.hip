@@ -4890,7 +4890,8 @@ DQ_DEV void small_part(const uint32_t (&e)[16], uint32_t w, bool utf8, const uin
 __global__ void __launch_bounds__(256)
 freq_small_marginal(const Group* __restrict__ g, int64_t n, const uint8_t* __restrict__ arena, PartTypes t,
                     uint32_t try_sides, unsigned long long* __restrict__ hk0, unsigned long long* __restrict__ hk1,
-                    SmallEntry* __restrict__ out, uint32_t* __restrict__ nout, unsigned int* __restrict__ fail) {
+                    SmallEntry* __restrict__ out, uint32_t* __restrict__ nout, unsigned int* __restrict__ fail,
+                    RecIn* __restrict__ rec0, RecIn* __restrict__ rec1) {
   __shared__ unsigned long long s_h[4][2][kSmallMarg], s_c[4][2][kSmallMarg];
   __shared__ uint32_t s_w[4][2][kSmallMarg][8];
   constexpr int U = 2;  // groups per lane per step, every load of the step in flight together
@@ -4925,6 +4926,14 @@ freq_small_marginal(const Group* __restrict__ g, int64_t n, const uint8_t* __res
         uint64_t h;
         small_part(e[u], w, t.types[k] == DQ_UTF8, enc, nw, h, pw);
         if (on[u]) (k ? hk1 : hk0)[i] = h;
+        RecIn* ro = k ? rec1 : rec0;  // freq_project2's record of this side, for a general marginal
+        if (ro && on[u]) {            // (a utf8 part's key hash is its row hash)
+          RecIn r;
+          r.key = t.types[k] == DQ_UTF8 ? h : ((uint64_t)pw[1] | ((uint64_t)pw[2] << 32));
+          r.count = gi[u].count;
+          r.enc_off = gi[u].rep + 4ull * w;
+          ro[i] = r;
+        }
         if (!dead[k] && __ballot(on[u] && (!pw[0] || nw > 8u))) dead[k] = true;  // NULL part, long key
         if (!dead[k]) {
           int m = -1;
@@ -5602,6 +5611,11 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
   const char* fsm = getenv("DQ_FREQ_MI_NOSMALL");  // =1: no small-marginal pass (A/B, tests)
   bool small[2] = {false, false};  // side k's marginal aggregated by freq_small_marginal
   DevBuf<unsigned long long> hk[2];
+  // each side's records of the joint groups (kept: the lookups read their keys), written by the
+  // small-marginal pass for both sides (a side that is not small needs them; otherwise
+  // freq_project2 makes them in a pass of its own)
+  DevBuf<RecIn> rec[2];
+  bool rec_done = false;
   if (!force_lookup && !(fsm && atoi(fsm))) {
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((n + 511) / 512, 1), 2048);
     const int64_t nw = (int64_t)grid * 4;
@@ -5613,10 +5627,14 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
     HIP_TRY(ent.ensure((size_t)nw * 2 * kSmallMarg));
     HIP_TRY(nout.ensure((size_t)nw * 2));
     HIP_TRY(sfail.ensure(2));
+    HIP_TRY(rec[0].ensure(n));
+    HIP_TRY(rec[1].ensure(n));
     HIP_TRY(hipMemsetAsync(sfail.p, 0, 8, stream));
     hipLaunchKernelGGL(freq_small_marginal, dim3(grid), dim3(256), 0, stream, joint->compact.p, n,
-                       arena_of(joint), part_types(joint, 1), 3u, hk[0].p, hk[1].p, ent.p, nout.p, sfail.p);
+                       arena_of(joint), part_types(joint, 1), 3u, hk[0].p, hk[1].p, ent.p, nout.p, sfail.p,
+                       rec[0].p, rec[1].p);
     HIP_TRY(hipGetLastError());
+    rec_done = true;
     unsigned int hf[2];
     HIP_TRY(d2h(hf, sfail.p, 8, stream));
     if (!hf[0] || !hf[1]) {  // merge the waves' lists of each small side by (hash, words)
@@ -5655,11 +5673,9 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
     }
     stamp("small marginals");
   }
-  // the other sides' records in one pass over the joint groups (kept: the lookups read their keys)
-  DevBuf<RecIn> rec[2];
   for (int k = 0; k < 2; ++k)
     if (!small[k]) HIP_TRY(rec[k].ensure(n));
-  if (!small[0] || !small[1]) {
+  if (!rec_done && (!small[0] || !small[1])) {
     hipLaunchKernelGGL(freq_project2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, joint->stream,
                        joint->compact.p, n, arena_of(joint), part_types(joint, 1),
                        small[0] ? nullptr : rec[0].p, small[1] ? nullptr : rec[1].p);
