@@ -79,6 +79,12 @@ DQ_RUN_WORKERS=2 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps
 DQ_RUN_WORKERS=3 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 3 > $O/wl_c5w3_$T.json 2>&1 &&
 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 1 --pyprof > $O/pyprof_c5_$T.log 2>&1 &&
 DQ_RUN_TRACE=1 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 1 > $O/trace_c5_$T.log 2>&1
+elif [ "${PART}" = 15 ]; then
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke_$T.log 2>&1 &&
+timeout -k 10 200 python -u bench.py > $O/bench_$T.json 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_s10_$T -o run -- python3 bench.py --steps 20 > $O/prof_s10_$T.log 2>&1 &&
+timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 3 > $O/wl_c3_$T.json 2>&1 &&
+timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 10 --warmup 3 > $O/wl_c4_$T.json 2>&1
 elif [ "${PART}" = 14 ]; then
 timeout -k 10 400 python -u -m pytest tests/test_gpu_datatype_mi.py tests/test_gpu_configs4.py -x -q --timeout 200 --timeout-method thread > $O/gpu_tests_q_$T.log 2>&1 &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1 &&
