@@ -161,7 +161,13 @@ def test_mutual_information_hash_lookups_equal_byte_lookups(kinds, gpu_device, m
                                          (("string", "string"), (4, 3)),
                                          (("long", "string"), (7, 60_000)),
                                          (("double", "long"), (12, 5)),
-                                         (("string", "long"), (20, 9))])
+                                         (("string", "long"), (20, 9)),
+                                         # a general side of each record kind next to a small
+                                         # one: fixed-width, and utf8 over 16 bytes (hashed
+                                         # from memory)
+                                         (("long", "string"), (80_000, 3)),
+                                         (("double", "string"), (70_000, 4)),
+                                         (("lstring", "string"), (40_000, 5))])
 def test_mutual_information_small_marginals(kinds, cards, gpu_device, monkeypatch):
     """A side with few values has its marginal aggregated in one pass over the joint groups
     (freq_small_marginal: per-wave value lists merged by hash and key words); a side with more
@@ -177,14 +183,19 @@ def test_mutual_information_small_marginals(kinds, cards, gpu_device, monkeypatc
         mask = rng.random(n) < 0.05
         if kind == "string":
             return pa.array([None if m else f"val-{x}" for x, m in zip(v, mask)], pa.string())
+        if kind == "lstring":
+            return pa.array([None if m else f"a-value-longer-than-sixteen-bytes-{x}"
+                             for x, m in zip(v, mask)], pa.string())
         if kind == "double":
             return pa.array(v * 0.5 - 1.0, mask=mask, type=pa.float64())
         return pa.array(v, mask=mask, type=pa.int64())
     a, b = col(kinds[0], cards[0]), col(kinds[1], cards[1])
     df = _df({"a": a, "b": b}, gpu_device, 40_000)
     got = MutualInformation("a", "b").calculate(df).value.get()
+    okind = {"lstring": "string"}
     exp = mutual_information(OTable({"a": a.to_pylist(), "b": b.to_pylist()},
-                                    {"a": kinds[0], "b": kinds[1]}), "a", "b")
+                                    {"a": okind.get(kinds[0], kinds[0]),
+                                     "b": okind.get(kinds[1], kinds[1])}), "a", "b")
     assert abs(got - exp) <= 1e-12 * max(1.0, abs(exp)), (got, exp)
     monkeypatch.setenv("DQ_FREQ_MI_NOSMALL", "1")
     ref = MutualInformation("a", "b").calculate(df).value.get()

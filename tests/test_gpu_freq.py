@@ -690,3 +690,42 @@ def test_two_small_string_columns_dedupe_on_short_forms(long_frac, gpu_device):
     assert s.n_unique == sum(1 for c in exp.values() if c == 1)
     assert dict(ft.export()) == exp
     assert _rel_close(s.entropy, O.entropy(exp, n))
+
+
+def test_large_export_reads_back_past_the_pinned_staging(gpu_device):
+    """An export of 3.2M groups (77 MB of records) takes d2h's plain-copy path (blocks over 64 MB
+    are not staged through pinned memory); every group and count must come back."""
+    rng = np.random.default_rng(77)
+    n = 3_400_000
+    ids = rng.permutation(np.arange(n, dtype=np.int64) * 7919)[: 3_200_000]
+    ids = np.concatenate([ids, ids[:200_000]])  # 200k keys twice
+    t = pa.table({"id": pa.array(ids, type=pa.int64())})
+    ft = _freq_table(t, ["id"], gpu_device)
+    got = dict(ft.export())
+    keys, counts = np.unique(ids, return_counts=True)
+    assert len(got) == len(keys)
+    assert sum(got.values()) == len(ids)
+    exp = dict(zip(keys.tolist(), counts.tolist()))
+    assert got == {(k,): c for k, c in exp.items()}
+
+
+def test_many_small_key_tables_reuse_pinned_words(gpu_device):
+    """More tables than one pinned block holds (512 small-key flag words), each created,
+    filled through the small-key path and destroyed: every one counts its groups right."""
+    from deequ_amd.analyzers.grouping import _fold_null_group
+    from deequ_amd import _native as N
+    rng = np.random.default_rng(5)
+    n = 5000
+    words = np.array(["a", "bb", "ccc", "dd"])
+    for i in range(600):
+        v = words[rng.integers(0, len(words) - (i % 2), n)]
+        mask = rng.random(n) < 0.1
+        t = pa.table({"s": pa.array([None if m else x for x, m in zip(v, mask)], pa.string())})
+        ft = _freq_table(t, ["s"], gpu_device, null_as_group=True)
+        top, bins = _fold_null_group(ft, N.UTF8, 10)
+        exp = {}
+        for x, m in zip(v, mask):
+            k = "NullValue" if m else x
+            exp[k] = exp.get(k, 0) + 1
+        assert dict(top) == exp and bins == len(exp), i
+        del ft
