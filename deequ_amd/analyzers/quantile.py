@@ -82,10 +82,9 @@ class QuantileSummaries:
         """values[j] = the sorted value at rank floor(j (count-1) / (m-1)): a GK summary with
         g = the rank gap, delta = 0."""
         m = len(values)
-        ranks = [(j * (count - 1)) // (m - 1) for j in range(m)]
-        out: List[Sample] = [(float(values[0]), 1, 0)]
-        for j in range(1, m):
-            out.append((float(values[j]), ranks[j] - ranks[j - 1], 0))
+        ranks = [(j * (count - 1)) // (m - 1) for j in range(m)]  # (exact: Python integers)
+        gaps = [1] + [ranks[j] - ranks[j - 1] for j in range(1, m)]
+        out: List[Sample] = list(zip(np.asarray(values, np.float64)[:m].tolist(), gaps, [0] * m))
         return QuantileSummaries(relative_error, out, count).compress()
 
     def compress(self) -> "QuantileSummaries":
