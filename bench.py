@@ -266,6 +266,7 @@ def main():
                 "algorithmic_bytes_per_launch": b_alg,
                 "scan_ms": scan_ms,
                 "kernel": "dq::scan_mixed_kernel (+ finalize1/finalize2)",
+                "scan_code_object_sha": scan_code_object_hash(),
             },
         }
         if world == 1 and not args.no_h2d:
@@ -277,23 +278,38 @@ def main():
         dist.destroy_process_group()
 
 
-SCAN_SOURCES = ("scan.hip", "kernels.h", "engine.h", "device_util.h", "stream_load.h")
-
-
-def scan_source_hash() -> str:
-    """sha256 (16 hex digits) of the sources the scan kernel is compiled from: a PMC traffic
-    figure only describes the build whose sources hash the same."""
+def scan_code_object_hash() -> str:
+    """sha256 (16 hex digits) of the gfx950 code object that holds dq::scan_mixed_kernel, read from
+    the clang offload bundles in libdeequ_amd.so's .hip_fatbin section.  Each HIP translation unit
+    is its own bundle, so this is exactly scan.hip's device code as built: host-only edits (a
+    prototype in kernels.h) leave it unchanged, any change to the scan kernels' ISA changes it.  A
+    PMC traffic figure only describes the build whose code object hashes the same."""
     import hashlib
-    h = hashlib.sha256()
-    for name in SCAN_SOURCES:
-        h.update(open(os.path.join(ROOT, "deequ_amd", "csrc", name), "rb").read())
-    return h.hexdigest()[:16]
+    import struct
+    from deequ_amd import _native
+    data = open(_native.LIB_PATH, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    pos = data.find(magic)
+    while pos >= 0:
+        p = pos + len(magic)
+        (entries,) = struct.unpack_from("<Q", data, p)
+        p += 8
+        for _ in range(entries):
+            off, size, tlen = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            triple = data[p:p + tlen].decode()
+            p += tlen
+            code = data[pos + off:pos + off + size]
+            if "gfx950" in triple and b"scan_mixed_kernel" in code:
+                return hashlib.sha256(code).hexdigest()[:16]
+        pos = data.find(magic, pos + 1)
+    raise RuntimeError("no gfx950 code object with scan_mixed_kernel in " + _native.LIB_PATH)
 
 
 def load_traffic(rows: int, b_alg: int):
     """(HBM bytes per scan launch, source) from the committed rocprofv3 PMC passes
     (profiles/traffic_s10.json) when they were recorded for this workload size AND this build of
-    the scan kernel (source hash); else (None, why)."""
+    the scan kernel (its gfx950 code object's hash); else (None, why)."""
     path = os.path.join(ROOT, "profiles", "traffic_s10.json")
     try:
         d = json.load(open(path))
@@ -301,12 +317,13 @@ def load_traffic(rows: int, b_alg: int):
         return None, "no profiles/traffic_s10.json"
     if int(d.get("rows_per_gpu", -1)) != rows:
         return None, f"profiles/traffic_s10.json is for {d.get('rows_per_gpu')} rows per GPU"
-    if d.get("scan_source_sha") != scan_source_hash():
+    sha = scan_code_object_hash()
+    if d.get("scan_code_object_sha") != sha:
         return None, (f"profiles/traffic_s10.json ({d.get('tag')}) was measured on another build "
-                      f"of the scan kernel (source hash {d.get('scan_source_sha')} != "
-                      f"{scan_source_hash()})")
+                      f"of the scan kernel (code object hash {d.get('scan_code_object_sha')} != "
+                      f"{sha})")
     return d["hbm_bytes_per_launch"], (
-        f"profiles/traffic_s10.json ({d.get('tag')}, scan source hash {d['scan_source_sha']}): "
+        f"profiles/traffic_s10.json ({d.get('tag')}, scan.hip gfx950 code object sha256 {sha}): "
         "HBM bytes per scan launch from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
         "of this command (FETCH_SIZE x 2 on gfx950, KiB units), not this run")
 

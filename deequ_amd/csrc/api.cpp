@@ -219,6 +219,19 @@ static void compile_postfix(const Node& n, std::vector<XInstr>& prog, std::strin
   prog.push_back(ins);
 }
 
+// CAST(x AS FLOAT) of a string operand (a utf8 column or a string literal): Spark parses it with
+// Float.parseFloat, which the interpreter does not restate (it would parse a double and skip the
+// float rounding), so the plan refuses it rather than compute a different value.
+static bool casts_string_to_float(const Node& n, const std::vector<int32_t>& types) {
+  if (n.op == DQ_X_CAST_F32 && !n.kids.empty()) {
+    const Node& x = *n.kids[0];
+    if (x.op == DQ_X_STR || (x.op == DQ_X_COL && types[x.col] == DQ_UTF8)) return true;
+  }
+  for (auto& k : n.kids)
+    if (casts_string_to_float(*k, types)) return true;
+  return false;
+}
+
 static int stack_depth(const Node& n) {
   int best = 0, k = 0;
   for (auto& c : n.kids) best = std::max(best, k++ + stack_depth(*c));
@@ -463,6 +476,8 @@ extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
       return fail(DQ_ERR_INVALID_ARGUMENT, "malformed expression %d", e);
     if (stack_depth(*n) > kMaxStack)
       return fail(DQ_ERR_UNSUPPORTED, "expression %d nests deeper than %d", e, kMaxStack);
+    if (casts_string_to_float(*n, p->types))
+      return fail(DQ_ERR_UNSUPPORTED, "expression %d casts a string to FLOAT", e);
     p->exprs.push_back(std::move(n));
   }
   p->aggs.assign(desc->aggs, desc->aggs + desc->n_aggs);
@@ -1853,15 +1868,25 @@ void dev_free(void* p, size_t bytes, int dev) {
 }
 
 namespace {
-struct PinnedPool {  // page-locked staging blocks (powers of two >= 4 KB), kept to process exit
+struct PinnedPool {  // page-locked staging blocks (powers of two >= 4 KB), at most kPinnedKeep
   std::mutex m;
   std::multimap<size_t, void*> free_blocks;
+  size_t cached = 0;
 };
+constexpr size_t kPinnedKeep = 256u << 20;  // bytes of idle blocks kept for reuse
 PinnedPool& pinned_pool() {
   static PinnedPool* pool = new PinnedPool;
   return *pool;
 }
 }  // namespace
+
+void release_pinned_staging() {
+  PinnedPool& pool = pinned_pool();
+  std::lock_guard<std::mutex> lock(pool.m);
+  for (auto& kv : pool.free_blocks) (void)hipHostFree(kv.second);
+  pool.free_blocks.clear();
+  pool.cached = 0;
+}
 
 hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
   if (!bytes) return hipStreamSynchronize(st);
@@ -1875,6 +1900,7 @@ hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
     if (it != pool.free_blocks.end()) {
       want = it->first;
       buf = it->second;
+      pool.cached -= want;
       pool.free_blocks.erase(it);
     }
   }
@@ -1888,13 +1914,29 @@ hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
   }
   hipError_t e = hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e == hipSuccess) memcpy(dst, buf, bytes);
-  std::lock_guard<std::mutex> lock(pool.m);
-  pool.free_blocks.emplace(want, buf);
-  return e;
+  if (e != hipSuccess) return e;  // (the block is dropped: a DMA may still be writing it)
+  memcpy(dst, buf, bytes);
+  bool keep;
+  {
+    std::lock_guard<std::mutex> lock(pool.m);
+    keep = pool.cached + want <= kPinnedKeep;
+    if (keep) {
+      pool.free_blocks.emplace(want, buf);
+      pool.cached += want;
+    }
+  }
+  if (!keep) (void)hipHostFree(buf);
+  return hipSuccess;
 }
 
 }  // namespace dq
+
+extern "C" int64_t dq_cached_device_bytes(int device) {
+  if (device < 0 || device >= dq::kPoolDevices) return 0;
+  dq::DevPool& pool = dq::dev_pool();
+  std::lock_guard<std::mutex> lock(pool.m);
+  return (int64_t)pool.cached[device];
+}
 
 extern "C" void dq_release_cached_memory(void) {
   int cur = 0;
@@ -1909,4 +1951,5 @@ extern "C" void dq_release_cached_memory(void) {
     dq::release_cached(d);
   }
   (void)hipSetDevice(cur);
+  dq::release_pinned_staging();
 }

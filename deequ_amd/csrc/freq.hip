@@ -3975,8 +3975,9 @@ static hipError_t pinned_word_get(unsigned long long** out) {
   w.free_words.pop_back();
   return hipSuccess;
 }
+// The caller has synchronized the stream of the last copy into the word (dq_freq_destroy), so
+// no copy can still land in it; no device-wide barrier (it would wait for other tables' streams).
 static void pinned_word_put(unsigned long long* p) {
-  (void)hipDeviceSynchronize();  // (as hipHostFree: no copy may still land in the word)
   PinnedWords& w = pinned_words();
   std::lock_guard<std::mutex> lock(w.m);
   w.free_words.push_back(p);
@@ -4024,6 +4025,7 @@ struct dq_freq {
   bool fast_off = false;
   struct PinnedWord {
     unsigned long long* p = nullptr;
+    hipStream_t last_copy = nullptr;  // the stream of the last copy into *p
     ~PinnedWord() {
       if (p) pinned_word_put(p);
     }
@@ -5400,6 +5402,8 @@ extern "C" void dq_freq_destroy(dq_freq* f) {
   if (!f) return;
   (void)hipSetDevice(f->device);
   (void)hipStreamSynchronize(f->stream);
+  if (f->fast_seen.last_copy && f->fast_seen.last_copy != f->stream)
+    (void)hipStreamSynchronize(f->fast_seen.last_copy);  // (the word's copies, pinned_word_put)
   delete f;
 }
 
@@ -5481,8 +5485,10 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     launch_phaseA<true>(f, a, false);
   }
   HIP_TRY(hipGetLastError());
-  if (small)  // the host learns (late, without a wait) whether the attempt gave the batch up
+  if (small) {  // the host learns (late, without a wait) whether the attempt gave the batch up
     HIP_TRY(hipMemcpyAsync(f->fast_seen.p, a.fast_words, 8, hipMemcpyDeviceToHost, f->stream));
+    f->fast_seen.last_copy = f->stream;
+  }
   f->n_chunks += chunks;
   f->counters_stale = true;  // read back at finalize / merge / arena growth
   return DQ_OK;

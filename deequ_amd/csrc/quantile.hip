@@ -470,6 +470,18 @@ struct Passer {
   std::vector<unsigned long long> h, mmh;
   dq_status run(const Source& src, const std::vector<uint64_t>& prefixes, int bits, int D, Pass& p) {
     const int A = (int)prefixes.size(), nb = A << D;
+    // LDS of rs_hist: A prefixes + their min / max (24 B each), the prefix map (16 KB at 13 bits)
+    // and the bins (A << D <= kSelBins counters): at most 2048 ranks -> 96 KB, inside gfx950's
+    // 160 KB per workgroup; checked against the device so a smaller part fails loudly
+    {
+      const Pass q{nullptr, A, bits, D, src.R};
+      const size_t need = pass_lds_words(q, bits > 0) * 8 + (size_t)nb * 4;
+      int dev = 0, cap = 0;
+      HIP_TRY(hipGetDevice(&dev));
+      HIP_TRY(hipDeviceGetAttribute(&cap, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+      if (need > (size_t)cap)
+        return fail(DQ_ERR_UNSUPPORTED, "radix select pass needs %zu B of LDS (device: %d)", need, cap);
+    }
     HIP_TRY(act.ensure(A));
     HIP_TRY(hipMemcpyAsync(act.p, prefixes.data(), (size_t)A * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(partial.ensure((size_t)src.G * nb));

@@ -407,11 +407,36 @@ def _stages_of(job):
     return None
 
 
+def _launch_failed(st) -> bool:
+    """The launch stage of _histogram_and_grouping_job / _histogram_scan_launch built no table."""
+    return st[6] is None if len(st) == 7 else st[2] is not None
+
+
+def _table_fits_beside(job) -> bool:
+    """Whether job's group-by table fits on the device while the previous job's table is still
+    held: its estimate (about 64 bytes per row plus twice its key bytes, as _job_workers) against
+    the device's free bytes plus the idle blocks of the engine's cache."""
+    data = job.args[0]
+    cols = [job.args[1]] if job.func is _histogram_and_grouping_job else [job.args[1][0].column]
+    try:
+        import torch
+        dev = data.device_index()
+        need = 64 * data.num_rows + 2 * sum(b[c].nbytes() for b in data.batches for c in cols
+                                            if c in b)
+        free, _ = torch.cuda.mem_get_info(dev)
+        from .. import _native as N
+        return free + int(N.lib.dq_cached_device_bytes(dev)) >= need
+    except Exception:  # noqa: BLE001  (no estimate: do not overlap)
+        return False
+
+
 def _run_jobs_pipelined(jobs, trace: bool = False) -> list:
     """One job at a time, except that a Histogram job's host-only stage runs after the next
     Histogram job's batches are queued, so the device works through that job's phase A
-    meanwhile (the host stage touches only the finished table's caches).  trace
-    (DQ_RUN_TRACE=2): each stage's wall time on stderr."""
+    meanwhile (the host stage touches only the finished table's caches).  That holds two tables
+    on the device at once, so it is done only when the next table's estimate fits beside the
+    held one (_table_fits_beside); a launch that fails beside it runs again after the held
+    table's host stage.  trace (DQ_RUN_TRACE=2): each stage's wall time on stderr."""
     out = [None] * len(jobs)
     pending = None  # (index, host stage, state) of a job whose host stage has not run
     clock = time.perf_counter
@@ -429,9 +454,15 @@ def _run_jobs_pipelined(jobs, trace: bool = False) -> list:
         stages = _stages_of(job)
         if stages is not None:
             launch, device, host = stages
+            if pending is not None and not _table_fits_beside(job):
+                out[pending[0]] = stage("host", pending[0], pending[1], pending[2])
+                pending = None
             st = stage("launch", i, launch, *job.args)
             if pending is not None:
                 out[pending[0]] = stage("host", pending[0], pending[1], pending[2])
+                pending = None
+                if _launch_failed(st):  # (maybe out of memory beside the other table: again alone)
+                    st = stage("launch", i, launch, *job.args)
             stage("device", i, device, st)
             pending = (i, host, st)
             continue

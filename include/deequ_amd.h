@@ -166,8 +166,9 @@ typedef enum dq_xop {
                           PatternMatch.scala:44-46).                                           */
   DQ_X_CAST_F32 = 22   /* [op, x]  CAST(x AS FLOAT): an integral x rounds to the nearest float,
                           a double one too (Spark's Cast to FloatType, `.toFloat`); the value
-                          then prints as Float.toString.  (A string x is refused by the host
-                          compiler: Float.parseFloat's direct rounding is not restated.)       */
+                          then prints as Float.toString.  A string x (utf8 column or literal)
+                          is refused by dq_plan_create with DQ_ERR_UNSUPPORTED:
+                          Float.parseFloat's direct rounding is not restated.                  */
 } dq_xop;
 
 typedef struct dq_expr {
@@ -434,6 +435,12 @@ dq_status dq_key_partition(const dq_column* batches, int n_batches, int n_parts,
  * to a per-device cache when freed, so building many tables does not hipMalloc / hipFree
  * gigabytes each time) to the HIP runtime. */
 void dq_release_cached_memory(void);
+
+/* Bytes of idle device blocks the engine's cache holds for `device` (reusable by the next dq_*
+ * allocation without a hipMalloc; the runner adds them to hipMemGetInfo's free bytes when it
+ * decides whether two group-by tables may be on the device at once).  No reference counterpart:
+ * Spark's memory manager is the JVM's. */
+int64_t dq_cached_device_bytes(int device);
 
 /* Spark 2.2 Cast(StringType -> LongType | DoubleType) of a utf8 column, on the device: the
  * ColumnProfiler's cast of string columns inferred numeric (profiles/ColumnProfiler.scala:311-320,

@@ -90,6 +90,40 @@ def test_bad_expression_is_an_analysis_error():
         Plan(schema, Compliance("r", "attNoSuchColumn > 3").aggregation_functions())
 
 
+@pytest.mark.parametrize("operand", ["column", "literal"])
+def test_plan_refuses_cast_of_a_string_to_float(operand):
+    """DQ_X_CAST_F32 over a utf8 column or a string literal: Spark's Float.parseFloat is not
+    restated, so dq_plan_create refuses it (a C-ABI caller cannot bypass sqlexpr's check)."""
+    import ctypes
+    import struct
+    from deequ_amd import _native as N
+    x = [N.X_COL, 0] if operand == "column" else [N.X_STR, 3, int.from_bytes(b"1.5", "little")]
+    one = struct.unpack("<q", struct.pack("<d", 1.0))[0]
+    words = [N.X_GT, N.X_CAST_F32] + x + [N.X_F64, one]
+    buf = (ctypes.c_int64 * len(words))(*words)
+    expr = (N.dq_expr * 1)()
+    expr[0].words = ctypes.cast(buf, ctypes.POINTER(ctypes.c_int64))
+    expr[0].n_words = len(words)
+    agg = N.dq_agg()
+    agg.kind, agg.col, agg.col2, agg.expr, agg.where = N.AGG_COUNT_TRUE, -1, -1, 0, -1
+    aggs = (N.dq_agg * 1)(agg)
+    types = (ctypes.c_int32 * 1)(N.UTF8)
+    desc = N.dq_plan_desc()
+    desc.n_columns, desc.column_types, desc.n_exprs, desc.exprs = 1, types, 1, expr
+    desc.n_aggs, desc.aggs = 1, aggs
+    handle = ctypes.c_void_p()
+    assert N.lib.dq_plan_create(ctypes.byref(desc), ctypes.byref(handle)) == N.ERR_UNSUPPORTED
+    assert b"FLOAT" in N.lib.dq_last_error()
+    # the same cast of an integral column plans
+    types[0] = N.INT64
+    words[2:2 + len(x)] = [N.X_COL, 0]
+    buf = (ctypes.c_int64 * len(words))(*words)
+    expr[0].words = ctypes.cast(buf, ctypes.POINTER(ctypes.c_int64))
+    expr[0].n_words = len(words)
+    assert N.lib.dq_plan_create(ctypes.byref(desc), ctypes.byref(handle)) == 0
+    N.lib.dq_plan_destroy(handle)
+
+
 def test_hll_count_matches_oracle_on_random_registers():
     import random
     from deequ_amd import _native as N

@@ -34,6 +34,8 @@ def test_staged_jobs_overlap_host_with_the_next_launch(monkeypatch):
         return (launch, device, host) if job.func is _staged else None
 
     monkeypatch.setattr(R, "_stages_of", stages_of)
+    monkeypatch.setattr(R, "_table_fits_beside", lambda job: True)
+    monkeypatch.setattr(R, "_launch_failed", lambda st: False)
     jobs = [functools.partial(_plain, log, "p0"), functools.partial(_staged, "a"),
             functools.partial(_staged, "b"), functools.partial(_staged, "c"),
             functools.partial(_plain, log, "p1"), functools.partial(_staged, "d")]
@@ -45,6 +47,48 @@ def test_staged_jobs_overlap_host_with_the_next_launch(monkeypatch):
                    ("launch", "c"), ("host", "b"), ("device", "c"),
                    ("host", "c"), ("job", "p1"),
                    ("launch", "d"), ("device", "d"), ("host", "d")]
+
+
+def test_staged_jobs_do_not_overlap_without_device_memory(monkeypatch):
+    """overlapping holds two tables on the device.  A job whose table does not fit
+    beside the held one runs after that job's host stage; a launch that fails beside it (out of
+    memory) runs again once the held table's host stage is done."""
+    log = []
+    fails = {"c": 1}  # c's first launch fails
+
+    def launch(name):
+        log.append(("launch", name))
+        if fails.get(name):
+            fails[name] -= 1
+            return "failed:" + name
+        return name
+
+    def device(st):
+        log.append(("device", st))
+
+    def host(st):
+        log.append(("host", st))
+        return "metrics:" + st
+
+    monkeypatch.setattr(R, "_stages_of", lambda job: (launch, device, host)
+                        if job.func is _staged else None)
+    monkeypatch.setattr(R, "_table_fits_beside", lambda job: job.args[0] != "b")
+    monkeypatch.setattr(R, "_launch_failed", lambda st: st.startswith("failed:"))
+    jobs = [functools.partial(_staged, n) for n in "abcd"]
+    out = R._run_jobs_pipelined(jobs)
+    assert out == ["metrics:a", "metrics:b", "metrics:c", "metrics:d"]
+    assert log == [("launch", "a"), ("device", "a"),
+                   ("host", "a"), ("launch", "b"), ("device", "b"),       # b does not fit beside a
+                   ("launch", "c"), ("host", "b"), ("launch", "c"),       # c failed beside b
+                   ("device", "c"),
+                   ("launch", "d"), ("host", "c"), ("device", "d"), ("host", "d")]
+
+
+def test_launch_failed_reads_both_staged_job_kinds():
+    assert R._launch_failed((None,) * 7)
+    assert not R._launch_failed((None,) * 6 + (object(),))
+    assert R._launch_failed((object(), None, ValueError("x")))
+    assert not R._launch_failed((object(), object(), None))
 
 
 def test_histogram_scan_jobs_are_staged_only_without_state_io():

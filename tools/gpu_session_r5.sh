@@ -1,0 +1,41 @@
+#!/bin/bash
+# Round-5 sessions; TAG names outputs, PART selects the steps.  Every GPU step runs under its own
+# time limit and the steps are chained with &&: a failure, fault or time-out ends the session.
+#  PART=full:  the stated-size checks (tests/test_gpu_fullsize.py), the whole -m gpu suite, then
+#              the S10 evidence session (tools/gpu_s10_prof.sh: bench line, kernel stats,
+#              FETCH_SIZE / WRITE_SIZE passes).
+#  PART=tests: the -m gpu suite only (TESTS narrows it).
+#  PART=wl:    configs[2] / [3] / [4] lines (tools/bench_workloads.py).
+#  PART=c3:    configs[2] line, its rocprof kernel stats and PMC passes (tools/gpu_pmc_c3.sh).
+#  PART=c5:    configs[4] line and its rocprof kernel stats.
+set -o pipefail
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+O=gpurun_out
+T=${TAG:-r5}
+mkdir -p $O
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+case "${PART:-full}" in
+full)
+  timeout -k 10 600 $PYT tests/test_gpu_fullsize.py > $O/gpu_fullsize_$T.log 2>&1 &&
+  timeout -k 10 700 $PYT tests -m gpu --ignore=tests/test_gpu_fullsize.py > $O/gpu_tests_$T.log 2>&1 &&
+  TAG=$T bash tools/gpu_s10_prof.sh
+  ;;
+tests)
+  timeout -k 10 ${LIMIT:-800} $PYT ${TESTS:-tests} -m gpu > $O/gpu_tests_$T.log 2>&1
+  ;;
+wl)
+  timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
+  timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 10 --warmup 3 > $O/wl_c4_$T.json 2>&1 &&
+  timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_$T.json 2>&1
+  ;;
+c3)
+  timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_$T -o run -- python3 tools/bench_workloads.py c3 --steps 2 > $O/prof_c3_$T.log 2>&1 &&
+  TAG=$T bash tools/gpu_pmc_c3.sh
+  ;;
+c5)
+  timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_$T.json 2>&1 &&
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1
+  ;;
+esac

@@ -89,10 +89,14 @@ def main():
             summary["traffic_over_algorithmic"] = d["hbm_bytes_per_dispatch"] / b_alg
     json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
     if dominant and kernels[dominant]["hbm_bytes_per_dispatch"]:
-        sys.path.insert(0, ROOT)
-        from bench import scan_source_hash
+        # the code object the profiled bench ran (its own line), else this tree's build
+        sha = (bench or {}).get("roofline", {}).get("scan_code_object_sha")
+        if not sha:
+            sys.path.insert(0, ROOT)
+            from bench import scan_code_object_hash
+            sha = scan_code_object_hash()
         json.dump({"tag": tag, "rows_per_gpu": rows, "kernel": dominant,
-                   "scan_source_sha": scan_source_hash(),
+                   "scan_code_object_sha": sha,
                    "hbm_bytes_per_launch": kernels[dominant]["hbm_bytes_per_dispatch"],
                    "source": f"profiles/{tag}/dq_counters.csv (2 x FETCH_SIZE + WRITE_SIZE, KiB)"},
                   open(os.path.join(ROOT, "profiles", "traffic_s10.json"), "w"), indent=1)
