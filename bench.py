@@ -3,8 +3,9 @@
 
 One step = one pass of the hot path over the table resident in HBM: reset the aggregation state,
 the fused scan of every record batch in ONE launch (+ the finalize launch), the state read-back
-and, with N > 1 ranks, the exchange step (all-gather of the serialized per-rank states over RCCL
-and the rank-ordered merge).  Rows are sharded across ranks with no data-path collective, so
+and, with N > 1 ranks, the exchange step on the device (distributed.exchange_states: counters in
+one RCCL all-reduce SUM, extremes and HLL registers in one all-reduce MAX, the fp64 moments
+all-gathered and merged in rank order by a kernel).  Rows are sharded across ranks with no data-path collective, so
 per-GPU work is fixed (weak scaling); `value` = rows of all ranks / max-over-ranks step time.
 
 Output: ONE JSON line (rank 0).  `roofline.achieved` = algorithmic bytes of the suite (the distinct
@@ -179,7 +180,7 @@ def main():
 
     from deequ_amd import _native as N
     from deequ_amd.analyzers.base import AggSpec  # noqa: F401
-    from deequ_amd.distributed import merge_states_across_ranks
+    from deequ_amd.distributed import exchange_states
     from deequ_amd.runners.engine import get_plan, read_row, scan_into
     from deequ_amd.synth import item_table_device
 
@@ -201,9 +202,9 @@ def main():
         scan_into(table, plan, state, sh)
         if i is not None:
             ev1[i].record(stream)
+        if world > 1:  # SUM / MAX all-reduces + gathered moments merged on the device
+            return exchange_states(plan, state, device)
         N.check(N.lib.dq_state_sync(state))
-        if world > 1:
-            return merge_states_across_ranks(plan, state, device)
         return read_row(plan, state)
 
     for _ in range(args.warmup):

@@ -753,6 +753,10 @@ struct dq_state {
   DevBuf<Acc> d_acc, d_partial, d_partial2;
   DevBuf<uint8_t> d_hll;
   DevBuf<uint32_t> d_hll_stage;  // per-launch HLL registers (u32), kept zero between launches
+  DevBuf<int64_t> d_rows;        // the merged row count of an exchange (dq_state_exchange_unpack)
+  DevBuf<int32_t> d_kinds;       // the plan's task kinds (the exchange kernels)
+  hipEvent_t ev_xchg = nullptr;  // orders the exchange kernels and the collectives' stream
+  bool rows_on_device = false;   // ... not yet read back (dq_state_sync reads it with the rest)
   DevBuf<uint32_t> d_queue;      // work-item counters of the scan kernels, kept zero between launches
   DevBuf<uint32_t> d_order[2];   // mixed launch: queue position -> item (per descriptor slot)
   std::vector<uint32_t> order_sig[2];  // per-class item ranges d_order[slot] was built for
@@ -789,6 +793,7 @@ struct dq_state {
       if (h_cols[k]) (void)hipHostFree(h_cols[k]);
       if (ev[k]) (void)hipEventDestroy(ev[k]);
     }
+    if (ev_xchg) (void)hipEventDestroy(ev_xchg);
   }
 };
 
@@ -927,6 +932,7 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
   HIP_TRY(s->d_partial.ensure(1024));
   HIP_TRY(s->d_partial2.ensure(nt * (size_t)kFinParts));
   for (int k = 0; k < 2; ++k) HIP_TRY(hipEventCreateWithFlags(&s->ev[k], hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&s->ev_xchg, hipEventDisableTiming));
   // expression programs and string pools
   std::vector<XInstr> prog;
   std::string pool;
@@ -1103,6 +1109,10 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
   if (s->device < 0) return fail(DQ_ERR_STATE, "host-only state (device -1) cannot scan");
   hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
   HIP_TRY(hipSetDevice(s->device));
+  if (s->rows_on_device) {  // an exchange's merged rows: read back before adding to them
+    const dq_status rs = dq_state_sync(s);
+    if (rs != DQ_OK) return rs;
+  }
   if (s->stream_set && s->stream != stream) HIP_TRY(hipStreamSynchronize(s->stream));
   s->stream = stream;
   s->stream_set = true;
@@ -1389,17 +1399,21 @@ extern "C" dq_status dq_state_sync(dq_state* s) {
   HIP_TRY(hipSetDevice(s->device));
   // both read-backs queued behind the scan on its stream, one host wait
   const size_t ab = s->acc.size() * sizeof(Acc), hb = s->hll.size();
+  const size_t rb = s->rows_on_device ? 8 : 0;
   {
-    const dq_status ps = pin_ensure(s, ab + hb);
+    const dq_status ps = pin_ensure(s, ab + hb + 8);
     if (ps != DQ_OK) return ps;
   }
   uint8_t* pin = static_cast<uint8_t*>(s->h_pin);
   if (ab) HIP_TRY(hipMemcpyAsync(pin, s->d_acc.p, ab, hipMemcpyDeviceToHost, s->stream));
   if (hb) HIP_TRY(hipMemcpyAsync(pin + ab, s->d_hll.p, hb, hipMemcpyDeviceToHost, s->stream));
+  if (rb) HIP_TRY(hipMemcpyAsync(pin + ab + hb, s->d_rows.p, rb, hipMemcpyDeviceToHost, s->stream));
   HIP_TRY(hipStreamSynchronize(s->stream));
   s->pin_pending = false;
   if (ab) memcpy(s->acc.data(), pin, ab);
   if (hb) memcpy(s->hll.data(), pin + ab, hb);
+  if (rb) memcpy(&s->rows, pin + ab + hb, 8);
+  s->rows_on_device = false;
   s->synced = true;
   return DQ_OK;
 }
@@ -1493,6 +1507,196 @@ extern "C" dq_status dq_state_get_all(const dq_state* s, int n, dq_value* out) {
     const dq_status st = dq_state_get(s, k, out + k);
     if (st != DQ_OK) return st;
   }
+  return DQ_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// State exchange across ranks (distributed.py exchange_states): the counters and
+// wrapping Long sums meet in ONE SUM all-reduce, the extremes and the HLL registers in ONE MAX
+// all-reduce, and the fp64 moments in ONE all-gather that a kernel merges in rank order with
+// acc_merge's rules (StandardDeviation.scala:37-44, Correlation.scala:37-52).  The result equals
+// dq_state_merge over the ranks' states in rank order, bit for bit: integer adds wrap and are
+// associative, max / min are exact, and the fp64 merges run in the same order from the same inputs.
+//   isum[10 T + 1]        every task's Acc.i (TK_NUMERIC's min / max keys as 0), then the rows
+//   imax[2 T + 512 n_hll] TK_NUMERIC max keys, then ~min keys (bitwise NOT reverses the signed
+//                         order: MAX of ~min = ~MIN), then the HLL registers widened to int64
+//   mom[8 T]              per task: n, 1 when acc_merge would not skip the buffer, d0..d5;
+//                         gathered rank-major as [world][8 T]
+// ------------------------------------------------------------------------------------------------
+namespace {
+constexpr int kMomW = 8;
+
+DQ_HD void xchg_pack_task(int kind, const Acc& a, int k, int T, int64_t* isum, int64_t* imax,
+                          double* mom) {
+  for (int q = 0; q < 10; ++q) isum[10 * k + q] = a.i[q];
+  if (kind == TK_NUMERIC) {
+    isum[10 * k + 2] = isum[10 * k + 3] = 0;
+    imax[k] = a.i[3];
+    imax[T + k] = ~a.i[2];
+  } else {
+    imax[k] = imax[T + k] = INT64_MIN;
+  }
+  double* m = mom + (size_t)kMomW * k;
+  const bool live = kind == TK_NUMERIC ? (a.i[0] || a.i[7] || a.i[8] || a.i[9]) : a.i[0] != 0;
+  m[0] = (double)a.i[0];
+  m[1] = live ? 1.0 : 0.0;
+  for (int q = 0; q < 6; ++q) m[2 + q] = a.d[q];
+}
+
+// The merged Acc of task k: acc_merge(init, rank 0, rank 1, ...) restated over the exchange
+DQ_HD void xchg_merge_task(int kind, int k, int T, int world, const int64_t* isum,
+                           const int64_t* imax, const double* momg, Acc& out) {
+  for (int q = 0; q < 10; ++q) out.i[q] = isum[10 * k + q];
+  for (int q = 0; q < 6; ++q) out.d[q] = 0.0;
+  if (kind == TK_NUMERIC) {
+    out.i[2] = ~imax[T + k];
+    out.i[3] = imax[k];
+  }
+  double na = 0.0;
+  for (int r = 0; r < world; ++r) {
+    const double* b = momg + ((size_t)r * T + k) * kMomW;
+    if (kind == TK_NUMERIC) {
+      if (b[1] == 0.0) continue;
+      if (b[0] > 0.0) {
+        if (na == 0.0) {
+          out.d[1] = b[3];
+          out.d[2] = b[4];
+        } else {
+          moments_merge(na, out.d[1], out.d[2], b[0], b[3], b[4]);
+        }
+      }
+      na += b[0];
+      out.d[0] += b[2];
+    } else if (kind == TK_COMOMENTS) {
+      if (b[0] == 0.0) continue;
+      if (na == 0.0) {
+        for (int q = 0; q < 6; ++q) out.d[q] = b[2 + q];
+      } else {
+        comoments_merge(na, out.d, b[0], b + 2);
+      }
+      na += b[0];
+    }
+  }
+}
+
+__global__ void xchg_pack_kernel(const Acc* acc, const uint8_t* hll, const int32_t* kinds, int T,
+                                 int nh, int64_t rows, int64_t* isum, int64_t* imax, double* mom) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < T) xchg_pack_task(kinds[i], acc[i], i, T, isum, imax, mom);
+  if (i < nh) imax[2 * T + i] = hll[i];
+  if (i == 0) isum[10 * T] = rows;
+}
+
+__global__ void xchg_unpack_kernel(const int32_t* kinds, int T, int nh, int world,
+                                   const int64_t* isum, const int64_t* imax, const double* momg,
+                                   Acc* acc, uint8_t* hll, int64_t* rows) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < T) xchg_merge_task(kinds[i], i, T, world, isum, imax, momg, acc[i]);
+  if (i < nh) hll[i] = (uint8_t)imax[2 * T + i];
+  if (i == 0) *rows = isum[10 * T];
+}
+
+// the task kinds on the device (a few words, uploaded per call; plans are immutable)
+dq_status xchg_kinds(const dq_plan* p, DevBuf<int32_t>& buf, hipStream_t st) {
+  std::vector<int32_t> k(std::max<size_t>(1, p->tasks.size()), 0);
+  for (size_t t = 0; t < p->tasks.size(); ++t) k[t] = p->tasks[t].kind;
+  HIP_TRY(buf.ensure(k.size()));
+  HIP_TRY(hipMemcpyAsync(buf.p, k.data(), k.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));  // (k dies here)
+  return DQ_OK;
+}
+}  // namespace
+
+extern "C" dq_status dq_state_exchange_sizes(const dq_plan* plan, int64_t* n_sum, int64_t* n_max,
+                                             int64_t* n_mom) {
+  if (!plan || !n_sum || !n_max || !n_mom) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  const int64_t T = (int64_t)plan->tasks.size();
+  *n_sum = 10 * T + 1;
+  *n_max = 2 * T + (int64_t)plan->n_hll * kHllM;
+  *n_mom = kMomW * T;
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_state_exchange_pack(dq_state* s, int64_t* isum, int64_t* imax, double* mom,
+                                            void* hip_stream) {
+  if (!s || !isum || !imax || !mom) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  const dq_plan* p = s->plan;
+  const int T = (int)p->tasks.size(), nh = (int)s->hll.size();
+  if (s->device < 0 || (s->synced && !s->rows_on_device)) {
+    if (s->device >= 0) {  // host mirror current: pack it on the host, copy up
+      std::vector<int64_t> hs(10 * (size_t)T + 1), hm(2 * (size_t)T + nh);
+      std::vector<double> hd((size_t)kMomW * T);
+      for (int k = 0; k < T; ++k) xchg_pack_task(p->tasks[k].kind, s->acc[k], k, T, hs.data(), hm.data(), hd.data());
+      for (int i = 0; i < nh; ++i) hm[2 * (size_t)T + i] = s->hll[i];
+      hs[10 * (size_t)T] = s->rows;
+      hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
+      HIP_TRY(hipSetDevice(s->device));
+      HIP_TRY(hipMemcpyAsync(isum, hs.data(), hs.size() * 8, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(imax, hm.data(), hm.size() * 8, hipMemcpyHostToDevice, st));
+      if (T) HIP_TRY(hipMemcpyAsync(mom, hd.data(), hd.size() * 8, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipStreamSynchronize(st));  // (the host vectors die here)
+      return DQ_OK;
+    }
+    for (int k = 0; k < T; ++k) xchg_pack_task(p->tasks[k].kind, s->acc[k], k, T, isum, imax, mom);
+    for (int i = 0; i < nh; ++i) imax[2 * (size_t)T + i] = s->hll[i];
+    isum[10 * (size_t)T] = s->rows;
+    return DQ_OK;
+  }
+  // the device accumulators are newer than the host mirror: pack them where they are, on the
+  // state's stream, and order the caller's stream (the collectives) after it
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = s->stream_set ? s->stream : reinterpret_cast<hipStream_t>(hip_stream);
+  if (s->rows_on_device)
+    return fail(DQ_ERR_STATE, "state holds an unsynced exchange result (call dq_state_sync)");
+  dq_status ks = xchg_kinds(p, s->d_kinds, st);
+  if (ks != DQ_OK) return ks;
+  const int n = std::max(std::max(T, nh), 1);
+  hipLaunchKernelGGL(xchg_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, st, s->d_acc.p, s->d_hll.p,
+                     s->d_kinds.p, T, nh, s->rows, isum, imax, mom);
+  HIP_TRY(hipGetLastError());
+  hipStream_t cs = reinterpret_cast<hipStream_t>(hip_stream);
+  if (cs != st) {
+    HIP_TRY(hipEventRecord(s->ev_xchg, st));
+    HIP_TRY(hipStreamWaitEvent(cs, s->ev_xchg, 0));
+  }
+  return DQ_OK;
+}
+
+extern "C" dq_status dq_state_exchange_unpack(dq_state* s, const int64_t* isum, const int64_t* imax,
+                                              const double* mom_gathered, int world, void* hip_stream) {
+  if (!s || !isum || !imax || (!mom_gathered && !s->plan->tasks.empty()) || world < 1)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "bad argument");
+  const dq_plan* p = s->plan;
+  const int T = (int)p->tasks.size(), nh = (int)s->hll.size();
+  if (s->device < 0) {
+    for (int k = 0; k < T; ++k) xchg_merge_task(p->tasks[k].kind, k, T, world, isum, imax, mom_gathered, s->acc[k]);
+    for (int i = 0; i < nh; ++i) s->hll[i] = (uint8_t)imax[2 * (size_t)T + i];
+    s->rows = isum[10 * (size_t)T];
+    s->synced = true;
+    s->host_dirty = true;
+    return DQ_OK;
+  }
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t cs = reinterpret_cast<hipStream_t>(hip_stream);
+  if (!s->stream_set) {
+    s->stream = cs;
+    s->stream_set = true;
+  }
+  hipStream_t st = s->stream;
+  if (cs != st) {
+    HIP_TRY(hipEventRecord(s->ev_xchg, cs));
+    HIP_TRY(hipStreamWaitEvent(st, s->ev_xchg, 0));
+  }
+  dq_status ks = xchg_kinds(p, s->d_kinds, st);
+  if (ks != DQ_OK) return ks;
+  HIP_TRY(s->d_rows.ensure(1));
+  const int n = std::max(std::max(T, nh), 1);
+  hipLaunchKernelGGL(xchg_unpack_kernel, dim3((n + 255) / 256), dim3(256), 0, st, s->d_kinds.p, T, nh,
+                     world, isum, imax, mom_gathered, s->d_acc.p, s->d_hll.p, s->d_rows.p);
+  HIP_TRY(hipGetLastError());
+  s->rows_on_device = true;
+  s->synced = false;
+  s->host_dirty = false;
   return DQ_OK;
 }
 

@@ -1,9 +1,10 @@
 """Multi-GPU sharding: one process per GPU, rows sharded contiguously across
-ranks, each rank runs the fused scan on its shard, and the per-rank aggregation buffers meet in
-ONE collective -- an all-gather of the serialized states (a few hundred bytes; latency-bound, so
-one gather beats separate sum / min / max / register-max all-reduces) -- followed by a
-deterministic rank-ordered merge with the engine's own Spark-merge rules (dq_state_merge).  Over
-RCCL (`nccl` backend) the gather runs on the device; with `gloo` (CPU tests) on host tensors.
+ranks, each rank runs the fused scan on its shard, and the per-rank aggregation buffers meet on
+the device (exchange_states): counters and wrapping sums in one all-reduce SUM, extremes and HLL
+registers in one all-reduce MAX, the fp64 moments in one all-gather merged in rank order by a
+kernel -- the Spark merge rules, no host merge.  The previous exchange (an all-gather of the
+serialized states + the rank-ordered host merge, merge_states_across_ranks) is kept as the check.
+Over RCCL (`nccl` backend) the collectives run on the device; with `gloo` on host tensors.
 """
 from __future__ import annotations
 
@@ -91,6 +92,47 @@ def merge_states_across_ranks(plan, state, device=None):
     return merge_serialized(plan, images)
 
 
+def exchange_states(plan, state, device=None):
+    """All ranks: the scan states merged on the device, as north_star states them -- counters and
+    wrapping Long sums by ONE all-reduce SUM, extremes and HLL registers by ONE all-reduce MAX (min
+    keys travel bitwise-NOT), the fp64 moments by ONE all-gather merged in rank order by a kernel
+    (dq_state_exchange_pack / _unpack).  No host merge: the one read-back is the merged state's
+    (dq_state_sync).  Equal, byte for byte, to merge_states_across_ranks (the rank-ordered
+    dq_state_merge of the serialized states, kept as the check).  `device` None: a host-only state
+    (device -1; the CPU tests), collectives over gloo on host tensors.  Returns the result row."""
+    import torch
+    import torch.distributed as dist
+    from .runners.engine import read_row
+    world = dist.get_world_size()
+    ns, nm, nd = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    N.check(N.lib.dq_state_exchange_sizes(plan.handle, ctypes.byref(ns), ctypes.byref(nm),
+                                          ctypes.byref(nd)))
+    home = torch.device(device) if device is not None else torch.device("cpu")
+    cdev = _comm_device(home) if device is not None else "cpu"
+    isum = torch.empty(ns.value, dtype=torch.int64, device=home)
+    imax = torch.empty(nm.value, dtype=torch.int64, device=home)
+    mom = torch.empty(max(1, nd.value), dtype=torch.float64, device=home)
+    stream = (ctypes.c_void_p(torch.cuda.current_stream(home).cuda_stream)
+              if home.type == "cuda" else None)
+    N.check(N.lib.dq_state_exchange_pack(state, isum.data_ptr(), imax.data_ptr(), mom.data_ptr(),
+                                         stream))
+    isum_c, imax_c, mom_c = isum.to(cdev), imax.to(cdev), mom[: nd.value].to(cdev)
+    dist.all_reduce(isum_c, op=dist.ReduceOp.SUM)
+    dist.all_reduce(imax_c, op=dist.ReduceOp.MAX)
+    gathered = torch.empty(world * nd.value, dtype=torch.float64, device=cdev)
+    if nd.value:
+        dist.all_gather_into_tensor(gathered, mom_c)
+    _count_reduce(isum_c)
+    _count_reduce(imax_c)
+    _count_gather(nd.value * 8, world)
+    isum, imax = isum_c.to(home), imax_c.to(home)
+    gathered = gathered.to(home) if nd.value else mom
+    N.check(N.lib.dq_state_exchange_unpack(state, isum.data_ptr(), imax.data_ptr(),
+                                           gathered.data_ptr(), world, stream))
+    N.check(N.lib.dq_state_sync(state))
+    return read_row(plan, state)
+
+
 def shard_bounds(n_rows: int, rank: int, world: int, align: int = 4096):
     """Contiguous row range of `rank`, boundaries aligned so every shard keeps the vector path."""
     per = -(-n_rows // world)
@@ -101,13 +143,13 @@ def shard_bounds(n_rows: int, rank: int, world: int, align: int = 4096):
 
 def run_scan_distributed(table_shard, specs):
     """The distributed counterpart of runners.engine.run_scan: scan the local shard, then the
-    all-gather + rank-ordered merge."""
+    device-side state exchange (exchange_states)."""
     from .runners.engine import get_plan, scan_into
     plan = get_plan(table_shard.schema, specs)
     state = plan.state(table_shard.device_index())
     N.check(N.lib.dq_state_reset(state))
     scan_into(table_shard, plan, state)
-    return merge_states_across_ranks(plan, state, table_shard.device)
+    return exchange_states(plan, state, table_shard.device)
 
 
 # ------------------------------------------------------------------------------------------------

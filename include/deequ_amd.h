@@ -279,6 +279,27 @@ int64_t dq_state_serialized_size(const dq_plan* plan);
 dq_status dq_state_serialize(const dq_state* state, void* buf, int64_t buf_len);
 dq_status dq_state_deserialize(dq_state* state, const void* buf, int64_t buf_len);
 
+/* State exchange across ranks, on the device (distributed.py exchange_states):
+ * the merge Spark performs over partition states (Analyzer.scala:337-362 / StateLoader) split
+ * into the collectives each field's merge rule allows:
+ *   isum[n_sum]   int64, all-reduce SUM: every task's counters and wrapping Long sums, the rows;
+ *   imax[n_max]   int64, all-reduce MAX: max keys, bitwise-NOT min keys (MAX of ~x = ~MIN), the
+ *                 HLL registers widened (StatefulHyperloglogPlus.scala:119-137 merges by max);
+ *   mom[n_mom]    double, all-GATHER (rank-major [world][n_mom]): n and the fp64 moments, merged
+ *                 in rank order by the Chan / co-moment rules (StandardDeviation.scala:37-44,
+ *                 Correlation.scala:37-52).
+ * pack fills the three buffers from the state (device pointers for a device state: a kernel on the
+ * state's stream that hip_stream is made to wait for; host pointers for a host state, device
+ * -1); unpack writes the merged result into the state (device: a kernel on the state's stream
+ * after hip_stream; read it with dq_state_sync).  The result equals dq_state_merge over the
+ * ranks' states in rank order, byte for byte. */
+dq_status dq_state_exchange_sizes(const dq_plan* plan, int64_t* n_sum, int64_t* n_max,
+                                  int64_t* n_mom);
+dq_status dq_state_exchange_pack(dq_state* state, int64_t* isum, int64_t* imax, double* mom,
+                                 void* hip_stream);
+dq_status dq_state_exchange_unpack(dq_state* state, const int64_t* isum, const int64_t* imax,
+                                   const double* mom_gathered, int world, void* hip_stream);
+
 /* HyperLogLogPlusPlusUtils.count (StatefulHyperloglogPlus.scala:208-255) on 52 register words.
  * `bias_corrected` is set to 1 when the estimate fell in the empirical-bias range (E < 5M with no
  * linear counting); that branch needs Spark's RAW_ESTIMATE_DATA/BIAS_DATA tables, which are not

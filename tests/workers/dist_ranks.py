@@ -13,6 +13,47 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
+def exchange_check(df):
+    """The scan states of the suite exchanged on the device (exchange_states: SUM / MAX
+    all-reduces + the gathered moments merged by a kernel) and by the serialized all-gather +
+    rank-ordered host merge (merge_states_across_ranks): the merged states' bytes must agree."""
+    import ctypes
+
+    from deequ_amd import _native as N
+    from deequ_amd.analyzers.base import ScanShareableAnalyzer
+    from deequ_amd.distributed import exchange_states, merge_states_across_ranks, serialize_state
+    from deequ_amd.runners.engine import get_plan, scan_into
+    from dist_suite import suite
+    specs = [s for a in suite() if isinstance(a, ScanShareableAnalyzer)
+             for s in a.aggregation_functions()]
+    plan = get_plan(df.schema, specs)
+    out = []
+    for how in ("device", "host"):
+        st = ctypes.c_void_p()
+        N.check(N.lib.dq_state_create(plan.handle, 0, ctypes.byref(st)))
+        scan_into(df, plan, st)
+        if how == "device":
+            row = exchange_states(plan, st, df.device)
+            img = serialize_state(plan, st)
+        else:
+            row = merge_states_across_ranks(plan, st, df.device)
+            from deequ_amd.distributed import all_gather_bytes
+            imgs = all_gather_bytes(serialize_state(plan, st), df.device)
+            acc, tmp = ctypes.c_void_p(), ctypes.c_void_p()
+            N.check(N.lib.dq_state_create(plan.handle, -1, ctypes.byref(acc)))
+            N.check(N.lib.dq_state_create(plan.handle, -1, ctypes.byref(tmp)))
+            for b in imgs:
+                buf = ctypes.create_string_buffer(b, len(b))
+                N.check(N.lib.dq_state_deserialize(tmp, buf, len(b)))
+                N.check(N.lib.dq_state_merge(acc, tmp))
+            img = serialize_state(plan, acc)
+            N.lib.dq_state_destroy(acc)
+            N.lib.dq_state_destroy(tmp)
+        N.lib.dq_state_destroy(st)
+        out.append((img, repr(row)))
+    return [out[0][0] == out[1][0], out[0][1] == out[1][1]]
+
+
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     import torch.distributed as dist
@@ -27,6 +68,7 @@ def main():
     df = Table.from_arrow(t.slice(lo, hi - lo), device="cuda:0", max_batch_rows=6000)
     ctx = AnalysisRunner.do_analysis_run(df, suite())
     res = metrics_of(ctx)
+    res["__exchange__"] = exchange_check(df)
     dist.barrier()
     if rank == 0:
         with open(out, "w") as f:
