@@ -2318,7 +2318,7 @@ struct CArgs {
   const FEntry* entries;  // nullptr: the first pass over every partition
   unsigned long long* part_groups;
   unsigned long long* part_unique;
-  double* part_entropy;
+  unsigned long long* part_entropy;  // per partition: the fixed-point sum (lo, hi)
   unsigned long long* part_off;  // materialised groups of partition p start here
   FEntry* ovf_out;
   unsigned int* ovf_n;
@@ -2430,6 +2430,51 @@ __device__ __attribute__((noinline)) double entropy_term(uint64_t c, double n) {
   return -pr * log(pr);
 }
 
+// ---- Exact sums of fp64 terms (Entropy's -p ln p, MutualInformation's p ln(p / (px py))) ----
+// A term enters as a signed 128-bit fixed-point integer at 2^-112 (exact for every term of
+// magnitude >= 2^-60, cut below 2^-112), so a sum is the same integer in ANY order: the table's
+// entropy is the sum of its groups' terms whatever the phase-C insert order, the partition depth,
+// the recount subsets or the order partial sums meet in -- bit-stable from run to run.  Terms are
+// bounded (|term| <= ln(rows) < 2^6), sums stay far inside 2^15.
+using fix128 = __int128;
+constexpr double kFixUlp = 0x1p-112;
+DQ_HD fix128 fix_of(double x) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, x);
+  const int ex = (int)((b >> 52) & 0x7ff);
+  if (ex == 0) return 0;  // zero (and subnormals, < 2^-1022: cut)
+  const uint64_t m = (b & ((1ULL << 52) - 1)) | (1ULL << 52);
+  const int sh = ex - 1075 + 112;  // x = m 2^(ex - 1075); fixed = m 2^(ex - 1075 + 112)
+  const fix128 v = sh >= 0 ? ((fix128)m << sh) : (sh > -64 ? (fix128)(m >> -sh) : (fix128)0);
+  return (b >> 63) ? -v : v;
+}
+// (a fixed sequence of roundings: deterministic, within 2 ulp)
+DQ_HD double fix_to_f64(fix128 v) {
+  const int64_t hi = (int64_t)(v >> 64);
+  const uint64_t lo = (uint64_t)v;
+  return ((double)hi * 18446744073709551616.0 + (double)lo) * kFixUlp;
+}
+DQ_DEV fix128 wave_sum_fix(fix128 v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const uint64_t lo = __shfl_xor((unsigned long long)(uint64_t)v, o);
+    const uint64_t hi = __shfl_xor((unsigned long long)(uint64_t)(v >> 64), o);
+    v += (fix128)(((unsigned __int128)hi << 64) | lo);
+  }
+  return v;
+}
+// p[0..1] += v (lo, hi words): the carry of each lo add goes with that add's hi, so the total is
+// exact whatever order the adds land in
+DQ_DEV void atomic_add_fix(unsigned long long* p, fix128 v) {
+  const uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+  const uint64_t old = atomicAdd(p, (unsigned long long)lo);
+  const uint64_t up = hi + (old + lo < old ? 1u : 0u);
+  if (up) atomicAdd(p + 1, (unsigned long long)up);
+}
+DQ_DEV void store_fix(unsigned long long* p, fix128 v) {
+  p[0] = (uint64_t)v;
+  p[1] = (uint64_t)(v >> 64);
+}
+
 // Per work item: the inserts, then ONE pass over the LDS table that reads every slot once for
 // the statistics, the Histogram candidates (kept in registers) and the lit probe, and clears it
 // for the next item (when the groups are materialised, the output pass clears instead).  The
@@ -2443,11 +2488,11 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
   __shared__ uint64_t trep[HASHED ? KT : 1];
   __shared__ uint32_t s_wg[NW], s_wc[NW];
   __shared__ uint64_t s_red[NW];
-  __shared__ double s_redf[NW];
   __shared__ uint32_t s_ovf[2];
   __shared__ unsigned long long s_spec_cnt[2], s_gbase;
   __shared__ uint64_t s_spec_rep[2];
   __shared__ uint32_t s_chist[2][kSmallCounts];
+  __shared__ unsigned long long s_efix[2][2];  // per item parity: the entropy, fixed point (lo, hi)
   // Histogram candidates: packed (count << 16 | tid << 2 | q) maxima, top-1 .. top-kCand
   __shared__ unsigned long long s_top[2][kCand];
 
@@ -2466,6 +2511,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     for (int r = 0; r < kCand; ++r) s_top[tid][r] = 0;
   }
   if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
+  if (tid < 4) (&s_efix[0][0])[tid] = 0;
   // exact mode fetches records two items ahead: item i + 2's loads are in flight through all of
   // item i + 1 (one item's inserts and reduction are shorter than an HBM round trip under load).
   // Hashed mode has no registers for it and fetches one item ahead.
@@ -2617,6 +2663,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       for (int r = 0; r < kCand; ++r) s_top[par ^ 1u][r] = 0;
     }
     if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
+    if (tid < 2) s_efix[par ^ 1u][tid] = 0;
     const bool overflow = *ovf != 0;
     const uint64_t sc = *spec_cnt, sr = HASHED ? *spec_rep : 0;
 
@@ -2626,16 +2673,15 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     const bool cand = a.want_cand && f == 0;
     uint32_t g = 0;
     uint64_t un = 0;
-    double e = 0.0;
     uint64_t tc[kCand], tk[kCand], tr[kCand];
 #pragma unroll
     for (int q = 0; q < kCand; ++q) tc[q] = tk[q] = tr[q] = 0;
-    auto term = [&](uint64_t c) { return entropy_term(c, a.num_rows); };
+    auto term = [&](uint64_t c) { return fix_of(entropy_term(c, a.num_rows)); };
     auto count_group = [&](uint64_t c) {
       ++g;
       if (c == 1) ++un;  // the common count: a register, not an LDS atomic on one address
       else if (c < kSmallCounts) atomicAdd(&s_chist[par][c], 1u);
-      else e += term(c);
+      else atomic_add_fix(&s_efix[par][0], term(c));  // (rare: fixed point, any order)
     };
     auto offer = [&](uint64_t c, uint64_t k, uint64_t r) {  // insertion, static indices
 #pragma unroll
@@ -2723,10 +2769,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
       continue;
     }
     if (tid > 1 && tid < kSmallCounts && s_chist[par][tid])
-      e += (double)s_chist[par][tid] * term(tid);
-    if (tid == 0 && utot) e += (double)utot * term(1);
-    e = __ockl_wfred_add_f64(e);
-    if (lane == 0) s_redf[wave] = e;
+      atomic_add_fix(&s_efix[par][0], term(tid) * (fix128)s_chist[par][tid]);
+    if (tid == 0 && utot) atomic_add_fix(&s_efix[par][0], term(1) * (fix128)utot);
     if (cand) {  // round 2: the largest of the rest (the top-1 owner offers its second)
       const uint64_t top1 = s_top[par][0];
       taken = top1 && top1 == pack(0) ? 1 : 0;
@@ -2741,19 +2785,17 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
     __syncthreads();  //                                                            [barrier 3]
     mark(3);
     if (tid == 0) {
-      double etot = 0.0;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) etot += s_redf[w];
+      const fix128 etot = (fix128)(((unsigned __int128)s_efix[par][1] << 64) | s_efix[par][0]);
       if (!keep || !sub) {
         if (sub) atomicAdd(&a.part_groups[p], (unsigned long long)gtot);
         else a.part_groups[p] = gtot;
       }
       if (sub) {
         if (utot) atomicAdd(&a.part_unique[p], (unsigned long long)utot);
-        if (etot != 0.0) atomicAdd(&a.part_entropy[p], etot);
+        if (etot) atomic_add_fix(&a.part_entropy[2 * (uint64_t)p], etot);
       } else {
         a.part_unique[p] = utot;
-        a.part_entropy[p] = etot;
+        store_fix(&a.part_entropy[2 * (uint64_t)p], etot);
       }
     }
     if (cand) {
@@ -2855,8 +2897,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
   __shared__ uint32_t s_n[2], s_ovf[2];
   __shared__ unsigned long long s_spec[2];
   __shared__ uint32_t s_chist[2][kSmallCounts];
+  __shared__ unsigned long long s_efix[2][2];  // per item parity: the entropy, fixed point (lo, hi)
   __shared__ unsigned long long s_wun[2][NW], s_wmax[2][NW];
-  __shared__ double s_went[2][NW];
   __shared__ double s_term[kSmallCounts];
   // each wave's top kCand groups of the item (count 0: none), merged by the next item's tail
   __shared__ uint64_t s_wk[2][NW][kCand], s_wc[2][NW][kCand];
@@ -2878,6 +2920,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     s_tfl[tid] = 0;
   }
   if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
+  if (tid < 4) (&s_efix[0][0])[tid] = 0;
   if (tid < kSmallCounts) s_term[tid] = tid ? entropy_term((uint64_t)tid, a.num_rows) : 0.0;
   const bool keep = a.groups != nullptr;
 
@@ -2918,26 +2961,23 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     }
     if (wv != 0) return;
     const uint32_t hc = lane > 1 ? s_chist[q][lane] : 0u;
-    double t = hc ? (double)hc * s_term[lane] : 0.0;
-    t = __ballot(hc != 0) ? __ockl_wfred_add_f64(t) : 0.0;  // (no counts 2..63: nothing to add)
+    // counts 2..63 join the item's LDS sum (this wave's LDS operations complete in order, so
+    // lane 0 reads it after every lane's add)
+    if (hc) atomic_add_fix(&s_efix[q][0], fix_of(s_term[lane]) * (fix128)hc);
     if (lane == 0) {
       uint64_t utot = 0;
-      double etot = 0.0;
+      fix128 etot = (fix128)(((unsigned __int128)s_efix[q][1] << 64) | s_efix[q][0]);
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        utot += s_wun[q][w];
-        etot += s_went[q][w];
-      }
-      etot += t;
-      if (utot) etot += (double)utot * s_term[1];
+      for (int w = 0; w < NW; ++w) utot += s_wun[q][w];
+      if (utot) etot += fix_of(s_term[1]) * (fix128)utot;
       if (sub) {
         if (!keep) atomicAdd(&a.part_groups[p], (unsigned long long)gtot);
         if (utot) atomicAdd(&a.part_unique[p], (unsigned long long)utot);
-        if (etot != 0.0) atomicAdd(&a.part_entropy[p], etot);
+        if (etot) atomic_add_fix(&a.part_entropy[2 * (uint64_t)p], etot);
       } else {
         a.part_groups[p] = gtot;
         a.part_unique[p] = utot;
-        a.part_entropy[p] = etot;
+        store_fix(&a.part_entropy[2 * (uint64_t)p], etot);
       }
       if (keep) a.part_off[p] = s_tr0[q];
     }
@@ -3089,6 +3129,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       s_tfl[par ^ 1u] = 0;
     }
     if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
+    if (tid < 2) s_efix[par ^ 1u][tid] = 0;
     const uint32_t gtot = n + (sc ? 1u : 0u);
     uint64_t gbase = 0;
     if (keep && sub && !overflow) {  // block-uniform
@@ -3100,7 +3141,6 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
 
     // statistics over the list, clearing the table
     uint64_t un = 0, mx = 0;
-    double e = 0.0;
     uint64_t tc[kCand], tk[kCand];  // this lane's top groups with count > 1
 #pragma unroll
     for (int q = 0; q < kCand; ++q) tc[q] = tk[q] = 0;
@@ -3110,7 +3150,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       if (keep) a.groups[obase + i] = Group{k, c, 0};
       if (c == 1) ++un;
       else if (c < kSmallCounts) atomicAdd(&s_chist[par][c], 1u);
-      else e += entropy_term(c, a.num_rows);
+      else atomic_add_fix(&s_efix[par][0], fix_of(entropy_term(c, a.num_rows)));  // (rare)
       mx = c > mx ? c : mx;
       if (cand) {
         if (c == 1) {
@@ -3216,11 +3256,9 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     }
     {
       const uint64_t wun = __ockl_wfred_add_u64(un);
-      const double we = __ballot(e != 0.0) ? __ockl_wfred_add_f64(e) : 0.0;
       const uint64_t wmx = wmx1;
       if (lane == 0) {
         s_wun[par][wave] = wun;
-        s_went[par][wave] = we;
         s_wmax[par][wave] = wmx;
       }
     }
@@ -3296,8 +3334,8 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
   __shared__ uint16_t list[KL];
   __shared__ uint32_t s_n[2], s_ovf[2];
   __shared__ uint32_t s_chist[2][kSmallCounts];
+  __shared__ unsigned long long s_efix[2][2];  // per item parity: the entropy, fixed point (lo, hi)
   __shared__ unsigned long long s_wun[2][NW], s_wmax[2][NW];
-  __shared__ double s_went[2][NW];
   __shared__ double s_term[kSmallCounts];
   // each wave's top kCand groups of the item (count 0: none), merged by the next item's tail
   __shared__ uint64_t s_wk[2][NW][kCand], s_wc[2][NW][kCand], s_wr[2][NW][kCand];
@@ -3317,6 +3355,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
     s_tfl[tid] = 0;
   }
   if (tid < 2 * kSmallCounts) (&s_chist[0][0])[tid] = 0;
+  if (tid < 4) (&s_efix[0][0])[tid] = 0;
   if (tid < kSmallCounts) s_term[tid] = tid ? entropy_term((uint64_t)tid, a.num_rows) : 0.0;
   const bool keep = a.groups != nullptr;
 
@@ -3353,21 +3392,18 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
     }
     if (wv != 0) return;
     const uint32_t hc = lane > 1 ? s_chist[q][lane] : 0u;
-    double t = hc ? (double)hc * s_term[lane] : 0.0;
-    t = __ballot(hc != 0) ? __ockl_wfred_add_f64(t) : 0.0;  // (no counts 2..63: nothing to add)
+    // counts 2..63 join the item's LDS sum (this wave's LDS operations complete in order, so
+    // lane 0 reads it after every lane's add)
+    if (hc) atomic_add_fix(&s_efix[q][0], fix_of(s_term[lane]) * (fix128)hc);
     if (lane == 0) {
       uint64_t utot = 0;
-      double etot = 0.0;
+      fix128 etot = (fix128)(((unsigned __int128)s_efix[q][1] << 64) | s_efix[q][0]);
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        utot += s_wun[q][w];
-        etot += s_went[q][w];
-      }
-      etot += t;
-      if (utot) etot += (double)utot * s_term[1];
+      for (int w = 0; w < NW; ++w) utot += s_wun[q][w];
+      if (utot) etot += fix_of(s_term[1]) * (fix128)utot;
       a.part_groups[p] = gtot;
       a.part_unique[p] = utot;
-      a.part_entropy[p] = etot;
+      store_fix(&a.part_entropy[2 * (uint64_t)p], etot);
       if (keep) a.part_off[p] = s_tr0[q];
     }
   };
@@ -3545,11 +3581,11 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
       s_tfl[par ^ 1u] = 0;
     }
     if (tid < kSmallCounts) s_chist[par ^ 1u][tid] = 0;
+    if (tid < 2) s_efix[par ^ 1u][tid] = 0;
     const uint32_t gtot = n;
     const uint64_t obase = a.group_stride ? (uint64_t)wi * a.group_stride : r0;
 
     uint64_t un = 0, mx = 0;
-    double e = 0.0;
     uint64_t tc[kCand], tk[kCand], tr[kCand];
 #pragma unroll
     for (int q = 0; q < kCand; ++q) tc[q] = tk[q] = tr[q] = 0;
@@ -3561,7 +3597,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
       if (keep) a.groups[obase + i] = Group{k, c, r};
       if (c == 1) ++un;
       else if (c < kSmallCounts) atomicAdd(&s_chist[par][c], 1u);
-      else e += entropy_term(c, a.num_rows);
+      else atomic_add_fix(&s_efix[par][0], fix_of(entropy_term(c, a.num_rows)));  // (rare)
       mx = c > mx ? c : mx;
       if (cand) {
         if (c == 1) {
@@ -3666,11 +3702,9 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
     }
     {
       const uint64_t wun = __ockl_wfred_add_u64(un);
-      const double we = __ballot(e != 0.0) ? __ockl_wfred_add_f64(e) : 0.0;
       const uint64_t wmx = wmx1;
       if (lane == 0) {
         s_wun[par][wave] = wun;
-        s_went[par][wave] = we;
         s_wmax[par][wave] = wmx;
       }
     }
@@ -3707,40 +3741,44 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_h(CArgs a) {
 constexpr int kRedBlocks = 256;
 __global__ void __launch_bounds__(kThreads) freq_reduce_part(const unsigned long long* pg,
                                                              const unsigned long long* pu,
-                                                             const double* pe, int64_t n,
+                                                             const unsigned long long* pe, int64_t n,
                                                              unsigned long long* part) {
   __shared__ uint64_t s_red[kThreads / 64];
-  __shared__ double s_redf[kThreads / 64];
+  __shared__ fix128 s_rede[kThreads / 64];
   const int64_t per = (n + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * per, hi = min(lo + per, n);
   uint64_t g = 0, u = 0;
-  double e = 0.0;
+  fix128 e = 0;
   for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) {
     g += pg[i];
     u += pu[i];
-    e += pe[i];
+    e += (fix128)(((unsigned __int128)pe[2 * i + 1] << 64) | pe[2 * i]);
   }
   g = block_sum_u64(g, s_red);
   u = block_sum_u64(u, s_red);
-  e = block_sum_f64(e, s_redf);
+  e = wave_sum_fix(e);
+  if (__lane_id() == 0) s_rede[threadIdx.x >> 6] = e;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    part[blockIdx.x * 3] = g;
-    part[blockIdx.x * 3 + 1] = u;
-    part[blockIdx.x * 3 + 2] = __builtin_bit_cast(unsigned long long, e);
+    fix128 t = 0;
+    for (int w = 0; w < kThreads / 64; ++w) t += s_rede[w];
+    part[blockIdx.x * 4] = g;
+    part[blockIdx.x * 4 + 1] = u;
+    store_fix(part + blockIdx.x * 4 + 2, t);
   }
 }
 __global__ void freq_reduce_final(const unsigned long long* part, int nb, unsigned long long* out) {
   if (threadIdx.x != 0) return;
   uint64_t g = 0, u = 0;
-  double e = 0.0;
+  fix128 e = 0;
   for (int b = 0; b < nb; ++b) {
-    g += part[b * 3];
-    u += part[b * 3 + 1];
-    e += __builtin_bit_cast(double, part[b * 3 + 2]);
+    g += part[b * 4];
+    u += part[b * 4 + 1];
+    e += (fix128)(((unsigned __int128)part[b * 4 + 3] << 64) | part[b * 4 + 2]);
   }
   out[0] = g;
   out[1] = u;
-  out[2] = __builtin_bit_cast(unsigned long long, e);
+  out[2] = __builtin_bit_cast(unsigned long long, fix_to_f64(e));
 }
 
 // Multi-block exclusive scan of u64 values in place, v[n] = total (large n; freq_part_scan is the
@@ -4049,7 +4087,7 @@ struct dq_freq {
   bool c_valid = false, c_groups = false, c_cand = false;
   double c_num_rows = -1.0;
   DevBuf<unsigned long long> part_groups, part_unique, part_off;
-  DevBuf<double> part_entropy;
+  DevBuf<unsigned long long> part_entropy;  // (lo, hi) fixed-point sum per partition
   DevBuf<Group> cand, groups, compact;
   int64_t n_compact = -1;
   DevBuf<FEntry> ovf_a, ovf_b;
@@ -4526,7 +4564,7 @@ static dq_status finalize_b(dq_freq* f) {
 
 // The partitions' statistics summed in a fixed order into f->red.
 static dq_status launch_reduce(dq_freq* f, int64_t P) {
-  HIP_TRY(f->scan_tmp.ensure(kRedBlocks * 3));
+  HIP_TRY(f->scan_tmp.ensure(kRedBlocks * 4));
   const unsigned nbr = (unsigned)std::max<int64_t>(1, std::min<int64_t>(kRedBlocks, (P + kThreads - 1) / kThreads));
   hipLaunchKernelGGL(freq_reduce_part, dim3(nbr), dim3(kThreads), 0, f->stream, f->part_groups.p,
                      f->part_unique.p, f->part_entropy.p, P, f->scan_tmp.p);
@@ -4558,14 +4596,14 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
   HIP_TRY(f->part_groups.ensure(P));
   HIP_TRY(f->part_unique.ensure(P));
   HIP_TRY(f->part_off.ensure(P));
-  HIP_TRY(f->part_entropy.ensure(P));
+  HIP_TRY(f->part_entropy.ensure(2 * P));
   HIP_TRY(f->red.ensure(4));
   HIP_TRY(hipMemsetAsync(f->red.p + 3, 0, 8, f->stream));
   HIP_TRY(f->ovf_n.ensure(1));
   HIP_TRY(hipMemsetAsync(f->part_groups.p, 0, P * 8, f->stream));
   HIP_TRY(hipMemsetAsync(f->part_unique.p, 0, P * 8, f->stream));
   HIP_TRY(hipMemsetAsync(f->part_off.p, 0, P * 8, f->stream));
-  HIP_TRY(hipMemsetAsync(f->part_entropy.p, 0, P * 8, f->stream));
+  HIP_TRY(hipMemsetAsync(f->part_entropy.p, 0, P * 16, f->stream));
   if (want_groups) HIP_TRY(f->groups.ensure(std::max<uint64_t>(f->R, 1)));
   if (want_cand) {
     HIP_TRY(f->cand.ensure((size_t)P * kCand));
@@ -5157,15 +5195,31 @@ __global__ void freq_mi_terms_h(const Group* __restrict__ gj, int64_t n, const u
   terms[i] = (pxy / total) * log((pxy / total) / ((px / total) * (py / total)));
 }
 
-// Fixed-order sum: block b adds its strided share in index order, then a fixed tree.
-__global__ void __launch_bounds__(256) freq_sum_f64(const double* __restrict__ x, int64_t n,
-                                                    double* __restrict__ partial) {
-  __shared__ double s_red[256 / 64];
-  double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    acc += x[i];
-  acc = block_sum_f64(acc, s_red);
-  if (threadIdx.x == 0) partial[blockIdx.x] = acc;
+// Order-independent sum of the MutualInformation terms (the joint groups' order is phase C's
+// output order, which varies from run to run): each term in fixed point (fix_of), summed as
+// integers; a non-finite term (a marginal count that is not there) is added as a double beside
+// (NaN / inf sums do not depend on order either).  partial[b] = {lo, hi, non-finite sum bits}.
+__global__ void __launch_bounds__(256) freq_sum_fix(const double* __restrict__ x, int64_t n,
+                                                    unsigned long long* __restrict__ partial) {
+  __shared__ fix128 s_red[256 / 64];
+  __shared__ double s_nf[256 / 64];
+  fix128 acc = 0;
+  double nf = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double t = x[i];
+    if (fabs(t) < 16384.0) acc += fix_of(t);
+    else nf += t;  // (NaN fails the test too)
+  }
+  acc = wave_sum_fix(acc);
+  nf = block_sum_f64(nf, s_nf);
+  if (__lane_id() == 0) s_red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    fix128 t = 0;
+    for (int w = 0; w < 256 / 64; ++w) t += s_red[w];
+    store_fix(partial + 3 * blockIdx.x, t);
+    partial[3 * blockIdx.x + 2] = __builtin_bit_cast(unsigned long long, nf);
+  }
 }
 
 static PartTypes part_types(const dq_freq* f, int parts) {
@@ -5813,9 +5867,10 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
     stamp(k ? "marginal 1 index" : "marginal 0 index");
   }
   if (res == DQ_OK) {
-    DevBuf<double> terms, partial;
+    DevBuf<double> terms;
+    DevBuf<unsigned long long> partial;
     constexpr int kSumBlocks = 1024;
-    if (terms.ensure(n) != hipSuccess || partial.ensure(kSumBlocks) != hipSuccess) {
+    if (terms.ensure(n) != hipSuccess || partial.ensure(3 * kSumBlocks) != hipSuccess) {
       res = fail(DQ_ERR_OUT_OF_MEMORY, "MutualInformation terms");
     } else {
       if (by_hash) {
@@ -5835,15 +5890,19 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
                            (double)joint->num_rows, terms.p);
       }
       stamp("terms");
-      hipLaunchKernelGGL(freq_sum_f64, dim3(kSumBlocks), dim3(256), 0, stream, terms.p, n, partial.p);
-      std::vector<double> h(kSumBlocks);
+      hipLaunchKernelGGL(freq_sum_fix, dim3(kSumBlocks), dim3(256), 0, stream, terms.p, n, partial.p);
+      std::vector<unsigned long long> h(3 * kSumBlocks);
       if (hipGetLastError() != hipSuccess ||
-          d2h(h.data(), partial.p, kSumBlocks * 8, stream) != hipSuccess) {
+          d2h(h.data(), partial.p, 3 * kSumBlocks * 8, stream) != hipSuccess) {
         res = fail(DQ_ERR_DEVICE, "MutualInformation launch failed");
       } else {
-        double sum = 0.0;
-        for (double v : h) sum += v;
-        *mi = sum;
+        fix128 sum = 0;
+        double nf = 0.0;
+        for (int b = 0; b < kSumBlocks; ++b) {
+          sum += (fix128)(((unsigned __int128)h[3 * b + 1] << 64) | h[3 * b]);
+          nf += __builtin_bit_cast(double, h[3 * b + 2]);
+        }
+        *mi = fix_to_f64(sum) + nf;
       }
     }
   }

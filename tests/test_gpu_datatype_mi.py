@@ -149,9 +149,9 @@ def test_mutual_information_hash_lookups_equal_byte_lookups(kinds, gpu_device, m
     fast = MutualInformation("a", "b").calculate(df).value.get()
     monkeypatch.setenv("DQ_FREQ_MI_LOOKUP", "1")
     slow = MutualInformation("a", "b").calculate(df).value.get()
-    # (each run builds its own joint table: the groups' order, and so the last bits of the
-    # fixed-order sum, may differ; the terms themselves are the same function of the counts)
-    assert abs(fast - slow) <= 1e-12 * abs(slow), (fast, slow)
+    # each run builds its own joint table (the groups come in another order), but the terms are
+    # the same function of the counts and their sum is order-free (fixed point): bit-identical
+    assert fast == slow, (fast, slow)
     exp = mutual_information(OTable({"a": a.to_pylist(), "b": b.to_pylist()},
                                     {"a": kinds[0], "b": kinds[1]}), "a", "b")
     assert abs(fast - exp) <= 1e-12 * max(1.0, abs(exp)), (fast, exp)
