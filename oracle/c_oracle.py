@@ -50,6 +50,9 @@ def lib():
         L.or_numeric_f64.argtypes = [vp, vp, i64, ctypes.c_double, i32, ctypes.POINTER(OrNumericD)]
         L.or_dfa_count.argtypes = [vp, vp, vp, i64, vp, vp, vp, i32, i32, i32]
         L.or_dfa_count.restype = i64
+        L.or_dtype_utf8.argtypes = [vp, vp, vp, i64, i32, vp]
+        L.or_mi_utf8.argtypes = [vp, vp, vp, vp, vp, vp, i64, i64, i32]
+        L.or_mi_utf8.restype = ctypes.c_double
         _LIB = L
     return _LIB
 
@@ -157,3 +160,16 @@ def dfa_count(offsets, data, valid_bits, n, compiled, threads: int = 1) -> int:
     nx = np.asarray(compiled.next, np.uint16)
     return int(lib().or_dfa_count(_p(offsets), _p(data), _p(valid_bits), int(n), _p(bc), _p(st),
                                   _p(nx), compiled.n_classes, compiled.start, int(threads)))
+
+
+def dtype_utf8(offsets, data, valid_bits, n, threads: int = 1):
+    """DataType's (NULL, Fractional, Integral, Boolean, String) counts of a utf8 column."""
+    out = np.zeros(5, np.int64)
+    lib().or_dtype_utf8(_p(offsets), _p(data), _p(valid_bits), int(n), int(threads), _p(out))
+    return tuple(int(v) for v in out)
+
+
+def mi_utf8(a, b, n, num_rows, threads: int = 1) -> float:
+    """MutualInformation of two utf8 columns; a / b = (offsets, data, validity)."""
+    return float(lib().or_mi_utf8(_p(a[0]), _p(a[1]), _p(a[2]), _p(b[0]), _p(b[1]), _p(b[2]),
+                                  int(n), int(num_rows), int(threads)))

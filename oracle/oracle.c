@@ -685,3 +685,228 @@ int64_t or_dfa_count(const int32_t* off, const uint8_t* data, const uint8_t* val
   }
   return hits;
 }
+
+/* DataType over a utf8 column (M/analyzers/catalyst/StatefulDataType.scala:36-69): each non-NULL
+ * value is classified by the first of three full matches, FRACTIONAL ^(-|\+)? ?\d*\.\d*$, then
+ * INTEGRAL ^(-|\+)? ?\d*$, then BOOLEAN ^(true|false)$ (\d = [0-9], Java's default), else String;
+ * NULL rows count apart.  out5 = (NULL, Fractional, Integral, Boolean, String). */
+static int dtype_class(const uint8_t* s, int32_t len) {
+  int32_t i = 0;
+  if (i < len && (s[i] == '-' || s[i] == '+')) ++i;
+  if (i < len && s[i] == ' ') ++i;
+  while (i < len && s[i] >= '0' && s[i] <= '9') ++i;
+  if (i == len) return 2;  /* INTEGRAL (the empty string too) */
+  if (s[i] == '.') {
+    ++i;
+    while (i < len && s[i] >= '0' && s[i] <= '9') ++i;
+    if (i == len) return 1;  /* FRACTIONAL */
+  }
+  if ((len == 4 && memcmp(s, "true", 4) == 0) || (len == 5 && memcmp(s, "false", 5) == 0)) return 3;
+  return 4;
+}
+
+void or_dtype_utf8(const int32_t* off, const uint8_t* data, const uint8_t* valid, int64_t n,
+                   int nthreads, int64_t* out5) {
+  int64_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+#pragma omp parallel for num_threads(nthreads) reduction(+ : c0, c1, c2, c3, c4) schedule(static)
+  for (int64_t r = 0; r < n; ++r) {
+    if (!bit(valid, r)) {
+      ++c0;
+      continue;
+    }
+    switch (dtype_class(data + off[r], off[r + 1] - off[r])) {
+      case 1: ++c1; break;
+      case 2: ++c2; break;
+      case 3: ++c3; break;
+      default: ++c4; break;
+    }
+  }
+  out5[0] = c0;
+  out5[1] = c1;
+  out5[2] = c2;
+  out5[3] = c3;
+  out5[4] = c4;
+}
+
+/* MutualInformation of two utf8 columns (M/analyzers/MutualInformation.scala:41-84): the joint
+ * frequencies of the rows where both are non-NULL (a hash-partitioned aggregation, as or_freq), the
+ * two marginals re-aggregated from the joint groups, and the sum over the joint groups of
+ * (c/n) ln((c/n) / ((cx/n)(cy/n))) with n = num_rows, partition partials added in partition order. */
+typedef struct {
+  int64_t row, c;
+} or_group;
+
+static inline uint64_t utf8_hash(const int32_t* off, const uint8_t* data, int64_t r, uint64_t seed) {
+  return or_xxh64(data + off[r], off[r + 1] - off[r], seed);
+}
+static inline int utf8_eq(const int32_t* off, const uint8_t* data, int64_t a, int64_t b) {
+  const int32_t la = off[a + 1] - off[a], lb = off[b + 1] - off[b];
+  return la == lb && memcmp(data + off[a], data + off[b], (size_t)la) == 0;
+}
+
+/* counts per distinct value of column (off, data) over the rows `rows[0..m)` weighted by w[]:
+ * a hash table of representative rows; returns the number of groups, fills grow/gcnt */
+static int64_t agg_rows(const int32_t* off, const uint8_t* data, const int64_t* rows,
+                        const int64_t* w, int64_t m, int64_t* grow, int64_t* gcnt, int64_t* slot_of) {
+  size_t cap = 16;
+  while (cap < (size_t)m * 2) cap <<= 1;
+  int64_t* trow = (int64_t*)malloc(cap * sizeof(int64_t));
+  int64_t* tidx = (int64_t*)malloc(cap * sizeof(int64_t));
+  uint64_t* th = (uint64_t*)malloc(cap * sizeof(uint64_t));
+  for (size_t i = 0; i < cap; ++i) trow[i] = -1;
+  int64_t g = 0;
+  for (int64_t i = 0; i < m; ++i) {
+    const int64_t r = rows[i];
+    const uint64_t h = utf8_hash(off, data, r, 0);
+    size_t s = (size_t)(h & (cap - 1));
+    for (;;) {
+      if (trow[s] < 0) {
+        trow[s] = r;
+        th[s] = h;
+        tidx[s] = g;
+        grow[g] = r;
+        gcnt[g] = w ? w[i] : 1;
+        slot_of[i] = g++;
+        break;
+      }
+      if (th[s] == h && utf8_eq(off, data, trow[s], r)) {
+        gcnt[tidx[s]] += w ? w[i] : 1;
+        slot_of[i] = tidx[s];
+        break;
+      }
+      s = (s + 1) & (cap - 1);
+    }
+  }
+  free(trow);
+  free(tidx);
+  free(th);
+  return g;
+}
+
+double or_mi_utf8(const int32_t* off1, const uint8_t* d1, const uint8_t* v1, const int32_t* off2,
+                  const uint8_t* d2, const uint8_t* v2, int64_t n, int64_t num_rows, int nthreads) {
+  /* joint rows by the hash of (x, y): P partitions, then per partition the joint groups */
+  const int P = 256;
+  int64_t* rows = (int64_t*)malloc((size_t)(n > 0 ? n : 1) * 8);
+  uint64_t* hs = (uint64_t*)malloc((size_t)(n > 0 ? n : 1) * 8);
+  int64_t* cnt = (int64_t*)calloc((size_t)nthreads * P, sizeof(int64_t));
+#pragma omp parallel num_threads(nthreads)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t r0 = n * t / nthreads, r1 = n * (t + 1) / nthreads;
+    for (int64_t r = r0; r < r1; ++r) {
+      if (!bit(v1, r) || !bit(v2, r)) {
+        hs[r] = 0;
+        continue;
+      }
+      hs[r] = utf8_hash(off1, d1, r, 0) * 31 + utf8_hash(off2, d2, r, 1);
+      ++cnt[(size_t)t * P + (hs[r] >> 56)];
+    }
+  }
+  int64_t* base = (int64_t*)malloc((size_t)nthreads * P * sizeof(int64_t));
+  int64_t* pbeg = (int64_t*)malloc((size_t)(P + 1) * sizeof(int64_t));
+  int64_t acc = 0;
+  for (int p = 0; p < P; ++p) {
+    pbeg[p] = acc;
+    for (int t = 0; t < nthreads; ++t) {
+      base[(size_t)t * P + p] = acc;
+      acc += cnt[(size_t)t * P + p];
+    }
+  }
+  pbeg[P] = acc;
+#pragma omp parallel num_threads(nthreads)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t r0 = n * t / nthreads, r1 = n * (t + 1) / nthreads;
+    int64_t* b = base + (size_t)t * P;
+    for (int64_t r = r0; r < r1; ++r)
+      if (bit(v1, r) && bit(v2, r)) rows[b[hs[r] >> 56]++] = r;
+  }
+  /* joint groups (representative row, count), partition by partition */
+  or_group* jg = (or_group*)malloc((size_t)(acc > 0 ? acc : 1) * sizeof(or_group));
+  int64_t* jn = (int64_t*)calloc(P, sizeof(int64_t));
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+  for (int p = 0; p < P; ++p) {
+    const int64_t m = pbeg[p + 1] - pbeg[p];
+    size_t cap = 16;
+    while (cap < (size_t)m * 2) cap <<= 1;
+    int64_t* trow = (int64_t*)malloc(cap * sizeof(int64_t));
+    int64_t* tix = (int64_t*)malloc(cap * sizeof(int64_t));
+    for (size_t i = 0; i < cap; ++i) trow[i] = -1;
+    or_group* out = jg + pbeg[p];
+    int64_t g = 0;
+    for (int64_t i = pbeg[p]; i < pbeg[p + 1]; ++i) {
+      const int64_t r = rows[i];
+      size_t s = (size_t)(hs[r] & (cap - 1));
+      for (;;) {
+        if (trow[s] < 0) {
+          trow[s] = r;
+          tix[s] = g;
+          out[g].row = r;
+          out[g].c = 1;
+          ++g;
+          break;
+        }
+        const int64_t q = trow[s];
+        if (hs[q] == hs[r] && utf8_eq(off1, d1, q, r) && utf8_eq(off2, d2, q, r)) {
+          ++out[tix[s]].c;
+          break;
+        }
+        s = (s + 1) & (cap - 1);
+      }
+    }
+    jn[p] = g;
+    free(trow);
+    free(tix);
+  }
+  /* compact the joint groups; the marginals from them (weighted by the joint counts) */
+  int64_t G = 0;
+  for (int p = 0; p < P; ++p) {
+    memmove(jg + G, jg + pbeg[p], (size_t)jn[p] * sizeof(or_group));
+    G += jn[p];
+  }
+  int64_t* grows = (int64_t*)malloc((size_t)(G > 0 ? G : 1) * 8);
+  int64_t* gw = (int64_t*)malloc((size_t)(G > 0 ? G : 1) * 8);
+  for (int64_t i = 0; i < G; ++i) {
+    grows[i] = jg[i].row;
+    gw[i] = jg[i].c;
+  }
+  int64_t* mrow = (int64_t*)malloc((size_t)(G > 0 ? G : 1) * 8);
+  int64_t* mx = (int64_t*)malloc((size_t)(G > 0 ? G : 1) * 8);
+  int64_t* my = (int64_t*)malloc((size_t)(G > 0 ? G : 1) * 8);
+  int64_t* sx = (int64_t*)malloc((size_t)(G > 0 ? G : 1) * 8);
+  int64_t* sy = (int64_t*)malloc((size_t)(G > 0 ? G : 1) * 8);
+  agg_rows(off1, d1, grows, gw, G, mrow, mx, sx);
+  agg_rows(off2, d2, grows, gw, G, mrow, my, sy);
+  const double tot = (double)num_rows;
+  double* pe = (double*)calloc((size_t)nthreads, sizeof(double));
+#pragma omp parallel num_threads(nthreads)
+  {
+    const int t = omp_get_thread_num();
+    const int64_t i0 = G * t / nthreads, i1 = G * (t + 1) / nthreads;
+    double e = 0.0;
+    for (int64_t i = i0; i < i1; ++i) {
+      const double pxy = (double)gw[i] / tot, px = (double)mx[sx[i]] / tot, py = (double)my[sy[i]] / tot;
+      e += pxy * log(pxy / (px * py));
+    }
+    pe[t] = e;
+  }
+  double mi = 0.0;
+  for (int t = 0; t < nthreads; ++t) mi += pe[t];
+  free(pe);
+  free(sy);
+  free(sx);
+  free(my);
+  free(mx);
+  free(mrow);
+  free(gw);
+  free(grows);
+  free(jn);
+  free(jg);
+  free(pbeg);
+  free(base);
+  free(cnt);
+  free(hs);
+  free(rows);
+  return mi;
+}

@@ -92,3 +92,30 @@ def test_c_dfa_walk_counts_like_the_python_oracle(pattern):
     off, data, valid = _buffers(pa.array(rows, pa.string()))
     got = C.dfa_count(off, data, valid, len(rows), compile_java_regex(pattern), threads=3)
     assert got == sum(O.regex_find_nonempty(r, pattern) for r in rows if r is not None)
+
+
+@pytest.mark.parametrize("threads", [1, 5])
+def test_c_datatype_matches_python_oracle(threads):
+    """or_dtype_utf8 (the configs[4] CPU baseline's DataType) against deequ_oracle.datatype_counts
+    (the three regexes of StatefulDataType.scala:36-38 through Python `re`)."""
+    rng = np.random.default_rng(threads)
+    pool = ["1.5", "-3", " 4", "+ 7", "- .5", "true", "false", "", ".", "abc", "1e5", "12a",
+            "+-1", "  1", "TRUE", "007", "3.", "-", "+", " ", "1.2.3", "falsey", "٣"]
+    vals = [None if rng.random() < 0.07 else str(rng.choice(pool)) for _ in range(20_011)]
+    arr = pa.array(vals, type=pa.string())
+    off, data, valid = _buffers(arr)
+    got = C.dtype_utf8(off, data, valid, len(vals), threads)
+    exp = O.datatype_counts(O.OTable({"s": vals}, {"s": "string"}), "s", None)
+    assert got == exp
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_c_mutual_information_matches_python_oracle(threads):
+    rng = np.random.default_rng(40 + threads)
+    n = 30_000
+    a = [None if rng.random() < 0.05 else f"a{v}" for v in rng.integers(0, 300, n)]
+    b = [None if rng.random() < 0.05 else f"b{v}" for v in rng.integers(0, 7, n)]
+    A, B = _buffers(pa.array(a, pa.string())), _buffers(pa.array(b, pa.string()))
+    got = C.mi_utf8(A, B, n, n, threads)
+    exp = O.mutual_information(O.OTable({"a": a, "b": b}, {"a": "string", "b": "string"}), "a", "b")
+    assert math.isclose(got, exp, rel_tol=1e-12), (got, exp)

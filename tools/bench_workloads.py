@@ -420,6 +420,7 @@ def cpu_baseline(args, table, min_seconds: float = 10.0):
         ints = [c for c in names if c == "id" or c.startswith("numViews")]
         dbls = [c for c in names if c.startswith("score")]
         strs = [c for c in names if c not in ints and c not in dbls]
+        nv2 = cols["numViews_2"][0].astype(np.float64)  # (Correlation(id, numViews_2) in doubles)
 
         def one():
             for c in ints:
@@ -440,12 +441,17 @@ def cpu_baseline(args, table, min_seconds: float = 10.0):
                 C.hll(8, o, d, m, n, threads)
                 C.freq("string", o, d, m, n, n, True, 1000, threads)
                 C.dfa_count(o, d, m, n, url, threads)
+                C.dtype_utf8(o, d, m, n, threads)            # DataType
             for x, y in (("numViews_0", "score_0"), ("numViews_1", "score_1")):
                 C.corr(cols[x][0], cols[x][2], cols[y][0].view(np.float64), cols[y][2], threads)
-        what = ("configs[4] minus DataType and MutualInformation: per numeric column the scan "
-                "aggregates (or_numeric_i64/_f64), or_hll, or_freq (Uniqueness..Histogram) and a "
-                "numpy sort for ApproxQuantile; per string column or_hll, or_freq and the URL "
-                "PatternMatch as a DFA walk (or_dfa_count); two Correlations")
+            C.corr(cols["id"][0], cols["id"][2], nv2, cols["numViews_2"][2], threads)
+            for x, y in (("priority_0", "priority_1"), ("name_0", "priority_2")):
+                C.mi_utf8(cols[x], cols[y], n, n, threads)   # MutualInformation
+        what = ("the whole configs[4] suite: per numeric column the scan aggregates "
+                "(or_numeric_i64/_f64), or_hll, or_freq (Uniqueness..Histogram) and a numpy sort "
+                "for ApproxQuantile; per string column or_hll, or_freq, the URL PatternMatch as a "
+                "DFA walk (or_dfa_count) and DataType (or_dtype_utf8); three Correlations; the two "
+                "MutualInformations (or_mi_utf8: joint hash aggregation + marginals)")
     one()
     reps, t0 = 0, time.perf_counter()
     while True:
