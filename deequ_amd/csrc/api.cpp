@@ -1097,6 +1097,80 @@ extern "C" dq_status dq_scan_device(const dq_plan* plan, const dq_column* cols, 
   return dq_scan_device_batches(plan, cols, n_cols, 1, s, hip_stream);
 }
 
+// ---- guided tail of the scan queue ----------------------------------------------------------
+constexpr int64_t kTailDiv = 32;      // the last 1/32 of a descriptor's items ...
+constexpr int64_t kTailCut = 8;       // ... are cut 8 ways
+constexpr int64_t kTailMinItems = 16;
+static bool tail_split() {  // DQ_TAIL_SPLIT=0: A/B hook, uniform items
+  static const bool on = [] {
+    const char* e = getenv("DQ_TAIL_SPLIT");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
+// Does launch L (one class, items [item_lo, item_hi)) have small tail items?
+static bool scan_has_tail(const TaskDesc* td, size_t n_desc, const ScanLaunch& L) {
+  for (size_t q = 0; q < n_desc; ++q)
+    if (td[q].n_items > td[q].n_big && (uint32_t)td[q].item_begin >= L.item_lo &&
+        (uint32_t)td[q].item_begin < L.item_hi)
+      return true;
+  return false;
+}
+
+// The queue order of the launches of one queue (one class, or the classes of a mixed launch),
+// appended to `out`: within the big items and within the small ones, the classes interleaved in
+// proportion to their counts; then each of the kernel's kQueueHeads slices (queue_next: entries
+// [n x / H, n (x + 1) / H)) is filled with its share of the big items followed by its share of
+// the small ones, so every slice ends on small items.
+static void scan_order(const TaskDesc* td, size_t n_desc, const std::vector<ScanLaunch>& G,
+                       std::vector<uint32_t>& out) {
+  std::vector<std::vector<uint32_t>> big(G.size()), small(G.size());
+  for (size_t c = 0; c < G.size(); ++c)
+    for (size_t q = 0; q < n_desc; ++q) {
+      const TaskDesc& t = td[q];
+      if (t.n_items == 0 || (uint32_t)t.item_begin < G[c].item_lo || (uint32_t)t.item_begin >= G[c].item_hi)
+        continue;
+      for (int64_t i = 0; i < t.n_items; ++i)
+        (i < t.n_big ? big[c] : small[c]).push_back((uint32_t)(t.item_begin + i));
+    }
+  auto interleave = [](std::vector<std::vector<uint32_t>>& lists) {
+    std::vector<uint32_t> r;
+    std::vector<size_t> next(lists.size(), 0);
+    size_t total = 0;
+    for (auto& l : lists) total += l.size();
+    r.reserve(total);
+    for (size_t k = 0; k < total; ++k) {
+      int best = -1;
+      double best_key = 0.0;
+      for (size_t c = 0; c < lists.size(); ++c) {
+        if (next[c] >= lists[c].size()) continue;
+        const double key = (next[c] + 0.5) / (double)lists[c].size();
+        if (best < 0 || key < best_key) {
+          best = (int)c;
+          best_key = key;
+        }
+      }
+      r.push_back(lists[best][next[best]++]);
+    }
+    return r;
+  };
+  const std::vector<uint32_t> B = interleave(big), S = interleave(small);
+  const uint64_t n = B.size() + S.size();
+  size_t bi = 0, si = 0;
+  for (int x = 0; x < kQueueHeads; ++x) {
+    const uint64_t len = n * (x + 1) / kQueueHeads - n * x / kQueueHeads;
+    const uint64_t want_s = (uint64_t)S.size() * (x + 1) / kQueueHeads - (uint64_t)si;
+    uint64_t ns = std::min<uint64_t>(want_s, len), nb = len - ns;
+    if (nb > B.size() - bi) {  // (rounding: not enough big items left, take small ones)
+      nb = B.size() - bi;
+      ns = len - nb;
+    }
+    for (uint64_t k = 0; k < nb; ++k) out.push_back(B[bi++]);
+    for (uint64_t k = 0; k < ns; ++k) out.push_back(S[si++]);
+  }
+}
+
 extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column* cols, int n_cols,
                                             int n_batches, dq_state* s, void* hip_stream) {
   if (!plan || !s || (n_cols > 0 && n_batches > 0 && !cols))
@@ -1305,6 +1379,17 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
       t.item_rows = item_rows;
       // a carried HLL task keeps its (empty) descriptors: finalize finds the task through them
       t.n_items = rows[b] > 0 && !tp.carried ? (rows[b] + item_rows - 1) / item_rows : 0;
+      t.n_big = t.n_items;
+      t.small_rows = item_rows;
+      // guided tail: the last 1/kTailDiv of a descriptor's items are cut kTailCut ways; the queue
+      // order hands these out last in every slice (scan_orders), so the waves of a launch finish
+      // within a small item of each other instead of a ~130 us big item (S10: ~3000 waves)
+      if (tail_split() && t.n_items >= kTailMinItems && item_rows >= kTailCut * kItemAlign) {
+        const int64_t k = (t.n_items + kTailDiv - 1) / kTailDiv;
+        t.n_big = t.n_items - k;
+        t.small_rows = item_rows / kTailCut;
+        t.n_items = t.n_big + (rows[b] - t.n_big * item_rows + t.small_rows - 1) / t.small_rows;
+      }
       t.item_begin = total_items;
       total_items += t.n_items;
       td[d] = t;
@@ -1317,56 +1402,74 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
   if (total_items >= ((int64_t)1 << 31))
     return fail(DQ_ERR_UNSUPPORTED, "scan of %lld work items exceeds one launch",
                 (long long)total_items);
-  // Two or more body classes: one mixed launch over their items, interleaved in proportion to
-  // each class's item count (item j of a class with n items sorts at (j + 1/2) / n), so string
-  // gathers, XXH64 hashing and streaming bodies run side by side.  HLL joins the mixed launch when
-  // its LDS registers fit (s->mix_hll), else it keeps its own launch.
+  // Queue orders.  Two or more body classes: one mixed launch over their items, interleaved in
+  // proportion to each class's item count (item j of a class with n items sorts at (j + 1/2) / n),
+  // so string gathers, XXH64 hashing and streaming bodies run side by side.  HLL joins the mixed
+  // launch when its LDS registers fit (s->mix_hll), else it keeps its own launch.  A launch whose
+  // descriptors have small tail items gets an order list too (scan_orders: big items, then the
+  // small ones at the end of every queue slice).
   {
     std::vector<ScanLaunch> plain, hll;
     for (const ScanLaunch& L : launches)
       // the fused body keeps HLL registers in LDS too, and the mixed kernel has no such body
       ((L.body == BC_HLL && !s->mix_hll) || L.body == BC_CORR_HLL ? hll : plain).push_back(L);
-    if (plain.size() >= 2 && !getenv("DQ_NO_MIXED")) {
-      std::vector<uint32_t> sig;
-      for (const ScanLaunch& L : plain) {
+    const bool mixed = plain.size() >= 2 && !getenv("DQ_NO_MIXED");
+    if (mixed && plain.front().item_lo != 0) return fail(DQ_ERR_STATE, "unexpected item layout");
+    std::vector<std::vector<ScanLaunch>> groups;  // the launches that share one queue
+    if (mixed) groups.push_back(plain);
+    else
+      for (const ScanLaunch& L : plain) groups.push_back({L});
+    for (const ScanLaunch& L : hll) groups.push_back({L});
+    std::vector<uint32_t> sig;
+    for (size_t q = 0; q < n_desc; ++q) {
+      sig.push_back((uint32_t)td[q].item_begin);
+      sig.push_back((uint32_t)td[q].n_big);
+      sig.push_back((uint32_t)td[q].n_items);
+    }
+    for (const auto& G : groups) {
+      sig.push_back(0xffffffffu);
+      for (const ScanLaunch& L : G) {
         sig.push_back(L.item_lo);
         sig.push_back(L.item_hi);
       }
-      const uint32_t n_order = plain.back().item_hi;  // classes are numbered in item order
-      if (plain.front().item_lo != 0) return fail(DQ_ERR_STATE, "unexpected item layout");
-      if (s->order_sig[slot] != sig) {
-        std::vector<uint32_t> order;
-        order.reserve(n_order);
-        std::vector<uint32_t> next(plain.size(), 0);
-        for (uint32_t q = 0; q < n_order; ++q) {
-          int best = -1;
-          double best_key = 0.0;
-          for (size_t c = 0; c < plain.size(); ++c) {
-            const uint32_t n = plain[c].item_hi - plain[c].item_lo;
-            if (next[c] >= n) continue;
-            const double key = (next[c] + 0.5) / (double)n;
-            if (best < 0 || key < best_key) {
-              best = (int)c;
-              best_key = key;
-            }
-          }
-          order.push_back(plain[best].item_lo + next[best]++);
-        }
-        HIP_TRY(s->d_order[slot].ensure(std::max<size_t>(1, order.size())));
-        HIP_TRY(hipMemcpy(s->d_order[slot].p, order.data(), order.size() * sizeof(uint32_t),
+    }
+    std::vector<size_t> off(groups.size(), 0), len(groups.size(), 0);
+    std::vector<uint32_t> all;
+    for (size_t g = 0; g < groups.size(); ++g) {
+      off[g] = all.size();
+      if (groups[g].size() >= 2 || scan_has_tail(td, n_desc, groups[g][0])) {
+        scan_order(td, n_desc, groups[g], all);
+        len[g] = all.size() - off[g];
+      }
+    }
+    if (s->order_sig[slot] != sig) {
+      HIP_TRY(s->d_order[slot].ensure(std::max<size_t>(1, all.size())));
+      if (!all.empty())
+        HIP_TRY(hipMemcpy(s->d_order[slot].p, all.data(), all.size() * sizeof(uint32_t),
                           hipMemcpyHostToDevice));
-        s->order_sig[slot] = sig;
+      s->order_sig[slot] = sig;
+    }
+    launches.clear();
+    for (size_t g = 0; g < groups.size(); ++g) {
+      const uint32_t* ord = len[g] ? s->d_order[slot].p + off[g] : nullptr;
+      if (groups[g].size() >= 2) {
+        bool has_hll = false;
+        uint32_t classes = 0;
+        for (const ScanLaunch& L : groups[g]) {
+          has_hll = has_hll || L.body == BC_HLL;
+          classes |= 1u << L.body;
+        }
+        launches.push_back(ScanLaunch{kBodyMixed, s->grid[kBodyMixed], 0, (uint32_t)len[g], ord,
+                                      has_hll ? s->mix_hll : 0, classes});
+      } else {
+        ScanLaunch L = groups[g][0];
+        if (ord) {
+          L.item_lo = 0;
+          L.item_hi = (uint32_t)len[g];
+          L.order = ord;
+        }
+        launches.push_back(L);
       }
-      launches.clear();
-      bool has_hll = false;
-      uint32_t classes = 0;
-      for (const ScanLaunch& L : plain) {
-        has_hll = has_hll || L.body == BC_HLL;
-        classes |= 1u << L.body;
-      }
-      launches.push_back(ScanLaunch{kBodyMixed, s->grid[kBodyMixed], 0, n_order,
-                                    s->d_order[slot].p, has_hll ? s->mix_hll : 0, classes});
-      for (const ScanLaunch& L : hll) launches.push_back(L);
     }
   }
   if (getenv("DQ_DEBUG")) {

@@ -77,6 +77,10 @@ struct TaskDesc {
   int64_t item_rows;      // rows per work item (multiple of kItemAlign)
   int64_t item_begin;     // first global item index of this descriptor
   int64_t n_items;
+  // guided tail: items [0, n_big) take item_rows rows each, the rest small_rows each (the queue
+  // hands the small ones out last, so waves finish within a small item of each other)
+  int64_t n_big;
+  int64_t small_rows;
   const uint8_t* valid;   // column 1
   const void* values;
   const uint8_t* data;

@@ -157,8 +157,9 @@ constexpr int kQueueWords = kQueues * kQueueHeads * kQueueStride;
 struct ScanLaunch {
   int32_t body;            // BodyClass, or kBodyMixed
   int32_t grid;
-  uint32_t item_lo, item_hi;  // kBodyMixed: item_lo = 0, item_hi = entries of `order`
-  const uint32_t* order;   // kBodyMixed: queue position -> global item index
+  uint32_t item_lo, item_hi;  // with `order`: item_lo = 0, item_hi = entries of `order`
+  const uint32_t* order;   // queue position -> global item index (kBodyMixed always; a one-class
+                           // launch when its descriptors have small tail items), else nullptr
   int32_t lds_hll = 0;     // kBodyMixed: HLL tasks whose registers the launch keeps in LDS
   uint32_t classes = 0;    // kBodyMixed: the body classes of its items (bit per BodyClass)
 };

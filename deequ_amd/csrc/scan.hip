@@ -918,6 +918,18 @@ DQ_DEV void corr_hll_chunk8(const TaskDesc& t, int64_t r0, bool xl, bool yl, int
 // turn.  Every call either returns an item or moves to the next slice, so a wave ends after at
 // most kQueueHeads empty pulls, and a queue that was not re-armed just ends every wave.
 // ------------------------------------------------------------------------------------------------
+// The rows of global work item `item` of descriptor t: big items first, then the small tail items.
+DQ_DEV void item_range(const TaskDesc& t, uint32_t item, int64_t& r_begin, int64_t& r_end) {
+  const int64_t li = (int64_t)item - t.item_begin;
+  if (li < t.n_big) {
+    r_begin = li * t.item_rows;
+    r_end = min(r_begin + t.item_rows, t.rows);
+  } else {
+    r_begin = t.n_big * t.item_rows + (li - t.n_big) * t.small_rows;
+    r_end = min(r_begin + t.small_rows, t.rows);
+  }
+}
+
 DQ_DEV bool queue_next(uint32_t* heads, uint32_t lo, uint32_t hi, int home, int& step,
                        uint32_t& item) {
   const uint32_t n = hi - lo;
@@ -952,6 +964,7 @@ DQ_DEV bool queue_next(uint32_t* heads, uint32_t lo, uint32_t hi, int home, int&
 template <int BC, int K = 8>
 __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? (K == 8 ? 4 : 5) : 1)) scan_kernel(const TaskDesc* __restrict__ tasks, int n_desc,
                                                       uint32_t item_lo, uint32_t item_hi,
+                                                      const uint32_t* __restrict__ order,
                                                       uint32_t* __restrict__ queue,
                                                       Acc* __restrict__ partial,
                                                       uint32_t* __restrict__ hll_stage, int n_hll) {
@@ -964,7 +977,9 @@ __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? (K == 8 ? 4 : 5) 
   const int l = lane_id();
   int step = 0;
   uint32_t item = 0;
+  // with an order list the queue runs over its entries (item_lo = 0, item_hi = entries)
   while (queue_next(queue, item_lo, item_hi, (int)(blockIdx.x % kQueueHeads), step, item)) {
+    if (order) item = order[item];
     // descriptor = the last one whose first item is <= item (empty descriptors share their
     // first item with the next non-empty one, so they are never selected)
     int lo = 0, hi = n_desc - 1;
@@ -974,8 +989,8 @@ __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? (K == 8 ? 4 : 5) 
       else hi = mid - 1;
     }
     const TaskDesc& t = tasks[lo];
-    const int64_t r_begin = ((int64_t)item - t.item_begin) * t.item_rows;
-    const int64_t r_end = min(r_begin + t.item_rows, t.rows);
+    int64_t r_begin, r_end;
+    item_range(t, item, r_begin, r_end);
     Acc a;
     acc_init(t.kind, a);
     if constexpr (BC == BC_NUM_I8) num_item<int8_t>(t, r_begin, r_end, a);
@@ -1047,8 +1062,8 @@ scan_mixed_kernel(const TaskDesc* __restrict__ tasks, int n_desc, uint32_t n_ord
       else hi = mid - 1;
     }
     const TaskDesc& t = tasks[lo];
-    const int64_t r_begin = ((int64_t)item - t.item_begin) * t.item_rows;
-    const int64_t r_end = min(r_begin + t.item_rows, t.rows);
+    int64_t r_begin, r_end;
+    item_range(t, item, r_begin, r_end);
     Acc a;
     acc_init(t.kind, a);
 #define DQ_BODY(BCV, CALL) \
@@ -1198,8 +1213,8 @@ static void launch_body(const ScanLaunch& L, const TaskDesc* tasks, int n_desc, 
                         uint32_t* queues, Acc* partial, uint32_t* hll_stage, hipStream_t stream) {
   auto go = [&](auto kernel) {
     hipLaunchKernelGGL(kernel, dim3(L.grid), dim3(kBlock), scan_lds_bytes(BC, n_hll), stream,
-                       tasks, n_desc, L.item_lo, L.item_hi, queues + BC * kQueueHeads * kQueueStride,
-                       partial, hll_stage, n_hll);
+                       tasks, n_desc, L.item_lo, L.item_hi, L.order,
+                       queues + BC * kQueueHeads * kQueueStride, partial, hll_stage, n_hll);
   };
   if constexpr (BC == BC_CORR_HLL) {
     if (corr_k() == 4) {
