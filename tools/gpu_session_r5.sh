@@ -5,6 +5,8 @@
 #              the S10 evidence session (tools/gpu_s10_prof.sh: bench line, kernel stats,
 #              FETCH_SIZE / WRITE_SIZE passes).
 #  PART=tests: the -m gpu suite only (TESTS narrows it).
+#  PART=all:   the whole -m gpu suite, then the configs[4] line with its CPU baseline and the
+#              configs[2] / [3] lines.
 #  PART=wl:    configs[2] / [3] / [4] lines (tools/bench_workloads.py).
 #  PART=c3:    configs[2] line, its rocprof kernel stats and PMC passes (tools/gpu_pmc_c3.sh).
 #  PART=c5:    configs[4] line and its rocprof kernel stats.
@@ -23,6 +25,17 @@ full)
   ;;
 tests)
   timeout -k 10 ${LIMIT:-800} $PYT ${TESTS:-tests} -m gpu > $O/gpu_tests_$T.log 2>&1
+  ;;
+all)
+  timeout -k 10 800 $PYT tests -m gpu > $O/gpu_tests_$T.log 2>&1 &&
+  timeout -k 10 200 python -u bench.py --no-cpu-baseline > $O/bench_$T.json 2>&1 &&
+  DQ_TAIL_SPLIT=0 timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-h2d > $O/bench_notail_$T.json 2>&1 &&
+  timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-h2d > $O/bench2_$T.json 2>&1 &&
+  timeout -k 10 500 python -u tools/bench_workloads.py c5 --steps 5 --cpu-baseline --cpu-rows 8388608 > $O/wl_c5_$T.json 2>&1 &&
+  timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
+  timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 10 --warmup 3 > $O/wl_c4_$T.json 2>&1 &&
+  DQ_FREQ_PARTITION_TARGET=3800 timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_t3800_$T.json 2>&1 &&
+  DQ_TAIL_SPLIT=0 timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 10 --warmup 3 > $O/wl_c4_notail_$T.json 2>&1
   ;;
 wl)
   timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
