@@ -76,6 +76,17 @@ class FrequencyTable:
         N.check(N.lib.dq_freq_num_groups(self.handle, ctypes.byref(n)))
         return int(n.value)
 
+    def hll_words(self, max_groups: int):
+        """ApproxCountDistinct's 52 register words (signed, as the scan's state holds them) from
+        this one-column table's groups (dq_freq_hll), or None when it has more than max_groups
+        groups or is not a one-column table: the caller scans the rows instead."""
+        words = (ctypes.c_uint64 * 52)()
+        done = ctypes.c_int()
+        N.check(N.lib.dq_freq_hll(self.handle, int(max_groups), words, ctypes.byref(done), None))
+        if not done.value:
+            return None
+        return tuple(int(w) - (1 << 64) if w >= (1 << 63) else int(w) for w in words)
+
     def null_literal(self) -> Tuple[int, int]:
         """(rows of the NULL group, count of the "NullValue" string group) of a Histogram table
         (dq_freq_null_literal); the second is 0 unless the key is one string column."""

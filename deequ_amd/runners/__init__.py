@@ -21,6 +21,7 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
 from ..analyzers.base import (Analyzer, GroupingAnalyzer, Preconditions, ScanShareableAnalyzer)
+from ..analyzers.scan import ApproxCountDistinct
 from ..analyzers.grouping import (FrequenciesAndNumRows, Histogram, KeyedFrequencies,
                                   ScanShareableFrequencyBasedAnalyzer, compute_frequencies,
                                   frequency_row)
@@ -183,8 +184,15 @@ class AnalysisRunner:
         scanning = [a for a in scanning if not (isinstance(a, Histogram) and a.column in hist_set)]
         shareable = [a for a in scanning if isinstance(a, ScanShareableAnalyzer)]
         others = [a for a in scanning if not isinstance(a, ScanShareableAnalyzer)]
+        # ApproxCountDistinct(c) beside a Histogram(c) table built in this run: the registers come
+        # from the table's groups when it has few of them (_hll_from_tables), so the scan skips c
+        hll_cols = _hll_table_columns(shareable, hist_cols, aggregate_with, save_states_with, data)
+        hll_words: Dict[str, tuple] = {}
+        for job in hist_jobs:
+            if job.args[1] in hll_cols:
+                job.keywords["hll_words"] = hll_words
         scan_jobs = [functools.partial(_run_scanning_analyzers, data, shareable, aggregate_with,
-                                       save_states_with)] + \
+                                       save_states_with, hll_words=hll_words if hll_cols else None)] + \
             [functools.partial(_run_scanning_analyzers, data, [a], aggregate_with, save_states_with)
              for a in others]
         group_jobs = [functools.partial(_run_grouping_analyzers, data, list(cols), group,
@@ -257,31 +265,71 @@ class AnalysisRunner:
         return precondition_failures + AnalyzerContext(non_grouped) + grouped
 
 
-def _histogram_and_grouping_job(data, col, hists, group, aggregate_with, save_states_with):
+def _histogram_and_grouping_job(data, col, hists, group, aggregate_with, save_states_with,
+                                hll_words=None):
     """Histogram(col) and the grouping of [col] from one table (_histogram_columns_for_groupings).
     Returns (Histogram metrics, grouping metrics).  If the Histogram table cannot be built, both
-    run (and fail) on their own, as in the reference's two group-bys."""
-    st = _histogram_and_grouping_launch(data, col, hists, group, aggregate_with, save_states_with)
+    run (and fail) on their own, as in the reference's two group-bys.  hll_words (a dict): the
+    column's HLL registers from the table's groups are put there (_hll_from_tables)."""
+    st = _histogram_and_grouping_launch(data, col, hists, group, aggregate_with, save_states_with,
+                                        hll_words)
     _histogram_and_grouping_device(st)
     return _histogram_and_grouping_host(st)
+
+
+# A column's ApproxCountDistinct is taken from its Histogram table (not scanned) when the table
+# has at most this many groups per row, and at most kHllTableMaxGroups: the groups are hashed on
+# the device (dq_freq_hll), a few per thousand rows instead of every row.
+kHllTableGroupsPerRow = 1.0 / 64
+kHllTableMaxGroups = 1 << 22
+
+
+def _hll_table_columns(shareable, hist_cols, aggregate_with, save_states_with, data) -> set:
+    """Columns whose ApproxCountDistinct (no where) may come from this run's Histogram table of
+    the column (DQ_HLL_FROM_TABLE=0 turns it off): one process, no state I/O (a loaded or saved
+    HLL state keeps its scan), and the jobs run one at a time (the scan job runs after the
+    Histogram jobs that fill the registers)."""
+    if (aggregate_with is not None or save_states_with is not None or is_distributed(data)
+            or os.environ.get("DQ_HLL_FROM_TABLE", "1") == "0"
+            or int(os.environ.get("DQ_RUN_WORKERS", "1") or 1) > 1):
+        return set()
+    want = {a.column for a in shareable if isinstance(a, ApproxCountDistinct) and a.where is None}
+    return want & set(hist_cols)
+
+
+def _hll_from_table(st, hll_words) -> None:
+    """The Histogram table's HLL registers into hll_words[col] when it has few groups."""
+    hs, col = st[6], st[1]
+    if hs is None or hll_words is None:
+        return
+    rows = max(1, int(hs.num_rows))
+    cap = min(kHllTableMaxGroups, int(rows * kHllTableGroupsPerRow))
+    try:
+        words = hs.frequencies.hll_words(cap)
+    except Exception:  # noqa: BLE001  (the scan computes it instead)
+        words = None
+    if words is not None:
+        hll_words[col] = words
 
 
 # The job in three stages, so that the sequential runner (_run_jobs) can run one job's host-only
 # stage while the device runs the next job's phase A: launch (the table's batches queued),
 # device (every device result the metrics need: finalize, the top-k, the NULL-group counts --
 # afterwards the table's calls answer from its caches), host (decoding and metric objects).
-def _histogram_and_grouping_launch(data, col, hists, group, aggregate_with, save_states_with):
+def _histogram_and_grouping_launch(data, col, hists, group, aggregate_with, save_states_with,
+                                   hll_words=None):
     try:
         hs = hists[0].compute_state_from(data)
     except Exception:  # noqa: BLE001
         hs = None
-    return (data, col, hists, group, aggregate_with, save_states_with, hs)
+    return (data, col, hists, group, aggregate_with, save_states_with, hs, hll_words)
 
 
 def _histogram_and_grouping_device(st):
     hs, hists = st[6], st[2]
     if hs is None:
         return
+    _hll_from_table(st, st[7])
     try:
         if hs.binning_udf is None and hists and all(h.binning_udf is None for h in hists):
             ft = hs.frequencies
@@ -304,7 +352,7 @@ def _histogram_and_grouping_device(st):
 
 
 def _histogram_and_grouping_host(st):
-    data, col, hists, group, aggregate_with, save_states_with, hs = st
+    data, col, hists, group, aggregate_with, save_states_with, hs, _ = st
     if hs is None:
         return (_run_scanning_analyzers(data, hists, aggregate_with, save_states_with),
                 _run_grouping_analyzers(data, [col], group, aggregate_with, save_states_with,
@@ -409,7 +457,7 @@ def _stages_of(job):
 
 def _launch_failed(st) -> bool:
     """The launch stage of _histogram_and_grouping_job / _histogram_scan_launch built no table."""
-    return st[6] is None if len(st) == 7 else st[2] is not None
+    return st[6] is None if len(st) == 8 else st[2] is not None
 
 
 def _table_fits_beside(job) -> bool:
@@ -441,11 +489,11 @@ def _run_jobs_pipelined(jobs, trace: bool = False) -> list:
     pending = None  # (index, host stage, state) of a job whose host stage has not run
     clock = time.perf_counter
 
-    def stage(what, i, fn, *a):
+    def stage(what, i, fn, *a, **kw):
         if not trace:
-            return fn(*a)
+            return fn(*a, **kw)
         t0 = clock()
-        r = fn(*a)
+        r = fn(*a, **kw)
         print(f"[dq run] {1e3 * t0:12.3f} {1e6 * (clock() - t0):9.1f} us {what} "
               f"{_job_name(jobs[i])}", file=sys.stderr)
         return r
@@ -457,12 +505,12 @@ def _run_jobs_pipelined(jobs, trace: bool = False) -> list:
             if pending is not None and not _table_fits_beside(job):
                 out[pending[0]] = stage("host", pending[0], pending[1], pending[2])
                 pending = None
-            st = stage("launch", i, launch, *job.args)
+            st = stage("launch", i, launch, *job.args, **job.keywords)
             if pending is not None:
                 out[pending[0]] = stage("host", pending[0], pending[1], pending[2])
                 pending = None
                 if _launch_failed(st):  # (maybe out of memory beside the other table: again alone)
-                    st = stage("launch", i, launch, *job.args)
+                    st = stage("launch", i, launch, *job.args, **job.keywords)
             stage("device", i, device, st)
             pending = (i, host, st)
             continue
@@ -529,11 +577,23 @@ def _precondition_failure_metrics(failed: Sequence[Analyzer], schema) -> Analyze
 
 
 def _run_scanning_analyzers(data, analyzers: Sequence[Analyzer], aggregate_with,
-                            save_states_with) -> AnalyzerContext:
-    """AnalysisRunner.runScanningAnalyzers (AnalysisRunner.scala:279-326)."""
+                            save_states_with, hll_words=None) -> AnalyzerContext:
+    """AnalysisRunner.runScanningAnalyzers (AnalysisRunner.scala:279-326).  hll_words: the
+    register words of columns whose Histogram table yielded them (_hll_from_tables): those
+    ApproxCountDistincts take their state from there and leave the fused scan."""
     shareable = [a for a in analyzers if isinstance(a, ScanShareableAnalyzer)]
     others = [a for a in analyzers if not isinstance(a, ScanShareableAnalyzer)]
     results: Dict[Analyzer, object] = {}
+    if hll_words:
+        from ..analyzers.scan import ApproxCountDistinctState
+        kept = []
+        for a in shareable:
+            if isinstance(a, ApproxCountDistinct) and a.where is None and a.column in hll_words:
+                results[a] = a.calculate_metric(ApproxCountDistinctState(hll_words[a.column]),
+                                                aggregate_with, save_states_with)
+            else:
+                kept.append(a)
+        shareable = kept
     if shareable:
         try:
             aggregations = [spec for a in shareable for spec in a.aggregation_functions()]

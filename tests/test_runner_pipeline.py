@@ -85,8 +85,8 @@ def test_staged_jobs_do_not_overlap_without_device_memory(monkeypatch):
 
 
 def test_launch_failed_reads_both_staged_job_kinds():
-    assert R._launch_failed((None,) * 7)
-    assert not R._launch_failed((None,) * 6 + (object(),))
+    assert R._launch_failed((None,) * 8)
+    assert not R._launch_failed((None,) * 6 + (object(), None))
     assert R._launch_failed((object(), None, ValueError("x")))
     assert not R._launch_failed((object(), object(), None))
 
