@@ -759,7 +759,8 @@ struct dq_state {
   bool rows_on_device = false;   // ... not yet read back (dq_state_sync reads it with the rest)
   DevBuf<uint32_t> d_queue;      // work-item counters of the scan kernels, kept zero between launches
   DevBuf<uint32_t> d_order[2];   // mixed launch: queue position -> item (per descriptor slot)
-  std::vector<uint32_t> order_sig[2];  // per-class item ranges d_order[slot] was built for
+  std::vector<uint32_t> order_sig[2];  // the descriptors and launches d_order[slot] was built for
+  std::vector<size_t> order_off[2], order_len[2];  // per queue group: its order list in d_order
   DevBuf<TaskDesc> d_tasks[2];
   TaskDesc* h_tasks[2] = {nullptr, nullptr};
   size_t h_tasks_cap[2] = {0, 0};
@@ -1433,16 +1434,20 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
         sig.push_back(L.item_hi);
       }
     }
-    std::vector<size_t> off(groups.size(), 0), len(groups.size(), 0);
-    std::vector<uint32_t> all;
-    for (size_t g = 0; g < groups.size(); ++g) {
-      off[g] = all.size();
-      if (groups[g].size() >= 2 || scan_has_tail(td, n_desc, groups[g][0])) {
-        scan_order(td, n_desc, groups[g], all);
-        len[g] = all.size() - off[g];
-      }
-    }
+    // (built only when the descriptors change: ~1e5 items per S10 step, cached per slot)
+    std::vector<size_t>& off = s->order_off[slot];
+    std::vector<size_t>& len = s->order_len[slot];
     if (s->order_sig[slot] != sig) {
+      off.assign(groups.size(), 0);
+      len.assign(groups.size(), 0);
+      std::vector<uint32_t> all;
+      for (size_t g = 0; g < groups.size(); ++g) {
+        off[g] = all.size();
+        if (groups[g].size() >= 2 || scan_has_tail(td, n_desc, groups[g][0])) {
+          scan_order(td, n_desc, groups[g], all);
+          len[g] = all.size() - off[g];
+        }
+      }
       HIP_TRY(s->d_order[slot].ensure(std::max<size_t>(1, all.size())));
       if (!all.empty())
         HIP_TRY(hipMemcpy(s->d_order[slot].p, all.data(), all.size() * sizeof(uint32_t),
