@@ -742,6 +742,9 @@ struct dq_state {
   std::vector<uint8_t> hll;
   int64_t rows = 0;
   bool host_dirty = false;   // host mirror newer than device (after merge / deserialize / reset)
+  // reset since the last scan: the next scan's finalize starts from the initial values instead of
+  // reading the device accumulators (dq_state_reset then queues no copies or memsets)
+  bool reset_pending = false;
   bool synced = true;        // host mirror reflects every scanned batch
   // pinned staging of the host mirror: resets upload it and syncs read it back with async copies
   // on the state's stream and one stream synchronisation, instead of pageable hipMemcpy calls
@@ -825,6 +828,7 @@ static dq_status pin_ensure(dq_state* s, size_t bytes) {
 
 static dq_status upload_host(dq_state* s) {
   if (!s->host_dirty || s->device < 0) return DQ_OK;
+  s->reset_pending = false;  // (the uploaded mirror is the device's base from here on)
   HIP_TRY(hipSetDevice(s->device));
   const size_t ab = s->acc.size() * sizeof(Acc), hb = s->hll.size();
   if (!s->stream_set) {  // no stream yet: blocking copies (the first scan may use any stream)
@@ -1026,6 +1030,13 @@ extern "C" dq_status dq_state_reset(dq_state* state) {
   if (!state) return fail(DQ_ERR_INVALID_ARGUMENT, "null state");
   if (state->stream_set && state->device >= 0) HIP_TRY(hipStreamSynchronize(state->stream));
   host_reset(state);
+  static const bool eager = getenv("DQ_EAGER_RESET") != nullptr;  // A/B hook
+  if (state->stream_set && state->device >= 0 && !eager) {
+    state->host_dirty = false;  // (the device words are ignored until the next scan rewrites them)
+    state->reset_pending = true;
+    state->rows_on_device = false;
+    return DQ_OK;
+  }
   return upload_host(state);
 }
 
@@ -1492,12 +1503,14 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
                            stream));
     HIP_TRY(launch_scan(s->d_tasks[slot].p, (int)n_desc, (int)plan->tasks.size(), launches.data(),
                         (int)launches.size(), plan->n_hll, s->d_queue.p, s->d_partial.p,
-                        s->d_partial2.p, s->d_hll_stage.p, s->d_acc.p, s->d_hll.p, stream));
+                        s->d_partial2.p, s->d_hll_stage.p, s->d_acc.p, s->d_hll.p, stream,
+                        s->reset_pending ? 1 : 0));
+    s->reset_pending = false;
+    s->synced = false;
   }
   HIP_TRY(hipEventRecord(s->ev[slot], stream));
   s->ev_used[slot] = true;
   s->rows += total_rows;
-  s->synced = false;
   return DQ_OK;
 }
 
@@ -1805,6 +1818,7 @@ extern "C" dq_status dq_state_exchange_unpack(dq_state* s, const int64_t* isum, 
   s->rows_on_device = true;
   s->synced = false;
   s->host_dirty = false;
+  s->reset_pending = false;
   return DQ_OK;
 }
 

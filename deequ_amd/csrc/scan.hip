@@ -1156,12 +1156,14 @@ __global__ void __launch_bounds__(kBlock) finalize1_kernel(const TaskDesc* __res
 
 // Stage 2: folds the kFinParts slice results (in order) into the running accumulator, merges the
 // HLL staging registers into the running registers (and clears them), and re-arms the queue.
+// reset: the state was reset since its last scan -- the running accumulator and registers start
+// from their initial values instead of being read (dq_state_reset queues no device work).
 __global__ void __launch_bounds__(64) finalize2_kernel(const TaskDesc* __restrict__ tasks, int n_desc,
                                                        const Acc* __restrict__ partial2,
                                                        Acc* __restrict__ acc,
                                                        uint32_t* __restrict__ hll_stage,
                                                        uint8_t* __restrict__ hll_acc,
-                                                       uint32_t* __restrict__ queue) {
+                                                       uint32_t* __restrict__ queue, int reset) {
   const int task = blockIdx.x;
   int64_t lo, hi;
   int kind, hll_out;
@@ -1169,7 +1171,7 @@ __global__ void __launch_bounds__(64) finalize2_kernel(const TaskDesc* __restric
   if (kind == TK_HLL) {
     for (int reg = threadIdx.x; reg < kHllM; reg += blockDim.x) {
       const int64_t i = (int64_t)hll_out * kHllM + reg;
-      const uint32_t m = hll_acc[i], v = hll_stage[i];
+      const uint32_t m = reset ? 0u : hll_acc[i], v = hll_stage[i];
       hll_acc[i] = (uint8_t)(v > m ? v : m);
       hll_stage[i] = 0;
     }
@@ -1183,7 +1185,9 @@ __global__ void __launch_bounds__(64) finalize2_kernel(const TaskDesc* __restric
       __syncthreads();
     }
     if (threadIdx.x == 0) {
-      Acc r = acc[task];
+      Acc r;
+      if (reset) acc_init(kind, r);
+      else r = acc[task];
       acc_merge(kind, r, sh2[0]);
       acc[task] = r;
     }
@@ -1242,7 +1246,8 @@ static int occupancy_of(int n_hll) {
 
 hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const ScanLaunch* launches,
                        int n_launches, int n_hll, uint32_t* queues, Acc* partial, Acc* partial2,
-                       uint32_t* hll_stage, Acc* acc, uint8_t* hll_acc, hipStream_t stream) {
+                       uint32_t* hll_stage, Acc* acc, uint8_t* hll_acc, hipStream_t stream,
+                       int reset) {
   if (n_desc == 0 || n_launches == 0) return hipSuccess;
   for (int k = 0; k < n_launches; ++k) {
     const ScanLaunch& L = launches[k];
@@ -1285,7 +1290,7 @@ hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const Sca
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(finalize2_kernel, dim3(n_tasks), dim3(64), 0, stream, tasks, n_desc, partial2,
-                     acc, hll_stage, hll_acc, queues);
+                     acc, hll_stage, hll_acc, queues, reset);
   return hipGetLastError();
 }
 
