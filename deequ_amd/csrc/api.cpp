@@ -723,8 +723,8 @@ extern "C" int dq_plan_launches_per_batch(const dq_plan* plan) {
     hll -= 1;
   }
   if (classes >= 2 && !getenv("DQ_NO_MIXED")) classes = 1;
-  // expression bitmaps + the scan launches + the two finalize launches
-  return (int)plan->mat.size() + classes + hll + (plan->tasks.empty() ? 0 : 2);
+  // expression bitmaps + the scan launches + the finalize launch
+  return (int)plan->mat.size() + classes + hll + (plan->tasks.empty() ? 0 : 1);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -756,6 +756,7 @@ struct dq_state {
   DevBuf<Acc> d_acc, d_partial, d_partial2;
   DevBuf<uint8_t> d_hll;
   DevBuf<uint32_t> d_hll_stage;  // per-launch HLL registers (u32), kept zero between launches
+  DevBuf<uint32_t> d_fin_arrivals;  // finalize: per task, its workgroups done (kept zero)
   DevBuf<int64_t> d_rows;        // the merged row count of an exchange (dq_state_exchange_unpack)
   DevBuf<int32_t> d_kinds;       // the plan's task kinds (the exchange kernels)
   hipEvent_t ev_xchg = nullptr;  // orders the exchange kernels and the collectives' stream
@@ -936,6 +937,8 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
   HIP_TRY(s->d_queue.ensure(kQueueWords));
   HIP_TRY(s->d_partial.ensure(1024));
   HIP_TRY(s->d_partial2.ensure(nt * (size_t)kFinParts));
+  HIP_TRY(s->d_fin_arrivals.ensure(nt));
+  HIP_TRY(hipMemset(s->d_fin_arrivals.p, 0, nt * sizeof(uint32_t)));
   for (int k = 0; k < 2; ++k) HIP_TRY(hipEventCreateWithFlags(&s->ev[k], hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&s->ev_xchg, hipEventDisableTiming));
   // expression programs and string pools
@@ -1503,8 +1506,8 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
                            stream));
     HIP_TRY(launch_scan(s->d_tasks[slot].p, (int)n_desc, (int)plan->tasks.size(), launches.data(),
                         (int)launches.size(), plan->n_hll, s->d_queue.p, s->d_partial.p,
-                        s->d_partial2.p, s->d_hll_stage.p, s->d_acc.p, s->d_hll.p, stream,
-                        s->reset_pending ? 1 : 0));
+                        s->d_partial2.p, s->d_hll_stage.p, s->d_acc.p, s->d_hll.p,
+                        s->d_fin_arrivals.p, stream, s->reset_pending ? 1 : 0));
     s->reset_pending = false;
     s->synced = false;
   }

@@ -182,8 +182,8 @@ constexpr int kMixedHllMax = 0;
 // clears them again).
 hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const ScanLaunch* launches,
                        int n_launches, int n_hll, uint32_t* queues, Acc* partial, Acc* partial2,
-                       uint32_t* hll_stage, Acc* acc, uint8_t* hll_acc, hipStream_t stream,
-                       int reset = 0);
+                       uint32_t* hll_stage, Acc* acc, uint8_t* hll_acc, uint32_t* arrivals,
+                       hipStream_t stream, int reset = 0);
 size_t scan_lds_bytes(int body, int n_hll);
 int scan_max_blocks_per_cu(int body, int n_hll);
 // Per column of a plan: 0 not read, 1 validity bitmap only, 2 every buffer (api.cpp).

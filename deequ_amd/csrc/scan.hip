@@ -1127,73 +1127,92 @@ DQ_DEV void task_range_block(const TaskDesc* tasks, int n_desc, int task, int64_
   __syncthreads();  // (the shared cells may be reused by a later call)
 }
 
-// Stage 1: workgroup (task, f) merges slice f of the task's item partials; thread i takes items
-// i, i + 256, ... of the slice in order, then a fixed tree.
-__global__ void __launch_bounds__(kBlock) finalize1_kernel(const TaskDesc* __restrict__ tasks,
-                                                           int n_desc,
-                                                           const Acc* __restrict__ partial,
-                                                           Acc* __restrict__ partial2) {
-  __shared__ Acc sh[kBlock];
+// acc_merge over the wave, lane i with lane i + s for s = 32, 16, ..., 1 (a fixed tree); the
+// wave's result in lane 0.  Shuffles, no LDS and no barriers.
+DQ_DEV void wave_merge_tree(int kind, Acc& a) {
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    Acc b;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) b.i[k] = __shfl_down(a.i[k], s);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) b.d[k] = __shfl_down(a.d[k], s);
+    if (lane_id() < s) acc_merge(kind, a, b);
+  }
+}
+
+// The finalize: workgroup (task, f) merges slice f of the task's item partials -- thread i takes
+// items i, i + kBlock, ... of the slice in order, then a fixed tree (each wave by shuffles, then
+// the waves in order) -- into partial2[task][f]; the LAST workgroup of a task to finish (an arrival
+// counter, left at zero for the next launch) folds the kFinParts slices in a fixed tree into the
+// running accumulator (reset: from the initial values, dq_state_reset queues no device work).
+// HLL tasks: slice 0 merges the staging registers into the running registers and clears them.
+// Workgroup (0, 0) re-arms the scan queues.  One launch (the two-launch form spent ~26 us per
+// S10 step, most of it in an 8-level LDS tree with a barrier per level).
+__global__ void __launch_bounds__(kBlock) finalize_kernel(const TaskDesc* __restrict__ tasks,
+                                                          int n_desc,
+                                                          const Acc* __restrict__ partial,
+                                                          Acc* __restrict__ partial2,
+                                                          Acc* __restrict__ acc,
+                                                          uint32_t* __restrict__ hll_stage,
+                                                          uint8_t* __restrict__ hll_acc,
+                                                          uint32_t* __restrict__ queue,
+                                                          uint32_t* __restrict__ arrivals, int reset) {
+  __shared__ Acc sh[kBlock / 64];
+  __shared__ Acc sh2[kFinParts];
+  __shared__ uint32_t s_last;
   const int task = blockIdx.x, f = blockIdx.y;
   int64_t lo, hi;
   int kind, hll_out;
   task_range_block(tasks, n_desc, task, lo, hi, kind, hll_out);
-  Acc a;
-  acc_init(kind, a);
-  if (kind != TK_HLL) {
-    const int64_t m = hi - lo;
-    const int64_t b = lo + m * f / kFinParts, e = lo + m * (f + 1) / kFinParts;
-    for (int64_t i = b + threadIdx.x; i < e; i += kBlock) acc_merge(kind, a, partial[i]);
-  }
-  sh[threadIdx.x] = a;
-  __syncthreads();
-  for (int s = kBlock / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) acc_merge(kind, sh[threadIdx.x], sh[threadIdx.x + s]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) partial2[(int64_t)task * kFinParts + f] = sh[0];
-}
-
-// Stage 2: folds the kFinParts slice results (in order) into the running accumulator, merges the
-// HLL staging registers into the running registers (and clears them), and re-arms the queue.
-// reset: the state was reset since its last scan -- the running accumulator and registers start
-// from their initial values instead of being read (dq_state_reset queues no device work).
-__global__ void __launch_bounds__(64) finalize2_kernel(const TaskDesc* __restrict__ tasks, int n_desc,
-                                                       const Acc* __restrict__ partial2,
-                                                       Acc* __restrict__ acc,
-                                                       uint32_t* __restrict__ hll_stage,
-                                                       uint8_t* __restrict__ hll_acc,
-                                                       uint32_t* __restrict__ queue, int reset) {
-  const int task = blockIdx.x;
-  int64_t lo, hi;
-  int kind, hll_out;
-  task_range_block(tasks, n_desc, task, lo, hi, kind, hll_out);
+  if (task == 0 && f == 0)
+    for (int i = threadIdx.x; i < kQueues * kQueueHeads; i += blockDim.x) queue[i * kQueueStride] = 0u;
   if (kind == TK_HLL) {
+    if (f != 0) return;
     for (int reg = threadIdx.x; reg < kHllM; reg += blockDim.x) {
       const int64_t i = (int64_t)hll_out * kHllM + reg;
       const uint32_t m = reset ? 0u : hll_acc[i], v = hll_stage[i];
       hll_acc[i] = (uint8_t)(v > m ? v : m);
       hll_stage[i] = 0;
     }
-  } else if (kind != 0) {  // (block-uniform) the slices in a fixed tree, then into the running
-    __shared__ Acc sh2[kFinParts];  // accumulator: parallel, and the same order on every run
-    static_assert(kFinParts <= 64 && (kFinParts & (kFinParts - 1)) == 0, "one wave, power of 2");
-    if (threadIdx.x < kFinParts) sh2[threadIdx.x] = partial2[(int64_t)task * kFinParts + threadIdx.x];
-    __syncthreads();
-    for (int s = kFinParts / 2; s > 0; s >>= 1) {
-      if (threadIdx.x < s) acc_merge(kind, sh2[threadIdx.x], sh2[threadIdx.x + s]);
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      Acc r;
-      if (reset) acc_init(kind, r);
-      else r = acc[task];
-      acc_merge(kind, r, sh2[0]);
-      acc[task] = r;
-    }
+    return;
   }
-  if (task == 0)
-    for (int i = threadIdx.x; i < kQueues * kQueueHeads; i += blockDim.x) queue[i * kQueueStride] = 0u;
+  if (kind == 0) return;  // (block-uniform: a task without descriptors)
+  Acc a;
+  acc_init(kind, a);
+  const int64_t m = hi - lo;
+  const int64_t b = lo + m * f / kFinParts, e = lo + m * (f + 1) / kFinParts;
+  for (int64_t i = b + threadIdx.x; i < e; i += kBlock) acc_merge(kind, a, partial[i]);
+  wave_merge_tree(kind, a);
+  const int wave = threadIdx.x >> 6;
+  if (lane_id() == 0) sh[wave] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Acc r = sh[0];
+    for (int w = 1; w < kBlock / 64; ++w) acc_merge(kind, r, sh[w]);
+    partial2[(int64_t)task * kFinParts + f] = r;
+    __threadfence();  // the slice is visible before the arrival
+    s_last = atomicAdd(&arrivals[task], 1u) == (uint32_t)(kFinParts - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the task's last workgroup: the kFinParts slices in a fixed tree, into the accumulator
+  __threadfence();
+  static_assert(kFinParts <= kBlock && (kFinParts & (kFinParts - 1)) == 0, "power of 2");
+  if (threadIdx.x < kFinParts) sh2[threadIdx.x] = partial2[(int64_t)task * kFinParts + threadIdx.x];
+  __syncthreads();
+  for (int s2 = kFinParts / 2; s2 > 0; s2 >>= 1) {
+    if (threadIdx.x < s2) acc_merge(kind, sh2[threadIdx.x], sh2[threadIdx.x + s2]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    Acc r;
+    if (reset) acc_init(kind, r);
+    else r = acc[task];
+    acc_merge(kind, r, sh2[0]);
+    acc[task] = r;
+    arrivals[task] = 0u;  // (for the next launch)
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1246,8 +1265,8 @@ static int occupancy_of(int n_hll) {
 
 hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const ScanLaunch* launches,
                        int n_launches, int n_hll, uint32_t* queues, Acc* partial, Acc* partial2,
-                       uint32_t* hll_stage, Acc* acc, uint8_t* hll_acc, hipStream_t stream,
-                       int reset) {
+                       uint32_t* hll_stage, Acc* acc, uint8_t* hll_acc, uint32_t* arrivals,
+                       hipStream_t stream, int reset) {
   if (n_desc == 0 || n_launches == 0) return hipSuccess;
   for (int k = 0; k < n_launches; ++k) {
     const ScanLaunch& L = launches[k];
@@ -1285,12 +1304,8 @@ hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const Sca
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(finalize1_kernel, dim3(n_tasks, kFinParts), dim3(kBlock), 0, stream, tasks,
-                     n_desc, partial, partial2);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(finalize2_kernel, dim3(n_tasks), dim3(64), 0, stream, tasks, n_desc, partial2,
-                     acc, hll_stage, hll_acc, queues, reset);
+  hipLaunchKernelGGL(finalize_kernel, dim3(n_tasks, kFinParts), dim3(kBlock), 0, stream, tasks,
+                     n_desc, partial, partial2, acc, hll_stage, hll_acc, queues, arrivals, reset);
   return hipGetLastError();
 }
 

@@ -64,8 +64,8 @@ def test_s10_plan_fuses_into_four_tasks_and_two_launches():
     assert text.count("task[") == 4, text
     assert "numeric col=3" in text and "str_in col=2" in text
     # ONE mixed scan launch for the three body classes (validity, numeric int64, string IN) + the
-    # two finalize launches
-    assert plan.launches_per_batch == 3
+    # finalize launch
+    assert plan.launches_per_batch == 2
 
 
 def test_where_filters_materialise_once_per_distinct_expression():

@@ -37,6 +37,17 @@ all)
   DQ_FREQ_PARTITION_TARGET=3800 timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_t3800_$T.json 2>&1 &&
   DQ_TAIL_SPLIT=0 timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 10 --warmup 3 > $O/wl_c4_notail_$T.json 2>&1
   ;;
+ab)
+  timeout -k 10 800 $PYT tests -m gpu > $O/gpu_tests_$T.log 2>&1 || exit 1
+  for k in 1 2; do
+    DQ_TAIL_SPLIT=0 timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-h2d > $O/bench_notail${k}_$T.json 2>&1 &&
+    timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-h2d > $O/bench_tail${k}_$T.json 2>&1 &&
+    DQ_EAGER_RESET=1 timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-h2d > $O/bench_eager${k}_$T.json 2>&1 || exit 1
+  done
+  DQ_HLL_FROM_TABLE=0 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_nohll_$T.json 2>&1 &&
+  timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_$T.json 2>&1 &&
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1
+  ;;
 wl)
   timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
   timeout -k 10 300 python -u tools/bench_workloads.py c4 --steps 10 --warmup 3 > $O/wl_c4_$T.json 2>&1 &&
