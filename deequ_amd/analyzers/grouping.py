@@ -76,13 +76,13 @@ class FrequencyTable:
         N.check(N.lib.dq_freq_num_groups(self.handle, ctypes.byref(n)))
         return int(n.value)
 
-    def hll_words(self, max_groups: int):
+    def hll_words(self, max_records: int):
         """ApproxCountDistinct's 52 register words (signed, as the scan's state holds them) from
-        this one-column table's groups (dq_freq_hll), or None when it has more than max_groups
-        groups or is not a one-column table: the caller scans the rows instead."""
+        this one-column table's partitioned records (dq_freq_hll), or None when it holds more
+        than max_records or is not a one-column table: the caller scans the rows instead."""
         words = (ctypes.c_uint64 * 52)()
         done = ctypes.c_int()
-        N.check(N.lib.dq_freq_hll(self.handle, int(max_groups), words, ctypes.byref(done), None))
+        N.check(N.lib.dq_freq_hll(self.handle, int(max_records), words, ctypes.byref(done), None))
         if not done.value:
             return None
         return tuple(int(w) - (1 << 64) if w >= (1 << 63) else int(w) for w in words)

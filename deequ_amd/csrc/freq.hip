@@ -5912,74 +5912,85 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
   return res;
 }
 
-// ---- HLL++ registers from a table's groups (ApproxCountDistinct beside a grouping) -------------
+// ---- HLL++ registers from a table's records (ApproxCountDistinct beside a grouping) ------------
 // The registers depend only on the set of distinct non-NULL values (StatefulHyperloglogPlus.scala:
-// 87-113: each value's XXH64, seed 42, raises one register; merges take the max), so a table that
-// holds every distinct value once yields them without a pass over the rows: each group's value
-// (exact mode: the bijective hash inverted; one utf8 key: its arena bytes) is hashed as Spark hashes
-// its type -- floating-point NaN canonical (doubleToLongBits / floatToIntBits), integers narrower
-// than long as Int -- and raises its register.
-__global__ void __launch_bounds__(256) freq_hll_groups(const Group* __restrict__ g, int64_t n, int exact,
-                                                       int type, const uint8_t* __restrict__ arena,
-                                                       uint32_t* __restrict__ regs) {
+// 87-113: each value's XXH64, seed 42, raises one register; merges take the max), and raising a
+// register twice changes nothing, so the table's partitioned records -- every distinct value at
+// least once, fewer records than rows once phase A has collapsed repeated keys -- yield them
+// without a pass over the rows and without counting the groups: each record's value (exact mode:
+// the bijective hash, its bucket bits from the record's partition, inverted; one utf8 key: its
+// arena bytes) is hashed as Spark hashes its type -- floating-point NaN canonical
+// (doubleToLongBits / floatToIntBits), integers narrower than long as Int -- and raises its
+// register.  One wave per partition.
+DQ_DEV uint64_t hll_value_hash(uint64_t v, int type) {  // v: the widened value (kwiden)
+  switch (type) {
+    case DQ_INT64: return xxh_long(v, 42);
+    case DQ_FLOAT64: {
+      const bool nan = (v & 0x7fffffffffffffffULL) > 0x7ff0000000000000ULL;
+      return xxh_long(nan ? 0x7ff8000000000000ULL : v, 42);
+    }
+    case DQ_FLOAT32: {
+      const uint32_t b = (uint32_t)v;
+      return xxh_int((b & 0x7fffffffu) > 0x7f800000u ? 0x7fc00000u : b, 42);
+    }
+    default: return xxh_int((uint32_t)v, 42);  // int8 / int16 / int32 / boolean (0 / 1)
+  }
+}
+
+__global__ void __launch_bounds__(256) freq_hll_records(const uint64_t* __restrict__ recs,
+                                                        const unsigned long long* __restrict__ part_base,
+                                                        int64_t P, int s, int exact, int type,
+                                                        const uint8_t* __restrict__ arena,
+                                                        uint32_t* __restrict__ regs) {
   __shared__ uint32_t s_reg[kHllM];
   for (int i = threadIdx.x; i < kHllM; i += 256) s_reg[i] = 0;
   __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    uint64_t x;
-    if (exact) {
-      const uint64_t v = fmix_inv(g[i].h);  // the widened value (kwiden, exact_canon)
-      switch (type) {
-        case DQ_INT64: x = xxh_long(v, 42); break;
-        case DQ_FLOAT64: {
-          const bool nan = (v & 0x7fffffffffffffffULL) > 0x7ff0000000000000ULL;
-          x = xxh_long(nan ? 0x7ff8000000000000ULL : v, 42);
-          break;
-        }
-        case DQ_FLOAT32: {
-          const uint32_t b = (uint32_t)v;
-          x = xxh_int((b & 0x7fffffffu) > 0x7f800000u ? 0x7fc00000u : b, 42);
-          break;
-        }
-        default: x = xxh_int((uint32_t)v, 42); break;  // int8 / int16 / int32 / boolean (0 / 1)
+  const int lane = (int)__lane_id(), wave = threadIdx.x >> 6;
+  for (int64_t p = (int64_t)blockIdx.x * 4 + wave; p < P; p += (int64_t)gridDim.x * 4) {
+    const uint64_t r0 = part_base[p], r1 = part_base[p + 1];
+    const uint32_t b = (uint32_t)(p >> s);
+    for (uint64_t i = r0 + lane; i < r1; i += 64) {
+      uint64_t x;
+      if (exact) {
+        x = hll_value_hash(fmix_inv(xrec_h(recs[i], b)), type);
+      } else {  // one utf8 key: the encoded {1, len, bytes}
+        const uint32_t* e = reinterpret_cast<const uint32_t*>(arena + (recs[2 * i + 1] >> 8));
+        x = xxh_bytes(MemBytes{reinterpret_cast<const uint8_t*>(e + 2)}, (int64_t)e[1], 42);
       }
-    } else {  // one utf8 key: the encoded {1, len, bytes}
-      const uint32_t* e = reinterpret_cast<const uint32_t*>(arena + g[i].rep);
-      x = xxh_bytes(MemBytes{reinterpret_cast<const uint8_t*>(e + 2)}, (int64_t)e[1], 42);
+      uint32_t idx, pw;
+      hll_index_rank(x, idx, pw);
+      if (pw > __hip_atomic_load(&s_reg[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+        atomicMax(&s_reg[idx], pw);
     }
-    uint32_t idx, pw;
-    hll_index_rank(x, idx, pw);
-    if (pw > __hip_atomic_load(&s_reg[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-      atomicMax(&s_reg[idx], pw);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kHllM; i += 256)
     if (s_reg[i]) atomicMax(&regs[i], s_reg[i]);
 }
 
-extern "C" dq_status dq_freq_hll(dq_freq* f, int64_t max_groups, uint64_t* words, int* done,
+extern "C" dq_status dq_freq_hll(dq_freq* f, int64_t max_records, uint64_t* words, int* done,
                                  void* hip_stream) {
   if (!f || !words || !done) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   *done = 0;
   if (f->n_keys != 1 || (!f->exact && f->types[0] != DQ_UTF8)) return DQ_OK;  // (not one value)
   HIP_TRY(hipSetDevice(f->device));
   if (hip_stream) f->stream = reinterpret_cast<hipStream_t>(hip_stream);
-  dq_status st = finalize_c(f, false, false);
+  dq_status st = finalize_b(f);
   if (st != DQ_OK) return st;
-  if ((int64_t)f->st_groups > max_groups) return DQ_OK;  // (the caller scans the rows instead)
-  st = compact_groups(f);
-  if (st != DQ_OK) return st;
+  if ((int64_t)f->R > max_records) return DQ_OK;  // (the caller scans the rows instead)
   DevBuf<uint32_t> regs;
   HIP_TRY(regs.ensure(kHllM));
   HIP_TRY(hipMemsetAsync(regs.p, 0, kHllM * 4, f->stream));
-  if (f->n_compact > 0) {
-    const unsigned grid = (unsigned)std::min<int64_t>((f->n_compact + 255) / 256, 1024);
-    hipLaunchKernelGGL(freq_hll_groups, dim3(grid), dim3(256), 0, f->stream, f->compact.p, f->n_compact,
+  if (f->R > 0) {
+    const int64_t P = (int64_t)kBuckets << f->s_bits;
+    const unsigned grid = (unsigned)std::min<int64_t>((P + 3) / 4, 2048);
+    hipLaunchKernelGGL(freq_hll_records, dim3(grid), dim3(256), 0, f->stream,
+                       reinterpret_cast<const uint64_t*>(f->recsB.p), f->part_base.p, P, f->s_bits,
                        f->exact ? 1 : 0, f->types[0], arena_of(f), regs.p);
     HIP_TRY(hipGetLastError());
   }
   uint32_t r[kHllM];
-  HIP_TRY(d2h(r, regs.p, sizeof(r), f->stream));
+  HIP_TRY(d2h(r, regs.p, sizeof(r), f->stream));  // (regs dies here)
   for (int w = 0; w < kHllWords; ++w) {  // StatefulHyperloglogPlus's 52-word layout
     uint64_t v = 0;
     for (int i = 0; i < kHllRegsPerWord; ++i) {

@@ -277,11 +277,12 @@ def _histogram_and_grouping_job(data, col, hists, group, aggregate_with, save_st
     return _histogram_and_grouping_host(st)
 
 
-# A column's ApproxCountDistinct is taken from its Histogram table (not scanned) when the table
-# has at most this many groups per row, and at most kHllTableMaxGroups: the groups are hashed on
-# the device (dq_freq_hll), a few per thousand rows instead of every row.
-kHllTableGroupsPerRow = 1.0 / 64
-kHllTableMaxGroups = 1 << 22
+# A column's ApproxCountDistinct is taken from its Histogram table (not scanned) when phase A
+# collapsed the column's repeated keys to at most this many partitioned records per row: the
+# records are hashed on the device (dq_freq_hll) instead of the rows.  Measured on configs[4]
+# (DESIGN.md §4.1): a table with a record per row (id, score) took 1.6 ms to hash its 125 M
+# records, while the fused scan, bound by its string columns, ran no faster without the column.
+kHllTableRecordsPerRow = 1.0 / 64
 
 
 def _hll_table_columns(shareable, hist_cols, aggregate_with, save_states_with, data) -> set:
@@ -298,12 +299,12 @@ def _hll_table_columns(shareable, hist_cols, aggregate_with, save_states_with, d
 
 
 def _hll_from_table(st, hll_words) -> None:
-    """The Histogram table's HLL registers into hll_words[col] when it has few groups."""
+    """The Histogram table's HLL registers into hll_words[col] when it has few records."""
     hs, col = st[6], st[1]
     if hs is None or hll_words is None:
         return
-    rows = max(1, int(hs.num_rows))
-    cap = min(kHllTableMaxGroups, int(rows * kHllTableGroupsPerRow))
+    per_row = float(os.environ.get("DQ_HLL_TABLE_RECORDS_PER_ROW", kHllTableRecordsPerRow))
+    cap = int(max(1, int(hs.num_rows)) * per_row)
     try:
         words = hs.frequencies.hll_words(cap)
     except Exception:  # noqa: BLE001  (the scan computes it instead)

@@ -373,11 +373,12 @@ dq_status dq_freq_marginal(dq_freq* joint, int key_index, dq_freq* out, void* hi
 dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int* is_null, void* hip_stream);
 
 /* ApproxCountDistinct's 52 register words (StatefulHyperloglogPlus.scala:87-113 layout) from a
- * one-column table's groups, when it has at most max_groups of them: the registers depend only on
- * the set of distinct non-NULL values, so a table already built for a grouping or Histogram of
- * the column yields them without a pass over the rows.  *done = 0 (words untouched) when the
- * table has more groups, or is not a one-column fixed-width / utf8 table; the caller then scans. */
-dq_status dq_freq_hll(dq_freq* table, int64_t max_groups, uint64_t* words, int* done,
+ * one-column table's partitioned records, when it holds at most max_records of them: the
+ * registers depend only on the set of distinct non-NULL values, so a table already built for a
+ * grouping or Histogram of the column yields them without a pass over the rows (its records are
+ * fewer than the rows once repeated keys collapsed).  *done = 0 (words untouched) when the table
+ * has more records, or is not a one-column fixed-width / utf8 table; the caller then scans. */
+dq_status dq_freq_hll(dq_freq* table, int64_t max_records, uint64_t* words, int* done,
                       void* hip_stream);
 
 /* Number of groups currently in the table (NULL group and every distinct key). */

@@ -1,7 +1,7 @@
-"""ApproxCountDistinct's HLL++ registers from a frequency table's groups (dq_freq_hll; the runner
+"""ApproxCountDistinct's HLL++ registers from a frequency table's records (dq_freq_hll; the runner
 takes them from a column's Histogram table instead of scanning it).  The
 registers depend only on the set of distinct non-NULL values (StatefulHyperloglogPlus.scala:87-113),
-so the table's groups must give the scan's register words bit for bit, for every key type: the
+so the table's records (each distinct value at least once) must give the scan's register words bit for bit, for every key type: the
 exact-mode values recovered from the bijective hash (int8..int64, boolean, float32 / float64 with
 NaN payloads, -0.0 and infinities -- Spark hashes doubleToLongBits / floatToIntBits), and utf8
 keys from the arena (empty strings, a real "NullValue", multibyte characters)."""
@@ -59,33 +59,37 @@ def test_table_registers_equal_the_scan(null_as_group, gpu_device):
         assert words == tuple(scan.words), c
         assert [w & ((1 << 64) - 1) for w in words] == \
             [w & ((1 << 64) - 1) for w in O.agg_hll(ot, c, None)], c
-        assert ft.hll_words(1) is None  # more groups than allowed: the caller scans
+        assert ft.hll_words(1) is None  # more records than allowed: the caller scans
 
 
 def test_runner_takes_registers_from_histogram_tables(gpu_device, monkeypatch):
     """AnalysisRunner over ApproxCountDistinct + Histogram of low-cardinality columns: the same
     metrics with the registers from the Histogram tables as with the scan (DQ_HLL_FROM_TABLE=0),
-    and a high-cardinality column keeps its scan."""
+    and high-cardinality columns keep their scan (a record per row: hashing the records would
+    cost as much as the scan)."""
     from deequ_amd.analyzers import ApproxCountDistinct, Histogram, Uniqueness
     from deequ_amd.runners import AnalysisRunner
     from deequ_amd.table import Table
     cols = _columns(70_001, 8)
     cols["hi"] = pa.array(np.arange(70_001, dtype=np.int64))
+    cols["hs"] = pa.array([f"key {i}" for i in range(70_001)])
     df = Table.from_arrow(pa.table(cols), device=gpu_device, max_batch_rows=30_000)
-    names = ["i64", "i32", "b", "s", "hi"]
+    names = ["i64", "i32", "b", "s", "hi", "hs"]
     suite = [a for c in names for a in (ApproxCountDistinct(c), Histogram(c), Uniqueness([c]))]
     from deequ_amd.analyzers.grouping import FrequencyTable
     from deequ_amd.metrics import Distribution
     taken = {}
     orig = FrequencyTable.hll_words
 
-    def spy(self, max_groups):  # which tables gave their registers
-        w = orig(self, max_groups)
+    def spy(self, max_records):  # which tables gave their registers
+        w = orig(self, max_records)
         taken[self.key_columns[0]] = w is not None
         return w
     monkeypatch.setattr(FrequencyTable, "hll_words", spy)
     got = AnalysisRunner.do_analysis_run(df, suite)
-    assert taken == {"i64": True, "i32": True, "b": True, "s": True, "hi": False}, taken
+    # low-cardinality tables collapse to a few records (the small-key path: one per group);
+    # a record per row keeps the scan
+    assert taken["b"] and taken["s"] and not taken["hi"] and not taken["hs"], taken
     monkeypatch.setenv("DQ_HLL_FROM_TABLE", "0")
     ref = AnalysisRunner.do_analysis_run(df, suite)
 

@@ -9,6 +9,7 @@
 #              configs[2] / [3] lines.
 #  PART=wl:    configs[2] / [3] / [4] lines (tools/bench_workloads.py).
 #  PART=c3:    configs[2] line, its rocprof kernel stats and PMC passes (tools/gpu_pmc_c3.sh).
+#  PART=hll:   the HLL-from-table tests, configs[4] with and without it.
 #  PART=c5:    configs[4] line and its rocprof kernel stats.
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
@@ -57,6 +58,13 @@ c3)
   timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_$T -o run -- python3 tools/bench_workloads.py c3 --steps 2 > $O/prof_c3_$T.log 2>&1 &&
   TAG=$T bash tools/gpu_pmc_c3.sh
+  ;;
+hll)
+  timeout -k 10 300 $PYT tests/test_gpu_hll_tables.py tests/test_gpu_determinism.py > $O/gpu_tests_$T.log 2>&1 &&
+  DQ_HLL_FROM_TABLE=0 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_nohll_$T.json 2>&1 &&
+  timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_$T.json 2>&1 &&
+  DQ_HLL_TABLE_RECORDS_PER_ROW=1 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_q_$T.json 2>&1 &&
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1
   ;;
 c5)
   timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_$T.json 2>&1 &&
