@@ -266,7 +266,7 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": b_alg,
                 "scan_ms": scan_ms,
-                "kernel": "dq::scan_mixed_kernel (+ finalize1/finalize2)",
+                "kernel": "dq::scan_mixed_kernel (+ finalize_kernel)",
                 "scan_code_object_sha": scan_code_object_hash(),
             },
         }
