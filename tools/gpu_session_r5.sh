@@ -9,6 +9,7 @@
 #              configs[2] / [3] lines.
 #  PART=wl:    configs[2] / [3] / [4] lines (tools/bench_workloads.py).
 #  PART=c3:    configs[2] line, its rocprof kernel stats and PMC passes (tools/gpu_pmc_c3.sh).
+#  PART=s10ab: parity tests, then scan ablation + bench of this build against the build at $VAR.
 #  PART=hll:   the HLL-from-table tests, configs[4] with and without it.
 #  PART=c5:    configs[4] line and its rocprof kernel stats.
 set -o pipefail
@@ -58,6 +59,18 @@ c3)
   timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3_$T -o run -- python3 tools/bench_workloads.py c3 --steps 2 > $O/prof_c3_$T.log 2>&1 &&
   TAG=$T bash tools/gpu_pmc_c3.sh
+  ;;
+s10ab)
+  # A/B of a scan-body variant built at $VAR (DQ_LIB_PATH: diagnostic builds only)
+  timeout -k 10 300 $PYT tests/test_gpu_parity.py tests/test_gpu_configs4.py tests/test_gpu_freq.py > $O/gpu_tests_$T.log 2>&1 &&
+  timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_new_$T.json 2>&1 &&
+  DQ_LIB_PATH=$VAR timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_var_$T.json 2>&1 &&
+  for k in 1 2; do
+    timeout -k 10 200 python -u tools/scan_ablation.py > $O/abl_new${k}_$T.log 2>&1 &&
+    DQ_LIB_PATH=$VAR timeout -k 10 200 python -u tools/scan_ablation.py > $O/abl_var${k}_$T.log 2>&1 &&
+    timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-h2d > $O/bench_new${k}_$T.json 2>&1 &&
+    DQ_LIB_PATH=$VAR timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-h2d > $O/bench_var${k}_$T.json 2>&1 || exit 1
+  done
   ;;
 hll)
   timeout -k 10 300 $PYT tests/test_gpu_hll_tables.py tests/test_gpu_determinism.py > $O/gpu_tests_$T.log 2>&1 &&
