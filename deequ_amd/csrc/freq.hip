@@ -273,6 +273,11 @@ struct AArgs {
   const uint32_t* ptot;  // [kBuckets]: the batch's rows per bucket
   uint32_t* pstart;      // [n_wg][kBuckets]
   uint32_t* plen;        // [n_wg][kBuckets]
+  // dense integer keys (freq_dense_count / freq_dense_emit; nullptr: not tried for this batch):
+  // {max, ~min} of the keyed values (sign-flipped, so unsigned order is signed order; 0 = none),
+  // the epoch of the last batch the dense path took, the epoch of the last one it declined
+  unsigned long long* dense_words;
+  uint64_t dense_epoch;
 };
 
 // Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
@@ -1084,6 +1089,10 @@ DQ_DEV uint64_t kload_at(const void* v, int64_t base, int r) {
   }
 }
 constexpr int kPreThreads = 1024;
+constexpr uint64_t kDenseSign = 1ULL << 63;
+// DENSE: also the batch's key range for the dense path (a second instantiation: the range's
+// registers cost the plain pre-pass a wave per SIMD)
+template <bool DENSE>
 __global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t* ph) {
   constexpr int ROUNDS = FM<false>::kTile / kPreThreads;
   __shared__ uint32_t bh[kBuckets];
@@ -1095,6 +1104,7 @@ __global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t*
   const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
   const int64_t t1 = min(t0 + (int64_t)a.tiles_per_wg, n_tiles);
   const bool full_ok = (reinterpret_cast<uintptr_t>(c.valid) & 7u) == 0 && (a.tile_items & 63) == 0;
+  uint64_t umax = 0, umin = ~0ULL;  // the keyed values' range, sign-flipped (dense path)
   auto tile_loop = [&](auto type_tag) {
     constexpr int TY = decltype(type_tag)::value;
     for (int64_t t = t0; t < t1; ++t) {
@@ -1136,7 +1146,14 @@ __global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t*
       }
 #pragma unroll
       for (int j = 0; j < ROUNDS; ++j)
-        if ((ok & vb) >> j & 1u) atomicAdd(&bh[bucket_of(fmix_bij(exact_canon(a.ks, v[j])))], 1u);
+        if ((ok & vb) >> j & 1u) {
+          atomicAdd(&bh[bucket_of(fmix_bij(exact_canon(a.ks, v[j])))], 1u);
+          if constexpr (DENSE) {
+            const uint64_t u = v[j] ^ kDenseSign;  // (integer keys: the widened value)
+            umax = u > umax ? u : umax;
+            umin = u < umin ? u : umin;
+          }
+        }
     }
   };
   switch (c.type) {  // block-uniform: one unrolled load loop per width
@@ -1148,7 +1165,24 @@ __global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t*
     case DQ_BOOL: tile_loop(std::integral_constant<int, DQ_BOOL>{}); break;
     default: tile_loop(std::integral_constant<int, DQ_INT64>{}); break;
   }
+  // the batch's key range for the dense path: waves -> LDS -> one global atomic per workgroup
+  // (per wave, ~15 K same-address atomics per batch serialised in L2: +40 % on this kernel)
+  __shared__ unsigned long long s_mm[2];
+  if (DENSE) {
+    if (tid < 2) s_mm[tid] = 0;
+    __syncthreads();
+    umax = __ockl_wfred_max_u64(umax);
+    umin = ~__ockl_wfred_max_u64(~umin);
+    if (__lane_id() == 0 && umin <= umax) {  // (a wave without keyed rows: umin > umax)
+      atomicMax(&s_mm[0], (unsigned long long)umax);
+      atomicMax(&s_mm[1], (unsigned long long)~umin);
+    }
+  }
   __syncthreads();
+  if (DENSE && tid == 0 && s_mm[0] | s_mm[1]) {
+    atomicMax(&a.dense_words[0], s_mm[0]);
+    atomicMax(&a.dense_words[1], s_mm[1]);
+  }
   for (int i = tid; i < kBuckets; i += kPreThreads) ph[(int64_t)blockIdx.x * kBuckets + i] = bh[i];
 }
 
@@ -1176,6 +1210,12 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
   __shared__ uint32_t s_hits, s_bypass, s_full;
   __shared__ unsigned long long s_maxcnt;
   const int tid = threadIdx.x;
+  if (a.dense_words && __hip_atomic_load(&a.dense_words[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                           a.dense_epoch) {  // the dense path took the batch: empty pieces
+    a.pstart[(int64_t)blockIdx.x * kBuckets + tid] = 0;
+    a.plen[(int64_t)blockIdx.x * kBuckets + tid] = 0;
+    return;
+  }
   const KeyCol& c = a.ks.cols[0];
   const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
   const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
@@ -1351,6 +1391,159 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
   wave_count(&a.counters[C_NULL_GROUP], nullg);
   wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
   if (tid == 0 && s_full) atomicAdd(&a.counters[C_DBG_FULL], (unsigned long long)s_full);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Phase A, dense integer keys: a batch of an integer (or boolean) key whose keyed values span
+// fewer than kDenseW consecutive values (the pre-pass measured the range: numViews, status codes,
+// years -- low-cardinality columns the bucket pieces would write a record per row for) is counted
+// by value in LDS instead: freq_dense_count adds each row to its value's counter (one LDS add,
+// no hash, no sort) and writes each workgroup's counters; freq_dense_emit sums them per value and
+// writes one record per nonzero count digit, bucket-sorted in the batch's first chunks -- the
+// chunk layout phase A leaves for collapsed keys, so phases B and C see a few records per value
+// instead of one per row.  A wider batch is declined (both kernels return at once) and
+// freq_phaseA_xp does it; when the dense path takes it, freq_phaseA_xp leaves empty pieces.
+// ------------------------------------------------------------------------------------------------
+constexpr int kDenseW = 1 << 15;   // values counted per batch (128 KiB of LDS counters)
+constexpr int kDenseV = 512;       // values per emitted chunk (<= 16 digits each: <= kTile records)
+constexpr int kDenseSumV = 128;    // values per summing workgroup (four threads each)
+constexpr int kDenseThreads = 1024;
+constexpr int kDenseBlocks = 256;  // counting workgroups (one per CU): their counter rows
+
+// The batch's window, or false (declined): the keyed values' range fits kDenseW and the
+// emitting chunks fit the batch's chunk slots (tiles + workgroup chunks).
+DQ_DEV bool dense_window(const AArgs& a, uint64_t& lo, uint32_t& nvals) {
+  const uint64_t mxe = __hip_atomic_load(&a.dense_words[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t mne = ~__hip_atomic_load(&a.dense_words[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (mxe < mne || mxe - mne >= (uint64_t)kDenseW) return false;  // (no keyed row / too wide)
+  nvals = (uint32_t)(mxe - mne) + 1u;
+  const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
+  const int64_t chunks = n_tiles + (n_tiles + a.tiles_per_wg - 1) / a.tiles_per_wg;
+  if ((int64_t)((nvals + kDenseV - 1) / kDenseV) > chunks) return false;
+  lo = mne ^ kDenseSign;  // the smallest keyed value (widened)
+  return true;
+}
+
+template <int TY>
+__global__ void __launch_bounds__(kDenseThreads) freq_dense_count(AArgs a, uint32_t* part) {
+  __shared__ uint32_t cnt[kDenseW];
+  uint64_t lo;
+  uint32_t nvals;
+  if (!dense_window(a, lo, nvals)) return;  // (block-uniform)
+  const int tid = threadIdx.x;
+  for (uint32_t i = tid; i < nvals; i += kDenseThreads) cnt[i] = 0;
+  __syncthreads();
+  const KeyCol& c = a.ks.cols[0];
+  unsigned long long nn = 0;
+  const int64_t stride = (int64_t)gridDim.x * kDenseThreads * 4;
+  for (int64_t r0 = (int64_t)blockIdx.x * kDenseThreads * 4; r0 < a.n_items; r0 += stride) {
+    uint64_t v[4];
+    uint32_t ok = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // rows r0 + 1024 j + tid: each wave-instruction contiguous
+      const int64_t r = r0 + (int64_t)j * kDenseThreads + tid;
+      const bool in = r < a.n_items;
+      v[j] = kwiden(TY, c.values, in ? r : 0);
+      ok |= (in && kbit(c.valid, r) ? 1u : 0u) << j;
+      nn += in && !((ok >> j) & 1u) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((ok >> j) & 1u) atomicAdd(&cnt[(uint32_t)(v[j] - lo)], 1u);
+  }
+  __shared__ unsigned long long s_nn;  // the workgroup's NULL rows: one global atomic
+  if (tid == 0) s_nn = 0;
+  __syncthreads();
+  nn = wave_sum(nn);
+  if (__lane_id() == 0 && nn) atomicAdd(&s_nn, nn);
+  __syncthreads();
+  if (tid == 0 && s_nn) atomicAdd(&a.counters[a.ks.null_as_group ? C_NULL_GROUP : C_NULL_ROWS], s_nn);
+  for (uint32_t i = tid; i < nvals; i += kDenseThreads) part[(size_t)blockIdx.x * kDenseW + i] = cnt[i];
+}
+
+// The counting workgroups' rows summed per value (kDenseSumV values per workgroup, a quarter of
+// the rows per thread): sums[v].
+__global__ void __launch_bounds__(kBuckets) freq_dense_sum(AArgs a, const uint32_t* part, int n_part,
+                                                           unsigned long long* sums) {
+  constexpr int kSlices = kBuckets / kDenseSumV;
+  __shared__ unsigned long long s_sum[kSlices][kDenseSumV];
+  uint64_t lo;
+  uint32_t nvals;
+  if (!dense_window(a, lo, nvals)) return;
+  const int tid = threadIdx.x, q = tid / kDenseSumV, i = tid % kDenseSumV;
+  const uint32_t v = blockIdx.x * kDenseSumV + (uint32_t)i;
+  if (blockIdx.x * kDenseSumV >= nvals) return;  // (block-uniform)
+  uint64_t acc = 0;
+  if (v < nvals) {
+#pragma unroll 16
+    for (int g = q; g < n_part; g += kSlices) acc += part[(size_t)g * kDenseW + v];
+  }
+  s_sum[q][i] = acc;
+  __syncthreads();
+  if (tid < kDenseSumV && v < nvals) {
+    uint64_t t = 0;
+#pragma unroll
+    for (int k = 0; k < kSlices; ++k) t += s_sum[k][tid];
+    sums[v] = t;
+  }
+}
+
+// One block per kDenseV values: one record per nonzero base-4 digit of each value's count,
+// counting-sorted by bucket into chunk blockIdx.x of the batch; the batch's other chunk rows are
+// emptied.
+__global__ void __launch_bounds__(kDenseV) freq_dense_emit(AArgs a, const unsigned long long* sums) {
+  __shared__ uint32_t bh[kBuckets];
+  __shared__ uint32_t s_wave[kDenseV / 64];
+  __shared__ unsigned long long s_maxcnt;
+  uint64_t lo;
+  uint32_t nvals;
+  const int tid = threadIdx.x;
+  if (!dense_window(a, lo, nvals)) {
+    if (blockIdx.x == 0 && tid == 0)
+      __hip_atomic_store(&a.dense_words[3], (unsigned long long)a.dense_epoch, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  static_assert(kDenseV == kBuckets, "one bucket per thread");
+  const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
+  const int64_t chunks = n_tiles + (n_tiles + a.tiles_per_wg - 1) / a.tiles_per_wg;
+  if ((int64_t)blockIdx.x >= chunks) return;  // (a batch of fewer chunks than blocks)
+  // the rows of the chunks past the grid: empty
+  for (int64_t r = (int64_t)gridDim.x + blockIdx.x; r < chunks; r += gridDim.x)
+    for (int i = tid; i < kHistRow; i += kDenseV) a.hist[r * kHistRow + i] = 0;
+  bh[tid] = 0;
+  if (tid == 0) s_maxcnt = 0;
+  __syncthreads();
+  const uint32_t v = blockIdx.x * kDenseV + tid;
+  const uint64_t cn = v < nvals ? sums[v] : 0ULL;
+  const uint64_t h = fmix_bij(lo + v);  // the exact key hash of value lo + v
+  uint32_t nd = 0;
+  for (uint64_t x = cn; x; x >>= 2) nd += (x & 3) ? 1u : 0u;
+  const uint32_t b = bucket_of(h);
+  const uint32_t rank = nd ? atomicAdd(&bh[b], nd) : 0u;
+  __syncthreads();
+  uint32_t total;
+  const uint32_t cb = bh[tid];
+  const uint32_t ex = block_excl_scan(cb, s_wave, total);
+  uint16_t* hrow = a.hist + (int64_t)blockIdx.x * kHistRow;
+  hrow[tid] = (uint16_t)ex;
+  if (tid == 0) hrow[kBuckets] = (uint16_t)total;
+  __syncthreads();
+  bh[tid] = ex;
+  __syncthreads();
+  if (nd) {
+    uint64_t* out = reinterpret_cast<uint64_t*>(a.recs) + (int64_t)blockIdx.x * FM<false>::kTile;
+    uint32_t pos = bh[b] + rank;
+    for_digits(cn, [&](uint32_t code) { out[pos++] = (h << 8) | code; });
+  }
+  wave_max_lds(&s_maxcnt, cn);
+  __syncthreads();
+  if (tid == 0) {
+    if (s_maxcnt) atomicMax(&a.counters[C_MAXCNT], s_maxcnt);
+    if (blockIdx.x == 0)
+      __hip_atomic_store(&a.dense_words[2], (unsigned long long)a.dense_epoch, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Per bucket (one block each): ph[*][b] -> its exclusive prefix over the workgroups, tot[b] = sum.
@@ -4068,6 +4261,14 @@ struct dq_freq {
       if (p) pinned_word_put(p);
     }
   } fast_seen;
+  // the dense integer path (freq_dense_count / _emit): its device words (AArgs::dense_words), the
+  // epoch of its last attempt, the counting workgroups' counters, and a pinned copy of the epoch
+  // it last declined (a table it declined stops trying)
+  DevBuf<unsigned long long> dense_words;
+  DevBuf<uint32_t> dense_part;
+  uint64_t dense_epoch = 0;
+  bool dense_off = false;
+  PinnedWord dense_seen;
   // finalize cache (phase B)
   bool b_valid = false;
   int s_bits = 0;
@@ -4322,9 +4523,31 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
   const size_t rows_need = (size_t)(f->n_prow + n_wg) * kBuckets;
   HIP_TRY(grow_keep(f->pstart, (size_t)f->n_prow * kBuckets, rows_need, f->stream));
   HIP_TRY(grow_keep(f->plen, (size_t)f->n_prow * kBuckets, rows_need, f->stream));
-  hipLaunchKernelGGL(freq_prepass_x, dim3((unsigned)n_wg), dim3(kPreThreads), 0, f->stream, a, f->ph.p);
+  if (a.dense_words)
+    hipLaunchKernelGGL(freq_prepass_x<true>, dim3((unsigned)n_wg), dim3(kPreThreads), 0, f->stream, a, f->ph.p);
+  else
+    hipLaunchKernelGGL(freq_prepass_x<false>, dim3((unsigned)n_wg), dim3(kPreThreads), 0, f->stream, a, f->ph.p);
   hipLaunchKernelGGL(freq_prepass_scan, dim3(kBuckets), dim3(256), 0, f->stream, f->ph.p, n_wg, f->ptot.p);
   HIP_TRY(hipGetLastError());
+  if (a.dense_words) {  // the dense path first (it declines at once when the range is too wide)
+    const int g = (int)std::min<int64_t>(kDenseBlocks, (a.n_items + 4 * kDenseThreads - 1) / (4 * kDenseThreads));
+    HIP_TRY(f->dense_part.ensure((size_t)kDenseBlocks * kDenseW + 2 * kDenseW));  // + the u64 sums
+    auto go = [&](auto kernel) {
+      hipLaunchKernelGGL(kernel, dim3((unsigned)g), dim3(kDenseThreads), 0, f->stream, a, f->dense_part.p);
+    };
+    switch (a.ks.cols[0].type) {
+      case DQ_INT8: go(freq_dense_count<DQ_INT8>); break;
+      case DQ_INT16: go(freq_dense_count<DQ_INT16>); break;
+      case DQ_INT32: go(freq_dense_count<DQ_INT32>); break;
+      case DQ_BOOL: go(freq_dense_count<DQ_BOOL>); break;
+      default: go(freq_dense_count<DQ_INT64>); break;
+    }
+    unsigned long long* sums = reinterpret_cast<unsigned long long*>(f->dense_part.p + (size_t)kDenseBlocks * kDenseW);
+    hipLaunchKernelGGL(freq_dense_sum, dim3(kDenseW / kDenseSumV), dim3(kBuckets), 0, f->stream, a,
+                       f->dense_part.p, g, sums);
+    hipLaunchKernelGGL(freq_dense_emit, dim3(kDenseW / kDenseV), dim3(kDenseV), 0, f->stream, a, sums);
+    HIP_TRY(hipGetLastError());
+  }
   a.ph = f->ph.p;
   a.ptot = f->ptot.p;
   a.pstart = f->pstart.p + (size_t)f->n_prow * kBuckets;
@@ -4355,8 +4578,24 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
   const unsigned long long base = (unsigned long long)f->n_chunks * f->tile;
   for (int64_t w = 0; w < n_wg; ++w) f->h_pbase.push_back(base);
   f->n_prow += n_wg;
-  f->n_empty_chunks += chunks;
+  if (!a.dense_words) f->n_empty_chunks += chunks;  // (a dense batch's records are in chunk rows)
   return DQ_OK;
+}
+
+// Whether this batch tries the dense path: one integer / boolean key of an exact table that has
+// not declined it before (DQ_FREQ_DENSE=0: never).  The declines come back late, through a pinned
+// word the stream copies into, so a wide column stops trying after a batch or two.
+static bool dense_worth_trying(dq_freq* f, const dq_column& k, int64_t rows) {
+  const char* e = getenv("DQ_FREQ_DENSE");  // (read per batch: tests switch it)
+  if ((e && atoi(e) == 0) || f->dense_off || !f->exact || f->n_keys != 1 || rows < 4 * kDenseThreads) return false;
+  if (k.type != DQ_INT8 && k.type != DQ_INT16 && k.type != DQ_INT32 && k.type != DQ_INT64 &&
+      k.type != DQ_BOOL)
+    return false;
+  if (f->dense_seen.p && *(volatile unsigned long long*)f->dense_seen.p != 0) {
+    f->dense_off = true;  // a batch was declined
+    return false;
+  }
+  return true;
 }
 
 // ---- finalize: phase B ------------------------------------------------------------------------
@@ -5458,6 +5697,8 @@ extern "C" void dq_freq_destroy(dq_freq* f) {
   (void)hipStreamSynchronize(f->stream);
   if (f->fast_seen.last_copy && f->fast_seen.last_copy != f->stream)
     (void)hipStreamSynchronize(f->fast_seen.last_copy);  // (the word's copies, pinned_word_put)
+  if (f->dense_seen.last_copy && f->dense_seen.last_copy != f->stream)
+    (void)hipStreamSynchronize(f->dense_seen.last_copy);
   delete f;
 }
 
@@ -5531,8 +5772,26 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     if (ss != DQ_OK) return ss;
   }
   if (f->exact && pieces_enabled()) {
+    const bool dense = dense_worth_trying(f, keys[0], rows);
+    if (dense) {
+      if (!f->dense_seen.p) {
+        HIP_TRY(pinned_word_get(&f->dense_seen.p));
+        *f->dense_seen.p = 0;
+      }
+      if (!f->dense_words.p) {
+        HIP_TRY(f->dense_words.ensure(4));
+        HIP_TRY(hipMemsetAsync(f->dense_words.p, 0, 4 * 8, f->stream));
+      }
+      HIP_TRY(hipMemsetAsync(f->dense_words.p, 0, 2 * 8, f->stream));  // the batch's range
+      a.dense_words = f->dense_words.p;
+      a.dense_epoch = ++f->dense_epoch;
+    }
     dq_status ps = launch_pieces(f, a, chunks);
     if (ps != DQ_OK) return ps;
+    if (dense) {  // the host learns (late, without a wait) whether the batch was declined
+      HIP_TRY(hipMemcpyAsync(f->dense_seen.p, f->dense_words.p + 3, 8, hipMemcpyDeviceToHost, f->stream));
+      f->dense_seen.last_copy = f->stream;
+    }
   } else if (f->exact) {
     launch_phaseA<false>(f, a, false);
   } else {
