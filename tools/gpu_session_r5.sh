@@ -10,6 +10,7 @@
 #  PART=wl:    configs[2] / [3] / [4] lines (tools/bench_workloads.py).
 #  PART=c3:    configs[2] line, its rocprof kernel stats and PMC passes (tools/gpu_pmc_c3.sh).
 #  PART=s10ab: parity tests, then scan ablation + bench of this build against the build at $VAR.
+#  PART=pmc:   the configs[2] and configs[4] PMC passes (tools/gpu_pmc_c3.sh, gpu_pmc_c5.sh).
 #  PART=dense: the group-by tests with the dense integer path, configs[4] with and without it,
 #              configs[2], and configs[4]'s kernel stats.
 #  PART=hll:   the HLL-from-table tests, configs[4] with and without it.
@@ -73,6 +74,9 @@ s10ab)
     timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-h2d > $O/bench_new${k}_$T.json 2>&1 &&
     DQ_LIB_PATH=$VAR timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-h2d > $O/bench_var${k}_$T.json 2>&1 || exit 1
   done
+  ;;
+pmc)
+  TAG=$T bash tools/gpu_pmc_c3.sh && TAG=$T bash tools/gpu_pmc_c5.sh
   ;;
 dense)
   timeout -k 10 400 $PYT tests/test_gpu_freq_dense.py tests/test_gpu_freq.py tests/test_gpu_configs4.py tests/test_gpu_hll_tables.py tests/test_gpu_determinism.py > $O/gpu_tests_$T.log 2>&1 &&

@@ -1,4 +1,5 @@
-"""Per-kernel summary of the configs[2] PMC passes (tools/gpu_pmc_c3.sh, 1e8 rows, one step).
+"""Per-kernel summary of the configs[2] / [4] PMC passes (tools/gpu_pmc_c3.sh at 1e8 rows,
+tools/gpu_pmc_c5.sh; one step each), with the step's totals over every kernel but the generators.
 
 Usage: python tools/summarize_c3_pmc.py TAG [WORKLOAD]   (WORKLOAD c3 (default) or c5)
   reads  gpurun_out/{pmcf,pmcw,pmc,pmc2}_WORKLOAD_TAG/*_counter_collection.csv
@@ -26,9 +27,15 @@ def main():
     for pas in ("pmcf", "pmcw", "pmc", "pmc2"):
         for path in glob.glob(os.path.join(src, f"{pas}_{wl}_{tag}", "*_counter_collection.csv")):
             for r in csv.DictReader(open(path)):
-                if not r["Kernel_Name"].startswith(("dq::", "void dq::")):
+                name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+                # every kernel of the step but the synthetic table's generation, which runs once
+                # before the step in the same process: its HIP generators and the torch kernels
+                # around them (at::native, and torch's bundled rocPRIM 4.0.1 for cumsum; the
+                # engine's own rocPRIM is 4.2)
+                if ("gen_" in name.split("(")[0] or "dq_synth" in name or "at::native" in name
+                        or "ROCPRIM_400001" in name):
                     continue
-                k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+                k = name.split("(")[0].replace("void ", "")
                 acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[k].add((pas, r["Dispatch_Id"]))
     out = {}
@@ -47,7 +54,12 @@ def main():
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     what = {"c3": "c3 --rows 100000000 --steps 1 --warmup 0", "c5": "c5 --steps 1 --warmup 0"}[wl]
-    json.dump({"tag": tag, "workload": what, "kernels": out},
+    tot_f = sum(d.get("fetch_bytes_raw", 0.0) for d in out.values())
+    tot_w = sum(d.get("write_bytes", 0.0) for d in out.values())
+    totals = {"fetch_bytes_raw": tot_f, "write_bytes": tot_w,
+              "fetch_x2_plus_write": 2 * tot_f + tot_w}
+    print("totals (GB):", {k: round(v / 1e9, 2) for k, v in totals.items()})
+    json.dump({"tag": tag, "workload": what, "totals": totals, "kernels": out},
               open(os.path.join(dst, f"{wl}_counters.json"), "w"), indent=1)
     for k in sorted(out, key=lambda k: -out[k].get("fetch_bytes_raw", 0)):
         d = out[k]
