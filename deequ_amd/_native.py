@@ -126,6 +126,7 @@ def _load() -> ctypes.CDLL:
         "dq_release_cached_memory": (None, []),
         "dq_cached_device_bytes": (c_int64, [c_int]),
         "dq_freq_hll": (c_int, [c_void_p, c_int64, c_void_p, POINTER(c_int), c_void_p]),
+        "dq_freq_folded_nan_rows": (c_int, [c_void_p, POINTER(c_int64)]),
         "dq_state_exchange_sizes": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64),
                                             POINTER(c_int64)]),
         "dq_state_exchange_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -174,7 +175,7 @@ EXPORTED = [
     "dq_state_destroy", "dq_state_reset", "dq_scan_device", "dq_scan_device_batches",
     "dq_state_sync", "dq_state_get", "dq_state_get_all", "dq_state_merge", "dq_state_serialized_size",
     "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_column_release", "dq_java_double_to_string", "dq_java_float_to_string", "dq_java_doubles_to_strings", "dq_freq_create",
-    "dq_freq_destroy", "dq_freq_reset", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_summarize_keys", "dq_sorted_sample", "dq_freq_marginal", "dq_freq_mutual_information", "dq_freq_num_groups", "dq_freq_null_literal", "dq_freq_import", "dq_cast_utf8", "dq_release_cached_memory", "dq_cached_device_bytes", "dq_freq_hll",
+    "dq_freq_destroy", "dq_freq_reset", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_summarize_keys", "dq_sorted_sample", "dq_freq_marginal", "dq_freq_mutual_information", "dq_freq_num_groups", "dq_freq_null_literal", "dq_freq_import", "dq_cast_utf8", "dq_release_cached_memory", "dq_cached_device_bytes", "dq_freq_hll", "dq_freq_folded_nan_rows",
     "dq_state_exchange_sizes", "dq_state_exchange_pack", "dq_state_exchange_unpack",
     "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge", "dq_freq_topk", "dq_loader_create",
     "dq_loader_destroy", "dq_loader_stage", "dq_loader_release", "dq_scan_host",

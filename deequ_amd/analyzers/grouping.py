@@ -87,6 +87,14 @@ class FrequencyTable:
             return None
         return tuple(int(w) - (1 << 64) if w >= (1 << 63) else int(w) for w in words)
 
+    def folded_nan_rows(self) -> int:
+        """Keyed rows of this Histogram-mode floating-point table whose NaN payload was folded into
+        the canonical NaN (dq_freq_folded_nan_rows); 0: its keyed groups are the grouping's;
+        -1: not counted."""
+        n = ctypes.c_int64()
+        N.check(N.lib.dq_freq_folded_nan_rows(self.handle, ctypes.byref(n)))
+        return int(n.value)
+
     def null_literal(self) -> Tuple[int, int]:
         """(rows of the NULL group, count of the "NullValue" string group) of a Histogram table
         (dq_freq_null_literal); the second is 0 unless the key is one string column."""
@@ -676,10 +684,12 @@ class Histogram(Analyzer):
         Entropy, ... on [column])?  Integral, boolean and string columns: their NULL rows form a
         separate group that the keyed view drops (a string column's NULL group is folded into the
         "NullValue" string only when Histogram reads the table, _fold_null_group).
-        Floating-point never: Histogram folds NaN payloads (cast to string), the grouping does
-        not."""
+        Floating-point columns too, provisionally: Histogram folds NaN payloads (cast to string)
+        and the grouping does not, so the table serves the grouping only when it folded no row
+        (FrequencyTable.folded_nan_rows() == 0, checked by the runner after the table is built;
+        otherwise the grouping runs its own group-by)."""
         dtype = data.schema[column].dtype
-        return dtype in (N.BOOL, N.INT8, N.INT16, N.INT32, N.INT64, N.UTF8)
+        return dtype in (N.BOOL, N.INT8, N.INT16, N.INT32, N.INT64, N.UTF8, N.FLOAT32, N.FLOAT64)
 
     def compute_state_from(self, data):
         from ..distributed import compute_frequencies_distributed, is_distributed

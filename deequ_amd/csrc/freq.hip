@@ -70,8 +70,10 @@ constexpr uint64_t kNotReady = ~0ULL;
 
 // C_MAXCNT: an upper bound of the count any phase-A record carries (packed phase-C slots at
 // fewer than kMaxSubBits sub-bits need every record count below 2^(s-3); merges add the bounds)
+// C_NAN_FOLDED: keyed rows of a Histogram-mode floating-point table whose NaN payload was folded
+// into the canonical NaN (zero: the table's groups are also the grouping's, dq_freq_folded_nan_rows)
 enum Counter { C_NULL_ROWS = 0, C_NULL_GROUP, C_COLLISIONS, C_DBG_NOTREADY, C_DBG_DIFF, C_DBG_FULL, C_DBG_BYPASS,
-               C_MAXCNT, C_N };
+               C_MAXCNT, C_NAN_FOLDED, C_N };
 
 template <bool HASHED>
 struct FM;
@@ -1241,7 +1243,7 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
     s_full = 0;
     s_maxcnt = 0;
   }
-  unsigned long long nulls = 0, nullg = 0, dbg_bypass = 0;
+  unsigned long long nulls = 0, nullg = 0, dbg_bypass = 0, nanf = 0;
   uint64_t* out = reinterpret_cast<uint64_t*>(a.recs);
   // the full-tile loads: 8-byte-aligned bitmap words, tiles on 64-row boundaries
   const bool full_ok = (reinterpret_cast<uintptr_t>(c.valid) & 7u) == 0 && (a.tile_items & 63) == 0;
@@ -1317,6 +1319,11 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
         nullg += ng;
         nulls += nn - ng;
       }
+      if constexpr (TY == DQ_FLOAT64 || TY == DQ_FLOAT32) {  // (Histogram mode folds NaN payloads)
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          nanf += ((keyed >> j) & 1u) && exact_canon(a.ks, h[j]) != h[j] ? 1u : 0u;
+      }
 #pragma unroll
       for (int j = 0; j < R; ++j) h[j] = fmix_bij(exact_canon(a.ks, h[j]));
       // 2. dedupe: round 0 of a probing tile measures the hit rate, which decides the bypass
@@ -1390,6 +1397,7 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
   wave_count(&a.counters[C_NULL_ROWS], nulls);
   wave_count(&a.counters[C_NULL_GROUP], nullg);
   wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
+  wave_count(&a.counters[C_NAN_FOLDED], nanf);
   if (tid == 0 && s_full) atomicAdd(&a.counters[C_DBG_FULL], (unsigned long long)s_full);
 }
 
@@ -4254,6 +4262,9 @@ struct dq_freq {
   // the epoch it last gave up (copied back asynchronously: a table it gave up on stops trying)
   uint64_t fast_epoch = 0;
   bool fast_off = false;
+  // every batch went through freq_phaseA_xp, which counts C_NAN_FOLDED (records, merges and the
+  // other phase-A kernels do not)
+  bool nan_counted = true;
   struct PinnedWord {
     unsigned long long* p = nullptr;
     hipStream_t last_copy = nullptr;  // the stream of the last copy into *p
@@ -4557,6 +4568,7 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
     return e && atoi(e) != 0;
   }();
   if (generic) {
+    f->nan_counted = false;
     launch_phaseA<false>(f, a, false);
   } else {
     static_assert(kAXThreads == kBuckets, "one bucket per thread");
@@ -5675,6 +5687,7 @@ extern "C" dq_status dq_freq_reset(dq_freq* f, void* hip_stream) {
   f->stream = reinterpret_cast<hipStream_t>(hip_stream);
   HIP_TRY(hipMemsetAsync(f->dev_words.p, 0, (C_N + 4) * 8, f->stream));
   for (int k = 0; k < C_N; ++k) f->h_counters[k] = 0;
+  f->nan_counted = true;
   f->arena_used = 0;
   f->arena_view = nullptr;  // (a reset table owns its keys again)
   f->rec_var_base = 0;
@@ -5793,6 +5806,7 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
       f->dense_seen.last_copy = f->stream;
     }
   } else if (f->exact) {
+    f->nan_counted = false;
     launch_phaseA<false>(f, a, false);
   } else {
     launch_phaseA<true>(f, a, false);
@@ -6263,6 +6277,15 @@ extern "C" dq_status dq_freq_hll(dq_freq* f, int64_t max_records, uint64_t* word
   return DQ_OK;
 }
 
+extern "C" dq_status dq_freq_folded_nan_rows(dq_freq* f, int64_t* n) {
+  if (!f || !n) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+  HIP_TRY(hipSetDevice(f->device));
+  dq_status st = sync_counters(f);
+  if (st != DQ_OK) return st;
+  *n = f->nan_counted ? (int64_t)f->h_counters[C_NAN_FOLDED] : -1;
+  return DQ_OK;
+}
+
 extern "C" dq_status dq_freq_num_groups(dq_freq* f, int64_t* n) {
   if (!f || !n) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   HIP_TRY(hipSetDevice(f->device));
@@ -6537,6 +6560,7 @@ extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src_c) {
   if (dst->n_keys != src->n_keys || dst->types != src->types)
     return fail(DQ_ERR_STATE, "frequency tables group on different key types");
   if (dst->device != src->device) return fail(DQ_ERR_UNSUPPORTED, "tables on different devices");
+  dst->nan_counted = dst->nan_counted && src->nan_counted;
   if (dst->mode_null_as_group >= 0 && src->mode_null_as_group >= 0 &&
       dst->mode_null_as_group != src->mode_null_as_group)
     return fail(DQ_ERR_STATE, "frequency tables differ in NULL handling");
@@ -6661,6 +6685,7 @@ static dq_status add_records(dq_freq* f, const dq_freq_record* records, const ui
   if (!f || !src_records || !src_var_bytes || !special)
     return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   if (f->arena_view) return fail(DQ_ERR_STATE, "a table reading another table's keys takes no adds");
+  f->nan_counted = false;
   if (borrow && (f->exact || f->arena_used || f->n_chunks))
     return fail(DQ_ERR_STATE, "only a fresh hashed table can borrow var bytes");
   if (n_src < 1 || n_src > kMaxParts)

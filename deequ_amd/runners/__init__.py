@@ -20,6 +20,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
+from .. import _native as N
 from ..analyzers.base import (Analyzer, GroupingAnalyzer, Preconditions, ScanShareableAnalyzer)
 from ..analyzers.scan import ApproxCountDistinct
 from ..analyzers.grouping import (FrequenciesAndNumRows, Histogram, KeyedFrequencies,
@@ -362,6 +363,8 @@ def _histogram_and_grouping_host(st):
     for h in hists:
         hist_metrics[h] = h.compute_metric_from(dataclasses.replace(hs, binning_udf=h.binning_udf))
     state = FrequenciesAndNumRows(KeyedFrequencies(hs.frequencies), hs.num_rows)
+    if data.schema[col].dtype in (N.FLOAT32, N.FLOAT64) and hs.frequencies.folded_nan_rows() != 0:
+        state = None  # (NaN payloads folded for Histogram: the grouping groups the column itself)
     _, metrics = _run_grouping_analyzers(data, [col], group, aggregate_with, save_states_with,
                                          None, state)
     return AnalyzerContext(hist_metrics), metrics

@@ -381,6 +381,13 @@ dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int* is_null, v
 dq_status dq_freq_hll(dq_freq* table, int64_t max_records, uint64_t* words, int* done,
                       void* hip_stream);
 
+/* Keyed rows of a Histogram-mode floating-point table (null_as_group) whose NaN payload was folded
+ * into the canonical NaN -- Histogram groups cast(col as string), where every NaN prints "NaN"
+ * (Histogram.scala:63), while a grouping keeps Spark 2.2's binary key equality.  0: the table's
+ * keyed groups are exactly the grouping's of the same column (the runner then groups the column
+ * once); -1: not counted (a batch took a path that does not count, or records were merged in). */
+dq_status dq_freq_folded_nan_rows(dq_freq* table, int64_t* n);
+
 /* Number of groups currently in the table (NULL group and every distinct key). */
 dq_status dq_freq_num_groups(dq_freq* freq, int64_t* n_groups);
 /* Histogram's NULL fold (Histogram.scala:59-66, na.fill("NullValue") before the groupBy): the rows

@@ -24,10 +24,12 @@ def test_strings_share_with_or_without_nulls():
     assert Histogram.table_serves_grouping(_data(N.UTF8, [False, True]), "c")
 
 
-def test_floating_point_never_shares():
-    # Histogram folds NaN payloads (cast to string); the grouping keeps them apart
+def test_floating_point_shares_provisionally():
+    # Histogram folds NaN payloads (cast to string), the grouping keeps them apart: the table
+    # serves the grouping only when it folded no row, which the runner checks after building it
+    # (FrequencyTable.folded_nan_rows; tests/test_gpu_float_sharing.py)
     for t in (N.FLOAT32, N.FLOAT64):
-        assert not Histogram.table_serves_grouping(_data(t, [False]), "c")
+        assert Histogram.table_serves_grouping(_data(t, [False]), "c")
 
 
 def test_no_sharing_when_states_are_aggregated_or_saved():

@@ -79,7 +79,7 @@ pmc)
   TAG=$T bash tools/gpu_pmc_c3.sh && TAG=$T bash tools/gpu_pmc_c5.sh
   ;;
 dense)
-  timeout -k 10 400 $PYT tests/test_gpu_freq_dense.py tests/test_gpu_freq.py tests/test_gpu_configs4.py tests/test_gpu_hll_tables.py tests/test_gpu_determinism.py > $O/gpu_tests_$T.log 2>&1 &&
+  timeout -k 10 400 $PYT ${TESTS:-tests/test_gpu_freq_dense.py tests/test_gpu_freq.py tests/test_gpu_configs4.py tests/test_gpu_hll_tables.py tests/test_gpu_determinism.py} > $O/gpu_tests_$T.log 2>&1 &&
   timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_$T.json 2>&1 &&
   DQ_FREQ_DENSE=0 timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_nodense_$T.json 2>&1 &&
   timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
