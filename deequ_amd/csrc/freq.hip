@@ -1412,7 +1412,7 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
 // instead of one per row.  A wider batch is declined (both kernels return at once) and
 // freq_phaseA_xp does it; when the dense path takes it, freq_phaseA_xp leaves empty pieces.
 // ------------------------------------------------------------------------------------------------
-constexpr int kDenseW = 1 << 15;   // values counted per batch (128 KiB of LDS counters)
+constexpr int kDenseW = 79 * 512;  // values counted per batch (158 KiB of LDS counters)
 constexpr int kDenseV = 512;       // values per emitted chunk (<= 16 digits each: <= kTile records)
 constexpr int kDenseSumV = 128;    // values per summing workgroup (four threads each)
 constexpr int kDenseThreads = 1024;

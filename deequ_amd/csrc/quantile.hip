@@ -85,6 +85,7 @@ struct Pass {
   const uint64_t* act;
   int A, bits, D;
   int64_t R;
+  int minmax;  // also each prefix's min / max key (every pass with bits > 0; pass 0 of integers)
 };
 
 template <int TY> struct Ty { using T = double; };
@@ -204,7 +205,7 @@ rs_hist(Srcs ss, Pass p, uint32_t* __restrict__ partial, unsigned long long* __r
   extern __shared__ uint64_t rs_lds[];
   int64_t lb;
   const Src& s = block_src(ss, lb);
-  const bool minmax = p.bits > 0;
+  const bool minmax = p.minmax != 0;
   PassLds L;
   L.load(p, rs_lds, minmax);
   const int nb = p.A << p.D;
@@ -213,6 +214,9 @@ rs_hist(Srcs ss, Pass p, uint32_t* __restrict__ partial, unsigned long long* __r
   __syncthreads();
   const int64_t r_begin = lb * p.R;
   const int64_t r_end = r_begin + p.R < s.rows ? r_begin + p.R : s.rows;
+  // pass 0 (one prefix, the whole column): each thread's running min / max, reduced once
+  const bool mm0 = minmax && p.bits == 0;
+  uint64_t tlo = ~0ULL, thi = 0ULL;
   for (int64_t i0 = r_begin; i0 < r_end; i0 += kRsStep) {
     uint64_t k[kRsK];
     bool ok[kRsK];
@@ -221,7 +225,12 @@ rs_hist(Srcs ss, Pass p, uint32_t* __restrict__ partial, unsigned long long* __r
     for (int u = 0; u < kRsK; ++u) {
       const int a = ok[u] ? L.index(p, k[u]) : -1;
       if (a >= 0) atomicAdd(&s_hist[(a << p.D) | (int)digit_of(p, k[u])], 1u);
-      if (minmax) {  // a wave whose keys share one prefix (narrow data) reduces before its atomic
+      if (mm0) {
+        if (ok[u]) {
+          tlo = k[u] < tlo ? k[u] : tlo;
+          thi = k[u] > thi ? k[u] : thi;
+        }
+      } else if (minmax) {  // a wave whose keys share one prefix (narrow data) reduces before its atomic
         const int a0 = __builtin_amdgcn_readfirstlane(a);
         if (__ballot(a == a0) == ~0ULL) {
           if (a0 >= 0) {
@@ -236,6 +245,14 @@ rs_hist(Srcs ss, Pass p, uint32_t* __restrict__ partial, unsigned long long* __r
           atomicMax(&L.mx[a], (unsigned long long)k[u]);
         }
       }
+    }
+  }
+  if (mm0) {
+    tlo = __ockl_wfred_min_u64(tlo);
+    thi = __ockl_wfred_max_u64(thi);
+    if (__lane_id() == 0) {
+      atomicMin(&L.mn[0], (unsigned long long)tlo);
+      atomicMax(&L.mx[0], (unsigned long long)thi);
     }
   }
   __syncthreads();
@@ -373,6 +390,44 @@ __global__ void select_pick(const uint64_t* __restrict__ keys, const int64_t* __
   if (j < m) out[j] = from_ordered(keys[idx[j]]);
 }
 
+// Dense counting select for integer columns of a narrow range (every keyed value in
+// [lo, lo + n_vals), n_vals <= kDenseQ and its counters fit the device's LDS): each workgroup adds its rows to per-value LDS counters
+// (one LDS add per row) and writes them to its row of `partial`; rs_sum then totals them per value
+// and the host reads the ranks off the running counts -- one pass over the column instead of the
+// radix select's histogram passes and compaction.  The value is the one the select would return:
+// the row's double (Spark feeds ApproxQuantile doubles), as an integer.
+constexpr int kDenseQ = 40960;  // 160 KiB of u32 counters: one workgroup per CU
+constexpr int kDenseQThreads = 1024;
+template <int TY>
+__global__ void __launch_bounds__(kDenseQThreads)
+rs_dense(Srcs ss, int64_t lo, int n_vals, uint32_t* __restrict__ partial) {
+  extern __shared__ uint32_t dq_cnt[];
+  for (int i = threadIdx.x; i < n_vals; i += kDenseQThreads) dq_cnt[i] = 0;
+  __syncthreads();
+  using T = typename Ty<TY>::T;
+  for (int j = 0; j < ss.n; ++j) {  // every source, grid-strided (a few rows per thread in flight)
+    const Src& s = ss.s[j];
+    const T* vals = reinterpret_cast<const T*>(s.values);
+    const int64_t stride = (int64_t)gridDim.x * kDenseQThreads * 4;
+    for (int64_t r0 = (int64_t)blockIdx.x * kDenseQThreads * 4; r0 < s.rows; r0 += stride) {
+      T v[4];
+      uint32_t ok = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t r = r0 + (int64_t)u * kDenseQThreads + threadIdx.x;
+        const bool in = r < s.rows;
+        v[u] = vals[in ? r : 0];
+        ok |= (in && (!s.valid || ((s.valid[r >> 3] >> (r & 7)) & 1u)) ? 1u : 0u) << u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if ((ok >> u) & 1u) atomicAdd(&dq_cnt[(uint32_t)((int64_t)(double)v[u] - lo)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n_vals; i += kDenseQThreads) partial[(size_t)blockIdx.x * n_vals + i] = dq_cnt[i];
+}
+
 // out[j] = from_ordered(sorted[j])
 __global__ void keys_to_doubles(const uint64_t* __restrict__ sorted, int64_t n, double* __restrict__ out) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
@@ -428,7 +483,7 @@ void for_launches(const Source& src, F&& f) {
 template <int TY, bool VEC>
 void launch_hist_t(const Source& src, Pass p, uint32_t* partial, unsigned long long* pmm, hipStream_t st) {
   p.R = src.R;
-  const size_t lds = pass_lds_words(p, p.bits > 0) * 8 + (size_t)(p.A << p.D) * 4;
+  const size_t lds = pass_lds_words(p, p.minmax != 0) * 8 + (size_t)(p.A << p.D) * 4;
   for_launches(src, [&](const Srcs& ss, unsigned blocks) {
     hipLaunchKernelGGL(HIP_KERNEL_NAME(rs_hist<TY, VEC>), dim3(blocks), dim3(kRsThreads), lds, st, ss, p, partial, pmm);
   });
@@ -468,14 +523,16 @@ struct Passer {
   DevBuf<uint64_t> act;
   DevBuf<uint32_t> sel;
   std::vector<unsigned long long> h, mmh;
-  dq_status run(const Source& src, const std::vector<uint64_t>& prefixes, int bits, int D, Pass& p) {
+  dq_status run(const Source& src, const std::vector<uint64_t>& prefixes, int bits, int D, Pass& p,
+                bool with_minmax = false) {
     const int A = (int)prefixes.size(), nb = A << D;
+    const bool minmax = bits > 0 || with_minmax;
     // LDS of rs_hist: A prefixes + their min / max (24 B each), the prefix map (16 KB at 13 bits)
     // and the bins (A << D <= kSelBins counters): at most 2048 ranks -> 96 KB, inside gfx950's
     // 160 KB per workgroup; checked against the device so a smaller part fails loudly
     {
-      const Pass q{nullptr, A, bits, D, src.R};
-      const size_t need = pass_lds_words(q, bits > 0) * 8 + (size_t)nb * 4;
+      const Pass q{nullptr, A, bits, D, src.R, minmax ? 1 : 0};
+      const size_t need = pass_lds_words(q, minmax) * 8 + (size_t)nb * 4;
       int dev = 0, cap = 0;
       HIP_TRY(hipGetDevice(&dev));
       HIP_TRY(hipDeviceGetAttribute(&cap, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
@@ -487,8 +544,8 @@ struct Passer {
     HIP_TRY(partial.ensure((size_t)src.G * nb));
     HIP_TRY(hist.ensure(nb));
     HIP_TRY(hipMemsetAsync(hist.p, 0, (size_t)nb * 8, st));
-    p = Pass{act.p, A, bits, D, src.R};
-    if (bits > 0) {
+    p = Pass{act.p, A, bits, D, src.R, minmax ? 1 : 0};
+    if (minmax) {
       HIP_TRY(pmm.ensure((size_t)src.G * 2 * A));
       HIP_TRY(mm.ensure((size_t)2 * A));
       std::vector<unsigned long long> init(2 * (size_t)A);
@@ -502,14 +559,14 @@ struct Passer {
     hipLaunchKernelGGL(rs_sum, dim3((unsigned)((nb + 255) / 256), gy), dim3(256), 0, st, partial.p, src.G,
                        nb, hist.p);
     HIP_TRY(hipGetLastError());
-    if (bits > 0) {
+    if (minmax) {
       hipLaunchKernelGGL(rs_minmax, dim3((unsigned)((A + 255) / 256), gy), dim3(256), 0, st, pmm.p, src.G,
                          A, mm.p);
       HIP_TRY(hipGetLastError());
     }
     h.resize(nb);
     HIP_TRY(d2h(h.data(), hist.p, (size_t)nb * 8, st));
-    if (bits > 0) HIP_TRY(d2h(mmh.data(), mm.p, (size_t)A * 16, st));
+    if (minmax) HIP_TRY(d2h(mmh.data(), mm.p, (size_t)A * 16, st));
     return DQ_OK;
   }
   // the keys of the last pass's selected bins (mask: nb bits) -> dst (T of them)
@@ -560,7 +617,7 @@ dq_status radix_select(Source src, Passer& ps, Pass p, std::vector<Target> tg, s
     std::vector<Target> left;
     for (Target& t : tg) {
       const int a = (int)(std::lower_bound(cur.begin(), cur.end(), t.prefix) - cur.begin());
-      if (p.bits > 0 && ps.mmh[2 * a] == ps.mmh[2 * a + 1]) {
+      if (p.minmax && ps.mmh[2 * a] == ps.mmh[2 * a + 1]) {
         res[t.j] = from_ordered(ps.mmh[2 * a]);
         continue;
       }
@@ -675,7 +732,9 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   ps.st = stream;
   Pass p;
   constexpr int kD0 = 13;
-  dq_status st = ps.run(col, std::vector<uint64_t>{0}, 0, kD0, p);
+  const int ty = batches[0].type;
+  const bool integral = ty == DQ_INT8 || ty == DQ_INT16 || ty == DQ_INT32 || ty == DQ_INT64;
+  dq_status st = ps.run(col, std::vector<uint64_t>{0}, 0, kD0, p, integral);
   if (st != DQ_OK) return st;
   unsigned long long count = 0;
   for (unsigned long long x : ps.h) count += x;
@@ -714,6 +773,57 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
     }
     return DQ_OK;
   }
+  // a narrow integer column: the values at the ranks by dense counting (DQ_QUANTILE_DENSE=0: never)
+  const char* dense_env = getenv("DQ_QUANTILE_DENSE");
+  if (integral && !(dense_env && atoi(dense_env) == 0)) {
+    const double dlo = from_ordered(ps.mmh[0]), dhi = from_ordered(ps.mmh[1]);
+    const int64_t lo = dlo > -0x1p62 ? (int64_t)dlo : 0, hi = dhi < 0x1p62 ? (int64_t)dhi : 0;
+    if (dlo > -0x1p62 && dhi < 0x1p62 && hi >= lo && (uint64_t)(hi - lo) < (uint64_t)kDenseQ) {
+      const int nv = (int)(hi - lo) + 1;
+      int dev = 0, cus = 0, lds_cap = 0;
+      HIP_TRY(hipGetDevice(&dev));
+      HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      HIP_TRY(hipDeviceGetAttribute(&lds_cap, hipDeviceAttributeMaxSharedMemoryPerBlock, dev));
+      if ((int64_t)nv * 4 > lds_cap) goto radix;  // (a part with less LDS: the radix select)
+      const int64_t G = std::max<int64_t>(1, std::min<int64_t>(cus, (rows + 4 * kDenseQThreads - 1) / (4 * kDenseQThreads)));
+      HIP_TRY(ps.partial.ensure((size_t)G * nv));
+      HIP_TRY(ps.hist.ensure(nv));
+      HIP_TRY(hipMemsetAsync(ps.hist.p, 0, (size_t)nv * 8, stream));
+      for (size_t i = 0; i < col.parts.size(); i += kMaxSrc) {  // (the launches add into one row set)
+        Srcs ss;
+        ss.n = (int)std::min<size_t>(kMaxSrc, col.parts.size() - i);
+        for (int j = 0; j < ss.n; ++j) ss.s[j] = col.parts[i + j];
+        auto go = [&](auto kernel) {
+          hipLaunchKernelGGL(kernel, dim3((unsigned)G), dim3(kDenseQThreads), (size_t)nv * 4, stream, ss, lo, nv,
+                             ps.partial.p);
+        };
+        switch (ty) {
+          case DQ_INT8: go(rs_dense<DQ_INT8>); break;
+          case DQ_INT16: go(rs_dense<DQ_INT16>); break;
+          case DQ_INT32: go(rs_dense<DQ_INT32>); break;
+          default: go(rs_dense<DQ_INT64>); break;
+        }
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(rs_sum, dim3((unsigned)((nv + 255) / 256), (unsigned)((G + 31) / 32)), dim3(256), 0, stream,
+                           ps.partial.p, G, nv, ps.hist.p);
+        HIP_TRY(hipGetLastError());
+      }
+      std::vector<unsigned long long> cnt(nv);
+      HIP_TRY(d2h(cnt.data(), ps.hist.p, (size_t)nv * 8, stream));
+      std::vector<int64_t> cum(nv);
+      int64_t run = 0;
+      for (int i = 0; i < nv; ++i) cum[i] = run += (int64_t)cnt[i];
+      if (run != (int64_t)count) return fail(DQ_ERR_STATE, "dense quantile counts %lld of %llu rows",
+                                             (long long)run, (unsigned long long)count);
+      for (int64_t j = 0; j < n; ++j) {
+        const int64_t q = (int64_t)(((__int128)j * ((int64_t)count - 1)) / (n - 1));
+        const int64_t i = std::upper_bound(cum.begin(), cum.end(), q) - cum.begin();
+        out[j] = (double)(lo + i);
+      }
+      return DQ_OK;
+    }
+  }
+radix:
   // the values at the ranks floor(j (count - 1) / (n - 1)), by radix select from pass 0
   std::vector<Target> tg(n);
   for (int64_t j = 0; j < n; ++j)

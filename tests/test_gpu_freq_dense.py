@@ -1,9 +1,10 @@
 """The dense integer path of the group-by (freq.hip freq_dense_count / freq_dense_emit): a batch of
-an integer or boolean key whose values span fewer than 2^15 consecutive values is counted by value
+an integer or boolean key whose values span at most kDenseW consecutive values is counted by value
 in LDS instead of written as a record per row.  Parity bar: every group's count bit-exact against
 a host count of the same column (the reference's groupBy(col).count(),
 GroupingAnalyzers.scala:53-80), NULL rows kept apart (or as the NULL group in Histogram mode), for
-every integer width, negative and extreme values, the window's edges (2^15 - 1 and 2^15 wide), and
+every integer width, negative and extreme values, the window's edges (kDenseW and kDenseW + 1
+values), and
 tables whose batches alternate between the dense path and the bucket pieces."""
 from collections import Counter
 
@@ -13,7 +14,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-W = 1 << 15
+W = 79 * 512  # freq.hip kDenseW: values a dense batch may span
 
 
 def _groups(ft):
