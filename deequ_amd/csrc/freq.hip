@@ -3980,6 +3980,8 @@ __global__ void freq_reduce_final(const unsigned long long* part, int nb, unsign
   out[0] = g;
   out[1] = u;
   out[2] = __builtin_bit_cast(unsigned long long, fix_to_f64(e));
+  out[4] = (uint64_t)e;  // (out[3]: the "NullValue" literal's count, written by phase C)
+  out[5] = (uint64_t)(e >> 64);
 }
 
 // Multi-block exclusive scan of u64 values in place, v[n] = total (large n; freq_part_scan is the
@@ -4307,6 +4309,7 @@ struct dq_freq {
   DevBuf<unsigned long long> red;
   uint64_t st_groups = 0, st_unique = 0;
   double st_entropy = 0.0;
+  fix128 st_entropy_fix = 0;  // the same sum, before its rounding to fp64
   uint64_t st_literal = 0;  // Histogram on a string: count of the "NullValue" string group
   bool recounted = false;
   // last top-k (dq_freq_topk is called twice: sizes, then data)
@@ -4848,7 +4851,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
   HIP_TRY(f->part_unique.ensure(P));
   HIP_TRY(f->part_off.ensure(P));
   HIP_TRY(f->part_entropy.ensure(2 * P));
-  HIP_TRY(f->red.ensure(4));
+  HIP_TRY(f->red.ensure(6));
   HIP_TRY(hipMemsetAsync(f->red.p + 3, 0, 8, f->stream));
   HIP_TRY(f->ovf_n.ensure(1));
   HIP_TRY(hipMemsetAsync(f->part_groups.p, 0, P * 8, f->stream));
@@ -5009,12 +5012,13 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     dq_status rs = launch_reduce(f, P);
     if (rs != DQ_OK) return rs;
   }
-  unsigned long long r[4];
+  unsigned long long r[6];
   HIP_TRY(d2h(r, f->red.p, sizeof(r), f->stream));
   f->st_groups = r[0];
   f->st_unique = r[1];
   f->st_entropy = __builtin_bit_cast(double, r[2]);
   f->st_literal = r[3];
+  f->st_entropy_fix = (fix128)(((unsigned __int128)r[5] << 64) | r[4]);
   f->c_valid = true;
   f->c_num_rows = nr;
   f->c_groups = want_groups;
@@ -5373,6 +5377,16 @@ __global__ void freq_mi_terms(const Group* __restrict__ gj, int64_t n, const uin
 struct CountSlot {
   unsigned long long h, count;
 };
+// -sum (c/n) ln(c/n) over a small marginal's value counts (count 0: an empty slot), as the
+// fixed-point sum phase C keeps (same device entropy_term, so the same bits as a table's)
+__global__ void __launch_bounds__(256) freq_slots_entropy(const CountSlot* __restrict__ t, uint64_t n_slots,
+                                                          double num_rows, unsigned long long* out) {
+  fix128 e = 0;
+  for (uint64_t i = threadIdx.x; i < n_slots; i += 256)
+    if (t[i].count) e += fix_of(entropy_term(t[i].count, num_rows));
+  e = wave_sum_fix(e);
+  if (__lane_id() == 0 && e) atomic_add_fix(out, e);
+}
 __global__ void freq_count_index(const Group* __restrict__ g, int64_t n, uint64_t mask,
                                  CountSlot* __restrict__ slots) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -6030,12 +6044,57 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
                         vb, joint->num_rows, special, 0, hip_stream, !marg[k]->exact);
     }
     stamp(k ? "marginal 1 records" : "marginal 0 records");
-    // (the groups stay where phase C put them, per partition; compacted only for the
-    // byte-compare lookups)
-    if (res == DQ_OK) res = finalize_c(marg[k], true, false);
-    stamp(k ? "marginal 1 groups" : "marginal 0 groups");
+    // statistics first: the entropy identity below may make the groups unnecessary
+    if (res == DQ_OK) res = finalize_c(marg[k], false, false);
+    stamp(k ? "marginal 1 statistics" : "marginal 0 statistics");
     if (res != DQ_OK) break;
     if (marg[k]->h_counters[C_COLLISIONS]) by_hash = false;
+  }
+  // MI = E(X) + E(Y) - E(X, Y), every entropy normalised by the same numRows as the reference's
+  // terms ((pxy/n) ln((pxy/n) / ((px/n)(py/n))) summed over the joint groups, the marginals
+  // summed over them too: MutualInformation.scala:41-75) -- exact algebra over the fixed-point
+  // sums of the tables' own -p ln p terms (the joint's and a general side's from phase C, a small
+  // side's from its value counts with the same device term).  Taken when MI >= 1/100 of
+  // E(X) + E(Y) + E(X, Y): each entropy's rounding is then below 1e-13 of MI (two columns close
+  // to independent keep the per-group terms, whose sum does not cancel).
+  if (res == DQ_OK) {
+    fix128 ex[2];
+    for (int k = 0; k < 2 && res == DQ_OK; ++k) {
+      if (!small[k]) {
+        ex[k] = marg[k]->st_entropy_fix;
+        continue;
+      }
+      DevBuf<unsigned long long> acc;
+      unsigned long long w[2];
+      if (acc.ensure(2) != hipSuccess || hipMemsetAsync(acc.p, 0, 16, stream) != hipSuccess) {
+        res = fail(DQ_ERR_OUT_OF_MEMORY, "MutualInformation entropy");
+        break;
+      }
+      hipLaunchKernelGGL(freq_slots_entropy, dim3(1), dim3(256), 0, stream, cslots[k].p, cmask[k] + 1,
+                         (double)joint->num_rows, acc.p);
+      if (hipGetLastError() != hipSuccess || d2h(w, acc.p, 16, stream) != hipSuccess) {
+        res = fail(DQ_ERR_DEVICE, "MutualInformation entropy");
+        break;
+      }
+      ex[k] = (fix128)(((unsigned __int128)w[1] << 64) | w[0]);
+    }
+    if (res == DQ_OK) {
+      const fix128 exy = joint->st_entropy_fix, v = ex[0] + ex[1] - exy;
+      if (v > 0 && v * 100 >= ex[0] + ex[1] + exy) {
+        *mi = fix_to_f64(v);
+        for (int k = 0; k < 2; ++k)
+          if (marg[k]) dq_freq_destroy(marg[k]);
+        stamp("entropy identity");
+        return DQ_OK;
+      }
+    }
+  }
+  for (int k = 0; k < 2 && res == DQ_OK; ++k) {  // the per-group terms: each general side's groups
+    if (small[k]) continue;
+    // (the groups stay where phase C put them, per partition; compacted only for the
+    // byte-compare lookups)
+    res = finalize_c(marg[k], true, false);
+    stamp(k ? "marginal 1 groups" : "marginal 0 groups");
   }
   if (res == DQ_OK && !by_hash && (small[0] || small[1])) {
     // a general side counted a hash collision: the byte-compare lookups need both sides as
