@@ -275,6 +275,11 @@ struct AArgs {
   const uint32_t* ptot;  // [kBuckets]: the batch's rows per bucket
   uint32_t* pstart;      // [n_wg][kBuckets]
   uint32_t* plen;        // [n_wg][kBuckets]
+  // one-utf8-column rows into bucket pieces of fixed capacity (pstart != nullptr in
+  // freq_phaseA<STR1>): piece (workgroup w, bucket b) holds up to piece_cap records at
+  // piece_base + (w * kBuckets + b) * piece_cap; a tile's records past a full piece go to its chunk
+  uint32_t piece_cap;
+  uint64_t piece_base;
   // dense integer keys (freq_dense_count / freq_dense_emit; nullptr: not tried for this batch):
   // {max, ~min} of the keyed values (sign-flipped, so unsigned order is signed order; 0 = none),
   // the epoch of the last batch the dense path took, the epoch of the last one it declined
@@ -408,6 +413,10 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   // exact rows into bucket pieces (a.pstart): each bucket's next record slot in the batch region
   constexpr bool XP = !HASHED && !FROM_REC;
   __shared__ uint32_t wcur[XP ? kBuckets : 1];
+  // STR1 rows into fixed-capacity bucket pieces: each piece's fill (u16: the LDS of two
+  // workgroups per CU has 1.7 KB left)
+  __shared__ uint16_t wfill[STR1 ? kBuckets : 1];
+  const bool hpieces = STR1 && a.pstart != nullptr;
 
   const int tid = threadIdx.x;
   if constexpr (STR1) {
@@ -433,6 +442,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     if (SK) dsk1[i] = kShortNotReady;
   }
   for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
+  if constexpr (STR1)
+    if (hpieces)
+      for (int i = tid; i < kBuckets; i += kThreads) wfill[i] = 0;
   if (tid == 0) s_bypass = 0;
   if constexpr (STR1) {
     // the arena bytes of every key this workgroup may encode, reserved once: at most 8 + len + 3
@@ -504,8 +516,37 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   };
   auto end_chunk = [&]() {
     __syncthreads();
+    if constexpr (STR1)
+      if (hpieces)  // the tile's records taken by each piece
+        for (int i = tid; i < kBuckets; i += kThreads)
+          wfill[i] = (uint16_t)(wfill[i] + min(bh[i], a.piece_cap - (uint32_t)wfill[i]));
     for (int i = tid; i < kBuckets; i += kThreads) bh[i] = 0;
     __syncthreads();
+  };
+  // STR1 pieces: the tile's chunk holds only what its pieces cannot take; bcur[b] = the bucket's
+  // overflow offset in the chunk << 16 | the rank counter of its records in this tile
+  auto begin_tile_pieces = [&](int64_t chunk) {
+    __syncthreads();
+    uint32_t ovf = 0, total;
+    if (tid < kBuckets) ovf = bh[tid] - min(bh[tid], a.piece_cap - (uint32_t)wfill[tid]);
+    const uint32_t ex = block_excl_scan(ovf, s_wave, total);
+    uint16_t* hrow = a.hist + chunk * kHistRow;
+    if (tid < kBuckets) {
+      bcur[tid] = ex << 16;
+      hrow[tid] = (uint16_t)ex;
+    }
+    if (tid == 0) hrow[kBuckets] = (uint16_t)total;
+    __syncthreads();
+  };
+  auto put_pieces = [&](int64_t chunk, uint64_t h, uint32_t code, uint64_t rep) {
+    const uint32_t b = bucket_of(h);
+    const uint32_t o = atomicAdd(&bcur[b], 1u), k = o & 0xffffu;
+    const uint32_t fill = wfill[b], take = min(bh[b], a.piece_cap - fill);
+    const uint64_t slot = k < take
+        ? a.piece_base + ((uint64_t)blockIdx.x * kBuckets + b) * a.piece_cap + fill + k
+        : (uint64_t)chunk * T + (o >> 16) + (k - take);
+    *reinterpret_cast<ulonglong2*>(reinterpret_cast<uint64_t*>(a.recs) + slot * W) =
+        make_ulonglong2(h, (rep << 8) | code);
   };
   auto put = [&](int64_t chunk, uint64_t h, uint32_t code, uint64_t rep) {
     const uint32_t pos = atomicAdd(&bcur[bucket_of(h)], 1u);
@@ -946,7 +987,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         continue;
       }
     }
-    const uint32_t ctotal = begin_chunk(t, need);
+    uint32_t ctotal = 0;
+    if (STR1 && hpieces) begin_tile_pieces(t);
+    else ctotal = begin_chunk(t, need);
     mark(t, 3);
     if constexpr (!HASHED && !FROM_REC) {
       // exact rows (count 1: one record each): sorted in LDS over the stash, then written out as
@@ -1001,7 +1044,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         } else {
           row_encode_dw(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
         }
-        put(t, stash[q * W], 1u, off);  // (row keys: one record, the count-1 digit code)
+        if (STR1 && hpieces) put_pieces(t, stash[q * W], 1u, off);
+        else put(t, stash[q * W], 1u, off);  // (row keys: one record, the count-1 digit code)
       }
     } else {
 #pragma unroll 1
@@ -1067,6 +1111,12 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     wave_count(&a.counters[C_NULL_ROWS], nulls);
     wave_count(&a.counters[C_NULL_GROUP], nullg);
   }
+  if constexpr (STR1)
+    if (hpieces && tid < kBuckets) {  // this workgroup's pieces: their starts and fills
+      const int64_t r = (int64_t)blockIdx.x * kBuckets + tid;
+      a.pstart[r] = (uint32_t)(a.piece_base + (uint64_t)r * a.piece_cap);
+      a.plen[r] = wfill[tid];
+    }
   __syncthreads();
   if (tid == 0 && s_maxcnt) atomicMax(&a.counters[C_MAXCNT], s_maxcnt);
   if (tid < 3 && s_dbg[tid]) atomicAdd(&a.counters[C_DBG_NOTREADY + tid], (unsigned long long)s_dbg[tid]);
@@ -4173,6 +4223,18 @@ __global__ void freq_rebase(uint64_t* recs, const uint16_t* hist, int64_t chunk0
   for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) recs[(c * tile + i) * 2 + 1] += delta << 8;
 }
 
+// the same for the records of bucket pieces (hashed: one-utf8-column tables): piece row r's
+// bucket b holds plen[r][b] records from pbase[r] + pstart[r][b]
+__global__ void freq_rebase_pieces(uint64_t* recs, const uint32_t* pstart, const uint32_t* plen,
+                                   const unsigned long long* pbase, uint64_t delta) {
+  const int64_t r = blockIdx.x;
+  for (int b = threadIdx.x; b < kBuckets; b += blockDim.x) {
+    const uint64_t s0 = pbase[r] + pstart[r * kBuckets + b];
+    const uint32_t n = plen[r * kBuckets + b];
+    for (uint32_t i = 0; i < n; ++i) recs[(s0 + i) * 2 + 1] += delta << 8;
+  }
+}
+
 // compact the materialised groups: partition p's g_p groups start at src_off[p], go to dst_off[p]
 __global__ void freq_compact(const Group* src, const unsigned long long* src_off,
                              const unsigned long long* cnt, const unsigned long long* dst_off,
@@ -4515,6 +4577,12 @@ static AArgs base_args(dq_freq* f) {
   a.arena_cursor = f->dev_words.p + C_N;
   a.counters = f->dev_words.p;
   return a;
+}
+
+// One-utf8-column rows into fixed-capacity bucket pieces (DQ_FREQ_HPIECES=0: chunks only)
+static bool hpieces_enabled() {
+  const char* e = getenv("DQ_FREQ_HPIECES");  // (read per batch: A/B in one process)
+  return !e || atoi(e) != 0;
 }
 
 // Exact rows written bucket-major per batch (DQ_FREQ_PIECES=0: the per-tile chunk layout).
@@ -5679,8 +5747,20 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
   HIP_TRY(hipMemsetAsync(f->dev_words.p, 0, (C_N + 4) * 8, nullptr));
   HIP_TRY(hipStreamSynchronize(nullptr));
   if (capacity_hint > 0) {  // the chunks phase A writes for that many rows (+ per-batch rounding)
-    const int64_t chunks = phaseA_chunks(!f->exact, false, capacity_hint, f->tile, nullptr) +
-                           2 * (capacity_hint >> 24) + 16;
+    int64_t chunks = phaseA_chunks(!f->exact, false, capacity_hint, f->tile, nullptr) +
+                     2 * (capacity_hint >> 24) + 16;
+    // one utf8 key: + the fixed-capacity bucket pieces (1.5x the rows; dq_freq_add_device), and
+    // their piece rows (growing any of them copies the table and waits for the stream)
+    const bool hp = !f->exact && n_keys == 1 && key_types[0] == DQ_UTF8 && hpieces_enabled();
+    if (hp) {
+      int64_t n_wg = 0;
+      phaseA_chunks(true, false, capacity_hint, f->tile, &n_wg);
+      n_wg += 2 * (capacity_hint >> 24) + 16;
+      const int64_t cap = (3 * (int64_t)f->tile * AKeys<true, false>::kTilesPerWg / kBuckets + 1) / 2;
+      chunks += (n_wg * kBuckets * cap + f->tile - 1) / f->tile;
+      HIP_TRY(f->pstart.ensure((size_t)n_wg * kBuckets));
+      HIP_TRY(f->plen.ensure((size_t)n_wg * kBuckets));
+    }
     dq_status st = ensure_chunks(f.get(), chunks);
     if (st != DQ_OK) return st;
     if (f->exact && pieces_enabled()) {  // the pre-pass rows too: growing them waits for the stream
@@ -5753,7 +5833,22 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
   invalidate(f);
   if (rows == 0) return DQ_OK;
   const int64_t chunks = phaseA_chunks(!f->exact, false, rows, f->tile, nullptr);
-  dq_status st = ensure_chunks(f, chunks);
+  // one utf8 key not tried by the small-key kernel: bucket pieces of fixed capacity after the
+  // batch's chunks (1.5x a workgroup's mean rows per bucket; a tile's records past a full piece
+  // stay in its chunk), so phase B reads runs of ~60 records instead of ~4 per chunk
+  const bool small = small_keys_worth_trying(f, keys[0], rows);
+  int64_t hp_wg = 0, piece_chunks = 0;
+  uint32_t hp_cap = 0;
+  if (!f->exact && n_keys == 1 && keys[0].type == DQ_UTF8 && !small && hpieces_enabled()) {
+    phaseA_chunks(true, false, rows, f->tile, &hp_wg);
+    hp_cap = (uint32_t)((3 * (int64_t)f->tile * AKeys<true, false>::kTilesPerWg / kBuckets + 1) / 2);
+    if (const char* e = getenv("DQ_FREQ_HPIECE_CAP"))  // (tests: small pieces, overflowing tiles)
+      hp_cap = (uint32_t)std::max(1, std::min(atoi(e), (int)hp_cap));
+    const int64_t recs = hp_wg * kBuckets * (int64_t)hp_cap;
+    piece_chunks = (recs + f->tile - 1) / f->tile;
+    if ((chunks + piece_chunks) * f->tile >= (int64_t)UINT32_MAX) piece_chunks = 0;  // (u32 starts)
+  }
+  dq_status st = ensure_chunks(f, chunks + piece_chunks);
   if (st != DQ_OK) return st;
   if (!f->exact) {
     // arena room for the worst case (every row its own record), see row_enc_size; a utf8 key's
@@ -5793,7 +5888,20 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     a.ks.cols[k] = KeyCol{keys[k].type, 0, keys[k].validity, keys[k].values, keys[k].data};
   a.n_items = rows;
   a.tile_items = f->tile;
-  const bool small = small_keys_worth_trying(f, keys[0], rows);
+  if (piece_chunks) {  // the piece chunks' rows hold no records; the pieces' rows of this batch
+    HIP_TRY(hipMemsetAsync(f->hist.p + (size_t)(f->n_chunks + chunks) * kHistRow, 0,
+                           (size_t)piece_chunks * kHistRow * sizeof(uint16_t), f->stream));
+    const size_t rows_need = (size_t)(f->n_prow + hp_wg) * kBuckets;
+    HIP_TRY(grow_keep(f->pstart, (size_t)f->n_prow * kBuckets, rows_need, f->stream));
+    HIP_TRY(grow_keep(f->plen, (size_t)f->n_prow * kBuckets, rows_need, f->stream));
+    a.pstart = f->pstart.p + (size_t)f->n_prow * kBuckets;
+    a.plen = f->plen.p + (size_t)f->n_prow * kBuckets;
+    a.piece_cap = hp_cap;
+    a.piece_base = (uint64_t)chunks * f->tile;
+    const unsigned long long base = (unsigned long long)f->n_chunks * f->tile;
+    for (int64_t w = 0; w < hp_wg; ++w) f->h_pbase.push_back(base);
+    f->n_prow += hp_wg;
+  }
   if (small) {
     dq_status ss = launch_phaseA_small(f, a);
     if (ss != DQ_OK) return ss;
@@ -5830,7 +5938,7 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     HIP_TRY(hipMemcpyAsync(f->fast_seen.p, a.fast_words, 8, hipMemcpyDeviceToHost, f->stream));
     f->fast_seen.last_copy = f->stream;
   }
-  f->n_chunks += chunks;
+  f->n_chunks += chunks + piece_chunks;
   f->counters_stale = true;  // read back at finalize / merge / arena growth
   return DQ_OK;
 }
@@ -6649,6 +6757,18 @@ extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src_c) {
                          reinterpret_cast<uint64_t*>(dst->recs.p), dst->hist.p, dst->n_chunks,
                          dst->tile, (uint64_t)dst->arena_used);
       HIP_TRY(hipGetLastError());
+      if (src->n_prow) {  // (the pieces' records are outside the chunk rows' counts)
+        DevBuf<unsigned long long> pb;
+        std::vector<unsigned long long> hb(src->h_pbase);
+        for (auto& b : hb) b += (unsigned long long)dst->n_chunks * dst->tile;
+        HIP_TRY(pb.ensure(hb.size()));
+        HIP_TRY(hipMemcpyAsync(pb.p, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, dst->stream));
+        hipLaunchKernelGGL(freq_rebase_pieces, dim3((unsigned)src->n_prow), dim3(256), 0, dst->stream,
+                           reinterpret_cast<uint64_t*>(dst->recs.p), src->pstart.p, src->plen.p, pb.p,
+                           (uint64_t)dst->arena_used);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(dst->stream));  // (hb and pb die here)
+      }
       dst->arena_used += src->arena_used;
     }
     if (src->n_prow) {  // the source's bucket pieces, their regions moved with its chunks
