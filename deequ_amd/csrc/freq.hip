@@ -1256,7 +1256,11 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
   __shared__ uint32_t bh[kBuckets];     // counts of the tile's raw rows, then their sorted starts
   __shared__ uint32_t gdel[kBuckets];   // region slot of a sorted position, minus that position
   __shared__ uint32_t wcur[kBuckets];   // each bucket's next region slot (the workgroup's piece)
-  __shared__ unsigned long long dkey[D], dcnt[D];
+  // fixed-capacity pieces (a.piece_cap > 0): the chunk slot of a sorted position past the piece's
+  // room, minus that position
+  __shared__ uint32_t odel[kBuckets];
+  __shared__ unsigned long long dkey[D];
+  __shared__ uint32_t dcnt[D];          // (a workgroup's rows: < 2^32)
   __shared__ uint64_t stash[T];
   __shared__ uint32_t s_wave[kAXThreads / 64];
   __shared__ uint32_t s_hits, s_bypass, s_full;
@@ -1276,11 +1280,18 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
     dkey[i] = kEmptyKey;
     dcnt[i] = 0;
   }
+  const uint32_t cap = a.piece_cap;  // 0: pieces laid out by the pre-pass's counts
   {
-    uint32_t all;
-    const uint32_t bb = block_excl_scan(a.ptot[tid], s_wave, all);  // (kAXThreads == kBuckets)
-    const uint32_t st = bb + a.ph[(int64_t)blockIdx.x * kBuckets + tid];
-    wcur[tid] = st;
+    uint32_t st;
+    if (cap) {  // piece (w, b) at piece_base + (w kBuckets + b) cap; wcur = its fill
+      st = (uint32_t)(a.piece_base + ((uint64_t)blockIdx.x * kBuckets + tid) * cap);
+      wcur[tid] = 0;
+    } else {
+      uint32_t all;
+      const uint32_t bb = block_excl_scan(a.ptot[tid], s_wave, all);  // (kAXThreads == kBuckets)
+      st = bb + a.ph[(int64_t)blockIdx.x * kBuckets + tid];
+      wcur[tid] = st;
+    }
     a.pstart[(int64_t)blockIdx.x * kBuckets + tid] = st;
     bh[tid] = 0;
     // the batch's chunk rows hold no records: empty histograms
@@ -1305,13 +1316,13 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
       if (k == kEmptyKey) {
         const unsigned long long prev = atomicCAS(&dkey[slot], kEmptyKey, (unsigned long long)h);
         if (prev == kEmptyKey) {
-          atomicAdd(&dcnt[slot], 1ULL);
+          atomicAdd(&dcnt[slot], 1u);
           return 1;
         }
         k = prev;
       }
       if (k == h) {
-        atomicAdd(&dcnt[slot], 1ULL);
+        atomicAdd(&dcnt[slot], 1u);
         return 2;
       }
       slot = (slot + 1) & (D - 1);
@@ -1413,18 +1424,44 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
       uint32_t ctotal;
       const uint32_t cnt = bh[tid];
       const uint32_t ex = block_excl_scan(cnt, s_wave, ctotal);
+      uint32_t lim = 0;  // (cap: sorted positions below ex + take go to the piece)
+      if (cap) {  // the piece takes what fits; the rest goes to this tile's chunk, bucket-sorted
+        const uint32_t take = min(cnt, cap - wcur[tid]), ovf = cnt - take;
+        uint32_t otot;
+        const uint32_t oex = block_excl_scan(ovf, s_wave, otot);
+        gdel[tid] = (uint32_t)(a.piece_base + ((uint64_t)blockIdx.x * kBuckets + tid) * cap) + wcur[tid] - ex;
+        odel[tid] = (uint32_t)(t * T) + oex - ex - take;
+        if (otot) {  // (the tile's chunk row was emptied at the start)
+          uint16_t* hrow = a.hist + t * kHistRow;
+          hrow[tid] = (uint16_t)oex;
+          if (tid == 0) hrow[kBuckets] = (uint16_t)otot;
+        }
+        wcur[tid] += take;
+        lim = ex + take;
+      } else {
+        gdel[tid] = wcur[tid] - ex;
+        wcur[tid] += cnt;
+      }
       bh[tid] = ex;
-      gdel[tid] = wcur[tid] - ex;
-      wcur[tid] += cnt;
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < R; ++j)
         if ((raw >> j) & 1u) stash[bh[bucket_of(h[j])] + rk[j]] = h[j];
       __syncthreads();
       // 4. the sorted tile to each bucket's next slots: runs of ~16 records per bucket
-      for (uint32_t i = tid; i < ctotal; i += kAXThreads) {
-        const uint64_t hh = stash[i];
-        out[(uint32_t)(gdel[bucket_of(hh)] + i)] = (hh << 8) | 1u;  // the count-1 digit code
+      if (cap) {
+        bh[tid] = lim;
+        __syncthreads();
+        for (uint32_t i = tid; i < ctotal; i += kAXThreads) {
+          const uint64_t hh = stash[i];
+          const uint32_t b = bucket_of(hh);
+          out[(uint32_t)((i < bh[b] ? gdel[b] : odel[b]) + i)] = (hh << 8) | 1u;
+        }
+      } else {
+        for (uint32_t i = tid; i < ctotal; i += kAXThreads) {
+          const uint64_t hh = stash[i];
+          out[(uint32_t)(gdel[bucket_of(hh)] + i)] = (hh << 8) | 1u;  // the count-1 digit code
+        }
       }
       __syncthreads();
       bh[tid] = 0;  // (visible after the next tile's barriers)
@@ -1433,17 +1470,51 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
   // the collapsed groups into their buckets' pieces, then the pieces' lengths
   __syncthreads();
   uint64_t maxcnt = 1;
-  for (int sl = tid; sl < D; sl += kAXThreads) {
-    const uint64_t k = dkey[sl];
-    if (k == kEmptyKey) continue;
-    const uint32_t b = bucket_of(k);
-    maxcnt = dcnt[sl] > maxcnt ? dcnt[sl] : maxcnt;
-    for_digits(dcnt[sl], [&](uint32_t code) { out[atomicAdd(&wcur[b], 1u)] = (k << 8) | code; });
+  if (cap) {  // (one dedupe slot per thread) the digits that fit the piece, the rest bucket-sorted
+              // into this workgroup's chunk
+    static_assert(D == kAXThreads, "one dedupe slot per thread");
+    odel[tid] = 0;
+    __syncthreads();
+    const uint64_t k = dkey[tid];
+    const uint32_t c = k == kEmptyKey ? 0u : dcnt[tid], b = k == kEmptyKey ? 0u : bucket_of(k);
+    uint32_t nd = 0;
+    for (uint32_t x = c; x; x >>= 2) nd += (x & 3) ? 1u : 0u;
+    const uint32_t s0 = nd ? atomicAdd(&wcur[b], nd) : 0u;
+    const uint32_t np = s0 < cap ? min(nd, cap - s0) : 0u;
+    const uint32_t o = nd > np ? atomicAdd(&odel[b], nd - np) : 0u;
+    maxcnt = c > maxcnt ? c : maxcnt;
+    __syncthreads();
+    uint32_t otot;
+    const uint32_t oex = block_excl_scan(odel[tid], s_wave, otot);
+    const int64_t wchunk = n_tiles + blockIdx.x;
+    if (otot) {
+      uint16_t* hrow = a.hist + wchunk * kHistRow;
+      hrow[tid] = (uint16_t)oex;
+      if (tid == 0) hrow[kBuckets] = (uint16_t)otot;
+    }
+    gdel[tid] = oex;
+    __syncthreads();
+    const uint64_t pb = a.piece_base + ((uint64_t)blockIdx.x * kBuckets + b) * cap;
+    uint32_t d = 0;
+    for_digits(c, [&](uint32_t code) {
+      const uint64_t slot = d < np ? pb + s0 + d : (uint64_t)wchunk * T + gdel[b] + o + (d - np);
+      out[slot] = (k << 8) | code;
+      ++d;
+    });
+  } else {
+    for (int sl = tid; sl < D; sl += kAXThreads) {
+      const uint64_t k = dkey[sl];
+      if (k == kEmptyKey) continue;
+      const uint32_t b = bucket_of(k);
+      maxcnt = dcnt[sl] > maxcnt ? dcnt[sl] : maxcnt;
+      for_digits(dcnt[sl], [&](uint32_t code) { out[atomicAdd(&wcur[b], 1u)] = (k << 8) | code; });
+    }
   }
   wave_max_lds(&s_maxcnt, maxcnt);
   __syncthreads();
   if (tid == 0 && s_maxcnt) atomicMax(&a.counters[C_MAXCNT], s_maxcnt);
-  a.plen[(int64_t)blockIdx.x * kBuckets + tid] = wcur[tid] - a.pstart[(int64_t)blockIdx.x * kBuckets + tid];
+  a.plen[(int64_t)blockIdx.x * kBuckets + tid] =
+      cap ? min(wcur[tid], cap) : wcur[tid] - a.pstart[(int64_t)blockIdx.x * kBuckets + tid];
   wave_count(&a.counters[C_NULL_ROWS], nulls);
   wave_count(&a.counters[C_NULL_GROUP], nullg);
   wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
@@ -4579,6 +4650,13 @@ static AArgs base_args(dq_freq* f) {
   return a;
 }
 
+// Exact rows into fixed-capacity bucket pieces without the pre-pass (DQ_FREQ_XFIXED=0: pieces
+// laid out by the pre-pass's counts)
+static bool xfixed_enabled() {
+  const char* e = getenv("DQ_FREQ_XFIXED");  // (read per batch: A/B in one process)
+  return !e || atoi(e) != 0;
+}
+
 // One-utf8-column rows into fixed-capacity bucket pieces (DQ_FREQ_HPIECES=0: chunks only)
 static bool hpieces_enabled() {
   const char* e = getenv("DQ_FREQ_HPIECES");  // (read per batch: A/B in one process)
@@ -4607,9 +4685,10 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
   HIP_TRY(grow_keep(f->plen, (size_t)f->n_prow * kBuckets, rows_need, f->stream));
   if (a.dense_words)
     hipLaunchKernelGGL(freq_prepass_x<true>, dim3((unsigned)n_wg), dim3(kPreThreads), 0, f->stream, a, f->ph.p);
-  else
+  else if (!a.piece_cap)  // (fixed-capacity pieces need no pre-pass)
     hipLaunchKernelGGL(freq_prepass_x<false>, dim3((unsigned)n_wg), dim3(kPreThreads), 0, f->stream, a, f->ph.p);
-  hipLaunchKernelGGL(freq_prepass_scan, dim3(kBuckets), dim3(256), 0, f->stream, f->ph.p, n_wg, f->ptot.p);
+  if (!a.piece_cap)
+    hipLaunchKernelGGL(freq_prepass_scan, dim3(kBuckets), dim3(256), 0, f->stream, f->ph.p, n_wg, f->ptot.p);
   HIP_TRY(hipGetLastError());
   if (a.dense_words) {  // the dense path first (it declines at once when the range is too wide)
     const int g = (int)std::min<int64_t>(kDenseBlocks, (a.n_items + 4 * kDenseThreads - 1) / (4 * kDenseThreads));
@@ -4640,6 +4719,7 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
   }();
   if (generic) {
     f->nan_counted = false;
+    a.piece_cap = 0;  // (the generic kernel lays pieces out by the pre-pass)
     launch_phaseA<false>(f, a, false);
   } else {
     static_assert(kAXThreads == kBuckets, "one bucket per thread");
@@ -4661,7 +4741,8 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
   const unsigned long long base = (unsigned long long)f->n_chunks * f->tile;
   for (int64_t w = 0; w < n_wg; ++w) f->h_pbase.push_back(base);
   f->n_prow += n_wg;
-  if (!a.dense_words) f->n_empty_chunks += chunks;  // (a dense batch's records are in chunk rows)
+  // (a dense batch's records are in chunk rows, and so are fixed-capacity pieces' overflows)
+  if (!a.dense_words && !a.piece_cap) f->n_empty_chunks += chunks;
   return DQ_OK;
 }
 
@@ -5752,6 +5833,13 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
     // one utf8 key: + the fixed-capacity bucket pieces (1.5x the rows; dq_freq_add_device), and
     // their piece rows (growing any of them copies the table and waits for the stream)
     const bool hp = !f->exact && n_keys == 1 && key_types[0] == DQ_UTF8 && hpieces_enabled();
+    if (f->exact && pieces_enabled() && xfixed_enabled()) {  // + exact fixed-capacity pieces
+      int64_t n_wg = 0;
+      phaseA_chunks(false, false, capacity_hint, f->tile, &n_wg);
+      n_wg += 2 * (capacity_hint >> 24) + 16;
+      const int64_t cap = (5 * (int64_t)f->tile * AKeys<false, false>::kTilesPerWg / kBuckets + 3) / 4;
+      chunks += (n_wg * kBuckets * cap + f->tile - 1) / f->tile;
+    }
     if (hp) {
       int64_t n_wg = 0;
       phaseA_chunks(true, false, capacity_hint, f->tile, &n_wg);
@@ -5837,9 +5925,22 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
   // batch's chunks (1.5x a workgroup's mean rows per bucket; a tile's records past a full piece
   // stay in its chunk), so phase B reads runs of ~60 records instead of ~4 per chunk
   const bool small = small_keys_worth_trying(f, keys[0], rows);
+  const bool xpieces = f->exact && pieces_enabled();
+  const bool dense = xpieces && dense_worth_trying(f, keys[0], rows);
   int64_t hp_wg = 0, piece_chunks = 0;
   uint32_t hp_cap = 0;
-  if (!f->exact && n_keys == 1 && keys[0].type == DQ_UTF8 && !small && hpieces_enabled()) {
+  if (xpieces && !dense && xfixed_enabled()) {
+    // exact rows into fixed-capacity pieces (1.25x a workgroup's mean rows per bucket; a tile's
+    // records past a full piece stay in its chunk): no pre-pass over the keys
+    phaseA_chunks(false, false, rows, f->tile, &hp_wg);
+    hp_cap = (uint32_t)((5 * (int64_t)f->tile * AKeys<false, false>::kTilesPerWg / kBuckets + 3) / 4);
+    if (const char* e = getenv("DQ_FREQ_XPIECE_CAP"))  // (tests: small pieces, overflowing tiles)
+      hp_cap = (uint32_t)std::max(1, std::min(atoi(e), (int)hp_cap));
+    const int64_t recs = hp_wg * kBuckets * (int64_t)hp_cap;
+    piece_chunks = (recs + f->tile - 1) / f->tile;
+    if ((chunks + piece_chunks) * f->tile >= (int64_t)UINT32_MAX) piece_chunks = 0;  // (u32 starts)
+    if (!piece_chunks) hp_cap = 0;
+  } else if (!f->exact && n_keys == 1 && keys[0].type == DQ_UTF8 && !small && hpieces_enabled()) {
     phaseA_chunks(true, false, rows, f->tile, &hp_wg);
     hp_cap = (uint32_t)((3 * (int64_t)f->tile * AKeys<true, false>::kTilesPerWg / kBuckets + 1) / 2);
     if (const char* e = getenv("DQ_FREQ_HPIECE_CAP"))  // (tests: small pieces, overflowing tiles)
@@ -5888,7 +5989,12 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     a.ks.cols[k] = KeyCol{keys[k].type, 0, keys[k].validity, keys[k].values, keys[k].data};
   a.n_items = rows;
   a.tile_items = f->tile;
-  if (piece_chunks) {  // the piece chunks' rows hold no records; the pieces' rows of this batch
+  if (piece_chunks && f->exact) {  // the piece chunks' rows hold no records
+    HIP_TRY(hipMemsetAsync(f->hist.p + (size_t)(f->n_chunks + chunks) * kHistRow, 0,
+                           (size_t)piece_chunks * kHistRow * sizeof(uint16_t), f->stream));
+    a.piece_cap = hp_cap;
+    a.piece_base = (uint64_t)chunks * f->tile;
+  } else if (piece_chunks) {  // the piece chunks' rows hold no records; the pieces' rows of this batch
     HIP_TRY(hipMemsetAsync(f->hist.p + (size_t)(f->n_chunks + chunks) * kHistRow, 0,
                            (size_t)piece_chunks * kHistRow * sizeof(uint16_t), f->stream));
     const size_t rows_need = (size_t)(f->n_prow + hp_wg) * kBuckets;
@@ -5906,8 +6012,7 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     dq_status ss = launch_phaseA_small(f, a);
     if (ss != DQ_OK) return ss;
   }
-  if (f->exact && pieces_enabled()) {
-    const bool dense = dense_worth_trying(f, keys[0], rows);
+  if (xpieces) {
     if (dense) {
       if (!f->dense_seen.p) {
         HIP_TRY(pinned_word_get(&f->dense_seen.p));

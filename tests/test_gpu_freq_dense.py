@@ -140,3 +140,38 @@ def test_runner_metrics_with_and_without_dense(gpu_device, monkeypatch):
     assert h1.number_of_bins == h2.number_of_bins
     assert sorted(x.absolute for x in h1.values.values()) == \
         sorted(x.absolute for x in h2.values.values())
+
+
+@pytest.mark.parametrize("cap", [None, "1", "9"])
+@pytest.mark.parametrize("null_as_group", [False, True])
+def test_fixed_capacity_pieces(cap, null_as_group, gpu_device, monkeypatch):
+    """Exact keys the dense path declines (wide integers, doubles) go to fixed-capacity bucket
+    pieces without the pre-pass (freq_phaseA_xp with AArgs::piece_cap): the same groups as the
+    pre-pass layout (DQ_FREQ_XFIXED=0), with the default capacity and with tiny ones that send most
+    records to the tiles' chunks, heavy keys collapsing in the dedupe table included."""
+    from deequ_amd import _native as N
+    rng = np.random.default_rng(21)
+    n = 300_001
+    v = np.concatenate([rng.integers(-10 ** 15, 10 ** 15, n - n // 3),
+                        rng.integers(0, 40, n // 3) * 10 ** 13]).astype(np.int64)
+    rng.shuffle(v)
+    mask = rng.random(n) < 0.05
+    d = (v % 1000).astype(np.float64) / 8
+    if cap:
+        monkeypatch.setenv("DQ_FREQ_XPIECE_CAP", cap)
+    monkeypatch.setenv("DQ_FREQ_DENSE", "0")
+    for arr, t in ((pa.array(v, mask=mask, type=pa.int64()), N.INT64),
+                   (pa.array(d, mask=mask, type=pa.float64()), N.FLOAT64)):
+        ft = _run(arr, t, gpu_device, 70_000, null_as_group)
+        got, s = _groups(ft), ft.summarize()
+        monkeypatch.setenv("DQ_FREQ_XFIXED", "0")
+        ft0 = _run(arr, t, gpu_device, 70_000, null_as_group)
+        monkeypatch.delenv("DQ_FREQ_XFIXED")
+        assert got == _groups(ft0)
+        s0 = ft0.summarize()
+        assert (s.n_groups, s.n_unique, s.entropy) == (s0.n_groups, s0.n_unique, s0.entropy)
+    exp = _expected(v, mask)
+    if null_as_group:
+        exp[None] = int(mask.sum())
+    assert _groups(_run(pa.array(v, mask=mask, type=pa.int64()), N.INT64, gpu_device, 70_000,
+                        null_as_group)) == exp

@@ -83,6 +83,7 @@ dense)
   timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_$T.json 2>&1 &&
   env ${AB:-DQ_FREQ_DENSE=0} timeout -k 10 400 python -u tools/bench_workloads.py c5 --steps 5 > $O/wl_c5_nodense_$T.json 2>&1 &&
   timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_$T.json 2>&1 &&
+  env ${AB:-DQ_FREQ_DENSE=0} timeout -k 10 300 python -u tools/bench_workloads.py c3 --steps 5 > $O/wl_c3_ab_$T.json 2>&1 &&
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5_$T -o run -- python3 tools/bench_workloads.py c5 --steps 2 > $O/prof_c5_$T.log 2>&1
   ;;
 hll)
