@@ -93,8 +93,10 @@ struct FM<true> {
   static constexpr int kTableC = 2560;
   static constexpr int kTarget = 1200;
 };
-// records per phase-B unit (whole chunk segments of one bucket; ~32 records per partition run)
-constexpr int kUnitTiles = 2;
+// records per phase-B unit (whole chunk segments of one bucket): hashed two tiles (~32 records per
+// partition run); exact one (8192 records: the whole-unit scatter then stages 64 KB and two
+// workgroups share a CU, configs[2] 26.3 -> 25.0 ms)
+constexpr int kUnitTilesH = 2, kUnitTilesX = 1;
 
 struct RecIn {  // == dq_freq_record
   uint64_t key;
@@ -2461,10 +2463,16 @@ __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter_u(BArgs a) {
   constexpr int W = FM<HASHED>::kRB / 8;
   constexpr int SMAX = 1 << kMaxSubBits;
   constexpr uint32_t NR = (uint32_t)PER * kThreads;
-  __shared__ UnitLds L;
+  // the segment window is dead once the unit's records are in registers, before anything is
+  // staged: one LDS region for both (PER = 8: 76 KB, two workgroups per CU)
+  __shared__ union {
+    UnitLds L;
+    uint64_t staged[NR * W];
+  } su;
+  UnitLds& L = su.L;
+  uint64_t* staged = su.staged;
   __shared__ unsigned long long gbs[SMAX];  // the unit's output base per sub-bucket
   __shared__ uint32_t hcnt[SMAX];           // the unit's count, then its local base, per sub-bucket
-  __shared__ uint64_t staged[NR * W];
   // XCD-contiguous units: workgroup g runs on XCD g % 8; XCD x takes units [x*q, (x+1)*q)
   const uint32_t g = blockIdx.x, q = (a.n_units + 7) / 8;
   const uint32_t w = (g & 7u) * q + (g >> 3);
@@ -4841,9 +4849,9 @@ static dq_status finalize_b(dq_freq* f) {
   while (s < kMaxSubBits && ((uint64_t)kBuckets << s) * (uint64_t)target < R) ++s;
   static const int unit_tiles = [] {  // DQ_FREQ_UNIT_TILES: A/B hook for the phase-B unit size
     const char* e = getenv("DQ_FREQ_UNIT_TILES");
-    return e ? std::max(1, atoi(e)) : kUnitTiles;
+    return e ? std::max(1, atoi(e)) : 0;
   }();
-  const uint64_t H = (uint64_t)f->tile * unit_tiles;
+  const uint64_t H = (uint64_t)f->tile * (unit_tiles ? unit_tiles : f->exact ? kUnitTilesX : kUnitTilesH);
   uint32_t u = 0;
   for (int b = 0; b < kBuckets; ++b) {
     f->h_unit_start[b] = u;
@@ -4945,6 +4953,8 @@ static dq_status finalize_b(dq_freq* f) {
     hipLaunchKernelGGL((freq_phaseB_scatter_p<false, 16>), dim3(pgrid), dim3(kThreads), 0, f->stream, a);
   } else if (bsub == 0 && !f->exact && H <= kUnitH && !b3u) {
     hipLaunchKernelGGL((freq_phaseB_scatter_p<true, 4>), dim3(pgrid), dim3(kThreads), 0, f->stream, a);
+  } else if (bsub == 0 && f->exact && H <= kUnitX / 2) {  // (64 KB staged: two workgroups per CU)
+    hipLaunchKernelGGL((freq_phaseB_scatter_u<false, 8>), dim3(grid), dim3(kThreads), 0, f->stream, a);
   } else if (bsub == 0 && f->exact && H <= kUnitX) {
     hipLaunchKernelGGL((freq_phaseB_scatter_u<false, 16>), dim3(grid), dim3(kThreads), 0, f->stream, a);
   } else if (bsub == 0 && !f->exact && H <= kUnitH) {
