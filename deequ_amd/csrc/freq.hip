@@ -4938,14 +4938,15 @@ static dq_status finalize_b(dq_freq* f) {
     return e ? atoi(e) : 0;
   }();
   constexpr uint64_t kUnitX = 16 * kThreads, kUnitH = 4 * kThreads;  // whole-unit capacities
-  // exact units: one per workgroup (measured faster than the persistent form, configs[2]: 5.08
-  // vs 5.61 ms); hashed units: persistent.  DQ_FREQ_B3U=1 / DQ_FREQ_B3P=1: A/B hooks
+  // one unit per workgroup (measured faster than the persistent form: exact, configs[2] 5.08 vs
+  // 5.61 ms; hashed, configs[4] 678 vs 826 us per launch once the segment window shares the
+  // staging LDS and two workgroups fit a CU).  DQ_FREQ_B3U=1 / DQ_FREQ_B3P=1: A/B hooks
   static const int b3_env = [] {
     const char* e = getenv("DQ_FREQ_B3U");
     const char* p = getenv("DQ_FREQ_B3P");
     return e && atoi(e) ? 1 : (p && atoi(p) ? 2 : 0);
   }();
-  const bool b3u = b3_env == 1 || (b3_env == 0 && f->exact);
+  const bool b3u = b3_env != 2;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, f->device);
   const unsigned pgrid = (unsigned)std::max(8, cus / 8 * 8);  // one per CU (LDS), XCD multiple
