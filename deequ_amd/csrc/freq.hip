@@ -5301,6 +5301,99 @@ struct SmallEntry {
   unsigned long long h, count;
   uint32_t w[8];
 };
+// freq_small_marginal's per-wave lists of the small sides merged on the device (one workgroup per
+// side): values claimed by hash in an LDS table, counts added, then every entry's words checked
+// against the first entry of its hash -- the host reads a few KB instead of every wave's list (12.6
+// MB for a 1.2e8-group joint, ~4 ms of copies and map inserts).  out_n[k]: the merged values, or
+// kSmallMergeHost (more values than the table takes: the host merges the lists as before), or
+// kSmallMergeClash (two values on one hash, or the side failed: not small).
+constexpr int kSmallMergeSlots = 1024, kSmallMerged = 512;
+constexpr uint32_t kSmallMergeHost = 0xFFFFFFFFu, kSmallMergeClash = 0xFFFFFFFEu;
+__global__ void __launch_bounds__(1024) freq_small_merge(const SmallEntry* __restrict__ ent,
+                                                         const uint32_t* __restrict__ nout, int64_t nw,
+                                                         const unsigned int* __restrict__ fail,
+                                                         SmallEntry* __restrict__ out, uint32_t* __restrict__ out_n) {
+  constexpr int S = kSmallMergeSlots;
+  constexpr unsigned long long kFree = ~0ULL;
+  __shared__ unsigned long long s_h[S], s_c[S], s_first[S];
+  __shared__ uint32_t s_w[S][8];
+  __shared__ uint32_t s_full, s_clash;
+  const int k = blockIdx.x, tid = threadIdx.x;
+  if (fail[k]) {
+    if (tid == 0) out_n[k] = kSmallMergeClash;
+    return;
+  }
+  for (int i = tid; i < S; i += blockDim.x) {
+    s_h[i] = kFree;
+    s_c[i] = 0;
+    s_first[i] = kFree;
+  }
+  if (tid == 0) s_full = s_clash = 0;
+  __syncthreads();
+  const int64_t ne = nw * kSmallMarg;
+  // the slot of entry x's hash (claimed when `claim`), or S: none / the table is full
+  auto slot_of = [&](const SmallEntry& e, bool claim) -> uint32_t {
+    uint32_t sl = (uint32_t)e.h & (S - 1);
+    for (int pr = 0; pr < S; ++pr, sl = (sl + 1) & (S - 1)) {
+      const unsigned long long old = claim ? atomicCAS(&s_h[sl], kFree, e.h) : s_h[sl];
+      if (old == e.h || (claim && old == kFree)) return sl;
+      if (!claim && old == kFree) return S;
+    }
+    return S;
+  };
+  for (int64_t x = tid; x < ne; x += blockDim.x) {  // claims, counts, the first entry per value
+    const int64_t gwv = x / kSmallMarg;
+    if ((uint32_t)(x % kSmallMarg) >= nout[gwv * 2 + k]) continue;
+    const SmallEntry& e = ent[(gwv * 2 + k) * kSmallMarg + x % kSmallMarg];
+    const uint32_t sl = e.h == kFree ? (uint32_t)S : slot_of(e, true);
+    if (sl == (uint32_t)S) {
+      s_full = 1;
+      continue;
+    }
+    atomicAdd(&s_c[sl], e.count);
+    atomicMin(&s_first[sl], (unsigned long long)x);
+  }
+  __syncthreads();
+  if (s_full) {
+    if (tid == 0) out_n[k] = kSmallMergeHost;
+    return;
+  }
+  for (int64_t x = tid; x < ne; x += blockDim.x) {  // the first entry of each value: its words
+    const int64_t gwv = x / kSmallMarg;
+    if ((uint32_t)(x % kSmallMarg) >= nout[gwv * 2 + k]) continue;
+    const SmallEntry& e = ent[(gwv * 2 + k) * kSmallMarg + x % kSmallMarg];
+    const uint32_t sl = slot_of(e, false);
+    if (sl < (uint32_t)S && s_first[sl] == (unsigned long long)x)
+      for (int j = 0; j < 8; ++j) s_w[sl][j] = e.w[j];
+  }
+  __syncthreads();
+  for (int64_t x = tid; x < ne; x += blockDim.x) {  // every entry's words against its value's
+    const int64_t gwv = x / kSmallMarg;
+    if ((uint32_t)(x % kSmallMarg) >= nout[gwv * 2 + k]) continue;
+    const SmallEntry& e = ent[(gwv * 2 + k) * kSmallMarg + x % kSmallMarg];
+    const uint32_t sl = slot_of(e, false);
+    bool eq = sl < (uint32_t)S;
+    for (int j = 0; j < 8 && eq; ++j) eq = s_w[sl][j] == e.w[j];
+    if (!eq) s_clash = 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t m = 0;
+    for (int sl = 0; sl < S && m <= (uint32_t)kSmallMerged; ++sl) {
+      if (s_h[sl] == kFree) continue;
+      if (m < (uint32_t)kSmallMerged) {
+        SmallEntry o;
+        o.h = s_h[sl];
+        o.count = s_c[sl];
+        for (int j = 0; j < 8; ++j) o.w[j] = s_w[sl][j];
+        out[(int64_t)k * kSmallMerged + m] = o;
+      }
+      ++m;
+    }
+    out_n[k] = s_clash ? kSmallMergeClash : (m > (uint32_t)kSmallMerged ? kSmallMergeHost : m);
+  }
+}
+
 // A side's part of an encoded key from the 16 words loaded at the key's start: its word count,
 // its row hash (utf8 <= 16 bytes and fixed-width from the words; longer utf8 from memory) and
 // its first 8 words (a side with a longer key is not aggregated here)
@@ -6209,17 +6302,40 @@ extern "C" dq_status dq_freq_mutual_information(dq_freq* joint, double* mi, int*
     unsigned int hf[2];
     HIP_TRY(d2h(hf, sfail.p, 8, stream));
     if (!hf[0] || !hf[1]) {  // merge the waves' lists of each small side by (hash, words)
-      std::vector<uint32_t> hn((size_t)nw * 2);
-      std::vector<SmallEntry> he((size_t)nw * 2 * kSmallMarg);
-      HIP_TRY(d2h(hn.data(), nout.p, hn.size() * 4, stream));
-      HIP_TRY(d2h(he.data(), ent.p, he.size() * sizeof(SmallEntry), stream));
+      DevBuf<SmallEntry> mo;
+      DevBuf<uint32_t> mn;
+      HIP_TRY(mo.ensure(2 * (size_t)kSmallMerged));
+      HIP_TRY(mn.ensure(2));
+      hipLaunchKernelGGL(freq_small_merge, dim3(2), dim3(1024), 0, stream, ent.p, nout.p, nw, sfail.p, mo.p, mn.p);
+      HIP_TRY(hipGetLastError());
+      uint32_t hm[2];
+      HIP_TRY(d2h(hm, mn.p, 8, stream));
+      const char* hmg = getenv("DQ_FREQ_MI_HOSTMERGE");  // =1: the host merge (A/B, tests)
+      if (hmg && atoi(hmg))
+        for (int k = 0; k < 2; ++k)
+          if (hm[k] != kSmallMergeClash) hm[k] = kSmallMergeHost;
+      std::vector<SmallEntry> hme(2 * (size_t)kSmallMerged);
+      HIP_TRY(d2h(hme.data(), mo.p, hme.size() * sizeof(SmallEntry), stream));
+      // (the host merge of every wave's list, for a side the device table could not take)
+      std::vector<uint32_t> hn;
+      std::vector<SmallEntry> he;
+      if ((!hf[0] && hm[0] == kSmallMergeHost) || (!hf[1] && hm[1] == kSmallMergeHost)) {
+        hn.resize((size_t)nw * 2);
+        he.resize((size_t)nw * 2 * kSmallMarg);
+        HIP_TRY(d2h(hn.data(), nout.p, hn.size() * 4, stream));
+        HIP_TRY(d2h(he.data(), ent.p, he.size() * sizeof(SmallEntry), stream));
+      }
       for (int k = 0; k < 2; ++k) {
-        if (hf[k]) continue;
+        if (hf[k] || hm[k] == kSmallMergeClash) continue;
+        const bool host = hm[k] == kSmallMergeHost;
+        // (merged on the device: one list of hm[k] entries, as if from one wave)
+        const int64_t lists = host ? nw : 1;
         std::map<uint64_t, std::pair<std::array<uint32_t, 8>, uint64_t>> vals;
         bool ok = true;
-        for (int64_t gwv = 0; gwv < nw && ok; ++gwv)
-          for (uint32_t c = 0; c < hn[gwv * 2 + k] && ok; ++c) {
-            const SmallEntry& e = he[((size_t)gwv * 2 + k) * kSmallMarg + c];
+        for (int64_t gwv = 0; gwv < lists && ok; ++gwv)
+          for (uint32_t c = 0; c < (host ? hn[gwv * 2 + k] : hm[k]) && ok; ++c) {
+            const SmallEntry& e = host ? he[((size_t)gwv * 2 + k) * kSmallMarg + c]
+                                       : hme[(size_t)k * kSmallMerged + c];
             std::array<uint32_t, 8> wv;
             for (int q = 0; q < 8; ++q) wv[q] = e.w[q];
             auto it = vals.find(e.h);

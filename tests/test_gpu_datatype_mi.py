@@ -197,6 +197,12 @@ def test_mutual_information_small_marginals(kinds, cards, gpu_device, monkeypatc
                                     {"a": okind.get(kinds[0], kinds[0]),
                                      "b": okind.get(kinds[1], kinds[1])}), "a", "b")
     assert abs(got - exp) <= 1e-12 * max(1.0, abs(exp)), (got, exp)
+    # the waves' lists merged on the host instead of by freq_small_merge: the same value counts,
+    # so the same bits
+    monkeypatch.setenv("DQ_FREQ_MI_HOSTMERGE", "1")
+    host = MutualInformation("a", "b").calculate(df).value.get()
+    assert host == got, (host, got)
+    monkeypatch.delenv("DQ_FREQ_MI_HOSTMERGE")
     monkeypatch.setenv("DQ_FREQ_MI_NOSMALL", "1")
     ref = MutualInformation("a", "b").calculate(df).value.get()
     assert abs(got - ref) <= 1e-12 * max(1.0, abs(ref)), (got, ref)
