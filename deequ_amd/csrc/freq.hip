@@ -375,6 +375,88 @@ DQ_DEV void multi_short_key(const KeySet& ks, int64_t r, uint64_t& k0, uint64_t&
   k1 = w[1];
 }
 
+// Two-utf8-column keys (the MutualInformation joints of string columns) in phase A: each row's
+// offsets, then <= 16 bytes per value as the aligned dwords that hold them (STR1's row loads), so
+// a thread issues every round's loads before it uses any; the row hash, short key and encoding
+// are row_hash_hashed_dw's, multi_short_key's and row_encode_dw's, computed from registers.
+struct Str2Row {
+  int32_t s0[2], len[2];
+  int sh[2];
+  uint32_t d[2][5];
+};
+DQ_DEV bool str2_key(const KeySet& ks) {
+  return ks.n_keys == 2 && ks.cols[0].type == DQ_UTF8 && ks.cols[1].type == DQ_UTF8 && !ks.null_as_group;
+}
+DQ_DEV void str2_offsets(const KeySet& ks, int64_t r, Str2Row& x) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int32_t* off = reinterpret_cast<const int32_t*>(ks.cols[c].values);
+    x.s0[c] = off[r];
+    x.len[c] = off[r + 1];
+  }
+}
+// (after str2_offsets' loads: len becomes the length; a value that is empty, NULL or longer
+// than 16 bytes reads its column's first offset instead, always mapped)
+DQ_DEV void str2_bytes(const KeySet& ks, Str2Row& x) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    x.len[c] -= x.s0[c];
+    const bool reg = x.len[c] > 0 && x.len[c] <= 16;
+    const uint8_t* p = reg ? ks.cols[c].data + x.s0[c] : reinterpret_cast<const uint8_t*>(ks.cols[c].values);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+    x.sh[c] = (int)(reinterpret_cast<uintptr_t>(p) & 3u);
+    const int last = reg ? ((x.sh[c] + x.len[c] + 3) >> 2) - 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) x.d[c][k] = q[k < last ? k : last];
+  }
+}
+DQ_DEV void str2_words(const Str2Row& x, int c, uint64_t& w0, uint64_t& w1) {
+  w0 = w1 = 0;
+  if (x.len[c] > 0 && x.len[c] <= kHash16Max) str16_from_dwords(x.d[c], x.sh[c], x.len[c], w0, w1);
+}
+DQ_DEV uint64_t str2_hash(const KeySet& ks, const Str2Row& x, uint64_t& k0, uint64_t& k1) {
+  uint64_t h = kRowHashSeed, sw[2];
+  bool shrt = true;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    uint64_t w0, w1;
+    str2_words(x, c, w0, w1);
+    const uint64_t ch = x.len[c] <= kHash16Max ? str_hash16(w0, w1, x.len[c], 17 + c)
+                                               : str_hash_long_dev(ks.cols[c].data + x.s0[c], x.len[c], c);
+    h = fold_col_hash(h, ch);
+    shrt = shrt && x.len[c] <= 7;
+    sw[c] = w0 | ((uint64_t)(uint32_t)x.len[c] << 56);
+  }
+  k0 = shrt ? sw[0] : 0;
+  k1 = shrt ? sw[1] : kNoShort;
+  return fmix_bij(h);
+}
+DQ_DEV uint32_t str2_enc_size(const Str2Row& x) {
+  return 16 + pad4((uint32_t)x.len[0]) + pad4((uint32_t)x.len[1]);
+}
+DQ_DEV void str2_encode(const KeySet& ks, const Str2Row& x, uint32_t* dst) {
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    *dst++ = 1;
+    *dst++ = (uint32_t)x.len[c];
+    if (x.len[c] <= kHash16Max) {
+      uint64_t w0, w1;
+      str2_words(x, c, w0, w1);
+      const uint32_t d[4] = {(uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (4 * q < x.len[c]) *dst++ = d[q];
+    } else {
+      const uint8_t* b = ks.cols[c].data + x.s0[c];
+      for (int32_t q = 0; q < x.len[c]; q += 4) {
+        uint32_t w = 0;
+        for (int k = 0; k < 4 && q + k < x.len[c]; ++k) w |= (uint32_t)b[q + k] << (8 * k);
+        *dst++ = w;
+      }
+    }
+  }
+}
+
 template <bool HASHED, bool FROM_REC>
 struct AKeys {
   static constexpr int kDedupe = FROM_REC ? (HASHED ? 128 : 256) : (HASHED ? 256 : 512);
@@ -419,6 +501,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
   // workgroups per CU has 1.7 KB left)
   __shared__ uint16_t wfill[STR1 ? kBuckets : 1];
   const bool hpieces = STR1 && a.pstart != nullptr;
+  const bool str2 = HASHED && !FROM_REC && !STR1 && str2_key(a.ks);  // (block-uniform)
 
   const int tid = threadIdx.x;
   if constexpr (STR1) {
@@ -813,6 +896,44 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
           ssk1[q] = k1;
         }
       }
+    } else if (str2) {  // two utf8 columns: two rounds' loads in flight at a time, then hash
+      constexpr int G = 2;  // (rounds per group: four held 64 more VGPRs and spilled)
+#pragma unroll 1
+      for (int j0 = 0; j0 < ROUNDS; j0 += G) {
+        Str2Row x[G];
+        uint32_t byte[2][G];
+        int64_t ic[G];
+        uint32_t ok = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int64_t i = i0 + (int64_t)(j0 + g) * kThreads + tid;
+          ok |= (i < i1 ? 1u : 0u) << g;
+          ic[g] = i < i1 ? i : i1 - 1;
+          str2_offsets(a.ks, ic[g], x[g]);
+#pragma unroll
+          for (int c = 0; c < 2; ++c) byte[c][g] = a.ks.cols[c].valid ? a.ks.cols[c].valid[ic[g] >> 3] : 0xffu;
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) str2_bytes(a.ks, x[g]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          if (!((ok >> g) & 1u)) continue;
+          const bool valid = ((byte[0][g] & byte[1][g]) >> (ic[g] & 7)) & 1u;
+          if (!valid) {  // a NULL key: the row is skipped (row_kind)
+            ++nulls;
+            continue;
+          }
+          const int j = j0 + g, q = j * kThreads + tid;
+          uint64_t k0, k1;
+          keyed |= 1u << j;
+          stash[q * W] = str2_hash(a.ks, x[g], k0, k1);
+          stash[q * W + 1] = (uint64_t)ic[g];
+          if constexpr (SK) {
+            ssk0[q] = k0;
+            ssk1[q] = k1;
+          }
+        }
+      }
     } else {  // several key columns
 #pragma unroll 1
       for (int j = 0; j < ROUNDS; ++j) {
@@ -939,7 +1060,21 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
       continue;
     }
     uint64_t need = 0;
-    if constexpr (HASHED && !FROM_REC) {
+    // two utf8 columns: every raw round's offsets loaded together, then the bytes needed
+    auto str2_raw_offsets = [&](Str2Row (&x)[ROUNDS]) {
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j)
+        str2_offsets(a.ks, (raw >> j) & 1u ? (int64_t)stash[(j * kThreads + tid) * W + 1] : i0, x[j]);
+    };
+    if (HASHED && !FROM_REC && !STR1 && str2) {
+      Str2Row x[ROUNDS];
+      str2_raw_offsets(x);
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j)
+        need += (raw >> j) & 1u ? 16u + pad4((uint32_t)(x[j].len[0] - x[j].s0[0])) +
+                                      pad4((uint32_t)(x[j].len[1] - x[j].s0[1]))
+                                : 0u;
+    } else if constexpr (HASHED && !FROM_REC) {
 #pragma unroll 1
       for (int j = 0; j < ROUNDS; ++j)
         if ((raw >> j) & 1u) {
@@ -1017,6 +1152,37 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         reinterpret_cast<ulonglong2*>(out)[i] = v;
       }
       if ((ctotal & 1u) && tid == 0) out[ctotal - 1] = stash[ctotal - 1];
+    } else if (HASHED && !FROM_REC && !STR1 && str2) {
+      // two utf8 columns: each round's arena bytes (one LDS atomic per wave and round) and
+      // encodings
+      constexpr int G = 2;  // rounds whose values are in flight together (again: L2 hits)
+#pragma unroll 1
+      for (int j0 = 0; j0 < ROUNDS; j0 += G) {
+        Str2Row x[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+          str2_offsets(a.ks, (raw >> (j0 + g)) & 1u ? (int64_t)stash[((j0 + g) * kThreads + tid) * W + 1] : i0,
+                       x[g]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) str2_bytes(a.ks, x[g]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {  // (wave-uniform trip count)
+          const int j = j0 + g;
+          const bool on = (raw >> j) & 1u;
+          const int q = j * kThreads + tid;
+          const uint32_t sz = on ? str2_enc_size(x[g]) : 0u;
+          const uint32_t incl = __ockl_wfscan_add_u32(sz, true);
+          const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+          unsigned long long wbase = 0;
+          if (__lane_id() == 63 && wtot) wbase = atomicAdd(&s_arena_cur, (unsigned long long)wtot);
+          wbase = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(wbase >> 32), 63) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wbase, 63);
+          if (!on) continue;
+          const uint64_t off = s_arena_base + wbase + (incl - sz);
+          str2_encode(a.ks, x[g], reinterpret_cast<uint32_t*>(a.arena + off));
+          put(t, stash[q * W], 1u, off);
+        }
+      }
     } else if constexpr (HASHED && !FROM_REC) {
       // row keys into the arena: each wave reserves its round's bytes with one LDS atomic (a
       // per-row atomic on the one cursor word serialised every row of the tile)

@@ -729,3 +729,44 @@ def test_many_small_key_tables_reuse_pinned_words(gpu_device):
             exp[k] = exp.get(k, 0) + 1
         assert dict(top) == exp and bins == len(exp), i
         del ft
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("offset", [0, 3])
+def test_two_string_columns_all_length_classes(offset, gpu_device):
+    """Two utf8 key columns (MutualInformation joints of string columns) take phase A's
+    two-column path: both values' offsets and <= 16 bytes loaded as aligned dwords for two rounds
+    at once, the row hash and encoding from registers.  Values of every length class (empty,
+    <= 7 bytes: short keys, 8..16, > 16: the long hash and byte encoding), NULLs in either column,
+    high cardinality (most rows go to the arena raw) and sliced batches: the groups, Σ[c==1] and
+    the entropy vs the oracle."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    from oracle import deequ_oracle as O
+    rng = np.random.default_rng(41 + offset)
+    n = 150_000 + offset
+    stems = ["", "q", "abcdefg", "abcdefgh", "0123456789abcdef", "a value over sixteen bytes",
+             "x" * 40]
+
+    def col(card):
+        v = rng.integers(0, card, n)
+        s = rng.integers(0, len(stems), n)
+        m = rng.random(n) < 0.05
+        return pa.array([None if mm else (stems[ss] + (str(vv) if ss else ""))[: 60]
+                         for vv, ss, mm in zip(v, s, m)], pa.string())
+    a, b = col(40_000), col(30)
+    t = pa.table({"a": a, "b": b}).slice(offset)
+    ot = O.OTable({"a": t.column("a").to_pylist(), "b": t.column("b").to_pylist()},
+                  {"a": "string", "b": "string"})
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=37_000)
+    ft = FrequencyTable(["a", "b"], [df.schema["a"].dtype, df.schema["b"].dtype], 0)
+    for bt in df.batches:
+        ft.add([bt["a"], bt["b"]])
+    exp = O.frequencies(ot, ["a", "b"])
+    s = ft.summarize()
+    assert s.n_groups == len(exp)
+    assert s.n_unique == sum(1 for c in exp.values() if c == 1)
+    assert dict(ft.export()) == exp
+    # (~1e5 groups: the oracle's running sum drifts by ~1e-12; the terms summed exactly instead)
+    m = t.num_rows
+    assert _rel_close(s.entropy, math.fsum(-(c / m) * math.log(c / m) for c in exp.values()))
