@@ -461,7 +461,9 @@ template <bool HASHED, bool FROM_REC>
 struct AKeys {
   static constexpr int kDedupe = FROM_REC ? (HASHED ? 128 : 256) : (HASHED ? 256 : 512);
   // a workgroup's rows: counts < 4^(kTile / kDedupe), so the digits of every entry fit
-  static constexpr int kTilesPerWg = FROM_REC ? 1 : (HASHED ? 15 : 16);
+  // (records: tiles of tile / max-digits records, so many per workgroup -- one per workgroup made a
+  // 1.2e8-record marginal 234 K workgroups and as many workgroup chunks)
+  static constexpr int kTilesPerWg = FROM_REC ? 16 : (HASHED ? 15 : 16);
   // the string rows: 512-thread workgroups, two per CU (LDS <= 80 KB, <= 128 VGPRs), so one
   // workgroup's load latency overlaps the other's hashing and dedupe between their barriers
   static constexpr int kThreads = HASHED && !FROM_REC ? 512 : 1024;
@@ -4696,8 +4698,8 @@ static dq_status push_counters(dq_freq* f) {
 // Chunks one phase-A launch over n items writes: one per tile + one per workgroup.
 static int64_t phaseA_chunks(bool hashed, bool from_rec, int64_t n_items, int64_t tile_items,
                              int64_t* n_wg_out) {
-  const int tpw = from_rec ? 1 : (hashed ? AKeys<true, false>::kTilesPerWg
-                                         : AKeys<false, false>::kTilesPerWg);
+  const int tpw = from_rec ? (hashed ? AKeys<true, true>::kTilesPerWg : AKeys<false, true>::kTilesPerWg)
+                           : (hashed ? AKeys<true, false>::kTilesPerWg : AKeys<false, false>::kTilesPerWg);
   const int64_t tiles = (n_items + tile_items - 1) / tile_items;
   const int64_t n_wg = (tiles + tpw - 1) / tpw;
   if (n_wg_out) *n_wg_out = n_wg;
