@@ -5498,7 +5498,6 @@ __global__ void __launch_bounds__(1024) freq_small_merge(const SmallEntry* __res
   }
   if (tid == 0) s_full = s_clash = 0;
   __syncthreads();
-  const int64_t ne = nw * kSmallMarg;
   // the slot of entry x's hash (claimed when `claim`), or S: none / the table is full
   auto slot_of = [&](const SmallEntry& e, bool claim) -> uint32_t {
     uint32_t sl = (uint32_t)e.h & (S - 1);
@@ -5509,41 +5508,39 @@ __global__ void __launch_bounds__(1024) freq_small_merge(const SmallEntry* __res
     }
     return S;
   };
-  for (int64_t x = tid; x < ne; x += blockDim.x) {  // claims, counts, the first entry per value
-    const int64_t gwv = x / kSmallMarg;
-    if ((uint32_t)(x % kSmallMarg) >= nout[gwv * 2 + k]) continue;
-    const SmallEntry& e = ent[(gwv * 2 + k) * kSmallMarg + x % kSmallMarg];
+  // a thread per wave list (its count read once); f(e, x) for each entry x of side k
+  auto for_entries = [&](auto&& f) {
+    for (int64_t gwv = tid; gwv < nw; gwv += blockDim.x) {
+      const uint32_t nl = nout[gwv * 2 + k];
+      for (uint32_t c = 0; c < nl; ++c) f(ent[(gwv * 2 + k) * kSmallMarg + c], gwv * kSmallMarg + c);
+    }
+  };
+  for_entries([&](const SmallEntry& e, int64_t x) {  // claims, counts, the first entry per value
     const uint32_t sl = e.h == kFree ? (uint32_t)S : slot_of(e, true);
     if (sl == (uint32_t)S) {
       s_full = 1;
-      continue;
+      return;
     }
     atomicAdd(&s_c[sl], e.count);
     atomicMin(&s_first[sl], (unsigned long long)x);
-  }
+  });
   __syncthreads();
   if (s_full) {
     if (tid == 0) out_n[k] = kSmallMergeHost;
     return;
   }
-  for (int64_t x = tid; x < ne; x += blockDim.x) {  // the first entry of each value: its words
-    const int64_t gwv = x / kSmallMarg;
-    if ((uint32_t)(x % kSmallMarg) >= nout[gwv * 2 + k]) continue;
-    const SmallEntry& e = ent[(gwv * 2 + k) * kSmallMarg + x % kSmallMarg];
+  for_entries([&](const SmallEntry& e, int64_t x) {  // the first entry of each value: its words
     const uint32_t sl = slot_of(e, false);
     if (sl < (uint32_t)S && s_first[sl] == (unsigned long long)x)
-      for (int j = 0; j < 8; ++j) s_w[sl][j] = e.w[j];
-  }
+      for (int q = 0; q < 8; ++q) s_w[sl][q] = e.w[q];
+  });
   __syncthreads();
-  for (int64_t x = tid; x < ne; x += blockDim.x) {  // every entry's words against its value's
-    const int64_t gwv = x / kSmallMarg;
-    if ((uint32_t)(x % kSmallMarg) >= nout[gwv * 2 + k]) continue;
-    const SmallEntry& e = ent[(gwv * 2 + k) * kSmallMarg + x % kSmallMarg];
+  for_entries([&](const SmallEntry& e, int64_t) {  // every entry's words against its value's
     const uint32_t sl = slot_of(e, false);
     bool eq = sl < (uint32_t)S;
-    for (int j = 0; j < 8 && eq; ++j) eq = s_w[sl][j] == e.w[j];
+    for (int q = 0; q < 8 && eq; ++q) eq = s_w[sl][q] == e.w[q];
     if (!eq) s_clash = 1;
-  }
+  });
   __syncthreads();
   if (tid == 0) {
     uint32_t m = 0;
