@@ -879,6 +879,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
           } else {
             h = fmix_bij(fold_col_hash(kRowHashSeed, str_hash_long_dev(c.data + s0[j], len[j], 0)));
           }
+          // a key without a short form carries its offset and length instead (k0 is only read
+          // beside a short k1), so its arena copy needs no second read of the offsets
+          if (k1 == kNoShort) k0 = ((uint64_t)(uint32_t)len[j] << 32) | (uint32_t)s0[j];
         } else {
           // a NULL row.  Histogram: the NULL rows are one group kept apart (C_NULL_GROUP), so
           // this table also serves the column's grouping; the caller folds it into the
@@ -1076,7 +1079,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         need += (raw >> j) & 1u ? 16u + pad4((uint32_t)(x[j].len[0] - x[j].s0[0])) +
                                       pad4((uint32_t)(x[j].len[1] - x[j].s0[1]))
                                 : 0u;
-    } else if constexpr (HASHED && !FROM_REC) {
+    } else if constexpr (HASHED && !FROM_REC && !STR1) {  // (STR1 reserved its arena up front)
 #pragma unroll 1
       for (int j = 0; j < ROUNDS; ++j)
         if ((raw >> j) & 1u) {
@@ -1194,7 +1197,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         const int q = j * kThreads + tid;
         const int64_t row = on ? (int64_t)stash[q * W + 1] : 0;
         const uint64_t k0 = SK && on ? ssk0[q] : 0, k1 = SK && on ? ssk1[q] : kNoShort;
-        uint32_t sz = on ? enc_size_sk(row, k1) : 0u;
+        // (STR1: a long key's offset and length from k0)
+        uint32_t sz = !on ? 0u : STR1 && k1 == kNoShort ? 8u + pad4((uint32_t)(k0 >> 32)) : enc_size_sk(row, k1);
         if constexpr (STR1) sz = (sz + 15u) & ~15u;  // 16-byte aligned keys: vector stores
         const uint32_t incl = __ockl_wfscan_add_u32(sz, true);
         const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
@@ -1208,8 +1212,8 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
           if (k1 != kNoShort) {
             str1_encode_short16(k0, k1, reinterpret_cast<uint32_t*>(a.arena + off));
           } else {
-            const SView v = str1_view(a.ks, row);
-            str1_encode_copy16(v.p, v.len, reinterpret_cast<uint32_t*>(a.arena + off));
+            str1_encode_copy16(a.ks.cols[0].data + (uint32_t)k0, (int32_t)(k0 >> 32),
+                               reinterpret_cast<uint32_t*>(a.arena + off));
           }
         } else {
           row_encode_dw(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
