@@ -2500,6 +2500,67 @@ __global__ void __launch_bounds__(kThreads) freq_phaseB_count(BArgs a) {
   for (int i = threadIdx.x; i < S; i += kThreads) row[i] = sh[i];
 }
 
+// B1, one wave per unit: the sixteen waves of a workgroup count sixteen units each on its own, in
+// a histogram of its own in LDS, with no block barrier -- a unit's chain of dependent loads
+// (unit -> bucket -> segments -> records) overlaps fifteen others' instead of stalling its
+// workgroup (one unit per 1024-thread workgroup left ~two chains in flight per CU).  Same counts.
+constexpr int kBcWaves = 16;
+template <bool HASHED>
+__global__ void __launch_bounds__(kBcWaves * 64) freq_phaseB_count_w(BArgs a) {
+  constexpr int W = FM<HASHED>::kRB / 8, PB = 8;
+  __shared__ uint32_t sh[kBcWaves][1 << kMaxSubBits];
+  __shared__ uint32_t s_pos[kBcWaves][64];
+  __shared__ unsigned long long s_st[kBcWaves][64];
+  const int lane = (int)__lane_id(), wv = threadIdx.x >> 6;
+  const uint32_t w = blockIdx.x * kBcWaves + (uint32_t)wv;
+  if (w >= a.n_units) return;  // (wave-uniform: nothing below waits for the other waves)
+  const int S = 1 << a.s;
+  uint32_t* h = sh[wv];
+  for (int i = lane; i < S; i += 64) h[i] = 0;
+  const uint32_t b = a.unit_b[w];
+  const int64_t n = a.nseg[b];
+  const uint32_t* P = a.segP + (int64_t)b * (a.J + 1);
+  const uint32_t lo = (w - a.unit_start[b]) * a.H;
+  const uint32_t hi = (uint32_t)min((uint64_t)lo + a.H, (uint64_t)P[n]);
+  const int64_t c0 = min((int64_t)a.unit_c0[w], n);
+  const int64_t c1 = w + 1 < a.unit_start[b + 1] ? min((int64_t)a.unit_c0[w + 1] + 1, n) : n;
+  for (int64_t cw = c0; cw < c1; cw += 64) {  // windows of 64 segments, a lane each
+    const int64_t c = cw + lane;
+    uint32_t len = 0;
+    unsigned long long st = 0;
+    if (c < c1) {
+      const uint32_t ps = P[c], pe = P[c + 1];
+      const uint32_t a0 = max(ps, lo), a1 = min(pe, hi);
+      len = a1 > a0 ? a1 - a0 : 0u;
+      st = a.segS[(int64_t)b * a.J + c] + (a0 - ps);
+    }
+    const uint32_t incl = __ockl_wfscan_add_u32(len, true);
+    const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    s_pos[wv][lane] = incl - len;
+    s_st[wv][lane] = st;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the window, before any lane reads it
+    const uint32_t nwin = (uint32_t)min((int64_t)64, c1 - cw);
+    for (uint32_t base = 0; base < wtot; base += (uint32_t)PB * 64) {
+      uint64_t rv[PB];
+#pragma unroll
+      for (int k = 0; k < PB; ++k) {
+        uint32_t li = base + (uint32_t)k * 64 + (uint32_t)lane;
+        li = li < wtot ? li : wtot - 1;
+        const uint32_t j = seg_of(s_pos[wv], nwin, li);
+        rv[k] = reinterpret_cast<const uint64_t*>(a.recs)[(s_st[wv][j] + (li - s_pos[wv][j])) * W];
+      }
+#pragma unroll
+      for (int k = 0; k < PB; ++k)
+        if (base + (uint32_t)k * 64 + (uint32_t)lane < wtot)
+          atomicAdd(&h[sub_of(HASHED ? rv[k] : rv[k] >> 8, a.s)], 1u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every lane's reads of the window done
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // every count in
+  uint32_t* row = a.uhist + (int64_t)w * S;
+  for (int i = lane; i < S; i += 64) row[i] = h[i];
+}
+
 // B2: per bucket, each unit's offset inside every partition, and the partitions' sizes
 __global__ void __launch_bounds__(kThreads) freq_phaseB_scan(BArgs a) {
   const uint32_t b = blockIdx.x, S = 1u << a.s;
@@ -5085,7 +5146,16 @@ static dq_status finalize_b(dq_freq* f) {
   a.uhist = f->uhist.p;
   a.part_base = f->part_base.p;
   a.recsB = f->recsB.p;
-  if (f->exact)
+  static const bool count_w = [] {  // DQ_FREQ_BCOUNT_WAVE=0: A/B hook, a workgroup per unit
+    const char* e = getenv("DQ_FREQ_BCOUNT_WAVE");
+    return !(e && atoi(e) == 0);
+  }();
+  const unsigned ugrid = (unsigned)((u + kBcWaves - 1) / kBcWaves);
+  if (count_w && f->exact)
+    hipLaunchKernelGGL(freq_phaseB_count_w<false>, dim3(ugrid), dim3(kBcWaves * 64), 0, f->stream, a);
+  else if (count_w)
+    hipLaunchKernelGGL(freq_phaseB_count_w<true>, dim3(ugrid), dim3(kBcWaves * 64), 0, f->stream, a);
+  else if (f->exact)
     hipLaunchKernelGGL(freq_phaseB_count<false>, dim3(u), dim3(kThreads), 0, f->stream, a);
   else
     hipLaunchKernelGGL(freq_phaseB_count<true>, dim3(u), dim3(kThreads), 0, f->stream, a);
