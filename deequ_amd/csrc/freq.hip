@@ -91,7 +91,10 @@ struct FM<true> {
   static constexpr int kRB = 16;
   static constexpr int kDedupe = 1024;
   static constexpr int kTableC = 2560;
-  static constexpr int kTarget = 1200;
+  // (freq_phaseC_h takes up to 4096 records and 3584 groups per partition: ~1900-record partitions
+  // halve its per-item costs against ~950, configs[4] 176.3 -> 171.5 ms, A/B
+  // DQ_FREQ_PARTITION_TARGET_H)
+  static constexpr int kTarget = 2400;
 };
 // records per phase-B unit (whole chunk segments of one bucket): hashed two tiles (~32 records per
 // partition run); exact one (8192 records: the whole-unit scatter then stages 64 KB and two
@@ -5078,6 +5081,8 @@ static dq_status finalize_b(dq_freq* f) {
   // test hook: a small target forces deep partitioning (all s) on small inputs, a huge one the
   // recount path of overflowing partitions
   if (const char* e = getenv("DQ_FREQ_PARTITION_TARGET")) target = std::max(1, atoi(e));
+  if (const char* e = getenv("DQ_FREQ_PARTITION_TARGET_H"))  // (A/B: hashed tables only)
+    if (!f->exact) target = std::max(1, atoi(e));
   int s = 0;
   while (s < kMaxSubBits && ((uint64_t)kBuckets << s) * (uint64_t)target < R) ++s;
   static const int unit_tiles = [] {  // DQ_FREQ_UNIT_TILES: A/B hook for the phase-B unit size
