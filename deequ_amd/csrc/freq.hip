@@ -5085,6 +5085,15 @@ static dq_status finalize_b(dq_freq* f) {
     if (!f->exact) target = std::max(1, atoi(e));
   int s = 0;
   while (s < kMaxSubBits && ((uint64_t)kBuckets << s) * (uint64_t)target < R) ++s;
+  // exact tables: one level shallower when the partitions stay packed (pk_ok: s >= kMinPkSubBits,
+  // record counts within the count field) and hold <= kTargetPk records on average -- packed
+  // slots take up to 4096 -- so phase C's per-item costs cover twice the records (configs[2]
+  // 24.75 -> 24.2 ms); a shallower table would fall to the two-word slots (configs[4] +29 ms)
+  constexpr uint64_t kTargetPk = 3700;
+  if (f->exact && !getenv("DQ_FREQ_PARTITION_TARGET"))
+    while (s - 1 >= kMinPkSubBits && ((uint64_t)kBuckets << (s - 1)) * kTargetPk >= R &&
+           f->h_counters[C_MAXCNT] < (1ULL << (s - 1 - 3)))
+      --s;
   static const int unit_tiles = [] {  // DQ_FREQ_UNIT_TILES: A/B hook for the phase-B unit size
     const char* e = getenv("DQ_FREQ_UNIT_TILES");
     return e ? std::max(1, atoi(e)) : 0;
