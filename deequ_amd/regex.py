@@ -165,6 +165,17 @@ class Anchor:
     kind: str  # "^", "$", "\\b"
 
 
+@dataclass(frozen=True)
+class DollarLook(Look):
+    """Java's $ inside a pattern, as the lookahead (?=(\\r\\n|[line terminator])?END)."""
+
+
+@dataclass(frozen=True)
+class EndText:
+    """Inside a lookahead only: the text ends here (the anchors inside a pattern, see
+    _rewrite_inner_anchors)."""
+
+
 EMPTY = Seq(())
 
 
@@ -425,7 +436,7 @@ def nullable(n) -> bool:
         return n.lo == 0 or nullable(n.node)
     if isinstance(n, Group):
         return nullable(n.node)
-    if isinstance(n, (Look, Anchor)):
+    if isinstance(n, (Look, Anchor, EndText)):
         return True
     if isinstance(n, BackRef):
         return True  # conservatively (the group may match "")
@@ -583,15 +594,18 @@ def _split(a: int, b: int, n: int) -> List[List[Tuple[int, int]]]:
 
 
 class NFA:
-    """Thompson-style NFA: trans[s] = list of (symbol bitmask, t); eps[s] = list of t."""
+    """Thompson-style NFA: trans[s] = list of (symbol bitmask, t); eps[s] = list of t; at0[s] =
+    list of t reached without input only at the start of the text (an inner `^`)."""
 
     def __init__(self):
         self.trans: List[List[Tuple[int, int]]] = []
         self.eps: List[List[int]] = []
+        self.at0: List[List[int]] = []
 
     def new(self) -> int:
         self.trans.append([])
         self.eps.append([])
+        self.at0.append([])
         return len(self.trans) - 1
 
 
@@ -613,15 +627,16 @@ class DFA:
         return len(self.nxt)
 
 
-def determinize(nfa: NFA, start: int, finals: FrozenSet[int], univ: int = -1) -> DFA:
+def determinize(nfa: NFA, start: int, finals: FrozenSet[int], univ: int = -1,
+                at_start: bool = True) -> DFA:
     """Subset construction.  `univ` (optional) is a state whose language is everything (Sigma* EOT):
     a subset containing it is that state alone, which keeps the search automaton from tracking
     candidates once one has matched."""
-    def closure(states):
+    def closure(states, at_start=False):
         stack, seen = list(states), set(states)
         while stack:
             s = stack.pop()
-            for t in nfa.eps[s]:
+            for t in nfa.eps[s] + (nfa.at0[s] if at_start else []):
                 if t not in seen:
                     seen.add(t)
                     stack.append(t)
@@ -632,7 +647,7 @@ def determinize(nfa: NFA, start: int, finals: FrozenSet[int], univ: int = -1) ->
     def canon(t):
         return u0 if u0 is not None and univ in t else t
 
-    s0 = canon(closure([start]))
+    s0 = canon(closure([start], at_start=at_start))
     index: Dict[FrozenSet[int], int] = {s0: 0}
     order = [s0]
     nxt: List[List[int]] = []
@@ -848,6 +863,13 @@ class _Compiler:
             mark = self.nfa.new()
             self.pending.append((s, mark, node))  # before cont: lookaheads after it come later
             cont(mark)
+        elif isinstance(node, Anchor) and node.kind == "^":  # the start of the text only
+            t = self.nfa.new()
+            self.nfa.at0[s].append(t)
+            cont(t)
+        elif isinstance(node, EndText):  # (in a lookahead: the next symbol ends the text)
+            self.nfa.trans[s].append((1 << EOT, self.final))
+            cont(self.nfa.new())  # (nothing follows the end)
         elif isinstance(node, Anchor):
             raise PatternNotSupported(f"anchor {node.kind} inside the pattern")
         elif isinstance(node, BackRef):
@@ -855,9 +877,39 @@ class _Compiler:
         else:
             raise TypeError(node)
 
+    def check_inner_anchors(self):
+        """Before the lookaheads are resolved: an inner ^ must not follow a lookahead (its
+        continuation is compiled as if inside the text), and an inner $ must not follow a byte
+        \\r (Java's $ never matches between \\r and \\n; its lookahead would)."""
+        nfa = self.nfa
+        for s, mark, node in self.pending:
+            seen, stack = {mark}, [mark]
+            while stack:
+                q = stack.pop()
+                if nfa.at0[q]:
+                    raise PatternNotSupported("^ after a lookahead or $ inside the pattern")
+                for t in nfa.eps[q] + [t for _, t in nfa.trans[q]]:
+                    if t not in seen:
+                        seen.add(t)
+                        stack.append(t)
+            if isinstance(node, DollarLook):
+                pred, stack = {s}, [s]
+                while stack:  # states that reach s without input
+                    q = stack.pop()
+                    for u in range(len(nfa.eps)):
+                        if u not in pred and (q in nfa.eps[u] or q in nfa.at0[u]):
+                            pred.add(u)
+                            stack.append(u)
+                for u in range(len(nfa.trans)):
+                    if any(t in pred and (m >> 13) & 1 for m, t in nfa.trans[u]):
+                        raise PatternNotSupported("$ after a pattern that may end in \\r")
+
     def resolve_lookaheads(self):
         for s, mark, node in reversed(self.pending):
-            d_cont = minimize(determinize(self.nfa, mark, frozenset([self.final]), self.univ))
+            # (a continuation starts inside the text: no inner ^ is reachable from it, checked by
+            # check_inner_anchors)
+            d_cont = minimize(determinize(self.nfa, mark, frozenset([self.final]), self.univ,
+                                          at_start=False))
             x = _Compiler()
             xs = x.nfa.new()
             x.final = x.nfa.new()
@@ -978,9 +1030,7 @@ def compile_java_regex(pattern: str) -> CompiledRegex:
         # whether it is the non-empty one depends on the match PREFERENCE (greedy / lazy,
         # alternation order), modelled by an ordered-thread automaton
         return compile_nullable(pattern, Seq(tuple(items)))
-    body = expand_backrefs(Seq(tuple(items)))
-    if _has_anchor(body):
-        raise PatternNotSupported("anchors or \\b inside the pattern")
+    body = _rewrite_inner_anchors(expand_backrefs(Seq(tuple(items))))
     if nullable(body):
         raise PatternNotSupported(
             "a pattern that can match the empty string next to an anchor, a lookaround or a "
@@ -1036,6 +1086,7 @@ def compile_java_regex(pattern: str) -> CompiledRegex:
             c.nfa.eps[st].append(c.univ)
 
     c.build(body, p, tail)
+    c.check_inner_anchors()
     c.resolve_lookaheads()
     d = minimize(determinize(c.nfa, s0, frozenset([c.final]), c.univ))
     return _finish(pattern, d)
@@ -1225,6 +1276,34 @@ def compile_nullable(pattern: str, ast) -> CompiledRegex:
         row[EOT] = ACC if b_end == 2 else REJ
     d = minimize(DFA(table, accept, s0))
     return _finish(pattern, d)
+
+
+_LINE_END = Alt((Seq((Chars(((13, 13),)), Chars(((10, 10),)))), Chars(LINE_TERMINATORS)))
+
+
+def _rewrite_inner_anchors(n, in_look: bool = False):
+    """Anchors inside a (non-nullable) pattern: $ and \\Z become the lookahead "at most one
+    line terminator, then the end" (DollarLook), \\z the lookahead "the end", ^ and \\A an edge
+    taken only at the start of the text (NFA.at0); \\b inside a pattern is refused."""
+    if isinstance(n, Anchor):
+        if n.kind == "$":
+            return DollarLook(Seq((Repeat(_LINE_END, 0, 1), EndText())), False)
+        if n.kind == "\\z":
+            return Look(EndText(), False)
+        if n.kind == "^" and not in_look:
+            return n
+        raise PatternNotSupported(f"anchor {n.kind} inside the pattern")
+    if isinstance(n, Seq):
+        return Seq(tuple(_rewrite_inner_anchors(x, in_look) for x in n.items))
+    if isinstance(n, Alt):
+        return Alt(tuple(_rewrite_inner_anchors(x, in_look) for x in n.options))
+    if isinstance(n, Group):
+        return Group(_rewrite_inner_anchors(n.node, in_look), n.index)
+    if isinstance(n, Repeat):
+        return Repeat(_rewrite_inner_anchors(n.node, in_look), n.lo, n.hi, n.greedy)
+    if isinstance(n, Look):
+        return type(n)(_rewrite_inner_anchors(n.node, True), n.negative)
+    return n
 
 
 def _has_anchor(n) -> bool:

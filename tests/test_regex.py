@@ -61,6 +61,15 @@ FUZZ = [
     (r"a\d$", "a1\r\n\u2028x", 7),
     (r"a\d\Z", "a1\r\n\u0085", 7),
     (r"a\d\z", "a1\r\n", 6),
+    # anchors inside the pattern: ^ / \A only at the start of the text, $ / \Z / \z as
+    # lookaheads at the end (before one final terminator for $ and \Z)
+    (r"(^|,)ab", "ab,x", 7),
+    (r"ab($|,)", "ab,\n\r", 7),
+    (r"(^|;)[a-c]+($|;)", "abc;d\n", 8),
+    (r"x(?:\z|y)", "xy\n", 6),
+    (r"(?:\Ab|c)d", "bcd\u2028", 6),
+    (r"a(\Z|b)c?", "abc\r\n\u0085", 7),
+    (r"(?:q|^)r(?:s|$)", "qrs \n", 6),
 ]
 
 
@@ -113,7 +122,10 @@ def test_nullable_known_answers():
 
 
 @pytest.mark.parametrize("pattern", [r"(?<=a)b", r"a++", r"x\Bz", r"a\s$", r"a*$", r"(?s)a",
-                                     r"(?=x)a*", r"(a?)\1"])
+                                     r"(?=x)a*", r"(a?)\1",
+                                     # inner anchors the automaton cannot decide: a $ after a
+                                     # possible \r, a ^ after a lookahead, \b inside, ^ in a loop
+                                     r"(?:a|\r)$x?", r"(?=a)(^|b)a", r"a\bb", r"(?:^a)+"])
 def test_unsupported_patterns_are_refused(pattern):
     with pytest.raises(PatternNotSupported):
         compile_java_regex(pattern)
