@@ -156,6 +156,14 @@ class Look:
 
 
 @dataclass(frozen=True)
+class Behind:
+    """(?<=X) / (?<!X): the text before the position (from the text's start) ends / does not end
+    with a string of X (X of bounded length, as Java requires)."""
+    node: object
+    negative: bool
+
+
+@dataclass(frozen=True)
 class BackRef:
     index: int
 
@@ -288,6 +296,10 @@ class _Parser:
                 neg = self.s[self.i + 1] == "!"
                 self.i += 2
                 node = Look(self.alt(), neg)
+            elif self.s.startswith("?<=", self.i) or self.s.startswith("?<!", self.i):
+                neg = self.s[self.i + 2] == "!"
+                self.i += 3
+                node = Behind(self.alt(), neg)
             elif self.peek() == "?":
                 self.error("unsupported group construct (lookbehind, named group or inline flag)")
             else:
@@ -367,9 +379,7 @@ class _Parser:
         elif c.isdigit() and not in_class:
             return BackRef(int(c))
         elif c in "bB" and not in_class:
-            if c == "B":
-                self.error("\\B")
-            return Anchor("\\b")
+            return Anchor("\\b" if c == "b" else "\\B")
         elif c in "AzZ" and not in_class:
             return Anchor({"A": "^", "Z": "$", "z": "\\z"}[c])
         elif c.isalnum():
@@ -436,11 +446,33 @@ def nullable(n) -> bool:
         return n.lo == 0 or nullable(n.node)
     if isinstance(n, Group):
         return nullable(n.node)
-    if isinstance(n, (Look, Anchor, EndText)):
+    if isinstance(n, (Look, Anchor, EndText, Behind)):
         return True
     if isinstance(n, BackRef):
         return True  # conservatively (the group may match "")
     raise TypeError(n)
+
+
+def max_length(n) -> Optional[int]:
+    """The most code points a match of `n` spans, or None when unbounded."""
+    if isinstance(n, Chars):
+        return 1
+    if isinstance(n, Seq):
+        parts = [max_length(x) for x in n.items]
+        return None if any(p is None for p in parts) else sum(parts)
+    if isinstance(n, Alt):
+        parts = [max_length(x) for x in n.options]
+        return None if any(p is None for p in parts) else max(parts, default=0)
+    if isinstance(n, Group):
+        return max_length(n.node)
+    if isinstance(n, Repeat):
+        if n.hi == 0:
+            return 0
+        inner = max_length(n.node)
+        return None if n.hi is None or inner is None else n.hi * inner
+    if isinstance(n, (Look, Anchor, Behind, EndText)):
+        return 0
+    return None
 
 
 def finite_strings(n, limit=64) -> Optional[List[str]]:
@@ -505,8 +537,8 @@ def _subst(n, index: int, value: str):
         return Alt(tuple(_subst(x, index, value) for x in n.options))
     if isinstance(n, Repeat):
         return Repeat(_subst(n.node, index, value), n.lo, n.hi)
-    if isinstance(n, Look):
-        return Look(_subst(n.node, index, value), n.negative)
+    if isinstance(n, (Look, Behind)):
+        return type(n)(_subst(n.node, index, value), n.negative)
     return n
 
 
@@ -521,7 +553,7 @@ def _find_group(n, index):
                 g = _find_group(x, index)
                 if g is not None:
                     return g
-    if isinstance(n, (Repeat, Look)):
+    if isinstance(n, (Repeat, Look, Behind)):
         return _find_group(n.node, index)
     return None
 
@@ -534,7 +566,7 @@ def _backrefs(n) -> List[int]:
         if hasattr(n, attr):
             for x in getattr(n, attr):
                 out += _backrefs(x)
-    if isinstance(n, (Repeat, Look, Group)):
+    if isinstance(n, (Repeat, Look, Group, Behind)):
         out += _backrefs(n.node)
     return out
 
@@ -601,11 +633,14 @@ class NFA:
         self.trans: List[List[Tuple[int, int]]] = []
         self.eps: List[List[int]] = []
         self.at0: List[List[int]] = []
+        # (k, t): taken when lookbehind k holds at this position (determinize's `behinds`)
+        self.behind: List[List[Tuple[int, int]]] = []
 
     def new(self) -> int:
         self.trans.append([])
         self.eps.append([])
         self.at0.append([])
+        self.behind.append([])
         return len(self.trans) - 1
 
 
@@ -628,7 +663,62 @@ class DFA:
 
 
 def determinize(nfa: NFA, start: int, finals: FrozenSet[int], univ: int = -1,
-                at_start: bool = True) -> DFA:
+                at_start: bool = True, behinds=()) -> DFA:
+    """(behinds: per lookbehind k, (its suffix DFA -- accepting iff the text read so far ends
+    with a string of its body -- and whether it is negative); a DFA state is then the NFA subset
+    with every suffix DFA's state, and nfa.behind edges are followed where lookbehind k holds.)"""
+    if behinds:
+        return _determinize_behind(nfa, start, finals, univ, behinds)
+    return _determinize(nfa, start, finals, univ, at_start)
+
+
+def _determinize_behind(nfa: NFA, start: int, finals: FrozenSet[int], univ: int, behinds) -> DFA:
+    def closure(states, at_start, sig):
+        stack, seen = list(states), set(states)
+        while stack:
+            s = stack.pop()
+            nxt = list(nfa.eps[s]) + (nfa.at0[s] if at_start else [])
+            nxt += [t for k, t in nfa.behind[s]
+                    if behinds[k][0].accept[sig[k]] != behinds[k][1]]
+            for t in nxt:
+                if t not in seen:
+                    seen.add(t)
+                    stack.append(t)
+        return frozenset(seen)
+
+    sig0 = tuple(d.start for d, _ in behinds)
+    u0 = (closure([univ], False, sig0), ()) if univ >= 0 else None
+
+    def canon(key):
+        return u0 if u0 is not None and univ in key[0] else key
+
+    k0 = canon((closure([start], True, sig0), sig0))
+    index = {k0: 0}
+    order = [k0]
+    nxt, accept = [], []
+    i = 0
+    while i < len(order):
+        cur, sig = order[i]
+        i += 1
+        accept.append(bool(cur & finals))
+        edges = [(m, t) for s in cur for m, t in nfa.trans[s]]
+        row = [0] * NSYM
+        for sym in range(NSYM):
+            tgt = frozenset(t for m, t in edges if (m >> sym) & 1)
+            sig2 = tuple(d.nxt[q][sym] for (d, _), q in zip(behinds, sig))
+            key = canon((closure(tgt, False, sig2), sig2)) if tgt else (frozenset(), ())
+            if key not in index:
+                if len(order) >= MAX_STATES:
+                    raise PatternNotSupported(f"automaton exceeds {MAX_STATES} states")
+                index[key] = len(order)
+                order.append(key)
+            row[sym] = index[key]
+        nxt.append(row)
+    return DFA(nxt, accept, 0)
+
+
+def _determinize(nfa: NFA, start: int, finals: FrozenSet[int], univ: int = -1,
+                 at_start: bool = True) -> DFA:
     """Subset construction.  `univ` (optional) is a state whose language is everything (Sigma* EOT):
     a subset containing it is that state alone, which keeps the search automaton from tracking
     candidates once one has matched."""
@@ -790,6 +880,7 @@ class _Compiler:
         self.final = -1
         self._univ = -1
         self.pending: List[Tuple[int, int, object]] = []
+        self.behinds: List[Tuple[DFA, bool]] = []  # (suffix DFA, negative) per lookbehind
 
     @property
     def univ(self) -> int:
@@ -867,6 +958,20 @@ class _Compiler:
             t = self.nfa.new()
             self.nfa.at0[s].append(t)
             cont(t)
+        elif isinstance(node, Behind):  # an edge taken where the text so far ends with node
+            if _has_look(node.node) or _backrefs(node.node):
+                raise PatternNotSupported("a lookaround, anchor or back-reference in a lookbehind")
+            if max_length(node.node) is None:  # (Java: "no obvious maximum length")
+                raise PatternNotSupported("lookbehind without a bounded length")
+            x = _Compiler()
+            xs = x.nfa.new()
+            x.final = x.nfa.new()
+            x.build(node.node, x.anything(xs), lambda st: x.nfa.eps[st].append(x.final))
+            d = minimize(determinize(x.nfa, xs, frozenset([x.final])))
+            t = self.nfa.new()
+            self.nfa.behind[s].append((len(self.behinds), t))
+            self.behinds.append((d, node.negative))
+            cont(t)
         elif isinstance(node, EndText):  # (in a lookahead: the next symbol ends the text)
             self.nfa.trans[s].append((1 << EOT, self.final))
             cont(self.nfa.new())  # (nothing follows the end)
@@ -886,8 +991,9 @@ class _Compiler:
             seen, stack = {mark}, [mark]
             while stack:
                 q = stack.pop()
-                if nfa.at0[q]:
-                    raise PatternNotSupported("^ after a lookahead or $ inside the pattern")
+                if nfa.at0[q] or nfa.behind[q]:
+                    raise PatternNotSupported("^, \\b or a lookbehind after a lookahead or $ "
+                                              "inside the pattern")
                 for t in nfa.eps[q] + [t for _, t in nfa.trans[q]]:
                     if t not in seen:
                         seen.add(t)
@@ -897,7 +1003,8 @@ class _Compiler:
                 while stack:  # states that reach s without input
                     q = stack.pop()
                     for u in range(len(nfa.eps)):
-                        if u not in pred and (q in nfa.eps[u] or q in nfa.at0[u]):
+                        if u not in pred and (q in nfa.eps[u] or q in nfa.at0[u] or
+                                              any(t == q for _, t in nfa.behind[u])):
                             pred.add(u)
                             stack.append(u)
                 for u in range(len(nfa.trans)):
@@ -925,7 +1032,7 @@ class _Compiler:
 
 
 def _has_look(n) -> bool:
-    if isinstance(n, (Look, Anchor)):
+    if isinstance(n, (Look, Anchor, Behind)):
         return True
     for attr in ("items", "options"):
         if hasattr(n, attr):
@@ -942,7 +1049,7 @@ def _may_end_with(node, cp: int) -> bool:
         return any(a <= cp <= b for a, b in node.ranges)
     if isinstance(node, Seq):
         for x in reversed(node.items):
-            if isinstance(x, (Look, Anchor)):
+            if isinstance(x, (Look, Anchor, Behind)):
                 continue
             if _may_end_with(x, cp):
                 return True
@@ -969,7 +1076,7 @@ def _first_last_word(node, last: bool) -> Optional[bool]:
     if isinstance(node, Seq):
         items = list(reversed(node.items)) if last else list(node.items)
         for x in items:
-            if isinstance(x, (Look, Anchor)):
+            if isinstance(x, (Look, Anchor, Behind)):
                 continue
             r = _first_last_word(x, last)
             if nullable(x):
@@ -1021,9 +1128,10 @@ def compile_java_regex(pattern: str) -> CompiledRegex:
     ast = _Parser(pattern).parse()
     items = list(ast.items) if isinstance(ast, Seq) else [ast]
     start_anchor = end_anchor = None
-    if items and isinstance(items[0], Anchor):
+    # (anchors the edge handling below decides; any other one is an inner anchor)
+    if items and isinstance(items[0], Anchor) and items[0].kind in ("^", "\\b"):
         start_anchor = items.pop(0).kind
-    if items and isinstance(items[-1], Anchor):
+    if items and isinstance(items[-1], Anchor) and items[-1].kind in ("$", "\\z", "\\b"):
         end_anchor = items.pop().kind
     if nullable(Seq(tuple(items))) and start_anchor in (None, "^") and end_anchor is None:
         # the empty match at offset 0 always succeeds, so find()'s first match starts there:
@@ -1088,7 +1196,7 @@ def compile_java_regex(pattern: str) -> CompiledRegex:
     c.build(body, p, tail)
     c.check_inner_anchors()
     c.resolve_lookaheads()
-    d = minimize(determinize(c.nfa, s0, frozenset([c.final]), c.univ))
+    d = minimize(determinize(c.nfa, s0, frozenset([c.final]), c.univ, behinds=c.behinds))
     return _finish(pattern, d)
 
 
@@ -1284,7 +1392,8 @@ _LINE_END = Alt((Seq((Chars(((13, 13),)), Chars(((10, 10),)))), Chars(LINE_TERMI
 def _rewrite_inner_anchors(n, in_look: bool = False):
     """Anchors inside a (non-nullable) pattern: $ and \\Z become the lookahead "at most one
     line terminator, then the end" (DollarLook), \\z the lookahead "the end", ^ and \\A an edge
-    taken only at the start of the text (NFA.at0); \\b inside a pattern is refused."""
+    taken only at the start of the text (NFA.at0); \\b / \\B the lookbehind-and-lookahead pairs
+    of Java's Bound."""
     if isinstance(n, Anchor):
         if n.kind == "$":
             return DollarLook(Seq((Repeat(_LINE_END, 0, 1), EndText())), False)
@@ -1292,6 +1401,10 @@ def _rewrite_inner_anchors(n, in_look: bool = False):
             return Look(EndText(), False)
         if n.kind == "^" and not in_look:
             return n
+        if n.kind in ("\\b", "\\B") and not in_look:  # Java's Bound over \b's word characters
+            w = Chars(bound_word_chars())
+            b = n.kind == "\\b"  # \b: the two sides differ; \B: they agree
+            return Alt((Seq((Behind(w, False), Look(w, b))), Seq((Behind(w, True), Look(w, not b)))))
         raise PatternNotSupported(f"anchor {n.kind} inside the pattern")
     if isinstance(n, Seq):
         return Seq(tuple(_rewrite_inner_anchors(x, in_look) for x in n.items))
@@ -1301,7 +1414,7 @@ def _rewrite_inner_anchors(n, in_look: bool = False):
         return Group(_rewrite_inner_anchors(n.node, in_look), n.index)
     if isinstance(n, Repeat):
         return Repeat(_rewrite_inner_anchors(n.node, in_look), n.lo, n.hi, n.greedy)
-    if isinstance(n, Look):
+    if isinstance(n, (Look, Behind)):
         return type(n)(_rewrite_inner_anchors(n.node, True), n.negative)
     return n
 

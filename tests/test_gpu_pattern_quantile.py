@@ -83,7 +83,10 @@ def test_pattern_match_floating_point_columns_match_oracle(pattern, dtype, gpu_d
                                      r"\d*", r"\d*?", r"(?i)http", r"(?i)HT(?-i)tp?s*",
                                      r"[0-9]*(\.[0-9]+)?", r"(a|ae)*?x?", r"^\s*[a-z]*",
                                      # anchors inside the pattern
-                                     r"(^|/)ht(tp|$)", r"(?:\Ax|o)[a-z]+(?: |\z)"])
+                                     r"(^|/)ht(tp|$)", r"(?:\Ax|o)[a-z]+(?: |\z)",
+                                     # lookbehind and \b / \B inside the pattern
+                                     r"(?<=/)[a-z]{2}", r"(?<!\d)\d{3}(?!\d)", r"t\Bp",
+                                     r"\b[a-z]+\b:"])
 def test_pattern_match_matches_oracle_on_random_rows(pattern, gpu_device):
     from deequ_amd.analyzers import PatternMatch
     from oracle.deequ_oracle import OTable, agg_pattern_match

@@ -70,6 +70,15 @@ FUZZ = [
     (r"(?:\Ab|c)d", "bcd\u2028", 6),
     (r"a(\Z|b)c?", "abc\r\n\u0085", 7),
     (r"(?:q|^)r(?:s|$)", "qrs \n", 6),
+    # lookbehind (bounded, as Java requires) and \b / \B inside a pattern: suffix automata run
+    # from the text's start beside the subset construction
+    (r"(?<=a)b", "abcab ba", 7),
+    (r"(?<!a)b", "abcab ba", 7),
+    (r"x(?<=ax)y", "axyxyaxy", 8),
+    (r"(?<!\d)\d{3}(?!\d)", "1234 567 89x", 10),
+    (r"ab\b|cd", "ab cd abx", 8),
+    (r"x\By", "xy x y", 6),
+    (r"\b\d+\b ", "12 3a 45 ", 9),
 ]
 
 
@@ -121,11 +130,14 @@ def test_nullable_known_answers():
     assert not compile_java_regex(r"(?:a??)+b?").matches("ab")
 
 
-@pytest.mark.parametrize("pattern", [r"(?<=a)b", r"a++", r"x\Bz", r"a\s$", r"a*$", r"(?s)a",
-                                     r"(?=x)a*", r"(a?)\1",
+@pytest.mark.parametrize("pattern", [r"a++", r"a\s$", r"a*$", r"(?s)a", r"(?=x)a*", r"(a?)\1",
                                      # inner anchors the automaton cannot decide: a $ after a
-                                     # possible \r, a ^ after a lookahead, \b inside, ^ in a loop
-                                     r"(?:a|\r)$x?", r"(?=a)(^|b)a", r"a\bb", r"(?:^a)+"])
+                                     # possible \r, a ^ after a lookahead, ^ in a loop
+                                     r"(?:a|\r)$x?", r"(?=a)(^|b)a", r"(?:^a)+",
+                                     # lookbehinds: unbounded (Java refuses it too), holding a
+                                     # lookaround, in a lookahead's continuation, in a loop
+                                     r"(?<=a+)b", r"(?<=(?=a)a)b", r"(?=a)a(?<=a)b", r"(?:(?<=a)b)+",
+                                     r"(?=a)a\bb"])
 def test_unsupported_patterns_are_refused(pattern):
     with pytest.raises(PatternNotSupported):
         compile_java_regex(pattern)
