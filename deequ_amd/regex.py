@@ -20,9 +20,13 @@ negation, nested escapes and \\d \\D \\s \\S \\w \\W (ASCII, as Java without UNI
 groups ( ), (?: ), alternation, greedy / lazy quantifiers * + ? {n} {n,} {n,m}, lookaheads (?= )
 (?! ), back-references to groups with a finite language (expanded: the CREDITCARD separators),
 ^ / \\A at the start; $ / \\Z (end, or before one final line terminator, "\\r\\n" included) and
-\\z (strict end) at the end; \\b at the start or end of the pattern; the case flag (?i) (?-i)
-(?i: ) (?-i: ) anywhere (ASCII case folding, Java without UNICODE_CASE; to the end of the
-enclosing group, alternatives included).
+\\z (strict end) at the end; \\b at the start or end of the pattern; anchors, \\b / \\B and
+bounded lookbehinds inside the pattern (see _rewrite_inner_anchors); the embedded flags
+(?idmsux-idmsux) and (?idmsux-idmsux: ) anywhere, each to the end of the enclosing group,
+alternatives included: i (ASCII case folding, Java without UNICODE_CASE), d (UNIX_LINES), m
+(MULTILINE: Pattern.java's Caret / Dollar(true) and their UNIX_LINES forms), s (DOTALL), x
+(COMMENTS: white space and #-comments skipped wherever Java's parser peeks, classes included), u
+(no effect without i).
 
 Nullable patterns (``\\d*``, ``(?i)x?y*``, ``[0-9]*(\\.[0-9]+)?``): the empty match at offset 0
 always exists, so find()'s first match starts there and the row counts iff Java's PREFERRED
@@ -31,8 +35,9 @@ match at offset 0 is non-empty -- compiled from a priority-ordered thread automa
 consuming nothing ends its loop), with no anchor but a leading ^.
 
 Rejected (a PatternNotSupported error, never a silently different answer): nullable patterns with
-a lookaround, back-reference or trailing anchor, possessive quantifiers, lookbehind, flags other
-than i, \\b / anchors elsewhere, $ after a pattern that may end in "\\r" (Java's $ never matches
+a lookaround, back-reference or trailing anchor, possessive quantifiers, unbounded lookbehinds,
+the flags U and i with u, anchors / lookbehinds the automaton cannot place (after a lookahead, in
+a quantifier or a lookaround), $ after a pattern that may end in "\\r" (Java's $ never matches
 between "\\r\\n"), and automata above ``MAX_STATES``.
 
 \\b is Java's Bound: a word character is '_' or Character.isLetterOrDigit (categories L* and Nd),
@@ -91,6 +96,7 @@ WORD = cs_norm([(48, 57), (65, 90), (95, 95), (97, 122)])
 SPACE = cs_norm([(9, 13), (32, 32)])  # [ \t\n\x0B\f\r]
 LINE_TERMINATORS = cs_norm([(10, 10), (13, 13), (0x85, 0x85), (0x2028, 0x2029)])
 DOT = cs_neg(LINE_TERMINATORS)
+DOT_UNIX = cs_neg(((10, 10),))  # . under UNIX_LINES
 ANY = ((0, MAX_CP),)
 # \b's word characters are decided exactly in these blocks (see the module docstring)
 _BOUND_EXACT = ((0, 0x7FF), (0x2000, 0x2BFF), (0x3000, 0x303F), (0xFF00, 0xFFEF))
@@ -188,19 +194,60 @@ EMPTY = Seq(())
 
 
 class _Parser:
+    # Java's embedded flags, each to the end of its group (or inside a (?flags:...) group)
+    FLAGS = ("ci", "unix", "multiline", "dotall", "ucase", "comments")
+    FLAG_LETTERS = {"i": "ci", "d": "unix", "m": "multiline", "s": "dotall", "u": "ucase",
+                    "x": "comments"}
+
     def __init__(self, pattern: str):
         self.s = pattern
         self.i = 0
         self.groups = 0
         self.ci = False  # CASE_INSENSITIVE ((?i)): ASCII letters only, as Java without UNICODE_CASE
+        self.unix = False  # UNIX_LINES ((?d)): '\n' is the only line terminator of . ^ $
+        self.multiline = False  # MULTILINE ((?m)): ^ / $ at line starts / ends too
+        self.dotall = False  # DOTALL ((?s)): . matches line terminators too
+        self.ucase = False  # UNICODE_CASE ((?u)): refused together with (?i)
+        self.comments = False  # COMMENTS ((?x)): white space and #-comments in the pattern ignored
+
+    def _flags(self):
+        return tuple(getattr(self, f) for f in self.FLAGS)
+
+    def _set_flags(self, v):
+        for f, x in zip(self.FLAGS, v):
+            setattr(self, f, x)
+
+    def _skip_comments(self):
+        """COMMENTS mode: Java's peekPastWhitespace -- ASCII white space, and '#' up to the end of
+        the line (UNIX_LINES: '\n'), are skipped wherever the parser peeks or takes a
+        character, inside classes too, but never right after a backslash."""
+        while self.i < len(self.s):
+            c = self.s[self.i]
+            if c in " \t\n\x0b\f\r":
+                self.i += 1
+            elif c == "#":
+                while self.i < len(self.s):
+                    c = self.s[self.i]
+                    self.i += 1
+                    if c == "\n" or (not self.unix and c in "\r\x85\u2028\u2029"):
+                        break
+            else:
+                break
 
     def error(self, msg):
         raise PatternNotSupported(f"{msg} at position {self.i} of /{self.s}/")
 
     def peek(self):
+        if self.comments:
+            self._skip_comments()
         return self.s[self.i] if self.i < len(self.s) else None
 
     def take(self):
+        if self.comments:
+            self._skip_comments()
+        return self.take_raw()
+
+    def take_raw(self):
         c = self.s[self.i]
         self.i += 1
         return c
@@ -271,24 +318,24 @@ class _Parser:
 
     def _group_body(self):
         """A group's alternatives; an inline flag inside applies up to the group's end."""
-        saved = self.ci
+        saved = self._flags()
         node = self.alt()
-        self.ci = saved
+        self._set_flags(saved)
         return node
 
     def atom(self):
         c = self.take()
         if c == "(":
             flags = self._inline_flags()
-            if flags is not None:  # (?i) (?-i): up to the end of the enclosing group
-                on, scoped = flags
+            if flags is not None:  # (?imsx-imsx): up to the end of the enclosing group
+                new, scoped = flags
                 if not scoped:
-                    self.ci = on
+                    self._set_flags(new)
                     return EMPTY
-                saved = self.ci
-                self.ci = on
+                saved = self._flags()
+                self._set_flags(new)
                 node = Group(self._group_body(), None)
-                self.ci = saved
+                self._set_flags(saved)
             elif self.s.startswith("?:", self.i):
                 self.i += 2
                 node = Group(self._group_body(), None)
@@ -301,7 +348,7 @@ class _Parser:
                 self.i += 3
                 node = Behind(self.alt(), neg)
             elif self.peek() == "?":
-                self.error("unsupported group construct (lookbehind, named group or inline flag)")
+                self.error("unsupported group construct (named group, atomic group or flag)")
             else:
                 self.groups += 1
                 idx = self.groups
@@ -313,11 +360,11 @@ class _Parser:
         if c == "[":
             return Chars(self.char_class())
         if c == ".":
-            return Chars(DOT)
+            return Chars(ANY if self.dotall else DOT_UNIX if self.unix else DOT)
         if c == "^":
-            return Anchor("^")
+            return Anchor("^" + ("m" if self.multiline else "") + ("d" if self.multiline and self.unix else ""))
         if c == "$":
-            return Anchor("$")
+            return Anchor("$" + ("m" if self.multiline else "") + ("d" if self.unix else ""))
         if c == "\\":
             return self.escape(in_class=False)
         if c in "*+?":
@@ -325,23 +372,41 @@ class _Parser:
         return Chars(self.fold(((ord(c), ord(c)),)))
 
     def _inline_flags(self):
-        """At '(' : (?i) / (?-i) -> (on, False); (?i: / (?-i: -> (on, True), consumed; else
-        None.  Other flags (d m s u x U, and combinations) are not supported."""
-        for text, on, scoped in (("?i)", True, False), ("?-i)", False, False),
-                                 ("?i:", True, True), ("?-i:", False, True)):
-            if self.s.startswith(text, self.i):
-                self.i += len(text)
-                return on, scoped
+        """At '(' : (?flags-flags) -> (the new flag tuple, False); (?flags-flags: -> (the
+        group's flag tuple, True), consumed; else None.  Flags: i d m s u x; U
+        (UNICODE_CHARACTER_CLASS) is refused, and so is u together with i (Unicode case
+        folding)."""
         j = self.i
-        if self.s.startswith("?", j) and j + 1 < len(self.s) and (self.s[j + 1].isalpha()
-                                                                  or self.s[j + 1] == "-"):
-            self.error("inline flags other than (?i) / (?-i)")
-        return None
+        if not (self.s.startswith("?", j) and j + 1 < len(self.s)
+                and (self.s[j + 1].isalpha() or self.s[j + 1] == "-")):
+            return None
+        j += 1
+        vals = dict(zip(self.FLAGS, self._flags()))
+        on = True
+        while j < len(self.s) and self.s[j] not in "):":
+            c = self.s[j]
+            if c == "-" and on:
+                on = False
+            elif c in self.FLAG_LETTERS:
+                vals[self.FLAG_LETTERS[c]] = on
+            elif c == "U":
+                self.i = j
+                self.error("the UNICODE_CHARACTER_CLASS flag (?U)")
+            else:
+                self.i = j
+                self.error(f"unknown inline flag {c!r}")
+            j += 1
+        if j >= len(self.s):
+            self.error("unterminated inline flag group")
+        self.i = j + 1
+        return tuple(vals[f] for f in self.FLAGS), self.s[j] == ":"
 
     def fold(self, ranges):
         """Under (?i): the ranges plus the other case of every ASCII letter in them."""
         if not self.ci:
             return ranges
+        if self.ucase:
+            self.error("case-insensitive matching with UNICODE_CASE (?iu)")
         extra = []
         for a, b in ranges:
             for lo, hi, d in ((65, 90, 32), (97, 122, -32)):
@@ -351,9 +416,9 @@ class _Parser:
         return cs_norm(list(ranges) + extra)
 
     def escape(self, in_class: bool):
-        if self.peek() is None:
+        if self.i >= len(self.s):  # (raw: COMMENTS mode skips nothing after a backslash)
             self.error("trailing backslash")
-        c = self.take()
+        c = self.take_raw()
         simple = {"t": 9, "n": 10, "r": 13, "f": 12, "a": 7, "e": 27}
         if c in simple:
             v = simple[c]
@@ -375,13 +440,13 @@ class _Parser:
             v = int(self.s[self.i:j] or "0", 8)
             self.i = j
         elif c == "c":
-            v = ord(self.take()) ^ 64
+            v = ord(self.take_raw()) ^ 64
         elif c.isdigit() and not in_class:
             return BackRef(int(c))
         elif c in "bB" and not in_class:
             return Anchor("\\b" if c == "b" else "\\B")
         elif c in "AzZ" and not in_class:
-            return Anchor({"A": "^", "Z": "$", "z": "\\z"}[c])
+            return Anchor({"A": "^", "Z": "$d" if self.unix else "$", "z": "\\z"}[c])
         elif c.isalnum():
             self.error(f"unsupported escape \\{c}")
         else:
@@ -1389,7 +1454,8 @@ def compile_nullable(pattern: str, ast) -> CompiledRegex:
 _LINE_END = Alt((Seq((Chars(((13, 13),)), Chars(((10, 10),)))), Chars(LINE_TERMINATORS)))
 
 
-def _rewrite_inner_anchors(n, in_look: bool = False):
+def _rewrite_inner_anchors(n, in_look: bool = False, consumes_after: bool = False,
+                           no_cr_before: bool = False):
     """Anchors inside a (non-nullable) pattern: $ and \\Z become the lookahead "at most one
     line terminator, then the end" (DollarLook), \\z the lookahead "the end", ^ and \\A an edge
     taken only at the start of the text (NFA.at0); \\b / \\B the lookbehind-and-lookahead pairs
@@ -1401,17 +1467,45 @@ def _rewrite_inner_anchors(n, in_look: bool = False):
             return Look(EndText(), False)
         if n.kind == "^" and not in_look:
             return n
+        # UNIX_LINES / MULTILINE forms (Pattern.java's UnixDollar, Dollar(true), UnixCaret, Caret)
+        cr, lf = Chars(((13, 13),)), Chars(((10, 10),))
+        if n.kind == "$d":  # the end, or before a final '\n'
+            return Look(Seq((Repeat(lf, 0, 1), EndText())), False)
+        if n.kind == "$md":  # before any '\n', or at the end
+            return Look(Alt((lf, EndText())), False)
+        if n.kind == "$m":  # before any line terminator but never between "\r\n", or at the end
+            if no_cr_before:  # (the previous character is never '\r': no lookbehind needed)
+                return Look(Alt((Chars(LINE_TERMINATORS), EndText())), False)
+            return Alt((Seq((Behind(cr, True), Look(lf, False))),
+                        Look(Chars(cs_norm([(13, 13), (0x85, 0x85), (0x2028, 0x2029)])), False),
+                        Look(EndText(), False)))
+        if n.kind in ("^m", "^md") and not in_look:
+            # the start, or after a line terminator (never between "\r\n"), but not at the end
+            if n.kind == "^md":
+                after = Behind(lf, False)
+            else:
+                after = Alt((Behind(Chars(cs_norm([(10, 10), (0x85, 0x85), (0x2028, 0x2029)])), False),
+                             Seq((Behind(cr, False), Look(lf, True)))))
+            if consumes_after:  # (a character follows in every match: never at the end)
+                return Alt((Anchor("^"), after))
+            return Seq((Alt((Anchor("^"), after)), Look(Chars(ANY), False)))
         if n.kind in ("\\b", "\\B") and not in_look:  # Java's Bound over \b's word characters
             w = Chars(bound_word_chars())
             b = n.kind == "\\b"  # \b: the two sides differ; \B: they agree
             return Alt((Seq((Behind(w, False), Look(w, b))), Seq((Behind(w, True), Look(w, not b)))))
         raise PatternNotSupported(f"anchor {n.kind} inside the pattern")
     if isinstance(n, Seq):
-        return Seq(tuple(_rewrite_inner_anchors(x, in_look) for x in n.items))
+        def before(k):  # whether the character before item k is never a '\r'
+            pre = Seq(n.items[:k])
+            return not _may_end_with(pre, 13) and (no_cr_before or not nullable(pre))
+        return Seq(tuple(_rewrite_inner_anchors(x, in_look, consumes_after
+                                                or not nullable(Seq(n.items[k + 1:])), before(k))
+                         for k, x in enumerate(n.items)))
     if isinstance(n, Alt):
-        return Alt(tuple(_rewrite_inner_anchors(x, in_look) for x in n.options))
+        return Alt(tuple(_rewrite_inner_anchors(x, in_look, consumes_after, no_cr_before)
+                         for x in n.options))
     if isinstance(n, Group):
-        return Group(_rewrite_inner_anchors(n.node, in_look), n.index)
+        return Group(_rewrite_inner_anchors(n.node, in_look, consumes_after, no_cr_before), n.index)
     if isinstance(n, Repeat):
         return Repeat(_rewrite_inner_anchors(n.node, in_look), n.lo, n.hi, n.greedy)
     if isinstance(n, (Look, Behind)):

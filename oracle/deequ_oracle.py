@@ -710,33 +710,77 @@ def _java_word_class() -> str:
 _JAVA_WORD = None
 
 
+_PY_DOT = {"": "[^\\n\\r\\u0085\\u2028\\u2029]", "d": "[^\\n]"}
+# Pattern.java (JDK 8): Caret / UnixCaret (MULTILINE ^: the start, or after a line terminator --
+# never between "\r\n" -- and never at the end), Dollar(true) / UnixDollar(true) (MULTILINE $:
+# before a line terminator -- never between "\r\n" -- or at the end), UnixDollar(false)
+_PY_CARET_M = "(?:\\A|(?<=[\\n\\x85\\u2028\\u2029])|(?<=\\r)(?!\\n))(?!\\Z)"
+_PY_CARET_MD = "(?:\\A|(?<=\\n))(?!\\Z)"
+_PY_DOLLAR_M = "(?:(?<!\\r)(?=\\n)|(?=[\\r\\x85\\u2028\\u2029])|\\Z)"
+_PY_DOLLAR_MD = "(?=\\n|\\Z)"
+_PY_DOLLAR_D = "(?:\\Z|(?=\\n\\Z))"
+
+
 def java_regex_to_python(pattern: str) -> str:
     """Java -> Python `re` (used with re.ASCII, which gives Java's ASCII \\d \\w \\s):
     `.` outside a class excludes every Java line terminator (Python's excludes only \\n); `$` and
     `\\Z` are Java's Dollar (end, or before one final terminator, "\\r\\n" included, never
     between "\\r\\n"); `\\z` is the strict end; `\\b` is Java's Bound over Unicode letters and
-    digits (Python's ASCII \\b would call every non-ASCII code point a non-word one)."""
+    digits (Python's ASCII \\b would call every non-ASCII code point a non-word one).  Embedded
+    flags i d m s x (and u without i) are tracked here with Java's scoping and each construct they
+    change is written out explicitly, so Python's own flag semantics never apply."""
     global _JAVA_WORD
     out, i, in_class = [], 0, False
-    # Java's inline (?i) / (?-i) applies to the end of the enclosing group, alternatives included
-    # (Python's applies to the whole pattern): restated as scoped (?i:...) groups closed at each
-    # '|' and ')' of that group and re-opened after a '|'.  (?i) is ASCII-only in Java without
-    # UNICODE_CASE, as in Python under re.ASCII.
+    # Java's inline flags apply to the end of the enclosing group, alternatives included (Python's
+    # apply to the whole pattern).  (?i) is restated as scoped (?i:...) groups closed at each '|'
+    # and ')' of that group and re-opened after a '|' -- ASCII-only in Java without UNICODE_CASE,
+    # as in Python under re.ASCII; d m s x are applied by the translation itself.
     scopes = [[]]
+    fl = {"i": False, "d": False, "m": False, "s": False, "x": False, "u": False}
+    saved = []  # the flags at each open group
     while i < len(pattern):
         c = pattern[i]
+        if fl["x"] and c in " \t\n\x0b\f\r":  # COMMENTS: white space ignored, classes too
+            i += 1
+            continue
+        if fl["x"] and c == "#":  # ... and a comment up to the end of the line
+            while i < len(pattern):
+                i += 1
+                if pattern[i - 1] == "\n" or (not fl["d"] and pattern[i - 1] in "\r\x85\u2028\u2029"):
+                    break
+            continue
         if not in_class:
-            m = re.match(r"\(\?(-?)i\)", pattern[i:])
-            if m:
-                opener = "(?-i:" if m.group(1) else "(?i:"
-                out.append(opener)
-                scopes[-1].append(opener)
+            m = re.match(r"\(\?([idmsux]*)(?:-([idmsux]*))?([):])", pattern[i:])
+            if m and (m.group(1) or m.group(2) is not None):
+                new = dict(fl)
+                for f in m.group(1):
+                    new[f] = True
+                for f in m.group(2) or "":
+                    new[f] = False
+                assert not (new["i"] and new["u"]), "UNICODE_CASE is not restated"
+                opener = None
+                if new["i"] != fl["i"]:
+                    opener = "(?i:" if new["i"] else "(?-i:"
+                if m.group(3) == ")":
+                    if opener:
+                        out.append(opener)
+                        scopes[-1].append(opener)
+                else:  # (?flags:...): a group of its own
+                    saved.append(fl)
+                    scopes.append([])
+                    out.append("(?:")
+                    if opener:
+                        out.append(opener)
+                        scopes[-1].append(opener)
+                fl = new
                 i += m.end()
                 continue
             if c == "(":
                 scopes.append([])
+                saved.append(dict(fl))
             elif c == ")" and len(scopes) > 1:
                 out.append(")" * len(scopes.pop()))
+                fl = saved.pop()
             elif c == "|":
                 out.append(")" * len(scopes[-1]))
                 out.append("|")
@@ -751,7 +795,7 @@ def java_regex_to_python(pattern: str) -> str:
                 w = _JAVA_WORD
                 out.append(f"(?:(?<!{w})(?={w})|(?<={w})(?!{w}))")
             elif not in_class and e == "\\Z":
-                out.append(_JAVA_DOLLAR)
+                out.append(_PY_DOLLAR_D if fl["d"] else _JAVA_DOLLAR)
             elif not in_class and e == "\\z":
                 out.append("\\Z")
             else:
@@ -770,9 +814,14 @@ def java_regex_to_python(pattern: str) -> str:
                 continue
             out.append(c)
         elif c == ".":
-            out.append("[^\\n\\r\\u0085\\u2028\\u2029]")
+            out.append("(?s:.)" if fl["s"] else _PY_DOT["d" if fl["d"] else ""])
+        elif c == "^":
+            out.append((_PY_CARET_MD if fl["d"] else _PY_CARET_M) if fl["m"] else "\\A")
         elif c == "$":
-            out.append(_JAVA_DOLLAR)
+            if fl["m"]:
+                out.append(_PY_DOLLAR_MD if fl["d"] else _PY_DOLLAR_M)
+            else:
+                out.append(_PY_DOLLAR_D if fl["d"] else _JAVA_DOLLAR)
         else:
             out.append(c)
         i += 1

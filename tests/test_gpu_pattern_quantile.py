@@ -86,7 +86,9 @@ def test_pattern_match_floating_point_columns_match_oracle(pattern, dtype, gpu_d
                                      r"(^|/)ht(tp|$)", r"(?:\Ax|o)[a-z]+(?: |\z)",
                                      # lookbehind and \b / \B inside the pattern
                                      r"(?<=/)[a-z]{2}", r"(?<!\d)\d{3}(?!\d)", r"t\Bp",
-                                     r"\b[a-z]+\b:"])
+                                     r"\b[a-z]+\b:",
+                                     # embedded flags
+                                     r"(?m)^h[a-z]*$", r"(?sx) h . t  # comment", r"(?d)\d$"])
 def test_pattern_match_matches_oracle_on_random_rows(pattern, gpu_device):
     from deequ_amd.analyzers import PatternMatch
     from oracle.deequ_oracle import OTable, agg_pattern_match

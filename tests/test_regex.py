@@ -79,6 +79,25 @@ FUZZ = [
     (r"ab\b|cd", "ab cd abx", 8),
     (r"x\By", "xy x y", 6),
     (r"\b\d+\b ", "12 3a 45 ", 9),
+    # embedded flags: DOTALL, UNIX_LINES, MULTILINE (Pattern.java's Caret / Dollar(true) and their
+    # UNIX_LINES forms, never between "\r\n"), COMMENTS (white space and #-comments ignored,
+    # inside classes too), each scoped to its group as (?i) is
+    (r"(?s)a.b", "ab\r\n\x85\u2028x", 6),
+    (r"(?d)a.b", "ab\r\n\x85x", 6),
+    (r"a(?s:.)b|c.d", "abcd\n\r", 6),
+    (r"(?m)^ab", "ab\r\nx\x85\u2028", 8),
+    (r"(?m)ab$", "ab\r\nx\x85\u2029", 8),
+    (r"(?m)^a+$", "ab\r\n\x85", 8),
+    (r"(?m)x\r$", "x\r\n", 6),
+    (r"(?m)(?:^|,)a(?:,|$)", "a,\n\rb", 8),
+    (r"(?md)^ab$", "ab\r\nx", 8),
+    (r"(?d)ab$|c\Z", "abc\r\nx", 6),
+    (r"(?x) a b # c", "ab #c", 6),
+    (r"(?x)[a b]c", "abc ", 6),
+    (r"(?x)a\ b|(?-x: c)", "abc ", 6),
+    (r"(?is)A.B|(?-i)c", "aAbBcC\n", 6),
+    (r"((?m)^a|b)$", "ab\n", 6),
+    (r"(?m)^\s*#", " #\n\r\x85a", 8),
 ]
 
 
@@ -130,7 +149,9 @@ def test_nullable_known_answers():
     assert not compile_java_regex(r"(?:a??)+b?").matches("ab")
 
 
-@pytest.mark.parametrize("pattern", [r"a++", r"a\s$", r"a*$", r"(?s)a", r"(?=x)a*", r"(a?)\1",
+@pytest.mark.parametrize("pattern", [r"a++", r"a\s$", r"a*$", r"(?=x)a*", r"(a?)\1",
+                                     # Unicode case folding / character classes
+                                     r"(?iu)a", r"(?U)\w", r"(?m)^$", r"(?sm)^.+$",
                                      # inner anchors the automaton cannot decide: a $ after a
                                      # possible \r, a ^ after a lookahead, ^ in a loop
                                      r"(?:a|\r)$x?", r"(?=a)(^|b)a", r"(?:^a)+",
