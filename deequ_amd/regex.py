@@ -17,7 +17,9 @@ stops early.
 Supported Java syntax: literals and escapes (\\t \\n \\r \\f \\a \\e \\xhh \\uhhhh \\0o \\cX and
 escaped metacharacters), ``.`` (any code point but the Java line terminators), classes with ranges,
 negation, nested escapes and \\d \\D \\s \\S \\w \\W (ASCII, as Java without UNICODE_CHARACTER_CLASS),
-groups ( ), (?: ), alternation, greedy / lazy quantifiers * + ? {n} {n,} {n,m}, lookaheads (?= )
+\\h \\H \\v \\V, the US-ASCII POSIX classes \\p{Lower} ... \\p{Space} and their \\P{...}
+complements, \\Q...\\E (Pattern.java's RemoveQEQuoting, before parsing), groups ( ), (?: ),
+named groups (?<name> ) with \\k<name>, alternation, greedy / lazy quantifiers * + ? {n} {n,} {n,m}, lookaheads (?= )
 (?! ), back-references to groups with a finite language (expanded: the CREDITCARD separators),
 ^ / \\A at the start; $ / \\Z (end, or before one final line terminator, "\\r\\n" included) and
 \\z (strict end) at the end; \\b at the start or end of the pattern; anchors, \\b / \\B and
@@ -97,6 +99,19 @@ SPACE = cs_norm([(9, 13), (32, 32)])  # [ \t\n\x0B\f\r]
 LINE_TERMINATORS = cs_norm([(10, 10), (13, 13), (0x85, 0x85), (0x2028, 0x2029)])
 DOT = cs_neg(LINE_TERMINATORS)
 DOT_UNIX = cs_neg(((10, 10),))  # . under UNIX_LINES
+# \h and \v (Pattern.java, JDK 8: horizontal / vertical white space)
+HSPACE = cs_norm([(9, 9), (32, 32), (0xA0, 0xA0), (0x1680, 0x1680), (0x180E, 0x180E),
+                  (0x2000, 0x200A), (0x202F, 0x202F), (0x205F, 0x205F), (0x3000, 0x3000)])
+VSPACE = cs_norm([(10, 13), (0x85, 0x85), (0x2028, 0x2029)])
+# \p{...}: the POSIX classes, US-ASCII only (Java without UNICODE_CHARACTER_CLASS)
+_PUNCT = ((33, 47), (58, 64), (91, 96), (123, 126))
+POSIX_CLASSES = {
+    "Lower": ((97, 122),), "Upper": ((65, 90),), "ASCII": ((0, 127),),
+    "Alpha": ((65, 90), (97, 122)), "Digit": DIGIT, "Alnum": ((48, 57), (65, 90), (97, 122)),
+    "Punct": _PUNCT, "Graph": ((33, 126),), "Print": ((32, 126),), "Blank": ((9, 9), (32, 32)),
+    "Cntrl": ((0, 31), (127, 127)), "XDigit": ((48, 57), (65, 70), (97, 102)),
+    "Space": ((9, 13), (32, 32)),
+}
 ANY = ((0, MAX_CP),)
 # \b's word characters are decided exactly in these blocks (see the module docstring)
 _BOUND_EXACT = ((0, 0x7FF), (0x2000, 0x2BFF), (0x3000, 0x303F), (0xFF00, 0xFFEF))
@@ -193,6 +208,27 @@ class EndText:
 EMPTY = Seq(())
 
 
+def _remove_qe_quoting(p: str) -> str:
+    """\\Q...\\E as Pattern.java's RemoveQEQuoting does it, before parsing: each quoted ASCII
+    character that is not a letter or digit is escaped (so a following quantifier binds to the
+    last quoted character, and classes see literals); an unterminated \\Q runs to the end."""
+    out, i, n = [], 0, len(p)
+    while i < n:
+        if p[i] == "\\" and i + 1 < n and p[i + 1] == "Q":
+            j = p.find("\\E", i + 2)
+            j = n if j < 0 else j
+            for ch in p[i + 2:j]:
+                out.append(ch if not ch.isascii() or ch.isalnum() else "\\" + ch)
+            i = j + 2
+        elif p[i] == "\\":
+            out.append(p[i:i + 2])
+            i += 2
+        else:
+            out.append(p[i])
+            i += 1
+    return "".join(out)
+
+
 class _Parser:
     # Java's embedded flags, each to the end of its group (or inside a (?flags:...) group)
     FLAGS = ("ci", "unix", "multiline", "dotall", "ucase", "comments")
@@ -200,9 +236,10 @@ class _Parser:
                     "x": "comments"}
 
     def __init__(self, pattern: str):
-        self.s = pattern
+        self.s = _remove_qe_quoting(pattern)
         self.i = 0
         self.groups = 0
+        self.names: Dict[str, int] = {}
         self.ci = False  # CASE_INSENSITIVE ((?i)): ASCII letters only, as Java without UNICODE_CASE
         self.unix = False  # UNIX_LINES ((?d)): '\n' is the only line terminator of . ^ $
         self.multiline = False  # MULTILINE ((?m)): ^ / $ at line starts / ends too
@@ -347,6 +384,18 @@ class _Parser:
                 neg = self.s[self.i + 2] == "!"
                 self.i += 3
                 node = Behind(self.alt(), neg)
+            elif self.s.startswith("?<", self.i):  # (?<name>X): a capturing group with a name
+                j = self.s.find(">", self.i)
+                name = self.s[self.i + 2:j] if j > 0 else ""
+                if not (name[:1].isascii() and name[:1].isalpha() and name.isascii()
+                        and name.isalnum()):
+                    self.error("bad group name")
+                if name in self.names:
+                    self.error(f"named group <{name}> defined twice")
+                self.i = j + 1
+                self.groups += 1
+                self.names[name] = idx = self.groups
+                node = Group(self._group_body(), idx)
             elif self.peek() == "?":
                 self.error("unsupported group construct (named group, atomic group or flag)")
             else:
@@ -424,9 +473,31 @@ class _Parser:
             v = simple[c]
             return Chars(((v, v),)) if not in_class else ((v, v),)
         classes = {"d": DIGIT, "D": cs_neg(DIGIT), "s": SPACE, "S": cs_neg(SPACE), "w": WORD,
-                   "W": cs_neg(WORD)}
+                   "W": cs_neg(WORD), "h": HSPACE, "H": cs_neg(HSPACE), "v": VSPACE,
+                   "V": cs_neg(VSPACE)}
         if c in classes:
             return Chars(classes[c]) if not in_class else classes[c]
+        if c in "pP":  # \p{Name} / \pL: the POSIX classes only
+            if self.s.startswith("{", self.i):
+                j = self.s.find("}", self.i)
+                if j < 0:
+                    self.error("unclosed \\p{")
+                name, self.i = self.s[self.i + 1:j], j + 1
+            else:
+                name = self.take_raw() if self.i < len(self.s) else ""
+            if name not in POSIX_CLASSES:
+                self.error(f"unsupported property \\{c}{{{name}}}")
+            if self.ci and name in ("Lower", "Upper"):  # (JDK 8 does not fold these; later JDKs do)
+                self.error(f"\\p{{{name}}} under (?i)")
+            r = POSIX_CLASSES[name] if c == "p" else cs_neg(POSIX_CLASSES[name])
+            return Chars(r) if not in_class else r
+        if c == "k" and not in_class:  # \k<name>
+            j = self.s.find(">", self.i)
+            name = self.s[self.i + 1:j] if self.s.startswith("<", self.i) and j > 0 else None
+            if name not in self.names:
+                self.error("back-reference to an unknown group name")
+            self.i = j + 1
+            return BackRef(self.names[name])
         if c == "x":
             v = int(self.s[self.i:self.i + 2], 16)
             self.i += 2

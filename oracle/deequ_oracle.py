@@ -721,6 +721,34 @@ _PY_DOLLAR_MD = "(?=\\n|\\Z)"
 _PY_DOLLAR_D = "(?:\\Z|(?=\\n\\Z))"
 
 
+# Pattern.java (JDK 8): the US-ASCII POSIX classes of \p{...}, \h / \v
+_JAVA_POSIX = {"Lower": "a-z", "Upper": "A-Z", "ASCII": "\\x00-\\x7f", "Alpha": "a-zA-Z",
+               "Digit": "0-9", "Alnum": "0-9a-zA-Z", "Punct": "!-/:-@\\[-`{-~", "Graph": "!-~",
+               "Print": " -~", "Blank": " \\t", "Cntrl": "\\x00-\\x1f\\x7f",
+               "XDigit": "0-9a-fA-F", "Space": " \\t\\n\\x0b\\f\\r"}
+_HSP = " \\t\\xa0\\u1680\\u180e\\u2000-\\u200a\\u202f\\u205f\\u3000"
+_VSP = "\\n\\x0b\\f\\r\\x85\\u2028\\u2029"
+_JAVA_HV = {"\\h": _HSP, "\\H": _HSP, "\\v": _VSP, "\\V": _VSP}
+
+
+def _java_remove_qe(p: str) -> str:
+    """Pattern.java's RemoveQEQuoting: \\Q...\\E becomes its characters, each escaped."""
+    out, i = [], 0
+    while i < len(p):
+        if p.startswith("\\Q", i):
+            j = p.find("\\E", i + 2)
+            j = len(p) if j < 0 else j
+            out.append("".join(re.escape(ch) for ch in p[i + 2:j]))
+            i = j + 2
+        elif p[i] == "\\":
+            out.append(p[i:i + 2])
+            i += 2
+        else:
+            out.append(p[i])
+            i += 1
+    return "".join(out)
+
+
 def java_regex_to_python(pattern: str) -> str:
     """Java -> Python `re` (used with re.ASCII, which gives Java's ASCII \\d \\w \\s):
     `.` outside a class excludes every Java line terminator (Python's excludes only \\n); `$` and
@@ -730,6 +758,7 @@ def java_regex_to_python(pattern: str) -> str:
     flags i d m s x (and u without i) are tracked here with Java's scoping and each construct they
     change is written out explicitly, so Python's own flag semantics never apply."""
     global _JAVA_WORD
+    pattern = _java_remove_qe(pattern)
     out, i, in_class = [], 0, False
     # Java's inline flags apply to the end of the enclosing group, alternatives included (Python's
     # apply to the whole pattern).  (?i) is restated as scoped (?i:...) groups closed at each '|'
@@ -775,6 +804,12 @@ def java_regex_to_python(pattern: str) -> str:
                 fl = new
                 i += m.end()
                 continue
+            if pattern.startswith("(?<", i) and pattern[i + 3:i + 4].isalpha():  # named group
+                scopes.append([])
+                saved.append(dict(fl))
+                out.append("(?P<")
+                i += 3
+                continue
             if c == "(":
                 scopes.append([])
                 saved.append(dict(fl))
@@ -798,6 +833,26 @@ def java_regex_to_python(pattern: str) -> str:
                 out.append(_PY_DOLLAR_D if fl["d"] else _JAVA_DOLLAR)
             elif not in_class and e == "\\z":
                 out.append("\\Z")
+            elif e in ("\\p", "\\P"):  # the POSIX classes (US-ASCII)
+                if pattern.startswith("{", i + 2):
+                    j = pattern.index("}", i)
+                    name = pattern[i + 3:j]
+                else:
+                    j, name = i + 2, pattern[i + 2]
+                body = _JAVA_POSIX[name]
+                assert not (in_class and e == "\\P"), "a negated property inside a class"
+                out.append(body if in_class else ("[" if e == "\\p" else "[^") + body + "]")
+                i = j + 1
+                continue
+            elif e in _JAVA_HV:
+                body = _JAVA_HV[e]
+                assert not (in_class and e[1].isupper()), "\\H / \\V inside a class"
+                out.append(body if in_class else ("[^" if e[1].isupper() else "[") + body + "]")
+            elif e == "\\k":  # \k<name>
+                j = pattern.index(">", i)
+                out.append(f"(?P={pattern[i + 3:j]})")
+                i = j + 1
+                continue
             else:
                 out.append(e)
             i += 2

@@ -98,6 +98,15 @@ FUZZ = [
     (r"(?is)A.B|(?-i)c", "aAbBcC\n", 6),
     (r"((?m)^a|b)$", "ab\n", 6),
     (r"(?m)^\s*#", " #\n\r\x85a", 8),
+    # the US-ASCII POSIX classes \p{...} / \P{...}, \h \v, \Q...\E (Pattern.java's
+    # RemoveQEQuoting: a quantifier binds to the last quoted character), named groups
+    (r"\p{Alpha}+\d", "aZ1 _\u00e9", 6),
+    (r"[\p{Punct}\h]x", "!x ~ \t_\u3000", 5),
+    (r"\P{Digit}a|\p{XDigit}{2}\p{Space}", "1a 0F\n", 6),
+    (r"\QA.b\E+|x\Q(*)\E", "A.bxB(*)", 6),
+    (r"(?<sep>[-/])\d\k<sep>\d", "-/1", 6),
+    (r"\va\V", "a\n\r\x85 x", 5),
+    (r"(?x)\p{Upper} \Q a b\E", "A ab", 7),
 ]
 
 
@@ -152,6 +161,8 @@ def test_nullable_known_answers():
 @pytest.mark.parametrize("pattern", [r"a++", r"a\s$", r"a*$", r"(?=x)a*", r"(a?)\1",
                                      # Unicode case folding / character classes
                                      r"(?iu)a", r"(?U)\w", r"(?m)^$", r"(?sm)^.+$",
+                                     # Unicode properties, \p{Lower} / \p{Upper} under (?i)
+                                     r"\pL", r"\p{IsDigit}", r"(?i)\p{Lower}",
                                      # inner anchors the automaton cannot decide: a $ after a
                                      # possible \r, a ^ after a lookahead, ^ in a loop
                                      r"(?:a|\r)$x?", r"(?=a)(^|b)a", r"(?:^a)+",
