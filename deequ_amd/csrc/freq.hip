@@ -1985,21 +1985,27 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   // count the rows of `pend` (bit i: key[i]) that match a candidate; returns the rest.  Each row
   // finds its candidate index (unused candidates hold kFreeCand, which no row's key equals) and adds
   // one to that index's byte of a packed per-lane counter word (<= 16 per byte per call).
-  auto count = [&](const uint64_t* key, uint32_t pend) -> uint32_t {
+  // NC: the candidates compared (a wave with at most 4 -- 3-value columns like priority -- skips
+  // the other half of the compares; the slots past nc hold kFreeCand)
+  auto count_nc = [&](const uint64_t* key, uint32_t pend, auto nc_const) -> uint32_t {
+    constexpr int NC = decltype(nc_const)::value;
     uint64_t packed = 0;
     uint32_t miss = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       int idx = kSmallCand;
 #pragma unroll
-      for (int k = 0; k < kSmallCand; ++k) idx = key[i] == cand[k] ? k : idx;
+      for (int k = 0; k < NC; ++k) idx = key[i] == cand[k] ? k : idx;
       const bool p = (pend >> i) & 1u;
       packed += (p && idx < kSmallCand) ? (1ULL << (8 * idx)) : 0ULL;
       miss |= (p && idx == kSmallCand ? 1u : 0u) << i;
     }
 #pragma unroll
-    for (int k = 0; k < kSmallCand; ++k) cnt[k] += (uint32_t)(packed >> (8 * k)) & 0xffu;
+    for (int k = 0; k < NC; ++k) cnt[k] += (uint32_t)(packed >> (8 * k)) & 0xffu;
     return miss;
+  };
+  auto count = [&](const uint64_t* key, uint32_t pend) -> uint32_t {
+    return count_nc(key, pend, std::integral_constant<int, kSmallCand>{});
   };
   // rows whose key is not yet a candidate: add their keys (wave-uniform), then count them
   auto admit = [&](const uint64_t* key, uint32_t pend) {
@@ -2079,7 +2085,9 @@ __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
         cur.load(off, vsrc, rn, lane);
       }
       nulls += 16 - __popc(vb);
-      const uint32_t pend = count(key, vb);
+      const uint32_t pend = __builtin_amdgcn_readfirstlane(nc) <= 4
+                                ? count_nc(key, vb, std::integral_constant<int, 4>{})
+                                : count(key, vb);
       if (__ballot(pend != 0)) admit(key, pend);
       if (flag == a.fast_epoch) gave_up = true;
       r0 += stride;
