@@ -36,11 +36,16 @@ match at offset 0 is non-empty -- compiled from a priority-ordered thread automa
 (``compile_nullable``: alternation order, greedy / lazy preference, Java's rule that an iteration
 consuming nothing ends its loop), with no anchor but a leading ^.
 
+A lookahead inside a quantifier (``a(?:(?!b).)*c``, the "tempered dot") cannot be compiled
+against its continuation, which loops back through it: it becomes an obligation instead -- a
+thread of the subset construction that crosses it carries the lookahead's automaton, advanced
+with every symbol, and dies when it fails (_determinize_obligations).
+
 Rejected (a PatternNotSupported error, never a silently different answer): nullable patterns with
 a lookaround, back-reference or trailing anchor, possessive quantifiers, unbounded lookbehinds,
-the flags U and i with u, anchors / lookbehinds the automaton cannot place (after a lookahead, in
-a quantifier or a lookaround), $ after a pattern that may end in "\\r" (Java's $ never matches
-between "\\r\\n"), and automata above ``MAX_STATES``.
+the flags U and i with u, anchors / lookbehinds the automaton cannot place (after a lookahead, or
+inside a lookaround), $ after a pattern that may end in "\\r" (Java's $ never matches between
+"\\r\\n"), and automata above ``MAX_STATES``.
 
 \\b is Java's Bound: a word character is '_' or Character.isLetterOrDigit (categories L* and Nd),
 taken from Python's Unicode database.  Exact for U+0000-U+07FF and the punctuation / symbol blocks
@@ -771,12 +776,15 @@ class NFA:
         self.at0: List[List[int]] = []
         # (k, t): taken when lookbehind k holds at this position (determinize's `behinds`)
         self.behind: List[List[Tuple[int, int]]] = []
+        # (k, t): taken under the obligation that lookahead k holds here (determinize's `aheads`)
+        self.ahead: List[List[Tuple[int, int]]] = []
 
     def new(self) -> int:
         self.trans.append([])
         self.eps.append([])
         self.at0.append([])
         self.behind.append([])
+        self.ahead.append([])
         return len(self.trans) - 1
 
 
@@ -799,13 +807,134 @@ class DFA:
 
 
 def determinize(nfa: NFA, start: int, finals: FrozenSet[int], univ: int = -1,
-                at_start: bool = True, behinds=()) -> DFA:
+                at_start: bool = True, behinds=(), aheads=()) -> DFA:
     """(behinds: per lookbehind k, (its suffix DFA -- accepting iff the text read so far ends
     with a string of its body -- and whether it is negative); a DFA state is then the NFA subset
-    with every suffix DFA's state, and nfa.behind edges are followed where lookbehind k holds.)"""
+    with every suffix DFA's state, and nfa.behind edges are followed where lookbehind k holds.
+    aheads: per lookahead k compiled as an obligation (one inside a quantifier), _Ahead.)"""
+    if aheads:
+        return _determinize_obligations(nfa, start, finals, univ, at_start, behinds, aheads)
     if behinds:
         return _determinize_behind(nfa, start, finals, univ, behinds)
     return _determinize(nfa, start, finals, univ, at_start)
+
+
+class _Ahead:
+    """A lookahead (?=X) / (?!X) as an obligation: the DFA of X Sigma* EOT run from the point it is
+    asserted, with the states from which every / no continuation is accepted (it is then decided
+    and dropped, or kills its thread)."""
+
+    def __init__(self, d: DFA, negative: bool):
+        self.d, self.negative = d, negative
+        n = d.n
+        good_end = [d.accept[d.nxt[q][EOT]] for q in range(n)]
+        rev: List[List[int]] = [[] for _ in range(n)]
+        for q in range(n):
+            for t in set(d.nxt[q][:256]):
+                rev[t].append(q)
+
+        def back(seeds):
+            seen, stack = set(seeds), list(seeds)
+            while stack:
+                for p in rev[stack.pop()]:
+                    if p not in seen:
+                        seen.add(p)
+                        stack.append(p)
+            return seen
+        may_fail = back([q for q in range(n) if not good_end[q]])
+        may_hold = back([q for q in range(n) if good_end[q]])
+        self.holds = [q not in may_fail for q in range(n)]  # X has matched: holds for any rest
+        self.never = [q not in may_hold for q in range(n)]  # X cannot match any more
+
+    def settle(self, q: int) -> int:
+        """0: undecided, 1: the assertion holds, -1: it fails."""
+        if self.holds[q]:
+            return -1 if self.negative else 1
+        if self.never[q]:
+            return 1 if self.negative else -1
+        return 0
+
+
+def _determinize_obligations(nfa: NFA, start: int, finals: FrozenSet[int], univ: int,
+                             at_start: bool, behinds, aheads) -> DFA:
+    """Subset construction over threads (NFA state, obligations): a lookahead edge adds its
+    automaton's start state as an obligation of the thread, every symbol advances the thread's
+    obligations with it, and a thread dies when one fails (or, at EOT, is not accepted)."""
+    def closure(threads, at0, sig):
+        stack, seen = list(threads), set(threads)
+        while stack:
+            s, obl = stack.pop()
+            nxt = [(t, obl) for t in nfa.eps[s]]
+            if at0:
+                nxt += [(t, obl) for t in nfa.at0[s]]
+            nxt += [(t, obl) for k, t in nfa.behind[s]
+                    if behinds[k][0].accept[sig[k]] != behinds[k][1]]
+            for k, t in nfa.ahead[s]:
+                a = aheads[k]
+                st = a.settle(a.d.start)
+                if st >= 0:
+                    nxt.append((t, obl if st else obl | {(k, a.d.start)}))
+            for x in nxt:
+                if x not in seen:
+                    seen.add(x)
+                    stack.append(x)
+        return frozenset(seen)
+
+    def step(threads, sym):
+        out = set()
+        for s, obl in threads:
+            moves = [t for m, t in nfa.trans[s] if (m >> sym) & 1]
+            if not moves:
+                continue
+            kept, ok = [], True
+            for k, q in obl:
+                a = aheads[k]
+                q2 = a.d.nxt[q][sym]
+                if sym == EOT:
+                    if a.d.accept[q2] == a.negative:
+                        ok = False
+                        break
+                    continue
+                st = a.settle(q2)
+                if st < 0:
+                    ok = False
+                    break
+                if st == 0:
+                    kept.append((k, q2))
+            if ok:
+                o2 = frozenset(kept)
+                out.update((t, o2) for t in moves)
+        return out
+
+    sig0 = tuple(d.start for d, _ in behinds)
+    none = frozenset()
+    u0 = (closure([(univ, none)], False, sig0), ()) if univ >= 0 else None
+
+    def canon(key):
+        return u0 if u0 is not None and (univ, none) in key[0] else key
+
+    k0 = canon((closure([(start, none)], at_start, sig0), sig0))
+    index = {k0: 0}
+    order = [k0]
+    nxt, accept = [], []
+    i = 0
+    while i < len(order):
+        cur, sig = order[i]
+        i += 1
+        accept.append(any(s in finals and not obl for s, obl in cur))
+        row = [0] * NSYM
+        for sym in range(NSYM):
+            sig2 = tuple(d.nxt[q][sym] for (d, _), q in zip(behinds, sig)) if sig else sig
+            tgt = step(cur, sym)
+            key = canon((closure(tgt, False, sig2), sig2)) if tgt else (frozenset(), ())
+            if key not in index:
+                if len(order) >= MAX_STATES:
+                    raise PatternNotSupported(f"automaton exceeds {MAX_STATES} states")
+                index[key] = len(order)
+                order.append(key)
+            row[sym] = index[key]
+        nxt.append(row)
+    return DFA(nxt, accept, 0)
 
 
 def _determinize_behind(nfa: NFA, start: int, finals: FrozenSet[int], univ: int, behinds) -> DFA:
@@ -1017,6 +1146,8 @@ class _Compiler:
         self._univ = -1
         self.pending: List[Tuple[int, int, object]] = []
         self.behinds: List[Tuple[DFA, bool]] = []  # (suffix DFA, negative) per lookbehind
+        self.aheads: List[_Ahead] = []  # lookaheads inside a quantifier, as obligations
+        self.loop_depth = 0
 
     @property
     def univ(self) -> int:
@@ -1068,9 +1199,9 @@ class _Compiler:
         elif isinstance(node, Group):
             self.build(node.node, s, cont)
         elif isinstance(node, Repeat):
-            if _has_look(node.node):
-                raise PatternNotSupported("lookaround inside a quantifier")
+            # (a lookbehind or ^ is positional, and a lookahead inside becomes an obligation)
             j, to_j = self.join(cont)
+            self.loop_depth += 1
 
             def rep(k, st):
                 if k < node.lo:
@@ -1085,7 +1216,23 @@ class _Compiler:
                     if k < node.hi:
                         self.build(node.node, st, lambda x: rep(k + 1, x))
             rep(0, s)
+            self.loop_depth -= 1
             cont(j)
+        elif isinstance(node, Look) and self.loop_depth:  # an obligation (its continuation loops)
+            if isinstance(node, DollarLook):
+                raise PatternNotSupported("$ inside a quantifier")
+            x = _Compiler()
+            xs = x.nfa.new()
+            x.final = x.nfa.new()
+            x.build(node.node, xs, lambda st: x.nfa.eps[st].append(x.univ))
+            if x.behinds or any(x.nfa.at0):
+                raise PatternNotSupported("an anchor or lookbehind inside a lookahead in a quantifier")
+            x.resolve_lookaheads()
+            d_x = minimize(determinize(x.nfa, xs, frozenset([x.final]), x.univ, aheads=x.aheads))
+            t = self.nfa.new()
+            self.nfa.ahead[s].append((len(self.aheads), t))
+            self.aheads.append(_Ahead(d_x, node.negative))
+            cont(t)
         elif isinstance(node, Look):
             mark = self.nfa.new()
             self.pending.append((s, mark, node))  # before cont: lookaheads after it come later
@@ -1130,7 +1277,7 @@ class _Compiler:
                 if nfa.at0[q] or nfa.behind[q]:
                     raise PatternNotSupported("^, \\b or a lookbehind after a lookahead or $ "
                                               "inside the pattern")
-                for t in nfa.eps[q] + [t for _, t in nfa.trans[q]]:
+                for t in nfa.eps[q] + [t for _, t in nfa.trans[q]] + [t for _, t in nfa.ahead[q]]:
                     if t not in seen:
                         seen.add(t)
                         stack.append(t)
@@ -1152,19 +1299,33 @@ class _Compiler:
             # (a continuation starts inside the text: no inner ^ is reachable from it, checked by
             # check_inner_anchors)
             d_cont = minimize(determinize(self.nfa, mark, frozenset([self.final]), self.univ,
-                                          at_start=False))
+                                          at_start=False, aheads=self.aheads))
             x = _Compiler()
             xs = x.nfa.new()
             x.final = x.nfa.new()
             x.build(node.node, xs, lambda st: x.nfa.eps[st].append(x.univ))
             x.resolve_lookaheads()
-            d_x = minimize(determinize(x.nfa, xs, frozenset([x.final]), x.univ))
+            d_x = minimize(determinize(x.nfa, xs, frozenset([x.final]), x.univ, aheads=x.aheads))
             op = (lambda p, q: p and not q) if node.negative else (lambda p, q: p and q)
             d = minimize(product(d_cont, d_x, op))
             st, fi = dfa_to_nfa(d, self.nfa, self.univ)
             self.nfa.eps[s].append(st)
             self.nfa.eps[fi].append(self.final)
         self.pending = []
+
+
+def _has_lookahead(n) -> bool:
+    """Whether n holds a lookahead (or an anchor other than ^, which becomes one)."""
+    if isinstance(n, Look) or (isinstance(n, Anchor) and n.kind != "^"):
+        return True
+    if isinstance(n, Behind):
+        return False
+    for attr in ("items", "options"):
+        if hasattr(n, attr) and any(_has_lookahead(x) for x in getattr(n, attr)):
+            return True
+    if isinstance(n, (Repeat, Group)):
+        return _has_lookahead(n.node)
+    return False
 
 
 def _has_look(n) -> bool:
@@ -1332,7 +1493,8 @@ def compile_java_regex(pattern: str) -> CompiledRegex:
     c.build(body, p, tail)
     c.check_inner_anchors()
     c.resolve_lookaheads()
-    d = minimize(determinize(c.nfa, s0, frozenset([c.final]), c.univ, behinds=c.behinds))
+    d = minimize(determinize(c.nfa, s0, frozenset([c.final]), c.univ, behinds=c.behinds,
+                             aheads=c.aheads))
     return _finish(pattern, d)
 
 
@@ -1533,6 +1695,8 @@ def _rewrite_inner_anchors(n, in_look: bool = False, consumes_after: bool = Fals
     of Java's Bound."""
     if isinstance(n, Anchor):
         if n.kind == "$":
+            if in_look and not no_cr_before:  # (the NFA check below sees only the outer pattern)
+                raise PatternNotSupported("$ inside a lookahead, after a possible \\r")
             return DollarLook(Seq((Repeat(_LINE_END, 0, 1), EndText())), False)
         if n.kind == "\\z":
             return Look(EndText(), False)
@@ -1547,6 +1711,8 @@ def _rewrite_inner_anchors(n, in_look: bool = False, consumes_after: bool = Fals
         if n.kind == "$m":  # before any line terminator but never between "\r\n", or at the end
             if no_cr_before:  # (the previous character is never '\r': no lookbehind needed)
                 return Look(Alt((Chars(LINE_TERMINATORS), EndText())), False)
+            if in_look:
+                raise PatternNotSupported("$ inside a lookahead, after a possible \\r")
             return Alt((Seq((Behind(cr, True), Look(lf, False))),
                         Look(Chars(cs_norm([(13, 13), (0x85, 0x85), (0x2028, 0x2029)])), False),
                         Look(EndText(), False)))
@@ -1579,8 +1745,12 @@ def _rewrite_inner_anchors(n, in_look: bool = False, consumes_after: bool = Fals
         return Group(_rewrite_inner_anchors(n.node, in_look, consumes_after, no_cr_before), n.index)
     if isinstance(n, Repeat):
         return Repeat(_rewrite_inner_anchors(n.node, in_look), n.lo, n.hi, n.greedy)
-    if isinstance(n, (Look, Behind)):
-        return type(n)(_rewrite_inner_anchors(n.node, True), n.negative)
+    if isinstance(n, Behind) and in_look:  # (a lookahead's automaton does not track them)
+        raise PatternNotSupported("a lookbehind inside a lookahead")
+    if isinstance(n, Look):  # (its body starts where the lookahead stands)
+        return Look(_rewrite_inner_anchors(n.node, True, False, no_cr_before), n.negative)
+    if isinstance(n, Behind):
+        return Behind(_rewrite_inner_anchors(n.node, True), n.negative)
     return n
 
 

@@ -107,6 +107,18 @@ FUZZ = [
     (r"(?<sep>[-/])\d\k<sep>\d", "-/1", 6),
     (r"\va\V", "a\n\r\x85 x", 5),
     (r"(?x)\p{Upper} \Q a b\E", "A ab", 7),
+    # lookaheads inside a quantifier (obligations carried by each thread of the subset
+    # construction), lookbehinds and ^ inside one (positional)
+    (r"a(?:(?!b).)*c", "abcx", 8),
+    (r"a(?:(?!bc).)+d", "abcdx", 9),
+    (r"<(?:(?!<).)*>", "<a>b<", 8),
+    (r"(?:\w(?=\d))+\d", "a1b2_", 8),
+    (r"(?:a\b)+", "a b", 6),
+    (r"q(?:(?!x|yz)[xyz])*q", "qxyz", 8),
+    (r"(?:a(?=b|$))+", "ab\n\r", 6),
+    (r"(?=a)(?:a(?!a))+b", "ab", 6),
+    (r"(?:(?<=a)b)+c", "abc", 7),
+    (r"(?m)(?:^a)+|x(?:(?<![0-9])[a-c])*y", "a\nbxy1c", 8),
 ]
 
 
@@ -165,10 +177,12 @@ def test_nullable_known_answers():
                                      r"\pL", r"\p{IsDigit}", r"(?i)\p{Lower}",
                                      # inner anchors the automaton cannot decide: a $ after a
                                      # possible \r, a ^ after a lookahead, ^ in a loop
-                                     r"(?:a|\r)$x?", r"(?=a)(^|b)a", r"(?:^a)+",
+                                     r"(?:a|\r)$x?", r"(?=a)(^|b)a",
+                                     # $ in a lookahead after a possible \r, a lookbehind in one
+                                     r"\r(?=$)", r"a(?=\r$)", r"(?=(?<=a)b)b",
                                      # lookbehinds: unbounded (Java refuses it too), holding a
                                      # lookaround, in a lookahead's continuation, in a loop
-                                     r"(?<=a+)b", r"(?<=(?=a)a)b", r"(?=a)a(?<=a)b", r"(?:(?<=a)b)+",
+                                     r"(?<=a+)b", r"(?<=(?=a)a)b", r"(?=a)a(?<=a)b",
                                      r"(?=a)a\bb"])
 def test_unsupported_patterns_are_refused(pattern):
     with pytest.raises(PatternNotSupported):
