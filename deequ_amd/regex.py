@@ -74,6 +74,11 @@ class PatternNotSupported(ValueError):
     pass
 
 
+class _NeedsObligations(PatternNotSupported):
+    """Refused by the lookahead product construction only: compile_java_regex retries with every
+    lookahead as an obligation (exact $, lookbehinds and ^ after lookaheads)."""
+
+
 # ------------------------------------------------------------------------------------------------
 # Character sets: sorted disjoint code point intervals
 # ------------------------------------------------------------------------------------------------
@@ -1148,6 +1153,7 @@ class _Compiler:
         self.behinds: List[Tuple[DFA, bool]] = []  # (suffix DFA, negative) per lookbehind
         self.aheads: List[_Ahead] = []  # lookaheads inside a quantifier, as obligations
         self.loop_depth = 0
+        self.all_aheads = False  # every lookahead an obligation (compile_java_regex's retry)
 
     @property
     def univ(self) -> int:
@@ -1218,7 +1224,7 @@ class _Compiler:
             rep(0, s)
             self.loop_depth -= 1
             cont(j)
-        elif isinstance(node, Look) and self.loop_depth:  # an obligation (its continuation loops)
+        elif isinstance(node, Look) and (self.loop_depth or self.all_aheads):  # an obligation
             if isinstance(node, DollarLook):
                 raise PatternNotSupported("$ inside a quantifier")
             x = _Compiler()
@@ -1275,8 +1281,8 @@ class _Compiler:
             while stack:
                 q = stack.pop()
                 if nfa.at0[q] or nfa.behind[q]:
-                    raise PatternNotSupported("^, \\b or a lookbehind after a lookahead or $ "
-                                              "inside the pattern")
+                    raise _NeedsObligations("^, \\b or a lookbehind after a lookahead or $ "
+                                            "inside the pattern")
                 for t in nfa.eps[q] + [t for _, t in nfa.trans[q]] + [t for _, t in nfa.ahead[q]]:
                     if t not in seen:
                         seen.add(t)
@@ -1292,7 +1298,7 @@ class _Compiler:
                             stack.append(u)
                 for u in range(len(nfa.trans)):
                     if any(t in pred and (m >> 13) & 1 for m, t in nfa.trans[u]):
-                        raise PatternNotSupported("$ after a pattern that may end in \\r")
+                        raise _NeedsObligations("$ after a pattern that may end in \\r")
 
     def resolve_lookaheads(self):
         for s, mark, node in reversed(self.pending):
@@ -1422,31 +1428,41 @@ class CompiledRegex:
 
 def compile_java_regex(pattern: str) -> CompiledRegex:
     """Java regex -> DFA over UTF-8 bytes with PatternMatch's find-non-empty semantics."""
+    try:
+        return _compile_java_regex(pattern, False)
+    except _NeedsObligations:
+        return _compile_java_regex(pattern, True)
+
+
+def _compile_java_regex(pattern: str, exact: bool) -> CompiledRegex:
+    """exact: every lookahead as an obligation, and $ compiled as Java's Dollar exactly."""
     ast = _Parser(pattern).parse()
     items = list(ast.items) if isinstance(ast, Seq) else [ast]
     start_anchor = end_anchor = None
     # (anchors the edge handling below decides; any other one is an inner anchor)
     if items and isinstance(items[0], Anchor) and items[0].kind in ("^", "\\b"):
         start_anchor = items.pop(0).kind
-    if items and isinstance(items[-1], Anchor) and items[-1].kind in ("$", "\\z", "\\b"):
+    if items and isinstance(items[-1], Anchor) and items[-1].kind in (
+            ("\\z", "\\b") if exact else ("$", "\\z", "\\b")):
         end_anchor = items.pop().kind
     if nullable(Seq(tuple(items))) and start_anchor in (None, "^") and end_anchor is None:
         # the empty match at offset 0 always succeeds, so find()'s first match starts there:
         # whether it is the non-empty one depends on the match PREFERENCE (greedy / lazy,
         # alternation order), modelled by an ordered-thread automaton
         return compile_nullable(pattern, Seq(tuple(items)))
-    body = _rewrite_inner_anchors(expand_backrefs(Seq(tuple(items))))
+    body = _rewrite_inner_anchors(expand_backrefs(Seq(tuple(items))), exact=exact)
     if nullable(body):
         raise PatternNotSupported(
             "a pattern that can match the empty string next to an anchor, a lookaround or a "
             "back-reference (the first match need not start at offset 0)")
     c = _Compiler()
+    c.all_aheads = exact
     s0 = c.nfa.new()
     c.final = c.nfa.new()
     bound_word = bound_word_chars() if "\\b" in (start_anchor, end_anchor) else WORD
     non_word = cs_neg(bound_word)
     if end_anchor == "$" and _may_end_with(body, 13):
-        raise PatternNotSupported("$ after a pattern that may end in \\r")
+        raise _NeedsObligations("$ after a pattern that may end in \\r")
     # prefix: Sigma*, honouring a leading ^ or \b
     if start_anchor == "^":
         p = s0
@@ -1688,15 +1704,23 @@ _LINE_END = Alt((Seq((Chars(((13, 13),)), Chars(((10, 10),)))), Chars(LINE_TERMI
 
 
 def _rewrite_inner_anchors(n, in_look: bool = False, consumes_after: bool = False,
-                           no_cr_before: bool = False):
+                           no_cr_before: bool = False, exact: bool = False):
     """Anchors inside a (non-nullable) pattern: $ and \\Z become the lookahead "at most one
     line terminator, then the end" (DollarLook), \\z the lookahead "the end", ^ and \\A an edge
     taken only at the start of the text (NFA.at0); \\b / \\B the lookbehind-and-lookahead pairs
-    of Java's Bound."""
+    of Java's Bound.  exact (every lookahead an obligation): $ and \\Z as Java's Dollar exactly,
+    its "never between \\r\\n" a lookbehind."""
     if isinstance(n, Anchor):
         if n.kind == "$":
             if in_look and not no_cr_before:  # (the NFA check below sees only the outer pattern)
                 raise PatternNotSupported("$ inside a lookahead, after a possible \\r")
+            if exact and not in_look:
+                cr, lf = Chars(((13, 13),)), Chars(((10, 10),))
+                other = Chars(cs_norm([(13, 13), (0x85, 0x85), (0x2028, 0x2029)]))
+                return Alt((Look(EndText(), False),
+                            Seq((Behind(cr, True), Look(Seq((lf, EndText())), False))),
+                            Look(Seq((other, EndText())), False),
+                            Look(Seq((cr, lf, EndText())), False)))
             return DollarLook(Seq((Repeat(_LINE_END, 0, 1), EndText())), False)
         if n.kind == "\\z":
             return Look(EndText(), False)
@@ -1736,21 +1760,21 @@ def _rewrite_inner_anchors(n, in_look: bool = False, consumes_after: bool = Fals
             pre = Seq(n.items[:k])
             return not _may_end_with(pre, 13) and (no_cr_before or not nullable(pre))
         return Seq(tuple(_rewrite_inner_anchors(x, in_look, consumes_after
-                                                or not nullable(Seq(n.items[k + 1:])), before(k))
+                                                or not nullable(Seq(n.items[k + 1:])), before(k), exact)
                          for k, x in enumerate(n.items)))
     if isinstance(n, Alt):
-        return Alt(tuple(_rewrite_inner_anchors(x, in_look, consumes_after, no_cr_before)
+        return Alt(tuple(_rewrite_inner_anchors(x, in_look, consumes_after, no_cr_before, exact)
                          for x in n.options))
     if isinstance(n, Group):
-        return Group(_rewrite_inner_anchors(n.node, in_look, consumes_after, no_cr_before), n.index)
+        return Group(_rewrite_inner_anchors(n.node, in_look, consumes_after, no_cr_before, exact), n.index)
     if isinstance(n, Repeat):
-        return Repeat(_rewrite_inner_anchors(n.node, in_look), n.lo, n.hi, n.greedy)
+        return Repeat(_rewrite_inner_anchors(n.node, in_look, exact=exact), n.lo, n.hi, n.greedy)
     if isinstance(n, Behind) and in_look:  # (a lookahead's automaton does not track them)
         raise PatternNotSupported("a lookbehind inside a lookahead")
     if isinstance(n, Look):  # (its body starts where the lookahead stands)
-        return Look(_rewrite_inner_anchors(n.node, True, False, no_cr_before), n.negative)
+        return Look(_rewrite_inner_anchors(n.node, True, False, no_cr_before, exact), n.negative)
     if isinstance(n, Behind):
-        return Behind(_rewrite_inner_anchors(n.node, True), n.negative)
+        return Behind(_rewrite_inner_anchors(n.node, True, exact=exact), n.negative)
     return n
 
 
