@@ -19,7 +19,8 @@ escaped metacharacters), ``.`` (any code point but the Java line terminators), c
 negation, nested escapes and \\d \\D \\s \\S \\w \\W (ASCII, as Java without UNICODE_CHARACTER_CLASS),
 \\h \\H \\v \\V, the US-ASCII POSIX classes \\p{Lower} ... \\p{Space} and their \\P{...}
 complements, \\Q...\\E (Pattern.java's RemoveQEQuoting, before parsing), groups ( ), (?: ),
-named groups (?<name> ) with \\k<name>, alternation, greedy / lazy quantifiers * + ? {n} {n,} {n,m}, lookaheads (?= )
+named groups (?<name> ) with \\k<name>, class unions [a[b]] and intersections [a-z&&[^b]],
+alternation, greedy / lazy quantifiers * + ? {n} {n,} {n,m}, lookaheads (?= )
 (?! ), back-references to groups with a finite language (expanded: the CREDITCARD separators),
 ^ / \\A at the start; $ / \\Z (end, or before one final line terminator, "\\r\\n" included) and
 \\z (strict end) at the end; \\b at the start or end of the pattern; anchors, \\b / \\B and
@@ -90,6 +91,10 @@ def cs_norm(r: Sequence[Tuple[int, int]]) -> Tuple[Tuple[int, int], ...]:
         else:
             out.append([a, b])
     return tuple((a, b) for a, b in out)
+
+
+def cs_and(a, b) -> Tuple[Tuple[int, int], ...]:
+    return cs_neg(list(cs_neg(a)) + list(cs_neg(b)))
 
 
 def cs_neg(r) -> Tuple[Tuple[int, int], ...]:
@@ -534,12 +539,38 @@ class _Parser:
             v = ord(c)
         return Chars(self.fold(((v, v),))) if not in_class else ((v, v),)
 
+    def _class_item(self):
+        """One plain item of a class (a character, an escape or a range), as code point ranges."""
+        c = self.take()
+        lo_set = self.escape(in_class=True) if c == "\\" else ((ord(c), ord(c)),)
+        if (len(lo_set) == 1 and lo_set[0][0] == lo_set[0][1] and self.peek() == "-"
+                and self.i + 1 < len(self.s) and self.s[self.i + 1] not in "[]"):
+            self.take()
+            d = self.take()
+            if d == "\\":
+                hi_set = self.escape(in_class=True)
+                if len(hi_set) != 1 or hi_set[0][0] != hi_set[0][1]:
+                    self.error("class range to a class")
+                hi = hi_set[0][0]
+            else:
+                hi = ord(d)
+            if hi < lo_set[0][0]:
+                self.error("inverted class range")
+            return ((lo_set[0][0], hi),)
+        return lo_set
+
     def char_class(self):
+        """A class after its '['.  Nested classes are unions and '&&' intersects what precedes
+        with its right operand (one nested class, or plain items up to ']' / '&&'), as Pattern.java
+        (JDK 8) parses them; each item is case folded before the sets combine.  A negated class
+        holding either is refused: JDK 8 negates only its plain items there (later JDKs the
+        whole class), and nothing here pins which one the reference ran."""
         neg = False
         if self.peek() == "^":
             self.take()
             neg = True
         ranges: List[Tuple[int, int]] = []
+        acc: Optional[Tuple[Tuple[int, int], ...]] = None  # nested classes / intersections so far
         first = True
         while True:
             c = self.peek()
@@ -549,32 +580,36 @@ class _Parser:
                 self.take()
                 break
             first = False
-            if c == "[":
-                self.error("nested character class")
-            if c == "&" and self.s.startswith("&&", self.i):
-                self.error("class intersection")
-            self.take()
-            if c == "\\":
-                lo_set = self.escape(in_class=True)
-            else:
-                lo_set = ((ord(c), ord(c)),)
-            if (len(lo_set) == 1 and lo_set[0][0] == lo_set[0][1] and self.peek() == "-"
-                    and self.i + 1 < len(self.s) and self.s[self.i + 1] != "]"):
-                self.take()
-                d = self.take()
-                if d == "\\":
-                    hi_set = self.escape(in_class=True)
-                    if len(hi_set) != 1 or hi_set[0][0] != hi_set[0][1]:
-                        self.error("class range to a class")
-                    hi = hi_set[0][0]
+            if c == "[" or (c == "&" and self.s.startswith("&&", self.i)):
+                if neg:
+                    self.error("a nested class or && inside a negated class")
+                left = cs_norm(list(self.fold(cs_norm(ranges))) + list(acc or ()))
+                if c == "[":
+                    self.take()
+                    acc, ranges = cs_norm(list(left) + list(self.char_class())), []
+                    continue
+                had_left = bool(ranges) or acc is not None
+                self.i += 2
+                if self.peek() == "[":
+                    self.take()
+                    right = self.char_class()
                 else:
-                    hi = ord(d)
-                if hi < lo_set[0][0]:
-                    self.error("inverted class range")
-                ranges.append((lo_set[0][0], hi))
-            else:
-                ranges.extend(lo_set)
+                    items: List[Tuple[int, int]] = []
+                    while self.peek() is not None and self.peek() != "]" and not (
+                            self.peek() == "&" and self.s.startswith("&&", self.i)):
+                        if self.peek() == "[":
+                            self.error("a right operand of && mixing a class and items")
+                        items.extend(self._class_item())
+                    right = self.fold(cs_norm(items))
+                if not (self.peek() == "]" or self.s.startswith("&&", self.i)):
+                    self.error("a right operand of && followed by more items")
+                acc = cs_and(left, right) if had_left else right
+                ranges = []
+                continue
+            ranges.extend(self._class_item())
         r = self.fold(cs_norm(ranges))  # (case folded before the negation, as Java)
+        if acc is not None:
+            r = cs_norm(list(r) + list(acc))
         return cs_neg(r) if neg else r
 
 

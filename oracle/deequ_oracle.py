@@ -731,6 +731,96 @@ _VSP = "\\n\\x0b\\f\\r\\x85\\u2028\\u2029"
 _JAVA_HV = {"\\h": _HSP, "\\H": _HSP, "\\v": _VSP, "\\V": _VSP}
 
 
+def _java_class_has_ops(p: str, i: int) -> bool:
+    """Whether the class opening at p[i] holds a nested class or && (Java class set operations)."""
+    j = i + 1
+    if p.startswith("^", j):
+        j += 1
+    first = True
+    while j < len(p):
+        c = p[j]
+        if c == "\\":
+            j += 2
+        elif c == "]" and not first:
+            return False
+        elif c == "[" or p.startswith("&&", j):
+            return True
+        else:
+            j += 1
+        first = False
+    return False
+
+
+def _java_class_to_py(p: str, i: int):
+    """A Java class with nested classes / && (JDK 8 Pattern.clazz, non-negated) at p[i] -> a
+    Python one-character expression: a union as an alternation of classes, A && B as the
+    lookahead (?=A) before B.  Returns (expression, index after the class)."""
+    i += 1
+    assert not p.startswith("^", i), "a negated class with set operations is not restated"
+    alts, plain, first = [], [], True
+
+    def item(i):
+        if p[i] != "\\":
+            return p[i], i + 1
+        e = p[i:i + 2]
+        if e in ("\\p", "\\P"):
+            j = p.index("}", i) if p.startswith("{", i + 2) else i + 2
+            name = p[i + 3:j] if p.startswith("{", i + 2) else p[i + 2]
+            assert e == "\\p", "\\P inside a class with set operations"
+            return _JAVA_POSIX[name], j + 1
+        if e in _JAVA_HV:
+            assert e[1].islower()
+            return _JAVA_HV[e], i + 2
+        return e, i + 2
+
+    def union(alts, plain):
+        parts = list(alts) + (["[" + "".join(plain) + "]"] if plain else [])
+        return "(?:" + "|".join(parts) + ")" if parts else None
+
+    while True:
+        c = p[i]
+        if c == "]" and not first:
+            i += 1
+            break
+        first = False
+        if c == "[":
+            sub, i = _java_class_to_py(p, i) if _java_class_has_ops(p, i) else _py_plain_class(p, i)
+            alts.append(sub)
+        elif p.startswith("&&", i):
+            left = union(alts, plain)
+            i += 2
+            if p[i] == "[":
+                right, i = (_java_class_to_py(p, i) if _java_class_has_ops(p, i)
+                            else _py_plain_class(p, i))
+            else:
+                items = []
+                while p[i] != "]" and not p.startswith("&&", i):
+                    x, i = item(i)
+                    items.append(x)
+                right = "[" + "".join(items) + "]"
+            alts, plain = [right if left is None else f"(?:(?={left}){right})"], []
+        else:
+            x, i = item(i)
+            plain.append(x)
+    return union(alts, plain) or "[^\\s\\S]", i
+
+
+def _py_plain_class(p: str, i: int):
+    """A plain Java class (no set operations) at p[i], copied as a Python class."""
+    j = i + 1
+    if p.startswith("^", j):
+        j += 1
+    first = True
+    while True:
+        if p[j] == "\\":
+            j += 2
+        elif p[j] == "]" and not first:
+            return p[i:j + 1], j + 1
+        else:
+            j += 1
+        first = False
+
+
 def _java_remove_qe(p: str) -> str:
     """Pattern.java's RemoveQEQuoting: \\Q...\\E becomes its characters, each escaped."""
     out, i = [], 0
@@ -861,6 +951,10 @@ def java_regex_to_python(pattern: str) -> str:
             if c == "]" and not (out and out[-1] in ("[", "[^")):
                 in_class = False
             out.append(c)
+        elif c == "[" and _java_class_has_ops(pattern, i):  # class set operations
+            expr, i = _java_class_to_py(pattern, i)
+            out.append(expr)
+            continue
         elif c == "[":
             in_class = True
             if pattern.startswith("[^", i):

@@ -130,6 +130,13 @@ FUZZ = [
     (r"(?=a)(^|b)a", "ab", 5),
     (r"(?=a)a(?<=a)b|(?=a)a\bb", "ab ", 5),
     (r"(?=.*\d)\w+\r$", "a1\r\n", 6),
+    # class set operations (JDK 8 Pattern.clazz): nested classes are unions, && intersects
+    (r"[a-z&&[^aeiou]]{2}", "abeiz1", 6),
+    (r"x[a-d[m-p]]y", "xaymyzy", 6),
+    (r"[\w&&[^\d_]]+\d", "a1_Z9 ", 6),
+    (r"[a-z&&def]!|[abc&&b-d&&[^c]]", "abcdf!", 5),
+    (r"(?i)[a-c&&[B-Z]]x", "aAbBcCx", 5),
+    (r"[[a-c][x-z]&&[^by]]q|[\p{Alpha}&&[^a-f]][a[b]c]", "abcxyzqfg", 5),
 ]
 
 
@@ -190,7 +197,10 @@ def test_nullable_known_answers():
                                      r"\r(?=$)", r"a(?=\r$)", r"(?=(?<=a)b)b",
                                      # lookbehinds: unbounded (Java refuses it too), holding a
                                      # lookaround
-                                     r"(?<=a+)b", r"(?<=(?=a)a)b"])
+                                     r"(?<=a+)b", r"(?<=(?=a)a)b",
+                                     # set operations in a negated class (JDK 8 negates only
+                                     # its plain items), a mixed right operand of &&
+                                     r"[^a[b]]", r"[^a&&b]", r"[a&&[b]c]"])
 def test_unsupported_patterns_are_refused(pattern):
     with pytest.raises(PatternNotSupported):
         compile_java_regex(pattern)
