@@ -43,7 +43,8 @@ thread of the subset construction that crosses it carries the lookahead's automa
 with every symbol, and dies when it fails (_determinize_obligations).
 
 Rejected (a PatternNotSupported error, never a silently different answer): nullable patterns with
-a lookaround, back-reference or trailing anchor, possessive quantifiers, unbounded lookbehinds,
+a lookaround, back-reference or trailing anchor, possessive quantifiers over more than one
+character class (over one, C*+ is C*(?!C)), atomic groups, unbounded lookbehinds,
 the flags U and i with u, anchors / lookbehinds the automaton cannot place (after a lookahead, or
 inside a lookaround), $ after a pattern that may end in "\\r" (Java's $ never matches between
 "\\r\\n"), and automata above ``MAX_STATES``.
@@ -348,9 +349,24 @@ class _Parser:
             if self.peek() == "?":  # lazy: the same language, shortest first
                 self.take()
                 greedy = False
-            elif self.peek() == "+":
-                self.error("possessive quantifier")
+            elif self.peek() == "+":  # possessive: C*+ never gives back a C
+                self.take()
+                atom = self._possessive(atom, lo, hi)
+                continue
             atom = Repeat(atom, lo, hi, greedy)
+
+    def _possessive(self, atom, lo, hi):
+        """C{lo,hi}+ over one character class C: as many C as there are, up to hi, never fewer --
+        C{lo,}(?!C), or C{hi} | C{lo,hi-1}(?!C).  (Over anything longer the committed match is
+        not a regular property of the text here.)"""
+        if not isinstance(atom, Chars):
+            self.error("possessive quantifier over more than one character class")
+        if hi is not None and hi == lo:
+            return Repeat(atom, lo, hi, True)
+        stop = Look(atom, True)
+        if hi is None:
+            return Seq((Repeat(atom, lo, None, True), stop))
+        return Alt((Repeat(atom, hi, hi, True), Seq((Repeat(atom, lo, hi - 1, True), stop))))
 
     def _is_counted(self):
         j = self.i + 1

@@ -857,6 +857,7 @@ def java_regex_to_python(pattern: str) -> str:
     scopes = [[]]
     fl = {"i": False, "d": False, "m": False, "s": False, "x": False, "u": False}
     saved = []  # the flags at each open group
+    atom_at, n_atomic = None, 0  # where the last one-character atom's output starts
     while i < len(pattern):
         c = pattern[i]
         if fl["x"] and c in " \t\n\x0b\f\r":  # COMMENTS: white space ignored, classes too
@@ -912,6 +913,22 @@ def java_regex_to_python(pattern: str) -> str:
                 out.extend(scopes[-1])
                 i += 1
                 continue
+        if not in_class:  # a possessive quantifier over the last atom: Python 3.10 has none, so
+            # the atomic-group idiom (?=(?P<a>X*))(?P=a) -- the lookahead's preferred match, kept
+            q = re.match(r"(?:[*+?]|\{\d+(?:,\d*)?\})\+", pattern[i:])
+            if q and i > 0 and pattern[i - 1] != "(":
+                assert atom_at is not None, "possessive quantifier over a group is not restated"
+                atom = "".join(out[atom_at:])
+                del out[atom_at:]
+                out.append(f"(?=(?P<_pq{n_atomic}>{atom}{q.group(0)[:-1]}))(?P=_pq{n_atomic})")
+                n_atomic += 1
+                atom_at = None
+                i += q.end()
+                continue
+            if c == "\\" or c == "[" or c == "." or c not in "()|*+?{}^$":
+                atom_at = len(out)
+            elif c in ")|(":
+                atom_at = None
         if c == "\\":
             e = pattern[i:i + 2]
             if not in_class and e == "\\b":

@@ -96,7 +96,9 @@ def test_pattern_match_floating_point_columns_match_oracle(pattern, dtype, gpu_d
                                      # exact $ (never between CR and LF), a lookbehind after a lookahead
                                      r"[a-z]\s$", r"(?=\d)\d(?<=[0-4])[5-9]",
                                      # class set operations
-                                     r"[a-z&&[^aeiou]]{2}\d", r"[\d[h-t]&&[^5-9p]]{3}"])
+                                     r"[a-z&&[^aeiou]]{2}\d", r"[\d[h-t]&&[^5-9p]]{3}",
+                                     # possessive quantifiers
+                                     r"[a-z]++\d", r"\d{2,3}+-"])
 def test_pattern_match_matches_oracle_on_random_rows(pattern, gpu_device):
     from deequ_amd.analyzers import PatternMatch
     from oracle.deequ_oracle import OTable, agg_pattern_match

@@ -137,6 +137,12 @@ FUZZ = [
     (r"[a-z&&def]!|[abc&&b-d&&[^c]]", "abcdf!", 5),
     (r"(?i)[a-c&&[B-Z]]x", "aAbBcCx", 5),
     (r"[[a-c][x-z]&&[^by]]q|[\p{Alpha}&&[^a-f]][a[b]c]", "abcxyzqfg", 5),
+    # possessive quantifiers over one character class: C{lo,}(?!C), C{hi} | C{lo,hi-1}(?!C)
+    (r"a*+a|[a-z]++\d", "ab1 ", 6),
+    (r'"[^"]*+"', 'a""b', 6),
+    (r"\d{2,4}+5", "1235x", 7),
+    (r"b(?:a++|c)+d|x?+x", "abcdxy", 7),
+    (r"(?i)A++b|[ab]{1,3}+b", "aAbB", 6),
 ]
 
 
@@ -188,7 +194,7 @@ def test_nullable_known_answers():
     assert not compile_java_regex(r"(?:a??)+b?").matches("ab")
 
 
-@pytest.mark.parametrize("pattern", [r"a++", r"a*$", r"(?=x)a*", r"(a?)\1",
+@pytest.mark.parametrize("pattern", [r"(?:ab)++", r"a*$", r"(?=x)a*", r"(a?)\1",
                                      # Unicode case folding / character classes
                                      r"(?iu)a", r"(?U)\w", r"(?m)^$",
                                      # Unicode properties, \p{Lower} / \p{Upper} under (?i)
