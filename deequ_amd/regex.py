@@ -44,7 +44,8 @@ with every symbol, and dies when it fails (_determinize_obligations).
 
 Rejected (a PatternNotSupported error, never a silently different answer): nullable patterns with
 a lookaround, back-reference or trailing anchor, possessive quantifiers over more than one
-character class (over one, C*+ is C*(?!C)), atomic groups, unbounded lookbehinds,
+character class (over one, C*+ is C*(?!C)), atomic groups over unbounded languages (see
+_Parser._atomic), unbounded lookbehinds,
 the flags U and i with u, anchors / lookbehinds the automaton cannot place (after a lookahead, or
 inside a lookaround), $ after a pattern that may end in "\\r" (Java's $ never matches between
 "\\r\\n"), and automata above ``MAX_STATES``.
@@ -245,6 +246,53 @@ def _remove_qe_quoting(p: str) -> str:
     return "".join(out)
 
 
+def _preference_order(n, cap: int):
+    """The sequences of character classes X can match, in Java's backtracking order (alternatives
+    left to right, a greedy repeat's next iteration before its exit), or None when X has
+    anything else (an unbounded repeat, a lookaround, a nullable repeated body) or more than
+    `cap` of them."""
+    if isinstance(n, Chars):
+        return [(n,)]
+    if isinstance(n, Group):
+        return _preference_order(n.node, cap)
+    if isinstance(n, Seq):
+        out = [()]
+        for item in n.items:
+            opts = _preference_order(item, cap)
+            if opts is None:
+                return None
+            out = [a + b for a in out for b in opts]
+            if len(out) > cap:
+                return None
+        return out
+    if isinstance(n, Alt):
+        out = []
+        for o in n.options:
+            opts = _preference_order(o, cap)
+            if opts is None:
+                return None
+            out += opts
+        return out if len(out) <= cap else None
+    if isinstance(n, Repeat):
+        body = _preference_order(n.node, cap)
+        if n.hi is None or body is None or any(not b for b in body):
+            return None
+
+        def rep(k):
+            res = []
+            more = [b + r for b in body for r in rep(k + 1)] if k < n.hi else []
+            stop = [()] if k >= n.lo else []
+            res = more + stop if n.greedy else stop + more
+            if len(res) > cap:
+                raise OverflowError
+            return res
+        try:
+            return rep(0)
+        except OverflowError:
+            return None
+    return None
+
+
 class _Parser:
     # Java's embedded flags, each to the end of its group (or inside a (?flags:...) group)
     FLAGS = ("ci", "unix", "multiline", "dotall", "ucase", "comments")
@@ -368,6 +416,24 @@ class _Parser:
             return Seq((Repeat(atom, lo, None, True), stop))
         return Alt((Repeat(atom, hi, hi, True), Seq((Repeat(atom, lo, hi - 1, True), stop))))
 
+    def _atomic(self, x):
+        """(?>X): the first match of X in backtracking order, never given back.  One character
+        class repeated is the possessive form; a finite X is the alternation, over X's sequences
+        s1, s2, ... in that order, of "s_k where no earlier s_j starts here"."""
+        while isinstance(x, Group):
+            x = x.node
+        if isinstance(x, Repeat) and isinstance(x.node, Chars):
+            return self._possessive(x.node, x.lo, x.hi) if x.greedy else Repeat(x.node, x.lo, x.lo, True)
+        seqs = _preference_order(x, 32)
+        if seqs is None:
+            self.error("atomic group over an unbounded or large language")
+        opts = []
+        for k, sk in enumerate(seqs):
+            if any(seqs[j] == sk for j in range(k)):
+                continue
+            opts.append(Seq(tuple(Look(Seq(seqs[j]), True) for j in range(k)) + sk))
+        return Alt(tuple(opts)) if len(opts) != 1 else opts[0]
+
     def _is_counted(self):
         j = self.i + 1
         while j < len(self.s) and (self.s[j].isdigit() or self.s[j] == ","):
@@ -415,6 +481,9 @@ class _Parser:
                 neg = self.s[self.i + 2] == "!"
                 self.i += 3
                 node = Behind(self.alt(), neg)
+            elif self.s.startswith("?>", self.i):  # (?>X): atomic
+                self.i += 2
+                node = self._atomic(self._group_body())
             elif self.s.startswith("?<", self.i):  # (?<name>X): a capturing group with a name
                 j = self.s.find(">", self.i)
                 name = self.s[self.i + 2:j] if j > 0 else ""

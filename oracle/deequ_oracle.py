@@ -858,6 +858,7 @@ def java_regex_to_python(pattern: str) -> str:
     fl = {"i": False, "d": False, "m": False, "s": False, "x": False, "u": False}
     saved = []  # the flags at each open group
     atom_at, n_atomic = None, 0  # where the last one-character atom's output starts
+    closers = []  # per open group: what follows its ')' (an atomic group's backreference)
     while i < len(pattern):
         c = pattern[i]
         if fl["x"] and c in " \t\n\x0b\f\r":  # COMMENTS: white space ignored, classes too
@@ -888,6 +889,7 @@ def java_regex_to_python(pattern: str) -> str:
                 else:  # (?flags:...): a group of its own
                     saved.append(fl)
                     scopes.append([])
+                    closers.append("")
                     out.append("(?:")
                     if opener:
                         out.append(opener)
@@ -898,15 +900,30 @@ def java_regex_to_python(pattern: str) -> str:
             if pattern.startswith("(?<", i) and pattern[i + 3:i + 4].isalpha():  # named group
                 scopes.append([])
                 saved.append(dict(fl))
+                closers.append("")
                 out.append("(?P<")
+                i += 3
+                continue
+            if pattern.startswith("(?>", i):  # atomic group: the lookahead-and-backreference idiom
+                scopes.append([])
+                saved.append(dict(fl))
+                closers.append(f"))(?P=_ag{n_atomic})")
+                out.append(f"(?=(?P<_ag{n_atomic}>(?:")
+                n_atomic += 1
+                atom_at = None
                 i += 3
                 continue
             if c == "(":
                 scopes.append([])
                 saved.append(dict(fl))
+                closers.append("")
             elif c == ")" and len(scopes) > 1:
                 out.append(")" * len(scopes.pop()))
                 fl = saved.pop()
+                out.append(")" + closers.pop())
+                atom_at = None
+                i += 1
+                continue
             elif c == "|":
                 out.append(")" * len(scopes[-1]))
                 out.append("|")

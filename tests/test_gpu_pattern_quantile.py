@@ -98,7 +98,9 @@ def test_pattern_match_floating_point_columns_match_oracle(pattern, dtype, gpu_d
                                      # class set operations
                                      r"[a-z&&[^aeiou]]{2}\d", r"[\d[h-t]&&[^5-9p]]{3}",
                                      # possessive quantifiers
-                                     r"[a-z]++\d", r"\d{2,3}+-"])
+                                     r"[a-z]++\d", r"\d{2,3}+-",
+                                     # atomic groups
+                                     r"(?>ht|h)t", r"(?>\d{1,2})\d-"])
 def test_pattern_match_matches_oracle_on_random_rows(pattern, gpu_device):
     from deequ_amd.analyzers import PatternMatch
     from oracle.deequ_oracle import OTable, agg_pattern_match

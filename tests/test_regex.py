@@ -143,6 +143,13 @@ FUZZ = [
     (r"\d{2,4}+5", "1235x", 7),
     (r"b(?:a++|c)+d|x?+x", "abcdxy", 7),
     (r"(?i)A++b|[ab]{1,3}+b", "aAbB", 6),
+    # atomic groups: one class repeated (the possessive form), or a finite language as "s_k where
+    # no earlier s_j (backtracking order) starts here"
+    (r"(?>ab|a)b|(?>a|ab)c", "abc", 6),
+    (r"x(?>a*)a|x(?>a+?)a", "xa", 6),
+    (r"(?>(?:a|ab){0,2})c", "abc", 7),
+    (r"(?>[0-9]{1,3})5|(?i)(?>A|B)c", "0159aAbBcC", 6),
+    (r"(?>a?b?)c|q|(?>x(?:y|yz))z", "abcqxyz", 6),
 ]
 
 
@@ -194,7 +201,7 @@ def test_nullable_known_answers():
     assert not compile_java_regex(r"(?:a??)+b?").matches("ab")
 
 
-@pytest.mark.parametrize("pattern", [r"(?:ab)++", r"a*$", r"(?=x)a*", r"(a?)\1",
+@pytest.mark.parametrize("pattern", [r"(?:ab)++", r"(?>a+b)", r"a*$", r"(?=x)a*", r"(a?)\1",
                                      # Unicode case folding / character classes
                                      r"(?iu)a", r"(?U)\w", r"(?m)^$",
                                      # Unicode properties, \p{Lower} / \p{Upper} under (?i)
