@@ -17,7 +17,7 @@ stops early.
 Supported Java syntax: literals and escapes (\\t \\n \\r \\f \\a \\e \\xhh \\uhhhh \\0o \\cX and
 escaped metacharacters), ``.`` (any code point but the Java line terminators), classes with ranges,
 negation, nested escapes and \\d \\D \\s \\S \\w \\W (ASCII, as Java without UNICODE_CHARACTER_CLASS),
-\\h \\H \\v \\V, the US-ASCII POSIX classes \\p{Lower} ... \\p{Space} and their \\P{...}
+\\h \\H \\v \\V \\R, the US-ASCII POSIX classes \\p{Lower} ... \\p{Space} and their \\P{...}
 complements, \\Q...\\E (Pattern.java's RemoveQEQuoting, before parsing), groups ( ), (?: ),
 named groups (?<name> ) with \\k<name>, class unions [a[b]] and intersections [a-z&&[^b]],
 alternation, greedy / lazy quantifiers * + ? {n} {n,} {n,m}, lookaheads (?= )
@@ -591,6 +591,8 @@ class _Parser:
                 self.error(f"\\p{{{name}}} under (?i)")
             r = POSIX_CLASSES[name] if c == "p" else cs_neg(POSIX_CLASSES[name])
             return Chars(r) if not in_class else r
+        if c == "R" and not in_class:  # Java 8's LineEnding: \r\n taken whole, never given back
+            return self._atomic(Alt((Seq((Chars(((13, 13),)), Chars(((10, 10),)))), Chars(VSPACE))))
         if c == "k" and not in_class:  # \k<name>
             j = self.s.find(">", self.i)
             name = self.s[self.i + 1:j] if self.s.startswith("<", self.i) and j > 0 else None

@@ -907,8 +907,8 @@ def java_regex_to_python(pattern: str) -> str:
             if pattern.startswith("(?>", i):  # atomic group: the lookahead-and-backreference idiom
                 scopes.append([])
                 saved.append(dict(fl))
-                closers.append(f"))(?P=_ag{n_atomic})")
-                out.append(f"(?=(?P<_ag{n_atomic}>(?:")
+                closers.append(f"))(?P=_ag{n_atomic}))")  # (one group: a quantifier repeats it all)
+                out.append(f"(?:(?=(?P<_ag{n_atomic}>(?:")
                 n_atomic += 1
                 atom_at = None
                 i += 3
@@ -972,6 +972,9 @@ def java_regex_to_python(pattern: str) -> str:
                 body = _JAVA_HV[e]
                 assert not (in_class and e[1].isupper()), "\\H / \\V inside a class"
                 out.append(body if in_class else ("[^" if e[1].isupper() else "[") + body + "]")
+            elif e == "\\R" and not in_class:  # LineEnding (JDK 8): atomic \r\n | one terminator
+                out.append(f"(?:(?=(?P<_ag{n_atomic}>(?:\\r\\n|[{_VSP}])))(?P=_ag{n_atomic}))")
+                n_atomic += 1
             elif e == "\\k":  # \k<name>
                 j = pattern.index(">", i)
                 out.append(f"(?P={pattern[i + 3:j]})")

@@ -150,6 +150,10 @@ FUZZ = [
     (r"(?>(?:a|ab){0,2})c", "abc", 7),
     (r"(?>[0-9]{1,3})5|(?i)(?>A|B)c", "0159aAbBcC", 6),
     (r"(?>a?b?)c|q|(?>x(?:y|yz))z", "abcqxyz", 6),
+    (r"(?>ab|a){2}b", "ab", 7),
+    # \R: JDK 8's LineEnding, "\r\n" taken whole and never given back
+    (r"a\R\n|a\Rb", "ab\r\n\x0b\x85", 6),
+    (r"\R{2}x", "\r\nx\u2028", 6),
 ]
 
 
