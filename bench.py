@@ -147,7 +147,14 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=20_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-h2d", action="store_true", help="skip the host-fed (PCIe) measurement")
+    ap.add_argument("--workloads", default="c3,c4,c5",
+                    help="after the S10 leg (N=1 only): configs[2] (c3), configs[3] (c4) and "
+                         "configs[4] (c5) timed at their stated sizes; '' skips them")
+    ap.add_argument("--workload-budget-s", type=float, default=360.0,
+                    help="wall-clock budget of the whole run: a workload is skipped (and says so) "
+                         "once it would start past this many seconds")
     args = ap.parse_args()
+    t_start = time.perf_counter()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: relaunch under torch.distributed.run as a CHILD process, before this
@@ -274,9 +281,42 @@ def main():
             out["h2d_inclusive"] = h2d_inclusive(plan, state, args.seed)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.seed)
+        if world == 1 and args.workloads:
+            del table, state, plan
+            N.release_cached_memory()
+            out["workloads"] = other_workloads(args, t_start)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+WORKLOAD_CONFIG = {"c3": "configs[2]", "c4": "configs[3]", "c5": "configs[4]"}
+
+
+def other_workloads(args, t_start: float) -> dict:
+    """BASELINE.json configs[2]-[4] on this GPU, after the S10 leg and outside its timed region
+    (tools/bench_workloads.run_single: each builds its synthetic table at the stated per-GPU size,
+    runs untimed warmup steps, then times its steps between two device syncs).  Each record carries
+    ms_per_step, algorithmic_bytes and frac (= algorithmic bytes / device time per step / 8 TB/s)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_workloads as W
+    from deequ_amd import _native as N
+    res = {}
+    for wl in [w for w in args.workloads.split(",") if w]:
+        key = WORKLOAD_CONFIG[wl]
+        if time.perf_counter() - t_start > args.workload_budget_s:
+            res[key] = {"workload": wl, "skipped": f"past the {args.workload_budget_s:.0f} s budget"}
+            continue
+        steps = min(args.steps, 5) if wl == "c5" else args.steps
+        t0 = time.perf_counter()
+        r = W.run_single(wl, W.DEFAULT_ROWS[wl], steps, max(1, min(args.warmup, 2)),
+                         args.batch_rows)
+        r["wall_s_incl_table_build"] = time.perf_counter() - t0
+        res[key] = r
+        N.release_cached_memory()
+        print(f"bench.py: {key} ({wl}) {r['ms_per_step']:.2f} ms/step, frac "
+              f"{r['frac']:.4f}", file=sys.stderr, flush=True)
+    return res
 
 
 def scan_code_object_hash() -> str:

@@ -78,24 +78,38 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         return run_distributed(args, world, rank, local)
-    dev = "cuda:0"
+    rows = args.rows or DEFAULT_ROWS[args.workload]
+    out = run_single(args.workload, rows, args.steps, args.warmup, args.batch_rows,
+                     runner=args.runner, pyprof=args.pyprof, verbose=True,
+                     cpu_rows=args.cpu_rows if args.cpu_baseline else None)
+    print(json.dumps(out), flush=True)
+
+
+DEFAULT_ROWS = {"c3": 1_000_000_000, "c4": 1_250_000_000, "c5": 125_000_000}
+
+
+def run_single(workload: str, rows: int, steps: int, warmup: int, batch_rows: int = 1 << 26,
+               runner: bool = False, pyprof: bool = False, verbose: bool = False,
+               cpu_rows=None, dev: str = "cuda:0") -> dict:
+    """One workload on one GPU: builds its synthetic table in HBM, runs `warmup` untimed steps,
+    times `steps` steps (wall clock between two device syncs, and HIP events on the stream per
+    step) and returns the JSON record.  bench.py calls it for configs[2]-[4] after its S10 leg."""
+    import torch
     from deequ_amd.synth import item_table_device
-    # c5: the per-GPU shard of 1e9 rows over 8 GPUs (20 columns, ~280 B/row with the strings)
-    rows = args.rows or {"c3": 1_000_000_000, "c4": 1_250_000_000, "c5": 125_000_000}[args.workload]
-    if args.workload == "c5":
+    if workload == "c5":
         from deequ_amd.synth import profiling_table_device
         # description strings average ~40 B: 2^25-row batches keep int32 offsets in range
-        table = profiling_table_device(rows, batch_rows=min(args.batch_rows, 1 << 25), device=dev)
+        table = profiling_table_device(rows, batch_rows=min(batch_rows, 1 << 25), device=dev)
         torch.cuda.empty_cache()  # the generator's temporaries: the group-bys allocate with hipMalloc
     else:
-        table = item_table_device(rows, seed=9, batch_rows=args.batch_rows, device=dev,
-                                  extra=args.workload == "c4")
+        table = item_table_device(rows, seed=9, batch_rows=batch_rows, device=dev,
+                                  extra=workload == "c4")
     stream = torch.cuda.current_stream(dev)
-    e0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    e1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    e0 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    e1 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     nb = lambda n: (n + 7) // 8  # noqa: E731
 
-    if args.workload == "c3":
+    if workload == "c3":
         from deequ_amd import _native as N
         from deequ_amd.analyzers.grouping import FrequencyTable
 
@@ -116,7 +130,7 @@ def main():
                  for a in (Uniqueness([c]), Distinctness([c]), Entropy(c), Histogram(c))]
 
         def step():
-            if args.runner:
+            if runner:
                 ctx = AnalysisRunner.do_analysis_run(table, suite)
                 return {str(a): ctx.metric(a).value for a in suite}
             out = {}
@@ -140,7 +154,7 @@ def main():
                 "(~N groups, exact mode) and string priority (3 groups, hashed mode) over a "
                 "synthetic Item table, 5% nulls (BASELINE.json configs[2], 1 GPU)")
         metric_unit = "rows/s"
-    elif args.workload == "c5":
+    elif workload == "c5":
         from deequ_amd import analyzers as A
         from deequ_amd.runners import AnalysisRunner
         suite = c5_suite()
@@ -189,9 +203,9 @@ def main():
                 "rows over 8 GPUs = 1.25e9 rows, 1 GPU)")
         metric_unit = "rows/s"
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         res = step()
-    if args.pyprof:
+    if pyprof:
         import cProfile
         import io
         import pstats
@@ -217,7 +231,7 @@ def main():
     step_host = []
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(steps):
         e0[i].record(stream)
         n_gc = len(gc_log)
         ts = time.perf_counter()
@@ -225,26 +239,32 @@ def main():
         step_host.append((time.perf_counter() - ts, gc_log[n_gc:], torch.cuda.mem_get_info(dev)[0]))
         e1[i].record(stream)
     torch.cuda.synchronize(dev)
-    el = (time.perf_counter() - t0) / args.steps
+    el = (time.perf_counter() - t0) / steps
+    gc.callbacks.remove(on_gc)
     per_step = [a.elapsed_time(b) for a, b in zip(e0, e1)]
-    print("device ms per step: " + " ".join(f"{x:.1f}" for x in per_step), file=sys.stderr)
-    for i, (h, gcs, free) in enumerate(step_host):
+    if verbose:
+        print("device ms per step: " + " ".join(f"{x:.1f}" for x in per_step), file=sys.stderr)
+    for i, (h, gcs, free) in enumerate(step_host if verbose else []):
         print(f"step {i}: host {h * 1e3:.1f} ms, free {free / 2**30:.1f} GiB, {len(gcs)} gc collections, "
               f"{sum(d for _, d, _ in gcs) * 1e3:.1f} ms, gen2: " +
               ", ".join(f"{d * 1e3:.1f} ms" for g, d, _ in gcs if g == 2), file=sys.stderr)
-    dev_ms = sum(per_step) / args.steps
+    dev_ms = sum(per_step) / steps
     achieved = b_alg / (dev_ms * 1e-3)
-    cpu = cpu_baseline(args, table) if args.cpu_baseline else None
-    print(json.dumps({
+    cpu = cpu_baseline(workload, cpu_rows, table) if cpu_rows else None
+    out = {
         "cpu_baseline": cpu,
-        "workload": args.workload, "desc": desc, "rows": rows, "unit": metric_unit,
+        "workload": workload, "desc": desc, "rows": rows, "unit": metric_unit,
         "value": rows / el, "ms_per_step": el * 1e3, "device_ms_per_step": dev_ms,
-        "steps": args.steps, "warmup": args.warmup,
+        "steps": steps, "warmup": warmup, "algorithmic_bytes": b_alg, "frac": achieved / PEAK,
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK / 1e9,
                      "unit": "GB/s", "frac": achieved / PEAK, "algorithmic_bytes": b_alg,
                      "kernel": kernel},
         "result": repr(res)[:300],
-    }), flush=True)
+    }
+    if not verbose:
+        del out["result"]
+    del table
+    return out
 
 
 def gather_rank_stats(seconds: float, sent: int, recv: int, device: str):
@@ -379,7 +399,7 @@ def _host_column(col, n):
     return col.values[:n].cpu().numpy().copy(), None, valid
 
 
-def cpu_baseline(args, table, min_seconds: float = 10.0):
+def cpu_baseline(workload: str, cpu_rows: int, table, min_seconds: float = 10.0):
     """The same workload's semantics restated in C/OpenMP (oracle/oracle.c: or_freq = the hash
     Exchange + HashAggregate of Spark local[T], or_hll / or_corr = the partial + final
     aggregation) on a bounded sample: the first rows of the table's first batch, repeated until
@@ -390,8 +410,8 @@ def cpu_baseline(args, table, min_seconds: float = 10.0):
     threads, host = available_cpus()
     b0 = table.batches[0]
     first = next(iter(b0.values()))
-    n = min(args.cpu_rows, first.length)
-    if args.workload == "c3":
+    n = min(cpu_rows, first.length)
+    if workload == "c3":
         cols = {c: _host_column(b0[c], n) for c in ("id", "priority")}
 
         def one():
@@ -400,7 +420,7 @@ def cpu_baseline(args, table, min_seconds: float = 10.0):
                 C.freq(kind, v, d, m, n, n, null_as_group=True, k=1000, threads=threads)
         what = ("Uniqueness/Distinctness/Entropy + Histogram top-1000 of id and priority: "
                 "or_freq (hash-partitioned count, 256 shuffle partitions)")
-    elif args.workload == "c4":
+    elif workload == "c4":
         import numpy as np
         idv, _, idm = _host_column(b0["id"], n)
         sv, _, sm = _host_column(b0["score"], n)
