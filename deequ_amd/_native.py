@@ -14,16 +14,56 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # DQ_LIB_PATH: diagnostic A/B builds only (tools/); the product loads the in-tree library
 LIB_PATH = os.environ.get("DQ_LIB_PATH") or os.path.join(_HERE, "libdeequ_amd.so")
 
-# dq_type
-BOOL, INT8, INT16, INT32, INT64, FLOAT32, FLOAT64, UTF8 = range(1, 9)
+# dq_type (a type word: the dq_type in bits 0-7; a decimal's precision / scale in bits 8-15 / 16-23)
+BOOL, INT8, INT16, INT32, INT64, FLOAT32, FLOAT64, UTF8, DECIMAL128, DATE32, TIMESTAMP_US = range(1, 12)
+# a column of an Arrow type the engine does not read (list, struct, ...): only its validity bitmap
+# reaches the device (Completeness / Size work, anything else is a WrongColumnTypeException)
+UNSUPPORTED = 0
 TYPE_NAMES = {BOOL: "BooleanType", INT8: "ByteType", INT16: "ShortType", INT32: "IntegerType",
-              INT64: "LongType", FLOAT32: "FloatType", FLOAT64: "DoubleType", UTF8: "StringType"}
+              INT64: "LongType", FLOAT32: "FloatType", FLOAT64: "DoubleType", UTF8: "StringType",
+              DATE32: "DateType", TIMESTAMP_US: "TimestampType"}
 NUMERIC_TYPES = {INT8, INT16, INT32, INT64, FLOAT32, FLOAT64}
 INTEGRAL_TYPES = {INT8, INT16, INT32, INT64}
 
+
+def type_id(t: int) -> int:
+    return t & 0xFF
+
+
+def decimal_type(precision: int, scale: int) -> int:
+    """DQ_DECIMAL_TYPE(p, s): Spark DecimalType(p, s) (1 <= p <= 38, 0 <= s <= p)."""
+    if not (1 <= precision <= 38 and 0 <= scale <= precision):
+        raise ValueError(f"decimal({precision},{scale}): the engine reads 1 <= p <= 38, 0 <= s <= p")
+    return DECIMAL128 | (precision << 8) | (scale << 16)
+
+
+def is_decimal(t: int) -> bool:
+    return t & 0xFF == DECIMAL128
+
+
+def decimal_precision(t: int) -> int:
+    return (t >> 8) & 0xFF
+
+
+def decimal_scale(t: int) -> int:
+    return (t >> 16) & 0xFF
+
+
+def is_numeric(t: int) -> bool:
+    """Preconditions.isNumeric (Analyzer.scala:322-333): Byte .. Double and every DecimalType."""
+    return t in NUMERIC_TYPES or is_decimal(t)
+
+
+def type_name(t: int) -> str:
+    """Spark's name of a type word (DecimalType(p,s) with its precision and scale)."""
+    if is_decimal(t):
+        return f"DecimalType({decimal_precision(t)},{decimal_scale(t)})"
+    return TYPE_NAMES.get(t, "UnsupportedType")
+
 # dq_xop
 (X_COL, X_NULL, X_BOOL, X_I64, X_F64, X_STR, X_IS_NULL, X_IS_NOT_NULL, X_NOT, X_AND, X_OR, X_EQ,
- X_NE, X_LT, X_LE, X_GT, X_GE, X_EQ_NULL_SAFE, X_IN, X_CAST_F64, X_REGEX, X_CAST_F32) = range(1, 23)
+ X_NE, X_LT, X_LE, X_GT, X_GE, X_EQ_NULL_SAFE, X_IN, X_CAST_F64, X_REGEX, X_CAST_F32,
+ X_DEC128) = range(1, 24)
 
 # dq_agg_kind
 (AGG_COUNT_ALL, AGG_COUNT_NOTNULL, AGG_COUNT_TRUE, AGG_SUM, AGG_MIN, AGG_MAX, AGG_STDDEV_POP,
@@ -128,10 +168,14 @@ def _load() -> ctypes.CDLL:
         "dq_freq_hll": (c_int, [c_void_p, c_int64, c_void_p, POINTER(c_int), c_void_p]),
         "dq_freq_folded_nan_rows": (c_int, [c_void_p, POINTER(c_int64)]),
         "dq_state_exchange_sizes": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64),
-                                            POINTER(c_int64)]),
-        "dq_state_exchange_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-        "dq_state_exchange_unpack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                                             c_void_p]),
+                                            POINTER(c_int64), POINTER(c_int64)]),
+        "dq_state_exchange_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p]),
+        "dq_state_exchange_unpack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_int, c_void_p]),
+        "dq_host_wait_count": (c_int64, []),
+        "dq_decimal_to_double": (c_double, [c_uint64, c_int64, c_int32]),
+        "dq_format_values": (c_int, [c_int32, c_void_p, c_int64, c_void_p, c_void_p]),
         "dq_cast_utf8": (c_int, [POINTER(dq_column), c_int, c_void_p, c_void_p, POINTER(c_int64), c_void_p]),
         "dq_freq_import": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                    c_int64, c_int, c_void_p]),
@@ -177,6 +221,7 @@ EXPORTED = [
     "dq_state_serialize", "dq_state_deserialize", "dq_hll_count", "dq_xxhash64", "dq_column_release", "dq_java_double_to_string", "dq_java_float_to_string", "dq_java_doubles_to_strings", "dq_freq_create",
     "dq_freq_destroy", "dq_freq_reset", "dq_freq_add_device", "dq_freq_summarize", "dq_freq_summarize_keys", "dq_sorted_sample", "dq_freq_marginal", "dq_freq_mutual_information", "dq_freq_num_groups", "dq_freq_null_literal", "dq_freq_import", "dq_cast_utf8", "dq_release_cached_memory", "dq_cached_device_bytes", "dq_freq_hll", "dq_freq_folded_nan_rows",
     "dq_state_exchange_sizes", "dq_state_exchange_pack", "dq_state_exchange_unpack",
+    "dq_host_wait_count", "dq_decimal_to_double", "dq_format_values",
     "dq_freq_num_rows", "dq_freq_export", "dq_freq_merge", "dq_freq_topk", "dq_loader_create",
     "dq_loader_destroy", "dq_loader_stage", "dq_loader_release", "dq_scan_host",
     "dq_freq_add_host", "dq_freq_partition_sizes", "dq_freq_partition",
@@ -256,3 +301,35 @@ def retry_on_oom(fn, *args, **kwargs):
             raise
     release_cached_memory()
     return fn(*args, **kwargs)
+
+
+def decimal_to_double(unscaled: int, scale: int) -> float:
+    """Cast(Decimal AS DOUBLE) of one unscaled value (the device's dec_to_double, on the host)."""
+    u = unscaled & ((1 << 128) - 1)
+    hi = u >> 64
+    return float(lib.dq_decimal_to_double(u & 0xFFFFFFFFFFFFFFFF, hi - (1 << 64) if hi >= (1 << 63) else hi,
+                                          scale))
+
+
+def format_values(dtype: int, values) -> list:
+    """Spark 2.2's cast to string of date / timestamp / decimal values (dq_format_values): ints of
+    days / microseconds, or unscaled ints for a decimal type word."""
+    import numpy as np
+    n = len(values)
+    if is_decimal(dtype):
+        raw = np.zeros(2 * max(1, n), np.uint64)
+        for i, v in enumerate(values):
+            u = int(v) & ((1 << 128) - 1)
+            raw[2 * i] = u & 0xFFFFFFFFFFFFFFFF
+            raw[2 * i + 1] = u >> 64
+    elif dtype == DATE32:
+        raw = np.ascontiguousarray(list(values) or [0], np.int32)
+    elif dtype == TIMESTAMP_US:
+        raw = np.ascontiguousarray(list(values) or [0], np.int64)
+    else:
+        raise ValueError(f"format_values: type {dtype}")
+    out = np.zeros(max(1, n) * 64, np.uint8)
+    lens = np.zeros(max(1, n), np.int32)
+    check(lib.dq_format_values(dtype, raw.ctypes.data, n, out.ctypes.data, lens.ctypes.data))
+    data = out.tobytes()
+    return [data[64 * i: 64 * i + ln].decode("ascii") for i, ln in enumerate(lens[:n].tolist())]

@@ -124,10 +124,10 @@ class Preconditions:
     def is_numeric(column: str):
         def check(schema):
             dtype = schema[column].dtype
-            if dtype not in N.NUMERIC_TYPES:
+            if not N.is_numeric(dtype):
                 raise WrongColumnTypeException(
                     f"Expected type of column {column} to be one of ({_NUMERIC_NAMES}), but found "
-                    f"{N.TYPE_NAMES[dtype]} instead!")
+                    f"{schema[column].type_name} instead!")
         return check
 
 

@@ -154,6 +154,10 @@ class FrequencyTable:
         last = len(words) - 1
         tags = words[at]
         w1 = words[np.minimum(at + 1, last)]
+        if _wide_decimal(t):  # 16-byte strings of the unscaled value (dq_freq_export)
+            starts = (4 * at + 8).tolist()
+            return [(int.from_bytes(data[b: b + 16], "little", signed=True),) if tg else (None,)
+                    for b, tg in zip(starts, tags.tolist())]
         if t == N.UTF8:
             starts = (4 * at + 8).tolist()
             return [(data[b: b + ln].decode("utf-8", "replace"),) if tg else (None,)
@@ -178,7 +182,11 @@ class FrequencyTable:
             if tag == 0:
                 key.append(None)
                 continue
-            if t == N.UTF8:
+            if _wide_decimal(t):
+                pos += 4  # (the length word: 16)
+                key.append(int.from_bytes(data[pos: pos + 16], "little", signed=True))
+                pos += 16
+            elif t == N.UTF8:
                 ln = struct.unpack_from("<I", data, pos)[0]
                 pos += 4
                 key.append(data[pos: pos + ln].decode("utf-8", "replace"))
@@ -202,11 +210,14 @@ class FrequencyTable:
     @staticmethod
     def encode_key(key: tuple, key_types: Sequence[int]) -> bytes:
         """A group key in the dq_freq_export format (per column: u32 tag, then 8 value bytes or a
-        u32 length + the UTF-8 bytes padded to 4)."""
+        u32 length + the UTF-8 bytes padded to 4; a decimal(p > 18) key: length 16 + the
+        little-endian unscaled value)."""
         out = []
         for v, t in zip(key, key_types):
             if v is None:
                 out.append(struct.pack("<I", 0))
+            elif _wide_decimal(t):
+                out.append(struct.pack("<II", 1, 16) + int(v).to_bytes(16, "little", signed=True))
             elif t == N.UTF8:
                 b = v.encode("utf-8")
                 out.append(struct.pack("<II", 1, len(b)) + b + b"\0" * ((-len(b)) % 4))
@@ -266,6 +277,12 @@ class KeyedFrequencies:
 
     def count(self) -> int:
         return int(self.summarize().n_groups)
+
+
+def _wide_decimal(t: int) -> bool:
+    """A decimal(p > 18) key: the table groups it as a 16-byte string of its unscaled value (a
+    decimal(p <= 18) key is its unscaled long, a date / timestamp key its int32 / int64)."""
+    return N.is_decimal(t) and N.decimal_precision(t) > 18
 
 
 def _encode_fixed(t: int, v) -> int:
@@ -569,10 +586,15 @@ def java_float_to_string(f: float) -> str:
 
 
 def cast_to_string(value, dtype: int) -> str:
+    """Spark 2.2's Cast(x AS STRING) of a key (Histogram.scala:63).  Date / timestamp / decimal
+    keys are held as their days / microseconds / unscaled value and formatted by the engine's
+    formatter (dq_format_values: BigDecimal.toString, yyyy-MM-dd, yyyy-MM-dd HH:mm:ss[.f] UTC)."""
     if value is None:
         return NULL_FIELD_REPLACEMENT
     if dtype == N.UTF8:
         return value
+    if dtype in (N.DATE32, N.TIMESTAMP_US) or N.is_decimal(dtype):
+        return N.format_values(dtype, [int(value)])[0]
     if dtype == N.BOOL:
         return "true" if value else "false"
     if dtype == N.FLOAT64:
@@ -606,6 +628,9 @@ def _fold_null_group(frequencies, dtype: int, k: int):
             if not (key is None or (dtype == N.UTF8 and key == NULL_FIELD_REPLACEMENT))]
     if dtype in (N.FLOAT64, N.FLOAT32):  # Double/Float.toString of every key in one call
         texts = N.java_doubles_to_strings([k for k, _ in kept], dtype == N.FLOAT32)
+        top = [(s, c) for s, (_, c) in zip(texts, kept)]
+    elif dtype in (N.DATE32, N.TIMESTAMP_US) or N.is_decimal(dtype):  # one formatter call
+        texts = N.format_values(dtype, [k for k, _ in kept])
         top = [(s, c) for s, (_, c) in zip(texts, kept)]
     else:
         top = [(cast_to_string(k, dtype), c) for k, c in kept]
@@ -689,7 +714,10 @@ class Histogram(Analyzer):
         (FrequencyTable.folded_nan_rows() == 0, checked by the runner after the table is built;
         otherwise the grouping runs its own group-by)."""
         dtype = data.schema[column].dtype
-        return dtype in (N.BOOL, N.INT8, N.INT16, N.INT32, N.INT64, N.UTF8, N.FLOAT32, N.FLOAT64)
+        # (date / timestamp / decimal: their casts to string are injective, so the string groups
+        # and the value groups are the same groups)
+        return (dtype in (N.BOOL, N.INT8, N.INT16, N.INT32, N.INT64, N.UTF8, N.FLOAT32, N.FLOAT64,
+                          N.DATE32, N.TIMESTAMP_US) or N.is_decimal(dtype))
 
     def compute_state_from(self, data):
         from ..distributed import compute_frequencies_distributed, is_distributed

@@ -216,7 +216,7 @@ class HdfsStateProvider(StateLoader, StatePersister):
         else:
             groups = state.frequencies.export()
             cols = list(state.frequencies.key_columns)
-            arrays = [pa.array([k[i] for k, _ in groups], type=_ARROW[t])
+            arrays = [_key_array([k[i] for k, _ in groups], t)
                       for i, t in enumerate(state.frequencies.key_types)]
             counts = [c for _, c in groups]
         # the frequency DataFrame's count column: Analyzers.COUNT_COL for a grouping
@@ -284,7 +284,8 @@ class HdfsStateProvider(StateLoader, StatePersister):
         count_col = "count" if hist else COUNT_COL
         names = [n for n in table.column_names if n != count_col]
         types = [_from_arrow(table.schema.field(n).type) for n in names]
-        keys = list(zip(*[table.column(n).to_pylist() for n in names])) if names else []
+        keys = list(zip(*[_key_values(table.column(n), t) for n, t in zip(names, types)])) \
+            if names else []
         counts = table.column(count_col).to_pylist()
         ft = G.FrequencyTable.from_groups(names, types, self.device, list(zip(keys, counts)),
                                           num_rows=num_rows, null_as_group=hist)
@@ -320,10 +321,47 @@ def _from_arrow(t) -> int:
         if v == t:
             return k
     import pyarrow as pa
+    from .. import _native as N
     if t == pa.large_string():
-        from .. import _native as N
         return N.UTF8
+    if t == pa.date32():
+        return N.DATE32
+    if pa.types.is_timestamp(t):
+        return N.TIMESTAMP_US
+    if pa.types.is_decimal128(t):
+        return N.decimal_type(t.precision, t.scale)
     raise ValueError(f"unsupported frequency key type {t}")
+
+
+def _key_array(values, t: int):
+    """A frequency table's key column as the Spark type it holds: dates / timestamps (held as
+    days / microseconds) as date32 / timestamp[us], decimals (held unscaled) as decimal128(p, s)."""
+    import pyarrow as pa
+    from decimal import Decimal
+    from .. import _native as N
+    if t == N.DATE32:
+        return pa.array(values, type=pa.int32()).cast(pa.date32())
+    if t == N.TIMESTAMP_US:
+        return pa.array(values, type=pa.int64()).cast(pa.timestamp("us"))
+    if N.is_decimal(t):
+        sc = N.decimal_scale(t)
+        return pa.array([None if v is None else Decimal(int(v)).scaleb(-sc) for v in values],
+                        type=pa.decimal128(N.decimal_precision(t), sc))
+    return pa.array(values, type=_ARROW[t])
+
+
+def _key_values(column, t: int) -> list:
+    """The inverse of _key_array: days / microseconds / unscaled ints."""
+    import pyarrow as pa
+    from .. import _native as N
+    if t == N.DATE32:
+        return column.cast(pa.int32()).to_pylist()
+    if t == N.TIMESTAMP_US:
+        return column.cast(pa.int64()).to_pylist()
+    if N.is_decimal(t):
+        sc = N.decimal_scale(t)
+        return [None if v is None else int(v.scaleb(sc)) for v in column.to_pylist()]
+    return column.to_pylist()
 
 
 __all__ = ["StateLoader", "StatePersister", "InMemoryStateProvider", "HdfsStateProvider",

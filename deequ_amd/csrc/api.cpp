@@ -16,11 +16,27 @@
 #include <tuple>
 #include <vector>
 
+#include "decimal.h"
 #include "engine.h"
 #include "kernels.h"
 #include "jfmt.h"
 
 using namespace dq;
+
+// Every host wait on device work this file makes (stream / event synchronisations) is counted:
+// dq_host_wait_count() lets tests assert how many a path takes (the state exchange: one, the
+// read-back of the merged state).
+#include <atomic>
+static std::atomic<long long> g_host_waits{0};
+static hipError_t host_wait(hipStream_t st) {
+  g_host_waits.fetch_add(1, std::memory_order_relaxed);
+  return hipStreamSynchronize(st);
+}
+static hipError_t host_wait_event(hipEvent_t ev) {
+  g_host_waits.fetch_add(1, std::memory_order_relaxed);
+  return hipEventSynchronize(ev);
+}
+extern "C" int64_t dq_host_wait_count(void) { return g_host_waits.load(std::memory_order_relaxed); }
 
 // ------------------------------------------------------------------------------------------------
 // Errors
@@ -49,8 +65,29 @@ extern "C" int dq_device_count(void) {
 static bool is_numeric(int t) { return t >= DQ_INT8 && t <= DQ_FLOAT64; }
 static bool is_integral(int t) { return t >= DQ_INT8 && t <= DQ_INT64; }
 static bool is_floating(int t) { return t == DQ_FLOAT32 || t == DQ_FLOAT64; }
+static bool is_decimal(int t) { return DQ_TYPE_ID(t) == DQ_DECIMAL128; }
+// date / timestamp / decimal: types with no native arithmetic in the scan bodies' numeric paths
+static bool is_temporal(int t) { return t == DQ_DATE32 || t == DQ_TIMESTAMP_US; }
+// A well-formed type word (decimal: 1 <= p <= 38, 0 <= s <= p, nothing above bit 23).
+static bool valid_type(int t) {
+  if (is_decimal(t)) {
+    const int p = DQ_DECIMAL_PRECISION(t), sc = DQ_DECIMAL_SCALE(t);
+    return (t >> 24) == 0 && p >= 1 && p <= 38 && sc <= p;
+  }
+  return t >= DQ_BOOL && t <= DQ_TIMESTAMP_US;
+}
+// The physical layout a kernel that only compares / hashes values may treat a column as: a date is
+// an int32 (hashInt, XxHash64Function on DateType), a timestamp an int64 (hashLong).
+static int phys_type(int t) {
+  if (t == DQ_DATE32) return DQ_INT32;
+  if (t == DQ_TIMESTAMP_US) return DQ_INT64;
+  return t;
+}
 static int type_size(int t) {
+  if (is_decimal(t)) return 16;
   switch (t) {
+    case DQ_DATE32: return 4;
+    case DQ_TIMESTAMP_US: return 8;
     case DQ_INT8: return 1;
     case DQ_INT16: return 2;
     case DQ_INT32: return 4;
@@ -99,6 +136,11 @@ static bool parse_node(const int64_t* w, int n, int& pos, std::unique_ptr<Node>&
       break;
     case DQ_X_F64:
       if (pos >= n) return false;
+      memcpy(&node->d, &w[pos++], 8);
+      break;
+    case DQ_X_DEC128:  // i = low word, d = high word's bits
+      if (pos + 1 >= n) return false;
+      node->i = w[pos++];
       memcpy(&node->d, &w[pos++], 8);
       break;
     case DQ_X_STR: {
@@ -194,6 +236,13 @@ static void compile_postfix(const Node& n, std::vector<XInstr>& prog, std::strin
       ins = {XI_F64, 0, b};
       break;
     }
+    case DQ_X_DEC128: {  // two words: the low word's instruction, then the high word's
+      int64_t hi;
+      memcpy(&hi, &n.d, 8);
+      prog.push_back(XInstr{XI_DEC128, 0, n.i});
+      ins = {XI_DEC128_HI, 0, hi};
+      break;
+    }
     case DQ_X_STR: {
       while (pool.size() % 4) pool.push_back('\0');
       ins = {XI_STR, (int32_t)n.s.size(), (int64_t)pool.size()};
@@ -230,6 +279,57 @@ static bool casts_string_to_float(const Node& n, const std::vector<int32_t>& typ
   for (auto& k : n.kids)
     if (casts_string_to_float(*k, types)) return true;
   return false;
+}
+
+// Where a decimal / date / timestamp column may appear in an expression (deequ_amd.h, DQ_X_DEC128):
+// the interpreter has no other arithmetic for them, so anything else is refused, never evaluated
+// in the wrong domain.  Returns false and names the offending use in `why`.
+static bool typed_uses_ok(const Node& n, const std::vector<int32_t>& types, std::string& why) {
+  auto dec_col = [&](const Node* x) { return x->op == DQ_X_COL && is_decimal(types[x->col]); };
+  auto special = [&](const Node* x) {
+    return x->op == DQ_X_COL && (is_decimal(types[x->col]) || is_temporal(types[x->col]));
+  };
+  switch (n.op) {
+    case DQ_X_COL:
+      if (special(&n)) {
+        why = "a decimal / date / timestamp column used outside IS [NOT] NULL, a comparison with a "
+              "decimal literal, CAST AS DOUBLE or a regex";
+        return false;
+      }
+      return true;
+    case DQ_X_DEC128:
+      why = "a decimal literal outside a comparison with a decimal column";
+      return false;
+    case DQ_X_IS_NULL:
+    case DQ_X_IS_NOT_NULL:
+    case DQ_X_REGEX:
+      if (special(n.kids[0].get())) return true;
+      break;
+    case DQ_X_CAST_F64:
+      if (dec_col(n.kids[0].get())) return true;
+      break;
+    case DQ_X_IN:
+      if (dec_col(n.kids[0].get())) {
+        for (size_t k = 1; k < n.kids.size(); ++k)
+          if (n.kids[k]->op != DQ_X_DEC128 && n.kids[k]->op != DQ_X_NULL) {
+            why = "a decimal column IN a list of non-decimal items";
+            return false;
+          }
+        return true;
+      }
+      break;
+    default:
+      if (is_cmp(n.op) || n.op == DQ_X_EQ_NULL_SAFE) {
+        const Node* a = n.kids[0].get();
+        const Node* b = n.kids[1].get();
+        if (dec_col(a) && (b->op == DQ_X_DEC128 || b->op == DQ_X_NULL)) return true;
+        if (dec_col(b) && (a->op == DQ_X_DEC128 || a->op == DQ_X_NULL)) return true;
+      }
+      break;
+  }
+  for (auto& k : n.kids)
+    if (!typed_uses_ok(*k, types, why)) return false;
+  return true;
 }
 
 static int stack_depth(const Node& n) {
@@ -425,6 +525,7 @@ static int body_class(const dq_plan* p, const TaskPlan& t) {
     case TK_STR_IN: return BC_STR_IN;
     case TK_DTYPE: return BC_DTYPE;
     case TK_COMOMENTS: return t.fused_hll >= 0 ? BC_CORR_HLL : BC_CORR;
+    case TK_DECIMAL: return BC_DECIMAL;
     default: return BC_HLL;
   }
 }
@@ -467,7 +568,7 @@ extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
   auto p = std::make_unique<dq_plan>();
   p->types.assign(desc->column_types, desc->column_types + desc->n_columns);
   for (int t : p->types)
-    if (t < DQ_BOOL || t > DQ_UTF8) return fail(DQ_ERR_INVALID_ARGUMENT, "unknown column type %d", t);
+    if (!valid_type(t)) return fail(DQ_ERR_INVALID_ARGUMENT, "unknown column type %d", t);
   for (int e = 0; e < desc->n_exprs; ++e) {
     std::unique_ptr<Node> n;
     int pos = 0;
@@ -478,6 +579,8 @@ extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
       return fail(DQ_ERR_UNSUPPORTED, "expression %d nests deeper than %d", e, kMaxStack);
     if (casts_string_to_float(*n, p->types))
       return fail(DQ_ERR_UNSUPPORTED, "expression %d casts a string to FLOAT", e);
+    std::string why;
+    if (!typed_uses_ok(*n, p->types, why)) return fail(DQ_ERR_UNSUPPORTED, "expression %d: %s", e, why.c_str());
     p->exprs.push_back(std::move(n));
   }
   p->aggs.assign(desc->aggs, desc->aggs + desc->n_aggs);
@@ -506,10 +609,11 @@ extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
         if ((st = where_of(a, w)) != DQ_OK) return st;
         s.src = SRC_TASK;
         s.notnull_rows = true;
-        // share the numeric task when one exists for (col, where); else a popcount task
+        // share the numeric (decimal) task when one exists for (col, where); else a popcount task
         int found = -1;
         for (size_t k = 0; k < p->tasks.size(); ++k)
-          if (p->tasks[k].kind == TK_NUMERIC && p->tasks[k].col == a.col && p->tasks[k].where == w)
+          if ((p->tasks[k].kind == TK_NUMERIC || p->tasks[k].kind == TK_DECIMAL) &&
+              p->tasks[k].col == a.col && p->tasks[k].where == w)
             found = (int)k;
         s.task = found >= 0 ? found : find_or_add_task(p.get(), TK_VALIDITY, a.col, -1, w);
         break;
@@ -573,17 +677,21 @@ extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
       case DQ_AGG_MAX:
       case DQ_AGG_STDDEV_POP: {
         if ((st = check_col(a.col)) != DQ_OK) return st;
-        if (!is_numeric(p->types[a.col]))
+        if (!is_numeric(p->types[a.col]) && !is_decimal(p->types[a.col]))
           return fail(DQ_ERR_WRONG_TYPE, "column %d is not numeric", a.col);
         if ((st = where_of(a, w)) != DQ_OK) return st;
         s.src = SRC_TASK;
-        s.task = find_or_add_task(p.get(), TK_NUMERIC, a.col, -1, w);
+        s.task = find_or_add_task(p.get(), is_decimal(p->types[a.col]) ? TK_DECIMAL : TK_NUMERIC,
+                                  a.col, -1, w);
         s.col_type = p->types[a.col];
         break;
       }
       case DQ_AGG_CORR: {
         if ((st = check_col(a.col)) != DQ_OK) return st;
         if ((st = check_col(a.col2)) != DQ_OK) return st;
+        if (is_decimal(p->types[a.col]) || is_decimal(p->types[a.col2]))
+          return fail(DQ_ERR_UNSUPPORTED, "correlation over a decimal column: cast it to double "
+                                          "first (the engine's co-moment bodies read Long / Double)");
         if (!is_numeric(p->types[a.col]) || !is_numeric(p->types[a.col2]))
           return fail(DQ_ERR_WRONG_TYPE, "correlation needs numeric columns");
         if ((st = where_of(a, w)) != DQ_OK) return st;
@@ -615,7 +723,8 @@ extern "C" dq_status dq_plan_create(const dq_plan_desc* desc, dq_plan** out) {
     if (s.kind != DQ_AGG_COUNT_NOTNULL) continue;
     const TaskPlan& t = p->tasks[s.task];
     for (size_t k = 0; k < p->tasks.size(); ++k)
-      if (p->tasks[k].kind == TK_NUMERIC && p->tasks[k].col == t.col && p->tasks[k].where == t.where)
+      if ((p->tasks[k].kind == TK_NUMERIC || p->tasks[k].kind == TK_DECIMAL) &&
+          p->tasks[k].col == t.col && p->tasks[k].where == t.where)
         s.task = (int)k;
   }
   // drop validity tasks nobody references any more, renumber
@@ -675,6 +784,7 @@ static const char* kind_name(int k) {
     case TK_COMOMENTS: return "comoments";
     case TK_HLL: return "hll";
     case TK_DTYPE: return "dtype";
+    case TK_DECIMAL: return "decimal";
     default: return "?";
   }
 }
@@ -711,7 +821,7 @@ extern "C" int dq_plan_launches_per_batch(const dq_plan* plan) {
   for (int c = 0; c < kBodyClasses; ++c) {
     bool used = false;
     for (const TaskPlan& t : plan->tasks) used = used || (body_class(plan, t) == c && !t.carried);
-    if (c == BC_HLL || c == BC_CORR_HLL) hll += used ? 1 : 0;
+    if (c == BC_HLL || c == BC_CORR_HLL || c == BC_DECIMAL) hll += used ? 1 : 0;  // own launches
     else classes += used ? 1 : 0;
   }
   // two or more body classes share one mixed launch (dq_scan_device_batches); HLL joins it when
@@ -758,7 +868,9 @@ struct dq_state {
   DevBuf<uint32_t> d_hll_stage;  // per-launch HLL registers (u32), kept zero between launches
   DevBuf<uint32_t> d_fin_arrivals;  // finalize: per task, its workgroups done (kept zero)
   DevBuf<int64_t> d_rows;        // the merged row count of an exchange (dq_state_exchange_unpack)
-  DevBuf<int32_t> d_kinds;       // the plan's task kinds (the exchange kernels)
+  DevBuf<int32_t> d_kinds;       // the plan's task kinds (the exchange kernels), uploaded once
+  std::vector<int32_t> h_kinds;  // (their source, alive while the upload may be queued)
+  bool kinds_ready = false;
   hipEvent_t ev_xchg = nullptr;  // orders the exchange kernels and the collectives' stream
   bool rows_on_device = false;   // ... not yet read back (dq_state_sync reads it with the rest)
   DevBuf<uint32_t> d_queue;      // work-item counters of the scan kernels, kept zero between launches
@@ -816,7 +928,7 @@ static void host_reset(dq_state* s) {
 static dq_status pin_ensure(dq_state* s, size_t bytes) {
   if (s->h_pin_cap >= bytes) return DQ_OK;
   if (s->pin_pending) {
-    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(host_wait(s->stream));
     s->pin_pending = false;
   }
   if (s->h_pin) (void)hipHostFree(s->h_pin);
@@ -837,12 +949,12 @@ static dq_status upload_host(dq_state* s) {
     if (hb) HIP_TRY(hipMemcpy(s->d_hll.p, s->hll.data(), hb, hipMemcpyHostToDevice));
     HIP_TRY(hipMemsetAsync(s->d_queue.p, 0, kQueueWords * sizeof(uint32_t), nullptr));
     HIP_TRY(hipMemsetAsync(s->d_hll_stage.p, 0, s->d_hll_stage.n * sizeof(uint32_t), nullptr));
-    HIP_TRY(hipStreamSynchronize(nullptr));  // the first scan may run on a non-blocking stream
+    HIP_TRY(host_wait(nullptr));  // the first scan may run on a non-blocking stream
     s->host_dirty = false;
     return DQ_OK;
   }
   // on the state's stream, ordered before the next scan: no host wait
-  if (s->pin_pending) HIP_TRY(hipStreamSynchronize(s->stream));  // h_pin is about to be rewritten
+  if (s->pin_pending) HIP_TRY(host_wait(s->stream));  // h_pin is about to be rewritten
   s->pin_pending = false;
   {
     const dq_status ps = pin_ensure(s, ab + hb);
@@ -1024,14 +1136,14 @@ extern "C" dq_status dq_state_create(const dq_plan* plan, int device, dq_state**
 
 extern "C" void dq_state_destroy(dq_state* state) {
   if (!state) return;
-  if (state->stream_set && state->device >= 0) (void)hipStreamSynchronize(state->stream);
+  if (state->stream_set && state->device >= 0) (void)host_wait(state->stream);
   if (state->h_pin) (void)hipHostFree(state->h_pin);
   delete state;
 }
 
 extern "C" dq_status dq_state_reset(dq_state* state) {
   if (!state) return fail(DQ_ERR_INVALID_ARGUMENT, "null state");
-  if (state->stream_set && state->device >= 0) HIP_TRY(hipStreamSynchronize(state->stream));
+  if (state->stream_set && state->device >= 0) HIP_TRY(host_wait(state->stream));
   host_reset(state);
   static const bool eager = getenv("DQ_EAGER_RESET") != nullptr;  // A/B hook
   if (state->stream_set && state->device >= 0 && !eager) {
@@ -1202,7 +1314,7 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
     const dq_status rs = dq_state_sync(s);
     if (rs != DQ_OK) return rs;
   }
-  if (s->stream_set && s->stream != stream) HIP_TRY(hipStreamSynchronize(s->stream));
+  if (s->stream_set && s->stream != stream) HIP_TRY(host_wait(s->stream));
   s->stream = stream;
   s->stream_set = true;
   dq_status st = upload_host(s);
@@ -1227,7 +1339,7 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
 
   const int slot = s->flip;
   s->flip ^= 1;
-  if (s->ev_used[slot]) HIP_TRY(hipEventSynchronize(s->ev[slot]));
+  if (s->ev_used[slot]) HIP_TRY(host_wait_event(s->ev[slot]));
 
   // materialised expressions -> bitmaps, per batch at a 16-byte aligned word offset
   std::vector<size_t> bm_off(n_batches);
@@ -1240,7 +1352,7 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
   const size_t n_mat = plan->mat.size();
   if (n_mat) {
     if (words > s->bitmap_words || !s->d_bitmaps.p) {
-      HIP_TRY(hipStreamSynchronize(stream));
+      HIP_TRY(host_wait(stream));
       HIP_TRY(s->d_bitmaps.ensure(words * 2 * n_mat));
       s->bitmap_words = words;
     }
@@ -1326,7 +1438,9 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
       bool vec = aligned(t.w_val, 16) && aligned(t.w_vld, 16);
       if (tp.col >= 0) {
         const dq_column& c = bc[tp.col];
-        t.type = c.type;
+        // an HLL task hashes a date as its int32 and a timestamp as its int64 (the bodies' fast
+        // paths); every other body reads the column as its own type
+        t.type = tp.kind == TK_HLL ? phys_type(c.type) : c.type;
         t.valid = c.validity;
         t.values = c.values;
         t.data = c.data;
@@ -1427,7 +1541,8 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
     std::vector<ScanLaunch> plain, hll;
     for (const ScanLaunch& L : launches)
       // the fused body keeps HLL registers in LDS too, and the mixed kernel has no such body
-      ((L.body == BC_HLL && !s->mix_hll) || L.body == BC_CORR_HLL ? hll : plain).push_back(L);
+      ((L.body == BC_HLL && !s->mix_hll) || L.body == BC_CORR_HLL || L.body == BC_DECIMAL ? hll : plain)
+          .push_back(L);
     const bool mixed = plain.size() >= 2 && !getenv("DQ_NO_MIXED");
     if (mixed && plain.front().item_lo != 0) return fail(DQ_ERR_STATE, "unexpected item layout");
     std::vector<std::vector<ScanLaunch>> groups;  // the launches that share one queue
@@ -1532,7 +1647,7 @@ extern "C" dq_status dq_state_sync(dq_state* s) {
   if (ab) HIP_TRY(hipMemcpyAsync(pin, s->d_acc.p, ab, hipMemcpyDeviceToHost, s->stream));
   if (hb) HIP_TRY(hipMemcpyAsync(pin + ab, s->d_hll.p, hb, hipMemcpyDeviceToHost, s->stream));
   if (rb) HIP_TRY(hipMemcpyAsync(pin + ab + hb, s->d_rows.p, rb, hipMemcpyDeviceToHost, s->stream));
-  HIP_TRY(hipStreamSynchronize(s->stream));
+  HIP_TRY(host_wait(s->stream));
   s->pin_pending = false;
   if (ab) memcpy(s->acc.data(), pin, ab);
   if (hb) memcpy(s->hll.data(), pin + ab, hb);
@@ -1586,7 +1701,16 @@ extern "C" dq_status dq_state_get(const dq_state* s, int agg_index, dq_value* ou
       break;
     case DQ_AGG_SUM:
       out->is_null = a.i[0] == 0;
-      if (is_integral(sl.col_type)) {
+      if (is_decimal(sl.col_type)) {  // exact sum; NULL when it overflows the result type
+        for (int q = 0; q < 3; ++q) out->words[q] = (uint64_t)a.i[1 + q];
+        out->words[3] = a.i[3] < 0 ? ~0ULL : 0ULL;
+        if (!out->is_null && !dec_sum_fits((uint64_t)a.i[1], (uint64_t)a.i[2], (uint64_t)a.i[3],
+                                           DQ_DECIMAL_PRECISION(sl.col_type)))
+          out->is_null = 1;
+        out->f64[0] = out->is_null ? 0.0
+                                   : dec192_to_double((uint64_t)a.i[1], (uint64_t)a.i[2],
+                                                      (uint64_t)a.i[3], DQ_DECIMAL_SCALE(sl.col_type));
+      } else if (is_integral(sl.col_type)) {
         out->i64 = a.i[1];
         out->f64[0] = (double)a.i[1];
       } else {
@@ -1596,6 +1720,15 @@ extern "C" dq_status dq_state_get(const dq_state* s, int agg_index, dq_value* ou
     case DQ_AGG_MIN:
     case DQ_AGG_MAX: {
       out->is_null = a.i[0] == 0;
+      if (is_decimal(sl.col_type)) {
+        const int at = sl.kind == DQ_AGG_MIN ? 4 : 6;
+        out->words[0] = (uint64_t)a.i[at];
+        out->words[1] = (uint64_t)a.i[at + 1];
+        out->f64[0] = out->is_null ? 0.0
+                                   : dec_to_double((uint64_t)a.i[at], a.i[at + 1],
+                                                   DQ_DECIMAL_SCALE(sl.col_type));
+        break;
+      }
       int64_t k = sl.kind == DQ_AGG_MIN ? a.i[2] : a.i[3];
       if (is_integral(sl.col_type)) {
         out->i64 = k;
@@ -1636,19 +1769,26 @@ extern "C" dq_status dq_state_get_all(const dq_state* s, int n, dq_value* out) {
 
 // ------------------------------------------------------------------------------------------------
 // State exchange across ranks (distributed.py exchange_states): the counters and
-// wrapping Long sums meet in ONE SUM all-reduce, the extremes and the HLL registers in ONE MAX
-// all-reduce, and the fp64 moments in ONE all-gather that a kernel merges in rank order with
-// acc_merge's rules (StandardDeviation.scala:37-44, Correlation.scala:37-52).  The result equals
-// dq_state_merge over the ranks' states in rank order, bit for bit: integer adds wrap and are
-// associative, max / min are exact, and the fp64 merges run in the same order from the same inputs.
-//   isum[10 T + 1]        every task's Acc.i (TK_NUMERIC's min / max keys as 0), then the rows
-//   imax[2 T + 512 n_hll] TK_NUMERIC max keys, then ~min keys (bitwise NOT reverses the signed
-//                         order: MAX of ~min = ~MIN), then the HLL registers widened to int64
-//   mom[8 T]              per task: n, 1 when acc_merge would not skip the buffer, d0..d5;
-//                         gathered rank-major as [world][8 T]
+// wrapping Long sums meet in ONE SUM all-reduce, the extremes in ONE MAX all-reduce, the HLL
+// registers (u8) in ONE MAX all-reduce, and the fp64 moments in ONE all-gather that a kernel merges
+// in rank order with acc_merge's rules (StandardDeviation.scala:37-44, Correlation.scala:37-52).
+// The result equals dq_state_merge over the ranks' states in rank order, bit for bit: integer adds
+// wrap and are associative, max / min are exact, and the fp64 merges run in the same order from
+// the same inputs.
+//   isum[10 T + 1]   every task's Acc.i (TK_NUMERIC's min / max keys and TK_DECIMAL's 128-bit
+//                    words as 0), then the rows
+//   imax[2 T]        TK_NUMERIC max keys, then ~min keys (bitwise NOT reverses the signed order:
+//                    MAX of ~min = ~MIN)
+//   hll[512 n_hll]   the HLL registers (StatefulHyperloglogPlus.scala:119-137 merges by max)
+//   mom[16 T]        per task: n, 1 when acc_merge would not skip the buffer, d0..d5, then (TK_DECIMAL)
+//                    its i1..i7 as raw bits -- the 192-bit sum and 128-bit extremes, whose carries
+//                    and lexicographic order no word-wise collective keeps -- merged in rank order
+//                    by acc_merge; gathered rank-major as [world][16 T]
+// The task kinds live on the device from the state's first exchange (plans are immutable): no
+// upload and no host wait per call.
 // ------------------------------------------------------------------------------------------------
 namespace {
-constexpr int kMomW = 8;
+constexpr int kMomW = 16;
 
 DQ_HD void xchg_pack_task(int kind, const Acc& a, int k, int T, int64_t* isum, int64_t* imax,
                           double* mom) {
@@ -1665,11 +1805,31 @@ DQ_HD void xchg_pack_task(int kind, const Acc& a, int k, int T, int64_t* isum, i
   m[0] = (double)a.i[0];
   m[1] = live ? 1.0 : 0.0;
   for (int q = 0; q < 6; ++q) m[2 + q] = a.d[q];
+  for (int q = 8; q < kMomW; ++q) m[q] = 0.0;
+  if (kind == TK_DECIMAL) {
+    for (int q = 1; q < 8; ++q) {
+      isum[10 * k + q] = 0;
+      m[7 + q] = __builtin_bit_cast(double, a.i[q]);
+    }
+  }
 }
 
 // The merged Acc of task k: acc_merge(init, rank 0, rank 1, ...) restated over the exchange
 DQ_HD void xchg_merge_task(int kind, int k, int T, int world, const int64_t* isum,
                            const int64_t* imax, const double* momg, Acc& out) {
+  if (kind == TK_DECIMAL) {  // every field from the gathered words, in rank order
+    acc_init(kind, out);
+    for (int r = 0; r < world; ++r) {
+      const double* b = momg + ((size_t)r * T + k) * kMomW;
+      Acc a;
+      acc_init(kind, a);
+      a.i[0] = (int64_t)b[0];
+      for (int q = 1; q < 8; ++q) a.i[q] = __builtin_bit_cast(int64_t, b[7 + q]);
+      for (int q = 0; q < 6; ++q) a.d[q] = b[2 + q];
+      acc_merge(kind, out, a);
+    }
+    return;
+  }
   for (int q = 0; q < 10; ++q) out.i[q] = isum[10 * k + q];
   for (int q = 0; q < 6; ++q) out.d[q] = 0.0;
   if (kind == TK_NUMERIC) {
@@ -1704,82 +1864,87 @@ DQ_HD void xchg_merge_task(int kind, int k, int T, int world, const int64_t* isu
 }
 
 __global__ void xchg_pack_kernel(const Acc* acc, const uint8_t* hll, const int32_t* kinds, int T,
-                                 int nh, int64_t rows, int64_t* isum, int64_t* imax, double* mom) {
+                                 int nh, int64_t rows, int64_t* isum, int64_t* imax, double* mom,
+                                 uint8_t* hll_out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < T) xchg_pack_task(kinds[i], acc[i], i, T, isum, imax, mom);
-  if (i < nh) imax[2 * T + i] = hll[i];
+  if (i < nh) hll_out[i] = hll[i];
   if (i == 0) isum[10 * T] = rows;
 }
 
 __global__ void xchg_unpack_kernel(const int32_t* kinds, int T, int nh, int world,
                                    const int64_t* isum, const int64_t* imax, const double* momg,
-                                   Acc* acc, uint8_t* hll, int64_t* rows) {
+                                   const uint8_t* hll_in, Acc* acc, uint8_t* hll, int64_t* rows) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < T) xchg_merge_task(kinds[i], i, T, world, isum, imax, momg, acc[i]);
-  if (i < nh) hll[i] = (uint8_t)imax[2 * T + i];
+  if (i < nh) hll[i] = hll_in[i];
   if (i == 0) *rows = isum[10 * T];
 }
 
-// the task kinds on the device (a few words, uploaded per call; plans are immutable)
-dq_status xchg_kinds(const dq_plan* p, DevBuf<int32_t>& buf, hipStream_t st) {
-  std::vector<int32_t> k(std::max<size_t>(1, p->tasks.size()), 0);
-  for (size_t t = 0; t < p->tasks.size(); ++t) k[t] = p->tasks[t].kind;
-  HIP_TRY(buf.ensure(k.size()));
-  HIP_TRY(hipMemcpyAsync(buf.p, k.data(), k.size() * 4, hipMemcpyHostToDevice, st));
-  HIP_TRY(hipStreamSynchronize(st));  // (k dies here)
+// The plan's task kinds on the device, uploaded once per state (stream-ordered before the first
+// exchange kernel that reads them; the host vector lives in the state until then).
+dq_status xchg_kinds(dq_state* s, hipStream_t st) {
+  if (s->kinds_ready) return DQ_OK;
+  const dq_plan* p = s->plan;
+  s->h_kinds.assign(std::max<size_t>(1, p->tasks.size()), 0);
+  for (size_t t = 0; t < p->tasks.size(); ++t) s->h_kinds[t] = p->tasks[t].kind;
+  HIP_TRY(s->d_kinds.ensure(s->h_kinds.size()));
+  HIP_TRY(hipMemcpyAsync(s->d_kinds.p, s->h_kinds.data(), s->h_kinds.size() * 4,
+                         hipMemcpyHostToDevice, st));
+  s->kinds_ready = true;
   return DQ_OK;
 }
 }  // namespace
 
 extern "C" dq_status dq_state_exchange_sizes(const dq_plan* plan, int64_t* n_sum, int64_t* n_max,
-                                             int64_t* n_mom) {
-  if (!plan || !n_sum || !n_max || !n_mom) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+                                             int64_t* n_mom, int64_t* n_hll) {
+  if (!plan || !n_sum || !n_max || !n_mom || !n_hll)
+    return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   const int64_t T = (int64_t)plan->tasks.size();
   *n_sum = 10 * T + 1;
-  *n_max = 2 * T + (int64_t)plan->n_hll * kHllM;
+  *n_max = 2 * T;
   *n_mom = kMomW * T;
+  *n_hll = (int64_t)plan->n_hll * kHllM;
   return DQ_OK;
 }
 
 extern "C" dq_status dq_state_exchange_pack(dq_state* s, int64_t* isum, int64_t* imax, double* mom,
-                                            void* hip_stream) {
-  if (!s || !isum || !imax || !mom) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
+                                            uint8_t* hll, void* hip_stream) {
+  if (!s || !isum || !imax || !mom || (!hll && s->plan->n_hll))
+    return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   const dq_plan* p = s->plan;
   const int T = (int)p->tasks.size(), nh = (int)s->hll.size();
-  if (s->device < 0 || (s->synced && !s->rows_on_device)) {
-    if (s->device >= 0) {  // host mirror current: pack it on the host, copy up
-      std::vector<int64_t> hs(10 * (size_t)T + 1), hm(2 * (size_t)T + nh);
-      std::vector<double> hd((size_t)kMomW * T);
-      for (int k = 0; k < T; ++k) xchg_pack_task(p->tasks[k].kind, s->acc[k], k, T, hs.data(), hm.data(), hd.data());
-      for (int i = 0; i < nh; ++i) hm[2 * (size_t)T + i] = s->hll[i];
-      hs[10 * (size_t)T] = s->rows;
-      hipStream_t st = reinterpret_cast<hipStream_t>(hip_stream);
-      HIP_TRY(hipSetDevice(s->device));
-      HIP_TRY(hipMemcpyAsync(isum, hs.data(), hs.size() * 8, hipMemcpyHostToDevice, st));
-      HIP_TRY(hipMemcpyAsync(imax, hm.data(), hm.size() * 8, hipMemcpyHostToDevice, st));
-      if (T) HIP_TRY(hipMemcpyAsync(mom, hd.data(), hd.size() * 8, hipMemcpyHostToDevice, st));
-      HIP_TRY(hipStreamSynchronize(st));  // (the host vectors die here)
-      return DQ_OK;
-    }
+  if (s->device < 0) {  // host-only state: host buffers
     for (int k = 0; k < T; ++k) xchg_pack_task(p->tasks[k].kind, s->acc[k], k, T, isum, imax, mom);
-    for (int i = 0; i < nh; ++i) imax[2 * (size_t)T + i] = s->hll[i];
+    for (int i = 0; i < nh; ++i) hll[i] = s->hll[i];
     isum[10 * (size_t)T] = s->rows;
     return DQ_OK;
   }
-  // the device accumulators are newer than the host mirror: pack them where they are, on the
-  // state's stream, and order the caller's stream (the collectives) after it
-  HIP_TRY(hipSetDevice(s->device));
-  hipStream_t st = s->stream_set ? s->stream : reinterpret_cast<hipStream_t>(hip_stream);
   if (s->rows_on_device)
     return fail(DQ_ERR_STATE, "state holds an unsynced exchange result (call dq_state_sync)");
-  dq_status ks = xchg_kinds(p, s->d_kinds, st);
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t cs = reinterpret_cast<hipStream_t>(hip_stream);
+  hipStream_t st = s->stream_set ? s->stream : cs;
+  // the host mirror is newer than the device words (a merge / deserialize): upload it first, on
+  // the state's stream
+  if (!s->stream_set) {
+    s->stream = st;
+    s->stream_set = true;
+  }
+  dq_status us = upload_host(s);
+  if (us != DQ_OK) return us;
+  if (s->reset_pending) {  // reset and never scanned: the device words are stale, pack the mirror
+    s->host_dirty = true;
+    us = upload_host(s);
+    if (us != DQ_OK) return us;
+  }
+  dq_status ks = xchg_kinds(s, st);
   if (ks != DQ_OK) return ks;
   const int n = std::max(std::max(T, nh), 1);
   hipLaunchKernelGGL(xchg_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, st, s->d_acc.p, s->d_hll.p,
-                     s->d_kinds.p, T, nh, s->rows, isum, imax, mom);
+                     s->d_kinds.p, T, nh, s->rows, isum, imax, mom, hll);
   HIP_TRY(hipGetLastError());
-  hipStream_t cs = reinterpret_cast<hipStream_t>(hip_stream);
-  if (cs != st) {
+  if (cs != st) {  // order the caller's stream (the collectives) after the pack
     HIP_TRY(hipEventRecord(s->ev_xchg, st));
     HIP_TRY(hipStreamWaitEvent(cs, s->ev_xchg, 0));
   }
@@ -1787,14 +1952,16 @@ extern "C" dq_status dq_state_exchange_pack(dq_state* s, int64_t* isum, int64_t*
 }
 
 extern "C" dq_status dq_state_exchange_unpack(dq_state* s, const int64_t* isum, const int64_t* imax,
-                                              const double* mom_gathered, int world, void* hip_stream) {
-  if (!s || !isum || !imax || (!mom_gathered && !s->plan->tasks.empty()) || world < 1)
+                                              const double* mom_gathered, const uint8_t* hll,
+                                              int world, void* hip_stream) {
+  if (!s || !isum || !imax || (!mom_gathered && !s->plan->tasks.empty()) ||
+      (!hll && s->plan->n_hll) || world < 1)
     return fail(DQ_ERR_INVALID_ARGUMENT, "bad argument");
   const dq_plan* p = s->plan;
   const int T = (int)p->tasks.size(), nh = (int)s->hll.size();
   if (s->device < 0) {
     for (int k = 0; k < T; ++k) xchg_merge_task(p->tasks[k].kind, k, T, world, isum, imax, mom_gathered, s->acc[k]);
-    for (int i = 0; i < nh; ++i) s->hll[i] = (uint8_t)imax[2 * (size_t)T + i];
+    for (int i = 0; i < nh; ++i) s->hll[i] = hll[i];
     s->rows = isum[10 * (size_t)T];
     s->synced = true;
     s->host_dirty = true;
@@ -1811,12 +1978,12 @@ extern "C" dq_status dq_state_exchange_unpack(dq_state* s, const int64_t* isum, 
     HIP_TRY(hipEventRecord(s->ev_xchg, cs));
     HIP_TRY(hipStreamWaitEvent(st, s->ev_xchg, 0));
   }
-  dq_status ks = xchg_kinds(p, s->d_kinds, st);
+  dq_status ks = xchg_kinds(s, st);
   if (ks != DQ_OK) return ks;
   HIP_TRY(s->d_rows.ensure(1));
   const int n = std::max(std::max(T, nh), 1);
   hipLaunchKernelGGL(xchg_unpack_kernel, dim3((n + 255) / 256), dim3(256), 0, st, s->d_kinds.p, T, nh,
-                     world, isum, imax, mom_gathered, s->d_acc.p, s->d_hll.p, s->d_rows.p);
+                     world, isum, imax, mom_gathered, hll, s->d_acc.p, s->d_hll.p, s->d_rows.p);
   HIP_TRY(hipGetLastError());
   s->rows_on_device = true;
   s->synced = false;
@@ -1867,7 +2034,7 @@ extern "C" dq_status dq_state_deserialize(dq_state* s, const void* buf, int64_t 
   memcpy(hdr, b, 32);
   if (hdr[0] != kMagic || hdr[1] != s->plan->tasks.size() || hdr[2] != (uint64_t)s->plan->n_hll)
     return fail(DQ_ERR_STATE, "serialized state does not match this plan");
-  if (s->stream_set && s->device >= 0) HIP_TRY(hipStreamSynchronize(s->stream));
+  if (s->stream_set && s->device >= 0) HIP_TRY(host_wait(s->stream));
   s->rows = (int64_t)hdr[3];
   if (!s->acc.empty()) memcpy(s->acc.data(), b + 32, s->acc.size() * sizeof(Acc));
   if (!s->hll.empty()) memcpy(s->hll.data(), b + 32 + s->acc.size() * sizeof(Acc), s->hll.size());
@@ -1940,6 +2107,30 @@ extern "C" void dq_java_doubles_to_strings(const double* values, int64_t n, int 
                        : jfmt::double_to_java(values[i], out + 32 * i);
 }
 
+extern "C" double dq_decimal_to_double(uint64_t lo, int64_t hi, int32_t scale) {
+  return dec_to_double(lo, hi, scale < 0 ? 0 : (scale > 38 ? 38 : scale));
+}
+
+extern "C" dq_status dq_format_values(int32_t type, const void* values, int64_t n, char* out,
+                                      int32_t* lens) {
+  if (n < 0 || (n > 0 && (!values || !out || !lens))) return fail(DQ_ERR_INVALID_ARGUMENT, "bad argument");
+  if (!valid_type(type)) return fail(DQ_ERR_INVALID_ARGUMENT, "unknown column type %d", type);
+  for (int64_t i = 0; i < n; ++i) {
+    char* o = out + (int64_t)kFmtMax * i;
+    if (is_decimal(type)) {
+      const uint64_t* v = static_cast<const uint64_t*>(values) + 2 * i;
+      lens[i] = dec_format(v[0], (int64_t)v[1], DQ_DECIMAL_SCALE(type), o);
+    } else if (type == DQ_DATE32) {
+      lens[i] = date_format(static_cast<const int32_t*>(values)[i], o);
+    } else if (type == DQ_TIMESTAMP_US) {
+      lens[i] = ts_format(static_cast<const int64_t*>(values)[i], o);
+    } else {
+      return fail(DQ_ERR_WRONG_TYPE, "dq_format_values formats decimal / date / timestamp values");
+    }
+  }
+  return DQ_OK;
+}
+
 // Bitmaps re-based for sliced Arrow arrays, owned by the library until dq_column_release.
 namespace {
 struct OwnedBitmap {
@@ -1977,7 +2168,7 @@ dq_status bitmap_at(const uint8_t* src, int64_t bit, int64_t rows, const uint8_t
     hipError_t e = dev_alloc(&p, n + 16, &got, &dev);
     if (e == hipSuccess) e = hipMemsetAsync(p, 0, got, nullptr);
     if (e == hipSuccess) e = launch_bitmap_rebase(src, bit, rows, static_cast<uint8_t*>(p), nullptr);
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e == hipSuccess) e = host_wait(nullptr);
     (void)hipSetDevice(cur);
     if (e != hipSuccess) {
       if (p) dev_free(p, got, dev);
@@ -2036,7 +2227,17 @@ extern "C" dq_status dq_column_from_arrow(const struct ArrowArray* array,
   else if (f == "f") type = DQ_FLOAT32;
   else if (f == "g") type = DQ_FLOAT64;
   else if (f == "u") type = DQ_UTF8;
-  else return fail(DQ_ERR_UNSUPPORTED, "Arrow format '%s'", schema->format);
+  else if (f == "tdD") type = DQ_DATE32;
+  else if (f.compare(0, 4, "tsu:") == 0) type = DQ_TIMESTAMP_US;  // any zone: the values are UTC
+  else if (f.compare(0, 2, "d:") == 0) {  // "d:precision,scale[,bitwidth]"
+    int prec = -1, sc = -1, bw = 128;
+    char tail = 0;
+    const int got = sscanf(f.c_str() + 2, "%d,%d,%d%c", &prec, &sc, &bw, &tail);
+    if (got < 2 || got > 3 || bw != 128 || prec < 1 || prec > 38 || sc < 0 || sc > prec)
+      return fail(DQ_ERR_UNSUPPORTED, "Arrow decimal format '%s' (decimal128, 1 <= p <= 38, "
+                                      "0 <= s <= p)", schema->format);
+    type = DQ_DECIMAL_TYPE(prec, sc);
+  } else return fail(DQ_ERR_UNSUPPORTED, "Arrow format '%s'", schema->format);
   int64_t need = type == DQ_UTF8 ? 3 : 2;
   if (array->n_buffers < need) return fail(DQ_ERR_INVALID_ARGUMENT, "too few Arrow buffers");
   const int64_t off = array->offset, n = array->length;
@@ -2062,8 +2263,7 @@ extern "C" dq_status dq_column_from_arrow(const struct ArrowArray* array,
     c.values = vals ? vals + 4 * off : nullptr;
     c.data = static_cast<const uint8_t*>(array->buffers[2]);
   } else {
-    const int64_t w = type == DQ_INT8 ? 1 : type == DQ_INT16 ? 2
-                    : (type == DQ_INT32 || type == DQ_FLOAT32) ? 4 : 8;
+    const int64_t w = type_size(type);
     c.values = vals ? vals + w * off : nullptr;
   }
   *out = c;
@@ -2218,7 +2418,7 @@ void release_pinned_staging() {
 }
 
 hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
-  if (!bytes) return hipStreamSynchronize(st);
+  if (!bytes) return host_wait(st);
   size_t want = 4096;
   while (want < bytes) want <<= 1;
   PinnedPool& pool = pinned_pool();
@@ -2234,7 +2434,7 @@ hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
     }
   }
   if (!buf && want > (64u << 20)) {  // (large copies: not worth pinning a block for)
-    hipError_t e = hipStreamSynchronize(st);
+    hipError_t e = host_wait(st);
     return e != hipSuccess ? e : hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
   }
   if (!buf) {
@@ -2242,7 +2442,7 @@ hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   hipError_t e = hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess) e = host_wait(st);
   if (e != hipSuccess) return e;  // (the block is dropped: a DMA may still be writing it)
   memcpy(dst, buf, bytes);
   bool keep;

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "decimal.h"
 #include "engine.h"
 
 namespace dq {
@@ -147,7 +148,13 @@ DQ_HD bool is_float_type(int type) { return type == DQ_FLOAT32 || type == DQ_FLO
 // Spark XxHash64Function.hash(value, type, 42) for one non-null row.
 DQ_DEV uint64_t hash_row(int type, const void* values, const uint8_t* data, int64_t r) {
   const uint64_t seed = 42;
-  switch (type) {
+  switch (DQ_TYPE_ID(type)) {
+    case DQ_DATE32: return xxh_int((uint32_t)reinterpret_cast<const int32_t*>(values)[r], seed);
+    case DQ_TIMESTAMP_US: return xxh_long((uint64_t)reinterpret_cast<const int64_t*>(values)[r], seed);
+    case DQ_DECIMAL128: {
+      const uint64_t* v = reinterpret_cast<const uint64_t*>(values) + 2 * r;
+      return dec_hash(v[0], (int64_t)v[1], DQ_DECIMAL_PRECISION(type), seed);
+    }
     case DQ_INT8: return xxh_int((uint32_t)(int32_t)reinterpret_cast<const int8_t*>(values)[r], seed);
     case DQ_INT16:
       return xxh_int((uint32_t)(int32_t)reinterpret_cast<const int16_t*>(values)[r], seed);

@@ -24,7 +24,8 @@ enum TaskKind : int32_t {
   TK_BOOLMAP = 4,    // counts over a materialised predicate bitmap (generic predicates / where)
   TK_COMOMENTS = 5,  // two numeric columns: (n, xAvg, yAvg, ck, xMk, yMk)
   TK_HLL = 6,        // HLL++ registers (P = 9, 512 registers) of one column
-  TK_DTYPE = 7       // DataType: counts of NULL / Fractional / Integral / Boolean / String values
+  TK_DTYPE = 7,      // DataType: counts of NULL / Fractional / Integral / Boolean / String values
+  TK_DECIMAL = 8     // one decimal(p, s) column: n, exact Sum, 128-bit Min / Max, (n, avg, m2)
 };
 
 constexpr int kMaxPreds = 3;          // fused predicates per TK_NUMERIC task
@@ -107,6 +108,9 @@ struct TaskDesc {
 //   TK_STR_IN / TK_BOOLMAP : i0 TRUE count, i1 non-NULL count
 //   TK_COMOMENTS: i0 n; d0 xAvg, d1 yAvg, d2 ck, d3 xMk, d4 yMk
 //   TK_DTYPE    : i0 NULL, i1 Fractional, i2 Integral, i3 Boolean, i4 String
+//   TK_DECIMAL  : i0 n, i1..i3 the sum of the unscaled values (192-bit two's complement, little-
+//                 endian limbs: exact for any row count), i4/i5 min (lo, hi), i6/i7 max (lo, hi);
+//                 d1 avg, d2 m2 of the values cast to double (as TK_NUMERIC)
 struct alignas(16) Acc {
   int64_t i[10];
   double d[6];
@@ -118,6 +122,43 @@ DQ_HD void acc_init(int kind, Acc& a) {
   if (kind == TK_NUMERIC) {
     a.i[2] = INT64_MAX;  // min key
     a.i[3] = INT64_MIN;  // max key
+  }
+  if (kind == TK_DECIMAL) {  // min = INT128_MAX, max = INT128_MIN
+    a.i[4] = -1;
+    a.i[5] = INT64_MAX;
+    a.i[6] = 0;
+    a.i[7] = INT64_MIN;
+  }
+}
+
+// 128-bit signed order of (lo, hi) pairs held in int64 words
+DQ_HD bool i128_lt(int64_t alo, int64_t ahi, int64_t blo, int64_t bhi) {
+  return ahi < bhi || (ahi == bhi && (uint64_t)alo < (uint64_t)blo);
+}
+// s[0..2] += sign-extended (lo, hi)
+DQ_HD void add192(int64_t* s, uint64_t lo, int64_t hi) {
+  const uint64_t x[3] = {lo, (uint64_t)hi, hi < 0 ? ~0ULL : 0ULL};
+  uint64_t c = 0;
+  for (int k = 0; k < 3; ++k) {
+    const uint64_t a = (uint64_t)s[k];
+    const uint64_t t = a + x[k];
+    const uint64_t c1 = t < a ? 1 : 0;
+    const uint64_t u = t + c;
+    const uint64_t c2 = u < t ? 1 : 0;
+    s[k] = (int64_t)u;
+    c = c1 + c2;
+  }
+}
+DQ_HD void add192_3(int64_t* s, const int64_t* b) {
+  uint64_t c = 0;
+  for (int k = 0; k < 3; ++k) {
+    const uint64_t a = (uint64_t)s[k];
+    const uint64_t t = a + (uint64_t)b[k];
+    const uint64_t c1 = t < a ? 1 : 0;
+    const uint64_t u = t + c;
+    const uint64_t c2 = u < t ? 1 : 0;
+    s[k] = (int64_t)u;
+    c = c1 + c2;
   }
 }
 
@@ -197,6 +238,25 @@ DQ_HD void acc_merge(int kind, Acc& a, const Acc& b) {
     case TK_DTYPE:
       for (int k = 0; k < 5; ++k) a.i[k] += b.i[k];
       break;
+    case TK_DECIMAL: {
+      if (b.i[0] == 0) return;
+      if (a.i[0] == 0) {
+        a = b;
+        return;
+      }
+      moments_merge((double)a.i[0], a.d[1], a.d[2], (double)b.i[0], b.d[1], b.d[2]);
+      a.i[0] += b.i[0];
+      add192_3(&a.i[1], &b.i[1]);
+      if (i128_lt(b.i[4], b.i[5], a.i[4], a.i[5])) {
+        a.i[4] = b.i[4];
+        a.i[5] = b.i[5];
+      }
+      if (i128_lt(a.i[6], a.i[7], b.i[6], b.i[7])) {
+        a.i[6] = b.i[6];
+        a.i[7] = b.i[7];
+      }
+      break;
+    }
     default:
       a.i[0] += b.i[0];
       a.i[1] += b.i[1];

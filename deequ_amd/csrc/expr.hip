@@ -18,7 +18,8 @@ namespace dq {
 // into Arrow boolean bitmaps (value bits, validity bits).
 // ------------------------------------------------------------------------------------------------
 struct V {
-  int32_t tag;  // 0 NULL, 1 BOOL, 2 I64, 3 F64, 4 STR
+  int32_t tag;  // 0 NULL, 1 BOOL, 2 I64, 3 F64, 4 STR, 5 DECIMAL (i = low word, d = high word's
+                // bits, len = scale), 6 DATE (i = days), 7 TIMESTAMP (i = microseconds)
   int32_t len;
   int64_t i;
   double d;
@@ -37,6 +38,13 @@ DQ_DEV int cmp_str(const uint8_t* a, int32_t la, const uint8_t* b, int32_t lb) {
 
 // three-way compare of two non-NULL values; returns 2 when incomparable
 DQ_DEV int cmp_vals(const V& a, const V& b) {
+  if (a.tag == 5 && b.tag == 5) {  // unscaled at one scale (the plan aligns a literal's scale)
+    const int64_t ah = __builtin_bit_cast(int64_t, a.d), bh = __builtin_bit_cast(int64_t, b.d);
+    if (ah != bh) return ah < bh ? -1 : 1;
+    if (a.i == b.i) return 0;
+    return (uint64_t)a.i < (uint64_t)b.i ? -1 : 1;
+  }
+  if (a.tag >= 5 || b.tag >= 5) return 2;  // (dq_plan_create admits no other pairing)
   if (a.tag == 4 && b.tag == 4) return cmp_str(a.p, a.len, b.p, b.len);
   if (a.tag == 4 || b.tag == 4) return 2;
   if (a.tag == 3 || b.tag == 3) {
@@ -163,8 +171,21 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
           case XI_COL: {
             const DevCol& c = cols[ins.a];
             V v{};
+            const int tid = DQ_TYPE_ID(c.type);
             if (!bit1(c.valid, r)) {
               v.tag = 0;
+            } else if (tid == DQ_DECIMAL128) {
+              const uint64_t* dv = reinterpret_cast<const uint64_t*>(c.values) + 2 * r;
+              v.tag = 5;
+              v.i = (int64_t)dv[0];
+              v.d = __builtin_bit_cast(double, dv[1]);
+              v.len = DQ_DECIMAL_SCALE(c.type);
+            } else if (tid == DQ_DATE32) {
+              v.tag = 6;
+              v.i = reinterpret_cast<const int32_t*>(c.values)[r];
+            } else if (tid == DQ_TIMESTAMP_US) {
+              v.tag = 7;
+              v.i = reinterpret_cast<const int64_t*>(c.values)[r];
             } else if (c.type == DQ_UTF8) {
               const int32_t* off = reinterpret_cast<const int32_t*>(c.values);
               v.tag = 4;
@@ -188,6 +209,8 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
           case XI_BOOL: st[sp++] = V{1, 0, ins.imm, 0.0, nullptr}; break;
           case XI_I64: st[sp++] = V{2, 0, ins.imm, 0.0, nullptr}; break;
           case XI_F64: st[sp++] = V{3, 0, 0, __builtin_bit_cast(double, ins.imm), nullptr}; break;
+          case XI_DEC128: st[sp++] = V{5, 0, ins.imm, 0.0, nullptr}; break;
+          case XI_DEC128_HI: st[sp - 1].d = __builtin_bit_cast(double, ins.imm); break;
           case XI_STR: st[sp++] = V{4, ins.a, 0, 0.0, pool + ins.imm}; break;
           case XI_IS_NULL: st[sp - 1] = V{1, 0, st[sp - 1].tag == 0 ? 1 : 0, 0.0, nullptr}; break;
           case XI_IS_NOT_NULL: st[sp - 1] = V{1, 0, st[sp - 1].tag != 0 ? 1 : 0, 0.0, nullptr}; break;
@@ -258,6 +281,9 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
             if (a.tag == 2 || a.tag == 1) {
               a.d = to_f32 ? (double)(float)a.i : (double)a.i;  // (float)long: one rounding
               a.tag = 3;
+            } else if (a.tag == 5) {  // Decimal.toDouble: correctly rounded
+              a.d = dec_to_double((uint64_t)a.i, __builtin_bit_cast(int64_t, a.d), a.len);
+              a.tag = 3;
             } else if (a.tag == 4) {
               double d;
               if (parse_f64(a.p, a.len, d)) a = V{3, 0, 0, d, nullptr};
@@ -286,10 +312,17 @@ __global__ void __launch_bounds__(kBlock) expr_kernel(const XInstr* __restrict__
             if (a.tag == 4) {
               DevBytes rd{a.p};
               for (int32_t k = 0; k < a.len && !status[q]; ++k) q = nx[q * nc + cls[rd.u8(k)]];
-            } else {  // Spark's cast to string: decimal integer, true / false, Double.toString
-              char buf[jfmt::kMaxChars];
+            } else {  // Spark's cast to string: decimal integer, true / false, Double.toString,
+                      // BigDecimal.toString, yyyy-MM-dd [HH:mm:ss[.f]] (decimal.h)
+              char buf[kFmtMax > jfmt::kMaxChars ? kFmtMax : jfmt::kMaxChars];
               int nb = 0;
-              if (a.tag == 3) {
+              if (a.tag == 5) {
+                nb = dec_format((uint64_t)a.i, __builtin_bit_cast(int64_t, a.d), a.len, buf);
+              } else if (a.tag == 6) {
+                nb = date_format(a.i, buf);
+              } else if (a.tag == 7) {
+                nb = ts_format(a.i, buf);
+              } else if (a.tag == 3) {
                 nb = a.len ? jfmt::float_to_java((float)a.d, buf) : jfmt::double_to_java(a.d, buf);
               } else if (a.tag == 1) {
                 const char* t = a.i ? "true" : "false";

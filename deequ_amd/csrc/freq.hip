@@ -4621,7 +4621,14 @@ static void pinned_word_put(unsigned long long* p) {
 struct dq_freq {
   int device = 0;
   int n_keys = 0;
+  // key types as the caller declared them, and the physical layout the group-by runs on
+  // (freq_phys_type: dates / timestamps as their integers, decimals as their unscaled long or
+  // 16-byte string); every kernel below sees only `types`
+  std::vector<int32_t> logical;
   std::vector<int32_t> types;
+  bool relabel = false;  // some logical type differs from its physical one
+  DevBuf<int64_t> dec_long[kMaxKeys];  // decimal(p <= 18) keys narrowed to their unscaled long
+  DevBuf<int32_t> dec_off;             // decimal(p > 18) keys: offsets 0, 16, 32, ... (shared)
   bool exact = false;
   int mode_null_as_group = -1;  // fixed by the first add
   int tile = 0, rb = 0;
@@ -6180,6 +6187,76 @@ static dq_status select_top(dq_freq* f, const Group* arr, int64_t n, int k, std:
 }
 
 // ------------------------------------------------------------------------------------------------
+// Date / timestamp / decimal keys.  Grouping on cast(col as string) (Histogram.scala:63) or on the
+// value (GroupingAnalyzers.scala:62-72) puts the same rows together for these types (the casts to
+// string are injective at a fixed scale and in UTC), so a table groups the values themselves: a
+// date as its int32 and a timestamp as its int64 (the same bytes, relabelled), a decimal(p <= 18)
+// as its unscaled long (narrowed: the 16-byte value's low word), a decimal(p > 18) as a 16-byte
+// string of its little-endian unscaled value (offsets 0, 16, ...; the value buffer is the
+// character data, no copy).  Keys export in those physical forms (deequ_amd.h dq_freq_export).
+// ------------------------------------------------------------------------------------------------
+static int freq_phys_type(int t) {
+  if (t == DQ_DATE32) return DQ_INT32;
+  if (t == DQ_TIMESTAMP_US) return DQ_INT64;
+  if (DQ_TYPE_ID(t) == DQ_DECIMAL128) return DQ_DECIMAL_PRECISION(t) <= 18 ? DQ_INT64 : DQ_UTF8;
+  return t;
+}
+
+namespace dq {
+__global__ void dec_narrow_kernel(const uint64_t* __restrict__ in, int64_t* __restrict__ out,
+                                  int64_t rows) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (int64_t)in[2 * i];
+}
+__global__ void iota16_kernel(int32_t* __restrict__ out, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (int32_t)(16 * i);
+}
+}  // namespace dq
+
+static dq_status physical_keys(dq_freq* f, const dq_column* keys, int n_keys, hipStream_t st,
+                               dq_column* out) {
+  for (int k = 0; k < n_keys; ++k) {
+    if (keys[k].type != f->logical[k]) return fail(DQ_ERR_WRONG_TYPE, "key %d has the wrong type", k);
+    dq_column c = keys[k];
+    c.type = f->types[k];
+    const int64_t rows = c.length;
+    if (DQ_TYPE_ID(f->logical[k]) == DQ_DECIMAL128 && rows > 0) {
+      if (!keys[k].values) return fail(DQ_ERR_INVALID_ARGUMENT, "key %d has no values", k);
+      const unsigned grid = (unsigned)std::min<int64_t>((rows + 255) / 256, 4096);
+      if (c.type == DQ_INT64) {
+        if (f->dec_long[k].n < (size_t)rows) {
+          HIP_TRY(hipStreamSynchronize(st));  // (the previous batch may still read the buffer)
+          HIP_TRY(f->dec_long[k].ensure((size_t)rows));
+        }
+        hipLaunchKernelGGL(dec_narrow_kernel, dim3(grid), dim3(256), 0, st,
+                           static_cast<const uint64_t*>(keys[k].values), f->dec_long[k].p, rows);
+        HIP_TRY(hipGetLastError());
+        c.values = f->dec_long[k].p;
+      } else {  // 16-byte strings over the value buffer itself
+        if (rows >= ((int64_t)1 << 27))
+          return fail(DQ_ERR_UNSUPPORTED, "decimal(p > 18) key batch of %lld rows (at most 2^27: "
+                                          "int32 string offsets)", (long long)rows);
+        if (f->dec_off.n < (size_t)rows + 1) {
+          HIP_TRY(hipStreamSynchronize(st));
+          HIP_TRY(f->dec_off.ensure((size_t)rows + 1));
+          hipLaunchKernelGGL(iota16_kernel, dim3((unsigned)std::min<int64_t>((f->dec_off.n + 255) / 256, 4096)),
+                             dim3(256), 0, st, f->dec_off.p, (int64_t)f->dec_off.n);
+          HIP_TRY(hipGetLastError());
+        }
+        c.values = f->dec_off.p;
+        c.data = static_cast<const uint8_t*>(keys[k].values);
+        c.data_bytes = (int32_t)(16 * rows);
+      }
+    }
+    out[k] = c;
+  }
+  return DQ_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------------
 extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_types,
@@ -6190,9 +6267,15 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
   auto f = std::make_unique<dq_freq>();
   f->device = device;
   f->n_keys = n_keys;
-  f->types.assign(key_types, key_types + n_keys);
-  for (int t : f->types)
-    if (t < DQ_BOOL || t > DQ_UTF8) return fail(DQ_ERR_INVALID_ARGUMENT, "bad key type %d", t);
+  f->logical.assign(key_types, key_types + n_keys);
+  for (int t : f->logical) {
+    const int p = DQ_DECIMAL_PRECISION(t), sc = DQ_DECIMAL_SCALE(t);
+    const bool ok = DQ_TYPE_ID(t) == DQ_DECIMAL128 ? ((t >> 24) == 0 && p >= 1 && p <= 38 && sc <= p)
+                                                   : (t >= DQ_BOOL && t <= DQ_TIMESTAMP_US);
+    if (!ok) return fail(DQ_ERR_INVALID_ARGUMENT, "bad key type %d", t);
+    f->types.push_back(freq_phys_type(t));
+    f->relabel = f->relabel || f->types.back() != t;
+  }
   f->exact = n_keys == 1 && f->types[0] != DQ_UTF8;
   f->tile = f->exact ? FM<false>::kTile : FM<true>::kTile;
   f->rb = f->exact ? FM<false>::kRB : FM<true>::kRB;
@@ -6206,7 +6289,7 @@ extern "C" dq_status dq_freq_create(int device, int n_keys, const int32_t* key_t
                      2 * (capacity_hint >> 24) + 16;
     // one utf8 key: + the fixed-capacity bucket pieces (1.5x the rows; dq_freq_add_device), and
     // their piece rows (growing any of them copies the table and waits for the stream)
-    const bool hp = !f->exact && n_keys == 1 && key_types[0] == DQ_UTF8 && hpieces_enabled();
+    const bool hp = !f->exact && n_keys == 1 && f->types[0] == DQ_UTF8 && hpieces_enabled();
     if (f->exact && pieces_enabled() && xfixed_enabled()) {  // + exact fixed-capacity pieces
       int64_t n_wg = 0;
       phaseA_chunks(false, false, capacity_hint, f->tile, &n_wg);
@@ -6275,6 +6358,13 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
                                         int null_as_group, void* hip_stream) {
   if (!f || !keys) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   if (n_keys != f->n_keys) return fail(DQ_ERR_INVALID_ARGUMENT, "expected %d key columns", f->n_keys);
+  dq_column phys[kMaxKeys];
+  if (f->relabel) {  // the caller's date / timestamp / decimal keys in the table's physical layout
+    HIP_TRY(hipSetDevice(f->device));
+    const dq_status ps = physical_keys(f, keys, n_keys, reinterpret_cast<hipStream_t>(hip_stream), phys);
+    if (ps != DQ_OK) return ps;
+    keys = phys;
+  }
   if (f->arena_view) return fail(DQ_ERR_STATE, "a table reading another table's keys takes no adds");
   const int mode = null_as_group ? 1 : 0;
   if (f->mode_null_as_group >= 0 && f->mode_null_as_group != mode)
@@ -6475,7 +6565,7 @@ static dq_status marginal_of(dq_freq* joint, int key_index, dq_freq* out, void* 
   if (!joint || !out) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   if (joint->exact || joint->n_keys < 2) return fail(DQ_ERR_INVALID_ARGUMENT, "not a multi-key table");
   if (key_index < 0 || key_index >= joint->n_keys) return fail(DQ_ERR_INVALID_ARGUMENT, "bad key index");
-  if (out->n_keys != 1 || out->types[0] != joint->types[key_index])
+  if (out->n_keys != 1 || out->logical[0] != joint->logical[key_index])
     return fail(DQ_ERR_WRONG_TYPE, "the marginal table must have one key of the column's type");
   if (joint->mode_null_as_group > 0) return fail(DQ_ERR_UNSUPPORTED, "marginal of a Histogram table");
   HIP_TRY(hipSetDevice(joint->device));
@@ -6915,6 +7005,10 @@ extern "C" dq_status dq_freq_hll(dq_freq* f, int64_t max_records, uint64_t* word
   if (!f || !words || !done) return fail(DQ_ERR_INVALID_ARGUMENT, "null argument");
   *done = 0;
   if (f->n_keys != 1 || (!f->exact && f->types[0] != DQ_UTF8)) return DQ_OK;  // (not one value)
+  // a decimal(p > 18) table holds 16-byte strings, which Spark hashes as BigInteger.toByteArray,
+  // not these bytes: the caller scans (decimal(p <= 18) keys are the unscaled longs, hashLong --
+  // Spark's; dates / timestamps are their int32 / int64, hashInt / hashLong -- Spark's)
+  if (DQ_TYPE_ID(f->logical[0]) == DQ_DECIMAL128 && f->types[0] == DQ_UTF8) return DQ_OK;
   HIP_TRY(hipSetDevice(f->device));
   if (hip_stream) f->stream = reinterpret_cast<hipStream_t>(hip_stream);
   dq_status st = finalize_b(f);
@@ -7226,7 +7320,7 @@ extern "C" dq_status dq_freq_merge(dq_freq* dst, const dq_freq* src_c) {
   dq_freq* src = const_cast<dq_freq*>(src_c);
   if (dst == src) return fail(DQ_ERR_INVALID_ARGUMENT, "cannot merge a table into itself");
   if (dst->arena_view) return fail(DQ_ERR_STATE, "a table reading another table's keys takes no adds");
-  if (dst->n_keys != src->n_keys || dst->types != src->types)
+  if (dst->n_keys != src->n_keys || dst->logical != src->logical)
     return fail(DQ_ERR_STATE, "frequency tables group on different key types");
   if (dst->device != src->device) return fail(DQ_ERR_UNSUPPORTED, "tables on different devices");
   dst->nan_counted = dst->nan_counted && src->nan_counted;
@@ -7582,11 +7676,13 @@ extern "C" dq_status dq_key_partition(const dq_column* batches, int n_batches, i
   if (n_parts < 1 || n_parts > kMaxParts)
     return fail(DQ_ERR_UNSUPPORTED, "n_parts must be in [1, %d]", kMaxParts);
   int64_t rows = 0;
-  int type = n_batches ? batches[0].type : DQ_INT64;
+  const int ltype = n_batches ? batches[0].type : DQ_INT64;
+  // a date / timestamp key is its int32 / int64 (equal keys, equal owner, as a table counts them)
+  const int type = ltype == DQ_DATE32 ? DQ_INT32 : ltype == DQ_TIMESTAMP_US ? DQ_INT64 : ltype;
   const int elem = raw_key_elem(type);
   if (!elem) return fail(DQ_ERR_WRONG_TYPE, "raw-key repartition needs a fixed-width key");
   for (int b = 0; b < n_batches; ++b) {
-    if (batches[b].type != type) return fail(DQ_ERR_WRONG_TYPE, "batches differ in type");
+    if (batches[b].type != ltype) return fail(DQ_ERR_WRONG_TYPE, "batches differ in type");
     if (batches[b].length < 0 || (batches[b].length && !batches[b].values))
       return fail(DQ_ERR_INVALID_ARGUMENT, "batch %d has no values", b);
     rows += batches[b].length;

@@ -103,7 +103,9 @@ enum XiOp : int32_t {
   XI_CMP,        // a = dq_xop comparison
   XI_IN,         // a = number of list items
   XI_CAST_F64,
-  XI_REGEX       // a = null_mode, imm = offset of the automaton in the pool
+  XI_REGEX,      // a = null_mode, imm = offset of the automaton in the pool
+  XI_DEC128,     // imm = low word of a decimal literal (unscaled at its column's scale) ...
+  XI_DEC128_HI   // ... imm = its high word (always right after XI_DEC128)
 };
 
 struct XInstr {
@@ -139,6 +141,7 @@ enum BodyClass : int32_t {
   BC_CORR,
   BC_HLL,
   BC_CORR_HLL,  // TK_COMOMENTS task that also fills an HLL task's registers from one of its columns
+  BC_DECIMAL,   // TK_DECIMAL (always its own launch: the mixed kernel has no decimal body)
   kBodyClasses
 };
 // A launch of the mixed kernel: every non-HLL body class in one grid, items taken in an
@@ -163,8 +166,8 @@ struct ScanLaunch {
   int32_t lds_hll = 0;     // kBodyMixed: HLL tasks whose registers the launch keeps in LDS
   uint32_t classes = 0;    // kBodyMixed: the body classes of its items (bit per BodyClass)
 };
-// Mixed-kernel instantiations: every class, and BASELINE configs[1]'s three
-constexpr uint32_t kMixedAll = (1u << kBodyClasses) - 1u;
+// Mixed-kernel instantiations: every class it has a body for, and BASELINE configs[1]'s three
+constexpr uint32_t kMixedAll = ((1u << kBodyClasses) - 1u) & ~(1u << BC_DECIMAL);
 constexpr uint32_t kMixedS10 = (1u << BC_BITS) | (1u << BC_NUM_I64) | (1u << BC_STR_IN);
 
 // Most HLL tasks whose LDS registers (2 KiB each) ride in the mixed launch.  0 = HLL always keeps

@@ -58,11 +58,12 @@ void host_copy(uint8_t* dst, const void* src, size_t bytes) {
 }
 
 size_t fixed_width(int t) {
+  if (DQ_TYPE_ID(t) == DQ_DECIMAL128) return 16;
   switch (t) {
     case DQ_INT8: return 1;
     case DQ_INT16: return 2;
-    case DQ_INT32: case DQ_FLOAT32: return 4;
-    case DQ_INT64: case DQ_FLOAT64: return 8;
+    case DQ_INT32: case DQ_FLOAT32: case DQ_DATE32: return 4;
+    case DQ_INT64: case DQ_FLOAT64: case DQ_TIMESTAMP_US: return 8;
     default: return 0;
   }
 }

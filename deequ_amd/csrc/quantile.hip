@@ -20,6 +20,8 @@
 // (deequ_amd/analyzers/quantile.py).
 #include <hip/hip_runtime.h>
 
+#include <memory>
+
 #include <cstring>  // rocprim headers use memset without including it
 
 #include <rocprim/rocprim.hpp>
@@ -28,6 +30,7 @@
 #include <vector>
 
 #include "device_util.h"
+#include "decimal.h"
 #include "kernels.h"
 
 using namespace dq;
@@ -700,6 +703,15 @@ dq_status radix_select(Source src, Passer& ps, Pass p, std::vector<Target> tg, s
 
 }  // namespace
 
+namespace dq {
+__global__ void dec_to_f64_kernel(const uint64_t* __restrict__ in, double* __restrict__ out,
+                                  int64_t rows, int scale) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = dec_to_double(in[2 * i], (int64_t)in[2 * i + 1], scale);
+}
+}  // namespace dq
+
 extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int n_batches,
                                       int64_t head_values, int64_t max_values, double* out,
                                       int64_t* n_out, int64_t* count_out, void* hip_stream) {
@@ -709,9 +721,10 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
   HIP_TRY(hipSetDevice(device));
   int64_t rows = 0;
+  const bool dec = n_batches > 0 && DQ_TYPE_ID(batches[0].type) == DQ_DECIMAL128;
   for (int b = 0; b < n_batches; ++b) {
     const dq_column& c = batches[b];
-    if (c.type == DQ_UTF8 || c.type == DQ_BOOL || c.type < DQ_BOOL || c.type > DQ_UTF8)
+    if (!dec && (c.type == DQ_UTF8 || c.type == DQ_BOOL || c.type < DQ_BOOL || c.type > DQ_UTF8))
       return fail(DQ_ERR_WRONG_TYPE, "ApproxQuantile needs a numeric column");
     if (b && c.type != batches[0].type) return fail(DQ_ERR_WRONG_TYPE, "batches differ in type");
     if (c.length < 0 || (c.length > 0 && !c.values))
@@ -721,6 +734,27 @@ extern "C" dq_status dq_sorted_sample(int device, const dq_column* batches, int 
   *n_out = 0;
   *count_out = 0;
   if (rows == 0) return DQ_OK;
+  // a decimal column enters as its values cast to double (StatefulApproxQuantile's DoubleType
+  // input: Decimal.toDouble, correctly rounded, decimal.h), one device buffer per batch
+  std::vector<dq_column> as_f64;
+  std::vector<std::unique_ptr<DevBuf<double>>> f64_bufs;
+  if (dec) {
+    for (int b = 0; b < n_batches; ++b) {
+      dq_column c = batches[b];
+      f64_bufs.emplace_back(new DevBuf<double>());
+      HIP_TRY(f64_bufs.back()->ensure((size_t)std::max<int64_t>(1, c.length)));
+      if (c.length) {
+        hipLaunchKernelGGL(dec_to_f64_kernel, dim3((unsigned)std::min<int64_t>((c.length + 255) / 256, 4096)),
+                           dim3(256), 0, stream, static_cast<const uint64_t*>(c.values),
+                           f64_bufs.back()->p, c.length, DQ_DECIMAL_SCALE(c.type));
+        HIP_TRY(hipGetLastError());
+      }
+      c.type = DQ_FLOAT64;
+      c.values = f64_bufs.back()->p;
+      as_f64.push_back(c);
+    }
+    batches = as_f64.data();
+  }
   // pass 0 over the columns: the count and the keys' top bits (through the engine's device cache:
   // buffers reused across columns, released on OOM)
   Source col;

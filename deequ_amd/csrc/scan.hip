@@ -574,11 +574,21 @@ DQ_DEV void dtype_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& a
     for (int q = 0; q < 5; ++q) acc.i[q] = c[q];
     return;
   }
+  const int tid = DQ_TYPE_ID(t.type);
   for (int64_t r = r_begin + lane_id(); r < r_end; r += 64) {
     const uint32_t w = t.w_val ? bit1(t.w_val, r) & bit1(t.w_vld, r) : 1u;
     int k;
     if (!w || !bit1(t.valid, r)) {
       k = DT_NULL;
+    } else if (tid == DQ_DATE32 || tid == DQ_TIMESTAMP_US) {
+      k = DT_STRING;  // "yyyy-MM-dd[ HH:mm:ss...]" matches none of the three patterns
+    } else if (tid == DQ_DECIMAL128) {
+      // BigDecimal.toString: an integer at scale 0, plain "d.ddd" while the adjusted exponent is
+      // >= -6, else "d.dddE-n" (which no pattern matches)
+      const uint64_t* v = reinterpret_cast<const uint64_t*>(t.values) + 2 * r;
+      const int sc = DQ_DECIMAL_SCALE(t.type);
+      k = sc == 0 ? DT_INTEGRAL
+                  : (dec_adjusted(v[0], (int64_t)v[1], sc) >= -6 ? DT_FRACTIONAL : DT_STRING);
     } else if (t.type == DQ_UTF8) {
       const int32_t s = off[r];
       k = dtype_of_string(t.data + s, off[r + 1] - s);
@@ -596,6 +606,80 @@ DQ_DEV void dtype_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& a
   }
 #pragma unroll
   for (int q = 0; q < 5; ++q) acc.i[q] = c[q];
+}
+
+// ------------------------------------------------------------------------------------------------
+// TK_DECIMAL: one decimal(p, s) column, 16 bytes per row.  Lane l takes row r0 + 64 k + l of each
+// 256-row step (every wave-instruction reads one contiguous 1 KiB of values): n, the exact 192-bit
+// sum of the unscaled values (Spark's decimal Sum before its result-type check), the 128-bit Min /
+// Max in the column's own order, and the moments of the values cast to double
+// (CentralMomentAgg's DoubleType input: Decimal.toDouble, correctly rounded, dec_to_double) --
+// a lane's 4 rows two-pass, then one Chan merge.
+// ------------------------------------------------------------------------------------------------
+DQ_DEV void dec_item(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& acc) {
+  const int scale = DQ_DECIMAL_SCALE(t.type);
+  const uint4* v = reinterpret_cast<const uint4*>(t.values);
+  const int l = lane_id();
+  int64_t n = 0;
+  int64_t s[3] = {0, 0, 0};
+  int64_t mnlo = -1, mnhi = INT64_MAX, mxlo = 0, mxhi = INT64_MIN;
+  double mean = 0.0, m2 = 0.0;
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += 256) {
+    double x[4];
+    uint32_t sel = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t r = r0 + 64 * k + l;
+      x[k] = 0.0;
+      if (r >= r_end) continue;
+      uint32_t ok = bit1(t.valid, r);
+      if (t.w_val) ok &= bit1(t.w_val, r) & bit1(t.w_vld, r);
+      if (!ok) continue;
+      const uint4 q = v[r];
+      const uint64_t lo = (uint64_t)q.x | ((uint64_t)q.y << 32);
+      const int64_t hi = (int64_t)((uint64_t)q.z | ((uint64_t)q.w << 32));
+      add192(s, lo, hi);
+      if (i128_lt((int64_t)lo, hi, mnlo, mnhi)) {
+        mnlo = (int64_t)lo;
+        mnhi = hi;
+      }
+      if (i128_lt(mxlo, mxhi, (int64_t)lo, hi)) {
+        mxlo = (int64_t)lo;
+        mxhi = hi;
+      }
+      x[k] = dec_to_double(lo, hi, scale);
+      sel |= 1u << k;
+    }
+    const int nb = __popc(sel);
+    if (!nb) continue;
+    double sum = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sum += x[k];
+    const double mb = sum / (double)nb;
+    double m2b = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double d = x[k] - mb;
+      m2b += ((sel >> k) & 1u) ? d * d : 0.0;
+    }
+    if (n == 0) {
+      mean = mb;
+      m2 = m2b;
+    } else {
+      moments_merge((double)n, mean, m2, (double)nb, mb, m2b);
+    }
+    n += nb;
+  }
+  acc.i[0] = n;
+  acc.i[1] = s[0];
+  acc.i[2] = s[1];
+  acc.i[3] = s[2];
+  acc.i[4] = mnlo;
+  acc.i[5] = mnhi;
+  acc.i[6] = mxlo;
+  acc.i[7] = mxhi;
+  acc.d[1] = mean;
+  acc.d[2] = m2;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1003,6 +1087,7 @@ __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? (K == 8 ? 4 : 5) 
     if constexpr (BC == BC_STR_IN) str_in_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_DTYPE) dtype_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_CORR) corr_item(t, r_begin, r_end, a);
+    if constexpr (BC == BC_DECIMAL) dec_item(t, r_begin, r_end, a);
     if constexpr (BC == BC_CORR_HLL) corr_rows<true, K>(t, r_begin, r_end, a, hll_lds + t.hll_out * kHllM);
     if constexpr (BC == BC_HLL) {
       hll_item(t, r_begin, r_end, hll_lds + t.hll_out * kHllM);
@@ -1011,6 +1096,7 @@ __global__ void __launch_bounds__(kBlock, (BC == BC_CORR_HLL ? (K == 8 ? 4 : 5) 
                            : BC == BC_BITS  ? TK_VALIDITY
                            : BC == BC_DTYPE ? TK_DTYPE
                            : BC == BC_CORR || BC == BC_CORR_HLL ? TK_COMOMENTS
+                           : BC == BC_DECIMAL ? TK_DECIMAL
                                             : TK_STR_IN;
       wave_reduce(kind, a);
       if (l == 0) partial[item] = a;
@@ -1299,6 +1385,7 @@ hipError_t launch_scan(const TaskDesc* tasks, int n_desc, int n_tasks, const Sca
       case BC_CORR: launch_body<BC_CORR>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       case BC_HLL: launch_body<BC_HLL>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       case BC_CORR_HLL: launch_body<BC_CORR_HLL>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
+      case BC_DECIMAL: launch_body<BC_DECIMAL>(L, tasks, n_desc, n_hll, queues, partial, hll_stage, stream); break;
       default: return hipErrorInvalidValue;
     }
     hipError_t e = hipGetLastError();
@@ -1323,6 +1410,7 @@ int scan_max_blocks_per_cu(int body, int n_hll) {
     case BC_CORR: return occupancy_of<BC_CORR>(n_hll);
     case BC_HLL: return occupancy_of<BC_HLL>(n_hll);
     case BC_CORR_HLL: return occupancy_of<BC_CORR_HLL>(n_hll);
+    case BC_DECIMAL: return occupancy_of<BC_DECIMAL>(n_hll);
     case kBodyMixed: {
       int n = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scan_mixed_kernel<kMixedAll>, kBlock,

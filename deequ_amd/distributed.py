@@ -92,43 +92,82 @@ def merge_states_across_ranks(plan, state, device=None):
     return merge_serialized(plan, images)
 
 
+_XCHG_BUFS: dict = {}
+
+
+def _exchange_buffers(plan, home, cdev, world: int):
+    """The exchange's buffers for (plan, device, world), allocated once and reused every step:
+    isum / imax (int64), mom (fp64), hll (uint8) on the state's side, their collective-side
+    copies (the same tensors when the collectives run on the state's device) and the gathered
+    moments."""
+    import torch
+    key = (id(plan), str(home), str(cdev), world)
+    hit = _XCHG_BUFS.get(key)
+    if hit is not None and hit["plan"] is plan:
+        return hit
+    ns, nm, nd, nh = (ctypes.c_int64() for _ in range(4))
+    N.check(N.lib.dq_state_exchange_sizes(plan.handle, ctypes.byref(ns), ctypes.byref(nm),
+                                          ctypes.byref(nd), ctypes.byref(nh)))
+    b = {"plan": plan, "nd": nd.value, "nh": nh.value,
+         "isum": torch.empty(ns.value, dtype=torch.int64, device=home),
+         "imax": torch.empty(max(1, nm.value), dtype=torch.int64, device=home),
+         "mom": torch.empty(max(1, nd.value), dtype=torch.float64, device=home),
+         "hll": torch.empty(max(1, nh.value), dtype=torch.uint8, device=home)}
+    same = str(home) == str(cdev)
+    for k in ("isum", "imax", "mom", "hll"):
+        b[k + "_c"] = b[k] if same else torch.empty_like(b[k], device=cdev)
+    b["gathered_c"] = torch.empty(max(1, world * nd.value), dtype=torch.float64, device=cdev)
+    b["gathered"] = b["gathered_c"] if same else torch.empty_like(b["gathered_c"], device=home)
+    b["nm"] = nm.value
+    _XCHG_BUFS[key] = b
+    return b
+
+
 def exchange_states(plan, state, device=None):
     """All ranks: the scan states merged on the device, as north_star states them -- counters and
-    wrapping Long sums by ONE all-reduce SUM, extremes and HLL registers by ONE all-reduce MAX (min
-    keys travel bitwise-NOT), the fp64 moments by ONE all-gather merged in rank order by a kernel
-    (dq_state_exchange_pack / _unpack).  No host merge: the one read-back is the merged state's
-    (dq_state_sync).  Equal, byte for byte, to merge_states_across_ranks (the rank-ordered
-    dq_state_merge of the serialized states, kept as the check).  `device` None: a host-only state
-    (device -1; the CPU tests), collectives over gloo on host tensors.  Returns the result row."""
+    wrapping Long sums by ONE all-reduce SUM, extremes by ONE all-reduce MAX (min keys travel
+    bitwise-NOT), the HLL registers as uint8 by ONE all-reduce MAX, the fp64 moments (and a decimal
+    task's exact words) by ONE all-gather merged in rank order by a kernel
+    (dq_state_exchange_pack / _unpack).  No host merge and no host wait but the merged state's
+    read-back (dq_state_sync); the buffers are reused across steps (_exchange_buffers).  Equal,
+    byte for byte, to merge_states_across_ranks (the rank-ordered dq_state_merge of the serialized
+    states, kept as the check).  `device` None: a host-only state (device -1; the CPU tests),
+    collectives over gloo on host tensors.  Returns the result row."""
     import torch
     import torch.distributed as dist
     from .runners.engine import read_row
     world = dist.get_world_size()
-    ns, nm, nd = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-    N.check(N.lib.dq_state_exchange_sizes(plan.handle, ctypes.byref(ns), ctypes.byref(nm),
-                                          ctypes.byref(nd)))
     home = torch.device(device) if device is not None else torch.device("cpu")
-    cdev = _comm_device(home) if device is not None else "cpu"
-    isum = torch.empty(ns.value, dtype=torch.int64, device=home)
-    imax = torch.empty(nm.value, dtype=torch.int64, device=home)
-    mom = torch.empty(max(1, nd.value), dtype=torch.float64, device=home)
+    cdev = _comm_device(home) if device is not None else torch.device("cpu")
+    b = _exchange_buffers(plan, home, cdev, world)
+    nd, nh, nm = b["nd"], b["nh"], b["nm"]
     stream = (ctypes.c_void_p(torch.cuda.current_stream(home).cuda_stream)
               if home.type == "cuda" else None)
-    N.check(N.lib.dq_state_exchange_pack(state, isum.data_ptr(), imax.data_ptr(), mom.data_ptr(),
-                                         stream))
-    isum_c, imax_c, mom_c = isum.to(cdev), imax.to(cdev), mom[: nd.value].to(cdev)
-    dist.all_reduce(isum_c, op=dist.ReduceOp.SUM)
-    dist.all_reduce(imax_c, op=dist.ReduceOp.MAX)
-    gathered = torch.empty(world * nd.value, dtype=torch.float64, device=cdev)
-    if nd.value:
-        dist.all_gather_into_tensor(gathered, mom_c)
-    _count_reduce(isum_c)
-    _count_reduce(imax_c)
-    _count_gather(nd.value * 8, world)
-    isum, imax = isum_c.to(home), imax_c.to(home)
-    gathered = gathered.to(home) if nd.value else mom
-    N.check(N.lib.dq_state_exchange_unpack(state, isum.data_ptr(), imax.data_ptr(),
-                                           gathered.data_ptr(), world, stream))
+    N.check(N.lib.dq_state_exchange_pack(state, b["isum"].data_ptr(), b["imax"].data_ptr(),
+                                         b["mom"].data_ptr(), b["hll"].data_ptr(), stream))
+    if b["isum_c"] is not b["isum"]:
+        for k in ("isum", "imax", "mom", "hll"):
+            b[k + "_c"].copy_(b[k])
+    dist.all_reduce(b["isum_c"], op=dist.ReduceOp.SUM)
+    if nm:
+        dist.all_reduce(b["imax_c"], op=dist.ReduceOp.MAX)
+    if nh:
+        dist.all_reduce(b["hll_c"], op=dist.ReduceOp.MAX)
+    if nd:
+        dist.all_gather_into_tensor(b["gathered_c"][: world * nd], b["mom_c"][:nd])
+    _count_reduce(b["isum_c"])
+    if nm:
+        _count_reduce(b["imax_c"])
+    if nh:
+        _count_reduce(b["hll_c"])
+    _count_gather(nd * 8, world)
+    if b["isum_c"] is not b["isum"]:
+        for k in ("isum", "imax", "hll"):
+            b[k].copy_(b[k + "_c"])
+        b["gathered"].copy_(b["gathered_c"])
+    N.check(N.lib.dq_state_exchange_unpack(state, b["isum"].data_ptr(), b["imax"].data_ptr(),
+                                           b["gathered"].data_ptr(), b["hll"].data_ptr(), world,
+                                           stream))
     N.check(N.lib.dq_state_sync(state))
     return read_row(plan, state)
 
@@ -374,7 +413,8 @@ def is_distributed(data=None) -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
 
-RAW_KEY_ELEM = {N.INT8: 1, N.INT16: 2, N.INT32: 4, N.INT64: 8, N.FLOAT32: 4, N.FLOAT64: 8}
+RAW_KEY_ELEM = {N.INT8: 1, N.INT16: 2, N.INT32: 4, N.INT64: 8, N.FLOAT32: 4, N.FLOAT64: 8,
+                N.DATE32: 4, N.TIMESTAMP_US: 8}  # (a date / timestamp key: its int32 / int64)
 RAW_SAMPLE_ROWS = 1 << 20
 RAW_MIN_DISTINCT = 0.5  # sampled groups per non-NULL row at or above which raw keys travel
 

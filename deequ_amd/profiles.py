@@ -95,15 +95,21 @@ class _GenericStatistics:
         return merged[column]
 
 
-def _known_type(dtype: int) -> DataTypeInstances:
-    # ShortType | LongType | IntegerType -> Integral; FloatType | DoubleType -> Fractional;
-    # BooleanType -> Boolean; anything else (ByteType included) is "Unable to map" -> Unknown
+def _known_type(dtype: int, spark_name: str = "") -> DataTypeInstances:
+    # ColumnProfiler.scala:374-381: ShortType | LongType | IntegerType -> Integral;
+    # DecimalType() | FloatType | DoubleType -> Fractional; BooleanType -> Boolean;
+    # TimestampType -> String; anything else (ByteType, DateType, BinaryType ...) is
+    # "Unable to map" -> Unknown
+    if spark_name == "BinaryType":
+        return DataTypeInstances.Unknown
     if dtype in (N.INT16, N.INT32, N.INT64):
         return DataTypeInstances.Integral
-    if dtype in (N.FLOAT32, N.FLOAT64):
+    if dtype in (N.FLOAT32, N.FLOAT64) or N.is_decimal(dtype):
         return DataTypeInstances.Fractional
     if dtype == N.BOOL:
         return DataTypeInstances.Boolean
+    if dtype == N.TIMESTAMP_US:
+        return DataTypeInstances.String
     return DataTypeInstances.Unknown
 
 
@@ -132,7 +138,7 @@ class ColumnProfiler:
             if columns and f.name not in columns:
                 continue
             first += [Completeness(f.name), ApproxCountDistinct(f.name)]
-            if f.dtype == N.UTF8:
+            if f.type_name == "StringType":
                 first.append(DataType(f.name))
         builder = AnalysisRunBuilder(data).add_analyzers(first).add_analyzer(Size())
         first_results = _with_repository(builder, *repo).run()
@@ -214,8 +220,8 @@ def _extract_generic_statistics(columns, schema, results) -> _GenericStatistics:
                 distincts[a.column] = int(m.value.get())  # Double.toLong truncates
         elif isinstance(a, Completeness):
             compl[a.column] = m.value.get()
-    known = {f.name: _known_type(f.dtype) for f in schema.fields
-             if f.name in columns and f.dtype != N.UTF8}
+    known = {f.name: _known_type(f.dtype, f.type_name) for f in schema.fields
+             if f.name in columns and f.type_name != "StringType"}
     return _GenericStatistics(num_records, inferred, known, hists, distincts, compl)
 
 
@@ -250,7 +256,7 @@ def _cast_column(data, name: str, to_type: int):
 def _cast_numeric_string_columns(columns, data, generic):
     out = data
     for name in columns:
-        if data.schema[name].dtype != N.UTF8:
+        if data.schema[name].type_name != "StringType":
             continue  # a cast of a numeric column to long / double leaves every metric unchanged
         t = generic.type_of(name)
         if t == DataTypeInstances.Integral:
@@ -290,7 +296,7 @@ def _target_columns_for_histograms(schema, generic, threshold) -> List[str]:
     are missing, HllBiasTablesUnavailableException), but there linear counting already puts it
     above LINEAR_COUNTING_FLOOR distinct values: it is not a target for any threshold below that,
     and a larger threshold cannot be decided without the tables (raised, never guessed)."""
-    strings = {f.name for f in schema.fields if f.dtype == N.UTF8}
+    strings = {f.name for f in schema.fields if f.type_name == "StringType"}
     out = []
     for c, n in generic.approximate_num_distincts.items():
         if c not in strings or generic.type_of(c) != DataTypeInstances.String:

@@ -13,7 +13,7 @@ from typing import Dict, List, Sequence, Tuple
 
 from .. import _native as N
 from ..analyzers.base import AggSpec
-from ..exceptions import AnalysisException
+from ..exceptions import AnalysisException, WrongColumnTypeException
 from ..sqlexpr import SqlError, compile_expr
 
 
@@ -23,7 +23,7 @@ class Plan:
     def __init__(self, schema, specs: Sequence[AggSpec]):
         self.schema = schema
         self.specs = list(specs)
-        self.types = [f.dtype for f in schema.fields]
+        self.types = [f.engine_type for f in schema.fields]
         names = schema.field_names
 
         def col_index(name: str) -> int:
@@ -47,8 +47,19 @@ class Plan:
             expr_words.append(compiled.words)
             return len(expr_sql) - 1
 
+        def readable(name: str, kind: int) -> None:
+            """An UNSUPPORTED column reaches the device as its validity bitmap only: a
+            Completeness numerator reads nothing else; anything more is refused here."""
+            f = schema[schema.resolve(name) or name] if schema.resolve(name) else None
+            if f is not None and f.dtype == N.UNSUPPORTED and kind != N.AGG_COUNT_NOTNULL:
+                raise WrongColumnTypeException(
+                    f"Column {f.name} has type {f.type_name}, which the engine does not read")
+
         aggs = []
         for s in self.specs:
+            for c in (s.col, s.col2):
+                if c is not None:
+                    readable(c, s.kind)
             a = N.dq_agg()
             a.kind = s.kind
             a.col = col_index(s.col) if s.col is not None else -1

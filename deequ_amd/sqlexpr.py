@@ -80,6 +80,10 @@ class Node:
     name: Optional[str] = None   # column name / comparison symbol / cast type
     value: object = None         # literal value
     ltype: Optional[str] = None  # literal type: int, float, str, bool, null
+    # numeric literals: the exact value (int or decimal.Decimal) and whether Spark 2.2 types it
+    # DoubleType (a D suffix; every other fractional / exponent literal is a DecimalType literal)
+    exact: object = None
+    dbl: bool = False
 
 
 _KW = {"AND", "OR", "NOT", "IS", "NULL", "IN", "TRUE", "FALSE", "BETWEEN", "CAST", "AS", "RLIKE"}
@@ -211,6 +215,7 @@ class _Parser:
                 raise SqlError("unary minus only supported on numeric literals")
             if t.text == "-":
                 inner.value = -inner.value
+                inner.exact = -inner.exact if inner.exact is not None else None
             return inner
         if t.kind == "num":
             return _num_literal(t.text)
@@ -258,9 +263,10 @@ def _num_literal(text: str) -> Node:
     m = re.match(r"^((?:\d+\.\d*|\.\d+|\d+)(?:[eE][+-]?\d+)?)([A-Za-z]*)$", text)
     body, suffix = m.group(1), m.group(2).upper()
     if suffix in ("D", "BD") or any(c in body for c in ".eE"):
-        return Node("lit", value=float(body), ltype="float")
+        from decimal import Decimal
+        return Node("lit", value=float(body), ltype="float", exact=Decimal(body), dbl=suffix == "D")
     if suffix in ("", "L", "S", "Y"):
-        return Node("lit", value=int(body), ltype="int")
+        return Node("lit", value=int(body), ltype="int", exact=int(body))
     raise SqlError(f"bad numeric literal {text}")
 
 
@@ -282,7 +288,34 @@ def _kind_of_type(t: int) -> str:
         return "bool"
     if t in N.INTEGRAL_TYPES:
         return "int"
+    if N.is_decimal(t):
+        return "dec"
+    if t == N.DATE32:
+        return "date"
+    if t == N.TIMESTAMP_US:
+        return "ts"
+    if t == N.UNSUPPORTED:
+        raise SqlError("a column of a type the engine does not read appears in an expression")
     return "float"
+
+
+_DEC_LIMIT = 10 ** 38  # |unscaled| of any decimal(38) value is below it
+
+
+def _dec128_words(v: int) -> List[int]:
+    """An unscaled value (clamped to +-10^38: still on the right side of every column value) as
+    the [X_DEC128, lo, hi] words (signed int64 each)."""
+    v = max(-_DEC_LIMIT, min(_DEC_LIMIT, v)) & ((1 << 128) - 1)
+    lo, hi = v & 0xFFFFFFFFFFFFFFFF, v >> 64
+    sg = lambda x: x - (1 << 64) if x >= (1 << 63) else x  # noqa: E731
+    return [N.X_DEC128, sg(lo), sg(hi)]
+
+
+def _exact_literal(n: "Node"):
+    """The exact value of an int / decimal literal (None for a double literal or a non-number)."""
+    if n.op != "lit" or n.ltype not in ("int", "float") or n.dbl or n.exact is None:
+        return None
+    return n.exact
 
 
 class _Emitter:
@@ -314,8 +347,8 @@ class _Emitter:
             w += [N.X_COL, self.col_index(n.name)]
             if n.name not in self.columns:
                 self.columns.append(n.name)
-            if want == "float" and self.type_of(n) == "str":
-                w.insert(len(w) - 2, N.X_CAST_F64)
+            if want == "float" and self.type_of(n) in ("str", "dec"):
+                w.insert(len(w) - 2, N.X_CAST_F64)  # (a decimal: Decimal.toDouble)
             return
         if n.op == "lit":
             v, t = n.value, n.ltype
@@ -366,6 +399,12 @@ class _Emitter:
         if n.op == "cmp":
             a, b = n.kids
             ta, tb = self.type_of(a), self.type_of(b)
+            if "dec" in (ta, tb) and self._emit_dec_cmp(n.name, a, ta, b, tb):
+                return
+            for t in (ta, tb):
+                if t in ("date", "ts"):
+                    raise SqlError("comparisons of date / timestamp columns are not supported by "
+                                   "the engine")
             target = _common_cmp_type(ta, tb)
             w.append(_CMP[n.name])
             self.emit(a, target)
@@ -375,6 +414,12 @@ class _Emitter:
             x, items = n.kids[0], n.kids[1:]
             tx = self.type_of(x)
             tis = [self.type_of(i) for i in items]
+            if tx == "dec":
+                self._emit_dec_in(x, items)
+                return
+            if tx in ("date", "ts") or any(t in ("dec", "date", "ts") for t in tis):
+                raise SqlError("IN over a date / timestamp / decimal value is not supported by the "
+                               "engine")
             target = tx
             if any(t not in (tx, "null") for t in tis):
                 kinds = {tx} | {t for t in tis if t != "null"}
@@ -393,7 +438,7 @@ class _Emitter:
             tx = self.type_of(n.kids[0])
             # a non-string operand is matched as Spark's cast to string: decimal integers,
             # true / false, Double.toString / Float.toString (csrc/jfmt.h, on the device)
-            if tx not in ("str", "int", "float", "bool", "null"):
+            if tx not in ("str", "int", "float", "bool", "null", "dec", "date", "ts"):
                 raise SqlError(f"cannot match a regex against a {tx} value")
             blob = _compiled_regex(n.value, n.name == "rlike")
             w += [N.X_REGEX, 1 if n.name == "nonempty" else 0, len(blob)]
@@ -402,6 +447,65 @@ class _Emitter:
             self.emit(n.kids[0])
             return
         raise SqlError(f"unsupported expression node {n.op}")
+
+    # -- decimal columns (Spark 2.2 DecimalPrecision: exact against integral / decimal literals,
+    #    through Cast(AS DOUBLE) against doubles)
+    def _scale_of(self, n: Node) -> int:
+        return N.decimal_scale(self.schema[self.schema.resolve(n.name)].dtype)
+
+    def _emit_dec_cmp(self, sym: str, a: Node, ta: str, b: Node, tb: str) -> bool:
+        """Emits a comparison with a decimal column operand; False when it is not one of the forms
+        handled here (the generic path then raises or casts)."""
+        if ta == "dec" and tb == "dec":
+            raise SqlError("comparisons of two decimal values are not supported by the engine")
+        col, lit, op = (a, b, sym) if ta == "dec" else (b, a, _FLIP.get(sym, sym))
+        tl = tb if ta == "dec" else ta
+        if tl in ("float", "str") and _exact_literal(lit) is None:
+            return False  # double / string: both sides as double (Cast(decimal AS DOUBLE))
+        if tl == "null":
+            self.words.append(_CMP[sym])
+            self.emit(a)
+            self.emit(b)
+            return True
+        exact = _exact_literal(lit)
+        if exact is None:
+            raise SqlError("a decimal column compared with a non-literal value is not supported by "
+                           "the engine")
+        from fractions import Fraction
+        t = Fraction(exact) * 10 ** self._scale_of(col)
+        if t.denominator == 1:
+            op, v = op, int(t)
+        elif op in ("<", "<="):  # x < t  <=>  x <= floor(t)  (x an integer)
+            op, v = "<=", t.numerator // t.denominator
+        elif op in (">", ">="):
+            op, v = ">=", -((-t.numerator) // t.denominator)
+        else:  # =, <>, <=> against a value no column value equals
+            v = _DEC_LIMIT
+        self.words.append(_CMP[op])
+        self.emit(col)
+        self.words.extend(_dec128_words(v))
+        return True
+
+    def _emit_dec_in(self, x: Node, items: List[Node]) -> None:
+        from fractions import Fraction
+        sc = self._scale_of(x)
+        words = []
+        for it in items:
+            if self.type_of(it) == "null":
+                words.append(N.X_NULL)
+                continue
+            exact = _exact_literal(it)
+            if exact is None:
+                raise SqlError("a decimal column IN a list of non-literal / double items is not "
+                               "supported by the engine")
+            t = Fraction(exact) * 10 ** sc
+            words.extend(_dec128_words(int(t) if t.denominator == 1 else _DEC_LIMIT))
+        self.words += [N.X_IN, len(items)]
+        self.emit(x)
+        self.words.extend(words)
+
+
+_FLIP = {"<": ">", "<=": ">=", ">": "<", ">=": "<="}
 
 
 _REGEX_CACHE = {}
@@ -426,6 +530,8 @@ def _compiled_regex(pattern: str, any_match: bool) -> bytes:
 def _common_cmp_type(ta: str, tb: str) -> Optional[str]:
     if ta == "null" or tb == "null":
         return None
+    if "dec" in (ta, tb) and ({ta, tb} - {"dec"}) <= {"float", "str"}:
+        return "float"  # decimal vs double (or a string cast to double): Cast(decimal AS DOUBLE)
     if ta == tb:
         return ta if ta != "int" else None
     if {ta, tb} <= {"int", "float"}:

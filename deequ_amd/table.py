@@ -19,19 +19,54 @@ from . import _native as N
 _ARROW_TO_DQ = {
     "bool": N.BOOL, "int8": N.INT8, "int16": N.INT16, "int32": N.INT32, "int64": N.INT64,
     "float": N.FLOAT32, "double": N.FLOAT64, "string": N.UTF8, "large_string": N.UTF8,
+    "binary": N.UTF8, "large_binary": N.UTF8, "date32[day]": N.DATE32,
 }
 _NP_OF = {N.INT8: np.int8, N.INT16: np.int16, N.INT32: np.int32, N.INT64: np.int64,
-          N.FLOAT32: np.float32, N.FLOAT64: np.float64}
+          N.FLOAT32: np.float32, N.FLOAT64: np.float64, N.DATE32: np.int32,
+          N.TIMESTAMP_US: np.int64}
+
+
+def arrow_field_type(t):
+    """(dq type word, Spark type name override or None, the Arrow type the column is imported as)
+    of an Arrow type.  Spark's types map onto the engine's: binary is read as its bytes (hashed,
+    grouped and matched exactly like a string, Spark's BinaryType), date64 as date32 days, a
+    timestamp of any unit / zone as UTC microseconds (Spark's TimestampType), decimal128(p, s) as
+    itself.  Anything else (lists, structs, maps, decimal256, ...) is UNSUPPORTED: only its validity
+    bitmap reaches the device."""
+    import pyarrow as pa
+    key = str(t)
+    if key in ("binary", "large_binary"):
+        return N.UTF8, "BinaryType", pa.binary()
+    if key in _ARROW_TO_DQ:
+        return _ARROW_TO_DQ[key], None, t
+    if pa.types.is_date64(t):
+        return N.DATE32, None, pa.date32()
+    if pa.types.is_timestamp(t):
+        return N.TIMESTAMP_US, None, pa.timestamp("us", tz=t.tz)
+    if pa.types.is_decimal128(t) and 1 <= t.precision <= 38 and 0 <= t.scale <= t.precision:
+        return N.decimal_type(t.precision, t.scale), None, t
+    return N.UNSUPPORTED, None, t
 
 
 @dataclass
 class StructField:
     name: str
-    dtype: int  # dq type code
+    dtype: int  # dq type word (N.UNSUPPORTED: an Arrow type the engine does not read)
+    spark_name: Optional[str] = None  # Spark's type name when the type word does not say it
+    arrow_type: Optional[str] = None  # the Arrow type of an UNSUPPORTED column
 
     @property
     def type_name(self) -> str:
-        return N.TYPE_NAMES[self.dtype]
+        if self.spark_name:
+            return self.spark_name
+        if self.dtype == N.UNSUPPORTED:
+            return f"UnsupportedType({self.arrow_type})"
+        return N.type_name(self.dtype)
+
+    @property
+    def engine_type(self) -> int:
+        """The type word the engine's plan sees (an UNSUPPORTED column: a validity-only stand-in)."""
+        return N.INT8 if self.dtype == N.UNSUPPORTED else self.dtype
 
 
 @dataclass
@@ -69,6 +104,7 @@ class ColumnBatch:
     values: object              # torch tensor (values / bit-packed bools / int32 offsets)
     data: Optional[object] = None  # torch.uint8 tensor (utf8 bytes)
     null_count: int = 0
+    stand_in: bool = False  # an UNSUPPORTED column: validity only, `values` a 16-byte stand-in
 
     def to_c(self) -> N.dq_column:
         c = N.dq_column()
@@ -145,17 +181,19 @@ class Table:
             batches = data.to_batches(max_chunksize=max_batch_rows)
         else:
             batches = data.combine_chunks().to_batches() if data.num_rows else []
-        fields = []
+        fields, casts = [], []
         for f in data.schema:
-            key = str(f.type)
-            if key not in _ARROW_TO_DQ:
-                raise TypeError(f"unsupported Arrow type {f.type} for column {f.name}")
-            fields.append(StructField(f.name, _ARROW_TO_DQ[key]))
+            dtype, spark_name, as_type = arrow_field_type(f.type)
+            fields.append(StructField(f.name, dtype, spark_name,
+                                      str(f.type) if dtype == N.UNSUPPORTED else None))
+            casts.append(as_type if dtype != N.UNSUPPORTED and as_type != f.type else None)
         schema = StructType(fields)
         out = []
         for rb in batches:
             cols = {}
-            for f, arr in zip(fields, rb.columns):
+            for f, arr, cast in zip(fields, rb.columns, casts):
+                if cast is not None:  # (exact: a cast that would drop digits raises)
+                    arr = arr.cast(cast)
                 cols[f.name] = _array_to_device(arr, f.dtype, device)
             out.append(cols)
         if not out:
@@ -166,12 +204,15 @@ class Table:
     def from_pydict(columns: Dict[str, Sequence], types: Optional[Dict[str, str]] = None,
                     device: str = "cuda:0") -> "Table":
         """Test helper: python lists (None = NULL) -> device table.  ``types`` maps a column to an
-        Arrow type name ("int64", "double", "string", ...)."""
+        Arrow type name ("int64", "double", "string", ...) or a pyarrow DataType
+        (pa.decimal128(38, 18), pa.timestamp("us"), ...)."""
         import pyarrow as pa
         arrays, names = [], []
         for name, vals in columns.items():
             t = (types or {}).get(name)
-            arrays.append(pa.array(list(vals), type=getattr(pa, t)() if t else None))
+            if isinstance(t, str):
+                t = getattr(pa, t)()
+            arrays.append(pa.array(list(vals), type=t))
             names.append(name)
         return Table.from_arrow(pa.Table.from_arrays(arrays, names=names), device=device)
 
@@ -183,14 +224,18 @@ def _slice_column(c: ColumnBatch, lo: int, hi: int) -> ColumnBatch:
                          f"of 8 rows (bitmap views are byte-addressed)")
     m = hi - lo
     validity = c.validity[lo // 8:] if c.validity is not None else None
-    if c.dtype == N.BOOL:
+    if c.stand_in:
+        values = c.values
+    elif N.is_decimal(c.dtype):
+        values = c.values[2 * lo:]  # two uint64 words per row
+    elif c.dtype == N.BOOL:
         values = c.values[lo // 8:]
     elif c.dtype == N.UTF8:
         values = c.values[lo:]  # absolute offsets into the same character buffer
     else:
         values = c.values[lo:]
     # null_count of a view is not recounted (it stays informational: the bitmap is the truth)
-    return ColumnBatch(c.dtype, m, validity, values, c.data, 0)
+    return ColumnBatch(c.dtype, m, validity, values, c.data, 0, c.stand_in)
 
 
 def _to_device(np_buf: np.ndarray, device: str):
@@ -200,6 +245,9 @@ def _to_device(np_buf: np.ndarray, device: str):
 
 
 def _empty_column(dtype: int, device: str) -> ColumnBatch:
+    if dtype == N.UNSUPPORTED:
+        return ColumnBatch(N.INT8, 0, None, _to_device(np.zeros(16, np.uint8), device),
+                           stand_in=True)
     if dtype == N.UTF8:
         return ColumnBatch(dtype, 0, None, _to_device(np.zeros(1, np.int32), device),
                            _to_device(np.zeros(16, np.uint8), device))
@@ -228,6 +276,11 @@ def array_to_host(arr, dtype: int):
     n = len(arr)
     bufs = arr.buffers()
     validity = _bits(bufs[0], arr.offset, n) if arr.null_count else None
+    if dtype == N.UNSUPPORTED:  # the validity bitmap alone; a stand-in values buffer
+        return validity, np.zeros(16, np.uint8), None
+    if N.is_decimal(dtype):  # 16-byte little-endian unscaled values, as two uint64 words each
+        vals = np.frombuffer(bufs[1], dtype="<u8")[2 * arr.offset: 2 * (arr.offset + n)]
+        return validity, np.concatenate([vals, np.zeros(2, np.uint64)]), None
     if dtype == N.BOOL:
         values = _bits(bufs[1], arr.offset, n)
         if values is None:
@@ -235,8 +288,8 @@ def array_to_host(arr, dtype: int):
         return validity, values, None
     if dtype == N.UTF8:
         import pyarrow as pa
-        if str(arr.type) == "large_string":
-            arr = arr.cast(pa.string())
+        if str(arr.type) in ("large_string", "large_binary"):
+            arr = arr.cast(pa.binary() if "binary" in str(arr.type) else pa.string())
             bufs = arr.buffers()
         offs = np.frombuffer(bufs[1], dtype=np.int32)[arr.offset: arr.offset + n + 1].astype(np.int64)
         base = int(offs[0]) if n else 0
@@ -255,6 +308,9 @@ def array_to_host(arr, dtype: int):
 
 def _array_to_device(arr, dtype: int, device: str) -> ColumnBatch:
     validity, values, data = array_to_host(arr, dtype)
-    return ColumnBatch(dtype, len(arr), _to_device(validity, device) if validity is not None else None,
+    stand_in = dtype == N.UNSUPPORTED
+    return ColumnBatch(N.INT8 if stand_in else dtype, len(arr),  # (StructField.engine_type)
+                       _to_device(validity, device) if validity is not None else None,
                        _to_device(values, device),
-                       _to_device(data, device) if data is not None else None, arr.null_count)
+                       _to_device(data, device) if data is not None else None, arr.null_count,
+                       stand_in)

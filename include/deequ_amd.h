@@ -66,11 +66,26 @@ typedef enum dq_type {
   DQ_INT64 = 5,   /* "l" */
   DQ_FLOAT32 = 6, /* "f" */
   DQ_FLOAT64 = 7, /* "g" */
-  DQ_UTF8 = 8     /* "u": int32 offsets (length+1) + bytes                           */
+  DQ_UTF8 = 8,    /* "u": int32 offsets (length+1) + bytes                           */
+  /* Spark DecimalType(p, s) (Analyzer.scala:277-278, 322-327 count it numeric): Arrow "d:p,s"
+   * (decimal128), 16-byte little-endian two's-complement unscaled values, 1 <= p <= 38,
+   * 0 <= s <= p.  The type word carries p and s: DQ_DECIMAL_TYPE(p, s).                     */
+  DQ_DECIMAL128 = 9,
+  DQ_DATE32 = 10,      /* Spark DateType, Arrow "tdD": int32 days since 1970-01-01           */
+  DQ_TIMESTAMP_US = 11 /* Spark TimestampType, Arrow "tsu:<tz>": int64 microseconds since
+                          1970-01-01T00:00:00Z (text forms use UTC as the session time zone)  */
 } dq_type;
 
+/* A column type word: the dq_type in bits 0-7; for DQ_DECIMAL128 the precision in bits 8-15 and
+ * the scale in bits 16-23 (a plan's column_types, dq_column.type and dq_freq key types all carry
+ * the full word, so two decimal columns of different precision or scale are different types). */
+#define DQ_TYPE_ID(t) ((int32_t)(t) & 0xff)
+#define DQ_DECIMAL_TYPE(p, s) ((int32_t)DQ_DECIMAL128 | ((int32_t)(p) << 8) | ((int32_t)(s) << 16))
+#define DQ_DECIMAL_PRECISION(t) (((int32_t)(t) >> 8) & 0xff)
+#define DQ_DECIMAL_SCALE(t) (((int32_t)(t) >> 16) & 0xff)
+
 typedef struct dq_column {
-  int32_t type;            /* dq_type                                                         */
+  int32_t type;            /* type word (dq_type, + precision / scale for DQ_DECIMAL128)     */
   int32_t data_bytes;      /* DQ_UTF8: optional size hint, >= offsets[length] - offsets[0] (the
                               group-by then sizes its key arena without reading the offsets
                               back); 0 = unknown.  Ignored for other types.                  */
@@ -164,11 +179,19 @@ typedef enum dq_xop {
                           string).  A NULL x gives NULL (null_mode 0, RLIKE) or FALSE
                           (null_mode 1: when(regexp_extract(x, p, 0) != "", 1).otherwise(0),
                           PatternMatch.scala:44-46).                                           */
-  DQ_X_CAST_F32 = 22   /* [op, x]  CAST(x AS FLOAT): an integral x rounds to the nearest float,
+  DQ_X_CAST_F32 = 22,  /* [op, x]  CAST(x AS FLOAT): an integral x rounds to the nearest float,
                           a double one too (Spark's Cast to FloatType, `.toFloat`); the value
                           then prints as Float.toString.  A string x (utf8 column or literal)
                           is refused by dq_plan_create with DQ_ERR_UNSUPPORTED:
                           Float.parseFloat's direct rounding is not restated.                  */
+  DQ_X_DEC128 = 23     /* [op, lo, hi]  decimal literal as an unscaled 128-bit value at the scale of
+                          the DQ_DECIMAL128 column it is compared with (the host rescales it, so
+                          the comparison is exact, as Spark's DecimalPrecision makes it).  A
+                          decimal column may appear under IS [NOT] NULL, in comparisons / IN with
+                          DQ_X_DEC128 items, under DQ_X_CAST_F64 (Decimal.toDouble, correctly
+                          rounded) and as a regex operand (BigDecimal.toString text); a date /
+                          timestamp column under IS [NOT] NULL and as a regex operand.  Any other
+                          use is refused by dq_plan_create with DQ_ERR_UNSUPPORTED.            */
 } dq_xop;
 
 typedef struct dq_expr {
@@ -249,9 +272,16 @@ dq_status dq_state_sync(dq_state* state);
 
 /* One typed aggregation result (one slot of the reference's result Row).
  *   COUNT_*  : i64 (is_null per Spark: a sum over no non-null input is NULL)
- *   SUM      : integral input: i64 = wrapping Long sum, f64[0] = (double)i64; floating: f64[0]
- *   MIN/MAX  : f64[0] (= cast of the native-typed extreme); i64 = the native integral extreme
- *   STDDEV   : f64[0..2] = n, avg, m2 (never NULL; n == 0 means no input)
+ *   SUM      : integral input: i64 = wrapping Long sum, f64[0] = (double)i64; floating: f64[0];
+ *              decimal(p, s): words[0..3] = the exact sum of the unscaled values (256-bit two's
+ *              complement, little-endian words), f64[0] = Cast(sum AS DOUBLE) correctly rounded;
+ *              is_null also when the sum does not fit Spark 2.2's result type
+ *              decimal(min(p + 10, 38), s) (Sum.scala:35 over Spark's Sum)
+ *   MIN/MAX  : f64[0] (= cast of the native-typed extreme); i64 = the native integral extreme;
+ *              decimal: words[0..1] = the unscaled 128-bit extreme, f64[0] its correctly rounded
+ *              cast
+ *   STDDEV   : f64[0..2] = n, avg, m2 (never NULL; n == 0 means no input); a decimal column's
+ *              values enter as their cast to double (CentralMomentAgg's DoubleType input)
  *   CORR     : f64[0..5] = n, xAvg, yAvg, ck, xMk, yMk
  *   HLL      : words[0..51] = the 52 register words in reference order (never NULL)      */
 typedef struct dq_value {
@@ -283,22 +313,30 @@ dq_status dq_state_deserialize(dq_state* state, const void* buf, int64_t buf_len
  * the merge Spark performs over partition states (Analyzer.scala:337-362 / StateLoader) split
  * into the collectives each field's merge rule allows:
  *   isum[n_sum]   int64, all-reduce SUM: every task's counters and wrapping Long sums, the rows;
- *   imax[n_max]   int64, all-reduce MAX: max keys, bitwise-NOT min keys (MAX of ~x = ~MIN), the
- *                 HLL registers widened (StatefulHyperloglogPlus.scala:119-137 merges by max);
+ *   imax[n_max]   int64, all-reduce MAX: max keys, bitwise-NOT min keys (MAX of ~x = ~MIN);
+ *   hll[n_hll]    uint8, all-reduce MAX: the HLL registers (StatefulHyperloglogPlus.scala:119-137
+ *                 merges by max);
  *   mom[n_mom]    double, all-GATHER (rank-major [world][n_mom]): n and the fp64 moments, merged
  *                 in rank order by the Chan / co-moment rules (StandardDeviation.scala:37-44,
- *                 Correlation.scala:37-52).
- * pack fills the three buffers from the state (device pointers for a device state: a kernel on the
+ *                 Correlation.scala:37-52), and a decimal task's exact 192-bit sum and 128-bit
+ *                 extremes as raw words (merged in the same rank-ordered pass).
+ * pack fills the four buffers from the state (device pointers for a device state: a kernel on the
  * state's stream that hip_stream is made to wait for; host pointers for a host state, device
  * -1); unpack writes the merged result into the state (device: a kernel on the state's stream
- * after hip_stream; read it with dq_state_sync).  The result equals dq_state_merge over the
- * ranks' states in rank order, byte for byte. */
+ * after hip_stream; read it with dq_state_sync).  Neither waits on the host (the plan's task kinds
+ * reach the device once per state).  The result equals dq_state_merge over the ranks' states in
+ * rank order, byte for byte. */
 dq_status dq_state_exchange_sizes(const dq_plan* plan, int64_t* n_sum, int64_t* n_max,
-                                  int64_t* n_mom);
+                                  int64_t* n_mom, int64_t* n_hll);
 dq_status dq_state_exchange_pack(dq_state* state, int64_t* isum, int64_t* imax, double* mom,
-                                 void* hip_stream);
+                                 uint8_t* hll, void* hip_stream);
 dq_status dq_state_exchange_unpack(dq_state* state, const int64_t* isum, const int64_t* imax,
-                                   const double* mom_gathered, int world, void* hip_stream);
+                                   const double* mom_gathered, const uint8_t* hll, int world,
+                                   void* hip_stream);
+/* Host waits on device work (stream / event synchronisations) the state and scan entry points
+ * have made in this process: a diagnostic counter (tests assert a path's waits, e.g. one per state
+ * exchange -- the merged state's read-back). */
+int64_t dq_host_wait_count(void);
 
 /* HyperLogLogPlusPlusUtils.count (StatefulHyperloglogPlus.scala:208-255) on 52 register words.
  * `bias_corrected` is set to 1 when the estimate fell in the empirical-bias range (E < 5M with no
@@ -317,6 +355,18 @@ int dq_java_float_to_string(float value, char* buf);
  * out + 32 i, its length in lens[i]; is_float: Float.toString of (float) values[i]. */
 void dq_java_doubles_to_strings(const double* values, int64_t n, int is_float, char* out,
                                 int32_t* lens);
+/* Spark's Cast(DecimalType(p, s) AS DOUBLE) (Decimal.toDouble = java.math.BigDecimal.doubleValue:
+ * the double nearest to unscaled / 10^s, ties to even) of one 128-bit unscaled value given as its
+ * low and high words: the device conversion (decimal.h) run on the host. */
+double dq_decimal_to_double(uint64_t lo, int64_t hi, int32_t scale);
+/* Spark 2.2's Cast(x AS STRING) of n values of a DQ_DECIMAL128 / DQ_DATE32 / DQ_TIMESTAMP_US
+ * column (`type` = its type word, values as the column stores them): java.math.BigDecimal
+ * .toString (plain, or E-notation when the adjusted exponent is below -6), "yyyy-MM-dd"
+ * (DateTimeUtils.dateToString) and "yyyy-MM-dd HH:mm:ss[.fraction]" in UTC
+ * (DateTimeUtils.timestampToString; the fraction is the nanoseconds without trailing zeros).
+ * Value i's text at out + 64 i (no NUL), its length in lens[i].  Histogram's keys of such a column
+ * (Histogram.scala:63); the device formats the same text for PatternMatch (dtfmt.h). */
+dq_status dq_format_values(int32_t type, const void* values, int64_t n, char* out, int32_t* lens);
 
 /* ------------------------------------------------------------------------------------------------
  * Frequency path: hash group-by (FrequencyBasedAnalyzer.computeFrequencies) on the GPU.

@@ -8,7 +8,10 @@ reference): CentralMomentAgg / Corr update+merge, Count/Sum/Mi
 (checked against the `xxhash` 3.8.1 package), HyperLogLogPlusPlus register update, cast-to-string.
 
 Data model: a table is a dict {column: list of python values, None = NULL} plus a dict of Spark
-type names {column: "long" | "int" | "double" | "float" | "string" | "boolean"}.  Rows are
+type names {column: "long" | "int" | "double" | "float" | "string" | "boolean" | "decimal(p,s)" |
+"date" | "timestamp"}.  Decimal values are decimal.Decimal, dates datetime.date, timestamps
+datetime.datetime (UTC, naive) -- the oracle's own representations, independent of the engine's
+unscaled integers / day and microsecond counts.  Rows are
 processed sequentially per "partition" (Spark's per-task update loop), and partitions are merged
 with the aggregate's merge rule -- so the oracle reproduces Spark's evaluation order, not just its
 mathematics.
@@ -23,15 +26,36 @@ import re
 import struct
 from typing import Dict, List, Optional, Sequence, Tuple
 
+import datetime
+import decimal
+from decimal import Decimal
+
 import xxhash
 
 INT_TYPES = {"byte", "short", "int", "long"}
 NUM_TYPES = INT_TYPES | {"float", "double"}
+# exact decimal arithmetic: 100 significant digits hold any sum of decimal(38) values
+_DEC_CTX = decimal.Context(prec=100)
+
+
+def decimal_ps(ty: str):
+    """(precision, scale) of an oracle type "decimal(p,s)", else None."""
+    m = re.match(r"^decimal\((\d+),(\d+)\)$", ty or "")
+    return (int(m.group(1)), int(m.group(2))) if m else None
+
+
+def unscaled(v: Decimal, scale: int) -> int:
+    """The unscaled integer of a decimal value at `scale` (the value must have at most that many
+    fraction digits, as a column of that DecimalType holds)."""
+    u = v.scaleb(scale, context=_DEC_CTX)
+    if u != u.to_integral_value():
+        raise ValueError(f"{v} has more than {scale} fraction digits")
+    return int(u)
 
 # ------------------------------------------------------------------------------------------------
 # SQL predicates (Spark SQL subset, three-valued logic) -- an independent little evaluator
 # ------------------------------------------------------------------------------------------------
-_TOK = re.compile(r"\s*(?:(\d+\.\d*(?:[eE][+-]?\d+)?|\d+(?:[eE][+-]?\d+)?)|('(?:[^']|'')*')|"
+_TOK = re.compile(r"\s*(?:((?:\d+\.\d*(?:[eE][+-]?\d+)?|\d+(?:[eE][+-]?\d+)?)[dD]?)(?![A-Za-z_])|('(?:[^']|'')*')|"
                   r"(<=>|<=|>=|<>|!=|==|=|<|>|\(|\)|,|-)|([A-Za-z_][A-Za-z0-9_]*))")
 
 
@@ -45,7 +69,12 @@ def _tokens(s: str):
         pos = m.end()
         num, st, op, ident = m.groups()
         if num is not None:
-            out.append(("num", float(num) if any(c in num for c in ".eE") else int(num)))
+            # Spark 2.2 types a fractional / exponent literal DecimalType: exact (a double column
+            # compares it as a double, _cmp3); a D suffix makes a DoubleType literal
+            if num[-1] in "dD":
+                out.append(("num", float(num[:-1])))
+            else:
+                out.append(("num", Decimal(num) if any(c in num for c in ".eE") else int(num)))
         elif st is not None:
             out.append(("str", st[1:-1].replace("''", "'")))
         elif op is not None:
@@ -170,7 +199,7 @@ def _cmp3(a, b) -> Optional[int]:
             return None
     if isinstance(a, bool) or isinstance(b, bool):
         return (a > b) - (a < b)
-    if isinstance(a, float) or isinstance(b, float):
+    if isinstance(a, float) or isinstance(b, float):  # (a decimal vs a double: Cast AS DOUBLE)
         a, b = float(a), float(b)
         an, bn = math.isnan(a), math.isnan(b)
         if (an and bn) or a == b:
@@ -328,8 +357,29 @@ def agg_compliance(t: OTable, predicate: str, where: Optional[str]) -> Optional[
     return None if not nn else sum(1 for v in nn if v)
 
 
+def agg_sum_decimal(t: OTable, column: str, where: Optional[str]) -> Optional[Decimal]:
+    """Spark 2.2 Sum over decimal(p, s): the exact sum in the result type decimal(min(p + 10, 38),
+    s), NULL when it does not fit (Cast's changePrecision; a per-partition overflow inside Spark
+    is not restated -- parity unpinned)."""
+    p, sc = decimal_ps(t.types[column])
+    vals = [v for v in _sel(t, column, where) if v is not None]
+    if not vals:
+        return None
+    acc = Decimal(0)
+    for v in vals:
+        acc = _DEC_CTX.add(acc, v)
+    rp = min(p + 10, 38)
+    if abs(unscaled(acc, sc)) >= 10 ** rp:
+        return None
+    return acc
+
+
 def agg_sum(t: OTable, column: str, where: Optional[str]) -> Optional[float]:
-    """Sum.scala:35: sum(col).cast(Double); integral columns sum as a wrapping Long first."""
+    """Sum.scala:35: sum(col).cast(Double); integral columns sum as a wrapping Long first; a
+    decimal column sums exactly and casts once (Decimal.toDouble: correctly rounded)."""
+    if decimal_ps(t.types[column]):
+        d = agg_sum_decimal(t, column, where)
+        return None if d is None else float(d)
     vals = [v for v in _sel(t, column, where) if v is not None]
     if not vals:
         return None
@@ -453,10 +503,37 @@ M = 1 << P
 NUM_WORDS = 52
 
 
+_EPOCH_DATE = datetime.date(1970, 1, 1)
+_EPOCH_TS = datetime.datetime(1970, 1, 1)
+
+
+def days_of(d: datetime.date) -> int:
+    return (d - _EPOCH_DATE).days
+
+
+def micros_of(ts: datetime.datetime) -> int:
+    delta = ts - _EPOCH_TS
+    return (delta.days * 86400 + delta.seconds) * 1000000 + delta.microseconds
+
+
 def spark_xxhash64(value, spark_type: str, seed: int = 42) -> int:
     """XxHash64Function.hash(v, type, seed) (Spark 2.2 HashExpression): standard XXH64 over the
     little-endian bytes: long/double as 8 bytes (double via doubleToLongBits, NaN canonical),
-    int/short/byte/boolean/float as 4 bytes (float via floatToIntBits), string as its UTF-8."""
+    int/short/byte/boolean/float as 4 bytes (float via floatToIntBits), string as its UTF-8; a
+    date as its int days (hashInt), a timestamp as its long microseconds (hashLong), a decimal of
+    precision <= 18 as its unscaled long (hashLong), above as BigInteger.toByteArray of the unscaled
+    value (the minimal big-endian two's complement, hashUnsafeBytes)."""
+    ps = decimal_ps(spark_type)
+    if ps:
+        u = unscaled(value, ps[1])
+        if ps[0] <= 18:
+            return xxhash.xxh64_intdigest(struct.pack("<q", u), seed=seed)
+        n = ((u if u >= 0 else ~u).bit_length()) // 8 + 1
+        return xxhash.xxh64_intdigest(u.to_bytes(n, "big", signed=True), seed=seed)
+    if spark_type == "date":
+        return xxhash.xxh64_intdigest(struct.pack("<i", days_of(value)), seed=seed)
+    if spark_type == "timestamp":
+        return xxhash.xxh64_intdigest(struct.pack("<q", micros_of(value)), seed=seed)
     if spark_type == "string":
         data = value.encode("utf-8")
     elif spark_type in ("long",):
@@ -657,8 +734,47 @@ def java_float_to_string(f: float) -> str:
     return _java_layout("-" if f < 0 else "", mant.replace(".", ""), int(exp))
 
 
+def java_bigdecimal_to_string(v: Decimal, scale: int) -> str:
+    """java.math.BigDecimal.toString (Spark 2.2 Decimal.toString) of a value at `scale`: the
+    unscaled digits, plain when the adjusted exponent (digits - 1 - scale) >= -6 (with a '.'
+    before the last `scale` digits), else one digit, '.', the rest, 'E' and the exponent."""
+    u = unscaled(v, scale)
+    digits = str(abs(u))
+    sign = "-" if u < 0 else ""
+    adjusted = len(digits) - 1 - scale
+    if scale == 0:
+        return sign + digits
+    if adjusted >= -6:
+        if len(digits) > scale:
+            return sign + digits[:-scale] + "." + digits[-scale:]
+        return sign + "0." + "0" * (scale - len(digits)) + digits
+    body = digits[0] + ("." + digits[1:] if len(digits) > 1 else "")
+    return sign + body + "E" + str(adjusted)
+
+
+def java_date_to_string(d: datetime.date) -> str:
+    """DateTimeUtils.dateToString: yyyy-MM-dd (years 1..9999)."""
+    return f"{d.year:04d}-{d.month:02d}-{d.day:02d}"
+
+
+def java_timestamp_to_string(ts: datetime.datetime) -> str:
+    """DateTimeUtils.timestampToString in UTC: yyyy-MM-dd HH:mm:ss, then java.sql.Timestamp's
+    fraction (the nanoseconds, trailing zeros dropped) unless it is ".0"."""
+    base = f"{ts.year:04d}-{ts.month:02d}-{ts.day:02d} {ts.hour:02d}:{ts.minute:02d}:{ts.second:02d}"
+    if ts.microsecond:
+        return base + "." + f"{ts.microsecond * 1000:09d}".rstrip("0")
+    return base
+
+
 def java_to_string(v, ty: str) -> str:
     """Spark's cast to string of a non-NULL value of oracle type `ty`."""
+    ps = decimal_ps(ty)
+    if ps:
+        return java_bigdecimal_to_string(v, ps[1])
+    if ty == "date":
+        return java_date_to_string(v)
+    if ty == "timestamp":
+        return java_timestamp_to_string(v)
     if ty == "string":
         return v
     if ty == "boolean":

@@ -1,5 +1,6 @@
 """The reference's test fixtures as data (src/test/scala/com/amazon/deequ/utils/FixtureSupport.scala
 and NullHandlingTests.scala:14-35), with their Spark column types."""
+from decimal import Decimal
 
 FIXTURES = {
     # FixtureSupport.scala:29-46
@@ -65,6 +66,10 @@ FIXTURES = {
         "numericCol3": "double"}),
     # AnalyzerTests.scala:508 -- sparkContext.range(-1000, 1000)
     "range2000": ({"att1": list(range(-1000, 1000))}, {"att1": "long"}),
+    # AnalyzerTests.scala:454-466 -- three rows of DecimalType.SYSTEM_DEFAULT = decimal(38,18)
+    # (Scala's BigDecimal(123.45) of a double is decimal("123.45"))
+    "dfDecimalMinimum": ({"num": [Decimal("123.45"), Decimal("99"), Decimal("678")]},
+                         {"num": "decimal(38,18)"}),
     # examples/BasicExample.scala:29-34 (Item entity, entities.scala:19-25)
     "basicExampleItems": ({
         "id": [1, 2, 3, 4, 5],
@@ -81,10 +86,25 @@ ARROW_TYPES = {"string": "string", "int": "int32", "long": "int64", "double": "f
                "float": "float32", "boolean": "bool_", "short": "int16", "byte": "int8"}
 
 
+def arrow_type(ty: str):
+    """The Arrow type of an oracle / Spark type name (decimal(p,s), date, timestamp included)."""
+    import re
+
+    import pyarrow as pa
+    m = re.match(r"^decimal\((\d+),(\d+)\)$", ty)
+    if m:
+        return pa.decimal128(int(m.group(1)), int(m.group(2)))
+    if ty == "date":
+        return pa.date32()
+    if ty == "timestamp":
+        return pa.timestamp("us")
+    return getattr(pa, ARROW_TYPES[ty])()
+
+
 def arrow_table(name):
     import pyarrow as pa
     cols, types = FIXTURES[name]
-    arrays = [pa.array(v, type=getattr(pa, ARROW_TYPES[types[k]])()) for k, v in cols.items()]
+    arrays = [pa.array(v, type=arrow_type(types[k])) for k, v in cols.items()]
     return pa.Table.from_arrays(arrays, names=list(cols))
 
 

@@ -22,7 +22,7 @@ def oracle_metric(t: "O.OTable", cls: str, args, kwargs):
             return FAILURE
     if cls in ("Sum", "Mean", "Minimum", "Maximum", "StandardDeviation", "Correlation"):
         for c in need_cols:
-            if t.types[c] not in NUMERIC:
+            if t.types[c] not in NUMERIC and not O.decimal_ps(t.types[c]):
                 return FAILURE
     try:
         if cls == "Size":

@@ -7,7 +7,9 @@ DQ_HD functions in api.cpp).  Bar: the merged states are equal byte for byte (VE
 Every rank crafts every rank's aggregation buffers from a seed (the scan's layout per task kind,
 api.cpp / engine.h Acc: a task's unused fields zero), so the reference merge needs no collective.
 Cases the merge rules single out are planted: empty ranks (n = 0: skipped, or copied into an empty
-accumulator), -0.0 double sums, Long sums that wrap, extremes at INT64_MIN / INT64_MAX.
+accumulator), -0.0 double sums, Long sums that wrap, extremes at INT64_MIN / INT64_MAX, and a
+decimal(38, 4) column's task (192-bit sums with carries across words, 128-bit extremes: the words
+travel in the gathered block and merge in rank order, not through the word-wise collectives).
 """
 import os
 import socket
@@ -33,12 +35,17 @@ def _plan():
     from deequ_amd.runners.engine import get_plan
     from deequ_amd.table import StructField, StructType
     sch = StructType([StructField("x", N.INT64), StructField("d", N.FLOAT64),
-                      StructField("s", N.UTF8)])
+                      StructField("s", N.UTF8), StructField("m", N.decimal_type(38, 4))])
     suite = [Size(), Completeness("s"), Compliance("c", "x >= 0"), Sum("x"), Mean("x"),
              StandardDeviation("x"), Minimum("x"), Maximum("x"), Minimum("d"), Maximum("d"),
              Sum("d"), Correlation("x", "d"), ApproxCountDistinct("x"), ApproxCountDistinct("s"),
-             DataType("s"), Compliance("c2", "s = 'a' OR x > 3")]
+             DataType("s"), Compliance("c2", "s = 'a' OR x > 3"), Sum("m"), Minimum("m"),
+             Maximum("m"), StandardDeviation("m"), Completeness("m")]
     return get_plan(sch, [s for a in suite for s in a.aggregation_functions()])
+
+
+def _s64(v):
+    return v - (1 << 64) if v >= (1 << 63) else v
 
 
 def _kinds(plan):
@@ -78,6 +85,21 @@ def _image(plan, seed, rank):
             if n:
                 d[:5] = [float(v) for v in rng.normal(0, 1e6, 5)]
                 d[3], d[4] = abs(d[3]), abs(d[4])
+        elif k == "decimal":
+            i[0] = n
+            i[4], i[5], i[6], i[7] = -1, I64_MAX, 0, I64_MIN  # the empty extremes
+            if n:
+                w = int(rng.integers(0, 1 << 62)) << 100 | int(rng.integers(0, 1 << 62))
+                w = -w if rng.random() < 0.5 else w  # a 192-bit sum: carries cross the words
+                w &= (1 << 192) - 1
+                i[1:4] = [_s64(w >> (64 * q) & 0xFFFFFFFFFFFFFFFF) for q in range(3)]
+                lo, hi = sorted(int(rng.integers(-(1 << 62), 1 << 62)) << 60 | int(rng.integers(0, 1 << 60))
+                                for _ in range(2))
+                for at, v in ((4, lo), (6, hi)):
+                    v &= (1 << 128) - 1
+                    i[at], i[at + 1] = _s64(v & 0xFFFFFFFFFFFFFFFF), _s64(v >> 64)
+                d[1] = float(rng.normal(0, 1e6))
+                d[2] = float(abs(rng.normal(0, 1e15)))
         elif k == "dtype":
             i[:5] = [0 if empty else int(v) for v in rng.integers(0, 1 << 30, 5)]
         elif k in ("boolmap", "str_in"):
@@ -160,8 +182,9 @@ def test_exchange_sizes_follow_the_plan():
     from deequ_amd import _native as N
     plan = _plan()
     kinds = _kinds(plan)
-    ns, nm, nd = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    ns, nm, nd, nh = (ctypes.c_int64() for _ in range(4))
     N.check(N.lib.dq_state_exchange_sizes(plan.handle, ctypes.byref(ns), ctypes.byref(nm),
-                                          ctypes.byref(nd)))
+                                          ctypes.byref(nd), ctypes.byref(nh)))
     T, H = len(kinds), kinds.count("hll")
-    assert (ns.value, nm.value, nd.value) == (10 * T + 1, 2 * T + 512 * H, 8 * T)
+    assert "decimal" in kinds
+    assert (ns.value, nm.value, nd.value, nh.value) == (10 * T + 1, 2 * T, 16 * T, 512 * H)
