@@ -877,6 +877,8 @@ struct dq_state {
   DevBuf<uint32_t> d_order[2];   // mixed launch: queue position -> item (per descriptor slot)
   std::vector<uint32_t> order_sig[2];  // the descriptors and launches d_order[slot] was built for
   std::vector<size_t> order_off[2], order_len[2];  // per queue group: its order list in d_order
+  uint32_t* h_order[2] = {nullptr, nullptr};  // pinned staging of d_order[slot] (async upload)
+  size_t h_order_cap[2] = {0, 0};
   DevBuf<TaskDesc> d_tasks[2];
   TaskDesc* h_tasks[2] = {nullptr, nullptr};
   size_t h_tasks_cap[2] = {0, 0};
@@ -908,6 +910,7 @@ struct dq_state {
     for (int k = 0; k < 2; ++k) {
       if (h_tasks[k]) (void)hipHostFree(h_tasks[k]);
       if (h_cols[k]) (void)hipHostFree(h_cols[k]);
+      if (h_order[k]) (void)hipHostFree(h_order[k]);
       if (ev[k]) (void)hipEventDestroy(ev[k]);
     }
     if (ev_xchg) (void)hipEventDestroy(ev_xchg);
@@ -1578,9 +1581,21 @@ extern "C" dq_status dq_scan_device_batches(const dq_plan* plan, const dq_column
         }
       }
       HIP_TRY(s->d_order[slot].ensure(std::max<size_t>(1, all.size())));
-      if (!all.empty())
-        HIP_TRY(hipMemcpy(s->d_order[slot].p, all.data(), all.size() * sizeof(uint32_t),
-                          hipMemcpyHostToDevice));
+      if (!all.empty()) {
+        // staged in the slot's pinned buffer and queued on `stream`: the slot's event was waited
+        // above, so neither buffer is still read, and the other slot's work is not waited for
+        if (s->h_order_cap[slot] < all.size()) {
+          if (s->h_order[slot]) HIP_TRY(hipHostFree(s->h_order[slot]));
+          s->h_order[slot] = nullptr;
+          s->h_order_cap[slot] = 0;
+          HIP_TRY(hipHostMalloc((void**)&s->h_order[slot], all.size() * sizeof(uint32_t),
+                                hipHostMallocDefault));
+          s->h_order_cap[slot] = all.size();
+        }
+        memcpy(s->h_order[slot], all.data(), all.size() * sizeof(uint32_t));
+        HIP_TRY(hipMemcpyAsync(s->d_order[slot].p, s->h_order[slot], all.size() * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, stream));
+      }
       s->order_sig[slot] = sig;
     }
     launches.clear();

@@ -4671,6 +4671,15 @@ struct dq_freq {
   struct PinnedWord {
     unsigned long long* p = nullptr;
     hipStream_t last_copy = nullptr;  // the stream of the last copy into *p
+    // Before a copy into *p is queued on `st`: a copy still queued on another stream could land
+    // after it (and after dq_freq_destroy synced only `st`, recycling the word to another table),
+    // so that stream is waited for first.  Same stream: stream order already holds.
+    hipError_t before_copy(hipStream_t st) {
+      hipError_t e = hipSuccess;
+      if (last_copy && last_copy != st) e = hipStreamSynchronize(last_copy);
+      last_copy = st;
+      return e;
+    }
     ~PinnedWord() {
       if (p) pinned_word_put(p);
     }
@@ -6493,8 +6502,8 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     dq_status ps = launch_pieces(f, a, chunks);
     if (ps != DQ_OK) return ps;
     if (dense) {  // the host learns (late, without a wait) whether the batch was declined
+      HIP_TRY(f->dense_seen.before_copy(f->stream));
       HIP_TRY(hipMemcpyAsync(f->dense_seen.p, f->dense_words.p + 3, 8, hipMemcpyDeviceToHost, f->stream));
-      f->dense_seen.last_copy = f->stream;
     }
   } else if (f->exact) {
     f->nan_counted = false;
@@ -6504,8 +6513,8 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
   }
   HIP_TRY(hipGetLastError());
   if (small) {  // the host learns (late, without a wait) whether the attempt gave the batch up
+    HIP_TRY(f->fast_seen.before_copy(f->stream));
     HIP_TRY(hipMemcpyAsync(f->fast_seen.p, a.fast_words, 8, hipMemcpyDeviceToHost, f->stream));
-    f->fast_seen.last_copy = f->stream;
   }
   f->n_chunks += chunks + piece_chunks;
   f->counters_stale = true;  // read back at finalize / merge / arena growth

@@ -234,8 +234,14 @@ def _remove_qe_quoting(p: str) -> str:
         if p[i] == "\\" and i + 1 < n and p[i + 1] == "Q":
             j = p.find("\\E", i + 2)
             j = n if j < 0 else j
-            for ch in p[i + 2:j]:
-                out.append(ch if not ch.isascii() or ch.isalnum() else "\\" + ch)
+            for k, ch in enumerate(p[i + 2:j]):
+                if ch.isascii() and ch.isdigit() and k == 0:
+                    # a digit first in the section becomes \x3N, so an octal escape or a
+                    # back-reference just before the \Q cannot absorb it (RemoveQEQuoting's
+                    # beginQuote)
+                    out.append("\\x3" + ch)
+                else:
+                    out.append(ch if not ch.isascii() or ch.isalnum() else "\\" + ch)
             i = j + 2
         elif p[i] == "\\":
             out.append(p[i:i + 2])
@@ -607,11 +613,16 @@ class _Parser:
             v = int(self.s[self.i:self.i + 4], 16)
             self.i += 4
         elif c == "0":
-            j = self.i
-            while j < len(self.s) and j < self.i + 3 and self.s[j] in "01234567":
-                j += 1
-            v = int(self.s[self.i:j] or "0", 8)
-            self.i = j
+            # Pattern.o(): one or two octal digits, a third only when the first is 0-3; none is
+            # "Illegal octal escape sequence"
+            d = self.s[self.i:self.i + 3]
+            k = 0
+            while k < len(d) and d[k] in "01234567" and (k < 2 or d[0] in "0123"):
+                k += 1
+            if k == 0:
+                self.error("illegal octal escape sequence")
+            v = int(d[:k], 8)
+            self.i += k
         elif c == "c":
             v = ord(self.take_raw()) ^ 64
         elif c.isdigit() and not in_class:

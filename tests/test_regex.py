@@ -223,6 +223,20 @@ def test_unsupported_patterns_are_refused(pattern):
         compile_java_regex(pattern)
 
 
+def test_octal_escapes_and_quoted_digits_as_jdk8():
+    # Pattern.o(): a third octal digit only after a first digit 0-3; \0 with none is illegal
+    assert compile_java_regex(r"\0101").matches("xA")            # 0101 = 'A'
+    c = compile_java_regex(r"\0477")                              # 047 = "'", then a literal 7
+    assert c.matches("'7") and not c.matches("\u0137")
+    # RemoveQEQuoting writes a digit first in a \Q section as \x3N: no escape absorbs it
+    c = compile_java_regex(r"(a)\Q1\E")                           # not the back-reference \11
+    assert c.matches("a1") and not c.matches("aa")
+    assert compile_java_regex(r"\Q12\E").matches("x12")
+    for bad in [r"\0", r"\0x", r"\08", r"\0\Q1\E"]:                      # Java: Illegal octal escape
+        with pytest.raises(PatternNotSupported):
+            compile_java_regex(bad)
+
+
 def test_blob_layout():
     c = compile_java_regex(r"\d")
     b = c.blob()
