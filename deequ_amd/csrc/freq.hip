@@ -51,6 +51,15 @@
 #include "kernels.h"
 #include "stream_load.h"
 
+// freq_phaseC_x's probe rounds: branch-light (1) or round 5's per-record branches (0, a build
+// for A/B runs through DQ_LIB_PATH)
+#ifndef DQ_LEAN_PROBE
+#define DQ_LEAN_PROBE 1
+#endif
+#ifndef DQ_C_EXPERIMENT  // timing builds only (wrong results): 1 no statistics, 2 no inserts
+#define DQ_C_EXPERIMENT 0
+#endif
+
 namespace dq {
 
 #define DQ_DEV __device__ __forceinline__
@@ -2916,6 +2925,13 @@ struct CArgs {
   // 0: groups materialise at their partition's record offset; else work item wi's groups go to
   // groups[wi * group_stride ..] (dq_freq_topk's recount of a few partitions)
   uint32_t group_stride;
+  // freq_phaseC_x, first pass: the work items' record ranges come from a per-lane cache of 64
+  // items' bounds (vector loads issued 64 items ahead) instead of scalar loads per item (< 2^32
+  // records; 0: the scalar loads)
+  uint32_t bcache;
+  // freq_phaseC_x: workgroup g takes the contiguous items [g * ipw, (g + 1) * ipw) instead of
+  // g, g + grid, ... (0: strided)
+  uint32_t contig;
 };
 
 // Is the encoded one-column utf8 key at p the 9-byte string "NullValue"?
@@ -2926,6 +2942,9 @@ DQ_DEV bool enc_is_null_literal(const uint8_t* p) {
 }
 
 constexpr int kCThreads = 512;  // phase-C workgroup: two per CU by LDS, 128 VGPRs per lane
+// freq_phaseC_x's workgroup: packed tables run one 1024-thread workgroup per CU (a 128 KB table)
+template <bool PK>
+constexpr int kCThreadsX = PK ? 1024 : kCThreads;
 // records per thread loaded ahead: exact partitions (~kTarget records) arrive whole
 template <bool HASHED>
 constexpr int kPF = HASHED ? 2 : 4;
@@ -2981,7 +3000,7 @@ DQ_DEV void c_bounds(const CArgs& a, int wi, CBounds& bd) {
 }
 
 // Work item wi (bounds bd): the raw words of its first kPF * kCThreads records.
-template <bool HASHED>
+template <bool HASHED, int CTH = kCThreads>
 DQ_DEV void c_fetch(const CArgs& a, int wi, const CBounds& bd, CItem<HASHED>& it) {
   constexpr int W = FM<HASHED>::kRB / 8;
   it.valid = 0;
@@ -2991,11 +3010,13 @@ DQ_DEV void c_fetch(const CArgs& a, int wi, const CBounds& bd, CItem<HASHED>& it
   it.fv = bd.fv;
   it.r0 = bd.r0;
   it.r1 = bd.r1;
-  const uint64_t n = it.r1 - it.r0;
+  // (32-bit lane offsets: a partition's prefetch window is kPF * CTH records)
+  const uint64_t n64 = it.r1 - it.r0;
+  const uint32_t n = n64 < (uint64_t)kPF<HASHED> * CTH ? (uint32_t)n64 : (uint32_t)kPF<HASHED> * CTH;
   const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + it.r0 * W;
 #pragma unroll
   for (int q = 0; q < kPF<HASHED>; ++q) {
-    const uint64_t li = (uint64_t)q * kCThreads + threadIdx.x;
+    const uint32_t li = (uint32_t)q * CTH + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < W; ++k) it.w[q][k] = 0;
     if (li < n) {
@@ -3467,9 +3488,15 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
 // partition has more than 4096 records; such an item is handed on (an ovf entry of the whole
 // partition, f = 0) to the two-word kernel.  (s = 7..9: the configs[4]-sized tables.)
 template <bool DBG, bool PK>
-__global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
-  constexpr int KT = PK ? 8192 : FM<false>::kTableC, NW = kCThreads / 64, PF = kPF<false>;
-  constexpr int KL = PK ? 2 * PF * kCThreads : KT;  // list capacity
+__global__ void __launch_bounds__(kCThreadsX<PK>, 4) freq_phaseC_x(CArgs a) {
+  // PK: one 1024-thread workgroup per CU over a 16384-slot table (128 KB of LDS): an item of up
+  // to 4096 records is inserted in ONE round at a load factor <= 1/4.  The probe rounds are a
+  // chain of LDS atomic round trips (~600 cycles each under load: tools/micro/lds_insert_bench),
+  // and a round takes as many as its wave's longest probe sequence -- two rounds at up to 44 %
+  // load took ~11 of them per item, one round at <= 25 % takes ~4.
+  constexpr int CT = kCThreadsX<PK>;
+  constexpr int KT = PK ? 16384 : FM<false>::kTableC, NW = CT / 64, PF = kPF<false>;
+  constexpr int KL = PK ? 4096 : KT;  // list capacity
   // PK: the partition fixes the hash's top 9 + s bits, the slot keeps the other KB = 55 - s
   // (45..48 for s = 10..7) under a count field of 9 + s bits
   const int KB = 55 - (int)a.s;
@@ -3492,7 +3519,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
   enum { TF_VALID = 1, TF_SUB = 2, TF_CANDFAST = 4, TF_CANDONE = 8 };
 
   const int tid = threadIdx.x, lane = __lane_id(), wave = tid >> 6;
-  for (int i = tid; i < KT; i += kCThreads) {
+  for (int i = tid; i < KT; i += CT) {
     tkey[i] = kEmptyKey;
     if (!PK) tcnt[i] = 0;
   }
@@ -3506,15 +3533,26 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
   if (tid < 4) (&s_efix[0][0])[tid] = 0;
   if (tid < kSmallCounts) s_term[tid] = tid ? entropy_term((uint64_t)tid, a.num_rows) : 0.0;
   const bool keep = a.groups != nullptr;
+  // (a scan of the whole table instead of the list of claimed slots -- 16 slots per thread,
+  // conflict-free 16-byte reads, no list appends -- measured slower: statistics 3.5 against
+  // 2.0 us per item, profiles/r6j; kept off)
+  constexpr bool scan_stats = false;
+  __shared__ uint32_t s_wgn[2][NW];  // scan_stats: each wave's groups of the item
 
   // Wave 0: the statistics and candidates of the item of parity q (its words stay untouched until
   // the item after next resets them, behind that item's barrier 1).
   // (wv 1 merges the candidates while wv 0 writes the statistics: neither holds up the inserts
   // that wait at barrier 1 for the slowest wave)
   auto tail = [&](uint32_t q, int wv) {
-    const uint32_t fl = s_tfl[q];
+    // (wave-uniform words: scalars, so the candidates' addresses take no VGPRs)
+    const uint32_t fl = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tfl[q]);
     if (!(fl & TF_VALID)) return;
-    const uint32_t p = s_tp[q], gtot = s_tg[q];
+    const uint32_t p = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tp[q]);
+    uint32_t gtot = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tg[q]);
+    if (scan_stats) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) gtot += s_wgn[q][w];
+    }
     const bool sub = (fl & TF_SUB) != 0;
     if ((fl & TF_CANDFAST) && wv == 1) {  // the item's top kCand: rounds of wave maxima over the waves' lists
       static_assert(NW * kCand <= 64, "one wave merges the lists");
@@ -3566,13 +3604,62 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     }
   };
 
+  // Bounds ring (a.bcache, the first pass): this workgroup's items t's record ranges (32-bit start,
+  // count) at ring[t % 512], filled 256 items at a time, 256 items ahead (one load per thread and
+  // one exposed round trip per 256 items).  A scalar load of the bounds of item i + 2 per item was
+  // waited for by the item's first LDS wait (s_waitcnt lgkmcnt(0) covers SMEM loads too): one HBM
+  // round trip per item exposed in its CAS rounds.
+  // this workgroup's item t -> work item (a.n_work: none).  Contiguous items (a.contig) walk the
+  // records region in order (one page run per workgroup), strided ones jump P / grid partitions.
+  const int ipw = a.contig ? (a.n_work + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  auto wmap = [&](int t) -> int {
+    if (ipw) {
+      const int w = (int)blockIdx.x * ipw + t;
+      return t < ipw && w < a.n_work ? w : a.n_work;
+    }
+    return (int)blockIdx.x + t * (int)gridDim.x;
+  };
+  constexpr int kRing = 512;
+  __shared__ uint32_t ring_r0[kRing], ring_n[kRing];
+  const bool bcache = a.bcache != 0 && a.entries == nullptr;  // (block-uniform)
+  auto bfill = [&](int t0, int cnt) {  // items [t0, t0 + cnt), one per thread (cnt <= CT)
+    if (tid < cnt) {
+      const int64_t w = wmap(t0 + tid);
+      uint32_t r0v = 0, nv = 0;
+      if (w < a.n_work) {
+        const uint64_t x0 = a.part_base[w], x1 = a.part_base[w + 1];
+        r0v = (uint32_t)x0;
+        nv = (uint32_t)(x1 - x0);
+      }
+      ring_r0[(t0 + tid) & (kRing - 1)] = r0v;
+      ring_n[(t0 + tid) & (kRing - 1)] = nv;
+    }
+  };
+  auto bget = [&](int t, CBounds& bd) {  // this workgroup's item t (in the ring)
+    const int64_t w = wmap(t);
+    if (w >= a.n_work) return;
+    bd.p = (uint32_t)w;
+    bd.f = bd.fv = 0;
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring_r0[t & (kRing - 1)]);
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring_n[t & (kRing - 1)]);
+    bd.r0 = r0;
+    bd.r1 = (uint64_t)r0 + n;
+  };
+
   // One item ahead, issued at the top of an item and taken over at its end: the records of item
   // i + 1 and the bounds of item i + 2 are in flight through all of item i.
   CBounds nb;
   CItem<false> cur;
-  c_bounds(a, blockIdx.x, nb);
-  c_fetch<false>(a, blockIdx.x, nb, cur);
-  c_bounds(a, blockIdx.x + gridDim.x, nb);
+  if (bcache) {
+    bfill(0, CT < kRing ? CT : kRing);
+    __syncthreads();
+    bget(0, nb);
+  } else {
+    c_bounds(a, wmap(0), nb);
+  }
+  c_fetch<false, CT>(a, wmap(0), nb, cur);
+  if (bcache) bget(1, nb);
+  else c_bounds(a, wmap(1), nb);
   __syncthreads();
 
   uint32_t par = 0;
@@ -3581,7 +3668,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     if constexpr (DBG)
       if (blockIdx.x == 0 && tid == 0 && item < 16) a.dbg_clock[item * 8 + kk] = wall_clock64();
   };
-  for (int wi = blockIdx.x; wi < a.n_work; wi += gridDim.x, par ^= 1u, ++item) {
+  for (int wi = wmap(0); wi < a.n_work; par ^= 1u, ++item, wi = wmap(item)) {
     mark(0);
     const uint32_t p = cur.p, b = p >> a.s, f = cur.f, fv = cur.fv;
     const uint32_t fmask = (1u << f) - 1u;
@@ -3619,35 +3706,91 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       // Probe rounds with every pending record's CAS in flight together (a wave takes as many
       // rounds as its longest probe sequence, not the sum over its records); double hashing (an
       // odd step from high hash bits) keeps those sequences short.
-      // (PK: the step comes from key bits 32..44 of the packed word -- bits 45 and up are the
-      // count, and records of one key with different counts must walk the same sequence)
+      // (PK: the step comes from key bits 30..43 of the packed word -- bits 45 and up may be the
+      // count (KB = 55 - s >= 45), and records of one key with different counts must walk the
+      // same sequence; the slot is bits 0..13)
       uint32_t step[PF];
 #pragma unroll
-      for (int q = 0; q < PF; ++q) step[q] = ((uint32_t)(h[q] >> (PK ? 32 : 40)) | 1u) & (KT - 1);
+      for (int q = 0; q < PF; ++q) step[q] = ((uint32_t)(h[q] >> (PK ? 30 : 40)) | 1u) & (KT - 1);
       uint32_t mine = 0;
-      for (int pr = 0; todo && pr < KT; ++pr) {
+#if DQ_C_EXPERIMENT & 2  // (timing experiment only: no inserts)
+      todo = 0;
+#endif
+      if constexpr (PK && DQ_LEAN_PROBE) {
+        // One CAS instruction per probe round: each lane works on its next pending record, so a
+        // round is a full-width LDS atomic while the wave's records last, instead of PF
+        // instructions whose lanes thin out to the longest probe sequence.  The CAS instructions,
+        // not the lanes in them, set an LDS atomic round trip (16 waves queue theirs), and a
+        // wave's chain of round trips sets the insert phase (tools/micro/lds_insert_bench).
+        // The lane's records move through a shift register (a PK first pass has no hash filter,
+        // so its pending records are a prefix of the PF); the slots it claims go to cl[0..ncl)
+        // (then to the list below, as `mine` bits 0..ncl-1 over slot[]).
+        uint64_t ch = h[0], ca = c[0] << KB;
+        uint32_t cs = slot[0], cst = step[0];
+        uint32_t rest = todo >> 1, ncl = 0, cl[PF];
 #pragma unroll
-        for (int q = 0; q < PF; ++q)
-          old[q] = (todo >> q) & 1u ? atomicCAS((unsigned long long*)&tkey[slot[q]], kEmptyKey, h[q]) : 0ULL;
+        for (int x = 0; x < PF; ++x) cl[x] = 0;
+        bool act = (todo & 1u) != 0;
+        for (int pr = 0; act && pr < 4 * KT; ++pr) {
+          const uint64_t o = atomicCAS((unsigned long long*)&tkey[cs], kEmptyKey, ch);
+          const bool e = o == kEmptyKey;
+          const bool m = !e && ((o ^ ch) & MK) == 0;
+          if (m) atomicAdd((unsigned long long*)&tkey[cs], (unsigned long long)ca);
+          if (e || m) {
+            if (e) {
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-          if (!((todo >> q) & 1u)) continue;
-          const bool claimed = old[q] == kEmptyKey;
-          const bool match = PK ? ((old[q] ^ h[q]) & MK) == 0 : old[q] == h[q];
-          if (claimed || match) {
-            if constexpr (PK) {
-              if (!claimed) atomicAdd((unsigned long long*)&tkey[slot[q]], (unsigned long long)(c[q] << KB));
-            } else {
-              atomicAdd((unsigned long long*)&tcnt[slot[q]], (unsigned long long)c[q]);
+              for (int x = 0; x < PF; ++x) cl[x] = (uint32_t)x == ncl ? cs : cl[x];
+              ++ncl;
             }
-            if (claimed) mine |= 1u << q;
-            todo &= ~(1u << q);
+            act = (rest & 1u) != 0;
+            rest >>= 1;
+            ch = h[1];
+            ca = c[1] << KB;
+            cs = slot[1];
+            cst = step[1];
+#pragma unroll
+            for (int x = 1; x + 1 < PF; ++x) {
+              h[x] = h[x + 1];
+              c[x] = c[x + 1];
+              slot[x] = slot[x + 1];
+              step[x] = step[x + 1];
+            }
           } else {
-            slot[q] = (slot[q] + step[q]) & (KT - 1);
+            cs = (cs + cst) & (KT - 1);
+          }
+        }
+        todo = act ? 1u : 0u;  // (a record still pending: the table is full)
+        mine = (1u << ncl) - 1u;
+#pragma unroll
+        for (int x = 0; x < PF; ++x) slot[x] = cl[x];
+      } else {  // (PF records per lane in flight together; -DDQ_LEAN_PROBE=0: also for PK)
+        // (a branch-light form of these rounds -- outcomes as bit masks, slots advanced with
+        // selects -- measured no faster, profiles/r6g, and spilled the two-word kernel)
+        for (int pr = 0; todo && pr < KT; ++pr) {
+#pragma unroll
+          for (int q = 0; q < PF; ++q)
+            old[q] = (todo >> q) & 1u ? atomicCAS((unsigned long long*)&tkey[slot[q]], kEmptyKey, h[q]) : 0ULL;
+#pragma unroll
+          for (int q = 0; q < PF; ++q) {
+            if (!((todo >> q) & 1u)) continue;
+            const bool claimed = old[q] == kEmptyKey;
+            const bool match = PK ? ((old[q] ^ h[q]) & MK) == 0 : old[q] == h[q];
+            if (claimed || match) {
+              if constexpr (PK) {
+                if (!claimed) atomicAdd((unsigned long long*)&tkey[slot[q]], (unsigned long long)(c[q] << KB));
+              } else {
+                atomicAdd((unsigned long long*)&tcnt[slot[q]], (unsigned long long)c[q]);
+              }
+              if (claimed) mine |= 1u << q;
+              todo &= ~(1u << q);
+            } else {
+              slot[q] = (slot[q] + step[q]) & (KT - 1);
+            }
           }
         }
       }
       if (todo) s_ovf[par] = 1;  // the table is full
+      if (scan_stats) mine = 0;  // (no list: the statistics scan the table)
       const uint32_t nm = (uint32_t)__builtin_popcount(mine);
       const uint32_t incl = __ockl_wfscan_add_u32(nm, true);
       const uint32_t wtot = __builtin_amdgcn_readlane(incl, 63);
@@ -3661,38 +3804,54 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       }
       mark(6);
     };
+    // the ring's other half: items [item + 256, item + 512), read from item + 254 on (barriers
+    // between); the half it replaces held items before this one
+    if (bcache && item > 0 && (item & (kRing / 2 - 1)) == 0) bfill(item + kRing / 2, kRing / 2);
     const bool too_long = PK && nrec > (uint64_t)KL;  // (handed on whole, see `overflow`)
+    // The rest of a long partition (packed items hold up to 2 * PF * CT records; a column
+    // of heavy values puts every workgroup's records of a heavy key in one partition): the first
+    // round's issue slot loads this item's second round of words, and the LAST round's issue slot
+    // prefetches the next item -- so neither is an exposed HBM round trip, and at most one round of
+    // words is in flight beside the round being inserted (VGPRs: the kernel sits at 128).
+    constexpr uint64_t STEP = (uint64_t)PF * CT;
+    const bool rest = nrec > STEP && !too_long;
+    // (the rounds' words travel in pf's registers: the next item's prefetch goes out last, and a
+    // second buffer, live where the two paths join, spilled the kernel)
+    auto load = [&](uint64_t base) {  // (32-bit offsets inside the round)
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + r0 + base;
+      const uint64_t left = nrec - base;
+      const uint32_t m = left < STEP ? (uint32_t)left : (uint32_t)STEP;
+      pf.valid = 0;
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const uint32_t li = (uint32_t)q * CT + tid;
+        pf.w[q][0] = li < m ? src[li] : 0ULL;
+        pf.valid |= (li < m ? 1u : 0u) << q;
+      }
+    };
+    auto issue_next = [&]() {
+      if (bcache) bget(item + 2, nb2);
+      c_fetch<false, CT>(a, wmap(item + 1), nb, pf);
+      if (!bcache) c_bounds(a, wmap(item + 2), nb2);
+    };
     insert_round(cur.w, too_long ? 0u : cur.valid, [&]() {
-      c_fetch<false>(a, wi + gridDim.x, nb, pf);
-      c_bounds(a, wi + 2 * gridDim.x, nb2);
+      if (rest) load(STEP);
+      else issue_next();
     });
     // the last item's outputs, after this wave's inserts (its records are no longer live; the
     // stores come after the prefetch, so the next item's wait for its records leaves them be)
     if (wave < 2) tail(par ^ 1u, wave);
-    if (nrec > (uint64_t)PF * kCThreads && !too_long) {  // the rest of a long partition
-      // (a column of heavy values: every workgroup's records of a heavy key land in one
-      // partition) -- the next round's words in flight while this round inserts
-      const uint64_t* src = reinterpret_cast<const uint64_t*>(a.recsB) + r0;
-      constexpr uint64_t STEP = (uint64_t)PF * kCThreads;
-      uint64_t wn[PF][1];
-      uint32_t vn = 0;
-      auto load = [&](uint64_t base) {
-        vn = 0;
-#pragma unroll
-        for (int q = 0; q < PF; ++q) {
-          const uint64_t li = base + (uint64_t)q * kCThreads + tid;
-          wn[q][0] = li < nrec ? src[li] : 0ULL;
-          vn |= (li < nrec ? 1u : 0u) << q;
-        }
-      };
-      load(STEP);
+    if (rest) {
       for (uint64_t base = STEP; base < nrec; base += STEP) {
         uint64_t w[PF][1];
 #pragma unroll
-        for (int q = 0; q < PF; ++q) w[q][0] = wn[q][0];
-        const uint32_t valid = vn;
-        if (base + STEP < nrec) load(base + STEP);
-        insert_round(w, valid, []() {});
+        for (int q = 0; q < PF; ++q) w[q][0] = pf.w[q][0];
+        const uint32_t valid = pf.valid;
+        const bool last = base + STEP >= nrec;
+        if (!last) load(base + STEP);
+        insert_round(w, valid, [&]() {
+          if (last) issue_next();
+        });
       }
     }
     __syncthreads();  //                                                            [barrier 1]
@@ -3700,7 +3859,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     const uint32_t n = s_n[par];
     const uint64_t sc = s_spec[par];
     // PK: any count field at risk, or a partition longer than the list: the two-word kernel
-    const bool overflow = s_ovf[par] != 0 || n > (uint32_t)(KT * 7 / 8) ||
+    const bool overflow = s_ovf[par] != 0 || (!scan_stats && n > (uint32_t)(KT * 7 / 8)) ||
                           (PK && nrec > (uint64_t)KL);
     const bool sub = f != 0;  // a recount subset: several work items add to one partition
     const bool cand = a.want_cand && f == 0 && !overflow;
@@ -3722,24 +3881,34 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
     }
     const uint64_t obase = a.group_stride ? (uint64_t)wi * a.group_stride : r0 + gbase;
 
-    // statistics over the list, clearing the table
-    uint64_t un = 0, mx = 0;
+    // statistics over the list, clearing the table.  Per group: a count-1 test and a 32-bit
+    // count; counts above 1 (rare in a high-cardinality key) take the branch with the histogram,
+    // the entropy term and the candidate insertion; a PK key is rebuilt from its packed word only
+    // where it is kept (materialised groups, candidates)
+    uint32_t un = 0;
+    bool gt1 = false;  // some count of this lane's groups exceeds 1
     uint64_t tc[kCand], tk[kCand];  // this lane's top groups with count > 1
 #pragma unroll
     for (int q = 0; q < kCand; ++q) tc[q] = tk[q] = 0;
-    uint64_t k1 = 0;  // a count-1 group of this lane (k1c: present)
+    uint64_t k1 = 0;  // a count-1 group of this lane (k1c: present; PK: its packed word)
     bool k1c = false;
+    // k: the key, or (PK) the packed slot word, rebuilt by key_of
+    auto key_of = [&](uint64_t k) -> uint64_t { return PK ? (((uint64_t)p << KB) | (k & MK)) : k; };
     auto stat = [&](uint32_t i, uint64_t k, uint64_t c) {
-      if (keep) a.groups[obase + i] = Group{k, c, 0};
-      if (c == 1) ++un;
-      else if (c < kSmallCounts) atomicAdd(&s_chist[par][c], 1u);
-      else atomic_add_fix(&s_efix[par][0], fix_of(entropy_term(c, a.num_rows)));  // (rare)
-      mx = c > mx ? c : mx;
-      if (cand) {
-        if (c == 1) {
-          if (!k1c) k1 = k;
-          k1c = true;
-        } else if (c > tc[kCand - 1]) {
+#if DQ_C_EXPERIMENT & 1  // (timing experiment only: no statistics)
+      return;
+#endif
+      if (keep) a.groups[obase + i] = Group{key_of(k), c, 0};
+      if (c == 1) {
+        ++un;
+        if (cand && !k1c) k1 = k;
+        k1c = true;
+      } else {
+        gt1 = true;
+        if (c < kSmallCounts) atomicAdd(&s_chist[par][c], 1u);
+        else atomic_add_fix(&s_efix[par][0], fix_of(entropy_term(c, a.num_rows)));  // (rare)
+        if (cand && c > tc[kCand - 1]) {
+          k = key_of(k);
 #pragma unroll
           for (int q = 0; q < kCand; ++q) {
             if (c > tc[q]) {
@@ -3753,13 +3922,39 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
         }
       }
     };
-    {  // the first 4 entries per thread with all their LDS reads in flight, then the rest
+    uint32_t gn = 0;  // scan_stats: this lane's groups
+    if (scan_stats) {
+      static_assert(!PK || KT % (2 * CT) == 0, "whole 16-byte pairs per thread");
+      constexpr int J = PK ? KT / (2 * CT) : 2, JH = J / 2;  // (two halves: registers)
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        ulonglong2 v[JH];
+#pragma unroll
+        for (int j = 0; j < JH; ++j) v[j] = reinterpret_cast<const ulonglong2*>(tkey)[(half * JH + j) * CT + tid];
+#pragma unroll
+        for (int j = 0; j < JH; ++j)
+          reinterpret_cast<ulonglong2*>(tkey)[(half * JH + j) * CT + tid] = make_ulonglong2(kEmptyKey, kEmptyKey);
+        if (!overflow) {
+#pragma unroll
+          for (int j = 0; j < JH; ++j) {
+            if (v[j].x != kEmptyKey) {
+              ++gn;
+              stat(0, v[j].x, v[j].x >> KB);
+            }
+            if (v[j].y != kEmptyKey) {
+              ++gn;
+              stat(0, v[j].y, v[j].y >> KB);
+            }
+          }
+        }
+      }
+    } else {  // the first 4 entries per thread with all their LDS reads in flight, then the rest
       constexpr int U = 4;
       uint32_t sl[U];
       uint64_t kv[U], cv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t i = tid + (uint32_t)u * kCThreads;
+        const uint32_t i = tid + (uint32_t)u * CT;
         sl[u] = i < n ? list[i] : 0u;
       }
 #pragma unroll
@@ -3769,40 +3964,34 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t i = tid + (uint32_t)u * kCThreads;
+        const uint32_t i = tid + (uint32_t)u * CT;
         if (i < n) {
           tkey[sl[u]] = kEmptyKey;
           if (!PK) tcnt[sl[u]] = 0;
         }
-        if (PK) {  // unpack: the partition's 19 fixed hash bits over the key's 45
-          cv[u] = kv[u] >> KB;
-          kv[u] = ((uint64_t)p << KB) | (kv[u] & MK);
-        }
+        if (PK) cv[u] = kv[u] >> KB;  // (the key stays packed: key_of)
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t i = tid + (uint32_t)u * kCThreads;
+        const uint32_t i = tid + (uint32_t)u * CT;
         if (i < n && !overflow) stat(i, kv[u], cv[u]);
       }
-      for (uint32_t i = tid + (uint32_t)U * kCThreads; i < n; i += kCThreads) {
+      for (uint32_t i = tid + (uint32_t)U * CT; i < n; i += CT) {
         const uint32_t s = list[i];
         uint64_t kk = tkey[s], c = PK ? 0 : tcnt[s];
         tkey[s] = kEmptyKey;
         if (!PK) tcnt[s] = 0;
-        if (PK) {
-          c = kk >> KB;
-          kk = ((uint64_t)p << KB) | (kk & MK);
-        }
+        if (PK) c = kk >> KB;
         if (!overflow) stat(i, kk, c);
       }
     }
-    if (tid == 0 && sc && !overflow) stat(n, kEmptyKey, sc);
-    const uint64_t wmx1 = __ockl_wfred_max_u64(mx);
-    if (cand && wmx1 <= 1) {  // every count of the wave is 1: its first four count-1 groups
+    if (tid == 0 && sc && !overflow) stat(n, kEmptyKey, sc);  // (!PK only: PK never counts sc)
+    const bool wgt1 = __ballot(gt1) != 0;
+    if (cand && !wgt1) {  // every count of the wave is 1: its first four count-1 groups
       const uint64_t bal = __ballot(k1c);
       const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ULL << lane) - 1ULL));
       if (k1c && rank < (uint32_t)kCand) {
-        s_wk[par][wave][rank] = k1;
+        s_wk[par][wave][rank] = key_of(k1);
         s_wc[par][wave][rank] = 1;
       }
       if (lane < kCand && (uint32_t)lane >= (uint32_t)__builtin_popcountll(bal)) s_wc[par][wave][lane] = 0;
@@ -3819,7 +4008,7 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
                                 : (one ? (1ULL << 8) | ((uint64_t)lane << 2) | 3ULL : 0ULL);
         const uint64_t wm = __ockl_wfred_max_u64(mine);
         if (wm && wm == mine) {
-          uint64_t kk = k1, cc = 1;
+          uint64_t kk = key_of(k1), cc = 1;
           if (!one) {
 #pragma unroll
             for (int i2 = 0; i2 < kCand; ++i2) {
@@ -3838,11 +4027,12 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC_x(CArgs a) {
       }
     }
     {
-      const uint64_t wun = __ockl_wfred_add_u64(un);
-      const uint64_t wmx = wmx1;
+      const uint32_t wun = __ockl_wfred_add_u32(un);
+      const uint32_t wgn = scan_stats ? __ockl_wfred_add_u32(gn) : 0u;
       if (lane == 0) {
+        s_wgn[par][wave] = wgn;
         s_wun[par][wave] = wun;
-        s_wmax[par][wave] = wmx;
+        s_wmax[par][wave] = wgt1 ? 2u : 0u;  // (> 1: some count above 1)
       }
     }
     __syncthreads();  //                                                            [barrier 2]
@@ -5122,8 +5312,11 @@ static dq_status finalize_b(dq_freq* f) {
   // record counts within the count field) and hold <= kTargetPk records on average -- packed
   // slots take up to 4096 -- so phase C's per-item costs cover twice the records (configs[2]
   // 24.75 -> 24.2 ms); a shallower table would fall to the two-word slots (configs[4] +29 ms)
-  constexpr uint64_t kTargetPk = 3700;
-  if (f->exact && !getenv("DQ_FREQ_PARTITION_TARGET"))
+  static const uint64_t kTargetPk = [] {  // DQ_FREQ_TARGET_PK: A/B hook (0: no shallower step)
+    const char* e = getenv("DQ_FREQ_TARGET_PK");
+    return e ? (uint64_t)std::max(0, atoi(e)) : (uint64_t)3700;
+  }();
+  if (f->exact && !getenv("DQ_FREQ_PARTITION_TARGET") && kTargetPk)
     while (s - 1 >= kMinPkSubBits && ((uint64_t)kBuckets << (s - 1)) * kTargetPk >= R &&
            f->h_counters[C_MAXCNT] < (1ULL << (s - 1 - 3)))
       --s;
@@ -5337,6 +5530,16 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     }
     HIP_TRY(f->ovf_a.ensure(2 * P));
     HIP_TRY(hipMemsetAsync(f->ovf_n.p, 0, 4, f->stream));
+    static const bool no_bcache = [] {  // DQ_FREQ_CBCACHE=0: A/B hook, scalar bounds per item
+      const char* e = getenv("DQ_FREQ_CBCACHE");
+      return e && atoi(e) == 0;
+    }();
+    a.bcache = !no_bcache && f->R < (1ULL << 32) ? 1u : 0u;
+    static const bool no_contig = [] {  // DQ_FREQ_CCONTIG=0: A/B hook, strided phase-C items
+      const char* e = getenv("DQ_FREQ_CCONTIG");
+      return e && atoi(e) == 0;
+    }();
+    a.contig = no_contig ? 0u : 1u;
     a.entries = nullptr;
     a.ovf_out = f->ovf_a.p;
     a.ovf_n = f->ovf_n.p;
@@ -5370,12 +5573,14 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     for (int round = 0; round < 24; ++round) {
       // packed slots: the first pass of a table partitioned to the full depth (19 fixed bits)
       const bool pk = round == 0 && pk_ok(f) && !no_pk;
+      // (packed: one 1024-thread workgroup per CU)
+      const unsigned grid_pk = (unsigned)std::min<int64_t>(P, std::max(1, cus));
       if (f->exact && !old_c && clk && pk)
-        hipLaunchKernelGGL((freq_phaseC_x<true, true>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
+        hipLaunchKernelGGL((freq_phaseC_x<true, true>), dim3(grid_pk), dim3(kCThreadsX<true>), 0, f->stream, a);
       else if (f->exact && !old_c && clk)
         hipLaunchKernelGGL((freq_phaseC_x<true, false>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else if (f->exact && !old_c && pk)
-        hipLaunchKernelGGL((freq_phaseC_x<false, true>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
+        hipLaunchKernelGGL((freq_phaseC_x<false, true>), dim3(grid_pk), dim3(kCThreadsX<true>), 0, f->stream, a);
       else if (f->exact && !old_c)
         hipLaunchKernelGGL((freq_phaseC_x<false, false>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else if (f->exact)

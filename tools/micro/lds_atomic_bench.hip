@@ -4,7 +4,10 @@
 #include <cstdio>
 #include <cstdint>
 
-constexpr int KT = 4096, T = 512, ROUNDS = 256;
+#ifndef KTS
+#define KTS 8192
+#endif
+constexpr int KT = KTS, T = 512, ROUNDS = 256;
 
 __device__ __forceinline__ uint64_t mix(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ULL; x ^= x >> 33;
@@ -13,9 +16,11 @@ __device__ __forceinline__ uint64_t mix(uint64_t x) {
 
 template <int MODE>
 __global__ void __launch_bounds__(T, 4) k(unsigned long long* out, int reps) {
-  __shared__ unsigned long long tab[KT];
-  __shared__ unsigned long long cnt[KT];
-  __shared__ uint32_t tab32[KT];
+  // one 64 KB region (two workgroups per CU, as phase C): the arrays alias (a rate benchmark)
+  __shared__ unsigned long long buf[KT];
+  unsigned long long* tab = buf;
+  unsigned long long* cnt = buf;
+  uint32_t* tab32 = reinterpret_cast<uint32_t*>(buf);
   for (int i = threadIdx.x; i < KT; i += T) { tab[i] = ~0ULL; cnt[i] = 0; tab32[i] = ~0u; }
   __syncthreads();
   unsigned long long acc = 0;
@@ -55,6 +60,9 @@ __global__ void __launch_bounds__(T, 4) k(unsigned long long* out, int reps) {
     } else if (MODE == 5) {  // add32 no return only
 #pragma unroll
       for (int q = 0; q < 4; ++q) atomicAdd(&tab32[sl[q]], 1u);
+    } else if (MODE == 6) {  // the hashing alone
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc += h[q] ^ sl[q];
     }
     if ((r & 15) == 15) {  // keep the table from filling (reset every 16 rounds)
       __syncthreads();
@@ -68,11 +76,11 @@ __global__ void __launch_bounds__(T, 4) k(unsigned long long* out, int reps) {
 int main() {
   unsigned long long* out;
   hipMalloc(&out, 8);
-  const char* names[] = {"cas64", "cas64+add64", "cas32", "rw64", "add64", "add32"};
+  const char* names[] = {"cas64", "cas64+add64", "cas32", "rw64", "add64", "add32", "hash-only"};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int mode = 0; mode < 6; ++mode) {
+  for (int mode = 0; mode < 7; ++mode) {
     for (int it = 0; it < 2; ++it) {
       hipEventRecord(e0);
       switch (mode) {
@@ -82,6 +90,7 @@ int main() {
         case 3: hipLaunchKernelGGL(k<3>, dim3(512), dim3(T), 0, 0, out, ROUNDS); break;
         case 4: hipLaunchKernelGGL(k<4>, dim3(512), dim3(T), 0, 0, out, ROUNDS); break;
         case 5: hipLaunchKernelGGL(k<5>, dim3(512), dim3(T), 0, 0, out, ROUNDS); break;
+        case 6: hipLaunchKernelGGL(k<6>, dim3(512), dim3(T), 0, 0, out, ROUNDS); break;
       }
       hipEventRecord(e1);
       hipEventSynchronize(e1);
