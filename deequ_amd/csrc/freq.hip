@@ -3496,7 +3496,11 @@ __global__ void __launch_bounds__(kCThreadsX<PK>, 4) freq_phaseC_x(CArgs a) {
   // load took ~11 of them per item, one round at <= 25 % takes ~4.
   constexpr int CT = kCThreadsX<PK>;
   constexpr int KT = PK ? 16384 : FM<false>::kTableC, NW = CT / 64, PF = kPF<false>;
-  constexpr int KL = PK ? 4096 : KT;  // list capacity
+  // list capacity = most records of a packed item: two insert rounds of PF * CT, the table then
+  // at most half full.  (Items of ~7,300 records -- kTargetPk 7400, one level shallower -- ran
+  // phase C in the same time as ~3,600 in one round, 6.46 ms both, profiles/r6n: half the items'
+  // fixed costs against longer probe chains at twice the load; ~1,800 took 9.2 ms, r6l.)
+  constexpr int KL = PK ? 2 * PF * CT : KT;
   // PK: the partition fixes the hash's top 9 + s bits, the slot keeps the other KB = 55 - s
   // (45..48 for s = 10..7) under a count field of 9 + s bits
   const int KB = 55 - (int)a.s;
@@ -3725,8 +3729,10 @@ __global__ void __launch_bounds__(kCThreadsX<PK>, 4) freq_phaseC_x(CArgs a) {
         // The lane's records move through a shift register (a PK first pass has no hash filter,
         // so its pending records are a prefix of the PF); the slots it claims go to cl[0..ncl)
         // (then to the list below, as `mine` bits 0..ncl-1 over slot[]).
-        uint64_t ch = h[0], ca = c[0] << KB;
-        uint32_t cs = slot[0], cst = step[0];
+        // (a record's slot, step and count add all come from its packed word: slot = bits 0..13,
+        // step = bits 30..43 | 1, add = the count field -- only the words ride the shift register)
+        uint64_t ch = h[0];
+        uint32_t cs = (uint32_t)ch & (KT - 1), cst = ((uint32_t)(ch >> 30) | 1u) & (KT - 1);
         uint32_t rest = todo >> 1, ncl = 0, cl[PF];
 #pragma unroll
         for (int x = 0; x < PF; ++x) cl[x] = 0;
@@ -3735,7 +3741,7 @@ __global__ void __launch_bounds__(kCThreadsX<PK>, 4) freq_phaseC_x(CArgs a) {
           const uint64_t o = atomicCAS((unsigned long long*)&tkey[cs], kEmptyKey, ch);
           const bool e = o == kEmptyKey;
           const bool m = !e && ((o ^ ch) & MK) == 0;
-          if (m) atomicAdd((unsigned long long*)&tkey[cs], (unsigned long long)ca);
+          if (m) atomicAdd((unsigned long long*)&tkey[cs], (unsigned long long)(ch & ~MK));
           if (e || m) {
             if (e) {
 #pragma unroll
@@ -3745,16 +3751,10 @@ __global__ void __launch_bounds__(kCThreadsX<PK>, 4) freq_phaseC_x(CArgs a) {
             act = (rest & 1u) != 0;
             rest >>= 1;
             ch = h[1];
-            ca = c[1] << KB;
-            cs = slot[1];
-            cst = step[1];
+            cs = (uint32_t)ch & (KT - 1);
+            cst = ((uint32_t)(ch >> 30) | 1u) & (KT - 1);
 #pragma unroll
-            for (int x = 1; x + 1 < PF; ++x) {
-              h[x] = h[x + 1];
-              c[x] = c[x + 1];
-              slot[x] = slot[x + 1];
-              step[x] = step[x + 1];
-            }
+            for (int x = 1; x + 1 < PF; ++x) h[x] = h[x + 1];
           } else {
             cs = (cs + cst) & (KT - 1);
           }
@@ -3834,26 +3834,26 @@ __global__ void __launch_bounds__(kCThreadsX<PK>, 4) freq_phaseC_x(CArgs a) {
       c_fetch<false, CT>(a, wmap(item + 1), nb, pf);
       if (!bcache) c_bounds(a, wmap(item + 2), nb2);
     };
-    insert_round(cur.w, too_long ? 0u : cur.valid, [&]() {
-      if (rest) load(STEP);
-      else issue_next();
-    });
+    // One insert round per STEP records, all through ONE inlined insert_round (two copies, the
+    // first round and the rest, spilled the kernel): each round's issue slot loads the next round's
+    // words into pf, or -- in the last round -- prefetches the next item there.
+    {
+      uint32_t valid = too_long ? 0u : cur.valid;
+      for (uint64_t base = 0;; base += STEP) {
+        const bool last = !rest || base + STEP >= nrec;
+        insert_round(cur.w, valid, [&]() {
+          if (last) issue_next();
+          else load(base + STEP);
+        });
+        if (last) break;
+#pragma unroll
+        for (int q = 0; q < PF; ++q) cur.w[q][0] = pf.w[q][0];  // (cur's words are dead after decode)
+        valid = pf.valid;
+      }
+    }
     // the last item's outputs, after this wave's inserts (its records are no longer live; the
     // stores come after the prefetch, so the next item's wait for its records leaves them be)
     if (wave < 2) tail(par ^ 1u, wave);
-    if (rest) {
-      for (uint64_t base = STEP; base < nrec; base += STEP) {
-        uint64_t w[PF][1];
-#pragma unroll
-        for (int q = 0; q < PF; ++q) w[q][0] = pf.w[q][0];
-        const uint32_t valid = pf.valid;
-        const bool last = base + STEP >= nrec;
-        if (!last) load(base + STEP);
-        insert_round(w, valid, [&]() {
-          if (last) issue_next();
-        });
-      }
-    }
     __syncthreads();  //                                                            [barrier 1]
     mark(1);
     const uint32_t n = s_n[par];
