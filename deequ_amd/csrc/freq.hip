@@ -59,6 +59,9 @@
 #ifndef DQ_C_EXPERIMENT  // timing builds only (wrong results): 1 no statistics, 2 no inserts
 #define DQ_C_EXPERIMENT 0
 #endif
+#ifndef DQ_A_NOCOPY  // timing builds only (wrong results): phase A writes no arena key bytes
+#define DQ_A_NOCOPY 0
+#endif
 
 namespace dq {
 
@@ -661,9 +664,9 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
     const uint64_t off = s_arena_base + atomicAdd(&s_arena_cur, (unsigned long long)sz);
     if constexpr (STR1) {
       const SView v = str1_view(a.ks, row);
-      str1_encode_copy(v.p, v.len, reinterpret_cast<uint32_t*>(a.arena + off));
+      if (!DQ_A_NOCOPY) str1_encode_copy(v.p, v.len, reinterpret_cast<uint32_t*>(a.arena + off));
     } else {
-      row_encode_dw(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
+      if (!DQ_A_NOCOPY) row_encode_dw(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
     }
     return off;
   };
@@ -679,7 +682,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
       if (k1 != kNoShort) {
         const uint64_t off = s_arena_base +
             atomicAdd(&s_arena_cur, (unsigned long long)(8 + pad4(str1_short_len(k1))));
-        str1_encode_short(k0, k1, reinterpret_cast<uint32_t*>(a.arena + off));
+        if (!DQ_A_NOCOPY) str1_encode_short(k0, k1, reinterpret_cast<uint32_t*>(a.arena + off));
         return off;
       }
     }
@@ -1196,7 +1199,7 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wbase, 63);
           if (!on) continue;
           const uint64_t off = s_arena_base + wbase + (incl - sz);
-          str2_encode(a.ks, x[g], reinterpret_cast<uint32_t*>(a.arena + off));
+          if (!DQ_A_NOCOPY) str2_encode(a.ks, x[g], reinterpret_cast<uint32_t*>(a.arena + off));
           put(t, stash[q * W], 1u, off);
         }
       }
@@ -1222,13 +1225,13 @@ __global__ void __launch_bounds__((AKeys<HASHED, FROM_REC>::kThreads),
         const uint64_t off = s_arena_base + wbase + (incl - sz);
         if constexpr (STR1) {
           if (k1 != kNoShort) {
-            str1_encode_short16(k0, k1, reinterpret_cast<uint32_t*>(a.arena + off));
+            if (!DQ_A_NOCOPY) str1_encode_short16(k0, k1, reinterpret_cast<uint32_t*>(a.arena + off));
           } else {
-            str1_encode_copy16(a.ks.cols[0].data + (uint32_t)k0, (int32_t)(k0 >> 32),
+            if (!DQ_A_NOCOPY) str1_encode_copy16(a.ks.cols[0].data + (uint32_t)k0, (int32_t)(k0 >> 32),
                                reinterpret_cast<uint32_t*>(a.arena + off));
           }
         } else {
-          row_encode_dw(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
+          if (!DQ_A_NOCOPY) row_encode_dw(a.ks, row, reinterpret_cast<uint32_t*>(a.arena + off));
         }
         if (STR1 && hpieces) put_pieces(t, stash[q * W], 1u, off);
         else put(t, stash[q * W], 1u, off);  // (row keys: one record, the count-1 digit code)
@@ -4945,6 +4948,10 @@ static hipError_t grow_keep(DevBuf<T>& b, size_t used, size_t need, hipStream_t 
   DevBuf<T> nb;
   hipError_t e = nb.ensure(std::max(need, b.n * 2));
   if (e != hipSuccess) return e;
+#if DQ_A_NOCOPY  // (timing build: the never-written arena reads as zero words, so every key is 4 bytes)
+  e = hipMemsetAsync(nb.p, 0, nb.n * sizeof(T), st);
+  if (e != hipSuccess) return e;
+#endif
   if (used) {
     e = hipMemcpyAsync(nb.p, b.p, used * sizeof(T), hipMemcpyDeviceToDevice, st);
     if (e != hipSuccess) return e;
