@@ -146,15 +146,33 @@ DQ_DEV int64_t load_i64(int type, const void* v, int64_t r) {
 DQ_HD bool is_float_type(int type) { return type == DQ_FLOAT32 || type == DQ_FLOAT64; }
 
 // Spark XxHash64Function.hash(value, type, 42) for one non-null row.
+// A decimal row, out of line: inlined into the unrolled HLL loops (8 copies in the fused
+// Correlation + HLL body) its BigInteger byte hashing spilled 272 bytes per lane and took
+// configs[3] from 4.0 to 7.2 ms per step (round 6); a call on this rare path costs them nothing.
+static __device__ __attribute__((noinline)) uint64_t hash_row_decimal(int type, const void* values,
+                                                                      int64_t r) {
+  const uint64_t* v = reinterpret_cast<const uint64_t*>(values) + 2 * r;
+  return dec_hash(v[0], (int64_t)v[1], DQ_DECIMAL_PRECISION(type), 42);
+}
+
+// hash_row for the only columns the fused Correlation + HLL body takes (api.cpp: 8-byte int64 /
+// float64 columns): the general switch's other cases cost that unrolled body registers
+DQ_DEV uint64_t hash_wide(int type, const void* values, int64_t r) {
+  const uint64_t v = reinterpret_cast<const uint64_t*>(values)[r];
+  if (type == DQ_FLOAT64) {
+    const double d = __builtin_bit_cast(double, v);
+    return xxh_long(d != d ? 0x7ff8000000000000ULL : v, 42);  // doubleToLongBits
+  }
+  return xxh_long(v, 42);
+}
+
 DQ_DEV uint64_t hash_row(int type, const void* values, const uint8_t* data, int64_t r) {
   const uint64_t seed = 42;
-  switch (DQ_TYPE_ID(type)) {
-    case DQ_DATE32: return xxh_int((uint32_t)reinterpret_cast<const int32_t*>(values)[r], seed);
-    case DQ_TIMESTAMP_US: return xxh_long((uint64_t)reinterpret_cast<const int64_t*>(values)[r], seed);
-    case DQ_DECIMAL128: {
-      const uint64_t* v = reinterpret_cast<const uint64_t*>(values) + 2 * r;
-      return dec_hash(v[0], (int64_t)v[1], DQ_DECIMAL_PRECISION(type), seed);
-    }
+  int tid = DQ_TYPE_ID(type);
+  // dates hash as Spark's IntegerType, timestamps as LongType (their physical values)
+  tid = tid == DQ_DATE32 ? DQ_INT32 : tid == DQ_TIMESTAMP_US ? DQ_INT64 : tid;
+  switch (tid) {
+    case DQ_DECIMAL128: return hash_row_decimal(type, values, r);
     case DQ_INT8: return xxh_int((uint32_t)(int32_t)reinterpret_cast<const int8_t*>(values)[r], seed);
     case DQ_INT16:
       return xxh_int((uint32_t)(int32_t)reinterpret_cast<const int16_t*>(values)[r], seed);

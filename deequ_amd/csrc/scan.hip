@@ -807,7 +807,7 @@ DQ_DEV void corr_rows(const TaskDesc& t, int64_t r_begin, int64_t r_end, Acc& ac
           if constexpr (HLL) {
             const bool hy = t.hll_side != 0;
             if (bit1(hy ? t.valid2 : t.valid, r) & wm)
-              hll_update(regs, hash_row(hy ? t.type2 : t.type, hy ? t.values2 : t.values, nullptr, r));
+              hll_update(regs, hash_wide(hy ? t.type2 : t.type, hy ? t.values2 : t.values, r));
           }
         }
       }

@@ -9,6 +9,6 @@ O=gpurun_out
 T=${TAG:-r3}
 mkdir -p $O
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > $O/bench_$T.json 2> $O/bench_$T.err &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$T -o run -- python3 bench.py --steps 10 --warmup 2 --no-h2d --no-cpu-baseline > $O/prof_$T.log 2>&1 &&
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$T -o run -- python3 bench.py --steps 3 --warmup 1 --no-h2d --no-cpu-baseline > $O/pmc_fetch_$T.log 2>&1 &&
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$T -o run -- python3 bench.py --steps 3 --warmup 1 --no-h2d --no-cpu-baseline > $O/pmc_write_$T.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$T -o run -- python3 bench.py --steps 10 --warmup 2 --no-h2d --no-cpu-baseline --workloads '' > $O/prof_$T.log 2>&1 &&
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch_$T -o run -- python3 bench.py --steps 3 --warmup 1 --no-h2d --no-cpu-baseline --workloads '' > $O/pmc_fetch_$T.log 2>&1 &&
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write_$T -o run -- python3 bench.py --steps 3 --warmup 1 --no-h2d --no-cpu-baseline --workloads '' > $O/pmc_write_$T.log 2>&1
