@@ -59,6 +59,9 @@
 #ifndef DQ_C_EXPERIMENT  // timing builds only (wrong results): 1 no statistics, 2 no inserts
 #define DQ_C_EXPERIMENT 0
 #endif
+#ifndef DQ_AX_EXPERIMENT  // timing builds only (wrong results): freq_phaseA_xp 1 no record stores,
+#define DQ_AX_EXPERIMENT 0  // 2 no counting sort (records in row order), 3 neither
+#endif
 #ifndef DQ_A_NOCOPY  // timing builds only (wrong results): phase A writes no arena key bytes
 #define DQ_A_NOCOPY 0
 #endif
@@ -1604,6 +1607,15 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
         }
       }
       if (!__syncthreads_or(raw ? 1 : 0)) continue;  // every row collapsed: nothing to write
+#if DQ_AX_EXPERIMENT & 2  // (timing only: no counting sort -- the tile's records in row order)
+      {
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+          if (!(DQ_AX_EXPERIMENT & 1) && ((raw >> j) & 1u))
+            out[a.piece_base + (uint64_t)t * T + (uint64_t)(j * kAXThreads + tid)] = (h[j] << 8) | 1u;
+        continue;
+      }
+#endif
       // 3. counting sort by bucket: the counting atomic gives each raw row its rank
       uint32_t rk[R];
 #pragma unroll
@@ -1644,8 +1656,11 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
         for (uint32_t i = tid; i < ctotal; i += kAXThreads) {
           const uint64_t hh = stash[i];
           const uint32_t b = bucket_of(hh);
-          out[(uint32_t)((i < bh[b] ? gdel[b] : odel[b]) + i)] = (hh << 8) | 1u;
+          if (!(DQ_AX_EXPERIMENT & 1))  // (timing builds: 1 = no record stores)
+            out[(uint32_t)((i < bh[b] ? gdel[b] : odel[b]) + i)] = (hh << 8) | 1u;
         }
+        // (an unrolled form -- every round's stash words, then destinations, then stores --
+        // spilled the kernel at every batch size tried; not adopted)
       } else {
         for (uint32_t i = tid; i < ctotal; i += kAXThreads) {
           const uint64_t hh = stash[i];
