@@ -3505,15 +3505,19 @@ __global__ void __launch_bounds__(kCThreads, 4) freq_phaseC(CArgs a) {
 // bits can only overflow when some record carries a count >= 2^(s-3) (128 at s = 10) or the
 // partition has more than 4096 records; such an item is handed on (an ovf entry of the whole
 // partition, f = 0) to the two-word kernel.  (s = 7..9: the configs[4]-sized tables.)
-template <bool DBG, bool PK>
-__global__ void __launch_bounds__(kCThreadsX<PK>, 4) freq_phaseC_x(CArgs a) {
-  // PK: one 1024-thread workgroup per CU over a 16384-slot table (128 KB of LDS): an item of up
-  // to 4096 records is inserted in ONE round at a load factor <= 1/4.  The probe rounds are a
-  // chain of LDS atomic round trips (~600 cycles each under load: tools/micro/lds_insert_bench),
-  // and a round takes as many as its wave's longest probe sequence -- two rounds at up to 44 %
-  // load took ~11 of them per item, one round at <= 25 % takes ~4.
-  constexpr int CT = kCThreadsX<PK>;
-  constexpr int KT = PK ? 16384 : FM<false>::kTableC, NW = CT / 64, PF = kPF<false>;
+template <bool DBG, bool PK, bool BIG = false>
+__global__ void __launch_bounds__(kCThreadsX<PK && BIG>, 4) freq_phaseC_x(CArgs a) {
+  // PK && BIG (partitions of more than 2048 records on average: configs[2]'s 1e9-row keys): one
+  // 1024-thread workgroup per CU over a 16384-slot table (128 KB of LDS), so an item of up to 4096
+  // records is inserted in ONE round at a load factor <= 1/4.  The probe rounds are a chain of LDS
+  // atomic round trips (~600 cycles each under load: tools/micro/lds_insert_bench), and a round
+  // takes as many as its wave's longest probe sequence -- two rounds at up to 44 % load took ~11
+  // of them per item, one round at <= 25 % takes ~4.  Smaller partitions (configs[4]'s 1.25e8
+  // rows: ~1,800 records) keep two 512-thread workgroups per CU over 8192 slots, one round each:
+  // there the 1024-thread form ran 1.73 against 1.05 ms per table (profiles/r6p vs r5zi), its
+  // per-item costs spread over half the records.
+  constexpr int CT = kCThreadsX<PK && BIG>;
+  constexpr int KT = PK ? (BIG ? 16384 : 8192) : FM<false>::kTableC, NW = CT / 64, PF = kPF<false>;
   // list capacity = most records of a packed item: two insert rounds of PF * CT, the table then
   // at most half full.  (Items of ~7,300 records -- kTargetPk 7400, one level shallower -- ran
   // phase C in the same time as ~3,600 in one round, 6.46 ms both, profiles/r6n: half the items'
@@ -5595,14 +5599,19 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     for (int round = 0; round < 24; ++round) {
       // packed slots: the first pass of a table partitioned to the full depth (19 fixed bits)
       const bool pk = round == 0 && pk_ok(f) && !no_pk;
-      // (packed: one 1024-thread workgroup per CU)
+      // (packed, partitions of > 2048 records on average: one 1024-thread workgroup per CU)
+      const bool big = pk && f->R > (uint64_t)P * 2048;
       const unsigned grid_pk = (unsigned)std::min<int64_t>(P, std::max(1, cus));
-      if (f->exact && !old_c && clk && pk)
-        hipLaunchKernelGGL((freq_phaseC_x<true, true>), dim3(grid_pk), dim3(kCThreadsX<true>), 0, f->stream, a);
+      if (f->exact && !old_c && clk && pk && big)
+        hipLaunchKernelGGL((freq_phaseC_x<true, true, true>), dim3(grid_pk), dim3(kCThreadsX<true>), 0, f->stream, a);
+      else if (f->exact && !old_c && clk && pk)
+        hipLaunchKernelGGL((freq_phaseC_x<true, true>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else if (f->exact && !old_c && clk)
         hipLaunchKernelGGL((freq_phaseC_x<true, false>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
+      else if (f->exact && !old_c && pk && big)
+        hipLaunchKernelGGL((freq_phaseC_x<false, true, true>), dim3(grid_pk), dim3(kCThreadsX<true>), 0, f->stream, a);
       else if (f->exact && !old_c && pk)
-        hipLaunchKernelGGL((freq_phaseC_x<false, true>), dim3(grid_pk), dim3(kCThreadsX<true>), 0, f->stream, a);
+        hipLaunchKernelGGL((freq_phaseC_x<false, true>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else if (f->exact && !old_c)
         hipLaunchKernelGGL((freq_phaseC_x<false, false>), dim3(grid), dim3(kCThreads), 0, f->stream, a);
       else if (f->exact)
