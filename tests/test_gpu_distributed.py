@@ -36,8 +36,10 @@ def test_two_ranks_reproduce_one_rank(gpu_device, tmp_path):
     codes = [p.wait(timeout=240) for p in procs]
     assert codes == [0, 0], codes
     got = json.loads(out.read_text())
-    # the device-side exchange equals the serialized all-gather + rank-ordered merge, byte for byte
-    assert got.pop("__exchange__") == [True, True]
+    # the device-side exchange equals the serialized all-gather + rank-ordered merge, byte for
+    # byte, and waits on the host once (the merged state's read-back) -- pack / unpack queue
+    # without a wait
+    assert got.pop("__exchange__") == [True, True, 1]
     assert set(got) == set(whole)
     for k, v in whole.items():
         g = got[k]

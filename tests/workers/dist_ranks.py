@@ -16,7 +16,9 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def exchange_check(df):
     """The scan states of the suite exchanged on the device (exchange_states: SUM / MAX
     all-reduces + the gathered moments merged by a kernel) and by the serialized all-gather +
-    rank-ordered host merge (merge_states_across_ranks): the merged states' bytes must agree."""
+    rank-ordered host merge (merge_states_across_ranks): the merged states' bytes must agree.
+    Also returns the engine's host waits during the device exchange (dq_host_wait_count): one,
+    the merged state's read-back (dq_state_sync)."""
     import ctypes
 
     from deequ_amd import _native as N
@@ -33,7 +35,9 @@ def exchange_check(df):
         N.check(N.lib.dq_state_create(plan.handle, 0, ctypes.byref(st)))
         scan_into(df, plan, st)
         if how == "device":
+            w0 = N.lib.dq_host_wait_count()
             row = exchange_states(plan, st, df.device)
+            waits = N.lib.dq_host_wait_count() - w0  # the engine's host waits in the exchange
             img = serialize_state(plan, st)
         else:
             row = merge_states_across_ranks(plan, st, df.device)
@@ -51,7 +55,7 @@ def exchange_check(df):
             N.lib.dq_state_destroy(tmp)
         N.lib.dq_state_destroy(st)
         out.append((img, repr(row)))
-    return [out[0][0] == out[1][0], out[0][1] == out[1][1]]
+    return [out[0][0] == out[1][0], out[0][1] == out[1][1], waits]
 
 
 def main():
