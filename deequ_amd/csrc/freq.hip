@@ -2448,6 +2448,12 @@ struct BArgs {
   uint32_t* uhist;                        // [unit][S]: counts (B1) -> offsets in the partition (B2)
   unsigned long long* part_base;          // [P + 1]
   uint8_t* recsB;
+  // capacity layout (cap_mode): each unit's run of partition p at atomicAdd(part_end[p], run),
+  // within part_base[p] + bcap[bucket]; a run past it sets *bovf and is not written
+  int32_t cap_mode;
+  unsigned long long* part_end;
+  const unsigned long long* bcap;
+  unsigned int* bovf;
 };
 
 struct UnitLds {
@@ -2789,7 +2795,20 @@ __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter_u(BArgs a) {
   const uint32_t ex = block_excl_scan(cnt, L.s_wave, tot);  // (barriers: every count is read)
   if (tid < S) {
     hcnt[tid] = ex;
-    gbs[tid] = a.part_base[(uint64_t)L.s_b * S + tid] + a.uhist[(int64_t)w * S + tid];
+    if (a.cap_mode) {  // (the unit's run of each partition: one device-scope cursor add per run)
+      const uint64_t p = (uint64_t)L.s_b * S + tid;
+      unsigned long long g = 0;
+      if (cnt) {
+        g = atomicAdd(&a.part_end[p], (unsigned long long)cnt);
+        if (g + cnt > a.part_base[p] + a.bcap[L.s_b]) {  // past the capacity: not written
+          atomicOr(a.bovf, 1u);
+          g = ~0ULL;
+        }
+      }
+      gbs[tid] = g;
+    } else {
+      gbs[tid] = a.part_base[(uint64_t)L.s_b * S + tid] + a.uhist[(int64_t)w * S + tid];
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -2806,10 +2825,28 @@ __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter_u(BArgs a) {
 #pragma unroll
     for (int x = 0; x < W; ++x) r[x] = staged[i * W + x];
     const uint32_t sb = rec_sub(r, a.s, HASHED);
+    if (gbs[sb] == ~0ULL) continue;  // (an overflowing run: the table falls back to the count)
     const unsigned long long d = gbs[sb] + (i - hcnt[sb]);
 #pragma unroll
     for (int x = 0; x < W; ++x) out[d * W + x] = r[x];
   }
+}
+
+// The capacity layout's partition starts (bucket base + sub-bucket x the bucket's capacity), and
+// its cursors, which the scatter's adds advance to the partitions' ends.
+__global__ void __launch_bounds__(256) freq_cap_layout(const unsigned long long* __restrict__ words,
+                                                       int s, int64_t P,
+                                                       unsigned long long* __restrict__ part_base,
+                                                       unsigned long long* __restrict__ part_end) {
+  const unsigned long long* bbase = words;              // [kBuckets + 1]
+  const unsigned long long* bcap = words + kBuckets + 1;  // [kBuckets]
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < P; p += (int64_t)gridDim.x * 256) {
+    const int64_t b = p >> s, sb = p & ((1LL << s) - 1);
+    const unsigned long long v = bbase[b] + (unsigned long long)sb * bcap[b];
+    part_base[p] = v;
+    part_end[p] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) part_base[P] = bbase[kBuckets];
 }
 
 // B3, whole units, persistent: workgroup g of an XCD takes that XCD's units g, g + G/8, ... and
@@ -2917,7 +2954,8 @@ __global__ void __launch_bounds__(kThreads) freq_phaseB_scatter_p(BArgs a) {
 // ------------------------------------------------------------------------------------------------
 struct CArgs {
   const uint8_t* recsB;
-  const unsigned long long* part_base;  // partition p's records: [part_base[p], part_base[p + 1])
+  const unsigned long long* part_base;  // partition p's records: [part_base[p], part_end[p])
+  const unsigned long long* part_end;   // (the counted layout: part_base + 1)
   int32_t s;
   int32_t n_work;                       // partitions (first pass) or entries (recount)
   const uint8_t* arena;
@@ -3013,8 +3051,9 @@ DQ_DEV void c_bounds(const CArgs& a, int wi, CBounds& bd) {
     bd.p = (uint32_t)wi;
   }
   cu64* pb = (cu64*)(size_t)a.part_base;
+  cu64* pe = (cu64*)(size_t)a.part_end;
   bd.r0 = pb[bd.p];
-  bd.r1 = pb[bd.p + 1];
+  bd.r1 = pe[bd.p];
 }
 
 // Work item wi (bounds bd): the raw words of its first kPF * kCThreads records.
@@ -3653,7 +3692,7 @@ __global__ void __launch_bounds__(kCThreadsX<PK && BIG>, 4) freq_phaseC_x(CArgs 
       const int64_t w = wmap(t0 + tid);
       uint32_t r0v = 0, nv = 0;
       if (w < a.n_work) {
-        const uint64_t x0 = a.part_base[w], x1 = a.part_base[w + 1];
+        const uint64_t x0 = a.part_base[w], x1 = a.part_end[w];
         r0v = (uint32_t)x0;
         nv = (uint32_t)(x1 - x0);
       }
@@ -4918,6 +4957,15 @@ struct dq_freq {
   DevBuf<uint32_t> unit_start, unit_c0, uhist;
   DevBuf<uint16_t> unit_b;
   DevBuf<unsigned long long> totals, part_base;
+  // Capacity layout (exact tables, finalize_b): partition p's records are [part_base[p],
+  // part_end[p]) inside a fixed capacity, filled through atomic cursors (no count pass).  The
+  // counted layout's ends are part_base + 1.  Rcap: the records region's size in records.
+  DevBuf<unsigned long long> part_end, cap_words;  // cap_words: bucket bases [kBuckets + 1], caps
+  DevBuf<unsigned int> b_ovf;
+  std::vector<unsigned long long> h_cap_words;
+  const unsigned long long* part_end_ptr = nullptr;
+  uint64_t Rcap = 0;
+  bool cap_failed = false;  // a capacity layout overflowed: this table counts from now on
   DevBuf<uint8_t> recsB;
   // (phase C)
   bool c_valid = false, c_groups = false, c_cand = false;
@@ -5289,6 +5337,8 @@ static dq_status finalize_b(dq_freq* f) {
   f->n_units = 0;
   HIP_TRY(f->part_base.ensure(kBuckets + 1));
   const int64_t J = n + f->n_prow;  // segment columns: chunks, then bucket pieces
+  f->part_end_ptr = f->part_base.p + 1;  // (the counted layout's ends)
+  f->Rcap = 0;
   if (J == 0) {
     HIP_TRY(hipMemsetAsync(f->part_base.p, 0, (kBuckets + 1) * 8, f->stream));
     f->b_valid = true;
@@ -5378,6 +5428,8 @@ static dq_status finalize_b(dq_freq* f) {
   }
   const int64_t P = (int64_t)kBuckets << s;
   HIP_TRY(f->part_base.ensure(P + 1));
+  f->part_end_ptr = f->part_base.p + 1;
+  f->Rcap = R;
   HIP_TRY(f->unit_start.ensure(kBuckets + 1));
   HIP_TRY(hipMemcpy(f->unit_start.p, f->h_unit_start.data(), (kBuckets + 1) * 4,
                     hipMemcpyHostToDevice));
@@ -5412,6 +5464,66 @@ static dq_status finalize_b(dq_freq* f) {
   a.uhist = f->uhist.p;
   a.part_base = f->part_base.p;
   a.recsB = f->recsB.p;
+  const unsigned grid = (u + 7) / 8 * 8;
+  constexpr uint64_t kUnitX = 16 * kThreads, kUnitH = 4 * kThreads;  // whole-unit capacities
+  static const int bsub = [] {  // DQ_FREQ_BSUB: A/B hook for the phase-B3 round size (0: whole units)
+    const char* e = getenv("DQ_FREQ_BSUB");
+    return e ? atoi(e) : 0;
+  }();
+  // one unit per workgroup (measured faster than the persistent form: exact, configs[2] 5.08 vs
+  // 5.61 ms; hashed, configs[4] 678 vs 826 us per launch once the segment window shares the
+  // staging LDS and two workgroups fit a CU).  DQ_FREQ_B3U=1 / DQ_FREQ_B3P=1: A/B hooks
+  static const int b3_env = [] {
+    const char* e = getenv("DQ_FREQ_B3U");
+    const char* p = getenv("DQ_FREQ_B3P");
+    return e && atoi(e) ? 1 : (p && atoi(p) ? 2 : 0);
+  }();
+  const bool b3u = b3_env != 2;
+  // Exact tables: the capacity layout, no count pass.  Every partition of bucket b gets room for
+  // mean + 8 sqrt(mean) + 32 records (a bijective hash spreads distinct keys uniformly: the
+  // overflow odds per partition are ~1e-15), the units' runs are placed by device-scope cursor
+  // adds, and a table whose runs overflow anyway (heavy keys whose records all land in one
+  // partition) is scattered again by the counted path below, and counts from then on.
+  static const bool no_capb = [] {  // DQ_FREQ_CAPB=0: A/B hook, always the counted layout
+    const char* e = getenv("DQ_FREQ_CAPB");
+    return e && atoi(e) == 0;
+  }();
+  if (f->exact && !no_capb && !f->cap_failed && bsub == 0 && b3u && H <= kUnitX / 2) {
+    std::vector<unsigned long long>& w = f->h_cap_words;
+    w.assign(2 * kBuckets + 1, 0ULL);
+    for (int b = 0; b < kBuckets; ++b) {
+      const double mean = (double)tot[b] / (double)S;
+      const unsigned long long cap = tot[b] ? (unsigned long long)std::ceil(mean + 8.0 * std::sqrt(mean) + 32.0) : 0ULL;
+      w[kBuckets + 1 + b] = cap;
+      w[b + 1] = w[b] + cap * (unsigned long long)S;
+    }
+    const uint64_t Rcap = w[kBuckets];
+    HIP_TRY(f->recsB.ensure(std::max<uint64_t>(Rcap, 1) * f->rb));
+    HIP_TRY(f->part_end.ensure(P));
+    HIP_TRY(f->cap_words.ensure(2 * kBuckets + 1));
+    HIP_TRY(f->b_ovf.ensure(1));
+    HIP_TRY(hipMemcpyAsync(f->cap_words.p, w.data(), w.size() * 8, hipMemcpyHostToDevice, f->stream));
+    HIP_TRY(hipMemsetAsync(f->b_ovf.p, 0, 4, f->stream));
+    hipLaunchKernelGGL(freq_cap_layout, dim3((unsigned)std::min<int64_t>((P + 255) / 256, 4096)), dim3(256),
+                       0, f->stream, f->cap_words.p, s, P, f->part_base.p, f->part_end.p);
+    a.cap_mode = 1;
+    a.recsB = f->recsB.p;
+    a.part_end = f->part_end.p;
+    a.bcap = f->cap_words.p + kBuckets + 1;
+    a.bovf = f->b_ovf.p;
+    hipLaunchKernelGGL((freq_phaseB_scatter_u<false, 8>), dim3(grid), dim3(kThreads), 0, f->stream, a);
+    HIP_TRY(hipGetLastError());
+    unsigned int ovf = 0;
+    HIP_TRY(d2h(&ovf, f->b_ovf.p, 4, f->stream));  // (one wait; C would wait for the scatter anyway)
+    if (!ovf) {
+      f->Rcap = Rcap;
+      f->part_end_ptr = f->part_end.p;
+      f->b_valid = true;
+      return DQ_OK;
+    }
+    f->cap_failed = true;  // the counted layout, now and for this table's next finalizes
+    a.cap_mode = 0;
+  }
   static const bool count_w = [] {  // DQ_FREQ_BCOUNT_WAVE=0: A/B hook, a workgroup per unit
     const char* e = getenv("DQ_FREQ_BCOUNT_WAVE");
     return !(e && atoi(e) == 0);
@@ -5440,21 +5552,6 @@ static dq_status finalize_b(dq_freq* f) {
                        f->part_base.p, P, f->scan_tmp.p);
   }
   HIP_TRY(hipGetLastError());
-  const unsigned grid = (u + 7) / 8 * 8;
-  static const int bsub = [] {  // DQ_FREQ_BSUB: A/B hook for the phase-B3 round size (0: whole units)
-    const char* e = getenv("DQ_FREQ_BSUB");
-    return e ? atoi(e) : 0;
-  }();
-  constexpr uint64_t kUnitX = 16 * kThreads, kUnitH = 4 * kThreads;  // whole-unit capacities
-  // one unit per workgroup (measured faster than the persistent form: exact, configs[2] 5.08 vs
-  // 5.61 ms; hashed, configs[4] 678 vs 826 us per launch once the segment window shares the
-  // staging LDS and two workgroups fit a CU).  DQ_FREQ_B3U=1 / DQ_FREQ_B3P=1: A/B hooks
-  static const int b3_env = [] {
-    const char* e = getenv("DQ_FREQ_B3U");
-    const char* p = getenv("DQ_FREQ_B3P");
-    return e && atoi(e) ? 1 : (p && atoi(p) ? 2 : 0);
-  }();
-  const bool b3u = b3_env != 2;
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, f->device);
   const unsigned pgrid = (unsigned)std::max(8, cus / 8 * 8);  // one per CU (LDS), XCD multiple
@@ -5526,7 +5623,8 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
   HIP_TRY(hipMemsetAsync(f->part_unique.p, 0, P * 8, f->stream));
   HIP_TRY(hipMemsetAsync(f->part_off.p, 0, P * 8, f->stream));
   HIP_TRY(hipMemsetAsync(f->part_entropy.p, 0, P * 16, f->stream));
-  if (want_groups) HIP_TRY(f->groups.ensure(std::max<uint64_t>(f->R, 1)));
+  // (groups materialise at their partition's record offsets: the records region's size)
+  if (want_groups) HIP_TRY(f->groups.ensure(std::max<uint64_t>(f->Rcap, 1)));
   if (want_cand) {
     HIP_TRY(f->cand.ensure((size_t)P * kCand));
     HIP_TRY(hipMemsetAsync(f->cand.p, 0, (size_t)P * kCand * sizeof(Group), f->stream));
@@ -5537,6 +5635,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     memset(&a, 0, sizeof(a));
     a.recsB = f->recsB.p;
     a.part_base = f->part_base.p;
+    a.part_end = f->part_end_ptr;
     a.s = f->s_bits;
     a.arena = arena_of(f);
     for (int k = 0; k < f->n_keys; ++k) a.types[k] = f->types[k];
@@ -5560,7 +5659,7 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
       const char* e = getenv("DQ_FREQ_CBCACHE");
       return e && atoi(e) == 0;
     }();
-    a.bcache = !no_bcache && f->R < (1ULL << 32) ? 1u : 0u;
+    a.bcache = !no_bcache && f->Rcap < (1ULL << 32) ? 1u : 0u;
     static const bool no_contig = [] {  // DQ_FREQ_CCONTIG=0: A/B hook, strided phase-C items
       const char* e = getenv("DQ_FREQ_CCONTIG");
       return e && atoi(e) == 0;
@@ -7216,6 +7315,7 @@ DQ_DEV uint64_t hll_value_hash(uint64_t v, int type) {  // v: the widened value 
 
 __global__ void __launch_bounds__(256) freq_hll_records(const uint64_t* __restrict__ recs,
                                                         const unsigned long long* __restrict__ part_base,
+                                                        const unsigned long long* __restrict__ part_end,
                                                         int64_t P, int s, int exact, int type,
                                                         const uint8_t* __restrict__ arena,
                                                         uint32_t* __restrict__ regs) {
@@ -7224,7 +7324,7 @@ __global__ void __launch_bounds__(256) freq_hll_records(const uint64_t* __restri
   __syncthreads();
   const int lane = (int)__lane_id(), wave = threadIdx.x >> 6;
   for (int64_t p = (int64_t)blockIdx.x * 4 + wave; p < P; p += (int64_t)gridDim.x * 4) {
-    const uint64_t r0 = part_base[p], r1 = part_base[p + 1];
+    const uint64_t r0 = part_base[p], r1 = part_end[p];
     const uint32_t b = (uint32_t)(p >> s);
     for (uint64_t i = r0 + lane; i < r1; i += 64) {
       uint64_t x;
@@ -7266,7 +7366,7 @@ extern "C" dq_status dq_freq_hll(dq_freq* f, int64_t max_records, uint64_t* word
     const int64_t P = (int64_t)kBuckets << f->s_bits;
     const unsigned grid = (unsigned)std::min<int64_t>((P + 3) / 4, 2048);
     hipLaunchKernelGGL(freq_hll_records, dim3(grid), dim3(256), 0, f->stream,
-                       reinterpret_cast<const uint64_t*>(f->recsB.p), f->part_base.p, P, f->s_bits,
+                       reinterpret_cast<const uint64_t*>(f->recsB.p), f->part_base.p, f->part_end_ptr, P, f->s_bits,
                        f->exact ? 1 : 0, f->types[0], arena_of(f), regs.p);
     HIP_TRY(hipGetLastError());
   }
@@ -7432,6 +7532,7 @@ static dq_status topk_recount(dq_freq* f, int k, FEntry* list, int64_t nb, std::
   memset(&a, 0, sizeof(a));
   a.recsB = f->recsB.p;
   a.part_base = f->part_base.p;
+  a.part_end = f->part_end_ptr;
   a.s = f->s_bits;
   a.arena = arena_of(f);
   for (int q = 0; q < f->n_keys; ++q) a.types[q] = f->types[q];
