@@ -5491,9 +5491,13 @@ static dq_status finalize_b(dq_freq* f) {
   if (f->exact && !no_capb && !f->cap_failed && bsub == 0 && b3u && H <= kUnitX / 2) {
     std::vector<unsigned long long>& w = f->h_cap_words;
     w.assign(2 * kBuckets + 1, 0ULL);
+    // test hook (read per finalize): DQ_FREQ_CAP_SCALE < 1 shrinks the room so runs overflow
+    const char* cse = getenv("DQ_FREQ_CAP_SCALE");
+    const double cscale = cse ? atof(cse) : 1.0;
     for (int b = 0; b < kBuckets; ++b) {
       const double mean = (double)tot[b] / (double)S;
-      const unsigned long long cap = tot[b] ? (unsigned long long)std::ceil(mean + 8.0 * std::sqrt(mean) + 32.0) : 0ULL;
+      const unsigned long long cap =
+          tot[b] ? (unsigned long long)std::ceil(cscale * (mean + 8.0 * std::sqrt(mean) + 32.0)) : 0ULL;
       w[kBuckets + 1 + b] = cap;
       w[b + 1] = w[b] + cap * (unsigned long long)S;
     }

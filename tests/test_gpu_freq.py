@@ -622,6 +622,40 @@ def test_exact_bucket_pieces_at_scale(nulls, gpu_device):
     assert top[0][0][0] == 42
 
 
+@pytest.mark.parametrize("scale,heavy", [("1", 0), ("1", 400), ("0.5", 0), ("0.97", 0)])
+def test_capacity_layout_and_its_counted_fallback(scale, heavy, gpu_device, monkeypatch):
+    """Exact phase B without the count pass (finalize_b's capacity layout): partitions of fixed
+    room filled through cursor adds.  DQ_FREQ_CAP_SCALE shrinks the room so runs overflow and the
+    table is scattered again by the counted path (0.5: every partition; 0.97: a few); `heavy`
+    keys repeated once per 8192-row tile bypass phase A's dedupe and crowd one partition.  Every
+    case against numpy's exact counts, the entropy within 1e-12, and the top 3."""
+    from deequ_amd.analyzers.grouping import FrequencyTable
+    from deequ_amd.table import Table
+    monkeypatch.setenv("DQ_FREQ_CAP_SCALE", scale)
+    n = 6_000_000
+    rng = np.random.default_rng(5)
+    ids = rng.integers(-2**62, 2**62, n, dtype=np.int64)     # distinct: the dedupe bypasses
+    if heavy:
+        ids[::8192][:heavy] = 7                                  # one key in every tile
+    t = pa.table({"id": pa.array(ids)})
+    df = Table.from_arrow(t, device=gpu_device, max_batch_rows=2_000_000)
+    ft = FrequencyTable(["id"], [df.schema["id"].dtype], 0)
+    for b in df.batches:
+        ft.add([b["id"]])
+    s = ft.summarize()
+    vals, counts = np.unique(ids, return_counts=True)
+    assert s.num_rows == n
+    assert s.n_groups == len(vals)
+    assert s.n_unique == int((counts == 1).sum())
+    p = counts / n
+    ent = -math.fsum((p * np.log(p)).tolist())
+    assert abs(s.entropy - ent) <= 1e-12 * abs(ent)
+    top = ft.topk(3)
+    assert [c for _, c in top][:1] == [int(counts.max())]
+    if heavy:
+        assert top[0][0][0] == 7
+
+
 @pytest.mark.parametrize("batch", [None, 9_000])
 def test_long_string_keys_match_oracle(batch, gpu_device):
     """One-column and two-column keys over strings of 17..80 bytes (the chunked long-string hash:
