@@ -1653,14 +1653,21 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
       if (cap) {
         bh[tid] = lim;
         __syncthreads();
-        for (uint32_t i = tid; i < ctotal; i += kAXThreads) {
+        auto put = [&](uint32_t i) {
           const uint64_t hh = stash[i];
           const uint32_t b = bucket_of(hh);
           if (!(DQ_AX_EXPERIMENT & 1))  // (timing builds: 1 = no record stores)
             out[(uint32_t)((i < bh[b] ? gdel[b] : odel[b]) + i)] = (hh << 8) | 1u;
+        };
+        // int64 keys: four records' LDS reads in flight per step (422 -> 414-419 us per configs[2]
+        // batch, profiles/r6ak/); the other widths spill with it.  (Fully unrolled -- every
+        // round's stash words, then destinations, then stores -- spilled at every batch size.)
+        if constexpr (TY == DQ_INT64) {
+#pragma unroll 4
+          for (uint32_t i = tid; i < ctotal; i += kAXThreads) put(i);
+        } else {
+          for (uint32_t i = tid; i < ctotal; i += kAXThreads) put(i);
         }
-        // (an unrolled form -- every round's stash words, then destinations, then stores --
-        // spilled the kernel at every batch size tried; not adopted)
       } else {
         for (uint32_t i = tid; i < ctotal; i += kAXThreads) {
           const uint64_t hh = stash[i];
@@ -1712,289 +1719,6 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
       const uint32_t b = bucket_of(k);
       maxcnt = dcnt[sl] > maxcnt ? dcnt[sl] : maxcnt;
       for_digits(dcnt[sl], [&](uint32_t code) { out[atomicAdd(&wcur[b], 1u)] = (k << 8) | code; });
-    }
-  }
-  wave_max_lds(&s_maxcnt, maxcnt);
-  __syncthreads();
-  if (tid == 0 && s_maxcnt) atomicMax(&a.counters[C_MAXCNT], s_maxcnt);
-  a.plen[(int64_t)blockIdx.x * kBuckets + tid] =
-      cap ? min(wcur[tid], cap) : wcur[tid] - a.pstart[(int64_t)blockIdx.x * kBuckets + tid];
-  wave_count(&a.counters[C_NULL_ROWS], nulls);
-  wave_count(&a.counters[C_NULL_GROUP], nullg);
-  wave_count(&a.counters[C_DBG_BYPASS], dbg_bypass);
-  wave_count(&a.counters[C_NAN_FOLDED], nanf);
-  if (tid == 0 && s_full) atomicAdd(&a.counters[C_DBG_FULL], (unsigned long long)s_full);
-}
-
-// ------------------------------------------------------------------------------------------------
-// Phase A, 8-byte exact keys, the next tile staged through LDS (freq_phaseA_xg): freq_phaseA_xp's
-// tiles and output layout (same pieces, chunk overflows, dedupe table and bypass probing), but
-// each tile's keys arrive by LDS-DMA (global_load_lds_dwordx4, 1 KB per wave instruction, no
-// registers held) while the previous tile is hashed, deduped, ranked and written: a tile starts
-// with its keys read from the one 64 KB staging buffer into registers, then the next tile's DMA
-// is issued into it.  The records leave straight from registers to their slots (region slot of
-// the bucket + the row's rank, from the counting atomic) instead of through a sorted LDS stash --
-// the stash's 64 KB is the staging buffer, so two workgroups still share a CU; a bucket's ~16
-// records of a tile are one 128-byte line, merged in L2.  (freq_phaseA_xp's loads wait in
-// registers at the top of each tile: its loads and hashing alone ran at 3.2 TB/s.)  The DMA is
-// issued from inline asm, so the compiler's wait counting does not see it and drains nothing
-// early; each tile waits vmcnt(0) (this wave's DMA, and the previous tile's stores), then a
-// barrier (every wave's DMA landed).  Partial tiles load directly.
-// ------------------------------------------------------------------------------------------------
-DQ_DEV uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
-}
-
-template <int TY>
-__global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xg(AArgs a) {
-  static_assert(TY == DQ_INT64, "8-byte integer keys (the float64 instance spilled 116 bytes)");
-  constexpr int NT = kAXThreads, T = FM<false>::kTile, R = T / NT, D = AKeys<false, false>::kDedupe;
-  static_assert(NT == kBuckets && NT == D && R <= 32 && T * 8 == NT * 128, "a wave's DMA share: 8 KB");
-  __shared__ uint64_t buf[T];            // the next tile's raw keys
-  __shared__ uint32_t bh[kBuckets];      // counts of the tile's raw rows
-  __shared__ uint32_t dg[kBuckets];      // a rank's region slot (rank < tk), minus the rank
-  __shared__ uint32_t dof[kBuckets];     // a rank's chunk slot (rank >= tk), minus the rank
-  __shared__ uint16_t tk[kBuckets];      // the ranks the piece takes this tile
-  __shared__ uint32_t wcur[kBuckets];    // each bucket's next region slot (the workgroup's piece)
-  __shared__ unsigned long long dkey[D];
-  __shared__ uint32_t dcnt[D];
-  __shared__ uint32_t s_wave[NT / 64];
-  __shared__ uint32_t s_hits, s_bypass, s_full;
-  __shared__ unsigned long long s_maxcnt;
-  const int tid = threadIdx.x;
-  if (a.dense_words && __hip_atomic_load(&a.dense_words[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                           a.dense_epoch) {  // the dense path took the batch: empty pieces
-    a.pstart[(int64_t)blockIdx.x * kBuckets + tid] = 0;
-    a.plen[(int64_t)blockIdx.x * kBuckets + tid] = 0;
-    return;
-  }
-  const KeyCol& c = a.ks.cols[0];
-  const int64_t n_tiles = (a.n_items + a.tile_items - 1) / a.tile_items;
-  const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_wg;
-  const int64_t t1 = min(t0 + (int64_t)a.tiles_per_wg, n_tiles);
-  // the full-tile loads: 8-byte-aligned bitmap words, tiles on 64-row boundaries, 16-byte DMA
-  const bool full_ok = (reinterpret_cast<uintptr_t>(c.valid) & 7u) == 0 && (a.tile_items & 63) == 0 &&
-                       (reinterpret_cast<uintptr_t>(c.values) & 15u) == 0;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  auto is_full = [&](int64_t t) { return full_ok && t * a.tile_items + T <= a.n_items; };
-  // tile t's keys into buf: wave w moves bytes [8192 w, 8192 w + 8192) of the tile
-  auto stage = [&](int64_t t) {
-    // (a uniform 64-bit base in SGPRs and one 32-bit lane offset: no 64-bit address registers)
-    const char* g = reinterpret_cast<const char*>(c.values) + (t * a.tile_items) * 8 + wave * 8192;
-    const uint32_t base = lds_addr(&buf[0]) + wave * 8192;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      unsigned keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep)
-                   : "v"((uint32_t)(__lane_id() * 16 + k * 1024)), "s"(g), "s"(base + k * 1024)
-                   : "memory");
-    }
-  };
-  bool staged = t0 < t1 && is_full(t0);
-  if (staged) stage(t0);  // (the first tile's DMA overlaps the set-up)
-  for (int i = tid; i < D; i += NT) {
-    dkey[i] = kEmptyKey;
-    dcnt[i] = 0;
-  }
-  const uint32_t cap = a.piece_cap;  // 0: pieces laid out by the pre-pass's counts
-  {
-    uint32_t st;
-    if (cap) {  // piece (w, b) at piece_base + (w kBuckets + b) cap; wcur = its fill
-      st = (uint32_t)(a.piece_base + ((uint64_t)blockIdx.x * kBuckets + tid) * cap);
-      wcur[tid] = 0;
-    } else {
-      uint32_t all;
-      const uint32_t bb = block_excl_scan(a.ptot[tid], s_wave, all);
-      st = bb + a.ph[(int64_t)blockIdx.x * kBuckets + tid];
-      wcur[tid] = st;
-    }
-    a.pstart[(int64_t)blockIdx.x * kBuckets + tid] = st;
-    bh[tid] = 0;
-    for (int64_t r = t0; r < t1; ++r)
-      for (int i = tid; i < kHistRow; i += NT) a.hist[r * kHistRow + i] = 0;
-    for (int i = tid; i < kHistRow; i += NT) a.hist[(n_tiles + blockIdx.x) * kHistRow + i] = 0;
-  }
-  if (tid == 0) {
-    s_bypass = 0;
-    s_full = 0;
-    s_maxcnt = 0;
-  }
-  unsigned long long nulls = 0, nullg = 0, dbg_bypass = 0, nanf = 0;
-  uint64_t* out = reinterpret_cast<uint64_t*>(a.recs);
-  auto dedupe = [&](uint64_t h) -> int {  // 1 claimed, 2 added, 0 table full (the row stays raw)
-    uint32_t slot = (uint32_t)(h >> 20) & (D - 1);
-    for (int pr = 0; pr < 4; ++pr) {
-      unsigned long long k = lds_load(reinterpret_cast<const uint64_t*>(&dkey[slot]));
-      if (k == kEmptyKey) {
-        const unsigned long long prev = atomicCAS(&dkey[slot], kEmptyKey, (unsigned long long)h);
-        if (prev == kEmptyKey) {
-          atomicAdd(&dcnt[slot], 1u);
-          return 1;
-        }
-        k = prev;
-      }
-      if (k == h) {
-        atomicAdd(&dcnt[slot], 1u);
-        return 2;
-      }
-      slot = (slot + 1) & (D - 1);
-    }
-    return 0;
-  };
-#pragma unroll 1
-  for (int64_t t = t0; t < t1; ++t) {
-    const int64_t i0 = t * a.tile_items, i1 = min(i0 + a.tile_items, a.n_items);
-    const bool probe = ((t - t0) & 7) == 0;
-    uint64_t h[R];
-    uint32_t ok = 0, vb = ~0u;
-    if (staged) {  // (block-uniform)
-      ok = (1u << R) - 1u;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < R; ++j) h[j] = buf[j * NT + tid];
-      if (c.valid) {
-        const int64_t wrow = i0 + 64 * (int64_t)wave;
-        vb = 0;
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-          const uint64_t w = *reinterpret_cast<const uint64_t*>(c.valid + ((wrow + (int64_t)j * NT) >> 3));
-          vb |= (uint32_t)((w >> __lane_id()) & 1u) << j;
-        }
-      }
-      __syncthreads();  // every wave holds its rows: the buffer takes the next tile
-    } else {  // branch-free clamped loads (an out-of-tile lane re-reads the tile's last row)
-      int64_t ic[R];
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const int64_t i = i0 + (int64_t)j * NT + tid;
-        ok |= (i < i1 ? 1u : 0u) << j;
-        ic[j] = i < i1 ? i : i1 - 1;
-      }
-#pragma unroll
-      for (int j = 0; j < R; ++j) h[j] = kwiden(TY, c.values, ic[j]);
-      if (c.valid) {
-        uint32_t byte[R];
-#pragma unroll
-        for (int j = 0; j < R; ++j) byte[j] = c.valid[ic[j] >> 3];
-        vb = 0;
-#pragma unroll
-        for (int j = 0; j < R; ++j) vb |= ((byte[j] >> (ic[j] & 7)) & 1u) << j;
-      }
-    }
-    staged = t + 1 < t1 && is_full(t + 1);
-    if (staged) stage(t + 1);
-    const uint32_t keyed = ok & vb;
-    {
-      const unsigned long long nn = (unsigned long long)__builtin_popcount(ok & ~vb);
-      const unsigned long long ng = a.ks.null_as_group ? nn : 0ULL;
-      nullg += ng;
-      nulls += nn - ng;
-    }
-#pragma unroll
-    for (int j = 0; j < R; ++j) h[j] = fmix_bij(exact_canon(a.ks, h[j]));
-    // dedupe: round 0 of a probing tile measures the hit rate, which decides the bypass
-    uint32_t raw = keyed;
-    if (probe) {
-      if (tid == 0) s_hits = 0;
-      __syncthreads();
-      int res = -1;
-      if (keyed & 1u) {
-        res = dedupe(h[0]);
-        if (res) raw &= ~1u;
-        if (!res) atomicAdd(&s_full, 1u);
-      }
-      const uint32_t wh = (uint32_t)__builtin_popcountll(__ballot(res == 2));
-      if (__lane_id() == 0 && wh) atomicAdd(&s_hits, wh);
-      __syncthreads();
-      if (tid == 0) s_bypass = s_hits * 16u < (uint32_t)NT ? 1u : 0u;
-      __syncthreads();
-      dbg_bypass += tid == 0 ? s_bypass : 0u;
-    }
-    if (!s_bypass) {
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        if (!((keyed >> j) & 1u) || (probe && j == 0)) continue;
-        const int res = dedupe(h[j]);
-        if (res) raw &= ~(1u << j);
-        else atomicAdd(&s_full, 1u);
-      }
-    }
-    if (!__syncthreads_or(raw ? 1 : 0)) continue;  // every row collapsed: nothing to write
-    // each raw row's rank in its bucket (the counting atomic), then the buckets' slots
-    uint32_t rk[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j)
-      if ((raw >> j) & 1u) rk[j] = atomicAdd(&bh[bucket_of(h[j])], 1u);
-    __syncthreads();
-    const uint32_t cnt = bh[tid];
-    bh[tid] = 0;  // (the next tile's atomics come after this tile's barriers)
-    if (cap) {  // the piece takes what fits; the rest goes to this tile's chunk, bucket-sorted
-      const uint32_t take = min(cnt, cap - wcur[tid]), ovf = cnt - take;
-      uint32_t otot;
-      const uint32_t oex = block_excl_scan(ovf, s_wave, otot);
-      dg[tid] = (uint32_t)(a.piece_base + ((uint64_t)blockIdx.x * kBuckets + tid) * cap) + wcur[tid];
-      dof[tid] = (uint32_t)(t * T) + oex - take;
-      tk[tid] = (uint16_t)take;
-      if (otot) {  // (the tile's chunk row was emptied at the start)
-        uint16_t* hrow = a.hist + t * kHistRow;
-        hrow[tid] = (uint16_t)oex;
-        if (tid == 0) hrow[kBuckets] = (uint16_t)otot;
-      }
-      wcur[tid] += take;
-    } else {
-      dg[tid] = wcur[tid];
-      tk[tid] = (uint16_t)min(cnt, 0xffffu);
-      wcur[tid] += cnt;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < R; ++j)
-      if ((raw >> j) & 1u) {
-        const uint32_t b = bucket_of(h[j]);
-        out[(uint32_t)((rk[j] < tk[b] ? dg[b] : dof[b]) + rk[j])] = (h[j] << 8) | 1u;  // count-1 digit
-      }
-  }
-  // the collapsed groups into their buckets' pieces, then the pieces' lengths
-  __syncthreads();
-  uint64_t maxcnt = 1;
-  if (cap) {  // (one dedupe slot per thread) the digits that fit the piece, the rest bucket-sorted
-              // into this workgroup's chunk
-    dof[tid] = 0;
-    __syncthreads();
-    const uint64_t k = dkey[tid];
-    const uint32_t c = k == kEmptyKey ? 0u : dcnt[tid], b = k == kEmptyKey ? 0u : bucket_of(k);
-    uint32_t nd = 0;
-    for (uint32_t x = c; x; x >>= 2) nd += (x & 3) ? 1u : 0u;
-    const uint32_t s0 = nd ? atomicAdd(&wcur[b], nd) : 0u;
-    const uint32_t np = s0 < cap ? min(nd, cap - s0) : 0u;
-    const uint32_t o = nd > np ? atomicAdd(&dof[b], nd - np) : 0u;
-    maxcnt = c > maxcnt ? c : maxcnt;
-    __syncthreads();
-    uint32_t otot;
-    const uint32_t oex = block_excl_scan(dof[tid], s_wave, otot);
-    const int64_t wchunk = n_tiles + blockIdx.x;
-    if (otot) {
-      uint16_t* hrow = a.hist + wchunk * kHistRow;
-      hrow[tid] = (uint16_t)oex;
-      if (tid == 0) hrow[kBuckets] = (uint16_t)otot;
-    }
-    dg[tid] = oex;
-    __syncthreads();
-    const uint64_t pb = a.piece_base + ((uint64_t)blockIdx.x * kBuckets + b) * cap;
-    uint32_t d = 0;
-    for_digits(c, [&](uint32_t code) {
-      const uint64_t slot = d < np ? pb + s0 + d : (uint64_t)wchunk * T + dg[b] + o + (d - np);
-      out[slot] = (k << 8) | code;
-      ++d;
-    });
-  } else {
-    const uint64_t k = dkey[tid];
-    if (k != kEmptyKey) {
-      const uint32_t b = bucket_of(k);
-      maxcnt = dcnt[tid] > maxcnt ? dcnt[tid] : maxcnt;
-      for_digits(dcnt[tid], [&](uint32_t code) { out[atomicAdd(&wcur[b], 1u)] = (k << 8) | code; });
     }
   }
   wave_max_lds(&s_maxcnt, maxcnt);
@@ -5496,13 +5220,6 @@ static bool pieces_enabled() {
   return on;
 }
 
-// int64 exact keys through freq_phaseA_xg (the next tile staged in LDS) with DQ_FREQ_AXG=1
-// (measured slower than freq_phaseA_xp: 451 against 412 us per configs[2] batch, profiles/r6aj/)
-static bool xg_enabled() {
-  const char* e = getenv("DQ_FREQ_AXG");  // (read per batch: A/B in one process)
-  return e && atoi(e) != 0;
-}
-
 // Pre-pass (rows per workgroup and bucket), its scan, and phase A into bucket pieces; the batch's
 // region is the `chunks` chunk slots at f->n_chunks (tiles + workgroup chunks >= rows records).
 static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
@@ -5558,9 +5275,6 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
     auto go = [&](auto kernel) {
       hipLaunchKernelGGL(kernel, dim3((unsigned)n_wg), dim3(kAXThreads), 0, f->stream, a);
     };
-    auto goxg = [&](auto kernel) {  // (the same grid)
-      hipLaunchKernelGGL(kernel, dim3((unsigned)n_wg), dim3(kAXThreads), 0, f->stream, a);
-    };
     switch (a.ks.cols[0].type) {  // one kernel per width (one kernel for all spilled heavily)
       case DQ_INT8: go(freq_phaseA_xp<DQ_INT8>); break;
       case DQ_INT16: go(freq_phaseA_xp<DQ_INT16>); break;
@@ -5568,10 +5282,7 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
       case DQ_FLOAT32: go(freq_phaseA_xp<DQ_FLOAT32>); break;
       case DQ_FLOAT64: go(freq_phaseA_xp<DQ_FLOAT64>); break;
       case DQ_BOOL: go(freq_phaseA_xp<DQ_BOOL>); break;
-      default:
-        if (xg_enabled()) goxg(freq_phaseA_xg<DQ_INT64>);
-        else go(freq_phaseA_xp<DQ_INT64>);
-        break;
+      default: go(freq_phaseA_xp<DQ_INT64>); break;
     }
   }
   HIP_TRY(hipGetLastError());
