@@ -632,8 +632,13 @@ def _fold_null_group(frequencies, dtype: int, k: int):
     elif dtype in (N.DATE32, N.TIMESTAMP_US) or N.is_decimal(dtype):  # one formatter call
         texts = N.format_values(dtype, [k for k, _ in kept])
         top = [(s, c) for s, (_, c) in zip(texts, kept)]
-    else:
-        top = [(cast_to_string(k, dtype), c) for k, c in kept]
+    elif dtype == N.UTF8:
+        top = kept
+    elif dtype == N.BOOL:
+        top = [("true" if k else "false", c) for k, c in kept]
+    else:  # integers: the decimal digits (cast_to_string per key held Histogram's host side for
+        # ~0.6 ms per 1000 keys, inside configs[2]'s step)
+        top = [(str(k), c) for k, c in kept]
     folded = nullg + lit
     if folded:
         at = next((i for i, (_, c) in enumerate(top) if c < folded), len(top))

@@ -2433,9 +2433,16 @@ void release_pinned_staging() {
 }
 
 hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
-  if (!bytes) return host_wait(st);
+  const D2HPart part{dst, src, bytes};
+  return d2h_n(&part, 1, st);
+}
+
+hipError_t d2h_n(const D2HPart* parts, int n, hipStream_t st) {
+  size_t total = 0;
+  for (int i = 0; i < n; ++i) total += (parts[i].bytes + 15) & ~(size_t)15;
+  if (!total) return host_wait(st);
   size_t want = 4096;
-  while (want < bytes) want <<= 1;
+  while (want < total) want <<= 1;
   PinnedPool& pool = pinned_pool();
   void* buf = nullptr;
   {
@@ -2450,16 +2457,28 @@ hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st) {
   }
   if (!buf && want > (64u << 20)) {  // (large copies: not worth pinning a block for)
     hipError_t e = host_wait(st);
-    return e != hipSuccess ? e : hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+    for (int i = 0; i < n && e == hipSuccess; ++i)
+      if (parts[i].bytes) e = hipMemcpy(parts[i].dst, parts[i].src, parts[i].bytes, hipMemcpyDeviceToHost);
+    return e;
   }
   if (!buf) {
     hipError_t e = hipHostMalloc(&buf, want, hipHostMallocDefault);
     if (e != hipSuccess) return e;
   }
-  hipError_t e = hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToHost, st);
+  hipError_t e = hipSuccess;
+  size_t off = 0;
+  for (int i = 0; i < n && e == hipSuccess; ++i) {
+    if (parts[i].bytes)
+      e = hipMemcpyAsync(static_cast<char*>(buf) + off, parts[i].src, parts[i].bytes, hipMemcpyDeviceToHost, st);
+    off += (parts[i].bytes + 15) & ~(size_t)15;
+  }
   if (e == hipSuccess) e = host_wait(st);
   if (e != hipSuccess) return e;  // (the block is dropped: a DMA may still be writing it)
-  memcpy(dst, buf, bytes);
+  off = 0;
+  for (int i = 0; i < n; ++i) {
+    if (parts[i].bytes) memcpy(parts[i].dst, static_cast<char*>(buf) + off, parts[i].bytes);
+    off += (parts[i].bytes + 15) & ~(size_t)15;
+  }
   bool keep;
   {
     std::lock_guard<std::mutex> lock(pool.m);

@@ -5044,14 +5044,17 @@ static dq_status ensure_chunks(dq_freq* f, int64_t add) {
   return DQ_OK;
 }
 
-static dq_status pull_counters(dq_freq* f) {
-  HIP_TRY(hipStreamSynchronize(f->stream));
-  unsigned long long w[C_N + 1];
-  HIP_TRY(d2h(w, f->dev_words.p, sizeof(w), f->stream));
+// the counters and the arena cursor as read back (dev_words: C_N counters + the cursor)
+static void apply_counters(dq_freq* f, const unsigned long long* w) {
   for (int k = 0; k < C_N; ++k) f->h_counters[k] = w[k];
   f->arena_used = w[C_N];
   f->arena_hi = f->arena_used;
   f->counters_stale = false;
+}
+static dq_status pull_counters(dq_freq* f) {  // (d2h is ordered after the stream's work)
+  unsigned long long w[C_N + 1];
+  HIP_TRY(d2h(w, f->dev_words.p, sizeof(w), f->stream));
+  apply_counters(f, w);
   return DQ_OK;
 }
 static dq_status sync_counters(dq_freq* f) { return f->counters_stale ? pull_counters(f) : DQ_OK; }
@@ -5375,12 +5378,13 @@ static dq_status finalize_b(dq_freq* f) {
   HIP_TRY(hipGetLastError());
   std::vector<unsigned long long> tot(kBuckets);
   if (f->counters_stale) {  // one stream wait for the counters and the bucket totals
-    dq_status cs = pull_counters(f);
-    if (cs != DQ_OK) return cs;
+    unsigned long long w[C_N + 1];
+    const D2HPart parts[2] = {{w, f->dev_words.p, sizeof(w)}, {tot.data(), f->totals.p, kBuckets * 8}};
+    HIP_TRY(d2h_n(parts, 2, f->stream));
+    apply_counters(f, w);
   } else {
-    HIP_TRY(hipStreamSynchronize(f->stream));
+    HIP_TRY(d2h(tot.data(), f->totals.p, kBuckets * 8, f->stream));
   }
-  HIP_TRY(d2h(tot.data(), f->totals.p, kBuckets * 8, f->stream));
   uint64_t R = 0;
   for (auto t : tot) R += t;
   int target = f->exact ? FM<false>::kTarget : FM<true>::kTarget;
@@ -5438,8 +5442,9 @@ static dq_status finalize_b(dq_freq* f) {
   f->part_end_ptr = f->part_base.p + 1;
   f->Rcap = R;
   HIP_TRY(f->unit_start.ensure(kBuckets + 1));
-  HIP_TRY(hipMemcpy(f->unit_start.p, f->h_unit_start.data(), (kBuckets + 1) * 4,
-                    hipMemcpyHostToDevice));
+  // (stream-ordered: the host copy is a member, unchanged until the next finalize)
+  HIP_TRY(hipMemcpyAsync(f->unit_start.p, f->h_unit_start.data(), (kBuckets + 1) * 4,
+                         hipMemcpyHostToDevice, f->stream));
   if (u == 0) {
     HIP_TRY(hipMemsetAsync(f->part_base.p, 0, (P + 1) * 8, f->stream));
     f->b_valid = true;
@@ -5615,6 +5620,8 @@ static bool pk_ok(const dq_freq* f) {
 
 static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
   bool reduced = false;  // f->red already holds this pass's sums
+  bool read_back = false;  // red_h / cw_h hold the reduction and the counters (one wait for both)
+  unsigned long long red_h[6], cw_h[C_N + 1];
   dq_status st = finalize_b(f);
   if (st != DQ_OK) return st;
   const double nr = (double)f->num_rows;
@@ -5739,7 +5746,14 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
         reduced = true;
       }
       unsigned int m = 0;
-      HIP_TRY(d2h(&m, f->ovf_n.p, 4, f->stream));
+      if (reduced) {  // the overflow count, the reduction and the counters behind one wait
+        const D2HPart parts[3] = {{&m, f->ovf_n.p, 4}, {red_h, f->red.p, sizeof(red_h)},
+                                  {cw_h, f->dev_words.p, sizeof(cw_h)}};
+        HIP_TRY(d2h_n(parts, 3, f->stream));
+        read_back = m == 0;
+      } else {
+        HIP_TRY(d2h(&m, f->ovf_n.p, 4, f->stream));
+      }
       if (m) reduced = false;
       if (clk && ((f->exact && !old_c) || (!f->exact && round == 0 && !old_hc))) {  // C_x / C_h: 8 stamps per item
         unsigned long long h[16 * 8];
@@ -5808,7 +5822,11 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
     if (rs != DQ_OK) return rs;
   }
   unsigned long long r[6];
-  HIP_TRY(d2h(r, f->red.p, sizeof(r), f->stream));
+  if (read_back) {
+    memcpy(r, red_h, sizeof(r));
+  } else {
+    HIP_TRY(d2h(r, f->red.p, sizeof(r), f->stream));
+  }
   f->st_groups = r[0];
   f->st_unique = r[1];
   f->st_entropy = __builtin_bit_cast(double, r[2]);
@@ -5819,6 +5837,10 @@ static dq_status finalize_c(dq_freq* f, bool want_groups, bool want_cand) {
   f->c_groups = want_groups;
   f->c_cand = want_cand;
   f->n_compact = -1;
+  if (read_back) {
+    apply_counters(f, cw_h);
+    return DQ_OK;
+  }
   return pull_counters(f);
 }
 
@@ -6445,8 +6467,8 @@ static dq_status encode_groups(dq_freq* f, const Group* g, int64_t n, std::vecto
   if (st != DQ_OK) return st;
   std::vector<RecIn> hr(rec[0]);
   std::vector<uint8_t> hv(var[0]);
-  HIP_TRY(d2h(hr.data(), dr.p, rec[0] * sizeof(RecIn), f->stream));
-  if (var[0]) HIP_TRY(d2h(hv.data(), dv.p, var[0], f->stream));
+  const D2HPart parts[2] = {{hr.data(), dr.p, rec[0] * sizeof(RecIn)}, {hv.data(), dv.p, var[0]}};
+  HIP_TRY(d2h_n(parts, var[0] ? 2 : 1, f->stream));
   for (const RecIn& r : hr) {
     offs.push_back((int64_t)bytes.size());
     counts.push_back((int64_t)r.count);
@@ -6519,22 +6541,26 @@ static dq_status select_top(dq_freq* f, const Group* arr, int64_t n, int k, std:
     }
   }
   const uint64_t cap = hi - lo == 1 ? (uint64_t)k - above : inbin;
+  const uint64_t take_cap = std::max<uint64_t>(total <= (uint64_t)k ? total : above, 1);
   DevBuf<Group> take, tie;
   DevBuf<unsigned long long> nt;
-  HIP_TRY(take.ensure(std::max<uint64_t>(total <= (uint64_t)k ? total : above, 1)));
+  HIP_TRY(take.ensure(take_cap));
   HIP_TRY(tie.ensure(std::max<uint64_t>(cap, 1)));
   HIP_TRY(nt.ensure(2));
   HIP_TRY(hipMemsetAsync(nt.p, 0, 16, f->stream));
   hipLaunchKernelGGL(freq_group_select, dim3(grid_for(n)), dim3(256), 0, f->stream, arr, n, hi, lo,
                      (unsigned long long)cap, take.p, nt.p, nt.p + 1, tie.p);
   HIP_TRY(hipGetLastError());
+  // the counts and both buffers at their capacities behind one wait (<= k + 4096 groups: a few
+  // tens of KB, against a host round trip per read-back)
   unsigned long long cnts[2];
-  HIP_TRY(d2h(cnts, nt.p, 16, f->stream));
-  const uint64_t nt_take = cnts[0], nt_tie = std::min<uint64_t>(cnts[1], cap);
-  out.resize(nt_take + nt_tie);
-  if (nt_take) HIP_TRY(d2h(out.data(), take.p, nt_take * sizeof(Group), f->stream));
-  if (nt_tie)
-    HIP_TRY(d2h(out.data() + nt_take, tie.p, nt_tie * sizeof(Group), f->stream));
+  std::vector<Group> ht(take_cap), hc(std::max<uint64_t>(cap, 1));
+  const D2HPart parts[3] = {{cnts, nt.p, 16}, {ht.data(), take.p, take_cap * sizeof(Group)},
+                            {hc.data(), tie.p, cap * sizeof(Group)}};
+  HIP_TRY(d2h_n(parts, 3, f->stream));
+  const uint64_t nt_take = std::min<uint64_t>(cnts[0], take_cap), nt_tie = std::min<uint64_t>(cnts[1], cap);
+  out.assign(ht.begin(), ht.begin() + nt_take);
+  out.insert(out.end(), hc.begin(), hc.begin() + nt_tie);
   std::stable_sort(out.begin(), out.end(),
                    [](const Group& x, const Group& y) { return x.count > y.count; });
   if (out.size() > (size_t)k) out.resize(k);

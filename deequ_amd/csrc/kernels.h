@@ -38,6 +38,15 @@ void dev_free(void* p, size_t bytes, int device);
 // then memcpy'd to `dst`.  A plain hipMemcpy into pageable memory goes through the runtime's own
 // staging: measured ~20 us for 16 bytes and ~100 us for 64 KB, against ~10 us from pinned.
 hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t st);
+// Several such copies behind ONE wait: each part stream-ordered into its slice of one staging
+// block, then the block waited for once (a finalize's counters, totals and reductions: one host
+// round trip instead of one per read-back).
+struct D2HPart {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+hipError_t d2h_n(const D2HPart* parts, int n, hipStream_t st);
 
 // Device buffer that grows on demand (contents are not preserved across growth).
 template <typename T>
