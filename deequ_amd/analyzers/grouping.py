@@ -617,16 +617,46 @@ def _python_dtype(value, column_dtype: int) -> int:
     return column_dtype
 
 
+_INT_KEY_TYPES = (N.INT8, N.INT16, N.INT32, N.INT64)
+
+
+def _int_key_strings(counts, offs, raw) -> List[Tuple[str, int]]:
+    """(Cast(key AS STRING), count) of a one-integer-column table's encoded groups (tag word, then
+    the value as 8 little-endian bytes: dq_freq_export), NULL keys dropped; the values
+    _decode_one_key gives, formatted as cast_to_string does."""
+    n = len(counts)
+    if not n:
+        return []
+    data = bytes(raw)
+    words = np.frombuffer(data[: len(data) // 4 * 4], np.uint32)
+    at = np.asarray(offs[:n], np.int64) // 4
+    last = len(words) - 1
+    tags = words[at]
+    bits = (words[np.minimum(at + 1, last)].astype(np.uint64) |
+            (words[np.minimum(at + 2, last)].astype(np.uint64) << np.uint64(32))).view(np.int64)
+    keep = tags != 0
+    return list(zip(map(str, bits[keep].tolist()), np.asarray(counts[:n])[keep].tolist()))
+
+
 def _fold_null_group(frequencies, dtype: int, k: int):
     """Histogram's details and numberOfBins from a table whose NULL rows form a group kept apart:
     na.fill("NullValue") (Histogram.scala:59-66) makes them one group with any real "NullValue"
     string, so that group's count is the sum of both (dq_freq_null_literal) and it is placed by
     that count among the device top-N (ties in any order, like rdd.top)."""
-    raw = frequencies.topk(k + 2)  # up to two raw entries fold into one
-    nullg, lit = frequencies.null_literal()  # (after topk: the same finalize serves both)
-    kept = [(key, c) for (key,), c in raw
-            if not (key is None or (dtype == N.UTF8 and key == NULL_FIELD_REPLACEMENT))]
-    if dtype in (N.FLOAT64, N.FLOAT32):  # Double/Float.toString of every key in one call
+    if dtype in _INT_KEY_TYPES and hasattr(frequencies, "topk_raw"):
+        # integer keys: decoded and cast to their digits with array operations, no per-key
+        # tuples (configs[2]'s id Histogram: ~0.4 -> 0.15 ms of host time per step)
+        top = _int_key_strings(*frequencies.topk_raw(k + 2))
+        nullg, lit = frequencies.null_literal()  # (after topk: the same finalize serves both)
+        kept = None
+    else:
+        raw = frequencies.topk(k + 2)  # up to two raw entries fold into one
+        nullg, lit = frequencies.null_literal()  # (after topk: the same finalize serves both)
+        kept = [(key, c) for (key,), c in raw
+                if not (key is None or (dtype == N.UTF8 and key == NULL_FIELD_REPLACEMENT))]
+    if kept is None:
+        pass
+    elif dtype in (N.FLOAT64, N.FLOAT32):  # Double/Float.toString of every key in one call
         texts = N.java_doubles_to_strings([k for k, _ in kept], dtype == N.FLOAT32)
         top = [(s, c) for s, (_, c) in zip(texts, kept)]
     elif dtype in (N.DATE32, N.TIMESTAMP_US) or N.is_decimal(dtype):  # one formatter call
