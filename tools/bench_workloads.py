@@ -216,6 +216,7 @@ def run_single(workload: str, rows: int, steps: int, warmup: int, batch_rows: in
         pr.disable()
         buf = io.StringIO()
         pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(40)
+        pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(40)
         print(buf.getvalue(), file=sys.stderr)
     import gc
     gc_log = []  # (generation, seconds) of every collection, and the host time of each step
