@@ -4950,6 +4950,11 @@ struct dq_freq {
   uint64_t dense_epoch = 0;
   bool dense_off = false;
   PinnedWord dense_seen;
+  // recorded behind the first tried batch's decline-word copy (ahead of its phase A): the second
+  // batch waits for that answer instead of trying again (a fresh table per run -- the runner's
+  // Histogram tables -- ran the range pre-pass on three or four batches of a wide column)
+  hipEvent_t dense_ev = nullptr;
+  bool dense_waited = false;
   // finalize cache (phase B)
   bool b_valid = false;
   int s_bits = 0;
@@ -5259,6 +5264,14 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
                        f->dense_part.p, g, sums);
     hipLaunchKernelGGL(freq_dense_emit, dim3(kDenseW / kDenseV), dim3(kDenseV), 0, f->stream, a, sums);
     HIP_TRY(hipGetLastError());
+    // the host learns (late, without a wait) whether the batch was declined -- copied ahead of
+    // the batch's phase A, so the first answer is back while that still runs
+    HIP_TRY(f->dense_seen.before_copy(f->stream));
+    HIP_TRY(hipMemcpyAsync(f->dense_seen.p, f->dense_words.p + 3, 8, hipMemcpyDeviceToHost, f->stream));
+    if (f->dense_epoch == 1) {
+      if (!f->dense_ev) HIP_TRY(hipEventCreateWithFlags(&f->dense_ev, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(f->dense_ev, f->stream));
+    }
   }
   a.ph = f->ph.p;
   a.ptot = f->ptot.p;
@@ -5306,6 +5319,10 @@ static bool dense_worth_trying(dq_freq* f, const dq_column& k, int64_t rows) {
   if (k.type != DQ_INT8 && k.type != DQ_INT16 && k.type != DQ_INT32 && k.type != DQ_INT64 &&
       k.type != DQ_BOOL)
     return false;
+  if (f->dense_ev && !f->dense_waited && f->dense_epoch == 1) {  // (its phase A keeps the device busy)
+    f->dense_waited = true;
+    (void)hipEventSynchronize(f->dense_ev);
+  }
   if (f->dense_seen.p && *(volatile unsigned long long*)f->dense_seen.p != 0) {
     f->dense_off = true;  // a batch was declined
     return false;
@@ -6732,6 +6749,7 @@ extern "C" void dq_freq_destroy(dq_freq* f) {
     (void)hipStreamSynchronize(f->fast_seen.last_copy);  // (the word's copies, pinned_word_put)
   if (f->dense_seen.last_copy && f->dense_seen.last_copy != f->stream)
     (void)hipStreamSynchronize(f->dense_seen.last_copy);
+  if (f->dense_ev) (void)hipEventDestroy(f->dense_ev);
   delete f;
 }
 
@@ -6871,12 +6889,8 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
       a.dense_words = f->dense_words.p;
       a.dense_epoch = ++f->dense_epoch;
     }
-    dq_status ps = launch_pieces(f, a, chunks);
+    dq_status ps = launch_pieces(f, a, chunks);  // (and the decline word's copy, when dense)
     if (ps != DQ_OK) return ps;
-    if (dense) {  // the host learns (late, without a wait) whether the batch was declined
-      HIP_TRY(f->dense_seen.before_copy(f->stream));
-      HIP_TRY(hipMemcpyAsync(f->dense_seen.p, f->dense_words.p + 3, 8, hipMemcpyDeviceToHost, f->stream));
-    }
   } else if (f->exact) {
     f->nan_counted = false;
     launch_phaseA<false>(f, a, false);
