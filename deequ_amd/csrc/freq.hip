@@ -4685,9 +4685,19 @@ __global__ void __launch_bounds__(256) freq_group_hist(const Group* g, int64_t n
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t c = g[i].count;
-    if (c == 0 || c < lo || c >= hi) continue;
-    const uint64_t bin = width ? (c - lo) / width : (uint64_t)(63 - __builtin_clzll(c));
-    atomicAdd(&lh[bin], 1u);
+    const bool act = !(c == 0 || c < lo || c >= hi);
+    const uint32_t bin = act ? (uint32_t)(width ? (c - lo) / width : (uint64_t)(63 - __builtin_clzll(c))) : 0u;
+    // a wave whose counted groups share one bin (a high-cardinality key: every count 1) adds
+    // once -- 64 same-address LDS atomics per wave instruction serialised the kernel
+    const uint64_t am = __ballot(act);
+    if (!am) continue;
+    const int first = __builtin_ctzll(am);
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bin, first);
+    if (__ballot(act && bin == b0) == am) {
+      if ((int)__lane_id() == first) atomicAdd(&lh[b0], (unsigned)__builtin_popcountll(am));
+    } else if (act) {
+      atomicAdd(&lh[bin], 1u);
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 1024; i += blockDim.x)
@@ -4697,15 +4707,32 @@ __global__ void __launch_bounds__(256) freq_group_hist(const Group* g, int64_t n
 __global__ void freq_group_select(const Group* g, int64_t n, uint64_t hi_take, uint64_t lo_tie,
                                   unsigned long long cap, Group* out, unsigned long long* n_take,
                                   unsigned long long* n_tie, Group* out_tie) {
+  // (wave-aggregated cursors: one device atomic per wave and list, not per group)
+  const uint64_t below = (1ULL << __lane_id()) - 1ULL;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const Group x = g[i];
-    if (x.count == 0) continue;
-    if (x.count >= hi_take) {
-      out[atomicAdd(n_take, 1ULL)] = x;
-    } else if (x.count >= lo_tie) {
-      const unsigned long long q = atomicAdd(n_tie, 1ULL);
-      if (q < cap) out_tie[q] = x;
+    const bool take = x.count != 0 && x.count >= hi_take;
+    const bool tie = x.count != 0 && !take && x.count >= lo_tie;
+    const uint64_t bt = __ballot(take), bi = __ballot(tie);
+    if (bt) {
+      const int first = __builtin_ctzll(bt);
+      unsigned long long base = 0;
+      if ((int)__lane_id() == first) base = atomicAdd(n_take, (unsigned long long)__builtin_popcountll(bt));
+      base = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(base >> 32), first) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, first);
+      if (take) out[base + (unsigned long long)__builtin_popcountll(bt & below)] = x;
+    }
+    // (once the tie list is full, later waves only read its cursor: a high-cardinality key's
+    // top-k ties ~1e6 candidates at count 1, and their adds on one address serialised in L2)
+    if (bi && __hip_atomic_load(n_tie, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cap) {
+      const int first = __builtin_ctzll(bi);
+      unsigned long long base = 0;
+      if ((int)__lane_id() == first) base = atomicAdd(n_tie, (unsigned long long)__builtin_popcountll(bi));
+      base = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(base >> 32), first) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, first);
+      const unsigned long long q = base + (unsigned long long)__builtin_popcountll(bi & below);
+      if (tie && q < cap) out_tie[q] = x;
     }
   }
 }
