@@ -6549,7 +6549,9 @@ static dq_status select_top(dq_freq* f, const Group* arr, int64_t n, int k, std:
   std::vector<unsigned long long> hb(kBins);
   auto run_hist = [&](uint64_t lo, uint64_t hi, uint64_t width, int nb) -> dq_status {
     HIP_TRY(hipMemsetAsync(hist.p, 0, kBins * 8, f->stream));
-    hipLaunchKernelGGL(freq_group_hist, dim3(grid_for(n)), dim3(256), 0, f->stream, arr, n, lo, hi,
+    // (512 workgroups, a few groups per thread: one global add per workgroup and bin -- 4096
+    // workgroups' adds on one bin serialised in L2, 53 us per 1e6 candidates)
+    hipLaunchKernelGGL(freq_group_hist, dim3(grid_for(n, 512)), dim3(256), 0, f->stream, arr, n, lo, hi,
                        width, hist.p);
     HIP_TRY(hipGetLastError());
     HIP_TRY(d2h(hb.data(), hist.p, nb * 8, f->stream));
@@ -6592,7 +6594,9 @@ static dq_status select_top(dq_freq* f, const Group* arr, int64_t n, int k, std:
   HIP_TRY(tie.ensure(std::max<uint64_t>(cap, 1)));
   HIP_TRY(nt.ensure(2));
   HIP_TRY(hipMemsetAsync(nt.p, 0, 16, f->stream));
-  hipLaunchKernelGGL(freq_group_select, dim3(grid_for(n)), dim3(256), 0, f->stream, arr, n, hi, lo,
+  // (512 workgroups: the tie cursor passes `cap` within the first round of waves, later rounds
+  // only read it)
+  hipLaunchKernelGGL(freq_group_select, dim3(grid_for(n, 512)), dim3(256), 0, f->stream, arr, n, hi, lo,
                      (unsigned long long)cap, take.p, nt.p, nt.p + 1, tie.p);
   HIP_TRY(hipGetLastError());
   // the counts and both buffers at their capacities behind one wait (<= k + 4096 groups: a few
