@@ -305,6 +305,9 @@ struct AArgs {
   // the epoch of the last batch the dense path took, the epoch of the last one it declined
   unsigned long long* dense_words;
   uint64_t dense_epoch;
+  // freq_phaseA_xp: hist rows [zero_off, zero_off + zero_rows) (the batch's piece chunks, which
+  // hold no records) zeroed by the kernel's workgroups instead of a memset launch per batch
+  int64_t zero_off, zero_rows;
 };
 
 // Dedupe slots: every entry's count digits must fit the flush chunk (D x digits <= kTile), and
@@ -1439,6 +1442,16 @@ __global__ void __launch_bounds__(kPreThreads) freq_prepass_x(AArgs a, uint32_t*
 // bucket-counting atomic returns the row's rank in its bucket, so the counting sort takes one LDS
 // atomic per row instead of two.
 // ------------------------------------------------------------------------------------------------
+// p[lo, hi) = 0 by the block's threads: 16-byte stores over the aligned middle (the tile rows of
+// a small-key workgroup are ~46 KB of u16, zeroed 2 bytes a store before)
+DQ_DEV void zero_u16(uint16_t* p, int64_t lo, int64_t hi, int tid, int nt) {
+  if (lo >= hi) return;
+  const int64_t a0 = min(hi, (lo + 7) & ~(int64_t)7), a1 = max(a0, hi & ~(int64_t)7);
+  for (int64_t i = lo + tid; i < a0; i += nt) p[i] = 0;
+  for (int64_t i = a0 / 8 + tid; i < a1 / 8; i += nt) reinterpret_cast<uint4*>(p)[i] = make_uint4(0, 0, 0, 0);
+  for (int64_t i = a1 + tid; i < hi; i += nt) p[i] = 0;
+}
+
 constexpr int kAXThreads = 512;
 
 template <int TY>
@@ -1458,6 +1471,11 @@ __global__ void __launch_bounds__(kAXThreads, 4) freq_phaseA_xp(AArgs a) {  // 4
   __shared__ uint32_t s_hits, s_bypass, s_full;
   __shared__ unsigned long long s_maxcnt;
   const int tid = threadIdx.x;
+  if (a.zero_rows) {  // this workgroup's share of the piece chunks' hist rows
+    const int64_t tot = a.zero_rows * kHistRow, per = (tot + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = a.zero_off * kHistRow + (int64_t)blockIdx.x * per;
+    zero_u16(a.hist, lo, min(lo + per, (a.zero_off + a.zero_rows) * kHistRow), tid, kAXThreads);
+  }
   if (a.dense_words && __hip_atomic_load(&a.dense_words[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                            a.dense_epoch) {  // the dense path took the batch: empty pieces
     a.pstart[(int64_t)blockIdx.x * kBuckets + tid] = 0;
@@ -1970,15 +1988,6 @@ struct StrOffsets {
   }
 };
 
-// p[lo, hi) = 0 by the block's threads: 16-byte stores over the aligned middle (the tile rows of
-// a small-key workgroup are ~46 KB of u16, zeroed 2 bytes a store before)
-DQ_DEV void zero_u16(uint16_t* p, int64_t lo, int64_t hi, int tid, int nt) {
-  if (lo >= hi) return;
-  const int64_t a0 = min(hi, (lo + 7) & ~(int64_t)7), a1 = max(a0, hi & ~(int64_t)7);
-  for (int64_t i = lo + tid; i < a0; i += nt) p[i] = 0;
-  for (int64_t i = a0 / 8 + tid; i < a1 / 8; i += nt) reinterpret_cast<uint4*>(p)[i] = make_uint4(0, 0, 0, 0);
-  for (int64_t i = a1 + tid; i < hi; i += nt) p[i] = 0;
-}
 
 __global__ void __launch_bounds__(kSmallThreads) freq_phaseA_small(AArgs a) {
   constexpr int NW = kSmallThreads / 64;
@@ -5309,6 +5318,10 @@ static dq_status launch_pieces(dq_freq* f, AArgs a, int64_t chunks) {
     return e && atoi(e) != 0;
   }();
   if (generic) {
+    if (a.zero_rows)  // (the generic kernel does not zero them)
+      HIP_TRY(hipMemsetAsync(a.hist + (size_t)a.zero_off * kHistRow, 0,
+                             (size_t)a.zero_rows * kHistRow * sizeof(uint16_t), f->stream));
+    a.zero_rows = 0;
     f->nan_counted = false;
     a.piece_cap = 0;  // (the generic kernel lays pieces out by the pre-pass)
     launch_phaseA<false>(f, a, false);
@@ -6883,9 +6896,9 @@ extern "C" dq_status dq_freq_add_device(dq_freq* f, const dq_column* keys, int n
     a.ks.cols[k] = KeyCol{keys[k].type, 0, keys[k].validity, keys[k].values, keys[k].data};
   a.n_items = rows;
   a.tile_items = f->tile;
-  if (piece_chunks && f->exact) {  // the piece chunks' rows hold no records
-    HIP_TRY(hipMemsetAsync(f->hist.p + (size_t)(f->n_chunks + chunks) * kHistRow, 0,
-                           (size_t)piece_chunks * kHistRow * sizeof(uint16_t), f->stream));
+  if (piece_chunks && f->exact) {  // the piece chunks' rows hold no records (zeroed by phase A)
+    a.zero_off = chunks;
+    a.zero_rows = piece_chunks;
     a.piece_cap = hp_cap;
     a.piece_base = (uint64_t)chunks * f->tile;
   } else if (piece_chunks) {  // the piece chunks' rows hold no records; the pieces' rows of this batch
